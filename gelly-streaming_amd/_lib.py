@@ -1,0 +1,120 @@
+"""ctypes binding of libgellyhip.so (include/gelly_hip.h).
+
+The product path: every operator of this package runs through these entry points.  If the
+library is missing or no HIP device is present, :func:`load` / :class:`Engine` raise — there is
+no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes
+from pathlib import Path
+
+import numpy as np
+
+PKG = Path(__file__).resolve().parent
+LIB_PATH = PKG / "libgellyhip.so"
+
+GS_OK, GS_EINVAL, GS_ECAPACITY, GS_EDEVICE, GS_ECOMM, GS_ENOMEM, GS_EUNSUPPORTED = 0, -1, -2, -3, -4, -5, -6
+GS_MEM_HOST, GS_MEM_DEVICE = 0, 1
+GS_I32, GS_I64, GS_F32, GS_F64, GS_NONE = 0, 1, 2, 3, 4
+GS_OP_SUM, GS_OP_MIN, GS_OP_MAX, GS_OP_COUNT = 0, 1, 2, 3
+STATUS_NAMES = {0: "GS_OK", -1: "GS_EINVAL", -2: "GS_ECAPACITY", -3: "GS_EDEVICE", -4: "GS_ECOMM",
+                -5: "GS_ENOMEM", -6: "GS_EUNSUPPORTED"}
+
+NP_DTYPE = {GS_I32: np.int32, GS_I64: np.int64, GS_F32: np.float32, GS_F64: np.float64}
+GS_DTYPE_OF = {np.dtype(np.int32): GS_I32, np.dtype(np.int64): GS_I64, np.dtype(np.float32): GS_F32,
+               np.dtype(np.float64): GS_F64}
+
+# every symbol include/gelly_hip.h declares (checked by tests/test_abi.py)
+EXPORTS = ("gs_abi_version", "gs_create", "gs_destroy", "gs_last_error", "gs_set_stream", "gs_synchronize",
+           "gs_alloc_pinned", "gs_free_pinned", "gs_window_reduce", "gs_window_fold",
+           "gs_window_fold_degree_max", "gs_window_csr", "gs_window_candidates", "gs_window_triangles",
+           "gs_generate_rmat", "gs_generate_uniform", "gs_generate_values", "gs_last_stage_times")
+
+P = ctypes.c_void_p
+u64, i64, i32, u32 = ctypes.c_uint64, ctypes.c_int64, ctypes.c_int32, ctypes.c_uint32
+
+
+class GsConfig(ctypes.Structure):
+    _fields_ = [("device", i32), ("flags", u32), ("reserve_edges", u64)]
+
+
+class GsEdgeBatch(ctypes.Structure):
+    _fields_ = [("src", P), ("dst", P), ("val", P), ("n", u64), ("val_dtype", i32), ("mem", i32),
+                ("window_end_ms", i64)]
+
+
+class GsVertexOut(ctypes.Structure):
+    _fields_ = [("keys", P), ("vals", P), ("capacity", u64), ("n_out", ctypes.POINTER(u64)), ("mem", i32),
+                ("reserved", i32)]
+
+
+class GsDegreeOut(ctypes.Structure):
+    _fields_ = [("keys", P), ("degree", P), ("max_neighbor", P), ("capacity", u64),
+                ("n_out", ctypes.POINTER(u64)), ("mem", i32), ("reserved", i32)]
+
+
+class GsCsrOut(ctypes.Structure):
+    _fields_ = [("keys", P), ("offsets", P), ("neighbors", P), ("vals", P), ("capacity_vertices", u64),
+                ("capacity_records", u64), ("n_vertices", ctypes.POINTER(u64)), ("n_records", ctypes.POINTER(u64)),
+                ("mem", i32), ("reserved", i32)]
+
+
+class GsPairOut(ctypes.Structure):
+    _fields_ = [("a", P), ("b", P), ("is_candidate", P), ("capacity", u64), ("n_out", ctypes.POINTER(u64)),
+                ("mem", i32), ("reserved", i32)]
+
+
+class GsStageTimes(ctypes.Structure):
+    _fields_ = [("keyinfo_ms", ctypes.c_float), ("sort_ms", ctypes.c_float), ("reduce_ms", ctypes.c_float),
+                ("total_ms", ctypes.c_float), ("sort_passes", u32), ("key_bits", u32), ("records", u64),
+                ("vertices", u64)]
+
+
+class GsError(RuntimeError):
+    """A non-zero gs_status — the Java wrapper maps these to an Exception (EdgesReduce.java:43 `throws Exception`)."""
+
+    def __init__(self, status: int, message: str):
+        super().__init__(f"{STATUS_NAMES.get(status, status)}: {message}")
+        self.status = status
+
+
+_lib = None
+
+
+def load() -> ctypes.CDLL:
+    """Load libgellyhip.so (build it first with __graft_entry__.build() or `make -C csrc`)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not LIB_PATH.exists():
+        raise ImportError(f"{LIB_PATH} is missing: the HIP engine is not built (run __graft_entry__.build())")
+    L = ctypes.CDLL(str(LIB_PATH))
+    st = ctypes.c_int32
+    sigs = {
+        "gs_abi_version": (i32, []),
+        "gs_create": (st, [ctypes.POINTER(GsConfig), ctypes.POINTER(P)]),
+        "gs_destroy": (None, [P]),
+        "gs_last_error": (ctypes.c_char_p, [P]),
+        "gs_set_stream": (st, [P, P]),
+        "gs_synchronize": (st, [P]),
+        "gs_alloc_pinned": (P, [ctypes.c_size_t]),
+        "gs_free_pinned": (None, [P]),
+        "gs_window_reduce": (st, [P, ctypes.POINTER(GsEdgeBatch), i32, i32, ctypes.POINTER(GsVertexOut)]),
+        "gs_window_fold": (st, [P, ctypes.POINTER(GsEdgeBatch), i32, i32, P, ctypes.POINTER(GsVertexOut)]),
+        "gs_window_fold_degree_max": (st, [P, ctypes.POINTER(GsEdgeBatch), i32, i64, ctypes.POINTER(GsDegreeOut)]),
+        "gs_window_csr": (st, [P, ctypes.POINTER(GsEdgeBatch), i32, ctypes.POINTER(GsCsrOut)]),
+        "gs_window_candidates": (st, [P, ctypes.POINTER(GsEdgeBatch), ctypes.POINTER(GsPairOut)]),
+        "gs_window_triangles": (st, [P, ctypes.POINTER(GsEdgeBatch), ctypes.POINTER(u64), ctypes.POINTER(i32),
+                                     ctypes.POINTER(i32)]),
+        "gs_generate_rmat": (st, [P, i32, u64, u64, u32, u32, u32, i32, i32, u64, P, P]),
+        "gs_generate_uniform": (st, [P, u64, u64, u64, u64, P, P]),
+        "gs_generate_values": (st, [P, u64, u64, u64, i32, P]),
+        "gs_last_stage_times": (st, [P, ctypes.POINTER(GsStageTimes)]),
+    }
+    for name, (res, args) in sigs.items():
+        f = getattr(L, name)
+        f.restype = res
+        f.argtypes = args
+    _lib = L
+    return L

@@ -1,0 +1,426 @@
+// gs_engine.hip — C ABI lifecycle, window sort orchestration and the reduce / fold operators.
+//
+//   gs_window_reduce          <- GraphWindowStream.reduceOnEdges  (GraphWindowStream.java:101-121)
+//   gs_window_fold            <- GraphWindowStream.foldNeighbors  (GraphWindowStream.java:62-87)
+//   gs_window_fold_degree_max <- foldNeighbors with a degree / max-neighbour EdgesFold
+// Window = one columnar batch: keyinfo -> LSD onesweep passes -> reduce-by-key.
+#include <stdarg.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <algorithm>
+
+#include "gs_ops.hpp"
+
+using namespace gs;
+
+namespace gs {
+
+
+gs_status set_error(gs_ctx* c, gs_status s, const char* fmt, ...) {
+  if (c) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    c->err = buf;
+  }
+  return s;
+}
+
+gs_status hip_check(gs_ctx* c, hipError_t e, const char* what) {
+  if (e == hipSuccess) return GS_OK;
+  return set_error(c, e == hipErrorOutOfMemory ? GS_ENOMEM : GS_EDEVICE, "%s: %s", what, hipGetErrorString(e));
+}
+
+gs_status ensure(gs_ctx* c, DevBuf& b, size_t bytes, bool zero) {
+  if (bytes == 0) bytes = 16;
+  if (b.bytes >= bytes) return GS_OK;
+  if (b.p) {
+    GS_HIP(hipStreamSynchronize(c->stream));
+    GS_HIP(hipFree(b.p));
+    b.p = nullptr;
+    b.bytes = 0;
+  }
+  size_t want = bytes + bytes / 8;  // headroom for slightly larger windows
+  GS_HIP(hipMalloc(&b.p, want));
+  b.bytes = want;
+  if (zero) GS_HIP(hipMemsetAsync(b.p, 0, want, c->stream));
+  return GS_OK;
+}
+
+// Epochs tag look-back granules so no status buffer is cleared between launches.
+uint32_t next_epoch(gs_ctx* c, size_t) {
+  c->epoch++;
+  if (c->epoch >= (1u << EPOCH_BITS) - 1) {
+    if (c->sort_status.p) hipMemsetAsync(c->sort_status.p, 0, c->sort_status.bytes, c->stream);
+    if (c->rbk_word.p) hipMemsetAsync(c->rbk_word.p, 0, c->rbk_word.bytes, c->stream);
+    c->epoch = 1;
+  }
+  return c->epoch;
+}
+
+gs_status stage_batch(gs_ctx* c, const gs_edge_batch* b, const int64_t** src, const int64_t** dst, const void** val,
+                      bool need_val) {
+  const size_t vb = dtype_bytes(b->val_dtype);
+  if (b->mem == GS_MEM_DEVICE) {
+    *src = b->src;
+    *dst = b->dst;
+    *val = b->val;
+    return GS_OK;
+  }
+  const size_t eb = b->n * sizeof(int64_t);
+  GS_TRY(ensure(c, c->in_src, eb));
+  GS_TRY(ensure(c, c->in_dst, eb));
+  GS_HIP(hipMemcpyAsync(c->in_src.p, b->src, eb, hipMemcpyHostToDevice, c->stream));
+  GS_HIP(hipMemcpyAsync(c->in_dst.p, b->dst, eb, hipMemcpyHostToDevice, c->stream));
+  *src = c->in_src.as<int64_t>();
+  *dst = c->in_dst.as<int64_t>();
+  *val = nullptr;
+  if (need_val && vb) {
+    GS_TRY(ensure(c, c->in_val, b->n * vb));
+    GS_HIP(hipMemcpyAsync(c->in_val.p, b->val, b->n * vb, hipMemcpyHostToDevice, c->stream));
+    *val = c->in_val.p;
+  }
+  return GS_OK;
+}
+
+static inline unsigned grid_for(uint64_t n, unsigned per_block, unsigned cap) {
+  const uint64_t g = (n + per_block - 1) / per_block;
+  return (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(g, cap));
+}
+
+template <int DIR>
+static gs_status launch_keyinfo(gs_ctx* c, const int64_t* src, const int64_t* dst, uint64_t n) {
+  char* sm = c->small.as<char>();
+  hipLaunchKernelGGL(k_keyinfo<DIR>, dim3(grid_for(n, 256 * 8, 2048)), dim3(256), 0, c->stream, src, dst, n,
+                     (unsigned long long*)(sm + SM_MASK), (uint32_t*)(sm + SM_HIST));
+  return hip_check(c, hipGetLastError(), "k_keyinfo");
+}
+template <int DIR>
+static gs_status launch_hist_wide(gs_ctx* c, const int64_t* src, const int64_t* dst, uint64_t n, uint64_t key_xor) {
+  char* sm = c->small.as<char>();
+  GS_HIP(hipMemsetAsync(sm + SM_HIST, 0, 8 * 256 * 4, c->stream));
+  hipLaunchKernelGGL(k_hist_wide<DIR>, dim3(grid_for(n, 256 * 8, 2048)), dim3(256), 0, c->stream, src, dst, n,
+                     key_xor, (uint32_t*)(sm + SM_HIST));
+  return hip_check(c, hipGetLastError(), "k_hist_wide");
+}
+
+template <typename K, typename V, bool HAS_V, class Src>
+static gs_status launch_pass(gs_ctx* c, Src src, K* kout, V* vout, uint32_t R, int pass, uint32_t shift) {
+  char* sm = c->small.as<char>();
+  const uint32_t tiles = (R + SORT_TILE - 1) / SORT_TILE;
+  const uint32_t ep = next_epoch(c, 0);
+  hipLaunchKernelGGL((k_onesweep<K, V, HAS_V, SORT_BLOCK, SORT_ITEMS, Src>), dim3(tiles), dim3(SORT_BLOCK), 0,
+                     c->stream, src, kout, vout, R, shift, (const uint32_t*)(sm + SM_BASE) + pass * RADIX,
+                     c->sort_status.as<uint64_t>(), (uint32_t*)(sm + SM_COUNTERS) + pass, ep,
+                     (uint32_t*)(sm + SM_TIMEOUT));
+  return hip_check(c, hipGetLastError(), "k_onesweep");
+}
+
+template <typename K, typename V, bool HAS_V, int DIR, int PAY>
+static gs_status run_passes(gs_ctx* c, const int64_t* src, const int64_t* dst, const void* val, uint32_t R,
+                            Sorted* out) {
+  K* ka = c->keysA.as<K>();
+  K* kb = c->keysB.as<K>();
+  V* va = c->valsA.as<V>();
+  V* vb = c->valsB.as<V>();
+  EdgeSrc<K, V, DIR, PAY> es{src, dst, (const V*)val, out->key_xor};
+  GS_TRY((launch_pass<K, V, HAS_V>(c, es, ka, va, R, 0, 0)));
+  for (int p = 1; p < out->passes; ++p) {
+    BufSrc<K, V> bs{ka, HAS_V ? va : nullptr, 0};
+    GS_TRY((launch_pass<K, V, HAS_V>(c, bs, kb, vb, R, p, 8u * p)));
+    std::swap(ka, kb);
+    std::swap(va, vb);
+  }
+  out->keys = ka;
+  out->vals = HAS_V ? (void*)va : nullptr;
+  return GS_OK;
+}
+
+template <typename K, int DIR>
+static gs_status dispatch_payload(gs_ctx* c, const int64_t* src, const int64_t* dst, const void* val, int vbytes,
+                                  uint32_t R, int payload, Sorted* out) {
+  switch (payload) {
+    case PAY_NONE: return run_passes<K, uint8_t, false, DIR, PAY_NONE>(c, src, dst, val, R, out);
+    case PAY_VAL:
+      if (vbytes == 4) return run_passes<K, uint32_t, true, DIR, PAY_VAL>(c, src, dst, val, R, out);
+      return run_passes<K, uint64_t, true, DIR, PAY_VAL>(c, src, dst, val, R, out);
+    case PAY_NBR: return run_passes<K, uint64_t, true, DIR, PAY_NBR>(c, src, dst, val, R, out);
+    case PAY_IDX: return run_passes<K, uint32_t, true, DIR, PAY_IDX>(c, src, dst, val, R, out);
+  }
+  return set_error(c, GS_EINVAL, "bad payload kind %d", payload);
+}
+
+template <int DIR>
+static gs_status sort_dir(gs_ctx* c, const int64_t* src, const int64_t* dst, const void* val, int vbytes,
+                          uint64_t n, int payload, Sorted* out) {
+  char* sm = c->small.as<char>();
+  const uint64_t R = (DIR == DIR_ALL) ? 2 * n : n;
+  GS_HIP(hipMemsetAsync(sm, 0, SM_BASE, c->stream));  // mask, k0, counters, timeout, hist
+  GS_TRY(launch_keyinfo<DIR>(c, src, dst, n));
+  const int64_t* k0p = (DIR == DIR_IN) ? dst : src;
+  GS_HIP(hipMemcpyAsync(sm + SM_K0, k0p, 8, hipMemcpyDeviceToDevice, c->stream));
+  GS_HIP(hipMemcpyAsync(c->host_small, sm, 16, hipMemcpyDeviceToHost, c->stream));
+  GS_HIP(hipStreamSynchronize(c->stream));
+  const uint64_t mask = c->host_small[0], k0 = c->host_small[1];
+  const int bits = mask ? 64 - __builtin_clzll(mask) : 0;
+  out->bits = bits;
+  out->wide = bits > 32;
+  out->passes = std::max(1, (bits + RADIX_BITS - 1) / RADIX_BITS);
+  out->records = R;
+  out->key_xor = out->wide ? (1ull << 63) : (k0 & 0xFFFFFFFF00000000ull);
+  if (out->wide) GS_TRY(launch_hist_wide<DIR>(c, src, dst, n, out->key_xor));
+  hipLaunchKernelGGL(k_digit_base, dim3(1), dim3(256), 0, c->stream, (const uint32_t*)(sm + SM_HIST),
+                     (uint32_t*)(sm + SM_BASE), out->passes);
+  GS_HIP(hipGetLastError());
+  hipEventRecord(c->ev[1], c->stream);
+  const size_t kb = out->wide ? 8 : 4;
+  const size_t vb = payload == PAY_NONE ? 0 : payload == PAY_IDX ? 4 : payload == PAY_NBR ? 8 : (size_t)vbytes;
+  const uint64_t tiles = (R + SORT_TILE - 1) / SORT_TILE;
+  GS_TRY(ensure(c, c->keysA, R * kb));
+  GS_TRY(ensure(c, c->keysB, R * kb));
+  if (vb) {
+    GS_TRY(ensure(c, c->valsA, R * vb));
+    GS_TRY(ensure(c, c->valsB, R * vb));
+  }
+  GS_TRY(ensure(c, c->sort_status, tiles * RADIX * 8, true));
+  if (out->wide) return dispatch_payload<uint64_t, DIR>(c, src, dst, val, vbytes, (uint32_t)R, payload, out);
+  return dispatch_payload<uint32_t, DIR>(c, src, dst, val, vbytes, (uint32_t)R, payload, out);
+}
+
+gs_status sort_window(gs_ctx* c, const int64_t* src, const int64_t* dst, const void* val, int val_bytes,
+                      uint64_t n_edges, int dir, int payload, Sorted* out) {
+  switch (dir) {
+    case DIR_IN: return sort_dir<DIR_IN>(c, src, dst, val, val_bytes, n_edges, payload, out);
+    case DIR_OUT: return sort_dir<DIR_OUT>(c, src, dst, val, val_bytes, n_edges, payload, out);
+    case DIR_ALL: return sort_dir<DIR_ALL>(c, src, dst, val, val_bytes, n_edges, payload, out);
+  }
+  return set_error(c, GS_EINVAL, "bad direction %d", dir);
+}
+
+namespace {
+// ---- reduce / fold ---------------------------------------------------------------------------------
+template <typename T, int OP>
+static gs_status value_rbk(gs_ctx* c, const Sorted& s, int64_t* keys, void* vals, bool has_init, const void* init,
+                           uint64_t* U) {
+  using Op = ValueOp<T, OP>;
+  ValueOut<Op, true> oi{keys, (T*)vals, has_init ? *(const T*)init : T{}};
+  ValueOut<Op, false> on{keys, (T*)vals, T{}};
+  if (s.wide) {
+    if (has_init) return launch_rbk<uint64_t, Op>(c, s, oi, U);
+    return launch_rbk<uint64_t, Op>(c, s, on, U);
+  }
+  if (has_init) return launch_rbk<uint32_t, Op>(c, s, oi, U);
+  return launch_rbk<uint32_t, Op>(c, s, on, U);
+}
+
+template <typename T>
+static gs_status value_rbk_op(gs_ctx* c, int op, const Sorted& s, int64_t* keys, void* vals, bool has_init,
+                              const void* init, uint64_t* U) {
+  switch (op) {
+    case OP_SUM: return value_rbk<T, OP_SUM>(c, s, keys, vals, has_init, init, U);
+    case OP_MIN: return value_rbk<T, OP_MIN>(c, s, keys, vals, has_init, init, U);
+    case OP_MAX: return value_rbk<T, OP_MAX>(c, s, keys, vals, has_init, init, U);
+  }
+  return set_error(c, GS_EINVAL, "bad op %d", op);
+}
+
+}  // namespace
+
+}  // namespace gs
+
+// =================================================================================================
+// C ABI
+// =================================================================================================
+extern "C" {
+
+int32_t gs_abi_version(void) { return GS_ABI_VERSION; }
+
+gs_status gs_create(const gs_config* cfg, gs_ctx** out) {
+  if (!out) return GS_EINVAL;
+  *out = nullptr;
+  gs_ctx* c = new (std::nothrow) gs_ctx();
+  if (!c) return GS_ENOMEM;
+  c->device = cfg ? cfg->device : 0;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= c->device) {
+    delete c;
+    return GS_EDEVICE;
+  }
+  if (hipSetDevice(c->device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+    delete c;
+    return GS_EDEVICE;
+  }
+  c->own_stream = true;
+  for (auto& e : c->ev) hipEventCreate(&e);
+  if (hipHostMalloc((void**)&c->host_small, 64, hipHostMallocDefault) != hipSuccess ||
+      ensure(c, c->small, SM_BYTES, true) != GS_OK) {
+    gs_destroy(c);
+    return GS_ENOMEM;
+  }
+  if (cfg && cfg->reserve_edges) {
+    const uint64_t R = 2 * cfg->reserve_edges;
+    if (ensure(c, c->keysA, R * 4) || ensure(c, c->keysB, R * 4) || ensure(c, c->valsA, R * 8) ||
+        ensure(c, c->valsB, R * 8)) {
+      gs_destroy(c);
+      return GS_ENOMEM;
+    }
+  }
+  hipStreamSynchronize(c->stream);
+  *out = c;
+  return GS_OK;
+}
+
+void gs_destroy(gs_ctx* c) {
+  if (!c) return;
+  hipSetDevice(c->device);
+  if (c->stream) hipStreamSynchronize(c->stream);
+  for (DevBuf* b : {&c->in_src, &c->in_dst, &c->in_val, &c->keysA, &c->keysB, &c->valsA, &c->valsB, &c->sort_status,
+                    &c->rbk_word, &c->rbk_agg, &c->rbk_inc, &c->small, &c->out_keys, &c->out_a, &c->out_b, &c->aux})
+    if (b->p) hipFree(b->p);
+  for (auto& e : c->ev)
+    if (e) hipEventDestroy(e);
+  if (c->host_small) hipHostFree(c->host_small);
+  if (c->own_stream && c->stream) hipStreamDestroy(c->stream);
+  delete c;
+}
+
+const char* gs_last_error(const gs_ctx* c) { return c ? c->err.c_str() : "null context"; }
+
+gs_status gs_set_stream(gs_ctx* c, void* s) {
+  if (!c) return GS_EINVAL;
+  hipSetDevice(c->device);
+  if (c->stream) hipStreamSynchronize(c->stream);
+  if (c->own_stream && c->stream) hipStreamDestroy(c->stream);
+  c->stream = (hipStream_t)s;  // NULL = the device's default stream
+  c->own_stream = false;
+  return GS_OK;
+}
+
+gs_status gs_synchronize(gs_ctx* c) {
+  if (!c) return GS_EINVAL;
+  return hip_check(c, hipStreamSynchronize(c->stream), "hipStreamSynchronize");
+}
+
+void* gs_alloc_pinned(size_t bytes) {
+  void* p = nullptr;
+  if (hipHostMalloc(&p, bytes ? bytes : 1, hipHostMallocDefault) != hipSuccess) return nullptr;
+  return p;
+}
+void gs_free_pinned(void* p) {
+  if (p) hipHostFree(p);
+}
+
+gs_status gs_last_stage_times(const gs_ctx* c, gs_stage_times* out) {
+  if (!c || !out) return GS_EINVAL;
+  *out = c->times;
+  return GS_OK;
+}
+
+static gs_status window_fold_impl(gs_ctx* c, const gs_edge_batch* b, int32_t dir, int32_t op, bool has_init,
+                                  const void* init, gs_vertex_out* out) {
+  GS_TRY(check_batch(c, b, dir));
+  if (!out || !out->n_out || (out->capacity && (!out->keys || !out->vals)))
+    return set_error(c, GS_EINVAL, "bad gs_vertex_out");
+  if (op < GS_OP_SUM || op > GS_OP_COUNT) return set_error(c, GS_EINVAL, "bad op %d", op);
+  if (op != GS_OP_COUNT && (b->val_dtype == GS_NONE || (b->n && !b->val)))
+    return set_error(c, GS_EINVAL, "op %d needs edge values", op);
+  if (has_init && !init) return set_error(c, GS_EINVAL, "null init");
+  GS_HIP(hipSetDevice(c->device));
+  const uint64_t R = dir == GS_DIR_ALL ? 2 * b->n : b->n;
+  if (R == 0) {
+    *out->n_out = 0;
+    return GS_OK;
+  }
+  hipEventRecord(c->ev[0], c->stream);
+  const int64_t *src, *dst;
+  const void* val;
+  GS_TRY(stage_batch(c, b, &src, &dst, &val, op != GS_OP_COUNT));
+  Sorted s;
+  const int vbytes = (int)dtype_bytes(b->val_dtype);
+  GS_TRY(sort_window(c, src, dst, val, vbytes, b->n, dir, op == GS_OP_COUNT ? PAY_NONE : PAY_VAL, &s));
+  hipEventRecord(c->ev[2], c->stream);
+  const size_t ob = op == GS_OP_COUNT ? 8 : (size_t)vbytes;
+  const bool direct = out->mem == GS_MEM_DEVICE && out->capacity >= R;
+  int64_t* kd = out->keys;
+  void* vd = out->vals;
+  if (!direct) {
+    GS_TRY(ensure(c, c->out_keys, R * 8));
+    GS_TRY(ensure(c, c->out_a, R * ob));
+    kd = c->out_keys.as<int64_t>();
+    vd = c->out_a.p;
+  }
+  uint64_t U = 0;
+  if (op == GS_OP_COUNT) {
+    CountOut o{kd, (int64_t*)vd, has_init ? *(const int64_t*)init : 0};
+    GS_TRY((s.wide ? launch_rbk<uint64_t, CountOp>(c, s, o, &U) : launch_rbk<uint32_t, CountOp>(c, s, o, &U)));
+  } else {
+    switch (b->val_dtype) {
+      case GS_I32: GS_TRY(value_rbk_op<int32_t>(c, op, s, kd, vd, has_init, init, &U)); break;
+      case GS_I64: GS_TRY(value_rbk_op<int64_t>(c, op, s, kd, vd, has_init, init, &U)); break;
+      case GS_F32: GS_TRY(value_rbk_op<float>(c, op, s, kd, vd, has_init, init, &U)); break;
+      case GS_F64: GS_TRY(value_rbk_op<double>(c, op, s, kd, vd, has_init, init, &U)); break;
+    }
+  }
+  finish_times(c, s, U);
+  *out->n_out = U;
+  if (U > out->capacity) return set_error(c, GS_ECAPACITY, "output needs %llu vertices", (unsigned long long)U);
+  GS_TRY(deliver(c, out->keys, kd, U * 8, out->mem));
+  GS_TRY(deliver(c, out->vals, vd, U * ob, out->mem));
+  if (!direct) GS_HIP(hipStreamSynchronize(c->stream));
+  return GS_OK;
+}
+
+gs_status gs_window_reduce(gs_ctx* c, const gs_edge_batch* b, int32_t dir, int32_t op, gs_vertex_out* out) {
+  return window_fold_impl(c, b, dir, op, false, nullptr, out);
+}
+
+gs_status gs_window_fold(gs_ctx* c, const gs_edge_batch* b, int32_t dir, int32_t op, const void* init,
+                         gs_vertex_out* out) {
+  return window_fold_impl(c, b, dir, op, true, init, out);
+}
+
+gs_status gs_window_fold_degree_max(gs_ctx* c, const gs_edge_batch* b, int32_t dir, int64_t init_max,
+                                    gs_degree_out* out) {
+  GS_TRY(check_batch(c, b, dir));
+  if (!out || !out->n_out || (out->capacity && (!out->keys || !out->degree || !out->max_neighbor)))
+    return set_error(c, GS_EINVAL, "bad gs_degree_out");
+  GS_HIP(hipSetDevice(c->device));
+  const uint64_t R = dir == GS_DIR_ALL ? 2 * b->n : b->n;
+  if (R == 0) {
+    *out->n_out = 0;
+    return GS_OK;
+  }
+  hipEventRecord(c->ev[0], c->stream);
+  const int64_t *src, *dst;
+  const void* val;
+  GS_TRY(stage_batch(c, b, &src, &dst, &val, false));
+  Sorted s;
+  GS_TRY(sort_window(c, src, dst, nullptr, 0, b->n, dir, PAY_NBR, &s));
+  hipEventRecord(c->ev[2], c->stream);
+  const bool direct = out->mem == GS_MEM_DEVICE && out->capacity >= R;
+  int64_t *kd = out->keys, *dd = out->degree, *md = out->max_neighbor;
+  if (!direct) {
+    GS_TRY(ensure(c, c->out_keys, R * 8));
+    GS_TRY(ensure(c, c->out_a, R * 8));
+    GS_TRY(ensure(c, c->out_b, R * 8));
+    kd = c->out_keys.as<int64_t>();
+    dd = c->out_a.as<int64_t>();
+    md = c->out_b.as<int64_t>();
+  }
+  DegMaxOut o{kd, dd, md, init_max};
+  uint64_t U = 0;
+  GS_TRY((s.wide ? launch_rbk<uint64_t, DegMaxOp>(c, s, o, &U) : launch_rbk<uint32_t, DegMaxOp>(c, s, o, &U)));
+  finish_times(c, s, U);
+  *out->n_out = U;
+  if (U > out->capacity) return set_error(c, GS_ECAPACITY, "output needs %llu vertices", (unsigned long long)U);
+  GS_TRY(deliver(c, out->keys, kd, U * 8, out->mem));
+  GS_TRY(deliver(c, out->degree, dd, U * 8, out->mem));
+  GS_TRY(deliver(c, out->max_neighbor, md, U * 8, out->mem));
+  if (!direct) GS_HIP(hipStreamSynchronize(c->stream));
+  return GS_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,80 @@
+// gs_internal.hpp — host-side context, workspace and the window sort shared by all operators.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <string>
+
+#include "../../include/gelly_hip.h"
+
+namespace gs {
+
+struct DevBuf {
+  void* p = nullptr;
+  size_t bytes = 0;
+  template <typename T>
+  T* as() const { return static_cast<T*>(p); }
+};
+
+// Result of the window sort: compact keys + payload in key order (stable).
+struct Sorted {
+  void* keys = nullptr;     // uint32_t or uint64_t
+  void* vals = nullptr;     // payload (nullptr when none)
+  bool wide = false;        // 64-bit keys
+  uint64_t key_xor = 0;     // key = key_xor ^ compact
+  uint64_t records = 0;
+  int bits = 0, passes = 0;
+};
+
+}  // namespace gs
+
+struct gs_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  bool own_stream = false;
+  std::string err;
+  uint32_t epoch = 0;
+  // input staging (host batches)
+  gs::DevBuf in_src, in_dst, in_val;
+  // sort ping-pong
+  gs::DevBuf keysA, keysB, valsA, valsB;
+  // look-back granules
+  gs::DevBuf sort_status, rbk_word, rbk_agg, rbk_inc;
+  // small scalars: see gs_engine.hip layout
+  gs::DevBuf small;
+  // output staging
+  gs::DevBuf out_keys, out_a, out_b, aux;
+  hipEvent_t ev[6] = {};
+  gs_stage_times times{};
+  uint64_t* host_small = nullptr;  // pinned mirror of small scalars
+};
+
+namespace gs {
+
+// small-buffer layout (bytes)
+constexpr size_t SM_MASK = 0;          // u64 OR(key ^ key0)
+constexpr size_t SM_K0 = 8;            // u64 key0 (device copy)
+constexpr size_t SM_NUNIQUE = 16;      // u64
+constexpr size_t SM_TIMEOUT = 24;      // u32
+constexpr size_t SM_COUNTERS = 32;     // u32[64] tile counters
+constexpr size_t SM_HIST = 32 + 256;   // u32[8][256]
+constexpr size_t SM_BASE = SM_HIST + 8 * 256 * 4;  // u32[8][256]
+constexpr size_t SM_BYTES = SM_BASE + 8 * 256 * 4;
+
+gs_status set_error(gs_ctx* c, gs_status s, const char* fmt, ...);
+gs_status hip_check(gs_ctx* c, hipError_t e, const char* what);
+gs_status ensure(gs_ctx* c, DevBuf& b, size_t bytes, bool zero = false);
+uint32_t next_epoch(gs_ctx* c, size_t status_bytes_hint);
+
+// Sort the window's records by key (stable).  payload: 0 none, 1 value (val_bytes 4|8),
+// 2 neighbour (int64), 3 record index (u32).  src/dst/val are device pointers.
+gs_status sort_window(gs_ctx* c, const int64_t* src, const int64_t* dst, const void* val, int val_bytes,
+                      uint64_t n_edges, int dir, int payload, Sorted* out);
+
+// Stage a batch on the device (copies host columns into ctx buffers); returns device pointers.
+gs_status stage_batch(gs_ctx* c, const gs_edge_batch* b, const int64_t** src, const int64_t** dst,
+                      const void** val, bool need_val);
+
+inline size_t dtype_bytes(int dt) { return (dt == GS_I32 || dt == GS_F32) ? 4 : (dt == GS_NONE ? 0 : 8); }
+
+}  // namespace gs

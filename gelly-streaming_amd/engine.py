@@ -1,0 +1,247 @@
+"""Engine: one gs_ctx (one HIP stream + workspace) driving the per-window operators.
+
+Inputs are either device tensors (torch, on the ctx's GPU: zero-copy, results stay in HBM) or host
+numpy arrays (copied in by the library, results copied back).  One Engine per thread, like one
+gs_ctx per Flink subtask (include/gelly_hip.h, "Conventions").
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import _lib as L
+from ._lib import GsError
+
+
+def _is_torch(x) -> bool:
+    return type(x).__module__.startswith("torch")
+
+
+def _ptr(x):
+    if x is None:
+        return None
+    if _is_torch(x):
+        return ctypes.c_void_p(x.data_ptr())
+    return ctypes.c_void_p(x.ctypes.data)
+
+
+def _gs_dtype(x) -> int:
+    if x is None:
+        return L.GS_NONE
+    if _is_torch(x):
+        import torch
+
+        return {torch.int32: L.GS_I32, torch.int64: L.GS_I64, torch.float32: L.GS_F32,
+                torch.float64: L.GS_F64}[x.dtype]
+    return L.GS_DTYPE_OF[np.dtype(x.dtype)]
+
+
+def fx32(p: float) -> int:
+    """probability -> 32-bit fixed point, as gs_generate_rmat / oracle take it"""
+    return int(p * 4294967296.0)
+
+
+@dataclass
+class StageTimes:
+    keyinfo_ms: float
+    sort_ms: float
+    reduce_ms: float
+    total_ms: float
+    sort_passes: int
+    key_bits: int
+    records: int
+    vertices: int
+
+
+class Engine:
+    def __init__(self, device: int = 0, reserve_edges: int = 0, torch_stream: bool = True):
+        self._L = L.load()
+        cfg = L.GsConfig(device, 0, reserve_edges)
+        ctx = ctypes.c_void_p()
+        st = self._L.gs_create(ctypes.byref(cfg), ctypes.byref(ctx))
+        if st != L.GS_OK:
+            raise GsError(st, f"gs_create(device={device}) failed — a HIP device is required")
+        self.ctx = ctx
+        self.device = device
+        if torch_stream:
+            # share torch's current stream so tensors allocated by torch are ordered with our kernels
+            self.use_torch_stream()
+
+    # -- lifecycle -------------------------------------------------------------------------------
+    def close(self):
+        if getattr(self, "ctx", None):
+            self._L.gs_destroy(self.ctx)
+            self.ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def _check(self, st: int):
+        if st != L.GS_OK:
+            raise GsError(st, self._L.gs_last_error(self.ctx).decode())
+
+    def set_stream(self, hip_stream_ptr: int):
+        """Run on an existing hipStream_t (e.g. torch.cuda.current_stream().cuda_stream; 0 = default stream)."""
+        self._check(self._L.gs_set_stream(self.ctx, ctypes.c_void_p(hip_stream_ptr) if hip_stream_ptr else None))
+
+    def use_torch_stream(self):
+        import torch
+
+        with torch.cuda.device(self.device):
+            self.set_stream(torch.cuda.current_stream(self.device).cuda_stream)
+
+    def synchronize(self):
+        self._check(self._L.gs_synchronize(self.ctx))
+
+    def stage_times(self) -> StageTimes:
+        t = L.GsStageTimes()
+        self._check(self._L.gs_last_stage_times(self.ctx, ctypes.byref(t)))
+        return StageTimes(t.keyinfo_ms, t.sort_ms, t.reduce_ms, t.total_ms, t.sort_passes, t.key_bits, t.records,
+                          t.vertices)
+
+    # -- helpers ---------------------------------------------------------------------------------
+    def _batch(self, src, dst, val):
+        dev = _is_torch(src)
+        if dev:
+            assert src.is_cuda and dst.is_cuda and (val is None or val.is_cuda), "mixed host/device columns"
+            assert src.is_contiguous() and dst.is_contiguous() and (val is None or val.is_contiguous())
+        else:
+            src = np.ascontiguousarray(src, dtype=np.int64)
+            dst = np.ascontiguousarray(dst, dtype=np.int64)
+            if val is not None:
+                val = np.ascontiguousarray(val)
+        if len(src) != len(dst) or (val is not None and len(val) != len(src)):
+            raise ValueError("src, dst and val must have the same length")
+        b = L.GsEdgeBatch(_ptr(src), _ptr(dst), _ptr(val), len(src), _gs_dtype(val),
+                          L.GS_MEM_DEVICE if dev else L.GS_MEM_HOST, 0)
+        return b, (src, dst, val), dev
+
+    def _empty(self, like_dev: bool, n: int, np_dtype):
+        if like_dev:
+            import torch
+
+            tdt = {np.int64: torch.int64, np.int32: torch.int32, np.float32: torch.float32,
+                   np.float64: torch.float64, np.uint64: torch.int64, np.uint8: torch.uint8}[np_dtype]
+            return torch.empty(max(n, 1), dtype=tdt, device=f"cuda:{self.device}")
+        return np.empty(max(n, 1), dtype=np_dtype)
+
+    @staticmethod
+    def _records(n, direction):
+        return 2 * n if int(direction) == 2 else n
+
+    # -- operators ------------------------------------------------------------------------------
+    def reduce(self, src, dst, val, direction, op):
+        """gs_window_reduce: reduceOnEdges with a built-in op. Returns (keys, values) trimmed to U."""
+        return self._fold(src, dst, val, direction, op, None)
+
+    def fold(self, src, dst, val, direction, op, init):
+        """gs_window_fold: foldNeighbors(init, op). Returns (keys, values)."""
+        return self._fold(src, dst, val, direction, op, init)
+
+    def _fold(self, src, dst, val, direction, op, init):
+        b, keep, dev = self._batch(src, dst, None if op == L.GS_OP_COUNT else val)
+        R = self._records(b.n, direction)
+        odt = np.int64 if op == L.GS_OP_COUNT else L.NP_DTYPE[b.val_dtype]
+        keys = self._empty(dev, R, np.int64)
+        vals = self._empty(dev, R, odt)
+        n_out = ctypes.c_uint64(0)
+        out = L.GsVertexOut(_ptr(keys), _ptr(vals), R, ctypes.pointer(n_out),
+                            L.GS_MEM_DEVICE if dev else L.GS_MEM_HOST, 0)
+        if init is None:
+            st = self._L.gs_window_reduce(self.ctx, ctypes.byref(b), int(direction), int(op), ctypes.byref(out))
+        else:
+            ia = np.array([init], dtype=odt)
+            st = self._L.gs_window_fold(self.ctx, ctypes.byref(b), int(direction), int(op),
+                                        ia.ctypes.data_as(ctypes.c_void_p), ctypes.byref(out))
+        self._check(st)
+        U = n_out.value
+        return keys[:U], vals[:U]
+
+    def fold_degree_max(self, src, dst, direction, init_max: int = -(1 << 63)):
+        b, keep, dev = self._batch(src, dst, None)
+        R = self._records(b.n, direction)
+        keys, deg, mx = (self._empty(dev, R, np.int64) for _ in range(3))
+        n_out = ctypes.c_uint64(0)
+        out = L.GsDegreeOut(_ptr(keys), _ptr(deg), _ptr(mx), R, ctypes.pointer(n_out),
+                            L.GS_MEM_DEVICE if dev else L.GS_MEM_HOST, 0)
+        self._check(self._L.gs_window_fold_degree_max(self.ctx, ctypes.byref(b), int(direction), int(init_max),
+                                                      ctypes.byref(out)))
+        U = n_out.value
+        return keys[:U], deg[:U], mx[:U]
+
+    def csr(self, src, dst, val, direction):
+        """gs_window_csr: (keys, offsets[U+1], neighbours[R], values[R] or None), arrival order per vertex."""
+        b, keep, dev = self._batch(src, dst, val)
+        R = self._records(b.n, direction)
+        keys = self._empty(dev, R, np.int64)
+        offs = self._empty(dev, R + 1, np.int64)
+        nbrs = self._empty(dev, R, np.int64)
+        vals = None if val is None else self._empty(dev, R, L.NP_DTYPE[b.val_dtype])
+        nv, nr = ctypes.c_uint64(0), ctypes.c_uint64(0)
+        out = L.GsCsrOut(_ptr(keys), _ptr(offs), _ptr(nbrs), _ptr(vals), R, R, ctypes.pointer(nv),
+                         ctypes.pointer(nr), L.GS_MEM_DEVICE if dev else L.GS_MEM_HOST, 0)
+        self._check(self._L.gs_window_csr(self.ctx, ctypes.byref(b), int(direction), ctypes.byref(out)))
+        U, RR = nv.value, nr.value
+        return keys[:U], offs[:U + 1], nbrs[:RR], (None if vals is None else vals[:RR])
+
+    def candidates(self, src, dst):
+        """gs_window_candidates: GenerateCandidateEdges records (a, b, is_candidate)."""
+        b, keep, dev = self._batch(src, dst, None)
+        n_out = ctypes.c_uint64(0)
+        probe = L.GsPairOut(None, None, None, 0, ctypes.pointer(n_out), L.GS_MEM_DEVICE if dev else L.GS_MEM_HOST, 0)
+        st = self._L.gs_window_candidates(self.ctx, ctypes.byref(b), ctypes.byref(probe))
+        if st not in (L.GS_OK, L.GS_ECAPACITY):
+            self._check(st)
+        P = n_out.value
+        a, bb = self._empty(dev, P, np.int64), self._empty(dev, P, np.int64)
+        f = self._empty(dev, P, np.uint8)
+        out = L.GsPairOut(_ptr(a), _ptr(bb), _ptr(f), P, ctypes.pointer(n_out),
+                          L.GS_MEM_DEVICE if dev else L.GS_MEM_HOST, 0)
+        self._check(self._L.gs_window_candidates(self.ctx, ctypes.byref(b), ctypes.byref(out)))
+        return a[:P], bb[:P], f[:P]
+
+    def triangles(self, src, dst):
+        """gs_window_triangles: (exact count, the Integer the reference emits, has_output)."""
+        b, keep, dev = self._batch(src, dst, None)
+        cnt, wrapped, has = ctypes.c_uint64(0), ctypes.c_int32(0), ctypes.c_int32(0)
+        self._check(self._L.gs_window_triangles(self.ctx, ctypes.byref(b), ctypes.byref(cnt), ctypes.byref(wrapped),
+                                                ctypes.byref(has)))
+        return cnt.value, wrapped.value, bool(has.value)
+
+    # -- synthetic streams (device) ----------------------------------------------------------------
+    def generate_rmat(self, scale, n, seed, a=0.57, b=0.19, c=0.19, permute=True, no_self_loops=False,
+                      first_edge=0, out=None):
+        import torch
+
+        src, dst = out if out is not None else (torch.empty(n, dtype=torch.int64, device=f"cuda:{self.device}"),
+                                                torch.empty(n, dtype=torch.int64, device=f"cuda:{self.device}"))
+        self._check(self._L.gs_generate_rmat(self.ctx, scale, n, seed, fx32(a), fx32(b), fx32(c), int(permute),
+                                             int(no_self_loops), first_edge, _ptr(src), _ptr(dst)))
+        return src, dst
+
+    def generate_uniform(self, num_vertices, n, seed, first_edge=0):
+        import torch
+
+        src = torch.empty(n, dtype=torch.int64, device=f"cuda:{self.device}")
+        dst = torch.empty(n, dtype=torch.int64, device=f"cuda:{self.device}")
+        self._check(self._L.gs_generate_uniform(self.ctx, num_vertices, n, seed, first_edge, _ptr(src), _ptr(dst)))
+        return src, dst
+
+    def generate_values(self, n, seed, dtype=L.GS_I64, first_edge=0):
+        import torch
+
+        tdt = {L.GS_I32: torch.int32, L.GS_I64: torch.int64, L.GS_F32: torch.float32, L.GS_F64: torch.float64}[dtype]
+        v = torch.empty(n, dtype=tdt, device=f"cuda:{self.device}")
+        self._check(self._L.gs_generate_values(self.ctx, n, seed, first_edge, dtype, _ptr(v)))
+        return v

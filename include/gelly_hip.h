@@ -1,0 +1,221 @@
+/*
+ * gelly_hip.h — C ABI of libgellyhip.so, the MI355X (gfx950) engine behind the
+ * per-tumbling-window neighbourhood path of gelly-streaming.
+ *
+ * The reference (Ren91/gelly-streaming, Java on Flink 1.0.3) has no native code.
+ * Its per-window path is
+ *
+ *   SimpleEdgeStream.slice(Time[, EdgeDirection])      SimpleEdgeStream.java:139-171
+ *     -> GraphWindowStream.reduceOnEdges(EdgesReduce)    GraphWindowStream.java:101-121
+ *     -> GraphWindowStream.foldNeighbors(init, EdgesFold) GraphWindowStream.java:62-87
+ *     -> GraphWindowStream.applyOnNeighbors(EdgesApply)  GraphWindowStream.java:130-182
+ *   and the WindowTriangles example                     example/WindowTriangles.java:51-140
+ *
+ * Flink runs those per (vertex, window) record by record.  This ABI takes ONE
+ * tumbling window as a columnar (SoA) edge batch and returns the per-vertex
+ * results for the whole window; the Java window-buffer operator described in
+ * INTEGRATION.md calls it once per window end.  Every entry point below names
+ * the reference interface it replaces.
+ *
+ * Conventions
+ *  - Plain C: no C++ or torch types cross this boundary.
+ *  - Nothing throws or aborts across the ABI.  Every call returns gs_status;
+ *    gs_last_error(ctx) holds the message of the last failure on that ctx.
+ *    The Java wrapper maps a non-zero status to an Exception, matching the
+ *    `throws Exception` of EdgesReduce.java:43 / EdgesFold.java:47 / EdgesApply.java:47.
+ *  - Buffers are caller-owned.  `mem` says whether a pointer is host memory
+ *    (pageable or from gs_alloc_pinned) or device memory (HBM) on ctx's device.
+ *    No pointer is retained after a call returns.
+ *  - A ctx is not re-entrant: one ctx per Flink subtask thread.  Distinct ctxs
+ *    are independent (own stream, own workspace).
+ *  - Keys are Java Long vertex IDs (int64).  Output keys are ascending.
+ */
+#ifndef GELLY_HIP_H
+#define GELLY_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GS_ABI_VERSION 1
+
+#if defined(__GNUC__) || defined(__clang__)
+#define GS_API __attribute__((visibility("default")))
+#else
+#define GS_API
+#endif
+
+typedef int32_t gs_status;
+enum {
+  GS_OK = 0,
+  GS_EINVAL = -1,       /* bad argument (null pointer, unknown enum, n too large)          */
+  GS_ECAPACITY = -2,    /* output capacity too small; *n_out holds the size needed          */
+  GS_EDEVICE = -3,      /* HIP runtime / kernel failure                                     */
+  GS_ECOMM = -4,        /* collective failure (multi-GPU)                                   */
+  GS_ENOMEM = -5,       /* device or pinned allocation failed                               */
+  GS_EUNSUPPORTED = -6  /* op/dtype combination not offered by the engine                   */
+};
+
+/* org.apache.flink.graph.EdgeDirection, same ordinals (IN, OUT, ALL).
+ * OUT: key = src, neighbour = dst            (SimpleEdgeStream.java:160-162)
+ * IN : key = dst, neighbour = src (reverse)  (SimpleEdgeStream.java:157-159, 332-341)
+ * ALL: both records, e then e.reverse(), in that arrival order (SimpleEdgeStream.java:163-167, 354-365) */
+typedef enum gs_dir { GS_DIR_IN = 0, GS_DIR_OUT = 1, GS_DIR_ALL = 2 } gs_dir;
+
+/* Built-in associative reducers that replace a user EdgesReduce / EdgesFold lambda.
+ * SUM/MIN/MAX fold the edge values of a vertex in its window (Java semantics:
+ * two's-complement wrap for I32/I64, Math.min/Math.max for floats, float sums
+ * within 1e-5 relative of the arrival-order fold).  COUNT yields the number of
+ * incident edge records (I64) and ignores values. */
+typedef enum gs_op { GS_OP_SUM = 0, GS_OP_MIN = 1, GS_OP_MAX = 2, GS_OP_COUNT = 3 } gs_op;
+
+/* Edge value type EV: Integer, Long, Float, Double, or NullValue (GS_NONE). */
+typedef enum gs_dtype { GS_I32 = 0, GS_I64 = 1, GS_F32 = 2, GS_F64 = 3, GS_NONE = 4 } gs_dtype;
+
+typedef enum gs_mem { GS_MEM_HOST = 0, GS_MEM_DEVICE = 1 } gs_mem;
+
+typedef struct gs_ctx gs_ctx;
+
+typedef struct gs_config {
+  int32_t device;          /* HIP device ordinal                                           */
+  uint32_t flags;          /* reserved, 0                                                  */
+  uint64_t reserve_edges;  /* pre-size the workspace for windows of this many edges (0 = lazy) */
+} gs_config;
+
+/* One tumbling window's edges, structure-of-arrays: Edge<Long, EV> = Tuple3(f0 src, f1 dst, f2 value).
+ * `val` may be NULL when val_dtype == GS_NONE (NullValue edges, e.g. WindowTriangles.java:185). */
+typedef struct gs_edge_batch {
+  const int64_t* src;
+  const int64_t* dst;
+  const void* val;
+  uint64_t n;              /* edges in the window (before direction expansion)             */
+  int32_t val_dtype;       /* gs_dtype                                                     */
+  int32_t mem;             /* gs_mem of src/dst/val                                        */
+  int64_t window_end_ms;   /* TimeWindow end; results carry end-1 (maxTimestamp)          */
+} gs_edge_batch;
+
+/* Per-vertex output: Tuple2<K, EV>(vertex, value) as emitted by reduceOnEdges' project(0, 2). */
+typedef struct gs_vertex_out {
+  int64_t* keys;           /* [capacity] ascending vertex IDs                              */
+  void* vals;              /* [capacity] values (batch dtype; I64 for COUNT)               */
+  uint64_t capacity;
+  uint64_t* n_out;         /* host pointer: number of vertices written / needed           */
+  int32_t mem;             /* gs_mem of keys/vals                                          */
+  int32_t reserved;
+} gs_vertex_out;
+
+/* Degree / max-neighbour fold output: (vertex, degree, max neighbour ID). */
+typedef struct gs_degree_out {
+  int64_t* keys;
+  int64_t* degree;
+  int64_t* max_neighbor;
+  uint64_t capacity;
+  uint64_t* n_out;
+  int32_t mem;
+  int32_t reserved;
+} gs_degree_out;
+
+/* Grouped neighbourhoods of one window (CSR), the input EdgesWindowFunction.apply
+ * hands to a user EdgesApply (GraphWindowStream.java:144-175): for vertex u,
+ * neighbours/values [offsets[u], offsets[u+1]) in arrival order, duplicates kept. */
+typedef struct gs_csr_out {
+  int64_t* keys;           /* [capacity_vertices]                                          */
+  uint64_t* offsets;       /* [capacity_vertices + 1]                                      */
+  int64_t* neighbors;      /* [capacity_records]                                           */
+  void* vals;              /* [capacity_records] or NULL                                   */
+  uint64_t capacity_vertices;
+  uint64_t capacity_records;
+  uint64_t* n_vertices;
+  uint64_t* n_records;
+  int32_t mem;
+  int32_t reserved;
+} gs_csr_out;
+
+/* Candidate records of WindowTriangles.GenerateCandidateEdges (WindowTriangles.java:83-116):
+ * Tuple3<Long, Long, Boolean>(a, b, isCandidate).  The flag is stored as one byte. */
+typedef struct gs_pair_out {
+  int64_t* a;
+  int64_t* b;
+  uint8_t* is_candidate;
+  uint64_t capacity;
+  uint64_t* n_out;         /* records written / needed (two-phase: call with capacity 0 to size) */
+  int32_t mem;
+  int32_t reserved;
+} gs_pair_out;
+
+/* ---- lifecycle ---------------------------------------------------------------------- */
+GS_API int32_t gs_abi_version(void);
+GS_API gs_status gs_create(const gs_config* cfg, gs_ctx** out);
+GS_API void gs_destroy(gs_ctx* ctx);
+GS_API const char* gs_last_error(const gs_ctx* ctx);
+/* Run this ctx's work on an existing hipStream_t (e.g. torch.cuda.current_stream()); NULL = the
+ * device's default stream.  gs_create gives each ctx a stream of its own until this is called. */
+GS_API gs_status gs_set_stream(gs_ctx* ctx, void* hip_stream);
+GS_API gs_status gs_synchronize(gs_ctx* ctx);
+GS_API void* gs_alloc_pinned(size_t bytes);
+GS_API void gs_free_pinned(void* p);
+
+/* ---- per-window neighbourhood operators ------------------------------------------- */
+
+/* Replaces GraphWindowStream.reduceOnEdges(EdgesReduce) (GraphWindowStream.java:101-121)
+ * with a built-in reducer: one (vertex, reduced value) per vertex with >=1 incident record. */
+GS_API gs_status gs_window_reduce(gs_ctx* ctx, const gs_edge_batch* batch, int32_t dir, int32_t op,
+                           gs_vertex_out* out);
+
+/* Replaces GraphWindowStream.foldNeighbors(initialValue, EdgesFold) (GraphWindowStream.java:62-87)
+ * for an associative fold over edge values: acc = op(... op(op(init, v1), v2) ...).
+ * `init` points to one host value of the batch dtype (I64 for COUNT). */
+GS_API gs_status gs_window_fold(gs_ctx* ctx, const gs_edge_batch* batch, int32_t dir, int32_t op,
+                         const void* init, gs_vertex_out* out);
+
+/* Replaces foldNeighbors with the degree / max-neighbour fold of TestSlice.java:233-239's shape:
+ * acc.f0 = vertex, acc.f1 += 1, acc.f2 = max(acc.f2, neighbour), starting from (v, 0, init_max). */
+GS_API gs_status gs_window_fold_degree_max(gs_ctx* ctx, const gs_edge_batch* batch, int32_t dir,
+                                    int64_t init_max, gs_degree_out* out);
+
+/* The grouping half of applyOnNeighbors (GraphWindowStream.java:130-175): the window's
+ * neighbourhoods as a CSR in arrival order, for a host-side user EdgesApply to iterate. */
+GS_API gs_status gs_window_csr(gs_ctx* ctx, const gs_edge_batch* batch, int32_t dir, gs_csr_out* out);
+
+/* applyOnNeighbors(GenerateCandidateEdges) on slice(ALL) (WindowTriangles.java:62-63, 83-116).
+ * Records per vertex v: (v, t, false) per neighbour record in arrival order, then the candidate
+ * pairs (ids[i], ids[j], true), i < len-1, j >= i, ids[i] > v, ids[j] > v, where ids is v's
+ * neighbour set in java.util.HashSet (JDK 8+) iteration order.  Vertices ascend. */
+GS_API gs_status gs_window_candidates(gs_ctx* ctx, const gs_edge_batch* batch, gs_pair_out* out);
+
+/* The whole WindowTriangles pipeline for one window (WindowTriangles.java:61-66):
+ * slice(ALL) -> GenerateCandidateEdges -> keyBy(0,1) CountTriangles -> timeWindowAll sum(0).
+ * *count is the exact 64-bit count; *count_ref_wrapped is the Integer the reference emits
+ * (mod 2^32 as signed).  *has_output = 0 when the window has no edge (no record is emitted). */
+GS_API gs_status gs_window_triangles(gs_ctx* ctx, const gs_edge_batch* batch, uint64_t* count,
+                              int32_t* count_ref_wrapped, int32_t* has_output);
+
+/* ---- synthetic streams (bit-identical to oracle/gs_oracle.c) ------------------------ */
+/* R-MAT: 2^scale vertices, probabilities a, b, c (d = 1-a-b-c) as 32-bit fixed point,
+ * optional seeded vertex permutation, optional self-loop removal (rewired, count kept). */
+GS_API gs_status gs_generate_rmat(gs_ctx* ctx, int32_t scale, uint64_t n, uint64_t seed, uint32_t a_fx,
+                           uint32_t b_fx, uint32_t c_fx, int32_t permute, int32_t no_self_loops,
+                           uint64_t first_edge, int64_t* src_dev, int64_t* dst_dev);
+/* Uniform: src, dst in [0, V), dst != src. */
+GS_API gs_status gs_generate_uniform(gs_ctx* ctx, uint64_t num_vertices, uint64_t n, uint64_t seed,
+                              uint64_t first_edge, int64_t* src_dev, int64_t* dst_dev);
+/* Edge values: I64 = splitmix64(seed, i) & 0xFFFF; F64 = top 53 bits / 2^53; I32/F32 likewise. */
+GS_API gs_status gs_generate_values(gs_ctx* ctx, uint64_t n, uint64_t seed, uint64_t first_edge,
+                             int32_t dtype, void* val_dev);
+
+/* ---- instrumentation ----------------------------------------------------------------- */
+/* Wall time (ms, device events on ctx's stream) of each stage of the last window call. */
+typedef struct gs_stage_times {
+  float keyinfo_ms, sort_ms, reduce_ms, total_ms;
+  uint32_t sort_passes, key_bits;
+  uint64_t records, vertices;
+} gs_stage_times;
+GS_API gs_status gs_last_stage_times(const gs_ctx* ctx, gs_stage_times* out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GELLY_HIP_H */

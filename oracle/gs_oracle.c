@@ -1,0 +1,706 @@
+/*
+ * gs_oracle.c — CPU restatement of gelly-streaming's per-window neighbourhood path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  Only tests/, __graft_entry__.smoke() and bench.py's
+ * cpu_baseline leg may load this library, and only as the checker / the timed CPU
+ * baseline.  The product path (gelly-streaming_amd + libgellyhip.so) never calls it.
+ *
+ * Parity pinning: the reference is Java on Flink 1.0.3 and cannot be compiled or run in
+ * this container (no JDK, no Flink jars, no network).  This restatement is
+ * pinned by the reference's own fixtures, extracted into tests/golden/ by
+ * tests/golden/extract_reference_fixtures.py:
+ *   - TestSlice.java:70-229 (9 goldens: fold/reduce/apply x OUT/IN/ALL on the 7-edge graph
+ *     of GraphStreamTestUtils.java:56-67),
+ *   - TestReverse / TestUndirected (direction expansion),
+ *   - WindowTrianglesITCase + ExamplesTestData.java:21-34 (3 windows of 400 ms).
+ * Large-scale behaviour is cross-checked between two independent triangle algorithms
+ * (the reference's candidate rule vs. the forward algorithm) in tests/.
+ *
+ * Semantics restated (file:line in /root/reference/src/main/java/org/apache/flink/graph/streaming):
+ *   direction expansion   SimpleEdgeStream.java:153-171 (OUT key=src; IN reverse() :332-341;
+ *                         ALL undirected() :354-365 emits e then e.reverse())
+ *   key selection         SimpleEdgeStream.java:173-183 (f0 of the expanded edge)
+ *   reduceOnEdges         GraphWindowStream.java:101-121: left fold of values in arrival order,
+ *                         output (vertex, value) after project(0, 2)
+ *   foldNeighbors         GraphWindowStream.java:62-87: acc = f(acc, vertex, neighbour, value)
+ *   applyOnNeighbors      GraphWindowStream.java:130-175: neighbours (f1, f2) in arrival order
+ *   GenerateCandidateEdges example/WindowTriangles.java:83-116 (HashSet order, j >= i, i < len-1)
+ *   CountTriangles        example/WindowTriangles.java:119-140 (int counters, emit iff edges > 0)
+ *   timeWindowAll.sum(0)  example/WindowTriangles.java:66 (Integer sum, wraps mod 2^32)
+ *
+ * Arithmetic follows Java: Integer/Long sums wrap (done in unsigned arithmetic),
+ * Float/Double sums are IEEE adds in arrival order, min/max follow Math.min/Math.max.
+ */
+#include <math.h>
+#include <pthread.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#define GSO_API __attribute__((visibility("default")))
+
+enum { DIR_IN = 0, DIR_OUT = 1, DIR_ALL = 2 };            /* EdgeDirection ordinals */
+enum { OP_SUM = 0, OP_MIN = 1, OP_MAX = 2, OP_COUNT = 3 };
+enum { DT_I32 = 0, DT_I64 = 1, DT_F32 = 2, DT_F64 = 3, DT_NONE = 4 };
+
+/* ------------------------------------------------------------------------------------ */
+/* counter-based RNG + synthetic streams (bit-identical to gelly-streaming_amd/csrc/gen) */
+/* ------------------------------------------------------------------------------------ */
+GSO_API uint64_t gso_splitmix64(uint64_t seed, uint64_t i) {
+  uint64_t z = seed + (i + 1) * 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+static uint64_t perm_vertex(uint64_t x, int scale, uint64_t seed) {
+  /* bijection on [0, 2^scale): 3 rounds of odd-multiply + xorshift, all mod 2^scale */
+  const uint64_t mask = (scale >= 64) ? ~0ull : ((1ull << scale) - 1);
+  const uint64_t k0 = gso_splitmix64(seed, 0x51) | 1ull, k1 = gso_splitmix64(seed, 0x52) | 1ull;
+  const uint64_t a0 = gso_splitmix64(seed, 0x53), a1 = gso_splitmix64(seed, 0x54);
+  const int sh = scale > 1 ? (scale + 1) / 2 : 1;
+  x = (x * k0 + a0) & mask;
+  x ^= x >> sh;
+  x = (x * k1 + a1) & mask;
+  x ^= x >> sh;
+  x = (x * k0 + a1) & mask;
+  return x;
+}
+
+/* R-MAT edge i: one 32-bit uniform per level (2 levels per splitmix64 call). */
+static void rmat_edge(int scale, uint64_t seed, uint32_t a, uint32_t ab, uint32_t abc, uint64_t i,
+                      uint64_t* s, uint64_t* d) {
+  uint64_t u = 0, v = 0, r = 0;
+  for (int l = 0; l < scale; ++l) {
+    if ((l & 1) == 0) r = gso_splitmix64(seed, i * (uint64_t)((scale + 1) / 2) + (uint64_t)(l >> 1));
+    const uint32_t x = (l & 1) ? (uint32_t)(r >> 32) : (uint32_t)r;
+    const uint64_t sb = (x >= ab), db = (x >= a && x < ab) || (x >= abc);
+    u = (u << 1) | sb;
+    v = (v << 1) | db;
+  }
+  *s = u;
+  *d = v;
+}
+
+GSO_API void gso_gen_rmat(int scale, uint64_t n, uint64_t seed, uint32_t a_fx, uint32_t b_fx,
+                          uint32_t c_fx, int permute, int no_self_loops, uint64_t first_edge,
+                          int64_t* src, int64_t* dst) {
+  const uint32_t a = a_fx, ab = a_fx + b_fx, abc = a_fx + b_fx + c_fx;
+  const uint64_t V = 1ull << scale;
+  for (uint64_t k = 0; k < n; ++k) {
+    const uint64_t i = first_edge + k;
+    uint64_t s, d;
+    rmat_edge(scale, seed, a, ab, abc, i, &s, &d);
+    if (no_self_loops && s == d) d = (s + 1 + gso_splitmix64(seed ^ 0x5E1F100Bull, i) % (V - 1)) & (V - 1);
+    if (permute) { s = perm_vertex(s, scale, seed); d = perm_vertex(d, scale, seed); }
+    src[k] = (int64_t)s;
+    dst[k] = (int64_t)d;
+  }
+}
+
+GSO_API void gso_gen_uniform(uint64_t V, uint64_t n, uint64_t seed, uint64_t first_edge, int64_t* src,
+                             int64_t* dst) {
+  for (uint64_t k = 0; k < n; ++k) {
+    const uint64_t i = first_edge + k;
+    const uint64_t s = gso_splitmix64(seed, 2 * i) % V;
+    const uint64_t d = (s + 1 + gso_splitmix64(seed, 2 * i + 1) % (V - 1)) % V;
+    src[k] = (int64_t)s;
+    dst[k] = (int64_t)d;
+  }
+}
+
+GSO_API void gso_gen_values(uint64_t n, uint64_t seed, uint64_t first_edge, int dtype, void* val) {
+  for (uint64_t k = 0; k < n; ++k) {
+    const uint64_t r = gso_splitmix64(seed ^ 0xA5A5A5A5F00DF00Dull, first_edge + k);
+    switch (dtype) {
+      case DT_I32: ((int32_t*)val)[k] = (int32_t)(r & 0xFFFF); break;
+      case DT_I64: ((int64_t*)val)[k] = (int64_t)(r & 0xFFFF); break;
+      case DT_F32: ((float*)val)[k] = (float)(r >> 40) * (1.0f / 16777216.0f); break;
+      case DT_F64: ((double*)val)[k] = (double)(r >> 11) * (1.0 / 9007199254740992.0); break;
+      default: break;
+    }
+  }
+}
+
+/* ------------------------------------------------------------------------------------ */
+/* direction expansion: record r of the keyed stream                                    */
+/* ------------------------------------------------------------------------------------ */
+static inline uint64_t n_records(uint64_t n, int dir) { return dir == DIR_ALL ? 2 * n : n; }
+/* returns edge index; sets key / neighbour of record r (ALL: r = 2i is e, r = 2i+1 is e.reverse()) */
+static inline uint64_t record(const int64_t* src, const int64_t* dst, int dir, uint64_t r, int64_t* key,
+                              int64_t* nbr) {
+  uint64_t i = r;
+  int rev = (dir == DIR_IN);
+  if (dir == DIR_ALL) { i = r >> 1; rev = (int)(r & 1); }
+  *key = rev ? dst[i] : src[i];
+  *nbr = rev ? src[i] : dst[i];
+  return i;
+}
+
+/* ------------------------------------------------------------------------------------ */
+/* open-addressing map vertex -> slot (slots in first-arrival order)                    */
+/* ------------------------------------------------------------------------------------ */
+typedef struct {
+  uint64_t cap;   /* power of two */
+  int64_t* keys;
+  int64_t* slot;  /* -1 empty */
+  uint64_t size;
+} vmap;
+
+static uint64_t mix64(uint64_t x) {
+  x ^= x >> 33; x *= 0xff51afd7ed558ccdull; x ^= x >> 33; x *= 0xc4ceb9fe1a85ec53ull; x ^= x >> 33;
+  return x;
+}
+static int vmap_init(vmap* m, uint64_t expect) {
+  uint64_t c = 16;
+  while (c < 2 * expect + 2) c <<= 1;
+  m->cap = c;
+  m->size = 0;
+  m->keys = (int64_t*)malloc(c * sizeof(int64_t));
+  m->slot = (int64_t*)malloc(c * sizeof(int64_t));
+  if (!m->keys || !m->slot) return -1;
+  memset(m->slot, 0xff, c * sizeof(int64_t));
+  return 0;
+}
+static void vmap_free(vmap* m) { free(m->keys); free(m->slot); }
+/* returns slot; *is_new set when inserted */
+static inline int64_t vmap_get(vmap* m, int64_t k, int* is_new) {
+  uint64_t h = mix64((uint64_t)k) & (m->cap - 1);
+  for (;;) {
+    if (m->slot[h] < 0) {
+      m->keys[h] = k;
+      m->slot[h] = (int64_t)m->size++;
+      *is_new = 1;
+      return m->slot[h];
+    }
+    if (m->keys[h] == k) { *is_new = 0; return m->slot[h]; }
+    h = (h + 1) & (m->cap - 1);
+  }
+}
+
+/* ------------------------------------------------------------------------------------ */
+/* Java arithmetic                                                                        */
+/* ------------------------------------------------------------------------------------ */
+static inline double java_min_d(double a, double b) {
+  if (a != a) return a;
+  if (a == 0.0 && b == 0.0 && signbit(b)) return b;
+  return (a <= b) ? a : b;
+}
+static inline double java_max_d(double a, double b) {
+  if (a != a) return a;
+  if (a == 0.0 && b == 0.0 && signbit(a)) return b;
+  return (a >= b) ? a : b;
+}
+static inline float java_min_f(float a, float b) {
+  if (a != a) return a;
+  if (a == 0.0f && b == 0.0f && signbit(b)) return b;
+  return (a <= b) ? a : b;
+}
+static inline float java_max_f(float a, float b) {
+  if (a != a) return a;
+  if (a == 0.0f && b == 0.0f && signbit(a)) return b;
+  return (a >= b) ? a : b;
+}
+
+/* acc (8 bytes, typed by dtype) = op(acc, value of edge i) */
+static inline void apply_op(int op, int dtype, uint64_t* acc, const void* val, uint64_t i) {
+  switch (dtype) {
+    case DT_I32: {
+      int32_t a = (int32_t)(uint32_t)*acc, v = ((const int32_t*)val)[i];
+      if (op == OP_SUM) a = (int32_t)((uint32_t)a + (uint32_t)v);
+      else if (op == OP_MIN) a = v < a ? v : a;
+      else if (op == OP_MAX) a = v > a ? v : a;
+      *acc = (uint32_t)a;
+      break;
+    }
+    case DT_I64: {
+      int64_t a = (int64_t)*acc, v = ((const int64_t*)val)[i];
+      if (op == OP_SUM) a = (int64_t)((uint64_t)a + (uint64_t)v);
+      else if (op == OP_MIN) a = v < a ? v : a;
+      else if (op == OP_MAX) a = v > a ? v : a;
+      *acc = (uint64_t)a;
+      break;
+    }
+    case DT_F32: {
+      float a, v = ((const float*)val)[i];
+      uint32_t bits = (uint32_t)*acc;
+      memcpy(&a, &bits, 4);
+      if (op == OP_SUM) a = a + v;
+      else if (op == OP_MIN) a = java_min_f(a, v);
+      else if (op == OP_MAX) a = java_max_f(a, v);
+      memcpy(&bits, &a, 4);
+      *acc = bits;
+      break;
+    }
+    case DT_F64: {
+      double a, v = ((const double*)val)[i];
+      memcpy(&a, acc, 8);
+      if (op == OP_SUM) a = a + v;
+      else if (op == OP_MIN) a = java_min_d(a, v);
+      else if (op == OP_MAX) a = java_max_d(a, v);
+      memcpy(acc, &a, 8);
+      break;
+    }
+  }
+}
+static inline uint64_t load_val(int dtype, const void* val, uint64_t i) {
+  uint64_t r = 0;
+  switch (dtype) {
+    case DT_I32: r = (uint32_t)((const int32_t*)val)[i]; break;
+    case DT_I64: r = (uint64_t)((const int64_t*)val)[i]; break;
+    case DT_F32: memcpy(&r, (const float*)val + i, 4); break;
+    case DT_F64: memcpy(&r, (const double*)val + i, 8); break;
+  }
+  return r;
+}
+static inline size_t dt_size(int dtype) { return (dtype == DT_I32 || dtype == DT_F32) ? 4 : 8; }
+static inline void store_val(int dtype, void* out, uint64_t j, uint64_t bits) {
+  if (dt_size(dtype) == 4) ((uint32_t*)out)[j] = (uint32_t)bits;
+  else ((uint64_t*)out)[j] = bits;
+}
+
+/* sort (key, slot) pairs by key so outputs ascend like the engine's */
+typedef struct { int64_t k; int64_t s; } kv;
+static int cmp_kv(const void* a, const void* b) {
+  const int64_t x = ((const kv*)a)->k, y = ((const kv*)b)->k;
+  return (x > y) - (x < y);
+}
+static kv* sorted_slots(vmap* m) {
+  kv* p = (kv*)malloc((m->size ? m->size : 1) * sizeof(kv));
+  uint64_t j = 0;
+  for (uint64_t h = 0; h < m->cap; ++h)
+    if (m->slot[h] >= 0) { p[j].k = m->keys[h]; p[j].s = m->slot[h]; ++j; }
+  qsort(p, m->size, sizeof(kv), cmp_kv);
+  return p;
+}
+
+/* ------------------------------------------------------------------------------------ */
+/* reduceOnEdges / foldNeighbors with a built-in associative op                          */
+/* ------------------------------------------------------------------------------------ */
+/* has_init = 0: reduceOnEdges (acc starts at the first value, GraphWindowStream.java:116-120)
+ * has_init = 1: foldNeighbors (acc starts at a copy of init, GraphWindowStream.java:62-80)
+ * COUNT: acc is an Int64 count (init + number of records).  Returns U, or -1 when cap < U. */
+static int64_t window_fold(const int64_t* src, const int64_t* dst, const void* val, uint64_t n,
+                           int dtype, int dir, int op, int has_init, uint64_t init_bits,
+                           int64_t* out_keys, void* out_vals, uint64_t cap) {
+  const uint64_t R = n_records(n, dir);
+  vmap m;
+  if (vmap_init(&m, R < 1024 ? R : R / 2) != 0) return -2;
+  uint64_t* acc = (uint64_t*)malloc((R ? R : 1) * sizeof(uint64_t));
+  for (uint64_t r = 0; r < R; ++r) {
+    int64_t key, nbr;
+    const uint64_t i = record(src, dst, dir, r, &key, &nbr);
+    int is_new;
+    const int64_t s = vmap_get(&m, key, &is_new);
+    if (op == OP_COUNT) {
+      if (is_new) acc[s] = has_init ? init_bits : 0;
+      acc[s] += 1;
+    } else if (is_new && !has_init) {
+      acc[s] = load_val(dtype, val, i);
+    } else {
+      if (is_new) acc[s] = init_bits;
+      apply_op(op, dtype, &acc[s], val, i);
+    }
+  }
+  const uint64_t U = m.size;
+  if (U <= cap) {
+    kv* p = sorted_slots(&m);
+    const int odt = (op == OP_COUNT) ? DT_I64 : dtype;
+    for (uint64_t j = 0; j < U; ++j) {
+      out_keys[j] = p[j].k;
+      store_val(odt, out_vals, j, acc[p[j].s]);
+    }
+    free(p);
+  }
+  free(acc);
+  vmap_free(&m);
+  return U <= cap ? (int64_t)U : -1 - (int64_t)U;
+}
+
+GSO_API int64_t gso_window_reduce(const int64_t* src, const int64_t* dst, const void* val, uint64_t n,
+                                  int dtype, int dir, int op, int64_t* out_keys, void* out_vals,
+                                  uint64_t cap) {
+  return window_fold(src, dst, val, n, dtype, dir, op, 0, 0, out_keys, out_vals, cap);
+}
+
+GSO_API int64_t gso_window_fold(const int64_t* src, const int64_t* dst, const void* val, uint64_t n,
+                                int dtype, int dir, int op, const void* init, int64_t* out_keys,
+                                void* out_vals, uint64_t cap) {
+  const uint64_t ib = (op == OP_COUNT) ? (uint64_t)*(const int64_t*)init : load_val(dtype, init, 0);
+  return window_fold(src, dst, val, n, dtype, dir, op, 1, ib, out_keys, out_vals, cap);
+}
+
+/* foldNeighbors(new Tuple3(0, 0, init_max), degree/max-neighbour fold) — TestSlice.java:233-239 shape */
+GSO_API int64_t gso_window_fold_degree_max(const int64_t* src, const int64_t* dst, uint64_t n, int dir,
+                                           int64_t init_max, int64_t* out_keys, int64_t* out_deg,
+                                           int64_t* out_max, uint64_t cap) {
+  const uint64_t R = n_records(n, dir);
+  vmap m;
+  if (vmap_init(&m, R < 1024 ? R : R / 2) != 0) return -2;
+  int64_t* deg = (int64_t*)malloc((R ? R : 1) * sizeof(int64_t));
+  int64_t* mx = (int64_t*)malloc((R ? R : 1) * sizeof(int64_t));
+  for (uint64_t r = 0; r < R; ++r) {
+    int64_t key, nbr;
+    record(src, dst, dir, r, &key, &nbr);
+    int is_new;
+    const int64_t s = vmap_get(&m, key, &is_new);
+    if (is_new) { deg[s] = 0; mx[s] = init_max; }
+    deg[s] += 1;
+    if (nbr > mx[s]) mx[s] = nbr;
+  }
+  const uint64_t U = m.size;
+  if (U <= cap) {
+    kv* p = sorted_slots(&m);
+    for (uint64_t j = 0; j < U; ++j) {
+      out_keys[j] = p[j].k;
+      out_deg[j] = deg[p[j].s];
+      out_max[j] = mx[p[j].s];
+    }
+    free(p);
+  }
+  free(deg); free(mx); vmap_free(&m);
+  return U <= cap ? (int64_t)U : -1 - (int64_t)U;
+}
+
+/* ------------------------------------------------------------------------------------ */
+/* applyOnNeighbors grouping: CSR in arrival order (GraphWindowStream.java:144-175)      */
+/* ------------------------------------------------------------------------------------ */
+GSO_API int64_t gso_window_csr(const int64_t* src, const int64_t* dst, const void* val, uint64_t n,
+                               int dtype, int dir, int64_t* keys, uint64_t* offsets, int64_t* nbrs,
+                               void* vals, uint64_t cap_v) {
+  const uint64_t R = n_records(n, dir);
+  vmap m;
+  if (vmap_init(&m, R < 1024 ? R : R / 2) != 0) return -2;
+  int64_t* slot_of = (int64_t*)malloc((R ? R : 1) * sizeof(int64_t));
+  uint64_t* cnt = (uint64_t*)calloc(R ? R : 1, sizeof(uint64_t));
+  for (uint64_t r = 0; r < R; ++r) {
+    int64_t key, nbr;
+    record(src, dst, dir, r, &key, &nbr);
+    int is_new;
+    slot_of[r] = vmap_get(&m, key, &is_new);
+    cnt[slot_of[r]]++;
+  }
+  const uint64_t U = m.size;
+  if (U <= cap_v) {
+    kv* p = sorted_slots(&m);
+    uint64_t* start = (uint64_t*)malloc((U ? U : 1) * sizeof(uint64_t));
+    uint64_t off = 0;
+    for (uint64_t j = 0; j < U; ++j) {
+      keys[j] = p[j].k;
+      offsets[j] = off;
+      start[p[j].s] = off;
+      off += cnt[p[j].s];
+    }
+    offsets[U] = off;
+    for (uint64_t r = 0; r < R; ++r) {
+      int64_t key, nbr;
+      const uint64_t i = record(src, dst, dir, r, &key, &nbr);
+      const uint64_t o = start[slot_of[r]]++;
+      nbrs[o] = nbr;
+      if (vals && dtype != DT_NONE) store_val(dtype, vals, o, load_val(dtype, val, i));
+    }
+    free(start);
+    free(p);
+  }
+  free(slot_of); free(cnt); vmap_free(&m);
+  return U <= cap_v ? (int64_t)U : -1 - (int64_t)U;
+}
+
+/* ------------------------------------------------------------------------------------ */
+/* java.util.HashSet<Long> iteration order (JDK 8+ HashMap, list bins)                   */
+/* ------------------------------------------------------------------------------------ */
+/* HashSet() -> HashMap(16, 0.75): table doubles when ++size > 0.75*cap.  Long.hashCode =
+ * (int)(x ^ (x >>> 32)); HashMap.hash spreads h ^ (h >>> 16); bucket = hash & (cap-1).
+ * Iteration walks buckets 0..cap-1, each bin in insertion order (resize splits preserve
+ * order).  Bins that would treeify (>= 9 entries at cap >= 64) are reported via *treeified. */
+GSO_API uint64_t gso_java_hashset_cap(uint64_t k) {
+  uint64_t cap = 16;
+  while ((double)k > 0.75 * (double)cap) cap <<= 1;
+  return cap;
+}
+GSO_API uint32_t gso_java_long_bucket(int64_t x, uint64_t cap) {
+  const uint32_t h = (uint32_t)((uint64_t)x ^ ((uint64_t)x >> 32));
+  return (h ^ (h >> 16)) & (uint32_t)(cap - 1);
+}
+typedef struct { uint32_t b; uint32_t ord; int64_t x; } hsent;
+static int cmp_hs(const void* a, const void* b) {
+  const hsent* p = (const hsent*)a; const hsent* q = (const hsent*)b;
+  if (p->b != q->b) return p->b < q->b ? -1 : 1;
+  return (p->ord > q->ord) - (p->ord < q->ord);
+}
+/* distinct[] in first-arrival order -> ids[] in HashSet iteration order; returns 1 if a bin treeifies */
+static int hashset_order(const int64_t* distinct, uint64_t k, int64_t* ids, hsent* tmp) {
+  const uint64_t cap = gso_java_hashset_cap(k);
+  for (uint64_t j = 0; j < k; ++j) {
+    tmp[j].b = gso_java_long_bucket(distinct[j], cap);
+    tmp[j].ord = (uint32_t)j;
+    tmp[j].x = distinct[j];
+  }
+  qsort(tmp, k, sizeof(hsent), cmp_hs);
+  int tree = 0;
+  uint64_t run = 0;
+  for (uint64_t j = 0; j < k; ++j) {
+    ids[j] = tmp[j].x;
+    run = (j > 0 && tmp[j].b == tmp[j - 1].b) ? run + 1 : 1;
+    if (run >= 9 && cap >= 64) tree = 1;
+  }
+  return tree;
+}
+
+/* per-vertex distinct neighbours (first arrival order) from the CSR */
+typedef struct {
+  uint64_t U, R;
+  int64_t* keys; uint64_t* off; int64_t* nbr;
+} csr_t;
+static int build_csr_all(const int64_t* src, const int64_t* dst, uint64_t n, csr_t* c) {
+  c->R = 2 * n;
+  c->keys = (int64_t*)malloc((c->R + 1) * sizeof(int64_t));
+  c->off = (uint64_t*)malloc((c->R + 2) * sizeof(uint64_t));
+  c->nbr = (int64_t*)malloc((c->R + 1) * sizeof(int64_t));
+  const int64_t u = gso_window_csr(src, dst, NULL, n, DT_NONE, DIR_ALL, c->keys, c->off, c->nbr, NULL,
+                                   c->R + 1);
+  c->U = (uint64_t)u;
+  return u < 0 ? -1 : 0;
+}
+static void free_csr(csr_t* c) { free(c->keys); free(c->off); free(c->nbr); }
+
+static uint64_t distinct_of(const int64_t* nb, uint64_t d, int64_t* out) {
+  /* first-arrival distinct; d is small in the oracle's test sizes -> local map */
+  vmap m;
+  vmap_init(&m, d);
+  uint64_t k = 0;
+  for (uint64_t j = 0; j < d; ++j) {
+    int is_new;
+    vmap_get(&m, nb[j], &is_new);
+    if (is_new) out[k++] = nb[j];
+  }
+  vmap_free(&m);
+  return k;
+}
+
+/* applyOnNeighbors(GenerateCandidateEdges) over slice(ALL) — WindowTriangles.java:83-116.
+ * Writes records in vertex-ascending order; returns the record count (or -1-needed when cap short).
+ * *treeified = 1 if some neighbour set would use a tree bin (iteration order then unpinned). */
+GSO_API int64_t gso_window_candidates(const int64_t* src, const int64_t* dst, uint64_t n, int64_t* a,
+                                      int64_t* b, uint8_t* flag, uint64_t cap, int* treeified) {
+  csr_t c;
+  if (build_csr_all(src, dst, n, &c) != 0) return -2;
+  int64_t* dist = (int64_t*)malloc((c.R + 1) * sizeof(int64_t));
+  int64_t* ids = (int64_t*)malloc((c.R + 1) * sizeof(int64_t));
+  hsent* tmp = (hsent*)malloc((c.R + 1) * sizeof(hsent));
+  uint64_t o = 0;
+  *treeified = 0;
+  for (uint64_t u = 0; u < c.U; ++u) {
+    const int64_t v = c.keys[u];
+    const uint64_t lo = c.off[u], hi = c.off[u + 1];
+    for (uint64_t j = lo; j < hi; ++j) {  /* (v, t, false) per neighbour record :96-100 */
+      if (o < cap) { a[o] = v; b[o] = c.nbr[j]; flag[o] = 0; }
+      ++o;
+    }
+    const uint64_t k = distinct_of(c.nbr + lo, hi - lo, dist);
+    *treeified |= hashset_order(dist, k, ids, tmp);
+    for (uint64_t i = 0; i + 1 < k; ++i)          /* i < len-1 :104 */
+      for (uint64_t j = i; j < k; ++j)            /* j = i (self pair) :105 */
+        if (ids[i] > v && ids[j] > v) {           /* :108 */
+          if (o < cap) { a[o] = ids[i]; b[o] = ids[j]; flag[o] = 1; }
+          ++o;
+        }
+  }
+  free(dist); free(ids); free(tmp); free_csr(&c);
+  return o <= cap ? (int64_t)o : -1 - (int64_t)o;
+}
+
+/* ------------------------------------------------------------------------------------ */
+/* WindowTriangles, reference rule: candidates -> keyBy(0,1) CountTriangles -> sum(0)    */
+/* ------------------------------------------------------------------------------------ */
+typedef struct { int64_t a, b; uint8_t f; } rec3;
+static int cmp_rec(const void* x, const void* y) {
+  const rec3* p = (const rec3*)x; const rec3* q = (const rec3*)y;
+  if (p->a != q->a) return p->a < q->a ? -1 : 1;
+  if (p->b != q->b) return p->b < q->b ? -1 : 1;
+  return 0;
+}
+/* Returns the Integer the reference emits (WindowTriangles.java:126-137, :66) and *exact. */
+GSO_API int32_t gso_window_triangles_ref(const int64_t* src, const int64_t* dst, uint64_t n,
+                                         uint64_t* exact, int* has_output, int* treeified) {
+  *exact = 0; *has_output = 0;
+  if (n == 0) return 0;
+  int64_t need = gso_window_candidates(src, dst, n, NULL, NULL, NULL, 0, treeified);
+  const uint64_t P = (uint64_t)(-1 - need);
+  int64_t* a = (int64_t*)malloc(P * sizeof(int64_t));
+  int64_t* b = (int64_t*)malloc(P * sizeof(int64_t));
+  uint8_t* f = (uint8_t*)malloc(P);
+  gso_window_candidates(src, dst, n, a, b, f, P, treeified);
+  rec3* r = (rec3*)malloc(P * sizeof(rec3));
+  for (uint64_t i = 0; i < P; ++i) { r[i].a = a[i]; r[i].b = b[i]; r[i].f = f[i]; }
+  qsort(r, P, sizeof(rec3), cmp_rec);
+  uint32_t sum = 0;   /* Integer sum, wraps */
+  uint64_t ex = 0;
+  for (uint64_t i = 0; i < P;) {
+    uint64_t j = i;
+    uint32_t cand = 0, edges = 0;
+    uint64_t cand64 = 0;
+    while (j < P && r[j].a == r[i].a && r[j].b == r[i].b) {
+      if (r[j].f) { cand++; cand64++; } else edges++;
+      ++j;
+    }
+    if (edges > 0) { sum += cand; ex += cand64; *has_output = 1; }
+    i = j;
+  }
+  free(a); free(b); free(f); free(r);
+  *exact = ex;
+  return (int32_t)sum;
+}
+
+/* ------------------------------------------------------------------------------------ */
+/* WindowTriangles, forward algorithm (independent check; scales to millions of edges)   */
+/* ------------------------------------------------------------------------------------ */
+static int cmp_i64(const void* x, const void* y) {
+  const int64_t p = *(const int64_t*)x, q = *(const int64_t*)y;
+  return (p > q) - (p < q);
+}
+/* count = T (triangles of the simple undirected graph, each once) + S (self-pair quirk:
+ * for each v, each distinct neighbour x > v that has a self-loop, except the last element
+ * of v's HashSet order).  Same value as gso_window_triangles_ref. */
+GSO_API int32_t gso_window_triangles_fwd(const int64_t* src, const int64_t* dst, uint64_t n,
+                                         uint64_t* exact, int* has_output) {
+  *exact = 0; *has_output = (n > 0);
+  if (n == 0) return 0;
+  csr_t c;
+  if (build_csr_all(src, dst, n, &c) != 0) return 0;
+  /* distinct neighbour lists (sorted), self-loop flags */
+  uint64_t* doff = (uint64_t*)malloc((c.U + 1) * sizeof(uint64_t));
+  int64_t* dn = (int64_t*)malloc((c.R + 1) * sizeof(int64_t));
+  uint8_t* loop = (uint8_t*)calloc(c.U + 1, 1);
+  int64_t* dist = (int64_t*)malloc((c.R + 1) * sizeof(int64_t));
+  int64_t* ids = (int64_t*)malloc((c.R + 1) * sizeof(int64_t));
+  hsent* tmp = (hsent*)malloc((c.R + 1) * sizeof(hsent));
+  uint64_t S = 0, o = 0;
+  for (uint64_t u = 0; u < c.U; ++u) {
+    const int64_t v = c.keys[u];
+    const uint64_t lo = c.off[u], hi = c.off[u + 1];
+    const uint64_t k = distinct_of(c.nbr + lo, hi - lo, dist);
+    doff[u] = o;
+    for (uint64_t j = 0; j < k; ++j) {
+      if (dist[j] == v) loop[u] = 1;
+      else dn[o++] = dist[j];
+    }
+    qsort(dn + doff[u], o - doff[u], sizeof(int64_t), cmp_i64);
+  }
+  doff[c.U] = o;
+  /* self-loop lookup by binary search over keys */
+  for (uint64_t u = 0; u < c.U; ++u) {
+    const int64_t v = c.keys[u];
+    const uint64_t lo = c.off[u], hi = c.off[u + 1];
+    const uint64_t k = distinct_of(c.nbr + lo, hi - lo, dist);
+    if (k < 2) continue;
+    hashset_order(dist, k, ids, tmp);
+    for (uint64_t i = 0; i + 1 < k; ++i) {
+      if (ids[i] <= v) continue;
+      int64_t* pos = (int64_t*)bsearch(&ids[i], c.keys, c.U, sizeof(int64_t), cmp_i64);
+      if (pos && loop[pos - c.keys]) S++;
+    }
+  }
+  /* T: for each u, for neighbours v > u, count w > v in N(u) ∩ N(v) */
+  uint64_t T = 0;
+  for (uint64_t u = 0; u < c.U; ++u) {
+    const int64_t uk = c.keys[u];
+    for (uint64_t p = doff[u]; p < doff[u + 1]; ++p) {
+      const int64_t vk = dn[p];
+      if (vk <= uk) continue;
+      int64_t* pos = (int64_t*)bsearch(&vk, c.keys, c.U, sizeof(int64_t), cmp_i64);
+      const uint64_t v = (uint64_t)(pos - c.keys);
+      uint64_t x = p + 1, y = doff[v];
+      while (x < doff[u + 1] && y < doff[v + 1]) {
+        if (dn[x] < dn[y]) ++x;
+        else if (dn[x] > dn[y]) ++y;
+        else { if (dn[x] > vk) T++; ++x; ++y; }
+      }
+    }
+  }
+  free(doff); free(dn); free(loop); free(dist); free(ids); free(tmp); free_csr(&c);
+  *exact = T + S;
+  return (int32_t)(uint32_t)(T + S);
+}
+
+/* ------------------------------------------------------------------------------------ */
+/* CPU baseline: keyBy(vertex) over P threads + per-subtask hash-map fold (bench only)  */
+/* ------------------------------------------------------------------------------------ */
+typedef struct {
+  const int64_t* src; const int64_t* dst; const void* val;
+  uint64_t n; int dtype, dir, op, P, tid;
+  /* phase 1 output: per (producer, consumer) record index lists */
+  uint64_t** part; uint64_t* part_n;   /* [P*P] */
+  uint64_t vertices;
+  pthread_barrier_t* bar;
+} bl_arg;
+
+static void* bl_worker(void* p) {
+  bl_arg* A = (bl_arg*)p;
+  const int P = A->P, t = A->tid;
+  const uint64_t R = n_records(A->n, A->dir);
+  const uint64_t lo = R * (uint64_t)t / (uint64_t)P, hi = R * (uint64_t)(t + 1) / (uint64_t)P;
+  /* phase 1: this source subtask routes its records by hash(key) % P (the keyBy shuffle) */
+  uint64_t* cnt = (uint64_t*)calloc((size_t)P, sizeof(uint64_t));
+  for (uint64_t r = lo; r < hi; ++r) {
+    int64_t key, nbr;
+    record(A->src, A->dst, A->dir, r, &key, &nbr);
+    cnt[mix64((uint64_t)key) % (uint64_t)P]++;
+  }
+  for (int q = 0; q < P; ++q) {
+    A->part[t * P + q] = (uint64_t*)malloc((cnt[q] ? cnt[q] : 1) * sizeof(uint64_t));
+    A->part_n[t * P + q] = 0;
+  }
+  for (uint64_t r = lo; r < hi; ++r) {
+    int64_t key, nbr;
+    record(A->src, A->dst, A->dir, r, &key, &nbr);
+    const int q = (int)(mix64((uint64_t)key) % (uint64_t)P);
+    A->part[t * P + q][A->part_n[t * P + q]++] = r;
+  }
+  free(cnt);
+  pthread_barrier_wait(A->bar);
+  /* phase 2: window operator subtask t folds its keys in arrival order */
+  uint64_t mine = 0;
+  for (int q = 0; q < P; ++q) mine += A->part_n[q * P + t];
+  vmap m;
+  vmap_init(&m, mine / 2 + 16);
+  uint64_t* acc = (uint64_t*)malloc((mine ? mine : 1) * sizeof(uint64_t));
+  for (int q = 0; q < P; ++q) {
+    const uint64_t* lst = A->part[q * P + t];
+    for (uint64_t j = 0; j < A->part_n[q * P + t]; ++j) {
+      int64_t key, nbr;
+      const uint64_t i = record(A->src, A->dst, A->dir, lst[j], &key, &nbr);
+      int is_new;
+      const int64_t s = vmap_get(&m, key, &is_new);
+      if (A->op == OP_COUNT) { if (is_new) acc[s] = 0; acc[s]++; }
+      else if (is_new) acc[s] = load_val(A->dtype, A->val, i);
+      else apply_op(A->op, A->dtype, &acc[s], A->val, i);
+    }
+  }
+  A->vertices = m.size;
+  free(acc);
+  vmap_free(&m);
+  return NULL;
+}
+
+/* Returns the number of output vertices (sum over subtasks). */
+GSO_API uint64_t gso_baseline_reduce(const int64_t* src, const int64_t* dst, const void* val, uint64_t n,
+                                     int dtype, int dir, int op, int threads) {
+  const int P = threads < 1 ? 1 : threads;
+  pthread_t* th = (pthread_t*)malloc((size_t)P * sizeof(pthread_t));
+  bl_arg* args = (bl_arg*)malloc((size_t)P * sizeof(bl_arg));
+  uint64_t** part = (uint64_t**)malloc((size_t)P * P * sizeof(uint64_t*));
+  uint64_t* part_n = (uint64_t*)calloc((size_t)P * P, sizeof(uint64_t));
+  pthread_barrier_t bar;
+  pthread_barrier_init(&bar, NULL, (unsigned)P);
+  for (int t = 0; t < P; ++t) {
+    args[t] = (bl_arg){src, dst, val, n, dtype, dir, op, P, t, part, part_n, 0, &bar};
+    pthread_create(&th[t], NULL, bl_worker, &args[t]);
+  }
+  uint64_t U = 0;
+  for (int t = 0; t < P; ++t) { pthread_join(th[t], NULL); U += args[t].vertices; }
+  pthread_barrier_destroy(&bar);
+  for (int i = 0; i < P * P; ++i) free(part[i]);
+  free(part); free(part_n); free(args); free(th);
+  return U;
+}

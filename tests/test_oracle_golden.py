@@ -1,0 +1,112 @@
+"""Pin the CPU oracle against the reference's own golden vectors (tests/golden/reference_fixtures.json,
+extracted from TestSlice / TestReverse / TestUndirected / WindowTrianglesITCase by
+tests/golden/extract_reference_fixtures.py).  CPU only."""
+import json
+from collections import defaultdict
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+FIX = json.loads((Path(__file__).parent / "golden" / "reference_fixtures.json").read_text())
+DIRS = {"IN": 0, "OUT": 1, "ALL": 2}
+
+
+def _graph():
+    e = np.array(FIX["slice_graph"]["edges"], dtype=np.int64)
+    return e[:, 0].copy(), e[:, 1].copy(), e[:, 2].copy()
+
+
+@pytest.mark.parametrize("case", FIX["slice_cases"], ids=lambda c: c["name"])
+def test_testslice_goldens(oracle, case):
+    s, d, v = _graph()
+    direction = DIRS[case["direction"]]
+    if case["kind"] == "reduce":       # SumEdgeValuesReduce, TestSlice.java:242-249
+        k, r = oracle.window_reduce(s, d, v, direction, oracle.OP_SUM)
+        got = {(str(a), str(b)) for a, b in zip(k, r)}
+    elif case["kind"] == "fold":       # SumEdgeValues from Tuple2(0, 0), TestSlice.java:233-240
+        k, r = oracle.window_fold(s, d, v, direction, oracle.OP_SUM, 0)
+        got = {(str(a), str(b)) for a, b in zip(k, r)}
+    else:                              # SumEdgeValuesApply: sum > 50 ? big : small, TestSlice.java:251-268
+        k, off, nb, vals = oracle.window_csr(s, d, v, direction)
+        got = set()
+        for u in range(len(k)):
+            tot = int(vals[off[u]:off[u + 1]].sum())
+            got.add((str(k[u]), "big" if tot > 50 else "small"))
+    assert got == {tuple(x) for x in case["expected"]}   # compareResultsByLinesInMemory: unordered
+
+
+def test_reverse_and_undirected_expansion(oracle):
+    s, d, v = _graph()
+    # IN-keyed records == reverse(): group the golden reverse() edge list by f0 in arrival order
+    for direction, golden in ((0, FIX["reverse_expected"]), (2, FIX["undirected_expected"])):
+        k, off, nb, vals = oracle.window_csr(s, d, v, direction)
+        want = defaultdict(list)
+        for a, b, w in golden:
+            want[a].append((b, w))
+        got = {int(k[u]): [(int(nb[j]), int(vals[j])) for j in range(off[u], off[u + 1])] for u in range(len(k))}
+        if direction == 2:
+            # the golden lists e, e.reverse() per edge; per-key arrival order must match exactly
+            assert got == {a: lst for a, lst in want.items()}
+        else:
+            assert got == dict(want)
+
+
+def test_window_triangles_itcase(oracle):
+    t = FIX["triangles"]
+    e = np.array(t["edges_src_trg_ts"], dtype=np.int64)
+    out = []
+    for start, idx in oracle.split_windows(e[:, 2], t["window_ms"]):
+        w_ref, ex_ref, has_ref, tree = oracle.window_triangles_ref(e[idx, 0], e[idx, 1])
+        w_fwd, ex_fwd, has_fwd = oracle.window_triangles_fwd(e[idx, 0], e[idx, 1])
+        assert (w_ref, ex_ref, has_ref) == (w_fwd, ex_fwd, has_fwd) and not tree
+        if has_ref:
+            out.append([w_ref, start + t["window_ms"] - 1])
+    assert sorted(out) == sorted(t["expected"])
+
+
+def test_triangle_algorithms_agree_random(oracle):
+    """The reference candidate rule and the forward algorithm agree (incl. multi-edges, self-loops)."""
+    rng = np.random.default_rng(5)
+    for trial in range(30):
+        V = int(rng.integers(3, 60))
+        n = int(rng.integers(1, 400))
+        s = rng.integers(0, V, n).astype(np.int64)
+        d = rng.integers(0, V, n).astype(np.int64)
+        if trial % 3 == 0:
+            s, d = s * 1_000_003 + 7, d * 1_000_003 + 7   # sparse large IDs -> non-trivial HashSet order
+        w_ref, ex_ref, has_ref, tree = oracle.window_triangles_ref(s, d)
+        w_fwd, ex_fwd, has_fwd = oracle.window_triangles_fwd(s, d)
+        assert (w_ref, ex_ref, has_ref) == (w_fwd, ex_fwd, has_fwd), trial
+
+
+def test_hashset_order_model(oracle):
+    """java.util.HashSet<Long> sizing used by the candidate rule: 16 buckets up to 12 entries, x2 after."""
+    assert [oracle.java_hashset_cap(k) for k in (0, 1, 12, 13, 24, 25, 48, 49)] == [16, 16, 16, 32, 32, 64, 64, 128]
+
+
+def test_generators_deterministic(oracle):
+    a = oracle.gen_rmat(10, 1000, 1)
+    b = oracle.gen_rmat(10, 1000, 1)
+    c = oracle.gen_rmat(10, 500, 1, first_edge=500)
+    assert np.array_equal(a[0], b[0]) and np.array_equal(a[0][500:], c[0]) and np.array_equal(a[1][500:], c[1])
+    s, d = oracle.gen_rmat(10, 5000, 2, no_self_loops=True)
+    assert not np.any(s == d)
+    s, d = oracle.gen_uniform(100, 5000, 3)
+    assert not np.any(s == d) and s.max() < 100 and d.min() >= 0
+
+
+def test_reduce_java_arithmetic(oracle):
+    s = np.zeros(3, np.int64)
+    d = np.ones(3, np.int64)
+    v = np.array([2**62, 2**62, 2**62], dtype=np.int64)
+    k, r = oracle.window_reduce(s, d, v, 1, 0)
+    assert int(r[0]) == -(2**62)  # 3 * 2^62 wraps (Long addition)
+    v32 = np.array([2**30, 2**30, 2**30], dtype=np.int32)
+    k, r = oracle.window_reduce(s, d, v32, 1, 0)
+    assert r[0] == np.int32(-(2**30))  # 3 * 2^30 wraps to -2^30
+    f = np.array([0.0, -0.0, np.nan], dtype=np.float64)
+    k, r = oracle.window_reduce(s[:2], d[:2], f[:2], 1, 1)
+    assert np.signbit(r[0])  # Math.min(0.0, -0.0) = -0.0
+    k, r = oracle.window_reduce(s, d, f, 1, 2)
+    assert np.isnan(r[0])
