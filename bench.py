@@ -1,0 +1,216 @@
+"""bench.py — edges/sec per tumbling slice for reduceOnEdges on the BASELINE C2 window.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+
+Workload (BASELINE.json configs[1]): one tumbling window of an R-MAT scale-24
+stream (Graph500 a,b,c,d = .57,.19,.19,.05, edge factor 16 -> E = 2^28 edges, seeded vertex
+permutation, seed 0x5EED02), Long edge values splitmix64 & 0xFFFF, slice(OUT).reduceOnEdges(SUM).
+A step = the whole window through the engine with the edge columns already resident in HBM:
+key scan -> LSD radix passes -> segmented reduce -> per-vertex (vertex, sum) in HBM.
+N > 1 (torchrun, one rank per GPU): each rank holds its own 2^28-edge slice of the stream
+(weak scaling); the step adds the RCCL keyBy exchange of per-vertex partials and the merge.
+Rank 0 prints one JSON line (roofline of the dominant kernel + the CPU baseline at N = 1).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+import torch
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+import __graft_entry__ as ge  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+METRIC = "edges/sec per tumbling slice (reduceOnEdges, window triangles) at 1/2/4/8 GPUs"
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=10)
+    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--scale", type=int, default=24)
+    p.add_argument("--edge-factor", type=int, default=16)
+    p.add_argument("--seed", type=lambda x: int(x, 0), default=0x5EED02)
+    p.add_argument("--dtype", default="int64", choices=["int64", "float64"])
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-sample-log2", type=int, default=25)
+    return p.parse_args()
+
+
+def kernel_table(times_list, E, U_avg):
+    """Average per-launch durations (device events inside the library, same stream) and the algorithmic
+    bytes each kernel must move."""
+    t0 = times_list[0]
+    kb, vb = t0.key_bytes, t0.payload_bytes
+    passes = t0.sort_passes
+    rows = {}
+    for p in range(passes):
+        ms = statistics.mean(t.pass_ms[p] for t in times_list)
+        # pass 0 reads the int64 key column + values, later passes the compact keys; all write compact
+        rd = (8 + vb) if p == 0 else (kb + vb)
+        rows[f"onesweep_pass{p}"] = {"ms": ms, "bytes": E * (rd + kb + vb)}
+    ms = statistics.mean(t.reduce_ms for t in times_list)
+    rows["reduce_by_key"] = {"ms": ms, "bytes": E * (kb + vb) + U_avg * 16}
+    ms = statistics.mean(t.keyinfo_ms for t in times_list)
+    rows["keyinfo(+host sync)"] = {"ms": ms, "bytes": E * 8}
+    for r in rows.values():
+        r["GB/s"] = r["bytes"] / (r["ms"] * 1e-3) / 1e9 if r["ms"] > 0 else 0.0
+        r["frac"] = r["GB/s"] / HBM_PEAK_GBS
+    return rows
+
+
+def pmc_traffic(kernel: str):
+    f = ROOT / "profiles" / "pmc_traffic.json"
+    if not f.exists():
+        return None
+    try:
+        d = json.loads(f.read_text())
+        return d.get(kernel, {}).get("bytes_per_launch")
+    except Exception:
+        return None
+
+
+def cpu_baseline(src, dst, val, sample_log2: int):
+    """The oracle's keyBy + hash-map fold (gso_baseline_reduce) on the first 2^k edges of the same
+    window, timed on this host: 1 warm-up, median of 3 (threads = min(16, cpus))."""
+    orc = ge.load_oracle()
+    S = min(1 << sample_log2, src.numel())
+    s = src[:S].cpu().numpy()
+    d = dst[:S].cpu().numpy()
+    v = val[:S].cpu().numpy()
+    threads = max(1, min(16, os.cpu_count() or 1))
+    orc.baseline_reduce(s[: S // 8], d[: S // 8], v[: S // 8], 1, 0, threads)
+    ts = []
+    for _ in range(3):
+        t = time.perf_counter()
+        orc.baseline_reduce(s, d, v, 1, 0, threads)
+        ts.append(time.perf_counter() - t)
+    tmed = statistics.median(ts)
+    S1 = S // 8
+    t = time.perf_counter()
+    orc.baseline_reduce(s[:S1], d[:S1], v[:S1], 1, 0, 1)
+    t1 = time.perf_counter() - t
+    return {"value": S / tmed, "unit": "edges/s", "cores": threads, "kind": "port",
+            "sample": f"first 2^{sample_log2} edges of the same R-MAT window, keyBy over {threads} threads + "
+                      f"per-subtask hash-map fold (oracle/gs_oracle.c gso_baseline_reduce), median of 3",
+            "single_core_value": S1 / t1}
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        torch.cuda.set_device(local)
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+    else:
+        dist = None
+        torch.cuda.set_device(0)
+    pkg = ge.load_package()
+    from importlib import import_module
+    D = import_module("gelly_streaming_amd.distributed")
+
+    eng = pkg.Engine(local)
+    E = a.edge_factor << a.scale
+    src, dst = eng.generate_rmat(a.scale, E, a.seed, first_edge=rank * E)
+    vdt = 1 if a.dtype == "int64" else 3
+    val = eng.generate_values(E, a.seed, vdt, first_edge=rank * E)
+    torch.cuda.synchronize()
+
+    local_times = []
+
+    def local_reduce(s_, d_, v_, direction, op):
+        r = eng.reduce(s_, d_, v_, direction, op)
+        if not local_times:
+            local_times.append(eng.stage_times())   # the window's own pipeline, not the merge
+        return r
+
+    def step():
+        local_times.clear()
+        if world == 1:
+            r = local_reduce(src, dst, val, 1, 0)
+        else:
+            r = D.reduce_window(local_reduce, src, dst, val, 1, 0)
+        return r[0], r[1], local_times[0]
+
+    for _ in range(a.warmup):
+        step()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    times, us = [], []
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        k, v, st = step()
+        times.append(st)
+        us.append(int(k.numel()))
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if dist:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    # local window only: the dominant kernel of the single-GPU pipeline
+    E_rec = times[0].records
+    U_avg = times[0].vertices
+    kt = kernel_table(times, E_rec, U_avg)
+    dom_name = max((n for n in kt if not n.startswith("keyinfo")), key=lambda n: kt[n]["ms"])
+    dom = kt[dom_name]
+    roofline = {"bound": "hbm", "kernel": dom_name, "achieved": round(dom["GB/s"], 1), "peak": HBM_PEAK_GBS,
+                "unit": "GB/s", "frac": round(dom["frac"], 4), "traffic": pmc_traffic(dom_name),
+                "algorithmic_bytes_per_launch": dom["bytes"], "avg_launch_ms": round(dom["ms"], 4)}
+
+    cpu = None
+    if world == 1 and rank == 0 and not a.no_cpu_baseline:
+        cpu = cpu_baseline(src, dst, val, a.cpu_sample_log2)
+
+    if rank == 0:
+        total_edges = E * world * a.steps
+        line = {
+            "metric": METRIC,
+            "value": total_edges / elapsed,
+            "unit": "edges/s",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": elapsed / a.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": a.dtype,
+            "data": "synthetic R-MAT (Graph500 .57/.19/.19/.05, permuted), generated on device (gs_generate_rmat)",
+            "config": {"workload": "C2: slice(OUT).reduceOnEdges(SUM) over one R-MAT scale-24 window",
+                       "scale": a.scale, "edges_per_window_per_gpu": E, "direction": "OUT", "op": "SUM",
+                       "value_dtype": a.dtype, "vertices_out": U_avg, "sort_passes": times[0].sort_passes,
+                       "key_bits": times[0].key_bits,
+                       "parallelism": f"vertex-range keyBy over {world} GPU(s)" if world > 1 else "1 GPU"},
+            "roofline": roofline,
+            "cpu_baseline": cpu,
+            "kernels": {n: {"avg_ms": round(r["ms"], 4), "GB/s": round(r["GB/s"], 1), "frac": round(r["frac"], 4)}
+                        for n, r in kt.items()},
+        }
+        print(json.dumps(line), flush=True)
+    if dist:
+        dist.destroy_process_group()
+    eng.close()
+
+
+if __name__ == "__main__":
+    main()

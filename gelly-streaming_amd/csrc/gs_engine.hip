@@ -127,13 +127,17 @@ static gs_status run_passes(gs_ctx* c, const int64_t* src, const int64_t* dst, c
   V* va = c->valsA.as<V>();
   V* vb = c->valsB.as<V>();
   EdgeSrc<K, V, DIR, PAY> es{src, dst, (const V*)val, out->key_xor};
+  hipEventRecord(c->pass_ev[0], c->stream);
   GS_TRY((launch_pass<K, V, HAS_V>(c, es, ka, va, R, 0, 0)));
+  hipEventRecord(c->pass_ev[1], c->stream);
   for (int p = 1; p < out->passes; ++p) {
     BufSrc<K, V> bs{ka, HAS_V ? va : nullptr, 0};
     GS_TRY((launch_pass<K, V, HAS_V>(c, bs, kb, vb, R, p, 8u * p)));
+    hipEventRecord(c->pass_ev[p + 1], c->stream);
     std::swap(ka, kb);
     std::swap(va, vb);
   }
+  out->payload_bytes = HAS_V ? (int)sizeof(V) : 0;
   out->keys = ka;
   out->vals = HAS_V ? (void*)va : nullptr;
   return GS_OK;
@@ -255,6 +259,7 @@ gs_status gs_create(const gs_config* cfg, gs_ctx** out) {
   }
   c->own_stream = true;
   for (auto& e : c->ev) hipEventCreate(&e);
+  for (auto& e : c->pass_ev) hipEventCreate(&e);
   if (hipHostMalloc((void**)&c->host_small, 64, hipHostMallocDefault) != hipSuccess ||
       ensure(c, c->small, SM_BYTES, true) != GS_OK) {
     gs_destroy(c);
@@ -281,6 +286,8 @@ void gs_destroy(gs_ctx* c) {
                     &c->rbk_word, &c->rbk_agg, &c->rbk_inc, &c->small, &c->out_keys, &c->out_a, &c->out_b, &c->aux})
     if (b->p) hipFree(b->p);
   for (auto& e : c->ev)
+    if (e) hipEventDestroy(e);
+  for (auto& e : c->pass_ev)
     if (e) hipEventDestroy(e);
   if (c->host_small) hipHostFree(c->host_small);
   if (c->own_stream && c->stream) hipStreamDestroy(c->stream);

@@ -24,6 +24,7 @@ struct Sorted {
   uint64_t key_xor = 0;     // key = key_xor ^ compact
   uint64_t records = 0;
   int bits = 0, passes = 0;
+  int payload_bytes = 0;
 };
 
 }  // namespace gs
@@ -45,6 +46,7 @@ struct gs_ctx {
   // output staging
   gs::DevBuf out_keys, out_a, out_b, aux;
   hipEvent_t ev[6] = {};
+  hipEvent_t pass_ev[9] = {};
   gs_stage_times times{};
   uint64_t* host_small = nullptr;  // pinned mirror of small scalars
 };

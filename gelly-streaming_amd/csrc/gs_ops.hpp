@@ -56,6 +56,13 @@ inline void finish_times(gs_ctx* c, const Sorted& s, uint64_t U) {
   c->times.key_bits = (uint32_t)s.bits;
   c->times.records = s.records;
   c->times.vertices = U;
+  for (int p = 0; p < 8; ++p) {
+    float t = 0;
+    if (p < s.passes) hipEventElapsedTime(&t, c->pass_ev[p], c->pass_ev[p + 1]);
+    c->times.pass_ms[p] = t;
+  }
+  c->times.key_bytes = s.wide ? 8 : 4;
+  c->times.payload_bytes = (uint32_t)s.payload_bytes;
 }
 
 // Copy U staged outputs to the caller (host or device) — only when the direct write was impossible.

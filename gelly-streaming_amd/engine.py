@@ -53,6 +53,9 @@ class StageTimes:
     key_bits: int
     records: int
     vertices: int
+    pass_ms: list
+    key_bytes: int
+    payload_bytes: int
 
 
 class Engine:
@@ -108,7 +111,7 @@ class Engine:
         t = L.GsStageTimes()
         self._check(self._L.gs_last_stage_times(self.ctx, ctypes.byref(t)))
         return StageTimes(t.keyinfo_ms, t.sort_ms, t.reduce_ms, t.total_ms, t.sort_passes, t.key_bits, t.records,
-                          t.vertices)
+                          t.vertices, list(t.pass_ms)[:t.sort_passes], t.key_bytes, t.payload_bytes)
 
     # -- helpers ---------------------------------------------------------------------------------
     def _batch(self, src, dst, val):

@@ -212,6 +212,8 @@ typedef struct gs_stage_times {
   float keyinfo_ms, sort_ms, reduce_ms, total_ms;
   uint32_t sort_passes, key_bits;
   uint64_t records, vertices;
+  float pass_ms[8];        /* each onesweep launch (device events around the launch)         */
+  uint32_t key_bytes, payload_bytes;  /* sorted key / payload widths                          */
 } gs_stage_times;
 GS_API gs_status gs_last_stage_times(const gs_ctx* ctx, gs_stage_times* out);
 

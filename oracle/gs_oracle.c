@@ -626,11 +626,12 @@ GSO_API int32_t gso_window_triangles_fwd(const int64_t* src, const int64_t* dst,
 /* ------------------------------------------------------------------------------------ */
 /* CPU baseline: keyBy(vertex) over P threads + per-subtask hash-map fold (bench only)  */
 /* ------------------------------------------------------------------------------------ */
+typedef struct { int64_t key; uint64_t val; } shuffled;  /* a record on the wire after keyBy */
 typedef struct {
   const int64_t* src; const int64_t* dst; const void* val;
   uint64_t n; int dtype, dir, op, P, tid;
-  /* phase 1 output: per (producer, consumer) record index lists */
-  uint64_t** part; uint64_t* part_n;   /* [P*P] */
+  /* phase 1 output: per (producer, consumer) record buffers — the keyBy network channels */
+  shuffled** part; uint64_t* part_n;   /* [P*P] */
   uint64_t vertices;
   pthread_barrier_t* bar;
 } bl_arg;
@@ -648,38 +649,49 @@ static void* bl_worker(void* p) {
     cnt[mix64((uint64_t)key) % (uint64_t)P]++;
   }
   for (int q = 0; q < P; ++q) {
-    A->part[t * P + q] = (uint64_t*)malloc((cnt[q] ? cnt[q] : 1) * sizeof(uint64_t));
+    A->part[t * P + q] = (shuffled*)malloc((cnt[q] ? cnt[q] : 1) * sizeof(shuffled));
     A->part_n[t * P + q] = 0;
   }
   for (uint64_t r = lo; r < hi; ++r) {
     int64_t key, nbr;
-    record(A->src, A->dst, A->dir, r, &key, &nbr);
+    const uint64_t i = record(A->src, A->dst, A->dir, r, &key, &nbr);
     const int q = (int)(mix64((uint64_t)key) % (uint64_t)P);
-    A->part[t * P + q][A->part_n[t * P + q]++] = r;
+    shuffled* o = &A->part[t * P + q][A->part_n[t * P + q]++];
+    o->key = key;
+    o->val = A->op == OP_COUNT ? 0 : load_val(A->dtype, A->val, i);
   }
   free(cnt);
   pthread_barrier_wait(A->bar);
-  /* phase 2: window operator subtask t folds its keys in arrival order */
+  /* phase 2: window operator subtask t folds its keys in arrival order into one open-addressing
+   * table of {key, acc} slots (one cache line touch per record) */
   uint64_t mine = 0;
   for (int q = 0; q < P; ++q) mine += A->part_n[q * P + t];
-  vmap m;
-  vmap_init(&m, mine / 2 + 16);
-  uint64_t* acc = (uint64_t*)malloc((mine ? mine : 1) * sizeof(uint64_t));
+  uint64_t cap = 16;
+  while (cap < 2 * (mine / 2 + 16)) cap <<= 1;
+  typedef struct { int64_t key; uint64_t acc; } slot_t;
+  slot_t* tab = (slot_t*)malloc(cap * sizeof(slot_t));
+  uint8_t* used = (uint8_t*)calloc(cap, 1);
+  uint64_t size = 0;
   for (int q = 0; q < P; ++q) {
-    const uint64_t* lst = A->part[q * P + t];
+    const shuffled* lst = A->part[q * P + t];
     for (uint64_t j = 0; j < A->part_n[q * P + t]; ++j) {
-      int64_t key, nbr;
-      const uint64_t i = record(A->src, A->dst, A->dir, lst[j], &key, &nbr);
-      int is_new;
-      const int64_t s = vmap_get(&m, key, &is_new);
-      if (A->op == OP_COUNT) { if (is_new) acc[s] = 0; acc[s]++; }
-      else if (is_new) acc[s] = load_val(A->dtype, A->val, i);
-      else apply_op(A->op, A->dtype, &acc[s], A->val, i);
+      uint64_t h = mix64((uint64_t)lst[j].key) & (cap - 1);
+      while (used[h] && tab[h].key != lst[j].key) h = (h + 1) & (cap - 1);
+      if (!used[h]) {
+        used[h] = 1;
+        tab[h].key = lst[j].key;
+        tab[h].acc = A->op == OP_COUNT ? 1 : lst[j].val;
+        ++size;
+      } else if (A->op == OP_COUNT) {
+        tab[h].acc++;
+      } else {
+        apply_op(A->op, A->dtype, &tab[h].acc, &lst[j].val, 0);
+      }
     }
   }
-  A->vertices = m.size;
-  free(acc);
-  vmap_free(&m);
+  A->vertices = size;
+  free(tab);
+  free(used);
   return NULL;
 }
 
@@ -689,7 +701,7 @@ GSO_API uint64_t gso_baseline_reduce(const int64_t* src, const int64_t* dst, con
   const int P = threads < 1 ? 1 : threads;
   pthread_t* th = (pthread_t*)malloc((size_t)P * sizeof(pthread_t));
   bl_arg* args = (bl_arg*)malloc((size_t)P * sizeof(bl_arg));
-  uint64_t** part = (uint64_t**)malloc((size_t)P * P * sizeof(uint64_t*));
+  shuffled** part = (shuffled**)malloc((size_t)P * P * sizeof(shuffled*));
   uint64_t* part_n = (uint64_t*)calloc((size_t)P * P, sizeof(uint64_t));
   pthread_barrier_t bar;
   pthread_barrier_init(&bar, NULL, (unsigned)P);
