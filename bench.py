@@ -43,6 +43,7 @@ def parse():
     p.add_argument("--dtype", default="int64", choices=["int64", "float64"])
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-sample-log2", type=int, default=25)
+    p.add_argument("--check", action="store_true", help="verify sum(per-vertex sums) == sum(values) after timing")
     return p.parse_args()
 
 
@@ -166,6 +167,10 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+
+    if a.check and world == 1:
+        k, v, _ = step()
+        assert int(v.sum()) == int(val.sum()) and bool((k[1:] > k[:-1]).all()), "bench window failed its check"
 
     # local window only: the dominant kernel of the single-GPU pipeline
     E_rec = times[0].records

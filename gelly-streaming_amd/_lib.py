@@ -7,12 +7,14 @@ no CPU fallback.
 from __future__ import annotations
 
 import ctypes
+import os
 from pathlib import Path
 
 import numpy as np
 
 PKG = Path(__file__).resolve().parent
-LIB_PATH = PKG / "libgellyhip.so"
+# GELLY_HIP_LIB selects a tuning build (csrc/Makefile `variant`); default is the in-tree library
+LIB_PATH = Path(os.environ.get("GELLY_HIP_LIB", PKG / "libgellyhip.so"))
 
 GS_OK, GS_EINVAL, GS_ECAPACITY, GS_EDEVICE, GS_ECOMM, GS_ENOMEM, GS_EUNSUPPORTED = 0, -1, -2, -3, -4, -5, -6
 GS_MEM_HOST, GS_MEM_DEVICE = 0, 1

@@ -94,8 +94,13 @@ static inline unsigned grid_for(uint64_t n, unsigned per_block, unsigned cap) {
 template <int DIR>
 static gs_status launch_keyinfo(gs_ctx* c, const int64_t* src, const int64_t* dst, uint64_t n) {
   char* sm = c->small.as<char>();
-  hipLaunchKernelGGL(k_keyinfo<DIR>, dim3(grid_for(n, 256 * 8, 2048)), dim3(256), 0, c->stream, src, dst, n,
-                     (unsigned long long*)(sm + SM_MASK), (uint32_t*)(sm + SM_HIST));
+  const bool vec = ((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst)) & 15) == 0;
+  if (vec)
+    hipLaunchKernelGGL((k_keyinfo<DIR, true>), dim3(grid_for(n, 2048, 2048)), dim3(256), 0, c->stream, src, dst, n,
+                       (unsigned long long*)(sm + SM_MASK), (uint32_t*)(sm + SM_HIST));
+  else
+    hipLaunchKernelGGL((k_keyinfo<DIR, false>), dim3(grid_for(n, 2048, 2048)), dim3(256), 0, c->stream, src, dst, n,
+                       (unsigned long long*)(sm + SM_MASK), (uint32_t*)(sm + SM_HIST));
   return hip_check(c, hipGetLastError(), "k_keyinfo");
 }
 template <int DIR>

@@ -15,8 +15,21 @@
 
 namespace gs {
 
-constexpr int SORT_BLOCK = 256, SORT_ITEMS = 16, SORT_TILE = SORT_BLOCK * SORT_ITEMS;
-constexpr int RBK_BLOCK = 256, RBK_ITEMS = 16, RBK_TILE = RBK_BLOCK * RBK_ITEMS;
+// tile shapes (overridable with -D for tuning builds: make VARIANT="-DGS_SORT_ITEMS=24")
+#ifndef GS_SORT_BLOCK
+#define GS_SORT_BLOCK 512
+#endif
+#ifndef GS_SORT_ITEMS
+#define GS_SORT_ITEMS 16
+#endif
+#ifndef GS_RBK_BLOCK
+#define GS_RBK_BLOCK 256
+#endif
+#ifndef GS_RBK_ITEMS
+#define GS_RBK_ITEMS 16
+#endif
+constexpr int SORT_BLOCK = GS_SORT_BLOCK, SORT_ITEMS = GS_SORT_ITEMS, SORT_TILE = SORT_BLOCK * SORT_ITEMS;
+constexpr int RBK_BLOCK = GS_RBK_BLOCK, RBK_ITEMS = GS_RBK_ITEMS, RBK_TILE = RBK_BLOCK * RBK_ITEMS;
 
 // ---- reduce-by-key launch ----------------------------------------------------------------------
 template <typename K, class Op, class Out>

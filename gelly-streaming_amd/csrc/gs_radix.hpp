@@ -60,7 +60,7 @@ struct BufSrc {
 };
 
 // ---- k_keyinfo ------------------------------------------------------------------------------
-template <int DIR>
+template <int DIR, bool VEC>
 __global__ __launch_bounds__(256) void k_keyinfo(const int64_t* __restrict__ src, const int64_t* __restrict__ dst,
                                                  uint64_t n, unsigned long long* __restrict__ mask_out,
                                                  uint32_t* __restrict__ hist_out /*[4][256]*/) {
@@ -77,10 +77,40 @@ __global__ __launch_bounds__(256) void k_keyinfo(const int64_t* __restrict__ src
     atomicAdd(&h[w][2][(k >> 16) & 255u], 1u);
     atomicAdd(&h[w][3][(k >> 24) & 255u], 1u);
   };
-  const uint64_t stride = (uint64_t)gridDim.x * 256u;
-  for (uint64_t i = (uint64_t)blockIdx.x * 256u + tid; i < n; i += stride) {
-    if (DIR != DIR_IN) add((uint64_t)src[i]);
-    if (DIR != DIR_OUT) add((uint64_t)dst[i]);
+  if constexpr (!VEC) {   // columns not 16-byte aligned (caller-provided slices)
+    const uint64_t stride = (uint64_t)gridDim.x * 256u;
+    for (uint64_t i = (uint64_t)blockIdx.x * 256u + tid; i < n; i += stride) {
+      if (DIR != DIR_IN) add((uint64_t)src[i]);
+      if (DIR != DIR_OUT) add((uint64_t)dst[i]);
+    }
+  } else {
+  // 16-byte loads, 4 in flight per column per thread: 8 keys per column per iteration
+  const uint64_t npair = n >> 1;
+  const longlong2* s2 = reinterpret_cast<const longlong2*>(src);
+  const longlong2* d2 = reinterpret_cast<const longlong2*>(dst);
+  const uint64_t stride = (uint64_t)gridDim.x * 1024u;
+  for (uint64_t q = (uint64_t)blockIdx.x * 1024u + tid; q < npair; q += stride) {
+    longlong2 a[4], b[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const uint64_t qq = q + 256u * u;
+      if (qq < npair) {
+        if (DIR != DIR_IN) a[u] = s2[qq];
+        if (DIR != DIR_OUT) b[u] = d2[qq];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if (q + 256u * u < npair) {
+        if (DIR != DIR_IN) { add((uint64_t)a[u].x); add((uint64_t)a[u].y); }
+        if (DIR != DIR_OUT) { add((uint64_t)b[u].x); add((uint64_t)b[u].y); }
+      }
+    }
+  }
+  if ((n & 1) && blockIdx.x == 0 && tid == 0) {
+    if (DIR != DIR_IN) add((uint64_t)src[n - 1]);
+    if (DIR != DIR_OUT) add((uint64_t)dst[n - 1]);
+  }
   }
   m = wave_or(m);
   if ((tid & 63) == 0 && m) atomicOr(mask_out, (unsigned long long)m);

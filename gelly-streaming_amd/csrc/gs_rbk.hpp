@@ -144,6 +144,29 @@ __device__ __forceinline__ Acc shfl_up_acc(Acc a, int o) {
   return u.a;
 }
 
+template <typename Acc>
+__device__ __forceinline__ Acc shfl_down_acc(Acc a, int o) {
+  union U {
+    Acc a;
+    uint32_t w[sizeof(Acc) / 4];
+  } u;
+  u.a = a;
+#pragma unroll
+  for (int i = 0; i < (int)(sizeof(Acc) / 4); ++i) u.w[i] = __shfl_down(u.w[i], o, WAVE);
+  return u.a;
+}
+template <typename Acc>
+__device__ __forceinline__ Acc shfl_acc(Acc a, int src) {
+  union U {
+    Acc a;
+    uint32_t w[sizeof(Acc) / 4];
+  } u;
+  u.a = a;
+#pragma unroll
+  for (int i = 0; i < (int)(sizeof(Acc) / 4); ++i) u.w[i] = __shfl(u.w[i], src, WAVE);
+  return u.a;
+}
+
 template <class Op>
 __device__ __forceinline__ Seg<typename Op::Acc> seg_combine(Seg<typename Op::Acc> a, Seg<typename Op::Acc> b) {
   if (!b.valid) return a;
@@ -272,7 +295,9 @@ __global__ __launch_bounds__(BLOCK) void k_reduce_by_key(const K* __restrict__ k
   if (lane == 63) s_wagg[wid] = inc;
   __syncthreads();
 
-  if (tid == 0) {
+  // tile aggregate -> publish -> wave-parallel decoupled look-back (wave 0: lane l inspects tile-1-l,
+  // 64 predecessors per round; the nearest INCLUSIVE granule ends the walk)
+  if (wid == 0) {
     S tot = s_wagg[0];
     for (int w = 1; w < NW; ++w) tot = seg_combine<Op>(tot, s_wagg[w]);
     S pre;
@@ -280,29 +305,55 @@ __global__ __launch_bounds__(BLOCK) void k_reduce_by_key(const K* __restrict__ k
     pre.valid = 0;
     uint64_t* w0 = st_word + tile;
     if (tile == 0) {
-      store_acc(st_inc + (uint64_t)tile * SLOTS, tot.v);
-      drain_stores();
-      st_agent(w0, granule(FLAG_INC, epoch, tot.cnt));
+      if (lane == 0) {
+        store_acc(st_inc, tot.v);
+        drain_stores();
+        st_agent(w0, granule(FLAG_INC, epoch, tot.cnt));
+      }
     } else {
-      store_acc(st_agg + (uint64_t)tile * SLOTS, tot.v);
-      drain_stores();
-      st_agent(w0, granule(FLAG_AGG, epoch, tot.cnt));
-      for (int64_t k = (int64_t)tile - 1; k >= 0; --k) {
-        const uint64_t g = poll_granule(st_word + k, epoch, timeout);
-        S p;
-        p.cnt = (uint32_t)g_value(g);
-        p.valid = 1;
-        p.v = load_acc<Acc>((g_flag(g) == FLAG_INC ? st_inc : st_agg) + (uint64_t)k * SLOTS);
-        pre = seg_combine<Op>(p, pre);
-        if (g_flag(g) == FLAG_INC) break;
+      if (lane == 0) {
+        store_acc(st_agg + (uint64_t)tile * SLOTS, tot.v);
+        drain_stores();
+        st_agent(w0, granule(FLAG_AGG, epoch, tot.cnt));
+      }
+      for (int64_t k = (int64_t)tile - 1;; k -= WAVE) {
+        const int64_t kk = k - lane;
+        uint64_t g = 0;
+        if (kk >= 0) g = poll_granule(st_word + kk, epoch, timeout);
+        const bool is_inc = kk >= 0 && g_flag(g) == FLAG_INC;
+        const uint64_t incm = ballot(is_inc);
+        const int stop = incm ? __builtin_ctzll(incm) : WAVE - 1;   // farthest lane that counts
+        S x;
+        x.valid = (kk >= 0 && lane <= stop) ? 1u : 0u;
+        x.cnt = x.valid ? (uint32_t)g_value(g) : 0u;
+        if (x.valid) x.v = load_acc<Acc>((is_inc ? st_inc : st_agg) + (uint64_t)kk * SLOTS);
+        // ordered reduction: higher lane = earlier tile
+#pragma unroll
+        for (int o = 1; o < WAVE; o <<= 1) {
+          S y;
+          y.cnt = __shfl_down(x.cnt, o, WAVE);
+          y.valid = __shfl_down(x.valid, o, WAVE);
+          y.v = shfl_down_acc(x.v, o);
+          if (lane + o < WAVE) x = seg_combine<Op>(y, x);
+        }
+        S r;
+        r.cnt = __shfl(x.cnt, 0, WAVE);
+        r.valid = __shfl(x.valid, 0, WAVE);
+        r.v = shfl_acc(x.v, 0);
+        pre = seg_combine<Op>(r, pre);
+        if (incm || k < WAVE) break;   // wave-uniform: an INCLUSIVE was seen or tile 0 covered
       }
       const S all = seg_combine<Op>(pre, tot);
-      store_acc(st_inc + (uint64_t)tile * SLOTS, all.v);
-      drain_stores();
-      st_agent(w0, granule(FLAG_INC, epoch, all.cnt));
+      if (lane == 0) {
+        store_acc(st_inc + (uint64_t)tile * SLOTS, all.v);
+        drain_stores();
+        st_agent(w0, granule(FLAG_INC, epoch, all.cnt));
+      }
     }
-    if (tile == ntiles - 1) *n_unique = (unsigned long long)seg_combine<Op>(pre, tot).cnt;
-    s_prefix = pre;
+    if (lane == 0) {
+      if (tile == ntiles - 1) *n_unique = (unsigned long long)seg_combine<Op>(pre, tot).cnt;
+      s_prefix = pre;
+    }
   }
   __syncthreads();
 

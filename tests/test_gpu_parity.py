@@ -148,3 +148,15 @@ def test_reduce_large_rmat_properties(engine):
     assert int(vc.sum()) == n and torch.equal(kc, k1)
     k2, v2 = engine.reduce(s, d, v, 1, 0)
     assert torch.equal(k1, k2) and torch.equal(v1, v2)
+
+
+def test_reduce_unaligned_device_slices(engine, oracle):
+    """Columns that are views at an odd offset (8-byte aligned only) take the scalar key-scan path."""
+    n = 70001
+    s, d = oracle.gen_rmat(15, n + 1, 77)
+    v = oracle.gen_values(n + 1, 78, oracle.DT_I64)
+    S, D, Vv = _dev(s, d, v)
+    for direction in (0, 1, 2):
+        rk, rv = oracle.window_reduce(s[1:], d[1:], v[1:], direction, 0)
+        gk, gv = engine.reduce(S[1:], D[1:], Vv[1:], direction, 0)
+        assert np.array_equal(_np(gk), rk) and np.array_equal(_np(gv), rv)
