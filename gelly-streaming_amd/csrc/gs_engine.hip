@@ -103,6 +103,10 @@ static gs_status launch_keyinfo(gs_ctx* c, const int64_t* src, const int64_t* ds
                        (unsigned long long*)(sm + SM_MASK), (uint32_t*)(sm + SM_HIST));
   return hip_check(c, hipGetLastError(), "k_keyinfo");
 }
+gs_status launch_keyinfo_all(gs_ctx* c, const int64_t* src, const int64_t* dst, uint64_t n) {
+  return launch_keyinfo<DIR_ALL>(c, src, dst, n);
+}
+
 template <int DIR>
 static gs_status launch_hist_wide(gs_ctx* c, const int64_t* src, const int64_t* dst, uint64_t n, uint64_t key_xor) {
   char* sm = c->small.as<char>();
@@ -199,6 +203,64 @@ static gs_status sort_dir(gs_ctx* c, const int64_t* src, const int64_t* dst, con
   return dispatch_payload<uint32_t, DIR>(c, src, dst, val, vbytes, (uint32_t)R, payload, out);
 }
 
+template <typename K, typename V, bool HAS_V>
+static gs_status buffer_passes(gs_ctx* c, const uint64_t* keys, const V* vals, uint32_t R, Sorted* out) {
+  K* ka = c->keysA.as<K>();
+  K* kb = c->keysB.as<K>();
+  V* va = c->valsA.as<V>();
+  V* vb = c->valsB.as<V>();
+  ConvSrc<K, V> cs{keys, HAS_V ? vals : nullptr, out->key_xor};
+  hipEventRecord(c->pass_ev[0], c->stream);
+  GS_TRY((launch_pass<K, V, HAS_V>(c, cs, ka, va, R, 0, 0)));
+  hipEventRecord(c->pass_ev[1], c->stream);
+  for (int p = 1; p < out->passes; ++p) {
+    BufSrc<K, V> bs{ka, HAS_V ? va : nullptr, 0};
+    GS_TRY((launch_pass<K, V, HAS_V>(c, bs, kb, vb, R, p, 8u * p)));
+    hipEventRecord(c->pass_ev[p + 1], c->stream);
+    std::swap(ka, kb);
+    std::swap(va, vb);
+  }
+  out->keys = ka;
+  out->vals = HAS_V ? (void*)va : nullptr;
+  out->payload_bytes = HAS_V ? (int)sizeof(V) : 0;
+  return GS_OK;
+}
+
+gs_status sort_buffer(gs_ctx* c, const uint64_t* keys, const uint32_t* vals, uint64_t n, Sorted* out) {
+  char* sm = c->small.as<char>();
+  GS_HIP(hipMemsetAsync(sm, 0, SM_BASE, c->stream));
+  hipLaunchKernelGGL(k_keyinfo_buf, dim3(grid_for(n, 512, 2048)), dim3(256), 0, c->stream, keys, n,
+                     (unsigned long long*)(sm + SM_MASK), (uint32_t*)(sm + SM_HIST));
+  GS_HIP(hipGetLastError());
+  GS_HIP(hipMemcpyAsync(sm + SM_K0, keys, 8, hipMemcpyDeviceToDevice, c->stream));
+  GS_HIP(hipMemcpyAsync(c->host_small, sm, 16, hipMemcpyDeviceToHost, c->stream));
+  GS_HIP(hipStreamSynchronize(c->stream));
+  const uint64_t mask = c->host_small[0], k0 = c->host_small[1];
+  const int bits = mask ? 64 - __builtin_clzll(mask) : 0;
+  out->bits = bits;
+  out->wide = bits > 32;
+  out->passes = std::max(1, (bits + RADIX_BITS - 1) / RADIX_BITS);
+  out->records = n;
+  out->key_xor = out->wide ? 0 : (k0 & 0xFFFFFFFF00000000ull);
+  hipLaunchKernelGGL(k_digit_base, dim3(1), dim3(256), 0, c->stream, (const uint32_t*)(sm + SM_HIST),
+                     (uint32_t*)(sm + SM_BASE), out->passes);
+  GS_HIP(hipGetLastError());
+  const size_t kb = out->wide ? 8 : 4;
+  const uint64_t tiles = (n + SORT_TILE - 1) / SORT_TILE;
+  GS_TRY(ensure(c, c->keysA, n * kb));
+  GS_TRY(ensure(c, c->keysB, n * kb));
+  if (vals) {
+    GS_TRY(ensure(c, c->valsA, n * 4));
+    GS_TRY(ensure(c, c->valsB, n * 4));
+  }
+  GS_TRY(ensure(c, c->sort_status, tiles * RADIX * 8, true));
+  if (out->wide)
+    return vals ? buffer_passes<uint64_t, uint32_t, true>(c, keys, vals, (uint32_t)n, out)
+                : buffer_passes<uint64_t, uint8_t, false>(c, keys, nullptr, (uint32_t)n, out);
+  return vals ? buffer_passes<uint32_t, uint32_t, true>(c, keys, vals, (uint32_t)n, out)
+              : buffer_passes<uint32_t, uint8_t, false>(c, keys, nullptr, (uint32_t)n, out);
+}
+
 gs_status sort_window(gs_ctx* c, const int64_t* src, const int64_t* dst, const void* val, int val_bytes,
                       uint64_t n_edges, int dir, int payload, Sorted* out) {
   switch (dir) {
@@ -288,7 +350,8 @@ void gs_destroy(gs_ctx* c) {
   hipSetDevice(c->device);
   if (c->stream) hipStreamSynchronize(c->stream);
   for (DevBuf* b : {&c->in_src, &c->in_dst, &c->in_val, &c->keysA, &c->keysB, &c->valsA, &c->valsB, &c->sort_status,
-                    &c->rbk_word, &c->rbk_agg, &c->rbk_inc, &c->small, &c->out_keys, &c->out_a, &c->out_b, &c->aux})
+                    &c->rbk_word, &c->rbk_agg, &c->rbk_inc, &c->small, &c->out_keys, &c->out_a, &c->out_b, &c->aux,
+                    &c->tri_loops, &c->tri_keep, &c->tri_tiles, &c->tri_pos, &c->tri_ou, &c->tri_onbr})
     if (b->p) hipFree(b->p);
   for (auto& e : c->ev)
     if (e) hipEventDestroy(e);

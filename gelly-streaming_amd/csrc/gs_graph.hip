@@ -30,6 +30,176 @@ __global__ __launch_bounds__(256) void k_gather_csr(const uint32_t* __restrict__
   }
 }
 
+
+// ---------------------------------------------------------------------------------------------
+// WindowTriangles: exact count of the reference's matched candidates without emitting them.
+//   T = triangles of the window's simple undirected graph (GenerateCandidateEdges emits each
+//       {b, c} pair of neighbours > v once per v; CountTriangles matches it iff b ~ c, and ALL
+//       makes both (b,c) and (c,b) edge records) -> counted once each by the forward algorithm
+//       on a (degree, id)-oriented CSR with sorted adjacency (merge intersection).
+//   S = self-pair quirk (j = i emits (x, x); matched only if x has a self-loop) — needs
+//       java.util.HashSet iteration order; only windows with self-loops have S != 0.
+// ---------------------------------------------------------------------------------------------
+constexpr uint64_t TRI_MAX_BITS = 28;
+
+// composite symmetric adjacency keys (a << B | b), both directions; self-loops -> sentinel + flag
+__global__ __launch_bounds__(256) void k_tri_sym(const int64_t* __restrict__ src, const int64_t* __restrict__ dst,
+                                                 uint64_t n, uint64_t key_xor, uint32_t B,
+                                                 uint64_t* __restrict__ out, uint32_t* __restrict__ loop_bits,
+                                                 unsigned long long* __restrict__ loops) {
+  const uint64_t sent = (B * 2 >= 64) ? ~0ull : ((1ull << (2 * B)) - 1);
+  for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) {
+    const uint64_t a = (uint64_t)src[i] ^ key_xor, b = (uint64_t)dst[i] ^ key_xor;
+    if (a != b) {
+      out[2 * i] = (a << B) | b;
+      out[2 * i + 1] = (b << B) | a;
+    } else {
+      out[2 * i] = sent;
+      out[2 * i + 1] = sent;
+      atomicOr(&loop_bits[a >> 5], 1u << (a & 31));
+      atomicAdd(loops, 1ull);
+    }
+  }
+}
+
+// per vertex row of the unique symmetric adjacency: deg[v], rowstart[v]
+struct RowOut {
+  uint32_t* deg;
+  uint32_t* rowstart;
+  __device__ void store(uint32_t, int64_t k, uint64_t cnt, uint32_t end_pos) const {
+    deg[k] = (uint32_t)cnt;
+    rowstart[k] = end_pos + 1 - (uint32_t)cnt;
+  }
+};
+
+__device__ __forceinline__ bool oriented(uint32_t du, uint32_t u, uint32_t dv, uint32_t v) {
+  return du < dv || (du == dv && u < v);
+}
+
+constexpr int SCAN_BLOCK = 256, SCAN_ITEMS = 16, SCAN_TILE = SCAN_BLOCK * SCAN_ITEMS;
+
+// keep flag per adjacency entry (u -> v kept iff (deg u, u) < (deg v, v)) + per-tile counts
+__global__ __launch_bounds__(SCAN_BLOCK) void k_orient_count(const uint64_t* __restrict__ adj, uint32_t E2, uint32_t B,
+                                                             const uint32_t* __restrict__ deg,
+                                                             uint8_t* __restrict__ keep, uint32_t* __restrict__ tile_sum) {
+  __shared__ uint32_t ws[SCAN_BLOCK / 64];
+  const uint64_t mask = (1ull << B) - 1;
+  uint32_t cnt = 0;
+  const uint32_t base = blockIdx.x * SCAN_TILE;
+#pragma unroll
+  for (int j = 0; j < SCAN_ITEMS; ++j) {
+    const uint32_t p = base + j * SCAN_BLOCK + threadIdx.x;
+    if (p < E2) {
+      const uint64_t k = adj[p];
+      const uint32_t u = (uint32_t)(k >> B), v = (uint32_t)(k & mask);
+      const bool kp = oriented(deg[u], u, deg[v], v);
+      keep[p] = kp;
+      cnt += kp;
+    }
+  }
+  cnt = wave_inclusive_sum(cnt);
+  if ((threadIdx.x & 63) == 63) ws[threadIdx.x >> 6] = cnt;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t t = 0;
+    for (int w = 0; w < SCAN_BLOCK / 64; ++w) t += ws[w];
+    tile_sum[blockIdx.x] = t;
+  }
+}
+
+// exclusive scan of tile sums in one workgroup (tiles <= a few 10^5); writes total at [ntiles]
+__global__ __launch_bounds__(1024) void k_scan_tiles(uint32_t* __restrict__ tile_sum, uint32_t ntiles) {
+  __shared__ uint32_t ws[16];
+  __shared__ uint32_t carry;
+  if (threadIdx.x == 0) carry = 0;
+  __syncthreads();
+  for (uint32_t base = 0; base < ntiles; base += 1024) {
+    const uint32_t i = base + threadIdx.x;
+    const uint32_t x = i < ntiles ? tile_sum[i] : 0u;
+    const uint32_t inc = wave_inclusive_sum(x);
+    if ((threadIdx.x & 63) == 63) ws[threadIdx.x >> 6] = inc;
+    __syncthreads();
+    uint32_t off = carry;
+    for (int w = 0; w < (int)(threadIdx.x >> 6); ++w) off += ws[w];
+    if (i < ntiles) tile_sum[i] = off + inc - x;
+    __syncthreads();
+    if (threadIdx.x == 1023) carry = off + inc;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) tile_sum[ntiles] = carry;
+}
+
+// pos[p] = #kept before p (pos[E2] = M); compacted oriented edges (ou, onbr), order preserved
+__global__ __launch_bounds__(SCAN_BLOCK) void k_orient_scatter(const uint64_t* __restrict__ adj, uint32_t E2, uint32_t B,
+                                                               const uint8_t* __restrict__ keep,
+                                                               const uint32_t* __restrict__ tile_off,
+                                                               uint32_t* __restrict__ pos, uint32_t* __restrict__ ou,
+                                                               uint32_t* __restrict__ onbr) {
+  __shared__ uint32_t ws[SCAN_BLOCK / 64];
+  const uint64_t mask = (1ull << B) - 1;
+  const uint32_t base = blockIdx.x * SCAN_TILE;
+  // blocked: thread t owns entries [base + t*ITEMS, +ITEMS) so the scan order is entry order
+  const uint32_t first = base + threadIdx.x * SCAN_ITEMS;
+  uint32_t cnt = 0;
+#pragma unroll
+  for (int j = 0; j < SCAN_ITEMS; ++j) {
+    const uint32_t p = first + j;
+    if (p < E2) cnt += keep[p];
+  }
+  const uint32_t inc = wave_inclusive_sum(cnt);
+  if ((threadIdx.x & 63) == 63) ws[threadIdx.x >> 6] = inc;
+  __syncthreads();
+  uint32_t off = tile_off[blockIdx.x] + inc - cnt;
+  for (int w = 0; w < (int)(threadIdx.x >> 6); ++w) off += ws[w];
+#pragma unroll
+  for (int j = 0; j < SCAN_ITEMS; ++j) {
+    const uint32_t p = first + j;
+    if (p < E2) {
+      pos[p] = off;
+      if (keep[p]) {
+        const uint64_t k = adj[p];
+        ou[off] = (uint32_t)(k >> B);
+        onbr[off] = (uint32_t)(k & mask);
+        ++off;
+      }
+    }
+  }
+  if (blockIdx.x == gridDim.x - 1 && threadIdx.x == SCAN_BLOCK - 1) pos[E2] = tile_off[gridDim.x];
+}
+
+// sum over oriented edges u -> v of |N+(u) ∩ N+(v)| (sorted lists: merge)
+__global__ __launch_bounds__(256) void k_tri_count(const uint32_t* __restrict__ ou, const uint32_t* __restrict__ onbr,
+                                                   uint32_t M, const uint32_t* __restrict__ deg,
+                                                   const uint32_t* __restrict__ rowstart,
+                                                   const uint32_t* __restrict__ pos,
+                                                   unsigned long long* __restrict__ total) {
+  uint64_t t = 0;
+  for (uint32_t q = blockIdx.x * 256u + threadIdx.x; q < M; q += gridDim.x * 256u) {
+    const uint32_t u = ou[q], v = onbr[q];
+    uint32_t a = pos[rowstart[u]], a1 = pos[rowstart[u] + deg[u]];
+    uint32_t b = pos[rowstart[v]], b1 = pos[rowstart[v] + deg[v]];
+    if (a == a1 || b == b1) continue;
+    uint32_t x = onbr[a], y = onbr[b];
+    while (true) {
+      if (x < y) {
+        if (++a == a1) break;
+        x = onbr[a];
+      } else if (x > y) {
+        if (++b == b1) break;
+        y = onbr[b];
+      } else {
+        ++t;
+        if (++a == a1 || ++b == b1) break;
+        x = onbr[a];
+        y = onbr[b];
+      }
+    }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) t += __shfl_xor(t, o, 64);
+  if ((threadIdx.x & 63) == 0 && t) atomicAdd(total, (unsigned long long)t);
+}
+
 }  // namespace gs
 
 using namespace gs;
@@ -116,12 +286,98 @@ gs_status gs_window_candidates(gs_ctx* c, const gs_edge_batch* b, gs_pair_out* o
 
 gs_status gs_window_triangles(gs_ctx* c, const gs_edge_batch* b, uint64_t* count, int32_t* count_ref_wrapped,
                               int32_t* has_output) {
-  if (!c) return GS_EINVAL;
-  (void)b;
-  (void)count;
-  (void)count_ref_wrapped;
-  (void)has_output;
-  return set_error(c, GS_EUNSUPPORTED, "gs_window_triangles: not built yet");
+  GS_TRY(check_batch(c, b, GS_DIR_ALL));
+  if (!count || !count_ref_wrapped || !has_output) return set_error(c, GS_EINVAL, "null output pointer");
+  GS_HIP(hipSetDevice(c->device));
+  *count = 0;
+  *count_ref_wrapped = 0;
+  *has_output = b->n > 0;   // every edge record forms a (v, t) group with edges > 0 (WindowTriangles.java:136)
+  if (b->n == 0) return GS_OK;
+  hipEventRecord(c->ev[0], c->stream);
+  const int64_t *src, *dst;
+  const void* val;
+  GS_TRY(stage_batch(c, b, &src, &dst, &val, false));
+  char* sm = c->small.as<char>();
+  const uint64_t n = b->n;
+  // key range of the window (same scan as the sort)
+  GS_HIP(hipMemsetAsync(sm, 0, SM_BASE, c->stream));
+  GS_TRY(launch_keyinfo_all(c, src, dst, n));
+  GS_HIP(hipMemcpyAsync(sm + SM_K0, src, 8, hipMemcpyDeviceToDevice, c->stream));
+  GS_HIP(hipMemcpyAsync(c->host_small, sm, 16, hipMemcpyDeviceToHost, c->stream));
+  GS_HIP(hipStreamSynchronize(c->stream));
+  const uint64_t mask = c->host_small[0], k0 = c->host_small[1];
+  const uint32_t B = mask ? 64 - __builtin_clzll(mask) : 1;
+  if (B > TRI_MAX_BITS)
+    return set_error(c, GS_EUNSUPPORTED, "window triangles: vertex IDs span %u bits (> %llu) — relabeling not built yet",
+                     B, (unsigned long long)TRI_MAX_BITS);
+  const uint64_t key_xor = k0 & ~((1ull << B) - 1);
+  const uint64_t R = 2 * n;
+  // 1. symmetric composite keys (+ self-loop bitmap)
+  GS_TRY(ensure(c, c->aux, R * 8));
+  const size_t words = ((1ull << B) + 31) / 32;
+  GS_TRY(ensure(c, c->tri_loops, words * 4));
+  GS_HIP(hipMemsetAsync(c->tri_loops.p, 0, words * 4, c->stream));
+  unsigned long long* d_loops = (unsigned long long*)(sm + SM_NUNIQUE);
+  const unsigned g = (unsigned)std::min<uint64_t>((n + 255) / 256, 8192);
+  hipLaunchKernelGGL(k_tri_sym, dim3(g), dim3(256), 0, c->stream, src, dst, n, key_xor, B, c->aux.as<uint64_t>(),
+                     c->tri_loops.as<uint32_t>(), d_loops);
+  GS_HIP(hipGetLastError());
+  GS_HIP(hipMemcpyAsync(c->host_small + 4, d_loops, 8, hipMemcpyDeviceToHost, c->stream));
+  // 2. sort + unique -> symmetric simple adjacency, sorted by (u, v)
+  Sorted s;
+  GS_TRY(sort_buffer(c, c->aux.as<uint64_t>(), nullptr, R, &s));
+  const uint64_t loops = c->host_small[4];
+  if (loops)
+    return set_error(c, GS_EUNSUPPORTED,
+                     "window triangles: %llu self-loop edge(s) — the HashSet-order self-pair term is not built yet",
+                     (unsigned long long)loops);
+  GS_TRY(ensure(c, c->out_keys, R * 8));
+  uint64_t E2 = 0;
+  UniqueOut uo{c->out_keys.as<uint64_t>(), nullptr};
+  GS_TRY((s.wide ? launch_rbk<uint64_t, CountOp>(c, s, uo, &E2) : launch_rbk<uint32_t, CountOp>(c, s, uo, &E2)));
+  // 3. rows: degree + row start per vertex (segment by u = key >> B)
+  const size_t V = 1ull << B;
+  GS_TRY(ensure(c, c->out_a, V * 4));
+  GS_TRY(ensure(c, c->out_b, V * 4));
+  Sorted adj;
+  adj.keys = c->out_keys.p;
+  adj.wide = true;
+  adj.key_xor = 0;
+  adj.records = E2;
+  RowOut ro{c->out_a.as<uint32_t>(), c->out_b.as<uint32_t>()};
+  uint64_t nv = 0;
+  GS_TRY((launch_rbk<uint64_t, CountOp>(c, adj, ro, &nv, B)));
+  // 4. orientation by (degree, id): keep flags, scan, compaction (order preserved)
+  const uint32_t tiles = (uint32_t)((E2 + SCAN_TILE - 1) / SCAN_TILE);
+  GS_TRY(ensure(c, c->tri_keep, E2 + 16));
+  GS_TRY(ensure(c, c->tri_tiles, (tiles + 1) * 4));
+  GS_TRY(ensure(c, c->tri_pos, (E2 + 1) * 4));
+  GS_TRY(ensure(c, c->tri_ou, E2 * 4));
+  GS_TRY(ensure(c, c->tri_onbr, E2 * 4));
+  hipLaunchKernelGGL(k_orient_count, dim3(tiles), dim3(SCAN_BLOCK), 0, c->stream, c->out_keys.as<uint64_t>(),
+                     (uint32_t)E2, B, c->out_a.as<uint32_t>(), c->tri_keep.as<uint8_t>(), c->tri_tiles.as<uint32_t>());
+  hipLaunchKernelGGL(k_scan_tiles, dim3(1), dim3(1024), 0, c->stream, c->tri_tiles.as<uint32_t>(), tiles);
+  hipLaunchKernelGGL(k_orient_scatter, dim3(tiles), dim3(SCAN_BLOCK), 0, c->stream, c->out_keys.as<uint64_t>(),
+                     (uint32_t)E2, B, c->tri_keep.as<uint8_t>(), c->tri_tiles.as<uint32_t>(),
+                     c->tri_pos.as<uint32_t>(), c->tri_ou.as<uint32_t>(), c->tri_onbr.as<uint32_t>());
+  GS_HIP(hipGetLastError());
+  const uint64_t M = E2 / 2;   // each undirected edge kept in exactly one direction
+  // 5. merge intersections
+  unsigned long long* d_total = (unsigned long long*)(sm + SM_NUNIQUE);
+  GS_HIP(hipMemsetAsync(d_total, 0, 8, c->stream));
+  const unsigned g2 = (unsigned)std::min<uint64_t>((M + 255) / 256, 16384);
+  hipLaunchKernelGGL(k_tri_count, dim3(std::max(1u, g2)), dim3(256), 0, c->stream, c->tri_ou.as<uint32_t>(),
+                     c->tri_onbr.as<uint32_t>(), (uint32_t)M, c->out_a.as<uint32_t>(), c->out_b.as<uint32_t>(),
+                     c->tri_pos.as<uint32_t>(), d_total);
+  GS_HIP(hipGetLastError());
+  hipEventRecord(c->ev[3], c->stream);
+  GS_HIP(hipMemcpyAsync(c->host_small, sm, 32, hipMemcpyDeviceToHost, c->stream));
+  GS_HIP(hipStreamSynchronize(c->stream));
+  if ((uint32_t)c->host_small[3] != 0) return set_error(c, GS_EDEVICE, "look-back spin timed out");
+  const uint64_t T = c->host_small[2];
+  *count = T;
+  *count_ref_wrapped = (int32_t)(uint32_t)T;   // Integer sum(0) wraps (WindowTriangles.java:66, :126)
+  return GS_OK;
 }
 
 }  // extern "C"

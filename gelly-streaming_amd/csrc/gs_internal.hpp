@@ -45,6 +45,8 @@ struct gs_ctx {
   gs::DevBuf small;
   // output staging
   gs::DevBuf out_keys, out_a, out_b, aux;
+  // triangles
+  gs::DevBuf tri_loops, tri_keep, tri_tiles, tri_pos, tri_ou, tri_onbr;
   hipEvent_t ev[6] = {};
   hipEvent_t pass_ev[9] = {};
   gs_stage_times times{};
@@ -72,6 +74,13 @@ uint32_t next_epoch(gs_ctx* c, size_t status_bytes_hint);
 // 2 neighbour (int64), 3 record index (u32).  src/dst/val are device pointers.
 gs_status sort_window(gs_ctx* c, const int64_t* src, const int64_t* dst, const void* val, int val_bytes,
                       uint64_t n_edges, int dir, int payload, Sorted* out);
+
+// Sort an unsigned 64-bit key buffer (stable), optional u32 payload; keys of <= 32 varying bits are
+// compacted to u32 (key = key_xor ^ compact).  `keys` must be 16-byte aligned.
+gs_status sort_buffer(gs_ctx* c, const uint64_t* keys, const uint32_t* vals, uint64_t n, Sorted* out);
+
+// k_keyinfo over both columns (ALL): mask at SM_MASK, byte histograms at SM_HIST
+gs_status launch_keyinfo_all(gs_ctx* c, const int64_t* src, const int64_t* dst, uint64_t n);
 
 // Stage a batch on the device (copies host columns into ctx buffers); returns device pointers.
 gs_status stage_batch(gs_ctx* c, const gs_edge_batch* b, const int64_t** src, const int64_t** dst,

@@ -33,7 +33,7 @@ constexpr int RBK_BLOCK = GS_RBK_BLOCK, RBK_ITEMS = GS_RBK_ITEMS, RBK_TILE = RBK
 
 // ---- reduce-by-key launch ----------------------------------------------------------------------
 template <typename K, class Op, class Out>
-inline gs_status launch_rbk(gs_ctx* c, const Sorted& s, Out o, uint64_t* n_unique_host) {
+inline gs_status launch_rbk(gs_ctx* c, const Sorted& s, Out o, uint64_t* n_unique_host, uint32_t key_shift = 0) {
   char* sm = c->small.as<char>();
   const uint32_t R = (uint32_t)s.records;
   const uint32_t tiles = (R + RBK_TILE - 1) / RBK_TILE;
@@ -43,7 +43,8 @@ inline gs_status launch_rbk(gs_ctx* c, const Sorted& s, Out o, uint64_t* n_uniqu
   GS_TRY(ensure(c, c->rbk_inc, (size_t)tiles * 8 * SLOTS));
   const uint32_t ep = next_epoch(c, 0);
   hipLaunchKernelGGL((k_reduce_by_key<K, Op, Out, RBK_BLOCK, RBK_ITEMS>), dim3(tiles), dim3(RBK_BLOCK), 0, c->stream,
-                     (const K*)s.keys, (const typename Op::In*)s.vals, R, s.key_xor, o, c->rbk_word.as<uint64_t>(),
+                     (const K*)s.keys, (const typename Op::In*)s.vals, R, s.key_xor, key_shift, o,
+                     c->rbk_word.as<uint64_t>(),
                      c->rbk_agg.as<uint64_t>(), c->rbk_inc.as<uint64_t>(), (uint32_t*)(sm + SM_COUNTERS) + 63, tiles,
                      ep, (uint32_t*)(sm + SM_TIMEOUT), (unsigned long long*)(sm + SM_NUNIQUE));
   GS_HIP(hipGetLastError());

@@ -59,6 +59,50 @@ struct BufSrc {
   }
 };
 
+// u64 key buffer (composite keys) -> key type K: k = (K)(key ^ key_xor)
+template <typename K, typename V>
+struct ConvSrc {
+  const uint64_t* keys;
+  const V* vals;
+  uint64_t key_xor;
+  __device__ __forceinline__ void load(uint32_t r, K& k, V& v) const {
+    k = (K)(keys[r] ^ key_xor);
+    if (vals) v = vals[r];
+  }
+};
+
+// mask + histograms of all 8 bytes of an unsigned 64-bit key buffer (16-byte aligned)
+static __global__ __launch_bounds__(256) void k_keyinfo_buf(const uint64_t* __restrict__ keys, uint64_t n,
+                                                     unsigned long long* __restrict__ mask_out,
+                                                     uint32_t* __restrict__ hist_out /*[8][256]*/) {
+  __shared__ uint32_t h[8][RADIX];
+  const int tid = threadIdx.x;
+  for (int i = tid; i < 8 * RADIX; i += 256) (&h[0][0])[i] = 0;
+  __syncthreads();
+  const uint64_t k0 = keys[0];
+  uint64_t m = 0;
+  auto add = [&](uint64_t k) {
+    m |= k ^ k0;
+#pragma unroll
+    for (int b = 0; b < 8; ++b) atomicAdd(&h[b][(k >> (8 * b)) & 255u], 1u);
+  };
+  const ulonglong2* k2 = reinterpret_cast<const ulonglong2*>(keys);
+  const uint64_t npair = n >> 1;
+  for (uint64_t q = (uint64_t)blockIdx.x * 256u + tid; q < npair; q += (uint64_t)gridDim.x * 256u) {
+    const ulonglong2 x = k2[q];
+    add(x.x);
+    add(x.y);
+  }
+  if ((n & 1) && blockIdx.x == 0 && tid == 0) add(keys[n - 1]);
+  m = wave_or(m);
+  if ((tid & 63) == 0 && m) atomicOr(mask_out, (unsigned long long)m);
+  __syncthreads();
+  for (int i = tid; i < 8 * RADIX; i += 256) {
+    const uint32_t c = (&h[0][0])[i];
+    if (c) atomicAdd(&hist_out[i], c);
+  }
+}
+
 // ---- k_keyinfo ------------------------------------------------------------------------------
 template <int DIR, bool VEC>
 __global__ __launch_bounds__(256) void k_keyinfo(const int64_t* __restrict__ src, const int64_t* __restrict__ dst,

@@ -104,6 +104,15 @@ struct CountOut {
     vals[u] = (int64_t)((uint64_t)init + a);
   }
 };
+// distinct keys of a sorted array (key_xor = 0): keys[u] = key, counts[u] = multiplicity (optional)
+struct UniqueOut {
+  uint64_t* keys;
+  uint32_t* counts;
+  __device__ void store(uint32_t u, int64_t k, uint64_t a, uint32_t) const {
+    keys[u] = (uint64_t)k;
+    if (counts) counts[u] = (uint32_t)a;
+  }
+};
 // CSR: offsets[u+1] = one past the last record of vertex u (offsets[0] = 0 is set by the host)
 struct CsrOut {
   int64_t* keys;
@@ -207,7 +216,8 @@ __device__ __forceinline__ uint32_t pad32(uint32_t i) { return i + (i >> 5); }
 // keys: sorted compact keys; vals: payload in the same order (unused when !Op::HAS_V)
 template <typename K, class Op, class Out, int BLOCK, int ITEMS>
 __global__ __launch_bounds__(BLOCK) void k_reduce_by_key(const K* __restrict__ keys, const typename Op::In* __restrict__ vals,
-                                                         uint32_t n, uint64_t key_xor, Out out, uint64_t* __restrict__ st_word,
+                                                         uint32_t n, uint64_t key_xor, uint32_t key_shift, Out out,
+                                                         uint64_t* __restrict__ st_word,
                                                          uint64_t* __restrict__ st_agg, uint64_t* __restrict__ st_inc,
                                                          uint32_t* __restrict__ tile_ctr, uint32_t ntiles, uint32_t epoch,
                                                          uint32_t* __restrict__ timeout, unsigned long long* __restrict__ n_unique) {
@@ -236,13 +246,13 @@ __global__ __launch_bounds__(BLOCK) void k_reduce_by_key(const K* __restrict__ k
   for (int j = 0; j < ITEMS; ++j) {
     const uint32_t i = (uint32_t)j * BLOCK + tid;
     if (i < tile_n) {
-      s_k[pad32(i)] = keys[tbase + i];
+      s_k[pad32(i)] = keys[tbase + i] >> key_shift;
       if constexpr (Op::HAS_V) s_v[pad32(i)] = vals[tbase + i];
     }
   }
   if (tid == 0) {
-    s_prev = tbase > 0 ? keys[tbase - 1] : (K)0;
-    s_next = (tbase + tile_n < n) ? keys[tbase + tile_n] : (K)0;
+    s_prev = tbase > 0 ? (K)(keys[tbase - 1] >> key_shift) : (K)0;
+    s_next = (tbase + tile_n < n) ? (K)(keys[tbase + tile_n] >> key_shift) : (K)0;
   }
   __syncthreads();
 
