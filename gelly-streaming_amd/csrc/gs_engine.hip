@@ -121,6 +121,7 @@ static gs_status launch_pass(gs_ctx* c, Src src, K* kout, V* vout, uint32_t R, i
   char* sm = c->small.as<char>();
   const uint32_t tiles = (R + SORT_TILE - 1) / SORT_TILE;
   const uint32_t ep = next_epoch(c, 0);
+  GS_HIP(hipMemsetAsync((uint32_t*)(sm + SM_COUNTERS) + pass, 0, 4, c->stream));
   hipLaunchKernelGGL((k_onesweep<K, V, HAS_V, SORT_BLOCK, SORT_ITEMS, Src>), dim3(tiles), dim3(SORT_BLOCK), 0,
                      c->stream, src, kout, vout, R, shift, (const uint32_t*)(sm + SM_BASE) + pass * RADIX,
                      c->sort_status.as<uint64_t>(), (uint32_t*)(sm + SM_COUNTERS) + pass, ep,

@@ -42,6 +42,7 @@ inline gs_status launch_rbk(gs_ctx* c, const Sorted& s, Out o, uint64_t* n_uniqu
   GS_TRY(ensure(c, c->rbk_agg, (size_t)tiles * 8 * SLOTS));
   GS_TRY(ensure(c, c->rbk_inc, (size_t)tiles * 8 * SLOTS));
   const uint32_t ep = next_epoch(c, 0);
+  GS_HIP(hipMemsetAsync((uint32_t*)(sm + SM_COUNTERS) + 63, 0, 4, c->stream));   // fresh tile counter per launch
   hipLaunchKernelGGL((k_reduce_by_key<K, Op, Out, RBK_BLOCK, RBK_ITEMS>), dim3(tiles), dim3(RBK_BLOCK), 0, c->stream,
                      (const K*)s.keys, (const typename Op::In*)s.vals, R, s.key_xor, key_shift, o,
                      c->rbk_word.as<uint64_t>(),

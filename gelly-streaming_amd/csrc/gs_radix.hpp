@@ -236,6 +236,7 @@ __global__ __launch_bounds__(BLOCK) void k_onesweep(Src src, K* __restrict__ kou
   __syncthreads();
   const uint32_t tile = s_tile;
   const uint32_t tbase = tile * (uint32_t)TILE;
+  if (tbase >= n) return;   // defensive: a stale counter can never index past the input
   const uint32_t tile_n = min((uint32_t)TILE, n - tbase);
 
   // load (wave-striped) + rank within the wave, in record order

@@ -238,6 +238,7 @@ __global__ __launch_bounds__(BLOCK) void k_reduce_by_key(const K* __restrict__ k
   if (tid == 0) s_tile = atomicAdd(tile_ctr, 1u);
   __syncthreads();
   const uint32_t tile = s_tile;
+  if (tile >= ntiles) return;   // defensive: a stale counter can never index past the input
   const uint32_t tbase = tile * (uint32_t)TILE;
   const uint32_t tile_n = min((uint32_t)TILE, n - tbase);
 

@@ -1,0 +1,69 @@
+"""CPU: the C-ABI library loads and exports every entry point include/gelly_hip.h declares.
+No compute call is made here (no GPU in the build container)."""
+import ctypes
+import re
+import subprocess
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent.parent
+HEADER = ROOT / "include" / "gelly_hip.h"
+
+
+def declared():
+    return sorted(set(re.findall(r"^GS_API\s+[\w\s\*]+?\b(gs_\w+)\s*\(", HEADER.read_text(), re.M)))
+
+
+def test_header_declares_abi():
+    names = declared()
+    assert "gs_window_reduce" in names and "gs_window_triangles" in names and len(names) >= 18
+
+
+def test_library_exports_every_declared_symbol(pkg):
+    lib = pkg.load_library()
+    so = Path(lib._name)
+    out = subprocess.run(["nm", "-D", "--defined-only", str(so)], capture_output=True, text=True, check=True).stdout
+    exported = set(re.findall(r"\bT (gs_\w+)", out))
+    missing = [n for n in declared() if n not in exported]
+    assert not missing, f"declared but not exported: {missing}"
+    for n in declared():
+        assert getattr(lib, n) is not None
+    from gelly_streaming_amd import _lib
+    assert sorted(_lib.EXPORTS) == declared()
+
+
+def test_abi_version_and_no_device_error(pkg):
+    lib = pkg.load_library()
+    assert lib.gs_abi_version() == 1
+    import torch
+    if not torch.cuda.is_available():
+        # lifecycle only: gs_create must fail cleanly (status, no abort) when no HIP device exists
+        ctx = ctypes.c_void_p()
+        from gelly_streaming_amd import _lib
+        st = lib.gs_create(ctypes.byref(_lib.GsConfig(0, 0, 0)), ctypes.byref(ctx))
+        assert st == _lib.GS_EDEVICE and not ctx.value
+        assert lib.gs_last_error(None) == b"null context"
+
+
+def test_engine_fails_loudly_without_device(pkg):
+    import pytest
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    with pytest.raises(pkg.GsError):
+        pkg.Engine(0)
+
+
+def test_struct_layouts_match_header(pkg):
+    """ctypes mirrors of the ABI structs have the sizes the C compiler gives them."""
+    from gelly_streaming_amd import _lib
+    src = "#include <stdio.h>\n#include \"gelly_hip.h\"\nint main(){printf(\"%zu %zu %zu %zu %zu %zu %zu\\n\"," \
+          "sizeof(gs_config),sizeof(gs_edge_batch),sizeof(gs_vertex_out),sizeof(gs_degree_out)," \
+          "sizeof(gs_csr_out),sizeof(gs_pair_out),sizeof(gs_stage_times));}"
+    tmp = ROOT / "gpurun_out"
+    tmp.mkdir(exist_ok=True)
+    (tmp / "sz.c").write_text(src)
+    subprocess.run(["gcc", "-I", str(ROOT / "include"), str(tmp / "sz.c"), "-o", str(tmp / "sz")], check=True)
+    got = [int(x) for x in subprocess.run([str(tmp / "sz")], capture_output=True, text=True).stdout.split()]
+    want = [ctypes.sizeof(t) for t in (_lib.GsConfig, _lib.GsEdgeBatch, _lib.GsVertexOut, _lib.GsDegreeOut,
+                                       _lib.GsCsrOut, _lib.GsPairOut, _lib.GsStageTimes)]
+    assert got == want

@@ -1,0 +1,83 @@
+"""CPU, world_size 2 (gloo): the keyBy exchange of distributed.py — per-rank pre-reduce, vertex-range
+owners, all_to_all of partials, merge — equals the single-window oracle on the whole window.
+The local per-rank reduce is the oracle here (test infrastructure); on GPUs it is the engine."""
+import os
+import socket
+import sys
+from pathlib import Path
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+ROOT = Path(__file__).resolve().parent.parent
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    sys.path.insert(0, str(ROOT))
+    import __graft_entry__ as ge
+    ge.load_package()
+    from gelly_streaming_amd import distributed as D
+    orc = ge.load_oracle()
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    n = 40000
+    s, d = orc.gen_rmat(12, n, 0x5EED03, a=0.65, b=0.15, c=0.15, permute=False, first_edge=rank * n)
+    v = orc.gen_values(n, 5, orc.DT_I64, first_edge=rank * n)
+
+    def local_reduce(src, dst, val, direction, op):
+        tn = lambda t: t.numpy() if isinstance(t, torch.Tensor) else t
+        k, r = orc.window_reduce(tn(src), tn(dst), tn(val), direction, op)
+        return torch.from_numpy(k.copy()), torch.from_numpy(r.copy())
+
+    def local_fold(src, dst, direction, init_max):
+        k, dg, mx = orc.window_fold_degree_max(src, dst, direction, init_max)
+        return torch.from_numpy(k.copy()), torch.from_numpy(dg.copy()), torch.from_numpy(mx.copy())
+
+    res = {}
+    for direction in (0, 1, 2):
+        for op in (0, 1, 2, 3):
+            k, r = D.reduce_window(local_reduce, s, d, v, direction, op)
+            res[(direction, op)] = (k.numpy(), r.numpy())
+        k, dg, mx = D.fold_degree_max_window(local_fold, local_reduce, s, d, direction, -(1 << 63))
+        res[(direction, "deg")] = (k.numpy(), dg.numpy(), mx.numpy())
+    q.put((rank, res))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_reduce_window_two_ranks(oracle):
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = dict(q.get(timeout=300) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    n = 40000
+    s, d = oracle.gen_rmat(12, 2 * n, 0x5EED03, a=0.65, b=0.15, c=0.15, permute=False)
+    v = oracle.gen_values(2 * n, 5, oracle.DT_I64)
+    for direction in (0, 1, 2):
+        for op in (0, 1, 2, 3):
+            k = np.concatenate([out[r][(direction, op)][0] for r in range(world)])
+            r_ = np.concatenate([out[r][(direction, op)][1] for r in range(world)])
+            wk, wv = oracle.window_reduce(s, d, v, direction, op)
+            assert np.array_equal(k, wk) and np.array_equal(r_, wv), (direction, op)
+        k = np.concatenate([out[r][(direction, "deg")][0] for r in range(world)])
+        dg = np.concatenate([out[r][(direction, "deg")][1] for r in range(world)])
+        mx = np.concatenate([out[r][(direction, "deg")][2] for r in range(world)])
+        wk, wd, wm = oracle.window_fold_degree_max(s, d, direction)
+        assert np.array_equal(k, wk) and np.array_equal(dg, wd) and np.array_equal(mx, wm)

@@ -1,0 +1,58 @@
+"""CPU: host-side logic of the API mirror (windowing, direction/time types, shuffle partitioning)."""
+import numpy as np
+import pytest
+
+
+def test_edge_direction_ordinals(pkg):
+    # org.apache.flink.graph.EdgeDirection: IN, OUT, ALL
+    assert [int(pkg.EdgeDirection.IN), int(pkg.EdgeDirection.OUT), int(pkg.EdgeDirection.ALL)] == [0, 1, 2]
+
+
+def test_time(pkg):
+    assert pkg.Time.of(1, pkg.TimeUnit.SECONDS).toMilliseconds() == 1000
+    assert pkg.Time.milliseconds(400).toMilliseconds() == 400
+
+
+def test_slice_rejects_bad_direction(pkg):
+    env = pkg.StreamExecutionEnvironment()
+    g = pkg.SimpleEdgeStream(env.fromCollection([(1, 2, 3)]), env)
+    with pytest.raises(ValueError):
+        g.slice(pkg.Time.seconds(1), 7)
+
+
+def test_tumbling_window_assignment(pkg):
+    """Flink 1.0.3 TumblingEventTimeWindows: start = ts - ts % size (Java remainder), ascending windows,
+    arrival order kept inside a window."""
+    env = pkg.StreamExecutionEnvironment()
+    ts = np.array([100, 150, 399, 400, 799, 800, 1000], dtype=np.int64)
+    cols = pkg.EdgeColumns(np.arange(7, dtype=np.int64), np.arange(7, dtype=np.int64) + 1,
+                           np.arange(7, dtype=np.int64), ts)
+    ws = pkg.SimpleEdgeStream(cols, env)._windows(400)
+    assert [(s, e) for s, e, _ in ws] == [(0, 400), (400, 800), (800, 1200)]
+    assert [list(w.src) for _, _, w in ws] == [[0, 1, 2], [3, 4], [5, 6]]
+    neg = pkg.EdgeColumns(np.array([1]), np.array([2]), None, np.array([-5], dtype=np.int64))
+    (s, e, _), = pkg.SimpleEdgeStream(neg, env)._windows(400)
+    assert s == 0   # Java: -5 % 400 == -5 -> start = -5 - (-5) = 0
+
+
+def test_undirected_and_reverse_columns(pkg):
+    """TestUndirected / TestReverse shapes on the columnar stream."""
+    env = pkg.StreamExecutionEnvironment()
+    g = pkg.SimpleEdgeStream(env.fromCollection([(1, 2, 12), (1, 3, 13)]), env)
+    u = g.undirected().getEdges()
+    assert list(zip(u.src, u.dst, u.val)) == [(1, 2, 12), (2, 1, 12), (1, 3, 13), (3, 1, 13)]
+    r = g.reverse().getEdges()
+    assert list(zip(r.src, r.dst, r.val)) == [(2, 1, 12), (3, 1, 13)]
+
+
+def test_owner_bounds_partition(pkg):
+    from gelly_streaming_amd import distributed as D
+    assert D.owner_bounds(0, 99, 4) == [25, 50, 75]
+    assert D.owner_bounds(-(1 << 63), (1 << 63) - 1, 2) == [0]
+    assert D.merge_op(D.COUNT) == D.SUM and D.merge_op(D.MAX) == D.MAX
+
+
+def test_candidates_dispatch_marker(pkg):
+    from gelly_streaming_amd import triangles
+    with pytest.raises(RuntimeError):
+        triangles.GenerateCandidateEdges().applyOnEdges(1, [], None)
