@@ -49,24 +49,32 @@ def parse():
 
 def kernel_table(times_list, E, U_avg):
     """Average per-launch durations (device events inside the library, same stream) and the algorithmic
-    bytes each kernel must move."""
+    bytes each kernel must move ("Kernels and their rooflines")."""
     t0 = times_list[0]
     kb, vb = t0.key_bytes, t0.payload_bytes
+    ab = 8                      # partial accumulator of a Long sum
     passes = t0.sort_passes
+    P = statistics.mean(t.partials for t in times_list)
     rows = {}
     for p in range(passes):
         ms = statistics.mean(t.pass_ms[p] for t in times_list)
-        # pass 0 reads the int64 key column + values, later passes the compact keys; all write compact
-        rd = (8 + vb) if p == 0 else (kb + vb)
-        rows[f"onesweep_pass{p}"] = {"ms": ms, "bytes": E * (rd + kb + vb)}
-    ms = statistics.mean(t.reduce_ms for t in times_list)
-    rows["reduce_by_key"] = {"ms": ms, "bytes": E * (kb + vb) + U_avg * 16}
+        if t0.fused_last and p == passes - 1:
+            rows["onesweep_combine(last pass)"] = {"ms": ms, "bytes": E * (kb + vb) + P * (kb + ab)}
+        else:
+            # pass 0 reads the int64 key column + values, later passes the compact keys; all write compact
+            rd = (8 + vb) if p == 0 else (kb + vb)
+            rows[f"onesweep_pass{p}"] = {"ms": ms, "bytes": E * (rd + kb + vb)}
+    ms = statistics.mean(t.reduce_ms - (t.pass_ms[passes - 1] if t0.fused_last else 0.0) for t in times_list)
+    if t0.fused_last:   # region table + compaction of the partials + reduce_by_key merge
+        rows["merge(compact+reduce_by_key)"] = {"ms": ms, "bytes": 3 * P * (kb + ab) + U_avg * 16}
+    else:
+        rows["reduce_by_key"] = {"ms": ms, "bytes": E * (kb + vb) + U_avg * 16}
     ms = statistics.mean(t.keyinfo_ms for t in times_list)
     rows["keyinfo(+host sync)"] = {"ms": ms, "bytes": E * 8}
     for r in rows.values():
         r["GB/s"] = r["bytes"] / (r["ms"] * 1e-3) / 1e9 if r["ms"] > 0 else 0.0
         r["frac"] = r["GB/s"] / HBM_PEAK_GBS
-    return rows
+    return rows, P
 
 
 def pmc_traffic(kernel: str):
@@ -175,7 +183,7 @@ def main():
     # local window only: the dominant kernel of the single-GPU pipeline
     E_rec = times[0].records
     U_avg = times[0].vertices
-    kt = kernel_table(times, E_rec, U_avg)
+    kt, partials = kernel_table(times, E_rec, U_avg)
     dom_name = max((n for n in kt if not n.startswith("keyinfo")), key=lambda n: kt[n]["ms"])
     dom = kt[dom_name]
     roofline = {"bound": "hbm", "kernel": dom_name, "achieved": round(dom["GB/s"], 1), "peak": HBM_PEAK_GBS,
@@ -204,7 +212,7 @@ def main():
             "config": {"workload": "C2: slice(OUT).reduceOnEdges(SUM) over one R-MAT scale-24 window",
                        "scale": a.scale, "edges_per_window_per_gpu": E, "direction": "OUT", "op": "SUM",
                        "value_dtype": a.dtype, "vertices_out": U_avg, "sort_passes": times[0].sort_passes,
-                       "key_bits": times[0].key_bits,
+                       "key_bits": times[0].key_bits, "partials_after_fused_pass": int(partials),
                        "parallelism": f"vertex-range keyBy over {world} GPU(s)" if world > 1 else "1 GPU"},
             "roofline": roofline,
             "cpu_baseline": cpu,

@@ -70,7 +70,8 @@ class GsPairOut(ctypes.Structure):
 class GsStageTimes(ctypes.Structure):
     _fields_ = [("keyinfo_ms", ctypes.c_float), ("sort_ms", ctypes.c_float), ("reduce_ms", ctypes.c_float),
                 ("total_ms", ctypes.c_float), ("sort_passes", u32), ("key_bits", u32), ("records", u64),
-                ("vertices", u64), ("pass_ms", ctypes.c_float * 8), ("key_bytes", u32), ("payload_bytes", u32)]
+                ("vertices", u64), ("pass_ms", ctypes.c_float * 8), ("key_bytes", u32), ("payload_bytes", u32),
+                ("partials", u64), ("fused_last", u32), ("reserved", u32)]
 
 
 class GsError(RuntimeError):

@@ -140,7 +140,7 @@ static gs_status run_passes(gs_ctx* c, const int64_t* src, const int64_t* dst, c
   hipEventRecord(c->pass_ev[0], c->stream);
   GS_TRY((launch_pass<K, V, HAS_V>(c, es, ka, va, R, 0, 0)));
   hipEventRecord(c->pass_ev[1], c->stream);
-  for (int p = 1; p < out->passes; ++p) {
+  for (int p = 1; p < out->done_passes; ++p) {
     BufSrc<K, V> bs{ka, HAS_V ? va : nullptr, 0};
     GS_TRY((launch_pass<K, V, HAS_V>(c, bs, kb, vb, R, p, 8u * p)));
     hipEventRecord(c->pass_ev[p + 1], c->stream);
@@ -169,7 +169,7 @@ static gs_status dispatch_payload(gs_ctx* c, const int64_t* src, const int64_t* 
 
 template <int DIR>
 static gs_status sort_dir(gs_ctx* c, const int64_t* src, const int64_t* dst, const void* val, int vbytes,
-                          uint64_t n, int payload, Sorted* out) {
+                          uint64_t n, int payload, Sorted* out, bool leave_last) {
   char* sm = c->small.as<char>();
   const uint64_t R = (DIR == DIR_ALL) ? 2 * n : n;
   GS_HIP(hipMemsetAsync(sm, 0, SM_BASE, c->stream));  // mask, k0, counters, timeout, hist
@@ -183,6 +183,7 @@ static gs_status sort_dir(gs_ctx* c, const int64_t* src, const int64_t* dst, con
   out->bits = bits;
   out->wide = bits > 32;
   out->passes = std::max(1, (bits + RADIX_BITS - 1) / RADIX_BITS);
+  out->done_passes = leave_last ? std::max(1, out->passes - 1) : out->passes;
   out->records = R;
   out->key_xor = out->wide ? (1ull << 63) : (k0 & 0xFFFFFFFF00000000ull);
   if (out->wide) GS_TRY(launch_hist_wide<DIR>(c, src, dst, n, out->key_xor));
@@ -241,6 +242,7 @@ gs_status sort_buffer(gs_ctx* c, const uint64_t* keys, const uint32_t* vals, uin
   out->bits = bits;
   out->wide = bits > 32;
   out->passes = std::max(1, (bits + RADIX_BITS - 1) / RADIX_BITS);
+  out->done_passes = out->passes;
   out->records = n;
   out->key_xor = out->wide ? 0 : (k0 & 0xFFFFFFFF00000000ull);
   hipLaunchKernelGGL(k_digit_base, dim3(1), dim3(256), 0, c->stream, (const uint32_t*)(sm + SM_HIST),
@@ -263,11 +265,11 @@ gs_status sort_buffer(gs_ctx* c, const uint64_t* keys, const uint32_t* vals, uin
 }
 
 gs_status sort_window(gs_ctx* c, const int64_t* src, const int64_t* dst, const void* val, int val_bytes,
-                      uint64_t n_edges, int dir, int payload, Sorted* out) {
+                      uint64_t n_edges, int dir, int payload, Sorted* out, bool leave_last) {
   switch (dir) {
-    case DIR_IN: return sort_dir<DIR_IN>(c, src, dst, val, val_bytes, n_edges, payload, out);
-    case DIR_OUT: return sort_dir<DIR_OUT>(c, src, dst, val, val_bytes, n_edges, payload, out);
-    case DIR_ALL: return sort_dir<DIR_ALL>(c, src, dst, val, val_bytes, n_edges, payload, out);
+    case DIR_IN: return sort_dir<DIR_IN>(c, src, dst, val, val_bytes, n_edges, payload, out, leave_last);
+    case DIR_OUT: return sort_dir<DIR_OUT>(c, src, dst, val, val_bytes, n_edges, payload, out, leave_last);
+    case DIR_ALL: return sort_dir<DIR_ALL>(c, src, dst, val, val_bytes, n_edges, payload, out, leave_last);
   }
   return set_error(c, GS_EINVAL, "bad direction %d", dir);
 }
@@ -281,11 +283,11 @@ static gs_status value_rbk(gs_ctx* c, const Sorted& s, int64_t* keys, void* vals
   ValueOut<Op, true> oi{keys, (T*)vals, has_init ? *(const T*)init : T{}};
   ValueOut<Op, false> on{keys, (T*)vals, T{}};
   if (s.wide) {
-    if (has_init) return launch_rbk<uint64_t, Op>(c, s, oi, U);
-    return launch_rbk<uint64_t, Op>(c, s, on, U);
+    if (has_init) return reduce_fused<uint64_t, Op>(c, s, oi, U);
+    return reduce_fused<uint64_t, Op>(c, s, on, U);
   }
-  if (has_init) return launch_rbk<uint32_t, Op>(c, s, oi, U);
-  return launch_rbk<uint32_t, Op>(c, s, on, U);
+  if (has_init) return reduce_fused<uint32_t, Op>(c, s, oi, U);
+  return reduce_fused<uint32_t, Op>(c, s, on, U);
 }
 
 template <typename T>
@@ -350,7 +352,8 @@ void gs_destroy(gs_ctx* c) {
   if (!c) return;
   hipSetDevice(c->device);
   if (c->stream) hipStreamSynchronize(c->stream);
-  for (DevBuf* b : {&c->in_src, &c->in_dst, &c->in_val, &c->keysA, &c->keysB, &c->valsA, &c->valsB, &c->sort_status,
+  for (DevBuf* b : {&c->part_k, &c->part_a, &c->comp_k, &c->comp_a,
+                    &c->in_src, &c->in_dst, &c->in_val, &c->keysA, &c->keysB, &c->valsA, &c->valsB, &c->sort_status,
                     &c->rbk_word, &c->rbk_agg, &c->rbk_inc, &c->small, &c->out_keys, &c->out_a, &c->out_b, &c->aux,
                     &c->tri_loops, &c->tri_keep, &c->tri_tiles, &c->tri_pos, &c->tri_ou, &c->tri_onbr})
     if (b->p) hipFree(b->p);
@@ -416,7 +419,8 @@ static gs_status window_fold_impl(gs_ctx* c, const gs_edge_batch* b, int32_t dir
   GS_TRY(stage_batch(c, b, &src, &dst, &val, op != GS_OP_COUNT));
   Sorted s;
   const int vbytes = (int)dtype_bytes(b->val_dtype);
-  GS_TRY(sort_window(c, src, dst, val, vbytes, b->n, dir, op == GS_OP_COUNT ? PAY_NONE : PAY_VAL, &s));
+  GS_TRY(sort_window(c, src, dst, val, vbytes, b->n, dir, op == GS_OP_COUNT ? PAY_NONE : PAY_VAL, &s, true));
+  s.fused = true;
   hipEventRecord(c->ev[2], c->stream);
   const size_t ob = op == GS_OP_COUNT ? 8 : (size_t)vbytes;
   const bool direct = out->mem == GS_MEM_DEVICE && out->capacity >= R;
@@ -431,7 +435,7 @@ static gs_status window_fold_impl(gs_ctx* c, const gs_edge_batch* b, int32_t dir
   uint64_t U = 0;
   if (op == GS_OP_COUNT) {
     CountOut o{kd, (int64_t*)vd, has_init ? *(const int64_t*)init : 0};
-    GS_TRY((s.wide ? launch_rbk<uint64_t, CountOp>(c, s, o, &U) : launch_rbk<uint32_t, CountOp>(c, s, o, &U)));
+    GS_TRY((s.wide ? reduce_fused<uint64_t, CountOp>(c, s, o, &U) : reduce_fused<uint32_t, CountOp>(c, s, o, &U)));
   } else {
     switch (b->val_dtype) {
       case GS_I32: GS_TRY(value_rbk_op<int32_t>(c, op, s, kd, vd, has_init, init, &U)); break;
@@ -474,7 +478,8 @@ gs_status gs_window_fold_degree_max(gs_ctx* c, const gs_edge_batch* b, int32_t d
   const void* val;
   GS_TRY(stage_batch(c, b, &src, &dst, &val, false));
   Sorted s;
-  GS_TRY(sort_window(c, src, dst, nullptr, 0, b->n, dir, PAY_NBR, &s));
+  GS_TRY(sort_window(c, src, dst, nullptr, 0, b->n, dir, PAY_NBR, &s, true));
+  s.fused = true;
   hipEventRecord(c->ev[2], c->stream);
   const bool direct = out->mem == GS_MEM_DEVICE && out->capacity >= R;
   int64_t *kd = out->keys, *dd = out->degree, *md = out->max_neighbor;
@@ -488,7 +493,7 @@ gs_status gs_window_fold_degree_max(gs_ctx* c, const gs_edge_batch* b, int32_t d
   }
   DegMaxOut o{kd, dd, md, init_max};
   uint64_t U = 0;
-  GS_TRY((s.wide ? launch_rbk<uint64_t, DegMaxOp>(c, s, o, &U) : launch_rbk<uint32_t, DegMaxOp>(c, s, o, &U)));
+  GS_TRY((s.wide ? reduce_fused<uint64_t, DegMaxOp>(c, s, o, &U) : reduce_fused<uint32_t, DegMaxOp>(c, s, o, &U)));
   finish_times(c, s, U);
   *out->n_out = U;
   if (U > out->capacity) return set_error(c, GS_ECAPACITY, "output needs %llu vertices", (unsigned long long)U);

@@ -25,6 +25,8 @@ struct Sorted {
   uint64_t records = 0;
   int bits = 0, passes = 0;
   int payload_bytes = 0;
+  int done_passes = 0;      // passes executed (passes - 1 when the last is left to a fused pass)
+  bool fused = false;       // the last pass ran fused with the combine (gs_combine.hpp)
 };
 
 }  // namespace gs
@@ -45,6 +47,8 @@ struct gs_ctx {
   gs::DevBuf small;
   // output staging
   gs::DevBuf out_keys, out_a, out_b, aux;
+  // fused last pass: partials with gaps, compacted partials
+  gs::DevBuf part_k, part_a, comp_k, comp_a;
   // triangles
   gs::DevBuf tri_loops, tri_keep, tri_tiles, tri_pos, tri_ou, tri_onbr;
   hipEvent_t ev[6] = {};
@@ -63,7 +67,9 @@ constexpr size_t SM_TIMEOUT = 24;      // u32
 constexpr size_t SM_COUNTERS = 32;     // u32[64] tile counters
 constexpr size_t SM_HIST = 32 + 256;   // u32[8][256]
 constexpr size_t SM_BASE = SM_HIST + 8 * 256 * 4;  // u32[8][256]
-constexpr size_t SM_BYTES = SM_BASE + 8 * 256 * 4;
+constexpr size_t SM_TOTAL = SM_BASE + 8 * 256 * 4;   // u64 partial count of the fused pass
+constexpr size_t SM_TABLE = SM_TOTAL + 64;            // u32[513] region table of the fused pass
+constexpr size_t SM_BYTES = SM_TABLE + 520 * 4;
 
 gs_status set_error(gs_ctx* c, gs_status s, const char* fmt, ...);
 gs_status hip_check(gs_ctx* c, hipError_t e, const char* what);
@@ -72,8 +78,9 @@ uint32_t next_epoch(gs_ctx* c, size_t status_bytes_hint);
 
 // Sort the window's records by key (stable).  payload: 0 none, 1 value (val_bytes 4|8),
 // 2 neighbour (int64), 3 record index (u32).  src/dst/val are device pointers.
+// leave_last: run passes 0..P-2 only (at least one) so the caller can fuse the last pass.
 gs_status sort_window(gs_ctx* c, const int64_t* src, const int64_t* dst, const void* val, int val_bytes,
-                      uint64_t n_edges, int dir, int payload, Sorted* out);
+                      uint64_t n_edges, int dir, int payload, Sorted* out, bool leave_last = false);
 
 // Sort an unsigned 64-bit key buffer (stable), optional u32 payload; keys of <= 32 varying bits are
 // compacted to u32 (key = key_xor ^ compact).  `keys` must be 16-byte aligned.

@@ -5,6 +5,7 @@
 #include "gs_internal.hpp"
 #include "gs_radix.hpp"
 #include "gs_rbk.hpp"
+#include "gs_combine.hpp"
 
 #define GS_TRY(x)                       \
   do {                                  \
@@ -28,6 +29,13 @@ namespace gs {
 #ifndef GS_RBK_ITEMS
 #define GS_RBK_ITEMS 16
 #endif
+#ifndef GS_COMB_BLOCK
+#define GS_COMB_BLOCK 256
+#endif
+#ifndef GS_COMB_ITEMS
+#define GS_COMB_ITEMS 16
+#endif
+constexpr int COMB_BLOCK = GS_COMB_BLOCK, COMB_ITEMS = GS_COMB_ITEMS, COMB_TILE = COMB_BLOCK * COMB_ITEMS;
 constexpr int SORT_BLOCK = GS_SORT_BLOCK, SORT_ITEMS = GS_SORT_ITEMS, SORT_TILE = SORT_BLOCK * SORT_ITEMS;
 constexpr int RBK_BLOCK = GS_RBK_BLOCK, RBK_ITEMS = GS_RBK_ITEMS, RBK_TILE = RBK_BLOCK * RBK_ITEMS;
 
@@ -71,13 +79,17 @@ inline void finish_times(gs_ctx* c, const Sorted& s, uint64_t U) {
   c->times.key_bits = (uint32_t)s.bits;
   c->times.records = s.records;
   c->times.vertices = U;
+  const int launched = s.done_passes + (s.fused ? 1 : 0);
   for (int p = 0; p < 8; ++p) {
     float t = 0;
-    if (p < s.passes) hipEventElapsedTime(&t, c->pass_ev[p], c->pass_ev[p + 1]);
+    if (p < launched) hipEventElapsedTime(&t, c->pass_ev[p], c->pass_ev[p + 1]);
     c->times.pass_ms[p] = t;
   }
+  c->times.sort_passes = (uint32_t)launched;
+  if (!s.fused) c->times.partials = 0;
   c->times.key_bytes = s.wide ? 8 : 4;
   c->times.payload_bytes = (uint32_t)s.payload_bytes;
+  c->times.fused_last = s.fused ? 1u : 0u;
 }
 
 // Copy U staged outputs to the caller (host or device) — only when the direct write was impossible.
@@ -98,6 +110,55 @@ inline gs_status check_batch(gs_ctx* c, const gs_edge_batch* b, int dir) {
   if (R >= (1ull << 32)) return set_error(c, GS_EINVAL, "window has %llu records; limit is 2^32-1",
                                           (unsigned long long)R);
   return GS_OK;
+}
+
+// The last radix pass fused with the per-vertex combine (gs_combine.hpp), then the merge of the
+// few partials a vertex leaves when its records straddle tiles.  `s` holds passes 0..P-2.
+template <typename K, class Op, class Out>
+inline gs_status reduce_fused(gs_ctx* c, const Sorted& s, Out o, uint64_t* U) {
+  using Acc = typename Op::Acc;
+  using V = std::conditional_t<Op::HAS_V, typename Op::In, uint8_t>;
+  using MOp = typename MergeOf<Op>::type;
+  char* sm = c->small.as<char>();
+  const uint32_t R = (uint32_t)s.records;
+  const int lp = s.passes - 1;
+  const uint32_t tiles = (R + COMB_TILE - 1) / COMB_TILE;
+  GS_TRY(ensure(c, c->part_k, (size_t)R * sizeof(K)));
+  GS_TRY(ensure(c, c->part_a, (size_t)R * sizeof(Acc)));
+  GS_TRY(ensure(c, c->comp_k, (size_t)R * sizeof(K)));
+  GS_TRY(ensure(c, c->comp_a, (size_t)R * sizeof(Acc)));
+  GS_TRY(ensure(c, c->sort_status, (size_t)tiles * RADIX * 8, true));
+  const uint32_t ep = next_epoch(c, 0);
+  uint32_t* ctr = (uint32_t*)(sm + SM_COUNTERS) + 40;
+  GS_HIP(hipMemsetAsync(ctr, 0, 4, c->stream));
+  const uint32_t* base = (const uint32_t*)(sm + SM_BASE) + lp * RADIX;
+  BufSrc<K, V> bs{(const K*)s.keys, Op::HAS_V ? (const V*)s.vals : nullptr, 0};
+  hipLaunchKernelGGL((k_onesweep_combine<K, Op, COMB_BLOCK, COMB_ITEMS, BufSrc<K, V>>), dim3(tiles), dim3(COMB_BLOCK),
+                     0, c->stream, bs, c->part_k.as<K>(), c->part_a.as<Acc>(), R, 8u * lp, base,
+                     c->sort_status.as<uint64_t>(), ctr, ep, (uint32_t*)(sm + SM_TIMEOUT));
+  GS_HIP(hipGetLastError());
+  hipEventRecord(c->pass_ev[s.done_passes + 1], c->stream);
+  uint32_t* table = (uint32_t*)(sm + SM_TABLE);
+  hipLaunchKernelGGL(k_region_table, dim3(1), dim3(RADIX), 0, c->stream, c->sort_status.as<uint64_t>(), tiles - 1, base,
+                     table, (unsigned long long*)(sm + SM_TOTAL));
+  GS_HIP(hipGetLastError());
+  GS_HIP(hipMemcpyAsync(c->host_small + 5, sm + SM_TOTAL, 8, hipMemcpyDeviceToHost, c->stream));
+  GS_HIP(hipStreamSynchronize(c->stream));
+  const uint64_t parts = c->host_small[5];
+  c->times.partials = parts;
+  const unsigned g = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((parts + 255) / 256, 8192));
+  hipLaunchKernelGGL((k_compact_runs<K, Acc>), dim3(g), dim3(256), 0, c->stream, c->part_k.as<K>(), c->part_a.as<Acc>(),
+                     table, (uint32_t)parts, c->comp_k.as<K>(), c->comp_a.as<Acc>());
+  GS_HIP(hipGetLastError());
+  Sorted m = s;
+  m.keys = c->comp_k.p;
+  m.vals = c->comp_a.p;
+  m.records = parts;
+  if (parts == 0) {
+    *U = 0;
+    return GS_OK;
+  }
+  return launch_rbk<K, MOp>(c, m, o, U);
 }
 
 }  // namespace gs

@@ -56,6 +56,8 @@ class StageTimes:
     pass_ms: list
     key_bytes: int
     payload_bytes: int
+    partials: int
+    fused_last: bool
 
 
 class Engine:
@@ -111,7 +113,8 @@ class Engine:
         t = L.GsStageTimes()
         self._check(self._L.gs_last_stage_times(self.ctx, ctypes.byref(t)))
         return StageTimes(t.keyinfo_ms, t.sort_ms, t.reduce_ms, t.total_ms, t.sort_passes, t.key_bits, t.records,
-                          t.vertices, list(t.pass_ms)[:t.sort_passes], t.key_bytes, t.payload_bytes)
+                          t.vertices, list(t.pass_ms)[:t.sort_passes], t.key_bytes, t.payload_bytes,
+                          t.partials, bool(t.fused_last))
 
     # -- helpers ---------------------------------------------------------------------------------
     def _batch(self, src, dst, val):

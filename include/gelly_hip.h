@@ -214,6 +214,9 @@ typedef struct gs_stage_times {
   uint64_t records, vertices;
   float pass_ms[8];        /* each onesweep launch (device events around the launch)         */
   uint32_t key_bytes, payload_bytes;  /* sorted key / payload widths                          */
+  uint64_t partials;       /* (vertex, partial) pairs left by the fused last pass               */
+  uint32_t fused_last;     /* 1: pass_ms[sort_passes] is the last pass fused with the combine   */
+  uint32_t reserved;
 } gs_stage_times;
 GS_API gs_status gs_last_stage_times(const gs_ctx* ctx, gs_stage_times* out);
 
