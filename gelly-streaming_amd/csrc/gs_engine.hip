@@ -95,12 +95,13 @@ template <int DIR>
 static gs_status launch_keyinfo(gs_ctx* c, const int64_t* src, const int64_t* dst, uint64_t n) {
   char* sm = c->small.as<char>();
   const bool vec = ((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst)) & 15) == 0;
+  const int nd = std::min(4, std::max(1, c->hist_digits));
   if (vec)
     hipLaunchKernelGGL((k_keyinfo<DIR, true>), dim3(grid_for(n, 2048, 2048)), dim3(256), 0, c->stream, src, dst, n,
-                       (unsigned long long*)(sm + SM_MASK), (uint32_t*)(sm + SM_HIST));
+                       nd, (unsigned long long*)(sm + SM_MASK), (uint32_t*)(sm + SM_HIST));
   else
     hipLaunchKernelGGL((k_keyinfo<DIR, false>), dim3(grid_for(n, 2048, 2048)), dim3(256), 0, c->stream, src, dst, n,
-                       (unsigned long long*)(sm + SM_MASK), (uint32_t*)(sm + SM_HIST));
+                       nd, (unsigned long long*)(sm + SM_MASK), (uint32_t*)(sm + SM_HIST));
   return hip_check(c, hipGetLastError(), "k_keyinfo");
 }
 gs_status launch_keyinfo_all(gs_ctx* c, const int64_t* src, const int64_t* dst, uint64_t n) {
@@ -108,12 +109,13 @@ gs_status launch_keyinfo_all(gs_ctx* c, const int64_t* src, const int64_t* dst, 
 }
 
 template <int DIR>
-static gs_status launch_hist_wide(gs_ctx* c, const int64_t* src, const int64_t* dst, uint64_t n, uint64_t key_xor) {
+static gs_status launch_hist_bytes(gs_ctx* c, const int64_t* src, const int64_t* dst, uint64_t n, uint64_t key_xor,
+                                   int b0, int b1) {
   char* sm = c->small.as<char>();
-  GS_HIP(hipMemsetAsync(sm + SM_HIST, 0, 8 * 256 * 4, c->stream));
-  hipLaunchKernelGGL(k_hist_wide<DIR>, dim3(grid_for(n, 256 * 8, 2048)), dim3(256), 0, c->stream, src, dst, n,
-                     key_xor, (uint32_t*)(sm + SM_HIST));
-  return hip_check(c, hipGetLastError(), "k_hist_wide");
+  GS_HIP(hipMemsetAsync(sm + SM_HIST + b0 * 256 * 4, 0, (b1 - b0) * 256 * 4, c->stream));
+  hipLaunchKernelGGL(k_hist_bytes<DIR>, dim3(grid_for(n, 256 * 8, 2048)), dim3(256), 0, c->stream, src, dst, n,
+                     key_xor, b0, b1, (uint32_t*)(sm + SM_HIST));
+  return hip_check(c, hipGetLastError(), "k_hist_bytes");
 }
 
 template <typename K, typename V, bool HAS_V, class Src>
@@ -186,7 +188,10 @@ static gs_status sort_dir(gs_ctx* c, const int64_t* src, const int64_t* dst, con
   out->done_passes = leave_last ? std::max(1, out->passes - 1) : out->passes;
   out->records = R;
   out->key_xor = out->wide ? (1ull << 63) : (k0 & 0xFFFFFFFF00000000ull);
-  if (out->wide) GS_TRY(launch_hist_wide<DIR>(c, src, dst, n, out->key_xor));
+  const int have = std::min(4, std::max(1, c->hist_digits));
+  if (out->wide) GS_TRY(launch_hist_bytes<DIR>(c, src, dst, n, out->key_xor, 0, out->passes));   // sign-flipped bytes
+  else if (out->passes > have) GS_TRY(launch_hist_bytes<DIR>(c, src, dst, n, out->key_xor, have, out->passes));
+  c->hist_digits = std::min(4, out->passes);
   hipLaunchKernelGGL(k_digit_base, dim3(1), dim3(256), 0, c->stream, (const uint32_t*)(sm + SM_HIST),
                      (uint32_t*)(sm + SM_BASE), out->passes);
   GS_HIP(hipGetLastError());

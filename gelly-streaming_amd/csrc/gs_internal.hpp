@@ -37,6 +37,7 @@ struct gs_ctx {
   bool own_stream = false;
   std::string err;
   uint32_t epoch = 0;
+  int hist_digits = 4;   // key-byte histograms keyinfo computes (learned from the previous window)
   // input staging (host batches)
   gs::DevBuf in_src, in_dst, in_val;
   // sort ping-pong

@@ -104,9 +104,11 @@ static __global__ __launch_bounds__(256) void k_keyinfo_buf(const uint64_t* __re
 }
 
 // ---- k_keyinfo ------------------------------------------------------------------------------
+// nd = number of low key bytes to histogram (the ctx predicts it from the previous window; a
+// window that needs more gets k_hist_bytes for the rest)
 template <int DIR, bool VEC>
 __global__ __launch_bounds__(256) void k_keyinfo(const int64_t* __restrict__ src, const int64_t* __restrict__ dst,
-                                                 uint64_t n, unsigned long long* __restrict__ mask_out,
+                                                 uint64_t n, int nd, unsigned long long* __restrict__ mask_out,
                                                  uint32_t* __restrict__ hist_out /*[4][256]*/) {
   __shared__ uint32_t h[4][4][RADIX];  // [wave][byte][bin]
   const int tid = threadIdx.x, w = tid >> 6;
@@ -117,9 +119,9 @@ __global__ __launch_bounds__(256) void k_keyinfo(const int64_t* __restrict__ src
   auto add = [&](uint64_t k) {
     m |= k ^ k0;
     atomicAdd(&h[w][0][k & 255u], 1u);
-    atomicAdd(&h[w][1][(k >> 8) & 255u], 1u);
-    atomicAdd(&h[w][2][(k >> 16) & 255u], 1u);
-    atomicAdd(&h[w][3][(k >> 24) & 255u], 1u);
+    if (nd > 1) atomicAdd(&h[w][1][(k >> 8) & 255u], 1u);
+    if (nd > 2) atomicAdd(&h[w][2][(k >> 16) & 255u], 1u);
+    if (nd > 3) atomicAdd(&h[w][3][(k >> 24) & 255u], 1u);
   };
   if constexpr (!VEC) {   // columns not 16-byte aligned (caller-provided slices)
     const uint64_t stride = (uint64_t)gridDim.x * 256u;
@@ -159,24 +161,24 @@ __global__ __launch_bounds__(256) void k_keyinfo(const int64_t* __restrict__ src
   m = wave_or(m);
   if ((tid & 63) == 0 && m) atomicOr(mask_out, (unsigned long long)m);
   __syncthreads();
-  for (int i = tid; i < 4 * RADIX; i += 256) {
+  for (int i = tid; i < nd * RADIX; i += 256) {
     const uint32_t c = h[0][0][i] + h[1][0][i] + h[2][0][i] + h[3][0][i];
     if (c) atomicAdd(&hist_out[i], c);
   }
 }
 
-// histograms of all 8 bytes of (key ^ key_xor) — only for windows whose keys vary above bit 31
+// histograms of key bytes [b0, b1) of (key ^ key_xor) — the bytes keyinfo did not predict
 template <int DIR>
-__global__ __launch_bounds__(256) void k_hist_wide(const int64_t* __restrict__ src, const int64_t* __restrict__ dst,
-                                                   uint64_t n, uint64_t key_xor, uint32_t* __restrict__ hist_out) {
+__global__ __launch_bounds__(256) void k_hist_bytes(const int64_t* __restrict__ src, const int64_t* __restrict__ dst,
+                                                    uint64_t n, uint64_t key_xor, int b0, int b1,
+                                                    uint32_t* __restrict__ hist_out /*[8][256]*/) {
   __shared__ uint32_t h[8][RADIX];
   const int tid = threadIdx.x;
   for (int i = tid; i < 8 * RADIX; i += 256) (&h[0][0])[i] = 0;
   __syncthreads();
   auto add = [&](uint64_t k) {
     k ^= key_xor;
-#pragma unroll
-    for (int b = 0; b < 8; ++b) atomicAdd(&h[b][(k >> (8 * b)) & 255u], 1u);
+    for (int b = b0; b < b1; ++b) atomicAdd(&h[b][(k >> (8 * b)) & 255u], 1u);
   };
   const uint64_t stride = (uint64_t)gridDim.x * 256u;
   for (uint64_t i = (uint64_t)blockIdx.x * 256u + tid; i < n; i += stride) {
@@ -184,7 +186,7 @@ __global__ __launch_bounds__(256) void k_hist_wide(const int64_t* __restrict__ s
     if (DIR != DIR_OUT) add((uint64_t)dst[i]);
   }
   __syncthreads();
-  for (int i = tid; i < 8 * RADIX; i += 256) {
+  for (int i = tid + b0 * RADIX; i < b1 * RADIX; i += 256) {
     const uint32_t c = (&h[0][0])[i];
     if (c) atomicAdd(&hist_out[i], c);
   }
@@ -289,6 +291,10 @@ __global__ __launch_bounds__(BLOCK) void k_onesweep(Src src, K* __restrict__ kou
     for (int w = 0; w < wid; ++w) off += s_wtot[w];
     s_start[tid] += off;
     uint64_t excl;
+#ifdef GS_ABLATE_NO_LOOKBACK   // timing-only build: plausible but WRONG offsets, no inter-tile wait
+    excl = digit_base[tid] + (uint64_t)tile * cnt;
+    if (excl + cnt > n) excl = n > cnt ? n - cnt : 0;
+#else
     if (tile == 0) {
       excl = digit_base[tid];
     } else {
@@ -300,6 +306,7 @@ __global__ __launch_bounds__(BLOCK) void k_onesweep(Src src, K* __restrict__ kou
       }
       st_agent(status + (uint64_t)tile * RADIX + tid, granule(FLAG_INC, epoch, excl + cnt));
     }
+#endif
     s_goff[tid] = (uint32_t)excl;
   }
   __syncthreads();
