@@ -63,6 +63,8 @@ __global__ __launch_bounds__(BLOCK) void k_onesweep_combine(Src src, K* __restri
   __shared__ uint32_t s_start[RADIX];
   __shared__ uint32_t s_rcnt[RADIX];
   __shared__ uint32_t s_rstart[RADIX];
+  __shared__ uint32_t s_hcnt[BLOCK + 1];   // heads before each thread's first record (+ total)
+  __shared__ uint32_t s_hmask[BLOCK];      // each thread's head bitmask
   __shared__ uint32_t s_goff[RADIX];
   __shared__ uint32_t s_wtot[NW];
   __shared__ S s_wagg[NW];
@@ -72,7 +74,6 @@ __global__ __launch_bounds__(BLOCK) void k_onesweep_combine(Src src, K* __restri
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   for (int i = tid; i < NW * RADIX; i += BLOCK) (&s_whist[0][0])[i] = 0;
-  for (int i = tid; i < RADIX; i += BLOCK) s_rcnt[i] = 0;
   if (tid == 0) s_tile = atomicAdd(tile_ctr, 1u);
   __syncthreads();
   const uint32_t tile = s_tile;
@@ -189,6 +190,9 @@ __global__ __launch_bounds__(BLOCK) void k_onesweep_combine(Src src, K* __restri
   start.valid = 0;
   for (int w = 0; w < wid; ++w) start = seg_combine<Op>(start, s_wagg[w]);
   start = seg_combine<Op>(start, excl);
+  s_hcnt[tid] = start.cnt;
+  s_hmask[tid] = headmask;
+  if (tid == BLOCK - 1) s_hcnt[BLOCK] = start.cnt + __popc(headmask);
 
   // runs that END in this thread: (key, partial, tile-local run index) kept in registers
   K rk[ITEMS];
@@ -217,28 +221,30 @@ __global__ __launch_bounds__(BLOCK) void k_onesweep_combine(Src src, K* __restri
           ra[nrun] = run;
           ri[nrun] = hidx - 1;
           ++nrun;
-          atomicAdd(&s_rcnt[(uint32_t)(k >> shift) & (RADIX - 1)], 1u);
         }
       }
     }
   }
   __syncthreads();
 
-  // 4. per digit: run counts -> publish -> decoupled look-back on run counts
+  // 4. per digit: runs of digit d = heads in its record range [s_start[d], s_start[d] + cnt) — read off the
+  //    owners' head masks (no atomics: runs of one digit are adjacent, so per-run counters would all collide)
   if (tid < RADIX) {
-    const uint32_t rc = s_rcnt[tid];
+    auto heads_before = [&](uint32_t p) -> uint32_t {
+      if (p >= tile_n) return s_hcnt[BLOCK];
+      const uint32_t t = p / ITEMS, o = p % ITEMS;
+      return s_hcnt[t] + __popc(s_hmask[t] & ((1u << o) - 1u));
+    };
+    const uint32_t h0 = heads_before(s_start[tid]);
+    const uint32_t rc = cnt ? heads_before(s_start[tid] + cnt) - h0 : 0u;
+    s_rcnt[tid] = rc;
     uint64_t* st = status + (uint64_t)tile * RADIX + tid;
     if (tile == 0) st_agent(st, granule(FLAG_INC, epoch, (uint64_t)digit_base[tid] + rc));
     else st_agent(st, granule(FLAG_AGG, epoch, rc));
-    const uint32_t incr = wave_inclusive_sum(rc);
-    if (lane == 63) s_wtot[wid] = incr;
-    s_rstart[tid] = incr - rc;
+    s_rstart[tid] = h0;   // runs are in digit order: the first run of digit d has index H(start of d)
   }
   __syncthreads();
   if (tid < RADIX) {
-    uint32_t off = 0;
-    for (int w = 0; w < wid; ++w) off += s_wtot[w];
-    s_rstart[tid] += off;
     uint64_t ex;
     if (tile == 0) {
       ex = digit_base[tid];
