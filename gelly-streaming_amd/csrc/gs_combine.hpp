@@ -194,14 +194,12 @@ __global__ __launch_bounds__(BLOCK) void k_onesweep_combine(Src src, K* __restri
   s_hmask[tid] = headmask;
   if (tid == BLOCK - 1) s_hcnt[BLOCK] = start.cnt + __popc(headmask);
 
-  // runs that END in this thread: (key, partial, tile-local run index) kept in registers
-  K rk[ITEMS];
+  // runs that END at item j of this thread: partial kept in ra[j] (static index: stays in registers);
+  // key re-read from LDS and run index recomputed from the head mask at scatter time
   Acc ra[ITEMS];
-  uint32_t ri[ITEMS];
-  int nrun = 0;
+  uint32_t endmask = 0;
   {
     Acc run = start.v;
-    uint32_t hidx = start.cnt;
 #pragma unroll
     for (int j = 0; j < ITEMS; ++j) {
       if ((uint32_t)j < mine) {
@@ -209,19 +207,10 @@ __global__ __launch_bounds__(BLOCK) void k_onesweep_combine(Src src, K* __restri
         In x{};
         if constexpr (Op::HAS_V) x = s_vals[pad32(first + j)];
         const Acc a = Op::from(x);
-        if (headmask & (1u << j)) {
-          run = a;
-          hidx++;
-        } else {
-          run = Op::combine(run, a);
-        }
+        run = (headmask & (1u << j)) ? a : Op::combine(run, a);
         const uint32_t nx = first + j + 1;
-        if (nx >= tile_n || s_keys[pad32(nx)] != k) {
-          rk[nrun] = k;
-          ra[nrun] = run;
-          ri[nrun] = hidx - 1;
-          ++nrun;
-        }
+        if (nx >= tile_n || s_keys[pad32(nx)] != k) endmask |= 1u << j;
+        ra[j] = run;
       }
     }
   }
@@ -264,10 +253,12 @@ __global__ __launch_bounds__(BLOCK) void k_onesweep_combine(Src src, K* __restri
   // 5. scatter the partials
 #pragma unroll
   for (int j = 0; j < ITEMS; ++j) {
-    if (j < nrun) {
-      const uint32_t d = (uint32_t)(rk[j] >> shift) & (RADIX - 1);
-      const uint32_t g = s_goff[d] + ri[j] - s_rstart[d];
-      kout[g] = rk[j];
+    if (endmask & (1u << j)) {
+      const K k = s_keys[pad32(first + j)];
+      const uint32_t ri = start.cnt + __popc(headmask & ((2u << j) - 1u)) - 1u;
+      const uint32_t d = (uint32_t)(k >> shift) & (RADIX - 1);
+      const uint32_t g = s_goff[d] + ri - s_rstart[d];
+      kout[g] = k;
       aout[g] = ra[j];
     }
   }

@@ -33,7 +33,7 @@ namespace gs {
 #define GS_COMB_BLOCK 256
 #endif
 #ifndef GS_COMB_ITEMS
-#define GS_COMB_ITEMS 16
+#define GS_COMB_ITEMS 12
 #endif
 constexpr int COMB_BLOCK = GS_COMB_BLOCK, COMB_ITEMS = GS_COMB_ITEMS, COMB_TILE = COMB_BLOCK * COMB_ITEMS;
 constexpr int SORT_BLOCK = GS_SORT_BLOCK, SORT_ITEMS = GS_SORT_ITEMS, SORT_TILE = SORT_BLOCK * SORT_ITEMS;
