@@ -61,6 +61,12 @@ uint32_t next_epoch(gs_ctx* c, size_t) {
   return c->epoch;
 }
 
+gs_status begin_call(gs_ctx* c) {
+  GS_HIP(hipSetDevice(c->device));
+  GS_HIP(hipMemsetAsync(c->small.as<char>() + SM_TIMEOUT, 0, 8, c->stream));
+  return GS_OK;
+}
+
 gs_status stage_batch(gs_ctx* c, const gs_edge_batch* b, const int64_t** src, const int64_t** dst, const void** val,
                       bool need_val) {
   const size_t vb = dtype_bytes(b->val_dtype);
@@ -174,7 +180,8 @@ static gs_status sort_dir(gs_ctx* c, const int64_t* src, const int64_t* dst, con
                           uint64_t n, int payload, Sorted* out, bool leave_last) {
   char* sm = c->small.as<char>();
   const uint64_t R = (DIR == DIR_ALL) ? 2 * n : n;
-  GS_HIP(hipMemsetAsync(sm, 0, SM_BASE, c->stream));  // mask, k0, counters, timeout, hist
+  GS_HIP(hipMemsetAsync(sm, 0, SM_TIMEOUT, c->stream));                            // mask, k0, n_unique
+  GS_HIP(hipMemsetAsync(sm + SM_COUNTERS, 0, SM_BASE - SM_COUNTERS, c->stream));   // counters, hist
   GS_TRY(launch_keyinfo<DIR>(c, src, dst, n));
   const int64_t* k0p = (DIR == DIR_IN) ? dst : src;
   GS_HIP(hipMemcpyAsync(sm + SM_K0, k0p, 8, hipMemcpyDeviceToDevice, c->stream));
@@ -235,7 +242,8 @@ static gs_status buffer_passes(gs_ctx* c, const uint64_t* keys, const V* vals, u
 
 gs_status sort_buffer(gs_ctx* c, const uint64_t* keys, const uint32_t* vals, uint64_t n, Sorted* out) {
   char* sm = c->small.as<char>();
-  GS_HIP(hipMemsetAsync(sm, 0, SM_BASE, c->stream));
+  GS_HIP(hipMemsetAsync(sm, 0, SM_TIMEOUT, c->stream));
+  GS_HIP(hipMemsetAsync(sm + SM_COUNTERS, 0, SM_BASE - SM_COUNTERS, c->stream));
   hipLaunchKernelGGL(k_keyinfo_buf, dim3(grid_for(n, 512, 2048)), dim3(256), 0, c->stream, keys, n,
                      (unsigned long long*)(sm + SM_MASK), (uint32_t*)(sm + SM_HIST));
   GS_HIP(hipGetLastError());
@@ -357,6 +365,8 @@ void gs_destroy(gs_ctx* c) {
   if (!c) return;
   hipSetDevice(c->device);
   if (c->stream) hipStreamSynchronize(c->stream);
+  for (DevBuf& b : c->hs)
+    if (b.p) hipFree(b.p);
   for (DevBuf* b : {&c->part_k, &c->part_a, &c->comp_k, &c->comp_a,
                     &c->in_src, &c->in_dst, &c->in_val, &c->keysA, &c->keysB, &c->valsA, &c->valsB, &c->sort_status,
                     &c->rbk_word, &c->rbk_agg, &c->rbk_inc, &c->small, &c->out_keys, &c->out_a, &c->out_b, &c->aux,
@@ -412,7 +422,7 @@ static gs_status window_fold_impl(gs_ctx* c, const gs_edge_batch* b, int32_t dir
   if (op != GS_OP_COUNT && (b->val_dtype == GS_NONE || (b->n && !b->val)))
     return set_error(c, GS_EINVAL, "op %d needs edge values", op);
   if (has_init && !init) return set_error(c, GS_EINVAL, "null init");
-  GS_HIP(hipSetDevice(c->device));
+  GS_TRY(begin_call(c));
   const uint64_t R = dir == GS_DIR_ALL ? 2 * b->n : b->n;
   if (R == 0) {
     *out->n_out = 0;
@@ -472,7 +482,7 @@ gs_status gs_window_fold_degree_max(gs_ctx* c, const gs_edge_batch* b, int32_t d
   GS_TRY(check_batch(c, b, dir));
   if (!out || !out->n_out || (out->capacity && (!out->keys || !out->degree || !out->max_neighbor)))
     return set_error(c, GS_EINVAL, "bad gs_degree_out");
-  GS_HIP(hipSetDevice(c->device));
+  GS_TRY(begin_call(c));
   const uint64_t R = dir == GS_DIR_ALL ? 2 * b->n : b->n;
   if (R == 0) {
     *out->n_out = 0;

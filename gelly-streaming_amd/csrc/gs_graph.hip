@@ -209,7 +209,7 @@ extern "C" {
 gs_status gs_window_csr(gs_ctx* c, const gs_edge_batch* b, int32_t dir, gs_csr_out* out) {
   GS_TRY(check_batch(c, b, dir));
   if (!out || !out->n_vertices || !out->n_records) return set_error(c, GS_EINVAL, "bad gs_csr_out");
-  GS_HIP(hipSetDevice(c->device));
+  GS_TRY(begin_call(c));
   const uint64_t R = dir == GS_DIR_ALL ? 2 * b->n : b->n;
   *out->n_records = R;
   if (R == 0) {
@@ -277,18 +277,11 @@ gs_status gs_window_csr(gs_ctx* c, const gs_edge_batch* b, int32_t dir, gs_csr_o
   return GS_OK;
 }
 
-gs_status gs_window_candidates(gs_ctx* c, const gs_edge_batch* b, gs_pair_out* out) {
-  if (!c) return GS_EINVAL;
-  (void)b;
-  (void)out;
-  return set_error(c, GS_EUNSUPPORTED, "gs_window_candidates: not built yet");
-}
-
 gs_status gs_window_triangles(gs_ctx* c, const gs_edge_batch* b, uint64_t* count, int32_t* count_ref_wrapped,
                               int32_t* has_output) {
   GS_TRY(check_batch(c, b, GS_DIR_ALL));
   if (!count || !count_ref_wrapped || !has_output) return set_error(c, GS_EINVAL, "null output pointer");
-  GS_HIP(hipSetDevice(c->device));
+  GS_TRY(begin_call(c));
   *count = 0;
   *count_ref_wrapped = 0;
   *has_output = b->n > 0;   // every edge record forms a (v, t) group with edges > 0 (WindowTriangles.java:136)
@@ -300,7 +293,8 @@ gs_status gs_window_triangles(gs_ctx* c, const gs_edge_batch* b, uint64_t* count
   char* sm = c->small.as<char>();
   const uint64_t n = b->n;
   // key range of the window (same scan as the sort)
-  GS_HIP(hipMemsetAsync(sm, 0, SM_BASE, c->stream));
+  GS_HIP(hipMemsetAsync(sm, 0, SM_TIMEOUT, c->stream));
+  GS_HIP(hipMemsetAsync(sm + SM_COUNTERS, 0, SM_BASE - SM_COUNTERS, c->stream));
   GS_TRY(launch_keyinfo_all(c, src, dst, n));
   GS_HIP(hipMemcpyAsync(sm + SM_K0, src, 8, hipMemcpyDeviceToDevice, c->stream));
   GS_HIP(hipMemcpyAsync(c->host_small, sm, 16, hipMemcpyDeviceToHost, c->stream));
@@ -327,14 +321,18 @@ gs_status gs_window_triangles(gs_ctx* c, const gs_edge_batch* b, uint64_t* count
   Sorted s;
   GS_TRY(sort_buffer(c, c->aux.as<uint64_t>(), nullptr, R, &s));
   const uint64_t loops = c->host_small[4];
-  if (loops)
-    return set_error(c, GS_EUNSUPPORTED,
-                     "window triangles: %llu self-loop edge(s) — the HashSet-order self-pair term is not built yet",
-                     (unsigned long long)loops);
   GS_TRY(ensure(c, c->out_keys, R * 8));
   uint64_t E2 = 0;
   UniqueOut uo{c->out_keys.as<uint64_t>(), nullptr};
   GS_TRY((s.wide ? launch_rbk<uint64_t, CountOp>(c, s, uo, &E2) : launch_rbk<uint32_t, CountOp>(c, s, uo, &E2)));
+  if (loops) E2 -= 1;   // the self-loop sentinel sorts last
+  if (E2 == 0) {        // only self-loops: no triangle; the self-pair term needs >= 2 neighbours
+    uint64_t S = 0;
+    GS_TRY(triangle_selfpair_term(c, src, dst, n, c->tri_loops.as<uint32_t>(), key_xor, &S));
+    *count = S;
+    *count_ref_wrapped = (int32_t)(uint32_t)S;
+    return GS_OK;
+  }
   // 3. rows: degree + row start per vertex (segment by u = key >> B)
   const size_t V = 1ull << B;
   GS_TRY(ensure(c, c->out_a, V * 4));
@@ -374,7 +372,12 @@ gs_status gs_window_triangles(gs_ctx* c, const gs_edge_batch* b, uint64_t* count
   GS_HIP(hipMemcpyAsync(c->host_small, sm, 32, hipMemcpyDeviceToHost, c->stream));
   GS_HIP(hipStreamSynchronize(c->stream));
   if ((uint32_t)c->host_small[3] != 0) return set_error(c, GS_EDEVICE, "look-back spin timed out");
-  const uint64_t T = c->host_small[2];
+  uint64_t T = c->host_small[2];
+  if (loops) {   // self-pair candidates (x, x, true) matched by a self-loop on x (WindowTriangles.java:105)
+    uint64_t S = 0;
+    GS_TRY(triangle_selfpair_term(c, src, dst, n, c->tri_loops.as<uint32_t>(), key_xor, &S));
+    T += S;
+  }
   *count = T;
   *count_ref_wrapped = (int32_t)(uint32_t)T;   // Integer sum(0) wraps (WindowTriangles.java:66, :126)
   return GS_OK;

@@ -52,6 +52,8 @@ struct gs_ctx {
   gs::DevBuf part_k, part_a, comp_k, comp_a;
   // triangles
   gs::DevBuf tri_loops, tri_keep, tri_tiles, tri_pos, tri_ou, tri_onbr;
+  // HashSet-order pipeline (gs_hashset.hip)
+  gs::DevBuf hs[20];
   hipEvent_t ev[6] = {};
   hipEvent_t pass_ev[9] = {};
   gs_stage_times times{};
@@ -86,6 +88,15 @@ gs_status sort_window(gs_ctx* c, const int64_t* src, const int64_t* dst, const v
 // Sort an unsigned 64-bit key buffer (stable), optional u32 payload; keys of <= 32 varying bits are
 // compacted to u32 (key = key_xor ^ compact).  `keys` must be 16-byte aligned.
 gs_status sort_buffer(gs_ctx* c, const uint64_t* keys, const uint32_t* vals, uint64_t n, Sorted* out);
+
+// HashSet-ordered distinct neighbour sets of an ALL window (gs_hashset.hip)
+gs_status hashset_order(gs_ctx* c, const int64_t* src, const int64_t* dst, uint64_t n, uint32_t* U_out,
+                        uint32_t* M_out, uint64_t* key_xor_out, bool* treeified);
+// WindowTriangles self-pair term for windows with self-loops (loops: bitmap over compact IDs)
+gs_status triangle_selfpair_term(gs_ctx* c, const int64_t* src, const int64_t* dst, uint64_t n,
+                                 const uint32_t* loops, uint64_t loops_xor, uint64_t* S);
+// clear the look-back timeout word at the start of a public call
+gs_status begin_call(gs_ctx* c);
 
 // k_keyinfo over both columns (ALL): mask at SM_MASK, byte histograms at SM_HIST
 gs_status launch_keyinfo_all(gs_ctx* c, const int64_t* src, const int64_t* dst, uint64_t n);

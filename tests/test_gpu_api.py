@@ -128,3 +128,63 @@ def test_triangles_matches_reference_rule(engine, oracle):
 def test_triangles_empty_window(engine):
     ex, wrapped, has = engine.triangles(np.empty(0, np.int64), np.empty(0, np.int64))
     assert (ex, wrapped, has) == (0, 0, False)
+
+
+def _cand_case(oracle, rng, kind):
+    if kind == "small_ids":
+        V, n = int(rng.integers(3, 60)), int(rng.integers(1, 500))
+        s, d = rng.integers(0, V, n), rng.integers(0, V, n)
+    elif kind == "sparse_ids":      # IDs >> table size: non-trivial HashSet order, multi-entry bins
+        V, n = int(rng.integers(5, 200)), int(rng.integers(50, 2000))
+        s, d = rng.integers(0, V, n) * 1_000_003 + 17, rng.integers(0, V, n) * 1_000_003 + 17
+    elif kind == "negative_ids":    # Long.hashCode of negative IDs, signed order of the > v filter
+        V, n = int(rng.integers(5, 100)), int(rng.integers(50, 1500))
+        s, d = rng.integers(-V, V, n) * 65537, rng.integers(-V, V, n) * 65537
+    else:                           # R-MAT with hubs
+        s, d = oracle.gen_rmat(10, 3000, int(rng.integers(1, 1 << 30)))
+    return np.asarray(s, np.int64), np.asarray(d, np.int64)
+
+
+@pytest.mark.parametrize("kind", ["small_ids", "sparse_ids", "negative_ids", "rmat"])
+def test_candidates_match_reference_rule(engine, oracle, kind):
+    """gs_window_candidates == GenerateCandidateEdges record-for-record (same per-vertex sequence,
+    including the JDK HashSet iteration order of the candidate pairs and the self pairs)."""
+    rng = np.random.default_rng({"small_ids": 1, "sparse_ids": 2, "negative_ids": 3, "rmat": 4}[kind])
+    for trial in range(6):
+        s, d = _cand_case(oracle, rng, kind)
+        ra, rb, rf, tree = oracle.window_candidates(s, d)
+        if tree:
+            continue
+        ga, gb, gf = engine.candidates(*[torch.from_numpy(x).cuda() for x in (s, d)])
+        assert np.array_equal(ga.cpu().numpy(), ra), (kind, trial)
+        assert np.array_equal(gb.cpu().numpy(), rb), (kind, trial)
+        assert np.array_equal(gf.cpu().numpy(), rf), (kind, trial)
+
+
+def test_candidates_through_api_and_host_buffers(pkg, engine, oracle):
+    s, d = _cand_case(oracle, np.random.default_rng(9), "sparse_ids")
+    ra, rb, rf, _ = oracle.window_candidates(s, d)
+    ga, gb, gf = engine.candidates(s, d)          # host columns
+    assert np.array_equal(ga, ra) and np.array_equal(gb, rb) and np.array_equal(gf, rf)
+    env = pkg.StreamExecutionEnvironment.getExecutionEnvironment()
+    g = pkg.SimpleEdgeStream(pkg.EdgeColumns(s, d), env)
+    recs = g.slice(pkg.Time.seconds(1), pkg.EdgeDirection.ALL).applyOnNeighbors(pkg.GenerateCandidateEdges()).collect()
+    assert recs == [(int(a), int(b), int(f)) for a, b, f in zip(ra, rb, rf)]
+
+
+def test_triangles_with_self_loops(engine, oracle):
+    """Windows with self-loops: the reference's self-pair quirk (j = i) counts (x, x) candidates when
+    x has a self-loop, except for the last HashSet element — reproduced exactly."""
+    rng = np.random.default_rng(12)
+    for trial in range(25):
+        V = int(rng.integers(2, 50))
+        n = int(rng.integers(1, 500))
+        s = rng.integers(0, V, n).astype(np.int64)
+        d = np.where(rng.random(n) < 0.15, s, rng.integers(0, V, n)).astype(np.int64)
+        if trial % 2:
+            s, d = s * 7919 + 3, d * 7919 + 3
+        w_ref, ex_ref, has_ref, tree = oracle.window_triangles_ref(s, d)
+        if tree:
+            continue
+        ex, wrapped, has = engine.triangles(s, d)
+        assert (ex, wrapped, has) == (ex_ref, w_ref, has_ref), trial
