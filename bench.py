@@ -44,6 +44,9 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-sample-log2", type=int, default=25)
     p.add_argument("--check", action="store_true", help="verify sum(per-vertex sums) == sum(values) after timing")
+    p.add_argument("--workload", default="reduce", choices=["reduce", "fold", "triangles"],
+                   help="reduce = C2 (default, the headline); fold = C3 degree/max on skewed R-MAT; "
+                        "triangles = WindowTriangles on an R-MAT window without self-loops (C4 shape)")
     return p.parse_args()
 
 
@@ -119,7 +122,7 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
+    if "WORLD_SIZE" in os.environ:   # launched by torchrun: RCCL path (also at world size 1)
         os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
         torch.cuda.set_device(local)
         import torch.distributed as dist
@@ -133,7 +136,13 @@ def main():
 
     eng = pkg.Engine(local)
     E = a.edge_factor << a.scale
-    src, dst = eng.generate_rmat(a.scale, E, a.seed, first_edge=rank * E)
+    if a.workload == "fold":      # C3: skewed R-MAT (.65/.15/.15/.05), no permutation -> hubs at low IDs
+        src, dst = eng.generate_rmat(a.scale, E, 0x5EED03, a=0.65, b=0.15, c=0.15, permute=False,
+                                     first_edge=rank * E)
+    elif a.workload == "triangles":   # C4 shape: R-MAT, self-loops removed
+        src, dst = eng.generate_rmat(a.scale, E, 0x5EED04, no_self_loops=True, first_edge=rank * E)
+    else:                         # C2
+        src, dst = eng.generate_rmat(a.scale, E, a.seed, first_edge=rank * E)
     vdt = 1 if a.dtype == "int64" else 3
     val = eng.generate_values(E, a.seed, vdt, first_edge=rank * E)
     torch.cuda.synchronize()
@@ -146,12 +155,31 @@ def main():
             local_times.append(eng.stage_times())   # the window's own pipeline, not the merge
         return r
 
+    def local_fold(s_, d_, direction, init_max):
+        r = eng.fold_degree_max(s_, d_, direction, init_max)
+        if not local_times:
+            local_times.append(eng.stage_times())
+        return r
+
+    def part_count(s_, d_, part, nparts):
+        r = eng.triangles_part(s_, d_, part, nparts)
+        local_times.append(eng.stage_times())
+        return r
+
     def step():
         local_times.clear()
-        if world == 1:
-            r = local_reduce(src, dst, val, 1, 0)
-        else:
-            r = D.reduce_window(local_reduce, src, dst, val, 1, 0)
+        if a.workload == "triangles":
+            if dist:
+                tot, _ = D.triangles_window(part_count, src, dst)
+            else:
+                tot = part_count(src, dst, 0, 1)
+            z = torch.zeros(1, dtype=torch.int64, device=src.device)
+            return z + tot, z, local_times[0]
+        if a.workload == "fold":
+            r = D.fold_degree_max_window(local_fold, local_reduce, src, dst, 1, -(1 << 63)) if dist \
+                else local_fold(src, dst, 1, -(1 << 63))
+            return r[0], r[1], local_times[0]
+        r = D.reduce_window(local_reduce, src, dst, val, 1, 0) if dist else local_reduce(src, dst, val, 1, 0)
         return r[0], r[1], local_times[0]
 
     for _ in range(a.warmup):
@@ -176,14 +204,18 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    if a.check and world == 1:
+    if a.check and world == 1 and a.workload == "reduce":
         k, v, _ = step()
         assert int(v.sum()) == int(val.sum()) and bool((k[1:] > k[:-1]).all()), "bench window failed its check"
 
     # local window only: the dominant kernel of the single-GPU pipeline
     E_rec = times[0].records
     U_avg = times[0].vertices
-    kt, partials = kernel_table(times, E_rec, U_avg)
+    kt, partials = kernel_table(times, E_rec, U_avg) if a.workload != "triangles" else ({}, 0)
+    if not kt:   # triangles: the stage table does not apply; report the whole window
+        kt = {"window_triangles": {"ms": elapsed / a.steps * 1e3, "bytes": E * 16, "GB/s": 0.0, "frac": 0.0}}
+        kt["window_triangles"]["GB/s"] = kt["window_triangles"]["bytes"] / (kt["window_triangles"]["ms"] * 1e-3) / 1e9
+        kt["window_triangles"]["frac"] = kt["window_triangles"]["GB/s"] / HBM_PEAK_GBS
     dom_name = max((n for n in kt if not n.startswith("keyinfo")), key=lambda n: kt[n]["ms"])
     dom = kt[dom_name]
     roofline = {"bound": "hbm", "kernel": dom_name, "achieved": round(dom["GB/s"], 1), "peak": HBM_PEAK_GBS,
@@ -191,7 +223,7 @@ def main():
                 "algorithmic_bytes_per_launch": dom["bytes"], "avg_launch_ms": round(dom["ms"], 4)}
 
     cpu = None
-    if world == 1 and rank == 0 and not a.no_cpu_baseline:
+    if world == 1 and rank == 0 and not a.no_cpu_baseline and a.workload == "reduce":
         cpu = cpu_baseline(src, dst, val, a.cpu_sample_log2)
 
     if rank == 0:
@@ -209,11 +241,14 @@ def main():
             "vs_baseline": None,
             "dtype": a.dtype,
             "data": "synthetic R-MAT (Graph500 .57/.19/.19/.05, permuted), generated on device (gs_generate_rmat)",
-            "config": {"workload": "C2: slice(OUT).reduceOnEdges(SUM) over one R-MAT scale-24 window",
+            "config": {"workload": {"reduce": f"C2: slice(OUT).reduceOnEdges(SUM) over one R-MAT scale-{a.scale} window",
+                                    "fold": f"C3: slice(OUT).foldNeighbors(degree, max neighbour), skewed R-MAT scale-{a.scale}",
+                                    "triangles": f"C4 shape: WindowTriangles over an R-MAT scale-{a.scale} window"}[a.workload],
                        "scale": a.scale, "edges_per_window_per_gpu": E, "direction": "OUT", "op": "SUM",
                        "value_dtype": a.dtype, "vertices_out": U_avg, "sort_passes": times[0].sort_passes,
                        "key_bits": times[0].key_bits, "partials_after_fused_pass": int(partials),
-                       "parallelism": f"vertex-range keyBy over {world} GPU(s)" if world > 1 else "1 GPU"},
+                       "parallelism": (f"vertex-range keyBy over {world} GPU(s), RCCL all-to-all" if dist
+                                       else "1 GPU")},
             "roofline": roofline,
             "cpu_baseline": cpu,
             "kernels": {n: {"avg_ms": round(r["ms"], 4), "GB/s": round(r["GB/s"], 1), "frac": round(r["frac"], 4)}

@@ -169,12 +169,12 @@ __global__ __launch_bounds__(SCAN_BLOCK) void k_orient_scatter(const uint64_t* _
 
 // sum over oriented edges u -> v of |N+(u) ∩ N+(v)| (sorted lists: merge)
 __global__ __launch_bounds__(256) void k_tri_count(const uint32_t* __restrict__ ou, const uint32_t* __restrict__ onbr,
-                                                   uint32_t M, const uint32_t* __restrict__ deg,
+                                                   uint32_t q0, uint32_t M, const uint32_t* __restrict__ deg,
                                                    const uint32_t* __restrict__ rowstart,
                                                    const uint32_t* __restrict__ pos,
                                                    unsigned long long* __restrict__ total) {
   uint64_t t = 0;
-  for (uint32_t q = blockIdx.x * 256u + threadIdx.x; q < M; q += gridDim.x * 256u) {
+  for (uint32_t q = q0 + blockIdx.x * 256u + threadIdx.x; q < M; q += gridDim.x * 256u) {
     const uint32_t u = ou[q], v = onbr[q];
     uint32_t a = pos[rowstart[u]], a1 = pos[rowstart[u] + deg[u]];
     uint32_t b = pos[rowstart[v]], b1 = pos[rowstart[v] + deg[v]];
@@ -277,14 +277,12 @@ gs_status gs_window_csr(gs_ctx* c, const gs_edge_batch* b, int32_t dir, gs_csr_o
   return GS_OK;
 }
 
-gs_status gs_window_triangles(gs_ctx* c, const gs_edge_batch* b, uint64_t* count, int32_t* count_ref_wrapped,
-                              int32_t* has_output) {
+static gs_status triangles_impl(gs_ctx* c, const gs_edge_batch* b, uint32_t part, uint32_t nparts, uint64_t* count) {
   GS_TRY(check_batch(c, b, GS_DIR_ALL));
-  if (!count || !count_ref_wrapped || !has_output) return set_error(c, GS_EINVAL, "null output pointer");
+  if (!count) return set_error(c, GS_EINVAL, "null output pointer");
+  if (nparts == 0 || part >= nparts) return set_error(c, GS_EINVAL, "bad part %u of %u", part, nparts);
   GS_TRY(begin_call(c));
   *count = 0;
-  *count_ref_wrapped = 0;
-  *has_output = b->n > 0;   // every edge record forms a (v, t) group with edges > 0 (WindowTriangles.java:136)
   if (b->n == 0) return GS_OK;
   hipEventRecord(c->ev[0], c->stream);
   const int64_t *src, *dst;
@@ -328,9 +326,8 @@ gs_status gs_window_triangles(gs_ctx* c, const gs_edge_batch* b, uint64_t* count
   if (loops) E2 -= 1;   // the self-loop sentinel sorts last
   if (E2 == 0) {        // only self-loops: no triangle; the self-pair term needs >= 2 neighbours
     uint64_t S = 0;
-    GS_TRY(triangle_selfpair_term(c, src, dst, n, c->tri_loops.as<uint32_t>(), key_xor, &S));
+    if (part == 0) GS_TRY(triangle_selfpair_term(c, src, dst, n, c->tri_loops.as<uint32_t>(), key_xor, &S));
     *count = S;
-    *count_ref_wrapped = (int32_t)(uint32_t)S;
     return GS_OK;
   }
   // 3. rows: degree + row start per vertex (segment by u = key >> B)
@@ -363,9 +360,11 @@ gs_status gs_window_triangles(gs_ctx* c, const gs_edge_batch* b, uint64_t* count
   // 5. merge intersections
   unsigned long long* d_total = (unsigned long long*)(sm + SM_NUNIQUE);
   GS_HIP(hipMemsetAsync(d_total, 0, 8, c->stream));
-  const unsigned g2 = (unsigned)std::min<uint64_t>((M + 255) / 256, 16384);
+  const uint64_t q0 = M * part / nparts, q1 = M * (part + 1) / nparts;   // this part's oriented edges
+  const unsigned g2 = (unsigned)std::min<uint64_t>((q1 - q0 + 255) / 256, 16384);
   hipLaunchKernelGGL(k_tri_count, dim3(std::max(1u, g2)), dim3(256), 0, c->stream, c->tri_ou.as<uint32_t>(),
-                     c->tri_onbr.as<uint32_t>(), (uint32_t)M, c->out_a.as<uint32_t>(), c->out_b.as<uint32_t>(),
+                     c->tri_onbr.as<uint32_t>(), (uint32_t)q0, (uint32_t)q1, c->out_a.as<uint32_t>(),
+                     c->out_b.as<uint32_t>(),
                      c->tri_pos.as<uint32_t>(), d_total);
   GS_HIP(hipGetLastError());
   hipEventRecord(c->ev[3], c->stream);
@@ -373,14 +372,32 @@ gs_status gs_window_triangles(gs_ctx* c, const gs_edge_batch* b, uint64_t* count
   GS_HIP(hipStreamSynchronize(c->stream));
   if ((uint32_t)c->host_small[3] != 0) return set_error(c, GS_EDEVICE, "look-back spin timed out");
   uint64_t T = c->host_small[2];
-  if (loops) {   // self-pair candidates (x, x, true) matched by a self-loop on x (WindowTriangles.java:105)
+  if (loops && part == 0) {   // self-pair candidates (x, x, true) matched by a self-loop on x (:105)
     uint64_t S = 0;
     GS_TRY(triangle_selfpair_term(c, src, dst, n, c->tri_loops.as<uint32_t>(), key_xor, &S));
     T += S;
   }
   *count = T;
-  *count_ref_wrapped = (int32_t)(uint32_t)T;   // Integer sum(0) wraps (WindowTriangles.java:66, :126)
   return GS_OK;
 }
+
+gs_status gs_window_triangles(gs_ctx* c, const gs_edge_batch* b, uint64_t* count, int32_t* count_ref_wrapped,
+                              int32_t* has_output) {
+  if (!c) return GS_EINVAL;
+  if (!count || !count_ref_wrapped || !has_output) return set_error(c, GS_EINVAL, "null output pointer");
+  uint64_t T = 0;
+  GS_TRY(triangles_impl(c, b, 0, 1, &T));
+  *count = T;
+  *count_ref_wrapped = (int32_t)(uint32_t)T;   // Integer sum(0) wraps (WindowTriangles.java:66, :126)
+  *has_output = b && b->n > 0;   // every edge record forms a (v, t) group with edges > 0 (WindowTriangles.java:136)
+  return GS_OK;
+}
+
+gs_status gs_window_triangles_part(gs_ctx* c, const gs_edge_batch* b, uint32_t part, uint32_t nparts,
+                                   uint64_t* partial_count) {
+  if (!c) return GS_EINVAL;
+  return triangles_impl(c, b, part, nparts, partial_count);
+}
+
 
 }  // extern "C"

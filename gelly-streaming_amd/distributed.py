@@ -84,3 +84,34 @@ def fold_degree_max_window(local_fold, local_reduce, src, dst, direction: int, i
     k1, d1 = local_reduce(rk, rk, rd, 1, SUM)
     _, m1 = local_reduce(rk, rk, rm, 1, MAX)
     return k1, d1, m1
+
+
+def gather_window(src: torch.Tensor, dst: torch.Tensor, group=None):
+    """All-gather every rank's slice of the window, in rank order (= stream order when rank r holds the
+    r-th slice).  Variable slice sizes: gather the sizes, pad to the largest, trim after."""
+    world = dist.get_world_size(group)
+    n = torch.tensor([src.numel()], dtype=torch.int64, device=src.device)
+    sizes = [torch.zeros_like(n) for _ in range(world)]
+    dist.all_gather(sizes, n, group=group)
+    sizes = [int(x) for x in sizes]
+    mx = max(sizes)
+    pad = lambda t: torch.cat([t, t.new_zeros(mx - t.numel())]) if t.numel() < mx else t
+    outs = []
+    for col in (src, dst):
+        buf = [col.new_empty(mx) for _ in range(world)]
+        dist.all_gather(buf, pad(col.contiguous()), group=group)
+        outs.append(torch.cat([b[:k] for b, k in zip(buf, sizes)]))
+    return outs[0], outs[1]
+
+
+def triangles_window(local_part_count, src, dst, group=None):
+    """WindowTriangles over a window spread across ranks: all-gather the adjacency,
+    count this rank's share of the oriented edges, all-reduce(SUM).  Returns (exact, Integer-wrapped)."""
+    world, rank = dist.get_world_size(group), dist.get_rank(group)
+    fs, fd = gather_window(src, dst, group)
+    part = local_part_count(fs, fd, rank, world)
+    t = torch.tensor([part], dtype=torch.int64, device=src.device)
+    dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
+    total = int(t.item()) & ((1 << 64) - 1)
+    wrapped = total & 0xFFFFFFFF
+    return total, wrapped - (1 << 32) if wrapped >= (1 << 31) else wrapped

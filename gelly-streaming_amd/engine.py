@@ -225,6 +225,13 @@ class Engine:
                                                 ctypes.byref(has)))
         return cnt.value, wrapped.value, bool(has.value)
 
+    def triangles_part(self, src, dst, part: int, nparts: int) -> int:
+        """gs_window_triangles_part: this part's share of the window's triangle count (multi-GPU)."""
+        b, keep, dev = self._batch(src, dst, None)
+        cnt = ctypes.c_uint64(0)
+        self._check(self._L.gs_window_triangles_part(self.ctx, ctypes.byref(b), part, nparts, ctypes.byref(cnt)))
+        return cnt.value
+
     # -- synthetic streams (device) ----------------------------------------------------------------
     def generate_rmat(self, scale, n, seed, a=0.57, b=0.19, c=0.19, permute=True, no_self_loops=False,
                       first_edge=0, out=None):

@@ -193,6 +193,12 @@ GS_API gs_status gs_window_candidates(gs_ctx* ctx, const gs_edge_batch* batch, g
 GS_API gs_status gs_window_triangles(gs_ctx* ctx, const gs_edge_batch* batch, uint64_t* count,
                               int32_t* count_ref_wrapped, int32_t* has_output);
 
+/* Multi-GPU WindowTriangles: every rank holds the whole window (all-gathered adjacency) and counts
+ * only part `part` of `nparts` of the oriented edges (plus the self-pair term on part 0); the sum of
+ * the parts over ranks (an all-reduce) equals gs_window_triangles' count. */
+GS_API gs_status gs_window_triangles_part(gs_ctx* ctx, const gs_edge_batch* batch, uint32_t part,
+                                          uint32_t nparts, uint64_t* partial_count);
+
 /* ---- synthetic streams (bit-identical to oracle/gs_oracle.c) ------------------------ */
 /* R-MAT: 2^scale vertices, probabilities a, b, c (d = 1-a-b-c) as 32-bit fixed point,
  * optional seeded vertex permutation, optional self-loop removal (rewired, count kept). */

@@ -51,6 +51,12 @@ def _worker(rank, world, port, q):
             res[(direction, op)] = (k.numpy(), r.numpy())
         k, dg, mx = D.fold_degree_max_window(local_fold, local_reduce, s, d, direction, -(1 << 63))
         res[(direction, "deg")] = (k.numpy(), dg.numpy(), mx.numpy())
+    # WindowTriangles across ranks: all-gathered adjacency must be the whole window in stream order;
+    # each rank contributes its part (here: rank 0 counts everything) and the all-reduce sums them
+    fs, fd = D.gather_window(torch.from_numpy(s), torch.from_numpy(d))
+    res["gathered"] = (fs.numpy(), fd.numpy())
+    part = lambda a, b, r, w: (orc.window_triangles_fwd(a.numpy(), b.numpy())[1] if r == 0 else 0)
+    res["tri"] = D.triangles_window(part, torch.from_numpy(s), torch.from_numpy(d))
     q.put((rank, res))
     dist.barrier()
     dist.destroy_process_group()
@@ -81,3 +87,7 @@ def test_reduce_window_two_ranks(oracle):
         mx = np.concatenate([out[r][(direction, "deg")][2] for r in range(world)])
         wk, wd, wm = oracle.window_fold_degree_max(s, d, direction)
         assert np.array_equal(k, wk) and np.array_equal(dg, wd) and np.array_equal(mx, wm)
+    for r in range(world):
+        assert np.array_equal(out[r]["gathered"][0], s) and np.array_equal(out[r]["gathered"][1], d)
+        w, ex, _ = oracle.window_triangles_fwd(s, d)
+        assert out[r]["tri"] == (ex, w)

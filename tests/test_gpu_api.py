@@ -188,3 +188,12 @@ def test_triangles_with_self_loops(engine, oracle):
             continue
         ex, wrapped, has = engine.triangles(s, d)
         assert (ex, wrapped, has) == (ex_ref, w_ref, has_ref), trial
+
+
+def test_triangles_parts_sum_to_whole(engine, oracle):
+    """gs_window_triangles_part over nparts (the multi-GPU split) sums to the whole-window count."""
+    s, d = oracle.gen_rmat(13, 120_000, 0x5EED04)   # includes self-loops (not removed)
+    S, D = [torch.from_numpy(x).cuda() for x in (s, d)]
+    whole, wrapped, _ = engine.triangles(S, D)
+    for nparts in (1, 2, 3, 8):
+        assert sum(engine.triangles_part(S, D, p, nparts) for p in range(nparts)) == whole
