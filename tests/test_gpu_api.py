@@ -192,7 +192,7 @@ def test_triangles_with_self_loops(engine, oracle):
 
 def test_triangles_parts_sum_to_whole(engine, oracle):
     """gs_window_triangles_part over nparts (the multi-GPU split) sums to the whole-window count."""
-    s, d = oracle.gen_rmat(13, 120_000, 0x5EED04)   # includes self-loops (not removed)
+    s, d = oracle.gen_rmat(13, 120_000, 0x5EED04, no_self_loops=True)
     S, D = [torch.from_numpy(x).cuda() for x in (s, d)]
     whole, wrapped, _ = engine.triangles(S, D)
     for nparts in (1, 2, 3, 8):
