@@ -43,6 +43,8 @@ def parse():
     p.add_argument("--dtype", default="int64", choices=["int64", "float64"])
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-sample-log2", type=int, default=25)
+    p.add_argument("--sort-only", action="store_true",
+                   help="ablation: reduce / fold through the full LSD sort + reduce-by-key path")
     p.add_argument("--check", action="store_true", help="verify sum(per-vertex sums) == sum(values) after timing")
     p.add_argument("--workload", default="reduce", choices=["reduce", "fold", "triangles"],
                    help="reduce = C2 (default, the headline); fold = C3 degree/max on skewed R-MAT; "
@@ -54,6 +56,8 @@ def kernel_table(times_list, E, U_avg):
     """Average per-launch durations (device events inside the library, same stream) and the algorithmic
     bytes each kernel must move ("Kernels and their rooflines")."""
     t0 = times_list[0]
+    if t0.path == 1:
+        return bucket_kernel_table(times_list, E, U_avg)
     kb, vb = t0.key_bytes, t0.payload_bytes
     ab = 8                      # partial accumulator of a Long sum
     passes = t0.sort_passes
@@ -78,6 +82,30 @@ def kernel_table(times_list, E, U_avg):
         r["GB/s"] = r["bytes"] / (r["ms"] * 1e-3) / 1e9 if r["ms"] > 0 else 0.0
         r["frac"] = r["GB/s"] / HBM_PEAK_GBS
     return rows, P
+
+
+def bucket_kernel_table(times_list, E, U_avg):
+    """Bucket path (gs_bucket.hpp): bk_info, 1-2 partition passes over the bucket index, LDS accumulate,
+    merge of multi-item buckets, emit.  Algorithmic bytes per launch as in DESIGN.md."""
+    t0 = times_list[0]
+    vb = t0.payload_bytes
+    ab = 8 if vb else 4          # staged accumulator (i64 sum / u32 count)
+    passes = t0.sort_passes
+    mean = lambda f: statistics.mean(f(t) for t in times_list)
+    rows = {}
+    for p in range(passes):
+        rd = (8 + vb) if p == 0 else (4 + vb)
+        wr = (2 if p == passes - 1 else 4) + vb
+        rows[f"bucket_partition{p}"] = {"ms": mean(lambda t: t.pass_ms[p]), "bytes": E * (rd + wr)}
+    rd = (2 + vb) if passes else (8 + vb)
+    rows["bucket_accumulate"] = {"ms": mean(lambda t: t.pass_ms[passes]), "bytes": E * rd + U_avg * (4 + ab)}
+    rows["bucket_merge"] = {"ms": mean(lambda t: t.pass_ms[passes + 1]), "bytes": 0}
+    rows["bucket_emit"] = {"ms": mean(lambda t: t.pass_ms[passes + 2]), "bytes": U_avg * (4 + ab + 16)}
+    rows["keyinfo(+host sync)"] = {"ms": mean(lambda t: t.keyinfo_ms), "bytes": E * 8}
+    for r in rows.values():
+        r["GB/s"] = r["bytes"] / (r["ms"] * 1e-3) / 1e9 if r["ms"] > 0 else 0.0
+        r["frac"] = r["GB/s"] / HBM_PEAK_GBS
+    return rows, mean(lambda t: t.partials)
 
 
 def pmc_traffic(kernel: str):
@@ -134,7 +162,7 @@ def main():
     from importlib import import_module
     D = import_module("gelly_streaming_amd.distributed")
 
-    eng = pkg.Engine(local)
+    eng = pkg.Engine(local, sort_only=a.sort_only)
     E = a.edge_factor << a.scale
     if a.workload == "fold":      # C3: skewed R-MAT (.65/.15/.15/.05), no permutation -> hubs at low IDs
         src, dst = eng.generate_rmat(a.scale, E, 0x5EED03, a=0.65, b=0.15, c=0.15, permute=False,
@@ -247,6 +275,7 @@ def main():
                        "scale": a.scale, "edges_per_window_per_gpu": E, "direction": "OUT", "op": "SUM",
                        "value_dtype": a.dtype, "vertices_out": U_avg, "sort_passes": times[0].sort_passes,
                        "key_bits": times[0].key_bits, "partials_after_fused_pass": int(partials),
+                       "pipeline": "bucket" if times[0].path == 1 else "sort",
                        "parallelism": (f"vertex-range keyBy over {world} GPU(s), RCCL all-to-all" if dist
                                        else "1 GPU")},
             "roofline": roofline,

@@ -38,6 +38,9 @@ P = ctypes.c_void_p
 u64, i64, i32, u32 = ctypes.c_uint64, ctypes.c_int64, ctypes.c_int32, ctypes.c_uint32
 
 
+GS_FLAG_SORT_ONLY = 1   # include/gelly_hip.h: reduce / fold always take the LSD sort path
+
+
 class GsConfig(ctypes.Structure):
     _fields_ = [("device", i32), ("flags", u32), ("reserve_edges", u64)]
 
@@ -72,7 +75,7 @@ class GsStageTimes(ctypes.Structure):
     _fields_ = [("keyinfo_ms", ctypes.c_float), ("sort_ms", ctypes.c_float), ("reduce_ms", ctypes.c_float),
                 ("total_ms", ctypes.c_float), ("sort_passes", u32), ("key_bits", u32), ("records", u64),
                 ("vertices", u64), ("pass_ms", ctypes.c_float * 8), ("key_bytes", u32), ("payload_bytes", u32),
-                ("partials", u64), ("fused_last", u32), ("reserved", u32)]
+                ("partials", u64), ("fused_last", u32), ("path", u32)]
 
 
 class GsError(RuntimeError):

@@ -1,0 +1,285 @@
+// gs_bucket.hip — host side of the bucket path (gs_bucket.hpp) for reduceOnEdges / foldNeighbors
+// with the associative built-ins (GraphWindowStream.java:62-87, 101-121).
+//
+// A window fits the path when its vertex range (max - min + 1) covers at most BK_MAXB buckets of
+// 2^S vertices (S = 13..15 by accumulator size: 2^24..2^26 vertices) and the op has an LDS
+// atomic: integer SUM / MIN / MAX, float SUM, COUNT, the degree / max-neighbour fold.  Anything
+// else returns GS_EUNSUPPORTED and the caller sorts (gs_engine.hip).
+#include <algorithm>
+
+#include "gs_bucket.hpp"
+#include "gs_ops.hpp"
+
+namespace gs {
+
+#ifndef GS_BK_ITEM_LOG
+#define GS_BK_ITEM_LOG 17
+#endif
+#ifndef GS_BK_UNROLL
+#define GS_BK_UNROLL 8
+#endif
+constexpr uint32_t BK_ITEM = 1u << GS_BK_ITEM_LOG;
+
+namespace {
+
+struct BkMeta {   // offsets (u32 units) inside ctx->bk_meta
+  static constexpr size_t HIST = 0, DBASE = HIST + BK_MAXB, BSTART = DBASE + 512, BCOUNT = BSTART + BK_MAXB + 4,
+                          BITEMS = BCOUNT + BK_MAXB, BSLAB = BITEMS + BK_MAXB, MLIST = BSLAB + BK_MAXB,
+                          TOTAL = MLIST + BK_MAXB;
+};
+
+struct BkGeom {
+  int64_t base = 0;
+  uint32_t nb = 1;
+  int passes = 0, w = 0;
+};
+
+template <int DIR>
+gs_status launch_info(gs_ctx* c, const int64_t* src, const int64_t* dst, uint64_t n, int64_t base, int S) {
+  char* sm = c->small.as<char>();
+  uint32_t* hist = c->bk_meta.as<uint32_t>() + BkMeta::HIST;
+  GS_HIP(hipMemsetAsync(sm + SM_BK_MM, 0, 32, c->stream));
+  GS_HIP(hipMemsetAsync(hist, 0, BK_MAXB * 4, c->stream));
+  const bool vec = ((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst)) & 15) == 0;
+  const unsigned grid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((n + 4095) / 4096, 1024));
+  if (vec)
+    hipLaunchKernelGGL((k_bk_info<DIR, true>), dim3(grid), dim3(BK_INFO_BLOCK), 0, c->stream, src, dst, n, base, S,
+                       (uint32_t)BK_MAXB, hist, (unsigned long long*)(sm + SM_BK_MM));
+  else
+    hipLaunchKernelGGL((k_bk_info<DIR, false>), dim3(grid), dim3(BK_INFO_BLOCK), 0, c->stream, src, dst, n, base, S,
+                       (uint32_t)BK_MAXB, hist, (unsigned long long*)(sm + SM_BK_MM));
+  return hip_check(c, hipGetLastError(), "k_bk_info");
+}
+
+// one partition pass: digit (key >> shift) & (2^DB - 1); K -> KO keys, payload V
+template <int DB, typename K, typename KO, typename V, bool HAS_V, class Src>
+gs_status launch_part(gs_ctx* c, Src src, KO* kout, V* vout, uint32_t R, int pass, uint32_t shift) {
+  char* sm = c->small.as<char>();
+  const uint32_t tiles = (R + SORT_TILE - 1) / SORT_TILE;
+  const uint32_t ep = next_epoch(c, 0);
+  GS_HIP(hipMemsetAsync((uint32_t*)(sm + SM_COUNTERS) + 48 + pass, 0, 4, c->stream));
+  hipLaunchKernelGGL((k_onesweep<K, V, HAS_V, SORT_BLOCK, SORT_ITEMS, Src, DB, KO>), dim3(tiles), dim3(SORT_BLOCK), 0,
+                     c->stream, src, kout, vout, R, shift,
+                     (const uint32_t*)(c->bk_meta.as<uint32_t>() + BkMeta::DBASE) + pass * 256,
+                     c->sort_status.as<uint64_t>(), (uint32_t*)(sm + SM_COUNTERS) + 48 + pass, ep,
+                     (uint32_t*)(sm + SM_TIMEOUT));
+  return hip_check(c, hipGetLastError(), "k_onesweep(bucket)");
+}
+
+template <typename K, typename KO, typename V, bool HAS_V, class Src>
+gs_status launch_part_w(gs_ctx* c, int w, Src src, KO* kout, V* vout, uint32_t R, int pass, uint32_t shift) {
+  switch (w) {
+    case 4: return launch_part<4, K, KO, V, HAS_V>(c, src, kout, vout, R, pass, shift);
+    case 5: return launch_part<5, K, KO, V, HAS_V>(c, src, kout, vout, R, pass, shift);
+    case 6: return launch_part<6, K, KO, V, HAS_V>(c, src, kout, vout, R, pass, shift);
+    case 8: return launch_part<8, K, KO, V, HAS_V>(c, src, kout, vout, R, pass, shift);
+  }
+  return set_error(c, GS_EINVAL, "bucket path: bad digit width %d", w);
+}
+
+void choose_passes(uint32_t nb, int* passes, int* w) {
+  const int nbits = nb <= 1 ? 0 : 32 - __builtin_clz(nb - 1);
+  if (nbits == 0) { *passes = 0; *w = 0; }
+  else if (nbits <= 4) { *passes = 1; *w = 4; }
+  else if (nbits <= 5) { *passes = 1; *w = 5; }
+  else if (nbits <= 6) { *passes = 1; *w = 6; }
+  else if (nbits <= 8) { *passes = 1; *w = 8; }
+  else if (nbits <= 10) { *passes = 2; *w = 5; }
+  else { *passes = 2; *w = 6; }
+}
+
+template <class P, int DIR>
+gs_status bucket_run(gs_ctx* c, const int64_t* src, const int64_t* dst, const void* val, uint64_t n,
+                     typename P::Out o, uint64_t* U) {
+  using Raw = typename P::Raw;
+  constexpr bool HAS_V = P::HAS_V;
+  constexpr int S = P::S;
+  char* sm = c->small.as<char>();
+  const uint64_t R = (DIR == DIR_ALL) ? 2 * n : n;
+  GS_TRY(ensure(c, c->bk_meta, BkMeta::TOTAL * 4, true));
+  uint32_t* meta = c->bk_meta.as<uint32_t>();
+
+  // 1. vertex range + bucket histogram against the predicted base
+  int64_t base = c->bk_base;
+  GS_TRY(launch_info<DIR>(c, src, dst, n, base, S));
+  GS_HIP(hipMemcpyAsync(c->host_small, sm + SM_BK_MM, 24, hipMemcpyDeviceToHost, c->stream));
+  GS_HIP(hipStreamSynchronize(c->stream));
+  const int64_t kmin = (int64_t)(~c->host_small[0] ^ (1ull << 63));
+  const int64_t kmax = (int64_t)(c->host_small[1] ^ (1ull << 63));
+  const uint64_t outside = c->host_small[2];
+  if ((((uint64_t)kmax - (uint64_t)kmin) >> S) >= (uint64_t)BK_MAXB) return GS_EUNSUPPORTED;
+  if (outside) {
+    base = kmin;
+    GS_TRY(launch_info<DIR>(c, src, dst, n, base, S));
+  }
+  c->bk_base = (kmin >= 0 && ((uint64_t)kmax >> S) < (uint64_t)BK_MAXB) ? 0 : kmin;
+  BkGeom g;
+  g.base = base;
+  g.nb = (uint32_t)((((uint64_t)kmax - (uint64_t)base) >> S) + 1);
+  choose_passes(g.nb, &g.passes, &g.w);
+
+  // 2. plan
+  const uint64_t max_items = R / BK_ITEM + g.nb + 1;
+  const uint64_t max_slabs = 2 * (R / BK_ITEM) + 2;
+  GS_TRY(ensure(c, c->bk_items, max_items * sizeof(BkItem)));
+  GS_TRY(ensure(c, c->bk_slabs, max_slabs * sizeof(typename P::Lds)));
+  uint32_t* ns = (uint32_t*)(sm + SM_BK_N);
+  BkPlanOut po{meta + BkMeta::DBASE, meta + BkMeta::BSTART, meta + BkMeta::BCOUNT, meta + BkMeta::BITEMS,
+               meta + BkMeta::BSLAB, meta + BkMeta::MLIST, c->bk_items.as<BkItem>(), ns + 0, ns + 1};
+  hipLaunchKernelGGL(k_bk_plan, dim3(1), dim3(BK_PLAN_BLOCK), 0, c->stream, meta + BkMeta::HIST, g.nb, g.passes, g.w,
+                     BK_ITEM, po);
+  GS_HIP(hipGetLastError());
+  hipEventRecord(c->ev[1], c->stream);
+  hipEventRecord(c->pass_ev[0], c->stream);
+
+  // 3. partition passes over the bucket index; the last stores the 16-bit bucket-local index
+  const size_t vb = HAS_V ? sizeof(Raw) : 0;
+  const size_t ab = std::max(sizeof(typename P::A), vb);
+  GS_TRY(ensure(c, c->keysA, R * 4));
+  GS_TRY(ensure(c, c->keysB, R * 4));
+  GS_TRY(ensure(c, c->valsA, R * std::max<size_t>(ab, 4)));
+  if (HAS_V) GS_TRY(ensure(c, c->valsB, R * vb));
+  if (std::is_same_v<P, BkDeg>) GS_TRY(ensure(c, c->aux, R * 8));
+  const uint32_t tiles = (uint32_t)((R + SORT_TILE - 1) / SORT_TILE);
+  GS_TRY(ensure(c, c->sort_status, (size_t)tiles * 256 * 8, true));
+  using ESrc = BaseSrc<Raw, DIR, P::PAY>;
+  const ESrc es{src, dst, (const Raw*)val, base};
+  uint16_t* k16 = c->keysB.as<uint16_t>();
+  Raw* vpart = HAS_V ? c->valsB.as<Raw>() : nullptr;
+  if (g.passes == 1) {
+    GS_TRY((launch_part_w<uint32_t, uint16_t, Raw, HAS_V>(c, g.w, es, k16, vpart, (uint32_t)R, 0, S)));
+    hipEventRecord(c->pass_ev[1], c->stream);
+  } else if (g.passes == 2) {
+    uint32_t* k32 = c->keysA.as<uint32_t>();
+    Raw* vmid = HAS_V ? c->valsA.as<Raw>() : nullptr;
+    GS_TRY((launch_part_w<uint32_t, uint32_t, Raw, HAS_V>(c, g.w, es, k32, vmid, (uint32_t)R, 0, S)));
+    hipEventRecord(c->pass_ev[1], c->stream);
+    const BufSrc<uint32_t, Raw> bs{k32, vmid, 0};
+    GS_TRY((launch_part_w<uint32_t, uint16_t, Raw, HAS_V>(c, g.w, bs, k16, vpart, (uint32_t)R, 1, S + g.w)));
+    hipEventRecord(c->pass_ev[2], c->stream);
+  }
+  hipEventRecord(c->ev[2], c->stream);
+
+  // 4. LDS accumulation (persistent), 5. merge of multi-item buckets, 6. emit
+  if (!c->n_cu) {
+    int cu = 0;
+    GS_HIP(hipDeviceGetAttribute(&cu, hipDeviceAttributeMultiprocessorCount, c->device));
+    c->n_cu = std::max(1, cu);
+  }
+  GS_HIP(hipMemsetAsync(ns + 2, 0, 4, c->stream));
+  BkStage st{c->keysA.as<uint32_t>(), c->valsA.p, std::is_same_v<P, BkDeg> ? c->aux.as<int64_t>() : nullptr};
+  auto* slabs = c->bk_slabs.as<typename P::Lds>();
+  if (g.passes == 0) {
+    hipLaunchKernelGGL((k_bk_accum<P, ESrc, GS_BK_UNROLL>), dim3(c->n_cu), dim3(BK_ACC_BLOCK), 0, c->stream, es,
+                       c->bk_items.as<BkItem>(), ns + 0, meta + BkMeta::BSTART, ns + 2, slabs, st,
+                       meta + BkMeta::BCOUNT);
+  } else {
+    const PartSrc<Raw> ps{k16, vpart};
+    hipLaunchKernelGGL((k_bk_accum<P, PartSrc<Raw>, GS_BK_UNROLL>), dim3(c->n_cu), dim3(BK_ACC_BLOCK), 0, c->stream,
+                       ps, c->bk_items.as<BkItem>(), ns + 0, meta + BkMeta::BSTART, ns + 2, slabs, st,
+                       meta + BkMeta::BCOUNT);
+  }
+  GS_HIP(hipGetLastError());
+  hipEventRecord(c->pass_ev[g.passes + 1], c->stream);
+  const unsigned mgrid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(g.nb, R / BK_ITEM + 1));
+  hipLaunchKernelGGL((k_bk_merge<P>), dim3(mgrid), dim3(BK_ACC_BLOCK), 0, c->stream, meta + BkMeta::MLIST, ns + 1,
+                     meta + BkMeta::BITEMS, meta + BkMeta::BSLAB, meta + BkMeta::BSTART, slabs, st,
+                     meta + BkMeta::BCOUNT);
+  GS_HIP(hipGetLastError());
+  hipEventRecord(c->pass_ev[g.passes + 2], c->stream);
+  hipLaunchKernelGGL((k_bk_emit<P>), dim3(g.nb), dim3(256), 0, c->stream, meta + BkMeta::BSTART, meta + BkMeta::BCOUNT,
+                     g.nb, st, base, o, (unsigned long long*)(sm + SM_BK_MM + 24));
+  GS_HIP(hipGetLastError());
+  hipEventRecord(c->pass_ev[g.passes + 3], c->stream);
+  hipEventRecord(c->ev[3], c->stream);
+  GS_HIP(hipMemcpyAsync(c->host_small, sm + SM_BK_MM, 48, hipMemcpyDeviceToHost, c->stream));
+  GS_HIP(hipMemcpyAsync(c->host_small + 6, sm + SM_TIMEOUT, 8, hipMemcpyDeviceToHost, c->stream));
+  GS_HIP(hipStreamSynchronize(c->stream));
+  if ((uint32_t)c->host_small[6] != 0) return set_error(c, GS_EDEVICE, "look-back spin timed out");
+  *U = c->host_small[3];
+  const uint32_t n_items = (uint32_t)c->host_small[4];
+
+  // stage times
+  float a = 0, b = 0, d = 0;
+  hipEventElapsedTime(&a, c->ev[0], c->ev[1]);
+  hipEventElapsedTime(&b, c->ev[1], c->ev[2]);
+  hipEventElapsedTime(&d, c->ev[2], c->ev[3]);
+  gs_stage_times& t = c->times;
+  t = gs_stage_times{};
+  t.keyinfo_ms = a;
+  t.sort_ms = b;
+  t.reduce_ms = d;
+  t.total_ms = a + b + d;
+  t.sort_passes = (uint32_t)g.passes;
+  t.key_bits = g.nb <= 1 ? (uint32_t)S : (uint32_t)(S + 32 - __builtin_clz(g.nb - 1));
+  t.records = R;
+  t.vertices = *U;
+  for (int p = 0; p < g.passes + 3 && p < 8; ++p) hipEventElapsedTime(&t.pass_ms[p], c->pass_ev[p], c->pass_ev[p + 1]);
+  t.key_bytes = 2;
+  t.payload_bytes = (uint32_t)vb;
+  t.partials = n_items;
+  t.fused_last = 0;
+  t.path = 1;
+  return GS_OK;
+}
+
+template <class P>
+gs_status bucket_dir(gs_ctx* c, int dir, const int64_t* src, const int64_t* dst, const void* val, uint64_t n,
+                     typename P::Out o, uint64_t* U) {
+  switch (dir) {
+    case DIR_IN: return bucket_run<P, DIR_IN>(c, src, dst, val, n, o, U);
+    case DIR_OUT: return bucket_run<P, DIR_OUT>(c, src, dst, val, n, o, U);
+    case DIR_ALL: return bucket_run<P, DIR_ALL>(c, src, dst, val, n, o, U);
+  }
+  return set_error(c, GS_EINVAL, "bad direction %d", dir);
+}
+
+template <typename T, int OP>
+gs_status bucket_value(gs_ctx* c, int dir, const int64_t* src, const int64_t* dst, const void* val, uint64_t n,
+                       bool has_init, const void* init, int64_t* keys, void* vals, uint64_t* U) {
+  using P = BkVal<T, OP>;
+  typename P::Out o{keys, (T*)vals, has_init ? *(const T*)init : T{}, has_init};
+  return bucket_dir<P>(c, dir, src, dst, val, n, o, U);
+}
+
+template <typename T>
+gs_status bucket_value_op(gs_ctx* c, int op, int dir, const int64_t* src, const int64_t* dst, const void* val,
+                          uint64_t n, bool has_init, const void* init, int64_t* keys, void* vals, uint64_t* U) {
+  switch (op) {
+    case OP_SUM: return bucket_value<T, OP_SUM>(c, dir, src, dst, val, n, has_init, init, keys, vals, U);
+    case OP_MIN:
+      if constexpr (std::is_integral_v<T>) return bucket_value<T, OP_MIN>(c, dir, src, dst, val, n, has_init, init, keys, vals, U);
+      break;
+    case OP_MAX:
+      if constexpr (std::is_integral_v<T>) return bucket_value<T, OP_MAX>(c, dir, src, dst, val, n, has_init, init, keys, vals, U);
+      break;
+  }
+  return GS_EUNSUPPORTED;
+}
+
+}  // namespace
+
+gs_status bucket_reduce(gs_ctx* c, const int64_t* src, const int64_t* dst, const void* val, uint64_t n, int dir,
+                        int op, int dtype, bool has_init, const void* init, int64_t* keys, void* vals, uint64_t* U) {
+  if (c->flags & GS_FLAG_SORT_ONLY) return GS_EUNSUPPORTED;
+  if (op == OP_COUNT) {
+    BkCount::Out o{keys, (int64_t*)vals, has_init ? *(const int64_t*)init : 0};
+    return bucket_dir<BkCount>(c, dir, src, dst, nullptr, n, o, U);
+  }
+  switch (dtype) {
+    case GS_I32: return bucket_value_op<int32_t>(c, op, dir, src, dst, val, n, has_init, init, keys, vals, U);
+    case GS_I64: return bucket_value_op<int64_t>(c, op, dir, src, dst, val, n, has_init, init, keys, vals, U);
+    case GS_F32: return bucket_value_op<float>(c, op, dir, src, dst, val, n, has_init, init, keys, vals, U);
+    case GS_F64: return bucket_value_op<double>(c, op, dir, src, dst, val, n, has_init, init, keys, vals, U);
+  }
+  return GS_EUNSUPPORTED;
+}
+
+gs_status bucket_degree_max(gs_ctx* c, const int64_t* src, const int64_t* dst, uint64_t n, int dir, int64_t init_max,
+                            int64_t* keys, int64_t* deg, int64_t* mx, uint64_t* U) {
+  if (c->flags & GS_FLAG_SORT_ONLY) return GS_EUNSUPPORTED;
+  BkDeg::Out o{keys, deg, mx, init_max};
+  return bucket_dir<BkDeg>(c, dir, src, dst, nullptr, n, o, U);
+}
+
+}  // namespace gs

@@ -1,0 +1,539 @@
+// gs_bucket.hpp — the bucket path for the associative built-ins (reduceOnEdges / foldNeighbors with
+// SUM, MIN, MAX, COUNT or the degree / max-neighbour fold).
+//
+// The reference folds each (vertex, window) group with Flink's reducing / folding window state
+// (GraphWindowStream.java:62-87, 101-121).  For an associative and commutative op the fold needs
+// the records GROUPED by vertex, not ORDERED within a vertex, so a full LSD sort is more than the
+// op requires.  This path sorts only the HIGH bits:
+//
+//   c = key - base                 (base = window's smallest vertex, or a predicted lower bound)
+//   bucket = c >> S                (S = 13..15: 2^S vertices whose accumulators fit one CU's LDS)
+//   k_bk_info    one read of the keys: min / max and the histogram of the bucket index;
+//   k_bk_plan    one block: per-pass digit bases, bucket starts, the work items;
+//   k_onesweep   1-2 LSD passes of 4-6-bit digits over the bucket index (long runs per digit, so
+//                the scatter writes are near-sequential); the last pass stores only the low 16 bits;
+//   k_bk_accum   one persistent workgroup per CU takes items (bucket, record range), adds every
+//                record into LDS accumulators with LDS atomics (ds_add/min/max), then writes the
+//                bucket's vertices in ascending order (wave ballot compaction) to a staging area;
+//                buckets larger than one item leave LDS slabs that k_bk_merge combines;
+//   k_bk_emit    staging -> (vertex, value) outputs, vertices ascending (the sort path's order).
+// Integer results are bit-exact (wrapping adds, min / max); f64 / f32 sums are summed in f64 in
+// LDS-atomic order, within the API's 1e-5 relative tolerance.  Float MIN / MAX keep the sort path
+// (Java's Math.min/max NaN and signed-zero rules have no LDS atomic).
+#pragma once
+#include <limits>
+#include <type_traits>
+
+#include "gs_radix.hpp"
+#include "gs_rbk.hpp"
+
+namespace gs {
+
+constexpr int BK_MAXB = 2048;          // buckets (the bucket index has <= 11 bits)
+constexpr int BK_INFO_BLOCK = 512;
+constexpr int BK_ACC_BLOCK = 1024;     // 16 waves: one workgroup per CU (LDS-bound)
+constexpr int BK_NW = BK_ACC_BLOCK / WAVE;
+constexpr int BK_PLAN_BLOCK = 1024;
+
+struct BkItem {
+  uint32_t bucket, begin, end, slab;   // slab = ~0u: the bucket is one item (finalize directly)
+};
+
+struct BkStage {
+  uint32_t* k;   // compact vertex (c)
+  void* a;       // per-vertex accumulator (policy type)
+  int64_t* b;    // second accumulator (degree fold: max neighbour)
+};
+
+struct BkPlanOut {
+  uint32_t* digit_base;    // [2][256]
+  uint32_t* bucket_start;  // [NB + 1]
+  uint32_t* bucket_count;  // [NB]   outputs per bucket (written by finalize)
+  uint32_t* b_items;       // [NB]
+  uint32_t* b_slab;        // [NB]   first slab of a multi-item bucket
+  uint32_t* mlist;         // [NB]   multi-item buckets
+  BkItem* items;
+  uint32_t* n_items;       // device scalars
+  uint32_t* n_multi;
+};
+
+// ---- policies: LDS accumulator layout and the op ------------------------------------------------
+template <typename T>
+__device__ __forceinline__ T bits_as(uint64_t r) {
+  if constexpr (sizeof(T) == 8) return __builtin_bit_cast(T, r);
+  else return __builtin_bit_cast(T, (uint32_t)r);
+}
+
+// value ops: SUM / MIN / MAX over I32 / I64, SUM over F32 / F64 (accumulated in f64)
+template <typename T, int OP>
+struct BkVal {
+  using Raw = std::conditional_t<sizeof(T) == 4, uint32_t, uint64_t>;
+  using A = std::conditional_t<std::is_floating_point_v<T>, double, T>;
+  static constexpr int S = sizeof(A) == 8 ? 14 : 15;
+  static constexpr uint32_t W = 1u << S;
+  static constexpr bool HAS_V = true;
+  static constexpr int PAY = PAY_VAL;
+  struct Lds {
+    A acc[W];
+    uint32_t bm[W / 32];
+  };
+  __device__ static A identity() {
+    if constexpr (OP == OP_SUM) return A(0);
+    else if constexpr (OP == OP_MIN) return std::numeric_limits<A>::max();
+    else return std::numeric_limits<A>::lowest();
+  }
+  __device__ static A combine(A a, A b) {
+    if constexpr (OP == OP_SUM) {
+      if constexpr (std::is_integral_v<A>) return (A)((std::make_unsigned_t<A>)a + (std::make_unsigned_t<A>)b);
+      else return a + b;
+    } else if constexpr (OP == OP_MIN) return b < a ? b : a;
+    else return b > a ? b : a;
+  }
+  __device__ static void init(Lds& s, int tid) {
+    for (uint32_t i = tid; i < W; i += BK_ACC_BLOCK) s.acc[i] = identity();
+    for (uint32_t i = tid; i < W / 32; i += BK_ACC_BLOCK) s.bm[i] = 0;
+  }
+  __device__ static void add(Lds& s, uint32_t i, Raw r) {
+    const T v = bits_as<T>(r);
+    if constexpr (OP == OP_SUM) {
+      if constexpr (std::is_integral_v<T>) {
+        using U = std::conditional_t<sizeof(T) == 8, unsigned long long, unsigned int>;
+        atomicAdd((U*)&s.acc[i], (U)v);
+      } else {
+        atomicAdd(&s.acc[i], (double)v);
+      }
+    } else if constexpr (OP == OP_MIN) {
+      using I = std::conditional_t<sizeof(T) == 8, long long, int>;
+      atomicMin((I*)&s.acc[i], (I)v);
+    } else {
+      using I = std::conditional_t<sizeof(T) == 8, long long, int>;
+      atomicMax((I*)&s.acc[i], (I)v);
+    }
+    atomicOr(&s.bm[i >> 5], 1u << (i & 31));
+  }
+  __device__ static bool present(const Lds& s, uint32_t i) { return (s.bm[i >> 5] >> (i & 31)) & 1u; }
+  __device__ static void stage(BkStage st, uint32_t pos, const Lds& s, uint32_t i) { ((A*)st.a)[pos] = s.acc[i]; }
+  __device__ static void merge(Lds& s, const Lds* g, int tid) {
+    for (uint32_t i = tid; i < W; i += BK_ACC_BLOCK) s.acc[i] = combine(s.acc[i], g->acc[i]);
+    for (uint32_t i = tid; i < W / 32; i += BK_ACC_BLOCK) s.bm[i] |= g->bm[i];
+  }
+  struct Out {
+    int64_t* keys;
+    T* vals;
+    T init;
+    bool has_init;
+  };
+  __device__ static void emit(const Out& o, uint64_t u, int64_t key, BkStage st, uint32_t j) {
+    const A a = ((const A*)st.a)[j];
+    o.keys[u] = key;
+    if constexpr (std::is_floating_point_v<T>) {
+      o.vals[u] = o.has_init ? (T)((double)o.init + a) : (T)a;
+    } else {
+      o.vals[u] = o.has_init ? ValueOp<T, OP>::combine(o.init, a) : a;
+    }
+  }
+};
+
+// COUNT: the number of incident records (foldNeighbors' init + count)
+struct BkCount {
+  using Raw = uint8_t;
+  using A = uint32_t;
+  static constexpr int S = 15;
+  static constexpr uint32_t W = 1u << S;
+  static constexpr bool HAS_V = false;
+  static constexpr int PAY = PAY_NONE;
+  struct Lds {
+    uint32_t cnt[W];
+  };
+  __device__ static void init(Lds& s, int tid) {
+    for (uint32_t i = tid; i < W; i += BK_ACC_BLOCK) s.cnt[i] = 0;
+  }
+  __device__ static void add(Lds& s, uint32_t i, Raw) { atomicAdd(&s.cnt[i], 1u); }
+  __device__ static bool present(const Lds& s, uint32_t i) { return s.cnt[i] != 0; }
+  __device__ static void stage(BkStage st, uint32_t pos, const Lds& s, uint32_t i) { ((uint32_t*)st.a)[pos] = s.cnt[i]; }
+  __device__ static void merge(Lds& s, const Lds* g, int tid) {
+    for (uint32_t i = tid; i < W; i += BK_ACC_BLOCK) s.cnt[i] += g->cnt[i];
+  }
+  struct Out {
+    int64_t* keys;
+    int64_t* vals;
+    int64_t init;
+  };
+  __device__ static void emit(const Out& o, uint64_t u, int64_t key, BkStage st, uint32_t j) {
+    o.keys[u] = key;
+    o.vals[u] = (int64_t)((uint64_t)o.init + ((const uint32_t*)st.a)[j]);
+  }
+};
+
+// degree / max-neighbour fold (TestSlice.java:233-239's shape)
+struct BkDeg {
+  using Raw = uint64_t;   // neighbour ID
+  using A = uint32_t;
+  static constexpr int S = 13;
+  static constexpr uint32_t W = 1u << S;
+  static constexpr bool HAS_V = true;
+  static constexpr int PAY = PAY_NBR;
+  struct Lds {
+    long long mx[W];
+    uint32_t cnt[W];
+  };
+  __device__ static void init(Lds& s, int tid) {
+    for (uint32_t i = tid; i < W; i += BK_ACC_BLOCK) {
+      s.cnt[i] = 0;
+      s.mx[i] = std::numeric_limits<long long>::lowest();
+    }
+  }
+  __device__ static void add(Lds& s, uint32_t i, Raw r) {
+    atomicAdd(&s.cnt[i], 1u);
+    atomicMax(&s.mx[i], (long long)r);
+  }
+  __device__ static bool present(const Lds& s, uint32_t i) { return s.cnt[i] != 0; }
+  __device__ static void stage(BkStage st, uint32_t pos, const Lds& s, uint32_t i) {
+    ((uint32_t*)st.a)[pos] = s.cnt[i];
+    st.b[pos] = s.mx[i];
+  }
+  __device__ static void merge(Lds& s, const Lds* g, int tid) {
+    for (uint32_t i = tid; i < W; i += BK_ACC_BLOCK) {
+      s.cnt[i] += g->cnt[i];
+      const long long m = g->mx[i];
+      if (m > s.mx[i]) s.mx[i] = m;
+    }
+  }
+  struct Out {
+    int64_t* keys;
+    int64_t* deg;
+    int64_t* mx;
+    int64_t init_max;
+  };
+  __device__ static void emit(const Out& o, uint64_t u, int64_t key, BkStage st, uint32_t j) {
+    o.keys[u] = key;
+    o.deg[u] = (int64_t)((const uint32_t*)st.a)[j];
+    const int64_t m = st.b[j];
+    o.mx[u] = m > o.init_max ? m : o.init_max;
+  }
+};
+
+// ---- record sources ------------------------------------------------------------------------------
+// window edge columns, key relative to `base` (direction expansion as in EdgeSrc)
+template <typename V, int DIR, int PAY>
+struct BaseSrc {
+  const int64_t* src;
+  const int64_t* dst;
+  const V* val;
+  int64_t base;
+  __device__ __forceinline__ void load(uint32_t r, uint32_t& k, V& v) const {
+    uint32_t i = r;
+    bool rev = (DIR == DIR_IN);
+    if (DIR == DIR_ALL) { i = r >> 1; rev = r & 1u; }
+    const int64_t a = rev ? dst[i] : src[i];
+    k = (uint32_t)((uint64_t)a - (uint64_t)base);
+    if constexpr (PAY == PAY_VAL) v = val[i];
+    else if constexpr (PAY == PAY_NBR) v = (V)(rev ? src[i] : dst[i]);
+  }
+};
+
+// partitioned records: 16-bit bucket-local index + payload
+template <typename V>
+struct PartSrc {
+  const uint16_t* keys;
+  const V* vals;
+  __device__ __forceinline__ void load(uint32_t r, uint32_t& k, V& v) const {
+    k = keys[r];
+    if constexpr (!std::is_same_v<V, uint8_t>) v = vals[r];
+  }
+};
+
+// ---- k_bk_info: min / max of the keys and the bucket histogram (relative to a predicted base) ----
+// mm[0] = max(~flip(key)) (i.e. min), mm[1] = max(flip(key)), mm[2] = keys outside the prediction
+template <int DIR, bool VEC>
+__global__ __launch_bounds__(BK_INFO_BLOCK) void k_bk_info(const int64_t* __restrict__ src,
+                                                           const int64_t* __restrict__ dst, uint64_t n,
+                                                           int64_t base, int S, uint32_t nb,
+                                                           uint32_t* __restrict__ hist,
+                                                           unsigned long long* __restrict__ mm) {
+  __shared__ uint32_t h[BK_MAXB];
+  const int tid = threadIdx.x;
+  for (int i = tid; i < BK_MAXB; i += BK_INFO_BLOCK) h[i] = 0;
+  __syncthreads();
+  uint64_t lo = 0, hi = 0;   // max of ~flip, max of flip
+  uint32_t ovf = 0;
+  auto add = [&](int64_t k) {
+    const uint64_t f = (uint64_t)k ^ (1ull << 63);
+    lo = max(lo, ~f);
+    hi = max(hi, f);
+    const uint64_t d = ((uint64_t)k - (uint64_t)base) >> S;
+    if (k < base || d >= nb) ++ovf;
+    else atomicAdd(&h[d], 1u);
+  };
+  if constexpr (!VEC) {
+    const uint64_t stride = (uint64_t)gridDim.x * BK_INFO_BLOCK;
+    for (uint64_t i = (uint64_t)blockIdx.x * BK_INFO_BLOCK + tid; i < n; i += stride) {
+      if (DIR != DIR_IN) add(src[i]);
+      if (DIR != DIR_OUT) add(dst[i]);
+    }
+  } else {
+    const uint64_t npair = n >> 1;
+    const longlong2* s2 = reinterpret_cast<const longlong2*>(src);
+    const longlong2* d2 = reinterpret_cast<const longlong2*>(dst);
+    constexpr int U = 4;
+    const uint64_t stride = (uint64_t)gridDim.x * BK_INFO_BLOCK * U;
+    for (uint64_t q = (uint64_t)blockIdx.x * BK_INFO_BLOCK * U + tid; q < npair; q += stride) {
+      longlong2 a[U], b[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const uint64_t qq = q + (uint64_t)BK_INFO_BLOCK * u;
+        if (qq < npair) {
+          if (DIR != DIR_IN) a[u] = s2[qq];
+          if (DIR != DIR_OUT) b[u] = d2[qq];
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if (q + (uint64_t)BK_INFO_BLOCK * u < npair) {
+          if (DIR != DIR_IN) { add(a[u].x); add(a[u].y); }
+          if (DIR != DIR_OUT) { add(b[u].x); add(b[u].y); }
+        }
+      }
+    }
+    if ((n & 1) && blockIdx.x == 0 && tid == 0) {
+      if (DIR != DIR_IN) add(src[n - 1]);
+      if (DIR != DIR_OUT) add(dst[n - 1]);
+    }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    lo = max(lo, (uint64_t)__shfl_xor((unsigned long long)lo, o, WAVE));
+    hi = max(hi, (uint64_t)__shfl_xor((unsigned long long)hi, o, WAVE));
+    ovf += __shfl_xor(ovf, o, WAVE);
+  }
+  if ((tid & 63) == 0) {
+    atomicMax(&mm[0], (unsigned long long)lo);
+    atomicMax(&mm[1], (unsigned long long)hi);
+    if (ovf) atomicAdd(&mm[2], (unsigned long long)ovf);
+  }
+  __syncthreads();
+  for (uint32_t i = tid; i < nb; i += BK_INFO_BLOCK) {
+    const uint32_t c = h[i];
+    if (c) atomicAdd(&hist[i], c);
+  }
+}
+
+// block-wide exclusive scan of one u32 per thread (BLOCK = BK_PLAN_BLOCK); returns the total
+__device__ __forceinline__ uint32_t bk_block_scan(uint32_t x, uint32_t* s_w, uint32_t& total) {
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  constexpr int NW = BK_PLAN_BLOCK / WAVE;
+  const uint32_t inc = wave_inclusive_sum(x);
+  if (lane == 63) s_w[w] = inc;
+  __syncthreads();
+  uint32_t off = 0, tot = 0;
+#pragma unroll
+  for (int i = 0; i < NW; ++i) {
+    const uint32_t v = s_w[i];
+    off += i < w ? v : 0u;
+    tot += v;
+  }
+  __syncthreads();
+  total = tot;
+  return off + inc - x;
+}
+
+// ---- k_bk_plan: digit bases of the partition passes, bucket starts, work items (one block) -------
+// pass p ranks digit (bucket >> (p * w)) & (2^w - 1); bucket b's records end up at
+// [bucket_start[b], bucket_start[b + 1]).  Items: a bucket of cnt records is split into
+// ceil(cnt / item_recs) items; multi-item buckets get consecutive slabs.
+static __global__ __launch_bounds__(BK_PLAN_BLOCK) void k_bk_plan(const uint32_t* __restrict__ hist, uint32_t nb,
+                                                                  int passes, int w, uint32_t item_recs,
+                                                                  BkPlanOut o) {
+  __shared__ uint32_t s_dh[2][256];
+  __shared__ uint32_t s_w[BK_PLAN_BLOCK / WAVE];
+  const int tid = threadIdx.x;
+  for (int i = tid; i < 2 * 256; i += BK_PLAN_BLOCK) (&s_dh[0][0])[i] = 0;
+  __syncthreads();
+  // two buckets per thread (BK_MAXB = 2 * BK_PLAN_BLOCK)
+  const uint32_t b0 = 2 * tid, b1 = 2 * tid + 1;
+  const uint32_t c0 = b0 < nb ? hist[b0] : 0u, c1 = b1 < nb ? hist[b1] : 0u;
+  const uint32_t dmask = (1u << w) - 1;
+  for (int p = 0; p < passes; ++p) {
+    if (c0) atomicAdd(&s_dh[p][(b0 >> (p * w)) & dmask], c0);
+    if (c1) atomicAdd(&s_dh[p][(b1 >> (p * w)) & dmask], c1);
+  }
+  uint32_t total;
+  const uint32_t start0 = bk_block_scan(c0 + c1, s_w, total);
+  if (b0 < nb) o.bucket_start[b0] = start0;
+  if (b1 < nb) o.bucket_start[b1] = start0 + c0;
+  if (tid == 0) o.bucket_start[nb] = total;
+  // digit bases (s_dh complete after the scan's barriers)
+  if (tid < passes) {   // <= 256 digits per pass, one thread each
+    uint32_t run = 0;
+    for (uint32_t d = 0; d <= dmask; ++d) {
+      o.digit_base[tid * 256 + d] = run;
+      run += s_dh[tid][d];
+    }
+  }
+  // items
+  auto nitems = [&](uint32_t c) { return c == 0 ? 0u : (c + item_recs - 1) / item_recs; };
+  const uint32_t i0 = nitems(c0), i1 = nitems(c1);
+  const uint32_t m0 = i0 > 1 ? i0 : 0u, m1 = i1 > 1 ? i1 : 0u;
+  uint32_t n_items, n_slabs, n_multi;
+  const uint32_t first0 = bk_block_scan(i0 + i1, s_w, n_items);
+  const uint32_t slab0 = bk_block_scan(m0 + m1, s_w, n_slabs);
+  const uint32_t mb0 = bk_block_scan((m0 ? 1u : 0u) + (m1 ? 1u : 0u), s_w, n_multi);
+  auto emit_bucket = [&](uint32_t b, uint32_t c, uint32_t ni, uint32_t first, uint32_t slab, uint32_t mb) {
+    if (b >= nb) return;
+    o.bucket_count[b] = 0;
+    o.b_items[b] = ni;
+    o.b_slab[b] = slab;
+    if (ni > 1) o.mlist[mb] = b;
+    for (uint32_t k = 0; k < ni; ++k) {
+      BkItem it;
+      it.bucket = b;
+      it.begin = k * item_recs;   // relative; made absolute below
+      it.end = min(c, (k + 1) * item_recs);
+      it.slab = ni > 1 ? slab + k : ~0u;
+      o.items[first + k] = it;
+    }
+  };
+  emit_bucket(b0, c0, i0, first0, slab0, mb0);
+  emit_bucket(b1, c1, i1, first0 + i0, slab0 + m0, mb0 + (m0 ? 1u : 0u));
+  if (tid == 0) {
+    *o.n_items = n_items;
+    *o.n_multi = n_multi;
+  }
+}
+
+// ---- k_bk_accum: persistent; LDS accumulation of (bucket, record range) items ---------------------
+// Finalize (shared with k_bk_merge): the bucket's vertices in ascending order -> staging at the
+// bucket's record offset (a bucket has at least as many records as vertices).
+template <class P>
+__device__ __forceinline__ void bk_finalize(const typename P::Lds& s, uint32_t bucket, uint32_t stage_at,
+                                            BkStage st, uint32_t* bucket_count, uint32_t* s_wc) {
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  constexpr uint32_t PER = P::W / BK_NW;   // entries per wave
+  const uint32_t e0 = (uint32_t)w * PER;
+  uint32_t cnt = 0;
+  for (uint32_t j = 0; j < PER; j += WAVE) cnt += (uint32_t)__popcll(ballot(P::present(s, e0 + j + lane)));
+  if (lane == 0) s_wc[w] = cnt;
+  __syncthreads();
+  uint32_t off = 0, tot = 0;
+#pragma unroll
+  for (int i = 0; i < BK_NW; ++i) {
+    const uint32_t v = s_wc[i];
+    off += i < w ? v : 0u;
+    tot += v;
+  }
+  const uint32_t cbase = bucket << P::S;
+  for (uint32_t j = 0; j < PER; j += WAVE) {
+    const uint32_t e = e0 + j + lane;
+    const bool p = P::present(s, e);
+    const uint64_t m = ballot(p);
+    if (p) {
+      const uint32_t pos = stage_at + off + mbcnt(m);
+      st.k[pos] = cbase | e;
+      P::stage(st, pos, s, e);
+    }
+    off += (uint32_t)__popcll(m);
+  }
+  if (tid == 0) bucket_count[bucket] = tot;
+}
+
+template <class P, class Src, int UNROLL>
+__global__ __launch_bounds__(BK_ACC_BLOCK) void k_bk_accum(Src src, const BkItem* __restrict__ items,
+                                                           const uint32_t* __restrict__ n_items_p,
+                                                           const uint32_t* __restrict__ bucket_start,
+                                                           uint32_t* __restrict__ ctr,
+                                                           typename P::Lds* __restrict__ slabs, BkStage st,
+                                                           uint32_t* __restrict__ bucket_count) {
+  __shared__ typename P::Lds s;
+  __shared__ uint32_t s_item;
+  __shared__ uint32_t s_wc[BK_NW];
+  using Raw = typename P::Raw;
+  const int tid = threadIdx.x;
+  const uint32_t n_items = *n_items_p;
+  for (;;) {
+    if (tid == 0) s_item = atomicAdd(ctr, 1u);
+    __syncthreads();
+    const uint32_t it = s_item;
+    if (it >= n_items) break;
+    const BkItem m = items[it];
+    const uint32_t b0 = bucket_start[m.bucket];
+    P::init(s, tid);
+    __syncthreads();
+    const uint32_t r0 = b0 + m.begin, r1 = b0 + m.end;
+    for (uint32_t r = r0 + tid; r < r1; r += BK_ACC_BLOCK * UNROLL) {
+      uint32_t k[UNROLL];
+      Raw v[UNROLL];
+#pragma unroll
+      for (int u = 0; u < UNROLL; ++u) {
+        const uint32_t q = r + (uint32_t)u * BK_ACC_BLOCK;
+        if (q < r1) src.load(q, k[u], v[u]);
+      }
+#pragma unroll
+      for (int u = 0; u < UNROLL; ++u) {
+        const uint32_t q = r + (uint32_t)u * BK_ACC_BLOCK;
+        if (q < r1) P::add(s, k[u] & (P::W - 1), v[u]);
+      }
+    }
+    __syncthreads();
+    if (m.slab == ~0u) {
+      bk_finalize<P>(s, m.bucket, b0, st, bucket_count, s_wc);
+    } else {
+      // dump the LDS accumulators (k_bk_merge, a later launch, combines the bucket's slabs)
+      const uint4* ls = reinterpret_cast<const uint4*>(&s);
+      uint4* gs = reinterpret_cast<uint4*>(slabs + m.slab);
+      for (uint32_t i = tid; i < sizeof(typename P::Lds) / 16; i += BK_ACC_BLOCK) gs[i] = ls[i];
+    }
+    __syncthreads();
+  }
+}
+
+template <class P>
+__global__ __launch_bounds__(BK_ACC_BLOCK) void k_bk_merge(const uint32_t* __restrict__ mlist,
+                                                           const uint32_t* __restrict__ n_multi_p,
+                                                           const uint32_t* __restrict__ b_items,
+                                                           const uint32_t* __restrict__ b_slab,
+                                                           const uint32_t* __restrict__ bucket_start,
+                                                           const typename P::Lds* __restrict__ slabs, BkStage st,
+                                                           uint32_t* __restrict__ bucket_count) {
+  __shared__ typename P::Lds s;
+  __shared__ uint32_t s_wc[BK_NW];
+  const int tid = threadIdx.x;
+  if (blockIdx.x >= *n_multi_p) return;
+  const uint32_t b = mlist[blockIdx.x];
+  const uint32_t n = b_items[b], f = b_slab[b];
+  // slab 0 initialises (a slab holds identities where its item saw no record)
+  {
+    const uint4* gs = reinterpret_cast<const uint4*>(slabs + f);
+    uint4* ls = reinterpret_cast<uint4*>(&s);
+    for (uint32_t i = tid; i < sizeof(typename P::Lds) / 16; i += BK_ACC_BLOCK) ls[i] = gs[i];
+  }
+  __syncthreads();
+  for (uint32_t k = 1; k < n; ++k) P::merge(s, slabs + f + k, tid);   // fixed element -> thread map
+  __syncthreads();
+  bk_finalize<P>(s, b, bucket_start[b], st, bucket_count, s_wc);
+}
+
+// ---- k_bk_emit: staging -> outputs, vertices ascending --------------------------------------------
+template <class P>
+__global__ __launch_bounds__(256) void k_bk_emit(const uint32_t* __restrict__ bucket_start,
+                                                 const uint32_t* __restrict__ bucket_count, uint32_t nb,
+                                                 BkStage st, int64_t base, typename P::Out o,
+                                                 unsigned long long* __restrict__ n_out) {
+  __shared__ uint32_t s_w[4];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const uint32_t b = blockIdx.x;
+  uint32_t part = 0;
+  for (uint32_t i = tid; i < b; i += 256) part += bucket_count[i];
+#pragma unroll
+  for (int o2 = 32; o2 > 0; o2 >>= 1) part += __shfl_xor(part, o2, WAVE);
+  if (lane == 0) s_w[w] = part;
+  __syncthreads();
+  const uint64_t off = (uint64_t)s_w[0] + s_w[1] + s_w[2] + s_w[3];
+  const uint32_t n = bucket_count[b], j0 = bucket_start[b];
+  for (uint32_t i = tid; i < n; i += 256) {
+    const uint32_t j = j0 + i;
+    P::emit(o, off + i, (int64_t)((uint64_t)base + st.k[j]), st, j);
+  }
+  if (b == nb - 1 && tid == 0) *n_out = off + n;
+}
+
+}  // namespace gs

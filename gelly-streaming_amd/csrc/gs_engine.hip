@@ -331,6 +331,7 @@ gs_status gs_create(const gs_config* cfg, gs_ctx** out) {
   gs_ctx* c = new (std::nothrow) gs_ctx();
   if (!c) return GS_ENOMEM;
   c->device = cfg ? cfg->device : 0;
+  c->flags = cfg ? cfg->flags : 0;
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= c->device) {
     delete c;
@@ -370,7 +371,7 @@ void gs_destroy(gs_ctx* c) {
   for (DevBuf* b : {&c->part_k, &c->part_a, &c->comp_k, &c->comp_a,
                     &c->in_src, &c->in_dst, &c->in_val, &c->keysA, &c->keysB, &c->valsA, &c->valsB, &c->sort_status,
                     &c->rbk_word, &c->rbk_agg, &c->rbk_inc, &c->small, &c->out_keys, &c->out_a, &c->out_b, &c->aux,
-                    &c->tri_loops, &c->tri_keep, &c->tri_tiles, &c->tri_pos, &c->tri_ou, &c->tri_onbr})
+                    &c->bk_meta, &c->bk_items, &c->bk_slabs, &c->tri_loops, &c->tri_keep, &c->tri_tiles, &c->tri_pos, &c->tri_ou, &c->tri_onbr})
     if (b->p) hipFree(b->p);
   for (auto& e : c->ev)
     if (e) hipEventDestroy(e);
@@ -413,6 +414,16 @@ gs_status gs_last_stage_times(const gs_ctx* c, gs_stage_times* out) {
   return GS_OK;
 }
 
+static gs_status finish_vertex_out(gs_ctx* c, gs_vertex_out* out, const int64_t* kd, const void* vd, size_t ob,
+                                   uint64_t U, bool direct) {
+  *out->n_out = U;
+  if (U > out->capacity) return set_error(c, GS_ECAPACITY, "output needs %llu vertices", (unsigned long long)U);
+  GS_TRY(deliver(c, out->keys, kd, U * 8, out->mem));
+  GS_TRY(deliver(c, out->vals, vd, U * ob, out->mem));
+  if (!direct) GS_HIP(hipStreamSynchronize(c->stream));
+  return GS_OK;
+}
+
 static gs_status window_fold_impl(gs_ctx* c, const gs_edge_batch* b, int32_t dir, int32_t op, bool has_init,
                                   const void* init, gs_vertex_out* out) {
   GS_TRY(check_batch(c, b, dir));
@@ -432,11 +443,7 @@ static gs_status window_fold_impl(gs_ctx* c, const gs_edge_batch* b, int32_t dir
   const int64_t *src, *dst;
   const void* val;
   GS_TRY(stage_batch(c, b, &src, &dst, &val, op != GS_OP_COUNT));
-  Sorted s;
   const int vbytes = (int)dtype_bytes(b->val_dtype);
-  GS_TRY(sort_window(c, src, dst, val, vbytes, b->n, dir, op == GS_OP_COUNT ? PAY_NONE : PAY_VAL, &s, true));
-  s.fused = true;
-  hipEventRecord(c->ev[2], c->stream);
   const size_t ob = op == GS_OP_COUNT ? 8 : (size_t)vbytes;
   const bool direct = out->mem == GS_MEM_DEVICE && out->capacity >= R;
   int64_t* kd = out->keys;
@@ -448,6 +455,15 @@ static gs_status window_fold_impl(gs_ctx* c, const gs_edge_batch* b, int32_t dir
     vd = c->out_a.p;
   }
   uint64_t U = 0;
+  const gs_status bs = bucket_reduce(c, src, dst, val, b->n, dir, op, b->val_dtype, has_init, init, kd, vd, &U);
+  if (bs != GS_EUNSUPPORTED) {
+    GS_TRY(bs);
+    return finish_vertex_out(c, out, kd, vd, ob, U, direct);
+  }
+  Sorted s;
+  GS_TRY(sort_window(c, src, dst, val, vbytes, b->n, dir, op == GS_OP_COUNT ? PAY_NONE : PAY_VAL, &s, true));
+  s.fused = true;
+  hipEventRecord(c->ev[2], c->stream);
   if (op == GS_OP_COUNT) {
     CountOut o{kd, (int64_t*)vd, has_init ? *(const int64_t*)init : 0};
     GS_TRY((s.wide ? reduce_fused<uint64_t, CountOp>(c, s, o, &U) : reduce_fused<uint32_t, CountOp>(c, s, o, &U)));
@@ -460,12 +476,7 @@ static gs_status window_fold_impl(gs_ctx* c, const gs_edge_batch* b, int32_t dir
     }
   }
   finish_times(c, s, U);
-  *out->n_out = U;
-  if (U > out->capacity) return set_error(c, GS_ECAPACITY, "output needs %llu vertices", (unsigned long long)U);
-  GS_TRY(deliver(c, out->keys, kd, U * 8, out->mem));
-  GS_TRY(deliver(c, out->vals, vd, U * ob, out->mem));
-  if (!direct) GS_HIP(hipStreamSynchronize(c->stream));
-  return GS_OK;
+  return finish_vertex_out(c, out, kd, vd, ob, U, direct);
 }
 
 gs_status gs_window_reduce(gs_ctx* c, const gs_edge_batch* b, int32_t dir, int32_t op, gs_vertex_out* out) {
@@ -492,10 +503,6 @@ gs_status gs_window_fold_degree_max(gs_ctx* c, const gs_edge_batch* b, int32_t d
   const int64_t *src, *dst;
   const void* val;
   GS_TRY(stage_batch(c, b, &src, &dst, &val, false));
-  Sorted s;
-  GS_TRY(sort_window(c, src, dst, nullptr, 0, b->n, dir, PAY_NBR, &s, true));
-  s.fused = true;
-  hipEventRecord(c->ev[2], c->stream);
   const bool direct = out->mem == GS_MEM_DEVICE && out->capacity >= R;
   int64_t *kd = out->keys, *dd = out->degree, *md = out->max_neighbor;
   if (!direct) {
@@ -506,10 +513,19 @@ gs_status gs_window_fold_degree_max(gs_ctx* c, const gs_edge_batch* b, int32_t d
     dd = c->out_a.as<int64_t>();
     md = c->out_b.as<int64_t>();
   }
-  DegMaxOut o{kd, dd, md, init_max};
   uint64_t U = 0;
-  GS_TRY((s.wide ? reduce_fused<uint64_t, DegMaxOp>(c, s, o, &U) : reduce_fused<uint32_t, DegMaxOp>(c, s, o, &U)));
-  finish_times(c, s, U);
+  const gs_status bs = bucket_degree_max(c, src, dst, b->n, dir, init_max, kd, dd, md, &U);
+  if (bs != GS_EUNSUPPORTED) {
+    GS_TRY(bs);
+  } else {
+    Sorted s;
+    GS_TRY(sort_window(c, src, dst, nullptr, 0, b->n, dir, PAY_NBR, &s, true));
+    s.fused = true;
+    hipEventRecord(c->ev[2], c->stream);
+    DegMaxOut o{kd, dd, md, init_max};
+    GS_TRY((s.wide ? reduce_fused<uint64_t, DegMaxOp>(c, s, o, &U) : reduce_fused<uint32_t, DegMaxOp>(c, s, o, &U)));
+    finish_times(c, s, U);
+  }
   *out->n_out = U;
   if (U > out->capacity) return set_error(c, GS_ECAPACITY, "output needs %llu vertices", (unsigned long long)U);
   GS_TRY(deliver(c, out->keys, kd, U * 8, out->mem));

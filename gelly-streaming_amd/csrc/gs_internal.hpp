@@ -38,6 +38,9 @@ struct gs_ctx {
   std::string err;
   uint32_t epoch = 0;
   int hist_digits = 4;   // key-byte histograms keyinfo computes (learned from the previous window)
+  uint32_t flags = 0;    // gs_config.flags
+  int64_t bk_base = 0;   // bucket path: predicted lower bound of the next window's vertex IDs
+  int n_cu = 0;          // compute units (persistent grids)
   // input staging (host batches)
   gs::DevBuf in_src, in_dst, in_val;
   // sort ping-pong
@@ -54,6 +57,8 @@ struct gs_ctx {
   gs::DevBuf tri_loops, tri_keep, tri_tiles, tri_pos, tri_ou, tri_onbr;
   // HashSet-order pipeline (gs_hashset.hip)
   gs::DevBuf hs[20];
+  // bucket path (gs_bucket.hip): plan tables, work items, LDS slabs of multi-item buckets
+  gs::DevBuf bk_meta, bk_items, bk_slabs;
   hipEvent_t ev[6] = {};
   hipEvent_t pass_ev[9] = {};
   gs_stage_times times{};
@@ -72,7 +77,9 @@ constexpr size_t SM_HIST = 32 + 256;   // u32[8][256]
 constexpr size_t SM_BASE = SM_HIST + 8 * 256 * 4;  // u32[8][256]
 constexpr size_t SM_TOTAL = SM_BASE + 8 * 256 * 4;   // u64 partial count of the fused pass
 constexpr size_t SM_TABLE = SM_TOTAL + 64;            // u32[513] region table of the fused pass
-constexpr size_t SM_BYTES = SM_TABLE + 520 * 4;
+constexpr size_t SM_BK_MM = SM_TABLE + 520 * 4;    // u64[4] bucket path: min', max', outside, U
+constexpr size_t SM_BK_N = SM_BK_MM + 32;            // u32[4] bucket path: items, multi buckets, claim ctr
+constexpr size_t SM_BYTES = SM_BK_N + 16;
 
 gs_status set_error(gs_ctx* c, gs_status s, const char* fmt, ...);
 gs_status hip_check(gs_ctx* c, hipError_t e, const char* what);
@@ -95,6 +102,12 @@ gs_status hashset_order(gs_ctx* c, const int64_t* src, const int64_t* dst, uint6
 // WindowTriangles self-pair term for windows with self-loops (loops: bitmap over compact IDs)
 gs_status triangle_selfpair_term(gs_ctx* c, const int64_t* src, const int64_t* dst, uint64_t n,
                                  const uint32_t* loops, uint64_t loops_xor, uint64_t* S);
+// Bucket path (gs_bucket.hip) for the associative built-ins; GS_EUNSUPPORTED (no message) when the
+// window or op does not fit it and the caller should take the sort path.  keys/vals: device.
+gs_status bucket_reduce(gs_ctx* c, const int64_t* src, const int64_t* dst, const void* val, uint64_t n, int dir,
+                        int op, int dtype, bool has_init, const void* init, int64_t* keys, void* vals, uint64_t* U);
+gs_status bucket_degree_max(gs_ctx* c, const int64_t* src, const int64_t* dst, uint64_t n, int dir, int64_t init_max,
+                            int64_t* keys, int64_t* deg, int64_t* mx, uint64_t* U);
 // clear the look-back timeout word at the start of a public call
 gs_status begin_call(gs_ctx* c);
 

@@ -90,6 +90,7 @@ inline void finish_times(gs_ctx* c, const Sorted& s, uint64_t U) {
   c->times.key_bytes = s.wide ? 8 : 4;
   c->times.payload_bytes = (uint32_t)s.payload_bytes;
   c->times.fused_last = s.fused ? 1u : 0u;
+  c->times.path = 0;
 }
 
 // Copy U staged outputs to the caller (host or device) — only when the direct write was impossible.

@@ -214,11 +214,16 @@ static __global__ __launch_bounds__(256) void k_digit_base(const uint32_t* __res
 // Tile = BLOCK*ITEMS records, wave-striped (wave w owns records [w*ITEMS*64, (w+1)*ITEMS*64)
 // of the tile, item j at lane l is record j*64 + l), so (wave, item, lane) order == record order
 // and ranking in that order keeps the pass stable.
-template <typename K, typename V, bool HAS_V, int BLOCK, int ITEMS, class Src>
-__global__ __launch_bounds__(BLOCK) void k_onesweep(Src src, K* __restrict__ kout, V* __restrict__ vout, uint32_t n,
+// DBITS: digit width (8 for the full LSD sort; 4-6 for the bucket path's partition passes).
+// KO: stored key type — the bucket path's last pass stores only the low 16 bits (the bucket-local
+// vertex index; the bucket itself is implied by the position).
+template <typename K, typename V, bool HAS_V, int BLOCK, int ITEMS, class Src, int DBITS = RADIX_BITS,
+          typename KO = K>
+__global__ __launch_bounds__(BLOCK) void k_onesweep(Src src, KO* __restrict__ kout, V* __restrict__ vout, uint32_t n,
                                                     uint32_t shift, const uint32_t* __restrict__ digit_base,
                                                     uint64_t* __restrict__ status, uint32_t* __restrict__ tile_ctr,
                                                     uint32_t epoch, uint32_t* __restrict__ timeout) {
+  constexpr int RADIX = 1 << DBITS;
   static_assert(BLOCK >= RADIX && BLOCK % WAVE == 0, "one thread per digit");
   constexpr int NW = BLOCK / WAVE;
   constexpr int TILE = BLOCK * ITEMS;
@@ -257,7 +262,7 @@ __global__ __launch_bounds__(BLOCK) void k_onesweep(Src src, K* __restrict__ kou
     const bool valid = r < n;
     const uint32_t d = valid ? (uint32_t)(key[j] >> shift) & (RADIX - 1) : 0u;
     const uint64_t active = ballot(valid);
-    const uint64_t peers = match_digit<RADIX_BITS>(d, active);
+    const uint64_t peers = match_digit<DBITS>(d, active);
     const uint32_t lt = mbcnt(peers);
     uint32_t base = 0;
     if (valid) base = s_whist[wid][d];
@@ -282,7 +287,7 @@ __global__ __launch_bounds__(BLOCK) void k_onesweep(Src src, K* __restrict__ kou
   // exclusive scan of the digit counts -> tile-local digit starts
   if (tid < RADIX) {
     const uint32_t inc = wave_inclusive_sum(cnt);
-    if (lane == 63) s_wtot[wid] = inc;
+    if (lane == (RADIX < WAVE ? RADIX - 1 : WAVE - 1)) s_wtot[wid] = inc;
     s_start[tid] = inc - cnt;
   }
   __syncthreads();
@@ -330,7 +335,7 @@ __global__ __launch_bounds__(BLOCK) void k_onesweep(Src src, K* __restrict__ kou
       const K k = s_keys[i];
       const uint32_t d = (uint32_t)(k >> shift) & (RADIX - 1);
       gpos[j] = s_goff[d] + i - s_start[d];
-      kout[gpos[j]] = k;
+      kout[gpos[j]] = (KO)k;
     }
   }
   if constexpr (HAS_V) {

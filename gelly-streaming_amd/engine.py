@@ -58,12 +58,13 @@ class StageTimes:
     payload_bytes: int
     partials: int
     fused_last: bool
+    path: int = 0          # 0: LSD sort + reduce-by-key; 1: bucket path (pass_ms = passes, accumulate, merge, emit)
 
 
 class Engine:
-    def __init__(self, device: int = 0, reserve_edges: int = 0, torch_stream: bool = True):
+    def __init__(self, device: int = 0, reserve_edges: int = 0, torch_stream: bool = True, sort_only: bool = False):
         self._L = L.load()
-        cfg = L.GsConfig(device, 0, reserve_edges)
+        cfg = L.GsConfig(device, L.GS_FLAG_SORT_ONLY if sort_only else 0, reserve_edges)
         ctx = ctypes.c_void_p()
         st = self._L.gs_create(ctypes.byref(cfg), ctypes.byref(ctx))
         if st != L.GS_OK:
@@ -112,9 +113,10 @@ class Engine:
     def stage_times(self) -> StageTimes:
         t = L.GsStageTimes()
         self._check(self._L.gs_last_stage_times(self.ctx, ctypes.byref(t)))
+        launched = t.sort_passes + (3 if t.path == 1 else 1 if t.fused_last else 0)
         return StageTimes(t.keyinfo_ms, t.sort_ms, t.reduce_ms, t.total_ms, t.sort_passes, t.key_bits, t.records,
-                          t.vertices, list(t.pass_ms)[:t.sort_passes], t.key_bytes, t.payload_bytes,
-                          t.partials, bool(t.fused_last))
+                          t.vertices, list(t.pass_ms)[:launched], t.key_bytes, t.payload_bytes,
+                          t.partials, bool(t.fused_last), t.path)
 
     # -- helpers ---------------------------------------------------------------------------------
     def _batch(self, src, dst, val):

@@ -79,9 +79,12 @@ typedef enum gs_mem { GS_MEM_HOST = 0, GS_MEM_DEVICE = 1 } gs_mem;
 
 typedef struct gs_ctx gs_ctx;
 
+/* gs_config.flags */
+#define GS_FLAG_SORT_ONLY 1u   /* reduce / fold: always take the full LSD sort + reduce-by-key path */
+
 typedef struct gs_config {
   int32_t device;          /* HIP device ordinal                                           */
-  uint32_t flags;          /* reserved, 0                                                  */
+  uint32_t flags;          /* GS_FLAG_* (0 = defaults)                                     */
   uint64_t reserve_edges;  /* pre-size the workspace for windows of this many edges (0 = lazy) */
 } gs_config;
 
@@ -222,7 +225,8 @@ typedef struct gs_stage_times {
   uint32_t key_bytes, payload_bytes;  /* sorted key / payload widths                          */
   uint64_t partials;       /* (vertex, partial) pairs left by the fused last pass               */
   uint32_t fused_last;     /* 1: pass_ms[sort_passes] is the last pass fused with the combine   */
-  uint32_t reserved;
+  uint32_t path;           /* 0: LSD sort + reduce-by-key; 1: bucket path (pass_ms[sort_passes..+2]
+                              = accumulate, merge, emit; partials = work items)                  */
 } gs_stage_times;
 GS_API gs_status gs_last_stage_times(const gs_ctx* ctx, gs_stage_times* out);
 

@@ -1,0 +1,166 @@
+"""GPU: the bucket path (gs_bucket.hpp) — reduceOnEdges / foldNeighbors built-ins through the high-bit
+partition + LDS accumulation — against the CPU oracle, at every pipeline shape it takes:
+
+  0 partition passes  (vertex range <= 2^S: one bucket, records read straight from the columns)
+  1 pass              (<= 2^(S+8) vertices), 2 passes (up to BK_MAXB = 2048 buckets)
+  multi-item buckets  (a bucket with more than 2^17 records: LDS slabs merged by k_bk_merge)
+  mispredicted base   (IDs far from 0 / negative: the info kernel reruns with base = min)
+  out of range        (vertex range > 2048 buckets: falls back to the LSD sort path, path 0)
+
+Integer results bit-exact; float sums within 1e-5 relative (north star)."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+FLOAT_RTOL = 1e-5
+
+
+def _dev(*arrs):
+    return [torch.from_numpy(np.ascontiguousarray(a)).cuda() for a in arrs]
+
+
+def _check(got_k, got_v, want_k, want_v, dtype, op):
+    assert np.array_equal(got_k.cpu().numpy(), want_k)
+    g = got_v.cpu().numpy()
+    if np.issubdtype(np.dtype(dtype), np.floating) and op == 0:
+        tol = FLOAT_RTOL * np.maximum(np.abs(want_v.astype(np.float64)), 1e-30)
+        assert not (np.abs(g.astype(np.float64) - want_v.astype(np.float64)) > tol).any()
+    else:
+        assert np.array_equal(g.view(np.uint8), want_v.view(np.uint8))
+
+
+def _window(rng, n, span, offset=0, hub_frac=0.0):
+    s = rng.integers(0, span, n).astype(np.int64) + offset
+    d = rng.integers(0, span, n).astype(np.int64) + offset
+    if hub_frac:
+        hub = rng.random(n) < hub_frac
+        s[hub] = offset + span // 3
+    return s, d
+
+
+# spans per accumulator width: S = 14 (8-byte), 15 (4-byte / count), 13 (degree)
+SPANS = {"one_bucket": 1 << 13, "one_pass": 1 << 19, "two_passes": 1 << 24}
+
+
+@pytest.mark.parametrize("shape", list(SPANS))
+@pytest.mark.parametrize("direction", [0, 1, 2])
+@pytest.mark.parametrize("dtype,op", [(np.int64, 0), (np.int64, 1), (np.int64, 2), (np.int32, 0), (np.int32, 1),
+                                      (np.int32, 2), (np.float64, 0), (np.float32, 0), (np.int64, 3)])
+def test_bucket_reduce_shapes(engine, oracle, shape, direction, dtype, op):
+    rng = np.random.default_rng(hash((shape, direction, op)) & 0xFFFF)
+    n = 60000
+    s, d = _window(rng, n, SPANS[shape])
+    v = oracle.gen_values(n, 11 + op, oracle.DT_OF_NP[np.dtype(dtype)])
+    rk, rv = oracle.window_reduce(s, d, v, direction, op)
+    gk, gv = engine.reduce(*_dev(s, d, v), direction, op)
+    assert engine.stage_times().path == 1
+    _check(gk, gv, rk, rv, dtype, op)
+
+
+def test_bucket_pass_counts(engine, oracle):
+    """The pipeline shape follows the vertex range (S = 14 for Long sums)."""
+    rng = np.random.default_rng(5)
+    for span, passes in ((1 << 14, 0), (1 << 18, 1), (1 << 22, 1), (1 << 23, 2), (1 << 25, 2)):
+        s, d = _window(rng, 20000, span)
+        s[0], d[0] = 0, span - 1
+        v = oracle.gen_values(20000, 1, oracle.DT_I64)
+        rk, rv = oracle.window_reduce(s, d, v, 2, 0)
+        gk, gv = engine.reduce(*_dev(s, d, v), 2, 0)
+        t = engine.stage_times()
+        assert (t.path, t.sort_passes) == (1, passes), span
+        _check(gk, gv, rk, rv, np.int64, 0)
+
+
+@pytest.mark.parametrize("op", [0, 1, 2, 3])
+def test_bucket_multi_item_hub(engine, oracle, op):
+    """A hub with 400k records in one bucket: several work items, LDS slabs merged in k_bk_merge."""
+    rng = np.random.default_rng(21 + op)
+    n = 700_000
+    s, d = _window(rng, n, 1 << 20, hub_frac=0.6)
+    v = oracle.gen_values(n, 3, oracle.DT_I64)
+    for direction in (1, 2):
+        rk, rv = oracle.window_reduce(s, d, v, direction, op)
+        gk, gv = engine.reduce(*_dev(s, d, v), direction, op)
+        t = engine.stage_times()
+        buckets = (1 << 20) >> (15 if op == 3 else 14)
+        assert t.path == 1 and t.partials > buckets      # the hub's bucket took several items
+        _check(gk, gv, rk, rv, np.int64, op)
+
+
+@pytest.mark.parametrize("offset", [-(1 << 40), -5000, 123_456_789_012, (1 << 62)])
+def test_bucket_base_prediction(engine, oracle, offset):
+    """IDs away from 0 (and a window after one at another offset): the predicted base misses, the info
+    kernel reruns with base = min, results stay exact; the next window at the same offset hits."""
+    rng = np.random.default_rng(abs(offset) % 1000)
+    for span in (1 << 12, 1 << 20, 1 << 20):
+        s, d = _window(rng, 40000, span, offset)
+        v = oracle.gen_values(40000, 9, oracle.DT_I64)
+        rk, rv = oracle.window_reduce(s, d, v, 2, 0)
+        gk, gv = engine.reduce(*_dev(s, d, v), 2, 0)
+        assert engine.stage_times().path == 1
+        _check(gk, gv, rk, rv, np.int64, 0)
+
+
+def test_bucket_out_of_range_falls_back(engine, oracle):
+    rng = np.random.default_rng(3)
+    s, d = _window(rng, 30000, 1 << 30)
+    v = oracle.gen_values(30000, 2, oracle.DT_I64)
+    rk, rv = oracle.window_reduce(s, d, v, 1, 0)
+    gk, gv = engine.reduce(*_dev(s, d, v), 1, 0)
+    assert engine.stage_times().path == 0
+    _check(gk, gv, rk, rv, np.int64, 0)
+
+
+@pytest.mark.parametrize("dtype,op,init", [(np.int64, 0, -77), (np.int64, 1, 5), (np.int64, 2, 40000),
+                                           (np.int32, 0, 2**31 - 5), (np.float64, 0, 0.25), (np.int64, 3, 1000)])
+def test_bucket_fold_init(engine, oracle, dtype, op, init):
+    rng = np.random.default_rng(op + 100)
+    n = 50000
+    s, d = _window(rng, n, 1 << 21)
+    v = oracle.gen_values(n, 4, oracle.DT_OF_NP[np.dtype(dtype)])
+    rk, rv = oracle.window_fold(s, d, v, 0, op, init)
+    gk, gv = engine.fold(*_dev(s, d, v), 0, op, init)
+    assert engine.stage_times().path == 1
+    _check(gk, gv, rk, rv, dtype, op)
+
+
+@pytest.mark.parametrize("span", [1 << 10, 1 << 17, 1 << 24])
+def test_bucket_degree_max(engine, oracle, span):
+    rng = np.random.default_rng(span % 97)
+    s, d = _window(rng, 80000, span, hub_frac=0.3)
+    for direction in (0, 1, 2):
+        for init_max in (np.iinfo(np.int64).min, span // 2):
+            rk, rd, rm = oracle.window_fold_degree_max(s, d, direction, init_max)
+            gk, gd, gm = engine.fold_degree_max(*_dev(s, d), direction, init_max)
+            assert engine.stage_times().path == 1
+            assert np.array_equal(gk.cpu().numpy(), rk)
+            assert np.array_equal(gd.cpu().numpy(), rd) and np.array_equal(gm.cpu().numpy(), rm)
+
+
+def test_sort_only_engine_matches(pkg, oracle):
+    """GS_FLAG_SORT_ONLY: the same window through the LSD sort path gives the same integer results."""
+    rng = np.random.default_rng(8)
+    s, d = _window(rng, 100000, 1 << 22, hub_frac=0.1)
+    v = oracle.gen_values(100000, 6, oracle.DT_I64)
+    with pkg.Engine(0) as eb, pkg.Engine(0, sort_only=True) as es:
+        kb, vb = eb.reduce(*_dev(s, d, v), 2, 0)
+        assert eb.stage_times().path == 1
+        ks, vs = es.reduce(*_dev(s, d, v), 2, 0)
+        assert es.stage_times().path == 0
+        assert torch.equal(kb, ks) and torch.equal(vb, vs)
+
+
+def test_bucket_large_rmat_properties(engine):
+    """R-MAT scale 22 (4M vertices, 64M edges): sum of per-vertex sums == sum of values, counts sum
+    to the records, keys strictly ascending — size-independent checks at a size the oracle skips."""
+    n = 1 << 26
+    s, d = engine.generate_rmat(22, n, 77)
+    v = engine.generate_values(n, 78, 1)
+    k, x = engine.reduce(s, d, v, 2, 0)
+    assert engine.stage_times().path == 1
+    assert bool((k[1:] > k[:-1]).all())
+    assert int(x.sum()) == 2 * int(v.sum())
+    k2, c = engine.reduce(s, d, v, 2, 3)
+    assert torch.equal(k, k2) and int(c.sum()) == 2 * n
