@@ -45,6 +45,8 @@ def parse():
     p.add_argument("--cpu-sample-log2", type=int, default=25)
     p.add_argument("--sort-only", action="store_true",
                    help="ablation: reduce / fold through the full LSD sort + reduce-by-key path")
+    p.add_argument("--bk-onesweep", action="store_true",
+                   help="ablation: bucket path partitions with 1-2 LSD passes instead of the direct scatter")
     p.add_argument("--check", action="store_true", help="verify sum(per-vertex sums) == sum(values) after timing")
     p.add_argument("--workload", default="reduce", choices=["reduce", "fold", "triangles"],
                    help="reduce = C2 (default, the headline); fold = C3 degree/max on skewed R-MAT; "
@@ -56,6 +58,8 @@ def kernel_table(times_list, E, U_avg):
     """Average per-launch durations (device events inside the library, same stream) and the algorithmic
     bytes each kernel must move ("Kernels and their rooflines")."""
     t0 = times_list[0]
+    if t0.path == 2:
+        return direct_kernel_table(times_list, E, U_avg)
     if t0.path == 1:
         return bucket_kernel_table(times_list, E, U_avg)
     kb, vb = t0.key_bytes, t0.payload_bytes
@@ -102,6 +106,26 @@ def bucket_kernel_table(times_list, E, U_avg):
     rows["bucket_merge"] = {"ms": mean(lambda t: t.pass_ms[passes + 1]), "bytes": 0}
     rows["bucket_emit"] = {"ms": mean(lambda t: t.pass_ms[passes + 2]), "bytes": U_avg * (4 + ab + 16)}
     rows["keyinfo(+host sync)"] = {"ms": mean(lambda t: t.keyinfo_ms), "bytes": E * 8}
+    for r in rows.values():
+        r["GB/s"] = r["bytes"] / (r["ms"] * 1e-3) / 1e9 if r["ms"] > 0 else 0.0
+        r["frac"] = r["GB/s"] / HBM_PEAK_GBS
+    return rows, mean(lambda t: t.partials)
+
+
+def direct_kernel_table(times_list, E, U_avg):
+    """Direct bucket path (gs_bucket.hpp k_dp_*): per-tile histogram, offset scans, ONE scatter, LDS
+    accumulate, merge, emit.  Algorithmic bytes per launch as in DESIGN.md §4 (E = records)."""
+    t0 = times_list[0]
+    vb = t0.payload_bytes
+    ab = 8 if vb else 4          # staged accumulator (i64 sum / u32 count)
+    mean = lambda f: statistics.mean(f(t) for t in times_list)
+    rows = {}
+    rows["dp_scatter"] = {"ms": mean(lambda t: t.pass_ms[1]), "bytes": E * ((8 + vb) + (2 + vb))}
+    rows["bucket_accumulate"] = {"ms": mean(lambda t: t.pass_ms[2]), "bytes": E * (2 + vb) + U_avg * (4 + ab)}
+    rows["bucket_merge"] = {"ms": mean(lambda t: t.pass_ms[3]), "bytes": 0}
+    rows["bucket_emit"] = {"ms": mean(lambda t: t.pass_ms[4]), "bytes": U_avg * (4 + ab + 16)}
+    rows["dp_offsets(up+spine+plan+down)"] = {"ms": mean(lambda t: t.pass_ms[0]), "bytes": 0}
+    rows["dp_hist(+host sync)"] = {"ms": mean(lambda t: t.keyinfo_ms), "bytes": E * 8}
     for r in rows.values():
         r["GB/s"] = r["bytes"] / (r["ms"] * 1e-3) / 1e9 if r["ms"] > 0 else 0.0
         r["frac"] = r["GB/s"] / HBM_PEAK_GBS
@@ -162,7 +186,7 @@ def main():
     from importlib import import_module
     D = import_module("gelly_streaming_amd.distributed")
 
-    eng = pkg.Engine(local, sort_only=a.sort_only)
+    eng = pkg.Engine(local, sort_only=a.sort_only, bk_onesweep=a.bk_onesweep)
     E = a.edge_factor << a.scale
     if a.workload == "fold":      # C3: skewed R-MAT (.65/.15/.15/.05), no permutation -> hubs at low IDs
         src, dst = eng.generate_rmat(a.scale, E, 0x5EED03, a=0.65, b=0.15, c=0.15, permute=False,
@@ -244,7 +268,7 @@ def main():
         kt = {"window_triangles": {"ms": elapsed / a.steps * 1e3, "bytes": E * 16, "GB/s": 0.0, "frac": 0.0}}
         kt["window_triangles"]["GB/s"] = kt["window_triangles"]["bytes"] / (kt["window_triangles"]["ms"] * 1e-3) / 1e9
         kt["window_triangles"]["frac"] = kt["window_triangles"]["GB/s"] / HBM_PEAK_GBS
-    dom_name = max((n for n in kt if not n.startswith("keyinfo")), key=lambda n: kt[n]["ms"])
+    dom_name = max((n for n in kt if "host sync" not in n), key=lambda n: kt[n]["ms"])
     dom = kt[dom_name]
     roofline = {"bound": "hbm", "kernel": dom_name, "achieved": round(dom["GB/s"], 1), "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": round(dom["frac"], 4), "traffic": pmc_traffic(dom_name),
@@ -275,7 +299,7 @@ def main():
                        "scale": a.scale, "edges_per_window_per_gpu": E, "direction": "OUT", "op": "SUM",
                        "value_dtype": a.dtype, "vertices_out": U_avg, "sort_passes": times[0].sort_passes,
                        "key_bits": times[0].key_bits, "partials_after_fused_pass": int(partials),
-                       "pipeline": "bucket" if times[0].path == 1 else "sort",
+                       "pipeline": {0: "sort", 1: "bucket-onesweep", 2: "bucket-direct"}[times[0].path],
                        "parallelism": (f"vertex-range keyBy over {world} GPU(s), RCCL all-to-all" if dist
                                        else "1 GPU")},
             "roofline": roofline,

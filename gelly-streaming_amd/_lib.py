@@ -39,6 +39,7 @@ u64, i64, i32, u32 = ctypes.c_uint64, ctypes.c_int64, ctypes.c_int32, ctypes.c_u
 
 
 GS_FLAG_SORT_ONLY = 1   # include/gelly_hip.h: reduce / fold always take the LSD sort path
+GS_FLAG_BK_ONESWEEP = 2   # bucket path: 1-2 LSD partition passes instead of the direct scatter (A/B)
 
 
 class GsConfig(ctypes.Structure):

@@ -5,6 +5,12 @@
 // 2^S vertices (S = 13..15 by accumulator size: 2^24..2^26 vertices) and the op has an LDS
 // atomic: integer SUM / MIN / MAX, float SUM, COUNT, the degree / max-neighbour fold.  Anything
 // else returns GS_EUNSUPPORTED and the caller sorts (gs_engine.hip).
+//
+// Two partition front ends feed the same LDS accumulation:
+//   direct  (default, stage_times.path = 2): per-tile bucket histograms, an offset table and ONE
+//           scatter pass (k_dp_*);
+//   onesweep (GS_FLAG_BK_ONESWEEP, path = 1): 1-2 stable LSD passes of 4-6-bit digits over the
+//           bucket index (k_onesweep with a global digit histogram), kept as the A/B baseline.
 #include <algorithm>
 
 #include "gs_bucket.hpp"
@@ -34,6 +40,14 @@ struct BkGeom {
   int passes = 0, w = 0;
 };
 
+int64_t key_min(const uint64_t* h) { return (int64_t)(~h[0] ^ (1ull << 63)); }
+int64_t key_max(const uint64_t* h) { return (int64_t)(h[1] ^ (1ull << 63)); }
+
+// base for the next window: 0 when the IDs are small non-negative numbers, else the window's minimum
+int64_t predict_base(int64_t kmin, int64_t kmax, int S) {
+  return (kmin >= 0 && ((uint64_t)kmax >> S) < (uint64_t)BK_MAXB) ? 0 : kmin;
+}
+
 template <int DIR>
 gs_status launch_info(gs_ctx* c, const int64_t* src, const int64_t* dst, uint64_t n, int64_t base, int S) {
   char* sm = c->small.as<char>();
@@ -49,6 +63,24 @@ gs_status launch_info(gs_ctx* c, const int64_t* src, const int64_t* dst, uint64_
     hipLaunchKernelGGL((k_bk_info<DIR, false>), dim3(grid), dim3(BK_INFO_BLOCK), 0, c->stream, src, dst, n, base, S,
                        (uint32_t)BK_MAXB, hist, (unsigned long long*)(sm + SM_BK_MM));
   return hip_check(c, hipGetLastError(), "k_bk_info");
+}
+
+template <int DIR>
+gs_status launch_dp_hist(gs_ctx* c, const int64_t* src, const int64_t* dst, uint64_t n, uint32_t nt, int64_t base,
+                         int S, uint32_t nbp) {
+  char* sm = c->small.as<char>();
+  auto* mm = (unsigned long long*)(sm + SM_BK_MM);
+  GS_HIP(hipMemsetAsync(mm, 0, 32, c->stream));
+  const bool vec = ((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst)) & 15) == 0;
+  const unsigned grid = std::max<uint32_t>(1, std::min<uint32_t>(nt, DP_HIST_GRID));
+  uint16_t* cnt = c->dp_cnt.as<uint16_t>();
+  if (vec)
+    hipLaunchKernelGGL((k_dp_hist<DIR, true>), dim3(grid), dim3(DP_BLOCK), 0, c->stream, src, dst, n, nt, base, S, nbp,
+                       cnt, mm);
+  else
+    hipLaunchKernelGGL((k_dp_hist<DIR, false>), dim3(grid), dim3(DP_BLOCK), 0, c->stream, src, dst, n, nt, base, S,
+                       nbp, cnt, mm);
+  return hip_check(c, hipGetLastError(), "k_dp_hist");
 }
 
 // one partition pass: digit (key >> shift) & (2^DB - 1); K -> KO keys, payload V
@@ -88,58 +120,234 @@ void choose_passes(uint32_t nb, int* passes, int* w) {
   else { *passes = 2; *w = 6; }
 }
 
+// records per accumulation work item: about four items per CU, at least 2^14 records
+uint32_t item_records(gs_ctx* c, uint64_t R) {
+  const uint64_t per = R / (4 * (uint64_t)std::max(1, c->n_cu));
+  return (uint32_t)std::max<uint64_t>(BK_ITEM, std::min<uint64_t>(per, 1u << 20));
+}
+
+gs_status ensure_cu(gs_ctx* c) {
+  if (!c->n_cu) {
+    int cu = 0;
+    GS_HIP(hipDeviceGetAttribute(&cu, hipDeviceAttributeMultiprocessorCount, c->device));
+    c->n_cu = std::max(1, cu);
+  }
+  return GS_OK;
+}
+
+// k_bk_plan over meta[HIST] (bucket totals): bucket starts, work items, multi-item buckets
+template <class P>
+gs_status launch_plan(gs_ctx* c, uint64_t R, uint32_t nb, int passes, int w, uint32_t item_recs) {
+  char* sm = c->small.as<char>();
+  uint32_t* meta = c->bk_meta.as<uint32_t>();
+  const uint64_t max_items = R / item_recs + nb + 1;
+  const uint64_t max_slabs = 2 * (R / item_recs) + 2;
+  GS_TRY(ensure(c, c->bk_items, max_items * sizeof(BkItem)));
+  GS_TRY(ensure(c, c->bk_slabs, max_slabs * sizeof(typename P::Lds)));
+  uint32_t* ns = (uint32_t*)(sm + SM_BK_N);
+  BkPlanOut po{meta + BkMeta::DBASE, meta + BkMeta::BSTART, meta + BkMeta::BCOUNT, meta + BkMeta::BITEMS,
+               meta + BkMeta::BSLAB, meta + BkMeta::MLIST, c->bk_items.as<BkItem>(), ns + 0, ns + 1};
+  hipLaunchKernelGGL(k_bk_plan, dim3(1), dim3(BK_PLAN_BLOCK), 0, c->stream, meta + BkMeta::HIST, nb, passes, w,
+                     item_recs, po);
+  return hip_check(c, hipGetLastError(), "k_bk_plan");
+}
+
+// The back end both front ends share: LDS accumulation of the partitioned records (or of the
+// columns themselves when the window is one bucket), merge of multi-item buckets, emit; then the
+// host reads U.  Records pass_ev[ev0 + 1 .. ev0 + 3] after the three launches.
+template <class P, class Src>
+gs_status bucket_accumulate(gs_ctx* c, Src rs, uint64_t R, uint32_t nb, int64_t base, typename P::Out o, int ev0,
+                            uint64_t* U, uint32_t* n_items) {
+  char* sm = c->small.as<char>();
+  uint32_t* meta = c->bk_meta.as<uint32_t>();
+  uint32_t* ns = (uint32_t*)(sm + SM_BK_N);
+  GS_HIP(hipMemsetAsync(ns + 2, 0, 4, c->stream));
+  BkStage st{c->keysA.as<uint32_t>(), c->valsA.p, std::is_same_v<P, BkDeg> ? c->aux.as<int64_t>() : nullptr};
+  auto* slabs = c->bk_slabs.as<typename P::Lds>();
+  hipLaunchKernelGGL((k_bk_accum<P, Src, GS_BK_UNROLL>), dim3(c->n_cu), dim3(BK_ACC_BLOCK), 0, c->stream, rs,
+                     c->bk_items.as<BkItem>(), ns + 0, meta + BkMeta::BSTART, ns + 2, slabs, st, meta + BkMeta::BCOUNT);
+  GS_HIP(hipGetLastError());
+  hipEventRecord(c->pass_ev[ev0 + 1], c->stream);
+  const unsigned mgrid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(nb, R / BK_ITEM + 1));
+  hipLaunchKernelGGL((k_bk_merge<P>), dim3(mgrid), dim3(BK_ACC_BLOCK), 0, c->stream, meta + BkMeta::MLIST, ns + 1,
+                     meta + BkMeta::BITEMS, meta + BkMeta::BSLAB, meta + BkMeta::BSTART, slabs, st,
+                     meta + BkMeta::BCOUNT);
+  GS_HIP(hipGetLastError());
+  hipEventRecord(c->pass_ev[ev0 + 2], c->stream);
+  hipLaunchKernelGGL((k_bk_emit<P>), dim3(nb), dim3(256), 0, c->stream, meta + BkMeta::BSTART, meta + BkMeta::BCOUNT,
+                     nb, st, base, o, (unsigned long long*)(sm + SM_BK_MM + 24));
+  GS_HIP(hipGetLastError());
+  hipEventRecord(c->pass_ev[ev0 + 3], c->stream);
+  hipEventRecord(c->ev[3], c->stream);
+  GS_HIP(hipMemcpyAsync(c->host_small, sm + SM_BK_MM, 48, hipMemcpyDeviceToHost, c->stream));
+  GS_HIP(hipMemcpyAsync(c->host_small + 6, sm + SM_TIMEOUT, 8, hipMemcpyDeviceToHost, c->stream));
+  GS_HIP(hipStreamSynchronize(c->stream));
+  if ((uint32_t)c->host_small[6] != 0) return set_error(c, GS_EDEVICE, "look-back spin timed out");
+  *U = c->host_small[3];
+  *n_items = (uint32_t)c->host_small[4];
+  return GS_OK;
+}
+
+void bucket_times(gs_ctx* c, int path, int passes, int launches, uint32_t key_bits, uint64_t R, uint64_t U,
+                  size_t vb, uint32_t n_items) {
+  float a = 0, b = 0, d = 0;
+  hipEventElapsedTime(&a, c->ev[0], c->ev[1]);
+  hipEventElapsedTime(&b, c->ev[1], c->ev[2]);
+  hipEventElapsedTime(&d, c->ev[2], c->ev[3]);
+  gs_stage_times& t = c->times;
+  t = gs_stage_times{};
+  t.keyinfo_ms = a;
+  t.sort_ms = b;
+  t.reduce_ms = d;
+  t.total_ms = a + b + d;
+  t.sort_passes = (uint32_t)passes;
+  t.key_bits = key_bits;
+  t.records = R;
+  t.vertices = U;
+  for (int p = 0; p < launches && p < 8; ++p) hipEventElapsedTime(&t.pass_ms[p], c->pass_ev[p], c->pass_ev[p + 1]);
+  t.key_bytes = 2;
+  t.payload_bytes = (uint32_t)vb;
+  t.partials = n_items;
+  t.fused_last = 0;
+  t.path = (uint32_t)path;
+}
+
+template <class P>
+gs_status ensure_stage(gs_ctx* c, uint64_t R) {
+  constexpr size_t vb = P::HAS_V ? sizeof(typename P::Raw) : 0;
+  constexpr size_t ab = std::max(sizeof(typename P::A), vb);
+  GS_TRY(ensure(c, c->keysA, R * 4));
+  GS_TRY(ensure(c, c->keysB, R * 4));
+  GS_TRY(ensure(c, c->valsA, R * std::max<size_t>(ab, 4)));
+  if (P::HAS_V) GS_TRY(ensure(c, c->valsB, R * vb));
+  if (std::is_same_v<P, BkDeg>) GS_TRY(ensure(c, c->aux, R * 8));
+  return GS_OK;
+}
+
+// ---- direct front end: hist -> offsets -> one scatter -------------------------------------------------
+// Events: ev[1] after the histogram (+ host read of the range); pass_ev[0..2] around the offset
+// scans and the scatter; then accumulate / merge / emit.
 template <class P, int DIR>
-gs_status bucket_run(gs_ctx* c, const int64_t* src, const int64_t* dst, const void* val, uint64_t n,
-                     typename P::Out o, uint64_t* U) {
+gs_status bucket_direct(gs_ctx* c, const int64_t* src, const int64_t* dst, const void* val, uint64_t n,
+                        typename P::Out o, uint64_t* U) {
+  using Raw = typename P::Raw;
+  constexpr int S = P::S;
+  char* sm = c->small.as<char>();
+  const uint64_t R = (DIR == DIR_ALL) ? 2 * n : n;
+  GS_TRY(ensure(c, c->bk_meta, BkMeta::TOTAL * 4, true));
+  GS_TRY(ensure_cu(c));
+  uint32_t* meta = c->bk_meta.as<uint32_t>();
+  constexpr uint32_t TE = dp_tile_edges<DIR>();
+  const uint32_t nt = (uint32_t)((n + TE - 1) / TE);
+  const uint32_t nch = (nt + DP_CHUNK - 1) / DP_CHUNK;
+
+  // 1. per-tile bucket counts against the predicted base and width: the window's one read of the
+  //    keys before the scatter; a key outside the prediction makes it count again with the range
+  int64_t base = c->bk_base;
+  uint32_t nb = c->bk_nbp ? c->bk_nbp : (uint32_t)BK_MAXB;
+  GS_TRY(ensure(c, c->dp_cnt, (size_t)nt * BK_MAXB * 2));
+  GS_TRY(launch_dp_hist<DIR>(c, src, dst, n, nt, base, S, nb));
+  GS_HIP(hipMemcpyAsync(c->host_small, sm + SM_BK_MM, 24, hipMemcpyDeviceToHost, c->stream));
+  GS_HIP(hipStreamSynchronize(c->stream));
+  const int64_t kmin = key_min(c->host_small), kmax = key_max(c->host_small);
+  if ((((uint64_t)kmax - (uint64_t)kmin) >> S) >= (uint64_t)BK_MAXB) return GS_EUNSUPPORTED;
+  if (c->host_small[2]) {
+    base = predict_base(kmin, kmax, S);
+    nb = (uint32_t)((((uint64_t)kmax - (uint64_t)base) >> S) + 1);
+    GS_TRY(launch_dp_hist<DIR>(c, src, dst, n, nt, base, S, nb));
+  }
+  {   // the next window predicts this base and this width rounded up to a power of two
+    const uint32_t need = (uint32_t)((((uint64_t)kmax - (uint64_t)base) >> S) + 1);
+    uint32_t p2 = 1;
+    while (p2 < need) p2 <<= 1;
+    c->bk_base = base;
+    c->bk_nbp = std::min<uint32_t>(p2, BK_MAXB);
+  }
+  hipEventRecord(c->ev[1], c->stream);
+  hipEventRecord(c->pass_ev[0], c->stream);
+
+  // 2. offsets: chunk counts, per-bucket spine (-> meta[HIST] totals), plan, per-tile offsets
+  const bool part = nb > 1;
+  const uint32_t item_recs = item_records(c, R);
+  GS_TRY(ensure(c, c->dp_csum, (size_t)nch * nb * 4));
+  uint16_t* cnt = c->dp_cnt.as<uint16_t>();
+  uint32_t* csum = c->dp_csum.as<uint32_t>();
+  const dim3 g2((nb + 255) / 256, nch);
+  hipLaunchKernelGGL(k_dp_up, g2, dim3(256), 0, c->stream, cnt, nt, nb, csum);
+  hipLaunchKernelGGL(k_dp_spine, dim3((nb + 63) / 64), dim3(1024), 0, c->stream, csum, nch, nb, meta + BkMeta::HIST);
+  GS_HIP(hipGetLastError());
+  GS_TRY(launch_plan<P>(c, R, nb, 0, 0, item_recs));
+  if (part) {
+    GS_TRY(ensure(c, c->dp_off, (size_t)nt * nb * 4));
+    hipLaunchKernelGGL(k_dp_down, g2, dim3(256), 0, c->stream, cnt, csum, meta + BkMeta::BSTART, nt, nb,
+                       c->dp_off.as<uint32_t>());
+    GS_HIP(hipGetLastError());
+  }
+  hipEventRecord(c->pass_ev[1], c->stream);
+
+  // 3. the scatter: (16-bit bucket-local index, payload) in bucket order
+  GS_TRY(ensure_stage<P>(c, R));
+  using ESrc = BaseSrc<Raw, DIR, P::PAY>;
+  const ESrc es{src, dst, (const Raw*)val, base};
+  uint16_t* k16 = c->keysB.as<uint16_t>();
+  Raw* vpart = P::HAS_V ? c->valsB.as<Raw>() : nullptr;
+  if (part) {
+    const uint32_t per = (nt + 7) / 8;
+    hipLaunchKernelGGL((k_dp_scatter<Raw, DIR, P::PAY>), dim3(per * 8), dim3(DP_BLOCK), 0, c->stream, es, n, S, nb,
+                       nt, c->dp_off.as<uint32_t>(), k16, vpart);
+    GS_HIP(hipGetLastError());
+  }
+  hipEventRecord(c->pass_ev[2], c->stream);
+  hipEventRecord(c->ev[2], c->stream);
+
+  // 4-6. accumulate, merge, emit
+  uint32_t n_items = 0;
+  if (part)
+    GS_TRY((bucket_accumulate<P>(c, PartSrc<Raw>{k16, vpart}, R, nb, base, o, 2, U, &n_items)));
+  else
+    GS_TRY((bucket_accumulate<P>(c, es, R, nb, base, o, 2, U, &n_items)));
+  const uint32_t key_bits = nb <= 1 ? (uint32_t)S : (uint32_t)(S + 32 - __builtin_clz(nb - 1));
+  bucket_times(c, 2, part ? 1 : 0, 5, key_bits, R, *U, P::HAS_V ? sizeof(Raw) : 0, n_items);
+  return GS_OK;
+}
+
+// ---- onesweep front end (GS_FLAG_BK_ONESWEEP): global histogram -> 1-2 stable LSD passes ----------
+template <class P, int DIR>
+gs_status bucket_onesweep(gs_ctx* c, const int64_t* src, const int64_t* dst, const void* val, uint64_t n,
+                          typename P::Out o, uint64_t* U) {
   using Raw = typename P::Raw;
   constexpr bool HAS_V = P::HAS_V;
   constexpr int S = P::S;
   char* sm = c->small.as<char>();
   const uint64_t R = (DIR == DIR_ALL) ? 2 * n : n;
   GS_TRY(ensure(c, c->bk_meta, BkMeta::TOTAL * 4, true));
-  uint32_t* meta = c->bk_meta.as<uint32_t>();
+  GS_TRY(ensure_cu(c));
 
   // 1. vertex range + bucket histogram against the predicted base
   int64_t base = c->bk_base;
   GS_TRY(launch_info<DIR>(c, src, dst, n, base, S));
   GS_HIP(hipMemcpyAsync(c->host_small, sm + SM_BK_MM, 24, hipMemcpyDeviceToHost, c->stream));
   GS_HIP(hipStreamSynchronize(c->stream));
-  const int64_t kmin = (int64_t)(~c->host_small[0] ^ (1ull << 63));
-  const int64_t kmax = (int64_t)(c->host_small[1] ^ (1ull << 63));
-  const uint64_t outside = c->host_small[2];
+  const int64_t kmin = key_min(c->host_small), kmax = key_max(c->host_small);
   if ((((uint64_t)kmax - (uint64_t)kmin) >> S) >= (uint64_t)BK_MAXB) return GS_EUNSUPPORTED;
-  if (outside) {
+  if (c->host_small[2]) {
     base = kmin;
     GS_TRY(launch_info<DIR>(c, src, dst, n, base, S));
   }
-  c->bk_base = (kmin >= 0 && ((uint64_t)kmax >> S) < (uint64_t)BK_MAXB) ? 0 : kmin;
+  c->bk_base = predict_base(kmin, kmax, S);
   BkGeom g;
   g.base = base;
   g.nb = (uint32_t)((((uint64_t)kmax - (uint64_t)base) >> S) + 1);
   choose_passes(g.nb, &g.passes, &g.w);
 
   // 2. plan
-  const uint64_t max_items = R / BK_ITEM + g.nb + 1;
-  const uint64_t max_slabs = 2 * (R / BK_ITEM) + 2;
-  GS_TRY(ensure(c, c->bk_items, max_items * sizeof(BkItem)));
-  GS_TRY(ensure(c, c->bk_slabs, max_slabs * sizeof(typename P::Lds)));
-  uint32_t* ns = (uint32_t*)(sm + SM_BK_N);
-  BkPlanOut po{meta + BkMeta::DBASE, meta + BkMeta::BSTART, meta + BkMeta::BCOUNT, meta + BkMeta::BITEMS,
-               meta + BkMeta::BSLAB, meta + BkMeta::MLIST, c->bk_items.as<BkItem>(), ns + 0, ns + 1};
-  hipLaunchKernelGGL(k_bk_plan, dim3(1), dim3(BK_PLAN_BLOCK), 0, c->stream, meta + BkMeta::HIST, g.nb, g.passes, g.w,
-                     BK_ITEM, po);
-  GS_HIP(hipGetLastError());
+  const uint32_t item_recs = item_records(c, R);
+  GS_TRY(launch_plan<P>(c, R, g.nb, g.passes, g.w, item_recs));
   hipEventRecord(c->ev[1], c->stream);
   hipEventRecord(c->pass_ev[0], c->stream);
 
   // 3. partition passes over the bucket index; the last stores the 16-bit bucket-local index
-  const size_t vb = HAS_V ? sizeof(Raw) : 0;
-  const size_t ab = std::max(sizeof(typename P::A), vb);
-  GS_TRY(ensure(c, c->keysA, R * 4));
-  GS_TRY(ensure(c, c->keysB, R * 4));
-  GS_TRY(ensure(c, c->valsA, R * std::max<size_t>(ab, 4)));
-  if (HAS_V) GS_TRY(ensure(c, c->valsB, R * vb));
-  if (std::is_same_v<P, BkDeg>) GS_TRY(ensure(c, c->aux, R * 8));
+  GS_TRY(ensure_stage<P>(c, R));
   const uint32_t tiles = (uint32_t)((R + SORT_TILE - 1) / SORT_TILE);
   GS_TRY(ensure(c, c->sort_status, (size_t)tiles * 256 * 8, true));
   using ESrc = BaseSrc<Raw, DIR, P::PAY>;
@@ -160,76 +368,30 @@ gs_status bucket_run(gs_ctx* c, const int64_t* src, const int64_t* dst, const vo
   }
   hipEventRecord(c->ev[2], c->stream);
 
-  // 4. LDS accumulation (persistent), 5. merge of multi-item buckets, 6. emit
-  if (!c->n_cu) {
-    int cu = 0;
-    GS_HIP(hipDeviceGetAttribute(&cu, hipDeviceAttributeMultiprocessorCount, c->device));
-    c->n_cu = std::max(1, cu);
-  }
-  GS_HIP(hipMemsetAsync(ns + 2, 0, 4, c->stream));
-  BkStage st{c->keysA.as<uint32_t>(), c->valsA.p, std::is_same_v<P, BkDeg> ? c->aux.as<int64_t>() : nullptr};
-  auto* slabs = c->bk_slabs.as<typename P::Lds>();
-  if (g.passes == 0) {
-    hipLaunchKernelGGL((k_bk_accum<P, ESrc, GS_BK_UNROLL>), dim3(c->n_cu), dim3(BK_ACC_BLOCK), 0, c->stream, es,
-                       c->bk_items.as<BkItem>(), ns + 0, meta + BkMeta::BSTART, ns + 2, slabs, st,
-                       meta + BkMeta::BCOUNT);
-  } else {
-    const PartSrc<Raw> ps{k16, vpart};
-    hipLaunchKernelGGL((k_bk_accum<P, PartSrc<Raw>, GS_BK_UNROLL>), dim3(c->n_cu), dim3(BK_ACC_BLOCK), 0, c->stream,
-                       ps, c->bk_items.as<BkItem>(), ns + 0, meta + BkMeta::BSTART, ns + 2, slabs, st,
-                       meta + BkMeta::BCOUNT);
-  }
-  GS_HIP(hipGetLastError());
-  hipEventRecord(c->pass_ev[g.passes + 1], c->stream);
-  const unsigned mgrid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(g.nb, R / BK_ITEM + 1));
-  hipLaunchKernelGGL((k_bk_merge<P>), dim3(mgrid), dim3(BK_ACC_BLOCK), 0, c->stream, meta + BkMeta::MLIST, ns + 1,
-                     meta + BkMeta::BITEMS, meta + BkMeta::BSLAB, meta + BkMeta::BSTART, slabs, st,
-                     meta + BkMeta::BCOUNT);
-  GS_HIP(hipGetLastError());
-  hipEventRecord(c->pass_ev[g.passes + 2], c->stream);
-  hipLaunchKernelGGL((k_bk_emit<P>), dim3(g.nb), dim3(256), 0, c->stream, meta + BkMeta::BSTART, meta + BkMeta::BCOUNT,
-                     g.nb, st, base, o, (unsigned long long*)(sm + SM_BK_MM + 24));
-  GS_HIP(hipGetLastError());
-  hipEventRecord(c->pass_ev[g.passes + 3], c->stream);
-  hipEventRecord(c->ev[3], c->stream);
-  GS_HIP(hipMemcpyAsync(c->host_small, sm + SM_BK_MM, 48, hipMemcpyDeviceToHost, c->stream));
-  GS_HIP(hipMemcpyAsync(c->host_small + 6, sm + SM_TIMEOUT, 8, hipMemcpyDeviceToHost, c->stream));
-  GS_HIP(hipStreamSynchronize(c->stream));
-  if ((uint32_t)c->host_small[6] != 0) return set_error(c, GS_EDEVICE, "look-back spin timed out");
-  *U = c->host_small[3];
-  const uint32_t n_items = (uint32_t)c->host_small[4];
-
-  // stage times
-  float a = 0, b = 0, d = 0;
-  hipEventElapsedTime(&a, c->ev[0], c->ev[1]);
-  hipEventElapsedTime(&b, c->ev[1], c->ev[2]);
-  hipEventElapsedTime(&d, c->ev[2], c->ev[3]);
-  gs_stage_times& t = c->times;
-  t = gs_stage_times{};
-  t.keyinfo_ms = a;
-  t.sort_ms = b;
-  t.reduce_ms = d;
-  t.total_ms = a + b + d;
-  t.sort_passes = (uint32_t)g.passes;
-  t.key_bits = g.nb <= 1 ? (uint32_t)S : (uint32_t)(S + 32 - __builtin_clz(g.nb - 1));
-  t.records = R;
-  t.vertices = *U;
-  for (int p = 0; p < g.passes + 3 && p < 8; ++p) hipEventElapsedTime(&t.pass_ms[p], c->pass_ev[p], c->pass_ev[p + 1]);
-  t.key_bytes = 2;
-  t.payload_bytes = (uint32_t)vb;
-  t.partials = n_items;
-  t.fused_last = 0;
-  t.path = 1;
+  // 4-6. accumulate, merge, emit
+  uint32_t n_items = 0;
+  if (g.passes == 0)
+    GS_TRY((bucket_accumulate<P>(c, es, R, g.nb, base, o, g.passes, U, &n_items)));
+  else
+    GS_TRY((bucket_accumulate<P>(c, PartSrc<Raw>{k16, vpart}, R, g.nb, base, o, g.passes, U, &n_items)));
+  const uint32_t key_bits = g.nb <= 1 ? (uint32_t)S : (uint32_t)(S + 32 - __builtin_clz(g.nb - 1));
+  bucket_times(c, 1, g.passes, g.passes + 3, key_bits, R, *U, HAS_V ? sizeof(Raw) : 0, n_items);
   return GS_OK;
 }
 
 template <class P>
 gs_status bucket_dir(gs_ctx* c, int dir, const int64_t* src, const int64_t* dst, const void* val, uint64_t n,
                      typename P::Out o, uint64_t* U) {
+  const bool os = c->flags & GS_FLAG_BK_ONESWEEP;
   switch (dir) {
-    case DIR_IN: return bucket_run<P, DIR_IN>(c, src, dst, val, n, o, U);
-    case DIR_OUT: return bucket_run<P, DIR_OUT>(c, src, dst, val, n, o, U);
-    case DIR_ALL: return bucket_run<P, DIR_ALL>(c, src, dst, val, n, o, U);
+    case DIR_IN:
+      return os ? bucket_onesweep<P, DIR_IN>(c, src, dst, val, n, o, U) : bucket_direct<P, DIR_IN>(c, src, dst, val, n, o, U);
+    case DIR_OUT:
+      return os ? bucket_onesweep<P, DIR_OUT>(c, src, dst, val, n, o, U)
+                : bucket_direct<P, DIR_OUT>(c, src, dst, val, n, o, U);
+    case DIR_ALL:
+      return os ? bucket_onesweep<P, DIR_ALL>(c, src, dst, val, n, o, U)
+                : bucket_direct<P, DIR_ALL>(c, src, dst, val, n, o, U);
   }
   return set_error(c, GS_EINVAL, "bad direction %d", dir);
 }

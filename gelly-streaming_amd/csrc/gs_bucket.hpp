@@ -401,6 +401,241 @@ static __global__ __launch_bounds__(BK_PLAN_BLOCK) void k_bk_plan(const uint32_t
   }
 }
 
+// ---- direct partition: the whole bucket index in ONE scatter pass ----------------------------------
+// A tile is the records of dp_tile_edges<DIR>() consecutive edges (at most DP_TILE records, so a
+// per-bucket count fits u16).
+//   k_dp_hist     per-tile bucket counts cnt[t][b] (u16, row-contiguous) + vertex min / max;
+//   k_dp_up       per chunk of DP_CHUNK tiles and bucket: the chunk's count;
+//   k_dp_spine    per bucket: exclusive scan of the chunk counts over chunks, bucket totals;
+//   (k_bk_plan    bucket starts from the totals, work items)
+//   k_dp_down     every tile's absolute write offset per bucket: off[t][b] (u32);
+//   k_dp_scatter  ranks the tile's records by bucket in LDS (LDS atomics: the order inside a bucket
+//                 is free, the ops are associative and commutative) and writes each bucket's run of
+//                 (16-bit bucket-local index, payload) at off[t][b].
+// Against the 2-pass LSD partition (k_onesweep twice) this moves 8 + 26 B per 8-byte-payload record
+// instead of 8 + 28 + 22.
+constexpr int DP_BLOCK = 1024;
+constexpr int DP_ITEMS = 10;
+constexpr uint32_t DP_TILE = DP_BLOCK * DP_ITEMS;   // 10240 records < 2^16
+constexpr uint32_t DP_CHUNK = 64;                   // tiles per up / down-sweep chunk
+constexpr int DP_HIST_GRID = 2048;                  // k_dp_hist blocks (each loops over tiles)
+template <int DIR>
+__host__ __device__ constexpr uint32_t dp_tile_edges() { return DIR == DIR_ALL ? DP_TILE / 2 : DP_TILE; }
+
+template <int DIR, bool VEC>
+__global__ __launch_bounds__(DP_BLOCK) void k_dp_hist(const int64_t* __restrict__ src, const int64_t* __restrict__ dst,
+                                                      uint64_t n, uint32_t nt, int64_t base, int S, uint32_t nbp,
+                                                      uint16_t* __restrict__ cnt,
+                                                      unsigned long long* __restrict__ mm) {
+  __shared__ uint32_t h[BK_MAXB];
+  __shared__ unsigned long long s_mm[3][DP_BLOCK / WAVE];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  constexpr uint32_t TE = dp_tile_edges<DIR>();
+  uint64_t lo = 0, hi = 0;   // max of ~flip(key), max of flip(key)
+  uint32_t ovf = 0;
+  for (uint32_t t = blockIdx.x; t < nt; t += gridDim.x) {
+    for (uint32_t i = tid; i < nbp; i += DP_BLOCK) h[i] = 0;
+    __syncthreads();
+    auto add = [&](int64_t k) {
+      const uint64_t f = (uint64_t)k ^ (1ull << 63);
+      lo = max(lo, ~f);
+      hi = max(hi, f);
+      const uint64_t d = ((uint64_t)k - (uint64_t)base) >> S;
+      if (k < base || d >= nbp) ++ovf;
+      else atomicAdd(&h[d], 1u);
+    };
+    const uint64_t e0 = (uint64_t)t * TE, e1 = min(n, e0 + TE);
+    if constexpr (VEC) {   // 16-byte pairs; TE is even, so only the window's last edge can be unpaired
+      const longlong2* s2 = reinterpret_cast<const longlong2*>(src);
+      const longlong2* d2 = reinterpret_cast<const longlong2*>(dst);
+      const uint64_t q0 = e0 >> 1, q1 = e1 >> 1;
+      constexpr int U = (TE / 2 + DP_BLOCK - 1) / DP_BLOCK;
+      longlong2 a[U], b[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const uint64_t q = q0 + (uint64_t)u * DP_BLOCK + tid;
+        if (q < q1) {
+          if (DIR != DIR_IN) a[u] = s2[q];
+          if (DIR != DIR_OUT) b[u] = d2[q];
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if (q0 + (uint64_t)u * DP_BLOCK + tid < q1) {
+          if (DIR != DIR_IN) { add(a[u].x); add(a[u].y); }
+          if (DIR != DIR_OUT) { add(b[u].x); add(b[u].y); }
+        }
+      }
+      if ((e1 & 1) && tid == 0) {
+        if (DIR != DIR_IN) add(src[e1 - 1]);
+        if (DIR != DIR_OUT) add(dst[e1 - 1]);
+      }
+    } else {
+      for (uint64_t i = e0 + tid; i < e1; i += DP_BLOCK) {
+        if (DIR != DIR_IN) add(src[i]);
+        if (DIR != DIR_OUT) add(dst[i]);
+      }
+    }
+    __syncthreads();
+    uint16_t* row = cnt + (uint64_t)t * nbp;
+    for (uint32_t i = tid; i < nbp; i += DP_BLOCK) row[i] = (uint16_t)h[i];
+  }
+  // one atomic per block and word (thousands of blocks on three words would serialise)
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    lo = max(lo, (uint64_t)__shfl_xor((unsigned long long)lo, o, WAVE));
+    hi = max(hi, (uint64_t)__shfl_xor((unsigned long long)hi, o, WAVE));
+    ovf += __shfl_xor(ovf, o, WAVE);
+  }
+  if (lane == 0) {
+    s_mm[0][w] = lo;
+    s_mm[1][w] = hi;
+    s_mm[2][w] = ovf;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    unsigned long long a = 0, b = 0, o2 = 0;
+    for (int i = 0; i < DP_BLOCK / WAVE; ++i) {
+      a = max(a, s_mm[0][i]);
+      b = max(b, s_mm[1][i]);
+      o2 += s_mm[2][i];
+    }
+    atomicMax(&mm[0], a);
+    atomicMax(&mm[1], b);
+    if (o2) atomicAdd(&mm[2], o2);
+  }
+}
+
+// chunk counts: csum[c][b] = sum of cnt[t][b] over the chunk's tiles
+static __global__ __launch_bounds__(256) void k_dp_up(const uint16_t* __restrict__ cnt, uint32_t nt, uint32_t nbp,
+                                                      uint32_t* __restrict__ csum) {
+  const uint32_t b = blockIdx.x * 256 + threadIdx.x;
+  if (b >= nbp) return;
+  const uint32_t c = blockIdx.y, t0 = c * DP_CHUNK, t1 = min(nt, t0 + DP_CHUNK);
+  uint32_t s = 0;
+#pragma unroll 8
+  for (uint32_t t = t0; t < t1; ++t) s += cnt[(uint64_t)t * nbp + b];
+  csum[(uint64_t)c * nbp + b] = s;
+}
+
+// per bucket (one lane each, 64 per block): exclusive scan of csum over chunks, in place; totals
+static __global__ __launch_bounds__(1024) void k_dp_spine(uint32_t* __restrict__ csum, uint32_t nch, uint32_t nbp,
+                                                          uint32_t* __restrict__ total) {
+  __shared__ uint32_t s[16][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const uint32_t b = blockIdx.x * 64 + lane;
+  const uint32_t per = (nch + 15) / 16, c0 = min(nch, w * per), c1 = min(nch, c0 + per);
+  uint32_t sum = 0;
+  if (b < nbp) {
+#pragma unroll 8
+    for (uint32_t c = c0; c < c1; ++c) sum += csum[(uint64_t)c * nbp + b];
+  }
+  s[w][lane] = sum;
+  __syncthreads();
+  uint32_t run = 0, tot = 0;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const uint32_t v = s[i][lane];
+    run += i < w ? v : 0u;
+    tot += v;
+  }
+  if (b < nbp) {
+    for (uint32_t c = c0; c < c1; ++c) {
+      const uint32_t v = csum[(uint64_t)c * nbp + b];
+      csum[(uint64_t)c * nbp + b] = run;
+      run += v;
+    }
+    if (w == 0) total[b] = tot;
+  }
+}
+
+// off[t][b] = bucket_start[b] + (records of bucket b in tiles before t)
+static __global__ __launch_bounds__(256) void k_dp_down(const uint16_t* __restrict__ cnt,
+                                                        const uint32_t* __restrict__ csum,
+                                                        const uint32_t* __restrict__ bucket_start, uint32_t nt,
+                                                        uint32_t nbp, uint32_t* __restrict__ off) {
+  const uint32_t b = blockIdx.x * 256 + threadIdx.x;
+  if (b >= nbp) return;
+  const uint32_t c = blockIdx.y, t0 = c * DP_CHUNK, t1 = min(nt, t0 + DP_CHUNK);
+  uint32_t run = bucket_start[b] + csum[(uint64_t)c * nbp + b];
+  for (uint32_t t = t0; t < t1; ++t) {
+    const uint64_t i = (uint64_t)t * nbp + b;
+    const uint32_t k = cnt[i];
+    off[i] = run;
+    run += k;
+  }
+}
+
+// one tile per block; blocks b and b + 8 share an XCD under round-robin dispatch (speed only), so
+// each XCD takes a contiguous range of tiles and the adjacent runs of a bucket meet in one L2
+template <typename V, int DIR, int PAY>
+__global__ __launch_bounds__(DP_BLOCK) void k_dp_scatter(BaseSrc<V, DIR, PAY> es, uint64_t n, int S, uint32_t nbp,
+                                                         uint32_t nt, const uint32_t* __restrict__ off,
+                                                         uint16_t* __restrict__ k16, V* __restrict__ vout) {
+  constexpr bool HAS_V = PAY != PAY_NONE;
+  __shared__ uint32_t s_key[DP_TILE];                // (bucket << 16) | bucket-local index, bucket order
+  __shared__ V s_val[HAS_V ? DP_TILE : 1];
+  __shared__ uint32_t s_cnt[BK_MAXB];                // counts, then run starts inside the tile
+  __shared__ uint32_t s_delta[BK_MAXB];              // global position - tile position of bucket b's run
+  __shared__ uint32_t s_w[DP_BLOCK / WAVE];
+  const int tid = threadIdx.x;
+  const uint32_t per = (nt + 7) / 8;
+  const uint32_t t = (blockIdx.x & 7u) * per + (blockIdx.x >> 3);
+  if (t >= nt) return;
+  constexpr uint32_t TE = dp_tile_edges<DIR>();
+  const uint64_t e0 = (uint64_t)t * TE, e1 = min(n, e0 + TE);
+  const uint32_t r0 = (uint32_t)(DIR == DIR_ALL ? 2 * e0 : e0);
+  const uint32_t nrec = (uint32_t)(DIR == DIR_ALL ? 2 * (e1 - e0) : e1 - e0);
+  for (uint32_t i = tid; i < nbp; i += DP_BLOCK) s_cnt[i] = 0;
+  __syncthreads();
+  const uint32_t lmask = (1u << S) - 1;
+  uint32_t kb[DP_ITEMS], rk[DP_ITEMS];
+  V v[DP_ITEMS];
+#pragma unroll
+  for (int u = 0; u < DP_ITEMS; ++u) {
+    const uint32_t j = (uint32_t)u * DP_BLOCK + tid;
+    if (j < nrec) {
+      uint32_t c;
+      es.load(r0 + j, c, v[u]);
+      kb[u] = ((c >> S) << 16) | (c & lmask);
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < DP_ITEMS; ++u) {
+    if ((uint32_t)u * DP_BLOCK + tid < nrec) rk[u] = atomicAdd(&s_cnt[kb[u] >> 16], 1u);
+  }
+  __syncthreads();
+  const uint32_t b0 = 2 * tid, b1 = 2 * tid + 1;   // BK_MAXB = 2 * DP_BLOCK
+  const uint32_t c0 = b0 < nbp ? s_cnt[b0] : 0u, c1 = b1 < nbp ? s_cnt[b1] : 0u;
+  uint32_t total;
+  const uint32_t st0 = bk_block_scan(c0 + c1, s_w, total);
+  const uint32_t* orow = off + (uint64_t)t * nbp;
+  if (b0 < nbp) {
+    s_cnt[b0] = st0;
+    s_delta[b0] = orow[b0] - st0;
+  }
+  if (b1 < nbp) {
+    s_cnt[b1] = st0 + c0;
+    s_delta[b1] = orow[b1] - (st0 + c0);
+  }
+  __syncthreads();
+#pragma unroll
+  for (int u = 0; u < DP_ITEMS; ++u) {
+    if ((uint32_t)u * DP_BLOCK + tid < nrec) {
+      const uint32_t pos = s_cnt[kb[u] >> 16] + rk[u];
+      s_key[pos] = kb[u];
+      if constexpr (HAS_V) s_val[pos] = v[u];
+    }
+  }
+  __syncthreads();
+  for (uint32_t j = tid; j < nrec; j += DP_BLOCK) {
+    const uint32_t kv = s_key[j];
+    const uint32_t d = s_delta[kv >> 16] + j;
+    k16[d] = (uint16_t)kv;
+    if constexpr (HAS_V) vout[d] = s_val[j];
+  }
+}
+
 // ---- k_bk_accum: persistent; LDS accumulation of (bucket, record range) items ---------------------
 // Finalize (shared with k_bk_merge): the bucket's vertices in ascending order -> staging at the
 // bucket's record offset (a bucket has at least as many records as vertices).

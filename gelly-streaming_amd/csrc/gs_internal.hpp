@@ -40,6 +40,7 @@ struct gs_ctx {
   int hist_digits = 4;   // key-byte histograms keyinfo computes (learned from the previous window)
   uint32_t flags = 0;    // gs_config.flags
   int64_t bk_base = 0;   // bucket path: predicted lower bound of the next window's vertex IDs
+  uint32_t bk_nbp = 0;   // direct bucket path: predicted bucket count (0 = BK_MAXB)
   int n_cu = 0;          // compute units (persistent grids)
   // input staging (host batches)
   gs::DevBuf in_src, in_dst, in_val;
@@ -59,6 +60,8 @@ struct gs_ctx {
   gs::DevBuf hs[20];
   // bucket path (gs_bucket.hip): plan tables, work items, LDS slabs of multi-item buckets
   gs::DevBuf bk_meta, bk_items, bk_slabs;
+  // direct partition: per-tile bucket counts (u16), chunk sums, per-tile write offsets
+  gs::DevBuf dp_cnt, dp_csum, dp_off;
   hipEvent_t ev[6] = {};
   hipEvent_t pass_ev[9] = {};
   gs_stage_times times{};

@@ -58,13 +58,17 @@ class StageTimes:
     payload_bytes: int
     partials: int
     fused_last: bool
-    path: int = 0          # 0: LSD sort + reduce-by-key; 1: bucket path (pass_ms = passes, accumulate, merge, emit)
+    path: int = 0          # 0: LSD sort + reduce-by-key; 1: bucket path, onesweep partition (pass_ms = passes,
+                           # accumulate, merge, emit); 2: bucket path, direct partition (pass_ms = offset scans,
+                           # scatter, accumulate, merge, emit; keyinfo_ms = per-tile histogram)
 
 
 class Engine:
-    def __init__(self, device: int = 0, reserve_edges: int = 0, torch_stream: bool = True, sort_only: bool = False):
+    def __init__(self, device: int = 0, reserve_edges: int = 0, torch_stream: bool = True, sort_only: bool = False,
+                 bk_onesweep: bool = False):
         self._L = L.load()
-        cfg = L.GsConfig(device, L.GS_FLAG_SORT_ONLY if sort_only else 0, reserve_edges)
+        flags = (L.GS_FLAG_SORT_ONLY if sort_only else 0) | (L.GS_FLAG_BK_ONESWEEP if bk_onesweep else 0)
+        cfg = L.GsConfig(device, flags, reserve_edges)
         ctx = ctypes.c_void_p()
         st = self._L.gs_create(ctypes.byref(cfg), ctypes.byref(ctx))
         if st != L.GS_OK:
@@ -113,7 +117,7 @@ class Engine:
     def stage_times(self) -> StageTimes:
         t = L.GsStageTimes()
         self._check(self._L.gs_last_stage_times(self.ctx, ctypes.byref(t)))
-        launched = t.sort_passes + (3 if t.path == 1 else 1 if t.fused_last else 0)
+        launched = 5 if t.path == 2 else t.sort_passes + (3 if t.path == 1 else 1 if t.fused_last else 0)
         return StageTimes(t.keyinfo_ms, t.sort_ms, t.reduce_ms, t.total_ms, t.sort_passes, t.key_bits, t.records,
                           t.vertices, list(t.pass_ms)[:launched], t.key_bytes, t.payload_bytes,
                           t.partials, bool(t.fused_last), t.path)

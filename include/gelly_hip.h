@@ -81,6 +81,8 @@ typedef struct gs_ctx gs_ctx;
 
 /* gs_config.flags */
 #define GS_FLAG_SORT_ONLY 1u   /* reduce / fold: always take the full LSD sort + reduce-by-key path */
+#define GS_FLAG_BK_ONESWEEP 2u /* bucket path: partition with 1-2 LSD passes instead of the one-pass
+                                  direct scatter (A/B measurement; same results)                   */
 
 typedef struct gs_config {
   int32_t device;          /* HIP device ordinal                                           */
@@ -225,8 +227,11 @@ typedef struct gs_stage_times {
   uint32_t key_bytes, payload_bytes;  /* sorted key / payload widths                          */
   uint64_t partials;       /* (vertex, partial) pairs left by the fused last pass               */
   uint32_t fused_last;     /* 1: pass_ms[sort_passes] is the last pass fused with the combine   */
-  uint32_t path;           /* 0: LSD sort + reduce-by-key; 1: bucket path (pass_ms[sort_passes..+2]
-                              = accumulate, merge, emit; partials = work items)                  */
+  uint32_t path;           /* 0: LSD sort + reduce-by-key;
+                              1: bucket path, onesweep partition (pass_ms[0..sort_passes) = LSD
+                                 passes, then accumulate, merge, emit; partials = work items);
+                              2: bucket path, direct partition (keyinfo_ms = per-tile histogram,
+                                 pass_ms[0..4] = offset scans, scatter, accumulate, merge, emit) */
 } gs_stage_times;
 GS_API gs_status gs_last_stage_times(const gs_ctx* ctx, gs_stage_times* out);
 

@@ -1,8 +1,9 @@
 """GPU: the bucket path (gs_bucket.hpp) — reduceOnEdges / foldNeighbors built-ins through the high-bit
 partition + LDS accumulation — against the CPU oracle, at every pipeline shape it takes:
 
-  0 partition passes  (vertex range <= 2^S: one bucket, records read straight from the columns)
-  1 pass              (<= 2^(S+8) vertices), 2 passes (up to BK_MAXB = 2048 buckets)
+  direct partition    (default, path 2): per-tile histograms -> offsets -> one scatter pass
+  onesweep partition  (GS_FLAG_BK_ONESWEEP, path 1): 1 pass (<= 2^(S+8) vertices) or 2 passes
+  no partition        (vertex range <= 2^S: one bucket, records read straight from the columns)
   multi-item buckets  (a bucket with more than 2^17 records: LDS slabs merged by k_bk_merge)
   mispredicted base   (IDs far from 0 / negative: the info kernel reruns with base = min)
   out of range        (vertex range > 2048 buckets: falls back to the LSD sort path, path 0)
@@ -15,6 +16,7 @@ import torch
 pytestmark = pytest.mark.gpu
 
 FLOAT_RTOL = 1e-5
+BUCKET = (1, 2)   # stage_times().path of the bucket path (onesweep / direct partition)
 
 
 def _dev(*arrs):
@@ -55,21 +57,60 @@ def test_bucket_reduce_shapes(engine, oracle, shape, direction, dtype, op):
     v = oracle.gen_values(n, 11 + op, oracle.DT_OF_NP[np.dtype(dtype)])
     rk, rv = oracle.window_reduce(s, d, v, direction, op)
     gk, gv = engine.reduce(*_dev(s, d, v), direction, op)
-    assert engine.stage_times().path == 1
+    assert engine.stage_times().path in BUCKET
     _check(gk, gv, rk, rv, dtype, op)
 
 
-def test_bucket_pass_counts(engine, oracle):
-    """The pipeline shape follows the vertex range (S = 14 for Long sums)."""
+def test_bucket_pass_counts(pkg, oracle):
+    """The pipeline shape follows the vertex range (S = 14 for Long sums): the direct partition is one
+    scatter pass; the onesweep partition takes 1-2 LSD passes.  A fresh engine per span, so the
+    direct path's predicted bucket count starts from the default."""
     rng = np.random.default_rng(5)
     for span, passes in ((1 << 14, 0), (1 << 18, 1), (1 << 22, 1), (1 << 23, 2), (1 << 25, 2)):
         s, d = _window(rng, 20000, span)
         s[0], d[0] = 0, span - 1
         v = oracle.gen_values(20000, 1, oracle.DT_I64)
         rk, rv = oracle.window_reduce(s, d, v, 2, 0)
-        gk, gv = engine.reduce(*_dev(s, d, v), 2, 0)
-        t = engine.stage_times()
-        assert (t.path, t.sort_passes) == (1, passes), span
+        with pkg.Engine(0, bk_onesweep=True) as eo:
+            gk, gv = eo.reduce(*_dev(s, d, v), 2, 0)
+            t = eo.stage_times()
+            assert (t.path, t.sort_passes) == (1, passes), span
+            _check(gk, gv, rk, rv, np.int64, 0)
+        with pkg.Engine(0) as ed:
+            for rep in range(2):   # the second window runs on the learned prediction (one bucket: no scatter)
+                gk, gv = ed.reduce(*_dev(s, d, v), 2, 0)
+                t = ed.stage_times()
+                assert t.path == 2 and t.sort_passes == (0 if rep and span <= 1 << 14 else 1), span
+                _check(gk, gv, rk, rv, np.int64, 0)
+
+
+@pytest.mark.parametrize("direction", [0, 1, 2])
+@pytest.mark.parametrize("op", [0, 1, 2, 3])
+def test_direct_matches_onesweep(pkg, oracle, direction, op):
+    """The two partition front ends feed the same accumulation: integer results are identical."""
+    rng = np.random.default_rng(40 + op)
+    s, d = _window(rng, 150_001, 1 << 23, hub_frac=0.05)
+    v = oracle.gen_values(150_001, 8, oracle.DT_I64)
+    with pkg.Engine(0) as ed, pkg.Engine(0, bk_onesweep=True) as eo:
+        kd, vd = ed.reduce(*_dev(s, d, v), direction, op)
+        ko, vo = eo.reduce(*_dev(s, d, v), direction, op)
+        assert (ed.stage_times().path, eo.stage_times().path) == (2, 1)
+        assert torch.equal(kd, ko) and torch.equal(vd, vo)
+    rk, rv = oracle.window_reduce(s, d, v, direction, op)
+    _check(kd, vd, rk, rv, np.int64, op)
+
+
+def test_direct_prediction_shrinks_and_grows(engine, oracle):
+    """The direct path predicts the next window's base and bucket count; windows that need more
+    buckets (or sit elsewhere) recount, windows that need fewer run on the wider table."""
+    rng = np.random.default_rng(17)
+    for span, off in ((1 << 24, 0), (1 << 16, 0), (1 << 16, 0), (1 << 24, 0), (1 << 20, -(1 << 33)),
+                      (1 << 24, 1 << 40), (1 << 24, 0)):
+        s, d = _window(rng, 30011, span, off)
+        v = oracle.gen_values(30011, 5, oracle.DT_I64)
+        rk, rv = oracle.window_reduce(s, d, v, 1, 0)
+        gk, gv = engine.reduce(*_dev(s, d, v), 1, 0)
+        assert engine.stage_times().path in BUCKET
         _check(gk, gv, rk, rv, np.int64, 0)
 
 
@@ -85,7 +126,7 @@ def test_bucket_multi_item_hub(engine, oracle, op):
         gk, gv = engine.reduce(*_dev(s, d, v), direction, op)
         t = engine.stage_times()
         buckets = (1 << 20) >> (15 if op == 3 else 14)
-        assert t.path == 1 and t.partials > buckets      # the hub's bucket took several items
+        assert t.path in BUCKET and t.partials > buckets      # the hub's bucket took several items
         _check(gk, gv, rk, rv, np.int64, op)
 
 
@@ -99,7 +140,7 @@ def test_bucket_base_prediction(engine, oracle, offset):
         v = oracle.gen_values(40000, 9, oracle.DT_I64)
         rk, rv = oracle.window_reduce(s, d, v, 2, 0)
         gk, gv = engine.reduce(*_dev(s, d, v), 2, 0)
-        assert engine.stage_times().path == 1
+        assert engine.stage_times().path in BUCKET
         _check(gk, gv, rk, rv, np.int64, 0)
 
 
@@ -122,7 +163,7 @@ def test_bucket_fold_init(engine, oracle, dtype, op, init):
     v = oracle.gen_values(n, 4, oracle.DT_OF_NP[np.dtype(dtype)])
     rk, rv = oracle.window_fold(s, d, v, 0, op, init)
     gk, gv = engine.fold(*_dev(s, d, v), 0, op, init)
-    assert engine.stage_times().path == 1
+    assert engine.stage_times().path in BUCKET
     _check(gk, gv, rk, rv, dtype, op)
 
 
@@ -134,7 +175,7 @@ def test_bucket_degree_max(engine, oracle, span):
         for init_max in (np.iinfo(np.int64).min, span // 2):
             rk, rd, rm = oracle.window_fold_degree_max(s, d, direction, init_max)
             gk, gd, gm = engine.fold_degree_max(*_dev(s, d), direction, init_max)
-            assert engine.stage_times().path == 1
+            assert engine.stage_times().path in BUCKET
             assert np.array_equal(gk.cpu().numpy(), rk)
             assert np.array_equal(gd.cpu().numpy(), rd) and np.array_equal(gm.cpu().numpy(), rm)
 
@@ -146,7 +187,7 @@ def test_sort_only_engine_matches(pkg, oracle):
     v = oracle.gen_values(100000, 6, oracle.DT_I64)
     with pkg.Engine(0) as eb, pkg.Engine(0, sort_only=True) as es:
         kb, vb = eb.reduce(*_dev(s, d, v), 2, 0)
-        assert eb.stage_times().path == 1
+        assert eb.stage_times().path in BUCKET
         ks, vs = es.reduce(*_dev(s, d, v), 2, 0)
         assert es.stage_times().path == 0
         assert torch.equal(kb, ks) and torch.equal(vb, vs)
@@ -159,7 +200,7 @@ def test_bucket_large_rmat_properties(engine):
     s, d = engine.generate_rmat(22, n, 77)
     v = engine.generate_values(n, 78, 1)
     k, x = engine.reduce(s, d, v, 2, 0)
-    assert engine.stage_times().path == 1
+    assert engine.stage_times().path in BUCKET
     assert bool((k[1:] > k[:-1]).all())
     assert int(x.sum()) == 2 * int(v.sum())
     k2, c = engine.reduce(s, d, v, 2, 3)
