@@ -71,8 +71,10 @@ gs_status launch_dp_hist(gs_ctx* c, const int64_t* src, const int64_t* dst, uint
   char* sm = c->small.as<char>();
   auto* mm = (unsigned long long*)(sm + SM_BK_MM);
   GS_HIP(hipMemsetAsync(mm, 0, 32, c->stream));
-  const bool vec = ((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst)) & 15) == 0;
-  const unsigned grid = std::max<uint32_t>(1, std::min<uint32_t>(nt, DP_HIST_GRID));
+  // VEC reads whole 16-byte pairs: every tile must hold one (only the last tile can be shorter)
+  const bool vec = ((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst)) & 15) == 0 &&
+                   n % dp_tile_edges<DIR>() != 1;
+  const unsigned grid = std::max<uint32_t>(1, std::min<uint32_t>(nt, (uint32_t)c->n_cu));
   uint16_t* cnt = c->dp_cnt.as<uint16_t>();
   if (vec)
     hipLaunchKernelGGL((k_dp_hist<DIR, true>), dim3(grid), dim3(DP_BLOCK), 0, c->stream, src, dst, n, nt, base, S, nbp,
@@ -292,9 +294,10 @@ gs_status bucket_direct(gs_ctx* c, const int64_t* src, const int64_t* dst, const
   uint16_t* k16 = c->keysB.as<uint16_t>();
   Raw* vpart = P::HAS_V ? c->valsB.as<Raw>() : nullptr;
   if (part) {
-    const uint32_t per = (nt + 7) / 8;
-    hipLaunchKernelGGL((k_dp_scatter<Raw, DIR, P::PAY>), dim3(per * 8), dim3(DP_BLOCK), 0, c->stream, es, n, S, nb,
-                       nt, c->dp_off.as<uint32_t>(), k16, vpart);
+    // full tiles by XCD slot + one block for the partial tile
+    const unsigned grid = (unsigned)(((n / dp_tile_edges<DIR>()) + 7) / 8 * 8 + 1);
+    hipLaunchKernelGGL((k_dp_scatter<Raw, DIR, P::PAY>), dim3(grid), dim3(DP_BLOCK), 0, c->stream, es, n, S, nb,
+                       c->dp_off.as<uint32_t>(), k16, vpart);
     GS_HIP(hipGetLastError());
   }
   hipEventRecord(c->pass_ev[2], c->stream);

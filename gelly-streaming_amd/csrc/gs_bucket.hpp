@@ -73,9 +73,13 @@ struct BkVal {
   static constexpr uint32_t W = 1u << S;
   static constexpr bool HAS_V = true;
   static constexpr int PAY = PAY_VAL;
+  // presence of a vertex: one byte each (a plain ds_write_b8, no atomic) where it fits next to 8-byte
+  // accumulators (128 + 16 KB); a bitmap with ds_or for 4-byte accumulators (2^15 of them)
+  static constexpr bool PB = sizeof(A) == 8;
+  static constexpr uint32_t PW = PB ? W / 4 : W / 32;   // presence words
   struct Lds {
     A acc[W];
-    uint32_t bm[W / 32];
+    uint32_t pm[PW];
   };
   __device__ static A identity() {
     if constexpr (OP == OP_SUM) return A(0);
@@ -91,7 +95,7 @@ struct BkVal {
   }
   __device__ static void init(Lds& s, int tid) {
     for (uint32_t i = tid; i < W; i += BK_ACC_BLOCK) s.acc[i] = identity();
-    for (uint32_t i = tid; i < W / 32; i += BK_ACC_BLOCK) s.bm[i] = 0;
+    for (uint32_t i = tid; i < PW; i += BK_ACC_BLOCK) s.pm[i] = 0;
   }
   __device__ static void add(Lds& s, uint32_t i, Raw r) {
     const T v = bits_as<T>(r);
@@ -109,13 +113,17 @@ struct BkVal {
       using I = std::conditional_t<sizeof(T) == 8, long long, int>;
       atomicMax((I*)&s.acc[i], (I)v);
     }
-    atomicOr(&s.bm[i >> 5], 1u << (i & 31));
+    if constexpr (PB) reinterpret_cast<uint8_t*>(s.pm)[i] = 1;
+    else atomicOr(&s.pm[i >> 5], 1u << (i & 31));
   }
-  __device__ static bool present(const Lds& s, uint32_t i) { return (s.bm[i >> 5] >> (i & 31)) & 1u; }
+  __device__ static bool present(const Lds& s, uint32_t i) {
+    if constexpr (PB) return reinterpret_cast<const uint8_t*>(s.pm)[i] != 0;
+    else return (s.pm[i >> 5] >> (i & 31)) & 1u;
+  }
   __device__ static void stage(BkStage st, uint32_t pos, const Lds& s, uint32_t i) { ((A*)st.a)[pos] = s.acc[i]; }
   __device__ static void merge(Lds& s, const Lds* g, int tid) {
     for (uint32_t i = tid; i < W; i += BK_ACC_BLOCK) s.acc[i] = combine(s.acc[i], g->acc[i]);
-    for (uint32_t i = tid; i < W / 32; i += BK_ACC_BLOCK) s.bm[i] |= g->bm[i];
+    for (uint32_t i = tid; i < PW; i += BK_ACC_BLOCK) s.pm[i] |= g->pm[i];
   }
   struct Out {
     int64_t* keys;
@@ -414,14 +422,21 @@ static __global__ __launch_bounds__(BK_PLAN_BLOCK) void k_bk_plan(const uint32_t
 //                 (16-bit bucket-local index, payload) at off[t][b].
 // Against the 2-pass LSD partition (k_onesweep twice) this moves 8 + 26 B per 8-byte-payload record
 // instead of 8 + 28 + 22.
+#ifndef GS_DP_ITEMS
+#define GS_DP_ITEMS 10
+#endif
+#ifndef GS_DP_XCD
+#define GS_DP_XCD 1
+#endif
 constexpr int DP_BLOCK = 1024;
-constexpr int DP_ITEMS = 10;
+constexpr int DP_ITEMS = GS_DP_ITEMS;
 constexpr uint32_t DP_TILE = DP_BLOCK * DP_ITEMS;   // 10240 records < 2^16
 constexpr uint32_t DP_CHUNK = 64;                   // tiles per up / down-sweep chunk
-constexpr int DP_HIST_GRID = 2048;                  // k_dp_hist blocks (each loops over tiles)
 template <int DIR>
 __host__ __device__ constexpr uint32_t dp_tile_edges() { return DIR == DIR_ALL ? DP_TILE / 2 : DP_TILE; }
 
+// Persistent, software-pipelined like k_dp_scatter: the next tile's keys are in flight while this
+// tile's counts go through LDS.  VEC: the tile's keys as 16-byte pairs (columns 16-byte aligned).
 template <int DIR, bool VEC>
 __global__ __launch_bounds__(DP_BLOCK) void k_dp_hist(const int64_t* __restrict__ src, const int64_t* __restrict__ dst,
                                                       uint64_t n, uint32_t nt, int64_t base, int S, uint32_t nbp,
@@ -431,54 +446,70 @@ __global__ __launch_bounds__(DP_BLOCK) void k_dp_hist(const int64_t* __restrict_
   __shared__ unsigned long long s_mm[3][DP_BLOCK / WAVE];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   constexpr uint32_t TE = dp_tile_edges<DIR>();
+  constexpr int U = VEC ? (TE / 2 + DP_BLOCK - 1) / DP_BLOCK : (TE + DP_BLOCK - 1) / DP_BLOCK;
+  using L = std::conditional_t<VEC, longlong2, int64_t>;
   uint64_t lo = 0, hi = 0;   // max of ~flip(key), max of flip(key)
   uint32_t ovf = 0;
-  for (uint32_t t = blockIdx.x; t < nt; t += gridDim.x) {
+  auto add = [&](int64_t k) {
+    const uint64_t f = (uint64_t)k ^ (1ull << 63);
+    lo = max(lo, ~f);
+    hi = max(hi, f);
+    const uint64_t d = ((uint64_t)k - (uint64_t)base) >> S;
+    if (k < base || d >= nbp) ++ovf;
+    else atomicAdd(&h[d], 1u);
+  };
+  // element u of tile tt: a 16-byte pair index (VEC) or an edge index
+  auto first = [&](uint32_t tt) { return VEC ? ((uint64_t)tt * TE) >> 1 : (uint64_t)tt * TE; };
+  auto last = [&](uint32_t tt) { const uint64_t e1 = min(n, (uint64_t)(tt + 1) * TE); return VEC ? e1 >> 1 : e1; };
+  // loads are unconditional (indices clamped into the tile; the host picks VEC only when every tile
+  // holds a whole pair): a load under a branch gets a register copy at the join that waits for it,
+  // which serialises the tile's loads
+  auto load = [&](uint32_t tt, L (&a)[U], L (&b)[U]) {
+    const uint64_t q0 = first(tt), q1 = last(tt);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint64_t q = min(q0 + (uint64_t)u * DP_BLOCK + tid, q1 - 1);
+      if (DIR != DIR_IN) a[u] = reinterpret_cast<const L*>(src)[q];
+      if (DIR != DIR_OUT) b[u] = reinterpret_cast<const L*>(dst)[q];
+    }
+  };
+  L ca[U], cb[U];
+  uint32_t t = blockIdx.x;
+  if (t < nt) load(t, ca, cb);
+  for (; t < nt; t += gridDim.x) {
     for (uint32_t i = tid; i < nbp; i += DP_BLOCK) h[i] = 0;
+    L na[U], nb2[U];
+    load(t + gridDim.x < nt ? t + gridDim.x : t, na, nb2);   // prefetch (the last round reloads this tile)
     __syncthreads();
-    auto add = [&](int64_t k) {
-      const uint64_t f = (uint64_t)k ^ (1ull << 63);
-      lo = max(lo, ~f);
-      hi = max(hi, f);
-      const uint64_t d = ((uint64_t)k - (uint64_t)base) >> S;
-      if (k < base || d >= nbp) ++ovf;
-      else atomicAdd(&h[d], 1u);
-    };
-    const uint64_t e0 = (uint64_t)t * TE, e1 = min(n, e0 + TE);
-    if constexpr (VEC) {   // 16-byte pairs; TE is even, so only the window's last edge can be unpaired
-      const longlong2* s2 = reinterpret_cast<const longlong2*>(src);
-      const longlong2* d2 = reinterpret_cast<const longlong2*>(dst);
-      const uint64_t q0 = e0 >> 1, q1 = e1 >> 1;
-      constexpr int U = (TE / 2 + DP_BLOCK - 1) / DP_BLOCK;
-      longlong2 a[U], b[U];
+    const uint64_t q0 = first(t), q1 = last(t);
 #pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const uint64_t q = q0 + (uint64_t)u * DP_BLOCK + tid;
-        if (q < q1) {
-          if (DIR != DIR_IN) a[u] = s2[q];
-          if (DIR != DIR_OUT) b[u] = d2[q];
+    for (int u = 0; u < U; ++u) {
+      if (q0 + (uint64_t)u * DP_BLOCK + tid < q1) {
+        if constexpr (VEC) {
+          if (DIR != DIR_IN) { add(ca[u].x); add(ca[u].y); }
+          if (DIR != DIR_OUT) { add(cb[u].x); add(cb[u].y); }
+        } else {
+          if (DIR != DIR_IN) add(ca[u]);
+          if (DIR != DIR_OUT) add(cb[u]);
         }
       }
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        if (q0 + (uint64_t)u * DP_BLOCK + tid < q1) {
-          if (DIR != DIR_IN) { add(a[u].x); add(a[u].y); }
-          if (DIR != DIR_OUT) { add(b[u].x); add(b[u].y); }
-        }
-      }
-      if ((e1 & 1) && tid == 0) {
+    }
+    if (VEC && tid == 0) {   // TE is even: only the window's last edge can be unpaired
+      const uint64_t e1 = min(n, (uint64_t)(t + 1) * TE);
+      if (e1 & 1) {
         if (DIR != DIR_IN) add(src[e1 - 1]);
         if (DIR != DIR_OUT) add(dst[e1 - 1]);
-      }
-    } else {
-      for (uint64_t i = e0 + tid; i < e1; i += DP_BLOCK) {
-        if (DIR != DIR_IN) add(src[i]);
-        if (DIR != DIR_OUT) add(dst[i]);
       }
     }
     __syncthreads();
     uint16_t* row = cnt + (uint64_t)t * nbp;
     for (uint32_t i = tid; i < nbp; i += DP_BLOCK) row[i] = (uint16_t)h[i];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      ca[u] = na[u];
+      cb[u] = nb2[u];
+    }
+    __syncthreads();
   }
   // one atomic per block and word (thousands of blocks on three words would serialise)
 #pragma unroll
@@ -566,11 +597,30 @@ static __global__ __launch_bounds__(256) void k_dp_down(const uint16_t* __restri
   }
 }
 
-// one tile per block; blocks b and b + 8 share an XCD under round-robin dispatch (speed only), so
-// each XCD takes a contiguous range of tiles and the adjacent runs of a bucket meet in one L2
+// raw record r of the window: the low half of its key (the bucket math is mod 2^32) and its payload
+template <typename V, int DIR, int PAY>
+__device__ __forceinline__ void dp_load_raw(const BaseSrc<V, DIR, PAY>& es, uint32_t r, uint32_t& klo, V& v) {
+  uint32_t i = r;
+  bool rev = DIR == DIR_IN;
+  if constexpr (DIR == DIR_ALL) {
+    i = r >> 1;
+    rev = r & 1u;
+  }
+  klo = reinterpret_cast<const uint32_t*>(rev ? es.dst : es.src)[2 * (uint64_t)i];
+  if constexpr (PAY == PAY_VAL) v = es.val[i];
+  else if constexpr (PAY == PAY_NBR) v = (V)(rev ? es.src : es.dst)[i];
+}
+
+// One full tile per block (1 block per CU: LDS-bound); blocks b and b + 8 share an XCD under
+// round-robin dispatch (speed only), so XCD slot b & 7 owns a contiguous range of tiles: the
+// adjacent runs of a bucket meet in one L2.  The last block takes the window's partial tile.
+// Every load is unconditional (clamped indices): a load under a branch gets a register copy at the
+// join that waits for it and serialises the tile (2.02 -> 1.59 ms on C2).  A persistent variant
+// that prefetched the next tile during the LDS phases measured slower (2.20 ms): its loop-carried
+// registers cost a full vmcnt(0) per tile, behind the previous tile's stores.
 template <typename V, int DIR, int PAY>
 __global__ __launch_bounds__(DP_BLOCK) void k_dp_scatter(BaseSrc<V, DIR, PAY> es, uint64_t n, int S, uint32_t nbp,
-                                                         uint32_t nt, const uint32_t* __restrict__ off,
+                                                         const uint32_t* __restrict__ off,
                                                          uint16_t* __restrict__ k16, V* __restrict__ vout) {
   constexpr bool HAS_V = PAY != PAY_NONE;
   __shared__ uint32_t s_key[DP_TILE];                // (bucket << 16) | bucket-local index, bucket order
@@ -579,60 +629,96 @@ __global__ __launch_bounds__(DP_BLOCK) void k_dp_scatter(BaseSrc<V, DIR, PAY> es
   __shared__ uint32_t s_delta[BK_MAXB];              // global position - tile position of bucket b's run
   __shared__ uint32_t s_w[DP_BLOCK / WAVE];
   const int tid = threadIdx.x;
-  const uint32_t per = (nt + 7) / 8;
-  const uint32_t t = (blockIdx.x & 7u) * per + (blockIdx.x >> 3);
-  if (t >= nt) return;
   constexpr uint32_t TE = dp_tile_edges<DIR>();
-  const uint64_t e0 = (uint64_t)t * TE, e1 = min(n, e0 + TE);
-  const uint32_t r0 = (uint32_t)(DIR == DIR_ALL ? 2 * e0 : e0);
-  const uint32_t nrec = (uint32_t)(DIR == DIR_ALL ? 2 * (e1 - e0) : e1 - e0);
-  for (uint32_t i = tid; i < nbp; i += DP_BLOCK) s_cnt[i] = 0;
-  __syncthreads();
-  const uint32_t lmask = (1u << S) - 1;
-  uint32_t kb[DP_ITEMS], rk[DP_ITEMS];
-  V v[DP_ITEMS];
-#pragma unroll
-  for (int u = 0; u < DP_ITEMS; ++u) {
-    const uint32_t j = (uint32_t)u * DP_BLOCK + tid;
-    if (j < nrec) {
-      uint32_t c;
-      es.load(r0 + j, c, v[u]);
-      kb[u] = ((c >> S) << 16) | (c & lmask);
-    }
-  }
-#pragma unroll
-  for (int u = 0; u < DP_ITEMS; ++u) {
-    if ((uint32_t)u * DP_BLOCK + tid < nrec) rk[u] = atomicAdd(&s_cnt[kb[u] >> 16], 1u);
-  }
-  __syncthreads();
+  const uint32_t nfull = (uint32_t)(n / TE);   // tile nfull, if any, is the window's partial last one
+  const uint32_t base32 = (uint32_t)es.base, lmask = (1u << S) - 1;
   const uint32_t b0 = 2 * tid, b1 = 2 * tid + 1;   // BK_MAXB = 2 * DP_BLOCK
-  const uint32_t c0 = b0 < nbp ? s_cnt[b0] : 0u, c1 = b1 < nbp ? s_cnt[b1] : 0u;
-  uint32_t total;
-  const uint32_t st0 = bk_block_scan(c0 + c1, s_w, total);
-  const uint32_t* orow = off + (uint64_t)t * nbp;
-  if (b0 < nbp) {
-    s_cnt[b0] = st0;
-    s_delta[b0] = orow[b0] - st0;
-  }
-  if (b1 < nbp) {
-    s_cnt[b1] = st0 + c0;
-    s_delta[b1] = orow[b1] - (st0 + c0);
-  }
-  __syncthreads();
+  const uint32_t bl0 = min(b0, nbp - 1), bl1 = min(b1, nbp - 1);
+
+  auto process = [&](auto full, uint32_t nrec, const uint32_t (&klo)[DP_ITEMS], const V (&vv)[DP_ITEMS],
+                     uint32_t o0, uint32_t o1) {
+    constexpr bool FULL = decltype(full)::value;
+    for (uint32_t i = tid; i < nbp; i += DP_BLOCK) s_cnt[i] = 0;
+    __syncthreads();
+    uint32_t kb[DP_ITEMS], rk[DP_ITEMS];
 #pragma unroll
-  for (int u = 0; u < DP_ITEMS; ++u) {
-    if ((uint32_t)u * DP_BLOCK + tid < nrec) {
-      const uint32_t pos = s_cnt[kb[u] >> 16] + rk[u];
-      s_key[pos] = kb[u];
-      if constexpr (HAS_V) s_val[pos] = v[u];
+    for (int u = 0; u < DP_ITEMS; ++u) {
+      const uint32_t c = klo[u] - base32;
+      kb[u] = ((c >> S) << 16) | (c & lmask);
+      if (FULL || (uint32_t)u * DP_BLOCK + tid < nrec) rk[u] = atomicAdd(&s_cnt[kb[u] >> 16], 1u);
+    }
+    __syncthreads();
+    const uint32_t c0 = b0 < nbp ? s_cnt[b0] : 0u, c1 = b1 < nbp ? s_cnt[b1] : 0u;
+    uint32_t total;
+    const uint32_t st0 = bk_block_scan(c0 + c1, s_w, total);
+    // unconditional: entries past nbp are never read, and a branch here would make the compiler
+    // wait for every outstanding load (the prefetch) before the offsets it guards
+    s_cnt[b0] = st0;
+    s_delta[b0] = o0 - st0;
+    s_cnt[b1] = st0 + c0;
+    s_delta[b1] = o1 - (st0 + c0);
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < DP_ITEMS; ++u) {
+      if (FULL || (uint32_t)u * DP_BLOCK + tid < nrec) {
+        const uint32_t pos = s_cnt[kb[u] >> 16] + rk[u];
+        s_key[pos] = kb[u];
+        if constexpr (HAS_V) s_val[pos] = vv[u];
+      }
+    }
+    __syncthreads();
+    if constexpr (FULL) {
+#pragma unroll
+      for (int u = 0; u < DP_ITEMS; ++u) {
+        const uint32_t j = (uint32_t)u * DP_BLOCK + tid;
+        const uint32_t kv = s_key[j];
+        const uint32_t d = s_delta[kv >> 16] + j;
+        k16[d] = (uint16_t)kv;
+        if constexpr (HAS_V) vout[d] = s_val[j];
+      }
+    } else {
+      for (uint32_t j = tid; j < nrec; j += DP_BLOCK) {
+        const uint32_t kv = s_key[j];
+        const uint32_t d = s_delta[kv >> 16] + j;
+        k16[d] = (uint16_t)kv;
+        if constexpr (HAS_V) vout[d] = s_val[j];
+      }
+    }
+  };
+  // tile tt holds records [tt * DP_TILE, + nrec); indices clamped into the tile
+  auto load_tile = [&](uint32_t tt, uint32_t nrec, uint32_t (&klo)[DP_ITEMS], V (&vv)[DP_ITEMS]) {
+    const uint32_t r0 = tt * DP_TILE;
+#pragma unroll
+    for (int u = 0; u < DP_ITEMS; ++u) dp_load_raw(es, r0 + min((uint32_t)u * DP_BLOCK + tid, nrec - 1), klo[u], vv[u]);
+  };
+  auto load_off = [&](uint32_t tt, uint32_t& o0, uint32_t& o1) {
+    const uint32_t* orow = off + (uint64_t)tt * nbp;
+    o0 = orow[bl0];
+    o1 = orow[bl1];
+  };
+  using Full = std::integral_constant<bool, true>;
+  uint32_t ka[DP_ITEMS];
+  V va[DP_ITEMS];
+  {   // one full tile per block (grid = 8 * ceil(nfull / 8) + 1; the last block takes the partial tile)
+#if GS_DP_XCD
+    const uint32_t per = (nfull + 7) / 8;
+    const uint32_t t = blockIdx.x == gridDim.x - 1 ? nfull : (blockIdx.x & 7u) * per + (blockIdx.x >> 3);
+#else
+    const uint32_t t = blockIdx.x;
+#endif
+    if (t < nfull) {
+      uint32_t o0, o1;
+      load_off(t, o0, o1);
+      load_tile(t, DP_TILE, ka, va);
+      process(Full{}, DP_TILE, ka, va, o0, o1);
     }
   }
-  __syncthreads();
-  for (uint32_t j = tid; j < nrec; j += DP_BLOCK) {
-    const uint32_t kv = s_key[j];
-    const uint32_t d = s_delta[kv >> 16] + j;
-    k16[d] = (uint16_t)kv;
-    if constexpr (HAS_V) vout[d] = s_val[j];
+  if ((uint64_t)nfull * TE < n && blockIdx.x == gridDim.x - 1) {   // the partial last tile
+    const uint32_t nrec = (uint32_t)((n - (uint64_t)nfull * TE) * (DIR == DIR_ALL ? 2 : 1));
+    uint32_t o0, o1;
+    load_off(nfull, o0, o1);
+    load_tile(nfull, nrec, ka, va);
+    process(std::integral_constant<bool, false>{}, nrec, ka, va, o0, o1);
   }
 }
 
@@ -700,7 +786,7 @@ __global__ __launch_bounds__(BK_ACC_BLOCK) void k_bk_accum(Src src, const BkItem
 #pragma unroll
       for (int u = 0; u < UNROLL; ++u) {
         const uint32_t q = r + (uint32_t)u * BK_ACC_BLOCK;
-        if (q < r1) src.load(q, k[u], v[u]);
+        src.load(q < r1 ? q : r1 - 1, k[u], v[u]);   // unconditional: see k_dp_hist
       }
 #pragma unroll
       for (int u = 0; u < UNROLL; ++u) {

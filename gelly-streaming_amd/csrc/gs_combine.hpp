@@ -89,7 +89,7 @@ __global__ __launch_bounds__(BLOCK) void k_onesweep_combine(Src src, K* __restri
 #pragma unroll
   for (int j = 0; j < ITEMS; ++j) {
     const uint32_t r = wrec + j * WAVE;
-    if (r < n) src.load(r, key[j], val[j]);
+    src.load(r < n ? r : n - 1, key[j], val[j]);   // unconditional: a load under a branch serialises
   }
 #pragma unroll
   for (int j = 0; j < ITEMS; ++j) {

@@ -55,7 +55,7 @@ struct BufSrc {
   uint64_t key_xor;  // unused
   __device__ __forceinline__ void load(uint32_t r, K& k, V& v) const {
     k = keys[r];
-    if (vals) v = vals[r];
+    if constexpr (!std::is_same_v<V, uint8_t>) v = vals[r];   // no payload: V = uint8_t
   }
 };
 
@@ -67,7 +67,7 @@ struct ConvSrc {
   uint64_t key_xor;
   __device__ __forceinline__ void load(uint32_t r, K& k, V& v) const {
     k = (K)(keys[r] ^ key_xor);
-    if (vals) v = vals[r];
+    if constexpr (!std::is_same_v<V, uint8_t>) v = vals[r];   // no payload: V = uint8_t
   }
 };
 
@@ -254,7 +254,7 @@ __global__ __launch_bounds__(BLOCK) void k_onesweep(Src src, KO* __restrict__ ko
 #pragma unroll
   for (int j = 0; j < ITEMS; ++j) {
     const uint32_t r = wrec + j * WAVE;
-    if (r < n) src.load(r, key[j], val[j]);
+    src.load(r < n ? r : n - 1, key[j], val[j]);   // unconditional: a load under a branch serialises
   }
 #pragma unroll
   for (int j = 0; j < ITEMS; ++j) {

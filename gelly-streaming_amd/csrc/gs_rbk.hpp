@@ -243,12 +243,20 @@ __global__ __launch_bounds__(BLOCK) void k_reduce_by_key(const K* __restrict__ k
   const uint32_t tile_n = min((uint32_t)TILE, n - tbase);
 
   // striped coalesced load into padded LDS
+  K lk[ITEMS];
+  In lv[ITEMS];
+#pragma unroll
+  for (int j = 0; j < ITEMS; ++j) {   // unconditional (clamped) loads: a load under a branch serialises
+    const uint32_t i = min((uint32_t)j * BLOCK + tid, tile_n - 1);
+    lk[j] = keys[tbase + i];
+    if constexpr (Op::HAS_V) lv[j] = vals[tbase + i];
+  }
 #pragma unroll
   for (int j = 0; j < ITEMS; ++j) {
     const uint32_t i = (uint32_t)j * BLOCK + tid;
     if (i < tile_n) {
-      s_k[pad32(i)] = keys[tbase + i] >> key_shift;
-      if constexpr (Op::HAS_V) s_v[pad32(i)] = vals[tbase + i];
+      s_k[pad32(i)] = lk[j] >> key_shift;
+      if constexpr (Op::HAS_V) s_v[pad32(i)] = lv[j];
     }
   }
   if (tid == 0) {

@@ -43,7 +43,7 @@ def test_reduce_rmat_small(engine, oracle, direction, dtype, op):
     _check_values(_np(gv), rv, dtype, op)
 
 
-@pytest.mark.parametrize("n", [1, 2, 63, 64, 65, 4095, 4096, 4097, 12345, 200003])
+@pytest.mark.parametrize("n", [1, 2, 63, 64, 65, 4095, 4096, 4097, 5120, 10239, 10240, 10241, 12345, 20481, 200003])
 def test_reduce_sizes_ragged(engine, oracle, n):
     s, d = oracle.gen_uniform(1 << 12, n, 99 + n)
     v = oracle.gen_values(n, 5, oracle.DT_I64)
