@@ -294,8 +294,7 @@ gs_status bucket_direct(gs_ctx* c, const int64_t* src, const int64_t* dst, const
   uint16_t* k16 = c->keysB.as<uint16_t>();
   Raw* vpart = P::HAS_V ? c->valsB.as<Raw>() : nullptr;
   if (part) {
-    // full tiles by XCD slot + one block for the partial tile
-    const unsigned grid = (unsigned)(((n / dp_tile_edges<DIR>()) + 7) / 8 * 8 + 1);
+    const unsigned grid = dp_scatter_grid<DIR>(n);
     hipLaunchKernelGGL((k_dp_scatter<Raw, DIR, P::PAY>), dim3(grid), dim3(DP_BLOCK), 0, c->stream, es, n, S, nb,
                        c->dp_off.as<uint32_t>(), k16, vpart);
     GS_HIP(hipGetLastError());

@@ -434,8 +434,13 @@ constexpr uint32_t DP_TILE = DP_BLOCK * DP_ITEMS;   // 10240 records < 2^16
 constexpr uint32_t DP_CHUNK = 64;                   // tiles per up / down-sweep chunk
 template <int DIR>
 __host__ __device__ constexpr uint32_t dp_tile_edges() { return DIR == DIR_ALL ? DP_TILE / 2 : DP_TILE; }
+// k_dp_scatter grid: the full tiles (in 8 XCD slots) + one block for the partial tile
+template <int DIR>
+__host__ __device__ inline uint32_t dp_scatter_grid(uint64_t n) {
+  return (uint32_t)((n / dp_tile_edges<DIR>() + 7) / 8 * 8 + 1);
+}
 
-// Persistent, software-pipelined like k_dp_scatter: the next tile's keys are in flight while this
+// Persistent, software-pipelined: the next tile's keys are in flight while this
 // tile's counts go through LDS.  VEC: the tile's keys as 16-byte pairs (columns 16-byte aligned).
 template <int DIR, bool VEC>
 __global__ __launch_bounds__(DP_BLOCK) void k_dp_hist(const int64_t* __restrict__ src, const int64_t* __restrict__ dst,
@@ -612,12 +617,13 @@ __device__ __forceinline__ void dp_load_raw(const BaseSrc<V, DIR, PAY>& es, uint
 }
 
 // One full tile per block (1 block per CU: LDS-bound); blocks b and b + 8 share an XCD under
-// round-robin dispatch (speed only), so XCD slot b & 7 owns a contiguous range of tiles: the
-// adjacent runs of a bucket meet in one L2.  The last block takes the window's partial tile.
-// Every load is unconditional (clamped indices): a load under a branch gets a register copy at the
-// join that waits for it and serialises the tile (2.02 -> 1.59 ms on C2).  A persistent variant
-// that prefetched the next tile during the LDS phases measured slower (2.20 ms): its loop-carried
-// registers cost a full vmcnt(0) per tile, behind the previous tile's stores.
+// round-robin dispatch (speed only), so XCD slot b & 7 owns a contiguous range of tiles and the
+// blocks an XCD runs at once write adjacent runs of each bucket through one L2 (without it: +14 %).
+// The last block takes the window's partial tile.  Every load is unconditional (clamped indices):
+// a load under a branch gets a register copy at the join that waits for it and serialises the tile
+// (2.02 -> 1.59 ms on C2).  Measured and dropped: a persistent loop prefetching the
+// next tile (2.20 ms), 2-8 unrolled tiles per block (1.68-2.43 ms), 5120-record tiles at 2 blocks
+// per CU (1.71 ms).
 template <typename V, int DIR, int PAY>
 __global__ __launch_bounds__(DP_BLOCK) void k_dp_scatter(BaseSrc<V, DIR, PAY> es, uint64_t n, int S, uint32_t nbp,
                                                          const uint32_t* __restrict__ off,
@@ -699,7 +705,7 @@ __global__ __launch_bounds__(DP_BLOCK) void k_dp_scatter(BaseSrc<V, DIR, PAY> es
   using Full = std::integral_constant<bool, true>;
   uint32_t ka[DP_ITEMS];
   V va[DP_ITEMS];
-  {   // one full tile per block (grid = 8 * ceil(nfull / 8) + 1; the last block takes the partial tile)
+  {   // one full tile per block
 #if GS_DP_XCD
     const uint32_t per = (nfull + 7) / 8;
     const uint32_t t = blockIdx.x == gridDim.x - 1 ? nfull : (blockIdx.x & 7u) * per + (blockIdx.x >> 3);
