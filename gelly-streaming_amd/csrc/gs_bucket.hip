@@ -28,6 +28,9 @@ constexpr uint32_t BK_ITEM = 1u << GS_BK_ITEM_LOG;
 
 namespace {
 
+// internal: the window does not fit the compact (32-bit offset) policy; rerun with the wide one
+constexpr gs_status GS_RETRY_WIDE = -100;
+
 struct BkMeta {   // offsets (u32 units) inside ctx->bk_meta
   static constexpr size_t HIST = 0, DBASE = HIST + BK_MAXB, BSTART = DBASE + 512, BCOUNT = BSTART + BK_MAXB + 4,
                           BITEMS = BCOUNT + BK_MAXB, BSLAB = BITEMS + BK_MAXB, MLIST = BSLAB + BK_MAXB,
@@ -164,13 +167,16 @@ gs_status bucket_accumulate(gs_ctx* c, Src rs, uint64_t R, uint32_t nb, int64_t 
   uint32_t* meta = c->bk_meta.as<uint32_t>();
   uint32_t* ns = (uint32_t*)(sm + SM_BK_N);
   GS_HIP(hipMemsetAsync(ns + 2, 0, 4, c->stream));
-  BkStage st{c->keysA.as<uint32_t>(), c->valsA.p, std::is_same_v<P, BkDeg> ? c->aux.as<int64_t>() : nullptr};
+  BkStage st{c->keysA.as<uint32_t>(), c->valsA.p,
+             (std::is_same_v<P, BkDeg> || std::is_same_v<P, BkDeg32>) ? c->aux.as<int64_t>() : nullptr};
   auto* slabs = c->bk_slabs.as<typename P::Lds>();
   hipLaunchKernelGGL((k_bk_accum<P, Src, GS_BK_UNROLL>), dim3(c->n_cu), dim3(BK_ACC_BLOCK), 0, c->stream, rs,
                      c->bk_items.as<BkItem>(), ns + 0, meta + BkMeta::BSTART, ns + 2, slabs, st, meta + BkMeta::BCOUNT);
   GS_HIP(hipGetLastError());
   hipEventRecord(c->pass_ev[ev0 + 1], c->stream);
   const unsigned mgrid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(nb, R / BK_ITEM + 1));
+  hipLaunchKernelGGL((k_bk_merge_slices<P>), dim3(mgrid, BK_MS_SLICES), dim3(BK_MS_BLOCK), 0, c->stream,
+                     meta + BkMeta::MLIST, ns + 1, meta + BkMeta::BITEMS, meta + BkMeta::BSLAB, slabs);
   hipLaunchKernelGGL((k_bk_merge<P>), dim3(mgrid), dim3(BK_ACC_BLOCK), 0, c->stream, meta + BkMeta::MLIST, ns + 1,
                      meta + BkMeta::BITEMS, meta + BkMeta::BSLAB, meta + BkMeta::BSTART, slabs, st,
                      meta + BkMeta::BCOUNT);
@@ -222,7 +228,7 @@ gs_status ensure_stage(gs_ctx* c, uint64_t R) {
   GS_TRY(ensure(c, c->keysB, R * 4));
   GS_TRY(ensure(c, c->valsA, R * std::max<size_t>(ab, 4)));
   if (P::HAS_V) GS_TRY(ensure(c, c->valsB, R * vb));
-  if (std::is_same_v<P, BkDeg>) GS_TRY(ensure(c, c->aux, R * 8));
+  if (std::is_same_v<P, BkDeg> || std::is_same_v<P, BkDeg32>) GS_TRY(ensure(c, c->aux, R * 8));
   return GS_OK;
 }
 
@@ -288,15 +294,20 @@ gs_status bucket_direct(gs_ctx* c, const int64_t* src, const int64_t* dst, const
   hipEventRecord(c->pass_ev[1], c->stream);
 
   // 3. the scatter: (16-bit bucket-local index, payload) in bucket order
+  if constexpr (P::REL) {
+    if (!part) return GS_RETRY_WIDE;   // offsets are checked by the scatter only
+  }
   GS_TRY(ensure_stage<P>(c, R));
-  using ESrc = BaseSrc<Raw, DIR, P::PAY>;
-  const ESrc es{src, dst, (const Raw*)val, base};
+  using Load = typename P::Load;
+  const BaseSrc<Load, DIR, P::PAY> ls{src, dst, (const Load*)val, base};
   uint16_t* k16 = c->keysB.as<uint16_t>();
   Raw* vpart = P::HAS_V ? c->valsB.as<Raw>() : nullptr;
+  uint32_t* rel_bad = (uint32_t*)(sm + SM_BK_N) + 3;
   if (part) {
+    if constexpr (P::REL) GS_HIP(hipMemsetAsync(rel_bad, 0, 4, c->stream));
     const unsigned grid = dp_scatter_grid<DIR>(n);
-    hipLaunchKernelGGL((k_dp_scatter<Raw, DIR, P::PAY>), dim3(grid), dim3(DP_BLOCK), 0, c->stream, es, n, S, nb,
-                       c->dp_off.as<uint32_t>(), k16, vpart);
+    hipLaunchKernelGGL((k_dp_scatter<Load, DIR, P::PAY, Raw, P::REL>), dim3(grid), dim3(DP_BLOCK), 0, c->stream, ls, n,
+                       S, nb, c->dp_off.as<uint32_t>(), k16, vpart, rel_bad);
     GS_HIP(hipGetLastError());
   }
   hipEventRecord(c->pass_ev[2], c->stream);
@@ -304,10 +315,15 @@ gs_status bucket_direct(gs_ctx* c, const int64_t* src, const int64_t* dst, const
 
   // 4-6. accumulate, merge, emit
   uint32_t n_items = 0;
-  if (part)
+  if (part) {
     GS_TRY((bucket_accumulate<P>(c, PartSrc<Raw>{k16, vpart}, R, nb, base, o, 2, U, &n_items)));
-  else
+  } else if constexpr (!P::REL) {
+    const BaseSrc<Raw, DIR, P::PAY> es{src, dst, (const Raw*)val, base};
     GS_TRY((bucket_accumulate<P>(c, es, R, nb, base, o, 2, U, &n_items)));
+  }
+  if constexpr (P::REL) {
+    if ((uint32_t)(c->host_small[5] >> 32) != 0) return GS_RETRY_WIDE;   // a neighbour outside base + 2^32
+  }
   const uint32_t key_bits = nb <= 1 ? (uint32_t)S : (uint32_t)(S + 32 - __builtin_clz(nb - 1));
   bucket_times(c, 2, part ? 1 : 0, 5, key_bits, R, *U, P::HAS_V ? sizeof(Raw) : 0, n_items);
   return GS_OK;
@@ -443,6 +459,10 @@ gs_status bucket_degree_max(gs_ctx* c, const int64_t* src, const int64_t* dst, u
                             int64_t* keys, int64_t* deg, int64_t* mx, uint64_t* U) {
   if (c->flags & GS_FLAG_SORT_ONLY) return GS_EUNSUPPORTED;
   BkDeg::Out o{keys, deg, mx, init_max};
+  if (!(c->flags & GS_FLAG_BK_ONESWEEP)) {   // neighbours as 32-bit offsets: 2^14 vertices per bucket
+    const gs_status st = bucket_dir<BkDeg32>(c, dir, src, dst, nullptr, n, o, U);
+    if (st != GS_RETRY_WIDE) return st;
+  }
   return bucket_dir<BkDeg>(c, dir, src, dst, nullptr, n, o, U);
 }
 

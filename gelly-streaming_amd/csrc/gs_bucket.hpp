@@ -68,6 +68,8 @@ __device__ __forceinline__ T bits_as(uint64_t r) {
 template <typename T, int OP>
 struct BkVal {
   using Raw = std::conditional_t<sizeof(T) == 4, uint32_t, uint64_t>;
+  using Load = Raw;                   // what the scatter loads (Raw: what it stores)
+  static constexpr bool REL = false;  // payload stored as an offset from the window base
   using A = std::conditional_t<std::is_floating_point_v<T>, double, T>;
   static constexpr int S = sizeof(A) == 8 ? 14 : 15;
   static constexpr uint32_t W = 1u << S;
@@ -121,17 +123,16 @@ struct BkVal {
     else return (s.pm[i >> 5] >> (i & 31)) & 1u;
   }
   __device__ static void stage(BkStage st, uint32_t pos, const Lds& s, uint32_t i) { ((A*)st.a)[pos] = s.acc[i]; }
-  __device__ static void merge(Lds& s, const Lds* g, int tid) {
-    for (uint32_t i = tid; i < W; i += BK_ACC_BLOCK) s.acc[i] = combine(s.acc[i], g->acc[i]);
-    for (uint32_t i = tid; i < PW; i += BK_ACC_BLOCK) s.pm[i] |= g->pm[i];
-  }
+  static constexpr uint32_t PWORDS = PW;   // presence words merged by OR
+  __device__ static void merge_el(Lds* d, const Lds* g, uint32_t i) { d->acc[i] = combine(d->acc[i], g->acc[i]); }
+  __device__ static void merge_pw(Lds* d, const Lds* g, uint32_t w) { d->pm[w] |= g->pm[w]; }
   struct Out {
     int64_t* keys;
     T* vals;
     T init;
     bool has_init;
   };
-  __device__ static void emit(const Out& o, uint64_t u, int64_t key, BkStage st, uint32_t j) {
+  __device__ static void emit(const Out& o, uint64_t u, int64_t key, BkStage st, uint32_t j, int64_t) {
     const A a = ((const A*)st.a)[j];
     o.keys[u] = key;
     if constexpr (std::is_floating_point_v<T>) {
@@ -145,6 +146,8 @@ struct BkVal {
 // COUNT: the number of incident records (foldNeighbors' init + count)
 struct BkCount {
   using Raw = uint8_t;
+  using Load = Raw;
+  static constexpr bool REL = false;
   using A = uint32_t;
   static constexpr int S = 15;
   static constexpr uint32_t W = 1u << S;
@@ -159,15 +162,15 @@ struct BkCount {
   __device__ static void add(Lds& s, uint32_t i, Raw) { atomicAdd(&s.cnt[i], 1u); }
   __device__ static bool present(const Lds& s, uint32_t i) { return s.cnt[i] != 0; }
   __device__ static void stage(BkStage st, uint32_t pos, const Lds& s, uint32_t i) { ((uint32_t*)st.a)[pos] = s.cnt[i]; }
-  __device__ static void merge(Lds& s, const Lds* g, int tid) {
-    for (uint32_t i = tid; i < W; i += BK_ACC_BLOCK) s.cnt[i] += g->cnt[i];
-  }
+  static constexpr uint32_t PWORDS = 0;
+  __device__ static void merge_el(Lds* d, const Lds* g, uint32_t i) { d->cnt[i] += g->cnt[i]; }
+  __device__ static void merge_pw(Lds*, const Lds*, uint32_t) {}
   struct Out {
     int64_t* keys;
     int64_t* vals;
     int64_t init;
   };
-  __device__ static void emit(const Out& o, uint64_t u, int64_t key, BkStage st, uint32_t j) {
+  __device__ static void emit(const Out& o, uint64_t u, int64_t key, BkStage st, uint32_t j, int64_t) {
     o.keys[u] = key;
     o.vals[u] = (int64_t)((uint64_t)o.init + ((const uint32_t*)st.a)[j]);
   }
@@ -176,6 +179,8 @@ struct BkCount {
 // degree / max-neighbour fold (TestSlice.java:233-239's shape)
 struct BkDeg {
   using Raw = uint64_t;   // neighbour ID
+  using Load = Raw;
+  static constexpr bool REL = false;
   using A = uint32_t;
   static constexpr int S = 13;
   static constexpr uint32_t W = 1u << S;
@@ -200,23 +205,69 @@ struct BkDeg {
     ((uint32_t*)st.a)[pos] = s.cnt[i];
     st.b[pos] = s.mx[i];
   }
-  __device__ static void merge(Lds& s, const Lds* g, int tid) {
-    for (uint32_t i = tid; i < W; i += BK_ACC_BLOCK) {
-      s.cnt[i] += g->cnt[i];
-      const long long m = g->mx[i];
-      if (m > s.mx[i]) s.mx[i] = m;
-    }
+  static constexpr uint32_t PWORDS = 0;
+  __device__ static void merge_el(Lds* d, const Lds* g, uint32_t i) {
+    d->cnt[i] += g->cnt[i];
+    d->mx[i] = max(d->mx[i], g->mx[i]);
   }
+  __device__ static void merge_pw(Lds*, const Lds*, uint32_t) {}
   struct Out {
     int64_t* keys;
     int64_t* deg;
     int64_t* mx;
     int64_t init_max;
   };
-  __device__ static void emit(const Out& o, uint64_t u, int64_t key, BkStage st, uint32_t j) {
+  __device__ static void emit(const Out& o, uint64_t u, int64_t key, BkStage st, uint32_t j, int64_t) {
     o.keys[u] = key;
     o.deg[u] = (int64_t)((const uint32_t*)st.a)[j];
     const int64_t m = st.b[j];
+    o.mx[u] = m > o.init_max ? m : o.init_max;
+  }
+};
+
+// degree / max-neighbour fold with the neighbour kept as a 32-bit offset from the window's vertex
+// base: 8 bytes of LDS per vertex (S = 14, half the buckets of BkDeg) and 4-byte payloads.  Valid
+// while every neighbour lies in [base, base + 2^32): k_dp_scatter flags any that does not and the
+// host reruns the window with BkDeg.
+struct BkDeg32 {
+  using Raw = uint32_t;    // stored payload: neighbour - base
+  using Load = uint64_t;   // loaded neighbour ID
+  using A = uint32_t;
+  static constexpr bool REL = true;
+  static constexpr int S = 14;
+  static constexpr uint32_t W = 1u << S;
+  static constexpr bool HAS_V = true;
+  static constexpr int PAY = PAY_NBR;
+  struct Lds {
+    uint32_t mx[W];
+    uint32_t cnt[W];
+  };
+  __device__ static void init(Lds& s, int tid) {
+    for (uint32_t i = tid; i < W; i += BK_ACC_BLOCK) {
+      s.cnt[i] = 0;
+      s.mx[i] = 0;
+    }
+  }
+  __device__ static void add(Lds& s, uint32_t i, Raw r) {
+    atomicAdd(&s.cnt[i], 1u);
+    atomicMax(&s.mx[i], r);
+  }
+  __device__ static bool present(const Lds& s, uint32_t i) { return s.cnt[i] != 0; }
+  __device__ static void stage(BkStage st, uint32_t pos, const Lds& s, uint32_t i) {
+    ((uint32_t*)st.a)[pos] = s.cnt[i];
+    st.b[pos] = s.mx[i];
+  }
+  static constexpr uint32_t PWORDS = 0;
+  __device__ static void merge_el(Lds* d, const Lds* g, uint32_t i) {
+    d->cnt[i] += g->cnt[i];
+    d->mx[i] = max(d->mx[i], g->mx[i]);
+  }
+  __device__ static void merge_pw(Lds*, const Lds*, uint32_t) {}
+  using Out = BkDeg::Out;
+  __device__ static void emit(const Out& o, uint64_t u, int64_t key, BkStage st, uint32_t j, int64_t base) {
+    o.keys[u] = key;
+    o.deg[u] = (int64_t)((const uint32_t*)st.a)[j];
+    const int64_t m = (int64_t)((uint64_t)base + (uint32_t)st.b[j]);
     o.mx[u] = m > o.init_max ? m : o.init_max;
   }
 };
@@ -623,14 +674,17 @@ __device__ __forceinline__ void dp_load_raw(const BaseSrc<V, DIR, PAY>& es, uint
 // a load under a branch gets a register copy at the join that waits for it and serialises the tile
 // (2.02 -> 1.59 ms on C2).  Measured and dropped: a persistent loop prefetching the
 // next tile (2.20 ms), 2-8 unrolled tiles per block (1.68-2.43 ms), 5120-record tiles at 2 blocks
-// per CU (1.71 ms).
-template <typename V, int DIR, int PAY>
+// per CU (1.71 ms), keys and values staged in turn through one region for 2 blocks per CU (1.81 ms
+// at 8192 records, 2.21 at 10240: the 64-VGPR cap spills).
+// V: loaded payload; VO: stored payload (REL: VO = V - base, out-of-range payloads set *rel_bad)
+template <typename V, int DIR, int PAY, typename VO = V, bool REL = false>
 __global__ __launch_bounds__(DP_BLOCK) void k_dp_scatter(BaseSrc<V, DIR, PAY> es, uint64_t n, int S, uint32_t nbp,
                                                          const uint32_t* __restrict__ off,
-                                                         uint16_t* __restrict__ k16, V* __restrict__ vout) {
+                                                         uint16_t* __restrict__ k16, VO* __restrict__ vout,
+                                                         uint32_t* __restrict__ rel_bad) {
   constexpr bool HAS_V = PAY != PAY_NONE;
   __shared__ uint32_t s_key[DP_TILE];                // (bucket << 16) | bucket-local index, bucket order
-  __shared__ V s_val[HAS_V ? DP_TILE : 1];
+  __shared__ VO s_val[HAS_V ? DP_TILE : 1];
   __shared__ uint32_t s_cnt[BK_MAXB];                // counts, then run starts inside the tile
   __shared__ uint32_t s_delta[BK_MAXB];              // global position - tile position of bucket b's run
   __shared__ uint32_t s_w[DP_BLOCK / WAVE];
@@ -640,6 +694,7 @@ __global__ __launch_bounds__(DP_BLOCK) void k_dp_scatter(BaseSrc<V, DIR, PAY> es
   const uint32_t base32 = (uint32_t)es.base, lmask = (1u << S) - 1;
   const uint32_t b0 = 2 * tid, b1 = 2 * tid + 1;   // BK_MAXB = 2 * DP_BLOCK
   const uint32_t bl0 = min(b0, nbp - 1), bl1 = min(b1, nbp - 1);
+  bool bad = false;
 
   auto process = [&](auto full, uint32_t nrec, const uint32_t (&klo)[DP_ITEMS], const V (&vv)[DP_ITEMS],
                      uint32_t o0, uint32_t o1) {
@@ -669,7 +724,13 @@ __global__ __launch_bounds__(DP_BLOCK) void k_dp_scatter(BaseSrc<V, DIR, PAY> es
       if (FULL || (uint32_t)u * DP_BLOCK + tid < nrec) {
         const uint32_t pos = s_cnt[kb[u] >> 16] + rk[u];
         s_key[pos] = kb[u];
-        if constexpr (HAS_V) s_val[pos] = vv[u];
+        if constexpr (REL) {
+          const uint64_t rel = (uint64_t)vv[u] - (uint64_t)es.base;
+          bad |= (rel >> 32) != 0;
+          s_val[pos] = (VO)rel;
+        } else if constexpr (HAS_V) {
+          s_val[pos] = vv[u];
+        }
       }
     }
     __syncthreads();
@@ -725,6 +786,9 @@ __global__ __launch_bounds__(DP_BLOCK) void k_dp_scatter(BaseSrc<V, DIR, PAY> es
     load_off(nfull, o0, o1);
     load_tile(nfull, nrec, ka, va);
     process(std::integral_constant<bool, false>{}, nrec, ka, va, o0, o1);
+  }
+  if constexpr (REL) {
+    if (__any(bad) && (threadIdx.x & 63) == 0) atomicOr(rel_bad, 1u);
   }
 }
 
@@ -813,6 +877,30 @@ __global__ __launch_bounds__(BK_ACC_BLOCK) void k_bk_accum(Src src, const BkItem
   }
 }
 
+// Slabs of a multi-item bucket merged into its first slab, BK_MS_SLICES blocks per bucket, each over
+// one slice of the vertex range (a hub bucket can leave hundreds of slabs: one block per bucket
+// merged them serially).  Fixed element -> thread map: deterministic merge order.
+constexpr uint32_t BK_MS_SLICES = 64, BK_MS_BLOCK = 256;
+template <class P>
+__global__ __launch_bounds__(BK_MS_BLOCK) void k_bk_merge_slices(const uint32_t* __restrict__ mlist,
+                                                                 const uint32_t* __restrict__ n_multi_p,
+                                                                 const uint32_t* __restrict__ b_items,
+                                                                 const uint32_t* __restrict__ b_slab,
+                                                                 typename P::Lds* __restrict__ slabs) {
+  if (blockIdx.x >= *n_multi_p) return;
+  const uint32_t b = mlist[blockIdx.x];
+  const uint32_t n = b_items[b], f = b_slab[b];
+  typename P::Lds* d = slabs + f;
+  constexpr uint32_t EL = P::W / BK_MS_SLICES, PWS = (P::PWORDS + BK_MS_SLICES - 1) / BK_MS_SLICES;
+  const uint32_t e0 = blockIdx.y * EL, w0 = blockIdx.y * PWS;
+  for (uint32_t k = 1; k < n; ++k) {
+    const typename P::Lds* g = slabs + f + k;
+    for (uint32_t i = threadIdx.x; i < EL; i += BK_MS_BLOCK) P::merge_el(d, g, e0 + i);
+    for (uint32_t w = threadIdx.x; w < PWS && w0 + w < P::PWORDS; w += BK_MS_BLOCK) P::merge_pw(d, g, w0 + w);
+  }
+}
+
+// finalize a multi-item bucket from its merged first slab
 template <class P>
 __global__ __launch_bounds__(BK_ACC_BLOCK) void k_bk_merge(const uint32_t* __restrict__ mlist,
                                                            const uint32_t* __restrict__ n_multi_p,
@@ -827,14 +915,12 @@ __global__ __launch_bounds__(BK_ACC_BLOCK) void k_bk_merge(const uint32_t* __res
   if (blockIdx.x >= *n_multi_p) return;
   const uint32_t b = mlist[blockIdx.x];
   const uint32_t n = b_items[b], f = b_slab[b];
-  // slab 0 initialises (a slab holds identities where its item saw no record)
+  (void)n;
   {
     const uint4* gs = reinterpret_cast<const uint4*>(slabs + f);
     uint4* ls = reinterpret_cast<uint4*>(&s);
     for (uint32_t i = tid; i < sizeof(typename P::Lds) / 16; i += BK_ACC_BLOCK) ls[i] = gs[i];
   }
-  __syncthreads();
-  for (uint32_t k = 1; k < n; ++k) P::merge(s, slabs + f + k, tid);   // fixed element -> thread map
   __syncthreads();
   bk_finalize<P>(s, b, bucket_start[b], st, bucket_count, s_wc);
 }
@@ -858,7 +944,7 @@ __global__ __launch_bounds__(256) void k_bk_emit(const uint32_t* __restrict__ bu
   const uint32_t n = bucket_count[b], j0 = bucket_start[b];
   for (uint32_t i = tid; i < n; i += 256) {
     const uint32_t j = j0 + i;
-    P::emit(o, off + i, (int64_t)((uint64_t)base + st.k[j]), st, j);
+    P::emit(o, off + i, (int64_t)((uint64_t)base + st.k[j]), st, j, base);
   }
   if (b == nb - 1 && tid == 0) *n_out = off + n;
 }

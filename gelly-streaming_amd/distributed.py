@@ -55,14 +55,19 @@ def exchange_sorted(keys: torch.Tensor, cols: list, group=None):
     dist.all_to_all_single(recv, send, group=group)
     send_l, recv_l = send.tolist(), recv.tolist()
     total = sum(recv_l)
-    rk = torch.empty(total, dtype=keys.dtype, device=dev)
-    dist.all_to_all_single(rk, keys, recv_l, send_l, group=group)
-    out = []
-    for c in cols:
-        rc = torch.empty(total, dtype=c.dtype, device=dev)
-        dist.all_to_all_single(rc, c.contiguous(), recv_l, send_l, group=group)
-        out.append(rc)
-    return rk, out
+    # one all-to-all of packed rows (key bytes, then each column's bytes) instead of one per column:
+    # fewer collective launches and one rendezvous per window
+    parts = [keys.contiguous()] + [c.contiguous() for c in cols]
+    widths = [p.element_size() for p in parts]
+    row = sum(widths)
+    packed = torch.cat([p.view(torch.uint8).view(-1, w) for p, w in zip(parts, widths)], dim=1)
+    rp = torch.empty((total, row), dtype=torch.uint8, device=dev)
+    dist.all_to_all_single(rp, packed, recv_l, send_l, group=group)
+    out, at = [], 0
+    for p, w in zip(parts, widths):
+        out.append(rp[:, at:at + w].contiguous().view(p.dtype).view(-1))
+        at += w
+    return out[0], out[1:]
 
 
 def reduce_window(local_reduce, src, dst, val, direction: int, op: int, group=None):

@@ -205,3 +205,19 @@ def test_bucket_large_rmat_properties(engine):
     assert int(x.sum()) == 2 * int(v.sum())
     k2, c = engine.reduce(s, d, v, 2, 3)
     assert torch.equal(k, k2) and int(c.sum()) == 2 * n
+
+
+@pytest.mark.parametrize("direction", [0, 1, 2])
+def test_degree_max_far_neighbours(engine, oracle, direction):
+    """Keys in a small range, neighbours 2^40 away: the 32-bit neighbour offsets of the compact
+    degree/max policy do not fit, the scatter flags it and the window reruns with 64-bit maxima."""
+    rng = np.random.default_rng(31 + direction)
+    n = 90000
+    s = rng.integers(0, 1 << 20, n).astype(np.int64)
+    d = rng.integers(0, 1 << 20, n).astype(np.int64)
+    d[::7] += 1 << 40
+    for init_max in (np.iinfo(np.int64).min, 1 << 41):
+        rk, rd, rm = oracle.window_fold_degree_max(s, d, direction, init_max)
+        gk, gd, gm = engine.fold_degree_max(*_dev(s, d), direction, init_max)
+        assert np.array_equal(gk.cpu().numpy(), rk)
+        assert np.array_equal(gd.cpu().numpy(), rd) and np.array_equal(gm.cpu().numpy(), rm)
