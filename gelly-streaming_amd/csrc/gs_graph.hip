@@ -4,6 +4,7 @@
 //   gs_window_candidates <- applyOnNeighbors(GenerateCandidateEdges)   (WindowTriangles.java:83-116)
 //   gs_window_triangles  <- slice(ALL) -> candidates -> CountTriangles -> sum(0) (WindowTriangles.java:61-66)
 #include "gs_ops.hpp"
+#include "gs_tricount.hpp"
 
 namespace gs {
 
@@ -167,39 +168,6 @@ __global__ __launch_bounds__(SCAN_BLOCK) void k_orient_scatter(const uint64_t* _
   if (blockIdx.x == gridDim.x - 1 && threadIdx.x == SCAN_BLOCK - 1) pos[E2] = tile_off[gridDim.x];
 }
 
-// sum over oriented edges u -> v of |N+(u) ∩ N+(v)| (sorted lists: merge)
-__global__ __launch_bounds__(256) void k_tri_count(const uint32_t* __restrict__ ou, const uint32_t* __restrict__ onbr,
-                                                   uint32_t q0, uint32_t M, const uint32_t* __restrict__ deg,
-                                                   const uint32_t* __restrict__ rowstart,
-                                                   const uint32_t* __restrict__ pos,
-                                                   unsigned long long* __restrict__ total) {
-  uint64_t t = 0;
-  for (uint32_t q = q0 + blockIdx.x * 256u + threadIdx.x; q < M; q += gridDim.x * 256u) {
-    const uint32_t u = ou[q], v = onbr[q];
-    uint32_t a = pos[rowstart[u]], a1 = pos[rowstart[u] + deg[u]];
-    uint32_t b = pos[rowstart[v]], b1 = pos[rowstart[v] + deg[v]];
-    if (a == a1 || b == b1) continue;
-    uint32_t x = onbr[a], y = onbr[b];
-    while (true) {
-      if (x < y) {
-        if (++a == a1) break;
-        x = onbr[a];
-      } else if (x > y) {
-        if (++b == b1) break;
-        y = onbr[b];
-      } else {
-        ++t;
-        if (++a == a1 || ++b == b1) break;
-        x = onbr[a];
-        y = onbr[b];
-      }
-    }
-  }
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) t += __shfl_xor(t, o, 64);
-  if ((threadIdx.x & 63) == 0 && t) atomicAdd(total, (unsigned long long)t);
-}
-
 }  // namespace gs
 
 using namespace gs;
@@ -339,6 +307,9 @@ static gs_status triangles_impl(gs_ctx* c, const gs_edge_batch* b, uint32_t part
   adj.wide = true;
   adj.key_xor = 0;
   adj.records = E2;
+  GS_HIP(hipMemsetAsync(c->out_a.p, 0, V * 4, c->stream));   // vertices without edges: degree 0
+  GS_TRY(ensure(c, c->tri_heavy, V * 4));
+  GS_TRY(ensure(c, c->tri_range, V * 8));
   RowOut ro{c->out_a.as<uint32_t>(), c->out_b.as<uint32_t>()};
   uint64_t nv = 0;
   GS_TRY((launch_rbk<uint64_t, CountOp>(c, adj, ro, &nv, B)));
@@ -357,15 +328,21 @@ static gs_status triangles_impl(gs_ctx* c, const gs_edge_batch* b, uint32_t part
                      c->tri_pos.as<uint32_t>(), c->tri_ou.as<uint32_t>(), c->tri_onbr.as<uint32_t>());
   GS_HIP(hipGetLastError());
   const uint64_t M = E2 / 2;   // each undirected edge kept in exactly one direction
-  // 5. merge intersections
+  // 5. intersections: vertex-centric LDS hash sets (k_tri_light), long out-lists in k_tri_heavy
   unsigned long long* d_total = (unsigned long long*)(sm + SM_NUNIQUE);
+  uint32_t* d_nheavy = (uint32_t*)(sm + SM_COUNTERS) + 62;
   GS_HIP(hipMemsetAsync(d_total, 0, 8, c->stream));
+  GS_HIP(hipMemsetAsync(d_nheavy, 0, 4, c->stream));
   const uint64_t q0 = M * part / nparts, q1 = M * (part + 1) / nparts;   // this part's oriented edges
-  const unsigned g2 = (unsigned)std::min<uint64_t>((q1 - q0 + 255) / 256, 16384);
-  hipLaunchKernelGGL(k_tri_count, dim3(std::max(1u, g2)), dim3(256), 0, c->stream, c->tri_ou.as<uint32_t>(),
-                     c->tri_onbr.as<uint32_t>(), (uint32_t)q0, (uint32_t)q1, c->out_a.as<uint32_t>(),
-                     c->out_b.as<uint32_t>(),
-                     c->tri_pos.as<uint32_t>(), d_total);
+  uint2* range = reinterpret_cast<uint2*>(c->tri_range.p);
+  hipLaunchKernelGGL(k_tri_rows, dim3((unsigned)std::min<uint64_t>((V + 255) / 256, 4096)), dim3(256), 0, c->stream,
+                     c->out_a.as<uint32_t>(), c->out_b.as<uint32_t>(), c->tri_pos.as<uint32_t>(), (uint32_t)V, range);
+  const unsigned nvb = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((V + TH_WPB - 1) / TH_WPB, 8192));
+  hipLaunchKernelGGL(k_tri_light, dim3(nvb), dim3(TH_BLOCK), 0, c->stream, c->tri_onbr.as<uint32_t>(), range,
+                     (uint32_t)V, (uint32_t)q0, (uint32_t)q1, c->tri_heavy.as<uint32_t>(), d_nheavy, d_total);
+  GS_HIP(hipGetLastError());
+  hipLaunchKernelGGL(k_tri_heavy, dim3(256), dim3(TH_HBLOCK), 0, c->stream, c->tri_onbr.as<uint32_t>(), range,
+                     c->tri_heavy.as<uint32_t>(), d_nheavy, d_total);
   GS_HIP(hipGetLastError());
   hipEventRecord(c->ev[3], c->stream);
   GS_HIP(hipMemcpyAsync(c->host_small, sm, 32, hipMemcpyDeviceToHost, c->stream));

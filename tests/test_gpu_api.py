@@ -91,7 +91,7 @@ def test_windowing_event_time(pkg, oracle):
     assert got == want
 
 
-@pytest.mark.parametrize("kind", ["uniform_c1", "rmat", "dense_small", "multi_edges"])
+@pytest.mark.parametrize("kind", ["uniform_c1", "rmat", "dense_small", "multi_edges", "heavy"])
 def test_triangles_vs_oracle(engine, oracle, kind):
     if kind == "uniform_c1":      # BASELINE C1 shape: uniform V=2^16, 1M edges, no self-loops
         s, d = oracle.gen_uniform(1 << 16, 1_000_000, 0x5EED01)
@@ -99,12 +99,39 @@ def test_triangles_vs_oracle(engine, oracle, kind):
         s, d = oracle.gen_rmat(14, 200_000, 0x5EED04, no_self_loops=True)
     elif kind == "dense_small":
         s, d = oracle.gen_uniform(40, 2000, 9)
+    elif kind == "heavy":         # dense: oriented out-degrees > TH_DMAX (512) take k_tri_heavy
+        rng = np.random.default_rng(11)
+        a, b = rng.integers(0, 1500, 900_000), rng.integers(0, 1500, 900_000)
+        keep = a != b
+        s, d = a[keep].astype(np.int64), b[keep].astype(np.int64)
     else:
         s0, d0 = oracle.gen_uniform(300, 5000, 10)
         s, d = np.concatenate([s0, d0, s0]), np.concatenate([d0, s0, d0])   # duplicates + reversed copies
     w_fwd, ex_fwd, has = oracle.window_triangles_fwd(s, d)
     ex, wrapped, has_g = engine.triangles(*[torch.from_numpy(x).cuda() for x in (s, d)])
     assert (ex, wrapped, has_g) == (ex_fwd, w_fwd, has)
+
+
+def _clique(n, shuffle_seed):
+    iu = np.triu_indices(n, 1)
+    s, d = iu[0].astype(np.int64) * 31 + 5, iu[1].astype(np.int64) * 31 + 5
+    p = np.random.default_rng(shuffle_seed).permutation(len(s))
+    return s[p], d[p]
+
+
+def test_triangles_clique_hub_chunks(engine, oracle):
+    """K_n has C(n, 3) triangles (pinned on K_30 by the oracle).  On K_4200 the (degree, id) orientation
+    gives out-lists up to 4199 > TH_VCH (4096): k_tri_heavy's several v chunks."""
+    from math import comb
+    s, d = _clique(30, 1)
+    w, ex, has = oracle.window_triangles_fwd(s, d)
+    assert (ex, has) == (comb(30, 3), True)
+    n = 4200
+    s, d = _clique(n, 2)
+    ex, wrapped, has = engine.triangles(*[torch.from_numpy(x).cuda() for x in (s, d)])
+    want = comb(n, 3)
+    w32 = want & 0xFFFFFFFF
+    assert (ex, wrapped, has) == (want, w32 - (1 << 32) if w32 >= (1 << 31) else w32, True)
 
 
 def test_triangles_matches_reference_rule(engine, oracle):
