@@ -41,18 +41,29 @@ __global__ __launch_bounds__(256) void k_tri_rows(const uint32_t* __restrict__ d
   }
 }
 
-constexpr int TH_ILP = 4;   // independent probes in flight per lane
+constexpr int TH_ILP = 4;   // consecutive items per lane: one search, TH_ILP probes in flight
+
+// N+(u) as an LDS hash set of 4-slot buckets (one 16-byte read answers almost every probe)
+__device__ __forceinline__ void th_insert(uint32_t* hs, uint32_t x, uint32_t bmask) {
+  for (uint32_t b = th_hash(x, bmask);; b = (b + 1) & bmask) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (atomicCAS(&hs[b * 4 + j], TH_EMPTY, x) == TH_EMPTY) return;
+  }
+}
 
 __global__ __launch_bounds__(TH_BLOCK) void k_tri_light(const uint32_t* __restrict__ onbr,
                                                         const uint2* __restrict__ range, uint32_t nv, uint32_t q0,
                                                         uint32_t q1, uint32_t* __restrict__ heavy,
                                                         uint32_t* __restrict__ n_heavy,
                                                         unsigned long long* __restrict__ total) {
-  __shared__ uint32_t s_hash[TH_WPB][TH_H];
-  __shared__ uint32_t s_off[TH_WPB][TH_DMAX + 1];   // exclusive prefix of |N+(v)|, v = i-th of N+(u)
-  __shared__ uint32_t s_st[TH_WPB][TH_DMAX];        // start of N+(v)
+  // 8 KiB per wave, 32 KiB per block: five blocks per CU
+  __shared__ uint4 s_hash[TH_WPB][TH_H / 4];
+  __shared__ uint32_t s_off[TH_WPB][TH_DMAX];   // exclusive prefix of |N+(v)| over the non-empty v of N+(u)
+  __shared__ uint32_t s_st[TH_WPB][TH_DMAX];    // start of that N+(v) in onbr
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  uint32_t* hs = s_hash[w];
+  uint4* hb = s_hash[w];
+  uint32_t* hs = reinterpret_cast<uint32_t*>(hb);
   uint32_t* po = s_off[w];
   uint32_t* ps = s_st[w];
   const uint32_t nw = gridDim.x * TH_WPB;
@@ -65,58 +76,88 @@ __global__ __launch_bounds__(TH_BLOCK) void k_tri_light(const uint32_t* __restri
       if (lane == 0) heavy[atomicAdd(n_heavy, 1u)] = u;
       continue;
     }
-    uint32_t hsize = 64;
-    while (hsize < 2 * d) hsize <<= 1;
-    const uint32_t mask = hsize - 1;
-    for (uint32_t i = lane; i < hsize; i += WAVE) hs[i] = TH_EMPTY;
+    uint32_t nb = 16;
+    while (nb < d && nb < TH_H / 4) nb <<= 1;
+    const uint32_t bmask = nb - 1;
+    for (uint32_t i = lane; i < nb * 4; i += WAVE) hs[i] = TH_EMPTY;
     wave_lds_sync();
-    uint32_t run = 0;
+    uint32_t run = 0, dn = 0;
     for (uint32_t i0 = 0; i0 < d; i0 += WAVE) {
       const uint32_t i = i0 + lane;
-      uint32_t dv = 0;
+      uint32_t dv = 0, sv = 0;
       if (i < d) {
         const uint32_t x = onbr[s + i];
-        uint32_t slot = th_hash(x, mask);
-        while (atomicCAS(&hs[slot], TH_EMPTY, x) != TH_EMPTY) slot = (slot + 1) & mask;
+        th_insert(hs, x, bmask);
         const uint2 rv = range[x];
         dv = rv.y - rv.x;
-        ps[i] = rv.x;
+        sv = rv.x;
       }
+      // keep only the v with a non-empty out-list: every kept list spans >= 1 item
+      const uint64_t ne = __ballot(dv != 0);
+      const uint32_t at = dn + (uint32_t)__builtin_amdgcn_mbcnt_hi((uint32_t)(ne >> 32),
+                                                                   __builtin_amdgcn_mbcnt_lo((uint32_t)ne, 0u));
       const uint32_t inc = wave_inclusive_sum(dv);
-      if (i < d) po[i] = run + inc - dv;
+      if (dv) {
+        po[at] = run + inc - dv;
+        ps[at] = sv;
+      }
       run += __shfl(inc, WAVE - 1, WAVE);
+      dn += (uint32_t)__popcll(ne);
     }
-    if (lane == 0) po[d] = run;   // > every item index: the clamped search below never passes it
     wave_lds_sync();
     uint32_t top = 1;
-    while (2 * top < d) top <<= 1;
+    while (2 * top < dn) top <<= 1;
     for (uint32_t k0 = 0; k0 < run; k0 += WAVE * TH_ILP) {
-      uint32_t k[TH_ILP], lo[TH_ILP], x[TH_ILP], sl[TH_ILP], y[TH_ILP];
+      const uint32_t kb = k0 + lane * TH_ILP;
+      const uint32_t kk = min(kb, run - 1);
+      // last kept v with po <= kk (po[dn] reads as run, above every item)
+      uint32_t lo = 0;
+      for (uint32_t st = top; st; st >>= 1) {
+        const uint32_t t = lo + st;
+        const uint32_t pv = t < dn ? po[min(t, dn - 1)] : run;
+        lo = pv <= kk ? t : lo;
+      }
+      // the next TH_ILP-1 boundaries (each list >= 1 item: at most that many crossed)
+      uint32_t bo[TH_ILP], bs[TH_ILP];
+#pragma unroll
+      for (int t = 0; t < TH_ILP; ++t) {
+        const uint32_t q = lo + t;
+        bo[t] = q < dn ? po[min(q, dn - 1)] : run;
+        bs[t] = ps[min(q, dn - 1)];
+      }
+      uint32_t x[TH_ILP];
 #pragma unroll
       for (int j = 0; j < TH_ILP; ++j) {
-        k[j] = min(k0 + j * WAVE + lane, run - 1);
-        lo[j] = 0;
+        const uint32_t kj = min(kb + j, run - 1);
+        uint32_t o = bo[0], st = bs[0];
+#pragma unroll
+        for (int t = 1; t < TH_ILP; ++t) {
+          o = bo[t] <= kj ? bo[t] : o;
+          st = bo[t] <= kj ? bs[t] : st;
+        }
+        x[j] = onbr[st + (kj - o)];
       }
-      for (uint32_t st = top; st; st >>= 1)   // last i with po[i] <= k, branchless, TH_ILP in lock step
+      uint32_t b[TH_ILP], pend = 0;
+#pragma unroll
+      for (int j = 0; j < TH_ILP; ++j) {
+        b[j] = th_hash(x[j], bmask);
+        pend |= (kb + j < run ? 1u : 0u) << j;
+      }
+      while (pend) {   // all pending probes of the lane read their bucket together
+        uint4 y[TH_ILP];
+#pragma unroll
+        for (int j = 0; j < TH_ILP; ++j) y[j] = hb[b[j]];
 #pragma unroll
         for (int j = 0; j < TH_ILP; ++j) {
-          const uint32_t t = lo[j] + st;
-          lo[j] = po[min(t, d)] <= k[j] ? t : lo[j];
+          if (!(pend >> j & 1)) continue;
+          const bool hit = y[j].x == x[j] || y[j].y == x[j] || y[j].z == x[j] || y[j].w == x[j];
+          const bool open = y[j].w == TH_EMPTY;   // slots fill in order: a free last slot ends the chain
+          if (hit || open) {
+            cnt += hit ? 1u : 0u;
+            pend &= ~(1u << j);
+          }
+          b[j] = (b[j] + 1) & bmask;
         }
-#pragma unroll
-      for (int j = 0; j < TH_ILP; ++j) x[j] = onbr[ps[lo[j]] + (k[j] - po[lo[j]])];
-#pragma unroll
-      for (int j = 0; j < TH_ILP; ++j) {
-        sl[j] = th_hash(x[j], mask);
-        y[j] = hs[sl[j]];
-      }
-#pragma unroll
-      for (int j = 0; j < TH_ILP; ++j) {
-        while (y[j] != x[j] && y[j] != TH_EMPTY) {
-          sl[j] = (sl[j] + 1) & mask;
-          y[j] = hs[sl[j]];
-        }
-        cnt += (y[j] == x[j] && k0 + j * WAVE + lane < run) ? 1u : 0u;
       }
     }
     wave_lds_sync();
