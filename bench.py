@@ -132,6 +132,28 @@ def direct_kernel_table(times_list, E, U_avg):
     return rows, mean(lambda t: t.partials)
 
 
+def triangle_kernel_table(times_list, n):
+    """WindowTriangles (stage_times path 3): algorithmic bytes per stage as in DESIGN.md §4 —
+    n input edges, E2 unique adjacency entries, M = E2 / 2 oriented edges, P hash probes."""
+    mean = lambda f: statistics.mean(f(t) for t in times_list)
+    E2 = mean(lambda t: t.records)
+    M, P, V = E2 / 2, mean(lambda t: t.partials), mean(lambda t: t.vertices)
+    rows = {
+        # edge list in, symmetric keys out, one read + write of the 2n keys
+        "tri_sym+sort": {"ms": mean(lambda t: t.pass_ms[0]), "bytes": 16 * n + 16 * n + 32 * n},
+        "tri_unique": {"ms": mean(lambda t: t.pass_ms[1]), "bytes": 16 * n + 8 * E2},
+        # rows (read keys, degree + row start out), keep flags (keys + two degrees), compaction
+        "tri_rows+orient": {"ms": mean(lambda t: t.pass_ms[2]), "bytes": 8 * E2 + 8 * V + 17 * E2 + 17 * E2},
+        # N+(v) and the in-list of each v (4 + 4 B), out-range of each in-neighbour (8 B), one 4-byte
+        # list item per probe
+        "tri_count(light+heavy)": {"ms": mean(lambda t: t.pass_ms[3] + t.pass_ms[4]), "bytes": 16 * M + 4 * P},
+    }
+    for r in rows.values():
+        r["GB/s"] = r["bytes"] / (r["ms"] * 1e-3) / 1e9 if r["ms"] > 0 else 0.0
+        r["frac"] = r["GB/s"] / HBM_PEAK_GBS
+    return rows, P
+
+
 def pmc_traffic(kernel: str):
     f = ROOT / "profiles" / "pmc_traffic.json"
     if not f.exists():
@@ -167,6 +189,33 @@ def cpu_baseline(src, dst, val, sample_log2: int):
             "sample": f"first 2^{sample_log2} edges of the same R-MAT window, keyBy over {threads} threads + "
                       f"per-subtask hash-map fold (oracle/gs_oracle.c gso_baseline_reduce), median of 3",
             "single_core_value": S1 / t1}
+
+
+def cpu_baseline_triangles(src, dst, max_candidates=40_000_000, max_log2=22, budget_s=4.0):
+    """The reference's WindowTriangles rule restated by the oracle (GenerateCandidateEdges with HashSet
+    order -> pair-keyed CountTriangles -> Integer sum; gso_window_triangles_ref, one thread) on the
+    first 2^k edges of the same window: k doubles from 16 while one run stays under budget_s and the
+    candidate count under max_candidates; the largest sample is reported."""
+    orc = ge.load_oracle()
+    best = None
+    for k in range(16, max_log2 + 1):
+        S = min(1 << k, src.numel())
+        s, d = src[:S].cpu().numpy(), dst[:S].cpu().numpy()
+        if orc.candidate_count(s, d) > max_candidates:
+            break
+        t = time.perf_counter()
+        orc.window_triangles_ref(s, d)
+        dt = time.perf_counter() - t
+        best = (k, S, dt)
+        if dt > budget_s or S == src.numel():
+            break
+    if best is None:
+        return None
+    k, S, dt = best
+    return {"value": S / dt, "unit": "edges/s", "cores": 1, "kind": "port",
+            "sample": f"first 2^{k} edges of the same window, the reference's candidate rule "
+                      f"(oracle/gs_oracle.c gso_window_triangles_ref: candidates in HashSet order, pair-keyed "
+                      f"count, Integer sum), one thread, {dt:.2f} s"}
 
 
 def main():
@@ -263,11 +312,10 @@ def main():
     # local window only: the dominant kernel of the single-GPU pipeline
     E_rec = times[0].records
     U_avg = times[0].vertices
-    kt, partials = kernel_table(times, E_rec, U_avg) if a.workload != "triangles" else ({}, 0)
-    if not kt:   # triangles: the stage table does not apply; report the whole window
-        kt = {"window_triangles": {"ms": elapsed / a.steps * 1e3, "bytes": E * 16, "GB/s": 0.0, "frac": 0.0}}
-        kt["window_triangles"]["GB/s"] = kt["window_triangles"]["bytes"] / (kt["window_triangles"]["ms"] * 1e-3) / 1e9
-        kt["window_triangles"]["frac"] = kt["window_triangles"]["GB/s"] / HBM_PEAK_GBS
+    if a.workload == "triangles":
+        kt, partials = triangle_kernel_table(times, E * world)
+    else:
+        kt, partials = kernel_table(times, E_rec, U_avg)
     dom_name = max((n for n in kt if "host sync" not in n), key=lambda n: kt[n]["ms"])
     dom = kt[dom_name]
     roofline = {"bound": "hbm", "kernel": dom_name, "achieved": round(dom["GB/s"], 1), "peak": HBM_PEAK_GBS,
@@ -275,8 +323,11 @@ def main():
                 "algorithmic_bytes_per_launch": dom["bytes"], "avg_launch_ms": round(dom["ms"], 4)}
 
     cpu = None
-    if world == 1 and rank == 0 and not a.no_cpu_baseline and a.workload == "reduce":
-        cpu = cpu_baseline(src, dst, val, a.cpu_sample_log2)
+    if world == 1 and rank == 0 and not a.no_cpu_baseline:
+        if a.workload == "reduce":
+            cpu = cpu_baseline(src, dst, val, a.cpu_sample_log2)
+        elif a.workload == "triangles":
+            cpu = cpu_baseline_triangles(src, dst)
 
     if rank == 0:
         total_edges = E * world * a.steps
@@ -296,10 +347,12 @@ def main():
             "config": {"workload": {"reduce": f"C2: slice(OUT).reduceOnEdges(SUM) over one R-MAT scale-{a.scale} window",
                                     "fold": f"C3: slice(OUT).foldNeighbors(degree, max neighbour), skewed R-MAT scale-{a.scale}",
                                     "triangles": f"C4 shape: WindowTriangles over an R-MAT scale-{a.scale} window"}[a.workload],
-                       "scale": a.scale, "edges_per_window_per_gpu": E, "direction": "OUT", "op": "SUM",
+                       "scale": a.scale, "edges_per_window_per_gpu": E,
+                       "direction": "ALL" if a.workload == "triangles" else "OUT",
+                       "op": {"reduce": "SUM", "fold": "DegreeMaxNeighbor", "triangles": "count"}[a.workload],
                        "value_dtype": a.dtype, "vertices_out": U_avg, "sort_passes": times[0].sort_passes,
                        "key_bits": times[0].key_bits, "partials_after_fused_pass": int(partials),
-                       "pipeline": {0: "sort", 1: "bucket-onesweep", 2: "bucket-direct"}[times[0].path],
+                       "pipeline": {0: "sort", 1: "bucket-onesweep", 2: "bucket-direct", 3: "triangles"}[times[0].path],
                        "parallelism": (f"vertex-range keyBy over {world} GPU(s), RCCL all-to-all" if dist
                                        else "1 GPU")},
             "roofline": roofline,

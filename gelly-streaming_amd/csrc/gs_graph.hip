@@ -130,11 +130,12 @@ __global__ __launch_bounds__(1024) void k_scan_tiles(uint32_t* __restrict__ tile
   if (threadIdx.x == 0) tile_sum[ntiles] = carry;
 }
 
-// pos[p] = #kept before p (pos[E2] = M); compacted oriented edges (ou, onbr), order preserved
+// pos[p] = #kept before p (pos[E2] = M); kept entries compact into onbr (out-lists), the others into
+// inbr (in-lists, at p - pos[p]); order preserved
 __global__ __launch_bounds__(SCAN_BLOCK) void k_orient_scatter(const uint64_t* __restrict__ adj, uint32_t E2, uint32_t B,
                                                                const uint8_t* __restrict__ keep,
                                                                const uint32_t* __restrict__ tile_off,
-                                                               uint32_t* __restrict__ pos, uint32_t* __restrict__ ou,
+                                                               uint32_t* __restrict__ pos, uint32_t* __restrict__ inbr,
                                                                uint32_t* __restrict__ onbr) {
   __shared__ uint32_t ws[SCAN_BLOCK / 64];
   const uint64_t mask = (1ull << B) - 1;
@@ -157,12 +158,9 @@ __global__ __launch_bounds__(SCAN_BLOCK) void k_orient_scatter(const uint64_t* _
     const uint32_t p = first + j;
     if (p < E2) {
       pos[p] = off;
-      if (keep[p]) {
-        const uint64_t k = adj[p];
-        ou[off] = (uint32_t)(k >> B);
-        onbr[off] = (uint32_t)(k & mask);
-        ++off;
-      }
+      const uint32_t x = (uint32_t)(adj[p] & mask);
+      if (keep[p]) onbr[off++] = x;
+      else inbr[p - off] = x;
     }
   }
   if (blockIdx.x == gridDim.x - 1 && threadIdx.x == SCAN_BLOCK - 1) pos[E2] = tile_off[gridDim.x];
@@ -286,11 +284,13 @@ static gs_status triangles_impl(gs_ctx* c, const gs_edge_batch* b, uint32_t part
   // 2. sort + unique -> symmetric simple adjacency, sorted by (u, v)
   Sorted s;
   GS_TRY(sort_buffer(c, c->aux.as<uint64_t>(), nullptr, R, &s));
+  hipEventRecord(c->ev[1], c->stream);
   const uint64_t loops = c->host_small[4];
   GS_TRY(ensure(c, c->out_keys, R * 8));
   uint64_t E2 = 0;
   UniqueOut uo{c->out_keys.as<uint64_t>(), nullptr};
   GS_TRY((s.wide ? launch_rbk<uint64_t, CountOp>(c, s, uo, &E2) : launch_rbk<uint32_t, CountOp>(c, s, uo, &E2)));
+  hipEventRecord(c->ev[2], c->stream);
   if (loops) E2 -= 1;   // the self-loop sentinel sorts last
   if (E2 == 0) {        // only self-loops: no triangle; the self-pair term needs >= 2 neighbours
     uint64_t S = 0;
@@ -309,7 +309,7 @@ static gs_status triangles_impl(gs_ctx* c, const gs_edge_batch* b, uint32_t part
   adj.records = E2;
   GS_HIP(hipMemsetAsync(c->out_a.p, 0, V * 4, c->stream));   // vertices without edges: degree 0
   GS_TRY(ensure(c, c->tri_heavy, V * 4));
-  GS_TRY(ensure(c, c->tri_range, V * 8));
+  GS_TRY(ensure(c, c->tri_range, V * 16));
   RowOut ro{c->out_a.as<uint32_t>(), c->out_b.as<uint32_t>()};
   uint64_t nv = 0;
   GS_TRY((launch_rbk<uint64_t, CountOp>(c, adj, ro, &nv, B)));
@@ -327,28 +327,57 @@ static gs_status triangles_impl(gs_ctx* c, const gs_edge_batch* b, uint32_t part
                      (uint32_t)E2, B, c->tri_keep.as<uint8_t>(), c->tri_tiles.as<uint32_t>(),
                      c->tri_pos.as<uint32_t>(), c->tri_ou.as<uint32_t>(), c->tri_onbr.as<uint32_t>());
   GS_HIP(hipGetLastError());
+  hipEventRecord(c->ev[4], c->stream);
   const uint64_t M = E2 / 2;   // each undirected edge kept in exactly one direction
+  GS_TRY(ensure(c, c->tri_queue, (M / TH_DMAX + 64) * 8));   // further in-list chunks: <= M / TH_DMAX
   // 5. intersections: vertex-centric LDS hash sets (k_tri_light), long out-lists in k_tri_heavy
   unsigned long long* d_total = (unsigned long long*)(sm + SM_NUNIQUE);
   uint32_t* d_nheavy = (uint32_t*)(sm + SM_COUNTERS) + 62;
+  unsigned long long* d_probes = (unsigned long long*)(sm + SM_TRI_PROBES);
   GS_HIP(hipMemsetAsync(d_total, 0, 8, c->stream));
+  GS_HIP(hipMemsetAsync(d_probes, 0, 8, c->stream));
   GS_HIP(hipMemsetAsync(d_nheavy, 0, 4, c->stream));
   const uint64_t q0 = M * part / nparts, q1 = M * (part + 1) / nparts;   // this part's oriented edges
-  uint2* range = reinterpret_cast<uint2*>(c->tri_range.p);
+  uint2* out_range = reinterpret_cast<uint2*>(c->tri_range.p);
+  uint2* in_range = out_range + V;
+  uint32_t* d_nqueue = d_nheavy + 1;
+  GS_HIP(hipMemsetAsync(d_nqueue, 0, 4, c->stream));
   hipLaunchKernelGGL(k_tri_rows, dim3((unsigned)std::min<uint64_t>((V + 255) / 256, 4096)), dim3(256), 0, c->stream,
-                     c->out_a.as<uint32_t>(), c->out_b.as<uint32_t>(), c->tri_pos.as<uint32_t>(), (uint32_t)V, range);
+                     c->out_a.as<uint32_t>(), c->out_b.as<uint32_t>(), c->tri_pos.as<uint32_t>(), (uint32_t)V,
+                     out_range, in_range);
   const unsigned nvb = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((V + TH_WPB - 1) / TH_WPB, 8192));
-  hipLaunchKernelGGL(k_tri_light, dim3(nvb), dim3(TH_BLOCK), 0, c->stream, c->tri_onbr.as<uint32_t>(), range,
-                     (uint32_t)V, (uint32_t)q0, (uint32_t)q1, c->tri_heavy.as<uint32_t>(), d_nheavy, d_total);
-  GS_HIP(hipGetLastError());
-  hipLaunchKernelGGL(k_tri_heavy, dim3(256), dim3(TH_HBLOCK), 0, c->stream, c->tri_onbr.as<uint32_t>(), range,
-                     c->tri_heavy.as<uint32_t>(), d_nheavy, d_total);
+  uint2* queue = c->tri_queue.as<uint2>();
+  for (int pass = 0; pass < 2; ++pass) {
+    hipLaunchKernelGGL(k_tri_light, dim3(pass == 0 ? nvb : 4096u), dim3(TH_BLOCK), 0, c->stream,
+                       c->tri_onbr.as<uint32_t>(), c->tri_ou.as<uint32_t>(), out_range, in_range, (uint32_t)V,
+                       (uint32_t)q0, (uint32_t)q1, pass, queue, d_nqueue, c->tri_heavy.as<uint32_t>(), d_nheavy,
+                       d_total, d_probes);
+    GS_HIP(hipGetLastError());
+  }
+  hipEventRecord(c->ev[5], c->stream);
+  hipLaunchKernelGGL(k_tri_heavy, dim3(256), dim3(TH_HBLOCK), 0, c->stream, c->tri_onbr.as<uint32_t>(),
+                     c->tri_ou.as<uint32_t>(), out_range, in_range, c->tri_heavy.as<uint32_t>(), d_nheavy, d_total,
+                     d_probes);
   GS_HIP(hipGetLastError());
   hipEventRecord(c->ev[3], c->stream);
   GS_HIP(hipMemcpyAsync(c->host_small, sm, 32, hipMemcpyDeviceToHost, c->stream));
+  GS_HIP(hipMemcpyAsync(c->host_small + 6, d_probes, 8, hipMemcpyDeviceToHost, c->stream));
   GS_HIP(hipStreamSynchronize(c->stream));
   if ((uint32_t)c->host_small[3] != 0) return set_error(c, GS_EDEVICE, "look-back spin timed out");
   uint64_t T = c->host_small[2];
+  {   // stage times (path 3): sym + sort, unique, rows + orientation, light count, heavy count
+    gs_stage_times& t = c->times;
+    t = gs_stage_times{};
+    const int order[6] = {0, 1, 2, 4, 5, 3};
+    for (int i = 0; i < 5; ++i) hipEventElapsedTime(&t.pass_ms[i], c->ev[order[i]], c->ev[order[i + 1]]);
+    hipEventElapsedTime(&t.total_ms, c->ev[0], c->ev[3]);
+    t.sort_passes = (uint32_t)s.passes;
+    t.key_bits = B;
+    t.records = E2;
+    t.vertices = nv;
+    t.partials = c->host_small[6];
+    t.path = 3;
+  }
   if (loops && part == 0) {   // self-pair candidates (x, x, true) matched by a self-loop on x (:105)
     uint64_t S = 0;
     GS_TRY(triangle_selfpair_term(c, src, dst, n, c->tri_loops.as<uint32_t>(), key_xor, &S));

@@ -55,7 +55,7 @@ struct gs_ctx {
   // fused last pass: partials with gaps, compacted partials
   gs::DevBuf part_k, part_a, comp_k, comp_a;
   // triangles
-  gs::DevBuf tri_loops, tri_keep, tri_tiles, tri_pos, tri_ou, tri_onbr, tri_heavy, tri_range;
+  gs::DevBuf tri_loops, tri_keep, tri_tiles, tri_pos, tri_ou, tri_onbr, tri_heavy, tri_range, tri_queue;
   // HashSet-order pipeline (gs_hashset.hip)
   gs::DevBuf hs[20];
   // bucket path (gs_bucket.hip): plan tables, work items, LDS slabs of multi-item buckets
@@ -82,7 +82,8 @@ constexpr size_t SM_TOTAL = SM_BASE + 8 * 256 * 4;   // u64 partial count of the
 constexpr size_t SM_TABLE = SM_TOTAL + 64;            // u32[513] region table of the fused pass
 constexpr size_t SM_BK_MM = SM_TABLE + 520 * 4;    // u64[4] bucket path: min', max', outside, U
 constexpr size_t SM_BK_N = SM_BK_MM + 32;            // u32[4] bucket path: items, multi buckets, claim ctr
-constexpr size_t SM_BYTES = SM_BK_N + 16;
+constexpr size_t SM_TRI_PROBES = SM_BK_N + 16;      // u64 triangles: hash probes of the counting step
+constexpr size_t SM_BYTES = SM_TRI_PROBES + 16;
 
 gs_status set_error(gs_ctx* c, gs_status s, const char* fmt, ...);
 gs_status hip_check(gs_ctx* c, hipError_t e, const char* what);

@@ -117,7 +117,7 @@ class Engine:
     def stage_times(self) -> StageTimes:
         t = L.GsStageTimes()
         self._check(self._L.gs_last_stage_times(self.ctx, ctypes.byref(t)))
-        launched = 5 if t.path == 2 else t.sort_passes + (3 if t.path == 1 else 1 if t.fused_last else 0)
+        launched = 5 if t.path in (2, 3) else t.sort_passes + (3 if t.path == 1 else 1 if t.fused_last else 0)
         return StageTimes(t.keyinfo_ms, t.sort_ms, t.reduce_ms, t.total_ms, t.sort_passes, t.key_bits, t.records,
                           t.vertices, list(t.pass_ms)[:launched], t.key_bytes, t.payload_bytes,
                           t.partials, bool(t.fused_last), t.path)

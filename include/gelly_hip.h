@@ -231,7 +231,11 @@ typedef struct gs_stage_times {
                               1: bucket path, onesweep partition (pass_ms[0..sort_passes) = LSD
                                  passes, then accumulate, merge, emit; partials = work items);
                               2: bucket path, direct partition (keyinfo_ms = per-tile histogram,
-                                 pass_ms[0..4] = offset scans, scatter, accumulate, merge, emit) */
+                                 pass_ms[0..4] = offset scans, scatter, accumulate, merge, emit);
+                              3: window triangles (pass_ms[0..4] = symmetric keys + sort, unique,
+                                 rows + orientation, light count, heavy count; records = unique
+                                 adjacency entries, vertices = vertices with edges, partials = hash
+                                 probes of the counting step, sort_passes = LSD passes)          */
 } gs_stage_times;
 GS_API gs_status gs_last_stage_times(const gs_ctx* ctx, gs_stage_times* out);
 

@@ -165,6 +165,14 @@ def window_candidates(src, dst):
     return a, b, f, bool(tree.value)
 
 
+def candidate_count(src, dst):
+    """Number of GenerateCandidateEdges records the window emits (the size query of gso_window_candidates)."""
+    src, dst = _i64(src), _i64(dst)
+    tree = ctypes.c_int(0)
+    need = lib().gso_window_candidates(_p(src), _p(dst), len(src), None, None, None, 0, ctypes.byref(tree))
+    return -1 - need if need < 0 else need
+
+
 def window_triangles_ref(src, dst):
     src, dst = _i64(src), _i64(dst)
     ex, has, tree = ctypes.c_uint64(0), ctypes.c_int(0), ctypes.c_int(0)
