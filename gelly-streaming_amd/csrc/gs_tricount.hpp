@@ -11,8 +11,8 @@
 // Probing N+(u) from the middle vertex costs sum_u d+(u)^2 probes, against sum over edges u -> v of
 // d+(v) from the first vertex (R-MAT scale 20: 2.47 G against 4.27 G).  In-lists longer than a chunk
 // queue their further chunks for a second pass (a hub's work spreads over many waves); vertices with
-// more than TH_DMAX out-neighbours go to k_tri_heavy (a block each, sorted N+(v) in LDS, binary
-// search).  Only vertices whose out-list starts in [q0, q1) count (the multi-GPU split).
+// more than TH_DMAX out-neighbours go to k_tri_heavy (a block each, N+(v) in a 128 KiB LDS hash
+// set).  Only vertices whose out-list starts in [q0, q1) count (the multi-GPU split).
 #pragma once
 #include "gs_device.hpp"
 
@@ -54,6 +54,32 @@ __device__ __forceinline__ void th_insert(uint32_t* hs, uint32_t x, uint32_t bma
     for (int j = 0; j < 4; ++j)
       if (atomicCAS(&hs[b * 4 + j], TH_EMPTY, x) == TH_EMPTY) return;
   }
+}
+
+// members among x[j] for the set bits j of pend; all pending probes of the lane read their bucket
+// together (one 16-byte LDS read each)
+__device__ __forceinline__ uint32_t th_probe(const uint4* hb, uint32_t bmask, const uint32_t (&x)[TH_ILP],
+                                             uint32_t pend) {
+  uint32_t b[TH_ILP], cnt = 0;
+#pragma unroll
+  for (int j = 0; j < TH_ILP; ++j) b[j] = th_hash(x[j], bmask);
+  while (pend) {
+    uint4 y[TH_ILP];
+#pragma unroll
+    for (int j = 0; j < TH_ILP; ++j) y[j] = hb[b[j]];
+#pragma unroll
+    for (int j = 0; j < TH_ILP; ++j) {
+      if (!(pend >> j & 1)) continue;
+      const bool hit = y[j].x == x[j] || y[j].y == x[j] || y[j].z == x[j] || y[j].w == x[j];
+      const bool open = y[j].w == TH_EMPTY;   // a free last slot ends the chain
+      if (hit || open) {
+        cnt += hit ? 1u : 0u;
+        pend &= ~(1u << j);
+      }
+      b[j] = (b[j] + 1) & bmask;
+    }
+  }
+  return cnt;
 }
 
 // one wave: |N+(u) ∩ N+(v)| summed over the in-neighbours u = inbr[c0 .. c1) of v
@@ -125,28 +151,10 @@ __device__ __forceinline__ uint32_t th_wave_chunk(const uint32_t* __restrict__ o
       }
       x[j] = onbr[st + (kj - o)];
     }
-    uint32_t b[TH_ILP], pend = 0;
+    uint32_t pend = 0;
 #pragma unroll
-    for (int j = 0; j < TH_ILP; ++j) {
-      b[j] = th_hash(x[j], bmask);
-      pend |= (kb + j < run ? 1u : 0u) << j;
-    }
-    while (pend) {   // all pending probes of the lane read their bucket together
-      uint4 y[TH_ILP];
-#pragma unroll
-      for (int j = 0; j < TH_ILP; ++j) y[j] = hb[b[j]];
-#pragma unroll
-      for (int j = 0; j < TH_ILP; ++j) {
-        if (!(pend >> j & 1)) continue;
-        const bool hit = y[j].x == x[j] || y[j].y == x[j] || y[j].z == x[j] || y[j].w == x[j];
-        const bool open = y[j].w == TH_EMPTY;   // a free last slot ends the chain
-        if (hit || open) {
-          cnt += hit ? 1u : 0u;
-          pend &= ~(1u << j);
-        }
-        b[j] = (b[j] + 1) & bmask;
-      }
-    }
+    for (int j = 0; j < TH_ILP; ++j) pend |= (kb + j < run ? 1u : 0u) << j;
+    cnt += th_probe(hb, bmask, x, pend);
   }
   wave_lds_sync();   // the next item clears the table
   return cnt;
@@ -205,10 +213,11 @@ __global__ __launch_bounds__(TH_BLOCK) void k_tri_light(const uint32_t* __restri
   if (lane == 0 && probes) atomicAdd(n_probes, (unsigned long long)probes);   // wave-uniform
 }
 
-// one block per heavy vertex v: N+(v) (sorted) in LDS when it fits, the in-neighbours' lists in
-// chunks of TH_VCH
+// one block per heavy vertex v: N+(v) as an LDS hash set (up to TH_NU entries; longer lists are
+// binary-searched in HBM), the in-neighbours' lists in chunks of TH_VCH, TH_ILP items per thread
+// with one search
 constexpr int TH_HBLOCK = 1024;
-constexpr uint32_t TH_NU = 16384, TH_VCH = 4096;
+constexpr uint32_t TH_NU = 16384, TH_HB = TH_NU / 2, TH_VCH = 2048;   // TH_HB 4-slot buckets: load <= 1/2
 __global__ __launch_bounds__(TH_HBLOCK) void k_tri_heavy(const uint32_t* __restrict__ onbr,
                                                          const uint32_t* __restrict__ inbr,
                                                          const uint2* __restrict__ out_range,
@@ -217,10 +226,12 @@ __global__ __launch_bounds__(TH_HBLOCK) void k_tri_heavy(const uint32_t* __restr
                                                          const uint32_t* __restrict__ n_heavy,
                                                          unsigned long long* __restrict__ total,
                                                          unsigned long long* __restrict__ n_probes) {
-  __shared__ uint32_t s_nv[TH_NU];
-  __shared__ uint32_t s_off[TH_VCH + 1];
-  __shared__ uint32_t s_st[TH_VCH];
+  __shared__ uint4 s_hash[TH_HB];               // 128 KiB: N+(v) as a hash set of 4-slot buckets
+  __shared__ uint32_t s_off[TH_VCH + 1];        // prefix of |N+(u)| over the chunk; [cn] = total
+  __shared__ uint32_t s_st[TH_VCH];             // start of that N+(u) in onbr
   __shared__ uint32_t s_w[TH_HBLOCK / WAVE];
+  constexpr int PER = TH_VCH / TH_HBLOCK;
+  uint32_t* hs = reinterpret_cast<uint32_t*>(s_hash);
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   uint64_t cnt = 0, probes = 0;
   const uint32_t nh = *n_heavy;
@@ -228,25 +239,28 @@ __global__ __launch_bounds__(TH_HBLOCK) void k_tri_heavy(const uint32_t* __restr
     const uint32_t v = heavy[hi];
     const uint2 ro = out_range[v], ri = in_range[v];
     const uint32_t d = ro.y - ro.x;
-    const bool in_lds = d <= TH_NU;
-    if (in_lds)
-      for (uint32_t i = tid; i < d; i += TH_HBLOCK) s_nv[i] = onbr[ro.x + i];
-    const uint32_t* nvl = in_lds ? s_nv : onbr + ro.x;
+    const bool in_lds = d <= TH_NU;   // else: binary search of the sorted list in HBM
+    uint32_t nb = 16;
+    while (nb * 2 < d && nb < TH_HB) nb <<= 1;
+    const uint32_t bmask = nb - 1;
+    __syncthreads();   // the previous vertex is done with the table
+    if (in_lds) {
+      for (uint32_t i = tid; i < nb * 4; i += TH_HBLOCK) hs[i] = TH_EMPTY;
+      __syncthreads();
+      for (uint32_t i = tid; i < d; i += TH_HBLOCK) th_insert(hs, onbr[ro.x + i], bmask);
+    }
+    const uint32_t* nvl = onbr + ro.x;
     for (uint32_t c0 = ri.x; c0 < ri.y; c0 += TH_VCH) {
       const uint32_t cn = min(TH_VCH, ri.y - c0);
       __syncthreads();
-      // prefix of |N+(u)| over this chunk of in-neighbours (4 per thread, block scan)
-      uint32_t du[4], su[4], sum = 0;
+      // prefix of |N+(u)| over this chunk of in-neighbours (PER per thread, block scan)
+      uint32_t du[PER], su[PER], sum = 0;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const uint32_t i = tid * 4 + j;
-        du[j] = 0;
-        su[j] = 0;
-        if (i < cn) {
-          const uint2 ru = out_range[inbr[c0 + i]];
-          su[j] = ru.x;
-          du[j] = ru.y - ru.x;
-        }
+      for (int j = 0; j < PER; ++j) {
+        const uint32_t i = tid * PER + j;
+        const uint2 ru = out_range[inbr[c0 + min(i, cn - 1)]];
+        su[j] = ru.x;
+        du[j] = i < cn ? ru.y - ru.x : 0u;
         sum += du[j];
       }
       const uint32_t inc = wave_inclusive_sum(sum);
@@ -259,8 +273,8 @@ __global__ __launch_bounds__(TH_HBLOCK) void k_tri_heavy(const uint32_t* __restr
       }
       uint32_t run = base + inc - sum;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const uint32_t i = tid * 4 + j;
+      for (int j = 0; j < PER; ++j) {
+        const uint32_t i = tid * PER + j;
         if (i < cn) {
           s_off[i] = run;
           s_st[i] = su[j];
@@ -270,24 +284,40 @@ __global__ __launch_bounds__(TH_HBLOCK) void k_tri_heavy(const uint32_t* __restr
       if (tid == 0) s_off[cn] = tot;
       probes += tot;   // block-uniform
       __syncthreads();
-      for (uint32_t k = tid; k < tot; k += TH_HBLOCK) {
-        uint32_t lo = 0, hi2 = cn - 1;
-        while (lo < hi2) {
-          const uint32_t mid = (lo + hi2 + 1) >> 1;
-          if (s_off[mid] <= k) lo = mid;
-          else hi2 = mid - 1;
+      for (uint32_t k0 = 0; k0 < tot; k0 += TH_HBLOCK * TH_ILP) {
+        const uint32_t kb = k0 + tid * TH_ILP;
+        // list of item kk: the last index with s_off <= kk (s_off[cn] = tot is above every item)
+        uint32_t lo = 0, h2 = cn - 1;
+        const uint32_t kk = min(kb, tot - 1);
+        while (lo < h2) {
+          const uint32_t mid = (lo + h2 + 1) >> 1;
+          if (s_off[mid] <= kk) lo = mid;
+          else h2 = mid - 1;
         }
-        const uint32_t x = onbr[s_st[lo] + (k - s_off[lo])];
-        uint32_t a = 0, b = d;   // lower bound of x in N+(v)
-        while (a < b) {
-          const uint32_t mid = (a + b) >> 1;
-          if (nvl[mid] < x) a = mid + 1;
-          else b = mid;
+        uint32_t x[TH_ILP], pend = 0;
+#pragma unroll
+        for (int j = 0; j < TH_ILP; ++j) {
+          const uint32_t kj = min(kb + j, tot - 1);
+          while (s_off[lo + 1] <= kj) ++lo;   // crosses empty lists too
+          x[j] = onbr[s_st[lo] + (kj - s_off[lo])];
+          pend |= (kb + j < tot ? 1u : 0u) << j;
         }
-        cnt += (a < d && nvl[a] == x) ? 1u : 0u;
+        if (in_lds) {
+          cnt += th_probe(s_hash, bmask, x, pend);
+        } else {
+#pragma unroll
+          for (int j = 0; j < TH_ILP; ++j) {
+            uint32_t a = 0, b = d;   // lower bound of x in N+(v)
+            while (a < b) {
+              const uint32_t mid = (a + b) >> 1;
+              if (nvl[mid] < x[j]) a = mid + 1;
+              else b = mid;
+            }
+            cnt += ((pend >> j & 1) && a < d && nvl[a] == x[j]) ? 1u : 0u;
+          }
+        }
       }
     }
-    __syncthreads();
   }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o, WAVE);
