@@ -4,7 +4,7 @@
 cd "$(dirname "$0")/.." || exit 1
 mkdir -p gpurun_out
 set -o pipefail
-timeout -k 10 900 python -m pytest tests/ -x -q -m gpu > gpurun_out/gpu_tests.log 2>&1 &&
+timeout -k 10 900 python -u -m pytest tests/ -x -v -m gpu --timeout 120 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1 &&
 timeout -k 10 300 python bench.py --check > gpurun_out/bench.json 2> gpurun_out/bench.err &&
 timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 \
     --master-port 29533 bench.py --gpus 1 --steps 5 --warmup 2 > gpurun_out/bench_torchrun.json 2> gpurun_out/bench_torchrun.err &&
