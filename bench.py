@@ -48,7 +48,9 @@ def parse():
     p.add_argument("--bk-onesweep", action="store_true",
                    help="ablation: bucket path partitions with 1-2 LSD passes instead of the direct scatter")
     p.add_argument("--check", action="store_true", help="verify sum(per-vertex sums) == sum(values) after timing")
-    p.add_argument("--workload", default="reduce", choices=["reduce", "fold", "triangles"],
+    p.add_argument("--windows-edges", type=float, default=1e8,
+                   help="apply (C5): edges per 1000 ms window of the continuous stream")
+    p.add_argument("--workload", default="reduce", choices=["reduce", "fold", "triangles", "c1", "apply", "candidates"],
                    help="reduce = C2 (default, the headline); fold = C3 degree/max on skewed R-MAT; "
                         "triangles = WindowTriangles on an R-MAT window without self-loops (C4 shape)")
     return p.parse_args()
@@ -218,8 +220,103 @@ def cpu_baseline_triangles(src, dst, max_candidates=40_000_000, max_log2=22, bud
                       f"count, Integer sum), one thread, {dt:.2f} s"}
 
 
+def window_stream_main(a):
+    """Secondary single-GPU workloads, one JSON line each:
+
+    c1          C1: WindowTriangles on the uniform 1M-edge stream (V = 2^16, self-loops rejected), one
+                1000 ms window; the CPU baseline runs the reference's candidate rule on the WHOLE window.
+    apply       C5: a continuous R-MAT scale-23 stream cut into 1000 ms windows of --windows-edges edges
+                (1e8 = the 100M edges/s target).  Per window: slice(ALL).applyOnNeighbors grouping
+                (gs_window_csr: every vertex's neighbour list in arrival order, what a user EdgesApply
+                consumes) and the GenerateCandidateEdges sizing pass (HashSet order + per-vertex pair
+                counts; emitting them is not possible at this size).  Reports sustained
+                windows/s and p50/p99 latency from window close (columns in HBM) to results in HBM.
+    candidates  GenerateCandidateEdges records emitted in full (gs_window_candidates) on R-MAT scale-23
+                windows of 2^22 edges."""
+    torch.cuda.set_device(0)
+    pkg = ge.load_package()
+    eng = pkg.Engine(0)
+    orc_cpu = None
+    lat, extra = [], {}
+    if a.workload == "c1":
+        E = 1_000_000
+        src, dst = eng.generate_uniform(1 << 16, E, 0x5EED01)
+        wins = [(src, dst)]
+        run = lambda s_, d_: eng.triangles(s_, d_)
+        bytes_per_window = 16 * E
+        desc = "C1: WindowTriangles over the uniform 1M-edge window (V = 2^16, self-loops rejected, one 1000 ms slice)"
+    else:
+        E = int(a.windows_edges) if a.workload == "apply" else 1 << 22
+        nwin = 2
+        wins = [eng.generate_rmat(23, E, 0x5EED05, first_edge=w * E) for w in range(nwin)]
+        if a.workload == "apply":
+            def run(s_, d_):
+                return eng.csr(s_, d_, None, 2), eng.candidate_count(s_, d_)
+            desc = (f"C5: continuous R-MAT scale-23 stream, 1000 ms windows of {E:.3g} edges: slice(ALL) "
+                    f"applyOnNeighbors grouping + GenerateCandidateEdges sizing")
+        else:
+            run = lambda s_, d_: eng.candidates(s_, d_)
+            desc = "C5 emission: GenerateCandidateEdges records for R-MAT scale-23 windows of 2^22 edges"
+    torch.cuda.synchronize()
+    for w in range(a.warmup):
+        r = run(*wins[w % len(wins)])
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for w in range(a.steps):
+        t = time.perf_counter()
+        r = run(*wins[w % len(wins)])
+        torch.cuda.synchronize()
+        lat.append(time.perf_counter() - t)
+    elapsed = time.perf_counter() - t0
+    if a.workload == "c1":
+        extra["triangles"] = r[0]
+        extra["reference_integer_output"] = r[1]
+        algo = bytes_per_window
+    elif a.workload == "apply":
+        (keys, offs, nbrs, _), P = r
+        extra.update(vertices=int(keys.numel()), csr_records=int(nbrs.numel()), candidate_records_needed=int(P),
+                     candidate_bytes_needed=int(P) * 17)
+        algo = 16 * E + 16 * keys.numel() + 8 * nbrs.numel()   # edges in; keys + offsets + neighbours out
+    else:
+        a_, b_, f_ = r
+        P = int(a_.numel())
+        extra.update(candidate_records=P, candidates_per_s=P * a.steps / elapsed)
+        algo = 16 * E + 17 * P
+    ms = statistics.mean(lat) * 1e3
+    cpu = None
+    if a.workload == "c1" and not a.no_cpu_baseline:
+        orc = ge.load_oracle()
+        s, d = src.cpu().numpy(), dst.cpu().numpy()
+        tt = time.perf_counter()
+        ref = orc.window_triangles_ref(s, d)
+        dt = time.perf_counter() - tt
+        extra["cpu_reference_rule_result"] = ref[1]
+        assert ref[1] == r[0] and ref[0] == r[1], "C1: GPU triangle count differs from the reference rule"
+        cpu = {"value": E / dt, "unit": "edges/s", "cores": 1, "kind": "port",
+               "sample": f"the whole C1 window (1M edges) through the reference's candidate rule "
+                         f"(oracle gso_window_triangles_ref), one thread, {dt:.2f} s"}
+    gbs = algo / (ms * 1e-3) / 1e9
+    line = {"metric": METRIC, "value": E * a.steps / elapsed, "unit": "edges/s", "n_gpus": 1, "steps": a.steps,
+            "warmup": a.warmup, "ms_per_step": elapsed / a.steps * 1e3, "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "int64",
+            "data": "synthetic (uniform / R-MAT, seeded), generated on device",
+            "config": {"workload": desc, "edges_per_window": E, "windows_per_s": 1e3 / ms,
+                       "latency_ms_p50": float(np.percentile(np.array(lat) * 1e3, 50)),
+                       "latency_ms_p99": float(np.percentile(np.array(lat) * 1e3, 99)),
+                       "sustains_target": (a.workload != "apply") or (E * 1e3 / ms >= a.windows_edges),
+                       **extra, "parallelism": "1 GPU"},
+            "roofline": {"bound": "hbm", "kernel": "whole window", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": None,
+                         "algorithmic_bytes_per_launch": algo, "avg_launch_ms": round(ms, 4)},
+            "cpu_baseline": cpu}
+    print(json.dumps(line), flush=True)
+    eng.close()
+
+
 def main():
     a = parse()
+    if a.workload in ("c1", "apply", "candidates"):
+        return window_stream_main(a)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))

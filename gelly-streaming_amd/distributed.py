@@ -55,9 +55,13 @@ def exchange_sorted(keys: torch.Tensor, cols: list, group=None):
     dist.all_to_all_single(recv, send, group=group)
     send_l, recv_l = send.tolist(), recv.tolist()
     total = sum(recv_l)
+    # keys travel as 32-bit offsets from the global minimum when the window's span allows (12-byte
+    # instead of 16-byte rows for a Long partial)
+    narrow = kmax - kmin < (1 << 32)
+    kpart = (keys - kmin).to(torch.int32) if narrow else keys.contiguous()
     # one all-to-all of packed rows (key bytes, then each column's bytes) instead of one per column:
     # fewer collective launches and one rendezvous per window
-    parts = [keys.contiguous()] + [c.contiguous() for c in cols]
+    parts = [kpart] + [c.contiguous() for c in cols]
     widths = [p.element_size() for p in parts]
     row = sum(widths)
     packed = torch.cat([p.view(torch.uint8).view(-1, w) for p, w in zip(parts, widths)], dim=1)
@@ -67,13 +71,16 @@ def exchange_sorted(keys: torch.Tensor, cols: list, group=None):
     for p, w in zip(parts, widths):
         out.append(rp[:, at:at + w].contiguous().view(p.dtype).view(-1))
         at += w
-    return out[0], out[1:]
+    rk = ((out[0].to(torch.int64) & 0xFFFFFFFF) + kmin) if narrow else out[0]
+    return rk, out[1:]
 
 
 def reduce_window(local_reduce, src, dst, val, direction: int, op: int, group=None):
     """reduceOnEdges over a window whose edges are spread over the ranks of `group`.
     Returns this rank's owned (vertex, value) pairs, vertices ascending."""
     k, v = local_reduce(src, dst, val, direction, op)
+    if dist.get_world_size(group) == 1:   # the only rank owns every vertex: no exchange, no merge
+        return k, v
     rk, (rv,) = exchange_sorted(k, [v], group)
     if rk.numel() == 0:
         return rk, rv
@@ -83,6 +90,8 @@ def reduce_window(local_reduce, src, dst, val, direction: int, op: int, group=No
 def fold_degree_max_window(local_fold, local_reduce, src, dst, direction: int, init_max: int, group=None):
     """foldNeighbors(degree, max-neighbour) across ranks: degrees merge by SUM, maxima by MAX."""
     k, d, m = local_fold(src, dst, direction, init_max)
+    if dist.get_world_size(group) == 1:
+        return k, d, m
     rk, (rd, rm) = exchange_sorted(k, [d, m], group)
     if rk.numel() == 0:
         return rk, rd, rm

@@ -223,6 +223,16 @@ class Engine:
         self._check(self._L.gs_window_candidates(self.ctx, ctypes.byref(b), ctypes.byref(out)))
         return a[:P], bb[:P], f[:P]
 
+    def candidate_count(self, src, dst) -> int:
+        """Sizing call of gs_window_candidates (capacity 0): the number of records the window emits."""
+        b, keep, dev = self._batch(src, dst, None)
+        n_out = ctypes.c_uint64(0)
+        probe = L.GsPairOut(None, None, None, 0, ctypes.pointer(n_out), L.GS_MEM_DEVICE if dev else L.GS_MEM_HOST, 0)
+        st = self._L.gs_window_candidates(self.ctx, ctypes.byref(b), ctypes.byref(probe))
+        if st not in (L.GS_OK, L.GS_ECAPACITY):
+            self._check(st)
+        return n_out.value
+
     def triangles(self, src, dst):
         """gs_window_triangles: (exact count, the Integer the reference emits, has_output)."""
         b, keep, dev = self._batch(src, dst, None)

@@ -51,6 +51,10 @@ def _worker(rank, world, port, q):
             res[(direction, op)] = (k.numpy(), r.numpy())
         k, dg, mx = D.fold_degree_max_window(local_fold, local_reduce, s, d, direction, -(1 << 63))
         res[(direction, "deg")] = (k.numpy(), dg.numpy(), mx.numpy())
+    # key spans that take the 32-bit relative encoding past 2^31 (4095 * 2^20 < 2^32) and the 64-bit one
+    for tag, mul, off in (("rel32", 1 << 20, -(1 << 40)), ("wide", 1 << 30, -(1 << 50))):
+        k, r = D.reduce_window(local_reduce, s * mul + off, d * mul + off, v, 1, 0)
+        res[tag] = (k.numpy(), r.numpy())
     # WindowTriangles across ranks: all-gathered adjacency must be the whole window in stream order;
     # each rank contributes its part (here: rank 0 counts everything) and the all-reduce sums them
     fs, fd = D.gather_window(torch.from_numpy(s), torch.from_numpy(d))
@@ -87,6 +91,11 @@ def test_reduce_window_two_ranks(oracle):
         mx = np.concatenate([out[r][(direction, "deg")][2] for r in range(world)])
         wk, wd, wm = oracle.window_fold_degree_max(s, d, direction)
         assert np.array_equal(k, wk) and np.array_equal(dg, wd) and np.array_equal(mx, wm)
+    for tag, mul, off in (("rel32", 1 << 20, -(1 << 40)), ("wide", 1 << 30, -(1 << 50))):
+        k = np.concatenate([out[r][tag][0] for r in range(world)])
+        r_ = np.concatenate([out[r][tag][1] for r in range(world)])
+        wk, wv = oracle.window_reduce(s * mul + off, d * mul + off, v, 1, 0)
+        assert np.array_equal(k, wk) and np.array_equal(r_, wv), tag
     for r in range(world):
         assert np.array_equal(out[r]["gathered"][0], s) and np.array_equal(out[r]["gathered"][1], d)
         w, ex, _ = oracle.window_triangles_fwd(s, d)
