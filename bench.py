@@ -281,6 +281,18 @@ def window_stream_main(a):
         a_, b_, f_ = r
         P = int(a_.numel())
         extra.update(candidate_records=P, candidates_per_s=P * a.steps / elapsed)
+        # stage 2 (keyBy(0,1) CountTriangles + sum(0)) on the emitted records, checked against the
+        # direct triangle count of the same window
+        t2 = []
+        for _ in range(3):
+            tt = time.perf_counter()
+            c2 = eng.count_candidates(a_, b_, f_)
+            torch.cuda.synchronize()
+            t2.append(time.perf_counter() - tt)
+        tri = eng.triangles(*wins[(a.steps - 1) % len(wins)])
+        assert c2[0] == tri[0], "stage-2 count differs from the window's triangle count"
+        extra.update(stage2_ms=statistics.median(t2) * 1e3, stage2_records_per_s=P / statistics.median(t2),
+                     triangles=c2[0], stage2_emitting_groups=c2[3])
         algo = 16 * E + 17 * P
     ms = statistics.mean(lat) * 1e3
     cpu = None

@@ -31,7 +31,7 @@ GS_DTYPE_OF = {np.dtype(np.int32): GS_I32, np.dtype(np.int64): GS_I64, np.dtype(
 EXPORTS = ("gs_abi_version", "gs_create", "gs_destroy", "gs_last_error", "gs_set_stream", "gs_synchronize",
            "gs_alloc_pinned", "gs_free_pinned", "gs_window_reduce", "gs_window_fold",
            "gs_window_fold_degree_max", "gs_window_csr", "gs_window_candidates", "gs_window_triangles",
-           "gs_window_triangles_part",
+           "gs_window_triangles_part", "gs_window_count_candidates",
            "gs_generate_rmat", "gs_generate_uniform", "gs_generate_values", "gs_last_stage_times")
 
 P = ctypes.c_void_p
@@ -70,6 +70,10 @@ class GsCsrOut(ctypes.Structure):
 class GsPairOut(ctypes.Structure):
     _fields_ = [("a", P), ("b", P), ("is_candidate", P), ("capacity", u64), ("n_out", ctypes.POINTER(u64)),
                 ("mem", i32), ("reserved", i32)]
+
+
+class GsPairBatch(ctypes.Structure):
+    _fields_ = [("a", P), ("b", P), ("is_candidate", P), ("n", u64), ("mem", i32), ("reserved", i32)]
 
 
 class GsStageTimes(ctypes.Structure):
@@ -116,6 +120,8 @@ def load() -> ctypes.CDLL:
         "gs_window_triangles": (st, [P, ctypes.POINTER(GsEdgeBatch), ctypes.POINTER(u64), ctypes.POINTER(i32),
                                      ctypes.POINTER(i32)]),
         "gs_window_triangles_part": (st, [P, ctypes.POINTER(GsEdgeBatch), u32, u32, ctypes.POINTER(u64)]),
+        "gs_window_count_candidates": (st, [P, ctypes.POINTER(GsPairBatch), ctypes.POINTER(u64), ctypes.POINTER(i32),
+                                            ctypes.POINTER(i32), ctypes.POINTER(u64)]),
         "gs_generate_rmat": (st, [P, i32, u64, u64, u32, u32, u32, i32, i32, u64, P, P]),
         "gs_generate_uniform": (st, [P, u64, u64, u64, u64, P, P]),
         "gs_generate_values": (st, [P, u64, u64, u64, i32, P]),

@@ -62,6 +62,8 @@ struct gs_ctx {
   gs::DevBuf bk_meta, bk_items, bk_slabs;
   // direct partition: per-tile bucket counts (u16), chunk sums, per-tile write offsets
   gs::DevBuf dp_cnt, dp_csum, dp_off;
+  // stage-2 candidate count (gs_pairs.hip): staged input columns, packed keys / payloads, group sums
+  gs::DevBuf pr_a, pr_b, pr_f, pr_key, pr_val, pr_gk, pr_gv, pr_small;
   hipEvent_t ev[6] = {};
   hipEvent_t pass_ev[9] = {};
   gs_stage_times times{};

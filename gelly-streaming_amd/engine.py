@@ -233,6 +233,29 @@ class Engine:
             self._check(st)
         return n_out.value
 
+    def count_candidates(self, a, b, is_candidate):
+        """gs_window_count_candidates: WindowTriangles stage 2 (keyBy(0, 1) CountTriangles + sum(0)) over
+        one window's candidate records.  Returns (exact, the Integer the reference emits, has_output,
+        records CountTriangles emits)."""
+        dev = _is_torch(a)
+        if dev:
+            import torch
+
+            assert a.is_cuda and b.is_cuda and is_candidate.is_cuda, "mixed host/device columns"
+            a, b = a.contiguous(), b.contiguous()
+            f = (is_candidate != 0).to(torch.uint8)
+        else:
+            a = np.ascontiguousarray(a, dtype=np.int64)
+            b = np.ascontiguousarray(b, dtype=np.int64)
+            f = np.ascontiguousarray(np.asarray(is_candidate) != 0, dtype=np.uint8)
+        if len(a) != len(b) or len(f) != len(a):
+            raise ValueError("a, b and is_candidate must have the same length")
+        pb = L.GsPairBatch(_ptr(a), _ptr(b), _ptr(f), len(a), L.GS_MEM_DEVICE if dev else L.GS_MEM_HOST, 0)
+        cnt, wrapped, has, groups = ctypes.c_uint64(0), ctypes.c_int32(0), ctypes.c_int32(0), ctypes.c_uint64(0)
+        self._check(self._L.gs_window_count_candidates(self.ctx, ctypes.byref(pb), ctypes.byref(cnt),
+                                                       ctypes.byref(wrapped), ctypes.byref(has), ctypes.byref(groups)))
+        return cnt.value, wrapped.value, bool(has.value), groups.value
+
     def triangles(self, src, dst):
         """gs_window_triangles: (exact count, the Integer the reference emits, has_output)."""
         b, keep, dev = self._batch(src, dst, None)

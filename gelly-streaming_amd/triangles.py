@@ -28,7 +28,22 @@ class GenerateCandidateEdges(EdgesApply):
 
 
 class CountTriangles:
-    """WindowTriangles.java:119-140: per (a, b) group, emit (#candidates, window.maxTimestamp) iff edges > 0."""
+    """WindowTriangles.java:119-140: per (a, b) group, emit (#candidates, window.maxTimestamp) iff edges > 0.
+    Runs in the engine through `count_triangles` (gs_window_count_candidates)."""
+
+
+def count_triangles(candidates: DataStream, engine) -> DataStream:
+    """Stage 2 of WindowTriangles over materialised candidate records (WindowTriangles.java:64-66):
+    .keyBy(0, 1).timeWindow(w).apply(CountTriangles()).timeWindowAll(w).sum(0).  Stage-1 records carry
+    ts = end - 1, so each stage-1 window is one stage-2 window; it yields one (Integer, end - 1) record
+    when any pair group emits."""
+    out = DataStream()
+    for w in candidates.windows:
+        a, b, f = w.columns
+        exact, wrapped, has, groups = engine.count_candidates(a, b, f)
+        if has:
+            out.windows.append(WindowOutput(w.start, w.end, ("records", [(wrapped, w.end - 1)])))
+    return out
 
 
 class RemoveEdgeValue:

@@ -204,6 +204,26 @@ GS_API gs_status gs_window_triangles(gs_ctx* ctx, const gs_edge_batch* batch, ui
 GS_API gs_status gs_window_triangles_part(gs_ctx* ctx, const gs_edge_batch* batch, uint32_t part,
                                           uint32_t nparts, uint64_t* partial_count);
 
+/* Candidate records of one window as produced by GenerateCandidateEdges (gs_pair_out layout). */
+typedef struct gs_pair_batch {
+  const int64_t* a;
+  const int64_t* b;
+  const uint8_t* is_candidate;   /* Boolean f2: non-zero = true                                  */
+  uint64_t n;
+  int32_t mem;             /* gs_mem of a/b/is_candidate                                       */
+  int32_t reserved;
+} gs_pair_batch;
+
+/* Stage 2 of WindowTriangles for callers that keep GenerateCandidateEdges and count downstream:
+ * keyBy(0, 1).timeWindow(w).apply(CountTriangles).timeWindowAll(w).sum(0)
+ * (WindowTriangles.java:64-66, CountTriangles :119-140).  The records (one window) are grouped by the
+ * ordered pair (a, b); a group with at least one edge record (is_candidate = 0) emits its number of
+ * candidate records; the all-window sum adds them.  *count = exact sum, *count_ref_wrapped = the
+ * Integer the reference emits, *has_output = 0 when no group emits (the reference emits no record),
+ * *groups = records CountTriangles emits.  IDs of a and of b must each span < 2^32 (GS_EUNSUPPORTED). */
+GS_API gs_status gs_window_count_candidates(gs_ctx* ctx, const gs_pair_batch* pairs, uint64_t* count,
+                                            int32_t* count_ref_wrapped, int32_t* has_output, uint64_t* groups);
+
 /* ---- synthetic streams (bit-identical to oracle/gs_oracle.c) ------------------------ */
 /* R-MAT: 2^scale vertices, probabilities a, b, c (d = 1-a-b-c) as 32-bit fixed point,
  * optional seeded vertex permutation, optional self-loop removal (rewired, count kept). */

@@ -173,6 +173,26 @@ def candidate_count(src, dst):
     return -1 - need if need < 0 else need
 
 
+def count_candidates(a, b, is_candidate):
+    """Stage 2 of WindowTriangles over one window's candidate records (example/WindowTriangles.java:64-66):
+    keyBy(0, 1) groups by the ordered pair (a, b); CountTriangles.apply (:119-140) counts candidate
+    (true) and edge (false) records and emits the candidate count iff edges > 0; timeWindowAll(..).sum(0)
+    adds the emitted Integers (wrapping).  Returns (Integer sum, exact sum, has_output, emitted records)."""
+    a, b = _i64(a), _i64(b)
+    f = np.asarray(is_candidate) != 0
+    if len(a) == 0:
+        return 0, 0, False, 0
+    pairs = np.stack([a, b], axis=1)
+    _, inv = np.unique(pairs, axis=0, return_inverse=True)
+    inv = inv.reshape(-1)
+    cand = np.bincount(inv, weights=f.astype(np.int64)).astype(np.int64)
+    edges = np.bincount(inv, weights=(~f).astype(np.int64)).astype(np.int64)
+    emit = edges > 0
+    exact = int(cand[emit].sum())
+    w = exact & 0xFFFFFFFF
+    return (w - (1 << 32) if w >= (1 << 31) else w), exact, bool(emit.any()), int(emit.sum())
+
+
 def window_triangles_ref(src, dst):
     src, dst = _i64(src), _i64(dst)
     ex, has, tree = ctypes.c_uint64(0), ctypes.c_int(0), ctypes.c_int(0)

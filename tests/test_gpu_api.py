@@ -224,3 +224,62 @@ def test_triangles_parts_sum_to_whole(engine, oracle):
     whole, wrapped, _ = engine.triangles(S, D)
     for nparts in (1, 2, 3, 8):
         assert sum(engine.triangles_part(S, D, p, nparts) for p in range(nparts)) == whole
+
+
+@pytest.mark.parametrize("kind", ["small_ids", "sparse_ids", "negative_ids", "rmat"])
+def test_count_candidates_matches_reference(engine, oracle, kind):
+    """gs_window_count_candidates (stage 2: keyBy(0,1) CountTriangles + sum(0)) over the window's
+    GenerateCandidateEdges records equals the oracle's restatement and the window's triangle count."""
+    rng = np.random.default_rng({"small_ids": 11, "sparse_ids": 12, "negative_ids": 13, "rmat": 14}[kind])
+    for trial in range(4):
+        s, d = _cand_case(oracle, rng, kind)
+        ra, rb, rf, tree = oracle.window_candidates(s, d)
+        want = oracle.count_candidates(ra, rb, rf)
+        got = engine.count_candidates(*[torch.from_numpy(x).cuda() for x in (ra, rb, rf)])
+        assert got == (want[1], want[0], want[2], want[3]), (kind, trial)
+        if not tree:
+            w_ref, ex_ref, has_ref, _ = oracle.window_triangles_ref(s, d)
+            assert (got[0], got[1], got[2]) == (ex_ref, w_ref, has_ref)
+
+
+def test_count_candidates_edge_cases(engine, oracle):
+    rng = np.random.default_rng(21)
+    # random records: candidate-only groups, edge-only groups, mixed; host columns
+    n = 200_000
+    a = rng.integers(-50, 50, n) * 1_000_003
+    b = rng.integers(0, 300, n)
+    f = (rng.random(n) < 0.8).astype(np.uint8)
+    want = oracle.count_candidates(a, b, f)
+    assert engine.count_candidates(a, b, f) == (want[1], want[0], want[2], want[3])
+    # all candidates -> no output; empty window -> no output
+    assert engine.count_candidates(a, b, np.ones(n, np.uint8))[2] is False
+    assert engine.count_candidates(a[:0], b[:0], f[:0]) == (0, 0, False, 0)
+    # IDs spanning 2^32 or more are refused, loudly
+    with pytest.raises(Exception, match="UNSUPPORTED|span"):
+        engine.count_candidates(np.array([0, 1 << 40]), np.array([0, 1]), np.array([0, 1], np.uint8))
+
+
+def test_count_candidates_large_window(engine, oracle):
+    """Full emission + stage 2 on a 2^16-edge R-MAT window equals the direct triangle count."""
+    s, d = oracle.gen_rmat(14, 1 << 16, 0x5EED04, no_self_loops=True)
+    ts, td = torch.from_numpy(s).cuda(), torch.from_numpy(d).cuda()
+    a, b, f = engine.candidates(ts, td)
+    got = engine.count_candidates(a, b, f)
+    ex, w, has = engine.triangles(ts, td)
+    assert (got[0], got[1], got[2]) == (ex, w, has)
+
+
+def test_two_stage_pipeline_itcase(pkg):
+    """WindowTriangles written as the reference writes it — applyOnNeighbors(GenerateCandidateEdges)
+    then keyBy(0,1) CountTriangles + sum(0) (here triangles.count_triangles) — gives the ITCase output."""
+    from gelly_streaming_amd import triangles
+
+    t = FIX["triangles"]
+    e = np.array(t["edges_src_trg_ts"], dtype=np.int64)
+    env = pkg.StreamExecutionEnvironment.getExecutionEnvironment()
+    g = pkg.SimpleEdgeStream(pkg.EdgeColumns(e[:, 0].copy(), e[:, 1].copy(), e[:, 2].copy()), env,
+                             pkg.EdgeValueTimestampExtractor())
+    ws = g.slice(pkg.Time.milliseconds(t["window_ms"]), pkg.EdgeDirection.ALL)
+    cands = ws.applyOnNeighbors(triangles.GenerateCandidateEdges())
+    got = triangles.count_triangles(cands, ws.engine).collect()
+    assert sorted(got) == sorted(tuple(x) for x in t["expected"])

@@ -110,3 +110,31 @@ def test_reduce_java_arithmetic(oracle):
     assert np.signbit(r[0])  # Math.min(0.0, -0.0) = -0.0
     k, r = oracle.window_reduce(s, d, f, 1, 2)
     assert np.isnan(r[0])
+
+
+def test_count_candidates_itcase_windows(oracle):
+    """Stage 2 (CountTriangles + sum) over the reference's own candidate records of each ITCase window
+    gives the ITCase outputs: (2,399) (3,799) (2,1199)."""
+    t = FIX["triangles"]
+    e = np.array(t["edges_src_trg_ts"], dtype=np.int64)
+    starts = e[:, 2] - e[:, 2] % t["window_ms"]
+    got = []
+    for st in np.unique(starts):
+        idx = starts == st
+        a, b, f, tree = oracle.window_candidates(e[idx, 0], e[idx, 1])
+        w, ex, has, groups = oracle.count_candidates(a, b, f)
+        w_ref, ex_ref, has_ref, _ = oracle.window_triangles_ref(e[idx, 0], e[idx, 1])
+        assert (w, ex, has) == (w_ref, ex_ref, has_ref)
+        if has:
+            got.append([w, int(st + t["window_ms"] - 1)])
+    assert sorted(got) == sorted(t["expected"])
+
+
+def test_count_candidates_rules(oracle):
+    """Groups without an edge record emit nothing; an edge-only group emits 0 (has_output, no count)."""
+    a = np.array([1, 1, 1, 2, 2, 3], np.int64)
+    b = np.array([5, 5, 5, 7, 7, 9], np.int64)
+    f = np.array([1, 1, 0, 1, 1, 0], np.uint8)
+    assert oracle.count_candidates(a, b, f) == (2, 2, True, 2)
+    assert oracle.count_candidates(a[3:5], b[3:5], f[3:5]) == (0, 0, False, 0)
+    assert oracle.count_candidates(a[:0], b[:0], f[:0]) == (0, 0, False, 0)
