@@ -50,7 +50,7 @@ def parse():
     p.add_argument("--check", action="store_true", help="verify sum(per-vertex sums) == sum(values) after timing")
     p.add_argument("--windows-edges", type=float, default=1e8,
                    help="apply (C5): edges per 1000 ms window of the continuous stream")
-    p.add_argument("--workload", default="reduce", choices=["reduce", "fold", "triangles", "c1", "apply", "candidates"],
+    p.add_argument("--workload", default="reduce", choices=["reduce", "fold", "triangles", "c1", "apply", "candidates", "parse"],
                    help="reduce = C2 (default, the headline); fold = C3 degree/max on skewed R-MAT; "
                         "triangles = WindowTriangles on an R-MAT window without self-loops (C4 shape)")
     return p.parse_args()
@@ -325,10 +325,66 @@ def window_stream_main(a):
     eng.close()
 
 
+def parse_main(a):
+    """Input path: the examples' "src trg ts" edge text (WindowTriangles.java:175-185)
+    parsed on the GPU (gs_parse_edges_text) from text resident in HBM: R-MAT scale-24 edges with
+    ascending millisecond timestamps, 2^24 lines.  CPU baseline: the oracle's parser (same rules), one
+    thread, on the whole text."""
+    torch.cuda.set_device(0)
+    pkg = ge.load_package()
+    from gelly_streaming_amd.textio import format_edges_text
+
+    eng = pkg.Engine(0)
+    n = 1 << 24
+    s, d = eng.generate_rmat(24, n, 0x5EED02)
+    ts = np.arange(n, dtype=np.int64) * 1000 // n + 1_700_000_000_000
+    text = format_edges_text(s.cpu().numpy(), d.cpu().numpy(), ts)
+    dev = torch.from_numpy(np.frombuffer(text, np.uint8).copy()).cuda()
+    for _ in range(a.warmup):
+        r = eng.parse_edges_text(dev)
+    torch.cuda.synchronize()
+    lat = []
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        t = time.perf_counter()
+        r = eng.parse_edges_text(dev)
+        torch.cuda.synchronize()
+        lat.append(time.perf_counter() - t)
+    elapsed = time.perf_counter() - t0
+    assert torch.equal(r[0], s) and torch.equal(r[1], d), "parsed columns differ from the generated edges"
+    ms = statistics.mean(lat) * 1e3
+    algo = len(text) + 24 * n      # text in, three int64 columns out (the staging copy is extra traffic)
+    cpu = None
+    if not a.no_cpu_baseline:
+        orc = ge.load_oracle()
+        tt = time.perf_counter()
+        cs, cd, ct = orc.parse_edges_text(text)
+        dt = time.perf_counter() - tt
+        assert np.array_equal(cs, s.cpu().numpy()) and np.array_equal(ct, ts)
+        cpu = {"value": n / dt, "unit": "edges/s", "cores": 1, "kind": "port",
+               "sample": f"the whole text ({len(text) / 1e6:.0f} MB) through oracle gso_parse_edges_text, one thread, "
+                         f"{dt:.2f} s"}
+    gbs = algo / (ms * 1e-3) / 1e9
+    print(json.dumps({
+        "metric": METRIC, "value": n * a.steps / elapsed, "unit": "edges/s", "n_gpus": 1, "steps": a.steps,
+        "warmup": a.warmup, "ms_per_step": elapsed / a.steps * 1e3, "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "u8", "data": "synthetic R-MAT scale-24 edge text, generated on the host",
+        "config": {"workload": "input path: 'src trg ts' edge text -> int64 columns (gs_parse_edges_text)",
+                   "records": n, "text_bytes": len(text), "latency_ms_p50": float(np.percentile(np.array(lat) * 1e3, 50)),
+                   "parallelism": "1 GPU"},
+        "roofline": {"bound": "hbm", "kernel": "parse call (stage + count + starts + parse)", "achieved": round(gbs, 1),
+                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": None,
+                     "algorithmic_bytes_per_launch": algo, "avg_launch_ms": round(ms, 4)},
+        "cpu_baseline": cpu}), flush=True)
+    eng.close()
+
+
 def main():
     a = parse()
     if a.workload in ("c1", "apply", "candidates"):
         return window_stream_main(a)
+    if a.workload == "parse":
+        return parse_main(a)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))

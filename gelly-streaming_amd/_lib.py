@@ -32,7 +32,7 @@ EXPORTS = ("gs_abi_version", "gs_create", "gs_destroy", "gs_last_error", "gs_set
            "gs_alloc_pinned", "gs_free_pinned", "gs_window_reduce", "gs_window_fold",
            "gs_window_fold_degree_max", "gs_window_csr", "gs_window_candidates", "gs_window_triangles",
            "gs_window_triangles_part", "gs_window_count_candidates",
-           "gs_generate_rmat", "gs_generate_uniform", "gs_generate_values", "gs_last_stage_times")
+           "gs_parse_edges_text", "gs_generate_rmat", "gs_generate_uniform", "gs_generate_values", "gs_last_stage_times")
 
 P = ctypes.c_void_p
 u64, i64, i32, u32 = ctypes.c_uint64, ctypes.c_int64, ctypes.c_int32, ctypes.c_uint32
@@ -122,6 +122,7 @@ def load() -> ctypes.CDLL:
         "gs_window_triangles_part": (st, [P, ctypes.POINTER(GsEdgeBatch), u32, u32, ctypes.POINTER(u64)]),
         "gs_window_count_candidates": (st, [P, ctypes.POINTER(GsPairBatch), ctypes.POINTER(u64), ctypes.POINTER(i32),
                                             ctypes.POINTER(i32), ctypes.POINTER(u64)]),
+        "gs_parse_edges_text": (st, [P, P, u64, i32, P, P, P, u64, i32, ctypes.POINTER(u64), ctypes.POINTER(u64)]),
         "gs_generate_rmat": (st, [P, i32, u64, u64, u32, u32, u32, i32, i32, u64, P, P]),
         "gs_generate_uniform": (st, [P, u64, u64, u64, u64, P, P]),
         "gs_generate_values": (st, [P, u64, u64, u64, i32, P]),

@@ -64,6 +64,8 @@ struct gs_ctx {
   gs::DevBuf dp_cnt, dp_csum, dp_off;
   // stage-2 candidate count (gs_pairs.hip): staged input columns, packed keys / payloads, group sums
   gs::DevBuf pr_a, pr_b, pr_f, pr_key, pr_val, pr_gk, pr_gv, pr_small;
+  // edge text parser (gs_text.hip): staged text, tile newline counts, record starts
+  gs::DevBuf tx_text, tx_cnt, tx_starts;
   hipEvent_t ev[6] = {};
   hipEvent_t pass_ev[9] = {};
   gs_stage_times times{};

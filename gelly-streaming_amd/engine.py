@@ -256,6 +256,29 @@ class Engine:
                                                        ctypes.byref(wrapped), ctypes.byref(has), ctypes.byref(groups)))
         return cnt.value, wrapped.value, bool(has.value), groups.value
 
+    def parse_edges_text(self, text, out_device: bool = True):
+        """gs_parse_edges_text: "src trg ts" records -> (src, dst, ts) int64 columns (WindowTriangles.java:175-185).
+        `text`: bytes / numpy uint8 (host) or a uint8 CUDA tensor.  Malformed records raise GsError."""
+        dev_in = _is_torch(text)
+        if dev_in:
+            assert text.is_cuda and text.dtype.itemsize == 1, "text must be a uint8 CUDA tensor"
+            text = text.contiguous()
+            ptr, nbytes = text.data_ptr(), text.numel()
+        else:
+            buf = np.frombuffer(text, dtype=np.uint8) if isinstance(text, (bytes, bytearray)) else \
+                np.ascontiguousarray(text, dtype=np.uint8)
+            text = buf
+            ptr, nbytes = (buf.ctypes.data if buf.size else None), buf.size
+        in_mem = L.GS_MEM_DEVICE if dev_in else L.GS_MEM_HOST
+        n_out, bad = ctypes.c_uint64(0), ctypes.c_uint64(0)
+        cap = nbytes // 6 + 1          # a record takes at least 6 bytes ("0 0 0\n"), the last one 5
+        cols = [self._empty(out_device, cap, np.int64) for _ in range(3)]
+        self._check(self._L.gs_parse_edges_text(self.ctx, ptr, nbytes, in_mem, _ptr(cols[0]), _ptr(cols[1]),
+                                                _ptr(cols[2]), cap, L.GS_MEM_DEVICE if out_device else L.GS_MEM_HOST,
+                                                ctypes.pointer(n_out), ctypes.pointer(bad)))
+        n = n_out.value
+        return tuple(c[:n] for c in cols)
+
     def triangles(self, src, dst):
         """gs_window_triangles: (exact count, the Integer the reference emits, has_output)."""
         b, keep, dev = self._batch(src, dst, None)

@@ -67,12 +67,13 @@ def window_triangles(edges: SimpleEdgeStream, window: Time) -> DataStream:
     return out
 
 
-def parse_edges_text(path: str):
-    """"src trg ts" per line (WindowTriangles.java:175-185) -> int64 columns."""
-    data = np.loadtxt(path, dtype=np.int64, ndmin=2)
-    if data.size == 0:
-        return np.empty(0, np.int64), np.empty(0, np.int64), np.empty(0, np.int64)
-    return data[:, 0].copy(), data[:, 1].copy(), data[:, 2].copy()
+def parse_edges_text(path: str, engine):
+    """"src trg ts" per line (WindowTriangles.java:175-185) -> int64 host columns, parsed on the GPU
+    (gs_parse_edges_text: the reference's split("\\s") + Long.parseLong rules; a malformed line raises
+    GsError, as the reference's map throws)."""
+    with open(path, "rb") as f:
+        text = f.read()
+    return engine.parse_edges_text(text, out_device=False)
 
 
 def default_edges():
@@ -90,7 +91,8 @@ def main(args=None, env: StreamExecutionEnvironment = None) -> list:
         if len(args) != 3:
             print("Usage: WindowTriangles <input edges path> <output path> <window time (ms)>", file=sys.stderr)
             return []
-        src, dst, ts = parse_edges_text(args[0])
+        env = env or StreamExecutionEnvironment.getExecutionEnvironment()
+        src, dst, ts = parse_edges_text(args[0], env.engine)
         window = Time.milliseconds(int(args[2]))
     else:
         src, dst, ts = default_edges()

@@ -224,6 +224,17 @@ typedef struct gs_pair_batch {
 GS_API gs_status gs_window_count_candidates(gs_ctx* ctx, const gs_pair_batch* pairs, uint64_t* count,
                                             int32_t* count_ref_wrapped, int32_t* has_output, uint64_t* groups);
 
+/* Edge text input of the examples: env.readTextFile(path).map(s.split("\\s") -> Long.parseLong of
+ * fields 0..2) (WindowTriangles.java:175-185).  Records end at '\n' (a trailing '\r' is dropped; text
+ * after the last '\n' is a record when non-empty); fields are separated by exactly one whitespace
+ * char; fields after the third are ignored.  Outputs src, dst, ts (the edge value the example turns
+ * into the event time) in record order.  Two-phase: *n_out = records (GS_ECAPACITY when capacity is
+ * short).  A record where the reference's map would throw gives GS_EINVAL and its index in
+ * *bad_record (~0 otherwise).  text < 4 GiB per call. */
+GS_API gs_status gs_parse_edges_text(gs_ctx* ctx, const char* text, uint64_t bytes, int32_t in_mem, int64_t* src,
+                                     int64_t* dst, int64_t* ts, uint64_t capacity, int32_t out_mem,
+                                     uint64_t* n_out, uint64_t* bad_record);
+
 /* ---- synthetic streams (bit-identical to oracle/gs_oracle.c) ------------------------ */
 /* R-MAT: 2^scale vertices, probabilities a, b, c (d = 1-a-b-c) as 32-bit fixed point,
  * optional seeded vertex permutation, optional self-loop removal (rewired, count kept). */

@@ -716,3 +716,74 @@ GSO_API uint64_t gso_baseline_reduce(const int64_t* src, const int64_t* dst, con
   free(part); free(part_n); free(args); free(th);
   return U;
 }
+
+/* ------------------------------------------------------------------------------------ */
+/* edge text input: example/WindowTriangles.java:175-185 (also ConnectedComponentsExample */
+/* .java:113-115): env.readTextFile(path) -> s.split("\\s") -> Long.parseLong(fields[0..2]) */
+/* ------------------------------------------------------------------------------------ */
+/* Flink 1.0.3 TextInputFormat: records are split at '\n'; a trailing '\r' is dropped from a
+ * record; the text after the last '\n' is a record only if it is non-empty.
+ * String.split("\\s") splits at every single whitespace char [ \t\n\x0B\f\r] and drops trailing
+ * empty strings, so field k (k < 3) is the run of non-whitespace chars that starts one separator
+ * after field k-1; an empty field (two separators in a row, leading whitespace, fewer than three
+ * fields) makes Long.parseLong throw, as does a sign without digits, any other char, or a value
+ * outside [-2^63, 2^63).  Fields after the third are ignored. */
+static int gso_is_ws(unsigned char ch) {
+  return ch == ' ' || ch == '\t' || ch == '\n' || ch == 0x0B || ch == '\f' || ch == '\r';
+}
+
+/* Long.parseLong(s[p..q)) -> 0 ok */
+static int gso_parse_long(const unsigned char* s, uint64_t p, uint64_t q, int64_t* out) {
+  if (p >= q) return -1;
+  int neg = 0;
+  if (s[p] == '-' || s[p] == '+') {
+    neg = s[p] == '-';
+    ++p;
+    if (p >= q) return -1;
+  }
+  const uint64_t lim = neg ? (1ull << 63) : (1ull << 63) - 1;
+  uint64_t v = 0;
+  for (; p < q; ++p) {
+    const unsigned d = (unsigned)s[p] - '0';
+    if (d > 9) return -1;
+    if (v > (lim - d) / 10) return -1;
+    v = v * 10 + d;
+  }
+  *out = neg ? (int64_t)(0 - v) : (int64_t)v;
+  return 0;
+}
+
+/* Parse one record s[p..q) (no '\n'); returns 0 ok. */
+static int gso_parse_record(const unsigned char* s, uint64_t p, uint64_t q, int64_t f[3]) {
+  if (q > p && s[q - 1] == '\r') --q;
+  uint64_t at = p;
+  for (int k = 0; k < 3; ++k) {
+    uint64_t e = at;
+    while (e < q && !gso_is_ws(s[e])) ++e;
+    if (gso_parse_long(s, at, e, &f[k])) return -1;
+    at = e + 1;
+  }
+  return 0;
+}
+
+/* returns the record count (>= 0), or -(1 + index of the first malformed record); outputs are
+ * written while the count fits cap */
+GSO_API int64_t gso_parse_edges_text(const char* text, uint64_t bytes, int64_t* src, int64_t* dst, int64_t* ts,
+                                     uint64_t cap) {
+  const unsigned char* s = (const unsigned char*)text;
+  uint64_t p = 0, n = 0;
+  while (p < bytes) {
+    const unsigned char* nl = memchr(s + p, '\n', bytes - p);
+    const uint64_t q = nl ? (uint64_t)(nl - s) : bytes;
+    int64_t f[3];
+    if (gso_parse_record(s, p, q, f)) return -1 - (int64_t)n;
+    if (n < cap) {
+      src[n] = f[0];
+      dst[n] = f[1];
+      ts[n] = f[2];
+    }
+    ++n;
+    p = q + 1;
+  }
+  return (int64_t)n;
+}

@@ -52,6 +52,7 @@ def lib():
             "gso_window_triangles_fwd": (ctypes.c_int32, [P, P, u64, P, P]),
             "gso_baseline_reduce": (u64, [P, P, P, u64, i32, i32, i32, i32]),
             "gso_java_hashset_cap": (u64, [u64]),
+            "gso_parse_edges_text": (i64, [ctypes.c_char_p, u64, P, P, P, u64]),
             "gso_java_long_bucket": (u32, [i64, u64]),
         }
         for name, (res, args) in sig.items():
@@ -171,6 +172,17 @@ def candidate_count(src, dst):
     tree = ctypes.c_int(0)
     need = lib().gso_window_candidates(_p(src), _p(dst), len(src), None, None, None, 0, ctypes.byref(tree))
     return -1 - need if need < 0 else need
+
+
+def parse_edges_text(text: bytes):
+    """"src trg ts" records (example/WindowTriangles.java:175-185, gso_parse_edges_text) -> int64 columns.
+    Raises ValueError(index of the first malformed record) where the reference's map throws."""
+    n = lib().gso_parse_edges_text(text, len(text), None, None, None, 0)
+    if n < 0:
+        raise ValueError(f"malformed edge record {-1 - n}")
+    s, d, t = np.empty(n, np.int64), np.empty(n, np.int64), np.empty(n, np.int64)
+    assert lib().gso_parse_edges_text(text, len(text), _p(s), _p(d), _p(t), n) == n
+    return s, d, t
 
 
 def count_candidates(a, b, is_candidate):

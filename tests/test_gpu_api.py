@@ -283,3 +283,50 @@ def test_two_stage_pipeline_itcase(pkg):
     cands = ws.applyOnNeighbors(triangles.GenerateCandidateEdges())
     got = triangles.count_triangles(cands, ws.engine).collect()
     assert sorted(got) == sorted(tuple(x) for x in t["expected"])
+
+
+def _edge_text(rng, n, crlf=False, extra=False):
+    from gelly_streaming_amd.textio import format_edges_text
+
+    cols = [rng.integers(-(1 << 40), 1 << 40, n), rng.integers(0, 1 << 62, n), rng.integers(-(1 << 63), (1 << 63) - 1, n)]
+    cols[0][: n // 4] = rng.integers(0, 100, n // 4)     # short lines too
+    t = format_edges_text(*cols, eol=b"\r\n" if crlf else b"\n")
+    if extra:
+        t = t.replace(b"\n", b" 17 junk\n", n // 2)    # fields after the third are ignored
+    return t, cols
+
+
+@pytest.mark.parametrize("case", ["plain", "crlf_extra", "no_final_newline", "device_text", "host_out"])
+def test_parse_edges_text_matches_oracle(engine, oracle, case):
+    rng = np.random.default_rng(["plain", "crlf_extra", "no_final_newline", "device_text", "host_out"].index(case))
+    n = 1 << 18
+    text, cols = _edge_text(rng, n, crlf=case == "crlf_extra", extra=case == "crlf_extra")
+    if case == "no_final_newline":
+        text = text[:-1]
+    want = oracle.parse_edges_text(text)
+    arg = torch.from_numpy(np.frombuffer(text, np.uint8).copy()).cuda() if case == "device_text" else text
+    got = engine.parse_edges_text(arg, out_device=case != "host_out")
+    for g, w, c in zip(got, want, cols):
+        g = g.cpu().numpy() if hasattr(g, "cpu") else g
+        assert np.array_equal(g, w) and np.array_equal(w, c)
+
+
+def test_parse_edges_text_errors_and_edges(engine, oracle):
+    from gelly_streaming_amd import GsError
+    from test_oracle_golden import BAD_RECORDS
+
+    rng = np.random.default_rng(5)
+    good, _ = _edge_text(rng, 5000)
+    lines = good.split(b"\n")
+    for bad in BAD_RECORDS:
+        at = int(rng.integers(0, 5000))
+        text = b"\n".join(lines[:at] + [bad] + lines[at:])
+        with pytest.raises(ValueError, match=f"record {at}$"):
+            oracle.parse_edges_text(text)
+        with pytest.raises(GsError, match=f"record {at} "):
+            engine.parse_edges_text(text)
+    assert [len(x) for x in engine.parse_edges_text(b"")] == [0, 0, 0]
+    for small in (b"1 2 3", b"1 2 3\n", b"1 2 3\r\n", b"-1\t-2\t-3 x"):
+        got = [x.cpu().numpy() for x in engine.parse_edges_text(small)]
+        want = oracle.parse_edges_text(small)
+        assert all(np.array_equal(g, w) for g, w in zip(got, want)), small

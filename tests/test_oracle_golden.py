@@ -138,3 +138,28 @@ def test_count_candidates_rules(oracle):
     assert oracle.count_candidates(a, b, f) == (2, 2, True, 2)
     assert oracle.count_candidates(a[3:5], b[3:5], f[3:5]) == (0, 0, False, 0)
     assert oracle.count_candidates(a[:0], b[:0], f[:0]) == (0, 0, False, 0)
+
+
+BAD_RECORDS = [b"1  2 3", b" 1 2 3", b"1 2", b"1 2 ", b"1 2 3x", b"1 2 9223372036854775808", b"", b"1 2 -",
+               b"1\t2\t+", b"1,2,3", b"1 2 -9223372036854775809", b"0x1 2 3"]
+
+
+def test_parse_edges_text_itcase_file(oracle):
+    """The ITCase input file ("src trg ts" lines, ExamplesTestData.java:21-34) parses to its edges."""
+    e = np.array(FIX["triangles"]["edges_src_trg_ts"], dtype=np.int64)
+    text = "\n".join(" ".join(str(x) for x in r) for r in e).encode()
+    s, d, t = oracle.parse_edges_text(text)
+    assert np.array_equal(np.stack([s, d, t], 1), e)
+
+
+def test_parse_edges_text_rules(oracle):
+    """split("\\s") + Long.parseLong: CRLF, tabs, a '+' sign, extreme values, extra fields, no final newline."""
+    s, d, t = oracle.parse_edges_text(b"1 2 3\r\n-4\t+5 6 extra fields\n9223372036854775807 "
+                                      b"-9223372036854775808 0\f\n7 8 9")
+    assert s.tolist() == [1, -4, 9223372036854775807, 7]
+    assert d.tolist() == [2, 5, -9223372036854775808, 8]
+    assert t.tolist() == [3, 6, 0, 9]
+    assert [len(x) for x in oracle.parse_edges_text(b"")] == [0, 0, 0]
+    for bad in BAD_RECORDS:
+        with pytest.raises(ValueError, match="record 1"):
+            oracle.parse_edges_text(b"1 2 3\n" + bad + b"\n4 5 6\n")
