@@ -27,6 +27,8 @@
  *   GenerateCandidateEdges example/WindowTriangles.java:83-116 (HashSet order, j >= i, i < len-1)
  *   CountTriangles        example/WindowTriangles.java:119-140 (int counters, emit iff edges > 0)
  *   timeWindowAll.sum(0)  example/WindowTriangles.java:66 (Integer sum, wraps mod 2^32)
+ *   edge text input       example/WindowTriangles.java:175-185 (readTextFile, split("\\s"),
+ *                         Long.parseLong; gso_parse_edges_text at the end of this file)
  *
  * Arithmetic follows Java: Integer/Long sums wrap (done in unsigned arithmetic),
  * Float/Double sums are IEEE adds in arrival order, min/max follow Math.min/Math.max.
