@@ -189,7 +189,7 @@ gs_status bucket_accumulate(gs_ctx* c, Src rs, uint64_t R, uint32_t nb, int64_t 
   hipEventRecord(c->ev[3], c->stream);
   GS_HIP(hipMemcpyAsync(c->host_small, sm + SM_BK_MM, 48, hipMemcpyDeviceToHost, c->stream));
   GS_HIP(hipMemcpyAsync(c->host_small + 6, sm + SM_TIMEOUT, 8, hipMemcpyDeviceToHost, c->stream));
-  GS_HIP(hipStreamSynchronize(c->stream));
+  GS_TRY(host_wait(c));
   if ((uint32_t)c->host_small[6] != 0) return set_error(c, GS_EDEVICE, "look-back spin timed out");
   *U = c->host_small[3];
   *n_items = (uint32_t)c->host_small[4];
@@ -256,7 +256,7 @@ gs_status bucket_direct(gs_ctx* c, const int64_t* src, const int64_t* dst, const
   GS_TRY(ensure(c, c->dp_cnt, (size_t)nt * BK_MAXB * 2));
   GS_TRY(launch_dp_hist<DIR>(c, src, dst, n, nt, base, S, nb));
   GS_HIP(hipMemcpyAsync(c->host_small, sm + SM_BK_MM, 24, hipMemcpyDeviceToHost, c->stream));
-  GS_HIP(hipStreamSynchronize(c->stream));
+  GS_TRY(host_wait(c));
   const int64_t kmin = key_min(c->host_small), kmax = key_max(c->host_small);
   if ((((uint64_t)kmax - (uint64_t)kmin) >> S) >= (uint64_t)BK_MAXB) return GS_EUNSUPPORTED;
   if (c->host_small[2]) {
@@ -345,7 +345,7 @@ gs_status bucket_onesweep(gs_ctx* c, const int64_t* src, const int64_t* dst, con
   int64_t base = c->bk_base;
   GS_TRY(launch_info<DIR>(c, src, dst, n, base, S));
   GS_HIP(hipMemcpyAsync(c->host_small, sm + SM_BK_MM, 24, hipMemcpyDeviceToHost, c->stream));
-  GS_HIP(hipStreamSynchronize(c->stream));
+  GS_TRY(host_wait(c));
   const int64_t kmin = key_min(c->host_small), kmax = key_max(c->host_small);
   if ((((uint64_t)kmax - (uint64_t)kmin) >> S) >= (uint64_t)BK_MAXB) return GS_EUNSUPPORTED;
   if (c->host_small[2]) {

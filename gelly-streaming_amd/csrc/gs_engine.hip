@@ -9,6 +9,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <chrono>
 
 #include "gs_ops.hpp"
 
@@ -29,6 +30,19 @@ gs_status set_error(gs_ctx* c, gs_status s, const char* fmt, ...) {
   return s;
 }
 
+gs_status host_wait(gs_ctx* c) {
+  if (!c->sync_ev) GS_HIP(hipEventCreateWithFlags(&c->sync_ev, hipEventDisableTiming));
+  GS_HIP(hipEventRecord(c->sync_ev, c->stream));
+  const auto t0 = std::chrono::steady_clock::now();
+  for (;;) {
+    const hipError_t e = hipEventQuery(c->sync_ev);
+    if (e == hipSuccess) return GS_OK;
+    if (e != hipErrorNotReady) return hip_check(c, e, "hipEventQuery");
+    if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(2)) break;
+  }
+  return hip_check(c, hipEventSynchronize(c->sync_ev), "hipEventSynchronize");
+}
+
 gs_status hip_check(gs_ctx* c, hipError_t e, const char* what) {
   if (e == hipSuccess) return GS_OK;
   return set_error(c, e == hipErrorOutOfMemory ? GS_ENOMEM : GS_EDEVICE, "%s: %s", what, hipGetErrorString(e));
@@ -38,7 +52,7 @@ gs_status ensure(gs_ctx* c, DevBuf& b, size_t bytes, bool zero) {
   if (bytes == 0) bytes = 16;
   if (b.bytes >= bytes) return GS_OK;
   if (b.p) {
-    GS_HIP(hipStreamSynchronize(c->stream));
+    GS_TRY(host_wait(c));
     GS_HIP(hipFree(b.p));
     b.p = nullptr;
     b.bytes = 0;
@@ -186,7 +200,7 @@ static gs_status sort_dir(gs_ctx* c, const int64_t* src, const int64_t* dst, con
   const int64_t* k0p = (DIR == DIR_IN) ? dst : src;
   GS_HIP(hipMemcpyAsync(sm + SM_K0, k0p, 8, hipMemcpyDeviceToDevice, c->stream));
   GS_HIP(hipMemcpyAsync(c->host_small, sm, 16, hipMemcpyDeviceToHost, c->stream));
-  GS_HIP(hipStreamSynchronize(c->stream));
+  GS_TRY(host_wait(c));
   const uint64_t mask = c->host_small[0], k0 = c->host_small[1];
   const int bits = mask ? 64 - __builtin_clzll(mask) : 0;
   out->bits = bits;
@@ -249,7 +263,7 @@ gs_status sort_buffer(gs_ctx* c, const uint64_t* keys, const uint32_t* vals, uin
   GS_HIP(hipGetLastError());
   GS_HIP(hipMemcpyAsync(sm + SM_K0, keys, 8, hipMemcpyDeviceToDevice, c->stream));
   GS_HIP(hipMemcpyAsync(c->host_small, sm, 16, hipMemcpyDeviceToHost, c->stream));
-  GS_HIP(hipStreamSynchronize(c->stream));
+  GS_TRY(host_wait(c));
   const uint64_t mask = c->host_small[0], k0 = c->host_small[1];
   const int bits = mask ? 64 - __builtin_clzll(mask) : 0;
   out->bits = bits;
@@ -379,6 +393,7 @@ void gs_destroy(gs_ctx* c) {
     if (e) hipEventDestroy(e);
   for (auto& e : c->pass_ev)
     if (e) hipEventDestroy(e);
+  if (c->sync_ev) hipEventDestroy(c->sync_ev);
   if (c->host_small) hipHostFree(c->host_small);
   if (c->own_stream && c->stream) hipStreamDestroy(c->stream);
   delete c;
@@ -422,7 +437,7 @@ static gs_status finish_vertex_out(gs_ctx* c, gs_vertex_out* out, const int64_t*
   if (U > out->capacity) return set_error(c, GS_ECAPACITY, "output needs %llu vertices", (unsigned long long)U);
   GS_TRY(deliver(c, out->keys, kd, U * 8, out->mem));
   GS_TRY(deliver(c, out->vals, vd, U * ob, out->mem));
-  if (!direct) GS_HIP(hipStreamSynchronize(c->stream));
+  if (!direct) GS_TRY(host_wait(c));
   return GS_OK;
 }
 
@@ -533,7 +548,7 @@ gs_status gs_window_fold_degree_max(gs_ctx* c, const gs_edge_batch* b, int32_t d
   GS_TRY(deliver(c, out->keys, kd, U * 8, out->mem));
   GS_TRY(deliver(c, out->degree, dd, U * 8, out->mem));
   GS_TRY(deliver(c, out->max_neighbor, md, U * 8, out->mem));
-  if (!direct) GS_HIP(hipStreamSynchronize(c->stream));
+  if (!direct) GS_TRY(host_wait(c));
   return GS_OK;
 }
 

@@ -239,7 +239,7 @@ gs_status gs_window_csr(gs_ctx* c, const gs_edge_batch* b, int32_t dir, gs_csr_o
   GS_TRY(deliver(c, out->offsets, od, (U + 1) * 8, out->mem));
   GS_TRY(deliver(c, out->neighbors, nd, R * 8, out->mem));
   if (want_vals) GS_TRY(deliver(c, out->vals, vd, R * vb, out->mem));
-  GS_HIP(hipStreamSynchronize(c->stream));
+  GS_TRY(host_wait(c));
   return GS_OK;
 }
 
@@ -262,7 +262,7 @@ static gs_status triangles_impl(gs_ctx* c, const gs_edge_batch* b, uint32_t part
   GS_TRY(launch_keyinfo_all(c, src, dst, n));
   GS_HIP(hipMemcpyAsync(sm + SM_K0, src, 8, hipMemcpyDeviceToDevice, c->stream));
   GS_HIP(hipMemcpyAsync(c->host_small, sm, 16, hipMemcpyDeviceToHost, c->stream));
-  GS_HIP(hipStreamSynchronize(c->stream));
+  GS_TRY(host_wait(c));
   const uint64_t mask = c->host_small[0], k0 = c->host_small[1];
   const uint32_t B = mask ? 64 - __builtin_clzll(mask) : 1;
   if (B > TRI_MAX_BITS)
@@ -362,7 +362,7 @@ static gs_status triangles_impl(gs_ctx* c, const gs_edge_batch* b, uint32_t part
   hipEventRecord(c->ev[3], c->stream);
   GS_HIP(hipMemcpyAsync(c->host_small, sm, 32, hipMemcpyDeviceToHost, c->stream));
   GS_HIP(hipMemcpyAsync(c->host_small + 6, d_probes, 8, hipMemcpyDeviceToHost, c->stream));
-  GS_HIP(hipStreamSynchronize(c->stream));
+  GS_TRY(host_wait(c));
   if ((uint32_t)c->host_small[3] != 0) return set_error(c, GS_EDEVICE, "look-back spin timed out");
   uint64_t T = c->host_small[2];
   {   // stage times (path 3): sym + sort, unique, rows + orientation, light count, heavy count

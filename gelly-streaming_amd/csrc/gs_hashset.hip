@@ -373,7 +373,7 @@ gs_status hashset_order(gs_ctx* c, const int64_t* src, const int64_t* dst, uint6
                      (uint32_t)U, c->hs[HS_IDS].as<int64_t>(), d_tree);
   GS_HIP(hipGetLastError());
   GS_HIP(hipMemcpyAsync(c->host_small + 6, sm + SM_TIMEOUT, 8, hipMemcpyDeviceToHost, c->stream));
-  GS_HIP(hipStreamSynchronize(c->stream));
+  GS_TRY(host_wait(c));
   *treeified = (c->host_small[6] >> 32) != 0;
   *U_out = (uint32_t)U;
   *M_out = (uint32_t)M;
@@ -396,7 +396,7 @@ gs_status triangle_selfpair_term(gs_ctx* c, const int64_t* src, const int64_t* d
                      c->hs[HS_DOFF].as<uint64_t>(), U, c->hs[HS_VKEYS].as<int64_t>(), loops, loops_xor, d);
   GS_HIP(hipGetLastError());
   GS_HIP(hipMemcpyAsync(c->host_small + 7, d, 8, hipMemcpyDeviceToHost, c->stream));
-  GS_HIP(hipStreamSynchronize(c->stream));
+  GS_TRY(host_wait(c));
   *S = c->host_small[7];
   return GS_OK;
 }
@@ -440,7 +440,7 @@ gs_status gs_window_candidates(gs_ctx* c, const gs_edge_batch* b, gs_pair_out* o
   GS_TRY(xscan(c, c->hs[HS_L].as<uint64_t>(), M, c->hs[HS_LS].as<uint64_t>()));
   uint64_t P = 0;
   GS_HIP(hipMemcpyAsync(&c->host_small[7], c->hs[HS_LS].as<uint64_t>() + M, 8, hipMemcpyDeviceToHost, c->stream));
-  GS_HIP(hipStreamSynchronize(c->stream));
+  GS_TRY(host_wait(c));
   P = c->host_small[7];
   const uint64_t total = R + P;
   *out->n_out = total;
@@ -468,7 +468,7 @@ gs_status gs_window_candidates(gs_ctx* c, const gs_edge_batch* b, gs_pair_out* o
     GS_HIP(hipMemcpyAsync(out->b, bb, total * 8, hipMemcpyDeviceToHost, c->stream));
     GS_HIP(hipMemcpyAsync(out->is_candidate, f, total, hipMemcpyDeviceToHost, c->stream));
   }
-  GS_HIP(hipStreamSynchronize(c->stream));
+  GS_TRY(host_wait(c));
   return GS_OK;
 }
 

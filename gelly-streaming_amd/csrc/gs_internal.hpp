@@ -67,6 +67,7 @@ struct gs_ctx {
   // edge text parser (gs_text.hip): staged text, tile newline counts, record starts
   gs::DevBuf tx_text, tx_cnt, tx_starts;
   hipEvent_t ev[6] = {};
+  hipEvent_t sync_ev = nullptr;   // host_wait: polled completion event
   hipEvent_t pass_ev[9] = {};
   gs_stage_times times{};
   uint64_t* host_small = nullptr;  // pinned mirror of small scalars
@@ -116,6 +117,10 @@ gs_status bucket_reduce(gs_ctx* c, const int64_t* src, const int64_t* dst, const
                         int op, int dtype, bool has_init, const void* init, int64_t* keys, void* vals, uint64_t* U);
 gs_status bucket_degree_max(gs_ctx* c, const int64_t* src, const int64_t* dst, uint64_t n, int dir, int64_t init_max,
                             int64_t* keys, int64_t* deg, int64_t* mx, uint64_t* U);
+// Wait on the host for the ctx stream: poll a completion event for up to 2 ms, then block.  The host
+// reads small results mid-window (vertex range, output count); a blocking wait's wake-up latency is
+// paid twice per window otherwise.
+gs_status host_wait(gs_ctx* c);
 // clear the look-back timeout word at the start of a public call
 gs_status begin_call(gs_ctx* c);
 

@@ -59,7 +59,7 @@ inline gs_status launch_rbk(gs_ctx* c, const Sorted& s, Out o, uint64_t* n_uniqu
   GS_HIP(hipGetLastError());
   hipEventRecord(c->ev[3], c->stream);
   GS_HIP(hipMemcpyAsync(c->host_small, sm, 32, hipMemcpyDeviceToHost, c->stream));
-  GS_HIP(hipStreamSynchronize(c->stream));
+  GS_TRY(host_wait(c));
   if ((uint32_t)c->host_small[3] != 0) return set_error(c, GS_EDEVICE, "look-back spin timed out");
   *n_unique_host = c->host_small[2];
   return GS_OK;
@@ -144,7 +144,7 @@ inline gs_status reduce_fused(gs_ctx* c, const Sorted& s, Out o, uint64_t* U) {
                      table, (unsigned long long*)(sm + SM_TOTAL));
   GS_HIP(hipGetLastError());
   GS_HIP(hipMemcpyAsync(c->host_small + 5, sm + SM_TOTAL, 8, hipMemcpyDeviceToHost, c->stream));
-  GS_HIP(hipStreamSynchronize(c->stream));
+  GS_TRY(host_wait(c));
   const uint64_t parts = c->host_small[5];
   c->times.partials = parts;
   const unsigned g = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((parts + 255) / 256, 8192));

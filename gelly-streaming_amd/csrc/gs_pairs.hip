@@ -123,7 +123,7 @@ extern "C" gs_status gs_window_count_candidates(gs_ctx* c, const gs_pair_batch* 
   GS_HIP(hipGetLastError());
   uint64_t h[4];
   GS_HIP(hipMemcpyAsync(h, mm, 32, hipMemcpyDeviceToHost, c->stream));
-  GS_HIP(hipStreamSynchronize(c->stream));
+  GS_TRY(host_wait(c));
   const int64_t amin = (int64_t)(~h[0] ^ (1ull << 63)), amax = (int64_t)(h[1] ^ (1ull << 63));
   const int64_t bmin = (int64_t)(~h[2] ^ (1ull << 63)), bmax = (int64_t)(h[3] ^ (1ull << 63));
   if ((uint64_t)amax - (uint64_t)amin >= (1ull << 32) || (uint64_t)bmax - (uint64_t)bmin >= (1ull << 32))
@@ -143,7 +143,7 @@ extern "C" gs_status gs_window_count_candidates(gs_ctx* c, const gs_pair_batch* 
   hipLaunchKernelGGL(k_pr_count, dim3(grid_for(c, U)), dim3(PR_BLOCK), 0, c->stream, c->pr_gv.as<int64_t>(), U, mm);
   GS_HIP(hipGetLastError());
   GS_HIP(hipMemcpyAsync(h, mm, 16, hipMemcpyDeviceToHost, c->stream));
-  GS_HIP(hipStreamSynchronize(c->stream));
+  GS_TRY(host_wait(c));
   *count = h[0];
   *count_ref_wrapped = (int32_t)(uint32_t)h[0];
   *groups = h[1];

@@ -279,7 +279,7 @@ extern "C" gs_status gs_parse_edges_text(gs_ctx* c, const char* text, uint64_t b
   uint8_t last = 0;
   GS_HIP(hipMemcpyAsync(h, cnt + nt, 4, hipMemcpyDeviceToHost, c->stream));
   GS_HIP(hipMemcpyAsync(&last, t + bytes - 1, 1, hipMemcpyDeviceToHost, c->stream));
-  GS_HIP(hipStreamSynchronize(c->stream));
+  GS_TRY(host_wait(c));
   const uint32_t nl = h[0];
   const uint64_t nrec = (uint64_t)nl + (last != '\n' ? 1 : 0);
   *n_out = nrec;
@@ -307,7 +307,7 @@ extern "C" gs_status gs_parse_edges_text(gs_ctx* c, const char* text, uint64_t b
   GS_HIP(hipGetLastError());
   uint64_t hb = 0;
   GS_HIP(hipMemcpyAsync(&hb, bad, 8, hipMemcpyDeviceToHost, c->stream));
-  GS_HIP(hipStreamSynchronize(c->stream));
+  GS_TRY(host_wait(c));
   if (hb != ~0ull) {
     *bad_record = hb;
     return set_error(c, GS_EINVAL, "parse_edges_text: malformed edge record %llu (Long.parseLong would throw)",
@@ -317,7 +317,7 @@ extern "C" gs_status gs_parse_edges_text(gs_ctx* c, const char* text, uint64_t b
     GS_HIP(hipMemcpyAsync(src, s, nrec * 8, hipMemcpyDeviceToHost, c->stream));
     GS_HIP(hipMemcpyAsync(dst, d, nrec * 8, hipMemcpyDeviceToHost, c->stream));
     GS_HIP(hipMemcpyAsync(ts, w, nrec * 8, hipMemcpyDeviceToHost, c->stream));
-    GS_HIP(hipStreamSynchronize(c->stream));
+    GS_TRY(host_wait(c));
   }
   return GS_OK;
 }
