@@ -34,26 +34,6 @@ def owner_bounds(kmin: int, kmax: int, world: int) -> list:
     return [kmin + (span * r) // world for r in range(1, world)]
 
 
-_pinned = {}
-
-
-def _host_read(t: torch.Tensor) -> list:
-    """Small device tensor -> Python list, waiting by polling an event: a blocking stream sync pays a
-    thread wake-up (measured ~0.25 ms each under an initialised RCCL communicator), twice per window."""
-    if not t.is_cuda:
-        return t.tolist()
-    key = (t.numel(), t.dtype)
-    h = _pinned.get(key)
-    if h is None:
-        h = _pinned[key] = torch.empty(t.numel(), dtype=t.dtype, pin_memory=True)
-    h.copy_(t.reshape(-1), non_blocking=True)
-    ev = torch.cuda.Event()
-    ev.record()
-    while not ev.query():
-        pass
-    return h.tolist()
-
-
 def exchange_sorted(keys: torch.Tensor, cols: list, group=None):
     """Send each owner its slice of (keys, *cols); keys must be ascending.  Returns received tensors."""
     world = dist.get_world_size(group)
@@ -63,7 +43,7 @@ def exchange_sorted(keys: torch.Tensor, cols: list, group=None):
     else:
         mm = torch.tensor([-(1 << 63), -(1 << 63)], dtype=torch.int64, device=dev)
     dist.all_reduce(mm, op=dist.ReduceOp.MAX, group=group)
-    mx = _host_read(mm)
+    mx = mm.tolist()
     kmax, kmin = mx[0], -mx[1]
     if kmax < kmin:   # no rank has a vertex in this window
         return keys[:0], [c[:0] for c in cols]
@@ -74,7 +54,7 @@ def exchange_sorted(keys: torch.Tensor, cols: list, group=None):
     send = (edges[1:] - edges[:-1]).to(torch.int64)
     recv = torch.empty_like(send)
     dist.all_to_all_single(recv, send, group=group)
-    sr = _host_read(torch.cat([send, recv]))
+    sr = torch.cat([send, recv]).tolist()   # one host read for both
     send_l, recv_l = sr[:world], sr[world:]
     total = sum(recv_l)
     # keys travel as 32-bit offsets from the global minimum when the window's span allows (12-byte

@@ -24,7 +24,7 @@ E = 1 << 28
 src, dst = eng.generate_rmat(24, E, 0x5EED02, first_edge=rank * E)
 val = eng.generate_values(E, 0x5EED02, 1, first_edge=rank * E)
 ph = {"local": [], "exchange": [], "merge": []}
-for it in range(6):
+for it in range(8):
     torch.cuda.synchronize(); dist.barrier(); torch.cuda.synchronize()
     t0 = time.perf_counter()
     k, v = eng.reduce(src, dst, val, 1, 0)
@@ -34,7 +34,9 @@ for it in range(6):
     mk, mv = eng.reduce(rk, rk, rv, 1, 0)
     torch.cuda.synchronize(); t3 = time.perf_counter()
     if it >= 2:
-        ph["local"].append((t1 - t0) * 1e3); ph["exchange"].append((t2 - t1) * 1e3); ph["merge"].append((t3 - t2) * 1e3)
+        ph["local"].append((t1 - t0) * 1e3)
+        ph["exchange"].append((t2 - t1) * 1e3)
+        ph["merge"].append((t3 - t2) * 1e3)
 if rank == 0:
     print({n: round(sum(x) / len(x), 3) for n, x in ph.items()}, "local U", k.numel(), "received", rk.numel(),
           "owned", mk.numel(), flush=True)
