@@ -7,7 +7,7 @@
 //
 // Middle-vertex order: a wave takes v, puts N+(v) into an LDS hash set of 4-slot buckets, spreads the
 // concatenation of N+(u) over a chunk of TH_DMAX in-neighbours u across its lanes (prefix of |N+(u)|
-// in LDS, one search per TH_ILP consecutive items) and probes each w with one 16-byte LDS read.
+// in LDS, one search per TH_ILP = 8 consecutive items) and probes each w with one 16-byte LDS read.
 // Probing N+(u) from the middle vertex costs sum_u d+(u)^2 probes, against sum over edges u -> v of
 // d+(v) from the first vertex (R-MAT scale 20: 2.47 G against 4.27 G).  In-lists longer than a chunk
 // queue their further chunks for a second pass (a hub's work spreads over many waves); vertices with
@@ -19,8 +19,17 @@
 namespace gs {
 
 constexpr int TH_BLOCK = 256, TH_WPB = TH_BLOCK / WAVE;
-constexpr uint32_t TH_DMAX = 512, TH_H = 1024, TH_EMPTY = 0xFFFFFFFFu;
-constexpr int TH_ILP = 4;   // consecutive items per lane: one search, TH_ILP probes in flight
+#ifndef GS_TH_DMAX
+#define GS_TH_DMAX 512
+#endif
+constexpr uint32_t TH_DMAX = GS_TH_DMAX, TH_H = 1024, TH_EMPTY = 0xFFFFFFFFu;
+// a light vertex's N+(v) (<= TH_DMAX entries) must leave the TH_H-slot table at most half full: insert
+// and probe chains end at a free slot, so a full table would never end them
+static_assert(TH_DMAX * 2 <= TH_H, "TH_DMAX must be <= TH_H / 2");
+#ifndef GS_TH_ILP
+#define GS_TH_ILP 8   // measured at R-MAT s22: 2 -> 93.9 ms, 4 -> 70.2, 6 -> 62.6, 8 -> 62.0, 12 -> 64.5, 16 -> 137.8
+#endif
+constexpr int TH_ILP = GS_TH_ILP;   // consecutive items per lane: one search, TH_ILP probes in flight
 
 __device__ __forceinline__ uint32_t th_hash(uint32_t x, uint32_t mask) { return ((x * 0x9E3779B1u) >> 7) & mask; }
 // LDS written by some lanes of a wave, then read by others
