@@ -5,6 +5,7 @@
 //   gs_window_fold_degree_max <- foldNeighbors with a degree / max-neighbour EdgesFold
 // Window = one columnar batch: keyinfo -> LSD onesweep passes -> reduce-by-key.
 #include <stdarg.h>
+#include <stdlib.h>
 #include <stdio.h>
 #include <string.h>
 
@@ -31,6 +32,8 @@ gs_status set_error(gs_ctx* c, gs_status s, const char* fmt, ...) {
 }
 
 gs_status host_wait(gs_ctx* c) {
+  static const bool blocking = getenv("GS_BLOCKING_WAIT") != nullptr;   // A/B switch for measurements
+  if (blocking) return hip_check(c, hipStreamSynchronize(c->stream), "hipStreamSynchronize");
   if (!c->sync_ev) GS_HIP(hipEventCreateWithFlags(&c->sync_ev, hipEventDisableTiming));
   GS_HIP(hipEventRecord(c->sync_ev, c->stream));
   const auto t0 = std::chrono::steady_clock::now();
