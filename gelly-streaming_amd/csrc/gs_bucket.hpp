@@ -479,6 +479,13 @@ static __global__ __launch_bounds__(BK_PLAN_BLOCK) void k_bk_plan(const uint32_t
 #ifndef GS_DP_XCD
 #define GS_DP_XCD 1
 #endif
+// 1: payloads go straight from registers to their global slot (off[t][b] + rank) instead of through
+// LDS; the tile's LDS drops to the staged keys + tables (two blocks per CU).  Measured on C2 (scatter,
+// ms): staged 10 items 1.65; direct 6 items 1.75 (staged 6 items 1.89); direct 8 and 10 items spill at
+// the 64-VGPR cap of two blocks per CU (2.20, 3.17).  Kept off; the A/B stays buildable.
+#ifndef GS_DP_VDIRECT
+#define GS_DP_VDIRECT 0
+#endif
 constexpr int DP_BLOCK = 1024;
 constexpr int DP_ITEMS = GS_DP_ITEMS;
 constexpr uint32_t DP_TILE = DP_BLOCK * DP_ITEMS;   // 10240 records < 2^16
@@ -677,14 +684,20 @@ __device__ __forceinline__ void dp_load_raw(const BaseSrc<V, DIR, PAY>& es, uint
 // per CU (1.71 ms), keys and values staged in turn through one region for 2 blocks per CU (1.81 ms
 // at 8192 records, 2.21 at 10240: the 64-VGPR cap spills).
 // V: loaded payload; VO: stored payload (REL: VO = V - base, out-of-range payloads set *rel_bad)
+#if GS_DP_VDIRECT
+#define GS_DP_SCATTER_ATTR __attribute__((amdgpu_waves_per_eu(8, 8)))   // two 16-wave blocks per CU
+#else
+#define GS_DP_SCATTER_ATTR
+#endif
 template <typename V, int DIR, int PAY, typename VO = V, bool REL = false>
-__global__ __launch_bounds__(DP_BLOCK) void k_dp_scatter(BaseSrc<V, DIR, PAY> es, uint64_t n, int S, uint32_t nbp,
+__global__ __launch_bounds__(DP_BLOCK) GS_DP_SCATTER_ATTR void k_dp_scatter(BaseSrc<V, DIR, PAY> es, uint64_t n, int S, uint32_t nbp,
                                                          const uint32_t* __restrict__ off,
                                                          uint16_t* __restrict__ k16, VO* __restrict__ vout,
                                                          uint32_t* __restrict__ rel_bad) {
   constexpr bool HAS_V = PAY != PAY_NONE;
+  constexpr bool STAGE_V = HAS_V && !GS_DP_VDIRECT;
   __shared__ uint32_t s_key[DP_TILE];                // (bucket << 16) | bucket-local index, bucket order
-  __shared__ VO s_val[HAS_V ? DP_TILE : 1];
+  __shared__ VO s_val[STAGE_V ? DP_TILE : 1];
   __shared__ uint32_t s_cnt[BK_MAXB];                // counts, then run starts inside the tile
   __shared__ uint32_t s_delta[BK_MAXB];              // global position - tile position of bucket b's run
   __shared__ uint32_t s_w[DP_BLOCK / WAVE];
@@ -724,13 +737,16 @@ __global__ __launch_bounds__(DP_BLOCK) void k_dp_scatter(BaseSrc<V, DIR, PAY> es
       if (FULL || (uint32_t)u * DP_BLOCK + tid < nrec) {
         const uint32_t pos = s_cnt[kb[u] >> 16] + rk[u];
         s_key[pos] = kb[u];
+        VO vo{};
         if constexpr (REL) {
           const uint64_t rel = (uint64_t)vv[u] - (uint64_t)es.base;
           bad |= (rel >> 32) != 0;
-          s_val[pos] = (VO)rel;
+          vo = (VO)rel;
         } else if constexpr (HAS_V) {
-          s_val[pos] = vv[u];
+          vo = vv[u];
         }
+        if constexpr (STAGE_V) s_val[pos] = vo;
+        else if constexpr (HAS_V) vout[s_delta[kb[u] >> 16] + pos] = vo;
       }
     }
     __syncthreads();
@@ -741,14 +757,14 @@ __global__ __launch_bounds__(DP_BLOCK) void k_dp_scatter(BaseSrc<V, DIR, PAY> es
         const uint32_t kv = s_key[j];
         const uint32_t d = s_delta[kv >> 16] + j;
         k16[d] = (uint16_t)kv;
-        if constexpr (HAS_V) vout[d] = s_val[j];
+        if constexpr (STAGE_V) vout[d] = s_val[j];
       }
     } else {
       for (uint32_t j = tid; j < nrec; j += DP_BLOCK) {
         const uint32_t kv = s_key[j];
         const uint32_t d = s_delta[kv >> 16] + j;
         k16[d] = (uint16_t)kv;
-        if constexpr (HAS_V) vout[d] = s_val[j];
+        if constexpr (STAGE_V) vout[d] = s_val[j];
       }
     }
   };
