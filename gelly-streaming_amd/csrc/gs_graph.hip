@@ -308,7 +308,7 @@ static gs_status triangles_impl(gs_ctx* c, const gs_edge_batch* b, uint32_t part
   adj.key_xor = 0;
   adj.records = E2;
   GS_HIP(hipMemsetAsync(c->out_a.p, 0, V * 4, c->stream));   // vertices without edges: degree 0
-  GS_TRY(ensure(c, c->tri_heavy, V * 4));
+  GS_TRY(ensure(c, c->tri_heavy, (V + E2 / 2 / TH_VCH + 64) * 8));   // (v, in-chunk) items
   GS_TRY(ensure(c, c->tri_range, V * 16));
   RowOut ro{c->out_a.as<uint32_t>(), c->out_b.as<uint32_t>()};
   uint64_t nv = 0;
@@ -350,13 +350,13 @@ static gs_status triangles_impl(gs_ctx* c, const gs_edge_batch* b, uint32_t part
   for (int pass = 0; pass < 2; ++pass) {
     hipLaunchKernelGGL(k_tri_light, dim3(pass == 0 ? nvb : 4096u), dim3(TH_BLOCK), 0, c->stream,
                        c->tri_onbr.as<uint32_t>(), c->tri_ou.as<uint32_t>(), out_range, in_range, (uint32_t)V,
-                       (uint32_t)q0, (uint32_t)q1, pass, queue, d_nqueue, c->tri_heavy.as<uint32_t>(), d_nheavy,
+                       (uint32_t)q0, (uint32_t)q1, pass, queue, d_nqueue, c->tri_heavy.as<uint2>(), d_nheavy,
                        d_total, d_probes);
     GS_HIP(hipGetLastError());
   }
   hipEventRecord(c->ev[5], c->stream);
   hipLaunchKernelGGL(k_tri_heavy, dim3(256), dim3(TH_HBLOCK), 0, c->stream, c->tri_onbr.as<uint32_t>(),
-                     c->tri_ou.as<uint32_t>(), out_range, in_range, c->tri_heavy.as<uint32_t>(), d_nheavy, d_total,
+                     c->tri_ou.as<uint32_t>(), out_range, in_range, c->tri_heavy.as<uint2>(), d_nheavy, d_total,
                      d_probes);
   GS_HIP(hipGetLastError());
   hipEventRecord(c->ev[3], c->stream);

@@ -19,6 +19,9 @@
 namespace gs {
 
 constexpr int TH_BLOCK = 256, TH_WPB = TH_BLOCK / WAVE;
+// k_tri_heavy: 1024 threads, N+(v) of up to TH_NU entries in LDS, in-neighbours in chunks of TH_VCH
+constexpr int TH_HBLOCK = 1024;
+constexpr uint32_t TH_NU = 16384, TH_HB = TH_NU / 2, TH_VCH = 2048;   // TH_HB 4-slot buckets: load <= 1/2
 #ifndef GS_TH_DMAX
 #define GS_TH_DMAX 512
 #endif
@@ -176,7 +179,7 @@ __global__ __launch_bounds__(TH_BLOCK) void k_tri_light(const uint32_t* __restri
                                                         const uint2* __restrict__ out_range,
                                                         const uint2* __restrict__ in_range, uint32_t nv, uint32_t q0,
                                                         uint32_t q1, int pass, uint2* __restrict__ queue,
-                                                        uint32_t* __restrict__ n_queue, uint32_t* __restrict__ heavy,
+                                                        uint32_t* __restrict__ n_queue, uint2* __restrict__ heavy,
                                                         uint32_t* __restrict__ n_heavy,
                                                         unsigned long long* __restrict__ total,
                                                         unsigned long long* __restrict__ n_probes) {
@@ -194,8 +197,12 @@ __global__ __launch_bounds__(TH_BLOCK) void k_tri_light(const uint32_t* __restri
       v = it;
       const uint2 ro = out_range[v], ri = in_range[v];
       if (ro.y == ro.x || ri.y == ri.x || ro.x < q0 || ro.x >= q1) continue;
-      if (ro.y - ro.x > TH_DMAX) {
-        if (lane == 0) heavy[atomicAdd(n_heavy, 1u)] = v;
+      if (ro.y - ro.x > TH_DMAX) {   // one heavy item per TH_VCH in-neighbours: a hub spreads over blocks
+        const uint32_t nhc = (ri.y - ri.x + TH_VCH - 1) / TH_VCH;
+        uint32_t at = 0;
+        if (lane == 0) at = atomicAdd(n_heavy, nhc);
+        at = __shfl(at, 0, WAVE);
+        for (uint32_t j = lane; j < nhc; j += WAVE) heavy[at + j] = make_uint2(v, j);
         continue;
       }
       const uint32_t nch = (ri.y - ri.x + TH_DMAX - 1) / TH_DMAX;
@@ -222,16 +229,15 @@ __global__ __launch_bounds__(TH_BLOCK) void k_tri_light(const uint32_t* __restri
   if (lane == 0 && probes) atomicAdd(n_probes, (unsigned long long)probes);   // wave-uniform
 }
 
-// one block per heavy vertex v: N+(v) as an LDS hash set (up to TH_NU entries; longer lists are
-// binary-searched in HBM), the in-neighbours' lists in chunks of TH_VCH, TH_ILP items per thread
-// with one search
-constexpr int TH_HBLOCK = 1024;
-constexpr uint32_t TH_NU = 16384, TH_HB = TH_NU / 2, TH_VCH = 2048;   // TH_HB 4-slot buckets: load <= 1/2
+// one block per heavy item (v, chunk of TH_VCH in-neighbours): N+(v) as an LDS hash set (up to TH_NU
+// entries; longer lists are binary-searched in HBM; rebuilt only when the block's item changes v),
+// the chunk's lists TH_ILP items per thread with one search.  One item per in-chunk spreads a hub over
+// many blocks (one block per heavy vertex left the hubs' blocks running long after the rest).
 __global__ __launch_bounds__(TH_HBLOCK) void k_tri_heavy(const uint32_t* __restrict__ onbr,
                                                          const uint32_t* __restrict__ inbr,
                                                          const uint2* __restrict__ out_range,
                                                          const uint2* __restrict__ in_range,
-                                                         const uint32_t* __restrict__ heavy,
+                                                         const uint2* __restrict__ heavy,
                                                          const uint32_t* __restrict__ n_heavy,
                                                          unsigned long long* __restrict__ total,
                                                          unsigned long long* __restrict__ n_probes) {
@@ -244,22 +250,26 @@ __global__ __launch_bounds__(TH_HBLOCK) void k_tri_heavy(const uint32_t* __restr
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   uint64_t cnt = 0, probes = 0;
   const uint32_t nh = *n_heavy;
+  uint32_t table_v = TH_EMPTY;   // the vertex whose N+ the LDS table holds (block-uniform)
   for (uint32_t hi = blockIdx.x; hi < nh; hi += gridDim.x) {
-    const uint32_t v = heavy[hi];
+    const uint2 item = heavy[hi];   // (v, in-chunk)
+    const uint32_t v = item.x;
     const uint2 ro = out_range[v], ri = in_range[v];
     const uint32_t d = ro.y - ro.x;
     const bool in_lds = d <= TH_NU;   // else: binary search of the sorted list in HBM
     uint32_t nb = 16;
     while (nb * 2 < d && nb < TH_HB) nb <<= 1;
     const uint32_t bmask = nb - 1;
-    __syncthreads();   // the previous vertex is done with the table
-    if (in_lds) {
+    __syncthreads();   // the previous item is done with the table
+    if (in_lds && table_v != v) {
       for (uint32_t i = tid; i < nb * 4; i += TH_HBLOCK) hs[i] = TH_EMPTY;
       __syncthreads();
       for (uint32_t i = tid; i < d; i += TH_HBLOCK) th_insert(hs, onbr[ro.x + i], bmask);
+      table_v = v;
     }
     const uint32_t* nvl = onbr + ro.x;
-    for (uint32_t c0 = ri.x; c0 < ri.y; c0 += TH_VCH) {
+    {
+      const uint32_t c0 = ri.x + item.y * TH_VCH;
       const uint32_t cn = min(TH_VCH, ri.y - c0);
       __syncthreads();
       // prefix of |N+(u)| over this chunk of in-neighbours (PER per thread, block scan)
