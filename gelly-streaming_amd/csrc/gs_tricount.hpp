@@ -21,7 +21,11 @@ namespace gs {
 constexpr int TH_BLOCK = 256, TH_WPB = TH_BLOCK / WAVE;
 // k_tri_heavy: 1024 threads, N+(v) of up to TH_NU entries in LDS, in-neighbours in chunks of TH_VCH
 constexpr int TH_HBLOCK = 1024;
-constexpr uint32_t TH_NU = 16384, TH_HB = TH_NU / 2, TH_VCH = 2048;   // TH_HB 4-slot buckets: load <= 1/2
+#ifndef GS_TH_VCH
+#define GS_TH_VCH 2048
+#endif
+constexpr uint32_t TH_NU = 16384, TH_HB = TH_NU / 2, TH_VCH = GS_TH_VCH;   // TH_HB 4-slot buckets: load <= 1/2
+static_assert(TH_VCH % TH_HBLOCK == 0, "TH_VCH must be a multiple of TH_HBLOCK");
 #ifndef GS_TH_DMAX
 #define GS_TH_DMAX 512
 #endif
