@@ -330,3 +330,27 @@ def test_parse_edges_text_errors_and_edges(engine, oracle):
         got = [x.cpu().numpy() for x in engine.parse_edges_text(small)]
         want = oracle.parse_edges_text(small)
         assert all(np.array_equal(g, w) for g, w in zip(got, want)), small
+
+
+@pytest.mark.parametrize("kind", ["small_ids", "sparse_ids", "rmat"])
+def test_candidate_count_sizing(engine, oracle, kind):
+    """The sizing call (capacity 0) of gs_window_candidates returns exactly the oracle's record count."""
+    rng = np.random.default_rng({"small_ids": 31, "sparse_ids": 32, "rmat": 33}[kind])
+    for _ in range(3):
+        s, d = _cand_case(oracle, rng, kind)
+        assert engine.candidate_count(s, d) == oracle.candidate_count(s, d)
+
+
+def test_text_to_window_reduce(engine, oracle):
+    """Input path end to end: edge text parsed on the GPU, then slice(OUT).reduceOnEdges(SUM) over the
+    third column as the value, equals the oracle on the oracle-parsed columns."""
+    from gelly_streaming_amd.textio import format_edges_text
+
+    s, d = oracle.gen_rmat(14, 1 << 17, 0x5EED07)
+    v = oracle.gen_values(1 << 17, 7, oracle.DT_I64)
+    text = format_edges_text(s, d, v)
+    gs, gd, gv = engine.parse_edges_text(text)
+    k, r = engine.reduce(gs, gd, gv, 1, 0)
+    os_, od, ov = oracle.parse_edges_text(text)
+    wk, wv = oracle.window_reduce(os_, od, ov, 1, 0)
+    assert np.array_equal(k.cpu().numpy(), wk) and np.array_equal(r.cpu().numpy(), wv)
