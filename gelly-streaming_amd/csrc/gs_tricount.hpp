@@ -36,7 +36,10 @@ static_assert(TH_DMAX * 2 <= TH_H, "TH_DMAX must be <= TH_H / 2");
 #ifndef GS_TH_ILP
 #define GS_TH_ILP 8   // measured at R-MAT s22: 2 -> 93.9 ms, 4 -> 70.2, 6 -> 62.6, 8 -> 62.0, 12 -> 64.5, 16 -> 137.8
 #endif
-constexpr int TH_ILP = GS_TH_ILP;   // consecutive items per lane: one search, TH_ILP probes in flight
+constexpr int TH_ILP = GS_TH_ILP;   // items per lane: TH_ILP probes in flight
+#ifndef GS_TH_LANEIL
+#define GS_TH_LANEIL 0   // light kernel: lane-interleaved items (1) or TH_ILP consecutive items per lane (0)
+#endif
 
 __device__ __forceinline__ uint32_t th_hash(uint32_t x, uint32_t mask) { return ((x * 0x9E3779B1u) >> 7) & mask; }
 // LDS written by some lanes of a wave, then read by others
@@ -137,6 +140,37 @@ __device__ __forceinline__ uint32_t th_wave_chunk(const uint32_t* __restrict__ o
   uint32_t top = 1;
   while (2 * top < dn) top <<= 1;
   uint32_t cnt = 0;
+#if GS_TH_LANEIL
+  // lane-interleaved items: the j-th gather of a wave reads 64 consecutive items of the concatenated
+  // lists (a few cache lines) instead of 64 runs of TH_ILP items spread over the whole chunk
+  for (uint32_t k0 = 0; k0 < run; k0 += WAVE * TH_ILP) {
+    uint32_t x[TH_ILP], pend = 0, lo = 0;
+    {
+      const uint32_t kk = min(k0 + (uint32_t)lane, run - 1);
+      for (uint32_t st = top; st; st >>= 1) {
+        const uint32_t t = lo + st;
+        const uint32_t pv = t < dn ? po[min(t, dn - 1)] : run;
+        lo = pv <= kk ? t : lo;
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < TH_ILP; ++j) {
+      const uint32_t kj = min(k0 + (uint32_t)(j * WAVE + lane), run - 1);
+      if (j) {
+        // 64 items further: at most 64 boundaries crossed (every kept list has >= 1 item)
+#pragma unroll
+        for (uint32_t st = WAVE; st; st >>= 1) {
+          const uint32_t t = lo + st;
+          const uint32_t pv = t < dn ? po[min(t, dn - 1)] : run;
+          lo = pv <= kj ? t : lo;
+        }
+      }
+      x[j] = onbr[ps[lo] + (kj - po[lo])];
+      pend |= (k0 + (uint32_t)(j * WAVE + lane) < run ? 1u : 0u) << j;
+    }
+    cnt += th_probe(hb, bmask, x, pend);
+  }
+#else
   for (uint32_t k0 = 0; k0 < run; k0 += WAVE * TH_ILP) {
     const uint32_t kb = k0 + lane * TH_ILP;
     const uint32_t kk = min(kb, run - 1);
@@ -172,6 +206,7 @@ __device__ __forceinline__ uint32_t th_wave_chunk(const uint32_t* __restrict__ o
     for (int j = 0; j < TH_ILP; ++j) pend |= (kb + j < run ? 1u : 0u) << j;
     cnt += th_probe(hb, bmask, x, pend);
   }
+#endif
   wave_lds_sync();   // the next item clears the table
   return cnt;
 }
