@@ -355,7 +355,7 @@ static gs_status triangles_impl(gs_ctx* c, const gs_edge_batch* b, uint32_t part
     GS_HIP(hipGetLastError());
   }
   hipEventRecord(c->ev[5], c->stream);
-  hipLaunchKernelGGL(k_tri_heavy, dim3(256), dim3(TH_HBLOCK), 0, c->stream, c->tri_onbr.as<uint32_t>(),
+  hipLaunchKernelGGL(k_tri_heavy, dim3(GS_TH_HGRID), dim3(TH_HBLOCK), 0, c->stream, c->tri_onbr.as<uint32_t>(),
                      c->tri_ou.as<uint32_t>(), out_range, in_range, c->tri_heavy.as<uint2>(), d_nheavy, d_total,
                      d_probes);
   GS_HIP(hipGetLastError());

@@ -11,7 +11,7 @@
 // Probing N+(u) from the middle vertex costs sum_u d+(u)^2 probes, against sum over edges u -> v of
 // d+(v) from the first vertex (R-MAT scale 20: 2.47 G against 4.27 G).  In-lists longer than a chunk
 // queue their further chunks for a second pass (a hub's work spreads over many waves); vertices with
-// more than TH_DMAX out-neighbours go to k_tri_heavy (a block each, N+(v) in a 128 KiB LDS hash
+// more than TH_DMAX out-neighbours go to k_tri_heavy (a block each, N+(v) in a 64 KiB LDS hash
 // set).  Only vertices whose out-list starts in [q0, q1) count (the multi-GPU split).
 #pragma once
 #include "gs_device.hpp"
@@ -19,12 +19,23 @@
 namespace gs {
 
 constexpr int TH_BLOCK = 256, TH_WPB = TH_BLOCK / WAVE;
-// k_tri_heavy: 1024 threads, N+(v) of up to TH_NU entries in LDS, in-neighbours in chunks of TH_VCH
-constexpr int TH_HBLOCK = 1024;
-#ifndef GS_TH_VCH
-#define GS_TH_VCH 2048
+// k_tri_heavy: 512 threads, two blocks per CU, N+(v) of up to TH_NU entries in LDS, in-neighbours in
+// chunks of TH_VCH (one 1024-thread block per CU with a 16384-entry table: s22 70.9 -> 67.8 ms, s24
+// 315.7 -> 307.0; chunks of 512 instead of 1024: 67.4 -> 66.2, 305.8 -> 302.5)
+#ifndef GS_TH_HBLOCK
+#define GS_TH_HBLOCK 512
 #endif
-constexpr uint32_t TH_NU = 16384, TH_HB = TH_NU / 2, TH_VCH = GS_TH_VCH;   // TH_HB 4-slot buckets: load <= 1/2
+#ifndef GS_TH_NU
+#define GS_TH_NU 8192
+#endif
+#ifndef GS_TH_HGRID
+#define GS_TH_HGRID 512   // heavy blocks in the grid: two per CU (68 KiB LDS each)
+#endif
+constexpr int TH_HBLOCK = GS_TH_HBLOCK;
+#ifndef GS_TH_VCH
+#define GS_TH_VCH 512
+#endif
+constexpr uint32_t TH_NU = GS_TH_NU, TH_HB = TH_NU / 2, TH_VCH = GS_TH_VCH;   // TH_HB 4-slot buckets: load <= 1/2
 static_assert(TH_VCH % TH_HBLOCK == 0, "TH_VCH must be a multiple of TH_HBLOCK");
 #ifndef GS_TH_DMAX
 #define GS_TH_DMAX 512
@@ -280,7 +291,7 @@ __global__ __launch_bounds__(TH_HBLOCK) void k_tri_heavy(const uint32_t* __restr
                                                          const uint32_t* __restrict__ n_heavy,
                                                          unsigned long long* __restrict__ total,
                                                          unsigned long long* __restrict__ n_probes) {
-  __shared__ uint4 s_hash[TH_HB];               // 128 KiB: N+(v) as a hash set of 4-slot buckets
+  __shared__ uint4 s_hash[TH_HB];               // TH_NU / 2 buckets (64 KiB): N+(v) as a hash set of 4-slot buckets
   __shared__ uint32_t s_off[TH_VCH + 1];        // prefix of |N+(u)| over the chunk; [cn] = total
   __shared__ uint32_t s_st[TH_VCH];             // start of that N+(u) in onbr
   __shared__ uint32_t s_w[TH_HBLOCK / WAVE];
