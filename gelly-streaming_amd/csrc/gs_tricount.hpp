@@ -38,9 +38,12 @@ constexpr int TH_HBLOCK = GS_TH_HBLOCK;
 constexpr uint32_t TH_NU = GS_TH_NU, TH_HB = TH_NU / 2, TH_VCH = GS_TH_VCH;   // TH_HB 4-slot buckets: load <= 1/2
 static_assert(TH_VCH % TH_HBLOCK == 0, "TH_VCH must be a multiple of TH_HBLOCK");
 #ifndef GS_TH_DMAX
-#define GS_TH_DMAX 512
+#define GS_TH_DMAX 256   // light/heavy split; 512 -> 256: s22 66.4 -> 55.8 ms, s24 302.6 -> 289.7 (128: 56.8, 296.1)
 #endif
-constexpr uint32_t TH_DMAX = GS_TH_DMAX, TH_H = 1024, TH_EMPTY = 0xFFFFFFFFu;
+#ifndef GS_TH_H
+#define GS_TH_H 1024
+#endif
+constexpr uint32_t TH_DMAX = GS_TH_DMAX, TH_H = GS_TH_H, TH_EMPTY = 0xFFFFFFFFu;
 // a light vertex's N+(v) (<= TH_DMAX entries) must leave the TH_H-slot table at most half full: insert
 // and probe chains end at a free slot, so a full table would never end them
 static_assert(TH_DMAX * 2 <= TH_H, "TH_DMAX must be <= TH_H / 2");
