@@ -48,7 +48,7 @@ constexpr uint32_t TH_DMAX = GS_TH_DMAX, TH_H = GS_TH_H, TH_EMPTY = 0xFFFFFFFFu;
 // and probe chains end at a free slot, so a full table would never end them
 static_assert(TH_DMAX * 2 <= TH_H, "TH_DMAX must be <= TH_H / 2");
 #ifndef GS_TH_ILP
-#define GS_TH_ILP 8   // measured at R-MAT s22: 2 -> 93.9 ms, 4 -> 70.2, 6 -> 62.6, 8 -> 62.0, 12 -> 64.5, 16 -> 137.8
+#define GS_TH_ILP 10   // R-MAT s22 (DMAX 512): 2 -> 93.9 ms, 4 -> 70.2, 6 -> 62.6, 8 -> 62.0, 12 -> 64.5, 16 -> 137.8; DMAX 256: 6 -> 55.3, 8 -> 55.8, 10 -> 54.5 (s24 291.9, 289.6, 279.7)
 #endif
 constexpr int TH_ILP = GS_TH_ILP;   // items per lane: TH_ILP probes in flight
 #ifndef GS_TH_LANEIL
