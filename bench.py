@@ -42,12 +42,17 @@ def parse():
     p.add_argument("--seed", type=lambda x: int(x, 0), default=0x5EED02)
     p.add_argument("--dtype", default="int64", choices=["int64", "float64"])
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--cpu-sample-log2", type=int, default=25)
+    p.add_argument("--windows", type=int, default=2, help="distinct windows of the stream the timed steps cycle through")
+    p.add_argument("--stream", default="rmat", choices=["rmat", "zipf"],
+                   help="fold (C3): skewed R-MAT (default) or the Zipf(1.1) source stream")
+    p.add_argument("--no-pack", action="store_true",
+                   help="ablation: integer SUM keeps 8-byte partitioned values instead of 4-byte packed records")
     p.add_argument("--sort-only", action="store_true",
                    help="ablation: reduce / fold through the full LSD sort + reduce-by-key path")
     p.add_argument("--bk-onesweep", action="store_true",
                    help="ablation: bucket path partitions with 1-2 LSD passes instead of the direct scatter")
-    p.add_argument("--check", action="store_true", help="verify sum(per-vertex sums) == sum(values) after timing")
+    p.add_argument("--check", action="store_true",
+                   help="after timing: sum(per-vertex sums) == sum(values) and ascending keys on each window")
     p.add_argument("--windows-edges", type=float, default=1e8,
                    help="apply (C5): edges per 1000 ms window of the continuous stream")
     p.add_argument("--workload", default="reduce", choices=["reduce", "fold", "triangles", "c1", "apply", "candidates", "parse"],
@@ -56,9 +61,17 @@ def parse():
     return p.parse_args()
 
 
+def algorithmic_bytes(workload, E, U, vb=8):
+    """SURVEY.md §8(d) algorithmic bytes of one window (E input edges, U output vertices):
+    reduce OUT/IN 16E + 16U (8-byte values; 4-byte: 12E + 12U), fold degree/max 16E + 24U."""
+    if workload == "fold":
+        return 16 * E + 24 * U
+    return (8 + vb) * E + (8 + vb) * U
+
+
 def kernel_table(times_list, E, U_avg):
-    """Average per-launch durations (device events inside the library, same stream) and the algorithmic
-    bytes each kernel must move ("Kernels and their rooflines")."""
+    """Average per-launch durations (device events inside the library, same stream) and each kernel's
+    own algorithmic bytes."""
     t0 = times_list[0]
     if t0.path == 2:
         return direct_kernel_table(times_list, E, U_avg)
@@ -84,9 +97,6 @@ def kernel_table(times_list, E, U_avg):
         rows["reduce_by_key"] = {"ms": ms, "bytes": E * (kb + vb) + U_avg * 16}
     ms = statistics.mean(t.keyinfo_ms for t in times_list)
     rows["keyinfo(+host sync)"] = {"ms": ms, "bytes": E * 8}
-    for r in rows.values():
-        r["GB/s"] = r["bytes"] / (r["ms"] * 1e-3) / 1e9 if r["ms"] > 0 else 0.0
-        r["frac"] = r["GB/s"] / HBM_PEAK_GBS
     return rows, P
 
 
@@ -108,29 +118,26 @@ def bucket_kernel_table(times_list, E, U_avg):
     rows["bucket_merge"] = {"ms": mean(lambda t: t.pass_ms[passes + 1]), "bytes": 0}
     rows["bucket_emit"] = {"ms": mean(lambda t: t.pass_ms[passes + 2]), "bytes": U_avg * (4 + ab + 16)}
     rows["keyinfo(+host sync)"] = {"ms": mean(lambda t: t.keyinfo_ms), "bytes": E * 8}
-    for r in rows.values():
-        r["GB/s"] = r["bytes"] / (r["ms"] * 1e-3) / 1e9 if r["ms"] > 0 else 0.0
-        r["frac"] = r["GB/s"] / HBM_PEAK_GBS
     return rows, mean(lambda t: t.partials)
 
 
 def direct_kernel_table(times_list, E, U_avg):
     """Direct bucket path (gs_bucket.hpp k_dp_*): per-tile histogram, offset scans, ONE scatter, LDS
-    accumulate, merge, emit.  Algorithmic bytes per launch as in DESIGN.md §4 (E = records)."""
+    accumulate, merge, emit.  Each kernel's own bytes (E = records): the packed scatter
+    writes 4-byte records (2-byte key + 2-byte value), the plain one a 2-byte key + the payload."""
     t0 = times_list[0]
-    vb = t0.payload_bytes
-    ab = 8 if vb else 4          # staged accumulator (i64 sum / u32 count)
+    vb = t0.payload_bytes        # packed: 2
+    lb = 8 if t0.packed else vb  # loaded value bytes
+    ab = 8 if (vb or t0.packed) else 4   # staged accumulator (i64 sum / u32 count)
     mean = lambda f: statistics.mean(f(t) for t in times_list)
     rows = {}
-    rows["dp_scatter"] = {"ms": mean(lambda t: t.pass_ms[1]), "bytes": E * ((8 + vb) + (2 + vb))}
+    name = "dp_scatter_pack" if t0.packed else "dp_scatter"
+    rows[name] = {"ms": mean(lambda t: t.pass_ms[1]), "bytes": E * ((8 + lb) + (2 + vb))}
     rows["bucket_accumulate"] = {"ms": mean(lambda t: t.pass_ms[2]), "bytes": E * (2 + vb) + U_avg * (4 + ab)}
     rows["bucket_merge"] = {"ms": mean(lambda t: t.pass_ms[3]), "bytes": 0}
     rows["bucket_emit"] = {"ms": mean(lambda t: t.pass_ms[4]), "bytes": U_avg * (4 + ab + 16)}
     rows["dp_offsets(up+spine+plan+down)"] = {"ms": mean(lambda t: t.pass_ms[0]), "bytes": 0}
-    rows["dp_hist(+host sync)"] = {"ms": mean(lambda t: t.keyinfo_ms), "bytes": E * 8}
-    for r in rows.values():
-        r["GB/s"] = r["bytes"] / (r["ms"] * 1e-3) / 1e9 if r["ms"] > 0 else 0.0
-        r["frac"] = r["GB/s"] / HBM_PEAK_GBS
+    rows["dp_hist"] = {"ms": mean(lambda t: t.keyinfo_ms), "bytes": E * 8}
     return rows, mean(lambda t: t.partials)
 
 
@@ -150,74 +157,79 @@ def triangle_kernel_table(times_list, n):
         # list item per probe
         "tri_count(light+heavy)": {"ms": mean(lambda t: t.pass_ms[3] + t.pass_ms[4]), "bytes": 16 * M + 4 * P},
     }
-    for r in rows.values():
-        r["GB/s"] = r["bytes"] / (r["ms"] * 1e-3) / 1e9 if r["ms"] > 0 else 0.0
-        r["frac"] = r["GB/s"] / HBM_PEAK_GBS
     return rows, P
 
 
-def pmc_traffic(kernel: str):
+def finish_rows(rows, B):
+    """GB/s and HBM fraction of each kernel on its own bytes, and on the window's §8(d) bytes B."""
+    for r in rows.values():
+        r["GB/s"] = r["bytes"] / (r["ms"] * 1e-3) / 1e9 if r["ms"] > 0 else 0.0
+        r["frac"] = r["GB/s"] / HBM_PEAK_GBS
+        r["frac_on_B"] = (B / (r["ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS) if r["ms"] > 0 else 0.0
+    return rows
+
+
+def pmc_table():
+    """profiles/pmc_traffic.json: per-kernel HBM bytes per launch from separate rocprofv3 --pmc passes
+    (tools/pmc_traffic.py, gfx950 FETCH_SIZE correction)."""
     f = ROOT / "profiles" / "pmc_traffic.json"
     if not f.exists():
-        return None
+        return {}
     try:
-        d = json.loads(f.read_text())
-        return d.get(kernel, {}).get("bytes_per_launch")
+        return json.loads(f.read_text())
     except Exception:
-        return None
+        return {}
 
 
-def cpu_baseline(src, dst, val, sample_log2: int):
-    """The oracle's keyBy + hash-map fold (gso_baseline_reduce) on the first 2^k edges of the same
-    window, timed on this host: 1 warm-up, median of 3 (threads = min(16, cpus))."""
+def cpu_baseline(wins, workload, threads, reps=5):
+    """BASELINE.md CPU baseline: the oracle's keyBy + per-subtask arrival-order hash-map fold
+    (gso_baseline_reduce; Flink's keyBy at local-env parallelism = threads) over WHOLE windows of the
+    same stream, cycling the bench's windows: 1 warm-up window, then the median of `reps`; plus a
+    one-thread figure on the first 1/8 of a window."""
+    orc = ge.load_oracle()
+    host = [tuple(x.cpu().numpy() if x is not None else None for x in w) for w in wins]
+    op = 4 if workload == "fold" else 0      # 4 = the degree / max-neighbour fold
+    run = lambda h, th, k=None: orc.baseline_reduce(h[0][:k], h[1][:k], (h[2] if h[2] is not None else h[0])[:k],
+                                                   1, op, th)
+    run(host[0], threads)
+    ts = []
+    for r in range(reps):
+        h = host[r % len(host)]
+        t = time.perf_counter()
+        run(h, threads)
+        ts.append(time.perf_counter() - t)
+    tmed = statistics.median(ts)
+    E = len(host[0][0])
+    k1 = E // 8
+    t = time.perf_counter()
+    run(host[0], 1, k1)
+    t1 = time.perf_counter() - t
+    what = "degree/max-neighbour fold" if workload == "fold" else "reduceOnEdges(SUM) fold"
+    return {"value": E / tmed, "unit": "edges/s", "cores": threads, "kind": "port",
+            "sample": f"whole {E}-edge windows of the same stream ({len(host)} distinct, cycled), keyBy over "
+                      f"{threads} threads + per-subtask arrival-order hash-map {what} (oracle/gs_oracle.c "
+                      f"gso_baseline_reduce), 1 warm-up + median of {reps}",
+            "window_s_median": tmed, "single_core_value": k1 / t1,
+            "single_core_sample": f"first {k1} edges of window 0, one thread"}
+
+
+def cpu_baseline_triangles(src, dst, threads, sample_log2=24):
+    """BASELINE.md C4 CPU baseline: the forward algorithm (the reference's O(sum d^2) candidate rule is
+    infeasible at this scale) over `threads` threads (oracle gso_triangles_fwd_mt) on the first
+    2^sample_log2 edges of the window, 1 warm-up + median of 3."""
     orc = ge.load_oracle()
     S = min(1 << sample_log2, src.numel())
-    s = src[:S].cpu().numpy()
-    d = dst[:S].cpu().numpy()
-    v = val[:S].cpu().numpy()
-    threads = max(1, min(16, os.cpu_count() or 1))
-    orc.baseline_reduce(s[: S // 8], d[: S // 8], v[: S // 8], 1, 0, threads)
+    s, d = src[:S].cpu().numpy(), dst[:S].cpu().numpy()
+    orc.triangles_fwd_mt(s[: S // 16], d[: S // 16], threads)
     ts = []
     for _ in range(3):
         t = time.perf_counter()
-        orc.baseline_reduce(s, d, v, 1, 0, threads)
+        T = orc.triangles_fwd_mt(s, d, threads)
         ts.append(time.perf_counter() - t)
-    tmed = statistics.median(ts)
-    S1 = S // 8
-    t = time.perf_counter()
-    orc.baseline_reduce(s[:S1], d[:S1], v[:S1], 1, 0, 1)
-    t1 = time.perf_counter() - t
-    return {"value": S / tmed, "unit": "edges/s", "cores": threads, "kind": "port",
-            "sample": f"first 2^{sample_log2} edges of the same R-MAT window, keyBy over {threads} threads + "
-                      f"per-subtask hash-map fold (oracle/gs_oracle.c gso_baseline_reduce), median of 3",
-            "single_core_value": S1 / t1}
-
-
-def cpu_baseline_triangles(src, dst, max_candidates=40_000_000, max_log2=22, budget_s=4.0):
-    """The reference's WindowTriangles rule restated by the oracle (GenerateCandidateEdges with HashSet
-    order -> pair-keyed CountTriangles -> Integer sum; gso_window_triangles_ref, one thread) on the
-    first 2^k edges of the same window: k doubles from 16 while one run stays under budget_s and the
-    candidate count under max_candidates; the largest sample is reported."""
-    orc = ge.load_oracle()
-    best = None
-    for k in range(16, max_log2 + 1):
-        S = min(1 << k, src.numel())
-        s, d = src[:S].cpu().numpy(), dst[:S].cpu().numpy()
-        if orc.candidate_count(s, d) > max_candidates:
-            break
-        t = time.perf_counter()
-        orc.window_triangles_ref(s, d)
-        dt = time.perf_counter() - t
-        best = (k, S, dt)
-        if dt > budget_s or S == src.numel():
-            break
-    if best is None:
-        return None
-    k, S, dt = best
-    return {"value": S / dt, "unit": "edges/s", "cores": 1, "kind": "port",
-            "sample": f"first 2^{k} edges of the same window, the reference's candidate rule "
-                      f"(oracle/gs_oracle.c gso_window_triangles_ref: candidates in HashSet order, pair-keyed "
-                      f"count, Integer sum), one thread, {dt:.2f} s"}
+    dt = statistics.median(ts)
+    return {"value": S / dt, "unit": "edges/s", "cores": threads, "kind": "port",
+            "sample": f"first 2^{sample_log2} edges of the window, forward-algorithm triangle count over {threads} "
+                      f"threads (oracle/gs_oracle.c gso_triangles_fwd_mt), median of 3: {dt:.2f} s, {T} triangles"}
 
 
 def window_stream_main(a):
@@ -400,17 +412,24 @@ def main():
     from importlib import import_module
     D = import_module("gelly_streaming_amd.distributed")
 
-    eng = pkg.Engine(local, sort_only=a.sort_only, bk_onesweep=a.bk_onesweep)
+    eng = pkg.Engine(local, sort_only=a.sort_only, bk_onesweep=a.bk_onesweep, no_pack=a.no_pack)
     E = a.edge_factor << a.scale
-    if a.workload == "fold":      # C3: skewed R-MAT (.65/.15/.15/.05), no permutation -> hubs at low IDs
-        src, dst = eng.generate_rmat(a.scale, E, 0x5EED03, a=0.65, b=0.15, c=0.15, permute=False,
-                                     first_edge=rank * E)
-    elif a.workload == "triangles":   # C4 shape: R-MAT, self-loops removed
-        src, dst = eng.generate_rmat(a.scale, E, 0x5EED04, no_self_loops=True, first_edge=rank * E)
-    else:                         # C2
-        src, dst = eng.generate_rmat(a.scale, E, a.seed, first_edge=rank * E)
     vdt = 1 if a.dtype == "int64" else 3
-    val = eng.generate_values(E, a.seed, vdt, first_edge=rank * E)
+    # a.windows distinct windows of the stream (rank r holds windows r*W .. r*W+W-1), cycled by the
+    # steps: every step is a different window than the one before it
+    wins = []
+    for w in range(a.windows):
+        fe = (rank * a.windows + w) * E
+        if a.workload == "fold" and a.stream == "zipf":   # C3: Zipf(1.1) sources over 2^scale IDs
+            src, dst = eng.generate_zipf(1 << a.scale, E, 0x5EED03, 1.1, first_edge=fe)
+        elif a.workload == "fold":   # C3: skewed R-MAT (.65/.15/.15/.05), no permutation -> hubs at low IDs
+            src, dst = eng.generate_rmat(a.scale, E, 0x5EED03, a=0.65, b=0.15, c=0.15, permute=False, first_edge=fe)
+        elif a.workload == "triangles":   # C4 shape: R-MAT, self-loops removed
+            src, dst = eng.generate_rmat(a.scale, E, 0x5EED04, no_self_loops=True, first_edge=fe)
+        else:                         # C2
+            src, dst = eng.generate_rmat(a.scale, E, a.seed, first_edge=fe)
+        val = eng.generate_values(E, a.seed, vdt, first_edge=fe) if a.workload == "reduce" else None
+        wins.append((src, dst, val))
     torch.cuda.synchronize()
 
     local_times = []
@@ -432,7 +451,8 @@ def main():
         local_times.append(eng.stage_times())
         return r
 
-    def step():
+    def step(i):
+        src, dst, val = wins[i % len(wins)]
         local_times.clear()
         if a.workload == "triangles":
             if dist:
@@ -448,16 +468,16 @@ def main():
         r = D.reduce_window(local_reduce, src, dst, val, 1, 0) if dist else local_reduce(src, dst, val, 1, 0)
         return r[0], r[1], local_times[0]
 
-    for _ in range(a.warmup):
-        step()
+    for i in range(a.warmup):
+        step(i)
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
     times, us = [], []
     t0 = time.perf_counter()
-    for _ in range(a.steps):
-        k, v, st = step()
+    for i in range(a.steps):
+        k, v, st = step(a.warmup + i)
         times.append(st)
         us.append(int(k.numel()))
     torch.cuda.synchronize()
@@ -470,59 +490,95 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
+    checks = {}
     if a.check and world == 1 and a.workload == "reduce":
-        k, v, _ = step()
-        assert int(v.sum()) == int(val.sum()) and bool((k[1:] > k[:-1]).all()), "bench window failed its check"
+        for i in range(min(2, len(wins))):
+            k, v, _ = step(i)
+            val = wins[i][2]
+            if a.dtype == "int64":
+                assert int(v.sum()) == int(val.sum()), "bench window: sum of per-vertex sums != sum of values"
+            assert bool((k[1:] > k[:-1]).all()), "bench window: keys not ascending"
+        checks["sums_and_order"] = "ok"
 
     # local window only: the dominant kernel of the single-GPU pipeline
     E_rec = times[0].records
-    U_avg = times[0].vertices
+    U_avg = statistics.mean(t.vertices for t in times)
     if a.workload == "triangles":
         kt, partials = triangle_kernel_table(times, E * world)
+        B = 16 * E       # §8(d): the edge-list term; the intersection term is per probe (kernels table)
     else:
         kt, partials = kernel_table(times, E_rec, U_avg)
-    dom_name = max((n for n in kt if "host sync" not in n), key=lambda n: kt[n]["ms"])
+        B = algorithmic_bytes(a.workload, E, U_avg, 8)
+    finish_rows(kt, B)
+    dom_name = max(kt, key=lambda n: kt[n]["ms"])
     dom = kt[dom_name]
-    roofline = {"bound": "hbm", "kernel": dom_name, "achieved": round(dom["GB/s"], 1), "peak": HBM_PEAK_GBS,
-                "unit": "GB/s", "frac": round(dom["frac"], 4), "traffic": pmc_traffic(dom_name),
-                "algorithmic_bytes_per_launch": dom["bytes"], "avg_launch_ms": round(dom["ms"], 4)}
+    ms_step = elapsed / a.steps * 1e3
+    pmc = pmc_table()
+    pmc_dom = pmc.get(dom_name, {}).get("bytes_per_launch") if a.workload == "reduce" and world == 1 else None
+    pmc_window = None
+    if a.workload == "reduce" and world == 1 and all(n in pmc for n in kt if kt[n]["bytes"]):
+        pmc_window = sum(pmc[n]["bytes_per_launch"] for n in kt if n in pmc)
+    window_gbs = B / (ms_step * 1e-3) / 1e9 / world
+    roofline = {"bound": "hbm", "kernel": dom_name,
+                "achieved": round(B / (dom["ms"] * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(dom["frac_on_B"], 4), "traffic": pmc_dom,
+                "algorithmic_bytes_per_launch": B,
+                "algorithmic_bytes_formula": {"reduce": "16E + 16U (SURVEY.md §8d, reduce OUT, 8-byte values)",
+                                              "fold": "16E + 24U (SURVEY.md §8d, fold degree/max)",
+                                              "triangles": "16E (SURVEY.md §8d edge-list term)"}[a.workload],
+                "avg_launch_ms": round(dom["ms"], 4),
+                "kernel_own_bytes_per_launch": dom["bytes"], "kernel_own_frac": round(dom["frac"], 4),
+                "whole_window": {"achieved": round(window_gbs, 1), "frac": round(window_gbs / HBM_PEAK_GBS, 4),
+                                 "ms": round(ms_step, 4)},
+                "window_traffic_pmc": pmc_window,
+                "window_traffic_over_B": round(pmc_window / B, 3) if pmc_window else None,
+                "timing": "device events on the library's stream around each launch (gs_last_stage_times)"}
 
     cpu = None
+    threads = max(1, min(16, os.cpu_count() or 1))
     if world == 1 and rank == 0 and not a.no_cpu_baseline:
-        if a.workload == "reduce":
-            cpu = cpu_baseline(src, dst, val, a.cpu_sample_log2)
+        if a.workload in ("reduce", "fold"):
+            cpu = cpu_baseline(wins, a.workload, threads)
         elif a.workload == "triangles":
-            cpu = cpu_baseline_triangles(src, dst)
+            cpu = cpu_baseline_triangles(wins[0][0], wins[0][1], threads)
+    value = E * world * a.steps / elapsed
+    if cpu:
+        cpu["gpu_over_cpu"] = round(value / cpu["value"], 1)
 
     if rank == 0:
-        total_edges = E * world * a.steps
+        t0s = times[0]
         line = {
             "metric": METRIC,
-            "value": total_edges / elapsed,
+            "value": value,
             "unit": "edges/s",
             "n_gpus": world,
             "steps": a.steps,
             "warmup": a.warmup,
-            "ms_per_step": elapsed / a.steps * 1e3,
+            "ms_per_step": ms_step,
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": a.dtype,
-            "data": "synthetic R-MAT (Graph500 .57/.19/.19/.05, permuted), generated on device (gs_generate_rmat)",
-            "config": {"workload": {"reduce": f"C2: slice(OUT).reduceOnEdges(SUM) over one R-MAT scale-{a.scale} window",
-                                    "fold": f"C3: slice(OUT).foldNeighbors(degree, max neighbour), skewed R-MAT scale-{a.scale}",
-                                    "triangles": f"C4 shape: WindowTriangles over an R-MAT scale-{a.scale} window"}[a.workload],
-                       "scale": a.scale, "edges_per_window_per_gpu": E,
+            "dtype": a.dtype if a.workload == "reduce" else "int64",
+            "data": ("synthetic " + ("Zipf(1.1) sources / uniform destinations" if a.stream == "zipf" and
+                                     a.workload == "fold" else "R-MAT") +
+                     f", seeded, generated on device; {a.windows} distinct windows per rank cycled by the steps"),
+            "config": {"workload": {"reduce": f"C2: slice(OUT).reduceOnEdges(SUM) over R-MAT scale-{a.scale} windows",
+                                    "fold": f"C3: slice(OUT).foldNeighbors(degree, max neighbour), skewed "
+                                            f"{'Zipf(1.1)' if a.stream == 'zipf' else 'R-MAT'} scale-{a.scale}",
+                                    "triangles": f"C4 shape: WindowTriangles over R-MAT scale-{a.scale} windows"}[a.workload],
+                       "scale": a.scale, "edges_per_window_per_gpu": E, "windows_cycled": a.windows,
                        "direction": "ALL" if a.workload == "triangles" else "OUT",
                        "op": {"reduce": "SUM", "fold": "DegreeMaxNeighbor", "triangles": "count"}[a.workload],
-                       "value_dtype": a.dtype, "vertices_out": U_avg, "sort_passes": times[0].sort_passes,
-                       "key_bits": times[0].key_bits, "partials_after_fused_pass": int(partials),
-                       "pipeline": {0: "sort", 1: "bucket-onesweep", 2: "bucket-direct", 3: "triangles"}[times[0].path],
+                       "value_dtype": a.dtype, "vertices_out": U_avg, "sort_passes": t0s.sort_passes,
+                       "key_bits": t0s.key_bits, "partials_after_fused_pass": int(partials),
+                       "pipeline": {0: "sort", 1: "bucket-onesweep", 2: "bucket-direct", 3: "triangles"}[t0s.path],
+                       "packed_records": bool(t0s.packed), "escaped_values": int(t0s.escapes),
                        "parallelism": (f"vertex-range keyBy over {world} GPU(s), RCCL all-to-all" if dist
-                                       else "1 GPU")},
+                                       else "1 GPU"), **checks},
             "roofline": roofline,
             "cpu_baseline": cpu,
-            "kernels": {n: {"avg_ms": round(r["ms"], 4), "GB/s": round(r["GB/s"], 1), "frac": round(r["frac"], 4)}
+            "kernels": {n: {"avg_ms": round(r["ms"], 4), "own_bytes": r["bytes"], "GB/s": round(r["GB/s"], 1),
+                            "frac": round(r["frac"], 4), "frac_on_B": round(r["frac_on_B"], 4)}
                         for n, r in kt.items()},
         }
         print(json.dumps(line), flush=True)

@@ -32,7 +32,7 @@ EXPORTS = ("gs_abi_version", "gs_create", "gs_destroy", "gs_last_error", "gs_set
            "gs_alloc_pinned", "gs_free_pinned", "gs_window_reduce", "gs_window_fold",
            "gs_window_fold_degree_max", "gs_window_csr", "gs_window_candidates", "gs_window_triangles",
            "gs_window_triangles_part", "gs_window_count_candidates",
-           "gs_parse_edges_text", "gs_generate_rmat", "gs_generate_uniform", "gs_generate_values", "gs_last_stage_times")
+           "gs_parse_edges_text", "gs_generate_rmat", "gs_generate_uniform", "gs_generate_zipf", "gs_generate_values", "gs_last_stage_times")
 
 P = ctypes.c_void_p
 u64, i64, i32, u32 = ctypes.c_uint64, ctypes.c_int64, ctypes.c_int32, ctypes.c_uint32
@@ -40,6 +40,8 @@ u64, i64, i32, u32 = ctypes.c_uint64, ctypes.c_int64, ctypes.c_int32, ctypes.c_u
 
 GS_FLAG_SORT_ONLY = 1   # include/gelly_hip.h: reduce / fold always take the LSD sort path
 GS_FLAG_BK_ONESWEEP = 2   # bucket path: 1-2 LSD partition passes instead of the direct scatter (A/B)
+GS_FLAG_NO_PACK = 4       # bucket path: integer SUM/MIN/MAX keep 8-byte partitioned values (A/B)
+GS_FLAG_TEST_TINY_TABLES = 8   # TEST ONLY: triangle hash sets of one bucket -> must fail with GS_EDEVICE
 
 
 class GsConfig(ctypes.Structure):
@@ -80,7 +82,8 @@ class GsStageTimes(ctypes.Structure):
     _fields_ = [("keyinfo_ms", ctypes.c_float), ("sort_ms", ctypes.c_float), ("reduce_ms", ctypes.c_float),
                 ("total_ms", ctypes.c_float), ("sort_passes", u32), ("key_bits", u32), ("records", u64),
                 ("vertices", u64), ("pass_ms", ctypes.c_float * 8), ("key_bytes", u32), ("payload_bytes", u32),
-                ("partials", u64), ("fused_last", u32), ("path", u32)]
+                ("partials", u64), ("fused_last", u32), ("path", u32), ("packed", u32), ("reserved", u32),
+                ("escapes", u64)]
 
 
 class GsError(RuntimeError):
@@ -125,6 +128,7 @@ def load() -> ctypes.CDLL:
         "gs_parse_edges_text": (st, [P, P, u64, i32, P, P, P, u64, i32, ctypes.POINTER(u64), ctypes.POINTER(u64)]),
         "gs_generate_rmat": (st, [P, i32, u64, u64, u32, u32, u32, i32, i32, u64, P, P]),
         "gs_generate_uniform": (st, [P, u64, u64, u64, u64, P, P]),
+        "gs_generate_zipf": (st, [P, u64, ctypes.c_double, u64, u64, u64, P, P]),
         "gs_generate_values": (st, [P, u64, u64, u64, i32, P]),
         "gs_last_stage_times": (st, [P, ctypes.POINTER(GsStageTimes)]),
     }

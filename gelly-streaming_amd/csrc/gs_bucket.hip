@@ -158,38 +158,47 @@ gs_status launch_plan(gs_ctx* c, uint64_t R, uint32_t nb, int passes, int w, uin
 }
 
 // The back end both front ends share: LDS accumulation of the partitioned records (or of the
-// columns themselves when the window is one bucket), merge of multi-item buckets, emit; then the
-// host reads U.  Records pass_ev[ev0 + 1 .. ev0 + 3] after the three launches.
+// columns themselves when the window is one bucket), merge of multi-item buckets, emit; then ONE
+// read-back of the window's scalars (vertex range, outside-prediction count, U, items, escapes,
+// timeout) into host_small[0..7].  The caller waits (host_wait) and interprets them.  Records
+// pass_ev[ev0 + 1 .. ev0 + 3] after the three launches.  Every launch exits at once when the
+// histogram saw a key outside the predicted range (mm[2] != 0).
 template <class P, class Src>
-gs_status bucket_accumulate(gs_ctx* c, Src rs, uint64_t R, uint32_t nb, int64_t base, typename P::Out o, int ev0,
-                            uint64_t* U, uint32_t* n_items) {
+gs_status bucket_accumulate(gs_ctx* c, Src rs, uint64_t R, uint32_t nb, int64_t base, typename P::Out o, int ev0) {
   char* sm = c->small.as<char>();
   uint32_t* meta = c->bk_meta.as<uint32_t>();
   uint32_t* ns = (uint32_t*)(sm + SM_BK_N);
+  const auto* mm = (const unsigned long long*)(sm + SM_BK_MM);
   GS_HIP(hipMemsetAsync(ns + 2, 0, 4, c->stream));
   BkStage st{c->keysA.as<uint32_t>(), c->valsA.p,
              (std::is_same_v<P, BkDeg> || std::is_same_v<P, BkDeg32>) ? c->aux.as<int64_t>() : nullptr};
   auto* slabs = c->bk_slabs.as<typename P::Lds>();
   hipLaunchKernelGGL((k_bk_accum<P, Src, GS_BK_UNROLL>), dim3(c->n_cu), dim3(BK_ACC_BLOCK), 0, c->stream, rs,
-                     c->bk_items.as<BkItem>(), ns + 0, meta + BkMeta::BSTART, ns + 2, slabs, st, meta + BkMeta::BCOUNT);
+                     c->bk_items.as<BkItem>(), ns + 0, meta + BkMeta::BSTART, ns + 2, slabs, st, meta + BkMeta::BCOUNT,
+                     mm);
   GS_HIP(hipGetLastError());
   hipEventRecord(c->pass_ev[ev0 + 1], c->stream);
   const unsigned mgrid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(nb, R / BK_ITEM + 1));
   hipLaunchKernelGGL((k_bk_merge_slices<P>), dim3(mgrid, BK_MS_SLICES), dim3(BK_MS_BLOCK), 0, c->stream,
-                     meta + BkMeta::MLIST, ns + 1, meta + BkMeta::BITEMS, meta + BkMeta::BSLAB, slabs);
+                     meta + BkMeta::MLIST, ns + 1, meta + BkMeta::BITEMS, meta + BkMeta::BSLAB, slabs, mm);
   hipLaunchKernelGGL((k_bk_merge<P>), dim3(mgrid), dim3(BK_ACC_BLOCK), 0, c->stream, meta + BkMeta::MLIST, ns + 1,
                      meta + BkMeta::BITEMS, meta + BkMeta::BSLAB, meta + BkMeta::BSTART, slabs, st,
-                     meta + BkMeta::BCOUNT);
+                     meta + BkMeta::BCOUNT, mm);
   GS_HIP(hipGetLastError());
   hipEventRecord(c->pass_ev[ev0 + 2], c->stream);
   hipLaunchKernelGGL((k_bk_emit<P>), dim3(nb), dim3(256), 0, c->stream, meta + BkMeta::BSTART, meta + BkMeta::BCOUNT,
-                     nb, st, base, o, (unsigned long long*)(sm + SM_BK_MM + 24));
+                     nb, st, base, o, (unsigned long long*)(sm + SM_BK_MM + 24), mm);
   GS_HIP(hipGetLastError());
   hipEventRecord(c->pass_ev[ev0 + 3], c->stream);
   hipEventRecord(c->ev[3], c->stream);
   GS_HIP(hipMemcpyAsync(c->host_small, sm + SM_BK_MM, 48, hipMemcpyDeviceToHost, c->stream));
   GS_HIP(hipMemcpyAsync(c->host_small + 6, sm + SM_TIMEOUT, 8, hipMemcpyDeviceToHost, c->stream));
-  GS_TRY(host_wait(c));
+  GS_HIP(hipMemcpyAsync(c->host_small + 7, sm + SM_BK_ESC, 8, hipMemcpyDeviceToHost, c->stream));
+  return GS_OK;
+}
+
+// after host_wait: the accumulate's results (GS_EDEVICE on a look-back timeout)
+gs_status bucket_results(gs_ctx* c, uint64_t* U, uint32_t* n_items) {
   if ((uint32_t)c->host_small[6] != 0) return set_error(c, GS_EDEVICE, "look-back spin timed out");
   *U = c->host_small[3];
   *n_items = (uint32_t)c->host_small[4];
@@ -233,13 +242,22 @@ gs_status ensure_stage(gs_ctx* c, uint64_t R) {
 }
 
 // ---- direct front end: hist -> offsets -> one scatter -------------------------------------------------
-// Events: ev[1] after the histogram (+ host read of the range); pass_ev[0..2] around the offset
-// scans and the scatter; then accumulate / merge / emit.
+// The whole window is enqueued against the PREDICTED vertex range (the previous window's base and
+// bucket count; the first window of a ctx assumes small non-negative IDs and BK_MAXB buckets) with
+// no host round trip inside it: k_dp_hist counts the keys outside the prediction and every later
+// launch exits at once when there are any.  One read-back at the end brings the measured range,
+// that count, U and the escape count; only a missed prediction reruns the window (with the measured
+// range, which cannot miss).
+// Integer SUM / MIN / MAX partition through k_dp_scatter_pack (4-byte records) unless the previous
+// window of this ctx had more than 1/8 escapes; every other op through k_dp_scatter.
+// Events: ev[1] / pass_ev[0] after the histogram; pass_ev[0..2] around the offset scans and the
+// scatter; then accumulate / merge / emit.
 template <class P, int DIR>
 gs_status bucket_direct(gs_ctx* c, const int64_t* src, const int64_t* dst, const void* val, uint64_t n,
                         typename P::Out o, uint64_t* U) {
   using Raw = typename P::Raw;
   constexpr int S = P::S;
+  constexpr bool CAN_PACK = P::PAY == PAY_VAL && !P::REL && std::is_integral_v<typename P::A>;
   char* sm = c->small.as<char>();
   const uint64_t R = (DIR == DIR_ALL) ? 2 * n : n;
   GS_TRY(ensure(c, c->bk_meta, BkMeta::TOTAL * 4, true));
@@ -248,21 +266,86 @@ gs_status bucket_direct(gs_ctx* c, const int64_t* src, const int64_t* dst, const
   constexpr uint32_t TE = dp_tile_edges<DIR>();
   const uint32_t nt = (uint32_t)((n + TE - 1) / TE);
   const uint32_t nch = (nt + DP_CHUNK - 1) / DP_CHUNK;
-
-  // 1. per-tile bucket counts against the predicted base and width: the window's one read of the
-  //    keys before the scatter; a key outside the prediction makes it count again with the range
+  GS_TRY(ensure(c, c->dp_cnt, (size_t)nt * BK_MAXB * 2));
+  GS_TRY(ensure(c, c->dp_csum, (size_t)nch * BK_MAXB * 4));
+  GS_TRY(ensure(c, c->dp_off, (size_t)nt * BK_MAXB * 4));
+  GS_TRY(ensure_stage<P>(c, R));
+  const bool pack = CAN_PACK && c->bk_wide_vals <= 0 && !(c->flags & GS_FLAG_NO_PACK);
   int64_t base = c->bk_base;
   uint32_t nb = c->bk_nbp ? c->bk_nbp : (uint32_t)BK_MAXB;
-  GS_TRY(ensure(c, c->dp_cnt, (size_t)nt * BK_MAXB * 2));
-  GS_TRY(launch_dp_hist<DIR>(c, src, dst, n, nt, base, S, nb));
-  GS_HIP(hipMemcpyAsync(c->host_small, sm + SM_BK_MM, 24, hipMemcpyDeviceToHost, c->stream));
-  GS_TRY(host_wait(c));
-  const int64_t kmin = key_min(c->host_small), kmax = key_max(c->host_small);
-  if ((((uint64_t)kmax - (uint64_t)kmin) >> S) >= (uint64_t)BK_MAXB) return GS_EUNSUPPORTED;
-  if (c->host_small[2]) {
-    base = predict_base(kmin, kmax, S);
-    nb = (uint32_t)((((uint64_t)kmax - (uint64_t)base) >> S) + 1);
+  const uint32_t item_recs = item_records(c, R);
+  uint16_t* cnt = c->dp_cnt.as<uint16_t>();
+  uint32_t* csum = c->dp_csum.as<uint32_t>();
+  uint16_t* k16 = c->keysB.as<uint16_t>();
+  Raw* vpart = P::HAS_V ? c->valsB.as<Raw>() : nullptr;
+  uint32_t* rel_bad = (uint32_t*)(sm + SM_BK_N) + 3;
+  auto* mm = (unsigned long long*)(sm + SM_BK_MM);
+  bool part = false;
+  int64_t kmin = 0, kmax = 0;
+  for (int attempt = 0;; ++attempt) {
+    // 1. per-tile bucket counts against the predicted base and width (the window's one read of
+    //    the keys before the scatter) + the measured range and the keys outside the prediction
     GS_TRY(launch_dp_hist<DIR>(c, src, dst, n, nt, base, S, nb));
+    GS_HIP(hipMemsetAsync(sm + SM_BK_ESC, 0, 8, c->stream));
+    hipEventRecord(c->ev[1], c->stream);
+    hipEventRecord(c->pass_ev[0], c->stream);
+
+    // 2. offsets: chunk counts, per-bucket spine (-> meta[HIST] totals), plan, per-tile offsets
+    part = nb > 1;
+    const dim3 g2((nb + 255) / 256, nch);
+    hipLaunchKernelGGL(k_dp_up, g2, dim3(256), 0, c->stream, cnt, nt, nb, csum);
+    hipLaunchKernelGGL(k_dp_spine, dim3((nb + 63) / 64), dim3(1024), 0, c->stream, csum, nch, nb, meta + BkMeta::HIST);
+    GS_HIP(hipGetLastError());
+    GS_TRY(launch_plan<P>(c, R, nb, 0, 0, item_recs));
+    if (part) {
+      hipLaunchKernelGGL(k_dp_down, g2, dim3(256), 0, c->stream, cnt, csum, meta + BkMeta::BSTART, nt, nb,
+                         c->dp_off.as<uint32_t>());
+      GS_HIP(hipGetLastError());
+    }
+    hipEventRecord(c->pass_ev[1], c->stream);
+
+    // 3. the scatter: bucket-local index + payload in bucket order
+    if constexpr (P::REL) {
+      if (!part) return GS_RETRY_WIDE;   // offsets are checked by the scatter only
+    }
+    using Load = typename P::Load;
+    const BaseSrc<Load, DIR, P::PAY> ls{src, dst, (const Load*)val, base};
+    if (part) {
+      const unsigned grid = dp_scatter_grid<DIR>(n);
+      if constexpr (CAN_PACK) {
+        if (pack) {
+          hipLaunchKernelGGL((k_dp_scatter_pack<Load, DIR>), dim3(grid), dim3(DP_BLOCK), 0, c->stream, ls, n, S, nb,
+                             (const uint32_t*)c->dp_off.as<uint32_t>(), c->keysB.as<uint32_t>(), vpart,
+                             (const unsigned long long*)mm, (unsigned long long*)(sm + SM_BK_ESC));
+          GS_HIP(hipGetLastError());
+        }
+      }
+      if (!pack) {
+        if constexpr (P::REL) GS_HIP(hipMemsetAsync(rel_bad, 0, 4, c->stream));
+        hipLaunchKernelGGL((k_dp_scatter<Load, DIR, P::PAY, Raw, P::REL>), dim3(grid), dim3(DP_BLOCK), 0, c->stream, ls,
+                           n, S, nb, c->dp_off.as<uint32_t>(), k16, vpart, rel_bad, (const unsigned long long*)mm);
+        GS_HIP(hipGetLastError());
+      }
+    }
+    hipEventRecord(c->pass_ev[2], c->stream);
+    hipEventRecord(c->ev[2], c->stream);
+
+    // 4-6. accumulate, merge, emit; one read-back
+    if (part) {
+      if (pack) GS_TRY((bucket_accumulate<P>(c, PackSrc<Raw>{c->keysB.as<uint32_t>(), vpart}, R, nb, base, o, 2)));
+      else GS_TRY((bucket_accumulate<P>(c, PartSrc<Raw>{k16, vpart}, R, nb, base, o, 2)));
+    } else if constexpr (!P::REL) {
+      const BaseSrc<Raw, DIR, P::PAY> es{src, dst, (const Raw*)val, base};
+      GS_TRY((bucket_accumulate<P>(c, es, R, nb, base, o, 2)));
+    }
+    GS_TRY(host_wait(c));
+    kmin = key_min(c->host_small);
+    kmax = key_max(c->host_small);
+    if ((((uint64_t)kmax - (uint64_t)kmin) >> S) >= (uint64_t)BK_MAXB) return GS_EUNSUPPORTED;
+    if (!c->host_small[2]) break;
+    if (attempt) return set_error(c, GS_EDEVICE, "bucket path: keys outside the measured vertex range");
+    base = predict_base(kmin, kmax, S);   // missed prediction: rerun with the measured range
+    nb = (uint32_t)((((uint64_t)kmax - (uint64_t)base) >> S) + 1);
   }
   {   // the next window predicts this base and this width rounded up to a power of two
     const uint32_t need = (uint32_t)((((uint64_t)kmax - (uint64_t)base) >> S) + 1);
@@ -271,61 +354,24 @@ gs_status bucket_direct(gs_ctx* c, const int64_t* src, const int64_t* dst, const
     c->bk_base = base;
     c->bk_nbp = std::min<uint32_t>(p2, BK_MAXB);
   }
-  hipEventRecord(c->ev[1], c->stream);
-  hipEventRecord(c->pass_ev[0], c->stream);
-
-  // 2. offsets: chunk counts, per-bucket spine (-> meta[HIST] totals), plan, per-tile offsets
-  const bool part = nb > 1;
-  const uint32_t item_recs = item_records(c, R);
-  GS_TRY(ensure(c, c->dp_csum, (size_t)nch * nb * 4));
-  uint16_t* cnt = c->dp_cnt.as<uint16_t>();
-  uint32_t* csum = c->dp_csum.as<uint32_t>();
-  const dim3 g2((nb + 255) / 256, nch);
-  hipLaunchKernelGGL(k_dp_up, g2, dim3(256), 0, c->stream, cnt, nt, nb, csum);
-  hipLaunchKernelGGL(k_dp_spine, dim3((nb + 63) / 64), dim3(1024), 0, c->stream, csum, nch, nb, meta + BkMeta::HIST);
-  GS_HIP(hipGetLastError());
-  GS_TRY(launch_plan<P>(c, R, nb, 0, 0, item_recs));
-  if (part) {
-    GS_TRY(ensure(c, c->dp_off, (size_t)nt * nb * 4));
-    hipLaunchKernelGGL(k_dp_down, g2, dim3(256), 0, c->stream, cnt, csum, meta + BkMeta::BSTART, nt, nb,
-                       c->dp_off.as<uint32_t>());
-    GS_HIP(hipGetLastError());
-  }
-  hipEventRecord(c->pass_ev[1], c->stream);
-
-  // 3. the scatter: (16-bit bucket-local index, payload) in bucket order
-  if constexpr (P::REL) {
-    if (!part) return GS_RETRY_WIDE;   // offsets are checked by the scatter only
-  }
-  GS_TRY(ensure_stage<P>(c, R));
-  using Load = typename P::Load;
-  const BaseSrc<Load, DIR, P::PAY> ls{src, dst, (const Load*)val, base};
-  uint16_t* k16 = c->keysB.as<uint16_t>();
-  Raw* vpart = P::HAS_V ? c->valsB.as<Raw>() : nullptr;
-  uint32_t* rel_bad = (uint32_t*)(sm + SM_BK_N) + 3;
-  if (part) {
-    if constexpr (P::REL) GS_HIP(hipMemsetAsync(rel_bad, 0, 4, c->stream));
-    const unsigned grid = dp_scatter_grid<DIR>(n);
-    hipLaunchKernelGGL((k_dp_scatter<Load, DIR, P::PAY, Raw, P::REL>), dim3(grid), dim3(DP_BLOCK), 0, c->stream, ls, n,
-                       S, nb, c->dp_off.as<uint32_t>(), k16, vpart, rel_bad);
-    GS_HIP(hipGetLastError());
-  }
-  hipEventRecord(c->pass_ev[2], c->stream);
-  hipEventRecord(c->ev[2], c->stream);
-
-  // 4-6. accumulate, merge, emit
   uint32_t n_items = 0;
-  if (part) {
-    GS_TRY((bucket_accumulate<P>(c, PartSrc<Raw>{k16, vpart}, R, nb, base, o, 2, U, &n_items)));
-  } else if constexpr (!P::REL) {
-    const BaseSrc<Raw, DIR, P::PAY> es{src, dst, (const Raw*)val, base};
-    GS_TRY((bucket_accumulate<P>(c, es, R, nb, base, o, 2, U, &n_items)));
-  }
+  GS_TRY(bucket_results(c, U, &n_items));
   if constexpr (P::REL) {
     if ((uint32_t)(c->host_small[5] >> 32) != 0) return GS_RETRY_WIDE;   // a neighbour outside base + 2^32
   }
+  if constexpr (CAN_PACK) {
+    // escapes common (> 1/8 of the records): the next 16 windows store 8-byte values, then packing
+    // is tried again
+    if (pack && c->host_small[7] > R / 8) c->bk_wide_vals = 16;
+    else if (!pack && c->bk_wide_vals > 0) --c->bk_wide_vals;
+  }
+  const uint64_t esc = pack ? c->host_small[7] : 0;
   const uint32_t key_bits = nb <= 1 ? (uint32_t)S : (uint32_t)(S + 32 - __builtin_clz(nb - 1));
-  bucket_times(c, 2, part ? 1 : 0, 5, key_bits, R, *U, P::HAS_V ? sizeof(Raw) : 0, n_items);
+  const size_t pb = pack ? 2 : (P::HAS_V ? sizeof(Raw) : 0);   // packed: 2 key + 2 value bytes per record
+  bucket_times(c, 2, part ? 1 : 0, 5, key_bits, R, *U, pb, n_items);
+  c->times.key_bytes = 2;
+  c->times.escapes = esc;
+  c->times.packed = pack ? 1u : 0u;
   return GS_OK;
 }
 
@@ -389,9 +435,11 @@ gs_status bucket_onesweep(gs_ctx* c, const int64_t* src, const int64_t* dst, con
   // 4-6. accumulate, merge, emit
   uint32_t n_items = 0;
   if (g.passes == 0)
-    GS_TRY((bucket_accumulate<P>(c, es, R, g.nb, base, o, g.passes, U, &n_items)));
+    GS_TRY((bucket_accumulate<P>(c, es, R, g.nb, base, o, g.passes)));
   else
-    GS_TRY((bucket_accumulate<P>(c, PartSrc<Raw>{k16, vpart}, R, g.nb, base, o, g.passes, U, &n_items)));
+    GS_TRY((bucket_accumulate<P>(c, PartSrc<Raw>{k16, vpart}, R, g.nb, base, o, g.passes)));
+  GS_TRY(host_wait(c));
+  GS_TRY(bucket_results(c, U, &n_items));
   const uint32_t key_bits = g.nb <= 1 ? (uint32_t)S : (uint32_t)(S + 32 - __builtin_clz(g.nb - 1));
   bucket_times(c, 1, g.passes, g.passes + 3, key_bits, R, *U, HAS_V ? sizeof(Raw) : 0, n_items);
   return GS_OK;

@@ -302,6 +302,27 @@ struct PartSrc {
   }
 };
 
+// packed partitioned records (integer SUM / MIN / MAX, k_dp_scatter_pack): one u32 per record,
+// bucket-local index in the low 16 bits, the value in the high 16 bits when it lies in [0, PK_ESC),
+// else PK_ESC there and the full value at the same position of `wide`
+constexpr uint32_t PK_ESC = 0xFFFFu;
+template <typename V>
+struct PackSrc {
+  const uint32_t* rec;
+  const V* wide;
+};
+template <class Src>
+struct is_pack_src : std::false_type {};
+template <typename V>
+struct is_pack_src<PackSrc<V>> : std::true_type {};
+
+template <typename V>
+__device__ __forceinline__ uint32_t pk_narrow(V v) {
+  using U = std::conditional_t<sizeof(V) == 8, uint64_t, uint32_t>;
+  const U u = (U)v;
+  return u < (U)PK_ESC ? (uint32_t)u : PK_ESC;
+}
+
 // ---- k_bk_info: min / max of the keys and the bucket histogram (relative to a predicted base) ----
 // mm[0] = max(~flip(key)) (i.e. min), mm[1] = max(flip(key)), mm[2] = keys outside the prediction
 template <int DIR, bool VEC>
@@ -693,8 +714,10 @@ template <typename V, int DIR, int PAY, typename VO = V, bool REL = false>
 __global__ __launch_bounds__(DP_BLOCK) GS_DP_SCATTER_ATTR void k_dp_scatter(BaseSrc<V, DIR, PAY> es, uint64_t n, int S, uint32_t nbp,
                                                          const uint32_t* __restrict__ off,
                                                          uint16_t* __restrict__ k16, VO* __restrict__ vout,
-                                                         uint32_t* __restrict__ rel_bad) {
+                                                         uint32_t* __restrict__ rel_bad,
+                                                         const unsigned long long* __restrict__ mm) {
   constexpr bool HAS_V = PAY != PAY_NONE;
+  if (mm[2]) return;   // keys outside the predicted range: the window is rerun
   constexpr bool STAGE_V = HAS_V && !GS_DP_VDIRECT;
   __shared__ uint32_t s_key[DP_TILE];                // (bucket << 16) | bucket-local index, bucket order
   __shared__ VO s_val[STAGE_V ? DP_TILE : 1];
@@ -808,6 +831,106 @@ __global__ __launch_bounds__(DP_BLOCK) GS_DP_SCATTER_ATTR void k_dp_scatter(Base
   }
 }
 
+// ---- packed scatter: integer SUM / MIN / MAX, 4 bytes per partitioned record ----------------------
+// The same tile, ranking and per-tile offsets as k_dp_scatter, but each record leaves as one u32
+// (bucket-local index | narrow value << 16, PackSrc) instead of a u16 key plus an 8-byte value: the
+// partition written and read back shrinks from 10 to 4 bytes per record.  A value outside
+// [0, PK_ESC) is an escape: PK_ESC in the record, the full value at the record's position of `wide`
+// (written from this kernel, read by k_bk_accum only for escapes; n_esc counts them so the host can
+// fall back to k_dp_scatter for windows where escapes are common).  LDS is 6 bytes per record
+// (76 KiB per 10240-record tile), so two 1024-thread blocks share a CU and one block's loads overlap
+// the other's LDS and store phases (k_dp_scatter: one block per CU).
+// mm[2] != 0 (k_dp_hist saw a key outside the predicted range): every block exits at once and the
+// host reruns the window with the measured range.
+#ifndef GS_PK_WAVES
+#define GS_PK_WAVES 8   // waves per SIMD: two 16-wave blocks per CU
+#endif
+template <typename V, int DIR>
+__global__ __launch_bounds__(DP_BLOCK) __attribute__((amdgpu_waves_per_eu(GS_PK_WAVES, GS_PK_WAVES)))
+void k_dp_scatter_pack(BaseSrc<V, DIR, PAY_VAL> es, uint64_t n, int S, uint32_t nbp,
+                       const uint32_t* __restrict__ off, uint32_t* __restrict__ rec, V* __restrict__ wide,
+                       const unsigned long long* __restrict__ mm, unsigned long long* __restrict__ n_esc) {
+  __shared__ uint32_t s_key[DP_TILE];      // (bucket << 16) | bucket-local index, bucket order
+  __shared__ uint16_t s_v16[DP_TILE];      // narrow value, same order
+  __shared__ uint32_t s_cnt[BK_MAXB];      // counts, then run starts inside the tile
+  __shared__ uint32_t s_delta[BK_MAXB];    // global position - tile position of bucket b's run
+  __shared__ uint32_t s_w[DP_BLOCK / WAVE];
+  if (mm[2]) return;
+  const int tid = threadIdx.x;
+  constexpr uint32_t TE = dp_tile_edges<DIR>();
+  const uint32_t nfull = (uint32_t)(n / TE);
+  const uint32_t base32 = (uint32_t)es.base, lmask = (1u << S) - 1;
+  const uint32_t b0 = 2 * tid, b1 = 2 * tid + 1;   // BK_MAXB = 2 * DP_BLOCK
+  const uint32_t bl0 = min(b0, nbp - 1), bl1 = min(b1, nbp - 1);
+  uint32_t t, nrec = DP_TILE;
+  if (blockIdx.x == gridDim.x - 1) {   // the window's partial last tile
+    if ((uint64_t)nfull * TE >= n) return;
+    t = nfull;
+    nrec = (uint32_t)((n - (uint64_t)nfull * TE) * (DIR == DIR_ALL ? 2 : 1));
+  } else {   // XCD slot b & 7 owns a contiguous range of full tiles (k_dp_scatter)
+    const uint32_t per = (nfull + 7) / 8;
+    t = (blockIdx.x & 7u) * per + (blockIdx.x >> 3);
+    if (t >= nfull) return;
+  }
+  const uint32_t r0 = t * DP_TILE;
+  const uint32_t* orow = off + (uint64_t)t * nbp;
+  const uint32_t o0 = orow[bl0], o1 = orow[bl1];
+  uint32_t kb[DP_ITEMS], v16[DP_ITEMS];
+#pragma unroll
+  for (int u = 0; u < DP_ITEMS; ++u) {   // unconditional loads, clamped into the tile (k_dp_scatter)
+    uint32_t kl;
+    V vv;
+    dp_load_raw(es, r0 + min((uint32_t)u * DP_BLOCK + tid, nrec - 1), kl, vv);
+    const uint32_t c = kl - base32;
+    kb[u] = ((c >> S) << 16) | (c & lmask);
+    v16[u] = pk_narrow(vv);
+  }
+  for (uint32_t i = tid; i < nbp; i += DP_BLOCK) s_cnt[i] = 0;
+  __syncthreads();
+  uint32_t rk[DP_ITEMS];
+#pragma unroll
+  for (int u = 0; u < DP_ITEMS; ++u)
+    if ((uint32_t)u * DP_BLOCK + tid < nrec) rk[u] = atomicAdd(&s_cnt[kb[u] >> 16], 1u);
+  __syncthreads();
+  const uint32_t c0 = b0 < nbp ? s_cnt[b0] : 0u, c1 = b1 < nbp ? s_cnt[b1] : 0u;
+  uint32_t total;
+  const uint32_t st0 = bk_block_scan(c0 + c1, s_w, total);
+  s_cnt[b0] = st0;   // unconditional: entries past nbp are never read
+  s_delta[b0] = o0 - st0;
+  s_cnt[b1] = st0 + c0;
+  s_delta[b1] = o1 - (st0 + c0);
+  __syncthreads();
+  uint32_t esc = 0;
+#pragma unroll
+  for (int u = 0; u < DP_ITEMS; ++u) {
+    const uint32_t j = (uint32_t)u * DP_BLOCK + tid;
+    if (j < nrec) {
+      const uint32_t pos = s_cnt[kb[u] >> 16] + rk[u];
+      s_key[pos] = kb[u];
+      s_v16[pos] = (uint16_t)v16[u];
+      if (v16[u] == PK_ESC) {   // rare: reload the full value for its slot of `wide`
+        const uint32_t r = r0 + j;
+        wide[s_delta[kb[u] >> 16] + pos] = es.val[DIR == DIR_ALL ? r >> 1 : r];
+        ++esc;
+      }
+    }
+  }
+  __syncthreads();
+  auto put = [&](uint32_t j) {
+    const uint32_t kv = s_key[j];
+    rec[s_delta[kv >> 16] + j] = (kv & 0xFFFFu) | ((uint32_t)s_v16[j] << 16);
+  };
+  if (nrec == DP_TILE) {
+#pragma unroll
+    for (int u = 0; u < DP_ITEMS; ++u) put((uint32_t)u * DP_BLOCK + tid);
+  } else {
+    for (uint32_t j = tid; j < nrec; j += DP_BLOCK) put(j);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) esc += __shfl_xor(esc, o, WAVE);
+  if ((tid & 63) == 0 && esc) atomicAdd(n_esc, (unsigned long long)esc);
+}
+
 // ---- k_bk_accum: persistent; LDS accumulation of (bucket, record range) items ---------------------
 // Finalize (shared with k_bk_merge): the bucket's vertices in ascending order -> staging at the
 // bucket's record offset (a bucket has at least as many records as vertices).
@@ -849,12 +972,14 @@ __global__ __launch_bounds__(BK_ACC_BLOCK) void k_bk_accum(Src src, const BkItem
                                                            const uint32_t* __restrict__ bucket_start,
                                                            uint32_t* __restrict__ ctr,
                                                            typename P::Lds* __restrict__ slabs, BkStage st,
-                                                           uint32_t* __restrict__ bucket_count) {
+                                                           uint32_t* __restrict__ bucket_count,
+                                                           const unsigned long long* __restrict__ mm) {
   __shared__ typename P::Lds s;
   __shared__ uint32_t s_item;
   __shared__ uint32_t s_wc[BK_NW];
   using Raw = typename P::Raw;
   const int tid = threadIdx.x;
+  if (mm[2]) return;   // keys outside the predicted range: the window is rerun
   const uint32_t n_items = *n_items_p;
   for (;;) {
     if (tid == 0) s_item = atomicAdd(ctr, 1u);
@@ -866,18 +991,37 @@ __global__ __launch_bounds__(BK_ACC_BLOCK) void k_bk_accum(Src src, const BkItem
     P::init(s, tid);
     __syncthreads();
     const uint32_t r0 = b0 + m.begin, r1 = b0 + m.end;
-    for (uint32_t r = r0 + tid; r < r1; r += BK_ACC_BLOCK * UNROLL) {
-      uint32_t k[UNROLL];
-      Raw v[UNROLL];
+    if constexpr (is_pack_src<Src>::value) {
+      for (uint32_t r = r0 + tid; r < r1; r += BK_ACC_BLOCK * UNROLL) {
+        uint32_t x[UNROLL];
 #pragma unroll
-      for (int u = 0; u < UNROLL; ++u) {
-        const uint32_t q = r + (uint32_t)u * BK_ACC_BLOCK;
-        src.load(q < r1 ? q : r1 - 1, k[u], v[u]);   // unconditional: see k_dp_hist
+        for (int u = 0; u < UNROLL; ++u) {
+          const uint32_t q = r + (uint32_t)u * BK_ACC_BLOCK;
+          x[u] = src.rec[q < r1 ? q : r1 - 1];   // unconditional: see k_dp_hist
+        }
+#pragma unroll
+        for (int u = 0; u < UNROLL; ++u) {
+          const uint32_t q = r + (uint32_t)u * BK_ACC_BLOCK;
+          if (q < r1) {
+            const uint32_t v16 = x[u] >> 16;
+            P::add(s, x[u] & (P::W - 1), v16 != PK_ESC ? (Raw)v16 : (Raw)src.wide[q]);
+          }
+        }
       }
+    } else {
+      for (uint32_t r = r0 + tid; r < r1; r += BK_ACC_BLOCK * UNROLL) {
+        uint32_t k[UNROLL];
+        Raw v[UNROLL];
 #pragma unroll
-      for (int u = 0; u < UNROLL; ++u) {
-        const uint32_t q = r + (uint32_t)u * BK_ACC_BLOCK;
-        if (q < r1) P::add(s, k[u] & (P::W - 1), v[u]);
+        for (int u = 0; u < UNROLL; ++u) {
+          const uint32_t q = r + (uint32_t)u * BK_ACC_BLOCK;
+          src.load(q < r1 ? q : r1 - 1, k[u], v[u]);   // unconditional: see k_dp_hist
+        }
+#pragma unroll
+        for (int u = 0; u < UNROLL; ++u) {
+          const uint32_t q = r + (uint32_t)u * BK_ACC_BLOCK;
+          if (q < r1) P::add(s, k[u] & (P::W - 1), v[u]);
+        }
       }
     }
     __syncthreads();
@@ -902,8 +1046,9 @@ __global__ __launch_bounds__(BK_MS_BLOCK) void k_bk_merge_slices(const uint32_t*
                                                                  const uint32_t* __restrict__ n_multi_p,
                                                                  const uint32_t* __restrict__ b_items,
                                                                  const uint32_t* __restrict__ b_slab,
-                                                                 typename P::Lds* __restrict__ slabs) {
-  if (blockIdx.x >= *n_multi_p) return;
+                                                                 typename P::Lds* __restrict__ slabs,
+                                                                 const unsigned long long* __restrict__ mm) {
+  if (mm[2] || blockIdx.x >= *n_multi_p) return;
   const uint32_t b = mlist[blockIdx.x];
   const uint32_t n = b_items[b], f = b_slab[b];
   typename P::Lds* d = slabs + f;
@@ -924,11 +1069,12 @@ __global__ __launch_bounds__(BK_ACC_BLOCK) void k_bk_merge(const uint32_t* __res
                                                            const uint32_t* __restrict__ b_slab,
                                                            const uint32_t* __restrict__ bucket_start,
                                                            const typename P::Lds* __restrict__ slabs, BkStage st,
-                                                           uint32_t* __restrict__ bucket_count) {
+                                                           uint32_t* __restrict__ bucket_count,
+                                                           const unsigned long long* __restrict__ mm) {
   __shared__ typename P::Lds s;
   __shared__ uint32_t s_wc[BK_NW];
   const int tid = threadIdx.x;
-  if (blockIdx.x >= *n_multi_p) return;
+  if (mm[2] || blockIdx.x >= *n_multi_p) return;
   const uint32_t b = mlist[blockIdx.x];
   const uint32_t n = b_items[b], f = b_slab[b];
   (void)n;
@@ -946,9 +1092,11 @@ template <class P>
 __global__ __launch_bounds__(256) void k_bk_emit(const uint32_t* __restrict__ bucket_start,
                                                  const uint32_t* __restrict__ bucket_count, uint32_t nb,
                                                  BkStage st, int64_t base, typename P::Out o,
-                                                 unsigned long long* __restrict__ n_out) {
+                                                 unsigned long long* __restrict__ n_out,
+                                                 const unsigned long long* __restrict__ mm) {
   __shared__ uint32_t s_w[4];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  if (mm[2]) return;
   const uint32_t b = blockIdx.x;
   uint32_t part = 0;
   for (uint32_t i = tid; i < b; i += 256) part += bucket_count[i];

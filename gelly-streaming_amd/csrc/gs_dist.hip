@@ -1,0 +1,432 @@
+// gs_dist.hip — multi-GPU keyBy for reduceOnEdges / foldNeighbors behind the C ABI.
+//
+// The reference spreads a window over subtasks with keyBy(NeighborKeySelector) (SimpleEdgeStream.java
+// :159-167): every record travels to the subtask that owns its key.  Here every rank pre-reduces its
+// own slice of the window (the bucket path), and only the per-vertex partials travel:
+//
+//   gs_window_reduce_partials      local reduce -> partials grouped by owner(v) = gs_owner_of(v, nparts)
+//                                  (a stable device-side partition: ascending keys within each owner),
+//                                  per-owner counts to the host
+//   (exchange)                     the caller's all-to-all (torch.distributed / Java), or the ctx-owned
+//                                  RCCL communicator below
+//   gs_merge_partials              the owner combines what it received (op: SUM / MIN / MAX; COUNT
+//                                  partials merge by SUM; foldNeighbors' init applied once, here)
+//   gs_window_reduce_dist          all three with the ctx's RCCL communicator (gs_comm_init)
+//
+// The owner is a hash of the vertex, as Flink's keyBy is; which rank owns a vertex is not observable in
+// the reference's output (per-vertex records, compared as unordered sets).  Integer results stay
+// bit-exact (the ops are associative and commutative); float sums move within the 1e-5 tolerance.
+// RCCL is resolved at gs_comm_init time (dlopen / the process's already-loaded RCCL, e.g. torch's), so
+// libgellyhip.so itself has no RCCL dependency.
+#include <dlfcn.h>
+#include <string.h>
+
+#include <vector>
+
+#include "gs_ops.hpp"
+
+namespace gs {
+
+__host__ __device__ inline uint32_t owner_of(int64_t v, uint32_t nparts) {
+  uint64_t x = (uint64_t)v;
+  x ^= x >> 33;
+  x *= 0xff51afd7ed558ccdull;
+  x ^= x >> 33;
+  x *= 0xc4ceb9fe1a85ec53ull;
+  x ^= x >> 33;
+  return (uint32_t)(((x >> 32) * (uint64_t)nparts) >> 32);
+}
+
+constexpr int OW_BLOCK = 256, OW_ITEMS = 16, OW_TILE = OW_BLOCK * OW_ITEMS, OW_MAXP = 64;
+
+// per tile: partials per owner -> cnt[owner * tiles + tile]
+__global__ __launch_bounds__(OW_BLOCK) void k_owner_count(const int64_t* __restrict__ keys, uint64_t U, uint32_t nparts,
+                                                          uint32_t tiles, uint32_t* __restrict__ cnt) {
+  __shared__ uint32_t s_c[OW_MAXP];
+  const int tid = threadIdx.x;
+  if (tid < OW_MAXP) s_c[tid] = 0;
+  __syncthreads();
+  const uint64_t base = (uint64_t)blockIdx.x * OW_TILE;
+#pragma unroll
+  for (int u = 0; u < OW_ITEMS; ++u) {
+    const uint64_t i = base + (uint64_t)u * OW_BLOCK + tid;
+    if (i < U) atomicAdd(&s_c[owner_of(keys[i], nparts)], 1u);
+  }
+  __syncthreads();
+  if (tid < (int)nparts) cnt[(uint64_t)tid * tiles + blockIdx.x] = s_c[tid];
+}
+
+// one block: exclusive scan of cnt[0 .. n) (owner-major) in place; totals[o] = partials of owner o
+__global__ __launch_bounds__(1024) void k_owner_scan(uint32_t* __restrict__ cnt, uint32_t n, uint32_t tiles,
+                                                     uint32_t nparts, unsigned long long* __restrict__ totals) {
+  __shared__ uint32_t s_w[16];
+  __shared__ uint32_t s_tot;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const uint32_t per = (n + 1023) / 1024, a = min(n, tid * per), b = min(n, a + per);
+  uint32_t sum = 0;
+  for (uint32_t i = a; i < b; ++i) sum += cnt[i];
+  const uint32_t inc = wave_inclusive_sum(sum);
+  if (lane == 63) s_w[w] = inc;
+  __syncthreads();
+  uint32_t off = 0, tot = 0;
+  for (int i = 0; i < 16; ++i) {
+    off += i < w ? s_w[i] : 0u;
+    tot += s_w[i];
+  }
+  uint32_t run = off + inc - sum;
+  for (uint32_t i = a; i < b; ++i) {
+    const uint32_t x = cnt[i];
+    cnt[i] = run;
+    run += x;
+  }
+  if (tid == 0) s_tot = tot;
+  __syncthreads();
+  if (tid < (int)nparts) {
+    const uint32_t lo = cnt[(uint64_t)tid * tiles], hi = tid + 1 < (int)nparts ? cnt[(uint64_t)(tid + 1) * tiles] : s_tot;
+    totals[tid] = hi - lo;
+  }
+}
+
+// stable partition: thread t of a tile owns OW_ITEMS consecutive partials; per-owner ranks from a
+// block scan over threads, bases from k_owner_scan
+template <typename V>
+__global__ __launch_bounds__(OW_BLOCK) void k_owner_scatter(const int64_t* __restrict__ keys, const V* __restrict__ vals,
+                                                            const int64_t* __restrict__ vals2, uint64_t U,
+                                                            uint32_t nparts, uint32_t tiles,
+                                                            const uint32_t* __restrict__ off, int64_t* __restrict__ okeys,
+                                                            V* __restrict__ ovals, int64_t* __restrict__ ovals2) {
+  __shared__ uint16_t s_r[OW_MAXP][OW_BLOCK];
+  __shared__ uint32_t s_w[OW_BLOCK / WAVE];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const uint64_t i0 = (uint64_t)blockIdx.x * OW_TILE + (uint64_t)tid * OW_ITEMS;
+  for (uint32_t o = 0; o < nparts; ++o) s_r[o][tid] = 0;
+  uint32_t own[OW_ITEMS];
+#pragma unroll
+  for (int j = 0; j < OW_ITEMS; ++j) {
+    own[j] = i0 + j < U ? owner_of(keys[i0 + j], nparts) : OW_MAXP;
+    if (own[j] < OW_MAXP) s_r[own[j]][tid]++;
+  }
+  for (uint32_t o = 0; o < nparts; ++o) {   // exclusive scan of owner o's counts over threads
+    const uint32_t x = s_r[o][tid];
+    const uint32_t inc = wave_inclusive_sum(x);
+    if (lane == 63) s_w[w] = inc;
+    __syncthreads();
+    uint32_t pre = 0;
+    for (int k = 0; k < w; ++k) pre += s_w[k];
+    s_r[o][tid] = (uint16_t)(pre + inc - x);
+    __syncthreads();
+  }
+#pragma unroll
+  for (int j = 0; j < OW_ITEMS; ++j) {
+    if (own[j] >= OW_MAXP) continue;
+    const uint32_t pos = off[(uint64_t)own[j] * tiles + blockIdx.x] + s_r[own[j]][tid]++;
+    okeys[pos] = keys[i0 + j];
+    ovals[pos] = vals[i0 + j];
+    if (vals2) ovals2[pos] = vals2[i0 + j];
+  }
+}
+
+gs_status owner_partition(gs_ctx* c, const int64_t* keys, const void* vals, size_t vb, const int64_t* vals2, uint64_t U,
+                          uint32_t nparts, int64_t* okeys, void* ovals, int64_t* ovals2, uint64_t* counts_host) {
+  char* sm = c->small.as<char>();
+  const uint32_t tiles = (uint32_t)std::max<uint64_t>(1, (U + OW_TILE - 1) / OW_TILE);
+  GS_TRY(ensure(c, c->dist_cnt, (size_t)tiles * nparts * 4 + 64 * 8));
+  uint32_t* cnt = c->dist_cnt.as<uint32_t>();
+  auto* totals = (unsigned long long*)(c->dist_cnt.as<char>() + (size_t)tiles * nparts * 4 + 7 * 8) ;
+  totals = (unsigned long long*)(((uintptr_t)totals) & ~(uintptr_t)7);
+  if (U) {
+    hipLaunchKernelGGL(k_owner_count, dim3(tiles), dim3(OW_BLOCK), 0, c->stream, keys, U, nparts, tiles, cnt);
+    hipLaunchKernelGGL(k_owner_scan, dim3(1), dim3(1024), 0, c->stream, cnt, tiles * nparts, tiles, nparts, totals);
+    if (vb == 8)
+      hipLaunchKernelGGL(k_owner_scatter<uint64_t>, dim3(tiles), dim3(OW_BLOCK), 0, c->stream, keys,
+                         (const uint64_t*)vals, vals2, U, nparts, tiles, cnt, okeys, (uint64_t*)ovals, ovals2);
+    else
+      hipLaunchKernelGGL(k_owner_scatter<uint32_t>, dim3(tiles), dim3(OW_BLOCK), 0, c->stream, keys,
+                         (const uint32_t*)vals, vals2, U, nparts, tiles, cnt, okeys, (uint32_t*)ovals, ovals2);
+    GS_HIP(hipGetLastError());
+    GS_HIP(hipMemcpyAsync(c->host_small + 8, totals, nparts * 8, hipMemcpyDeviceToHost, c->stream));
+    GS_TRY(host_wait(c));
+    memcpy(counts_host, c->host_small + 8, nparts * 8);
+  } else {
+    memset(counts_host, 0, nparts * 8);
+  }
+  (void)sm;
+  return GS_OK;
+}
+
+// ---- RCCL, resolved at run time -----------------------------------------------------------------------
+// ncclUniqueId is 128 bytes; ncclComm_t an opaque pointer; the enums below are RCCL's values.
+typedef void* nccl_comm_t;
+struct NcclApi {
+  int (*GetUniqueId)(void*) = nullptr;
+  int (*CommInitRank)(nccl_comm_t*, int, /* ncclUniqueId by value */ struct NcclId, int) = nullptr;
+  int (*CommDestroy)(nccl_comm_t) = nullptr;
+  int (*Send)(const void*, size_t, int, int, nccl_comm_t, hipStream_t) = nullptr;
+  int (*Recv)(void*, size_t, int, int, nccl_comm_t, hipStream_t) = nullptr;
+  int (*AllToAll)(const void*, void*, size_t, int, nccl_comm_t, hipStream_t) = nullptr;
+  int (*AllReduce)(const void*, void*, size_t, int, int, nccl_comm_t, hipStream_t) = nullptr;
+  int (*GroupStart)() = nullptr;
+  int (*GroupEnd)() = nullptr;
+  const char* (*GetErrorString)(int) = nullptr;
+  bool ok = false;
+};
+struct NcclId {
+  char internal[128];
+};
+constexpr int NCCL_UINT8 = 1, NCCL_UINT64 = 5, NCCL_SUM = 0;   // ncclUint8, ncclUint64, ncclSum
+
+static NcclApi& nccl() {
+  static NcclApi api;
+  static bool tried = false;
+  if (tried) return api;
+  tried = true;
+  void* h = nullptr;
+  if (dlsym(RTLD_DEFAULT, "ncclCommInitRank")) h = RTLD_DEFAULT;   // already loaded (e.g. by torch)
+  if (!h) h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+  if (!h) h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+  if (!h) return api;
+  auto sym = [&](const char* n) { return dlsym(h, n); };
+  api.GetUniqueId = (int (*)(void*))sym("ncclGetUniqueId");
+  api.CommInitRank = (int (*)(nccl_comm_t*, int, NcclId, int))sym("ncclCommInitRank");
+  api.CommDestroy = (int (*)(nccl_comm_t))sym("ncclCommDestroy");
+  api.Send = (int (*)(const void*, size_t, int, int, nccl_comm_t, hipStream_t))sym("ncclSend");
+  api.Recv = (int (*)(void*, size_t, int, int, nccl_comm_t, hipStream_t))sym("ncclRecv");
+  api.AllToAll = (int (*)(const void*, void*, size_t, int, nccl_comm_t, hipStream_t))sym("ncclAllToAll");
+  api.AllReduce = (int (*)(const void*, void*, size_t, int, int, nccl_comm_t, hipStream_t))sym("ncclAllReduce");
+  api.GroupStart = (int (*)())sym("ncclGroupStart");
+  api.GroupEnd = (int (*)())sym("ncclGroupEnd");
+  api.GetErrorString = (const char* (*)(int))sym("ncclGetErrorString");
+  api.ok = api.GetUniqueId && api.CommInitRank && api.CommDestroy && api.Send && api.Recv && api.AllToAll &&
+           api.AllReduce && api.GroupStart && api.GroupEnd && api.GetErrorString;
+  return api;
+}
+
+static gs_status nccl_check(gs_ctx* c, int r, const char* what) {
+  if (r == 0) return GS_OK;
+  return set_error(c, GS_ECOMM, "%s: %s", what, nccl().GetErrorString ? nccl().GetErrorString(r) : "RCCL error");
+}
+
+// exchange owner-grouped rows: send[p] rows of `row` bytes to peer p, receive recv[p] from each
+static gs_status exchange_rows(gs_ctx* c, const char* sendbuf, const uint64_t* send, char* recvbuf, const uint64_t* recv,
+                               size_t row) {
+  NcclApi& A = nccl();
+  const int P = c->comm_size;
+  GS_TRY(nccl_check(c, A.GroupStart(), "ncclGroupStart"));
+  uint64_t so = 0, ro = 0;
+  for (int p = 0; p < P; ++p) {
+    if (send[p]) GS_TRY(nccl_check(c, A.Send(sendbuf + so * row, send[p] * row, NCCL_UINT8, p, c->comm, c->stream), "ncclSend"));
+    if (recv[p]) GS_TRY(nccl_check(c, A.Recv(recvbuf + ro * row, recv[p] * row, NCCL_UINT8, p, c->comm, c->stream), "ncclRecv"));
+    so += send[p];
+    ro += recv[p];
+  }
+  return nccl_check(c, A.GroupEnd(), "ncclGroupEnd");
+}
+
+}  // namespace gs
+
+using namespace gs;
+
+extern "C" {
+
+uint32_t gs_owner_of(int64_t v, uint32_t nparts) { return nparts ? owner_of(v, nparts) : 0u; }
+
+static gs_status check_partials_out(gs_ctx* c, const gs_partials_out* out, uint32_t nparts, bool two) {
+  if (!out || !out->n_out || !out->owner_counts) return set_error(c, GS_EINVAL, "bad gs_partials_out");
+  if (out->capacity && (!out->keys || !out->vals || (two && !out->vals2)))
+    return set_error(c, GS_EINVAL, "bad gs_partials_out buffers");
+  if (nparts < 1 || nparts > (uint32_t)OW_MAXP) return set_error(c, GS_EINVAL, "nparts %u outside [1, 64]", nparts);
+  return GS_OK;
+}
+
+// local reduce into ctx staging, then the owner partition into the caller's buffers
+static gs_status partials_impl(gs_ctx* c, const gs_edge_batch* b, int32_t dir, int32_t op, bool degmax, int64_t init_max,
+                               uint32_t nparts, gs_partials_out* out) {
+  GS_TRY(check_batch(c, b, dir));
+  GS_TRY(check_partials_out(c, out, nparts, degmax));
+  const uint64_t R = dir == GS_DIR_ALL ? 2 * b->n : b->n;
+  GS_TRY(ensure(c, c->dist_k, R * 8 + 8));
+  GS_TRY(ensure(c, c->dist_v, R * 8 + 8));
+  if (degmax) GS_TRY(ensure(c, c->dist_v2, R * 8 + 8));
+  uint64_t U = 0;
+  size_t vb = 8;
+  if (degmax) {
+    gs_degree_out o{c->dist_k.as<int64_t>(), c->dist_v.as<int64_t>(), c->dist_v2.as<int64_t>(), R, &U, GS_MEM_DEVICE, 0};
+    GS_TRY(gs_window_fold_degree_max(c, b, dir, init_max, &o));
+  } else {
+    vb = op == GS_OP_COUNT ? 8 : dtype_bytes(b->val_dtype);
+    gs_vertex_out o{c->dist_k.as<int64_t>(), c->dist_v.p, R, &U, GS_MEM_DEVICE, 0};
+    GS_TRY(gs_window_reduce(c, b, dir, op, &o));
+  }
+  const gs_stage_times keep = c->times;   // the window's own pipeline (the partition is not part of it)
+  *out->n_out = U;
+  const bool direct = out->mem == GS_MEM_DEVICE && out->capacity >= U;
+  int64_t *ok = out->keys, *ov2 = out->vals2;
+  void* ov = out->vals;
+  if (!direct) {
+    GS_TRY(ensure(c, c->dist_k2, U * 8 + 8));
+    GS_TRY(ensure(c, c->dist_v3, U * 8 + 8));
+    if (degmax) GS_TRY(ensure(c, c->dist_v4, U * 8 + 8));
+    ok = c->dist_k2.as<int64_t>();
+    ov = c->dist_v3.p;
+    ov2 = degmax ? c->dist_v4.as<int64_t>() : nullptr;
+  }
+  GS_TRY(owner_partition(c, c->dist_k.as<int64_t>(), c->dist_v.p, vb, degmax ? c->dist_v2.as<int64_t>() : nullptr, U,
+                         nparts, ok, ov, ov2, out->owner_counts));
+  c->times = keep;
+  if (U > out->capacity) return set_error(c, GS_ECAPACITY, "partials need %llu rows", (unsigned long long)U);
+  if (!direct) {
+    GS_TRY(deliver(c, out->keys, ok, U * 8, out->mem));
+    GS_TRY(deliver(c, out->vals, ov, U * vb, out->mem));
+    if (degmax) GS_TRY(deliver(c, out->vals2, ov2, U * 8, out->mem));
+    GS_TRY(host_wait(c));
+  }
+  return GS_OK;
+}
+
+gs_status gs_window_reduce_partials(gs_ctx* c, const gs_edge_batch* b, int32_t dir, int32_t op, uint32_t nparts,
+                                    gs_partials_out* out) {
+  if (!c) return GS_EINVAL;
+  if (op < GS_OP_SUM || op > GS_OP_COUNT) return set_error(c, GS_EINVAL, "bad op %d", op);
+  return partials_impl(c, b, dir, op, false, 0, nparts, out);
+}
+
+gs_status gs_window_fold_degree_max_partials(gs_ctx* c, const gs_edge_batch* b, int32_t dir, uint32_t nparts,
+                                             gs_partials_out* out) {
+  if (!c) return GS_EINVAL;
+  return partials_impl(c, b, dir, 0, true, INT64_MIN, nparts, out);
+}
+
+gs_status gs_merge_partials(gs_ctx* c, const gs_partial_batch* p, int32_t op, const void* init, gs_vertex_out* out) {
+  if (!c) return GS_EINVAL;
+  if (!p || (p->n && (!p->keys || !p->vals))) return set_error(c, GS_EINVAL, "bad gs_partial_batch");
+  if (op < GS_OP_SUM || op > GS_OP_COUNT) return set_error(c, GS_EINVAL, "bad op %d", op);
+  const int32_t mop = op == GS_OP_COUNT ? GS_OP_SUM : op;            // counts merge by SUM
+  const int32_t dt = op == GS_OP_COUNT ? GS_I64 : p->val_dtype;
+  const gs_edge_batch b{p->keys, p->keys, p->vals, p->n, dt, p->mem, 0};
+  return init ? gs_window_fold(c, &b, GS_DIR_OUT, mop, init, out) : gs_window_reduce(c, &b, GS_DIR_OUT, mop, out);
+}
+
+gs_status gs_merge_degree_max_partials(gs_ctx* c, const gs_partial_batch* p, int64_t init_max, gs_degree_out* out) {
+  if (!c) return GS_EINVAL;
+  if (!p || (p->n && (!p->keys || !p->vals || !p->vals2))) return set_error(c, GS_EINVAL, "bad gs_partial_batch");
+  if (!out || !out->n_out || (out->capacity && (!out->keys || !out->degree || !out->max_neighbor)))
+    return set_error(c, GS_EINVAL, "bad gs_degree_out");
+  const gs_edge_batch bd{p->keys, p->keys, p->vals, p->n, GS_I64, p->mem, 0};
+  const gs_edge_batch bm{p->keys, p->keys, p->vals2, p->n, GS_I64, p->mem, 0};
+  gs_vertex_out od{out->keys, out->degree, out->capacity, out->n_out, out->mem, 0};
+  GS_TRY(gs_window_reduce(c, &bd, GS_DIR_OUT, GS_OP_SUM, &od));       // degrees add
+  gs_vertex_out om{out->keys, out->max_neighbor, out->capacity, out->n_out, out->mem, 0};
+  return gs_window_fold(c, &bm, GS_DIR_OUT, GS_OP_MAX, &init_max, &om);   // maxima, then the fold's init
+}
+
+// ---- ctx-owned RCCL communicator ----------------------------------------------------------------------
+gs_status gs_comm_unique_id(void* id128) {
+  if (!id128) return GS_EINVAL;
+  NcclApi& A = nccl();
+  if (!A.ok) return GS_ECOMM;
+  return A.GetUniqueId(id128) == 0 ? GS_OK : GS_ECOMM;
+}
+
+gs_status gs_comm_init(gs_ctx* c, int32_t nranks, int32_t rank, const void* id128) {
+  if (!c) return GS_EINVAL;
+  if (!id128 || nranks < 1 || nranks > OW_MAXP || rank < 0 || rank >= nranks)
+    return set_error(c, GS_EINVAL, "bad communicator arguments (%d ranks, rank %d)", nranks, rank);
+  NcclApi& A = nccl();
+  if (!A.ok) return set_error(c, GS_ECOMM, "RCCL not found (librccl.so.1)");
+  if (c->comm) {
+    A.CommDestroy(c->comm);
+    c->comm = nullptr;
+  }
+  GS_HIP(hipSetDevice(c->device));
+  NcclId id;
+  memcpy(id.internal, id128, 128);
+  nccl_comm_t comm = nullptr;
+  GS_TRY(nccl_check(c, A.CommInitRank(&comm, nranks, id, rank), "ncclCommInitRank"));
+  c->comm = comm;
+  c->comm_size = nranks;
+  c->comm_rank = rank;
+  return GS_OK;
+}
+
+gs_status gs_comm_destroy(gs_ctx* c) {
+  if (!c) return GS_EINVAL;
+  if (c->comm && nccl().ok) nccl().CommDestroy(c->comm);
+  c->comm = nullptr;
+  c->comm_size = 0;
+  return GS_OK;
+}
+
+// exact triangle count etc. add up over ranks: all-reduce (sum) of one u64
+gs_status gs_comm_allreduce_sum_u64(gs_ctx* c, uint64_t* value) {
+  if (!c || !value) return GS_EINVAL;
+  if (!c->comm) return set_error(c, GS_EINVAL, "no communicator (gs_comm_init)");
+  GS_TRY(ensure(c, c->dist_cnt, 64 * 8 + 64 * 4));
+  uint64_t* d = c->dist_cnt.as<uint64_t>();
+  c->host_small[8] = *value;
+  GS_HIP(hipMemcpyAsync(d, c->host_small + 8, 8, hipMemcpyHostToDevice, c->stream));
+  GS_TRY(nccl_check(c, nccl().AllReduce(d, d, 1, NCCL_UINT64, NCCL_SUM, c->comm, c->stream), "ncclAllReduce"));
+  GS_HIP(hipMemcpyAsync(c->host_small + 8, d, 8, hipMemcpyDeviceToHost, c->stream));
+  GS_TRY(host_wait(c));
+  *value = c->host_small[8];
+  return GS_OK;
+}
+
+// partials of this rank's slice -> all-to-all over the ctx's communicator -> the merge of what this
+// rank owns.  dev rows: key (8 B) + value (8 or 4 B) [+ 8 B maximum for the degree fold]
+static gs_status dist_impl(gs_ctx* c, const gs_edge_batch* b, int32_t dir, int32_t op, const void* init, bool degmax,
+                           int64_t init_max, gs_vertex_out* vout, gs_degree_out* dout) {
+  if (!c->comm) return set_error(c, GS_EINVAL, "no communicator (gs_comm_init)");
+  const uint32_t P = (uint32_t)c->comm_size;
+  const uint64_t R = dir == GS_DIR_ALL ? 2 * b->n : b->n;
+  std::vector<uint64_t> send(P), recv(P);
+  uint64_t U = 0;
+  GS_TRY(ensure(c, c->dist_k2, R * 8 + 8));
+  GS_TRY(ensure(c, c->dist_v3, R * 8 + 8));
+  if (degmax) GS_TRY(ensure(c, c->dist_v4, R * 8 + 8));
+  gs_partials_out po{c->dist_k2.as<int64_t>(), c->dist_v3.p, degmax ? c->dist_v4.as<int64_t>() : nullptr, R, &U,
+                     send.data(), GS_MEM_DEVICE, 0};
+  GS_TRY(partials_impl(c, b, dir, op, degmax, INT64_MIN, P, &po));
+  const gs_stage_times keep = c->times;
+  const size_t vb = degmax ? 8 : (op == GS_OP_COUNT ? 8 : dtype_bytes(b->val_dtype));
+  // counts: all-to-all of one u64 per peer
+  GS_TRY(ensure(c, c->dist_cnt, 64 * 8 * 2 + 64));
+  uint64_t* dc = c->dist_cnt.as<uint64_t>();
+  memcpy(c->host_small + 8, send.data(), P * 8);
+  GS_HIP(hipMemcpyAsync(dc, c->host_small + 8, P * 8, hipMemcpyHostToDevice, c->stream));
+  GS_TRY(nccl_check(c, nccl().AllToAll(dc, dc + 64, 1, NCCL_UINT64, c->comm, c->stream), "ncclAllToAll(counts)"));
+  GS_HIP(hipMemcpyAsync(c->host_small + 8, dc + 64, P * 8, hipMemcpyDeviceToHost, c->stream));
+  GS_TRY(host_wait(c));
+  memcpy(recv.data(), c->host_small + 8, P * 8);
+  uint64_t nrecv = 0;
+  for (uint32_t p = 0; p < P; ++p) nrecv += recv[p];
+  // payload: keys, values (and maxima) as separate column exchanges (no packing kernel)
+  GS_TRY(ensure(c, c->dist_k, nrecv * 8 + 8));
+  GS_TRY(ensure(c, c->dist_v, nrecv * 8 + 8));
+  if (degmax) GS_TRY(ensure(c, c->dist_v2, nrecv * 8 + 8));
+  GS_TRY(exchange_rows(c, c->dist_k2.as<char>(), send.data(), c->dist_k.as<char>(), recv.data(), 8));
+  GS_TRY(exchange_rows(c, c->dist_v3.as<char>(), send.data(), c->dist_v.as<char>(), recv.data(), vb));
+  if (degmax) GS_TRY(exchange_rows(c, c->dist_v4.as<char>(), send.data(), c->dist_v2.as<char>(), recv.data(), 8));
+  const int32_t pdt = degmax || op == GS_OP_COUNT ? GS_I64 : b->val_dtype;
+  const gs_partial_batch pb{c->dist_k.as<int64_t>(), c->dist_v.p, degmax ? c->dist_v2.as<int64_t>() : nullptr, nrecv,
+                            pdt, GS_MEM_DEVICE};
+  gs_status st = degmax ? gs_merge_degree_max_partials(c, &pb, init_max, dout) : gs_merge_partials(c, &pb, op, init, vout);
+  c->times = keep;
+  return st;
+}
+
+gs_status gs_window_reduce_dist(gs_ctx* c, const gs_edge_batch* b, int32_t dir, int32_t op, const void* init,
+                                gs_vertex_out* out) {
+  if (!c) return GS_EINVAL;
+  if (op < GS_OP_SUM || op > GS_OP_COUNT) return set_error(c, GS_EINVAL, "bad op %d", op);
+  GS_TRY(check_batch(c, b, dir));
+  return dist_impl(c, b, dir, op, init, false, 0, out, nullptr);
+}
+
+gs_status gs_window_fold_degree_max_dist(gs_ctx* c, const gs_edge_batch* b, int32_t dir, int64_t init_max,
+                                         gs_degree_out* out) {
+  if (!c) return GS_EINVAL;
+  GS_TRY(check_batch(c, b, dir));
+  return dist_impl(c, b, dir, 0, nullptr, true, init_max, nullptr, out);
+}
+
+}  // extern "C"

@@ -361,7 +361,7 @@ gs_status gs_create(const gs_config* cfg, gs_ctx** out) {
   c->own_stream = true;
   for (auto& e : c->ev) hipEventCreate(&e);
   for (auto& e : c->pass_ev) hipEventCreate(&e);
-  if (hipHostMalloc((void**)&c->host_small, 64, hipHostMallocDefault) != hipSuccess ||
+  if (hipHostMalloc((void**)&c->host_small, HOST_SMALL_WORDS * 8, hipHostMallocDefault) != hipSuccess ||
       ensure(c, c->small, SM_BYTES, true) != GS_OK) {
     gs_destroy(c);
     return GS_ENOMEM;
@@ -390,7 +390,7 @@ void gs_destroy(gs_ctx* c) {
                     &c->rbk_word, &c->rbk_agg, &c->rbk_inc, &c->small, &c->out_keys, &c->out_a, &c->out_b, &c->aux,
                     &c->bk_meta, &c->bk_items, &c->bk_slabs, &c->dp_cnt, &c->dp_csum, &c->dp_off, &c->tri_loops, &c->tri_keep, &c->tri_tiles, &c->tri_pos, &c->tri_ou, &c->tri_onbr, &c->tri_heavy, &c->tri_range, &c->tri_queue,
                     &c->pr_a, &c->pr_b, &c->pr_f, &c->pr_key, &c->pr_val, &c->pr_gk, &c->pr_gv, &c->pr_small,
-                    &c->tx_text, &c->tx_cnt, &c->tx_starts})
+                    &c->tx_text, &c->tx_cnt, &c->tx_starts, &c->zipf_cdf})
     if (b->p) hipFree(b->p);
   for (auto& e : c->ev)
     if (e) hipEventDestroy(e);

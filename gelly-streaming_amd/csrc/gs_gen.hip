@@ -1,6 +1,10 @@
 // gs_gen.hip — counter-based synthetic edge streams on the device.
 // Bit-identical to oracle/gs_oracle.c (gso_gen_*), so CPU and GPU see the same windows.
-#include "gs_internal.hpp"
+#include <math.h>
+
+#include <vector>
+
+#include "gs_ops.hpp"
 
 namespace gs {
 
@@ -73,6 +77,24 @@ __global__ __launch_bounds__(256) void k_gen_values(uint64_t n, uint64_t seed, u
   }
 }
 
+// Zipf sources: the smallest k with cdf[k] > u (53-bit fixed point, cdf[V - 1] = 2^53)
+__global__ __launch_bounds__(256) void k_gen_zipf(const uint64_t* __restrict__ cdf, uint64_t V, uint64_t n,
+                                                  uint64_t seed, uint64_t first, int64_t* __restrict__ src,
+                                                  int64_t* __restrict__ dst) {
+  for (uint64_t k = (uint64_t)blockIdx.x * 256 + threadIdx.x; k < n; k += (uint64_t)gridDim.x * 256) {
+    const uint64_t i = first + k;
+    const uint64_t u = splitmix64(seed ^ 0x21F0A5EDull, i) >> 11;
+    uint64_t lo = 0, hi = V - 1;
+    while (lo < hi) {
+      const uint64_t mid = (lo + hi) >> 1;
+      if (cdf[mid] > u) hi = mid;
+      else lo = mid + 1;
+    }
+    src[k] = (int64_t)lo;
+    dst[k] = (int64_t)(splitmix64(seed ^ 0xD5D5D5D5ull, i) % V);
+  }
+}
+
 static unsigned gen_grid(uint64_t n) {
   uint64_t g = (n + 255) / 256;
   return (unsigned)(g < 1 ? 1 : (g > 8192 ? 8192 : g));
@@ -113,6 +135,35 @@ gs_status gs_generate_uniform(gs_ctx* c, uint64_t V, uint64_t n, uint64_t seed, 
   hipSetDevice(c->device);
   hipLaunchKernelGGL(k_gen_uniform, dim3(gen_grid(n)), dim3(256), 0, c->stream, V, n, seed, first_edge, src, dst);
   return hip_check(c, hipGetLastError(), "k_gen_uniform");
+}
+
+gs_status gs_generate_zipf(gs_ctx* c, uint64_t V, double exponent, uint64_t n, uint64_t seed, uint64_t first_edge,
+                           int64_t* src, int64_t* dst) {
+  if (!c) return GS_EINVAL;
+  if (V < 2 || V > (1ull << 32) || !(exponent > 0.0) || (n && (!src || !dst)))
+    return set_error(c, GS_EINVAL, "bad Zipf arguments");
+  if (!n) return GS_OK;
+  hipSetDevice(c->device);
+  if (c->zipf_v != V || c->zipf_s != exponent) {
+    // the CDF table: a sequential double sum of pow() terms (the oracle's gso_zipf_cdf, same arithmetic)
+    std::vector<uint64_t> cdf(V);
+    double cum = 0.0;
+    for (uint64_t k = 0; k < V; ++k) cum += pow((double)(k + 1), -exponent);
+    const double total = cum;
+    cum = 0.0;
+    for (uint64_t k = 0; k < V; ++k) {
+      cum += pow((double)(k + 1), -exponent);
+      cdf[k] = (uint64_t)((cum / total) * 9007199254740992.0);
+    }
+    cdf[V - 1] = 1ull << 53;
+    GS_TRY(ensure(c, c->zipf_cdf, V * 8));
+    GS_HIP(hipMemcpy(c->zipf_cdf.p, cdf.data(), V * 8, hipMemcpyHostToDevice));
+    c->zipf_v = V;
+    c->zipf_s = exponent;
+  }
+  hipLaunchKernelGGL(k_gen_zipf, dim3(gen_grid(n)), dim3(256), 0, c->stream, c->zipf_cdf.as<uint64_t>(), V, n, seed,
+                     first_edge, src, dst);
+  return hip_check(c, hipGetLastError(), "k_gen_zipf");
 }
 
 gs_status gs_generate_values(gs_ctx* c, uint64_t n, uint64_t seed, uint64_t first_edge, int32_t dtype, void* val) {

@@ -337,6 +337,10 @@ static gs_status triangles_impl(gs_ctx* c, const gs_edge_batch* b, uint32_t part
   GS_HIP(hipMemsetAsync(d_total, 0, 8, c->stream));
   GS_HIP(hipMemsetAsync(d_probes, 0, 8, c->stream));
   GS_HIP(hipMemsetAsync(d_nheavy, 0, 4, c->stream));
+  uint32_t* d_err = (uint32_t*)(sm + SM_DEV_ERR);
+  GS_HIP(hipMemsetAsync(d_err, 0, 4, c->stream));
+  // LDS hash-set bucket cap: unlimited, or one bucket under GS_FLAG_TEST_TINY_TABLES (tests only)
+  const uint32_t nb_cap = (c->flags & GS_FLAG_TEST_TINY_TABLES) ? 1u : 0xFFFFFFFFu;
   const uint64_t q0 = M * part / nparts, q1 = M * (part + 1) / nparts;   // this part's oriented edges
   uint2* out_range = reinterpret_cast<uint2*>(c->tri_range.p);
   uint2* in_range = out_range + V;
@@ -351,19 +355,23 @@ static gs_status triangles_impl(gs_ctx* c, const gs_edge_batch* b, uint32_t part
     hipLaunchKernelGGL(k_tri_light, dim3(pass == 0 ? nvb : 4096u), dim3(TH_BLOCK), 0, c->stream,
                        c->tri_onbr.as<uint32_t>(), c->tri_ou.as<uint32_t>(), out_range, in_range, (uint32_t)V,
                        (uint32_t)q0, (uint32_t)q1, pass, queue, d_nqueue, c->tri_heavy.as<uint2>(), d_nheavy,
-                       d_total, d_probes);
+                       d_total, d_probes, nb_cap, d_err);
     GS_HIP(hipGetLastError());
   }
   hipEventRecord(c->ev[5], c->stream);
   hipLaunchKernelGGL(k_tri_heavy, dim3(GS_TH_HGRID), dim3(TH_HBLOCK), 0, c->stream, c->tri_onbr.as<uint32_t>(),
                      c->tri_ou.as<uint32_t>(), out_range, in_range, c->tri_heavy.as<uint2>(), d_nheavy, d_total,
-                     d_probes);
+                     d_probes, nb_cap, d_err);
   GS_HIP(hipGetLastError());
   hipEventRecord(c->ev[3], c->stream);
   GS_HIP(hipMemcpyAsync(c->host_small, sm, 32, hipMemcpyDeviceToHost, c->stream));
   GS_HIP(hipMemcpyAsync(c->host_small + 6, d_probes, 8, hipMemcpyDeviceToHost, c->stream));
+  c->host_small[7] = 0;   // (the copy below fills the low 4 bytes)
+  GS_HIP(hipMemcpyAsync(c->host_small + 7, d_err, 4, hipMemcpyDeviceToHost, c->stream));
   GS_TRY(host_wait(c));
   if ((uint32_t)c->host_small[3] != 0) return set_error(c, GS_EDEVICE, "look-back spin timed out");
+  if ((uint32_t)c->host_small[7] & GS_DERR_TABLE_FULL)
+    return set_error(c, GS_EDEVICE, "window triangles: an LDS hash set filled up (counting aborted)");
   uint64_t T = c->host_small[2];
   {   // stage times (path 3): sym + sort, unique, rows + orientation, light count, heavy count
     gs_stage_times& t = c->times;

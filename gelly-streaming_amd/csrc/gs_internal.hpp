@@ -41,6 +41,7 @@ struct gs_ctx {
   uint32_t flags = 0;    // gs_config.flags
   int64_t bk_base = 0;   // bucket path: predicted lower bound of the next window's vertex IDs
   uint32_t bk_nbp = 0;   // direct bucket path: predicted bucket count (0 = BK_MAXB)
+  int bk_wide_vals = 0;  // direct bucket path: > 0 = windows left that store 8-byte values (escapes were common)
   int n_cu = 0;          // compute units (persistent grids)
   // input staging (host batches)
   gs::DevBuf in_src, in_dst, in_val;
@@ -66,6 +67,10 @@ struct gs_ctx {
   gs::DevBuf pr_a, pr_b, pr_f, pr_key, pr_val, pr_gk, pr_gv, pr_small;
   // edge text parser (gs_text.hip): staged text, tile newline counts, record starts
   gs::DevBuf tx_text, tx_cnt, tx_starts;
+  // Zipf generator: CDF table of (zipf_v, zipf_s)
+  gs::DevBuf zipf_cdf;
+  uint64_t zipf_v = 0;
+  double zipf_s = 0.0;
   hipEvent_t ev[6] = {};
   hipEvent_t sync_ev = nullptr;   // host_wait: polled completion event
   hipEvent_t pass_ev[9] = {};
@@ -88,7 +93,12 @@ constexpr size_t SM_TABLE = SM_TOTAL + 64;            // u32[513] region table o
 constexpr size_t SM_BK_MM = SM_TABLE + 520 * 4;    // u64[4] bucket path: min', max', outside, U
 constexpr size_t SM_BK_N = SM_BK_MM + 32;            // u32[4] bucket path: items, multi buckets, claim ctr
 constexpr size_t SM_TRI_PROBES = SM_BK_N + 16;      // u64 triangles: hash probes of the counting step
-constexpr size_t SM_BYTES = SM_TRI_PROBES + 16;
+constexpr size_t SM_BK_ESC = SM_TRI_PROBES + 16;    // u64 packed scatter: escaped values
+constexpr size_t SM_DEV_ERR = SM_BK_ESC + 8;        // u32 device error flags (GS_DERR_*)
+constexpr size_t SM_BYTES = SM_DEV_ERR + 8;
+// device error flags (SM_DEV_ERR): a kernel that cannot finish its work sets one and returns
+constexpr uint32_t GS_DERR_TABLE_FULL = 1u;         // an LDS hash set filled up (triangle counting)
+constexpr size_t HOST_SMALL_WORDS = 32;             // pinned u64 mirror of small scalars
 
 gs_status set_error(gs_ctx* c, gs_status s, const char* fmt, ...);
 gs_status hip_check(gs_ctx* c, hipError_t e, const char* what);

@@ -15,6 +15,7 @@
 // set).  Only vertices whose out-list starts in [q0, q1) count (the multi-GPU split).
 #pragma once
 #include "gs_device.hpp"
+#include "gs_internal.hpp"
 
 namespace gs {
 
@@ -80,23 +81,35 @@ __global__ __launch_bounds__(256) void k_tri_rows(const uint32_t* __restrict__ d
   }
 }
 
+// Every insert and probe chain is bounded by the table's bucket count: a full table (which the
+// sizing rules exclude: TH_DMAX <= TH_H / 2, d <= TH_NU at <= half load) sets GS_DERR_TABLE_FULL in
+// *err and gives up, and the host returns GS_EDEVICE, instead of a chain that never ends.
+// (GS_FLAG_TEST_TINY_TABLES forces one-bucket tables so the tests can see that error.)
+__device__ __forceinline__ void th_fail(uint32_t* err) { atomicOr(err, GS_DERR_TABLE_FULL); }
+
 // N+(v) as an LDS hash set of 4-slot buckets; slots of a bucket fill in order
-__device__ __forceinline__ void th_insert(uint32_t* hs, uint32_t x, uint32_t bmask) {
-  for (uint32_t b = th_hash(x, bmask);; b = (b + 1) & bmask) {
+__device__ __forceinline__ void th_insert(uint32_t* hs, uint32_t x, uint32_t bmask, uint32_t* err) {
+  uint32_t b = th_hash(x, bmask);
+  for (uint32_t step = 0; step <= bmask; ++step, b = (b + 1) & bmask) {
 #pragma unroll
     for (int j = 0; j < 4; ++j)
       if (atomicCAS(&hs[b * 4 + j], TH_EMPTY, x) == TH_EMPTY) return;
   }
+  th_fail(err);
 }
 
 // members among x[j] for the set bits j of pend; all pending probes of the lane read their bucket
 // together (one 16-byte LDS read each)
 __device__ __forceinline__ uint32_t th_probe(const uint4* hb, uint32_t bmask, const uint32_t (&x)[TH_ILP],
-                                             uint32_t pend) {
+                                             uint32_t pend, uint32_t* err) {
   uint32_t b[TH_ILP], cnt = 0;
 #pragma unroll
   for (int j = 0; j < TH_ILP; ++j) b[j] = th_hash(x[j], bmask);
-  while (pend) {
+  for (uint32_t step = 0; pend; ++step) {
+    if (step > bmask) {   // no free last slot on a whole sweep: the table is full
+      th_fail(err);
+      break;
+    }
     uint4 y[TH_ILP];
 #pragma unroll
     for (int j = 0; j < TH_ILP; ++j) y[j] = hb[b[j]];
@@ -119,15 +132,16 @@ __device__ __forceinline__ uint32_t th_probe(const uint4* hb, uint32_t bmask, co
 __device__ __forceinline__ uint32_t th_wave_chunk(const uint32_t* __restrict__ onbr, const uint32_t* __restrict__ inbr,
                                                   const uint2* __restrict__ out_range, uint2 ro, uint32_t c0,
                                                   uint32_t c1, int lane, uint4* hb, uint32_t* po, uint32_t* ps,
-                                                  uint64_t& probes) {
+                                                  uint64_t& probes, uint32_t nb_cap, uint32_t* err) {
   uint32_t* hs = reinterpret_cast<uint32_t*>(hb);
   const uint32_t d = ro.y - ro.x;
   uint32_t nb = 16;
   while (nb < d && nb < TH_H / 4) nb <<= 1;
+  nb = min(nb, nb_cap);
   const uint32_t bmask = nb - 1;
   for (uint32_t i = lane; i < nb * 4; i += WAVE) hs[i] = TH_EMPTY;
   wave_lds_sync();
-  for (uint32_t i = lane; i < d; i += WAVE) th_insert(hs, onbr[ro.x + i], bmask);
+  for (uint32_t i = lane; i < d; i += WAVE) th_insert(hs, onbr[ro.x + i], bmask, err);
   uint32_t run = 0, dn = 0;
   for (uint32_t i0 = c0; i0 < c1; i0 += WAVE) {
     const uint32_t i = i0 + lane;
@@ -182,7 +196,7 @@ __device__ __forceinline__ uint32_t th_wave_chunk(const uint32_t* __restrict__ o
       x[j] = onbr[ps[lo] + (kj - po[lo])];
       pend |= (k0 + (uint32_t)(j * WAVE + lane) < run ? 1u : 0u) << j;
     }
-    cnt += th_probe(hb, bmask, x, pend);
+    cnt += th_probe(hb, bmask, x, pend, err);
   }
 #else
   for (uint32_t k0 = 0; k0 < run; k0 += WAVE * TH_ILP) {
@@ -218,7 +232,7 @@ __device__ __forceinline__ uint32_t th_wave_chunk(const uint32_t* __restrict__ o
     uint32_t pend = 0;
 #pragma unroll
     for (int j = 0; j < TH_ILP; ++j) pend |= (kb + j < run ? 1u : 0u) << j;
-    cnt += th_probe(hb, bmask, x, pend);
+    cnt += th_probe(hb, bmask, x, pend, err);
   }
 #endif
   wave_lds_sync();   // the next item clears the table
@@ -235,7 +249,8 @@ __global__ __launch_bounds__(TH_BLOCK) void k_tri_light(const uint32_t* __restri
                                                         uint32_t* __restrict__ n_queue, uint2* __restrict__ heavy,
                                                         uint32_t* __restrict__ n_heavy,
                                                         unsigned long long* __restrict__ total,
-                                                        unsigned long long* __restrict__ n_probes) {
+                                                        unsigned long long* __restrict__ n_probes, uint32_t nb_cap,
+                                                        uint32_t* __restrict__ err) {
   // 8 KiB per wave, 32 KiB per block: five blocks per CU
   __shared__ uint4 s_hash[TH_WPB][TH_H / 4];
   __shared__ uint32_t s_off[TH_WPB][TH_DMAX];   // exclusive prefix of |N+(u)| over the non-empty u
@@ -274,7 +289,8 @@ __global__ __launch_bounds__(TH_BLOCK) void k_tri_light(const uint32_t* __restri
       c0 = ri.x + q.y * TH_DMAX;
       c1 = min(ri.y, c0 + TH_DMAX);
     }
-    cnt += th_wave_chunk(onbr, inbr, out_range, out_range[v], c0, c1, lane, s_hash[w], s_off[w], s_st[w], probes);
+    cnt += th_wave_chunk(onbr, inbr, out_range, out_range[v], c0, c1, lane, s_hash[w], s_off[w], s_st[w], probes,
+                         nb_cap, err);
   }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o, WAVE);
@@ -293,7 +309,8 @@ __global__ __launch_bounds__(TH_HBLOCK) void k_tri_heavy(const uint32_t* __restr
                                                          const uint2* __restrict__ heavy,
                                                          const uint32_t* __restrict__ n_heavy,
                                                          unsigned long long* __restrict__ total,
-                                                         unsigned long long* __restrict__ n_probes) {
+                                                         unsigned long long* __restrict__ n_probes, uint32_t nb_cap,
+                                                         uint32_t* __restrict__ err) {
   __shared__ uint4 s_hash[TH_HB];               // TH_NU / 2 buckets (64 KiB): N+(v) as a hash set of 4-slot buckets
   __shared__ uint32_t s_off[TH_VCH + 1];        // prefix of |N+(u)| over the chunk; [cn] = total
   __shared__ uint32_t s_st[TH_VCH];             // start of that N+(u) in onbr
@@ -312,12 +329,13 @@ __global__ __launch_bounds__(TH_HBLOCK) void k_tri_heavy(const uint32_t* __restr
     const bool in_lds = d <= TH_NU;   // else: binary search of the sorted list in HBM
     uint32_t nb = 16;
     while (nb * 2 < d && nb < TH_HB) nb <<= 1;
+    nb = min(nb, nb_cap);
     const uint32_t bmask = nb - 1;
     __syncthreads();   // the previous item is done with the table
     if (in_lds && table_v != v) {
       for (uint32_t i = tid; i < nb * 4; i += TH_HBLOCK) hs[i] = TH_EMPTY;
       __syncthreads();
-      for (uint32_t i = tid; i < d; i += TH_HBLOCK) th_insert(hs, onbr[ro.x + i], bmask);
+      for (uint32_t i = tid; i < d; i += TH_HBLOCK) th_insert(hs, onbr[ro.x + i], bmask, err);
       table_v = v;
     }
     const uint32_t* nvl = onbr + ro.x;
@@ -375,7 +393,7 @@ __global__ __launch_bounds__(TH_HBLOCK) void k_tri_heavy(const uint32_t* __restr
           pend |= (kb + j < tot ? 1u : 0u) << j;
         }
         if (in_lds) {
-          cnt += th_probe(s_hash, bmask, x, pend);
+          cnt += th_probe(s_hash, bmask, x, pend, err);
         } else {
 #pragma unroll
           for (int j = 0; j < TH_ILP; ++j) {

@@ -61,13 +61,16 @@ class StageTimes:
     path: int = 0          # 0: LSD sort + reduce-by-key; 1: bucket path, onesweep partition (pass_ms = passes,
                            # accumulate, merge, emit); 2: bucket path, direct partition (pass_ms = offset scans,
                            # scatter, accumulate, merge, emit; keyinfo_ms = per-tile histogram)
+    packed: bool = False   # path 2: 4-byte packed partition records (k_dp_scatter_pack)
+    escapes: int = 0       # path 2, packed: values stored in full
 
 
 class Engine:
     def __init__(self, device: int = 0, reserve_edges: int = 0, torch_stream: bool = True, sort_only: bool = False,
-                 bk_onesweep: bool = False):
+                 bk_onesweep: bool = False, no_pack: bool = False, flags: int = 0):
         self._L = L.load()
-        flags = (L.GS_FLAG_SORT_ONLY if sort_only else 0) | (L.GS_FLAG_BK_ONESWEEP if bk_onesweep else 0)
+        flags |= (L.GS_FLAG_SORT_ONLY if sort_only else 0) | (L.GS_FLAG_BK_ONESWEEP if bk_onesweep else 0) | \
+            (L.GS_FLAG_NO_PACK if no_pack else 0)
         cfg = L.GsConfig(device, flags, reserve_edges)
         ctx = ctypes.c_void_p()
         st = self._L.gs_create(ctypes.byref(cfg), ctypes.byref(ctx))
@@ -120,7 +123,7 @@ class Engine:
         launched = 5 if t.path in (2, 3) else t.sort_passes + (3 if t.path == 1 else 1 if t.fused_last else 0)
         return StageTimes(t.keyinfo_ms, t.sort_ms, t.reduce_ms, t.total_ms, t.sort_passes, t.key_bits, t.records,
                           t.vertices, list(t.pass_ms)[:launched], t.key_bytes, t.payload_bytes,
-                          t.partials, bool(t.fused_last), t.path)
+                          t.partials, bool(t.fused_last), t.path, bool(t.packed), t.escapes)
 
     # -- helpers ---------------------------------------------------------------------------------
     def _batch(self, src, dst, val):
@@ -311,6 +314,16 @@ class Engine:
         src = torch.empty(n, dtype=torch.int64, device=f"cuda:{self.device}")
         dst = torch.empty(n, dtype=torch.int64, device=f"cuda:{self.device}")
         self._check(self._L.gs_generate_uniform(self.ctx, num_vertices, n, seed, first_edge, _ptr(src), _ptr(dst)))
+        return src, dst
+
+    def generate_zipf(self, num_vertices, n, seed, exponent=1.1, first_edge=0):
+        """Zipf(exponent) sources over [0, num_vertices) (hubs at the lowest IDs), uniform destinations."""
+        import torch
+
+        src = torch.empty(n, dtype=torch.int64, device=f"cuda:{self.device}")
+        dst = torch.empty(n, dtype=torch.int64, device=f"cuda:{self.device}")
+        self._check(self._L.gs_generate_zipf(self.ctx, num_vertices, float(exponent), n, seed, first_edge, _ptr(src),
+                                             _ptr(dst)))
         return src, dst
 
     def generate_values(self, n, seed, dtype=L.GS_I64, first_edge=0):

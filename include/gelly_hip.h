@@ -83,6 +83,10 @@ typedef struct gs_ctx gs_ctx;
 #define GS_FLAG_SORT_ONLY 1u   /* reduce / fold: always take the full LSD sort + reduce-by-key path */
 #define GS_FLAG_BK_ONESWEEP 2u /* bucket path: partition with 1-2 LSD passes instead of the one-pass
                                   direct scatter (A/B measurement; same results)                   */
+#define GS_FLAG_NO_PACK 4u     /* bucket path: integer SUM/MIN/MAX keep 8-byte partitioned values
+                                  instead of 4-byte packed records (A/B measurement; same results)  */
+#define GS_FLAG_TEST_TINY_TABLES 8u /* TEST ONLY: triangle counting sizes its LDS hash sets at one
+                                  bucket, so sets overflow and the call must fail with GS_EDEVICE   */
 
 typedef struct gs_config {
   int32_t device;          /* HIP device ordinal                                           */
@@ -244,6 +248,10 @@ GS_API gs_status gs_generate_rmat(gs_ctx* ctx, int32_t scale, uint64_t n, uint64
 /* Uniform: src, dst in [0, V), dst != src. */
 GS_API gs_status gs_generate_uniform(gs_ctx* ctx, uint64_t num_vertices, uint64_t n, uint64_t seed,
                               uint64_t first_edge, int64_t* src_dev, int64_t* dst_dev);
+/* Zipf(exponent) sources over [0, V) (P(k) ~ (k+1)^-exponent: hubs at the lowest IDs), uniform
+ * destinations — the power-law source stream of BASELINE config C3 (V = 2^24, exponent 1.1). */
+GS_API gs_status gs_generate_zipf(gs_ctx* ctx, uint64_t num_vertices, double exponent, uint64_t n, uint64_t seed,
+                                  uint64_t first_edge, int64_t* src_dev, int64_t* dst_dev);
 /* Edge values: I64 = splitmix64(seed, i) & 0xFFFF; F64 = top 53 bits / 2^53; I32/F32 likewise. */
 GS_API gs_status gs_generate_values(gs_ctx* ctx, uint64_t n, uint64_t seed, uint64_t first_edge,
                              int32_t dtype, void* val_dev);
@@ -267,6 +275,9 @@ typedef struct gs_stage_times {
                                  rows + orientation, light count, heavy count; records = unique
                                  adjacency entries, vertices = vertices with edges, partials = hash
                                  probes of the counting step, sort_passes = LSD passes)          */
+  uint32_t packed;         /* path 2: 1 = 4-byte packed partition records (k_dp_scatter_pack)    */
+  uint32_t reserved;
+  uint64_t escapes;        /* path 2, packed: values stored in full (outside [0, 0xFFFF))          */
 } gs_stage_times;
 GS_API gs_status gs_last_stage_times(const gs_ctx* ctx, gs_stage_times* out);
 

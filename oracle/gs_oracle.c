@@ -629,6 +629,7 @@ GSO_API int32_t gso_window_triangles_fwd(const int64_t* src, const int64_t* dst,
 /* CPU baseline: keyBy(vertex) over P threads + per-subtask hash-map fold (bench only)  */
 /* ------------------------------------------------------------------------------------ */
 typedef struct { int64_t key; uint64_t val; } shuffled;  /* a record on the wire after keyBy */
+enum { BL_DEGMAX = 4 };   /* gso_baseline_reduce op: the degree / max-neighbour fold (val = neighbour) */
 typedef struct {
   const int64_t* src; const int64_t* dst; const void* val;
   uint64_t n; int dtype, dir, op, P, tid;
@@ -660,7 +661,7 @@ static void* bl_worker(void* p) {
     const int q = (int)(mix64((uint64_t)key) % (uint64_t)P);
     shuffled* o = &A->part[t * P + q][A->part_n[t * P + q]++];
     o->key = key;
-    o->val = A->op == OP_COUNT ? 0 : load_val(A->dtype, A->val, i);
+    o->val = A->op == OP_COUNT ? 0 : A->op == BL_DEGMAX ? (uint64_t)nbr : load_val(A->dtype, A->val, i);
   }
   free(cnt);
   pthread_barrier_wait(A->bar);
@@ -670,7 +671,7 @@ static void* bl_worker(void* p) {
   for (int q = 0; q < P; ++q) mine += A->part_n[q * P + t];
   uint64_t cap = 16;
   while (cap < 2 * (mine / 2 + 16)) cap <<= 1;
-  typedef struct { int64_t key; uint64_t acc; } slot_t;
+  typedef struct { int64_t key; uint64_t acc; int64_t acc2; } slot_t;
   slot_t* tab = (slot_t*)malloc(cap * sizeof(slot_t));
   uint8_t* used = (uint8_t*)calloc(cap, 1);
   uint64_t size = 0;
@@ -682,10 +683,14 @@ static void* bl_worker(void* p) {
       if (!used[h]) {
         used[h] = 1;
         tab[h].key = lst[j].key;
-        tab[h].acc = A->op == OP_COUNT ? 1 : lst[j].val;
+        tab[h].acc = (A->op == OP_COUNT || A->op == BL_DEGMAX) ? 1 : lst[j].val;
+        tab[h].acc2 = (int64_t)lst[j].val;
         ++size;
       } else if (A->op == OP_COUNT) {
         tab[h].acc++;
+      } else if (A->op == BL_DEGMAX) {   /* foldNeighbors(degree, max neighbour) */
+        tab[h].acc++;
+        if ((int64_t)lst[j].val > tab[h].acc2) tab[h].acc2 = (int64_t)lst[j].val;
       } else {
         apply_op(A->op, A->dtype, &tab[h].acc, &lst[j].val, 0);
       }
@@ -788,4 +793,314 @@ GSO_API int64_t gso_parse_edges_text(const char* text, uint64_t bytes, int64_t* 
     p = q + 1;
   }
   return (int64_t)n;
+}
+
+/* ------------------------------------------------------------------------------------ */
+/* Zipf(s) source stream ("a Zipf(s=1.1) source stream over 2^24 IDs"): */
+/* src = k with probability (k+1)^-s / H(V, s), hubs at the lowest IDs; dst uniform.      */
+/* Inverse CDF over a 53-bit fixed-point table; the table is a sequential double sum of   */
+/* pow() terms, so gs_generate_zipf (library host code, same arithmetic) is bit-identical. */
+/* ------------------------------------------------------------------------------------ */
+GSO_API void gso_zipf_cdf(uint64_t V, double s, uint64_t* cdf) {
+  double cum = 0.0;
+  for (uint64_t k = 0; k < V; ++k) cum += pow((double)(k + 1), -s);
+  const double total = cum;
+  cum = 0.0;
+  for (uint64_t k = 0; k < V; ++k) {
+    cum += pow((double)(k + 1), -s);
+    cdf[k] = (uint64_t)((cum / total) * 9007199254740992.0);
+  }
+  cdf[V - 1] = 1ull << 53;
+}
+
+GSO_API int gso_gen_zipf(uint64_t V, double s, uint64_t n, uint64_t seed, uint64_t first_edge, int64_t* src,
+                         int64_t* dst) {
+  uint64_t* cdf = (uint64_t*)malloc(V * sizeof(uint64_t));
+  if (!cdf) return -1;
+  gso_zipf_cdf(V, s, cdf);
+  for (uint64_t k = 0; k < n; ++k) {
+    const uint64_t i = first_edge + k;
+    const uint64_t u = gso_splitmix64(seed ^ 0x21F0A5EDull, i) >> 11;
+    uint64_t lo = 0, hi = V - 1;   /* smallest j with cdf[j] > u */
+    while (lo < hi) {
+      const uint64_t mid = (lo + hi) >> 1;
+      if (cdf[mid] > u) hi = mid;
+      else lo = mid + 1;
+    }
+    src[k] = (int64_t)lo;
+    dst[k] = (int64_t)(gso_splitmix64(seed ^ 0xD5D5D5D5ull, i) % V);
+  }
+  free(cdf);
+  return 0;
+}
+
+/* ------------------------------------------------------------------------------------ */
+/* Large-window restatement of the folds (config-size parity).    */
+/* The same left fold as window_fold / gso_window_fold_degree_max, spread over P threads  */
+/* the way keyBy spreads a window over Flink subtasks (SimpleEdgeStream.java:159-167):    */
+/* producer p routes its contiguous record range by hash(key) % P; consumer q folds the   */
+/* records of producers 0..P-1 in that order, so every key still sees its records in      */
+/* arrival order (float sums identical to the sequential fold).  Outputs ascend by key.   */
+/* ------------------------------------------------------------------------------------ */
+enum { MT_REDUCE = 0, MT_FOLD = 1, MT_DEGMAX = 2 };
+typedef struct {
+  const int64_t* src; const int64_t* dst; const void* val;
+  uint64_t n; int dtype, dir, op, mode, P, tid;
+  uint64_t init_bits; int64_t init_max;
+  uint32_t** part; uint64_t* part_n;   /* [P*P] record indices routed producer -> consumer */
+  int64_t* keys; uint64_t* a; int64_t* b; uint64_t U;   /* consumer output, ascending keys */
+  int err;
+  pthread_barrier_t* bar;
+} mt_arg;
+
+static void* mt_worker(void* p) {
+  mt_arg* A = (mt_arg*)p;
+  const int P = A->P, t = A->tid;
+  const uint64_t R = n_records(A->n, A->dir);
+  const uint64_t lo = R * (uint64_t)t / (uint64_t)P, hi = R * (uint64_t)(t + 1) / (uint64_t)P;
+  uint64_t* cnt = (uint64_t*)calloc((size_t)P, sizeof(uint64_t));
+  for (uint64_t r = lo; r < hi; ++r) {
+    int64_t key, nbr;
+    record(A->src, A->dst, A->dir, r, &key, &nbr);
+    cnt[mix64((uint64_t)key) % (uint64_t)P]++;
+  }
+  for (int q = 0; q < P; ++q) {
+    A->part[t * P + q] = (uint32_t*)malloc((cnt[q] ? cnt[q] : 1) * sizeof(uint32_t));
+    A->part_n[t * P + q] = 0;
+  }
+  for (uint64_t r = lo; r < hi; ++r) {
+    int64_t key, nbr;
+    record(A->src, A->dst, A->dir, r, &key, &nbr);
+    const int q = (int)(mix64((uint64_t)key) % (uint64_t)P);
+    A->part[t * P + q][A->part_n[t * P + q]++] = (uint32_t)r;
+  }
+  free(cnt);
+  pthread_barrier_wait(A->bar);
+  uint64_t mine = 0;
+  for (int q = 0; q < P; ++q) mine += A->part_n[q * P + t];
+  vmap m;
+  if (vmap_init(&m, mine + 1) != 0) { A->err = 1; return NULL; }
+  uint64_t* acc = (uint64_t*)malloc((mine + 1) * sizeof(uint64_t));
+  int64_t* acc2 = A->mode == MT_DEGMAX ? (int64_t*)malloc((mine + 1) * sizeof(int64_t)) : NULL;
+  for (int q = 0; q < P; ++q) {          /* producers in order: arrival order per key */
+    const uint32_t* lst = A->part[q * P + t];
+    for (uint64_t j = 0; j < A->part_n[q * P + t]; ++j) {
+      int64_t key, nbr;
+      const uint64_t i = record(A->src, A->dst, A->dir, lst[j], &key, &nbr);
+      int is_new;
+      const int64_t s = vmap_get(&m, key, &is_new);
+      if (A->mode == MT_DEGMAX) {
+        if (is_new) { acc[s] = 0; acc2[s] = A->init_max; }
+        acc[s] += 1;
+        if (nbr > acc2[s]) acc2[s] = nbr;
+      } else if (A->op == OP_COUNT) {
+        if (is_new) acc[s] = A->mode == MT_FOLD ? A->init_bits : 0;
+        acc[s] += 1;
+      } else if (is_new && A->mode == MT_REDUCE) {
+        acc[s] = load_val(A->dtype, A->val, i);
+      } else {
+        if (is_new) acc[s] = A->init_bits;
+        apply_op(A->op, A->dtype, &acc[s], A->val, i);
+      }
+    }
+  }
+  kv* srt = sorted_slots(&m);
+  A->U = m.size;
+  A->keys = (int64_t*)malloc((m.size + 1) * sizeof(int64_t));
+  A->a = (uint64_t*)malloc((m.size + 1) * sizeof(uint64_t));
+  A->b = acc2 ? (int64_t*)malloc((m.size + 1) * sizeof(int64_t)) : NULL;
+  for (uint64_t j = 0; j < m.size; ++j) {
+    A->keys[j] = srt[j].k;
+    A->a[j] = acc[srt[j].s];
+    if (acc2) A->b[j] = acc2[srt[j].s];
+  }
+  free(srt); free(acc); free(acc2); vmap_free(&m);
+  return NULL;
+}
+
+/* mode MT_REDUCE (reduceOnEdges), MT_FOLD (foldNeighbors from *init), MT_DEGMAX (degree / max
+ * neighbour from init_max; out_b = maxima).  Returns U, -1 - U when cap is short, -2 on failure. */
+GSO_API int64_t gso_window_fold_mt(const int64_t* src, const int64_t* dst, const void* val, uint64_t n, int dtype,
+                                   int dir, int op, int mode, const void* init, int64_t init_max, int threads,
+                                   int64_t* out_keys, void* out_a, int64_t* out_b, uint64_t cap) {
+  const int P = threads < 1 ? 1 : threads;
+  uint64_t init_bits = 0;
+  if (mode == MT_FOLD) init_bits = (op == OP_COUNT) ? (uint64_t)*(const int64_t*)init : load_val(dtype, init, 0);
+  pthread_t* th = (pthread_t*)malloc((size_t)P * sizeof(pthread_t));
+  mt_arg* args = (mt_arg*)calloc((size_t)P, sizeof(mt_arg));
+  uint32_t** part = (uint32_t**)calloc((size_t)P * P, sizeof(uint32_t*));
+  uint64_t* part_n = (uint64_t*)calloc((size_t)P * P, sizeof(uint64_t));
+  pthread_barrier_t bar;
+  pthread_barrier_init(&bar, NULL, (unsigned)P);
+  for (int t = 0; t < P; ++t) {
+    args[t] = (mt_arg){src, dst, val, n, dtype, dir, op, mode, P, t, init_bits, init_max, part, part_n,
+                       NULL, NULL, NULL, 0, 0, &bar};
+    pthread_create(&th[t], NULL, mt_worker, &args[t]);
+  }
+  uint64_t U = 0;
+  int err = 0;
+  for (int t = 0; t < P; ++t) { pthread_join(th[t], NULL); U += args[t].U; err |= args[t].err; }
+  pthread_barrier_destroy(&bar);
+  for (int i = 0; i < P * P; ++i) free(part[i]);
+  int64_t ret = err ? -2 : (U <= cap ? (int64_t)U : -1 - (int64_t)U);
+  if (!err && U <= cap) {   /* P-way merge of the consumers' ascending outputs */
+    uint64_t* at = (uint64_t*)calloc((size_t)P, sizeof(uint64_t));
+    const int odt = (mode == MT_DEGMAX || op == OP_COUNT) ? DT_I64 : dtype;
+    for (uint64_t o = 0; o < U; ++o) {
+      int best = -1;
+      for (int t = 0; t < P; ++t)
+        if (at[t] < args[t].U && (best < 0 || args[t].keys[at[t]] < args[best].keys[at[best]])) best = t;
+      const uint64_t j = at[best]++;
+      out_keys[o] = args[best].keys[j];
+      store_val(odt, out_a, o, args[best].a[j]);
+      if (mode == MT_DEGMAX) out_b[o] = args[best].b[j];
+    }
+    free(at);
+  }
+  for (int t = 0; t < P; ++t) { free(args[t].keys); free(args[t].a); free(args[t].b); }
+  free(part); free(part_n); free(args); free(th);
+  return ret;
+}
+
+/* ------------------------------------------------------------------------------------ */
+/* Forward-algorithm triangle count, multi-threaded: an independent check of the engine's  */
+/* count at R-MAT scale 20-22 (the reference's candidate rule cannot run there).  Counts  */
+/* T, the triangles of the window's simple undirected graph (multi-edges deduplicated as  */
+/* the HashSet of WindowTriangles.java:101 does).  Self-loop-free windows only: returns -1 */
+/* when the window has a self-loop (its self-pair term: gso_window_triangles_fwd).         */
+/* IDs are arbitrary Longs (compacted by sort + unique).                                  */
+/* ------------------------------------------------------------------------------------ */
+static void radix_u64(uint64_t* a, uint64_t* tmp, uint64_t n, int bits) {
+  /* LSD radix sort of the low `bits` bits, 16-bit digits */
+  uint64_t* cnt = (uint64_t*)malloc(65536 * sizeof(uint64_t));
+  for (int sh = 0; sh < bits; sh += 16) {
+    memset(cnt, 0, 65536 * sizeof(uint64_t));
+    for (uint64_t i = 0; i < n; ++i) cnt[(a[i] >> sh) & 0xFFFF]++;
+    uint64_t run = 0;
+    for (int d = 0; d < 65536; ++d) { const uint64_t c = cnt[d]; cnt[d] = run; run += c; }
+    for (uint64_t i = 0; i < n; ++i) tmp[cnt[(a[i] >> sh) & 0xFFFF]++] = a[i];
+    uint64_t* x = a; a = tmp; tmp = x;
+    if (((bits + 15) / 16) % 2 == 1 && sh + 16 >= bits) memcpy(tmp, a, n * sizeof(uint64_t));
+  }
+  free(cnt);
+}
+
+typedef struct {
+  const int64_t* ids; uint64_t V;        /* sorted distinct IDs (compaction) */
+  const int64_t* in; uint32_t* out; uint64_t lo, hi;
+  const uint64_t* off; const uint32_t* nbr; /* oriented out-lists */
+  volatile uint64_t* next; uint64_t T;
+} tri_arg;
+
+static void* tri_map_worker(void* p) {   /* endpoint -> compact ID by binary search */
+  tri_arg* A = (tri_arg*)p;
+  for (uint64_t i = A->lo; i < A->hi; ++i) {
+    uint64_t lo = 0, hi = A->V - 1;
+    while (lo < hi) {
+      const uint64_t mid = (lo + hi) >> 1;
+      if (A->ids[mid] < A->in[i]) lo = mid + 1;
+      else hi = mid;
+    }
+    A->out[i] = (uint32_t)lo;
+  }
+  return NULL;
+}
+
+static void* tri_count_worker(void* p) {
+  tri_arg* A = (tri_arg*)p;
+  uint64_t T = 0;
+  for (;;) {
+    const uint64_t x0 = __sync_fetch_and_add(A->next, 256);
+    if (x0 >= A->V) break;
+    const uint64_t x1 = x0 + 256 < A->V ? x0 + 256 : A->V;
+    for (uint64_t x = x0; x < x1; ++x)
+      for (uint64_t p = A->off[x]; p < A->off[x + 1]; ++p) {
+        const uint32_t y = A->nbr[p];
+        uint64_t i = A->off[x], j = A->off[y];
+        while (i < A->off[x + 1] && j < A->off[y + 1]) {
+          if (A->nbr[i] < A->nbr[j]) ++i;
+          else if (A->nbr[i] > A->nbr[j]) ++j;
+          else { ++T; ++i; ++j; }
+        }
+      }
+  }
+  A->T = T;
+  return NULL;
+}
+
+GSO_API int gso_triangles_fwd_mt(const int64_t* src, const int64_t* dst, uint64_t n, int threads, uint64_t* T_out) {
+  const int P = threads < 1 ? 1 : threads;
+  *T_out = 0;
+  if (n == 0) return 0;
+  for (uint64_t i = 0; i < n; ++i)
+    if (src[i] == dst[i]) return -1;
+  /* 1. compact IDs: sort + unique of all endpoints (sign-flipped so the order is signed) */
+  uint64_t* e = (uint64_t*)malloc(2 * n * sizeof(uint64_t));
+  uint64_t* tmp = (uint64_t*)malloc(2 * n * sizeof(uint64_t));
+  for (uint64_t i = 0; i < n; ++i) {
+    e[2 * i] = (uint64_t)src[i] ^ (1ull << 63);
+    e[2 * i + 1] = (uint64_t)dst[i] ^ (1ull << 63);
+  }
+  radix_u64(e, tmp, 2 * n, 64);
+  uint64_t V = 0;
+  for (uint64_t i = 0; i < 2 * n; ++i)
+    if (i == 0 || e[i] != e[i - 1]) e[V++] = e[i];
+  int64_t* ids = (int64_t*)malloc(V * sizeof(int64_t));
+  for (uint64_t i = 0; i < V; ++i) ids[i] = (int64_t)(e[i] ^ (1ull << 63));
+  uint32_t* cs = (uint32_t*)malloc(n * sizeof(uint32_t));
+  uint32_t* cd = (uint32_t*)malloc(n * sizeof(uint32_t));
+  pthread_t* th = (pthread_t*)malloc((size_t)P * sizeof(pthread_t));
+  tri_arg* args = (tri_arg*)calloc((size_t)P, sizeof(tri_arg));
+  for (int side = 0; side < 2; ++side) {
+    for (int t = 0; t < P; ++t) {
+      args[t] = (tri_arg){ids, V, side ? dst : src, side ? cd : cs, n * (uint64_t)t / P, n * (uint64_t)(t + 1) / P,
+                          NULL, NULL, NULL, 0};
+      pthread_create(&th[t], NULL, tri_map_worker, &args[t]);
+    }
+    for (int t = 0; t < P; ++t) pthread_join(th[t], NULL);
+  }
+  /* 2. distinct undirected edges (min << 32 | max), degrees */
+  for (uint64_t i = 0; i < n; ++i) {
+    const uint64_t a = cs[i] < cd[i] ? cs[i] : cd[i], b = cs[i] < cd[i] ? cd[i] : cs[i];
+    e[i] = (a << 32) | b;
+  }
+  radix_u64(e, tmp, n, 64);
+  uint64_t m = 0;
+  for (uint64_t i = 0; i < n; ++i)
+    if (i == 0 || e[i] != e[i - 1]) e[m++] = e[i];
+  uint32_t* deg = (uint32_t*)calloc(V, sizeof(uint32_t));
+  for (uint64_t i = 0; i < m; ++i) { deg[e[i] >> 32]++; deg[(uint32_t)e[i]]++; }
+  /* 3. orientation x -> y iff (deg x, x) < (deg y, y); out-lists come out sorted (see below) */
+  uint64_t* off = (uint64_t*)calloc(V + 1, sizeof(uint64_t));
+#define TRI_FWD(a, b) (deg[a] < deg[b] || (deg[a] == deg[b] && (a) < (b)))
+  for (uint64_t i = 0; i < m; ++i) {
+    const uint32_t a = (uint32_t)(e[i] >> 32), b = (uint32_t)e[i];
+    off[(TRI_FWD(a, b) ? a : b) + 1]++;
+  }
+  for (uint64_t x = 0; x < V; ++x) off[x + 1] += off[x];
+  uint64_t* fill = (uint64_t*)malloc((V + 1) * sizeof(uint64_t));
+  memcpy(fill, off, (V + 1) * sizeof(uint64_t));
+  uint32_t* nbr = (uint32_t*)malloc((m + 1) * sizeof(uint32_t));
+  /* edges ascend by (a, b), a < b: first the partners below x (x = b, a ascending), then the
+   * partners above x (x = a, b ascending) -> every out-list ascends */
+  for (uint64_t i = 0; i < m; ++i) {
+    const uint32_t a = (uint32_t)(e[i] >> 32), b = (uint32_t)e[i];
+    if (!TRI_FWD(a, b)) nbr[fill[b]++] = a;
+  }
+  for (uint64_t i = 0; i < m; ++i) {
+    const uint32_t a = (uint32_t)(e[i] >> 32), b = (uint32_t)e[i];
+    if (TRI_FWD(a, b)) nbr[fill[a]++] = b;
+  }
+#undef TRI_FWD
+  /* 4. T = sum over oriented x -> y of |N+(x) ∩ N+(y)| */
+  volatile uint64_t next = 0;
+  for (int t = 0; t < P; ++t) {
+    args[t] = (tri_arg){NULL, V, NULL, NULL, 0, 0, off, nbr, &next, 0};
+    pthread_create(&th[t], NULL, tri_count_worker, &args[t]);
+  }
+  uint64_t T = 0;
+  for (int t = 0; t < P; ++t) { pthread_join(th[t], NULL); T += args[t].T; }
+  *T_out = T;
+  free(e); free(tmp); free(ids); free(cs); free(cd); free(th); free(args); free(deg); free(off); free(fill); free(nbr);
+  return 0;
 }

@@ -54,6 +54,10 @@ def lib():
             "gso_java_hashset_cap": (u64, [u64]),
             "gso_parse_edges_text": (i64, [ctypes.c_char_p, u64, P, P, P, u64]),
             "gso_java_long_bucket": (u32, [i64, u64]),
+            "gso_zipf_cdf": (None, [u64, ctypes.c_double, P]),
+            "gso_gen_zipf": (i32, [u64, ctypes.c_double, u64, u64, u64, P, P]),
+            "gso_window_fold_mt": (i64, [P, P, P, u64, i32, i32, i32, i32, P, i64, i32, P, P, P, u64]),
+            "gso_triangles_fwd_mt": (i32, [P, P, u64, i32, ctypes.POINTER(u64)]),
         }
         for name, (res, args) in sig.items():
             f = getattr(L, name)
@@ -95,6 +99,20 @@ def gen_values(n, seed, dtype=DT_I64, first_edge=0):
     v = np.empty(n, NP_OF_DT[dtype])
     lib().gso_gen_values(n, seed, first_edge, dtype, _p(v))
     return v
+
+
+def gen_zipf(num_vertices, n, seed, exponent=1.1, first_edge=0):
+    """Zipf(exponent) sources over [0, num_vertices) (hubs at the lowest IDs), uniform destinations."""
+    src = np.empty(n, np.int64)
+    dst = np.empty(n, np.int64)
+    assert lib().gso_gen_zipf(num_vertices, exponent, n, seed, first_edge, _p(src), _p(dst)) == 0
+    return src, dst
+
+
+def zipf_cdf(num_vertices, exponent=1.1):
+    cdf = np.empty(num_vertices, np.uint64)
+    lib().gso_zipf_cdf(num_vertices, exponent, _p(cdf))
+    return cdf
 
 
 # ---- window operators ----------------------------------------------------------------------
@@ -218,6 +236,50 @@ def window_triangles_fwd(src, dst):
     ex, has = ctypes.c_uint64(0), ctypes.c_int(0)
     w = lib().gso_window_triangles_fwd(_p(src), _p(dst), len(src), ctypes.byref(ex), ctypes.byref(has))
     return int(w), int(ex.value), bool(has.value)
+
+
+def default_threads():
+    """worker threads for the large-window restatements: this host's CPUs, at most 16 (the GPU box's
+    CPU share per GPU)"""
+    return max(1, min(16, os.cpu_count() or 1))
+
+
+def window_reduce_mt(src, dst, val, direction, op, threads=None, init=None):
+    """gso_window_fold_mt: the same results as window_reduce (init None) / window_fold, over threads
+    (keyBy-style routing keeps every key's arrival order)."""
+    src, dst = _i64(src), _i64(dst)
+    val = np.ascontiguousarray(val)
+    dt = DT_OF_NP[val.dtype]
+    cap = _nrec(len(src), direction) + 1
+    keys = np.empty(cap, np.int64)
+    odt = np.int64 if op == OP_COUNT else val.dtype
+    out = np.empty(cap, odt)
+    mode, ia = (0, None) if init is None else (1, np.array([init], dtype=odt))
+    u = lib().gso_window_fold_mt(_p(src), _p(dst), _p(val), len(src), dt, direction, op, mode, _p(ia), 0,
+                                 threads or default_threads(), _p(keys), _p(out), None, cap)
+    assert u >= 0, u
+    return keys[:u], out[:u]
+
+
+def window_fold_degree_max_mt(src, dst, direction, init_max=np.iinfo(np.int64).min, threads=None):
+    src, dst = _i64(src), _i64(dst)
+    cap = _nrec(len(src), direction) + 1
+    keys, deg, mx = (np.empty(cap, np.int64) for _ in range(3))
+    dummy = np.zeros(1, np.int64)
+    u = lib().gso_window_fold_mt(_p(src), _p(dst), _p(dummy), len(src), DT_I64, direction, OP_COUNT, 2, None,
+                                 int(init_max), threads or default_threads(), _p(keys), _p(deg), _p(mx), cap)
+    assert u >= 0, u
+    return keys[:u], deg[:u], mx[:u]
+
+
+def triangles_fwd_mt(src, dst, threads=None):
+    """Exact triangle count of a self-loop-free window (forward algorithm over compacted IDs)."""
+    src, dst = _i64(src), _i64(dst)
+    t = ctypes.c_uint64(0)
+    rc = lib().gso_triangles_fwd_mt(_p(src), _p(dst), len(src), threads or default_threads(), ctypes.byref(t))
+    if rc != 0:
+        raise ValueError("triangles_fwd_mt: the window has a self-loop")
+    return int(t.value)
 
 
 def baseline_reduce(src, dst, val, direction, op, threads):

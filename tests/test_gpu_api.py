@@ -354,3 +354,17 @@ def test_text_to_window_reduce(engine, oracle):
     os_, od, ov = oracle.parse_edges_text(text)
     wk, wv = oracle.window_reduce(os_, od, ov, 1, 0)
     assert np.array_equal(k.cpu().numpy(), wk) and np.array_equal(r.cpu().numpy(), wv)
+
+
+def test_triangle_table_overflow_is_an_error_not_a_hang(pkg, oracle):
+    """Every LDS hash-set insert / probe chain is bounded: with GS_FLAG_TEST_TINY_TABLES (one-bucket
+    sets) the sets overflow, the kernels give up and the call returns GS_EDEVICE instead of hanging."""
+    from gelly_streaming_amd import _lib as L
+    s, d = oracle.gen_rmat(14, 200_000, 0x5EED04, no_self_loops=True)
+    S, D = (torch.from_numpy(x).cuda() for x in (s, d))
+    with pkg.Engine(0, flags=L.GS_FLAG_TEST_TINY_TABLES) as e:
+        with pytest.raises(pkg.GsError) as ei:
+            e.triangles(S, D)
+        assert ei.value.status == L.GS_EDEVICE and "hash set" in str(ei.value)
+    with pkg.Engine(0) as e:   # the normal engine on the same window
+        assert e.triangles(S, D)[0] == oracle.window_triangles_fwd(s, d)[1]

@@ -221,3 +221,55 @@ def test_degree_max_far_neighbours(engine, oracle, direction):
         gk, gd, gm = engine.fold_degree_max(*_dev(s, d), direction, init_max)
         assert np.array_equal(gk.cpu().numpy(), rk)
         assert np.array_equal(gd.cpu().numpy(), rd) and np.array_equal(gm.cpu().numpy(), rm)
+
+
+VALUE_MIXES = {
+    "narrow": lambda rng, n: rng.integers(0, 0xFFFF, n),                       # every value packs
+    "boundary": lambda rng, n: rng.choice([0, 1, 0xFFFE, 0xFFFF, 0x10000, -1], n),   # escapes at 0xFFFF and up
+    "sparse_wide": lambda rng, n: np.where(rng.random(n) < 0.01, rng.integers(-(1 << 31), 1 << 31, n),
+                                           rng.integers(0, 0xFFFF, n)),
+    "all_wide": lambda rng, n: rng.integers(-(1 << 30), -1, n),                 # every value escapes
+}
+
+
+@pytest.mark.parametrize("dtype", [np.int64, np.int32])
+@pytest.mark.parametrize("op", [0, 1, 2])
+def test_packed_records_escapes(pkg, oracle, dtype, op):
+    """k_dp_scatter_pack: values in [0, 0xFFFF) travel in 16 bits, others escape (0xFFFF + the full value
+    beside the record).  Bit-exact against the oracle and against the unpacked scatter (GS_FLAG_NO_PACK),
+    for every mix of values; after a window where escapes are common the engine stores 8-byte values."""
+    rng = np.random.default_rng(1000 + op)
+    n = 200_003
+    s, d = _window(rng, n, 1 << 22, hub_frac=0.02)
+    with pkg.Engine(0) as ep, pkg.Engine(0, no_pack=True) as eu:
+        for w, mix in enumerate(("narrow", "sparse_wide", "boundary", "all_wide", "narrow")):
+            v = VALUE_MIXES[mix](rng, n).astype(dtype)
+            rk, rv = oracle.window_reduce(s, d, v, 1, op)
+            kp, vp = ep.reduce(*_dev(s, d, v), 1, op)
+            tp = ep.stage_times()
+            ku, vu = eu.reduce(*_dev(s, d, v), 1, op)
+            assert not eu.stage_times().packed
+            _check(kp, vp, rk, rv, dtype, op)
+            assert torch.equal(kp, ku) and torch.equal(vp, vu), mix
+            if mix == "narrow" and w == 0:
+                assert tp.packed and tp.escapes == 0
+            if mix == "sparse_wide":
+                assert tp.packed and 0 < tp.escapes < n // 8
+            if mix == "boundary":   # about half the values escape: the following windows store 8-byte values
+                assert tp.packed and tp.escapes > n // 8
+            if mix == "all_wide" or w == 4:
+                assert not tp.packed
+
+
+def test_packed_prediction_miss_reruns(pkg, oracle):
+    """No host round trip inside a window: a window whose IDs leave the predicted range is detected by
+    the histogram, every later launch exits, and the window reruns with the measured range."""
+    rng = np.random.default_rng(77)
+    with pkg.Engine(0) as e:
+        for span, off in ((1 << 20, 0), (1 << 23, 0), (1 << 20, 1 << 35), (1 << 16, -(1 << 50)), (1 << 24, 0)):
+            s, d = _window(rng, 123_457, span, off)
+            v = rng.integers(0, 0xFFFF, 123_457).astype(np.int64)
+            rk, rv = oracle.window_reduce(s, d, v, 1, 0)
+            gk, gv = e.reduce(*_dev(s, d, v), 1, 0)
+            assert e.stage_times().path == 2
+            _check(gk, gv, rk, rv, np.int64, 0)

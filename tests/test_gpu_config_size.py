@@ -1,0 +1,101 @@
+"""GPU parity at the BASELINE configs' own sizes, against the C oracle's large-window
+restatements (oracle/gs_oracle.c: gso_window_fold_mt — the arrival-order fold spread over threads the
+way keyBy spreads it over subtasks; gso_triangles_fwd_mt — an independent forward-algorithm count).
+
+  C2  R-MAT scale 24, E = 2^28, reduceOnEdges(SUM) OUT: Long values bit-exact, Double values within
+      1e-5 relative (north star), both on two distinct windows of the stream
+  C3  skewed R-MAT scale 24 (.65/.15/.15/.05, no permutation) and the Zipf(1.1) source stream, E = 2^28:
+      foldNeighbors(degree, max neighbour) bit-exact
+  C4  WindowTriangles on self-loop-free R-MAT windows at scales 20 and 22: the exact count equals the
+      forward algorithm's (and the reference's Integer is its low 32 bits)
+
+The windows are generated on the device (gs_generate_*, bit-identical to the oracle's generators:
+test_gpu_parity.test_generators_match_oracle, and re-checked here on a sample of each window)."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+FLOAT_RTOL = 1e-5  # north_star: float weight sums within 1e-5 relative
+
+
+def _sample_matches_oracle(oracle, src, dst, gen, first_edge, k=4096):
+    """Spot-check a device window against the oracle generator at three offsets."""
+    n = src.numel()
+    for off in (0, n // 2, n - k):
+        s, d = gen(k, first_edge + off)
+        assert np.array_equal(src[off:off + k].cpu().numpy(), s) and np.array_equal(dst[off:off + k].cpu().numpy(), d)
+
+
+@pytest.mark.parametrize("window", [0, 1])
+def test_c2_full_window_long_bit_exact(engine, oracle, window):
+    scale, E, seed = 24, 1 << 28, 0x5EED02
+    fe = window * E
+    src, dst = engine.generate_rmat(scale, E, seed, first_edge=fe)
+    val = engine.generate_values(E, seed, 1, first_edge=fe)
+    _sample_matches_oracle(oracle, src, dst, lambda k, f: oracle.gen_rmat(scale, k, seed, first_edge=f), fe)
+    gk, gv = engine.reduce(src, dst, val, 1, 0)
+    t = engine.stage_times()
+    assert t.path == 2
+    s_h, d_h, v_h = src.cpu().numpy(), dst.cpu().numpy(), val.cpu().numpy()
+    del src, dst
+    rk, rv = oracle.window_reduce_mt(s_h, d_h, v_h, 1, 0)
+    assert np.array_equal(gk.cpu().numpy(), rk), "vertex keys differ from the oracle"
+    assert np.array_equal(gv.cpu().numpy(), rv), "per-vertex Long sums differ from the oracle"
+
+
+def test_c2_full_window_double_within_tolerance(engine, oracle):
+    scale, E, seed = 24, 1 << 28, 0x5EED02
+    src, dst = engine.generate_rmat(scale, E, seed)
+    val = engine.generate_values(E, seed, 3)
+    gk, gv = engine.reduce(src, dst, val, 1, 0)
+    s_h, d_h, v_h = src.cpu().numpy(), dst.cpu().numpy(), val.cpu().numpy()
+    del src, dst, val
+    rk, rv = oracle.window_reduce_mt(s_h, d_h, v_h, 1, 0)
+    assert np.array_equal(gk.cpu().numpy(), rk)
+    g = gv.cpu().numpy()
+    bad = np.abs(g - rv) > FLOAT_RTOL * np.maximum(np.abs(rv), 1e-30)
+    assert not bad.any(), f"{int(bad.sum())} Double sums outside 1e-5 relative"
+
+
+@pytest.mark.parametrize("stream", ["rmat", "zipf"])
+def test_c3_full_window_degree_max(engine, oracle, stream):
+    scale, E, seed = 24, 1 << 28, 0x5EED03
+    if stream == "rmat":
+        src, dst = engine.generate_rmat(scale, E, seed, a=0.65, b=0.15, c=0.15, permute=False)
+        gen = lambda k, f: oracle.gen_rmat(scale, k, seed, a=0.65, b=0.15, c=0.15, permute=False, first_edge=f)
+    else:
+        src, dst = engine.generate_zipf(1 << scale, E, seed, 1.1)
+        gen = lambda k, f: oracle.gen_zipf(1 << scale, k, seed, 1.1, first_edge=f)
+    _sample_matches_oracle(oracle, src, dst, gen, 0)
+    gk, gd, gm = engine.fold_degree_max(src, dst, 1)
+    s_h, d_h = src.cpu().numpy(), dst.cpu().numpy()
+    del src, dst
+    rk, rd, rm = oracle.window_fold_degree_max_mt(s_h, d_h, 1)
+    assert np.array_equal(gk.cpu().numpy(), rk)
+    assert np.array_equal(gd.cpu().numpy(), rd), "degrees differ"
+    assert np.array_equal(gm.cpu().numpy(), rm), "max neighbours differ"
+    assert int(rd.max()) > 1 << 20, "the skewed stream should have a hub"
+
+
+@pytest.mark.parametrize("scale", [20, 22])
+def test_c4_shape_triangles_vs_forward_algorithm(engine, oracle, scale):
+    E, seed = 16 << scale, 0x5EED04
+    src, dst = engine.generate_rmat(scale, E, seed, no_self_loops=True)
+    exact, wrapped, has = engine.triangles(src, dst)
+    want = oracle.triangles_fwd_mt(src.cpu().numpy(), dst.cpu().numpy())
+    assert exact == want, (exact, want)
+    w = want & 0xFFFFFFFF
+    assert wrapped == (w - (1 << 32) if w >= 1 << 31 else w) and has
+
+
+def test_zipf_generator_matches_oracle(engine, oracle):
+    n = 1 << 18
+    for V, s, f in ((1 << 24, 1.1, 0), (1 << 10, 2.0, 77), (12345, 0.8, 1 << 30)):
+        gs_, gd_ = engine.generate_zipf(V, n, 0x5EED03, s, first_edge=f)
+        os_, od_ = oracle.gen_zipf(V, n, 0x5EED03, s, first_edge=f)
+        assert np.array_equal(gs_.cpu().numpy(), os_) and np.array_equal(gd_.cpu().numpy(), od_)
+    # hubs at the lowest IDs: ID 0 is the most frequent source
+    c = np.bincount(os_)
+    assert c.argmax() == 0

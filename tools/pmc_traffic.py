@@ -13,7 +13,8 @@ import re
 from collections import defaultdict
 from pathlib import Path
 
-NAMES = {"k_dp_scatter": "dp_scatter", "k_bk_accum": "bucket_accumulate", "k_dp_hist": "dp_hist(+host sync)",
+NAMES = {"k_dp_scatter": "dp_scatter", "k_dp_scatter_pack": "dp_scatter_pack", "k_bk_accum": "bucket_accumulate",
+         "k_dp_hist": "dp_hist",
          "k_bk_merge": "bucket_merge", "k_bk_emit": "bucket_emit"}
 
 
