@@ -45,6 +45,7 @@ def parse():
     p.add_argument("--windows", type=int, default=2, help="distinct windows of the stream the timed steps cycle through")
     p.add_argument("--stream", default="rmat", choices=["rmat", "zipf"],
                    help="fold (C3): skewed R-MAT (default) or the Zipf(1.1) source stream")
+    p.add_argument("--staging", default="direct", choices=["direct", "pinned"], help="e2e: window operator staging")
     p.add_argument("--no-pack", action="store_true",
                    help="ablation: integer SUM keeps 8-byte partitioned values instead of 4-byte packed records")
     p.add_argument("--sort-only", action="store_true",
@@ -55,7 +56,8 @@ def parse():
                    help="after timing: sum(per-vertex sums) == sum(values) and ascending keys on each window")
     p.add_argument("--windows-edges", type=float, default=1e8,
                    help="apply (C5): edges per 1000 ms window of the continuous stream")
-    p.add_argument("--workload", default="reduce", choices=["reduce", "fold", "triangles", "c1", "apply", "candidates", "parse"],
+    p.add_argument("--workload", default="reduce",
+                   choices=["reduce", "fold", "triangles", "c1", "apply", "candidates", "parse", "e2e"],
                    help="reduce = C2 (default, the headline); fold = C3 degree/max on skewed R-MAT; "
                         "triangles = WindowTriangles on an R-MAT window without self-loops (C4 shape)")
     return p.parse_args()
@@ -391,8 +393,83 @@ def parse_main(a):
     eng.close()
 
 
+def e2e_main(a):
+    """End-to-end windows (BASELINE.md "end-to-end incl. pinned H2D/D2H"): the C2 stream
+    (R-MAT scale-24 windows of 2^28 edges, Long values) arrives on the HOST with ascending event timestamps
+    (window k: ts in [k*1000, k*1000 + 1000)) and goes through the window-buffer operator (gs_stream_*):
+    host columns -> pinned window buffers -> the watermark fires the window -> H2D on the operator's copy
+    stream (overlapping the previous window's kernels) -> reduceOnEdges(SUM) -> D2H of the per-vertex
+    results.  value = edges / wall time over the timed windows; latency = window fire -> result on the
+    host.  Not the headline: the headline keeps the window resident in HBM."""
+    torch.cuda.set_device(0)
+    pkg = ge.load_package()
+    from gelly_streaming_amd import _lib as L
+    from gelly_streaming_amd.window_operator import WindowOperator
+    eng = pkg.Engine(0)
+    E = a.edge_factor << a.scale
+    ndist = 2                       # distinct host windows, cycled
+    host = []
+    for w in range(ndist):
+        s_, d_ = eng.generate_rmat(a.scale, E, a.seed, first_edge=w * E)
+        v_ = eng.generate_values(E, a.seed, 1, first_edge=w * E)
+        host.append((s_.cpu().numpy(), d_.cpu().numpy(), v_.cpu().numpy()))
+        del s_, d_, v_
+    torch.cuda.empty_cache()
+    ts0 = (np.arange(E, dtype=np.int64) * 1000) // E
+    total = a.warmup + a.steps
+    tss = [ts0 + k * 1000 for k in range(total)]   # window k's event times (prepared before timing)
+    lat, results = [], []
+    staging = L.GS_STAGE_DIRECT if a.staging == "direct" else L.GS_STAGE_PINNED
+    op = WindowOperator(eng, 1000, L.GS_STREAM_REDUCE, 1, 0, np.int64, L.GS_WATERMARK_ASCENDING, max_window_edges=E,
+                        staging=staging)
+    t0 = None
+    for k in range(total + 1):
+        if k == a.warmup:
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+        if k < total:
+            src, dst, val = host[k % ndist]
+            op.append(src, dst, val, tss[k])   # fires window k-1 (watermark = max ts - 1)
+        else:
+            op.flush()
+        while (r := op.poll(wait=(k == total))) is not None:
+            results.append(r)
+            if r.start >= a.warmup * 1000:
+                lat.append(r.latency_ms)
+            if k < total:
+                break
+    results += op.drain()
+    elapsed = time.perf_counter() - t0
+    timed = [r for r in results if r.start >= a.warmup * 1000]
+    assert len(timed) == a.steps and all(r.edges == E for r in timed)
+    lat = [r.latency_ms for r in timed]
+    if a.check:
+        for r in timed[:2]:
+            v = host[(r.start // 1000) % ndist][2]
+            assert int(r.columns[1].sum()) == int(v.sum()), "e2e window: sum of sums != sum of values"
+    op.close()
+    ms = elapsed / a.steps * 1e3
+    h2d_bytes = 24 * E
+    print(json.dumps({
+        "metric": METRIC, "value": E * a.steps / elapsed, "unit": "edges/s", "n_gpus": 1, "steps": a.steps,
+        "warmup": a.warmup, "ms_per_step": ms, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "dtype": "int64", "data": "synthetic R-MAT scale-24 windows generated on device, copied to host memory "
+                                  "before timing; ascending event timestamps",
+        "config": {"workload": f"end-to-end C2: host records -> gs_stream window operator ({a.staging} staging: "
+                               + ("pinned window buffers, H2D at firing" if a.staging == "pinned" else
+                                  "each append copied straight to HBM") + ", reduceOnEdges(SUM) OUT, D2H of results)",
+                   "edges_per_window": E, "windows_timed": a.steps,
+                   "latency_ms_p50": float(np.percentile(lat, 50)), "latency_ms_p99": float(np.percentile(lat, 99)),
+                   "h2d_bytes_per_window": h2d_bytes, "h2d_GBps_effective": h2d_bytes / (ms * 1e-3) / 1e9,
+                   "vertices_out_per_window": int(timed[-1].columns[0].size), "parallelism": "1 GPU"},
+        "roofline": None, "cpu_baseline": None}), flush=True)
+    eng.close()
+
+
 def main():
     a = parse()
+    if a.workload == "e2e":
+        return e2e_main(a)
     if a.workload in ("c1", "apply", "candidates"):
         return window_stream_main(a)
     if a.workload == "parse":
@@ -446,6 +523,20 @@ def main():
             local_times.append(eng.stage_times())
         return r
 
+    P_red, M_red, P_fold, M_fold = D.engine_halves(eng)
+
+    def partials_timed(*args):   # the window's own pipeline runs inside the partials half
+        r = P_red(*args)
+        if not local_times:
+            local_times.append(eng.stage_times())
+        return r
+
+    def fold_partials_timed(*args):
+        r = P_fold(*args)
+        if not local_times:
+            local_times.append(eng.stage_times())
+        return r
+
     def part_count(s_, d_, part, nparts):
         r = eng.triangles_part(s_, d_, part, nparts)
         local_times.append(eng.stage_times())
@@ -462,10 +553,10 @@ def main():
             z = torch.zeros(1, dtype=torch.int64, device=src.device)
             return z + tot, z, local_times[0]
         if a.workload == "fold":
-            r = D.fold_degree_max_window(local_fold, local_reduce, src, dst, 1, -(1 << 63)) if dist \
+            r = D.fold_degree_max_window(fold_partials_timed, M_fold, src, dst, 1, -(1 << 63)) if dist \
                 else local_fold(src, dst, 1, -(1 << 63))
             return r[0], r[1], local_times[0]
-        r = D.reduce_window(local_reduce, src, dst, val, 1, 0) if dist else local_reduce(src, dst, val, 1, 0)
+        r = D.reduce_window(partials_timed, M_red, src, dst, val, 1, 0) if dist else local_reduce(src, dst, val, 1, 0)
         return r[0], r[1], local_times[0]
 
     for i in range(a.warmup):
@@ -573,8 +664,8 @@ def main():
                        "key_bits": t0s.key_bits, "partials_after_fused_pass": int(partials),
                        "pipeline": {0: "sort", 1: "bucket-onesweep", 2: "bucket-direct", 3: "triangles"}[t0s.path],
                        "packed_records": bool(t0s.packed), "escaped_values": int(t0s.escapes),
-                       "parallelism": (f"vertex-range keyBy over {world} GPU(s), RCCL all-to-all" if dist
-                                       else "1 GPU"), **checks},
+                       "parallelism": (f"hash keyBy over {world} GPU(s): per-rank partials (gs_window_reduce_partials) "
+                                       f"-> RCCL all-to-all -> gs_merge_partials" if dist else "1 GPU"), **checks},
             "roofline": roofline,
             "cpu_baseline": cpu,
             "kernels": {n: {"avg_ms": round(r["ms"], 4), "own_bytes": r["bytes"], "GB/s": round(r["GB/s"], 1),

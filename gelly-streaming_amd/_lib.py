@@ -16,12 +16,15 @@ PKG = Path(__file__).resolve().parent
 # GELLY_HIP_LIB selects a tuning build (csrc/Makefile `variant`); default is the in-tree library
 LIB_PATH = Path(os.environ.get("GELLY_HIP_LIB", PKG / "libgellyhip.so"))
 
-GS_OK, GS_EINVAL, GS_ECAPACITY, GS_EDEVICE, GS_ECOMM, GS_ENOMEM, GS_EUNSUPPORTED = 0, -1, -2, -3, -4, -5, -6
+GS_OK, GS_EINVAL, GS_ECAPACITY, GS_EDEVICE, GS_ECOMM, GS_ENOMEM, GS_EUNSUPPORTED, GS_EAGAIN = 0, -1, -2, -3, -4, -5, -6, -7
+GS_STREAM_REDUCE, GS_STREAM_FOLD, GS_STREAM_DEGREE_MAX, GS_STREAM_TRIANGLES = 0, 1, 2, 3
+GS_WATERMARK_EXPLICIT, GS_WATERMARK_ASCENDING = 0, 1
+GS_STAGE_PINNED, GS_STAGE_DIRECT = 0, 1
 GS_MEM_HOST, GS_MEM_DEVICE = 0, 1
 GS_I32, GS_I64, GS_F32, GS_F64, GS_NONE = 0, 1, 2, 3, 4
 GS_OP_SUM, GS_OP_MIN, GS_OP_MAX, GS_OP_COUNT = 0, 1, 2, 3
 STATUS_NAMES = {0: "GS_OK", -1: "GS_EINVAL", -2: "GS_ECAPACITY", -3: "GS_EDEVICE", -4: "GS_ECOMM",
-                -5: "GS_ENOMEM", -6: "GS_EUNSUPPORTED"}
+                -5: "GS_ENOMEM", -6: "GS_EUNSUPPORTED", -7: "GS_EAGAIN"}
 
 NP_DTYPE = {GS_I32: np.int32, GS_I64: np.int64, GS_F32: np.float32, GS_F64: np.float64}
 GS_DTYPE_OF = {np.dtype(np.int32): GS_I32, np.dtype(np.int64): GS_I64, np.dtype(np.float32): GS_F32,
@@ -32,7 +35,11 @@ EXPORTS = ("gs_abi_version", "gs_create", "gs_destroy", "gs_last_error", "gs_set
            "gs_alloc_pinned", "gs_free_pinned", "gs_window_reduce", "gs_window_fold",
            "gs_window_fold_degree_max", "gs_window_csr", "gs_window_candidates", "gs_window_triangles",
            "gs_window_triangles_part", "gs_window_count_candidates",
-           "gs_parse_edges_text", "gs_generate_rmat", "gs_generate_uniform", "gs_generate_zipf", "gs_generate_values", "gs_last_stage_times")
+           "gs_parse_edges_text", "gs_fetch_last_output", "gs_fetch_last_degree_output", "gs_owner_of", "gs_window_reduce_partials", "gs_window_fold_degree_max_partials",
+           "gs_merge_partials", "gs_merge_degree_max_partials", "gs_comm_unique_id", "gs_comm_init", "gs_comm_destroy",
+           "gs_comm_allreduce_sum_u64", "gs_window_reduce_dist", "gs_window_fold_degree_max_dist",
+           "gs_stream_create", "gs_stream_destroy", "gs_stream_append", "gs_stream_watermark", "gs_stream_flush",
+           "gs_stream_poll", "gs_stream_stats", "gs_generate_rmat", "gs_generate_uniform", "gs_generate_zipf", "gs_generate_values", "gs_last_stage_times")
 
 P = ctypes.c_void_p
 u64, i64, i32, u32 = ctypes.c_uint64, ctypes.c_int64, ctypes.c_int32, ctypes.c_uint32
@@ -76,6 +83,31 @@ class GsPairOut(ctypes.Structure):
 
 class GsPairBatch(ctypes.Structure):
     _fields_ = [("a", P), ("b", P), ("is_candidate", P), ("n", u64), ("mem", i32), ("reserved", i32)]
+
+
+class GsPartialsOut(ctypes.Structure):
+    _fields_ = [("keys", P), ("vals", P), ("vals2", P), ("capacity", u64), ("n_out", ctypes.POINTER(u64)),
+                ("owner_counts", ctypes.POINTER(u64)), ("mem", i32), ("reserved", i32)]
+
+
+class GsPartialBatch(ctypes.Structure):
+    _fields_ = [("keys", P), ("vals", P), ("vals2", P), ("n", u64), ("val_dtype", i32), ("mem", i32)]
+
+
+class GsStreamConfig(ctypes.Structure):
+    _fields_ = [("window_ms", i64), ("kind", i32), ("dir", i32), ("op", i32), ("val_dtype", i32),
+                ("watermark_mode", i32), ("staging", i32), ("init", P), ("init_max", i64), ("max_window_edges", u64)]
+
+
+class GsWindowResult(ctypes.Structure):
+    _fields_ = [("window_start", i64), ("window_end", i64), ("max_timestamp", i64), ("edges", u64),
+                ("n_vertices", u64), ("keys", P), ("vals", P), ("vals2", P), ("triangles", u64),
+                ("triangles_ref", i32), ("has_output", i32), ("latency_ms", ctypes.c_double)]
+
+
+class GsStreamStats(ctypes.Structure):
+    _fields_ = [("watermark", i64), ("open_windows", u64), ("fired_windows", u64), ("pending_windows", u64),
+                ("late_records", u64), ("edges_fired", u64)]
 
 
 class GsStageTimes(ctypes.Structure):
@@ -126,6 +158,27 @@ def load() -> ctypes.CDLL:
         "gs_window_count_candidates": (st, [P, ctypes.POINTER(GsPairBatch), ctypes.POINTER(u64), ctypes.POINTER(i32),
                                             ctypes.POINTER(i32), ctypes.POINTER(u64)]),
         "gs_parse_edges_text": (st, [P, P, u64, i32, P, P, P, u64, i32, ctypes.POINTER(u64), ctypes.POINTER(u64)]),
+        "gs_fetch_last_output": (st, [P, ctypes.POINTER(GsVertexOut)]),
+        "gs_fetch_last_degree_output": (st, [P, ctypes.POINTER(GsDegreeOut)]),
+        "gs_owner_of": (u32, [i64, u32]),
+        "gs_stream_create": (st, [P, ctypes.POINTER(GsStreamConfig), ctypes.POINTER(P)]),
+        "gs_stream_destroy": (None, [P]),
+        "gs_stream_append": (st, [P, P, P, P, P, u64]),
+        "gs_stream_watermark": (st, [P, i64]),
+        "gs_stream_flush": (st, [P]),
+        "gs_stream_poll": (st, [P, i32, ctypes.POINTER(GsWindowResult)]),
+        "gs_stream_stats": (st, [P, ctypes.POINTER(GsStreamStats)]),
+        "gs_window_reduce_partials": (st, [P, ctypes.POINTER(GsEdgeBatch), i32, i32, u32, ctypes.POINTER(GsPartialsOut)]),
+        "gs_window_fold_degree_max_partials": (st, [P, ctypes.POINTER(GsEdgeBatch), i32, u32,
+                                                    ctypes.POINTER(GsPartialsOut)]),
+        "gs_merge_partials": (st, [P, ctypes.POINTER(GsPartialBatch), i32, P, ctypes.POINTER(GsVertexOut)]),
+        "gs_merge_degree_max_partials": (st, [P, ctypes.POINTER(GsPartialBatch), i64, ctypes.POINTER(GsDegreeOut)]),
+        "gs_comm_unique_id": (st, [P]),
+        "gs_comm_init": (st, [P, i32, i32, P]),
+        "gs_comm_destroy": (st, [P]),
+        "gs_comm_allreduce_sum_u64": (st, [P, ctypes.POINTER(u64)]),
+        "gs_window_reduce_dist": (st, [P, ctypes.POINTER(GsEdgeBatch), i32, i32, P, ctypes.POINTER(GsVertexOut)]),
+        "gs_window_fold_degree_max_dist": (st, [P, ctypes.POINTER(GsEdgeBatch), i32, i64, ctypes.POINTER(GsDegreeOut)]),
         "gs_generate_rmat": (st, [P, i32, u64, u64, u32, u32, u32, i32, i32, u64, P, P]),
         "gs_generate_uniform": (st, [P, u64, u64, u64, u64, P, P]),
         "gs_generate_zipf": (st, [P, u64, ctypes.c_double, u64, u64, u64, P, P]),

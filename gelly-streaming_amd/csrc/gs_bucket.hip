@@ -68,7 +68,7 @@ gs_status launch_info(gs_ctx* c, const int64_t* src, const int64_t* dst, uint64_
   return hip_check(c, hipGetLastError(), "k_bk_info");
 }
 
-template <int DIR>
+template <int DIR, int ITEMS>
 gs_status launch_dp_hist(gs_ctx* c, const int64_t* src, const int64_t* dst, uint64_t n, uint32_t nt, int64_t base,
                          int S, uint32_t nbp) {
   char* sm = c->small.as<char>();
@@ -76,14 +76,14 @@ gs_status launch_dp_hist(gs_ctx* c, const int64_t* src, const int64_t* dst, uint
   GS_HIP(hipMemsetAsync(mm, 0, 32, c->stream));
   // VEC reads whole 16-byte pairs: every tile must hold one (only the last tile can be shorter)
   const bool vec = ((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst)) & 15) == 0 &&
-                   n % dp_tile_edges<DIR>() != 1;
+                   n % dp_tile_edges<DIR, ITEMS>() != 1;
   const unsigned grid = std::max<uint32_t>(1, std::min<uint32_t>(nt, (uint32_t)c->n_cu));
   uint16_t* cnt = c->dp_cnt.as<uint16_t>();
   if (vec)
-    hipLaunchKernelGGL((k_dp_hist<DIR, true>), dim3(grid), dim3(DP_BLOCK), 0, c->stream, src, dst, n, nt, base, S, nbp,
+    hipLaunchKernelGGL((k_dp_hist<DIR, true, ITEMS>), dim3(grid), dim3(DP_BLOCK), 0, c->stream, src, dst, n, nt, base, S, nbp,
                        cnt, mm);
   else
-    hipLaunchKernelGGL((k_dp_hist<DIR, false>), dim3(grid), dim3(DP_BLOCK), 0, c->stream, src, dst, n, nt, base, S,
+    hipLaunchKernelGGL((k_dp_hist<DIR, false, ITEMS>), dim3(grid), dim3(DP_BLOCK), 0, c->stream, src, dst, n, nt, base, S,
                        nbp, cnt, mm);
   return hip_check(c, hipGetLastError(), "k_dp_hist");
 }
@@ -252,9 +252,9 @@ gs_status ensure_stage(gs_ctx* c, uint64_t R) {
 // window of this ctx had more than 1/8 escapes; every other op through k_dp_scatter.
 // Events: ev[1] / pass_ev[0] after the histogram; pass_ev[0..2] around the offset scans and the
 // scatter; then accumulate / merge / emit.
-template <class P, int DIR>
-gs_status bucket_direct(gs_ctx* c, const int64_t* src, const int64_t* dst, const void* val, uint64_t n,
-                        typename P::Out o, uint64_t* U) {
+template <class P, int DIR, int ITEMS>
+gs_status bucket_direct_t(gs_ctx* c, const int64_t* src, const int64_t* dst, const void* val, uint64_t n,
+                          typename P::Out o, uint64_t* U, bool pack) {
   using Raw = typename P::Raw;
   constexpr int S = P::S;
   constexpr bool CAN_PACK = P::PAY == PAY_VAL && !P::REL && std::is_integral_v<typename P::A>;
@@ -263,14 +263,13 @@ gs_status bucket_direct(gs_ctx* c, const int64_t* src, const int64_t* dst, const
   GS_TRY(ensure(c, c->bk_meta, BkMeta::TOTAL * 4, true));
   GS_TRY(ensure_cu(c));
   uint32_t* meta = c->bk_meta.as<uint32_t>();
-  constexpr uint32_t TE = dp_tile_edges<DIR>();
+  constexpr uint32_t TE = dp_tile_edges<DIR, ITEMS>();
   const uint32_t nt = (uint32_t)((n + TE - 1) / TE);
   const uint32_t nch = (nt + DP_CHUNK - 1) / DP_CHUNK;
   GS_TRY(ensure(c, c->dp_cnt, (size_t)nt * BK_MAXB * 2));
   GS_TRY(ensure(c, c->dp_csum, (size_t)nch * BK_MAXB * 4));
   GS_TRY(ensure(c, c->dp_off, (size_t)nt * BK_MAXB * 4));
   GS_TRY(ensure_stage<P>(c, R));
-  const bool pack = CAN_PACK && c->bk_wide_vals <= 0 && !(c->flags & GS_FLAG_NO_PACK);
   int64_t base = c->bk_base;
   uint32_t nb = c->bk_nbp ? c->bk_nbp : (uint32_t)BK_MAXB;
   const uint32_t item_recs = item_records(c, R);
@@ -285,7 +284,7 @@ gs_status bucket_direct(gs_ctx* c, const int64_t* src, const int64_t* dst, const
   for (int attempt = 0;; ++attempt) {
     // 1. per-tile bucket counts against the predicted base and width (the window's one read of
     //    the keys before the scatter) + the measured range and the keys outside the prediction
-    GS_TRY(launch_dp_hist<DIR>(c, src, dst, n, nt, base, S, nb));
+    GS_TRY((launch_dp_hist<DIR, ITEMS>(c, src, dst, n, nt, base, S, nb)));
     GS_HIP(hipMemsetAsync(sm + SM_BK_ESC, 0, 8, c->stream));
     hipEventRecord(c->ev[1], c->stream);
     hipEventRecord(c->pass_ev[0], c->stream);
@@ -311,16 +310,16 @@ gs_status bucket_direct(gs_ctx* c, const int64_t* src, const int64_t* dst, const
     using Load = typename P::Load;
     const BaseSrc<Load, DIR, P::PAY> ls{src, dst, (const Load*)val, base};
     if (part) {
-      const unsigned grid = dp_scatter_grid<DIR>(n);
+      const unsigned grid = dp_scatter_grid<DIR, ITEMS>(n);
       if constexpr (CAN_PACK) {
         if (pack) {
-          hipLaunchKernelGGL((k_dp_scatter_pack<Load, DIR>), dim3(grid), dim3(DP_BLOCK), 0, c->stream, ls, n, S, nb,
+          hipLaunchKernelGGL((k_dp_scatter_pack<Load, DIR, ITEMS>), dim3(grid), dim3(DP_BLOCK), 0, c->stream, ls, n, S, nb,
                              (const uint32_t*)c->dp_off.as<uint32_t>(), c->keysB.as<uint32_t>(), vpart,
                              (const unsigned long long*)mm, (unsigned long long*)(sm + SM_BK_ESC));
           GS_HIP(hipGetLastError());
         }
       }
-      if (!pack) {
+      if constexpr (ITEMS == DP_ITEMS) if (!pack) {
         if constexpr (P::REL) GS_HIP(hipMemsetAsync(rel_bad, 0, 4, c->stream));
         hipLaunchKernelGGL((k_dp_scatter<Load, DIR, P::PAY, Raw, P::REL>), dim3(grid), dim3(DP_BLOCK), 0, c->stream, ls,
                            n, S, nb, c->dp_off.as<uint32_t>(), k16, vpart, rel_bad, (const unsigned long long*)mm);
@@ -373,6 +372,17 @@ gs_status bucket_direct(gs_ctx* c, const int64_t* src, const int64_t* dst, const
   c->times.escapes = esc;
   c->times.packed = pack ? 1u : 0u;
   return GS_OK;
+}
+
+template <class P, int DIR>
+gs_status bucket_direct(gs_ctx* c, const int64_t* src, const int64_t* dst, const void* val, uint64_t n,
+                        typename P::Out o, uint64_t* U) {
+  constexpr bool CAN_PACK = P::PAY == PAY_VAL && !P::REL && std::is_integral_v<typename P::A>;
+  if constexpr (CAN_PACK) {
+    if (c->bk_wide_vals <= 0 && !(c->flags & GS_FLAG_NO_PACK))
+      return bucket_direct_t<P, DIR, PK_ITEMS>(c, src, dst, val, n, o, U, true);
+  }
+  return bucket_direct_t<P, DIR, DP_ITEMS>(c, src, dst, val, n, o, U, false);
 }
 
 // ---- onesweep front end (GS_FLAG_BK_ONESWEEP): global histogram -> 1-2 stable LSD passes ----------

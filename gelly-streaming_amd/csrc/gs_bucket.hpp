@@ -511,17 +511,25 @@ constexpr int DP_BLOCK = 1024;
 constexpr int DP_ITEMS = GS_DP_ITEMS;
 constexpr uint32_t DP_TILE = DP_BLOCK * DP_ITEMS;   // 10240 records < 2^16
 constexpr uint32_t DP_CHUNK = 64;                   // tiles per up / down-sweep chunk
-template <int DIR>
-__host__ __device__ constexpr uint32_t dp_tile_edges() { return DIR == DIR_ALL ? DP_TILE / 2 : DP_TILE; }
+// packed path (k_dp_scatter_pack): its own tile, 6 B of LDS per record (the histogram runs on the same tiles)
+#ifndef GS_PK_ITEMS
+#define GS_PK_ITEMS 16   // C2 scatter (ms): 10 items 1.18, 12 1.17, 14 1.144, 16 1.149 (fewer tiles: offsets 0.056 -> 0.043)
+#endif
+constexpr int PK_ITEMS = GS_PK_ITEMS;
+static_assert(DP_BLOCK * PK_ITEMS < 65536 && DP_BLOCK * DP_ITEMS < 65536, "per-tile bucket counts are u16");
+template <int DIR, int ITEMS = DP_ITEMS>
+__host__ __device__ constexpr uint32_t dp_tile_edges() {
+  return DIR == DIR_ALL ? DP_BLOCK * ITEMS / 2 : DP_BLOCK * ITEMS;
+}
 // k_dp_scatter grid: the full tiles (in 8 XCD slots) + one block for the partial tile
-template <int DIR>
+template <int DIR, int ITEMS = DP_ITEMS>
 __host__ __device__ inline uint32_t dp_scatter_grid(uint64_t n) {
-  return (uint32_t)((n / dp_tile_edges<DIR>() + 7) / 8 * 8 + 1);
+  return (uint32_t)((n / dp_tile_edges<DIR, ITEMS>() + 7) / 8 * 8 + 1);
 }
 
 // Persistent, software-pipelined: the next tile's keys are in flight while this
 // tile's counts go through LDS.  VEC: the tile's keys as 16-byte pairs (columns 16-byte aligned).
-template <int DIR, bool VEC>
+template <int DIR, bool VEC, int ITEMS>
 __global__ __launch_bounds__(DP_BLOCK) void k_dp_hist(const int64_t* __restrict__ src, const int64_t* __restrict__ dst,
                                                       uint64_t n, uint32_t nt, int64_t base, int S, uint32_t nbp,
                                                       uint16_t* __restrict__ cnt,
@@ -529,7 +537,7 @@ __global__ __launch_bounds__(DP_BLOCK) void k_dp_hist(const int64_t* __restrict_
   __shared__ uint32_t h[BK_MAXB];
   __shared__ unsigned long long s_mm[3][DP_BLOCK / WAVE];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  constexpr uint32_t TE = dp_tile_edges<DIR>();
+  constexpr uint32_t TE = dp_tile_edges<DIR, ITEMS>();
   constexpr int U = VEC ? (TE / 2 + DP_BLOCK - 1) / DP_BLOCK : (TE + DP_BLOCK - 1) / DP_BLOCK;
   using L = std::conditional_t<VEC, longlong2, int64_t>;
   uint64_t lo = 0, hi = 0;   // max of ~flip(key), max of flip(key)
@@ -843,26 +851,27 @@ __global__ __launch_bounds__(DP_BLOCK) GS_DP_SCATTER_ATTR void k_dp_scatter(Base
 // mm[2] != 0 (k_dp_hist saw a key outside the predicted range): every block exits at once and the
 // host reruns the window with the measured range.
 #ifndef GS_PK_WAVES
-#define GS_PK_WAVES 8   // waves per SIMD: two 16-wave blocks per CU
+#define GS_PK_WAVES 4   // waves per SIMD: 4 = one 16-wave block per CU (8: two, with the 64-VGPR cap)
 #endif
-template <typename V, int DIR>
+template <typename V, int DIR, int ITEMS>
 __global__ __launch_bounds__(DP_BLOCK) __attribute__((amdgpu_waves_per_eu(GS_PK_WAVES, GS_PK_WAVES)))
 void k_dp_scatter_pack(BaseSrc<V, DIR, PAY_VAL> es, uint64_t n, int S, uint32_t nbp,
                        const uint32_t* __restrict__ off, uint32_t* __restrict__ rec, V* __restrict__ wide,
                        const unsigned long long* __restrict__ mm, unsigned long long* __restrict__ n_esc) {
-  __shared__ uint32_t s_key[DP_TILE];      // (bucket << 16) | bucket-local index, bucket order
-  __shared__ uint16_t s_v16[DP_TILE];      // narrow value, same order
+  constexpr uint32_t TILE = DP_BLOCK * ITEMS;
+  __shared__ uint32_t s_key[TILE];         // (bucket << 16) | bucket-local index, bucket order
+  __shared__ uint16_t s_v16[TILE];         // narrow value, same order
   __shared__ uint32_t s_cnt[BK_MAXB];      // counts, then run starts inside the tile
   __shared__ uint32_t s_delta[BK_MAXB];    // global position - tile position of bucket b's run
   __shared__ uint32_t s_w[DP_BLOCK / WAVE];
   if (mm[2]) return;
   const int tid = threadIdx.x;
-  constexpr uint32_t TE = dp_tile_edges<DIR>();
+  constexpr uint32_t TE = dp_tile_edges<DIR, ITEMS>();
   const uint32_t nfull = (uint32_t)(n / TE);
   const uint32_t base32 = (uint32_t)es.base, lmask = (1u << S) - 1;
   const uint32_t b0 = 2 * tid, b1 = 2 * tid + 1;   // BK_MAXB = 2 * DP_BLOCK
   const uint32_t bl0 = min(b0, nbp - 1), bl1 = min(b1, nbp - 1);
-  uint32_t t, nrec = DP_TILE;
+  uint32_t t, nrec = TILE;
   if (blockIdx.x == gridDim.x - 1) {   // the window's partial last tile
     if ((uint64_t)nfull * TE >= n) return;
     t = nfull;
@@ -872,12 +881,12 @@ void k_dp_scatter_pack(BaseSrc<V, DIR, PAY_VAL> es, uint64_t n, int S, uint32_t 
     t = (blockIdx.x & 7u) * per + (blockIdx.x >> 3);
     if (t >= nfull) return;
   }
-  const uint32_t r0 = t * DP_TILE;
+  const uint32_t r0 = t * TILE;
   const uint32_t* orow = off + (uint64_t)t * nbp;
   const uint32_t o0 = orow[bl0], o1 = orow[bl1];
-  uint32_t kb[DP_ITEMS], v16[DP_ITEMS];
+  uint32_t kb[ITEMS], v16[ITEMS];
 #pragma unroll
-  for (int u = 0; u < DP_ITEMS; ++u) {   // unconditional loads, clamped into the tile (k_dp_scatter)
+  for (int u = 0; u < ITEMS; ++u) {   // unconditional loads, clamped into the tile (k_dp_scatter)
     uint32_t kl;
     V vv;
     dp_load_raw(es, r0 + min((uint32_t)u * DP_BLOCK + tid, nrec - 1), kl, vv);
@@ -887,9 +896,9 @@ void k_dp_scatter_pack(BaseSrc<V, DIR, PAY_VAL> es, uint64_t n, int S, uint32_t 
   }
   for (uint32_t i = tid; i < nbp; i += DP_BLOCK) s_cnt[i] = 0;
   __syncthreads();
-  uint32_t rk[DP_ITEMS];
+  uint32_t rk[ITEMS];
 #pragma unroll
-  for (int u = 0; u < DP_ITEMS; ++u)
+  for (int u = 0; u < ITEMS; ++u)
     if ((uint32_t)u * DP_BLOCK + tid < nrec) rk[u] = atomicAdd(&s_cnt[kb[u] >> 16], 1u);
   __syncthreads();
   const uint32_t c0 = b0 < nbp ? s_cnt[b0] : 0u, c1 = b1 < nbp ? s_cnt[b1] : 0u;
@@ -902,7 +911,7 @@ void k_dp_scatter_pack(BaseSrc<V, DIR, PAY_VAL> es, uint64_t n, int S, uint32_t 
   __syncthreads();
   uint32_t esc = 0;
 #pragma unroll
-  for (int u = 0; u < DP_ITEMS; ++u) {
+  for (int u = 0; u < ITEMS; ++u) {
     const uint32_t j = (uint32_t)u * DP_BLOCK + tid;
     if (j < nrec) {
       const uint32_t pos = s_cnt[kb[u] >> 16] + rk[u];
@@ -920,9 +929,9 @@ void k_dp_scatter_pack(BaseSrc<V, DIR, PAY_VAL> es, uint64_t n, int S, uint32_t 
     const uint32_t kv = s_key[j];
     rec[s_delta[kv >> 16] + j] = (kv & 0xFFFFu) | ((uint32_t)s_v16[j] << 16);
   };
-  if (nrec == DP_TILE) {
+  if (nrec == TILE) {
 #pragma unroll
-    for (int u = 0; u < DP_ITEMS; ++u) put((uint32_t)u * DP_BLOCK + tid);
+    for (int u = 0; u < ITEMS; ++u) put((uint32_t)u * DP_BLOCK + tid);
   } else {
     for (uint32_t j = tid; j < nrec; j += DP_BLOCK) put(j);
   }
@@ -992,22 +1001,35 @@ __global__ __launch_bounds__(BK_ACC_BLOCK) void k_bk_accum(Src src, const BkItem
     __syncthreads();
     const uint32_t r0 = b0 + m.begin, r1 = b0 + m.end;
     if constexpr (is_pack_src<Src>::value) {
-      for (uint32_t r = r0 + tid; r < r1; r += BK_ACC_BLOCK * UNROLL) {
-        uint32_t x[UNROLL];
+      // 16-byte loads (4 records per lane per load: 4x the bytes in flight of 4-byte loads; the
+      // 4-byte version was latency-bound); an unaligned head and the tail record by record
+      auto add1 = [&](uint32_t q, uint32_t x) {
+        const uint32_t v16 = x >> 16;
+        P::add(s, x & (P::W - 1), v16 != PK_ESC ? (Raw)v16 : (Raw)src.wide[q]);
+      };
+      const uint32_t a0 = min(r1, (r0 + 3) & ~3u), a1 = max(a0, r1 & ~3u);
+      if (r0 + tid < a0) add1(r0 + tid, src.rec[r0 + tid]);
+      const uint4* rec4 = reinterpret_cast<const uint4*>(src.rec);
+      constexpr int U4 = UNROLL / 2 > 0 ? UNROLL / 2 : 1;
+      for (uint32_t q4 = a0 / 4 + tid; q4 < a1 / 4; q4 += BK_ACC_BLOCK * U4) {
+        uint4 x[U4];
 #pragma unroll
-        for (int u = 0; u < UNROLL; ++u) {
-          const uint32_t q = r + (uint32_t)u * BK_ACC_BLOCK;
-          x[u] = src.rec[q < r1 ? q : r1 - 1];   // unconditional: see k_dp_hist
+        for (int u = 0; u < U4; ++u) {
+          const uint32_t qq = q4 + (uint32_t)u * BK_ACC_BLOCK;
+          x[u] = rec4[qq < a1 / 4 ? qq : a1 / 4 - 1];   // unconditional: see k_dp_hist
         }
 #pragma unroll
-        for (int u = 0; u < UNROLL; ++u) {
-          const uint32_t q = r + (uint32_t)u * BK_ACC_BLOCK;
-          if (q < r1) {
-            const uint32_t v16 = x[u] >> 16;
-            P::add(s, x[u] & (P::W - 1), v16 != PK_ESC ? (Raw)v16 : (Raw)src.wide[q]);
+        for (int u = 0; u < U4; ++u) {
+          const uint32_t qq = q4 + (uint32_t)u * BK_ACC_BLOCK;
+          if (qq < a1 / 4) {
+            add1(4 * qq, x[u].x);
+            add1(4 * qq + 1, x[u].y);
+            add1(4 * qq + 2, x[u].z);
+            add1(4 * qq + 3, x[u].w);
           }
         }
       }
+      if (a1 + tid < r1) add1(a1 + tid, src.rec[a1 + tid]);
     } else {
       for (uint32_t r = r0 + tid; r < r1; r += BK_ACC_BLOCK * UNROLL) {
         uint32_t k[UNROLL];

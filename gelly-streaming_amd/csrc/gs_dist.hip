@@ -130,10 +130,10 @@ gs_status owner_partition(gs_ctx* c, const int64_t* keys, const void* vals, size
                           uint32_t nparts, int64_t* okeys, void* ovals, int64_t* ovals2, uint64_t* counts_host) {
   char* sm = c->small.as<char>();
   const uint32_t tiles = (uint32_t)std::max<uint64_t>(1, (U + OW_TILE - 1) / OW_TILE);
-  GS_TRY(ensure(c, c->dist_cnt, (size_t)tiles * nparts * 4 + 64 * 8));
-  uint32_t* cnt = c->dist_cnt.as<uint32_t>();
-  auto* totals = (unsigned long long*)(c->dist_cnt.as<char>() + (size_t)tiles * nparts * 4 + 7 * 8) ;
-  totals = (unsigned long long*)(((uintptr_t)totals) & ~(uintptr_t)7);
+  // dist_cnt: [0, 1 KiB) per-call scalars (owner totals, exchange counts), then the tile counts
+  GS_TRY(ensure(c, c->dist_cnt, 1024 + (size_t)tiles * nparts * 4));
+  auto* totals = c->dist_cnt.as<unsigned long long>();
+  uint32_t* cnt = (uint32_t*)(c->dist_cnt.as<char>() + 1024);
   if (U) {
     hipLaunchKernelGGL(k_owner_count, dim3(tiles), dim3(OW_BLOCK), 0, c->stream, keys, U, nparts, tiles, cnt);
     hipLaunchKernelGGL(k_owner_scan, dim3(1), dim3(1024), 0, c->stream, cnt, tiles * nparts, tiles, nparts, totals);
@@ -244,6 +244,17 @@ static gs_status partials_impl(gs_ctx* c, const gs_edge_batch* b, int32_t dir, i
   GS_TRY(check_batch(c, b, dir));
   GS_TRY(check_partials_out(c, out, nparts, degmax));
   const uint64_t R = dir == GS_DIR_ALL ? 2 * b->n : b->n;
+  if (nparts == 1) {   // one owner: the window's own output, in place (no partition pass)
+    if (degmax) {
+      gs_degree_out o{out->keys, (int64_t*)out->vals, out->vals2, out->capacity, out->n_out, out->mem, 0};
+      GS_TRY(gs_window_fold_degree_max(c, b, dir, init_max, &o));
+    } else {
+      gs_vertex_out o{out->keys, out->vals, out->capacity, out->n_out, out->mem, 0};
+      GS_TRY(gs_window_reduce(c, b, dir, op, &o));
+    }
+    out->owner_counts[0] = *out->n_out;
+    return GS_OK;
+  }
   GS_TRY(ensure(c, c->dist_k, R * 8 + 8));
   GS_TRY(ensure(c, c->dist_v, R * 8 + 8));
   if (degmax) GS_TRY(ensure(c, c->dist_v2, R * 8 + 8));
@@ -311,12 +322,27 @@ gs_status gs_merge_degree_max_partials(gs_ctx* c, const gs_partial_batch* p, int
   if (!p || (p->n && (!p->keys || !p->vals || !p->vals2))) return set_error(c, GS_EINVAL, "bad gs_partial_batch");
   if (!out || !out->n_out || (out->capacity && (!out->keys || !out->degree || !out->max_neighbor)))
     return set_error(c, GS_EINVAL, "bad gs_degree_out");
-  const gs_edge_batch bd{p->keys, p->keys, p->vals, p->n, GS_I64, p->mem, 0};
-  const gs_edge_batch bm{p->keys, p->keys, p->vals2, p->n, GS_I64, p->mem, 0};
-  gs_vertex_out od{out->keys, out->degree, out->capacity, out->n_out, out->mem, 0};
-  GS_TRY(gs_window_reduce(c, &bd, GS_DIR_OUT, GS_OP_SUM, &od));       // degrees add
-  gs_vertex_out om{out->keys, out->max_neighbor, out->capacity, out->n_out, out->mem, 0};
-  return gs_window_fold(c, &bm, GS_DIR_OUT, GS_OP_MAX, &init_max, &om);   // maxima, then the fold's init
+  // both merges write the ctx's output staging (device), then the rows go to the caller
+  const uint64_t n = p->n;
+  GS_TRY(ensure(c, c->out_keys, n * 8 + 8));
+  GS_TRY(ensure(c, c->out_a, n * 8 + 8));
+  GS_TRY(ensure(c, c->out_b, n * 8 + 8));
+  const gs_edge_batch bd{p->keys, p->keys, p->vals, n, GS_I64, p->mem, 0};
+  const gs_edge_batch bm{p->keys, p->keys, p->vals2, n, GS_I64, p->mem, 0};
+  uint64_t U = 0;
+  gs_vertex_out od{c->out_keys.as<int64_t>(), c->out_a.p, n, &U, GS_MEM_DEVICE, 0};
+  GS_TRY(gs_window_reduce(c, &bd, GS_DIR_OUT, GS_OP_SUM, &od));            // degrees add
+  gs_vertex_out om{c->out_keys.as<int64_t>(), c->out_b.p, n, &U, GS_MEM_DEVICE, 0};
+  GS_TRY(gs_window_fold(c, &bm, GS_DIR_OUT, GS_OP_MAX, &init_max, &om));   // maxima, then the fold's init
+  *out->n_out = U;
+  c->last_U = U;
+  c->last_ob = 8;
+  c->last_kind = 2;
+  if (U > out->capacity) return set_error(c, GS_ECAPACITY, "output needs %llu vertices", (unsigned long long)U);
+  GS_TRY(deliver(c, out->keys, c->out_keys.as<int64_t>(), U * 8, out->mem));
+  GS_TRY(deliver(c, out->degree, c->out_a.p, U * 8, out->mem));
+  GS_TRY(deliver(c, out->max_neighbor, c->out_b.p, U * 8, out->mem));
+  return host_wait(c);
 }
 
 // ---- ctx-owned RCCL communicator ----------------------------------------------------------------------
@@ -360,7 +386,7 @@ gs_status gs_comm_destroy(gs_ctx* c) {
 gs_status gs_comm_allreduce_sum_u64(gs_ctx* c, uint64_t* value) {
   if (!c || !value) return GS_EINVAL;
   if (!c->comm) return set_error(c, GS_EINVAL, "no communicator (gs_comm_init)");
-  GS_TRY(ensure(c, c->dist_cnt, 64 * 8 + 64 * 4));
+  GS_TRY(ensure(c, c->dist_cnt, 1024));
   uint64_t* d = c->dist_cnt.as<uint64_t>();
   c->host_small[8] = *value;
   GS_HIP(hipMemcpyAsync(d, c->host_small + 8, 8, hipMemcpyHostToDevice, c->stream));
@@ -389,7 +415,7 @@ static gs_status dist_impl(gs_ctx* c, const gs_edge_batch* b, int32_t dir, int32
   const gs_stage_times keep = c->times;
   const size_t vb = degmax ? 8 : (op == GS_OP_COUNT ? 8 : dtype_bytes(b->val_dtype));
   // counts: all-to-all of one u64 per peer
-  GS_TRY(ensure(c, c->dist_cnt, 64 * 8 * 2 + 64));
+  GS_TRY(ensure(c, c->dist_cnt, 1024));
   uint64_t* dc = c->dist_cnt.as<uint64_t>();
   memcpy(c->host_small + 8, send.data(), P * 8);
   GS_HIP(hipMemcpyAsync(dc, c->host_small + 8, P * 8, hipMemcpyHostToDevice, c->stream));

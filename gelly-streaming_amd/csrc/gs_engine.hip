@@ -383,6 +383,7 @@ void gs_destroy(gs_ctx* c) {
   if (!c) return;
   hipSetDevice(c->device);
   if (c->stream) hipStreamSynchronize(c->stream);
+  if (c->comm) gs_comm_destroy(c);
   for (DevBuf& b : c->hs)
     if (b.p) hipFree(b.p);
   for (DevBuf* b : {&c->part_k, &c->part_a, &c->comp_k, &c->comp_a,
@@ -390,8 +391,11 @@ void gs_destroy(gs_ctx* c) {
                     &c->rbk_word, &c->rbk_agg, &c->rbk_inc, &c->small, &c->out_keys, &c->out_a, &c->out_b, &c->aux,
                     &c->bk_meta, &c->bk_items, &c->bk_slabs, &c->dp_cnt, &c->dp_csum, &c->dp_off, &c->tri_loops, &c->tri_keep, &c->tri_tiles, &c->tri_pos, &c->tri_ou, &c->tri_onbr, &c->tri_heavy, &c->tri_range, &c->tri_queue,
                     &c->pr_a, &c->pr_b, &c->pr_f, &c->pr_key, &c->pr_val, &c->pr_gk, &c->pr_gv, &c->pr_small,
-                    &c->tx_text, &c->tx_cnt, &c->tx_starts, &c->zipf_cdf})
+                    &c->tx_text, &c->tx_cnt, &c->tx_starts, &c->zipf_cdf,
+                    &c->dist_k, &c->dist_v, &c->dist_v2, &c->dist_k2, &c->dist_v3, &c->dist_v4, &c->dist_cnt})
     if (b->p) hipFree(b->p);
+  for (DevBuf& b : c->rl)
+    if (b.p) hipFree(b.p);
   for (auto& e : c->ev)
     if (e) hipEventDestroy(e);
   for (auto& e : c->pass_ev)
@@ -437,6 +441,9 @@ gs_status gs_last_stage_times(const gs_ctx* c, gs_stage_times* out) {
 static gs_status finish_vertex_out(gs_ctx* c, gs_vertex_out* out, const int64_t* kd, const void* vd, size_t ob,
                                    uint64_t U, bool direct) {
   *out->n_out = U;
+  c->last_U = U;   // the staged rows gs_fetch_last_output can deliver after GS_ECAPACITY
+  c->last_ob = ob;
+  c->last_kind = direct ? 0 : 1;
   if (U > out->capacity) return set_error(c, GS_ECAPACITY, "output needs %llu vertices", (unsigned long long)U);
   GS_TRY(deliver(c, out->keys, kd, U * 8, out->mem));
   GS_TRY(deliver(c, out->vals, vd, U * ob, out->mem));
@@ -499,6 +506,30 @@ static gs_status window_fold_impl(gs_ctx* c, const gs_edge_batch* b, int32_t dir
   return finish_vertex_out(c, out, kd, vd, ob, U, direct);
 }
 
+gs_status gs_fetch_last_output(gs_ctx* c, gs_vertex_out* out) {
+  if (!c) return GS_EINVAL;
+  if (c->last_kind != 1) return set_error(c, GS_EINVAL, "no staged (vertex, value) output to fetch");
+  if (!out || !out->n_out || (c->last_U && (!out->keys || !out->vals))) return set_error(c, GS_EINVAL, "bad gs_vertex_out");
+  *out->n_out = c->last_U;
+  if (c->last_U > out->capacity) return set_error(c, GS_ECAPACITY, "output needs %llu vertices", (unsigned long long)c->last_U);
+  GS_TRY(deliver(c, out->keys, c->out_keys.as<int64_t>(), c->last_U * 8, out->mem));
+  GS_TRY(deliver(c, out->vals, c->out_a.p, c->last_U * c->last_ob, out->mem));
+  return host_wait(c);
+}
+
+gs_status gs_fetch_last_degree_output(gs_ctx* c, gs_degree_out* out) {
+  if (!c) return GS_EINVAL;
+  if (c->last_kind != 2) return set_error(c, GS_EINVAL, "no staged degree / max output to fetch");
+  if (!out || !out->n_out || (c->last_U && (!out->keys || !out->degree || !out->max_neighbor)))
+    return set_error(c, GS_EINVAL, "bad gs_degree_out");
+  *out->n_out = c->last_U;
+  if (c->last_U > out->capacity) return set_error(c, GS_ECAPACITY, "output needs %llu vertices", (unsigned long long)c->last_U);
+  GS_TRY(deliver(c, out->keys, c->out_keys.as<int64_t>(), c->last_U * 8, out->mem));
+  GS_TRY(deliver(c, out->degree, c->out_a.p, c->last_U * 8, out->mem));
+  GS_TRY(deliver(c, out->max_neighbor, c->out_b.p, c->last_U * 8, out->mem));
+  return host_wait(c);
+}
+
 gs_status gs_window_reduce(gs_ctx* c, const gs_edge_batch* b, int32_t dir, int32_t op, gs_vertex_out* out) {
   return window_fold_impl(c, b, dir, op, false, nullptr, out);
 }
@@ -547,6 +578,9 @@ gs_status gs_window_fold_degree_max(gs_ctx* c, const gs_edge_batch* b, int32_t d
     finish_times(c, s, U);
   }
   *out->n_out = U;
+  c->last_U = U;
+  c->last_ob = 8;
+  c->last_kind = direct ? 0 : 2;
   if (U > out->capacity) return set_error(c, GS_ECAPACITY, "output needs %llu vertices", (unsigned long long)U);
   GS_TRY(deliver(c, out->keys, kd, U * 8, out->mem));
   GS_TRY(deliver(c, out->degree, dd, U * 8, out->mem));

@@ -264,11 +264,20 @@ static gs_status triangles_impl(gs_ctx* c, const gs_edge_batch* b, uint32_t part
   GS_HIP(hipMemcpyAsync(c->host_small, sm, 16, hipMemcpyDeviceToHost, c->stream));
   GS_TRY(host_wait(c));
   const uint64_t mask = c->host_small[0], k0 = c->host_small[1];
-  const uint32_t B = mask ? 64 - __builtin_clzll(mask) : 1;
-  if (B > TRI_MAX_BITS)
-    return set_error(c, GS_EUNSUPPORTED, "window triangles: vertex IDs span %u bits (> %llu) — relabeling not built yet",
-                     B, (unsigned long long)TRI_MAX_BITS);
-  const uint64_t key_xor = k0 & ~((1ull << B) - 1);
+  uint32_t B = mask ? 64 - __builtin_clzll(mask) : 1;
+  uint64_t key_xor = k0 & ~((1ull << B) - 1);
+  // IDs wider than the composite-key budget: relabel (order-preserving compact IDs); the originals
+  // stay for the self-pair term's HashSet order
+  const int64_t *osrc = src, *odst = dst, *uniq = nullptr;
+  uint64_t nuniq = 0;
+  if (B > TRI_MAX_BITS) {
+    GS_TRY(relabel_endpoints(c, osrc, odst, n, &src, &dst, &uniq, &nuniq));
+    B = nuniq > 1 ? 64 - __builtin_clzll(nuniq - 1) : 1;
+    key_xor = 0;
+    if (B > TRI_MAX_BITS)
+      return set_error(c, GS_EUNSUPPORTED, "window triangles: %llu distinct vertices (> 2^%llu)",
+                       (unsigned long long)nuniq, (unsigned long long)TRI_MAX_BITS);
+  }
   const uint64_t R = 2 * n;
   // 1. symmetric composite keys (+ self-loop bitmap)
   GS_TRY(ensure(c, c->aux, R * 8));
@@ -294,7 +303,7 @@ static gs_status triangles_impl(gs_ctx* c, const gs_edge_batch* b, uint32_t part
   if (loops) E2 -= 1;   // the self-loop sentinel sorts last
   if (E2 == 0) {        // only self-loops: no triangle; the self-pair term needs >= 2 neighbours
     uint64_t S = 0;
-    if (part == 0) GS_TRY(triangle_selfpair_term(c, src, dst, n, c->tri_loops.as<uint32_t>(), key_xor, &S));
+    if (part == 0) GS_TRY(triangle_selfpair_term(c, osrc, odst, n, c->tri_loops.as<uint32_t>(), key_xor, uniq, nuniq, &S));
     *count = S;
     return GS_OK;
   }
@@ -388,7 +397,7 @@ static gs_status triangles_impl(gs_ctx* c, const gs_edge_batch* b, uint32_t part
   }
   if (loops && part == 0) {   // self-pair candidates (x, x, true) matched by a self-loop on x (:105)
     uint64_t S = 0;
-    GS_TRY(triangle_selfpair_term(c, src, dst, n, c->tri_loops.as<uint32_t>(), key_xor, &S));
+    GS_TRY(triangle_selfpair_term(c, osrc, odst, n, c->tri_loops.as<uint32_t>(), key_xor, uniq, nuniq, &S));
     T += S;
   }
   *count = T;

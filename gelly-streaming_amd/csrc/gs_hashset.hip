@@ -261,13 +261,23 @@ __global__ __launch_bounds__(256) void k_hs_emit_pairs(uint32_t M, const uint64_
 __global__ __launch_bounds__(256) void k_hs_selfpairs(const int64_t* __restrict__ ids, uint32_t M,
                                                       const uint64_t* __restrict__ doff, uint32_t U,
                                                       const int64_t* __restrict__ vkeys, const uint32_t* __restrict__ loops,
-                                                      uint64_t key_xor, unsigned long long* __restrict__ S) {
+                                                      uint64_t key_xor, const int64_t* __restrict__ relabel,
+                                                      uint64_t nrel, unsigned long long* __restrict__ S) {
   uint64_t t = 0;
   for (uint32_t q = blockIdx.x * 256u + threadIdx.x; q < M; q += gridDim.x * 256u) {
     const uint32_t u = seg_of(doff, U, q);
     const int64_t v = vkeys[u], x = ids[q];
     if (q + 1 < doff[u + 1] && x > v) {   // rows i < len-1 emit (x, x) when x > v
-      const uint64_t c = (uint64_t)x ^ key_xor;
+      uint64_t c = (uint64_t)x ^ key_xor;
+      if (relabel) {   // rank of x among the window's sorted distinct IDs
+        uint64_t lo = 0, hi = nrel;
+        while (lo < hi) {
+          const uint64_t mid = (lo + hi) >> 1;
+          if (relabel[mid] < x) lo = mid + 1;
+          else hi = mid;
+        }
+        c = lo;
+      }
       if ((loops[c >> 5] >> (c & 31)) & 1u) ++t;
     }
   }
@@ -285,7 +295,7 @@ namespace gs {
 enum { HS_VKEYS, HS_OFF, HS_NBR, HS_USEG, HS_COMP, HS_PIDX, HS_DKEY, HS_DFIRST, HS_DOFF, HS_OKEY, HS_OMID,
        HS_UKEY, HS_ORD, HS_IDS, HS_G, HS_GX, HS_L, HS_LS, HS_TILES, HS_COUNT };
 
-static gs_status xscan(gs_ctx* c, const uint64_t* in, uint64_t n, uint64_t* out) {
+gs_status xscan(gs_ctx* c, const uint64_t* in, uint64_t n, uint64_t* out) {
   const uint32_t tiles = (uint32_t)std::max<uint64_t>(1, (n + XS_TILE - 1) / XS_TILE);
   GS_TRY(ensure(c, c->hs[HS_TILES], (size_t)(tiles + 1) * 8));
   uint64_t* ts = c->hs[HS_TILES].as<uint64_t>();
@@ -383,7 +393,8 @@ gs_status hashset_order(gs_ctx* c, const int64_t* src, const int64_t* dst, uint6
 
 // S term of the triangle count (see gs_graph.hip): loops = self-loop bitmap over compact IDs
 gs_status triangle_selfpair_term(gs_ctx* c, const int64_t* src, const int64_t* dst, uint64_t n,
-                                 const uint32_t* loops, uint64_t loops_xor, uint64_t* S) {
+                                 const uint32_t* loops, uint64_t loops_xor, const int64_t* relabel, uint64_t nrel,
+                                 uint64_t* S) {
   uint32_t U = 0, M = 0;
   uint64_t key_xor = 0;
   bool tree = false;
@@ -393,7 +404,8 @@ gs_status triangle_selfpair_term(gs_ctx* c, const int64_t* src, const int64_t* d
   unsigned long long* d = (unsigned long long*)(sm + SM_TOTAL);
   GS_HIP(hipMemsetAsync(d, 0, 8, c->stream));
   hipLaunchKernelGGL(k_hs_selfpairs, dim3(g256(M)), dim3(256), 0, c->stream, c->hs[HS_IDS].as<int64_t>(), M,
-                     c->hs[HS_DOFF].as<uint64_t>(), U, c->hs[HS_VKEYS].as<int64_t>(), loops, loops_xor, d);
+                     c->hs[HS_DOFF].as<uint64_t>(), U, c->hs[HS_VKEYS].as<int64_t>(), loops, loops_xor, relabel,
+                     nrel, d);
   GS_HIP(hipGetLastError());
   GS_HIP(hipMemcpyAsync(c->host_small + 7, d, 8, hipMemcpyDeviceToHost, c->stream));
   GS_TRY(host_wait(c));

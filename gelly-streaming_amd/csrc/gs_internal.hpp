@@ -41,7 +41,12 @@ struct gs_ctx {
   uint32_t flags = 0;    // gs_config.flags
   int64_t bk_base = 0;   // bucket path: predicted lower bound of the next window's vertex IDs
   uint32_t bk_nbp = 0;   // direct bucket path: predicted bucket count (0 = BK_MAXB)
-  int bk_wide_vals = 0;  // direct bucket path: > 0 = windows left that store 8-byte values (escapes were common)
+  int bk_wide_vals = 0;
+  // the last window call's output: U rows of ob-byte values, staged in out_keys / out_a (/ out_b) when
+  // last_kind is 1 (vertex, value) or 2 (degree / max) -- gs_fetch_last_output after GS_ECAPACITY
+  uint64_t last_U = 0;
+  size_t last_ob = 0;
+  int last_kind = 0;  // direct bucket path: > 0 = windows left that store 8-byte values (escapes were common)
   int n_cu = 0;          // compute units (persistent grids)
   // input staging (host batches)
   gs::DevBuf in_src, in_dst, in_val;
@@ -67,6 +72,13 @@ struct gs_ctx {
   gs::DevBuf pr_a, pr_b, pr_f, pr_key, pr_val, pr_gk, pr_gv, pr_small;
   // edge text parser (gs_text.hip): staged text, tile newline counts, record starts
   gs::DevBuf tx_text, tx_cnt, tx_starts;
+  // multi-GPU keyBy (gs_dist.hip): staging of the local reduce, owner-grouped partials, received rows,
+  // per-tile owner counts; the ctx-owned RCCL communicator (opaque ncclComm_t)
+  gs::DevBuf dist_k, dist_v, dist_v2, dist_k2, dist_v3, dist_v4, dist_cnt;
+  void* comm = nullptr;
+  int comm_size = 0, comm_rank = 0;
+  // relabeling of arbitrary vertex IDs (gs_relabel.hip)
+  gs::DevBuf rl[8];
   // Zipf generator: CDF table of (zipf_v, zipf_s)
   gs::DevBuf zipf_cdf;
   uint64_t zipf_v = 0;
@@ -98,7 +110,7 @@ constexpr size_t SM_DEV_ERR = SM_BK_ESC + 8;        // u32 device error flags (G
 constexpr size_t SM_BYTES = SM_DEV_ERR + 8;
 // device error flags (SM_DEV_ERR): a kernel that cannot finish its work sets one and returns
 constexpr uint32_t GS_DERR_TABLE_FULL = 1u;         // an LDS hash set filled up (triangle counting)
-constexpr size_t HOST_SMALL_WORDS = 32;             // pinned u64 mirror of small scalars
+constexpr size_t HOST_SMALL_WORDS = 128;            // pinned u64 mirror of small scalars
 
 gs_status set_error(gs_ctx* c, gs_status s, const char* fmt, ...);
 gs_status hip_check(gs_ctx* c, hipError_t e, const char* what);
@@ -118,9 +130,17 @@ gs_status sort_buffer(gs_ctx* c, const uint64_t* keys, const uint32_t* vals, uin
 // HashSet-ordered distinct neighbour sets of an ALL window (gs_hashset.hip)
 gs_status hashset_order(gs_ctx* c, const int64_t* src, const int64_t* dst, uint64_t n, uint32_t* U_out,
                         uint32_t* M_out, uint64_t* key_xor_out, bool* treeified);
-// WindowTriangles self-pair term for windows with self-loops (loops: bitmap over compact IDs)
+// WindowTriangles self-pair term for windows with self-loops (loops: bitmap over compact IDs: x ^ loops_xor,
+// or, for a relabeled window, the rank of x among the sorted distinct IDs `relabel[0 .. nrel)`)
 gs_status triangle_selfpair_term(gs_ctx* c, const int64_t* src, const int64_t* dst, uint64_t n,
-                                 const uint32_t* loops, uint64_t loops_xor, uint64_t* S);
+                                 const uint32_t* loops, uint64_t loops_xor, const int64_t* relabel, uint64_t nrel,
+                                 uint64_t* S);
+// exclusive scan of n u64 (gs_hashset.hip)
+gs_status xscan(gs_ctx* c, const uint64_t* in, uint64_t n, uint64_t* out);
+// order-preserving compaction of the IDs of two columns (gs_relabel.hip): *ca / *cb = ranks among the
+// *V sorted distinct IDs *uniq (device buffers of the ctx, valid until the next relabel)
+gs_status relabel_endpoints(gs_ctx* c, const int64_t* a, const int64_t* b, uint64_t n, const int64_t** ca,
+                            const int64_t** cb, const int64_t** uniq, uint64_t* V);
 // Bucket path (gs_bucket.hip) for the associative built-ins; GS_EUNSUPPORTED (no message) when the
 // window or op does not fit it and the caller should take the sort path.  keys/vals: device.
 gs_status bucket_reduce(gs_ctx* c, const int64_t* src, const int64_t* dst, const void* val, uint64_t n, int dir,

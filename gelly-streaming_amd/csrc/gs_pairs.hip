@@ -126,13 +126,21 @@ extern "C" gs_status gs_window_count_candidates(gs_ctx* c, const gs_pair_batch* 
   GS_TRY(host_wait(c));
   const int64_t amin = (int64_t)(~h[0] ^ (1ull << 63)), amax = (int64_t)(h[1] ^ (1ull << 63));
   const int64_t bmin = (int64_t)(~h[2] ^ (1ull << 63)), bmax = (int64_t)(h[3] ^ (1ull << 63));
-  if ((uint64_t)amax - (uint64_t)amin >= (1ull << 32) || (uint64_t)bmax - (uint64_t)bmin >= (1ull << 32))
-    return set_error(c, GS_EUNSUPPORTED, "count_candidates: vertex IDs of a or b span 2^32 or more");
+  int64_t amin_ = amin, bmin_ = bmin;
+  if ((uint64_t)amax - (uint64_t)amin >= (1ull << 32) || (uint64_t)bmax - (uint64_t)bmin >= (1ull << 32)) {
+    // IDs spanning 2^32 or more: order-preserving compact IDs of a and b (one ID space, < 2n values);
+    // grouping by (a, b) is unchanged
+    const int64_t* uniq = nullptr;
+    uint64_t V = 0;
+    GS_TRY(relabel_endpoints(c, a, b, n, &a, &b, &uniq, &V));
+    amin_ = 0;
+    bmin_ = 0;
+  }
   GS_TRY(ensure(c, c->pr_key, n * 8));
   GS_TRY(ensure(c, c->pr_val, n * 8));
   GS_TRY(ensure(c, c->pr_gk, n * 8));
   GS_TRY(ensure(c, c->pr_gv, n * 8));
-  hipLaunchKernelGGL(k_pr_pack, dim3(grid), dim3(PR_BLOCK), 0, c->stream, a, b, f, n, amin, bmin,
+  hipLaunchKernelGGL(k_pr_pack, dim3(grid), dim3(PR_BLOCK), 0, c->stream, a, b, f, n, amin_, bmin_,
                      c->pr_key.as<int64_t>(), c->pr_val.as<int64_t>());
   GS_HIP(hipGetLastError());
   gs_edge_batch kb{c->pr_key.as<int64_t>(), c->pr_key.as<int64_t>(), c->pr_val.p, n, GS_I64, GS_MEM_DEVICE, 0};

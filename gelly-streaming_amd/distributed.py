@@ -1,20 +1,26 @@
-"""Multi-GPU window: keyBy(vertex) across ranks with one RCCL all-to-all.
+"""Multi-GPU window: keyBy(vertex) across ranks, one process per GPU.
 
 The reference partitions each window by `keyBy(NeighborKeySelector)` (SimpleEdgeStream.java:159-167):
-every record travels to the subtask that owns its key, which folds it.  Here every rank first
-pre-reduces its own slice of the window on its GPU (sort + segmented reduce, associative ops only),
-then the per-vertex partials — far fewer than records — are exchanged once:
+every record travels to the subtask that owns its key, which folds it.  Here every rank pre-reduces its
+own slice of the window on its GPU and only the per-vertex partials travel, through the two halves of
+the C ABI (include/gelly_hip.h, gs_dist.hip) around one exchange:
 
-  1. local:   (keys, partials) = engine.reduce(slice)            keys ascending
-  2. owners:  vertex-range partition of [global min, global max] (all_reduce of 2 int64)
-              -> each owner's partials are a contiguous slice of the sorted local output
-  3. shuffle: all_to_all_single of counts, then of keys and partials (RCCL over xGMI)
-  4. merge:   engine.reduce(received keys, partials) with the merge op (COUNT merges by SUM)
+  1. partials: gs_window_reduce_partials -> this slice's (vertex, partial) rows grouped by
+               owner(v) = gs_owner_of(v, world) (a hash of the vertex, as keyBy is), with the
+               per-owner row counts; the owner split is computed on the device
+  2. exchange: all_to_all_single of [row count, key-width flag] per peer, then ONE all_to_all_single of
+               packed rows (RCCL over xGMI with the "nccl" backend; gloo in the CPU tests).  Keys travel
+               as 32-bit values when every rank's keys are non-negative and below 2^32 (12-byte rows
+               for a Long partial instead of 16)
+  3. merge:    gs_merge_partials -> the vertices this rank owns (COUNT partials add up; foldNeighbors'
+               init is applied once, here)
 
-Which rank owns a vertex is not observable in the reference's output (per-vertex records compared
-as unordered sets), so the range owner replaces Flink's hash owner.  Integer results stay bit-exact
-(the ops are associative and commutative); float sums move within the 1e-5 tolerance.
-`local_reduce` is injectable so the same exchange logic is exercised on CPU with gloo in tests.
+Which rank owns a vertex is not observable in the reference's output (per-vertex records compared as
+unordered sets).  Integer results stay bit-exact (the ops are associative and commutative); float
+sums move within the 1e-5 tolerance.  The halves are injectable callables so the exchange logic also
+runs on CPU with gloo in tests (tests/test_distributed_gloo.py); on GPUs they are Engine methods.
+The library also owns an RCCL communicator itself (Engine.comm_init + Engine.reduce_dist): the same
+three steps with the exchange inside gs_window_reduce_dist, for callers without torch.distributed.
 """
 from __future__ import annotations
 
@@ -28,78 +34,72 @@ def merge_op(op: int) -> int:
     return SUM if op == COUNT else op
 
 
-def owner_bounds(kmin: int, kmax: int, world: int) -> list:
-    """Split [kmin, kmax] into `world` contiguous vertex ranges; returns world-1 interior bounds."""
-    span = kmax - kmin + 1
-    return [kmin + (span * r) // world for r in range(1, world)]
+def _comm_device(group, like: torch.Tensor) -> torch.device:
+    """nccl exchanges device tensors; gloo host tensors."""
+    return like.device if dist.get_backend(group) == "nccl" else torch.device("cpu")
 
 
-def exchange_sorted(keys: torch.Tensor, cols: list, group=None):
-    """Send each owner its slice of (keys, *cols); keys must be ascending.  Returns received tensors."""
+def exchange_partials(keys: torch.Tensor, cols: list, counts: list, group=None):
+    """Send rows [sum(counts[:p]), sum(counts[:p+1])) of (keys, *cols) to rank p (rows grouped by owner).
+    Returns the received (keys, cols) on keys' device."""
     world = dist.get_world_size(group)
-    dev = keys.device
+    home = keys.device
+    cdev = _comm_device(group, keys)
     if keys.numel():
-        mm = torch.stack([keys[-1], -keys[0]]).to(torch.int64)
+        wide = (keys.min() < 0) | (keys.max() >= (1 << 32))
     else:
-        mm = torch.tensor([-(1 << 63), -(1 << 63)], dtype=torch.int64, device=dev)
-    dist.all_reduce(mm, op=dist.ReduceOp.MAX, group=group)
-    mx = mm.tolist()
-    kmax, kmin = mx[0], -mx[1]
-    if kmax < kmin:   # no rank has a vertex in this window
-        return keys[:0], [c[:0] for c in cols]
-    bounds = torch.tensor(owner_bounds(kmin, kmax, world), dtype=torch.int64, device=dev)
-    cuts = torch.searchsorted(keys, bounds, right=False) if world > 1 else bounds
-    edges = torch.cat([torch.zeros(1, dtype=torch.int64, device=dev), cuts,
-                       torch.full((1,), keys.numel(), dtype=torch.int64, device=dev)])
-    send = (edges[1:] - edges[:-1]).to(torch.int64)
+        wide = torch.zeros((), dtype=torch.bool, device=home)
+    send = torch.stack([torch.tensor(counts, dtype=torch.int64, device=home),
+                        wide.to(torch.int64).expand(world)], dim=1).to(cdev)
     recv = torch.empty_like(send)
     dist.all_to_all_single(recv, send, group=group)
-    sr = torch.cat([send, recv]).tolist()   # one host read for both
-    send_l, recv_l = sr[:world], sr[world:]
-    total = sum(recv_l)
-    # keys travel as 32-bit offsets from the global minimum when the window's span allows (12-byte
-    # instead of 16-byte rows for a Long partial)
-    narrow = kmax - kmin < (1 << 32)
-    kpart = (keys - kmin).to(torch.int32) if narrow else keys.contiguous()
-    # one all-to-all of packed rows (key bytes, then each column's bytes) instead of one per column:
-    # fewer collective launches and one rendezvous per window
+    rl = recv.tolist()                                   # the exchange's one host read
+    recv_counts = [r[0] for r in rl]
+    wide_any = any(r[1] for r in rl)
+    kpart = keys.contiguous() if wide_any else keys.to(torch.int32)
     parts = [kpart] + [c.contiguous() for c in cols]
     widths = [p.element_size() for p in parts]
     row = sum(widths)
-    packed = torch.cat([p.view(torch.uint8).view(-1, w) for p, w in zip(parts, widths)], dim=1)
-    rp = torch.empty((total, row), dtype=torch.uint8, device=dev)
-    dist.all_to_all_single(rp, packed, recv_l, send_l, group=group)
+    packed = torch.cat([p.view(torch.uint8).view(-1, w) for p, w in zip(parts, widths)], dim=1).to(cdev)
+    rp = torch.empty((sum(recv_counts), row), dtype=torch.uint8, device=cdev)
+    dist.all_to_all_single(rp, packed, recv_counts, list(counts), group=group)
+    rp = rp.to(home)
     out, at = [], 0
     for p, w in zip(parts, widths):
         out.append(rp[:, at:at + w].contiguous().view(p.dtype).view(-1))
         at += w
-    rk = ((out[0].to(torch.int64) & 0xFFFFFFFF) + kmin) if narrow else out[0]
+    rk = out[0] if wide_any else (out[0].to(torch.int64) & 0xFFFFFFFF)
     return rk, out[1:]
 
 
-def reduce_window(local_reduce, src, dst, val, direction: int, op: int, group=None):
-    """reduceOnEdges over a window whose edges are spread over the ranks of `group`.
-    Returns this rank's owned (vertex, value) pairs, vertices ascending."""
-    k, v = local_reduce(src, dst, val, direction, op)
-    if dist.get_world_size(group) == 1:   # the only rank owns every vertex: no exchange, no merge
+def reduce_window(partials, merge, src, dst, val, direction: int, op: int, init=None, group=None):
+    """reduceOnEdges (init None) / foldNeighbors over a window whose edges are spread over the ranks of
+    `group`.  partials(src, dst, val, direction, op, nparts) -> (keys, vals, counts);
+    merge(keys, vals, op, init) -> (keys, vals).  Returns this rank's owned (vertex, value) pairs,
+    vertices ascending."""
+    world = dist.get_world_size(group)
+    k, v, counts = partials(src, dst, val, direction, op, world)
+    if world == 1 and init is None:   # the only rank owns every vertex: nothing to exchange or merge
         return k, v
-    rk, (rv,) = exchange_sorted(k, [v], group)
-    if rk.numel() == 0:
-        return rk, rv
-    return local_reduce(rk, rk, rv, 1, merge_op(op))
+    rk, (rv,) = exchange_partials(k, [v], counts, group)
+    return merge(rk, rv, op, init)
 
 
-def fold_degree_max_window(local_fold, local_reduce, src, dst, direction: int, init_max: int, group=None):
-    """foldNeighbors(degree, max-neighbour) across ranks: degrees merge by SUM, maxima by MAX."""
-    k, d, m = local_fold(src, dst, direction, init_max)
-    if dist.get_world_size(group) == 1:
-        return k, d, m
-    rk, (rd, rm) = exchange_sorted(k, [d, m], group)
-    if rk.numel() == 0:
-        return rk, rd, rm
-    k1, d1 = local_reduce(rk, rk, rd, 1, SUM)
-    _, m1 = local_reduce(rk, rk, rm, 1, MAX)
-    return k1, d1, m1
+def fold_degree_max_window(partials, merge, src, dst, direction: int, init_max: int, group=None):
+    """foldNeighbors(degree, max neighbour) across ranks: degrees merge by SUM, maxima by MAX, then the
+    fold's init.  partials(src, dst, direction, nparts) -> (keys, deg, mx, counts);
+    merge(keys, deg, mx, init_max) -> (keys, deg, mx)."""
+    world = dist.get_world_size(group)
+    k, d, m, counts = partials(src, dst, direction, world)
+    if world == 1:
+        return merge(k, d, m, init_max) if init_max != -(1 << 63) else (k, d, m)
+    rk, (rd, rm) = exchange_partials(k, [d, m], counts, group)
+    return merge(rk, rd, rm, init_max)
+
+
+def engine_halves(eng):
+    """The Engine's partials / merge entry points in the shape reduce_window / fold_degree_max_window take."""
+    return (eng.reduce_partials, eng.merge_partials, eng.fold_degree_max_partials, eng.merge_degree_max_partials)
 
 
 def gather_window(src: torch.Tensor, dst: torch.Tensor, group=None):

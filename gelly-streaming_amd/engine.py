@@ -297,6 +297,139 @@ class Engine:
         self._check(self._L.gs_window_triangles_part(self.ctx, ctypes.byref(b), part, nparts, ctypes.byref(cnt)))
         return cnt.value
 
+    # -- multi-GPU keyBy halves (gs_dist.hip) --------------------------------------------------------
+    def reduce_partials(self, src, dst, val, direction, op, nparts: int):
+        """gs_window_reduce_partials: this slice's per-vertex partials grouped by owner (gs_owner_of).
+        Returns (keys, partials, owner_counts: list of nparts ints)."""
+        b, keep, dev = self._batch(src, dst, None if op == L.GS_OP_COUNT else val)
+        R = self._records(b.n, direction)
+        odt = np.int64 if op == L.GS_OP_COUNT else L.NP_DTYPE[b.val_dtype]
+        keys, vals = self._empty(dev, R, np.int64), self._empty(dev, R, odt)
+        n_out, counts = ctypes.c_uint64(0), (ctypes.c_uint64 * nparts)()
+        out = L.GsPartialsOut(_ptr(keys), _ptr(vals), None, R, ctypes.pointer(n_out), counts,
+                              L.GS_MEM_DEVICE if dev else L.GS_MEM_HOST, 0)
+        self._check(self._L.gs_window_reduce_partials(self.ctx, ctypes.byref(b), int(direction), int(op), nparts,
+                                                      ctypes.byref(out)))
+        U = n_out.value
+        return keys[:U], vals[:U], list(counts)
+
+    def fold_degree_max_partials(self, src, dst, direction, nparts: int):
+        """gs_window_fold_degree_max_partials: (keys, degrees, maxima, owner_counts), grouped by owner."""
+        b, keep, dev = self._batch(src, dst, None)
+        R = self._records(b.n, direction)
+        keys, deg, mx = (self._empty(dev, R, np.int64) for _ in range(3))
+        n_out, counts = ctypes.c_uint64(0), (ctypes.c_uint64 * nparts)()
+        out = L.GsPartialsOut(_ptr(keys), _ptr(deg), _ptr(mx), R, ctypes.pointer(n_out), counts,
+                              L.GS_MEM_DEVICE if dev else L.GS_MEM_HOST, 0)
+        self._check(self._L.gs_window_fold_degree_max_partials(self.ctx, ctypes.byref(b), int(direction), nparts,
+                                                               ctypes.byref(out)))
+        U = n_out.value
+        return keys[:U], deg[:U], mx[:U], list(counts)
+
+    def _partial_batch(self, keys, vals, vals2=None):
+        dev = _is_torch(keys)
+        if not dev:
+            keys = np.ascontiguousarray(keys, dtype=np.int64)
+            vals = np.ascontiguousarray(vals)
+            vals2 = None if vals2 is None else np.ascontiguousarray(vals2, dtype=np.int64)
+        else:
+            keys, vals = keys.contiguous(), vals.contiguous()
+            vals2 = None if vals2 is None else vals2.contiguous()
+        pb = L.GsPartialBatch(_ptr(keys), _ptr(vals), _ptr(vals2), len(keys), _gs_dtype(vals),
+                              L.GS_MEM_DEVICE if dev else L.GS_MEM_HOST)
+        return pb, (keys, vals, vals2), dev
+
+    def merge_partials(self, keys, vals, op, init=None):
+        """gs_merge_partials: an owner's received partials -> (keys, values), keys ascending."""
+        pb, keep, dev = self._partial_batch(keys, vals)
+        n = pb.n
+        odt = np.int64 if op == L.GS_OP_COUNT else L.NP_DTYPE[pb.val_dtype]
+        ko, vo = self._empty(dev, n, np.int64), self._empty(dev, n, odt)
+        n_out = ctypes.c_uint64(0)
+        out = L.GsVertexOut(_ptr(ko), _ptr(vo), n, ctypes.pointer(n_out), L.GS_MEM_DEVICE if dev else L.GS_MEM_HOST, 0)
+        ia = None if init is None else np.array([init], dtype=odt)
+        self._check(self._L.gs_merge_partials(self.ctx, ctypes.byref(pb), int(op),
+                                              None if ia is None else ia.ctypes.data_as(ctypes.c_void_p),
+                                              ctypes.byref(out)))
+        U = n_out.value
+        return ko[:U], vo[:U]
+
+    def merge_degree_max_partials(self, keys, deg, mx, init_max=-(1 << 63)):
+        pb, keep, dev = self._partial_batch(keys, deg, mx)
+        n = pb.n
+        ko, do, mo = (self._empty(dev, n, np.int64) for _ in range(3))
+        n_out = ctypes.c_uint64(0)
+        out = L.GsDegreeOut(_ptr(ko), _ptr(do), _ptr(mo), n, ctypes.pointer(n_out),
+                            L.GS_MEM_DEVICE if dev else L.GS_MEM_HOST, 0)
+        self._check(self._L.gs_merge_degree_max_partials(self.ctx, ctypes.byref(pb), int(init_max), ctypes.byref(out)))
+        U = n_out.value
+        return ko[:U], do[:U], mo[:U]
+
+    def owner_of(self, vertex: int, nparts: int) -> int:
+        return int(self._L.gs_owner_of(int(vertex), nparts))
+
+    # -- ctx-owned RCCL communicator -----------------------------------------------------------------
+    @staticmethod
+    def comm_unique_id() -> bytes:
+        buf = ctypes.create_string_buffer(128)
+        st = L.load().gs_comm_unique_id(buf)
+        if st != L.GS_OK:
+            raise GsError(st, "gs_comm_unique_id failed (RCCL not found?)")
+        return buf.raw
+
+    def comm_init(self, nranks: int, rank: int, unique_id: bytes):
+        buf = ctypes.create_string_buffer(bytes(unique_id), 128)
+        self._check(self._L.gs_comm_init(self.ctx, nranks, rank, buf))
+
+    def comm_destroy(self):
+        self._check(self._L.gs_comm_destroy(self.ctx))
+
+    def comm_allreduce_sum(self, value: int) -> int:
+        v = ctypes.c_uint64(value & ((1 << 64) - 1))
+        self._check(self._L.gs_comm_allreduce_sum_u64(self.ctx, ctypes.byref(v)))
+        return v.value
+
+    def reduce_dist(self, src, dst, val, direction, op, init=None):
+        """gs_window_reduce_dist: this rank's slice through partials -> RCCL all-to-all -> merge; returns
+        the (keys, values) this rank owns."""
+        b, keep, dev = self._batch(src, dst, None if op == L.GS_OP_COUNT else val)
+        odt = np.int64 if op == L.GS_OP_COUNT else L.NP_DTYPE[b.val_dtype]
+        cap = self._records(b.n, direction) + 1024   # a guess; more owned vertices: gs_fetch_last_output
+        keys, vals = self._empty(dev, cap, np.int64), self._empty(dev, cap, odt)
+        n_out = ctypes.c_uint64(0)
+        out = L.GsVertexOut(_ptr(keys), _ptr(vals), cap, ctypes.pointer(n_out), L.GS_MEM_DEVICE if dev else L.GS_MEM_HOST, 0)
+        ia = None if init is None else np.array([init], dtype=odt)
+        st = self._L.gs_window_reduce_dist(self.ctx, ctypes.byref(b), int(direction), int(op),
+                                          None if ia is None else ia.ctypes.data_as(ctypes.c_void_p), ctypes.byref(out))
+        if st == L.GS_ECAPACITY:   # more owned vertices than this guess: fetch the staged rows (no recompute)
+            U = n_out.value
+            keys, vals = self._empty(dev, U, np.int64), self._empty(dev, U, odt)
+            out = L.GsVertexOut(_ptr(keys), _ptr(vals), U, ctypes.pointer(n_out),
+                                L.GS_MEM_DEVICE if dev else L.GS_MEM_HOST, 0)
+            st = self._L.gs_fetch_last_output(self.ctx, ctypes.byref(out))
+        self._check(st)
+        U = n_out.value
+        return keys[:U], vals[:U]
+
+    def fold_degree_max_dist(self, src, dst, direction, init_max=-(1 << 63)):
+        b, keep, dev = self._batch(src, dst, None)
+        cap = self._records(b.n, direction) + 1024
+        keys, deg, mx = (self._empty(dev, cap, np.int64) for _ in range(3))
+        n_out = ctypes.c_uint64(0)
+        out = L.GsDegreeOut(_ptr(keys), _ptr(deg), _ptr(mx), cap, ctypes.pointer(n_out),
+                            L.GS_MEM_DEVICE if dev else L.GS_MEM_HOST, 0)
+        st = self._L.gs_window_fold_degree_max_dist(self.ctx, ctypes.byref(b), int(direction), int(init_max),
+                                                    ctypes.byref(out))
+        if st == L.GS_ECAPACITY:
+            U = n_out.value
+            keys, deg, mx = (self._empty(dev, U, np.int64) for _ in range(3))
+            out = L.GsDegreeOut(_ptr(keys), _ptr(deg), _ptr(mx), U, ctypes.pointer(n_out),
+                                L.GS_MEM_DEVICE if dev else L.GS_MEM_HOST, 0)
+            st = self._L.gs_fetch_last_degree_output(self.ctx, ctypes.byref(out))
+        self._check(st)
+        U = n_out.value
+        return keys[:U], deg[:U], mx[:U]
+
     # -- synthetic streams (device) ----------------------------------------------------------------
     def generate_rmat(self, scale, n, seed, a=0.57, b=0.19, c=0.19, permute=True, no_self_loops=False,
                       first_edge=0, out=None):

@@ -56,7 +56,8 @@ enum {
   GS_EDEVICE = -3,      /* HIP runtime / kernel failure                                     */
   GS_ECOMM = -4,        /* collective failure (multi-GPU)                                   */
   GS_ENOMEM = -5,       /* device or pinned allocation failed                               */
-  GS_EUNSUPPORTED = -6  /* op/dtype combination not offered by the engine                   */
+  GS_EUNSUPPORTED = -6, /* op/dtype combination not offered by the engine                   */
+  GS_EAGAIN = -7        /* gs_stream_poll: no window result ready (non-blocking poll)        */
 };
 
 /* org.apache.flink.graph.EdgeDirection, same ordinals (IN, OUT, ALL).
@@ -208,6 +209,70 @@ GS_API gs_status gs_window_triangles(gs_ctx* ctx, const gs_edge_batch* batch, ui
 GS_API gs_status gs_window_triangles_part(gs_ctx* ctx, const gs_edge_batch* batch, uint32_t part,
                                           uint32_t nparts, uint64_t* partial_count);
 
+/* Two-phase output without recomputation: after a window call returned GS_ECAPACITY (with the needed
+ * size in *n_out) and before the next call on the ctx, deliver the rows it left staged.  Covers
+ * gs_window_reduce / gs_window_fold / gs_merge_partials / gs_window_reduce_dist (gs_fetch_last_output)
+ * and the degree / max variants (gs_fetch_last_degree_output). */
+GS_API gs_status gs_fetch_last_output(gs_ctx* ctx, gs_vertex_out* out);
+GS_API gs_status gs_fetch_last_degree_output(gs_ctx* ctx, gs_degree_out* out);
+
+/* ---- multi-GPU keyBy (SimpleEdgeStream.java:159-167) ---------------------------------- */
+/* A window spread over nparts ranks: every rank pre-reduces its own slice, the per-vertex partials
+ * travel to their owner, the owner merges them.  owner(v) = gs_owner_of(v, nparts), a hash of the
+ * vertex as Flink's keyBy is (which subtask owns a vertex is not observable in the output).  The
+ * exchange between the halves is the caller's (e.g. an all-to-all in torch.distributed or the JVM), or
+ * the ctx-owned RCCL communicator (gs_comm_init + gs_window_*_dist). */
+GS_API uint32_t gs_owner_of(int64_t vertex, uint32_t nparts);
+
+/* Partials grouped by owner: rows of owner 0, then owner 1, ...; keys ascend within an owner. */
+typedef struct gs_partials_out {
+  int64_t* keys;           /* [capacity]                                                        */
+  void* vals;              /* [capacity] partial values (batch dtype; I64 for COUNT; degrees)   */
+  int64_t* vals2;          /* [capacity] degree/max fold: maxima (NULL otherwise)               */
+  uint64_t capacity;
+  uint64_t* n_out;         /* host: rows written / needed                                       */
+  uint64_t* owner_counts;  /* host: [nparts] rows per owner                                     */
+  int32_t mem;
+  int32_t reserved;
+} gs_partials_out;
+
+/* Rows an owner received (any order, any number of rows per vertex). */
+typedef struct gs_partial_batch {
+  const int64_t* keys;
+  const void* vals;
+  const int64_t* vals2;    /* degree/max fold: maxima                                           */
+  uint64_t n;
+  int32_t val_dtype;       /* gs_dtype of vals (I64 for COUNT partials and degrees)             */
+  int32_t mem;
+} gs_partial_batch;
+
+/* The first half of reduceOnEdges / foldNeighbors across ranks: this rank's slice reduced with `op`
+ * (no init; COUNT partials are I64 counts), partitioned by owner on the device. */
+GS_API gs_status gs_window_reduce_partials(gs_ctx* ctx, const gs_edge_batch* batch, int32_t dir, int32_t op,
+                                           uint32_t nparts, gs_partials_out* out);
+/* The same for the degree / max-neighbour fold: vals = degrees (I64), vals2 = maxima (no init). */
+GS_API gs_status gs_window_fold_degree_max_partials(gs_ctx* ctx, const gs_edge_batch* batch, int32_t dir,
+                                                    uint32_t nparts, gs_partials_out* out);
+/* The second half: merge the partials this owner received with `op` (COUNT partials add up);
+ * `init` (NULL for reduceOnEdges) is foldNeighbors' initial value, applied once per vertex. */
+GS_API gs_status gs_merge_partials(gs_ctx* ctx, const gs_partial_batch* partials, int32_t op, const void* init,
+                                   gs_vertex_out* out);
+GS_API gs_status gs_merge_degree_max_partials(gs_ctx* ctx, const gs_partial_batch* partials, int64_t init_max,
+                                              gs_degree_out* out);
+
+/* ctx-owned RCCL communicator (one rank per ctx; RCCL is loaded at gs_comm_init time).  Rank 0 calls
+ * gs_comm_unique_id and ships the 128 bytes to every rank out of band; every rank calls gs_comm_init. */
+GS_API gs_status gs_comm_unique_id(void* id128);
+GS_API gs_status gs_comm_init(gs_ctx* ctx, int32_t nranks, int32_t rank, const void* id128);
+GS_API gs_status gs_comm_destroy(gs_ctx* ctx);
+/* *value = the sum of *value over the communicator's ranks (e.g. per-rank triangle counts). */
+GS_API gs_status gs_comm_allreduce_sum_u64(gs_ctx* ctx, uint64_t* value);
+/* Partials -> RCCL all-to-all (counts, then rows) -> merge: `out` receives the vertices this rank owns. */
+GS_API gs_status gs_window_reduce_dist(gs_ctx* ctx, const gs_edge_batch* batch, int32_t dir, int32_t op,
+                                       const void* init, gs_vertex_out* out);
+GS_API gs_status gs_window_fold_degree_max_dist(gs_ctx* ctx, const gs_edge_batch* batch, int32_t dir,
+                                                int64_t init_max, gs_degree_out* out);
+
 /* Candidate records of one window as produced by GenerateCandidateEdges (gs_pair_out layout). */
 typedef struct gs_pair_batch {
   const int64_t* a;
@@ -238,6 +303,67 @@ GS_API gs_status gs_window_count_candidates(gs_ctx* ctx, const gs_pair_batch* pa
 GS_API gs_status gs_parse_edges_text(gs_ctx* ctx, const char* text, uint64_t bytes, int32_t in_mem, int64_t* src,
                                      int64_t* dst, int64_t* ts, uint64_t capacity, int32_t out_mem,
                                      uint64_t* n_out, uint64_t* bad_record);
+
+/* ---- the window-buffer operator: event-time tumbling windows over a record stream -------- */
+/* Replaces slice(size[, dir]) -> keyBy(vertex).timeWindow(size) -> the window function for the built-in
+ * operators (SimpleEdgeStream.java:153-171, GraphWindowStream.java:49-53, 62-182; Flink 1.0.3
+ * TumblingEventTimeWindows + EventTimeTrigger): records are appended with their event timestamps,
+ * buffered per window (start = ts - ts % size, Java remainder) in pinned host memory, and a window
+ * fires when the watermark reaches end - 1; its result carries the timestamp end - 1.  A fired
+ * window's columns are copied to HBM on the operator's own copy stream, so window k+1's copy overlaps
+ * window k's kernels.  Results come back in firing order from gs_stream_poll.  Records of a window
+ * that already fired are dropped and counted (late). */
+typedef struct gs_stream gs_stream;
+enum { GS_STREAM_REDUCE = 0, GS_STREAM_FOLD = 1, GS_STREAM_DEGREE_MAX = 2, GS_STREAM_TRIANGLES = 3 };
+enum { GS_WATERMARK_EXPLICIT = 0,    /* gs_stream_watermark only                                   */
+       GS_WATERMARK_ASCENDING = 1 }; /* AscendingTimestampExtractor: max timestamp seen - 1        */
+enum { GS_STAGE_PINNED = 0, GS_STAGE_DIRECT = 1 };
+
+typedef struct gs_stream_config {
+  int64_t window_ms;       /* tumbling window size (Time.milliseconds)                          */
+  int32_t kind;            /* GS_STREAM_*: reduceOnEdges / foldNeighbors / degree-max / triangles */
+  int32_t dir;             /* gs_dir (GS_STREAM_TRIANGLES: slice(ALL) regardless)               */
+  int32_t op;              /* gs_op for REDUCE / FOLD                                           */
+  int32_t val_dtype;       /* gs_dtype of appended values (GS_NONE: no value column)            */
+  int32_t watermark_mode;  /* GS_WATERMARK_*                                                    */
+  int32_t staging;         /* GS_STAGE_PINNED: records copied into pinned window buffers, the
+                              window's H2D at firing; GS_STAGE_DIRECT: each append is copied straight
+                              into the window's device columns (pageable H2D on the copy stream)  */
+  const void* init;        /* FOLD: one value of the result dtype (copied at create)           */
+  int64_t init_max;        /* DEGREE_MAX: initial maximum                                       */
+  uint64_t max_window_edges; /* expected window size: pinned / device buffers are sized for it  */
+} gs_stream_config;
+
+typedef struct gs_window_result {
+  int64_t window_start, window_end;
+  int64_t max_timestamp;   /* end - 1: the timestamp of every record this window emits          */
+  uint64_t edges;          /* records the window held                                           */
+  uint64_t n_vertices;     /* rows in keys / vals / vals2                                       */
+  const int64_t* keys;     /* pinned host rows, valid until the next gs_stream_poll             */
+  const void* vals;        /* REDUCE / FOLD values; DEGREE_MAX degrees (I64)                    */
+  const int64_t* vals2;    /* DEGREE_MAX maxima                                                 */
+  uint64_t triangles;      /* TRIANGLES: exact count                                            */
+  int32_t triangles_ref;   /* TRIANGLES: the Integer the reference emits                        */
+  int32_t has_output;      /* 0: the reference emits no record for this window                  */
+  double latency_ms;       /* host time from the window's firing to its result                  */
+} gs_window_result;
+
+typedef struct gs_stream_stats_t {
+  int64_t watermark;
+  uint64_t open_windows, fired_windows, pending_windows, late_records, edges_fired;
+} gs_stream_stats_t;
+
+GS_API gs_status gs_stream_create(gs_ctx* ctx, const gs_stream_config* cfg, gs_stream** out);
+GS_API void gs_stream_destroy(gs_stream* stream);
+/* Append n records in arrival order (host columns; `val` NULL for NullValue streams). */
+GS_API gs_status gs_stream_append(gs_stream* stream, const int64_t* src, const int64_t* dst, const void* val,
+                                  const int64_t* ts, uint64_t n);
+GS_API gs_status gs_stream_watermark(gs_stream* stream, int64_t watermark);
+/* End of a finite source: watermark Long.MAX_VALUE, every open window fires. */
+GS_API gs_status gs_stream_flush(gs_stream* stream);
+/* The next window result in firing order; GS_EAGAIN when none is ready (wait = 0). */
+GS_API gs_status gs_stream_poll(gs_stream* stream, int32_t wait, gs_window_result* out);
+GS_API gs_status gs_stream_stats(const gs_stream* stream, gs_stream_stats_t* out);
 
 /* ---- synthetic streams (bit-identical to oracle/gs_oracle.c) ------------------------ */
 /* R-MAT: 2^scale vertices, probabilities a, b, c (d = 1-a-b-c) as 32-bit fixed point,

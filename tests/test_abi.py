@@ -53,17 +53,28 @@ def test_engine_fails_loudly_without_device(pkg):
         pkg.Engine(0)
 
 
+STRUCTS = {"gs_config": "GsConfig", "gs_edge_batch": "GsEdgeBatch", "gs_vertex_out": "GsVertexOut",
+           "gs_degree_out": "GsDegreeOut", "gs_csr_out": "GsCsrOut", "gs_pair_out": "GsPairOut",
+           "gs_pair_batch": "GsPairBatch", "gs_stage_times": "GsStageTimes", "gs_partials_out": "GsPartialsOut",
+           "gs_partial_batch": "GsPartialBatch", "gs_stream_config": "GsStreamConfig",
+           "gs_window_result": "GsWindowResult", "gs_stream_stats_t": "GsStreamStats"}
+
+
 def test_struct_layouts_match_header(pkg):
-    """ctypes mirrors of the ABI structs have the sizes the C compiler gives them."""
+    """ctypes mirrors of the ABI structs have the sizes and field offsets the C compiler gives them."""
     from gelly_streaming_amd import _lib
-    src = "#include <stdio.h>\n#include \"gelly_hip.h\"\nint main(){printf(\"%zu %zu %zu %zu %zu %zu %zu\\n\"," \
-          "sizeof(gs_config),sizeof(gs_edge_batch),sizeof(gs_vertex_out),sizeof(gs_degree_out)," \
-          "sizeof(gs_csr_out),sizeof(gs_pair_out),sizeof(gs_stage_times));}"
+    lines, want = [], []
+    for c_name, py_name in STRUCTS.items():
+        t = getattr(_lib, py_name)
+        lines.append(f'printf("%zu\\n", sizeof({c_name}));')
+        want.append(ctypes.sizeof(t))
+        for f, _ in t._fields_:
+            lines.append(f'printf("%zu\\n", offsetof({c_name}, {f}));')
+            want.append(getattr(t, f).offset)
+    src = "#include <stdio.h>\n#include <stddef.h>\n#include \"gelly_hip.h\"\nint main(){" + "".join(lines) + "}"
     tmp = ROOT / "gpurun_out"
     tmp.mkdir(exist_ok=True)
     (tmp / "sz.c").write_text(src)
     subprocess.run(["gcc", "-I", str(ROOT / "include"), str(tmp / "sz.c"), "-o", str(tmp / "sz")], check=True)
     got = [int(x) for x in subprocess.run([str(tmp / "sz")], capture_output=True, text=True).stdout.split()]
-    want = [ctypes.sizeof(t) for t in (_lib.GsConfig, _lib.GsEdgeBatch, _lib.GsVertexOut, _lib.GsDegreeOut,
-                                       _lib.GsCsrOut, _lib.GsPairOut, _lib.GsStageTimes)]
     assert got == want

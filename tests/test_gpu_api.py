@@ -254,9 +254,10 @@ def test_count_candidates_edge_cases(engine, oracle):
     # all candidates -> no output; empty window -> no output
     assert engine.count_candidates(a, b, np.ones(n, np.uint8))[2] is False
     assert engine.count_candidates(a[:0], b[:0], f[:0]) == (0, 0, False, 0)
-    # IDs spanning 2^32 or more are refused, loudly
-    with pytest.raises(Exception, match="UNSUPPORTED|span"):
-        engine.count_candidates(np.array([0, 1 << 40]), np.array([0, 1]), np.array([0, 1], np.uint8))
+    # IDs spanning 2^32 or more go through relabeled IDs (host columns)
+    a2, b2, f2 = np.array([0, 1 << 40, 0, 1 << 40]), np.array([0, 1, 0, 1]), np.array([0, 1, 1, 0], np.uint8)
+    want = oracle.count_candidates(a2, b2, f2)
+    assert engine.count_candidates(a2, b2, f2) == (want[1], want[0], want[2], want[3])
 
 
 def test_count_candidates_large_window(engine, oracle):
@@ -368,3 +369,31 @@ def test_triangle_table_overflow_is_an_error_not_a_hang(pkg, oracle):
         assert ei.value.status == L.GS_EDEVICE and "hash set" in str(ei.value)
     with pkg.Engine(0) as e:   # the normal engine on the same window
         assert e.triangles(S, D)[0] == oracle.window_triangles_fwd(s, d)[1]
+
+
+@pytest.mark.parametrize("loops", [False, True])
+def test_triangles_arbitrary_long_ids(engine, oracle, loops):
+    """IDs spanning the whole Long range (sparse, negative): the window is relabeled (order-preserving
+    compact IDs) and the count equals the reference rule on the ORIGINAL IDs — with self-loops too, where
+    the self-pair term depends on the JDK HashSet order of the original Longs (WindowTriangles.java:95-105)."""
+    rng = np.random.default_rng(7 + loops)
+    s, d = oracle.gen_rmat(11, 60_000, 0x5EED04, no_self_loops=not loops)
+    ids = np.unique(rng.integers(-(1 << 62), 1 << 62, 5000))
+    ids = rng.permutation(ids)[: 1 << 11]
+    S_, D_ = ids[s], ids[d]
+    w, ex, has, tree = oracle.window_triangles_ref(S_, D_)
+    assert not tree
+    got = engine.triangles(*(torch.from_numpy(x).cuda() for x in (S_, D_)))
+    assert got == (ex, w, has)
+    if not loops:   # relabeling is order-preserving: the same count as the dense window
+        assert got[0] == engine.triangles(*(torch.from_numpy(x).cuda() for x in (s, d)))[0]
+
+
+def test_count_candidates_ids_spanning_2_pow_32(engine, oracle):
+    """Stage 2 over candidate records whose IDs span more than 2^32: grouped through relabeled IDs."""
+    s, d = oracle.gen_rmat(10, 20_000, 5, no_self_loops=True)
+    ids = np.random.default_rng(3).integers(-(1 << 60), 1 << 60, 1 << 10)
+    a, b, f, _ = oracle.window_candidates(ids[s], ids[d])
+    want = oracle.count_candidates(a, b, f)
+    got = engine.count_candidates(*(torch.from_numpy(np.ascontiguousarray(x)).cuda() for x in (a, b, f)))
+    assert (got[1], got[0], got[2], got[3]) == want

@@ -1,0 +1,123 @@
+"""GPU: the multi-GPU keyBy halves of the C ABI (gs_dist.hip) and the ctx-owned RCCL communicator.
+
+  - gs_window_reduce_partials / gs_window_fold_degree_max_partials: rows grouped by gs_owner_of (the
+    device split equals the numpy restatement), ascending within an owner, counts per owner;
+  - world 2 over gloo between two processes sharing this GPU: distributed.reduce_window /
+    fold_degree_max_window through the ENGINE's halves (partials on the device, rows exchanged on the
+    host, merge on the device) equal the whole-window oracle for every op, direction and init;
+  - world 1 over RCCL through the library's own communicator: gs_window_reduce_dist /
+    gs_window_fold_degree_max_dist equal the single-GPU window, gs_comm_allreduce_sum_u64 sums."""
+import os
+import sys
+from pathlib import Path
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+ROOT = Path(__file__).resolve().parent.parent
+sys.path.insert(0, str(ROOT / "tests"))
+from test_distributed_gloo import _free_port, check_cases, owner_np, run_cases  # noqa: E402
+
+
+@pytest.mark.parametrize("nparts", [1, 2, 3, 8, 64])
+def test_partials_grouped_by_owner(engine, oracle, nparts):
+    n = 300_001
+    s, d = oracle.gen_rmat(16, n, 0x5EED02)
+    v = oracle.gen_values(n, 3, oracle.DT_I64)
+    S, D, V = (torch.from_numpy(x).cuda() for x in (s, d, v))
+    for direction in (1, 2):
+        k, p, counts = engine.reduce_partials(S, D, V, direction, 0, nparts)
+        k, p = k.cpu().numpy(), p.cpu().numpy()
+        rk, rv = oracle.window_reduce(s, d, v, direction, 0)
+        assert sum(counts) == len(rk) == len(k)
+        own = owner_np(k, nparts)
+        bounds = np.concatenate([[0], np.cumsum(counts)])
+        for o in range(nparts):
+            seg = slice(bounds[o], bounds[o + 1])
+            assert (own[seg] == o).all() and (np.diff(k[seg]) > 0).all()
+        o = np.argsort(k)
+        assert np.array_equal(k[o], rk) and np.array_equal(p[o], rv)
+        assert all(engine.owner_of(int(x), nparts) == int(y) for x, y in zip(k[:50], own[:50]))
+    kd, dg, mx, counts = engine.fold_degree_max_partials(S, D, 0, nparts)
+    o = np.argsort(kd.cpu().numpy())
+    want = oracle.window_fold_degree_max(s, d, 0)
+    for g, w in zip((kd, dg, mx), want):
+        assert np.array_equal(g.cpu().numpy()[o], w)
+
+
+def test_merge_partials_ops(engine, oracle):
+    """The owner half alone: rows of several ranks for the same vertices merge by op (COUNT by SUM)."""
+    rng = np.random.default_rng(5)
+    k = rng.integers(0, 1 << 18, 200_000).astype(np.int64)
+    v = rng.integers(-(1 << 40), 1 << 40, 200_000).astype(np.int64)
+    K, Vv = torch.from_numpy(k).cuda(), torch.from_numpy(v).cuda()
+    for op, mop in ((0, 0), (1, 1), (2, 2), (3, 0)):
+        gk, gv = engine.merge_partials(K, Vv, op)
+        wk, wv = oracle.window_reduce(k, k, v, 1, mop)
+        assert np.array_equal(gk.cpu().numpy(), wk) and np.array_equal(gv.cpu().numpy(), wv)
+    gk, gv = engine.merge_partials(K, Vv, 1, init=-5)
+    wk, wv = oracle.window_fold(k, k, v, 1, 1, -5)
+    assert np.array_equal(gv.cpu().numpy(), wv)
+
+
+def _worker(rank, world, port, q):
+    sys.path.insert(0, str(ROOT))
+    sys.path.insert(0, str(ROOT / "tests"))
+    import __graft_entry__ as ge
+    pkg = ge.load_package()
+    from gelly_streaming_amd import distributed as D
+    orc = ge.load_oracle()
+    torch.cuda.set_device(0)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    n = 40000
+    s, d = orc.gen_rmat(12, n, 0x5EED03, a=0.65, b=0.15, c=0.15, permute=False, first_edge=rank * n)
+    v = orc.gen_values(n, 5, orc.DT_I64, first_edge=rank * n)
+    eng = pkg.Engine(0)
+    res = run_cases(D, D.engine_halves(eng), s, d, v, to_dev=lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda())
+    eng.close()
+    q.put((rank, res))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_engine_halves_two_ranks_gloo(oracle):
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = dict(q.get(timeout=100) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    n = 40000
+    s, d = oracle.gen_rmat(12, 2 * n, 0x5EED03, a=0.65, b=0.15, c=0.15, permute=False)
+    v = oracle.gen_values(2 * n, 5, oracle.DT_I64)
+    check_cases(oracle, out, world, s, d, v)
+
+
+def test_rccl_world_one_through_the_abi(pkg, oracle):
+    n = 250_000
+    s, d = oracle.gen_rmat(15, n, 0x5EED02)
+    v = oracle.gen_values(n, 8, oracle.DT_I64)
+    S, D, V = (torch.from_numpy(x).cuda() for x in (s, d, v))
+    with pkg.Engine(0) as e:
+        e.comm_init(1, 0, pkg.Engine.comm_unique_id())
+        for direction in (0, 1, 2):
+            for op in (0, 1, 2, 3):
+                gk, gv = e.reduce_dist(S, D, V, direction, op)
+                wk, wv = oracle.window_reduce(s, d, v, direction, op)
+                assert np.array_equal(gk.cpu().numpy(), wk) and np.array_equal(gv.cpu().numpy(), wv)
+        gk, gv = e.reduce_dist(S, D, V, 1, 0, init=10)
+        assert np.array_equal(gv.cpu().numpy(), oracle.window_fold(s, d, v, 1, 0, 10)[1])
+        got = e.fold_degree_max_dist(S, D, 2)
+        for g, w in zip(got, oracle.window_fold_degree_max(s, d, 2)):
+            assert np.array_equal(g.cpu().numpy(), w)
+        assert e.comm_allreduce_sum(12345) == 12345
+        e.comm_destroy()

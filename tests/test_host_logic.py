@@ -45,11 +45,19 @@ def test_undirected_and_reverse_columns(pkg):
     assert list(zip(r.src, r.dst, r.val)) == [(2, 1, 12), (3, 1, 13)]
 
 
-def test_owner_bounds_partition(pkg):
+def test_merge_op_and_owner_library(pkg):
+    """COUNT partials merge by SUM; gs_owner_of (host-callable, no device needed) equals the numpy
+    restatement the CPU exchange test uses."""
     from gelly_streaming_amd import distributed as D
-    assert D.owner_bounds(0, 99, 4) == [25, 50, 75]
-    assert D.owner_bounds(-(1 << 63), (1 << 63) - 1, 2) == [0]
     assert D.merge_op(D.COUNT) == D.SUM and D.merge_op(D.MAX) == D.MAX
+    import numpy as np
+    sys_path = __import__("sys").path
+    sys_path.insert(0, __import__("os").path.dirname(__file__))
+    from test_distributed_gloo import owner_np
+    L = pkg.load_library()
+    keys = np.array([0, 1, -1, 12345, 1 << 40, -(1 << 63), (1 << 63) - 1], dtype=np.int64)
+    for nparts in (1, 2, 7, 8, 64):
+        assert [L.gs_owner_of(int(k), nparts) for k in keys] == owner_np(keys, nparts).tolist()
 
 
 def test_candidates_dispatch_marker(pkg):
