@@ -158,6 +158,8 @@ def triangle_kernel_table(times_list, n):
         # N+(v) and the in-list of each v (4 + 4 B), out-range of each in-neighbour (8 B), one 4-byte
         # list item per probe
         "tri_count(light+heavy)": {"ms": mean(lambda t: t.pass_ms[3] + t.pass_ms[4]), "bytes": 16 * M + 4 * P},
+        "tri_count_light": {"ms": mean(lambda t: t.pass_ms[3]), "bytes": 0},
+        "tri_count_heavy": {"ms": mean(lambda t: t.pass_ms[4]), "bytes": 0},
     }
     return rows, P
 
@@ -601,7 +603,7 @@ def main():
         kt, partials = kernel_table(times, E_rec, U_avg)
         B = algorithmic_bytes(a.workload, E, U_avg, 8)
     finish_rows(kt, B)
-    dom_name = max(kt, key=lambda n: kt[n]["ms"])
+    dom_name = max((n for n in kt if n not in ("tri_count_light", "tri_count_heavy")), key=lambda n: kt[n]["ms"])
     dom = kt[dom_name]
     ms_step = elapsed / a.steps * 1e3
     pmc = pmc_table()

@@ -55,6 +55,11 @@ constexpr int TH_ILP = GS_TH_ILP;   // items per lane: TH_ILP probes in flight
 #ifndef GS_TH_LANEIL
 #define GS_TH_LANEIL 0   // light kernel: lane-interleaved items (1) or TH_ILP consecutive items per lane (0)
 #endif
+#ifndef GS_TH_LONG
+#define GS_TH_LONG 64    // light kernel: out-lists of >= TH_LONG items are gathered lane-interleaved (64 per load)
+#endif
+constexpr uint32_t TH_LONG = GS_TH_LONG;
+static_assert(TH_LONG >= 64, "a 64-item segment must not span more than two long lists");
 
 __device__ __forceinline__ uint32_t th_hash(uint32_t x, uint32_t mask) { return ((x * 0x9E3779B1u) >> 7) & mask; }
 // LDS written by some lanes of a wave, then read by others
@@ -98,31 +103,49 @@ __device__ __forceinline__ void th_insert(uint32_t* hs, uint32_t x, uint32_t bma
   th_fail(err);
 }
 
-// members among x[j] for the set bits j of pend; all pending probes of the lane read their bucket
-// together (one 16-byte LDS read each)
+// members among x[0 .. nv) (the lane's valid items are always a prefix).  At <= half load nearly every
+// probe ends in its first bucket (a hit, or a free last slot), so one branch-free round reads every
+// item's bucket (one 16-byte LDS read each) and only items whose first bucket was full without a hit
+// walk on.  The hit test is arithmetic (min of the XORs with the 4 slots == 0): written as compares
+// the compiler built a 4-bit mask per item through 16-bit ops (~20 VALU per probe, PMC at s22).
+__device__ __forceinline__ uint32_t slot_xor_min(const uint4& y, uint32_t x) {
+  return min(min(y.x ^ x, y.y ^ x), min(y.z ^ x, y.w ^ x));
+}
+
 __device__ __forceinline__ uint32_t th_probe(const uint4* hb, uint32_t bmask, const uint32_t (&x)[TH_ILP],
-                                             uint32_t pend, uint32_t* err) {
-  uint32_t b[TH_ILP], cnt = 0;
+                                             uint32_t nv, uint32_t* err) {
+  uint32_t b[TH_ILP], cnt = 0, walk = 0;
 #pragma unroll
   for (int j = 0; j < TH_ILP; ++j) b[j] = th_hash(x[j], bmask);
-  for (uint32_t step = 0; pend; ++step) {
-    if (step > bmask) {   // no free last slot on a whole sweep: the table is full
-      th_fail(err);
-      break;
-    }
-    uint4 y[TH_ILP];
+  uint4 y[TH_ILP];
 #pragma unroll
-    for (int j = 0; j < TH_ILP; ++j) y[j] = hb[b[j]];
+  for (int j = 0; j < TH_ILP; ++j) y[j] = hb[b[j]];
 #pragma unroll
-    for (int j = 0; j < TH_ILP; ++j) {
-      if (!(pend >> j & 1)) continue;
-      const bool hit = y[j].x == x[j] || y[j].y == x[j] || y[j].z == x[j] || y[j].w == x[j];
-      const bool open = y[j].w == TH_EMPTY;   // a free last slot ends the chain
-      if (hit || open) {
-        cnt += hit ? 1u : 0u;
-        pend &= ~(1u << j);
+  for (int j = 0; j < TH_ILP; ++j) {
+    const uint32_t m = slot_xor_min(y[j], x[j]);
+    const uint32_t on = (uint32_t)j < nv ? 1u : 0u;
+    cnt += (m == 0u) ? on : 0u;
+    walk |= ((m != 0u) & (y[j].w != TH_EMPTY) ? on : 0u) << j;
+  }
+  if (walk) {   // rare: chains that continue past their first bucket
+#pragma unroll
+    for (int j = 0; j < TH_ILP; ++j) b[j] = (b[j] + 1) & bmask;
+    for (uint32_t step = 1; walk; ++step) {
+      if (step > bmask) {   // no free last slot on a whole sweep: the table is full
+        th_fail(err);
+        break;
       }
-      b[j] = (b[j] + 1) & bmask;
+#pragma unroll
+      for (int j = 0; j < TH_ILP; ++j) {
+        if (!(walk >> j & 1)) continue;
+        const uint4 z = hb[b[j]];
+        const bool hit = slot_xor_min(z, x[j]) == 0u;
+        if (hit || z.w == TH_EMPTY) {
+          cnt += hit ? 1u : 0u;
+          walk &= ~(1u << j);
+        }
+        b[j] = (b[j] + 1) & bmask;
+      }
     }
   }
   return cnt;
@@ -142,7 +165,10 @@ __device__ __forceinline__ uint32_t th_wave_chunk(const uint32_t* __restrict__ o
   for (uint32_t i = lane; i < nb * 4; i += WAVE) hs[i] = TH_EMPTY;
   wave_lds_sync();
   for (uint32_t i = lane; i < d; i += WAVE) th_insert(hs, onbr[ro.x + i], bmask, err);
-  uint32_t run = 0, dn = 0;
+  // lists of >= TH_LONG items ("long") are gathered lane-interleaved (64 consecutive items per load:
+  // 2 cache lines); the short ones TH_ILP consecutive items per lane.  Short lists fill po / ps from
+  // the front (po = prefix of their lengths), long ones from the back (po = prefix over long lists)
+  uint32_t run = 0, dn = 0, lrun = 0, nl = 0;
   for (uint32_t i0 = c0; i0 < c1; i0 += WAVE) {
     const uint32_t i = i0 + lane;
     uint32_t du = 0, su = 0;
@@ -151,28 +177,61 @@ __device__ __forceinline__ uint32_t th_wave_chunk(const uint32_t* __restrict__ o
       du = ru.y - ru.x;
       su = ru.x;
     }
-    // keep only the u with a non-empty out-list: every kept list spans >= 1 item
-    const uint64_t ne = __ballot(du != 0);
-    const uint32_t at = dn + (uint32_t)__builtin_amdgcn_mbcnt_hi((uint32_t)(ne >> 32),
-                                                                 __builtin_amdgcn_mbcnt_lo((uint32_t)ne, 0u));
-    const uint32_t inc = wave_inclusive_sum(du);
-    if (du) {
-      po[at] = run + inc - du;
+    const bool lg = du >= TH_LONG, sh = du != 0 && !lg;
+    const uint64_t ms = __ballot(sh), ml = __ballot(lg);
+    const uint32_t ds = sh ? du : 0u, dl = lg ? du : 0u;
+    const uint32_t inc = wave_inclusive_sum(ds), incl = wave_inclusive_sum(dl);
+    if (sh) {
+      const uint32_t at = dn + mbcnt(ms);
+      po[at] = run + inc - ds;
+      ps[at] = su;
+    }
+    if (lg) {
+      const uint32_t at = TH_DMAX - 1 - (nl + mbcnt(ml));
+      po[at] = lrun + incl - dl;
       ps[at] = su;
     }
     run += __shfl(inc, WAVE - 1, WAVE);
-    dn += (uint32_t)__popcll(ne);
+    lrun += __shfl(incl, WAVE - 1, WAVE);
+    dn += (uint32_t)__popcll(ms);
+    nl += (uint32_t)__popcll(ml);
   }
   wave_lds_sync();
-  probes += run;
+  probes += run + lrun;
+  uint32_t lcnt = 0;
+  if (nl) {   // long lists: segment k of 64 items lies in list q or q + 1 (every long list >= 64 items)
+    uint32_t q = 0;
+    uint32_t qo = po[TH_DMAX - 1], qs = ps[TH_DMAX - 1];
+    uint32_t qe = nl > 1 ? po[TH_DMAX - 2] : lrun, q1s = nl > 1 ? ps[TH_DMAX - 2] : 0u;
+    for (uint32_t k0 = 0; k0 < lrun; k0 += WAVE * TH_ILP) {
+      uint32_t x[TH_ILP];
+#pragma unroll
+      for (int j = 0; j < TH_ILP; ++j) {
+        const uint32_t seg = k0 + (uint32_t)j * WAVE;   // wave-uniform
+        while (qe <= seg && q + 1 < nl) {                // advance to the list holding item seg
+          ++q;
+          qo = qe;
+          qs = q1s;
+          qe = q + 1 < nl ? po[TH_DMAX - 2 - q] : lrun;
+          q1s = q + 1 < nl ? ps[TH_DMAX - 2 - q] : 0u;
+        }
+        const uint32_t k = min(seg + (uint32_t)lane, lrun - 1);
+        x[j] = onbr[k < qe ? qs + (k - qo) : q1s + (k - qe)];
+      }
+      // valid items of this lane: segments j with k0 + 64 j + lane < lrun (a prefix of j)
+      const uint32_t rem = lrun - k0;
+      const uint32_t nv = rem > (uint32_t)lane ? min((uint32_t)TH_ILP, (rem - lane + WAVE - 1) / WAVE) : 0u;
+      lcnt += th_probe(hb, bmask, x, nv, err);
+    }
+  }
   uint32_t top = 1;
   while (2 * top < dn) top <<= 1;
-  uint32_t cnt = 0;
+  uint32_t cnt = lcnt;
 #if GS_TH_LANEIL
   // lane-interleaved items: the j-th gather of a wave reads 64 consecutive items of the concatenated
   // lists (a few cache lines) instead of 64 runs of TH_ILP items spread over the whole chunk
   for (uint32_t k0 = 0; k0 < run; k0 += WAVE * TH_ILP) {
-    uint32_t x[TH_ILP], pend = 0, lo = 0;
+    uint32_t x[TH_ILP], lo = 0;
     {
       const uint32_t kk = min(k0 + (uint32_t)lane, run - 1);
       for (uint32_t st = top; st; st >>= 1) {
@@ -194,9 +253,9 @@ __device__ __forceinline__ uint32_t th_wave_chunk(const uint32_t* __restrict__ o
         }
       }
       x[j] = onbr[ps[lo] + (kj - po[lo])];
-      pend |= (k0 + (uint32_t)(j * WAVE + lane) < run ? 1u : 0u) << j;
     }
-    cnt += th_probe(hb, bmask, x, pend, err);
+    const uint32_t rem = run - k0;
+    cnt += th_probe(hb, bmask, x, rem > (uint32_t)lane ? min((uint32_t)TH_ILP, (rem - lane + WAVE - 1) / WAVE) : 0u, err);
   }
 #else
   for (uint32_t k0 = 0; k0 < run; k0 += WAVE * TH_ILP) {
@@ -209,30 +268,22 @@ __device__ __forceinline__ uint32_t th_wave_chunk(const uint32_t* __restrict__ o
       const uint32_t pv = t < dn ? po[min(t, dn - 1)] : run;
       lo = pv <= kk ? t : lo;
     }
-    // the next TH_ILP-1 boundaries (each list >= 1 item: at most that many crossed)
-    uint32_t bo[TH_ILP], bs[TH_ILP];
-#pragma unroll
-    for (int t = 0; t < TH_ILP; ++t) {
-      const uint32_t q = lo + t;
-      bo[t] = q < dn ? po[min(q, dn - 1)] : run;
-      bs[t] = ps[min(q, dn - 1)];
-    }
+    // consecutive items cross at most one list boundary per step (every kept list has >= 1 item)
+    uint32_t o = po[lo], st = ps[lo], q = lo;
+    uint32_t nx = q + 1 < dn ? po[min(q + 1, dn - 1)] : run;
     uint32_t x[TH_ILP];
 #pragma unroll
     for (int j = 0; j < TH_ILP; ++j) {
       const uint32_t kj = min(kb + j, run - 1);
-      uint32_t o = bo[0], st = bs[0];
-#pragma unroll
-      for (int t = 1; t < TH_ILP; ++t) {
-        o = bo[t] <= kj ? bo[t] : o;
-        st = bo[t] <= kj ? bs[t] : st;
+      if (kj >= nx) {
+        ++q;
+        o = nx;
+        st = ps[q];
+        nx = q + 1 < dn ? po[q + 1] : run;
       }
       x[j] = onbr[st + (kj - o)];
     }
-    uint32_t pend = 0;
-#pragma unroll
-    for (int j = 0; j < TH_ILP; ++j) pend |= (kb + j < run ? 1u : 0u) << j;
-    cnt += th_probe(hb, bmask, x, pend, err);
+    cnt += th_probe(hb, bmask, x, kb < run ? min((uint32_t)TH_ILP, run - kb) : 0u, err);
   }
 #endif
   wave_lds_sync();   // the next item clears the table
@@ -241,7 +292,8 @@ __device__ __forceinline__ uint32_t th_wave_chunk(const uint32_t* __restrict__ o
 
 // pass 0: vertices, interleaved; first in-chunk here, further chunks queued, long out-lists to the
 //   heavy list.  pass 1: the queued (v, chunk) items.  n_probes counts the hash probes (bench bytes).
-__global__ __launch_bounds__(TH_BLOCK) void k_tri_light(const uint32_t* __restrict__ onbr,
+// 40 KiB of LDS per block -> four blocks (16 waves) per CU: registers capped to match (128 VGPRs)
+__global__ __launch_bounds__(TH_BLOCK) __attribute__((amdgpu_waves_per_eu(4, 4))) void k_tri_light(const uint32_t* __restrict__ onbr,
                                                         const uint32_t* __restrict__ inbr,
                                                         const uint2* __restrict__ out_range,
                                                         const uint2* __restrict__ in_range, uint32_t nv, uint32_t q0,
@@ -302,7 +354,8 @@ __global__ __launch_bounds__(TH_BLOCK) void k_tri_light(const uint32_t* __restri
 // entries; longer lists are binary-searched in HBM; rebuilt only when the block's item changes v),
 // the chunk's lists TH_ILP items per thread with one search.  One item per in-chunk spreads a hub over
 // many blocks (one block per heavy vertex left the hubs' blocks running long after the rest).
-__global__ __launch_bounds__(TH_HBLOCK) void k_tri_heavy(const uint32_t* __restrict__ onbr,
+// two 512-thread blocks per CU (72 KiB of LDS each): registers capped to match (128 VGPRs)
+__global__ __launch_bounds__(TH_HBLOCK) __attribute__((amdgpu_waves_per_eu(4, 4))) void k_tri_heavy(const uint32_t* __restrict__ onbr,
                                                          const uint32_t* __restrict__ inbr,
                                                          const uint2* __restrict__ out_range,
                                                          const uint2* __restrict__ in_range,
@@ -312,16 +365,23 @@ __global__ __launch_bounds__(TH_HBLOCK) void k_tri_heavy(const uint32_t* __restr
                                                          unsigned long long* __restrict__ n_probes, uint32_t nb_cap,
                                                          uint32_t* __restrict__ err) {
   __shared__ uint4 s_hash[TH_HB];               // TH_NU / 2 buckets (64 KiB): N+(v) as a hash set of 4-slot buckets
-  __shared__ uint32_t s_off[TH_VCH + 1];        // prefix of |N+(u)| over the chunk; [cn] = total
+  __shared__ uint32_t s_off[TH_VCH + 1];        // short lists of the chunk (compacted): prefix of |N+(u)|, [ns] = total
   __shared__ uint32_t s_st[TH_VCH];             // start of that N+(u) in onbr
-  __shared__ uint32_t s_w[TH_HBLOCK / WAVE];
+  __shared__ uint32_t s_loff[TH_VCH + 1];       // long lists (>= TH_LONG items), compacted the same way
+  __shared__ uint32_t s_lst[TH_VCH];
+  __shared__ uint4 s_w4[TH_HBLOCK / WAVE];
   constexpr int PER = TH_VCH / TH_HBLOCK;
+  constexpr int NW = TH_HBLOCK / WAVE;
   uint32_t* hs = reinterpret_cast<uint32_t*>(s_hash);
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   uint64_t cnt = 0, probes = 0;
   const uint32_t nh = *n_heavy;
   uint32_t table_v = TH_EMPTY;   // the vertex whose N+ the LDS table holds (block-uniform)
-  for (uint32_t hi = blockIdx.x; hi < nh; hi += gridDim.x) {
+  // a contiguous run of items per block: the chunks of one heavy vertex are consecutive items, so a
+  // block rebuilds its table only when its run moves to the next vertex
+  const uint32_t per_b = (nh + gridDim.x - 1) / gridDim.x;
+  const uint32_t h0 = min(nh, blockIdx.x * per_b), h1 = min(nh, h0 + per_b);
+  for (uint32_t hi = h0; hi < h1; ++hi) {
     const uint2 item = heavy[hi];   // (v, in-chunk)
     const uint32_t v = item.x;
     const uint2 ro = out_range[v], ri = in_range[v];
@@ -331,7 +391,7 @@ __global__ __launch_bounds__(TH_HBLOCK) void k_tri_heavy(const uint32_t* __restr
     while (nb * 2 < d && nb < TH_HB) nb <<= 1;
     nb = min(nb, nb_cap);
     const uint32_t bmask = nb - 1;
-    __syncthreads();   // the previous item is done with the table
+    __syncthreads();   // the previous item is done with the table and the list arrays
     if (in_lds && table_v != v) {
       for (uint32_t i = tid; i < nb * 4; i += TH_HBLOCK) hs[i] = TH_EMPTY;
       __syncthreads();
@@ -339,73 +399,127 @@ __global__ __launch_bounds__(TH_HBLOCK) void k_tri_heavy(const uint32_t* __restr
       table_v = v;
     }
     const uint32_t* nvl = onbr + ro.x;
-    {
-      const uint32_t c0 = ri.x + item.y * TH_VCH;
-      const uint32_t cn = min(TH_VCH, ri.y - c0);
-      __syncthreads();
-      // prefix of |N+(u)| over this chunk of in-neighbours (PER per thread, block scan)
-      uint32_t du[PER], su[PER], sum = 0;
+    auto probe = [&](const uint32_t (&x)[TH_ILP], uint32_t nv) -> uint32_t {
+      if (in_lds) return th_probe(s_hash, bmask, x, nv, err);
+      uint32_t c = 0;
 #pragma unroll
-      for (int j = 0; j < PER; ++j) {
-        const uint32_t i = tid * PER + j;
-        const uint2 ru = out_range[inbr[c0 + min(i, cn - 1)]];
-        su[j] = ru.x;
-        du[j] = i < cn ? ru.y - ru.x : 0u;
-        sum += du[j];
+      for (int j = 0; j < TH_ILP; ++j) {
+        uint32_t a = 0, b = d;   // lower bound of x in N+(v)
+        while (a < b) {
+          const uint32_t mid = (a + b) >> 1;
+          if (nvl[mid] < x[j]) a = mid + 1;
+          else b = mid;
+        }
+        c += ((uint32_t)j < nv && a < d && nvl[a] == x[j]) ? 1u : 0u;
       }
-      const uint32_t inc = wave_inclusive_sum(sum);
-      if (lane == 63) s_w[w] = inc;
-      __syncthreads();
-      uint32_t base = 0, tot = 0;
-      for (int i = 0; i < TH_HBLOCK / WAVE; ++i) {
-        base += i < w ? s_w[i] : 0u;
-        tot += s_w[i];
-      }
-      uint32_t run = base + inc - sum;
+      return c;
+    };
+    const uint32_t c0 = ri.x + item.y * TH_VCH;
+    const uint32_t cn = min(TH_VCH, ri.y - c0);
+    // the chunk's lists, split into short and long and compacted: one block scan of (short lists,
+    // short items, long lists, long items)
+    uint32_t du[PER], su[PER];
+    uint4 mine = make_uint4(0, 0, 0, 0);
 #pragma unroll
-      for (int j = 0; j < PER; ++j) {
-        const uint32_t i = tid * PER + j;
-        if (i < cn) {
-          s_off[i] = run;
-          s_st[i] = su[j];
-        }
-        run += du[j];
+    for (int j = 0; j < PER; ++j) {
+      const uint32_t i = tid * PER + j;
+      const uint2 ru = out_range[inbr[c0 + min(i, cn - 1)]];
+      su[j] = ru.x;
+      du[j] = i < cn ? ru.y - ru.x : 0u;
+      if (du[j] >= TH_LONG) { mine.z += 1; mine.w += du[j]; }
+      else if (du[j]) { mine.x += 1; mine.y += du[j]; }
+    }
+    uint4 inc = make_uint4(wave_inclusive_sum(mine.x), wave_inclusive_sum(mine.y), wave_inclusive_sum(mine.z),
+                           wave_inclusive_sum(mine.w));
+    if (lane == 63) s_w4[w] = inc;
+    __syncthreads();
+    uint4 base = make_uint4(0, 0, 0, 0), tot = make_uint4(0, 0, 0, 0);
+#pragma unroll
+    for (int i = 0; i < NW; ++i) {
+      const uint4 x = s_w4[i];
+      if (i < w) { base.x += x.x; base.y += x.y; base.z += x.z; base.w += x.w; }
+      tot.x += x.x; tot.y += x.y; tot.z += x.z; tot.w += x.w;
+    }
+    uint32_t si = base.x + inc.x - mine.x, so = base.y + inc.y - mine.y;
+    uint32_t li = base.z + inc.z - mine.z, lo_ = base.w + inc.w - mine.w;
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+      if (du[j] >= TH_LONG) {
+        s_loff[li] = lo_;
+        s_lst[li] = su[j];
+        ++li;
+        lo_ += du[j];
+      } else if (du[j]) {
+        s_off[si] = so;
+        s_st[si] = su[j];
+        ++si;
+        so += du[j];
       }
-      if (tid == 0) s_off[cn] = tot;
-      probes += tot;   // block-uniform
-      __syncthreads();
-      for (uint32_t k0 = 0; k0 < tot; k0 += TH_HBLOCK * TH_ILP) {
-        const uint32_t kb = k0 + tid * TH_ILP;
-        // list of item kk: the last index with s_off <= kk (s_off[cn] = tot is above every item)
-        uint32_t lo = 0, h2 = cn - 1;
-        const uint32_t kk = min(kb, tot - 1);
-        while (lo < h2) {
-          const uint32_t mid = (lo + h2 + 1) >> 1;
-          if (s_off[mid] <= kk) lo = mid;
-          else h2 = mid - 1;
+    }
+    const uint32_t ns = tot.x, srun = tot.y, nl = tot.z, lrun = tot.w;
+    if (tid == 0) {
+      s_off[ns] = srun;
+      s_loff[nl] = lrun;
+    }
+    probes += srun + lrun;   // block-uniform
+    __syncthreads();
+    // short lists: TH_ILP consecutive items per thread, at most one list boundary per step
+    uint32_t top = 1;
+    while (2 * top < ns) top <<= 1;
+    for (uint32_t k0 = 0; k0 < srun; k0 += TH_HBLOCK * TH_ILP) {
+      const uint32_t kb = k0 + tid * TH_ILP;
+      const uint32_t kk = min(kb, srun - 1);
+      uint32_t q = 0;
+      for (uint32_t st = top; st; st >>= 1) {
+        const uint32_t t = q + st;
+        q = (t < ns && s_off[min(t, ns - 1)] <= kk) ? t : q;
+      }
+      uint32_t o = s_off[q], sst = s_st[q], nx = s_off[q + 1];
+      uint32_t x[TH_ILP];
+#pragma unroll
+      for (int j = 0; j < TH_ILP; ++j) {
+        const uint32_t kj = min(kb + j, srun - 1);
+        if (kj >= nx) {
+          ++q;
+          o = nx;
+          sst = s_st[q];
+          nx = s_off[q + 1];
         }
-        uint32_t x[TH_ILP], pend = 0;
+        x[j] = onbr[sst + (kj - o)];
+      }
+      cnt += probe(x, kb < srun ? min((uint32_t)TH_ILP, srun - kb) : 0u);
+    }
+    // long lists: wave w walks items [w, w + 1) * lrun / NW in 64-item segments (one load of 64
+    // consecutive items); a segment spans at most two lists (every long list >= 64 items)
+    if (lrun) {
+      const uint32_t a0 = (uint32_t)((uint64_t)lrun * w / NW), a1 = (uint32_t)((uint64_t)lrun * (w + 1) / NW);
+      uint32_t q = 0;
+      {
+        uint32_t t2 = 1;
+        while (2 * t2 < nl) t2 <<= 1;
+        for (uint32_t st = t2; st; st >>= 1) {
+          const uint32_t t = q + st;
+          q = (t < nl && s_loff[min(t, nl - 1)] <= a0) ? t : q;
+        }
+      }
+      uint32_t qo = s_loff[q], qs = s_lst[q], qe = s_loff[q + 1], q1s = q + 1 < nl ? s_lst[q + 1] : 0u;
+      for (uint32_t k0 = a0; k0 < a1; k0 += WAVE * TH_ILP) {
+        uint32_t x[TH_ILP];
 #pragma unroll
         for (int j = 0; j < TH_ILP; ++j) {
-          const uint32_t kj = min(kb + j, tot - 1);
-          while (s_off[lo + 1] <= kj) ++lo;   // crosses empty lists too
-          x[j] = onbr[s_st[lo] + (kj - s_off[lo])];
-          pend |= (kb + j < tot ? 1u : 0u) << j;
-        }
-        if (in_lds) {
-          cnt += th_probe(s_hash, bmask, x, pend, err);
-        } else {
-#pragma unroll
-          for (int j = 0; j < TH_ILP; ++j) {
-            uint32_t a = 0, b = d;   // lower bound of x in N+(v)
-            while (a < b) {
-              const uint32_t mid = (a + b) >> 1;
-              if (nvl[mid] < x[j]) a = mid + 1;
-              else b = mid;
-            }
-            cnt += ((pend >> j & 1) && a < d && nvl[a] == x[j]) ? 1u : 0u;
+          const uint32_t seg = k0 + (uint32_t)j * WAVE;   // wave-uniform
+          while (qe <= seg && q + 1 < nl) {
+            ++q;
+            qo = qe;
+            qs = q1s;
+            qe = s_loff[q + 1];
+            q1s = q + 1 < nl ? s_lst[q + 1] : 0u;
           }
+          const uint32_t k = min(seg + (uint32_t)lane, a1 - 1);
+          x[j] = onbr[k < qe ? qs + (k - qo) : q1s + (k - qe)];
         }
+        const uint32_t rem = a1 - k0;
+        cnt += probe(x, rem > (uint32_t)lane ? min((uint32_t)TH_ILP, (rem - lane + WAVE - 1) / WAVE) : 0u);
       }
     }
   }
