@@ -145,19 +145,22 @@ def direct_kernel_table(times_list, E, U_avg):
 
 def triangle_kernel_table(times_list, n):
     """WindowTriangles (stage_times path 3): algorithmic bytes per stage as in DESIGN.md §4 —
-    n input edges, E2 unique adjacency entries, M = E2 / 2 oriented edges, P hash probes."""
+    n input edges, M unique (oriented) edges, P hash probes, V id range."""
     mean = lambda f: statistics.mean(f(t) for t in times_list)
-    E2 = mean(lambda t: t.records)
-    M, P, V = E2 / 2, mean(lambda t: t.partials), mean(lambda t: t.vertices)
+    M, P = mean(lambda t: t.records), mean(lambda t: t.partials)
+    V = 2 ** statistics.mean(t.key_bits for t in times_list)
     rows = {
-        # edge list in, symmetric keys out, one read + write of the 2n keys
-        "tri_sym+sort": {"ms": mean(lambda t: t.pass_ms[0]), "bytes": 16 * n + 16 * n + 32 * n},
-        "tri_unique": {"ms": mean(lambda t: t.pass_ms[1]), "bytes": 16 * n + 8 * E2},
-        # rows (read keys, degree + row start out), keep flags (keys + two degrees), compaction
-        "tri_rows+orient": {"ms": mean(lambda t: t.pass_ms[2]), "bytes": 8 * E2 + 8 * V + 17 * E2 + 17 * E2},
-        # N+(v) and the in-list of each v (4 + 4 B), out-range of each in-neighbour (8 B), one 4-byte
-        # list item per probe
-        "tri_count(light+heavy)": {"ms": mean(lambda t: t.pass_ms[3] + t.pass_ms[4]), "bytes": 16 * M + 4 * P},
+        # raw degrees (edge list in), degree-class ranks (2 reads + 1 write of V), oriented keys of the
+        # ranks (edge list in, 2 rank gathers, n keys out), one read + write of the n keys
+        "tri_rank+keys+sort": {"ms": mean(lambda t: t.pass_ms[0]),
+                               "bytes": 16 * n + 12 * V + 16 * n + 8 * n + 8 * n + 16 * n},
+        "tri_unique": {"ms": mean(lambda t: t.pass_ms[1]), "bytes": 8 * n + 8 * M},
+        # out-lists (keys in; neighbour ids, transposed keys + payload out), list ends, the transposed
+        # sort (one read + write of 8 B per edge), in-lists + suffix ranges (8 B in, 4 B gathered, 8 B out)
+        "tri_out+transpose+in": {"ms": mean(lambda t: t.pass_ms[2]),
+                                 "bytes": 8 * M + 16 * M + 8 * M + 4 * M + 16 * M + 20 * M + 16 * V},
+        # N+(v) (4 B per out-entry), one suffix range per in-entry (8 B), one 4-byte list item per probe
+        "tri_count(light+heavy)": {"ms": mean(lambda t: t.pass_ms[3] + t.pass_ms[4]), "bytes": 12 * M + 4 * P},
         "tri_count_light": {"ms": mean(lambda t: t.pass_ms[3]), "bytes": 0},
         "tri_count_heavy": {"ms": mean(lambda t: t.pass_ms[4]), "bytes": 0},
     }

@@ -43,127 +43,203 @@ __global__ __launch_bounds__(256) void k_gather_csr(const uint32_t* __restrict__
 // ---------------------------------------------------------------------------------------------
 constexpr uint64_t TRI_MAX_BITS = 28;
 
-// composite symmetric adjacency keys (a << B | b), both directions; self-loops -> sentinel + flag
-__global__ __launch_bounds__(256) void k_tri_sym(const int64_t* __restrict__ src, const int64_t* __restrict__ dst,
-                                                 uint64_t n, uint64_t key_xor, uint32_t B,
-                                                 uint64_t* __restrict__ out, uint32_t* __restrict__ loop_bits,
-                                                 unsigned long long* __restrict__ loops) {
+// Vertices are renumbered by degree before the adjacency is built: rank(x) orders (degree class, id),
+// so in the renumbered graph "u -> v iff u < v" is the degree orientation.  Only the oriented keys
+// (min rank << B | max rank) are sorted (n keys, not the 2n of a symmetric adjacency): unique -> the
+// out-lists, sorted in orientation order; a second, narrow sort of the unique edges by target
+// (B-bit keys, adjacency position as payload) groups them into in-lists.  Sorted out-lists are what
+// halve the probes: for u -> v only the part of N+(u) above v can hold a w with v -> w, so each
+// in-neighbour u of v contributes the suffix of N+(u) after v, and the in-list entry carries that
+// suffix's range (R-MAT scale 20: sum of d+(u)^2 = 2.47 G probes -> sum of d+(d+-1)/2 = 1.23 G).
+// Any total order gives the exact count; the degree classes only keep out-lists short.
+
+// raw degree per (compact) vertex over the window's records: the bucket path's COUNT over both
+// endpoints (bucket_reduce), scattered into a dense array.  Windows the bucket path does not take (id
+// range too wide for its buckets) count with global atomics instead -- one request per endpoint, and
+// an R-MAT hub's atomics serialize on its address, so each block first counts into an LDS table that
+// keeps the first ids to claim a slot (the frequent ones, almost surely) and flushes it at the end.
+__global__ __launch_bounds__(256) void k_tri_deg_scatter(const int64_t* __restrict__ keys, const int64_t* __restrict__ cnt,
+                                                         uint64_t U, uint64_t key_xor, uint32_t* __restrict__ deg) {
+  for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < U; i += (uint64_t)gridDim.x * 256)
+    deg[(uint64_t)keys[i] ^ key_xor] = (uint32_t)cnt[i];
+}
+
+constexpr int DG_BLOCK = 512, DG_SLOTS = 4096;
+__global__ __launch_bounds__(DG_BLOCK) void k_tri_deg(const int64_t* __restrict__ src, const int64_t* __restrict__ dst,
+                                                      uint64_t n, uint64_t key_xor, uint32_t* __restrict__ deg) {
+  __shared__ uint32_t s_key[DG_SLOTS], s_cnt[DG_SLOTS];
+  for (int i = threadIdx.x; i < DG_SLOTS; i += DG_BLOCK) {
+    s_key[i] = 0xFFFFFFFFu;
+    s_cnt[i] = 0;
+  }
+  __syncthreads();
+  auto add = [&](uint32_t x) {
+    const uint32_t h = (x * 0x9E3779B1u) >> (32 - 12);
+    uint32_t k = s_key[h];
+    if (k == 0xFFFFFFFFu) {
+      k = atomicCAS(&s_key[h], 0xFFFFFFFFu, x);
+      if (k == 0xFFFFFFFFu) k = x;
+    }
+    if (k == x) atomicAdd(&s_cnt[h], 1u);
+    else atomicAdd(&deg[x], 1u);
+  };
+  static_assert(DG_SLOTS == 1 << 12, "hash shift");
+  for (uint64_t i = (uint64_t)blockIdx.x * DG_BLOCK + threadIdx.x; i < n; i += (uint64_t)gridDim.x * DG_BLOCK) {
+    add((uint32_t)((uint64_t)src[i] ^ key_xor));
+    add((uint32_t)((uint64_t)dst[i] ^ key_xor));
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < DG_SLOTS; i += DG_BLOCK)
+    if (s_cnt[i]) atomicAdd(&deg[s_key[i]], s_cnt[i]);
+}
+
+// degree class: 0 for isolated ids, then two classes per octave
+constexpr int RK_BLOCK = 256, RK_STEPS = 32, RK_WAVES = RK_BLOCK / WAVE, RK_TILE = RK_BLOCK * RK_STEPS, RK_NC = 64;
+__device__ __forceinline__ uint32_t deg_class(uint32_t d) {
+  if (!d) return 0;
+  const uint32_t lz = 31u - (uint32_t)__clz(d);
+  const uint32_t half = lz ? (d >> (lz - 1)) & 1u : 0u;
+  return min((uint32_t)RK_NC - 1, 1u + 2u * lz + half);
+}
+
+// per tile of RK_TILE ids: ids per class -> cnt[class * tiles + tile]
+__global__ __launch_bounds__(RK_BLOCK) void k_rank_count(const uint32_t* __restrict__ deg, uint32_t V, uint32_t tiles,
+                                                         uint32_t* __restrict__ cnt) {
+  __shared__ uint32_t s_c[RK_NC];
+  const int tid = threadIdx.x;
+  if (tid < RK_NC) s_c[tid] = 0;
+  __syncthreads();
+  const uint32_t base = blockIdx.x * RK_TILE;
+  for (int j = 0; j < RK_STEPS; ++j) {
+    const uint32_t x = base + j * RK_BLOCK + tid;
+    if (x < V) atomicAdd(&s_c[deg_class(deg[x])], 1u);
+  }
+  __syncthreads();
+  if (tid < RK_NC) cnt[tid * tiles + blockIdx.x] = s_c[tid];
+}
+
+// one block: exclusive scan of cnt[0 .. n) (class-major) in place
+__global__ __launch_bounds__(1024) void k_rank_scan(uint32_t* __restrict__ cnt, uint32_t n) {
+  __shared__ uint32_t s_w[16];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const uint32_t per = (n + 1023) / 1024, a = min(n, tid * per), b = min(n, a + per);
+  uint32_t sum = 0;
+  for (uint32_t i = a; i < b; ++i) sum += cnt[i];
+  const uint32_t inc = wave_inclusive_sum(sum);
+  if (lane == 63) s_w[w] = inc;
+  __syncthreads();
+  uint32_t run = inc - sum;
+  for (int i = 0; i < w; ++i) run += s_w[i];
+  for (uint32_t i = a; i < b; ++i) {
+    const uint32_t x = cnt[i];
+    cnt[i] = run;
+    run += x;
+  }
+}
+
+// rank[x] = ids of lower classes + ids of x's class below x (a stable partition: deterministic, so
+// every rank of a multi-GPU job renumbers identically).  Wave w of a tile takes RK_STEPS groups of 64
+// consecutive ids; a lane's place among equal classes comes from a 7-ballot match mask.
+__global__ __launch_bounds__(RK_BLOCK) void k_rank_scatter(const uint32_t* __restrict__ deg, uint32_t V, uint32_t tiles,
+                                                           const uint32_t* __restrict__ off, uint32_t* __restrict__ rank) {
+  __shared__ uint32_t s_cnt[RK_WAVES][RK_NC];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  for (int i = tid; i < RK_WAVES * RK_NC; i += RK_BLOCK) (&s_cnt[0][0])[i] = 0;
+  __syncthreads();
+  const uint32_t base = blockIdx.x * RK_TILE + (uint32_t)w * (RK_STEPS * WAVE);
+  const uint64_t lt = (1ull << lane) - 1;
+  uint32_t cls[RK_STEPS], loc[RK_STEPS];
+#pragma unroll
+  for (int j = 0; j < RK_STEPS; ++j) {
+    const uint32_t x = base + j * WAVE + lane;
+    const uint32_t c = x < V ? deg_class(deg[x]) : 127u;
+    uint64_t m = ~0ull;
+#pragma unroll
+    for (int bit = 0; bit < 7; ++bit) {
+      const uint64_t bal = __ballot((c >> bit) & 1u);
+      m &= ((c >> bit) & 1u) ? bal : ~bal;
+    }
+    cls[j] = c;
+    uint32_t b0 = 0;
+    if (c < RK_NC) b0 = s_cnt[w][c];
+    loc[j] = b0 + (uint32_t)__popcll(m & lt);
+    if (c < RK_NC && (m & lt) == 0) s_cnt[w][c] = b0 + (uint32_t)__popcll(m);   // the class's lowest lane
+    wave_lds_sync();
+  }
+  __syncthreads();
+  if (tid < RK_NC) {   // exclusive prefix over the waves, per class
+    uint32_t run = 0;
+    for (int k = 0; k < RK_WAVES; ++k) {
+      const uint32_t t = s_cnt[k][tid];
+      s_cnt[k][tid] = run;
+      run += t;
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < RK_STEPS; ++j) {
+    const uint32_t x = base + j * WAVE + lane;
+    if (x < V) rank[x] = off[cls[j] * tiles + blockIdx.x] + s_cnt[w][cls[j]] + loc[j];
+  }
+}
+
+// oriented composite keys (min rank << B | max rank); self-loops -> sentinel (sorts last) + bitmap
+// and count
+__global__ __launch_bounds__(256) void k_tri_okeys(const int64_t* __restrict__ src, const int64_t* __restrict__ dst,
+                                                   uint64_t n, uint64_t key_xor, uint32_t B,
+                                                   const uint32_t* __restrict__ rank, uint64_t* __restrict__ out,
+                                                   uint32_t* __restrict__ loop_bits, unsigned long long* __restrict__ loops) {
   const uint64_t sent = (B * 2 >= 64) ? ~0ull : ((1ull << (2 * B)) - 1);
   for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) {
     const uint64_t a = (uint64_t)src[i] ^ key_xor, b = (uint64_t)dst[i] ^ key_xor;
+    uint64_t k = sent;
     if (a != b) {
-      out[2 * i] = (a << B) | b;
-      out[2 * i + 1] = (b << B) | a;
+      const uint64_t ra = rank[a], rb = rank[b];
+      k = ra < rb ? (ra << B) | rb : (rb << B) | ra;
     } else {
-      out[2 * i] = sent;
-      out[2 * i + 1] = sent;
       atomicOr(&loop_bits[a >> 5], 1u << (a & 31));
       atomicAdd(loops, 1ull);
     }
+    out[i] = k;
   }
 }
 
-// per vertex row of the unique symmetric adjacency: deg[v], rowstart[v]
-struct RowOut {
-  uint32_t* deg;
-  uint32_t* rowstart;
-  __device__ void store(uint32_t, int64_t k, uint64_t cnt, uint32_t end_pos) const {
-    deg[k] = (uint32_t)cnt;
-    rowstart[k] = end_pos + 1 - (uint32_t)cnt;
-  }
-};
-
-__device__ __forceinline__ bool oriented(uint32_t du, uint32_t u, uint32_t dv, uint32_t v) {
-  return du < dv || (du == dv && u < v);
-}
-
-constexpr int SCAN_BLOCK = 256, SCAN_ITEMS = 16, SCAN_TILE = SCAN_BLOCK * SCAN_ITEMS;
-
-// keep flag per adjacency entry (u -> v kept iff (deg u, u) < (deg v, v)) + per-tile counts
-__global__ __launch_bounds__(SCAN_BLOCK) void k_orient_count(const uint64_t* __restrict__ adj, uint32_t E2, uint32_t B,
-                                                             const uint32_t* __restrict__ deg,
-                                                             uint8_t* __restrict__ keep, uint32_t* __restrict__ tile_sum) {
-  __shared__ uint32_t ws[SCAN_BLOCK / 64];
+// the unique oriented edges (sorted keys u << B | v) -> out-lists: nbr[p] = v, out_range[u] =
+// [first, last + 1) (ranges of absent vertices were zeroed); the transposed sort's input: key v,
+// payload p
+__global__ __launch_bounds__(256) void k_tri_out(const uint64_t* __restrict__ keys, uint32_t M, uint32_t B,
+                                                 uint32_t* __restrict__ nbr, uint32_t* __restrict__ out_range,
+                                                 uint64_t* __restrict__ tkey, uint32_t* __restrict__ tval) {
   const uint64_t mask = (1ull << B) - 1;
-  uint32_t cnt = 0;
-  const uint32_t base = blockIdx.x * SCAN_TILE;
-#pragma unroll
-  for (int j = 0; j < SCAN_ITEMS; ++j) {
-    const uint32_t p = base + j * SCAN_BLOCK + threadIdx.x;
-    if (p < E2) {
-      const uint64_t k = adj[p];
-      const uint32_t u = (uint32_t)(k >> B), v = (uint32_t)(k & mask);
-      const bool kp = oriented(deg[u], u, deg[v], v);
-      keep[p] = kp;
-      cnt += kp;
-    }
-  }
-  cnt = wave_inclusive_sum(cnt);
-  if ((threadIdx.x & 63) == 63) ws[threadIdx.x >> 6] = cnt;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    uint32_t t = 0;
-    for (int w = 0; w < SCAN_BLOCK / 64; ++w) t += ws[w];
-    tile_sum[blockIdx.x] = t;
+  for (uint32_t p = blockIdx.x * 256u + threadIdx.x; p < M; p += gridDim.x * 256u) {
+    const uint64_t k = keys[p];
+    const uint32_t u = (uint32_t)(k >> B), v = (uint32_t)(k & mask);
+    nbr[p] = v;
+    tkey[p] = v;
+    tval[p] = p;
+    if (p == 0 || (uint32_t)(keys[p - 1] >> B) != u) out_range[2 * u] = p;
+    if (p + 1 == M || (uint32_t)(keys[p + 1] >> B) != u) out_range[2 * u + 1] = p + 1;
   }
 }
 
-// exclusive scan of tile sums in one workgroup (tiles <= a few 10^5); writes total at [ntiles]
-__global__ __launch_bounds__(1024) void k_scan_tiles(uint32_t* __restrict__ tile_sum, uint32_t ntiles) {
-  __shared__ uint32_t ws[16];
-  __shared__ uint32_t carry;
-  if (threadIdx.x == 0) carry = 0;
-  __syncthreads();
-  for (uint32_t base = 0; base < ntiles; base += 1024) {
-    const uint32_t i = base + threadIdx.x;
-    const uint32_t x = i < ntiles ? tile_sum[i] : 0u;
-    const uint32_t inc = wave_inclusive_sum(x);
-    if ((threadIdx.x & 63) == 63) ws[threadIdx.x >> 6] = inc;
-    __syncthreads();
-    uint32_t off = carry;
-    for (int w = 0; w < (int)(threadIdx.x >> 6); ++w) off += ws[w];
-    if (i < ntiles) tile_sum[i] = off + inc - x;
-    __syncthreads();
-    if (threadIdx.x == 1023) carry = off + inc;
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) tile_sum[ntiles] = carry;
+// end of the out-list holding each adjacency position
+__global__ __launch_bounds__(256) void k_tri_pairend(const uint64_t* __restrict__ keys, uint32_t M, uint32_t B,
+                                                     const uint2* __restrict__ out_range, uint32_t* __restrict__ pend) {
+  for (uint32_t p = blockIdx.x * 256u + threadIdx.x; p < M; p += gridDim.x * 256u)
+    pend[p] = out_range[(uint32_t)(keys[p] >> B)].y;
 }
 
-// pos[p] = #kept before p (pos[E2] = M); kept entries compact into onbr (out-lists), the others into
-// inbr (in-lists, at p - pos[p]); order preserved
-__global__ __launch_bounds__(SCAN_BLOCK) void k_orient_scatter(const uint64_t* __restrict__ adj, uint32_t E2, uint32_t B,
-                                                               const uint8_t* __restrict__ keep,
-                                                               const uint32_t* __restrict__ tile_off,
-                                                               uint32_t* __restrict__ pos, uint32_t* __restrict__ inbr,
-                                                               uint32_t* __restrict__ onbr) {
-  __shared__ uint32_t ws[SCAN_BLOCK / 64];
-  const uint64_t mask = (1ull << B) - 1;
-  const uint32_t base = blockIdx.x * SCAN_TILE;
-  // blocked: thread t owns entries [base + t*ITEMS, +ITEMS) so the scan order is entry order
-  const uint32_t first = base + threadIdx.x * SCAN_ITEMS;
-  uint32_t cnt = 0;
-#pragma unroll
-  for (int j = 0; j < SCAN_ITEMS; ++j) {
-    const uint32_t p = first + j;
-    if (p < E2) cnt += keep[p];
+// the edges sorted by target: in_range[v] = [first, last + 1) of v's in-entries; in-entry i
+// (u -> v at adjacency position q) gets the part of N+(u) past v: sfx[i] = [q + 1, end of N+(u))
+__global__ __launch_bounds__(256) void k_tri_in(const uint32_t* __restrict__ skey, const uint32_t* __restrict__ sval,
+                                                uint32_t M, const uint32_t* __restrict__ pend,
+                                                uint32_t* __restrict__ in_range, uint2* __restrict__ sfx) {
+  for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < M; i += gridDim.x * 256u) {
+    const uint32_t v = skey[i], q = sval[i];
+    sfx[i] = make_uint2(q + 1, pend[q]);
+    if (i == 0 || skey[i - 1] != v) in_range[2 * v] = i;
+    if (i + 1 == M || skey[i + 1] != v) in_range[2 * v + 1] = i + 1;
   }
-  const uint32_t inc = wave_inclusive_sum(cnt);
-  if ((threadIdx.x & 63) == 63) ws[threadIdx.x >> 6] = inc;
-  __syncthreads();
-  uint32_t off = tile_off[blockIdx.x] + inc - cnt;
-  for (int w = 0; w < (int)(threadIdx.x >> 6); ++w) off += ws[w];
-#pragma unroll
-  for (int j = 0; j < SCAN_ITEMS; ++j) {
-    const uint32_t p = first + j;
-    if (p < E2) {
-      pos[p] = off;
-      const uint32_t x = (uint32_t)(adj[p] & mask);
-      if (keep[p]) onbr[off++] = x;
-      else inbr[p - off] = x;
-    }
-  }
-  if (blockIdx.x == gridDim.x - 1 && threadIdx.x == SCAN_BLOCK - 1) pos[E2] = tile_off[gridDim.x];
 }
 
 }  // namespace gs
@@ -278,68 +354,97 @@ static gs_status triangles_impl(gs_ctx* c, const gs_edge_batch* b, uint32_t part
       return set_error(c, GS_EUNSUPPORTED, "window triangles: %llu distinct vertices (> 2^%llu)",
                        (unsigned long long)nuniq, (unsigned long long)TRI_MAX_BITS);
   }
-  const uint64_t R = 2 * n;
-  // 1. symmetric composite keys (+ self-loop bitmap)
-  GS_TRY(ensure(c, c->aux, R * 8));
-  const size_t words = ((1ull << B) + 31) / 32;
+  const size_t V = 1ull << B;
+  // 1. raw degrees (+ self-loop bitmap) -> degree-class ranks -> oriented composite keys of the ranks
+  GS_TRY(ensure(c, c->aux, n * 8));
+  const size_t words = (V + 31) / 32;
   GS_TRY(ensure(c, c->tri_loops, words * 4));
+  GS_TRY(ensure(c, c->out_a, V * 4));
+  GS_TRY(ensure(c, c->out_b, V * 4));
+  const uint32_t rk_tiles = (uint32_t)((V + RK_TILE - 1) / RK_TILE);
+  GS_TRY(ensure(c, c->tri_tiles, (size_t)rk_tiles * RK_NC * 4 + 8));
   GS_HIP(hipMemsetAsync(c->tri_loops.p, 0, words * 4, c->stream));
+  GS_HIP(hipMemsetAsync(c->out_a.p, 0, V * 4, c->stream));
   unsigned long long* d_loops = (unsigned long long*)(sm + SM_NUNIQUE);
   const unsigned g = (unsigned)std::min<uint64_t>((n + 255) / 256, 8192);
-  hipLaunchKernelGGL(k_tri_sym, dim3(g), dim3(256), 0, c->stream, src, dst, n, key_xor, B, c->aux.as<uint64_t>(),
-                     c->tri_loops.as<uint32_t>(), d_loops);
+  uint32_t* deg = c->out_a.as<uint32_t>();
+  uint32_t* rank = c->out_b.as<uint32_t>();
+  uint32_t* rk_cnt = c->tri_tiles.as<uint32_t>();
+  {
+    GS_TRY(ensure(c, c->out_keys, std::min<uint64_t>(2 * n, V) * 8));
+    GS_TRY(ensure(c, c->tri_sfx, std::min<uint64_t>(2 * n, V) * 8));
+    uint64_t U = 0;
+    const gs_status bs = bucket_reduce(c, src, dst, nullptr, n, DIR_ALL, OP_COUNT, GS_NONE, false, nullptr,
+                                       c->out_keys.as<int64_t>(), c->tri_sfx.p, &U);
+    if (bs == GS_OK) {
+      if (U)
+        hipLaunchKernelGGL(k_tri_deg_scatter, dim3((unsigned)std::min<uint64_t>((U + 255) / 256, 8192)), dim3(256), 0,
+                           c->stream, c->out_keys.as<int64_t>(), c->tri_sfx.as<int64_t>(), U, key_xor, deg);
+    } else if (bs == GS_EUNSUPPORTED) {
+      hipLaunchKernelGGL(k_tri_deg, dim3((unsigned)std::min<uint64_t>((n + DG_BLOCK - 1) / DG_BLOCK, 1024)),
+                         dim3(DG_BLOCK), 0, c->stream, src, dst, n, key_xor, deg);
+    } else {
+      return bs;
+    }
+  }
+  hipLaunchKernelGGL(k_rank_count, dim3(rk_tiles), dim3(RK_BLOCK), 0, c->stream, deg, (uint32_t)V, rk_tiles, rk_cnt);
+  hipLaunchKernelGGL(k_rank_scan, dim3(1), dim3(1024), 0, c->stream, rk_cnt, rk_tiles * RK_NC);
+  hipLaunchKernelGGL(k_rank_scatter, dim3(rk_tiles), dim3(RK_BLOCK), 0, c->stream, deg, (uint32_t)V, rk_tiles, rk_cnt,
+                     rank);
+  GS_HIP(hipMemsetAsync(d_loops, 0, 8, c->stream));
+  hipLaunchKernelGGL(k_tri_okeys, dim3(g), dim3(256), 0, c->stream, src, dst, n, key_xor, B, rank,
+                     c->aux.as<uint64_t>(), c->tri_loops.as<uint32_t>(), d_loops);
   GS_HIP(hipGetLastError());
   GS_HIP(hipMemcpyAsync(c->host_small + 4, d_loops, 8, hipMemcpyDeviceToHost, c->stream));
-  // 2. sort + unique -> symmetric simple adjacency, sorted by (u, v)
+  // ids of class 0 (no edge) = the offset of class 1 (the copy fills the low 4 bytes)
+  c->host_small[5] = 0;
+  GS_HIP(hipMemcpyAsync(c->host_small + 5, rk_cnt + rk_tiles, 4, hipMemcpyDeviceToHost, c->stream));
+  // 2. sort + unique -> the simple oriented graph, sorted by (u, v)
   Sorted s;
-  GS_TRY(sort_buffer(c, c->aux.as<uint64_t>(), nullptr, R, &s));
+  GS_TRY(sort_buffer(c, c->aux.as<uint64_t>(), nullptr, n, &s));
   hipEventRecord(c->ev[1], c->stream);
   const uint64_t loops = c->host_small[4];
-  GS_TRY(ensure(c, c->out_keys, R * 8));
-  uint64_t E2 = 0;
+  const uint64_t nv = V - (uint32_t)c->host_small[5];
+  GS_TRY(ensure(c, c->out_keys, n * 8));
+  uint64_t M = 0;
   UniqueOut uo{c->out_keys.as<uint64_t>(), nullptr};
-  GS_TRY((s.wide ? launch_rbk<uint64_t, CountOp>(c, s, uo, &E2) : launch_rbk<uint32_t, CountOp>(c, s, uo, &E2)));
+  GS_TRY((s.wide ? launch_rbk<uint64_t, CountOp>(c, s, uo, &M) : launch_rbk<uint32_t, CountOp>(c, s, uo, &M)));
   hipEventRecord(c->ev[2], c->stream);
-  if (loops) E2 -= 1;   // the self-loop sentinel sorts last
-  if (E2 == 0) {        // only self-loops: no triangle; the self-pair term needs >= 2 neighbours
+  if (loops) M -= 1;   // the self-loop sentinel sorts last
+  if (M == 0) {        // only self-loops: no triangle; the self-pair term needs >= 2 neighbours
     uint64_t S = 0;
     if (part == 0) GS_TRY(triangle_selfpair_term(c, osrc, odst, n, c->tri_loops.as<uint32_t>(), key_xor, uniq, nuniq, &S));
     *count = S;
     return GS_OK;
   }
-  // 3. rows: degree + row start per vertex (segment by u = key >> B)
-  const size_t V = 1ull << B;
-  GS_TRY(ensure(c, c->out_a, V * 4));
-  GS_TRY(ensure(c, c->out_b, V * 4));
-  Sorted adj;
-  adj.keys = c->out_keys.p;
-  adj.wide = true;
-  adj.key_xor = 0;
-  adj.records = E2;
-  GS_HIP(hipMemsetAsync(c->out_a.p, 0, V * 4, c->stream));   // vertices without edges: degree 0
-  GS_TRY(ensure(c, c->tri_heavy, (V + E2 / 2 / TH_VCH + 64) * 8));   // (v, in-chunk) items
+  // 3. out-lists, then in-lists (sorted by target) carrying each in-entry's suffix of N+(u)
+  GS_TRY(ensure(c, c->tri_heavy, (V + M / TH_VCH + 64) * 8));   // (v, in-chunk) items
   GS_TRY(ensure(c, c->tri_range, V * 16));
-  RowOut ro{c->out_a.as<uint32_t>(), c->out_b.as<uint32_t>()};
-  uint64_t nv = 0;
-  GS_TRY((launch_rbk<uint64_t, CountOp>(c, adj, ro, &nv, B)));
-  // 4. orientation by (degree, id): keep flags, scan, compaction (order preserved)
-  const uint32_t tiles = (uint32_t)((E2 + SCAN_TILE - 1) / SCAN_TILE);
-  GS_TRY(ensure(c, c->tri_keep, E2 + 16));
-  GS_TRY(ensure(c, c->tri_tiles, (tiles + 1) * 4));
-  GS_TRY(ensure(c, c->tri_pos, (E2 + 1) * 4));
-  GS_TRY(ensure(c, c->tri_ou, E2 * 4));
-  GS_TRY(ensure(c, c->tri_onbr, E2 * 4));
-  hipLaunchKernelGGL(k_orient_count, dim3(tiles), dim3(SCAN_BLOCK), 0, c->stream, c->out_keys.as<uint64_t>(),
-                     (uint32_t)E2, B, c->out_a.as<uint32_t>(), c->tri_keep.as<uint8_t>(), c->tri_tiles.as<uint32_t>());
-  hipLaunchKernelGGL(k_scan_tiles, dim3(1), dim3(1024), 0, c->stream, c->tri_tiles.as<uint32_t>(), tiles);
-  hipLaunchKernelGGL(k_orient_scatter, dim3(tiles), dim3(SCAN_BLOCK), 0, c->stream, c->out_keys.as<uint64_t>(),
-                     (uint32_t)E2, B, c->tri_keep.as<uint8_t>(), c->tri_tiles.as<uint32_t>(),
-                     c->tri_pos.as<uint32_t>(), c->tri_ou.as<uint32_t>(), c->tri_onbr.as<uint32_t>());
+  GS_TRY(ensure(c, c->tri_nbr, M * 4));
+  GS_TRY(ensure(c, c->tri_tval, M * 4));
+  GS_TRY(ensure(c, c->tri_pairend, M * 4));
+  GS_TRY(ensure(c, c->tri_sfx, M * 8));
+  uint2* out_range = reinterpret_cast<uint2*>(c->tri_range.p);
+  uint2* in_range = out_range + V;
+  GS_HIP(hipMemsetAsync(c->tri_range.p, 0, V * 16, c->stream));
+  const unsigned ge = (unsigned)std::min<uint64_t>((M + 255) / 256, 16384);
+  uint32_t* nbr = c->tri_nbr.as<uint32_t>();
+  uint2* sfx = c->tri_sfx.as<uint2>();
+  // (the oriented keys in aux are consumed: aux takes the transposed sort's keys)
+  hipLaunchKernelGGL(k_tri_out, dim3(ge), dim3(256), 0, c->stream, c->out_keys.as<uint64_t>(), (uint32_t)M, B, nbr,
+                     reinterpret_cast<uint32_t*>(out_range), c->aux.as<uint64_t>(), c->tri_tval.as<uint32_t>());
+  hipLaunchKernelGGL(k_tri_pairend, dim3(ge), dim3(256), 0, c->stream, c->out_keys.as<uint64_t>(), (uint32_t)M, B,
+                     out_range, c->tri_pairend.as<uint32_t>());
+  GS_HIP(hipGetLastError());
+  Sorted t;
+  GS_TRY(sort_buffer(c, c->aux.as<uint64_t>(), c->tri_tval.as<uint32_t>(), M, &t));
+  if (t.wide || t.key_xor) return set_error(c, GS_EDEVICE, "window triangles: transposed keys wider than 32 bits");
+  hipLaunchKernelGGL(k_tri_in, dim3(ge), dim3(256), 0, c->stream, (const uint32_t*)t.keys, (const uint32_t*)t.vals,
+                     (uint32_t)M, c->tri_pairend.as<uint32_t>(), reinterpret_cast<uint32_t*>(in_range), sfx);
   GS_HIP(hipGetLastError());
   hipEventRecord(c->ev[4], c->stream);
-  const uint64_t M = E2 / 2;   // each undirected edge kept in exactly one direction
   GS_TRY(ensure(c, c->tri_queue, (M / TH_DMAX + 64) * 8));   // further in-list chunks: <= M / TH_DMAX
-  // 5. intersections: vertex-centric LDS hash sets (k_tri_light), long out-lists in k_tri_heavy
+  // 4. intersections: vertex-centric LDS hash sets (k_tri_light), long out-lists in k_tri_heavy
   unsigned long long* d_total = (unsigned long long*)(sm + SM_NUNIQUE);
   uint32_t* d_nheavy = (uint32_t*)(sm + SM_COUNTERS) + 62;
   unsigned long long* d_probes = (unsigned long long*)(sm + SM_TRI_PROBES);
@@ -350,27 +455,21 @@ static gs_status triangles_impl(gs_ctx* c, const gs_edge_batch* b, uint32_t part
   GS_HIP(hipMemsetAsync(d_err, 0, 4, c->stream));
   // LDS hash-set bucket cap: unlimited, or one bucket under GS_FLAG_TEST_TINY_TABLES (tests only)
   const uint32_t nb_cap = (c->flags & GS_FLAG_TEST_TINY_TABLES) ? 1u : 0xFFFFFFFFu;
-  const uint64_t q0 = M * part / nparts, q1 = M * (part + 1) / nparts;   // this part's oriented edges
-  uint2* out_range = reinterpret_cast<uint2*>(c->tri_range.p);
-  uint2* in_range = out_range + V;
+  // this part's middle vertices: those whose out-list starts in [q0, q1) of the adjacency
+  const uint64_t q0 = M * part / nparts, q1 = M * (part + 1) / nparts;
   uint32_t* d_nqueue = d_nheavy + 1;
   GS_HIP(hipMemsetAsync(d_nqueue, 0, 4, c->stream));
-  hipLaunchKernelGGL(k_tri_rows, dim3((unsigned)std::min<uint64_t>((V + 255) / 256, 4096)), dim3(256), 0, c->stream,
-                     c->out_a.as<uint32_t>(), c->out_b.as<uint32_t>(), c->tri_pos.as<uint32_t>(), (uint32_t)V,
-                     out_range, in_range);
   const unsigned nvb = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((V + TH_WPB - 1) / TH_WPB, 8192));
   uint2* queue = c->tri_queue.as<uint2>();
   for (int pass = 0; pass < 2; ++pass) {
-    hipLaunchKernelGGL(k_tri_light, dim3(pass == 0 ? nvb : 4096u), dim3(TH_BLOCK), 0, c->stream,
-                       c->tri_onbr.as<uint32_t>(), c->tri_ou.as<uint32_t>(), out_range, in_range, (uint32_t)V,
-                       (uint32_t)q0, (uint32_t)q1, pass, queue, d_nqueue, c->tri_heavy.as<uint2>(), d_nheavy,
-                       d_total, d_probes, nb_cap, d_err);
+    hipLaunchKernelGGL(k_tri_light, dim3(pass == 0 ? nvb : 4096u), dim3(TH_BLOCK), 0, c->stream, nbr, sfx, out_range,
+                       in_range, (uint32_t)V, (uint32_t)q0, (uint32_t)q1, pass, queue, d_nqueue,
+                       c->tri_heavy.as<uint2>(), d_nheavy, d_total, d_probes, nb_cap, d_err);
     GS_HIP(hipGetLastError());
   }
   hipEventRecord(c->ev[5], c->stream);
-  hipLaunchKernelGGL(k_tri_heavy, dim3(GS_TH_HGRID), dim3(TH_HBLOCK), 0, c->stream, c->tri_onbr.as<uint32_t>(),
-                     c->tri_ou.as<uint32_t>(), out_range, in_range, c->tri_heavy.as<uint2>(), d_nheavy, d_total,
-                     d_probes, nb_cap, d_err);
+  hipLaunchKernelGGL(k_tri_heavy, dim3(GS_TH_HGRID), dim3(TH_HBLOCK), 0, c->stream, nbr, sfx, out_range, in_range,
+                     c->tri_heavy.as<uint2>(), d_nheavy, d_total, d_probes, nb_cap, d_err);
   GS_HIP(hipGetLastError());
   hipEventRecord(c->ev[3], c->stream);
   GS_HIP(hipMemcpyAsync(c->host_small, sm, 32, hipMemcpyDeviceToHost, c->stream));
@@ -390,8 +489,8 @@ static gs_status triangles_impl(gs_ctx* c, const gs_edge_batch* b, uint32_t part
     hipEventElapsedTime(&t.total_ms, c->ev[0], c->ev[3]);
     t.sort_passes = (uint32_t)s.passes;
     t.key_bits = B;
-    t.records = E2;
-    t.vertices = nv;
+    t.records = M;     // unique undirected edges
+    t.vertices = nv;   // vertices with edges
     t.partials = c->host_small[6];
     t.path = 3;
   }

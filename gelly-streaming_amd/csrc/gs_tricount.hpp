@@ -1,18 +1,18 @@
-// gs_tricount.hpp — the counting step of WindowTriangles (gs_graph.hip) on the (degree, id)-oriented
-// graph: every triangle is u -> v, u -> w, v -> w for exactly one (u, v, w), so
-//   T = sum over v of sum over u in N-(v) of |N+(u) ∩ N+(v)|.
-// Adjacency row r of vertex x (sorted, deduplicated) splits by the keep flag into its out-list
-// onbr[pos[r] ..) and its in-list inbr[r - pos[r] ..) (k_orient_scatter); k_tri_rows turns both into
-// one [start, end) pair per vertex.
+// gs_tricount.hpp — the counting step of WindowTriangles (gs_graph.hip) on the degree-renumbered graph
+// (u -> v iff u < v, out-lists sorted): every triangle is u -> v, u -> w, v -> w for exactly one
+// (u, v, w), and w > v, so
+//   T = sum over v of sum over u in N-(v) of |N+(u) after v  ∩  N+(v)|.
+// Row x of the adjacency is [in-list | out-list] in one array (onbr); k_tri_sfx gives every in-entry
+// u of v the range of N+(u) past v (sfx), so a chunk's lists come from one coalesced read.
 //
 // Middle-vertex order: a wave takes v, puts N+(v) into an LDS hash set of 4-slot buckets, spreads the
-// concatenation of N+(u) over a chunk of TH_DMAX in-neighbours u across its lanes (prefix of |N+(u)|
-// in LDS, one search per TH_ILP = 8 consecutive items) and probes each w with one 16-byte LDS read.
-// Probing N+(u) from the middle vertex costs sum_u d+(u)^2 probes, against sum over edges u -> v of
-// d+(v) from the first vertex (R-MAT scale 20: 2.47 G against 4.27 G).  In-lists longer than a chunk
-// queue their further chunks for a second pass (a hub's work spreads over many waves); vertices with
-// more than TH_DMAX out-neighbours go to k_tri_heavy (a block each, N+(v) in a 64 KiB LDS hash
-// set).  Only vertices whose out-list starts in [q0, q1) count (the multi-GPU split).
+// concatenation of the suffixes over a chunk of TH_DMAX in-neighbours u across its lanes (prefix of
+// the lengths in LDS, one search per TH_ILP consecutive items) and probes each w with one 16-byte LDS
+// read.  Probes: sum over u of d+(u)(d+(u)-1)/2 (R-MAT scale 20: 1.23 G; whole lists 2.47 G, first-
+// vertex order 4.42 G).  In-lists longer than a chunk queue their further chunks for a second pass (a
+// hub's work spreads over many waves); vertices with more than TH_DMAX out-neighbours go to
+// k_tri_heavy (a block each, N+(v) in a 64 KiB LDS hash set).  Only vertices whose out-list starts in
+// [q0, q1) count (the multi-GPU split).
 #pragma once
 #include "gs_device.hpp"
 #include "gs_internal.hpp"
@@ -62,28 +62,13 @@ constexpr uint32_t TH_LONG = GS_TH_LONG;
 static_assert(TH_LONG >= 64, "a 64-item segment must not span more than two long lists");
 
 __device__ __forceinline__ uint32_t th_hash(uint32_t x, uint32_t mask) { return ((x * 0x9E3779B1u) >> 7) & mask; }
+// a value the code keeps equal on every lane of the wave (LDS broadcast reads, per-wave bounds): into
+// an SGPR, so loops over it compile to scalar branches instead of exec-masked per-lane loops
+__device__ __forceinline__ uint32_t uni(uint32_t x) { return __builtin_amdgcn_readfirstlane(x); }
 // LDS written by some lanes of a wave, then read by others
 __device__ __forceinline__ void wave_lds_sync() {
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_wave_barrier();
-}
-
-// out-list and in-list [start, end) of every vertex (absent vertices: empty): one 8-byte load per
-// lookup instead of the deg -> rowstart -> pos chain
-__global__ __launch_bounds__(256) void k_tri_rows(const uint32_t* __restrict__ deg, const uint32_t* __restrict__ rowstart,
-                                                  const uint32_t* __restrict__ pos, uint32_t nv,
-                                                  uint2* __restrict__ out_range, uint2* __restrict__ in_range) {
-  for (uint32_t x = blockIdx.x * 256u + threadIdx.x; x < nv; x += gridDim.x * 256u) {
-    const uint32_t dg = deg[x];
-    uint2 ro = make_uint2(0, 0), ri = make_uint2(0, 0);
-    if (dg) {
-      const uint32_t rs = rowstart[x];
-      ro = make_uint2(pos[rs], pos[rs + dg]);
-      ri = make_uint2(rs - ro.x, rs + dg - ro.y);
-    }
-    out_range[x] = ro;
-    in_range[x] = ri;
-  }
 }
 
 // Every insert and probe chain is bounded by the table's bucket count: a full table (which the
@@ -125,7 +110,7 @@ __device__ __forceinline__ uint32_t th_probe(const uint4* hb, uint32_t bmask, co
     const uint32_t m = slot_xor_min(y[j], x[j]);
     const uint32_t on = (uint32_t)j < nv ? 1u : 0u;
     cnt += (m == 0u) ? on : 0u;
-    walk |= ((m != 0u) & (y[j].w != TH_EMPTY) ? on : 0u) << j;
+    walk |= (((m != 0u) & (y[j].w != TH_EMPTY)) ? on : 0u) << j;
   }
   if (walk) {   // rare: chains that continue past their first bucket
 #pragma unroll
@@ -151,9 +136,9 @@ __device__ __forceinline__ uint32_t th_probe(const uint4* hb, uint32_t bmask, co
   return cnt;
 }
 
-// one wave: |N+(u) ∩ N+(v)| summed over the in-neighbours u = inbr[c0 .. c1) of v
-__device__ __forceinline__ uint32_t th_wave_chunk(const uint32_t* __restrict__ onbr, const uint32_t* __restrict__ inbr,
-                                                  const uint2* __restrict__ out_range, uint2 ro, uint32_t c0,
+// one wave: |suffix of N+(u) ∩ N+(v)| summed over the in-entries c0 .. c1 of v
+__device__ __forceinline__ uint32_t th_wave_chunk(const uint32_t* __restrict__ onbr, const uint2* __restrict__ sfx,
+                                                  uint2 ro, uint32_t c0,
                                                   uint32_t c1, int lane, uint4* hb, uint32_t* po, uint32_t* ps,
                                                   uint64_t& probes, uint32_t nb_cap, uint32_t* err) {
   uint32_t* hs = reinterpret_cast<uint32_t*>(hb);
@@ -173,7 +158,7 @@ __device__ __forceinline__ uint32_t th_wave_chunk(const uint32_t* __restrict__ o
     const uint32_t i = i0 + lane;
     uint32_t du = 0, su = 0;
     if (i < c1) {
-      const uint2 ru = out_range[inbr[i]];
+      const uint2 ru = sfx[i];
       du = ru.y - ru.x;
       su = ru.x;
     }
@@ -191,8 +176,8 @@ __device__ __forceinline__ uint32_t th_wave_chunk(const uint32_t* __restrict__ o
       po[at] = lrun + incl - dl;
       ps[at] = su;
     }
-    run += __shfl(inc, WAVE - 1, WAVE);
-    lrun += __shfl(incl, WAVE - 1, WAVE);
+    run += uni(__shfl(inc, WAVE - 1, WAVE));
+    lrun += uni(__shfl(incl, WAVE - 1, WAVE));
     dn += (uint32_t)__popcll(ms);
     nl += (uint32_t)__popcll(ml);
   }
@@ -201,8 +186,8 @@ __device__ __forceinline__ uint32_t th_wave_chunk(const uint32_t* __restrict__ o
   uint32_t lcnt = 0;
   if (nl) {   // long lists: segment k of 64 items lies in list q or q + 1 (every long list >= 64 items)
     uint32_t q = 0;
-    uint32_t qo = po[TH_DMAX - 1], qs = ps[TH_DMAX - 1];
-    uint32_t qe = nl > 1 ? po[TH_DMAX - 2] : lrun, q1s = nl > 1 ? ps[TH_DMAX - 2] : 0u;
+    uint32_t qo = uni(po[TH_DMAX - 1]), qs = uni(ps[TH_DMAX - 1]);
+    uint32_t qe = nl > 1 ? uni(po[TH_DMAX - 2]) : lrun, q1s = nl > 1 ? uni(ps[TH_DMAX - 2]) : 0u;
     for (uint32_t k0 = 0; k0 < lrun; k0 += WAVE * TH_ILP) {
       uint32_t x[TH_ILP];
 #pragma unroll
@@ -212,8 +197,8 @@ __device__ __forceinline__ uint32_t th_wave_chunk(const uint32_t* __restrict__ o
           ++q;
           qo = qe;
           qs = q1s;
-          qe = q + 1 < nl ? po[TH_DMAX - 2 - q] : lrun;
-          q1s = q + 1 < nl ? ps[TH_DMAX - 2 - q] : 0u;
+          qe = q + 1 < nl ? uni(po[TH_DMAX - 2 - q]) : lrun;
+          q1s = q + 1 < nl ? uni(ps[TH_DMAX - 2 - q]) : 0u;
         }
         const uint32_t k = min(seg + (uint32_t)lane, lrun - 1);
         x[j] = onbr[k < qe ? qs + (k - qo) : q1s + (k - qe)];
@@ -294,7 +279,7 @@ __device__ __forceinline__ uint32_t th_wave_chunk(const uint32_t* __restrict__ o
 //   heavy list.  pass 1: the queued (v, chunk) items.  n_probes counts the hash probes (bench bytes).
 // 40 KiB of LDS per block -> four blocks (16 waves) per CU: registers capped to match (128 VGPRs)
 __global__ __launch_bounds__(TH_BLOCK) __attribute__((amdgpu_waves_per_eu(4, 4))) void k_tri_light(const uint32_t* __restrict__ onbr,
-                                                        const uint32_t* __restrict__ inbr,
+                                                        const uint2* __restrict__ sfx,
                                                         const uint2* __restrict__ out_range,
                                                         const uint2* __restrict__ in_range, uint32_t nv, uint32_t q0,
                                                         uint32_t q1, int pass, uint2* __restrict__ queue,
@@ -341,7 +326,7 @@ __global__ __launch_bounds__(TH_BLOCK) __attribute__((amdgpu_waves_per_eu(4, 4))
       c0 = ri.x + q.y * TH_DMAX;
       c1 = min(ri.y, c0 + TH_DMAX);
     }
-    cnt += th_wave_chunk(onbr, inbr, out_range, out_range[v], c0, c1, lane, s_hash[w], s_off[w], s_st[w], probes,
+    cnt += th_wave_chunk(onbr, sfx, out_range[v], c0, c1, lane, s_hash[w], s_off[w], s_st[w], probes,
                          nb_cap, err);
   }
 #pragma unroll
@@ -356,7 +341,7 @@ __global__ __launch_bounds__(TH_BLOCK) __attribute__((amdgpu_waves_per_eu(4, 4))
 // many blocks (one block per heavy vertex left the hubs' blocks running long after the rest).
 // two 512-thread blocks per CU (72 KiB of LDS each): registers capped to match (128 VGPRs)
 __global__ __launch_bounds__(TH_HBLOCK) __attribute__((amdgpu_waves_per_eu(4, 4))) void k_tri_heavy(const uint32_t* __restrict__ onbr,
-                                                         const uint32_t* __restrict__ inbr,
+                                                         const uint2* __restrict__ sfx,
                                                          const uint2* __restrict__ out_range,
                                                          const uint2* __restrict__ in_range,
                                                          const uint2* __restrict__ heavy,
@@ -423,7 +408,7 @@ __global__ __launch_bounds__(TH_HBLOCK) __attribute__((amdgpu_waves_per_eu(4, 4)
 #pragma unroll
     for (int j = 0; j < PER; ++j) {
       const uint32_t i = tid * PER + j;
-      const uint2 ru = out_range[inbr[c0 + min(i, cn - 1)]];
+      const uint2 ru = sfx[c0 + min(i, cn - 1)];
       su[j] = ru.x;
       du[j] = i < cn ? ru.y - ru.x : 0u;
       if (du[j] >= TH_LONG) { mine.z += 1; mine.w += du[j]; }
@@ -456,7 +441,7 @@ __global__ __launch_bounds__(TH_HBLOCK) __attribute__((amdgpu_waves_per_eu(4, 4)
         so += du[j];
       }
     }
-    const uint32_t ns = tot.x, srun = tot.y, nl = tot.z, lrun = tot.w;
+    const uint32_t ns = uni(tot.x), srun = uni(tot.y), nl = uni(tot.z), lrun = uni(tot.w);
     if (tid == 0) {
       s_off[ns] = srun;
       s_loff[nl] = lrun;
@@ -492,17 +477,18 @@ __global__ __launch_bounds__(TH_HBLOCK) __attribute__((amdgpu_waves_per_eu(4, 4)
     // long lists: wave w walks items [w, w + 1) * lrun / NW in 64-item segments (one load of 64
     // consecutive items); a segment spans at most two lists (every long list >= 64 items)
     if (lrun) {
-      const uint32_t a0 = (uint32_t)((uint64_t)lrun * w / NW), a1 = (uint32_t)((uint64_t)lrun * (w + 1) / NW);
+      const uint32_t wu = uni((uint32_t)w);
+      const uint32_t a0 = uni((uint32_t)((uint64_t)lrun * wu / NW)), a1 = uni((uint32_t)((uint64_t)lrun * (wu + 1) / NW));
       uint32_t q = 0;
       {
         uint32_t t2 = 1;
         while (2 * t2 < nl) t2 <<= 1;
         for (uint32_t st = t2; st; st >>= 1) {
           const uint32_t t = q + st;
-          q = (t < nl && s_loff[min(t, nl - 1)] <= a0) ? t : q;
+          q = (t < nl && uni(s_loff[min(t, nl - 1)]) <= a0) ? t : q;
         }
       }
-      uint32_t qo = s_loff[q], qs = s_lst[q], qe = s_loff[q + 1], q1s = q + 1 < nl ? s_lst[q + 1] : 0u;
+      uint32_t qo = uni(s_loff[q]), qs = uni(s_lst[q]), qe = uni(s_loff[q + 1]), q1s = q + 1 < nl ? uni(s_lst[q + 1]) : 0u;
       for (uint32_t k0 = a0; k0 < a1; k0 += WAVE * TH_ILP) {
         uint32_t x[TH_ILP];
 #pragma unroll
@@ -512,8 +498,8 @@ __global__ __launch_bounds__(TH_HBLOCK) __attribute__((amdgpu_waves_per_eu(4, 4)
             ++q;
             qo = qe;
             qs = q1s;
-            qe = s_loff[q + 1];
-            q1s = q + 1 < nl ? s_lst[q + 1] : 0u;
+            qe = uni(s_loff[q + 1]);
+            q1s = q + 1 < nl ? uni(s_lst[q + 1]) : 0u;
           }
           const uint32_t k = min(seg + (uint32_t)lane, a1 - 1);
           x[j] = onbr[k < qe ? qs + (k - qo) : q1s + (k - qe)];
