@@ -468,9 +468,23 @@ static gs_status triangles_impl(gs_ctx* c, const gs_edge_batch* b, uint32_t part
     GS_HIP(hipGetLastError());
   }
   hipEventRecord(c->ev[5], c->stream);
-  hipLaunchKernelGGL(k_tri_heavy, dim3(GS_TH_HGRID), dim3(TH_HBLOCK), 0, c->stream, nbr, sfx, out_range, in_range,
-                     c->tri_heavy.as<uint2>(), d_nheavy, d_total, d_probes, nb_cap, d_err);
-  GS_HIP(hipGetLastError());
+  // heavy items: work per item, exclusive scan, then equal-work runs per block
+  c->host_small[6] = 0;
+  GS_HIP(hipMemcpyAsync(c->host_small + 6, d_nheavy, 4, hipMemcpyDeviceToHost, c->stream));
+  GS_TRY(host_wait(c));
+  const uint32_t nh = (uint32_t)c->host_small[6];
+  if (nh) {
+    GS_TRY(ensure(c, c->tri_hwork, (size_t)nh * 16 + 8));
+    unsigned long long* hw = c->tri_hwork.as<unsigned long long>();
+    hipLaunchKernelGGL(k_tri_hwork, dim3((unsigned)std::min<uint64_t>((nh + 3) / 4, 16384)), dim3(256), 0, c->stream,
+                       sfx, in_range, c->tri_heavy.as<uint2>(), nh, hw);
+    GS_HIP(hipGetLastError());
+    GS_TRY(xscan(c, (const uint64_t*)hw, nh, (uint64_t*)hw + nh));
+    hipLaunchKernelGGL(k_tri_heavy, dim3(GS_TH_HGRID), dim3(TH_HBLOCK), 0, c->stream, nbr, sfx, out_range, in_range,
+                       c->tri_heavy.as<uint2>(), d_nheavy, (const unsigned long long*)hw + nh, d_total, d_probes,
+                       nb_cap, d_err);
+    GS_HIP(hipGetLastError());
+  }
   hipEventRecord(c->ev[3], c->stream);
   GS_HIP(hipMemcpyAsync(c->host_small, sm, 32, hipMemcpyDeviceToHost, c->stream));
   GS_HIP(hipMemcpyAsync(c->host_small + 6, d_probes, 8, hipMemcpyDeviceToHost, c->stream));

@@ -61,7 +61,7 @@ struct gs_ctx {
   // fused last pass: partials with gaps, compacted partials
   gs::DevBuf part_k, part_a, comp_k, comp_a;
   // triangles
-  gs::DevBuf tri_loops, tri_pairend, tri_tiles, tri_tval, tri_sfx, tri_nbr, tri_heavy, tri_range, tri_queue;
+  gs::DevBuf tri_loops, tri_pairend, tri_tiles, tri_tval, tri_sfx, tri_nbr, tri_heavy, tri_range, tri_queue, tri_hwork;
   // HashSet-order pipeline (gs_hashset.hip)
   gs::DevBuf hs[20];
   // bucket path (gs_bucket.hip): plan tables, work items, LDS slabs of multi-item buckets

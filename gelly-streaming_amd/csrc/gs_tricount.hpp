@@ -20,21 +20,21 @@
 namespace gs {
 
 constexpr int TH_BLOCK = 256, TH_WPB = TH_BLOCK / WAVE;
-// k_tri_heavy: 512 threads, two blocks per CU, N+(v) of up to TH_NU entries in LDS, in-neighbours in
-// chunks of TH_VCH (one 1024-thread block per CU with a 16384-entry table: s22 70.9 -> 67.8 ms, s24
-// 315.7 -> 307.0; chunks of 512 instead of 1024: 67.4 -> 66.2, 305.8 -> 302.5)
+// k_tri_heavy: 512 threads, three blocks per CU, N+(v) of up to TH_NU entries in LDS, in-entries in
+// chunks of TH_VCH (history: one 1024-thread block per CU with a 16384-entry table, s22 70.9 -> 67.8
+// ms; one 512-thread block per CU instead of two: 11.4 -> 17.9 ms; chunks of 512 / 1024 / 2048: equal)
 #ifndef GS_TH_HBLOCK
 #define GS_TH_HBLOCK 512
 #endif
 #ifndef GS_TH_NU
-#define GS_TH_NU 8192
+#define GS_TH_NU 4096   // heavy N+(v) up to 4096 in a 32 KiB LDS table (longer: HBM search)
 #endif
 #ifndef GS_TH_HGRID
-#define GS_TH_HGRID 512   // heavy blocks in the grid: two per CU (68 KiB LDS each)
+#define GS_TH_HGRID 768   // heavy blocks in the grid: three per CU (49 KiB LDS each)
 #endif
 constexpr int TH_HBLOCK = GS_TH_HBLOCK;
 #ifndef GS_TH_VCH
-#define GS_TH_VCH 512
+#define GS_TH_VCH 1024
 #endif
 constexpr uint32_t TH_NU = GS_TH_NU, TH_HB = TH_NU / 2, TH_VCH = GS_TH_VCH;   // TH_HB 4-slot buckets: load <= 1/2
 static_assert(TH_VCH % TH_HBLOCK == 0, "TH_VCH must be a multiple of TH_HBLOCK");
@@ -49,7 +49,7 @@ constexpr uint32_t TH_DMAX = GS_TH_DMAX, TH_H = GS_TH_H, TH_EMPTY = 0xFFFFFFFFu;
 // and probe chains end at a free slot, so a full table would never end them
 static_assert(TH_DMAX * 2 <= TH_H, "TH_DMAX must be <= TH_H / 2");
 #ifndef GS_TH_ILP
-#define GS_TH_ILP 10   // R-MAT s22 (DMAX 512): 2 -> 93.9 ms, 4 -> 70.2, 6 -> 62.6, 8 -> 62.0, 12 -> 64.5, 16 -> 137.8; DMAX 256: 6 -> 55.3, 8 -> 55.8, 10 -> 54.5 (s24 291.9, 289.6, 279.7)
+#define GS_TH_ILP 8    // R-MAT s22 (DMAX 512): 2 -> 93.9 ms, 4 -> 70.2, 6 -> 62.6, 8 -> 62.0, 12 -> 64.5, 16 -> 137.8; DMAX 256: 6 -> 55.3, 8 -> 55.8, 10 -> 54.5 (s24 291.9, 289.6, 279.7); 6 waves/SIMD: 6 -> 23.8, 8 -> 23.7, 10 -> 23.8 (spills)
 #endif
 constexpr int TH_ILP = GS_TH_ILP;   // items per lane: TH_ILP probes in flight
 #ifndef GS_TH_LANEIL
@@ -59,6 +59,12 @@ constexpr int TH_ILP = GS_TH_ILP;   // items per lane: TH_ILP probes in flight
 #define GS_TH_LONG 64    // light kernel: out-lists of >= TH_LONG items are gathered lane-interleaved (64 per load)
 #endif
 constexpr uint32_t TH_LONG = GS_TH_LONG;
+#ifndef GS_TH_LWAVES
+#define GS_TH_LWAVES 6   // k_tri_light waves per SIMD the registers are capped for (4 -> 6: s22 3.03 -> 2.38 ms)
+#endif
+#ifndef GS_TH_HWAVES
+#define GS_TH_HWAVES 6   // k_tri_heavy: three 512-thread blocks per CU (4 -> 6: s22 11.4 -> 9.8 ms, s24 72.3 -> 62.5)
+#endif
 static_assert(TH_LONG >= 64, "a 64-item segment must not span more than two long lists");
 
 __device__ __forceinline__ uint32_t th_hash(uint32_t x, uint32_t mask) { return ((x * 0x9E3779B1u) >> 7) & mask; }
@@ -136,23 +142,15 @@ __device__ __forceinline__ uint32_t th_probe(const uint4* hb, uint32_t bmask, co
   return cnt;
 }
 
-// one wave: |suffix of N+(u) ∩ N+(v)| summed over the in-entries c0 .. c1 of v
-__device__ __forceinline__ uint32_t th_wave_chunk(const uint32_t* __restrict__ onbr, const uint2* __restrict__ sfx,
-                                                  uint2 ro, uint32_t c0,
-                                                  uint32_t c1, int lane, uint4* hb, uint32_t* po, uint32_t* ps,
-                                                  uint64_t& probes, uint32_t nb_cap, uint32_t* err) {
-  uint32_t* hs = reinterpret_cast<uint32_t*>(hb);
-  const uint32_t d = ro.y - ro.x;
-  uint32_t nb = 16;
-  while (nb < d && nb < TH_H / 4) nb <<= 1;
-  nb = min(nb, nb_cap);
-  const uint32_t bmask = nb - 1;
-  for (uint32_t i = lane; i < nb * 4; i += WAVE) hs[i] = TH_EMPTY;
-  wave_lds_sync();
-  for (uint32_t i = lane; i < d; i += WAVE) th_insert(hs, onbr[ro.x + i], bmask, err);
-  // lists of >= TH_LONG items ("long") are gathered lane-interleaved (64 consecutive items per load:
-  // 2 cache lines); the short ones TH_ILP consecutive items per lane.  Short lists fill po / ps from
-  // the front (po = prefix of their lengths), long ones from the back (po = prefix over long lists)
+// one wave: |suffix of N+(u) ∩ N+(v)| summed over the in-entries c0 .. c1 (<= CAP) of v, N+(v)
+// behind probe(x, nv) (an LDS hash set, or a search in HBM)
+// lists of >= TH_LONG items ("long") are gathered lane-interleaved (64 consecutive items per load:
+// 2 cache lines); the short ones TH_ILP consecutive items per lane.  Short lists fill po / ps from the
+// front (po = prefix of their lengths), long ones from the back (po = prefix over long lists)
+template <uint32_t CAP, class Probe>
+__device__ __forceinline__ uint32_t th_wave_probe(const uint32_t* __restrict__ onbr, const uint2* __restrict__ sfx,
+                                                  uint32_t c0, uint32_t c1, int lane, uint32_t* po, uint32_t* ps,
+                                                  uint64_t& probes, Probe probe) {
   uint32_t run = 0, dn = 0, lrun = 0, nl = 0;
   for (uint32_t i0 = c0; i0 < c1; i0 += WAVE) {
     const uint32_t i = i0 + lane;
@@ -172,7 +170,7 @@ __device__ __forceinline__ uint32_t th_wave_chunk(const uint32_t* __restrict__ o
       ps[at] = su;
     }
     if (lg) {
-      const uint32_t at = TH_DMAX - 1 - (nl + mbcnt(ml));
+      const uint32_t at = CAP - 1 - (nl + mbcnt(ml));
       po[at] = lrun + incl - dl;
       ps[at] = su;
     }
@@ -183,11 +181,11 @@ __device__ __forceinline__ uint32_t th_wave_chunk(const uint32_t* __restrict__ o
   }
   wave_lds_sync();
   probes += run + lrun;
-  uint32_t lcnt = 0;
+  uint32_t cnt = 0;
   if (nl) {   // long lists: segment k of 64 items lies in list q or q + 1 (every long list >= 64 items)
     uint32_t q = 0;
-    uint32_t qo = uni(po[TH_DMAX - 1]), qs = uni(ps[TH_DMAX - 1]);
-    uint32_t qe = nl > 1 ? uni(po[TH_DMAX - 2]) : lrun, q1s = nl > 1 ? uni(ps[TH_DMAX - 2]) : 0u;
+    uint32_t qo = uni(po[CAP - 1]), qs = uni(ps[CAP - 1]);
+    uint32_t qe = nl > 1 ? uni(po[CAP - 2]) : lrun, q1s = nl > 1 ? uni(ps[CAP - 2]) : 0u;
     for (uint32_t k0 = 0; k0 < lrun; k0 += WAVE * TH_ILP) {
       uint32_t x[TH_ILP];
 #pragma unroll
@@ -197,8 +195,8 @@ __device__ __forceinline__ uint32_t th_wave_chunk(const uint32_t* __restrict__ o
           ++q;
           qo = qe;
           qs = q1s;
-          qe = q + 1 < nl ? uni(po[TH_DMAX - 2 - q]) : lrun;
-          q1s = q + 1 < nl ? uni(ps[TH_DMAX - 2 - q]) : 0u;
+          qe = q + 1 < nl ? uni(po[CAP - 2 - q]) : lrun;
+          q1s = q + 1 < nl ? uni(ps[CAP - 2 - q]) : 0u;
         }
         const uint32_t k = min(seg + (uint32_t)lane, lrun - 1);
         x[j] = onbr[k < qe ? qs + (k - qo) : q1s + (k - qe)];
@@ -206,43 +204,11 @@ __device__ __forceinline__ uint32_t th_wave_chunk(const uint32_t* __restrict__ o
       // valid items of this lane: segments j with k0 + 64 j + lane < lrun (a prefix of j)
       const uint32_t rem = lrun - k0;
       const uint32_t nv = rem > (uint32_t)lane ? min((uint32_t)TH_ILP, (rem - lane + WAVE - 1) / WAVE) : 0u;
-      lcnt += th_probe(hb, bmask, x, nv, err);
+      cnt += probe(x, nv);
     }
   }
   uint32_t top = 1;
   while (2 * top < dn) top <<= 1;
-  uint32_t cnt = lcnt;
-#if GS_TH_LANEIL
-  // lane-interleaved items: the j-th gather of a wave reads 64 consecutive items of the concatenated
-  // lists (a few cache lines) instead of 64 runs of TH_ILP items spread over the whole chunk
-  for (uint32_t k0 = 0; k0 < run; k0 += WAVE * TH_ILP) {
-    uint32_t x[TH_ILP], lo = 0;
-    {
-      const uint32_t kk = min(k0 + (uint32_t)lane, run - 1);
-      for (uint32_t st = top; st; st >>= 1) {
-        const uint32_t t = lo + st;
-        const uint32_t pv = t < dn ? po[min(t, dn - 1)] : run;
-        lo = pv <= kk ? t : lo;
-      }
-    }
-#pragma unroll
-    for (int j = 0; j < TH_ILP; ++j) {
-      const uint32_t kj = min(k0 + (uint32_t)(j * WAVE + lane), run - 1);
-      if (j) {
-        // 64 items further: at most 64 boundaries crossed (every kept list has >= 1 item)
-#pragma unroll
-        for (uint32_t st = WAVE; st; st >>= 1) {
-          const uint32_t t = lo + st;
-          const uint32_t pv = t < dn ? po[min(t, dn - 1)] : run;
-          lo = pv <= kj ? t : lo;
-        }
-      }
-      x[j] = onbr[ps[lo] + (kj - po[lo])];
-    }
-    const uint32_t rem = run - k0;
-    cnt += th_probe(hb, bmask, x, rem > (uint32_t)lane ? min((uint32_t)TH_ILP, (rem - lane + WAVE - 1) / WAVE) : 0u, err);
-  }
-#else
   for (uint32_t k0 = 0; k0 < run; k0 += WAVE * TH_ILP) {
     const uint32_t kb = k0 + lane * TH_ILP;
     const uint32_t kk = min(kb, run - 1);
@@ -268,17 +234,35 @@ __device__ __forceinline__ uint32_t th_wave_chunk(const uint32_t* __restrict__ o
       }
       x[j] = onbr[st + (kj - o)];
     }
-    cnt += th_probe(hb, bmask, x, kb < run ? min((uint32_t)TH_ILP, run - kb) : 0u, err);
+    cnt += probe(x, kb < run ? min((uint32_t)TH_ILP, run - kb) : 0u);
   }
-#endif
-  wave_lds_sync();   // the next item clears the table
+  wave_lds_sync();   // po / ps are reused by the next chunk
   return cnt;
+}
+
+// one wave: N+(v) into the wave's own LDS hash set, then the in-entries c0 .. c1 (<= TH_DMAX) of v
+__device__ __forceinline__ uint32_t th_wave_chunk(const uint32_t* __restrict__ onbr, const uint2* __restrict__ sfx,
+                                                  uint2 ro, uint32_t c0,
+                                                  uint32_t c1, int lane, uint4* hb, uint32_t* po, uint32_t* ps,
+                                                  uint64_t& probes, uint32_t nb_cap, uint32_t* err) {
+  uint32_t* hs = reinterpret_cast<uint32_t*>(hb);
+  const uint32_t d = ro.y - ro.x;
+  uint32_t nb = 16;
+  while (nb < d && nb < TH_H / 4) nb <<= 1;
+  nb = min(nb, nb_cap);
+  const uint32_t bmask = nb - 1;
+  for (uint32_t i = lane; i < nb * 4; i += WAVE) hs[i] = TH_EMPTY;
+  wave_lds_sync();
+  for (uint32_t i = lane; i < d; i += WAVE) th_insert(hs, onbr[ro.x + i], bmask, err);
+  wave_lds_sync();
+  return th_wave_probe<TH_DMAX>(onbr, sfx, c0, c1, lane, po, ps, probes,
+                                [&](const uint32_t (&x)[TH_ILP], uint32_t nv) { return th_probe(hb, bmask, x, nv, err); });
 }
 
 // pass 0: vertices, interleaved; first in-chunk here, further chunks queued, long out-lists to the
 //   heavy list.  pass 1: the queued (v, chunk) items.  n_probes counts the hash probes (bench bytes).
-// 40 KiB of LDS per block -> four blocks (16 waves) per CU: registers capped to match (128 VGPRs)
-__global__ __launch_bounds__(TH_BLOCK) __attribute__((amdgpu_waves_per_eu(4, 4))) void k_tri_light(const uint32_t* __restrict__ onbr,
+// 24 KiB of LDS per block -> six blocks (24 waves) per CU: registers capped to match (80 VGPRs)
+__global__ __launch_bounds__(TH_BLOCK) __attribute__((amdgpu_waves_per_eu(GS_TH_LWAVES, GS_TH_LWAVES))) void k_tri_light(const uint32_t* __restrict__ onbr,
                                                         const uint2* __restrict__ sfx,
                                                         const uint2* __restrict__ out_range,
                                                         const uint2* __restrict__ in_range, uint32_t nv, uint32_t q0,
@@ -288,7 +272,7 @@ __global__ __launch_bounds__(TH_BLOCK) __attribute__((amdgpu_waves_per_eu(4, 4))
                                                         unsigned long long* __restrict__ total,
                                                         unsigned long long* __restrict__ n_probes, uint32_t nb_cap,
                                                         uint32_t* __restrict__ err) {
-  // 8 KiB per wave, 32 KiB per block: five blocks per CU
+  // 6 KiB per wave (4 KiB table + 2 KiB list prefix), 24 KiB per block
   __shared__ uint4 s_hash[TH_WPB][TH_H / 4];
   __shared__ uint32_t s_off[TH_WPB][TH_DMAX];   // exclusive prefix of |N+(u)| over the non-empty u
   __shared__ uint32_t s_st[TH_WPB][TH_DMAX];    // start of that N+(u) in onbr
@@ -335,17 +319,39 @@ __global__ __launch_bounds__(TH_BLOCK) __attribute__((amdgpu_waves_per_eu(4, 4))
   if (lane == 0 && probes) atomicAdd(n_probes, (unsigned long long)probes);   // wave-uniform
 }
 
+// work of each heavy item (v, chunk of TH_VCH in-entries): its probes (the suffix lengths) plus a
+// fixed cost per in-entry; one wave per item
+__global__ __launch_bounds__(256) void k_tri_hwork(const uint2* __restrict__ sfx, const uint2* __restrict__ in_range,
+                                                   const uint2* __restrict__ heavy, uint32_t nh,
+                                                   unsigned long long* __restrict__ work) {
+  const int lane = threadIdx.x & 63;
+  for (uint32_t h = (blockIdx.x * 256u + threadIdx.x) / WAVE; h < nh; h += gridDim.x * (256u / WAVE)) {
+    const uint2 item = heavy[h];
+    const uint2 ri = in_range[item.x];
+    const uint32_t c0 = ri.x + item.y * TH_VCH, c1 = min(ri.y, c0 + TH_VCH);
+    uint32_t w = 0;
+    for (uint32_t i = c0 + lane; i < c1; i += WAVE) {
+      const uint2 r = sfx[i];
+      w += r.y - r.x + 4u;
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) w += __shfl_xor(w, o, WAVE);
+    if (lane == 0) work[h] = w;
+  }
+}
+
 // one block per heavy item (v, chunk of TH_VCH in-neighbours): N+(v) as an LDS hash set (up to TH_NU
 // entries; longer lists are binary-searched in HBM; rebuilt only when the block's item changes v),
 // the chunk's lists TH_ILP items per thread with one search.  One item per in-chunk spreads a hub over
 // many blocks (one block per heavy vertex left the hubs' blocks running long after the rest).
-// two 512-thread blocks per CU (72 KiB of LDS each): registers capped to match (128 VGPRs)
-__global__ __launch_bounds__(TH_HBLOCK) __attribute__((amdgpu_waves_per_eu(4, 4))) void k_tri_heavy(const uint32_t* __restrict__ onbr,
+// three 512-thread blocks per CU (49 KiB of LDS each): registers capped to match (80 VGPRs)
+__global__ __launch_bounds__(TH_HBLOCK) __attribute__((amdgpu_waves_per_eu(GS_TH_HWAVES, GS_TH_HWAVES))) void k_tri_heavy(const uint32_t* __restrict__ onbr,
                                                          const uint2* __restrict__ sfx,
                                                          const uint2* __restrict__ out_range,
                                                          const uint2* __restrict__ in_range,
                                                          const uint2* __restrict__ heavy,
                                                          const uint32_t* __restrict__ n_heavy,
+                                                         const unsigned long long* __restrict__ pre,
                                                          unsigned long long* __restrict__ total,
                                                          unsigned long long* __restrict__ n_probes, uint32_t nb_cap,
                                                          uint32_t* __restrict__ err) {
@@ -362,10 +368,25 @@ __global__ __launch_bounds__(TH_HBLOCK) __attribute__((amdgpu_waves_per_eu(4, 4)
   uint64_t cnt = 0, probes = 0;
   const uint32_t nh = *n_heavy;
   uint32_t table_v = TH_EMPTY;   // the vertex whose N+ the LDS table holds (block-uniform)
-  // a contiguous run of items per block: the chunks of one heavy vertex are consecutive items, so a
-  // block rebuilds its table only when its run moves to the next vertex
-  const uint32_t per_b = (nh + gridDim.x - 1) / gridDim.x;
-  const uint32_t h0 = min(nh, blockIdx.x * per_b), h1 = min(nh, h0 + per_b);
+  // a contiguous run of items per block, cut at equal shares of the items' work (k_tri_hwork +
+  // exclusive scan: pre[h] = work before item h, pre[nh] = total): the chunks of one heavy vertex are
+  // consecutive items, so a block rebuilds its table only when its run moves to the next vertex
+  uint32_t h0, h1;
+  {
+    const unsigned long long W = pre[nh];
+    auto lower = [&](unsigned long long t) {   // first h with pre[h] >= t
+      uint32_t a = 0, b = nh;
+      while (a < b) {
+        const uint32_t m = (a + b) >> 1;
+        if (pre[m] < t) a = m + 1;
+        else b = m;
+      }
+      return a;
+    };
+    const unsigned long long lo = W * blockIdx.x / gridDim.x, hi = W * (blockIdx.x + 1) / gridDim.x;
+    h0 = uni(lower(lo));
+    h1 = blockIdx.x + 1 == gridDim.x ? nh : uni(lower(hi));
+  }
   for (uint32_t hi = h0; hi < h1; ++hi) {
     const uint2 item = heavy[hi];   // (v, in-chunk)
     const uint32_t v = item.x;

@@ -121,7 +121,7 @@ def _clique(n, shuffle_seed):
 
 def test_triangles_clique_hub_chunks(engine, oracle):
     """K_n has C(n, 3) triangles (pinned on K_30 by the oracle).  On K_4200 the (degree, id) orientation
-    gives out-lists up to 4199 > TH_VCH (4096): k_tri_heavy's several v chunks."""
+    gives out-lists up to 4199 > TH_VCH: k_tri_heavy's several in-entry chunks."""
     from math import comb
     s, d = _clique(30, 1)
     w, ex, has = oracle.window_triangles_fwd(s, d)
@@ -215,6 +215,22 @@ def test_triangles_with_self_loops(engine, oracle):
             continue
         ex, wrapped, has = engine.triangles(s, d)
         assert (ex, wrapped, has) == (ex_ref, w_ref, has_ref), trial
+
+
+@pytest.mark.parametrize("flags", [0, 1, 2])
+def test_triangles_degree_paths(pkg, oracle, flags):
+    """The renumbering's raw degrees come from the bucket path (COUNT over both endpoints); a ctx
+    that refuses it (GS_FLAG_SORT_ONLY) or an id range too wide for its buckets takes the global-
+    atomic fallback (k_tri_deg).  Every path gives the exact count (any vertex order does)."""
+    from gelly_streaming_amd import _lib as L
+    s, d = oracle.gen_rmat(13, 150_000, 0x5EED07, no_self_loops=True)
+    if flags == 2:   # spread the ids over 2^27: beyond the bucket path's range, within 28 key bits
+        s, d = s * 13_001 + 5, d * 13_001 + 5
+        flags = 0
+    w, ex, has = oracle.window_triangles_fwd(s, d)
+    with pkg.Engine(0, flags=L.GS_FLAG_SORT_ONLY if flags else 0) as e:
+        got = e.triangles(*[torch.from_numpy(x).cuda() for x in (s, d)])
+    assert got == (ex, w, has)
 
 
 def test_triangles_parts_sum_to_whole(engine, oracle):
