@@ -257,11 +257,13 @@ static gs_status buffer_passes(gs_ctx* c, const uint64_t* keys, const V* vals, u
   return GS_OK;
 }
 
-gs_status sort_buffer(gs_ctx* c, const uint64_t* keys, const uint32_t* vals, uint64_t n, Sorted* out) {
+gs_status sort_buffer(gs_ctx* c, const uint64_t* keys, const void* vals, uint64_t n, Sorted* out, int bits_hint,
+                      int val_bytes) {
   char* sm = c->small.as<char>();
   GS_HIP(hipMemsetAsync(sm, 0, SM_TIMEOUT, c->stream));
   GS_HIP(hipMemsetAsync(sm + SM_COUNTERS, 0, SM_BASE - SM_COUNTERS, c->stream));
-  hipLaunchKernelGGL(k_keyinfo_buf, dim3(grid_for(n, 512, 2048)), dim3(256), 0, c->stream, keys, n,
+  const int nd = std::min(8, std::max(1, (bits_hint + 7) / 8));
+  hipLaunchKernelGGL(k_keyinfo_buf, dim3(grid_for(n, 512, 2048)), dim3(256), 0, c->stream, keys, n, nd,
                      (unsigned long long*)(sm + SM_MASK), (uint32_t*)(sm + SM_HIST));
   GS_HIP(hipGetLastError());
   GS_HIP(hipMemcpyAsync(sm + SM_K0, keys, 8, hipMemcpyDeviceToDevice, c->stream));
@@ -269,6 +271,7 @@ gs_status sort_buffer(gs_ctx* c, const uint64_t* keys, const uint32_t* vals, uin
   GS_TRY(host_wait(c));
   const uint64_t mask = c->host_small[0], k0 = c->host_small[1];
   const int bits = mask ? 64 - __builtin_clzll(mask) : 0;
+  if (bits > 8 * nd) return set_error(c, GS_EDEVICE, "sort_buffer: keys wider than the %d-bit hint", bits_hint);
   out->bits = bits;
   out->wide = bits > 32;
   out->passes = std::max(1, (bits + RADIX_BITS - 1) / RADIX_BITS);
@@ -282,16 +285,22 @@ gs_status sort_buffer(gs_ctx* c, const uint64_t* keys, const uint32_t* vals, uin
   const uint64_t tiles = (n + SORT_TILE - 1) / SORT_TILE;
   GS_TRY(ensure(c, c->keysA, n * kb));
   GS_TRY(ensure(c, c->keysB, n * kb));
+  if (vals && val_bytes != 4 && val_bytes != 8) return set_error(c, GS_EINVAL, "sort_buffer: %d-byte payload", val_bytes);
   if (vals) {
-    GS_TRY(ensure(c, c->valsA, n * 4));
-    GS_TRY(ensure(c, c->valsB, n * 4));
+    GS_TRY(ensure(c, c->valsA, n * val_bytes));
+    GS_TRY(ensure(c, c->valsB, n * val_bytes));
   }
   GS_TRY(ensure(c, c->sort_status, tiles * RADIX * 8, true));
-  if (out->wide)
-    return vals ? buffer_passes<uint64_t, uint32_t, true>(c, keys, vals, (uint32_t)n, out)
-                : buffer_passes<uint64_t, uint8_t, false>(c, keys, nullptr, (uint32_t)n, out);
-  return vals ? buffer_passes<uint32_t, uint32_t, true>(c, keys, vals, (uint32_t)n, out)
-              : buffer_passes<uint32_t, uint8_t, false>(c, keys, nullptr, (uint32_t)n, out);
+  const auto* v4 = (const uint32_t*)vals;
+  const auto* v8 = (const uint64_t*)vals;
+  if (out->wide) {
+    if (!vals) return buffer_passes<uint64_t, uint8_t, false>(c, keys, nullptr, (uint32_t)n, out);
+    return val_bytes == 8 ? buffer_passes<uint64_t, uint64_t, true>(c, keys, v8, (uint32_t)n, out)
+                          : buffer_passes<uint64_t, uint32_t, true>(c, keys, v4, (uint32_t)n, out);
+  }
+  if (!vals) return buffer_passes<uint32_t, uint8_t, false>(c, keys, nullptr, (uint32_t)n, out);
+  return val_bytes == 8 ? buffer_passes<uint32_t, uint64_t, true>(c, keys, v8, (uint32_t)n, out)
+                        : buffer_passes<uint32_t, uint32_t, true>(c, keys, v4, (uint32_t)n, out);
 }
 
 gs_status sort_window(gs_ctx* c, const int64_t* src, const int64_t* dst, const void* val, int val_bytes,
@@ -389,7 +398,7 @@ void gs_destroy(gs_ctx* c) {
   for (DevBuf* b : {&c->part_k, &c->part_a, &c->comp_k, &c->comp_a,
                     &c->in_src, &c->in_dst, &c->in_val, &c->keysA, &c->keysB, &c->valsA, &c->valsB, &c->sort_status,
                     &c->rbk_word, &c->rbk_agg, &c->rbk_inc, &c->small, &c->out_keys, &c->out_a, &c->out_b, &c->aux,
-                    &c->bk_meta, &c->bk_items, &c->bk_slabs, &c->dp_cnt, &c->dp_csum, &c->dp_off, &c->tri_loops, &c->tri_pairend, &c->tri_tiles, &c->tri_tval, &c->tri_sfx, &c->tri_nbr, &c->tri_heavy, &c->tri_range, &c->tri_queue, &c->tri_hwork,
+                    &c->bk_meta, &c->bk_items, &c->bk_slabs, &c->dp_cnt, &c->dp_csum, &c->dp_off, &c->tri_loops, &c->tri_tiles, &c->tri_sfx, &c->tri_nbr, &c->tri_heavy, &c->tri_range, &c->tri_queue, &c->tri_hwork,
                     &c->pr_a, &c->pr_b, &c->pr_f, &c->pr_key, &c->pr_val, &c->pr_gk, &c->pr_gv, &c->pr_small,
                     &c->tx_text, &c->tx_cnt, &c->tx_starts, &c->zipf_cdf,
                     &c->dist_k, &c->dist_v, &c->dist_v2, &c->dist_k2, &c->dist_v3, &c->dist_v4, &c->dist_cnt})

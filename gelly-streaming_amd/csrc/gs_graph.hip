@@ -205,38 +205,34 @@ __global__ __launch_bounds__(256) void k_tri_okeys(const int64_t* __restrict__ s
 }
 
 // the unique oriented edges (sorted keys u << B | v) -> out-lists: nbr[p] = v, out_range[u] =
-// [first, last + 1) (ranges of absent vertices were zeroed); the transposed sort's input: key v,
-// payload p
+// [first, last + 1) (ranges of absent vertices were zeroed); the transposed sort's keys: v
 __global__ __launch_bounds__(256) void k_tri_out(const uint64_t* __restrict__ keys, uint32_t M, uint32_t B,
                                                  uint32_t* __restrict__ nbr, uint32_t* __restrict__ out_range,
-                                                 uint64_t* __restrict__ tkey, uint32_t* __restrict__ tval) {
+                                                 uint64_t* __restrict__ tkey) {
   const uint64_t mask = (1ull << B) - 1;
   for (uint32_t p = blockIdx.x * 256u + threadIdx.x; p < M; p += gridDim.x * 256u) {
     const uint64_t k = keys[p];
     const uint32_t u = (uint32_t)(k >> B), v = (uint32_t)(k & mask);
     nbr[p] = v;
     tkey[p] = v;
-    tval[p] = p;
     if (p == 0 || (uint32_t)(keys[p - 1] >> B) != u) out_range[2 * u] = p;
     if (p + 1 == M || (uint32_t)(keys[p + 1] >> B) != u) out_range[2 * u + 1] = p + 1;
   }
 }
 
-// end of the out-list holding each adjacency position
-__global__ __launch_bounds__(256) void k_tri_pairend(const uint64_t* __restrict__ keys, uint32_t M, uint32_t B,
-                                                     const uint2* __restrict__ out_range, uint32_t* __restrict__ pend) {
+// the transposed sort's payload: for the edge u -> v at adjacency position p, the part of N+(u)
+// past v, [p + 1, end of N+(u)) -- sorted by v it becomes the in-entries' suffix ranges
+__global__ __launch_bounds__(256) void k_tri_sfx_pay(const uint64_t* __restrict__ keys, uint32_t M, uint32_t B,
+                                                     const uint2* __restrict__ out_range, uint2* __restrict__ pay) {
   for (uint32_t p = blockIdx.x * 256u + threadIdx.x; p < M; p += gridDim.x * 256u)
-    pend[p] = out_range[(uint32_t)(keys[p] >> B)].y;
+    pay[p] = make_uint2(p + 1, out_range[(uint32_t)(keys[p] >> B)].y);
 }
 
-// the edges sorted by target: in_range[v] = [first, last + 1) of v's in-entries; in-entry i
-// (u -> v at adjacency position q) gets the part of N+(u) past v: sfx[i] = [q + 1, end of N+(u))
-__global__ __launch_bounds__(256) void k_tri_in(const uint32_t* __restrict__ skey, const uint32_t* __restrict__ sval,
-                                                uint32_t M, const uint32_t* __restrict__ pend,
-                                                uint32_t* __restrict__ in_range, uint2* __restrict__ sfx) {
+// the edges sorted by target: in_range[v] = [first, last + 1) of v's in-entries
+__global__ __launch_bounds__(256) void k_tri_in(const uint32_t* __restrict__ skey, uint32_t M,
+                                                uint32_t* __restrict__ in_range) {
   for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < M; i += gridDim.x * 256u) {
-    const uint32_t v = skey[i], q = sval[i];
-    sfx[i] = make_uint2(q + 1, pend[q]);
+    const uint32_t v = skey[i];
     if (i == 0 || skey[i - 1] != v) in_range[2 * v] = i;
     if (i + 1 == M || skey[i + 1] != v) in_range[2 * v + 1] = i + 1;
   }
@@ -401,7 +397,7 @@ static gs_status triangles_impl(gs_ctx* c, const gs_edge_batch* b, uint32_t part
   GS_HIP(hipMemcpyAsync(c->host_small + 5, rk_cnt + rk_tiles, 4, hipMemcpyDeviceToHost, c->stream));
   // 2. sort + unique -> the simple oriented graph, sorted by (u, v)
   Sorted s;
-  GS_TRY(sort_buffer(c, c->aux.as<uint64_t>(), nullptr, n, &s));
+  GS_TRY(sort_buffer(c, c->aux.as<uint64_t>(), nullptr, n, &s, 2 * (int)B));
   hipEventRecord(c->ev[1], c->stream);
   const uint64_t loops = c->host_small[4];
   const uint64_t nv = V - (uint32_t)c->host_small[5];
@@ -421,26 +417,24 @@ static gs_status triangles_impl(gs_ctx* c, const gs_edge_batch* b, uint32_t part
   GS_TRY(ensure(c, c->tri_heavy, (V + M / TH_VCH + 64) * 8));   // (v, in-chunk) items
   GS_TRY(ensure(c, c->tri_range, V * 16));
   GS_TRY(ensure(c, c->tri_nbr, M * 4));
-  GS_TRY(ensure(c, c->tri_tval, M * 4));
-  GS_TRY(ensure(c, c->tri_pairend, M * 4));
   GS_TRY(ensure(c, c->tri_sfx, M * 8));
   uint2* out_range = reinterpret_cast<uint2*>(c->tri_range.p);
   uint2* in_range = out_range + V;
   GS_HIP(hipMemsetAsync(c->tri_range.p, 0, V * 16, c->stream));
   const unsigned ge = (unsigned)std::min<uint64_t>((M + 255) / 256, 16384);
   uint32_t* nbr = c->tri_nbr.as<uint32_t>();
-  uint2* sfx = c->tri_sfx.as<uint2>();
   // (the oriented keys in aux are consumed: aux takes the transposed sort's keys)
   hipLaunchKernelGGL(k_tri_out, dim3(ge), dim3(256), 0, c->stream, c->out_keys.as<uint64_t>(), (uint32_t)M, B, nbr,
-                     reinterpret_cast<uint32_t*>(out_range), c->aux.as<uint64_t>(), c->tri_tval.as<uint32_t>());
-  hipLaunchKernelGGL(k_tri_pairend, dim3(ge), dim3(256), 0, c->stream, c->out_keys.as<uint64_t>(), (uint32_t)M, B,
-                     out_range, c->tri_pairend.as<uint32_t>());
+                     reinterpret_cast<uint32_t*>(out_range), c->aux.as<uint64_t>());
+  hipLaunchKernelGGL(k_tri_sfx_pay, dim3(ge), dim3(256), 0, c->stream, c->out_keys.as<uint64_t>(), (uint32_t)M, B,
+                     out_range, c->tri_sfx.as<uint2>());
   GS_HIP(hipGetLastError());
   Sorted t;
-  GS_TRY(sort_buffer(c, c->aux.as<uint64_t>(), c->tri_tval.as<uint32_t>(), M, &t));
+  GS_TRY(sort_buffer(c, c->aux.as<uint64_t>(), c->tri_sfx.p, M, &t, (int)B, 8));
   if (t.wide || t.key_xor) return set_error(c, GS_EDEVICE, "window triangles: transposed keys wider than 32 bits");
-  hipLaunchKernelGGL(k_tri_in, dim3(ge), dim3(256), 0, c->stream, (const uint32_t*)t.keys, (const uint32_t*)t.vals,
-                     (uint32_t)M, c->tri_pairend.as<uint32_t>(), reinterpret_cast<uint32_t*>(in_range), sfx);
+  const uint2* sfx = (const uint2*)t.vals;   // the sort's payload buffer (valsA / valsB): read-only from here
+  hipLaunchKernelGGL(k_tri_in, dim3(ge), dim3(256), 0, c->stream, (const uint32_t*)t.keys, (uint32_t)M,
+                     reinterpret_cast<uint32_t*>(in_range));
   GS_HIP(hipGetLastError());
   hipEventRecord(c->ev[4], c->stream);
   GS_TRY(ensure(c, c->tri_queue, (M / TH_DMAX + 64) * 8));   // further in-list chunks: <= M / TH_DMAX

@@ -61,7 +61,7 @@ struct gs_ctx {
   // fused last pass: partials with gaps, compacted partials
   gs::DevBuf part_k, part_a, comp_k, comp_a;
   // triangles
-  gs::DevBuf tri_loops, tri_pairend, tri_tiles, tri_tval, tri_sfx, tri_nbr, tri_heavy, tri_range, tri_queue, tri_hwork;
+  gs::DevBuf tri_loops, tri_tiles, tri_sfx, tri_nbr, tri_heavy, tri_range, tri_queue, tri_hwork;
   // HashSet-order pipeline (gs_hashset.hip)
   gs::DevBuf hs[20];
   // bucket path (gs_bucket.hip): plan tables, work items, LDS slabs of multi-item buckets
@@ -125,7 +125,10 @@ gs_status sort_window(gs_ctx* c, const int64_t* src, const int64_t* dst, const v
 
 // Sort an unsigned 64-bit key buffer (stable), optional u32 payload; keys of <= 32 varying bits are
 // compacted to u32 (key = key_xor ^ compact).  `keys` must be 16-byte aligned.
-gs_status sort_buffer(gs_ctx* c, const uint64_t* keys, const uint32_t* vals, uint64_t n, Sorted* out);
+// bits_hint: an upper bound on the key width (the histograms cover only those bytes); payload of
+// val_bytes (4 or 8) per key, or none
+gs_status sort_buffer(gs_ctx* c, const uint64_t* keys, const void* vals, uint64_t n, Sorted* out,
+                      int bits_hint = 64, int val_bytes = 4);
 
 // HashSet-ordered distinct neighbour sets of an ALL window (gs_hashset.hip)
 gs_status hashset_order(gs_ctx* c, const int64_t* src, const int64_t* dst, uint64_t n, uint32_t* U_out,

@@ -72,33 +72,52 @@ struct ConvSrc {
 };
 
 // mask + histograms of all 8 bytes of an unsigned 64-bit key buffer (16-byte aligned)
-static __global__ __launch_bounds__(256) void k_keyinfo_buf(const uint64_t* __restrict__ keys, uint64_t n,
+// XOR-mask of a key buffer + the 256-bin histograms of its nd low bytes (the caller's bound on the
+// key width).  One table per wave, and the bin of the wave's first lane is counted once per wave
+// (a popcount): skewed digits -- R-MAT hubs, the top byte of narrow keys -- would otherwise serialize
+// 64 lanes on one LDS counter (triangles s24: 4.0 ms per 2 GB of keys).
+static __global__ __launch_bounds__(256) void k_keyinfo_buf(const uint64_t* __restrict__ keys, uint64_t n, int nd,
                                                      unsigned long long* __restrict__ mask_out,
                                                      uint32_t* __restrict__ hist_out /*[8][256]*/) {
-  __shared__ uint32_t h[8][RADIX];
-  const int tid = threadIdx.x;
-  for (int i = tid; i < 8 * RADIX; i += 256) (&h[0][0])[i] = 0;
+  __shared__ uint32_t h[4][8][RADIX];   // [wave][byte][bin]
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  for (int i = tid; i < 4 * 8 * RADIX; i += 256) (&h[0][0][0])[i] = 0;
   __syncthreads();
   const uint64_t k0 = keys[0];
+  const uint64_t lt = (1ull << lane) - 1;
   uint64_t m = 0;
-  auto add = [&](uint64_t k) {
-    m |= k ^ k0;
-#pragma unroll
-    for (int b = 0; b < 8; ++b) atomicAdd(&h[b][(k >> (8 * b)) & 255u], 1u);
+  auto add = [&](uint64_t k, bool valid) {
+    m |= valid ? k ^ k0 : 0ull;
+    for (int b = 0; b < nd; ++b) {
+      const uint32_t d = (uint32_t)(k >> (8 * b)) & 255u;
+      const uint32_t L = __builtin_amdgcn_readfirstlane(d);
+      const uint64_t same = __ballot(valid && d == L);
+      if (valid && d == L) {
+        if ((same & lt) == 0) atomicAdd(&h[w][b][L], (uint32_t)__popcll(same));
+      } else if (valid) {
+        atomicAdd(&h[w][b][d], 1u);
+      }
+    }
   };
   const ulonglong2* k2 = reinterpret_cast<const ulonglong2*>(keys);
   const uint64_t npair = n >> 1;
-  for (uint64_t q = (uint64_t)blockIdx.x * 256u + tid; q < npair; q += (uint64_t)gridDim.x * 256u) {
-    const ulonglong2 x = k2[q];
-    add(x.x);
-    add(x.y);
+  const uint64_t stride = (uint64_t)gridDim.x * 256u;
+  // every lane runs the same trip count (the ballots need the whole wave)
+  for (uint64_t q0 = (uint64_t)blockIdx.x * 256u; q0 < npair; q0 += stride) {
+    const uint64_t q = q0 + tid;
+    const bool ok = q < npair;
+    const ulonglong2 x = ok ? k2[q] : make_ulonglong2(0, 0);
+    add(x.x, ok);
+    add(x.y, ok);
   }
-  if ((n & 1) && blockIdx.x == 0 && tid == 0) add(keys[n - 1]);
+  if (n & 1) {
+    if (blockIdx.x == 0 && w == 0) add(keys[n - 1], lane == 0);
+  }
   m = wave_or(m);
-  if ((tid & 63) == 0 && m) atomicOr(mask_out, (unsigned long long)m);
+  if (lane == 0 && m) atomicOr(mask_out, (unsigned long long)m);
   __syncthreads();
-  for (int i = tid; i < 8 * RADIX; i += 256) {
-    const uint32_t c = (&h[0][0])[i];
+  for (int i = tid; i < nd * RADIX; i += 256) {
+    const uint32_t c = h[0][0][i] + h[1][0][i] + h[2][0][i] + h[3][0][i];
     if (c) atomicAdd(&hist_out[i], c);
   }
 }
