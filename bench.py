@@ -551,8 +551,9 @@ def main():
         src, dst, val = wins[i % len(wins)]
         local_times.clear()
         if a.workload == "triangles":
-            if dist:
-                tot, _ = D.triangles_window(part_count, src, dst)
+            if dist:   # the split window: degrees, routed oriented edges, all-gathered out-lists, share of the count
+                tot = D.triangles_window(eng, src, dst)[0]
+                local_times.append(eng.stage_times())
             else:
                 tot = part_count(src, dst, 0, 1)
             z = torch.zeros(1, dtype=torch.int64, device=src.device)

@@ -207,7 +207,7 @@ static gs_status nccl_check(gs_ctx* c, int r, const char* what) {
 }
 
 // exchange owner-grouped rows: send[p] rows of `row` bytes to peer p, receive recv[p] from each
-static gs_status exchange_rows(gs_ctx* c, const char* sendbuf, const uint64_t* send, char* recvbuf, const uint64_t* recv,
+gs_status exchange_rows(gs_ctx* c, const char* sendbuf, const uint64_t* send, char* recvbuf, const uint64_t* recv,
                                size_t row) {
   NcclApi& A = nccl();
   const int P = c->comm_size;
@@ -218,6 +218,48 @@ static gs_status exchange_rows(gs_ctx* c, const char* sendbuf, const uint64_t* s
     if (recv[p]) GS_TRY(nccl_check(c, A.Recv(recvbuf + ro * row, recv[p] * row, NCCL_UINT8, p, c->comm, c->stream), "ncclRecv"));
     so += send[p];
     ro += recv[p];
+  }
+  return nccl_check(c, A.GroupEnd(), "ncclGroupEnd");
+}
+
+gs_status comm_allreduce(gs_ctx* c, void* buf, size_t count, int nccl_dtype, int nccl_op) {
+  if (!c->comm) return set_error(c, GS_EINVAL, "no communicator (gs_comm_init)");
+  return nccl_check(c, nccl().AllReduce(buf, buf, count, nccl_dtype, nccl_op, c->comm, c->stream), "ncclAllReduce");
+}
+
+// every rank's u64 -> all[0 .. comm_size) on the host (a sum of one-hot rows)
+gs_status comm_allgather_u64(gs_ctx* c, uint64_t mine, uint64_t* all) {
+  if (!c->comm) return set_error(c, GS_EINVAL, "no communicator (gs_comm_init)");
+  const int P = c->comm_size;
+  GS_TRY(ensure(c, c->dist_cnt, 1024 + (size_t)P * 8));
+  uint64_t* d = (uint64_t*)(c->dist_cnt.as<char>() + 512);
+  GS_HIP(hipMemsetAsync(d, 0, P * 8, c->stream));
+  c->host_small[100] = mine;   // pinned source (HOST_SMALL_WORDS = 128; results land in [8, 8 + P))
+  GS_HIP(hipMemcpyAsync(d + c->comm_rank, c->host_small + 100, 8, hipMemcpyHostToDevice, c->stream));
+  GS_TRY(nccl_check(c, nccl().AllReduce(d, d, P, NCCL_UINT64, NCCL_SUM, c->comm, c->stream), "ncclAllReduce"));
+  GS_HIP(hipMemcpyAsync(c->host_small + 8, d, P * 8, hipMemcpyDeviceToHost, c->stream));
+  GS_TRY(host_wait(c));
+  memcpy(all, c->host_small + 8, P * 8);
+  return GS_OK;
+}
+
+// every rank's `mine` rows (row bytes each) concatenated in rank order into recvbuf; counts[p] = rows of
+// rank p (comm_allgather_u64)
+gs_status comm_allgatherv(gs_ctx* c, const void* sendbuf, char* recvbuf, const uint64_t* counts, size_t row) {
+  NcclApi& A = nccl();
+  const int P = c->comm_size, me = c->comm_rank;
+  uint64_t off = 0;
+  std::vector<uint64_t> at(P);
+  for (int p = 0; p < P; ++p) {
+    at[p] = off;
+    off += counts[p];
+  }
+  if (counts[me]) GS_HIP(hipMemcpyAsync(recvbuf + at[me] * row, sendbuf, counts[me] * row, hipMemcpyDeviceToDevice, c->stream));
+  GS_TRY(nccl_check(c, A.GroupStart(), "ncclGroupStart"));
+  for (int p = 0; p < P; ++p) {
+    if (p == me) continue;
+    if (counts[me]) GS_TRY(nccl_check(c, A.Send(sendbuf, counts[me] * row, NCCL_UINT8, p, c->comm, c->stream), "ncclSend"));
+    if (counts[p]) GS_TRY(nccl_check(c, A.Recv(recvbuf + at[p] * row, counts[p] * row, NCCL_UINT8, p, c->comm, c->stream), "ncclRecv"));
   }
   return nccl_check(c, A.GroupEnd(), "ncclGroupEnd");
 }

@@ -115,10 +115,10 @@ static inline unsigned grid_for(uint64_t n, unsigned per_block, unsigned cap) {
 }
 
 template <int DIR>
-static gs_status launch_keyinfo(gs_ctx* c, const int64_t* src, const int64_t* dst, uint64_t n) {
+static gs_status launch_keyinfo(gs_ctx* c, const int64_t* src, const int64_t* dst, uint64_t n, bool mask_only = false) {
   char* sm = c->small.as<char>();
   const bool vec = ((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst)) & 15) == 0;
-  const int nd = std::min(4, std::max(1, c->hist_digits));
+  const int nd = mask_only ? 0 : std::min(4, std::max(1, c->hist_digits));
   if (vec)
     hipLaunchKernelGGL((k_keyinfo<DIR, true>), dim3(grid_for(n, 2048, 2048)), dim3(256), 0, c->stream, src, dst, n,
                        nd, (unsigned long long*)(sm + SM_MASK), (uint32_t*)(sm + SM_HIST));
@@ -127,8 +127,8 @@ static gs_status launch_keyinfo(gs_ctx* c, const int64_t* src, const int64_t* ds
                        nd, (unsigned long long*)(sm + SM_MASK), (uint32_t*)(sm + SM_HIST));
   return hip_check(c, hipGetLastError(), "k_keyinfo");
 }
-gs_status launch_keyinfo_all(gs_ctx* c, const int64_t* src, const int64_t* dst, uint64_t n) {
-  return launch_keyinfo<DIR_ALL>(c, src, dst, n);
+gs_status launch_keyinfo_all(gs_ctx* c, const int64_t* src, const int64_t* dst, uint64_t n, bool mask_only) {
+  return launch_keyinfo<DIR_ALL>(c, src, dst, n, mask_only);
 }
 
 template <int DIR>
@@ -258,26 +258,32 @@ static gs_status buffer_passes(gs_ctx* c, const uint64_t* keys, const V* vals, u
 }
 
 gs_status sort_buffer(gs_ctx* c, const uint64_t* keys, const void* vals, uint64_t n, Sorted* out, int bits_hint,
-                      int val_bytes) {
+                      int val_bytes, bool hist_ready) {
   char* sm = c->small.as<char>();
-  GS_HIP(hipMemsetAsync(sm, 0, SM_TIMEOUT, c->stream));
-  GS_HIP(hipMemsetAsync(sm + SM_COUNTERS, 0, SM_BASE - SM_COUNTERS, c->stream));
   const int nd = std::min(8, std::max(1, (bits_hint + 7) / 8));
-  hipLaunchKernelGGL(k_keyinfo_buf, dim3(grid_for(n, 512, 2048)), dim3(256), 0, c->stream, keys, n, nd,
-                     (unsigned long long*)(sm + SM_MASK), (uint32_t*)(sm + SM_HIST));
-  GS_HIP(hipGetLastError());
-  GS_HIP(hipMemcpyAsync(sm + SM_K0, keys, 8, hipMemcpyDeviceToDevice, c->stream));
-  GS_HIP(hipMemcpyAsync(c->host_small, sm, 16, hipMemcpyDeviceToHost, c->stream));
-  GS_TRY(host_wait(c));
-  const uint64_t mask = c->host_small[0], k0 = c->host_small[1];
-  const int bits = mask ? 64 - __builtin_clzll(mask) : 0;
-  if (bits > 8 * nd) return set_error(c, GS_EDEVICE, "sort_buffer: keys wider than the %d-bit hint", bits_hint);
+  int bits = bits_hint;
+  uint64_t k0 = 0;
+  GS_HIP(hipMemsetAsync(sm, 0, SM_TIMEOUT, c->stream));   // mask, k0, unique count (reduce-by-key after us)
+  if (!hist_ready) {   // mask + histograms of the hinted bytes, then the measured width
+    GS_HIP(hipMemsetAsync(sm + SM_COUNTERS, 0, SM_BASE - SM_COUNTERS, c->stream));
+    hipLaunchKernelGGL(k_keyinfo_buf, dim3(grid_for(n, 512, 2048)), dim3(256), 0, c->stream, keys, n, nd,
+                       (unsigned long long*)(sm + SM_MASK), (uint32_t*)(sm + SM_HIST));
+    GS_HIP(hipGetLastError());
+    GS_HIP(hipMemcpyAsync(sm + SM_K0, keys, 8, hipMemcpyDeviceToDevice, c->stream));
+    GS_HIP(hipMemcpyAsync(c->host_small, sm, 16, hipMemcpyDeviceToHost, c->stream));
+    GS_TRY(host_wait(c));
+    const uint64_t mask = c->host_small[0];
+    k0 = c->host_small[1];
+    bits = mask ? 64 - __builtin_clzll(mask) : 0;
+    if (bits > 8 * nd) return set_error(c, GS_EDEVICE, "sort_buffer: keys wider than the %d-bit hint", bits_hint);
+  }
+  // (hist_ready: the producer of the keys filled SM_HIST for bits_hint-bit keys; no host round trip)
   out->bits = bits;
   out->wide = bits > 32;
   out->passes = std::max(1, (bits + RADIX_BITS - 1) / RADIX_BITS);
   out->done_passes = out->passes;
   out->records = n;
-  out->key_xor = out->wide ? 0 : (k0 & 0xFFFFFFFF00000000ull);
+  out->key_xor = (out->wide || hist_ready) ? 0 : (k0 & 0xFFFFFFFF00000000ull);
   hipLaunchKernelGGL(k_digit_base, dim3(1), dim3(256), 0, c->stream, (const uint32_t*)(sm + SM_HIST),
                      (uint32_t*)(sm + SM_BASE), out->passes);
   GS_HIP(hipGetLastError());
@@ -398,7 +404,7 @@ void gs_destroy(gs_ctx* c) {
   for (DevBuf* b : {&c->part_k, &c->part_a, &c->comp_k, &c->comp_a,
                     &c->in_src, &c->in_dst, &c->in_val, &c->keysA, &c->keysB, &c->valsA, &c->valsB, &c->sort_status,
                     &c->rbk_word, &c->rbk_agg, &c->rbk_inc, &c->small, &c->out_keys, &c->out_a, &c->out_b, &c->aux,
-                    &c->bk_meta, &c->bk_items, &c->bk_slabs, &c->dp_cnt, &c->dp_csum, &c->dp_off, &c->tri_loops, &c->tri_tiles, &c->tri_sfx, &c->tri_nbr, &c->tri_heavy, &c->tri_range, &c->tri_queue, &c->tri_hwork,
+                    &c->bk_meta, &c->bk_items, &c->bk_slabs, &c->dp_cnt, &c->dp_csum, &c->dp_off, &c->tri_loops, &c->tri_tiles, &c->tri_sfx, &c->tri_nbr, &c->tri_heavy, &c->tri_range, &c->tri_queue, &c->tri_hwork, &c->tri_d[0], &c->tri_d[1], &c->tri_d[2], &c->tri_d[3], &c->tri_d[4], &c->tri_d[5],
                     &c->pr_a, &c->pr_b, &c->pr_f, &c->pr_key, &c->pr_val, &c->pr_gk, &c->pr_gv, &c->pr_small,
                     &c->tx_text, &c->tx_cnt, &c->tx_starts, &c->zipf_cdf,
                     &c->dist_k, &c->dist_v, &c->dist_v2, &c->dist_k2, &c->dist_v3, &c->dist_v4, &c->dist_cnt})

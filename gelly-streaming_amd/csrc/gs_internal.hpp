@@ -62,6 +62,9 @@ struct gs_ctx {
   gs::DevBuf part_k, part_a, comp_k, comp_a;
   // triangles
   gs::DevBuf tri_loops, tri_tiles, tri_sfx, tri_nbr, tri_heavy, tri_range, tri_queue, tri_hwork;
+  gs::DevBuf tri_d[6];           // split-window triangles (gs_window_triangles_dist)
+  uint32_t tri_B = 0;            // split-window triangles: id geometry of the current window
+  uint64_t tri_key_xor = 0;
   // HashSet-order pipeline (gs_hashset.hip)
   gs::DevBuf hs[20];
   // bucket path (gs_bucket.hip): plan tables, work items, LDS slabs of multi-item buckets
@@ -126,9 +129,10 @@ gs_status sort_window(gs_ctx* c, const int64_t* src, const int64_t* dst, const v
 // Sort an unsigned 64-bit key buffer (stable), optional u32 payload; keys of <= 32 varying bits are
 // compacted to u32 (key = key_xor ^ compact).  `keys` must be 16-byte aligned.
 // bits_hint: an upper bound on the key width (the histograms cover only those bytes); payload of
-// val_bytes (4 or 8) per key, or none
+// val_bytes (4 or 8) per key, or none.  hist_ready: the kernel that wrote the keys (all < 2^bits_hint)
+// already filled the digit histograms (SM_HIST, wave_hist_add): no scan, no host round trip
 gs_status sort_buffer(gs_ctx* c, const uint64_t* keys, const void* vals, uint64_t n, Sorted* out,
-                      int bits_hint = 64, int val_bytes = 4);
+                      int bits_hint = 64, int val_bytes = 4, bool hist_ready = false);
 
 // HashSet-ordered distinct neighbour sets of an ALL window (gs_hashset.hip)
 gs_status hashset_order(gs_ctx* c, const int64_t* src, const int64_t* dst, uint64_t n, uint32_t* U_out,
@@ -138,6 +142,15 @@ gs_status hashset_order(gs_ctx* c, const int64_t* src, const int64_t* dst, uint6
 gs_status triangle_selfpair_term(gs_ctx* c, const int64_t* src, const int64_t* dst, uint64_t n,
                                  const uint32_t* loops, uint64_t loops_xor, const int64_t* relabel, uint64_t nrel,
                                  uint64_t* S);
+// ctx communicator helpers (gs_dist.hip; RCCL enums: ncclInt64 4, ncclUint32 3, ncclUint64 5; ncclSum 0,
+// ncclMax 2, ncclMin 3): in-place all-reduce of a device buffer; every rank's u64 to the host;
+// grouped send / recv of owner-grouped rows
+constexpr int NCCL_T_U32 = 3, NCCL_T_I64 = 4, NCCL_T_U64 = 5, NCCL_OP_SUM = 0, NCCL_OP_MAX = 2, NCCL_OP_MIN = 3;
+gs_status comm_allreduce(gs_ctx* c, void* buf, size_t count, int nccl_dtype, int nccl_op);
+gs_status comm_allgather_u64(gs_ctx* c, uint64_t mine, uint64_t* all);
+gs_status exchange_rows(gs_ctx* c, const char* sendbuf, const uint64_t* send, char* recvbuf, const uint64_t* recv,
+                        size_t row);
+gs_status comm_allgatherv(gs_ctx* c, const void* sendbuf, char* recvbuf, const uint64_t* counts, size_t row);
 // exclusive scan of n u64 (gs_hashset.hip)
 gs_status xscan(gs_ctx* c, const uint64_t* in, uint64_t n, uint64_t* out);
 // order-preserving compaction of the IDs of two columns (gs_relabel.hip): *ca / *cb = ranks among the
@@ -158,7 +171,7 @@ gs_status host_wait(gs_ctx* c);
 gs_status begin_call(gs_ctx* c);
 
 // k_keyinfo over both columns (ALL): mask at SM_MASK, byte histograms at SM_HIST
-gs_status launch_keyinfo_all(gs_ctx* c, const int64_t* src, const int64_t* dst, uint64_t n);
+gs_status launch_keyinfo_all(gs_ctx* c, const int64_t* src, const int64_t* dst, uint64_t n, bool mask_only = false);
 
 // Stage a batch on the device (copies host columns into ctx buffers); returns device pointers.
 gs_status stage_batch(gs_ctx* c, const gs_edge_batch* b, const int64_t** src, const int64_t** dst,

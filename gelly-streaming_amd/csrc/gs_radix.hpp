@@ -71,11 +71,36 @@ struct ConvSrc {
   }
 };
 
-// mask + histograms of all 8 bytes of an unsigned 64-bit key buffer (16-byte aligned)
+// One key into this wave's 256-bin histograms of its nd low bytes (hw = [nd][RADIX] in LDS).  The
+// bin of the wave's first lane is counted once per wave (a popcount): skewed digits -- R-MAT hubs,
+// the top byte of narrow keys -- would otherwise serialize 64 lanes on one LDS counter (triangles
+// s24: 4.0 ms per 2 GB of keys).  Every lane of the wave must call it (ballots).
+__device__ __forceinline__ void wave_hist_add(uint32_t (*hw)[RADIX], uint64_t k, bool valid, int nd) {
+  const uint64_t lt = (1ull << (threadIdx.x & 63)) - 1;
+  for (int b = 0; b < nd; ++b) {
+    const uint32_t d = (uint32_t)(k >> (8 * b)) & 255u;
+    const uint32_t L = __builtin_amdgcn_readfirstlane(d);
+    const uint64_t same = __ballot(valid && d == L);
+    if (valid && d == L) {
+      if ((same & lt) == 0) atomicAdd(&hw[b][L], (uint32_t)__popcll(same));
+    } else if (valid) {
+      atomicAdd(&hw[b][d], 1u);
+    }
+  }
+}
+// a block's per-wave tables h[NW][8][RADIX] (nd bytes used) into the global histograms
+template <int NW>
+__device__ __forceinline__ void flush_hist(uint32_t (*h)[8][RADIX], int nd, uint32_t* __restrict__ hist_out) {
+  for (int i = threadIdx.x; i < nd * RADIX; i += blockDim.x) {
+    uint32_t c = 0;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) c += h[w][0][i];
+    if (c) atomicAdd(&hist_out[i], c);
+  }
+}
+
 // XOR-mask of a key buffer + the 256-bin histograms of its nd low bytes (the caller's bound on the
-// key width).  One table per wave, and the bin of the wave's first lane is counted once per wave
-// (a popcount): skewed digits -- R-MAT hubs, the top byte of narrow keys -- would otherwise serialize
-// 64 lanes on one LDS counter (triangles s24: 4.0 ms per 2 GB of keys).
+// key width), one table per wave (wave_hist_add)
 static __global__ __launch_bounds__(256) void k_keyinfo_buf(const uint64_t* __restrict__ keys, uint64_t n, int nd,
                                                      unsigned long long* __restrict__ mask_out,
                                                      uint32_t* __restrict__ hist_out /*[8][256]*/) {
@@ -84,20 +109,10 @@ static __global__ __launch_bounds__(256) void k_keyinfo_buf(const uint64_t* __re
   for (int i = tid; i < 4 * 8 * RADIX; i += 256) (&h[0][0][0])[i] = 0;
   __syncthreads();
   const uint64_t k0 = keys[0];
-  const uint64_t lt = (1ull << lane) - 1;
   uint64_t m = 0;
   auto add = [&](uint64_t k, bool valid) {
     m |= valid ? k ^ k0 : 0ull;
-    for (int b = 0; b < nd; ++b) {
-      const uint32_t d = (uint32_t)(k >> (8 * b)) & 255u;
-      const uint32_t L = __builtin_amdgcn_readfirstlane(d);
-      const uint64_t same = __ballot(valid && d == L);
-      if (valid && d == L) {
-        if ((same & lt) == 0) atomicAdd(&h[w][b][L], (uint32_t)__popcll(same));
-      } else if (valid) {
-        atomicAdd(&h[w][b][d], 1u);
-      }
-    }
+    wave_hist_add(h[w], k, valid, nd);
   };
   const ulonglong2* k2 = reinterpret_cast<const ulonglong2*>(keys);
   const uint64_t npair = n >> 1;
@@ -116,10 +131,7 @@ static __global__ __launch_bounds__(256) void k_keyinfo_buf(const uint64_t* __re
   m = wave_or(m);
   if (lane == 0 && m) atomicOr(mask_out, (unsigned long long)m);
   __syncthreads();
-  for (int i = tid; i < nd * RADIX; i += 256) {
-    const uint32_t c = h[0][0][i] + h[1][0][i] + h[2][0][i] + h[3][0][i];
-    if (c) atomicAdd(&hist_out[i], c);
-  }
+  flush_hist<4>(h, nd, hist_out);
 }
 
 // ---- k_keyinfo ------------------------------------------------------------------------------
@@ -137,7 +149,7 @@ __global__ __launch_bounds__(256) void k_keyinfo(const int64_t* __restrict__ src
   uint64_t m = 0;
   auto add = [&](uint64_t k) {
     m |= k ^ k0;
-    atomicAdd(&h[w][0][k & 255u], 1u);
+    if (nd > 0) atomicAdd(&h[w][0][k & 255u], 1u);   // nd = 0: the mask alone
     if (nd > 1) atomicAdd(&h[w][1][(k >> 8) & 255u], 1u);
     if (nd > 2) atomicAdd(&h[w][2][(k >> 16) & 255u], 1u);
     if (nd > 3) atomicAdd(&h[w][3][(k >> 24) & 255u], 1u);

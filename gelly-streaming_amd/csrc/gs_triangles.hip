@@ -1,0 +1,1035 @@
+// gs_triangles.hip — WindowTriangles on one GPU and split over several.
+//
+//   gs_window_triangles       <- slice(ALL) -> GenerateCandidateEdges -> CountTriangles -> sum(0)
+//                                (WindowTriangles.java:61-66, :83-140)
+//   gs_window_triangles_part  one part of the count (balanced share of the work), for callers that
+//                                hold the whole window on every rank
+//   gs_tri_dist_*             the window split over ranks: local degrees (all-reduce), oriented edges
+//                                routed to owner(u) (all-to-all), local out-lists (all-gather), each
+//                                rank's balanced share of the count (all-reduce)
+#include <climits>
+#include <string.h>
+
+#include <vector>
+
+#include "gs_ops.hpp"
+#include "gs_tricount.hpp"
+
+namespace gs {
+
+// ---------------------------------------------------------------------------------------------
+// WindowTriangles: exact count of the reference's matched candidates without emitting them.
+//   T = triangles of the window's simple undirected graph (GenerateCandidateEdges emits each
+//       {b, c} pair of neighbours > v once per v; CountTriangles matches it iff b ~ c, and ALL
+//       makes both (b,c) and (c,b) edge records) -> counted once each by the forward algorithm
+//       on a (degree, id)-oriented CSR with sorted adjacency (merge intersection).
+//   S = self-pair quirk (j = i emits (x, x); matched only if x has a self-loop) — needs
+//       java.util.HashSet iteration order; only windows with self-loops have S != 0.
+// ---------------------------------------------------------------------------------------------
+constexpr uint64_t TRI_MAX_BITS = 28;
+
+// Vertices are renumbered by degree before the adjacency is built: rank(x) orders (degree class, id),
+// so in the renumbered graph "u -> v iff u < v" is the degree orientation.  Only the oriented keys
+// (min rank << B | max rank) are sorted (n keys, not the 2n of a symmetric adjacency): unique -> the
+// out-lists, sorted in orientation order; a second, narrow sort of the unique edges by target
+// (B-bit keys, adjacency position as payload) groups them into in-lists.  Sorted out-lists are what
+// halve the probes: for u -> v only the part of N+(u) above v can hold a w with v -> w, so each
+// in-neighbour u of v contributes the suffix of N+(u) after v, and the in-list entry carries that
+// suffix's range (R-MAT scale 20: sum of d+(u)^2 = 2.47 G probes -> sum of d+(d+-1)/2 = 1.23 G).
+// Any total order gives the exact count; the degree classes only keep out-lists short.
+
+// raw degree per (compact) vertex over the window's records: the bucket path's COUNT over both
+// endpoints (bucket_reduce), scattered into a dense array.  Windows the bucket path does not take (id
+// range too wide for its buckets) count with global atomics instead -- one request per endpoint, and
+// an R-MAT hub's atomics serialize on its address, so each block first counts into an LDS table that
+// keeps the first ids to claim a slot (the frequent ones, almost surely) and flushes it at the end.
+__global__ __launch_bounds__(256) void k_tri_deg_scatter(const int64_t* __restrict__ keys, const int64_t* __restrict__ cnt,
+                                                         uint64_t U, uint64_t key_xor, uint32_t* __restrict__ deg) {
+  for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < U; i += (uint64_t)gridDim.x * 256)
+    deg[(uint64_t)keys[i] ^ key_xor] = (uint32_t)cnt[i];
+}
+
+constexpr int DG_BLOCK = 512, DG_SLOTS = 4096;
+__global__ __launch_bounds__(DG_BLOCK) void k_tri_deg(const int64_t* __restrict__ src, const int64_t* __restrict__ dst,
+                                                      uint64_t n, uint64_t key_xor, uint32_t* __restrict__ deg) {
+  __shared__ uint32_t s_key[DG_SLOTS], s_cnt[DG_SLOTS];
+  for (int i = threadIdx.x; i < DG_SLOTS; i += DG_BLOCK) {
+    s_key[i] = 0xFFFFFFFFu;
+    s_cnt[i] = 0;
+  }
+  __syncthreads();
+  auto add = [&](uint32_t x) {
+    const uint32_t h = (x * 0x9E3779B1u) >> (32 - 12);
+    uint32_t k = s_key[h];
+    if (k == 0xFFFFFFFFu) {
+      k = atomicCAS(&s_key[h], 0xFFFFFFFFu, x);
+      if (k == 0xFFFFFFFFu) k = x;
+    }
+    if (k == x) atomicAdd(&s_cnt[h], 1u);
+    else atomicAdd(&deg[x], 1u);
+  };
+  static_assert(DG_SLOTS == 1 << 12, "hash shift");
+  for (uint64_t i = (uint64_t)blockIdx.x * DG_BLOCK + threadIdx.x; i < n; i += (uint64_t)gridDim.x * DG_BLOCK) {
+    add((uint32_t)((uint64_t)src[i] ^ key_xor));
+    add((uint32_t)((uint64_t)dst[i] ^ key_xor));
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < DG_SLOTS; i += DG_BLOCK)
+    if (s_cnt[i]) atomicAdd(&deg[s_key[i]], s_cnt[i]);
+}
+
+// degree class: 0 for isolated ids, then two classes per octave
+constexpr int RK_BLOCK = 256, RK_STEPS = 32, RK_WAVES = RK_BLOCK / WAVE, RK_TILE = RK_BLOCK * RK_STEPS, RK_NC = 64;
+__device__ __forceinline__ uint32_t deg_class(uint32_t d) {
+  if (!d) return 0;
+  const uint32_t lz = 31u - (uint32_t)__clz(d);
+  const uint32_t half = lz ? (d >> (lz - 1)) & 1u : 0u;
+  return min((uint32_t)RK_NC - 1, 1u + 2u * lz + half);
+}
+
+// per tile of RK_TILE ids: ids per class -> cnt[class * tiles + tile]
+__global__ __launch_bounds__(RK_BLOCK) void k_rank_count(const uint32_t* __restrict__ deg, uint32_t V, uint32_t tiles,
+                                                         uint32_t* __restrict__ cnt) {
+  __shared__ uint32_t s_c[RK_NC];
+  const int tid = threadIdx.x;
+  if (tid < RK_NC) s_c[tid] = 0;
+  __syncthreads();
+  const uint32_t base = blockIdx.x * RK_TILE;
+  for (int j = 0; j < RK_STEPS; ++j) {
+    const uint32_t x = base + j * RK_BLOCK + tid;
+    if (x < V) atomicAdd(&s_c[deg_class(deg[x])], 1u);
+  }
+  __syncthreads();
+  if (tid < RK_NC) cnt[tid * tiles + blockIdx.x] = s_c[tid];
+}
+
+// one block: exclusive scan of cnt[0 .. n) (class-major) in place
+__global__ __launch_bounds__(1024) void k_rank_scan(uint32_t* __restrict__ cnt, uint32_t n) {
+  __shared__ uint32_t s_w[16];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const uint32_t per = (n + 1023) / 1024, a = min(n, tid * per), b = min(n, a + per);
+  uint32_t sum = 0;
+  for (uint32_t i = a; i < b; ++i) sum += cnt[i];
+  const uint32_t inc = wave_inclusive_sum(sum);
+  if (lane == 63) s_w[w] = inc;
+  __syncthreads();
+  uint32_t run = inc - sum;
+  for (int i = 0; i < w; ++i) run += s_w[i];
+  for (uint32_t i = a; i < b; ++i) {
+    const uint32_t x = cnt[i];
+    cnt[i] = run;
+    run += x;
+  }
+}
+
+// rank[x] = ids of lower classes + ids of x's class below x (a stable partition: deterministic, so
+// every rank of a multi-GPU job renumbers identically).  Wave w of a tile takes RK_STEPS groups of 64
+// consecutive ids; a lane's place among equal classes comes from a 7-ballot match mask.
+__global__ __launch_bounds__(RK_BLOCK) void k_rank_scatter(const uint32_t* __restrict__ deg, uint32_t V, uint32_t tiles,
+                                                           const uint32_t* __restrict__ off, uint32_t* __restrict__ rank) {
+  __shared__ uint32_t s_cnt[RK_WAVES][RK_NC];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  for (int i = tid; i < RK_WAVES * RK_NC; i += RK_BLOCK) (&s_cnt[0][0])[i] = 0;
+  __syncthreads();
+  const uint32_t base = blockIdx.x * RK_TILE + (uint32_t)w * (RK_STEPS * WAVE);
+  const uint64_t lt = (1ull << lane) - 1;
+  uint32_t cls[RK_STEPS], loc[RK_STEPS];
+#pragma unroll
+  for (int j = 0; j < RK_STEPS; ++j) {
+    const uint32_t x = base + j * WAVE + lane;
+    const uint32_t c = x < V ? deg_class(deg[x]) : 127u;
+    uint64_t m = ~0ull;
+#pragma unroll
+    for (int bit = 0; bit < 7; ++bit) {
+      const uint64_t bal = __ballot((c >> bit) & 1u);
+      m &= ((c >> bit) & 1u) ? bal : ~bal;
+    }
+    cls[j] = c;
+    uint32_t b0 = 0;
+    if (c < RK_NC) b0 = s_cnt[w][c];
+    loc[j] = b0 + (uint32_t)__popcll(m & lt);
+    if (c < RK_NC && (m & lt) == 0) s_cnt[w][c] = b0 + (uint32_t)__popcll(m);   // the class's lowest lane
+    wave_lds_sync();
+  }
+  __syncthreads();
+  if (tid < RK_NC) {   // exclusive prefix over the waves, per class
+    uint32_t run = 0;
+    for (int k = 0; k < RK_WAVES; ++k) {
+      const uint32_t t = s_cnt[k][tid];
+      s_cnt[k][tid] = run;
+      run += t;
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < RK_STEPS; ++j) {
+    const uint32_t x = base + j * WAVE + lane;
+    if (x < V) rank[x] = off[cls[j] * tiles + blockIdx.x] + s_cnt[w][cls[j]] + loc[j];
+  }
+}
+
+// oriented composite keys (min rank << B | max rank); self-loops -> sentinel (sorts last) + bitmap
+// and count; the sort's digit histograms of the 2B-bit keys on the way (sort_buffer hist_ready)
+__global__ __launch_bounds__(256) void k_tri_okeys(const int64_t* __restrict__ src, const int64_t* __restrict__ dst,
+                                                   uint64_t n, uint64_t key_xor, uint32_t B,
+                                                   const uint32_t* __restrict__ rank, uint64_t* __restrict__ out,
+                                                   uint32_t* __restrict__ loop_bits, unsigned long long* __restrict__ loops,
+                                                   uint32_t* __restrict__ hist) {
+  __shared__ uint32_t h[4][8][RADIX];
+  const int tid = threadIdx.x, w = tid >> 6;
+  for (int i = tid; i < 4 * 8 * RADIX; i += 256) (&h[0][0][0])[i] = 0;
+  __syncthreads();
+  const int nd = (int)(2 * B + 7) / 8;
+  const uint64_t sent = (B * 2 >= 64) ? ~0ull : ((1ull << (2 * B)) - 1);
+  const uint64_t stride = (uint64_t)gridDim.x * 256;
+  for (uint64_t i0 = (uint64_t)blockIdx.x * 256; i0 < n; i0 += stride) {   // wave-uniform trip count
+    const uint64_t i = i0 + tid;
+    const bool ok = i < n;
+    uint64_t k = sent;
+    if (ok) {
+      const uint64_t a = (uint64_t)src[i] ^ key_xor, b = (uint64_t)dst[i] ^ key_xor;
+      if (a != b) {
+        const uint64_t ra = rank[a], rb = rank[b];
+        k = ra < rb ? (ra << B) | rb : (rb << B) | ra;
+      } else {
+        atomicOr(&loop_bits[a >> 5], 1u << (a & 31));
+        atomicAdd(loops, 1ull);
+      }
+      out[i] = k;
+    }
+    wave_hist_add(h[w], k, ok, nd);
+  }
+  __syncthreads();
+  flush_hist<4>(h, nd, hist);
+}
+
+// the unique oriented edges (sorted keys u << B | v) -> out-lists: nbr[p] = v, out_range[u] =
+// [first, last + 1) (ranges of absent vertices were zeroed)
+__global__ __launch_bounds__(256) void k_tri_out(const uint64_t* __restrict__ keys, uint32_t M, uint32_t B,
+                                                 uint32_t* __restrict__ nbr, uint32_t* __restrict__ out_range) {
+  const uint64_t mask = (1ull << B) - 1;
+  for (uint32_t p = blockIdx.x * 256u + threadIdx.x; p < M; p += gridDim.x * 256u) {
+    const uint64_t k = keys[p];
+    const uint32_t u = (uint32_t)(k >> B);
+    nbr[p] = (uint32_t)(k & mask);
+    if (p == 0 || (uint32_t)(keys[p - 1] >> B) != u) out_range[2 * u] = p;
+    if (p + 1 == M || (uint32_t)(keys[p + 1] >> B) != u) out_range[2 * u + 1] = p + 1;
+  }
+}
+
+// row (u) of each adjacency position of a slice, from the out-lists (one thread per u; d+(u) is
+// small under the degree orientation)
+__global__ __launch_bounds__(256) void k_tri_rowid(const uint2* __restrict__ out_range, uint32_t u0, uint32_t u1,
+                                                   uint32_t p0, uint32_t* __restrict__ rowid) {
+  for (uint32_t u = u0 + blockIdx.x * 256u + threadIdx.x; u < u1; u += gridDim.x * 256u) {
+    const uint2 r = out_range[u];
+    for (uint32_t p = r.x; p < r.y; ++p) rowid[p - p0] = u;
+  }
+}
+
+// the transposed sort's input over the slice [p0, p1) of the adjacency: key v, payload the part of
+// N+(u) past v, [p + 1, end of N+(u)) -- sorted by v it becomes the in-entries' suffix ranges; the
+// digit histograms of the B-bit keys on the way.  Row of p: the sorted keys (whole window) or rowid.
+template <bool ROWID>
+__global__ __launch_bounds__(256) void k_tri_tpay(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ rowid,
+                                                  const uint32_t* __restrict__ nbr, uint32_t p0, uint32_t p1,
+                                                  uint32_t B, const uint2* __restrict__ out_range,
+                                                  uint64_t* __restrict__ tkey, uint2* __restrict__ pay,
+                                                  uint32_t* __restrict__ hist) {
+  __shared__ uint32_t h[4][8][RADIX];
+  const int tid = threadIdx.x, w = tid >> 6;
+  for (int i = tid; i < 4 * 8 * RADIX; i += 256) (&h[0][0][0])[i] = 0;
+  __syncthreads();
+  const int nd = (int)(B + 7) / 8;
+  for (uint32_t q0 = p0 + blockIdx.x * 256u; q0 < p1; q0 += gridDim.x * 256u) {   // wave-uniform trip count
+    const uint32_t p = q0 + tid;
+    const bool ok = p < p1;
+    uint32_t v = 0;
+    if (ok) {
+      uint32_t u;
+      if constexpr (ROWID) u = rowid[p - p0];
+      else u = (uint32_t)(keys[p] >> B);
+      v = nbr[p];
+      tkey[p - p0] = v;
+      pay[p - p0] = make_uint2(p + 1, out_range[u].y);
+    }
+    wave_hist_add(h[w], v, ok, nd);
+  }
+  __syncthreads();
+  flush_hist<4>(h, nd, hist);
+}
+
+// the edges sorted by target: in_range[v] = [first, last + 1) of v's in-entries
+__global__ __launch_bounds__(256) void k_tri_in(const uint32_t* __restrict__ skey, uint32_t M,
+                                                uint32_t* __restrict__ in_range) {
+  for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < M; i += gridDim.x * 256u) {
+    const uint32_t v = skey[i];
+    if (i == 0 || skey[i - 1] != v) in_range[2 * v] = i;
+    if (i + 1 == M || skey[i + 1] != v) in_range[2 * v + 1] = i + 1;
+  }
+}
+
+// ---- the split over parts --------------------------------------------------------------------------
+// counting work of u: the suffixes of N+(u) it hands out, d(d-1)/2, plus one unit per in-entry
+__global__ __launch_bounds__(256) void k_tri_work(const uint2* __restrict__ out_range, uint32_t V,
+                                                  unsigned long long* __restrict__ work) {
+  for (uint32_t u = blockIdx.x * 256u + threadIdx.x; u < V; u += gridDim.x * 256u) {
+    const uint64_t d = out_range[u].y - out_range[u].x;
+    work[u] = d * (d + 1) / 2;
+  }
+}
+
+// part `part` of nparts: the u-range [u0, u1) holding its equal share of the work (pre = exclusive
+// prefix of k_tri_work, pre[V] = total), and that range's adjacency slice [p0, p1) -> out[0..3].
+// Slice ends: a search in the sorted keys (okeys), else the prefix-built out_range of u0 / u1.
+__global__ void k_tri_bounds(const unsigned long long* __restrict__ pre, uint32_t V, const uint2* __restrict__ out_range,
+                             const uint64_t* __restrict__ okeys, uint32_t B, uint32_t M, uint32_t part, uint32_t nparts,
+                             uint32_t* __restrict__ out) {
+  if (threadIdx.x != 0) return;
+  const unsigned long long W = pre[V];
+  auto lower = [&](unsigned long long t) {   // first u with pre[u] >= t
+    uint32_t a = 0, b = V;
+    while (a < b) {
+      const uint32_t m = (a + b) >> 1;
+      if (pre[m] < t) a = m + 1;
+      else b = m;
+    }
+    return a;
+  };
+  auto pos = [&](uint32_t u) -> uint32_t {   // first adjacency position of a row >= u
+    if (u >= V) return M;
+    if (!okeys) return out_range[u].x;
+    const uint64_t key = (uint64_t)u << B;
+    uint32_t a = 0, b = M;
+    while (a < b) {
+      const uint32_t m = (a + b) >> 1;
+      if (okeys[m] < key) a = m + 1;
+      else b = m;
+    }
+    return a;
+  };
+  const uint32_t u0 = part == 0 ? 0u : lower(W * part / nparts);
+  const uint32_t u1 = part + 1 == nparts ? V : lower(W * (part + 1) / nparts);
+  out[0] = u0;
+  out[1] = u1;
+  out[2] = pos(u0);
+  out[3] = max(pos(u0), pos(u1));
+}
+
+// out-lists from the (all-reduced) out-degrees: out_range[u] = [pre[u], pre[u] + d+(u))
+__global__ __launch_bounds__(256) void k_tri_ranges(const uint32_t* __restrict__ dplus, const unsigned long long* __restrict__ pre,
+                                                    uint32_t V, uint2* __restrict__ out_range) {
+  for (uint32_t u = blockIdx.x * 256u + threadIdx.x; u < V; u += gridDim.x * 256u) {
+    const uint32_t a = (uint32_t)pre[u];
+    out_range[u] = make_uint2(a, a + dplus[u]);
+  }
+}
+
+__global__ __launch_bounds__(256) void k_u32_to_u64(const uint32_t* __restrict__ in, uint32_t n,
+                                                    unsigned long long* __restrict__ out) {
+  for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < n; i += gridDim.x * 256u) out[i] = in[i];
+}
+
+// d+(u) of the local out-lists (the build step of the split window)
+__global__ __launch_bounds__(256) void k_tri_dplus(const uint2* __restrict__ out_range, uint32_t V, uint32_t* __restrict__ dplus) {
+  for (uint32_t u = blockIdx.x * 256u + threadIdx.x; u < V; u += gridDim.x * 256u)
+    dplus[u] = out_range[u].y - out_range[u].x;
+}
+
+// ---- routing oriented keys to owner(u) = u * nparts >> B (contiguous u ranges) ----------------------
+constexpr int RT_BLOCK = 256, RT_ITEMS = 16, RT_TILE = RT_BLOCK * RT_ITEMS, RT_MAXP = 64;
+__device__ __forceinline__ uint32_t tri_owner(uint64_t key, uint32_t B, uint32_t nparts) {
+  return (uint32_t)(((key >> B) * nparts) >> B);
+}
+__global__ __launch_bounds__(RT_BLOCK) void k_route_count(const uint64_t* __restrict__ keys, uint64_t n, uint32_t B,
+                                                          uint32_t nparts, uint32_t tiles, uint32_t* __restrict__ cnt) {
+  __shared__ uint32_t s_c[RT_MAXP];
+  const int tid = threadIdx.x;
+  if (tid < RT_MAXP) s_c[tid] = 0;
+  __syncthreads();
+  const uint64_t base = (uint64_t)blockIdx.x * RT_TILE;
+  const uint64_t sent = (B * 2 >= 64) ? ~0ull : ((1ull << (2 * B)) - 1);
+  for (int j = 0; j < RT_ITEMS; ++j) {
+    const uint64_t i = base + (uint64_t)j * RT_BLOCK + tid;
+    if (i < n && keys[i] != sent) atomicAdd(&s_c[tri_owner(keys[i], B, nparts)], 1u);
+  }
+  __syncthreads();
+  if (tid < (int)nparts) cnt[(uint64_t)tid * tiles + blockIdx.x] = s_c[tid];
+}
+// (k_rank_scan: the exclusive scan, owner-major) then the scatter; order inside an owner is free
+// (the owner sorts what it receives)
+__global__ __launch_bounds__(RT_BLOCK) void k_route_scatter(const uint64_t* __restrict__ keys, uint64_t n, uint32_t B,
+                                                            uint32_t nparts, uint32_t tiles,
+                                                            const uint32_t* __restrict__ off, uint64_t* __restrict__ out) {
+  __shared__ uint32_t s_c[RT_MAXP];
+  const int tid = threadIdx.x;
+  if (tid < (int)nparts) s_c[tid] = off[(uint64_t)tid * tiles + blockIdx.x];
+  __syncthreads();
+  const uint64_t base = (uint64_t)blockIdx.x * RT_TILE;
+  const uint64_t sent = (B * 2 >= 64) ? ~0ull : ((1ull << (2 * B)) - 1);
+  for (int j = 0; j < RT_ITEMS; ++j) {
+    const uint64_t i = base + (uint64_t)j * RT_BLOCK + tid;
+    if (i < n) {
+      const uint64_t k = keys[i];
+      if (k != sent) out[atomicAdd(&s_c[tri_owner(k, B, nparts)], 1u)] = k;
+    }
+  }
+}
+
+// signed min / max of every endpoint id -> mm[0] (min), mm[1] (max)
+__global__ __launch_bounds__(256) void k_tri_minmax(const int64_t* __restrict__ src, const int64_t* __restrict__ dst,
+                                                    uint64_t n, long long* __restrict__ mm) {
+  long long lo = LLONG_MAX, hi = LLONG_MIN;
+  for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) {
+    const long long a = src[i], b = dst[i];
+    lo = min(lo, min(a, b));
+    hi = max(hi, max(a, b));
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    lo = min(lo, (long long)__shfl_xor(lo, o, WAVE));
+    hi = max(hi, (long long)__shfl_xor(hi, o, WAVE));
+  }
+  if ((threadIdx.x & 63) == 0) {
+    atomicMin(&mm[0], lo);
+    atomicMax(&mm[1], hi);
+  }
+}
+
+// self-loop bitmap + count of a window (the self-pair term of a gathered window)
+__global__ __launch_bounds__(256) void k_tri_loops(const int64_t* __restrict__ src, const int64_t* __restrict__ dst,
+                                                   uint64_t n, uint64_t key_xor, uint32_t* __restrict__ loop_bits,
+                                                   unsigned long long* __restrict__ loops) {
+  for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) {
+    const uint64_t a = (uint64_t)src[i] ^ key_xor;
+    if (a == ((uint64_t)dst[i] ^ key_xor)) {
+      atomicOr(&loop_bits[a >> 5], 1u << (a & 31));
+      atomicAdd(loops, 1ull);
+    }
+  }
+}
+
+}  // namespace gs
+
+using namespace gs;
+
+// ---- host side ---------------------------------------------------------------------------------------
+namespace {
+
+struct TriGeom {
+  const int64_t *src = nullptr, *dst = nullptr;    // ids as counted (relabeled when wider than the budget)
+  const int64_t *osrc = nullptr, *odst = nullptr;  // the window's own ids (the self-pair term)
+  const int64_t* uniq = nullptr;                   // relabel table (sorted originals), or null
+  uint64_t nuniq = 0, n = 0;
+  uint32_t B = 1;
+  uint64_t key_xor = 0;
+  size_t V = 2;
+};
+
+void set_bits(TriGeom* g, uint32_t B) {
+  g->B = B;
+  g->V = 1ull << B;
+}
+
+// the window's id range -> B and key_xor; ids spanning more than TRI_MAX_BITS are relabeled
+// (order-preserving compact IDs; the originals stay for the self-pair term's HashSet order)
+gs_status tri_geometry(gs_ctx* c, const int64_t* src, const int64_t* dst, uint64_t n, TriGeom* g) {
+  char* sm = c->small.as<char>();
+  GS_HIP(hipMemsetAsync(sm, 0, SM_TIMEOUT, c->stream));
+  GS_HIP(hipMemsetAsync(sm + SM_COUNTERS, 0, SM_BASE - SM_COUNTERS, c->stream));
+  GS_TRY(launch_keyinfo_all(c, src, dst, n, true));   // the id range (no histograms)
+  GS_HIP(hipMemcpyAsync(sm + SM_K0, src, 8, hipMemcpyDeviceToDevice, c->stream));
+  GS_HIP(hipMemcpyAsync(c->host_small, sm, 16, hipMemcpyDeviceToHost, c->stream));
+  GS_TRY(host_wait(c));
+  const uint64_t mask = c->host_small[0], k0 = c->host_small[1];
+  g->src = g->osrc = src;
+  g->dst = g->odst = dst;
+  g->n = n;
+  set_bits(g, mask ? 64 - __builtin_clzll(mask) : 1);
+  g->key_xor = k0 & ~((1ull << g->B) - 1);
+  if (g->B > TRI_MAX_BITS) {
+    GS_TRY(relabel_endpoints(c, src, dst, n, &g->src, &g->dst, &g->uniq, &g->nuniq));
+    set_bits(g, g->nuniq > 1 ? 64 - __builtin_clzll(g->nuniq - 1) : 1);
+    g->key_xor = 0;
+    if (g->B > TRI_MAX_BITS)
+      return set_error(c, GS_EUNSUPPORTED, "window triangles: %llu distinct vertices (> 2^%llu)",
+                       (unsigned long long)g->nuniq, (unsigned long long)TRI_MAX_BITS);
+  }
+  return GS_OK;
+}
+
+// raw degree of every id over this window's (or this rank's) records: the bucket path's COUNT,
+// else global atomics
+gs_status tri_degrees(gs_ctx* c, const TriGeom& g, uint32_t* deg) {
+  GS_HIP(hipMemsetAsync(deg, 0, g.V * 4, c->stream));
+  if (g.n == 0) return GS_OK;
+  GS_TRY(ensure(c, c->out_keys, std::min<uint64_t>(2 * g.n, g.V) * 8));
+  GS_TRY(ensure(c, c->tri_sfx, std::min<uint64_t>(2 * g.n, g.V) * 8));
+  uint64_t U = 0;
+  const gs_status bs = bucket_reduce(c, g.src, g.dst, nullptr, g.n, DIR_ALL, OP_COUNT, GS_NONE, false, nullptr,
+                                     c->out_keys.as<int64_t>(), c->tri_sfx.p, &U);
+  if (bs == GS_OK) {
+    if (U)
+      hipLaunchKernelGGL(k_tri_deg_scatter, dim3((unsigned)std::min<uint64_t>((U + 255) / 256, 8192)), dim3(256), 0,
+                         c->stream, c->out_keys.as<int64_t>(), c->tri_sfx.as<int64_t>(), U, g.key_xor, deg);
+  } else if (bs == GS_EUNSUPPORTED) {
+    hipLaunchKernelGGL(k_tri_deg, dim3((unsigned)std::min<uint64_t>((g.n + DG_BLOCK - 1) / DG_BLOCK, 1024)),
+                       dim3(DG_BLOCK), 0, c->stream, g.src, g.dst, g.n, g.key_xor, deg);
+  } else {
+    return bs;
+  }
+  return hip_check(c, hipGetLastError(), "degrees");
+}
+
+// degree-class ranks; the ids without an edge (class 0) -> host_small[5] after the next wait
+gs_status tri_ranks(gs_ctx* c, const TriGeom& g, const uint32_t* deg, uint32_t* rank) {
+  const uint32_t rk_tiles = (uint32_t)((g.V + RK_TILE - 1) / RK_TILE);
+  GS_TRY(ensure(c, c->tri_tiles, (size_t)rk_tiles * RK_NC * 4 + 8));
+  uint32_t* rk_cnt = c->tri_tiles.as<uint32_t>();
+  hipLaunchKernelGGL(k_rank_count, dim3(rk_tiles), dim3(RK_BLOCK), 0, c->stream, deg, (uint32_t)g.V, rk_tiles, rk_cnt);
+  hipLaunchKernelGGL(k_rank_scan, dim3(1), dim3(1024), 0, c->stream, rk_cnt, rk_tiles * RK_NC);
+  hipLaunchKernelGGL(k_rank_scatter, dim3(rk_tiles), dim3(RK_BLOCK), 0, c->stream, deg, (uint32_t)g.V, rk_tiles, rk_cnt,
+                     rank);
+  GS_HIP(hipGetLastError());
+  c->host_small[5] = 0;   // (the copy fills the low 4 bytes)
+  GS_HIP(hipMemcpyAsync(c->host_small + 5, rk_cnt + rk_tiles, 4, hipMemcpyDeviceToHost, c->stream));
+  return GS_OK;
+}
+
+// oriented keys of the ranks into keys[0 .. n) (+ self-loop bitmap; loop count -> host_small[4] after
+// the next wait; the digit histograms into SM_HIST)
+gs_status tri_okeys(gs_ctx* c, const TriGeom& g, const uint32_t* rank, uint64_t* keys) {
+  char* sm = c->small.as<char>();
+  const size_t words = (g.V + 31) / 32;
+  GS_TRY(ensure(c, c->tri_loops, words * 4));
+  GS_HIP(hipMemsetAsync(c->tri_loops.p, 0, words * 4, c->stream));
+  unsigned long long* d_loops = (unsigned long long*)(sm + SM_NUNIQUE);
+  GS_HIP(hipMemsetAsync(d_loops, 0, 8, c->stream));
+  GS_HIP(hipMemsetAsync(sm + SM_HIST, 0, 8 * 256 * 4, c->stream));
+  if (g.n) {
+    const unsigned grid = (unsigned)std::min<uint64_t>((g.n + 255) / 256, 8192);
+    hipLaunchKernelGGL(k_tri_okeys, dim3(grid), dim3(256), 0, c->stream, g.src, g.dst, g.n, g.key_xor, g.B, rank, keys,
+                       c->tri_loops.as<uint32_t>(), d_loops, (uint32_t*)(sm + SM_HIST));
+    GS_HIP(hipGetLastError());
+  }
+  GS_HIP(hipMemcpyAsync(c->host_small + 4, d_loops, 8, hipMemcpyDeviceToHost, c->stream));
+  return GS_OK;
+}
+
+// sort + unique of n oriented keys -> c->out_keys[0 .. M); `sentinel`: the keys may end in self-loop
+// sentinels (dropped)
+gs_status tri_unique(gs_ctx* c, const uint64_t* keys, uint64_t n, uint32_t B, bool hist_ready, bool sentinel,
+                     uint64_t* M, Sorted* s) {
+  *M = 0;
+  if (n == 0) return GS_OK;
+  GS_TRY(sort_buffer(c, keys, nullptr, n, s, 2 * (int)B, 4, hist_ready));
+  hipEventRecord(c->ev[1], c->stream);
+  GS_TRY(ensure(c, c->out_keys, n * 8));
+  UniqueOut uo{c->out_keys.as<uint64_t>(), nullptr};
+  GS_TRY((s->wide ? launch_rbk<uint64_t, CountOp>(c, *s, uo, M) : launch_rbk<uint32_t, CountOp>(c, *s, uo, M)));
+  if (sentinel && *M) {   // the self-loop sentinel sorts last
+    uint64_t last = 0;
+    GS_HIP(hipMemcpy(&last, c->out_keys.as<uint64_t>() + *M - 1, 8, hipMemcpyDeviceToHost));
+    const uint64_t sent = (B * 2 >= 64) ? ~0ull : ((1ull << (2 * B)) - 1);
+    if (last == sent) *M -= 1;
+  }
+  return GS_OK;
+}
+
+// The counting step over the out-lists (nbr, out_range; M edges) for part `part` of nparts: its
+// balanced u-range's edges sorted by target (in-lists with suffix ranges), then the LDS hash-set
+// kernels.  okeys: the sorted unique keys (row of every position), else rows come from out_range.
+gs_status tri_count(gs_ctx* c, uint32_t B, size_t V, uint64_t M, const uint32_t* nbr, const uint2* out_range,
+                    const uint64_t* okeys, uint32_t part, uint32_t nparts, uint64_t* T, uint64_t* probes) {
+  char* sm = c->small.as<char>();
+  *T = 0;
+  *probes = 0;
+  uint32_t u0 = 0, u1 = (uint32_t)V, p0 = 0, p1 = (uint32_t)M;
+  if (nparts > 1) {
+    GS_TRY(ensure(c, c->tri_hwork, (V * 2 + 2) * 8));
+    unsigned long long* work = c->tri_hwork.as<unsigned long long>();
+    const unsigned gv = (unsigned)std::min<uint64_t>((V + 255) / 256, 16384);
+    hipLaunchKernelGGL(k_tri_work, dim3(gv), dim3(256), 0, c->stream, out_range, (uint32_t)V, work);
+    GS_TRY(xscan(c, (const uint64_t*)work, V, (uint64_t*)work + V + 1));
+    uint32_t* bnd = (uint32_t*)(sm + SM_TABLE);
+    hipLaunchKernelGGL(k_tri_bounds, dim3(1), dim3(64), 0, c->stream, (const unsigned long long*)work + V + 1,
+                       (uint32_t)V, out_range, okeys, B, (uint32_t)M, part, nparts, bnd);
+    GS_HIP(hipGetLastError());
+    GS_HIP(hipMemcpyAsync(c->host_small + 12, bnd, 16, hipMemcpyDeviceToHost, c->stream));
+    GS_TRY(host_wait(c));
+    const uint32_t* hb = reinterpret_cast<const uint32_t*>(c->host_small + 12);
+    u0 = hb[0];
+    u1 = hb[1];
+    p0 = hb[2];
+    p1 = hb[3];
+  }
+  const uint64_t Ms = p1 - p0;   // this part's edges
+  if (Ms == 0) {
+    hipEventRecord(c->ev[4], c->stream);
+    hipEventRecord(c->ev[5], c->stream);
+    hipEventRecord(c->ev[3], c->stream);
+    return GS_OK;
+  }
+  // 1. this part's edges by target: keys v, payload the suffix of N+(u) past v
+  GS_TRY(ensure(c, c->aux, Ms * 8));
+  GS_TRY(ensure(c, c->tri_sfx, Ms * 8));
+  GS_HIP(hipMemsetAsync(sm + SM_HIST, 0, 8 * 256 * 4, c->stream));
+  const unsigned ge = (unsigned)std::min<uint64_t>((Ms + 255) / 256, 16384);
+  if (okeys) {
+    hipLaunchKernelGGL(k_tri_tpay<false>, dim3(ge), dim3(256), 0, c->stream, okeys, nullptr, nbr, p0, p1, B, out_range,
+                       c->aux.as<uint64_t>(), c->tri_sfx.as<uint2>(), (uint32_t*)(sm + SM_HIST));
+  } else {
+    GS_TRY(ensure(c, c->tri_queue, Ms * 4));
+    hipLaunchKernelGGL(k_tri_rowid, dim3((unsigned)std::min<uint64_t>((u1 - u0 + 255) / 256, 16384)), dim3(256), 0,
+                       c->stream, out_range, u0, u1, p0, c->tri_queue.as<uint32_t>());
+    hipLaunchKernelGGL(k_tri_tpay<true>, dim3(ge), dim3(256), 0, c->stream, nullptr, c->tri_queue.as<uint32_t>(), nbr,
+                       p0, p1, B, out_range, c->aux.as<uint64_t>(), c->tri_sfx.as<uint2>(), (uint32_t*)(sm + SM_HIST));
+  }
+  GS_HIP(hipGetLastError());
+  Sorted t;
+  GS_TRY(sort_buffer(c, c->aux.as<uint64_t>(), c->tri_sfx.p, Ms, &t, (int)B, 8, true));
+  if (t.wide || t.key_xor) return set_error(c, GS_EDEVICE, "window triangles: transposed keys wider than 32 bits");
+  const uint2* sfx = (const uint2*)t.vals;   // the sort's payload buffer (valsA / valsB): read-only from here
+  uint2* in_range = const_cast<uint2*>(out_range) + V;
+  GS_HIP(hipMemsetAsync(in_range, 0, V * 8, c->stream));
+  hipLaunchKernelGGL(k_tri_in, dim3(ge), dim3(256), 0, c->stream, (const uint32_t*)t.keys, (uint32_t)Ms,
+                     reinterpret_cast<uint32_t*>(in_range));
+  GS_HIP(hipGetLastError());
+  hipEventRecord(c->ev[4], c->stream);
+  // 2. intersections: vertex-centric LDS hash sets (k_tri_light), long out-lists in k_tri_heavy
+  GS_TRY(ensure(c, c->tri_heavy, (V + Ms / TH_VCH + 64) * 8));   // (v, in-chunk) items
+  GS_TRY(ensure(c, c->tri_queue, (Ms / TH_DMAX + 64) * 8));      // further in-list chunks: <= Ms / TH_DMAX
+  unsigned long long* d_total = (unsigned long long*)(sm + SM_NUNIQUE);
+  uint32_t* d_nheavy = (uint32_t*)(sm + SM_COUNTERS) + 62;
+  unsigned long long* d_probes = (unsigned long long*)(sm + SM_TRI_PROBES);
+  GS_HIP(hipMemsetAsync(d_total, 0, 8, c->stream));
+  GS_HIP(hipMemsetAsync(d_probes, 0, 8, c->stream));
+  GS_HIP(hipMemsetAsync(d_nheavy, 0, 8, c->stream));   // heavy items, queued chunks
+  uint32_t* d_err = (uint32_t*)(sm + SM_DEV_ERR);
+  GS_HIP(hipMemsetAsync(d_err, 0, 4, c->stream));
+  // LDS hash-set bucket cap: unlimited, or one bucket under GS_FLAG_TEST_TINY_TABLES (tests only)
+  const uint32_t nb_cap = (c->flags & GS_FLAG_TEST_TINY_TABLES) ? 1u : 0xFFFFFFFFu;
+  uint32_t* d_nqueue = d_nheavy + 1;
+  const unsigned nvb = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((V + TH_WPB - 1) / TH_WPB, 8192));
+  uint2* queue = c->tri_queue.as<uint2>();
+  for (int pass = 0; pass < 2; ++pass) {
+    hipLaunchKernelGGL(k_tri_light, dim3(pass == 0 ? nvb : 4096u), dim3(TH_BLOCK), 0, c->stream, nbr, sfx, out_range,
+                       in_range, (uint32_t)V, 0u, 0xFFFFFFFFu, pass, queue, d_nqueue, c->tri_heavy.as<uint2>(), d_nheavy,
+                       d_total, d_probes, nb_cap, d_err);
+    GS_HIP(hipGetLastError());
+  }
+  hipEventRecord(c->ev[5], c->stream);
+  // heavy items: work per item, exclusive scan, then equal-work runs per block
+  c->host_small[6] = 0;
+  GS_HIP(hipMemcpyAsync(c->host_small + 6, d_nheavy, 4, hipMemcpyDeviceToHost, c->stream));
+  GS_TRY(host_wait(c));
+  const uint32_t nh = (uint32_t)c->host_small[6];
+  if (nh) {
+    GS_TRY(ensure(c, c->tri_hwork, (size_t)nh * 16 + 8));
+    unsigned long long* hw = c->tri_hwork.as<unsigned long long>();
+    hipLaunchKernelGGL(k_tri_hwork, dim3((unsigned)std::min<uint64_t>((nh + 3) / 4, 16384)), dim3(256), 0, c->stream,
+                       sfx, in_range, c->tri_heavy.as<uint2>(), nh, hw);
+    GS_HIP(hipGetLastError());
+    GS_TRY(xscan(c, (const uint64_t*)hw, nh, (uint64_t*)hw + nh));
+    hipLaunchKernelGGL(k_tri_heavy, dim3(GS_TH_HGRID), dim3(TH_HBLOCK), 0, c->stream, nbr, sfx, out_range, in_range,
+                       c->tri_heavy.as<uint2>(), d_nheavy, (const unsigned long long*)hw + nh, d_total, d_probes,
+                       nb_cap, d_err);
+    GS_HIP(hipGetLastError());
+  }
+  hipEventRecord(c->ev[3], c->stream);
+  GS_HIP(hipMemcpyAsync(c->host_small, sm, 32, hipMemcpyDeviceToHost, c->stream));
+  GS_HIP(hipMemcpyAsync(c->host_small + 6, d_probes, 8, hipMemcpyDeviceToHost, c->stream));
+  c->host_small[7] = 0;   // (the copy below fills the low 4 bytes)
+  GS_HIP(hipMemcpyAsync(c->host_small + 7, d_err, 4, hipMemcpyDeviceToHost, c->stream));
+  GS_TRY(host_wait(c));
+  if ((uint32_t)c->host_small[3] != 0) return set_error(c, GS_EDEVICE, "look-back spin timed out");
+  if ((uint32_t)c->host_small[7] & GS_DERR_TABLE_FULL)
+    return set_error(c, GS_EDEVICE, "window triangles: an LDS hash set filled up (counting aborted)");
+  *T = c->host_small[2];
+  *probes = c->host_small[6];
+  return GS_OK;
+}
+
+void tri_times(gs_ctx* c, const TriGeom& g, uint64_t M, uint64_t nv, uint64_t probes, int passes) {
+  // stage times (path 3): ranks + keys + sort, unique, out-lists + transposed sort, light, heavy
+  gs_stage_times& t = c->times;
+  t = gs_stage_times{};
+  const int order[6] = {0, 1, 2, 4, 5, 3};
+  for (int i = 0; i < 5; ++i) hipEventElapsedTime(&t.pass_ms[i], c->ev[order[i]], c->ev[order[i + 1]]);
+  hipEventElapsedTime(&t.total_ms, c->ev[0], c->ev[3]);
+  t.sort_passes = (uint32_t)passes;
+  t.key_bits = g.B;
+  t.records = M;     // unique undirected edges
+  t.vertices = nv;   // vertices with edges
+  t.partials = probes;
+  t.path = 3;
+}
+
+// the whole window on this GPU; part / nparts: count only that share of the work
+gs_status triangles_impl(gs_ctx* c, const gs_edge_batch* b, uint32_t part, uint32_t nparts, uint64_t* count) {
+  GS_TRY(check_batch(c, b, GS_DIR_ALL));
+  if (!count) return set_error(c, GS_EINVAL, "null output pointer");
+  if (nparts == 0 || part >= nparts) return set_error(c, GS_EINVAL, "bad part %u of %u", part, nparts);
+  GS_TRY(begin_call(c));
+  *count = 0;
+  if (b->n == 0) return GS_OK;
+  hipEventRecord(c->ev[0], c->stream);
+  const int64_t *src, *dst;
+  const void* val;
+  GS_TRY(stage_batch(c, b, &src, &dst, &val, false));
+  TriGeom g;
+  GS_TRY(tri_geometry(c, src, dst, b->n, &g));
+  // 1. raw degrees -> degree-class ranks -> oriented composite keys of the ranks
+  GS_TRY(ensure(c, c->out_a, g.V * 4));
+  GS_TRY(ensure(c, c->out_b, g.V * 4));
+  uint32_t* deg = c->out_a.as<uint32_t>();
+  uint32_t* rank = c->out_b.as<uint32_t>();
+  GS_TRY(tri_degrees(c, g, deg));
+  GS_TRY(tri_ranks(c, g, deg, rank));
+  GS_TRY(ensure(c, c->aux, g.n * 8));
+  GS_TRY(tri_okeys(c, g, rank, c->aux.as<uint64_t>()));
+  // 2. sort + unique -> the simple oriented graph, sorted by (u, v)
+  Sorted s;
+  uint64_t M = 0;
+  GS_TRY(tri_unique(c, c->aux.as<uint64_t>(), g.n, g.B, true, false, &M, &s));
+  const uint64_t loops = c->host_small[4];
+  const uint64_t nv = g.V - (uint32_t)c->host_small[5];
+  hipEventRecord(c->ev[2], c->stream);
+  if (loops) M -= 1;   // the self-loop sentinel sorts last
+  uint64_t T = 0, probes = 0;
+  if (M) {
+    // 3. out-lists; 4. the count
+    GS_TRY(ensure(c, c->tri_range, g.V * 16));
+    GS_TRY(ensure(c, c->tri_nbr, M * 4));
+    uint2* out_range = reinterpret_cast<uint2*>(c->tri_range.p);
+    GS_HIP(hipMemsetAsync(out_range, 0, g.V * 8, c->stream));
+    hipLaunchKernelGGL(k_tri_out, dim3((unsigned)std::min<uint64_t>((M + 255) / 256, 16384)), dim3(256), 0, c->stream,
+                       c->out_keys.as<uint64_t>(), (uint32_t)M, g.B, c->tri_nbr.as<uint32_t>(),
+                       reinterpret_cast<uint32_t*>(out_range));
+    GS_HIP(hipGetLastError());
+    GS_TRY(tri_count(c, g.B, g.V, M, c->tri_nbr.as<uint32_t>(), out_range, c->out_keys.as<uint64_t>(), part, nparts,
+                     &T, &probes));
+    tri_times(c, g, M, nv, probes, s.passes);
+  }
+  if (loops && part == 0) {   // self-pair candidates (x, x, true) matched by a self-loop on x (:105)
+    uint64_t S = 0;
+    GS_TRY(triangle_selfpair_term(c, g.osrc, g.odst, g.n, c->tri_loops.as<uint32_t>(), g.key_xor, g.uniq, g.nuniq, &S));
+    T += S;
+  }
+  *count = T;
+  return GS_OK;
+}
+
+// ---- the split window (gs_tri_dist_*) -------------------------------------------------------------
+// geometry from the ranks' common id range (no relabel: a split window must span <= 2^28 ids)
+gs_status tri_geometry_range(gs_ctx* c, int64_t gmin, int64_t gmax, TriGeom* g) {
+  if (gmin > gmax) {   // no record anywhere
+    set_bits(g, 1);
+    g->key_xor = 0;
+    return GS_OK;
+  }
+  const uint64_t d = (uint64_t)gmin ^ (uint64_t)gmax;
+  set_bits(g, d ? 64 - __builtin_clzll(d) : 1);
+  if (g->B > TRI_MAX_BITS)
+    return set_error(c, GS_EUNSUPPORTED, "split window triangles: ids span more than 2^%llu values",
+                     (unsigned long long)TRI_MAX_BITS);
+  g->key_xor = (uint64_t)gmin & ~((1ull << g->B) - 1);
+  return GS_OK;
+}
+
+gs_status dist_stage(gs_ctx* c, const gs_edge_batch* b, TriGeom* g) {
+  // (the stage timings of the bucket / sort passes inside start at ev[0])
+  hipEventRecord(c->ev[0], c->stream);
+  const int64_t *src = nullptr, *dst = nullptr;
+  const void* val;
+  if (b->n) GS_TRY(stage_batch(c, b, &src, &dst, &val, false));
+  g->src = g->osrc = src;
+  g->dst = g->odst = dst;
+  g->n = b->n;
+  set_bits(g, c->tri_B ? c->tri_B : 1);
+  g->key_xor = c->tri_key_xor;
+  return GS_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+gs_status gs_tri_dist_range(gs_ctx* c, const gs_edge_batch* b, int64_t* minmax) {
+  if (!c) return GS_EINVAL;
+  GS_TRY(check_batch(c, b, GS_DIR_ALL));
+  if (!minmax) return set_error(c, GS_EINVAL, "null output pointer");
+  GS_TRY(begin_call(c));
+  minmax[0] = INT64_MAX;
+  minmax[1] = INT64_MIN;
+  if (b->n == 0) return GS_OK;
+  const int64_t *src, *dst;
+  const void* val;
+  GS_TRY(stage_batch(c, b, &src, &dst, &val, false));
+  long long* mm = (long long*)(c->small.as<char>() + SM_TABLE);
+  c->host_small[12] = (uint64_t)INT64_MAX;
+  c->host_small[13] = (uint64_t)INT64_MIN;
+  GS_HIP(hipMemcpyAsync(mm, c->host_small + 12, 16, hipMemcpyHostToDevice, c->stream));
+  hipLaunchKernelGGL(k_tri_minmax, dim3((unsigned)std::min<uint64_t>((b->n + 255) / 256, 4096)), dim3(256), 0, c->stream,
+                     src, dst, b->n, mm);
+  GS_HIP(hipGetLastError());
+  GS_HIP(hipMemcpyAsync(c->host_small + 12, mm, 16, hipMemcpyDeviceToHost, c->stream));
+  GS_TRY(host_wait(c));
+  minmax[0] = (int64_t)c->host_small[12];
+  minmax[1] = (int64_t)c->host_small[13];
+  return GS_OK;
+}
+
+gs_status gs_tri_dist_degrees(gs_ctx* c, const gs_edge_batch* b, int64_t gmin, int64_t gmax, uint32_t* deg, uint64_t* V) {
+  if (!c) return GS_EINVAL;
+  GS_TRY(check_batch(c, b, GS_DIR_ALL));
+  if (!V) return set_error(c, GS_EINVAL, "null output pointer");
+  TriGeom g;
+  GS_TRY(tri_geometry_range(c, gmin, gmax, &g));
+  *V = g.V;
+  c->tri_B = g.B;
+  c->tri_key_xor = g.key_xor;
+  if (!deg) return GS_OK;   // the query: V only
+  GS_TRY(begin_call(c));
+  GS_TRY(dist_stage(c, b, &g));
+  GS_TRY(tri_degrees(c, g, deg));
+  return host_wait(c);
+}
+
+gs_status gs_tri_dist_route(gs_ctx* c, const gs_edge_batch* b, const uint32_t* deg, uint32_t nparts, uint64_t* keys_out,
+                            uint64_t* counts, uint64_t* loops) {
+  if (!c) return GS_EINVAL;
+  GS_TRY(check_batch(c, b, GS_DIR_ALL));
+  if (!deg || !counts || !loops || (b->n && !keys_out)) return set_error(c, GS_EINVAL, "null pointer");
+  if (nparts < 1 || nparts > (uint32_t)RT_MAXP) return set_error(c, GS_EINVAL, "nparts %u outside [1, 64]", nparts);
+  if (!c->tri_B) return set_error(c, GS_EINVAL, "gs_tri_dist_degrees first (the window's id geometry)");
+  GS_TRY(begin_call(c));
+  TriGeom g;
+  GS_TRY(dist_stage(c, b, &g));
+  GS_TRY(ensure(c, c->out_b, g.V * 4));
+  uint32_t* rank = c->out_b.as<uint32_t>();
+  GS_TRY(tri_ranks(c, g, deg, rank));
+  GS_TRY(ensure(c, c->aux, g.n * 8 + 8));
+  GS_TRY(tri_okeys(c, g, rank, c->aux.as<uint64_t>()));
+  const uint32_t tiles = (uint32_t)std::max<uint64_t>(1, (g.n + RT_TILE - 1) / RT_TILE);
+  GS_TRY(ensure(c, c->tri_tiles, (size_t)tiles * nparts * 4 + 8));
+  uint32_t* cnt = c->tri_tiles.as<uint32_t>();
+  if (g.n) {
+    hipLaunchKernelGGL(k_route_count, dim3(tiles), dim3(RT_BLOCK), 0, c->stream, c->aux.as<uint64_t>(), g.n, g.B, nparts,
+                       tiles, cnt);
+    hipLaunchKernelGGL(k_rank_scan, dim3(1), dim3(1024), 0, c->stream, cnt, tiles * nparts);
+    hipLaunchKernelGGL(k_route_scatter, dim3(tiles), dim3(RT_BLOCK), 0, c->stream, c->aux.as<uint64_t>(), g.n, g.B,
+                       nparts, tiles, cnt, keys_out);
+    GS_HIP(hipGetLastError());
+    // owner o's keys start at cnt[o * tiles] (exclusive scan, owner-major)
+    for (uint32_t o = 0; o < nparts; ++o)
+      GS_HIP(hipMemcpyAsync((uint32_t*)(c->host_small + 16) + o, cnt + (size_t)o * tiles, 4, hipMemcpyDeviceToHost, c->stream));
+  }
+  GS_TRY(host_wait(c));
+  *loops = c->host_small[4];
+  const uint64_t kept = g.n - *loops;
+  const uint32_t* st = (const uint32_t*)(c->host_small + 16);
+  for (uint32_t o = 0; o < nparts; ++o) counts[o] = g.n ? (o + 1 < nparts ? st[o + 1] : kept) - st[o] : 0;
+  return GS_OK;
+}
+
+gs_status gs_tri_dist_build(gs_ctx* c, const uint64_t* keys, uint64_t n, uint32_t* nbr_out, uint32_t* dplus_out,
+                            uint64_t* m_out) {
+  if (!c) return GS_EINVAL;
+  if (!m_out || !dplus_out || (n && (!keys || !nbr_out))) return set_error(c, GS_EINVAL, "null pointer");
+  if (!c->tri_B) return set_error(c, GS_EINVAL, "gs_tri_dist_degrees first (the window's id geometry)");
+  GS_TRY(begin_call(c));
+  hipEventRecord(c->ev[0], c->stream);
+  const uint32_t B = c->tri_B;
+  const size_t V = 1ull << B;
+  GS_TRY(ensure(c, c->tri_range, V * 16));
+  uint2* out_range = reinterpret_cast<uint2*>(c->tri_range.p);
+  GS_HIP(hipMemsetAsync(out_range, 0, V * 8, c->stream));
+  uint64_t M = 0;
+  if (n) {
+    Sorted s;
+    GS_TRY(tri_unique(c, keys, n, B, false, false, &M, &s));
+    if (M)
+      hipLaunchKernelGGL(k_tri_out, dim3((unsigned)std::min<uint64_t>((M + 255) / 256, 16384)), dim3(256), 0, c->stream,
+                         c->out_keys.as<uint64_t>(), (uint32_t)M, B, nbr_out, reinterpret_cast<uint32_t*>(out_range));
+  }
+  hipLaunchKernelGGL(k_tri_dplus, dim3((unsigned)std::min<uint64_t>((V + 255) / 256, 16384)), dim3(256), 0, c->stream,
+                     out_range, (uint32_t)V, dplus_out);
+  GS_HIP(hipGetLastError());
+  *m_out = M;
+  return host_wait(c);
+}
+
+gs_status gs_tri_dist_count(gs_ctx* c, const uint32_t* nbr, uint64_t M, const uint32_t* dplus, uint32_t part,
+                            uint32_t nparts, uint64_t* count) {
+  if (!c) return GS_EINVAL;
+  if (!count || !dplus || (M && !nbr)) return set_error(c, GS_EINVAL, "null pointer");
+  if (nparts == 0 || part >= nparts) return set_error(c, GS_EINVAL, "bad part %u of %u", part, nparts);
+  if (!c->tri_B) return set_error(c, GS_EINVAL, "gs_tri_dist_degrees first (the window's id geometry)");
+  if (M >= (1ull << 32)) return set_error(c, GS_EINVAL, "split window: %llu edges (limit 2^32-1)", (unsigned long long)M);
+  GS_TRY(begin_call(c));
+  *count = 0;
+  if (M == 0) return GS_OK;
+  hipEventRecord(c->ev[0], c->stream);
+  hipEventRecord(c->ev[1], c->stream);
+  const uint32_t B = c->tri_B;
+  const size_t V = 1ull << B;
+  GS_TRY(ensure(c, c->tri_range, V * 16));
+  GS_TRY(ensure(c, c->tri_d[5], (V + 1) * 16));
+  unsigned long long* d64 = c->tri_d[5].as<unsigned long long>();
+  uint2* out_range = reinterpret_cast<uint2*>(c->tri_range.p);
+  const unsigned gv = (unsigned)std::min<uint64_t>((V + 255) / 256, 16384);
+  hipLaunchKernelGGL(k_u32_to_u64, dim3(gv), dim3(256), 0, c->stream, dplus, (uint32_t)V, d64);
+  GS_TRY(xscan(c, (const uint64_t*)d64, V, (uint64_t*)d64 + V));
+  hipLaunchKernelGGL(k_tri_ranges, dim3(gv), dim3(256), 0, c->stream, dplus, (const unsigned long long*)d64 + V,
+                     (uint32_t)V, out_range);
+  GS_HIP(hipGetLastError());
+  hipEventRecord(c->ev[2], c->stream);
+  uint64_t T = 0, probes = 0;
+  GS_TRY(tri_count(c, B, V, M, nbr, out_range, nullptr, part, nparts, &T, &probes));
+  TriGeom g;
+  set_bits(&g, B);
+  tri_times(c, g, M, 0, probes, 0);
+  *count = T;
+  return GS_OK;
+}
+
+gs_status gs_window_triangles_selfpair(gs_ctx* c, const gs_edge_batch* b, uint64_t* S) {
+  if (!c) return GS_EINVAL;
+  GS_TRY(check_batch(c, b, GS_DIR_ALL));
+  if (!S) return set_error(c, GS_EINVAL, "null output pointer");
+  GS_TRY(begin_call(c));
+  *S = 0;
+  if (b->n == 0) return GS_OK;
+  const int64_t *src, *dst;
+  const void* val;
+  GS_TRY(stage_batch(c, b, &src, &dst, &val, false));
+  TriGeom g;
+  GS_TRY(tri_geometry(c, src, dst, b->n, &g));
+  const size_t words = (g.V + 31) / 32;
+  GS_TRY(ensure(c, c->tri_loops, words * 4));
+  GS_HIP(hipMemsetAsync(c->tri_loops.p, 0, words * 4, c->stream));
+  unsigned long long* d_loops = (unsigned long long*)(c->small.as<char>() + SM_NUNIQUE);
+  GS_HIP(hipMemsetAsync(d_loops, 0, 8, c->stream));
+  hipLaunchKernelGGL(k_tri_loops, dim3((unsigned)std::min<uint64_t>((b->n + 255) / 256, 8192)), dim3(256), 0, c->stream,
+                     g.src, g.dst, g.n, g.key_xor, c->tri_loops.as<uint32_t>(), d_loops);
+  GS_HIP(hipGetLastError());
+  GS_HIP(hipMemcpyAsync(c->host_small + 4, d_loops, 8, hipMemcpyDeviceToHost, c->stream));
+  GS_TRY(host_wait(c));
+  if (c->host_small[4] == 0) return GS_OK;
+  return triangle_selfpair_term(c, g.osrc, g.odst, g.n, c->tri_loops.as<uint32_t>(), g.key_xor, g.uniq, g.nuniq, S);
+}
+
+// The split window with the ctx communicator: every rank passes its own records of the window
+gs_status gs_window_triangles_dist(gs_ctx* c, const gs_edge_batch* b, uint64_t* count, int32_t* count_ref_wrapped,
+                                   int32_t* has_output) {
+  if (!c) return GS_EINVAL;
+  if (!count || !count_ref_wrapped || !has_output) return set_error(c, GS_EINVAL, "null output pointer");
+  if (!c->comm) return set_error(c, GS_EINVAL, "no communicator (gs_comm_init)");
+  const uint32_t P = (uint32_t)c->comm_size, me = (uint32_t)c->comm_rank;
+  // 1. the common id range
+  int64_t mm[2];
+  GS_TRY(gs_tri_dist_range(c, b, mm));
+  GS_TRY(ensure(c, c->tri_d[0], 64));
+  long long* dmm = c->tri_d[0].as<long long>();
+  c->host_small[12] = (uint64_t)mm[0];
+  c->host_small[13] = (uint64_t)mm[1];
+  GS_HIP(hipMemcpyAsync(dmm, c->host_small + 12, 16, hipMemcpyHostToDevice, c->stream));
+  GS_TRY(comm_allreduce(c, dmm, 1, NCCL_T_I64, NCCL_OP_MIN));
+  GS_TRY(comm_allreduce(c, dmm + 1, 1, NCCL_T_I64, NCCL_OP_MAX));
+  GS_HIP(hipMemcpyAsync(c->host_small + 12, dmm, 16, hipMemcpyDeviceToHost, c->stream));
+  GS_TRY(host_wait(c));
+  const int64_t gmin = (int64_t)c->host_small[12], gmax = (int64_t)c->host_small[13];
+  uint64_t total_n = b->n;
+  GS_TRY(gs_comm_allreduce_sum_u64(c, &total_n));
+  *count = 0;
+  *count_ref_wrapped = 0;
+  *has_output = total_n > 0;
+  if (total_n == 0) return GS_OK;
+  // 2. degrees, summed over ranks
+  uint64_t V = 0;
+  GS_TRY(gs_tri_dist_degrees(c, b, gmin, gmax, nullptr, &V));
+  GS_TRY(ensure(c, c->tri_d[1], V * 4));
+  uint32_t* deg = c->tri_d[1].as<uint32_t>();
+  GS_TRY(gs_tri_dist_degrees(c, b, gmin, gmax, deg, &V));
+  GS_TRY(comm_allreduce(c, deg, V, NCCL_T_U32, NCCL_OP_SUM));
+  // 3. oriented edges to owner(u): counts matrix, then the rows
+  GS_TRY(ensure(c, c->tri_d[2], b->n * 8 + 8));
+  std::vector<uint64_t> send(P), recv(P);
+  uint64_t loops = 0;
+  GS_TRY(gs_tri_dist_route(c, b, deg, P, c->tri_d[2].as<uint64_t>(), send.data(), &loops));
+  GS_TRY(ensure(c, c->tri_d[0], 64 + (size_t)P * P * 8));
+  uint64_t* dmat = (uint64_t*)(c->tri_d[0].as<char>() + 64);
+  GS_HIP(hipMemsetAsync(dmat, 0, (size_t)P * P * 8, c->stream));
+  memcpy(c->host_small + 16, send.data(), P * 8);
+  GS_HIP(hipMemcpyAsync(dmat + (size_t)me * P, c->host_small + 16, P * 8, hipMemcpyHostToDevice, c->stream));
+  GS_TRY(comm_allreduce(c, dmat, (size_t)P * P, NCCL_T_U64, NCCL_OP_SUM));
+  uint64_t nrecv = 0;
+  for (uint32_t p = 0; p < P; ++p) {   // column me of the matrix: what each rank sends me
+    GS_HIP(hipMemcpyAsync(c->host_small + 16 + p, dmat + (size_t)p * P + me, 8, hipMemcpyDeviceToHost, c->stream));
+  }
+  GS_TRY(host_wait(c));
+  for (uint32_t p = 0; p < P; ++p) nrecv += (recv[p] = c->host_small[16 + p]);
+  GS_TRY(ensure(c, c->tri_d[3], nrecv * 8 + 8));
+  GS_TRY(exchange_rows(c, c->tri_d[2].as<char>(), send.data(), c->tri_d[3].as<char>(), recv.data(), 8));
+  GS_TRY(gs_comm_allreduce_sum_u64(c, &loops));
+  // 4. local out-lists; out-degrees summed (every u has one owner), out-lists all-gathered in rank order
+  GS_TRY(ensure(c, c->tri_d[4], nrecv * 4 + 4));
+  GS_TRY(ensure(c, c->tri_d[1], V * 4));   // the degrees are consumed: d+ reuses the buffer
+  uint32_t* dplus = c->tri_d[1].as<uint32_t>();
+  uint64_t m = 0;
+  GS_TRY(gs_tri_dist_build(c, c->tri_d[3].as<uint64_t>(), nrecv, c->tri_d[4].as<uint32_t>(), dplus, &m));
+  GS_TRY(comm_allreduce(c, dplus, V, NCCL_T_U32, NCCL_OP_SUM));
+  std::vector<uint64_t> ms(P);
+  GS_TRY(comm_allgather_u64(c, m, ms.data()));
+  uint64_t M = 0;
+  for (uint32_t p = 0; p < P; ++p) M += ms[p];
+  GS_TRY(ensure(c, c->tri_d[2], M * 4 + 4));   // the routed keys are consumed
+  GS_TRY(comm_allgatherv(c, c->tri_d[4].p, c->tri_d[2].as<char>(), ms.data(), 4));
+  // 5. this rank's share of the count, summed
+  uint64_t T = 0;
+  GS_TRY(gs_tri_dist_count(c, c->tri_d[2].as<uint32_t>(), M, dplus, me, P, &T));
+  // 6. the self-pair term needs whole neighbour sets: windows with self-loops gather the records
+  if (loops) {
+    std::vector<uint64_t> ns(P);
+    GS_TRY(comm_allgather_u64(c, b->n, ns.data()));
+    const int64_t *src, *dst;
+    const void* val;
+    GS_TRY(stage_batch(c, b, &src, &dst, &val, false));
+    GS_TRY(ensure(c, c->tri_d[3], total_n * 16 + 16));
+    int64_t* all = c->tri_d[3].as<int64_t>();
+    GS_TRY(comm_allgatherv(c, src, (char*)all, ns.data(), 8));
+    GS_TRY(comm_allgatherv(c, dst, (char*)(all + total_n), ns.data(), 8));
+    GS_TRY(host_wait(c));
+    if (me == 0) {
+      const gs_edge_batch wb{all, all + total_n, nullptr, total_n, GS_NONE, GS_MEM_DEVICE, 0};
+      uint64_t S = 0;
+      GS_TRY(gs_window_triangles_selfpair(c, &wb, &S));
+      T += S;
+    }
+  }
+  GS_TRY(gs_comm_allreduce_sum_u64(c, &T));
+  *count = T;
+  *count_ref_wrapped = (int32_t)(uint32_t)T;
+  return GS_OK;
+}
+
+gs_status gs_window_triangles(gs_ctx* c, const gs_edge_batch* b, uint64_t* count, int32_t* count_ref_wrapped,
+                              int32_t* has_output) {
+  if (!c) return GS_EINVAL;
+  if (!count || !count_ref_wrapped || !has_output) return set_error(c, GS_EINVAL, "null output pointer");
+  uint64_t T = 0;
+  GS_TRY(triangles_impl(c, b, 0, 1, &T));
+  *count = T;
+  *count_ref_wrapped = (int32_t)(uint32_t)T;   // Integer sum(0) wraps (WindowTriangles.java:66, :126)
+  *has_output = b && b->n > 0;   // every edge record forms a (v, t) group with edges > 0 (WindowTriangles.java:136)
+  return GS_OK;
+}
+
+gs_status gs_window_triangles_part(gs_ctx* c, const gs_edge_batch* b, uint32_t part, uint32_t nparts,
+                                   uint64_t* partial_count) {
+  if (!c) return GS_EINVAL;
+  return triangles_impl(c, b, part, nparts, partial_count);
+}
+
+}  // extern "C"

@@ -120,14 +120,60 @@ def gather_window(src: torch.Tensor, dst: torch.Tensor, group=None):
     return outs[0], outs[1]
 
 
-def triangles_window(local_part_count, src, dst, group=None):
-    """WindowTriangles over a window spread across ranks: all-gather the adjacency,
-    count this rank's share of the oriented edges, all-reduce(SUM).  Returns (exact, Integer-wrapped)."""
+def triangles_window(eng, src, dst, group=None):
+    """WindowTriangles over a window whose records are split across the ranks of `group` (SURVEY.md §8e,
+    WindowTriangles.java:61-66).  The six steps of include/gelly_hip.h's gs_tri_dist_* with the
+    collectives in torch.distributed: nothing of the raw window travels (unless it has self-loops):
+      1. id range          all-reduce MIN / MAX
+      2. raw degrees       all-reduce SUM of an int32[V]          (every rank renumbers identically)
+      3. oriented edges    all-to-all of 8-byte keys to owner(u)  (contiguous ranges of the degree order)
+      4. out-lists         all-reduce SUM of d+ int32[V]; all-gather of the 4-byte targets (rank order)
+      5. count             each rank its equal-work share of the middle-vertex intersections; all-reduce
+      6. self-pair term    only when the window has self-loops: gather the records, rank 0 adds it
+    eng: an Engine on this rank's GPU; src, dst: this rank's records (device tensors).
+    Returns (exact, Integer-wrapped, has_output), the same on every rank."""
     world, rank = dist.get_world_size(group), dist.get_rank(group)
-    fs, fd = gather_window(src, dst, group)
-    part = local_part_count(fs, fd, rank, world)
-    t = torch.tensor([part], dtype=torch.int64, device=src.device)
+    home = src.device
+    cdev = _comm_device(group, src)
+    lo, hi = eng.tri_dist_range(src, dst)
+    mm = torch.tensor([lo, -hi, src.numel()], dtype=torch.int64, device=cdev)
+    dist.all_reduce(mm[:2], op=dist.ReduceOp.MIN, group=group)   # max as -min(-x)
+    nt = mm[2:].clone()
+    dist.all_reduce(nt, op=dist.ReduceOp.SUM, group=group)
+    gmin, gmax, total = int(mm[0]), -int(mm[1]), int(nt[0])
+    if total == 0:
+        return 0, 0, False
+    deg = eng.tri_dist_degrees(src, dst, gmin, gmax)
+    d = deg.to(cdev)
+    dist.all_reduce(d, op=dist.ReduceOp.SUM, group=group)
+    keys, counts, loops = eng.tri_dist_route(src, dst, d.to(home), world)
+    send = torch.tensor(counts, dtype=torch.int64, device=cdev)
+    recv = torch.empty_like(send)
+    dist.all_to_all_single(recv, send, group=group)
+    rc = recv.tolist()
+    rk = torch.empty(sum(rc), dtype=torch.int64, device=cdev)
+    dist.all_to_all_single(rk, keys.to(cdev), rc, counts, group=group)
+    lt = torch.tensor([loops], dtype=torch.int64, device=cdev)
+    dist.all_reduce(lt, op=dist.ReduceOp.SUM, group=group)
+    nbr, dplus = eng.tri_dist_build(rk.to(home), deg.numel())
+    dp = dplus.to(cdev)
+    dist.all_reduce(dp, op=dist.ReduceOp.SUM, group=group)
+    ms = [torch.zeros(1, dtype=torch.int64, device=cdev) for _ in range(world)]
+    dist.all_gather(ms, torch.tensor([nbr.numel()], dtype=torch.int64, device=cdev), group=group)
+    ms = [int(x) for x in ms]
+    mx = max(ms)
+    pad = torch.zeros(mx, dtype=torch.int32, device=cdev)
+    pad[:nbr.numel()] = nbr.to(cdev)
+    parts = [torch.empty(mx, dtype=torch.int32, device=cdev) for _ in range(world)]
+    dist.all_gather(parts, pad, group=group)
+    allnbr = torch.cat([p[:k] for p, k in zip(parts, ms)]).to(home)
+    T = eng.tri_dist_count(allnbr, dp.to(home), rank, world)
+    if int(lt[0]):
+        fs, fd = gather_window(src, dst, group)
+        if rank == 0:
+            T += eng.triangles_selfpair(fs, fd)
+    t = torch.tensor([T], dtype=torch.int64, device=cdev)
     dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
-    total = int(t.item()) & ((1 << 64) - 1)
-    wrapped = total & 0xFFFFFFFF
-    return total, wrapped - (1 << 32) if wrapped >= (1 << 31) else wrapped
+    total_t = int(t.item()) & ((1 << 64) - 1)
+    wrapped = total_t & 0xFFFFFFFF
+    return total_t, wrapped - (1 << 32) if wrapped >= (1 << 31) else wrapped, True

@@ -297,6 +297,76 @@ class Engine:
         self._check(self._L.gs_window_triangles_part(self.ctx, ctypes.byref(b), part, nparts, ctypes.byref(cnt)))
         return cnt.value
 
+    # -- WindowTriangles over a split window (gs_tri_dist_*, include/gelly_hip.h) -----------------------
+    # Device tensors in and out; the caller runs the collective after each step (distributed.py).
+    def tri_dist_range(self, src, dst):
+        """Step 1: this rank's (min, max) id (all-reduce MIN / MAX across ranks)."""
+        b, keep, dev = self._batch(src, dst, None)
+        mm = (ctypes.c_int64 * 2)()
+        self._check(self._L.gs_tri_dist_range(self.ctx, ctypes.byref(b), mm))
+        return int(mm[0]), int(mm[1])
+
+    def tri_dist_degrees(self, src, dst, gmin: int, gmax: int):
+        """Step 2: this rank's raw degrees over the common id range, an int32 tensor [V] (all-reduce SUM)."""
+        import torch
+
+        b, keep, dev = self._batch(src, dst, None)
+        V = ctypes.c_uint64(0)
+        self._check(self._L.gs_tri_dist_degrees(self.ctx, ctypes.byref(b), int(gmin), int(gmax), None, ctypes.byref(V)))
+        deg = torch.empty(V.value, dtype=torch.int32, device=f"cuda:{self.device}")
+        self._check(self._L.gs_tri_dist_degrees(self.ctx, ctypes.byref(b), int(gmin), int(gmax), _ptr(deg),
+                                                ctypes.byref(V)))
+        return deg
+
+    def tri_dist_route(self, src, dst, deg, nparts: int):
+        """Step 3: oriented edges grouped by owner(u): (int64 keys tensor, rows per owner, self-loops)."""
+        import torch
+
+        b, keep, dev = self._batch(src, dst, None)
+        keys = torch.empty(max(b.n, 1), dtype=torch.int64, device=f"cuda:{self.device}")
+        counts = (ctypes.c_uint64 * nparts)()
+        loops = ctypes.c_uint64(0)
+        self._check(self._L.gs_tri_dist_route(self.ctx, ctypes.byref(b), _ptr(deg.contiguous()), nparts, _ptr(keys),
+                                              counts, ctypes.byref(loops)))
+        counts = [int(x) for x in counts]
+        return keys[:sum(counts)], counts, loops.value
+
+    def tri_dist_build(self, keys, V: int):
+        """Step 4: the received rows -> this rank's out-lists: (int32 targets [m], int32 d+ [V])."""
+        import torch
+
+        keys = keys.contiguous()
+        nbr = torch.empty(max(keys.numel(), 1), dtype=torch.int32, device=f"cuda:{self.device}")
+        dplus = torch.empty(V, dtype=torch.int32, device=f"cuda:{self.device}")
+        m = ctypes.c_uint64(0)
+        self._check(self._L.gs_tri_dist_build(self.ctx, _ptr(keys), keys.numel(), _ptr(nbr), _ptr(dplus),
+                                              ctypes.byref(m)))
+        return nbr[:m.value], dplus
+
+    def tri_dist_count(self, nbr, dplus, part: int, nparts: int) -> int:
+        """Step 5: this rank's share of the count over the whole out-adjacency (all-reduce SUM)."""
+        cnt = ctypes.c_uint64(0)
+        nbr = nbr.contiguous()
+        self._check(self._L.gs_tri_dist_count(self.ctx, _ptr(nbr), nbr.numel(), _ptr(dplus.contiguous()), part, nparts,
+                                              ctypes.byref(cnt)))
+        return cnt.value
+
+    def triangles_selfpair(self, src, dst) -> int:
+        """gs_window_triangles_selfpair: the self-pair term of a whole window."""
+        b, keep, dev = self._batch(src, dst, None)
+        S = ctypes.c_uint64(0)
+        self._check(self._L.gs_window_triangles_selfpair(self.ctx, ctypes.byref(b), ctypes.byref(S)))
+        return S.value
+
+    def triangles_dist(self, src, dst):
+        """gs_window_triangles_dist: this rank's records of the window, the ctx communicator's ranks
+        together -> (exact count, the reference's Integer, has_output), the same on every rank."""
+        b, keep, dev = self._batch(src, dst, None)
+        cnt, wrapped, has = ctypes.c_uint64(0), ctypes.c_int32(0), ctypes.c_int32(0)
+        self._check(self._L.gs_window_triangles_dist(self.ctx, ctypes.byref(b), ctypes.byref(cnt), ctypes.byref(wrapped),
+                                                     ctypes.byref(has)))
+        return cnt.value, wrapped.value, bool(has.value)
+
     # -- multi-GPU keyBy halves (gs_dist.hip) --------------------------------------------------------
     def reduce_partials(self, src, dst, val, direction, op, nparts: int):
         """gs_window_reduce_partials: this slice's per-vertex partials grouped by owner (gs_owner_of).

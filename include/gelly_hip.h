@@ -203,11 +203,48 @@ GS_API gs_status gs_window_candidates(gs_ctx* ctx, const gs_edge_batch* batch, g
 GS_API gs_status gs_window_triangles(gs_ctx* ctx, const gs_edge_batch* batch, uint64_t* count,
                               int32_t* count_ref_wrapped, int32_t* has_output);
 
-/* Multi-GPU WindowTriangles: every rank holds the whole window (all-gathered adjacency) and counts
- * only part `part` of `nparts` of the oriented edges (plus the self-pair term on part 0); the sum of
- * the parts over ranks (an all-reduce) equals gs_window_triangles' count. */
+/* One share of WindowTriangles for a caller that holds the whole window: part `part` of `nparts`
+ * counts the triangles u -> v -> w whose first vertex u lies in the part's range of the degree order,
+ * the ranges cut at equal shares of the work sum_u d+(u)(d+(u)+1)/2 (plus the self-pair term on part
+ * 0); the parts sum (an all-reduce) to gs_window_triangles' count. */
 GS_API gs_status gs_window_triangles_part(gs_ctx* ctx, const gs_edge_batch* batch, uint32_t part,
                                           uint32_t nparts, uint64_t* partial_count);
+
+/* ---- WindowTriangles over a window split across ranks ------------------------
+ * Every rank holds only its own records of the window (the reference's subtasks after slice()).
+ * The steps, with the collective the caller runs after each (torch.distributed, the JVM's, or the
+ * ctx communicator: gs_window_triangles_dist does all of them with RCCL):
+ *   1. gs_tri_dist_range     local [min, max] id            -> all-reduce min of [0], max of [1]
+ *   2. gs_tri_dist_degrees   local raw degrees deg[V]       -> all-reduce (sum, u32) of deg
+ *      (deg == NULL: *V only, to size the buffer; V = 2^bits of the common id span, <= 2^28)
+ *   3. gs_tri_dist_route     oriented edges (u << B | v, u < v in the degree order) grouped by
+ *      owner(u) (contiguous ranges of the order) into keys_out, counts[p] rows for rank p
+ *                                                           -> all-to-all of the rows; all-reduce loops
+ *   4. gs_tri_dist_build     the received rows deduplicated into this rank's out-lists: nbr_out[m]
+ *      (targets, sorted per u) and dplus_out[V] (d+(u) of the owned u, 0 elsewhere)
+ *                                                           -> all-gather nbr (rank order), all-reduce dplus
+ *   5. gs_tri_dist_count     this rank's share (part = rank, nparts = ranks) of the count over the
+ *      whole out-adjacency                                  -> all-reduce (sum) of the counts
+ *   6. windows with self-loops (summed loops > 0): the self-pair term needs whole neighbour sets, so
+ *      the records are gathered and rank 0 adds gs_window_triangles_selfpair of the whole window.
+ * Exchanged per window: 8 B per local record (step 3), 4 B per unique edge + 4 B per id (step 4).
+ * Buffers: deg, keys_out, keys, nbr_out, dplus_out, nbr, dplus are device memory. */
+GS_API gs_status gs_tri_dist_range(gs_ctx* ctx, const gs_edge_batch* local, int64_t* minmax /* [2] */);
+GS_API gs_status gs_tri_dist_degrees(gs_ctx* ctx, const gs_edge_batch* local, int64_t id_min, int64_t id_max,
+                                     uint32_t* deg, uint64_t* V);
+GS_API gs_status gs_tri_dist_route(gs_ctx* ctx, const gs_edge_batch* local, const uint32_t* deg, uint32_t nparts,
+                                   uint64_t* keys_out /* [local n] */, uint64_t* counts /* host [nparts] */,
+                                   uint64_t* loops /* host */);
+GS_API gs_status gs_tri_dist_build(gs_ctx* ctx, const uint64_t* keys, uint64_t n, uint32_t* nbr_out /* [n] */,
+                                   uint32_t* dplus_out /* [V] */, uint64_t* m_out);
+GS_API gs_status gs_tri_dist_count(gs_ctx* ctx, const uint32_t* nbr, uint64_t M, const uint32_t* dplus, uint32_t part,
+                                   uint32_t nparts, uint64_t* partial_count);
+/* The self-pair term alone (WindowTriangles.java:105: (x, x) candidates matched by a self-loop on x)
+ * of a whole window. */
+GS_API gs_status gs_window_triangles_selfpair(gs_ctx* ctx, const gs_edge_batch* window, uint64_t* S);
+/* Steps 1-6 with the ctx communicator (gs_comm_init); every rank gets the window's count. */
+GS_API gs_status gs_window_triangles_dist(gs_ctx* ctx, const gs_edge_batch* local, uint64_t* count,
+                                          int32_t* count_ref_wrapped, int32_t* has_output);
 
 /* Two-phase output without recomputation: after a window call returned GS_ECAPACITY (with the needed
  * size in *n_out) and before the next call on the ctx, deliver the rows it left staged.  Covers

@@ -61,6 +61,90 @@ def oracle_halves(orc):
     return partials, merge, fold_partials, fold_merge
 
 
+class OracleTriEngine:
+    """The gs_tri_dist_* steps restated in numpy (test infrastructure, CPU): the same id geometry,
+    degree-class renumbering, owner(u) ranges, out-lists and equal-work parts as gs_triangles.hip, so
+    distributed.triangles_window's exchanges run on gloo here; the self-pair term comes from the oracle
+    (reference rule minus the simple graph's triangles)."""
+
+    def __init__(self, orc):
+        self.orc = orc
+
+    @staticmethod
+    def _np(t):
+        return t.numpy() if isinstance(t, torch.Tensor) else np.asarray(t)
+
+    def tri_dist_range(self, src, dst):
+        s, d = self._np(src), self._np(dst)
+        if len(s) == 0:
+            return np.iinfo(np.int64).max, np.iinfo(np.int64).min
+        return int(min(s.min(), d.min())), int(max(s.max(), d.max()))
+
+    def _geom(self, gmin, gmax):
+        x = (gmin ^ gmax) & ((1 << 64) - 1)
+        B = max(1, x.bit_length())
+        assert B <= 28
+        return B, gmin & ~((1 << B) - 1)
+
+    def tri_dist_degrees(self, src, dst, gmin, gmax):
+        self.B, self.xor = self._geom(gmin, gmax)
+        V = 1 << self.B
+        s, d = self._np(src) ^ self.xor, self._np(dst) ^ self.xor
+        return torch.from_numpy((np.bincount(s, minlength=V) + np.bincount(d, minlength=V)).astype(np.int32))
+
+    @staticmethod
+    def deg_class(d):
+        d = d.astype(np.int64)
+        lz = np.floor(np.log2(np.maximum(d, 1))).astype(np.int64)
+        half = np.where(lz > 0, (d >> np.maximum(lz - 1, 0)) & 1, 0)
+        return np.where(d == 0, 0, np.minimum(63, 1 + 2 * lz + half))
+
+    def tri_dist_route(self, src, dst, deg, nparts):
+        B, V = self.B, 1 << self.B
+        cls = self.deg_class(self._np(deg))
+        rank = np.empty(V, np.int64)
+        rank[np.argsort(cls, kind="stable")] = np.arange(V)
+        a, b = self._np(src) ^ self.xor, self._np(dst) ^ self.xor
+        keep = a != b
+        ra, rb = rank[a[keep]], rank[b[keep]]
+        u, v = np.minimum(ra, rb), np.maximum(ra, rb)
+        keys = (u << B) | v
+        own = (u * nparts) >> B
+        order = np.argsort(own, kind="stable")
+        return torch.from_numpy(keys[order]), np.bincount(own, minlength=nparts).tolist(), int((~keep).sum())
+
+    def tri_dist_build(self, keys, V):
+        k = np.unique(self._np(keys))
+        u, v = k >> self.B, k & ((1 << self.B) - 1)
+        return torch.from_numpy(v.astype(np.int32)), torch.from_numpy(np.bincount(u, minlength=V).astype(np.int32))
+
+    def tri_dist_count(self, nbr, dplus, part, nparts):
+        nbr, dp = self._np(nbr).astype(np.int64), self._np(dplus).astype(np.int64)
+        V = len(dp)
+        start = np.concatenate([[0], np.cumsum(dp)])
+        work = dp * (dp + 1) // 2
+        pre = np.concatenate([[0], np.cumsum(work)])   # pre[u] = work before u, pre[V] = total
+        W = int(pre[V])
+        lower = lambda t: int(np.searchsorted(pre[:V], t, side="left"))
+        u0 = 0 if part == 0 else lower(W * part // nparts)
+        u1 = V if part + 1 == nparts else lower(W * (part + 1) // nparts)
+        T = 0
+        for u in range(u0, u1):
+            L = nbr[start[u]:start[u + 1]]
+            for i, v in enumerate(L[:-1]):
+                T += len(np.intersect1d(L[i + 1:], nbr[start[v]:start[v + 1]], assume_unique=True))
+        return T
+
+    def triangles_selfpair(self, src, dst):
+        """reference rule minus the simple graph's triangles (this pipeline on the whole window)"""
+        s, d = self._np(src), self._np(dst)
+        lo, hi = self.tri_dist_range(s, d)
+        deg = self.tri_dist_degrees(s, d, lo, hi)
+        k, _, _ = self.tri_dist_route(s, d, deg, 1)
+        nbr, dp = self.tri_dist_build(k, len(deg))
+        return self.orc.window_triangles_ref(s, d)[1] - self.tri_dist_count(nbr, dp, 0, 1)
+
+
 def _free_port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
@@ -129,12 +213,16 @@ def _worker(rank, world, port, q):
     s, d = orc.gen_rmat(12, n, 0x5EED03, a=0.65, b=0.15, c=0.15, permute=False, first_edge=rank * n)
     v = orc.gen_values(n, 5, orc.DT_I64, first_edge=rank * n)
     res = run_cases(D, oracle_halves(orc), s, d, v)
-    # WindowTriangles across ranks: all-gathered adjacency must be the whole window in stream order;
-    # each rank contributes its part (here: rank 0 counts everything) and the all-reduce sums them
     fs, fd = D.gather_window(torch.from_numpy(s), torch.from_numpy(d))
     res["gathered"] = (fs.numpy(), fd.numpy())
-    part = lambda a, b, r, w: (orc.window_triangles_fwd(a.numpy(), b.numpy())[1] if r == 0 else 0)
-    res["tri"] = D.triangles_window(part, torch.from_numpy(s), torch.from_numpy(d))
+    # WindowTriangles over the split window: the real exchanges (ranges, degrees, routed oriented edges,
+    # all-gathered out-lists, equal-work parts) with the steps restated in numpy; plus a small window
+    # with self-loops (the gathered self-pair term)
+    te = OracleTriEngine(orc)
+    ts, td = orc.gen_rmat(11, 20000, 0x5EED05, no_self_loops=True, first_edge=rank * 20000)
+    res["tri"] = D.triangles_window(te, torch.from_numpy(ts), torch.from_numpy(td))
+    ls, ld = orc.gen_rmat(6, 1500, 0x5EED06, first_edge=rank * 1500)
+    res["tri_loops"] = D.triangles_window(te, torch.from_numpy(ls), torch.from_numpy(ld))
     q.put((rank, res))
     dist.barrier()
     dist.destroy_process_group()
@@ -155,10 +243,16 @@ def test_reduce_window_two_ranks(oracle):
     s, d = oracle.gen_rmat(12, 2 * n, 0x5EED03, a=0.65, b=0.15, c=0.15, permute=False)
     v = oracle.gen_values(2 * n, 5, oracle.DT_I64)
     check_cases(oracle, out, world, s, d, v)
+    ts, td = oracle.gen_rmat(11, 40000, 0x5EED05, no_self_loops=True)
+    w, ex, _ = oracle.window_triangles_fwd(ts, td)
+    ls, ld = oracle.gen_rmat(6, 3000, 0x5EED06)
+    assert (ls == ld).any()                       # the self-pair term is exercised
+    lw, lex, _, tree = oracle.window_triangles_ref(ls, ld)
+    assert not tree
     for r in range(world):
         assert np.array_equal(out[r]["gathered"][0], s) and np.array_equal(out[r]["gathered"][1], d)
-        w, ex, _ = oracle.window_triangles_fwd(s, d)
-        assert out[r]["tri"] == (ex, w)
+        assert out[r]["tri"] == (ex, w, True)
+        assert out[r]["tri_loops"] == (lex, lw, True)
 
 
 def test_owner_split_is_balanced():

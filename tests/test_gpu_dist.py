@@ -121,3 +121,84 @@ def test_rccl_world_one_through_the_abi(pkg, oracle):
             assert np.array_equal(g.cpu().numpy(), w)
         assert e.comm_allreduce_sum(12345) == 12345
         e.comm_destroy()
+
+
+# ---- WindowTriangles over a split window (gs_tri_dist_*) -------------------------------------------
+TRI_CASES = (("rmat", 14, 120_000, True), ("loops", 8, 6_000, False), ("wide", 13, 60_000, True))
+
+
+def _tri_case(orc, kind, scale, n, no_loops, rank):
+    s, d = orc.gen_rmat(scale, n, 0x5EED07, no_self_loops=no_loops, first_edge=rank * n)
+    if kind == "wide":   # ids spread over 2^27 (still one 28-bit geometry) and shifted far from 0
+        s, d = s * 13_001 + (5 << 40), d * 13_001 + (5 << 40)
+    return np.ascontiguousarray(s), np.ascontiguousarray(d)
+
+
+def _tri_worker(rank, world, port, q):
+    sys.path.insert(0, str(ROOT))
+    import __graft_entry__ as ge
+    pkg = ge.load_package()
+    from gelly_streaming_amd import distributed as D
+    orc = ge.load_oracle()
+    torch.cuda.set_device(0)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    eng = pkg.Engine(0)
+    res = {}
+    for kind, scale, n, no_loops in TRI_CASES:
+        s, d = _tri_case(orc, kind, scale, n, no_loops, rank)
+        res[kind] = D.triangles_window(eng, torch.from_numpy(s).cuda(), torch.from_numpy(d).cuda())
+    eng.close()
+    q.put((rank, res))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_split_window_triangles_two_ranks_gloo(oracle):
+    """Two processes sharing this GPU, gloo between them: every rank holds half of the window's records;
+    degrees all-reduced, oriented edges routed to owner(u), out-lists all-gathered, each rank counts its
+    equal-work share -> the whole window's count (forward algorithm; the reference rule with loops)."""
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_tri_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = dict(q.get(timeout=100) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for kind, scale, n, no_loops in TRI_CASES:
+        parts = [_tri_case(oracle, kind, scale, n, no_loops, r) for r in range(world)]
+        s = np.concatenate([p[0] for p in parts])
+        d = np.concatenate([p[1] for p in parts])
+        if no_loops:
+            w, ex, _ = oracle.window_triangles_fwd(s, d)
+        else:
+            assert (s == d).any()
+            w, ex, _, tree = oracle.window_triangles_ref(s, d)
+            assert not tree
+        for r in range(world):
+            assert out[r][kind] == (ex, w, True), (kind, r)
+
+
+def test_split_window_steps_and_rccl_world_one(pkg, oracle):
+    """The steps on one rank (nparts 1 and a 3-way split of the count summed) and gs_window_triangles_dist
+    over a world-1 RCCL communicator equal gs_window_triangles."""
+    s, d = oracle.gen_rmat(15, 300_000, 0x5EED08)
+    S, Dd = torch.from_numpy(s).cuda(), torch.from_numpy(d).cuda()
+    with pkg.Engine(0) as e:
+        whole = e.triangles(S, Dd)
+        lo, hi = e.tri_dist_range(S, Dd)
+        assert (lo, hi) == (int(min(s.min(), d.min())), int(max(s.max(), d.max())))
+        deg = e.tri_dist_degrees(S, Dd, lo, hi)
+        keys, counts, loops = e.tri_dist_route(S, Dd, deg, 1)
+        assert counts == [keys.numel()] and loops == int((s == d).sum())
+        nbr, dplus = e.tri_dist_build(keys, deg.numel())
+        assert int(dplus.sum()) == nbr.numel()
+        T = sum(e.tri_dist_count(nbr, dplus, p, 3) for p in range(3))
+        S_ = e.triangles_selfpair(S, Dd) if loops else 0
+        assert T + S_ == whole[0] == e.tri_dist_count(nbr, dplus, 0, 1) + S_
+        e.comm_init(1, 0, pkg.Engine.comm_unique_id())
+        assert e.triangles_dist(S, Dd) == whole
+        e.comm_destroy()
