@@ -18,5 +18,6 @@ from .stream import (AscendingTimestampExtractor, DataStream, EdgeColumns, EdgeD
                      EdgeValueTimestampExtractor, GraphWindowStream, SimpleEdgeStream, StreamExecutionEnvironment,
                      Time, TimeUnit)
 from .triangles import CountTriangles, GenerateCandidateEdges, window_triangles  # noqa: F401
+from .aggregation import ConnectedComponents, WindowGraphAggregation  # noqa: F401
 
 __all__ = [n for n in dir() if not n.startswith("_")]

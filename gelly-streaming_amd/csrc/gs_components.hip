@@ -1,0 +1,154 @@
+// gs_components.hip — ConnectedComponents over a window stream:
+//   library/ConnectedComponents.java:56-131 on WindowGraphAggregation.java:47-65 (GraphAggregation's
+//   Merger, transientState = false): every window's edges are folded into a DisjointSet (UpdateCC ->
+//   DisjointSet.union, example/util/DisjointSet.java:97-123) and merged into the running state
+//   (CombineCC -> DisjointSet.merge :132-136).  The state after a window is the partition of every
+//   vertex seen so far into weakly connected components.
+//
+// gs_window_components computes that state on the GPU from the window's edges and the previous state
+// (vertex, label) rows, which join the window as edges vertex -- label:
+//   1. compact IDs: relabel_endpoints (sort of the 2(n + m) endpoints, order-preserving)
+//   2. union-find with the larger root always linked under the smaller one (atomicCAS on the root,
+//      find with pointer halving; parents only ever decrease, so stale reads only cost retries)
+//   3. full compression: every vertex's root = the smallest compact ID of its component = the
+//      smallest vertex (the IDs are order-preserving), the canonical label of the partition
+// Which vertex the reference's DisjointSet keeps as a root depends on HashMap iteration order; the
+// partition (what ConnectedComponentsTest and DisjointSet.toString observe) does not.
+#include "gs_ops.hpp"
+
+namespace gs {
+
+__device__ __forceinline__ uint32_t cc_find(uint32_t* parent, uint32_t x) {
+  uint32_t y = parent[x];
+  if (y != x) {
+    uint32_t z;
+    while (y > (z = parent[y])) {   // pointer halving: x skips to its grandparent
+      parent[x] = z;
+      x = y;
+      y = z;
+    }
+  }
+  return y;
+}
+
+__global__ __launch_bounds__(256) void k_cc_init(uint32_t* __restrict__ parent, uint32_t n) {
+  for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < n; i += gridDim.x * 256u) parent[i] = i;
+}
+
+// one union per edge (compact endpoints at[2e], at[2e + 1])
+__global__ __launch_bounds__(256) void k_cc_hook(const uint32_t* __restrict__ at, uint64_t ne, uint32_t* parent) {
+  for (uint64_t e = (uint64_t)blockIdx.x * 256 + threadIdx.x; e < ne; e += (uint64_t)gridDim.x * 256) {
+    uint32_t a = cc_find(parent, at[2 * e]), b = cc_find(parent, at[2 * e + 1]);
+    while (a != b) {
+      const uint32_t hi = a > b ? a : b, lo = a > b ? b : a;
+      const uint32_t old = atomicCAS(&parent[hi], hi, lo);
+      if (old == hi) break;      // hi was a root: linked under lo
+      // hi got a parent meanwhile (always smaller): continue from its current root
+      a = cc_find(parent, old);
+      b = lo;
+    }
+  }
+}
+
+// roots (= smallest compact ID of the component) -> labels in original IDs
+__global__ __launch_bounds__(256) void k_cc_emit(uint32_t* parent, const int64_t* __restrict__ uniq, uint32_t n,
+                                                 int64_t* __restrict__ keys, int64_t* __restrict__ labels) {
+  for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < n; i += gridDim.x * 256u) {
+    uint32_t r = i;
+    while (parent[r] != r) r = parent[r];
+    keys[i] = uniq[i];
+    labels[i] = uniq[r];
+  }
+}
+
+__global__ __launch_bounds__(256) void k_cc_concat(const int64_t* __restrict__ a, const int64_t* __restrict__ b,
+                                                   uint64_t n, int64_t* __restrict__ oa, int64_t* __restrict__ ob) {
+  for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) {
+    oa[i] = a[i];
+    ob[i] = b[i];
+  }
+}
+
+}  // namespace gs
+
+using namespace gs;
+
+extern "C" {
+
+gs_status gs_window_components(gs_ctx* c, const gs_edge_batch* b, const gs_partial_batch* prev, gs_vertex_out* out) {
+  if (!c) return GS_EINVAL;
+  GS_TRY(check_batch(c, b, GS_DIR_OUT));
+  if (prev && prev->n && (!prev->keys || !prev->vals)) return set_error(c, GS_EINVAL, "bad previous state");
+  if (prev && prev->n && prev->val_dtype != GS_I64) return set_error(c, GS_EINVAL, "state labels must be I64");
+  if (!out || !out->n_out || (out->capacity && (!out->keys || !out->vals))) return set_error(c, GS_EINVAL, "bad gs_vertex_out");
+  GS_TRY(begin_call(c));
+  hipEventRecord(c->ev[0], c->stream);
+  const uint64_t n = b->n, m = prev ? prev->n : 0, N = n + m;
+  *out->n_out = 0;
+  if (N == 0) return GS_OK;
+  // 1. the window's edges + the state's (vertex, label) rows, on the device
+  GS_TRY(ensure(c, c->cc[0], N * 8));
+  GS_TRY(ensure(c, c->cc[1], N * 8));
+  int64_t* A = c->cc[0].as<int64_t>();
+  int64_t* Bc = c->cc[1].as<int64_t>();
+  if (n) {
+    const int64_t *src, *dst;
+    const void* val;
+    GS_TRY(stage_batch(c, b, &src, &dst, &val, false));
+    hipLaunchKernelGGL(k_cc_concat, dim3((unsigned)std::min<uint64_t>((n + 255) / 256, 8192)), dim3(256), 0, c->stream,
+                       src, dst, n, A, Bc);
+  }
+  if (m) {
+    const hipMemcpyKind k = prev->mem == GS_MEM_DEVICE ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
+    GS_HIP(hipMemcpyAsync(A + n, prev->keys, m * 8, k, c->stream));
+    GS_HIP(hipMemcpyAsync(Bc + n, prev->vals, m * 8, k, c->stream));
+  }
+  GS_HIP(hipGetLastError());
+  // 2. compact IDs
+  const int64_t *ca, *cb, *uniq;
+  uint64_t U = 0;
+  GS_TRY(relabel_endpoints(c, A, Bc, N, &ca, &cb, &uniq, &U));
+  hipEventRecord(c->ev[1], c->stream);
+  // 3. union-find over the compact endpoint pairs (rl[4]: at[2e], at[2e + 1])
+  GS_TRY(ensure(c, c->cc[2], U * 4 + 4));
+  uint32_t* parent = c->cc[2].as<uint32_t>();
+  const unsigned gu = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((U + 255) / 256, 16384));
+  const unsigned ge = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((N + 255) / 256, 16384));
+  hipLaunchKernelGGL(k_cc_init, dim3(gu), dim3(256), 0, c->stream, parent, (uint32_t)U);
+  hipLaunchKernelGGL(k_cc_hook, dim3(ge), dim3(256), 0, c->stream, c->rl[4].as<uint32_t>(), N, parent);
+  GS_HIP(hipGetLastError());
+  hipEventRecord(c->ev[2], c->stream);
+  // 4. labels
+  *out->n_out = U;
+  c->last_U = U;
+  if (U > out->capacity) return set_error(c, GS_ECAPACITY, "components need %llu vertices", (unsigned long long)U);
+  const bool direct = out->mem == GS_MEM_DEVICE;
+  int64_t* kd = out->keys;
+  int64_t* vd = (int64_t*)out->vals;
+  if (!direct) {
+    GS_TRY(ensure(c, c->out_keys, U * 8));
+    GS_TRY(ensure(c, c->out_a, U * 8));
+    kd = c->out_keys.as<int64_t>();
+    vd = c->out_a.as<int64_t>();
+  }
+  hipLaunchKernelGGL(k_cc_emit, dim3(gu), dim3(256), 0, c->stream, parent, uniq, (uint32_t)U, kd, vd);
+  GS_HIP(hipGetLastError());
+  hipEventRecord(c->ev[3], c->stream);
+  if (!direct) {
+    GS_TRY(deliver(c, out->keys, kd, U * 8, out->mem));
+    GS_TRY(deliver(c, out->vals, vd, U * 8, out->mem));
+  }
+  GS_TRY(host_wait(c));
+  gs_stage_times& t = c->times;
+  t = gs_stage_times{};
+  hipEventElapsedTime(&t.pass_ms[0], c->ev[0], c->ev[1]);   // staging + compact IDs
+  hipEventElapsedTime(&t.pass_ms[1], c->ev[1], c->ev[2]);   // union-find
+  hipEventElapsedTime(&t.pass_ms[2], c->ev[2], c->ev[3]);   // labels
+  hipEventElapsedTime(&t.total_ms, c->ev[0], c->ev[3]);
+  t.records = N;
+  t.vertices = U;
+  t.path = 4;
+  return GS_OK;
+}
+
+}  // extern "C"

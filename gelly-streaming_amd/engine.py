@@ -367,6 +367,30 @@ class Engine:
                                                      ctypes.byref(has)))
         return cnt.value, wrapped.value, bool(has.value)
 
+    # -- ConnectedComponents (gs_components.hip) -------------------------------------------------------
+    def components(self, src, dst, prev=None):
+        """gs_window_components: the running components after this window's edges; prev = (vertices,
+        labels) of the previous window's state or None.  Returns (vertices ascending, smallest vertex of
+        each one's component), on the columns' side (device tensors / numpy)."""
+        b, keep, dev = self._batch(src, dst, None)
+        pk = pv = None
+        pb = None
+        if prev is not None and len(prev[0]):
+            pk, pv = prev
+            if dev:
+                pk, pv = pk.contiguous(), pv.contiguous()
+            else:
+                pk, pv = np.ascontiguousarray(pk, np.int64), np.ascontiguousarray(pv, np.int64)
+            pb = L.GsPartialBatch(_ptr(pk), _ptr(pv), None, len(pk), L.GS_I64, L.GS_MEM_DEVICE if dev else L.GS_MEM_HOST)
+        cap = 2 * (b.n + (len(pk) if pk is not None else 0)) + 1
+        keys, labels = self._empty(dev, cap, np.int64), self._empty(dev, cap, np.int64)
+        n_out = ctypes.c_uint64(0)
+        out = L.GsVertexOut(_ptr(keys), _ptr(labels), cap, ctypes.pointer(n_out), L.GS_MEM_DEVICE if dev else L.GS_MEM_HOST, 0)
+        self._check(self._L.gs_window_components(self.ctx, ctypes.byref(b), ctypes.byref(pb) if pb is not None else None,
+                                                 ctypes.byref(out)))
+        U = n_out.value
+        return keys[:U], labels[:U]
+
     # -- multi-GPU keyBy halves (gs_dist.hip) --------------------------------------------------------
     def reduce_partials(self, src, dst, val, direction, op, nparts: int):
         """gs_window_reduce_partials: this slice's per-vertex partials grouped by owner (gs_owner_of).

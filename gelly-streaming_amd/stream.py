@@ -215,6 +215,10 @@ class SimpleEdgeStream:
         ts = None if e.ts is None else np.repeat(np.asarray(e.ts), 2)
         return SimpleEdgeStream(EdgeColumns(src, dst, val, ts), self.context)
 
+    def aggregate(self, graphAggregation) -> "DataStream":
+        """GraphStream.aggregate (SimpleEdgeStream.java:104-106): e.g. ConnectedComponents(mergeWindowTime)."""
+        return graphAggregation.run(self)
+
     def slice(self, size: Time, direction: EdgeDirection = EdgeDirection.OUT) -> "GraphWindowStream":
         """:139-171 tumbling windows keyed by the neighbour-key vertex."""
         if not isinstance(direction, EdgeDirection) and direction not in (0, 1, 2):

@@ -310,6 +310,16 @@ GS_API gs_status gs_window_reduce_dist(gs_ctx* ctx, const gs_edge_batch* batch, 
 GS_API gs_status gs_window_fold_degree_max_dist(gs_ctx* ctx, const gs_edge_batch* batch, int32_t dir,
                                                 int64_t init_max, gs_degree_out* out);
 
+/* ConnectedComponents over a window stream (library/ConnectedComponents.java:56-131 through
+ * WindowGraphAggregation.java:47-65): the running DisjointSet state after this window -- the previous
+ * state's (vertex, label) rows (NULL or n = 0 for the first window) merged with the window's edges
+ * (direction ignored: weakly connected).  out: every vertex seen so far, ascending, with the smallest
+ * vertex of its component (I64 labels); the partition is the reference's, the label is canonical (which
+ * vertex DisjointSet keeps as root depends on HashMap iteration order).  Feed the output back as `prev`
+ * for the next window (transientState = false). */
+GS_API gs_status gs_window_components(gs_ctx* ctx, const gs_edge_batch* window, const gs_partial_batch* prev,
+                                      gs_vertex_out* out);
+
 /* Candidate records of one window as produced by GenerateCandidateEdges (gs_pair_out layout). */
 typedef struct gs_pair_batch {
   const int64_t* a;

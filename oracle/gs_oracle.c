@@ -1104,3 +1104,82 @@ GSO_API int gso_triangles_fwd_mt(const int64_t* src, const int64_t* dst, uint64_
   free(e); free(tmp); free(ids); free(cs); free(cd); free(th); free(args); free(deg); free(off); free(fill); free(nbr);
   return 0;
 }
+
+/* ---- ConnectedComponents (library/ConnectedComponents.java:56-131, example/util/DisjointSet.java) ----
+ * DisjointSet restated over the window's ids (sorted distinct ids -> index): union(e1, e2) makes absent
+ * elements their own set, finds both roots with path compression (find :71-85) and links by rank,
+ * ties under root1 (:113-122).  merge(other) = union(key, value) over other's entries (:132-136).
+ * ConnectedComponents folds a window's edges into a DisjointSet (UpdateCC :86-90) and the Merger combines
+ * it into the running state (CombineCC :120-130; GraphAggregation Merger, transientState = false):
+ * the state after a window = union of the previous state's (vertex, parent) entries and the window's
+ * edges.  Output: every vertex of the state, ascending, with the smallest vertex of its component
+ * (the partition is what the reference's toString / ConnectedComponentsTest observe; which vertex is
+ * a root depends on HashMap iteration order and is not part of it).  Returns the vertex count. */
+static int64_t ds_find(int64_t* parent, int64_t e) {
+  int64_t p = parent[e];
+  if (p != e) {
+    const int64_t t = ds_find(parent, p);
+    if (t != p) {
+      p = t;
+      parent[e] = p;
+    }
+  }
+  return p;
+}
+
+static void ds_union(int64_t* parent, int32_t* rank, int64_t e1, int64_t e2) {
+  const int64_t r1 = ds_find(parent, e1), r2 = ds_find(parent, e2);
+  if (r1 == r2) return;
+  if (rank[r1] > rank[r2]) parent[r2] = r1;
+  else if (rank[r1] < rank[r2]) parent[r1] = r2;
+  else {
+    parent[r2] = r1;
+    rank[r1] += 1;
+  }
+}
+
+static int64_t idx_of(const int64_t* ids, int64_t n, int64_t x) {
+  int64_t a = 0, b = n;
+  while (a < b) {
+    const int64_t m = (a + b) / 2;
+    if (ids[m] < x) a = m + 1;
+    else b = m;
+  }
+  return a;
+}
+
+GSO_API int64_t gso_components(const int64_t* src, const int64_t* dst, uint64_t n, const int64_t* prev_v,
+                               const int64_t* prev_l, uint64_t m, int64_t* out_v, int64_t* out_l) {
+  const uint64_t tot = 2 * n + 2 * m;
+  int64_t* ids = (int64_t*)malloc((tot + 1) * sizeof(int64_t));
+  uint64_t k = 0;
+  for (uint64_t i = 0; i < n; ++i) { ids[k++] = src[i]; ids[k++] = dst[i]; }
+  for (uint64_t i = 0; i < m; ++i) { ids[k++] = prev_v[i]; ids[k++] = prev_l[i]; }
+  qsort(ids, k, sizeof(int64_t), cmp_i64);
+  int64_t u = 0;
+  for (uint64_t i = 0; i < k; ++i)
+    if (i == 0 || ids[i] != ids[i - 1]) ids[u++] = ids[i];
+  int64_t* parent = (int64_t*)malloc((u + 1) * sizeof(int64_t));
+  int32_t* rank = (int32_t*)calloc(u + 1, sizeof(int32_t));
+  for (int64_t i = 0; i < u; ++i) parent[i] = i;
+  /* the running state first (its entries merged edge by edge), then the window's edges: the partition
+   * is the same in any order */
+  for (uint64_t i = 0; i < m; ++i) ds_union(parent, rank, idx_of(ids, u, prev_v[i]), idx_of(ids, u, prev_l[i]));
+  for (uint64_t i = 0; i < n; ++i) ds_union(parent, rank, idx_of(ids, u, src[i]), idx_of(ids, u, dst[i]));
+  /* canonical label: the smallest vertex of the component */
+  int64_t* minv = (int64_t*)malloc((u + 1) * sizeof(int64_t));
+  for (int64_t i = 0; i < u; ++i) minv[i] = INT64_MAX;
+  for (int64_t i = 0; i < u; ++i) {
+    const int64_t r = ds_find(parent, i);
+    if (ids[i] < minv[r]) minv[r] = ids[i];
+  }
+  for (int64_t i = 0; i < u; ++i) {
+    out_v[i] = ids[i];
+    out_l[i] = minv[ds_find(parent, i)];
+  }
+  free(minv);
+  free(rank);
+  free(parent);
+  free(ids);
+  return u;
+}

@@ -58,6 +58,7 @@ def lib():
             "gso_gen_zipf": (i32, [u64, ctypes.c_double, u64, u64, u64, P, P]),
             "gso_window_fold_mt": (i64, [P, P, P, u64, i32, i32, i32, i32, P, i64, i32, P, P, P, u64]),
             "gso_triangles_fwd_mt": (i32, [P, P, u64, i32, ctypes.POINTER(u64)]),
+            "gso_components": (i64, [P, P, u64, P, P, u64, P, P]),
         }
         for name, (res, args) in sig.items():
             f = getattr(L, name)
@@ -307,3 +308,15 @@ def split_windows(ts, size):
 
 def java_hashset_cap(k):
     return int(lib().gso_java_hashset_cap(k))
+
+
+def components(src, dst, prev=None):
+    """ConnectedComponents after one window (gso_components): the running state `prev` = (vertices,
+    labels) or None, merged with the window's edges -> (vertices ascending, smallest vertex of each one's
+    component)."""
+    src, dst = _i64(src), _i64(dst)
+    pv, pl = (np.empty(0, np.int64), np.empty(0, np.int64)) if prev is None else (_i64(prev[0]), _i64(prev[1]))
+    cap = 2 * len(src) + 2 * len(pv) + 1
+    ov, ol = np.empty(cap, np.int64), np.empty(cap, np.int64)
+    u = lib().gso_components(_p(src), _p(dst), len(src), _p(pv), _p(pl), len(pv), _p(ov), _p(ol))
+    return ov[:u].copy(), ol[:u].copy()

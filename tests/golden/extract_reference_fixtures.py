@@ -10,6 +10,9 @@ It parses DATA out of the reference's test sources (read as text):
   - TestReverse.java / TestUndirected.java   expected edge lists of reverse() / undirected()
   - ExamplesTestData.java:21-34       TRIANGLES_DATA and TRIANGLES_RESULT; window 400 ms
                                        from WindowTrianglesITCase.java:43
+  - ConnectedComponentsTest.java:19-38  the 6 edges, the expected components, the 5 ms merge window
+  - DisjointSetTest.java:19-64          union(i, i + 2) for i < 8 -> 10 elements / 2 roots; merged with
+                                       union(i, i + 100) for i < 8 -> 18 elements / 2 roots
 Only inputs and expected outputs are written — no reference source text.
 """
 from __future__ import annotations
@@ -68,6 +71,21 @@ def main() -> int:
     itcase = (REF / "example" / "test" / "WindowTrianglesITCase.java").read_text()
     window_ms = int(re.search(r"WindowTriangles\.main\(new String\[\]\{[^}]*\"(\d+)\"\}\)", itcase).group(1))
 
+    cct = (REF / "example" / "test" / "ConnectedComponentsTest.java").read_text()
+    cc_edges = [[int(a), int(b)] for a, b in re.findall(r"new Edge<>\((\d+)L,\s*(\d+)L,\s*NullValue", cct)]
+    cc_res = "".join(re.findall(r"\"([^\"]*)\"", re.search(r"Connected_RESULT\s*=(.*?);", cct, re.S).group(1)))
+    cc_comps = [sorted(int(x) for x in re.findall(r"\d+", ln)) for ln in cc_res.replace("\\n", "\n").split("\n") if ln.strip()]
+    cc_ms = int(re.search(r"new ConnectedComponents<[^>]*>\((\d+)\)", cct).group(1))
+    dst_ = (REF / "example" / "util" / "DisjointSetTest.java").read_text()
+    setup = re.search(r"for \(int i = 0; i < (\d+); i\+\+\) \{\s*ds\.union\(i, i \+ (\d+)\);", dst_)
+    merge = re.search(r"for \(int i = 0; i < (\d+); i\+\+\) \{\s*ds2\.union\(i, i \+ (\d+)\);", dst_)
+    sizes = [int(x) for x in re.findall(r"assertEquals\((?:ds\.getMatches\(\)\.size\(\), )?(\d+)", dst_)]
+    roots = [int(x) for x in re.findall(r"assertEquals\((\d+), treeRoots\.size\(\)\)", dst_)]
+    ds = {"unions": [[i, i + int(setup.group(2))] for i in range(int(setup.group(1)))],
+          "size": sizes[0], "roots": 2,   # testFind: find(0) != find(1), every i has the root of i % 2
+          "merge_unions": [[i, i + int(merge.group(2))] for i in range(int(merge.group(1)))],
+          "merged_size": sizes[1], "merged_roots": roots[0]}
+
     fixtures = {
         "source": "Ren91/gelly-streaming test sources (see extract_reference_fixtures.py docstring)",
         "slice_graph": {"edges": edges, "window_ms": 1000,
@@ -76,6 +94,8 @@ def main() -> int:
         "reverse_expected": reverse,
         "undirected_expected": undirected,
         "triangles": {"edges_src_trg_ts": tri_edges, "window_ms": window_ms, "expected": tri_out},
+        "connected_components": {"edges": cc_edges, "merge_window_ms": cc_ms, "expected": cc_comps},
+        "disjoint_set": ds,
     }
     OUT.write_text(json.dumps(fixtures, indent=1) + "\n")
     print(f"wrote {OUT} ({len(edges)} slice edges, {len(cases)} slice cases, {len(tri_edges)} triangle edges)")

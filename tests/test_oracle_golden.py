@@ -163,3 +163,29 @@ def test_parse_edges_text_rules(oracle):
     for bad in BAD_RECORDS:
         with pytest.raises(ValueError, match="record 1"):
             oracle.parse_edges_text(b"1 2 3\n" + bad + b"\n4 5 6\n")
+
+
+def test_connected_components_fixture(oracle):
+    """ConnectedComponentsTest.java:19-38: edges 1-2 1-3 2-3 1-5 6-7 8-9 -> {1,2,3,5} {6,7} {8,9}."""
+    cc = FIX["connected_components"]
+    e = np.array(cc["edges"], dtype=np.int64)
+    v, lab = oracle.components(e[:, 0], e[:, 1])
+    comps = {}
+    for x, l in zip(v.tolist(), lab.tolist()):
+        comps.setdefault(l, []).append(x)
+    assert sorted(sorted(c) for c in comps.values()) == sorted(cc["expected"])
+    assert all(l == min(c) for l, c in comps.items())
+
+
+def test_disjoint_set_fixture(oracle):
+    """DisjointSetTest.java: union(i, i + 2), i < 8 -> 10 elements in 2 sets (evens, odds); merged into
+    a set of union(i, i + 100), i < 8 -> 18 elements in 2 sets."""
+    ds = FIX["disjoint_set"]
+    u = np.array(ds["unions"], dtype=np.int64)
+    v, lab = oracle.components(u[:, 0], u[:, 1])
+    assert len(v) == ds["size"] and len(set(lab.tolist())) == ds["roots"]
+    assert all(l == x % 2 for x, l in zip(v.tolist(), lab.tolist()))
+    m = np.array(ds["merge_unions"], dtype=np.int64)
+    v2, l2 = oracle.components(m[:, 0], m[:, 1])
+    vm, lm = oracle.components(u[:, 0], u[:, 1], prev=(v2, l2))   # ds2.merge(ds)
+    assert len(vm) == ds["merged_size"] and len(set(lm.tolist())) == ds["merged_roots"]
