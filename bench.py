@@ -57,9 +57,10 @@ def parse():
     p.add_argument("--windows-edges", type=float, default=1e8,
                    help="apply (C5): edges per 1000 ms window of the continuous stream")
     p.add_argument("--workload", default="reduce",
-                   choices=["reduce", "fold", "triangles", "c1", "apply", "candidates", "parse", "e2e"],
+                   choices=["reduce", "fold", "triangles", "cc", "c1", "apply", "candidates", "parse", "e2e"],
                    help="reduce = C2 (default, the headline); fold = C3 degree/max on skewed R-MAT; "
-                        "triangles = WindowTriangles on an R-MAT window without self-loops (C4 shape)")
+                        "triangles = WindowTriangles on an R-MAT window without self-loops (C4 shape); "
+                        "cc = ConnectedComponents of an R-MAT window (SURVEY.md §8f#4)")
     return p.parse_args()
 
 
@@ -218,6 +219,36 @@ def cpu_baseline(wins, workload, threads, reps=5):
                       f"gso_baseline_reduce), 1 warm-up + median of {reps}",
             "window_s_median": tmed, "single_core_value": k1 / t1,
             "single_core_sample": f"first {k1} edges of window 0, one thread"}
+
+
+def cc_kernel_table(times_list, E):
+    """ConnectedComponents (stage_times path 4): compact IDs (sort of the 2E endpoints with positions),
+    union-find over the E edges, labels out."""
+    mean = lambda f: statistics.mean(f(t) for t in times_list)
+    U = mean(lambda t: t.vertices)
+    return {
+        "cc_compact_ids(sort)": {"ms": mean(lambda t: t.pass_ms[0]), "bytes": 16 * E + 2 * E * 12 * 4 + 24 * E},
+        "cc_union_find": {"ms": mean(lambda t: t.pass_ms[1]), "bytes": 8 * E + 4 * U},
+        "cc_labels": {"ms": mean(lambda t: t.pass_ms[2]), "bytes": 4 * U + 8 * U + 16 * U},
+    }, U
+
+
+def cpu_baseline_cc(src, dst, sample_log2=23):
+    """ConnectedComponents on the host: the oracle's DisjointSet restatement (one thread, as the
+    reference's parallelism-1 merger) on the first 2^sample_log2 edges, 1 warm-up + median of 3."""
+    orc = ge.load_oracle()
+    S = min(1 << sample_log2, src.numel())
+    s, d = src[:S].cpu().numpy(), dst[:S].cpu().numpy()
+    orc.components(s[: S // 16], d[: S // 16])
+    ts = []
+    for _ in range(3):
+        t = time.perf_counter()
+        v, _ = orc.components(s, d)
+        ts.append(time.perf_counter() - t)
+    dt = statistics.median(ts)
+    return {"value": S / dt, "unit": "edges/s", "cores": 1, "kind": "port",
+            "sample": f"first 2^{sample_log2} edges of the window, union-find by rank with path compression "
+                      f"(oracle/gs_oracle.c gso_components, one thread), median of 3: {dt:.2f} s, {len(v)} vertices"}
 
 
 def cpu_baseline_triangles(src, dst, threads, sample_log2=24):
@@ -508,6 +539,8 @@ def main():
             src, dst = eng.generate_rmat(a.scale, E, 0x5EED03, a=0.65, b=0.15, c=0.15, permute=False, first_edge=fe)
         elif a.workload == "triangles":   # C4 shape: R-MAT, self-loops removed
             src, dst = eng.generate_rmat(a.scale, E, 0x5EED04, no_self_loops=True, first_edge=fe)
+        elif a.workload == "cc":          # ConnectedComponents: R-MAT (permuted ids)
+            src, dst = eng.generate_rmat(a.scale, E, 0x5EED05, first_edge=fe)
         else:                         # C2
             src, dst = eng.generate_rmat(a.scale, E, a.seed, first_edge=fe)
         val = eng.generate_values(E, a.seed, vdt, first_edge=fe) if a.workload == "reduce" else None
@@ -558,6 +591,9 @@ def main():
                 tot = part_count(src, dst, 0, 1)
             z = torch.zeros(1, dtype=torch.int64, device=src.device)
             return z + tot, z, local_times[0]
+        if a.workload == "cc":   # per-window components (replicas only across GPUs: no exchange)
+            r = eng.components(src, dst)
+            return r[0], r[1], eng.stage_times()
         if a.workload == "fold":
             r = D.fold_degree_max_window(fold_partials_timed, M_fold, src, dst, 1, -(1 << 63)) if dist \
                 else local_fold(src, dst, 1, -(1 << 63))
@@ -603,6 +639,10 @@ def main():
     if a.workload == "triangles":
         kt, partials = triangle_kernel_table(times, E * world)
         B = 16 * E       # §8(d): the edge-list term; the intersection term is per probe (kernels table)
+    elif a.workload == "cc":
+        kt, U_cc = cc_kernel_table(times, E)
+        partials = 0
+        B = 16 * E + 16 * U_cc
     else:
         kt, partials = kernel_table(times, E_rec, U_avg)
         B = algorithmic_bytes(a.workload, E, U_avg, 8)
@@ -622,7 +662,8 @@ def main():
                 "algorithmic_bytes_per_launch": B,
                 "algorithmic_bytes_formula": {"reduce": "16E + 16U (SURVEY.md §8d, reduce OUT, 8-byte values)",
                                               "fold": "16E + 24U (SURVEY.md §8d, fold degree/max)",
-                                              "triangles": "16E (SURVEY.md §8d edge-list term)"}[a.workload],
+                                              "triangles": "16E (SURVEY.md §8d edge-list term)",
+                                              "cc": "16E + 16U (edge list in, (vertex, label) out)"}[a.workload],
                 "avg_launch_ms": round(dom["ms"], 4),
                 "kernel_own_bytes_per_launch": dom["bytes"], "kernel_own_frac": round(dom["frac"], 4),
                 "whole_window": {"achieved": round(window_gbs, 1), "frac": round(window_gbs / HBM_PEAK_GBS, 4),
@@ -631,6 +672,17 @@ def main():
                 "window_traffic_over_B": round(pmc_window / B, 3) if pmc_window else None,
                 "timing": "device events on the library's stream around each launch (gs_last_stage_times)"}
 
+    if a.workload == "triangles":
+        # the count step is bound by LDS reads, not HBM: one 16-byte bucket read per hash probe ->
+        # 128 B/clk/CU x 256 CUs x 2.4 GHz / 16 B = 4.9 T probes/s (MI355X_MICROARCH.md LDS bandwidth)
+        t_cnt = kt["tri_count(light+heavy)"]["ms"] * 1e-3
+        peak = 128 * 256 * 2.4e9 / 16 / 1e9
+        ach = partials / t_cnt / 1e9 if t_cnt > 0 else 0.0
+        roofline["probe_roofline"] = {"bound": "lds", "kernel": "tri_count(light+heavy)", "achieved": round(ach, 1),
+                                      "peak": round(peak, 1), "unit": "G probes/s", "frac": round(ach / peak, 4),
+                                      "probes_per_window": int(partials),
+                                      "peak_formula": "LDS 128 B/clk/CU x 256 CUs x 2.4 GHz / 16 B per bucket read"}
+
     cpu = None
     threads = max(1, min(16, os.cpu_count() or 1))
     if world == 1 and rank == 0 and not a.no_cpu_baseline:
@@ -638,6 +690,8 @@ def main():
             cpu = cpu_baseline(wins, a.workload, threads)
         elif a.workload == "triangles":
             cpu = cpu_baseline_triangles(wins[0][0], wins[0][1], threads)
+        elif a.workload == "cc":
+            cpu = cpu_baseline_cc(wins[0][0], wins[0][1])
     value = E * world * a.steps / elapsed
     if cpu:
         cpu["gpu_over_cpu"] = round(value / cpu["value"], 1)
@@ -662,16 +716,24 @@ def main():
             "config": {"workload": {"reduce": f"C2: slice(OUT).reduceOnEdges(SUM) over R-MAT scale-{a.scale} windows",
                                     "fold": f"C3: slice(OUT).foldNeighbors(degree, max neighbour), skewed "
                                             f"{'Zipf(1.1)' if a.stream == 'zipf' else 'R-MAT'} scale-{a.scale}",
-                                    "triangles": f"C4 shape: WindowTriangles over R-MAT scale-{a.scale} windows"}[a.workload],
+                                    "triangles": f"C4 shape: WindowTriangles over R-MAT scale-{a.scale} windows",
+                                    "cc": f"ConnectedComponents of R-MAT scale-{a.scale} windows"}[a.workload],
                        "scale": a.scale, "edges_per_window_per_gpu": E, "windows_cycled": a.windows,
-                       "direction": "ALL" if a.workload == "triangles" else "OUT",
-                       "op": {"reduce": "SUM", "fold": "DegreeMaxNeighbor", "triangles": "count"}[a.workload],
+                       "direction": "ALL" if a.workload in ("triangles", "cc") else "OUT",
+                       "op": {"reduce": "SUM", "fold": "DegreeMaxNeighbor", "triangles": "count",
+                              "cc": "union-find"}[a.workload],
                        "value_dtype": a.dtype, "vertices_out": U_avg, "sort_passes": t0s.sort_passes,
                        "key_bits": t0s.key_bits, "partials_after_fused_pass": int(partials),
-                       "pipeline": {0: "sort", 1: "bucket-onesweep", 2: "bucket-direct", 3: "triangles"}[t0s.path],
+                       "pipeline": {0: "sort", 1: "bucket-onesweep", 2: "bucket-direct", 3: "triangles",
+                                    4: "components"}[t0s.path],
                        "packed_records": bool(t0s.packed), "escaped_values": int(t0s.escapes),
-                       "parallelism": (f"hash keyBy over {world} GPU(s): per-rank partials (gs_window_reduce_partials) "
-                                       f"-> RCCL all-to-all -> gs_merge_partials" if dist else "1 GPU"), **checks},
+                       "parallelism": ("1 GPU" if not dist else
+                                       f"{world} replicas (per-window components, no exchange)" if a.workload == "cc" else
+                                       f"split window over {world} GPUs: summed degrees, oriented edges to owner(u), "
+                                       f"all-gathered out-lists, equal-work count shares (gs_tri_dist_*)"
+                                       if a.workload == "triangles" else
+                                       f"hash keyBy over {world} GPU(s): per-rank partials (gs_window_reduce_partials) "
+                                       f"-> RCCL all-to-all -> gs_merge_partials"), **checks},
             "roofline": roofline,
             "cpu_baseline": cpu,
             "kernels": {n: {"avg_ms": round(r["ms"], 4), "own_bytes": r["bytes"], "GB/s": round(r["GB/s"], 1),

@@ -60,7 +60,9 @@ class StageTimes:
     fused_last: bool
     path: int = 0          # 0: LSD sort + reduce-by-key; 1: bucket path, onesweep partition (pass_ms = passes,
                            # accumulate, merge, emit); 2: bucket path, direct partition (pass_ms = offset scans,
-                           # scatter, accumulate, merge, emit; keyinfo_ms = per-tile histogram)
+                           # scatter, accumulate, merge, emit; keyinfo_ms = per-tile histogram); 3: triangles
+                           # (ranks + keys + sort, unique, out-lists + transposed sort, light, heavy); 4: connected
+                           # components (compact IDs, union-find, labels)
     packed: bool = False   # path 2: 4-byte packed partition records (k_dp_scatter_pack)
     escapes: int = 0       # path 2, packed: values stored in full
 
@@ -120,7 +122,8 @@ class Engine:
     def stage_times(self) -> StageTimes:
         t = L.GsStageTimes()
         self._check(self._L.gs_last_stage_times(self.ctx, ctypes.byref(t)))
-        launched = 5 if t.path in (2, 3) else t.sort_passes + (3 if t.path == 1 else 1 if t.fused_last else 0)
+        launched = 5 if t.path in (2, 3) else 3 if t.path == 4 else \
+            t.sort_passes + (3 if t.path == 1 else 1 if t.fused_last else 0)
         return StageTimes(t.keyinfo_ms, t.sort_ms, t.reduce_ms, t.total_ms, t.sort_passes, t.key_bits, t.records,
                           t.vertices, list(t.pass_ms)[:launched], t.key_bytes, t.payload_bytes,
                           t.partials, bool(t.fused_last), t.path, bool(t.packed), t.escapes)
@@ -210,8 +213,11 @@ class Engine:
         U, RR = nv.value, nr.value
         return keys[:U], offs[:U + 1], nbrs[:RR], (None if vals is None else vals[:RR])
 
-    def candidates(self, src, dst):
-        """gs_window_candidates: GenerateCandidateEdges records (a, b, is_candidate)."""
+    def candidates(self, src, dst, strict: bool = False):
+        """gs_window_candidates: GenerateCandidateEdges records (a, b, is_candidate).
+        self.last_candidates_treeified: a neighbour set of this window would use a treeified JDK HashMap
+        bin (> 8 ids in one bin), whose iteration order is not modelled -- those vertices' records are
+        in plain-bin order.  strict=True raises GS_EUNSUPPORTED for such windows instead."""
         b, keep, dev = self._batch(src, dst, None)
         n_out = ctypes.c_uint64(0)
         probe = L.GsPairOut(None, None, None, 0, ctypes.pointer(n_out), L.GS_MEM_DEVICE if dev else L.GS_MEM_HOST, 0)
@@ -224,6 +230,10 @@ class Engine:
         out = L.GsPairOut(_ptr(a), _ptr(bb), _ptr(f), P, ctypes.pointer(n_out),
                           L.GS_MEM_DEVICE if dev else L.GS_MEM_HOST, 0)
         self._check(self._L.gs_window_candidates(self.ctx, ctypes.byref(b), ctypes.byref(out)))
+        self.last_candidates_treeified = bool(out.reserved)
+        if strict and out.reserved:
+            raise GsError(L.GS_EUNSUPPORTED, "candidates: a neighbour set uses a treeified HashMap bin "
+                                             "(JDK iteration order not modelled)")
         return a[:P], bb[:P], f[:P]
 
     def candidate_count(self, src, dst) -> int:

@@ -413,3 +413,21 @@ def test_count_candidates_ids_spanning_2_pow_32(engine, oracle):
     want = oracle.count_candidates(a, b, f)
     got = engine.count_candidates(*(torch.from_numpy(np.ascontiguousarray(x)).cuda() for x in (a, b, f)))
     assert (got[1], got[0], got[2], got[3]) == want
+
+
+def test_candidates_treeified_flag(engine, oracle):
+    """A neighbour set with > 8 ids in one JDK HashMap bin (ids k << 24): the oracle reports a
+    treeified bin; engine.candidates surfaces it (last_candidates_treeified) and strict=True refuses."""
+    from gelly_streaming_amd import GsError
+    k = np.arange(1, 201, dtype=np.int64)
+    s, d = np.zeros(200, np.int64), k << 24
+    assert oracle.window_candidates(s, d)[3]
+    engine.candidates(s, d)
+    assert engine.last_candidates_treeified
+    with pytest.raises(GsError):
+        engine.candidates(s, d, strict=True)
+    s2, d2 = np.zeros(200, np.int64), k << 20        # same sizes, plain bins
+    ra, rb, rf, tree = oracle.window_candidates(s2, d2)
+    ga, gb, gf = engine.candidates(s2, d2, strict=True)
+    assert not tree and not engine.last_candidates_treeified
+    assert np.array_equal(ga, ra) and np.array_equal(gb, rb) and np.array_equal(gf, rf)
