@@ -7,7 +7,9 @@
 //
 // gs_window_components computes that state on the GPU from the window's edges and the previous state
 // (vertex, label) rows, which join the window as edges vertex -- label:
-//   1. compact IDs: relabel_endpoints (sort of the 2(n + m) endpoints, order-preserving)
+//   1. ids: when they span <= 2^28 values, the ids minus a common base index a parent array directly
+//      (present vertices found after the union-find and compacted by a scan); else compact IDs from
+//      relabel_endpoints (sort of the 2(n + m) endpoints, order-preserving)
 //   2. union-find with the larger root always linked under the smaller one (atomicCAS on the root,
 //      find with pointer halving; parents only ever decrease, so stale reads only cost retries)
 //   3. full compression: every vertex's root = the smallest compact ID of its component = the
@@ -69,6 +71,69 @@ __global__ __launch_bounds__(256) void k_cc_concat(const int64_t* __restrict__ a
   }
 }
 
+// ---- direct ids (the window's ids span <= CC_DIRECT_BITS bits: no relabel) ---------------------------
+constexpr uint32_t CC_DIRECT_BITS = 28;
+
+// OR of (id ^ k0) over both columns, k0 = *k0p (the first id of the call)
+__global__ __launch_bounds__(256) void k_cc_mask(const int64_t* __restrict__ a, const int64_t* __restrict__ b, uint64_t n,
+                                                 const int64_t* __restrict__ k0p, unsigned long long* __restrict__ mask) {
+  const uint64_t k0 = (uint64_t)*k0p;
+  uint64_t m = 0;
+  for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256)
+    m |= ((uint64_t)a[i] ^ k0) | ((uint64_t)b[i] ^ k0);
+  m = wave_or(m);
+  if ((threadIdx.x & 63) == 0 && m) atomicOr(mask, (unsigned long long)m);
+}
+
+// unions over (a[e] ^ key_xor, b[e] ^ key_xor); a self-loop marks its vertex present (it has no link)
+__global__ __launch_bounds__(256) void k_cc_hook_ids(const int64_t* __restrict__ a, const int64_t* __restrict__ b,
+                                                     uint64_t n, uint64_t key_xor, uint32_t* parent,
+                                                     uint8_t* __restrict__ mark) {
+  for (uint64_t e = (uint64_t)blockIdx.x * 256 + threadIdx.x; e < n; e += (uint64_t)gridDim.x * 256) {
+    const uint32_t x = (uint32_t)((uint64_t)a[e] ^ key_xor), y = (uint32_t)((uint64_t)b[e] ^ key_xor);
+    if (x == y) {
+      mark[x] = 1;
+      continue;
+    }
+    uint32_t p = cc_find(parent, x), q = cc_find(parent, y);
+    while (p != q) {
+      const uint32_t hi = p > q ? p : q, lo = p > q ? q : p;
+      const uint32_t old = atomicCAS(&parent[hi], hi, lo);
+      if (old == hi) break;
+      p = cc_find(parent, old);
+      q = lo;
+    }
+  }
+}
+
+// full compression; a linked vertex is present and so is its root (every root of a linked tree is an
+// endpoint: links only ever join the roots of trees that hold endpoints)
+__global__ __launch_bounds__(256) void k_cc_compress(uint32_t* parent, uint32_t V, uint8_t* __restrict__ mark) {
+  for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < V; i += gridDim.x * 256u) {
+    uint32_t r = parent[i];
+    if (r == i) continue;
+    while (parent[r] != r) r = parent[r];
+    parent[i] = r;
+    mark[i] = 1;
+    mark[r] = 1;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_cc_flags(const uint8_t* __restrict__ mark, uint32_t V, uint64_t* __restrict__ f) {
+  for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < V; i += gridDim.x * 256u) f[i] = mark[i];
+}
+
+__global__ __launch_bounds__(256) void k_cc_emit_ids(const uint32_t* __restrict__ parent, const uint8_t* __restrict__ mark,
+                                                     const uint64_t* __restrict__ pos, uint32_t V, uint64_t key_xor,
+                                                     int64_t* __restrict__ keys, int64_t* __restrict__ labels) {
+  for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < V; i += gridDim.x * 256u) {
+    if (!mark[i]) continue;
+    const uint64_t at = pos[i];
+    keys[at] = (int64_t)(key_xor ^ i);
+    labels[at] = (int64_t)(key_xor ^ parent[i]);
+  }
+}
+
 }  // namespace gs
 
 using namespace gs;
@@ -104,7 +169,77 @@ gs_status gs_window_components(gs_ctx* c, const gs_edge_batch* b, const gs_parti
     GS_HIP(hipMemcpyAsync(Bc + n, prev->vals, m * 8, k, c->stream));
   }
   GS_HIP(hipGetLastError());
-  // 2. compact IDs
+  // 2a. ids spanning <= CC_DIRECT_BITS bits: union-find over the ids themselves (no relabel sort)
+  {
+    char* sm = c->small.as<char>();
+    unsigned long long* dmask = (unsigned long long*)(sm + SM_TABLE);
+    GS_HIP(hipMemsetAsync(dmask, 0, 8, c->stream));
+    const unsigned gN = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((N + 255) / 256, 8192));
+    hipLaunchKernelGGL(k_cc_mask, dim3(gN), dim3(256), 0, c->stream, A, Bc, N, A, dmask);
+    GS_HIP(hipGetLastError());
+    GS_HIP(hipMemcpyAsync(c->host_small + 12, dmask, 8, hipMemcpyDeviceToHost, c->stream));
+    GS_HIP(hipMemcpyAsync(c->host_small + 13, A, 8, hipMemcpyDeviceToHost, c->stream));
+    GS_TRY(host_wait(c));
+    const uint64_t mask = c->host_small[12], k0 = c->host_small[13];
+    const uint32_t B = mask ? 64 - __builtin_clzll(mask) : 1;
+    if (B <= CC_DIRECT_BITS) {
+      const uint64_t key_xor = k0 & ~((1ull << B) - 1);
+      const uint32_t V = 1u << B;
+      GS_TRY(ensure(c, c->cc[2], (size_t)V * 4));
+      GS_TRY(ensure(c, c->out_b, (size_t)V));
+      GS_TRY(ensure(c, c->rl[2], (size_t)V * 8 + 8));
+      GS_TRY(ensure(c, c->rl[3], (size_t)V * 8 + 8));
+      uint32_t* parent = c->cc[2].as<uint32_t>();
+      uint8_t* mark = c->out_b.as<uint8_t>();
+      const unsigned gv = (unsigned)std::min<uint64_t>((V + 255) / 256, 16384);
+      hipLaunchKernelGGL(k_cc_init, dim3(gv), dim3(256), 0, c->stream, parent, V);
+      GS_HIP(hipMemsetAsync(mark, 0, V, c->stream));
+      hipEventRecord(c->ev[1], c->stream);
+      hipLaunchKernelGGL(k_cc_hook_ids, dim3(gN), dim3(256), 0, c->stream, A, Bc, N, key_xor, parent, mark);
+      hipLaunchKernelGGL(k_cc_compress, dim3(gv), dim3(256), 0, c->stream, parent, V, mark);
+      GS_HIP(hipGetLastError());
+      hipEventRecord(c->ev[2], c->stream);
+      uint64_t* flags = c->rl[2].as<uint64_t>();
+      uint64_t* pos = c->rl[3].as<uint64_t>();
+      hipLaunchKernelGGL(k_cc_flags, dim3(gv), dim3(256), 0, c->stream, mark, V, flags);
+      GS_TRY(xscan(c, flags, V, pos));
+      GS_HIP(hipMemcpyAsync(c->host_small + 12, pos + V, 8, hipMemcpyDeviceToHost, c->stream));
+      GS_TRY(host_wait(c));
+      const uint64_t U = c->host_small[12];
+      *out->n_out = U;
+      c->last_U = U;
+      if (U > out->capacity) return set_error(c, GS_ECAPACITY, "components need %llu vertices", (unsigned long long)U);
+      const bool direct = out->mem == GS_MEM_DEVICE;
+      int64_t* kd = out->keys;
+      int64_t* vd = (int64_t*)out->vals;
+      if (!direct) {
+        GS_TRY(ensure(c, c->out_keys, U * 8 + 8));
+        GS_TRY(ensure(c, c->out_a, U * 8 + 8));
+        kd = c->out_keys.as<int64_t>();
+        vd = c->out_a.as<int64_t>();
+      }
+      hipLaunchKernelGGL(k_cc_emit_ids, dim3(gv), dim3(256), 0, c->stream, parent, mark, pos, V, key_xor, kd, vd);
+      GS_HIP(hipGetLastError());
+      hipEventRecord(c->ev[3], c->stream);
+      if (!direct) {
+        GS_TRY(deliver(c, out->keys, kd, U * 8, out->mem));
+        GS_TRY(deliver(c, out->vals, vd, U * 8, out->mem));
+      }
+      GS_TRY(host_wait(c));
+      gs_stage_times& t = c->times;
+      t = gs_stage_times{};
+      hipEventElapsedTime(&t.pass_ms[0], c->ev[0], c->ev[1]);   // staging + id range + init
+      hipEventElapsedTime(&t.pass_ms[1], c->ev[1], c->ev[2]);   // union-find + compression
+      hipEventElapsedTime(&t.pass_ms[2], c->ev[2], c->ev[3]);   // present vertices -> labels
+      hipEventElapsedTime(&t.total_ms, c->ev[0], c->ev[3]);
+      t.records = N;
+      t.vertices = U;
+      t.key_bits = B;
+      t.path = 4;
+      return GS_OK;
+    }
+  }
+  // 2b. compact IDs
   const int64_t *ca, *cb, *uniq;
   uint64_t U = 0;
   GS_TRY(relabel_endpoints(c, A, Bc, N, &ca, &cb, &uniq, &U));
