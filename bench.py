@@ -46,6 +46,9 @@ def parse():
     p.add_argument("--stream", default="rmat", choices=["rmat", "zipf"],
                    help="fold (C3): skewed R-MAT (default) or the Zipf(1.1) source stream")
     p.add_argument("--staging", default="direct", choices=["direct", "pinned"], help="e2e: window operator staging")
+    p.add_argument("--e2e-kind", default="reduce", choices=["reduce", "triangles"],
+                   help="e2e: reduceOnEdges(SUM) on C2 windows, or WindowTriangles on C5-size windows "
+                        "(--windows-edges edges of an R-MAT --scale stream per 1000 ms window)")
     p.add_argument("--no-pack", action="store_true",
                    help="ablation: integer SUM keeps 8-byte partitioned values instead of 4-byte packed records")
     p.add_argument("--sort-only", action="store_true",
@@ -432,7 +435,7 @@ def parse_main(a):
 
 def e2e_main(a):
     """End-to-end windows (BASELINE.md "end-to-end incl. pinned H2D/D2H"): the C2 stream
-    (R-MAT scale-24 windows of 2^28 edges, Long values) arrives on the HOST with ascending event timestamps
+    (C2: R-MAT scale-24 windows of 2^28 edges with Long values; C5 with --e2e-kind triangles: --windows-edges per window) arrives on the HOST with ascending event timestamps
     (window k: ts in [k*1000, k*1000 + 1000)) and goes through the window-buffer operator (gs_stream_*):
     host columns -> pinned window buffers -> the watermark fires the window -> H2D on the operator's copy
     stream (overlapping the previous window's kernels) -> reduceOnEdges(SUM) -> D2H of the per-vertex
@@ -443,22 +446,32 @@ def e2e_main(a):
     from gelly_streaming_amd import _lib as L
     from gelly_streaming_amd.window_operator import WindowOperator
     eng = pkg.Engine(0)
-    E = a.edge_factor << a.scale
+    tri = a.e2e_kind == "triangles"
+    E = int(a.windows_edges) if tri else a.edge_factor << a.scale
     ndist = 2                       # distinct host windows, cycled
     host = []
     for w in range(ndist):
-        s_, d_ = eng.generate_rmat(a.scale, E, a.seed, first_edge=w * E)
-        v_ = eng.generate_values(E, a.seed, 1, first_edge=w * E)
-        host.append((s_.cpu().numpy(), d_.cpu().numpy(), v_.cpu().numpy()))
-        del s_, d_, v_
+        if tri:   # C5: a continuous R-MAT stream cut into windows of E edges (self-loops removed)
+            s_, d_ = eng.generate_rmat(a.scale, E, 0x5EED05, no_self_loops=True, first_edge=w * E)
+            host.append((s_.cpu().numpy(), d_.cpu().numpy(), None))
+        else:
+            s_, d_ = eng.generate_rmat(a.scale, E, a.seed, first_edge=w * E)
+            v_ = eng.generate_values(E, a.seed, 1, first_edge=w * E)
+            host.append((s_.cpu().numpy(), d_.cpu().numpy(), v_.cpu().numpy()))
+            del v_
+        del s_, d_
     torch.cuda.empty_cache()
     ts0 = (np.arange(E, dtype=np.int64) * 1000) // E
     total = a.warmup + a.steps
     tss = [ts0 + k * 1000 for k in range(total)]   # window k's event times (prepared before timing)
     lat, results = [], []
     staging = L.GS_STAGE_DIRECT if a.staging == "direct" else L.GS_STAGE_PINNED
-    op = WindowOperator(eng, 1000, L.GS_STREAM_REDUCE, 1, 0, np.int64, L.GS_WATERMARK_ASCENDING, max_window_edges=E,
-                        staging=staging)
+    if tri:
+        op = WindowOperator(eng, 1000, L.GS_STREAM_TRIANGLES, 2, 0, None, L.GS_WATERMARK_ASCENDING, max_window_edges=E,
+                            staging=staging)
+    else:
+        op = WindowOperator(eng, 1000, L.GS_STREAM_REDUCE, 1, 0, np.int64, L.GS_WATERMARK_ASCENDING, max_window_edges=E,
+                            staging=staging)
     t0 = None
     for k in range(total + 1):
         if k == a.warmup:
@@ -480,25 +493,29 @@ def e2e_main(a):
     timed = [r for r in results if r.start >= a.warmup * 1000]
     assert len(timed) == a.steps and all(r.edges == E for r in timed)
     lat = [r.latency_ms for r in timed]
-    if a.check:
+    if a.check and not tri:
         for r in timed[:2]:
             v = host[(r.start // 1000) % ndist][2]
             assert int(r.columns[1].sum()) == int(v.sum()), "e2e window: sum of sums != sum of values"
     op.close()
     ms = elapsed / a.steps * 1e3
-    h2d_bytes = 24 * E
+    h2d_bytes = (16 if tri else 24) * E
     print(json.dumps({
         "metric": METRIC, "value": E * a.steps / elapsed, "unit": "edges/s", "n_gpus": 1, "steps": a.steps,
         "warmup": a.warmup, "ms_per_step": ms, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-        "dtype": "int64", "data": "synthetic R-MAT scale-24 windows generated on device, copied to host memory "
+        "dtype": "int64", "data": f"synthetic R-MAT scale-{a.scale} windows generated on device, copied to host memory "
                                   "before timing; ascending event timestamps",
-        "config": {"workload": f"end-to-end C2: host records -> gs_stream window operator ({a.staging} staging: "
-                               + ("pinned window buffers, H2D at firing" if a.staging == "pinned" else
-                                  "each append copied straight to HBM") + ", reduceOnEdges(SUM) OUT, D2H of results)",
+        "config": {"workload": (f"end-to-end C5 shape: host records of an R-MAT scale-{a.scale} stream, {E} edges per "
+                                f"1000 ms window -> gs_stream window operator ({a.staging} staging) -> WindowTriangles"
+                                if tri else
+                                f"end-to-end C2: host records -> gs_stream window operator ({a.staging} staging: "
+                                + ("pinned window buffers, H2D at firing" if a.staging == "pinned" else
+                                   "each append copied straight to HBM") + ", reduceOnEdges(SUM) OUT, D2H of results)"),
                    "edges_per_window": E, "windows_timed": a.steps,
                    "latency_ms_p50": float(np.percentile(lat, 50)), "latency_ms_p99": float(np.percentile(lat, 99)),
                    "h2d_bytes_per_window": h2d_bytes, "h2d_GBps_effective": h2d_bytes / (ms * 1e-3) / 1e9,
-                   "vertices_out_per_window": int(timed[-1].columns[0].size), "parallelism": "1 GPU"},
+                   "vertices_out_per_window": None if tri else int(timed[-1].columns[0].size),
+                   "triangles_last_window": int(timed[-1].columns[0]) if tri else None, "parallelism": "1 GPU"},
         "roofline": None, "cpu_baseline": None}), flush=True)
     eng.close()
 

@@ -12,8 +12,9 @@
 //   ALL sort with record index -> CSR (arrival order) -> composite (vertex, neighbour) sort ->
 //   distinct pairs with first arrival (segmented MIN) -> per-vertex k -> order key
 //   (bucket, first arrival) -> sort, then stable sort by vertex -> ids per vertex in HashSet order.
-// Bins that would be treeified (>= 9 entries at capacity >= 64) have a different JDK order; such
-// windows are flagged (gs_pair_out.reserved = 1, "order unpinned").
+// A vertex whose insertion sequence ever fills a bin to 9 nodes leaves that model (treeifyBin: a
+// resize below capacity 64, a red-black tree bin above); those vertices are found exactly and re-run
+// through a per-vertex JDK HashMap simulation (gs_pair_out.reserved reports which case occurred).
 #include "gs_ops.hpp"
 
 namespace gs {
@@ -177,25 +178,12 @@ __global__ __launch_bounds__(256) void k_hs_vertex_of(const uint32_t* __restrict
   }
 }
 
-// ids in HashSet order (original IDs) + treeification check
+// ids in plain-bin HashSet order (original IDs)
 __global__ __launch_bounds__(256) void k_hs_ids(const uint32_t* __restrict__ ord, const uint64_t* __restrict__ dkey,
                                                 uint32_t M, uint32_t B, const int64_t* __restrict__ vkeys,
-                                                const uint64_t* __restrict__ doff,
-                                                uint32_t U, int64_t* __restrict__ ids, uint32_t* __restrict__ treeified) {
+                                                int64_t* __restrict__ ids) {
   const uint64_t mask = (B >= 64) ? ~0ull : ((1ull << B) - 1);
-  for (uint32_t q = blockIdx.x * 256u + threadIdx.x; q < M; q += gridDim.x * 256u) {
-    const uint64_t k = dkey[ord[q]];
-    const int64_t x = vkeys[k & mask];
-    ids[q] = x;
-    const uint32_t u = (uint32_t)(k >> B);
-    const uint64_t end = doff[u + 1];
-    const uint64_t cap = hs_capacity(end - doff[u]);
-    if (cap >= 64 && q + 8 < end) {
-      const uint64_t k8 = dkey[ord[q + 8]];
-      const int64_t x8 = vkeys[k8 & mask];
-      if (hs_bucket(x, cap) == hs_bucket(x8, cap)) atomicOr(treeified, 1u);
-    }
-  }
+  for (uint32_t q = blockIdx.x * 256u + threadIdx.x; q < M; q += gridDim.x * 256u) ids[q] = vkeys[dkey[ord[q]] & mask];
 }
 
 // gt[q] = ids[q] > v(u)   (signed Long order, WindowTriangles.java:108)
@@ -286,6 +274,365 @@ __global__ __launch_bounds__(256) void k_hs_selfpairs(const int64_t* __restrict_
   if ((threadIdx.x & 63) == 0 && t) atomicAdd(S, (unsigned long long)t);
 }
 
+// ---- vertices whose JDK HashMap leaves the plain-bin model ------------------------------------
+// Until some bin reaches 9 nodes the JDK map is the plain model at every step: stage capacity C
+// (16, 32, ..., final) holds the first min(k, 3C/4 + 1) distinct ids (the insert that crosses the
+// threshold lands before the resize), buckets only gain entries inside a stage, and resize splits keep
+// insertion order.  So a vertex is "complex" iff for some stage C a bucket of (hash & (C-1)) over its
+// first n_C arrivals reaches 9 -- one counter per (vertex, stage, bucket), filled with atomics.
+// Complex vertices are then simulated exactly (k_hs_jdk).
+__global__ __launch_bounds__(256) void k_hs_first(const uint32_t* __restrict__ dfirst, uint32_t M,
+                                                  uint64_t* __restrict__ F) {
+  for (uint32_t m = blockIdx.x * 256u + threadIdx.x; m < M; m += gridDim.x * 256u) F[dfirst[m]] = 1;
+}
+// counter space of a vertex: stages 16..cap hold 16+32+..+cap = 2cap - 16 buckets (k >= 9 only)
+__global__ __launch_bounds__(256) void k_hs_csize(const uint64_t* __restrict__ doff, uint32_t U,
+                                                  uint64_t* __restrict__ csz) {
+  for (uint32_t u = blockIdx.x * 256u + threadIdx.x; u < U; u += gridDim.x * 256u) {
+    const uint64_t k = doff[u + 1] - doff[u];
+    csz[u] = k >= 9 ? 2 * hs_capacity(k) - 16 : 0;
+  }
+}
+// arrival rank i of each distinct entry (FX = exclusive scan of the first-arrival flags), the
+// arrival-ordered ids (arr), and the per-stage bucket counters; a counter reaching 9 marks the vertex
+__global__ __launch_bounds__(256) void k_hs_detect(const uint64_t* __restrict__ dkey, const uint32_t* __restrict__ dfirst,
+                                                   uint32_t M, uint32_t B, const int64_t* __restrict__ vkeys,
+                                                   const uint64_t* __restrict__ doff, const uint64_t* __restrict__ FX,
+                                                   const uint64_t* __restrict__ cbase, uint32_t* __restrict__ cnt,
+                                                   int64_t* __restrict__ arr, uint32_t* __restrict__ cplx) {
+  const uint64_t mask = (B >= 64) ? ~0ull : ((1ull << B) - 1);
+  for (uint32_t m = blockIdx.x * 256u + threadIdx.x; m < M; m += gridDim.x * 256u) {
+    const uint64_t key = dkey[m];
+    const uint32_t u = (uint32_t)(key >> B);
+    const uint64_t d0 = doff[u], k = doff[u + 1] - d0;
+    if (k < 9) continue;
+    const int64_t x = vkeys[key & mask];
+    const uint64_t i = FX[dfirst[m]] - d0;
+    arr[d0 + i] = x;
+    const uint32_t h0 = (uint32_t)((uint64_t)x ^ ((uint64_t)x >> 32)), h = h0 ^ (h0 >> 16);
+    const uint64_t capf = hs_capacity(k), base = cbase[u];
+    for (uint64_t C = 16; C <= capf; C <<= 1) {
+      const uint64_t nC = C == capf ? k : (3 * C / 4 + 1);
+      if (i >= nC) continue;
+      if (atomicAdd(&cnt[base + C - 16 + (h & (uint32_t)(C - 1))], 1u) == 8u) cplx[u] = 1;
+    }
+  }
+}
+// compact list of complex vertices (+ table sizes for their exact maps)
+__global__ __launch_bounds__(256) void k_hs_clist(const uint32_t* __restrict__ cplx, uint32_t U,
+                                                  const uint64_t* __restrict__ doff, uint32_t* __restrict__ nc,
+                                                  uint32_t* __restrict__ list, uint64_t* __restrict__ tsz) {
+  for (uint32_t u = blockIdx.x * 256u + threadIdx.x; u < U; u += gridDim.x * 256u) {
+    if (!cplx[u]) continue;
+    const uint32_t s = atomicAdd(nc, 1u);
+    list[s] = u;
+    tsz[s] = max(hs_capacity(doff[u + 1] - doff[u]), (uint64_t)64);   // early resizes stop at 64
+  }
+}
+
+// One exact java.util.HashMap<Long> per complex vertex (JDK 8+ putVal / resize / treeifyBin /
+// TreeNode.treeify / putTreeVal / balanceInsertion / rotations / moveRootToFront / split / untreeify;
+// the same restatement as the oracle's hashset_order).  Nodes are indexed 0..k-1 in arrival order;
+// the table is resized in place (old bin j feeds new bins j and j + oldCap only).
+struct JNode {
+  uint32_t hash;
+  int32_t next, prev, parent, left, right;
+  uint8_t red, tree, pad[2];
+};
+struct JMap {
+  JNode* n;
+  const int64_t* key;
+  int32_t* tab;
+  uint32_t cap, thr, size, flags;
+};
+__device__ int j_dir(const JMap& m, int32_t p, uint32_t h, int64_t k) {
+  if (m.n[p].hash > h) return -1;
+  if (m.n[p].hash < h) return 1;
+  return k < m.key[p] ? -1 : 1;   // Long.compareTo; keys are distinct
+}
+__device__ int32_t j_rotl(JNode* n, int32_t root, int32_t p) {
+  int32_t r, pp, rl;
+  if (p >= 0 && (r = n[p].right) >= 0) {
+    if ((rl = n[p].right = n[r].left) >= 0) n[rl].parent = p;
+    if ((pp = n[r].parent = n[p].parent) < 0) {
+      root = r;
+      n[r].red = 0;
+    } else if (n[pp].left == p) {
+      n[pp].left = r;
+    } else {
+      n[pp].right = r;
+    }
+    n[r].left = p;
+    n[p].parent = r;
+  }
+  return root;
+}
+__device__ int32_t j_rotr(JNode* n, int32_t root, int32_t p) {
+  int32_t l, pp, lr;
+  if (p >= 0 && (l = n[p].left) >= 0) {
+    if ((lr = n[p].left = n[l].right) >= 0) n[lr].parent = p;
+    if ((pp = n[l].parent = n[p].parent) < 0) {
+      root = l;
+      n[l].red = 0;
+    } else if (n[pp].right == p) {
+      n[pp].right = l;
+    } else {
+      n[pp].left = l;
+    }
+    n[l].right = p;
+    n[p].parent = l;
+  }
+  return root;
+}
+__device__ int32_t j_balance(JNode* n, int32_t root, int32_t x) {
+  n[x].red = 1;
+  for (;;) {
+    int32_t xp = n[x].parent, xpp, xppl, xppr;
+    if (xp < 0) {
+      n[x].red = 0;
+      return x;
+    }
+    if (!n[xp].red || (xpp = n[xp].parent) < 0) return root;
+    if (xp == (xppl = n[xpp].left)) {
+      if ((xppr = n[xpp].right) >= 0 && n[xppr].red) {
+        n[xppr].red = 0;
+        n[xp].red = 0;
+        n[xpp].red = 1;
+        x = xpp;
+      } else {
+        if (x == n[xp].right) {
+          root = j_rotl(n, root, x = xp);
+          xpp = (xp = n[x].parent) < 0 ? -1 : n[xp].parent;
+        }
+        if (xp >= 0) {
+          n[xp].red = 0;
+          if (xpp >= 0) {
+            n[xpp].red = 1;
+            root = j_rotr(n, root, xpp);
+          }
+        }
+      }
+    } else {
+      if (xppl >= 0 && n[xppl].red) {
+        n[xppl].red = 0;
+        n[xp].red = 0;
+        n[xpp].red = 1;
+        x = xpp;
+      } else {
+        if (x == n[xp].left) {
+          root = j_rotr(n, root, x = xp);
+          xpp = (xp = n[x].parent) < 0 ? -1 : n[xp].parent;
+        }
+        if (xp >= 0) {
+          n[xp].red = 0;
+          if (xpp >= 0) {
+            n[xpp].red = 1;
+            root = j_rotl(n, root, xpp);
+          }
+        }
+      }
+    }
+  }
+}
+__device__ void j_root_front(JMap& m, int32_t root) {
+  JNode* n = m.n;
+  const uint32_t idx = n[root].hash & (m.cap - 1);
+  const int32_t first = m.tab[idx];
+  if (root != first) {
+    m.tab[idx] = root;
+    const int32_t rp = n[root].prev, rn = n[root].next;
+    if (rn >= 0) n[rn].prev = rp;
+    if (rp >= 0) n[rp].next = rn;
+    if (first >= 0) n[first].prev = root;
+    n[root].next = first;
+    n[root].prev = -1;
+  }
+}
+__device__ void j_treeify(JMap& m, int32_t hd) {
+  JNode* n = m.n;
+  int32_t root = -1;
+  for (int32_t x = hd, nx; x >= 0; x = nx) {
+    nx = n[x].next;
+    n[x].left = n[x].right = -1;
+    if (root < 0) {
+      n[x].parent = -1;
+      n[x].red = 0;
+      root = x;
+      continue;
+    }
+    for (int32_t p = root;;) {
+      const int dir = j_dir(m, p, n[x].hash, m.key[x]);
+      const int32_t xp = p;
+      if ((p = dir <= 0 ? n[p].left : n[p].right) < 0) {
+        n[x].parent = xp;
+        if (dir <= 0) n[xp].left = x;
+        else n[xp].right = x;
+        root = j_balance(n, root, x);
+        break;
+      }
+    }
+  }
+  j_root_front(m, root);
+}
+__device__ void j_untreeify(JNode* n, int32_t hd) {
+  for (int32_t x = hd; x >= 0; x = n[x].next) {
+    n[x].tree = 0;
+    n[x].left = n[x].right = n[x].parent = -1;
+  }
+}
+// m.cap is already the new capacity; old bin `index` splits into index / index + bit
+__device__ void j_split(JMap& m, int32_t b, uint32_t index, uint32_t bit) {
+  JNode* n = m.n;
+  int32_t loH = -1, loT = -1, hiH = -1, hiT = -1;
+  uint32_t lc = 0, hc = 0;
+  for (int32_t e = b, nx; e >= 0; e = nx) {
+    nx = n[e].next;
+    n[e].next = -1;
+    if ((n[e].hash & bit) == 0) {
+      if ((n[e].prev = loT) < 0) loH = e;
+      else n[loT].next = e;
+      loT = e;
+      ++lc;
+    } else {
+      if ((n[e].prev = hiT) < 0) hiH = e;
+      else n[hiT].next = e;
+      hiT = e;
+      ++hc;
+    }
+  }
+  if (loH >= 0) {
+    m.tab[index] = loH;
+    if (lc <= 6) j_untreeify(n, loH);
+    else if (hiH >= 0) j_treeify(m, loH);
+  }
+  if (hiH >= 0) {
+    m.tab[index + bit] = hiH;
+    if (hc <= 6) j_untreeify(n, hiH);
+    else if (loH >= 0) j_treeify(m, hiH);
+  }
+}
+__device__ void j_resize(JMap& m) {
+  const uint32_t ocap = m.cap, ncap = ocap ? ocap * 2 : 16;
+  JNode* n = m.n;
+  for (uint32_t i = ocap; i < ncap; ++i) m.tab[i] = -1;
+  m.cap = ncap;
+  for (uint32_t j = 0; j < ocap; ++j) {
+    const int32_t e = m.tab[j];
+    if (e < 0) continue;
+    m.tab[j] = -1;
+    if (n[e].next < 0) {
+      m.tab[n[e].hash & (ncap - 1)] = e;
+    } else if (n[e].tree) {
+      j_split(m, e, j, ocap);
+    } else {
+      int32_t loH = -1, loT = -1, hiH = -1, hiT = -1;
+      for (int32_t x = e, nx; x >= 0; x = nx) {
+        nx = n[x].next;
+        if ((n[x].hash & ocap) == 0) {
+          if (loT < 0) loH = x;
+          else n[loT].next = x;
+          loT = x;
+        } else {
+          if (hiT < 0) hiH = x;
+          else n[hiT].next = x;
+          hiT = x;
+        }
+      }
+      if (loT >= 0) {
+        n[loT].next = -1;
+        m.tab[j] = loH;
+      }
+      if (hiT >= 0) {
+        n[hiT].next = -1;
+        m.tab[j + ocap] = hiH;
+      }
+    }
+  }
+  m.thr = ncap / 4 * 3;
+}
+__device__ void j_treeify_bin(JMap& m, uint32_t hash) {
+  if (m.cap < 64) {   // MIN_TREEIFY_CAPACITY: resize instead
+    m.flags |= 2;
+    j_resize(m);
+    return;
+  }
+  JNode* n = m.n;
+  const int32_t hd = m.tab[hash & (m.cap - 1)];
+  int32_t tl = -1;
+  for (int32_t e = hd; e >= 0; e = n[e].next) {
+    n[e].tree = 1;
+    n[e].prev = tl;
+    tl = e;
+  }
+  m.flags |= 1;
+  j_treeify(m, hd);
+}
+__device__ void j_put(JMap& m, int32_t x) {
+  JNode* n = m.n;
+  if (m.cap == 0) j_resize(m);
+  const uint32_t h = n[x].hash, i = h & (m.cap - 1);
+  n[x].next = n[x].prev = n[x].parent = n[x].left = n[x].right = -1;
+  n[x].red = 0;
+  n[x].tree = 0;
+  int32_t p = m.tab[i];
+  if (p < 0) {
+    m.tab[i] = x;
+  } else if (n[p].tree) {   // putTreeVal from the bin's root
+    int32_t root = p;
+    while (n[root].parent >= 0) root = n[root].parent;
+    n[x].tree = 1;
+    for (int32_t q = root;;) {
+      const int dir = j_dir(m, q, h, m.key[x]);
+      const int32_t xp = q;
+      if ((q = dir <= 0 ? n[q].left : n[q].right) < 0) {
+        const int32_t xpn = n[xp].next;
+        n[x].next = xpn;
+        if (dir <= 0) n[xp].left = x;
+        else n[xp].right = x;
+        n[xp].next = x;
+        n[x].parent = n[x].prev = xp;
+        if (xpn >= 0) n[xpn].prev = x;
+        j_root_front(m, j_balance(n, root, x));
+        break;
+      }
+    }
+  } else {
+    for (int bin = 0;; ++bin) {
+      const int32_t e = n[p].next;
+      if (e < 0) {
+        n[p].next = x;
+        if (bin >= 7) j_treeify_bin(m, h);   // TREEIFY_THRESHOLD - 1
+        break;
+      }
+      p = e;
+    }
+  }
+  if (++m.size > m.thr) j_resize(m);
+}
+// thread per complex vertex: insert its ids in arrival order, then write them in iteration order
+__global__ __launch_bounds__(64) void k_hs_jdk(const uint32_t* __restrict__ list, const uint32_t* __restrict__ nc,
+                                               const uint64_t* __restrict__ doff, const int64_t* __restrict__ arr,
+                                               const uint64_t* __restrict__ tbase, JNode* __restrict__ nodes,
+                                               int32_t* __restrict__ tabs, int64_t* __restrict__ ids,
+                                               uint32_t* __restrict__ flags) {
+  const uint32_t count = *nc;
+  for (uint32_t s = blockIdx.x * 64u + threadIdx.x; s < count; s += gridDim.x * 64u) {
+    const uint32_t u = list[s];
+    const uint64_t d0 = doff[u], k = doff[u + 1] - d0;
+    JMap m{nodes + d0, arr + d0, tabs + tbase[s], 0, 0, 0, 0};
+    for (uint32_t j = 0; j < k; ++j) {
+      const int64_t x = m.key[j];
+      const uint32_t h0 = (uint32_t)((uint64_t)x ^ ((uint64_t)x >> 32));
+      m.n[j].hash = h0 ^ (h0 >> 16);
+      j_put(m, (int32_t)j);
+    }
+    uint64_t o = d0;
+    for (uint32_t b = 0; b < m.cap; ++b)
+      for (int32_t e = m.tab[b]; e >= 0; e = m.n[e].next) ids[o++] = m.key[e];
+    if (m.flags) atomicOr(flags, m.flags);
+  }
+}
+
 }  // namespace gs
 
 using namespace gs;
@@ -293,7 +640,9 @@ using namespace gs;
 namespace gs {
 
 enum { HS_VKEYS, HS_OFF, HS_NBR, HS_USEG, HS_COMP, HS_PIDX, HS_DKEY, HS_DFIRST, HS_DOFF, HS_OKEY, HS_OMID,
-       HS_UKEY, HS_ORD, HS_IDS, HS_G, HS_GX, HS_L, HS_LS, HS_TILES, HS_COUNT };
+       HS_UKEY, HS_ORD, HS_IDS, HS_G, HS_GX, HS_L, HS_LS, HS_TILES, HS_F, HS_FX, HS_CSZ, HS_CBASE, HS_CNT, HS_CPLX,
+       HS_CLIST, HS_TSZ, HS_TBASE, HS_ARR, HS_NODES, HS_TABS, HS_COUNT };
+static_assert(HS_COUNT <= 32, "gs_ctx::hs");
 
 gs_status xscan(gs_ctx* c, const uint64_t* in, uint64_t n, uint64_t* out) {
   const uint32_t tiles = (uint32_t)std::max<uint64_t>(1, (n + XS_TILE - 1) / XS_TILE);
@@ -310,8 +659,72 @@ static unsigned g256(uint64_t n) { return (unsigned)std::max<uint64_t>(1, std::m
 // Distinct neighbour sets of every vertex of an ALL window, in HashSet order.  Results in c->hs[...]:
 // HS_VKEYS[U] vertex IDs, HS_OFF[U+1] record offsets, HS_NBR[R] neighbours (arrival order),
 // HS_USEG[R] vertex of each record, HS_DOFF[U+1] distinct offsets, HS_IDS[M] ids in HashSet order.
+// Vertices that leave the plain-bin model get their exact JDK order (k_hs_detect, k_hs_jdk).
+// *jdk_flags: bit 0 = some bin was treeified, bit 1 = some bin forced a resize below capacity 64.
+static gs_status hashset_exact(gs_ctx* c, uint64_t R, uint64_t U, uint64_t M, uint32_t B, uint32_t* jdk_flags) {
+  char* sm = c->small.as<char>();
+  uint32_t* d_hs = (uint32_t*)(sm + SM_HS);   // [0] complex vertices, [1] JDK flags
+  GS_HIP(hipMemsetAsync(d_hs, 0, 8, c->stream));
+  // arrival rank of every distinct entry: scan of the first-arrival flags over record positions
+  GS_TRY(ensure(c, c->hs[HS_F], (R + 1) * 8));
+  GS_TRY(ensure(c, c->hs[HS_FX], (R + 1) * 8));
+  GS_HIP(hipMemsetAsync(c->hs[HS_F].p, 0, R * 8, c->stream));
+  hipLaunchKernelGGL(k_hs_first, dim3(g256(M)), dim3(256), 0, c->stream, c->hs[HS_DFIRST].as<uint32_t>(), (uint32_t)M,
+                     c->hs[HS_F].as<uint64_t>());
+  GS_TRY(xscan(c, c->hs[HS_F].as<uint64_t>(), R, c->hs[HS_FX].as<uint64_t>()));
+  GS_TRY(ensure(c, c->hs[HS_CSZ], (U + 1) * 8));
+  GS_TRY(ensure(c, c->hs[HS_CBASE], (U + 1) * 8));
+  hipLaunchKernelGGL(k_hs_csize, dim3(g256(U)), dim3(256), 0, c->stream, c->hs[HS_DOFF].as<uint64_t>(), (uint32_t)U,
+                     c->hs[HS_CSZ].as<uint64_t>());
+  GS_TRY(xscan(c, c->hs[HS_CSZ].as<uint64_t>(), U, c->hs[HS_CBASE].as<uint64_t>()));
+  c->host_small[6] = 0;
+  GS_HIP(hipMemcpyAsync(c->host_small + 6, c->hs[HS_CBASE].as<uint64_t>() + U, 8, hipMemcpyDeviceToHost, c->stream));
+  GS_TRY(host_wait(c));
+  const uint64_t CT = c->host_small[6];
+  *jdk_flags = 0;
+  if (CT == 0) return GS_OK;   // no vertex with 9 or more distinct neighbours
+  GS_TRY(ensure(c, c->hs[HS_CNT], CT * 4));
+  GS_TRY(ensure(c, c->hs[HS_CPLX], U * 4));
+  GS_TRY(ensure(c, c->hs[HS_ARR], M * 8));
+  GS_HIP(hipMemsetAsync(c->hs[HS_CNT].p, 0, CT * 4, c->stream));
+  GS_HIP(hipMemsetAsync(c->hs[HS_CPLX].p, 0, U * 4, c->stream));
+  hipLaunchKernelGGL(k_hs_detect, dim3(g256(M)), dim3(256), 0, c->stream, c->hs[HS_DKEY].as<uint64_t>(),
+                     c->hs[HS_DFIRST].as<uint32_t>(), (uint32_t)M, B, c->hs[HS_VKEYS].as<int64_t>(),
+                     c->hs[HS_DOFF].as<uint64_t>(), c->hs[HS_FX].as<uint64_t>(), c->hs[HS_CBASE].as<uint64_t>(),
+                     c->hs[HS_CNT].as<uint32_t>(), c->hs[HS_ARR].as<int64_t>(), c->hs[HS_CPLX].as<uint32_t>());
+  GS_TRY(ensure(c, c->hs[HS_CLIST], U * 4));
+  GS_TRY(ensure(c, c->hs[HS_TSZ], (U + 1) * 8));
+  GS_TRY(ensure(c, c->hs[HS_TBASE], (U + 1) * 8));
+  hipLaunchKernelGGL(k_hs_clist, dim3(g256(U)), dim3(256), 0, c->stream, c->hs[HS_CPLX].as<uint32_t>(), (uint32_t)U,
+                     c->hs[HS_DOFF].as<uint64_t>(), d_hs, c->hs[HS_CLIST].as<uint32_t>(),
+                     c->hs[HS_TSZ].as<uint64_t>());
+  GS_HIP(hipGetLastError());
+  c->host_small[6] = 0;
+  GS_HIP(hipMemcpyAsync(c->host_small + 6, d_hs, 4, hipMemcpyDeviceToHost, c->stream));
+  GS_TRY(host_wait(c));
+  const uint64_t nc = c->host_small[6] & 0xffffffffull;
+  if (nc == 0) return GS_OK;
+  GS_TRY(xscan(c, c->hs[HS_TSZ].as<uint64_t>(), nc, c->hs[HS_TBASE].as<uint64_t>()));
+  c->host_small[6] = 0;
+  GS_HIP(hipMemcpyAsync(c->host_small + 6, c->hs[HS_TBASE].as<uint64_t>() + nc, 8, hipMemcpyDeviceToHost, c->stream));
+  GS_TRY(host_wait(c));
+  const uint64_t T = c->host_small[6];
+  GS_TRY(ensure(c, c->hs[HS_NODES], M * sizeof(JNode)));
+  GS_TRY(ensure(c, c->hs[HS_TABS], T * 4));
+  const unsigned grid = (unsigned)std::min<uint64_t>((nc + 63) / 64, 4096);
+  hipLaunchKernelGGL(k_hs_jdk, dim3(grid), dim3(64), 0, c->stream, c->hs[HS_CLIST].as<uint32_t>(), d_hs,
+                     c->hs[HS_DOFF].as<uint64_t>(), c->hs[HS_ARR].as<int64_t>(), c->hs[HS_TBASE].as<uint64_t>(),
+                     c->hs[HS_NODES].as<JNode>(), c->hs[HS_TABS].as<int32_t>(), c->hs[HS_IDS].as<int64_t>(), d_hs + 1);
+  GS_HIP(hipGetLastError());
+  c->host_small[6] = 0;
+  GS_HIP(hipMemcpyAsync(c->host_small + 6, d_hs, 8, hipMemcpyDeviceToHost, c->stream));
+  GS_TRY(host_wait(c));
+  *jdk_flags = (uint32_t)(c->host_small[6] >> 32);
+  return GS_OK;
+}
+
 gs_status hashset_order(gs_ctx* c, const int64_t* src, const int64_t* dst, uint64_t n, uint32_t* U_out,
-                        uint32_t* M_out, uint64_t* key_xor_out, bool* treeified) {
+                        uint32_t* M_out, uint64_t* key_xor_out, uint32_t* jdk_flags) {
   char* sm = c->small.as<char>();
   const uint64_t R = 2 * n;
   Sorted s;
@@ -375,16 +788,11 @@ gs_status hashset_order(gs_ctx* c, const int64_t* src, const int64_t* dst, uint6
   Sorted sb;
   GS_TRY(sort_buffer(c, c->hs[HS_UKEY].as<uint64_t>(), c->hs[HS_OMID].as<uint32_t>(), M, &sb));
   GS_TRY(ensure(c, c->hs[HS_IDS], M * 8));
-  uint32_t* d_tree = (uint32_t*)(sm + SM_TIMEOUT) + 1;   // spare word next to the timeout flag
-  GS_HIP(hipMemsetAsync(d_tree, 0, 4, c->stream));
   hipLaunchKernelGGL(k_hs_ids, dim3(g256(M)), dim3(256), 0, c->stream, (const uint32_t*)sb.vals,
                      c->hs[HS_DKEY].as<uint64_t>(), (uint32_t)M, B, c->hs[HS_VKEYS].as<int64_t>(),
-                     c->hs[HS_DOFF].as<uint64_t>(),
-                     (uint32_t)U, c->hs[HS_IDS].as<int64_t>(), d_tree);
+                     c->hs[HS_IDS].as<int64_t>());
   GS_HIP(hipGetLastError());
-  GS_HIP(hipMemcpyAsync(c->host_small + 6, sm + SM_TIMEOUT, 8, hipMemcpyDeviceToHost, c->stream));
-  GS_TRY(host_wait(c));
-  *treeified = (c->host_small[6] >> 32) != 0;
+  GS_TRY(hashset_exact(c, R, U, M, B, jdk_flags));
   *U_out = (uint32_t)U;
   *M_out = (uint32_t)M;
   *key_xor_out = s.key_xor;
@@ -397,9 +805,8 @@ gs_status triangle_selfpair_term(gs_ctx* c, const int64_t* src, const int64_t* d
                                  uint64_t* S) {
   uint32_t U = 0, M = 0;
   uint64_t key_xor = 0;
-  bool tree = false;
-  GS_TRY(hashset_order(c, src, dst, n, &U, &M, &key_xor, &tree));
-  if (tree) return set_error(c, GS_EUNSUPPORTED, "triangles: a neighbour set would use a treeified HashMap bin");
+  uint32_t jdk_flags = 0;
+  GS_TRY(hashset_order(c, src, dst, n, &U, &M, &key_xor, &jdk_flags));
   char* sm = c->small.as<char>();
   unsigned long long* d = (unsigned long long*)(sm + SM_TOTAL);
   GS_HIP(hipMemsetAsync(d, 0, 8, c->stream));
@@ -433,9 +840,9 @@ gs_status gs_window_candidates(gs_ctx* c, const gs_edge_batch* b, gs_pair_out* o
   const uint64_t R = 2 * b->n;
   uint32_t U = 0, M = 0;
   uint64_t key_xor = 0;
-  bool tree = false;
-  GS_TRY(hashset_order(c, src, dst, b->n, &U, &M, &key_xor, &tree));
-  out->reserved = tree ? 1 : 0;   // 1 = a treeified bin: JDK order of that vertex not reproduced
+  uint32_t jdk_flags = 0;
+  GS_TRY(hashset_order(c, src, dst, b->n, &U, &M, &key_xor, &jdk_flags));
+  out->reserved = jdk_flags;   // bit 0 = a treeified bin, bit 1 = a collision resize (both simulated exactly)
   // rows: gt flags -> scan -> row lengths -> scan
   GS_TRY(ensure(c, c->hs[HS_G], (M + 1) * 8));
   GS_TRY(ensure(c, c->hs[HS_GX], (M + 1) * 8));

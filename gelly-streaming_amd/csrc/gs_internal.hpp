@@ -67,7 +67,7 @@ struct gs_ctx {
   uint32_t tri_B = 0;            // split-window triangles: id geometry of the current window
   uint64_t tri_key_xor = 0;
   // HashSet-order pipeline (gs_hashset.hip)
-  gs::DevBuf hs[20];
+  gs::DevBuf hs[32];
   // bucket path (gs_bucket.hip): plan tables, work items, LDS slabs of multi-item buckets
   gs::DevBuf bk_meta, bk_items, bk_slabs;
   // direct partition: per-tile bucket counts (u16), chunk sums, per-tile write offsets
@@ -111,7 +111,8 @@ constexpr size_t SM_BK_N = SM_BK_MM + 32;            // u32[4] bucket path: item
 constexpr size_t SM_TRI_PROBES = SM_BK_N + 16;      // u64 triangles: hash probes of the counting step
 constexpr size_t SM_BK_ESC = SM_TRI_PROBES + 16;    // u64 packed scatter: escaped values
 constexpr size_t SM_DEV_ERR = SM_BK_ESC + 8;        // u32 device error flags (GS_DERR_*)
-constexpr size_t SM_BYTES = SM_DEV_ERR + 8;
+constexpr size_t SM_HS = SM_DEV_ERR + 8;            // u32[4] HashSet order: complex vertices, JDK flags
+constexpr size_t SM_BYTES = SM_HS + 16;
 // device error flags (SM_DEV_ERR): a kernel that cannot finish its work sets one and returns
 constexpr uint32_t GS_DERR_TABLE_FULL = 1u;         // an LDS hash set filled up (triangle counting)
 constexpr size_t HOST_SMALL_WORDS = 128;            // pinned u64 mirror of small scalars

@@ -213,11 +213,10 @@ class Engine:
         U, RR = nv.value, nr.value
         return keys[:U], offs[:U + 1], nbrs[:RR], (None if vals is None else vals[:RR])
 
-    def candidates(self, src, dst, strict: bool = False):
-        """gs_window_candidates: GenerateCandidateEdges records (a, b, is_candidate).
-        self.last_candidates_treeified: a neighbour set of this window would use a treeified JDK HashMap
-        bin (> 8 ids in one bin), whose iteration order is not modelled -- those vertices' records are
-        in plain-bin order.  strict=True raises GS_EUNSUPPORTED for such windows instead."""
+    def candidates(self, src, dst):
+        """gs_window_candidates: GenerateCandidateEdges records (a, b, is_candidate), ids in exact JDK
+        HashSet order.  self.last_candidates_jdk_flags: bit 0 = some neighbour set used a treeified
+        HashMap bin, bit 1 = a bin of 9 forced a resize below capacity 64 (both simulated exactly)."""
         b, keep, dev = self._batch(src, dst, None)
         n_out = ctypes.c_uint64(0)
         probe = L.GsPairOut(None, None, None, 0, ctypes.pointer(n_out), L.GS_MEM_DEVICE if dev else L.GS_MEM_HOST, 0)
@@ -230,10 +229,7 @@ class Engine:
         out = L.GsPairOut(_ptr(a), _ptr(bb), _ptr(f), P, ctypes.pointer(n_out),
                           L.GS_MEM_DEVICE if dev else L.GS_MEM_HOST, 0)
         self._check(self._L.gs_window_candidates(self.ctx, ctypes.byref(b), ctypes.byref(out)))
-        self.last_candidates_treeified = bool(out.reserved)
-        if strict and out.reserved:
-            raise GsError(L.GS_EUNSUPPORTED, "candidates: a neighbour set uses a treeified HashMap bin "
-                                             "(JDK iteration order not modelled)")
+        self.last_candidates_jdk_flags = int(out.reserved)
         return a[:P], bb[:P], f[:P]
 
     def candidate_count(self, src, dst) -> int:

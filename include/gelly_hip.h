@@ -193,7 +193,10 @@ GS_API gs_status gs_window_csr(gs_ctx* ctx, const gs_edge_batch* batch, int32_t 
 /* applyOnNeighbors(GenerateCandidateEdges) on slice(ALL) (WindowTriangles.java:62-63, 83-116).
  * Records per vertex v: (v, t, false) per neighbour record in arrival order, then the candidate
  * pairs (ids[i], ids[j], true), i < len-1, j >= i, ids[i] > v, ids[j] > v, where ids is v's
- * neighbour set in java.util.HashSet (JDK 8+) iteration order.  Vertices ascend. */
+ * neighbour set in java.util.HashSet (JDK 8+) iteration order.  Vertices ascend.  A neighbour set
+ * whose insertion ever fills a HashMap bin to 9 nodes is simulated exactly (treeifyBin's resize below
+ * capacity 64, red-black tree bins above); out->reserved reports it: bit 0 = a tree bin, bit 1 = a
+ * collision resize. */
 GS_API gs_status gs_window_candidates(gs_ctx* ctx, const gs_edge_batch* batch, gs_pair_out* out);
 
 /* The whole WindowTriangles pipeline for one window (WindowTriangles.java:61-66):

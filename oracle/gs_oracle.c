@@ -409,12 +409,12 @@ GSO_API int64_t gso_window_csr(const int64_t* src, const int64_t* dst, const voi
 }
 
 /* ------------------------------------------------------------------------------------ */
-/* java.util.HashSet<Long> iteration order (JDK 8+ HashMap, list bins)                   */
+/* java.util.HashSet<Long> iteration order (JDK 8+ HashMap)                              */
 /* ------------------------------------------------------------------------------------ */
 /* HashSet() -> HashMap(16, 0.75): table doubles when ++size > 0.75*cap.  Long.hashCode =
  * (int)(x ^ (x >>> 32)); HashMap.hash spreads h ^ (h >>> 16); bucket = hash & (cap-1).
  * Iteration walks buckets 0..cap-1, each bin in insertion order (resize splits preserve
- * order).  Bins that would treeify (>= 9 entries at cap >= 64) are reported via *treeified. */
+ * order) -- as long as no bin ever reaches 9 nodes; hashset_order below simulates the whole map. */
 GSO_API uint64_t gso_java_hashset_cap(uint64_t k) {
   uint64_t cap = 16;
   while ((double)k > 0.75 * (double)cap) cap <<= 1;
@@ -430,8 +430,266 @@ static int cmp_hs(const void* a, const void* b) {
   if (p->b != q->b) return p->b < q->b ? -1 : 1;
   return (p->ord > q->ord) - (p->ord < q->ord);
 }
-/* distinct[] in first-arrival order -> ids[] in HashSet iteration order; returns 1 if a bin treeifies */
+
+/* The exact java.util.HashMap<Long, Object> of a HashSet<Long> built by add() in arrival order (JDK 8+
+ * HashMap.putVal / resize / treeifyBin / TreeNode.treeify / putTreeVal / balanceInsertion / rotateLeft /
+ * rotateRight / moveRootToFront / split / untreeify, restated over index-linked nodes):
+ *  - a list bin that reaches 9 nodes calls treeifyBin: below capacity 64 that resizes the table instead
+ *    (so the final capacity is not a function of the size alone);
+ *  - a tree bin keeps its nodes in a red-black tree ordered by (hash, Long value) AND in its `next`
+ *    list, which iteration follows: treeify keeps the list order but moves the root to the front; a
+ *    later insert goes right after its tree parent, then the (new) root moves to the front;
+ *  - resize splits every bin into lo / hi lists in list order; a tree half of <= 6 nodes becomes a list
+ *    again, a larger one is re-treeified (unless the other half is empty).
+ * Iteration walks bins 0..cap-1 and follows `next`. */
+typedef struct {
+  int64_t key;
+  uint32_t hash;
+  int32_t next, prev, parent, left, right;
+  uint8_t red, tree;
+} jnode;
+typedef struct {
+  jnode* nd;
+  int32_t* tab;
+  uint32_t cap, thr, size;
+  int flags;   /* bit 0: a bin treeified; bit 1: a collision resize (treeifyBin below capacity 64) */
+} jmap;
+
+static uint32_t j_hash(int64_t x) {
+  const uint32_t h = (uint32_t)((uint64_t)x ^ ((uint64_t)x >> 32));
+  return h ^ (h >> 16);
+}
+static int j_dir(const jnode* p, uint32_t h, int64_t k) {   /* putTreeVal / treeify comparison */
+  if (p->hash > h) return -1;
+  if (p->hash < h) return 1;
+  return k < p->key ? -1 : 1;   /* Long.compareTo; keys are distinct */
+}
+static int32_t j_rotl(jnode* n, int32_t root, int32_t p) {
+  int32_t r, pp, rl;
+  if (p >= 0 && (r = n[p].right) >= 0) {
+    if ((rl = n[p].right = n[r].left) >= 0) n[rl].parent = p;
+    if ((pp = n[r].parent = n[p].parent) < 0) { root = r; n[r].red = 0; }
+    else if (n[pp].left == p) n[pp].left = r;
+    else n[pp].right = r;
+    n[r].left = p;
+    n[p].parent = r;
+  }
+  return root;
+}
+static int32_t j_rotr(jnode* n, int32_t root, int32_t p) {
+  int32_t l, pp, lr;
+  if (p >= 0 && (l = n[p].left) >= 0) {
+    if ((lr = n[p].left = n[l].right) >= 0) n[lr].parent = p;
+    if ((pp = n[l].parent = n[p].parent) < 0) { root = l; n[l].red = 0; }
+    else if (n[pp].right == p) n[pp].right = l;
+    else n[pp].left = l;
+    n[l].right = p;
+    n[p].parent = l;
+  }
+  return root;
+}
+static int32_t j_balance(jnode* n, int32_t root, int32_t x) {
+  n[x].red = 1;
+  for (;;) {
+    int32_t xp = n[x].parent, xpp, xppl, xppr;
+    if (xp < 0) { n[x].red = 0; return x; }
+    if (!n[xp].red || (xpp = n[xp].parent) < 0) return root;
+    if (xp == (xppl = n[xpp].left)) {
+      if ((xppr = n[xpp].right) >= 0 && n[xppr].red) {
+        n[xppr].red = 0; n[xp].red = 0; n[xpp].red = 1; x = xpp;
+      } else {
+        if (x == n[xp].right) {
+          root = j_rotl(n, root, x = xp);
+          xpp = (xp = n[x].parent) < 0 ? -1 : n[xp].parent;
+        }
+        if (xp >= 0) {
+          n[xp].red = 0;
+          if (xpp >= 0) { n[xpp].red = 1; root = j_rotr(n, root, xpp); }
+        }
+      }
+    } else {
+      if (xppl >= 0 && n[xppl].red) {
+        n[xppl].red = 0; n[xp].red = 0; n[xpp].red = 1; x = xpp;
+      } else {
+        if (x == n[xp].left) {
+          root = j_rotr(n, root, x = xp);
+          xpp = (xp = n[x].parent) < 0 ? -1 : n[xp].parent;
+        }
+        if (xp >= 0) {
+          n[xp].red = 0;
+          if (xpp >= 0) { n[xpp].red = 1; root = j_rotl(n, root, xpp); }
+        }
+      }
+    }
+  }
+}
+static void j_root_front(jmap* m, int32_t root) {
+  jnode* n = m->nd;
+  const uint32_t idx = n[root].hash & (m->cap - 1);
+  const int32_t first = m->tab[idx];
+  if (root != first) {
+    m->tab[idx] = root;
+    const int32_t rp = n[root].prev, rn = n[root].next;
+    if (rn >= 0) n[rn].prev = rp;
+    if (rp >= 0) n[rp].next = rn;
+    if (first >= 0) n[first].prev = root;
+    n[root].next = first;
+    n[root].prev = -1;
+  }
+}
+/* TreeNode.treeify from list head hd (nodes already tree-marked, prev/next linked) */
+static void j_treeify(jmap* m, int32_t hd) {
+  jnode* n = m->nd;
+  int32_t root = -1;
+  for (int32_t x = hd, nx; x >= 0; x = nx) {
+    nx = n[x].next;
+    n[x].left = n[x].right = -1;
+    if (root < 0) { n[x].parent = -1; n[x].red = 0; root = x; continue; }
+    for (int32_t p = root;;) {
+      const int dir = j_dir(&n[p], n[x].hash, n[x].key);
+      const int32_t xp = p;
+      if ((p = dir <= 0 ? n[p].left : n[p].right) < 0) {
+        n[x].parent = xp;
+        if (dir <= 0) n[xp].left = x; else n[xp].right = x;
+        root = j_balance(n, root, x);
+        break;
+      }
+    }
+  }
+  j_root_front(m, root);
+}
+static void j_untreeify(jnode* n, int32_t hd) {
+  for (int32_t x = hd; x >= 0; x = n[x].next) { n[x].tree = 0; n[x].left = n[x].right = n[x].parent = -1; }
+}
+static void j_resize(jmap* m);
+static void j_split(jmap* m, int32_t* ntab, int32_t b, uint32_t index, uint32_t bit) {
+  jnode* n = m->nd;
+  int32_t loH = -1, loT = -1, hiH = -1, hiT = -1;
+  uint32_t lc = 0, hc = 0;
+  for (int32_t e = b, nx; e >= 0; e = nx) {
+    nx = n[e].next;
+    n[e].next = -1;
+    if ((n[e].hash & bit) == 0) {
+      if ((n[e].prev = loT) < 0) loH = e; else n[loT].next = e;
+      loT = e; ++lc;
+    } else {
+      if ((n[e].prev = hiT) < 0) hiH = e; else n[hiT].next = e;
+      hiT = e; ++hc;
+    }
+  }
+  /* treeify / root_front index through the new table */
+  int32_t* otab = m->tab; const uint32_t ocap = m->cap;
+  m->tab = ntab; m->cap = ocap * 2;
+  if (loH >= 0) {
+    if (lc <= 6) { j_untreeify(n, loH); ntab[index] = loH; }
+    else { ntab[index] = loH; if (hiH >= 0) j_treeify(m, loH); }
+  }
+  if (hiH >= 0) {
+    if (hc <= 6) { j_untreeify(n, hiH); ntab[index + bit] = hiH; }
+    else { ntab[index + bit] = hiH; if (loH >= 0) j_treeify(m, hiH); }
+  }
+  m->tab = otab; m->cap = ocap;
+}
+static void j_resize(jmap* m) {
+  const uint32_t ocap = m->cap, ncap = ocap ? ocap * 2 : 16;
+  int32_t* ntab = (int32_t*)malloc(ncap * sizeof(int32_t));
+  for (uint32_t i = 0; i < ncap; ++i) ntab[i] = -1;
+  jnode* n = m->nd;
+  for (uint32_t j = 0; j < ocap; ++j) {
+    const int32_t e = m->tab[j];
+    if (e < 0) continue;
+    if (n[e].next < 0) { ntab[n[e].hash & (ncap - 1)] = e; }
+    else if (n[e].tree) { j_split(m, ntab, e, j, ocap); }
+    else {
+      int32_t loH = -1, loT = -1, hiH = -1, hiT = -1;
+      for (int32_t x = e, nx; x >= 0; x = nx) {
+        nx = n[x].next;
+        if ((n[x].hash & ocap) == 0) { if (loT < 0) loH = x; else n[loT].next = x; loT = x; }
+        else { if (hiT < 0) hiH = x; else n[hiT].next = x; hiT = x; }
+      }
+      if (loT >= 0) { n[loT].next = -1; ntab[j] = loH; }
+      if (hiT >= 0) { n[hiT].next = -1; ntab[j + ocap] = hiH; }
+    }
+  }
+  free(m->tab);
+  m->tab = ntab;
+  m->cap = ncap;
+  m->thr = ncap / 4 * 3;
+}
+static void j_treeify_bin(jmap* m, uint32_t hash) {
+  if (m->cap < 64) { m->flags |= 2; j_resize(m); return; }
+  jnode* n = m->nd;
+  const int32_t hd = m->tab[hash & (m->cap - 1)];
+  int32_t tl = -1;
+  for (int32_t e = hd; e >= 0; e = n[e].next) { n[e].tree = 1; n[e].prev = tl; tl = e; }
+  m->flags |= 1;
+  j_treeify(m, hd);
+}
+/* HashMap.putVal for a key not yet present (the caller feeds distinct keys in arrival order) */
+static void j_put(jmap* m, int32_t x) {
+  jnode* n = m->nd;
+  if (!m->tab) j_resize(m);
+  const uint32_t h = n[x].hash, i = h & (m->cap - 1);
+  n[x].next = n[x].prev = n[x].parent = n[x].left = n[x].right = -1;
+  n[x].red = 0; n[x].tree = 0;
+  int32_t p = m->tab[i];
+  if (p < 0) {
+    m->tab[i] = x;
+  } else if (n[p].tree) {   /* putTreeVal: p is the bin's root (moveRootToFront) */
+    int32_t root = p;
+    while (n[root].parent >= 0) root = n[root].parent;
+    n[x].tree = 1;
+    for (int32_t q = root;;) {
+      const int dir = j_dir(&n[q], h, n[x].key);
+      const int32_t xp = q;
+      if ((q = dir <= 0 ? n[q].left : n[q].right) < 0) {
+        const int32_t xpn = n[xp].next;
+        n[x].next = xpn;
+        if (dir <= 0) n[xp].left = x; else n[xp].right = x;
+        n[xp].next = x;
+        n[x].parent = n[x].prev = xp;
+        if (xpn >= 0) n[xpn].prev = x;
+        j_root_front(m, j_balance(n, root, x));
+        break;
+      }
+    }
+  } else {
+    for (int bin = 0;; ++bin) {
+      const int32_t e = n[p].next;
+      if (e < 0) {
+        n[p].next = x;
+        if (bin >= 7) j_treeify_bin(m, h);
+        break;
+      }
+      p = e;
+    }
+  }
+  if (++m->size > m->thr) j_resize(m);
+}
+
+/* distinct[] in first-arrival order -> ids[] in HashSet iteration order; returns the flags above */
 static int hashset_order(const int64_t* distinct, uint64_t k, int64_t* ids, hsent* tmp) {
+  (void)tmp;
+  jmap m = {0};
+  m.nd = (jnode*)malloc((k + 1) * sizeof(jnode));
+  for (uint64_t j = 0; j < k; ++j) {
+    m.nd[j].key = distinct[j];
+    m.nd[j].hash = j_hash(distinct[j]);
+    j_put(&m, (int32_t)j);
+  }
+  uint64_t o = 0;
+  for (uint32_t b = 0; b < m.cap; ++b)
+    for (int32_t e = m.tab[b]; e >= 0; e = m.nd[e].next) ids[o++] = m.nd[e].key;
+  free(m.tab);
+  free(m.nd);
+  return m.flags;
+}
+
+/* the plain-bin model (final capacity from the size alone, insertion order inside a bin) -- what the
+ * GPU's sort-based order computes; tests compare it with the exact model */
+GSO_API int gso_hashset_order(const int64_t* distinct, uint64_t k, int64_t* ids_exact, int64_t* ids_plain) {
+  hsent* tmp = (hsent*)malloc((k + 1) * sizeof(hsent));
+  const int flags = hashset_order(distinct, k, ids_exact, tmp);
   const uint64_t cap = gso_java_hashset_cap(k);
   for (uint64_t j = 0; j < k; ++j) {
     tmp[j].b = gso_java_long_bucket(distinct[j], cap);
@@ -439,14 +697,9 @@ static int hashset_order(const int64_t* distinct, uint64_t k, int64_t* ids, hsen
     tmp[j].x = distinct[j];
   }
   qsort(tmp, k, sizeof(hsent), cmp_hs);
-  int tree = 0;
-  uint64_t run = 0;
-  for (uint64_t j = 0; j < k; ++j) {
-    ids[j] = tmp[j].x;
-    run = (j > 0 && tmp[j].b == tmp[j - 1].b) ? run + 1 : 1;
-    if (run >= 9 && cap >= 64) tree = 1;
-  }
-  return tree;
+  for (uint64_t j = 0; j < k; ++j) ids_plain[j] = tmp[j].x;
+  free(tmp);
+  return flags;
 }
 
 /* per-vertex distinct neighbours (first arrival order) from the CSR */

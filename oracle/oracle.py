@@ -52,6 +52,7 @@ def lib():
             "gso_window_triangles_fwd": (ctypes.c_int32, [P, P, u64, P, P]),
             "gso_baseline_reduce": (u64, [P, P, P, u64, i32, i32, i32, i32]),
             "gso_java_hashset_cap": (u64, [u64]),
+            "gso_hashset_order": (i32, [P, u64, P, P]),
             "gso_parse_edges_text": (i64, [ctypes.c_char_p, u64, P, P, P, u64]),
             "gso_java_long_bucket": (u32, [i64, u64]),
             "gso_zipf_cdf": (None, [u64, ctypes.c_double, P]),
@@ -182,7 +183,7 @@ def window_candidates(src, dst):
     f = np.empty(P, np.uint8)
     got = lib().gso_window_candidates(_p(src), _p(dst), len(src), _p(a), _p(b), _p(f), P, ctypes.byref(tree))
     assert got == P
-    return a, b, f, bool(tree.value)
+    return a, b, f, int(tree.value)   # JDK flags of hashset_order (nonzero: some set left the plain model)
 
 
 def candidate_count(src, dst):
@@ -229,7 +230,7 @@ def window_triangles_ref(src, dst):
     ex, has, tree = ctypes.c_uint64(0), ctypes.c_int(0), ctypes.c_int(0)
     w = lib().gso_window_triangles_ref(_p(src), _p(dst), len(src), ctypes.byref(ex), ctypes.byref(has),
                                        ctypes.byref(tree))
-    return int(w), int(ex.value), bool(has.value), bool(tree.value)
+    return int(w), int(ex.value), bool(has.value), int(tree.value)
 
 
 def window_triangles_fwd(src, dst):
@@ -320,3 +321,13 @@ def components(src, dst, prev=None):
     ov, ol = np.empty(cap, np.int64), np.empty(cap, np.int64)
     u = lib().gso_components(_p(src), _p(dst), len(src), _p(pv), _p(pl), len(pv), _p(ov), _p(ol))
     return ov[:u].copy(), ol[:u].copy()
+
+
+def hashset_order(ids):
+    """java.util.HashSet<Long> built by add() of `ids` (distinct, arrival order) -> (iteration order of the
+    exact JDK 8+ HashMap simulation, the plain-bin model's order, flags: 1 = a bin treeified,
+    2 = a collision resize below capacity 64)."""
+    ids = _i64(ids)
+    ex, pl = np.empty(len(ids) + 1, np.int64), np.empty(len(ids) + 1, np.int64)
+    f = lib().gso_hashset_order(_p(ids), len(ids), _p(ex), _p(pl))
+    return ex[:len(ids)].copy(), pl[:len(ids)].copy(), int(f)

@@ -179,10 +179,9 @@ def test_candidates_match_reference_rule(engine, oracle, kind):
     rng = np.random.default_rng({"small_ids": 1, "sparse_ids": 2, "negative_ids": 3, "rmat": 4}[kind])
     for trial in range(6):
         s, d = _cand_case(oracle, rng, kind)
-        ra, rb, rf, tree = oracle.window_candidates(s, d)
-        if tree:
-            continue
+        ra, rb, rf, flags = oracle.window_candidates(s, d)
         ga, gb, gf = engine.candidates(*[torch.from_numpy(x).cuda() for x in (s, d)])
+        assert engine.last_candidates_jdk_flags == flags, (kind, trial)
         assert np.array_equal(ga.cpu().numpy(), ra), (kind, trial)
         assert np.array_equal(gb.cpu().numpy(), rb), (kind, trial)
         assert np.array_equal(gf.cpu().numpy(), rf), (kind, trial)
@@ -210,9 +209,7 @@ def test_triangles_with_self_loops(engine, oracle):
         d = np.where(rng.random(n) < 0.15, s, rng.integers(0, V, n)).astype(np.int64)
         if trial % 2:
             s, d = s * 7919 + 3, d * 7919 + 3
-        w_ref, ex_ref, has_ref, tree = oracle.window_triangles_ref(s, d)
-        if tree:
-            continue
+        w_ref, ex_ref, has_ref, _ = oracle.window_triangles_ref(s, d)
         ex, wrapped, has = engine.triangles(s, d)
         assert (ex, wrapped, has) == (ex_ref, w_ref, has_ref), trial
 
@@ -249,13 +246,12 @@ def test_count_candidates_matches_reference(engine, oracle, kind):
     rng = np.random.default_rng({"small_ids": 11, "sparse_ids": 12, "negative_ids": 13, "rmat": 14}[kind])
     for trial in range(4):
         s, d = _cand_case(oracle, rng, kind)
-        ra, rb, rf, tree = oracle.window_candidates(s, d)
+        ra, rb, rf, _ = oracle.window_candidates(s, d)
         want = oracle.count_candidates(ra, rb, rf)
         got = engine.count_candidates(*[torch.from_numpy(x).cuda() for x in (ra, rb, rf)])
         assert got == (want[1], want[0], want[2], want[3]), (kind, trial)
-        if not tree:
-            w_ref, ex_ref, has_ref, _ = oracle.window_triangles_ref(s, d)
-            assert (got[0], got[1], got[2]) == (ex_ref, w_ref, has_ref)
+        w_ref, ex_ref, has_ref, _ = oracle.window_triangles_ref(s, d)
+        assert (got[0], got[1], got[2]) == (ex_ref, w_ref, has_ref)
 
 
 def test_count_candidates_edge_cases(engine, oracle):
@@ -415,19 +411,49 @@ def test_count_candidates_ids_spanning_2_pow_32(engine, oracle):
     assert (got[1], got[0], got[2], got[3]) == want
 
 
-def test_candidates_treeified_flag(engine, oracle):
-    """A neighbour set with > 8 ids in one JDK HashMap bin (ids k << 24): the oracle reports a
-    treeified bin; engine.candidates surfaces it (last_candidates_treeified) and strict=True refuses."""
-    from gelly_streaming_amd import GsError
-    k = np.arange(1, 201, dtype=np.int64)
-    s, d = np.zeros(200, np.int64), k << 24
-    assert oracle.window_candidates(s, d)[3]
-    engine.candidates(s, d)
-    assert engine.last_candidates_treeified
-    with pytest.raises(GsError):
-        engine.candidates(s, d, strict=True)
-    s2, d2 = np.zeros(200, np.int64), k << 20        # same sizes, plain bins
-    ra, rb, rf, tree = oracle.window_candidates(s2, d2)
-    ga, gb, gf = engine.candidates(s2, d2, strict=True)
-    assert not tree and not engine.last_candidates_treeified
-    assert np.array_equal(ga, ra) and np.array_equal(gb, rb) and np.array_equal(gf, rf)
+def _jdk_case(oracle, case):
+    rng = np.random.default_rng(sum(map(ord, case)))
+    if case == "resize16":            # a bin of 9 below capacity 64: treeifyBin resizes instead
+        s, d = np.zeros(20, np.int64), np.arange(1, 21, dtype=np.int64) * 16
+    elif case == "tree24":            # one tree bin at capacity 256
+        s, d = np.zeros(200, np.int64), np.arange(1, 201, dtype=np.int64) << 24
+    elif case == "tree20_split":      # tree bins split and re-treeified by later resizes
+        s, d = np.zeros(3000, np.int64), np.arange(1, 3001, dtype=np.int64) << 20
+    elif case == "many_vertices":     # hundreds of complex sets in one window, plus plain ones
+        V = 400
+        s = np.repeat(-np.arange(1, V + 1, dtype=np.int64), 20)
+        d = 16 * (np.tile(np.arange(1, 21, dtype=np.int64), V) + 20 * np.repeat(np.arange(V), 20))
+        d[: 20 * (V // 2)] += 3       # half the sets spread over buckets: plain
+    else:                             # R-MAT window over ids j << 20: complex sets of many sizes
+        s, d = oracle.gen_rmat(10, 20_000, 0x5EED31)
+        s, d = (np.asarray(s, np.int64) + 1) << 20, (np.asarray(d, np.int64) + 1) << 20
+    p = rng.permutation(len(s))
+    return np.ascontiguousarray(s[p]), np.ascontiguousarray(d[p])
+
+
+@pytest.mark.parametrize("case", ["resize16", "tree24", "tree20_split", "many_vertices", "rmat_shifted"])
+def test_candidates_exact_jdk_order(engine, oracle, case):
+    """Neighbour sets whose java.util.HashMap leaves the plain-bin model -- a bin of 9 that makes
+    treeifyBin resize below capacity 64, red-black tree bins, tree bins split by later resizes, many such
+    sets in one window -- are simulated exactly on the GPU (k_hs_detect finds them, k_hs_jdk replays
+    putVal): the records equal the oracle's exact JDK restatement, and the reported flags agree."""
+    s, d = _jdk_case(oracle, case)
+    ra, rb, rf, flags = oracle.window_candidates(s, d)
+    assert flags
+    ga, gb, gf = engine.candidates(*(torch.from_numpy(x).cuda() for x in (s, d)))
+    assert engine.last_candidates_jdk_flags == flags
+    assert np.array_equal(ga.cpu().numpy(), ra) and np.array_equal(gb.cpu().numpy(), rb)
+    assert np.array_equal(gf.cpu().numpy(), rf)
+
+
+def test_triangles_self_pairs_exact_jdk_order(engine, oracle):
+    """The self-pair term (self-loops) skips each set's LAST HashSet element, so it depends on the exact
+    JDK order: windows over ids j << 20 (tree bins and collision resizes) match the oracle."""
+    s, d = oracle.gen_rmat(10, 20_000, 0x5EED32)
+    s, d = np.asarray(s, np.int64), np.asarray(d, np.int64)
+    d[::7] = s[::7]                   # self-loops
+    s, d = (s + 1) << 20, (d + 1) << 20
+    w, ex, has = oracle.window_triangles_fwd(s, d)
+    assert engine.triangles(*(torch.from_numpy(x).cuda() for x in (s, d))) == (ex, w, has)
+    w2, ex2, has2, flags = oracle.window_triangles_ref(s[:4000], d[:4000])
+    assert flags and engine.triangles(s[:4000], d[:4000]) == (ex2, w2, has2)

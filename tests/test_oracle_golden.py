@@ -85,6 +85,43 @@ def test_hashset_order_model(oracle):
     assert [oracle.java_hashset_cap(k) for k in (0, 1, 12, 13, 24, 25, 48, 49)] == [16, 16, 16, 32, 32, 64, 64, 128]
 
 
+def test_hashset_exact_known_answers(oracle):
+    """Known answers of the exact JDK HashMap restatement, derived by hand from HashMap.putVal /
+    treeifyBin / resize / TreeNode.treeify (JDK 8+; no JVM in this image, so these pin it):
+     - 16, 32, .., 144 all hash to bucket 0 of 16; the 9th add makes treeifyBin resize (capacity 16 < 64)
+       to 32, where evens (bucket 0) precede odds (bucket 16), each in insertion order;
+     - eight of them stay one plain bin;
+     - 64, .., 704: the 9th and 10th adds resize to 32 and 64 (all still bucket 0), the 11th treeifies:
+       ascending inserts give the red-black root 256 (4th key), moveRootToFront puts it first."""
+    ex, pl, f = oracle.hashset_order([16 * j for j in range(1, 10)])
+    assert ex.tolist() == [32, 64, 96, 128, 16, 48, 80, 112, 144] and f == 2
+    assert pl.tolist() == [16 * j for j in range(1, 10)]
+    ex, pl, f = oracle.hashset_order([16 * j for j in range(1, 9)])
+    assert ex.tolist() == pl.tolist() == [16 * j for j in range(1, 9)] and f == 0
+    ex, pl, f = oracle.hashset_order([64 * j for j in range(1, 12)])
+    assert ex.tolist() == [256, 64, 128, 192] + [64 * j for j in range(5, 12)] and f == 3
+
+
+def test_hashset_exact_matches_plain_without_collisions(oracle):
+    """Random Long ids never fill a bin to 9 at these sizes: the exact simulation equals the plain-bin
+    model (capacity from the size, buckets ascending, insertion order inside a bin)."""
+    rng = np.random.default_rng(17)
+    for k in (1, 12, 13, 100, 1000, 5000):
+        ids = np.unique(rng.integers(-(1 << 62), 1 << 62, k))
+        ids = rng.permutation(ids)
+        ex, pl, f = oracle.hashset_order(ids)
+        assert f == 0 and np.array_equal(ex, pl) and sorted(ex.tolist()) == sorted(ids.tolist())
+
+
+def test_hashset_exact_tree_bins_split(oracle):
+    """Ids j << 20 crowd few buckets at every capacity: bins treeify at 64, and the later resizes split
+    tree bins (untreeify at <= 6, re-treeify above).  The order is always a permutation of the set."""
+    for k in (20, 200, 2000, 6000):
+        ids = np.arange(1, k + 1, dtype=np.int64) << 20
+        ex, pl, f = oracle.hashset_order(ids)
+        assert f == (2 if k == 20 else 3) and sorted(ex.tolist()) == ids.tolist() and not np.array_equal(ex, pl)
+
+
 def test_generators_deterministic(oracle):
     a = oracle.gen_rmat(10, 1000, 1)
     b = oracle.gen_rmat(10, 1000, 1)
