@@ -51,6 +51,9 @@ def parse():
                         "(--windows-edges edges of an R-MAT --scale stream per 1000 ms window)")
     p.add_argument("--no-pack", action="store_true",
                    help="ablation: integer SUM keeps 8-byte partitioned values instead of 4-byte packed records")
+    p.add_argument("--no-spec", action="store_true",
+                   help="ablation: packed windows count per-tile bucket histograms before the scatter instead of "
+                        "sizing bucket regions from the previous window's counts")
     p.add_argument("--sort-only", action="store_true",
                    help="ablation: reduce / fold through the full LSD sort + reduce-by-key path")
     p.add_argument("--bk-onesweep", action="store_true",
@@ -137,13 +140,17 @@ def direct_kernel_table(times_list, E, U_avg):
     ab = 8 if (vb or t0.packed) else 4   # staged accumulator (i64 sum / u32 count)
     mean = lambda f: statistics.mean(f(t) for t in times_list)
     rows = {}
-    name = "dp_scatter_pack" if t0.packed else "dp_scatter"
+    spec = t0.speculative == 1   # regions from the previous window's counts: no histogram, no offset scans
+    name = ("sp_scatter_pack" if spec else "dp_scatter_pack") if t0.packed else "dp_scatter"
     rows[name] = {"ms": mean(lambda t: t.pass_ms[1]), "bytes": E * ((8 + lb) + (2 + vb))}
     rows["bucket_accumulate"] = {"ms": mean(lambda t: t.pass_ms[2]), "bytes": E * (2 + vb) + U_avg * (4 + ab)}
     rows["bucket_merge"] = {"ms": mean(lambda t: t.pass_ms[3]), "bytes": 0}
     rows["bucket_emit"] = {"ms": mean(lambda t: t.pass_ms[4]), "bytes": U_avg * (4 + ab + 16)}
-    rows["dp_offsets(up+spine+plan+down)"] = {"ms": mean(lambda t: t.pass_ms[0]), "bytes": 0}
-    rows["dp_hist"] = {"ms": mean(lambda t: t.keyinfo_ms), "bytes": E * 8}
+    if spec:
+        rows["sp_regions"] = {"ms": mean(lambda t: t.keyinfo_ms), "bytes": 0}
+    else:
+        rows["dp_offsets(up+spine+plan+down)"] = {"ms": mean(lambda t: t.pass_ms[0]), "bytes": 0}
+        rows["dp_hist"] = {"ms": mean(lambda t: t.keyinfo_ms), "bytes": E * 8}
     return rows, mean(lambda t: t.partials)
 
 
@@ -543,7 +550,7 @@ def main():
     from importlib import import_module
     D = import_module("gelly_streaming_amd.distributed")
 
-    eng = pkg.Engine(local, sort_only=a.sort_only, bk_onesweep=a.bk_onesweep, no_pack=a.no_pack)
+    eng = pkg.Engine(local, sort_only=a.sort_only, bk_onesweep=a.bk_onesweep, no_pack=a.no_pack, no_spec=a.no_spec)
     E = a.edge_factor << a.scale
     vdt = 1 if a.dtype == "int64" else 3
     # a.windows distinct windows of the stream (rank r holds windows r*W .. r*W+W-1), cycled by the
@@ -745,6 +752,8 @@ def main():
                        "pipeline": {0: "sort", 1: "bucket-onesweep", 2: "bucket-direct", 3: "triangles",
                                     4: "components"}[t0s.path],
                        "packed_records": bool(t0s.packed), "escaped_values": int(t0s.escapes),
+                       "speculative_windows": sum(1 for t in times if getattr(t, "speculative", 0) == 1),
+                       "speculative_misses": sum(1 for t in times if getattr(t, "speculative", 0) == 2),
                        "parallelism": ("1 GPU" if not dist else
                                        f"{world} replicas (per-window components, no exchange)" if a.workload == "cc" else
                                        f"split window over {world} GPUs: summed degrees, oriented edges to owner(u), "

@@ -50,6 +50,7 @@ u64, i64, i32, u32 = ctypes.c_uint64, ctypes.c_int64, ctypes.c_int32, ctypes.c_u
 GS_FLAG_SORT_ONLY = 1   # include/gelly_hip.h: reduce / fold always take the LSD sort path
 GS_FLAG_BK_ONESWEEP = 2   # bucket path: 1-2 LSD partition passes instead of the direct scatter (A/B)
 GS_FLAG_NO_PACK = 4       # bucket path: integer SUM/MIN/MAX keep 8-byte partitioned values (A/B)
+GS_FLAG_NO_SPEC = 16      # bucket path: no speculative partition (per-tile histograms first; A/B)
 GS_FLAG_TEST_TINY_TABLES = 8   # TEST ONLY: triangle hash sets of one bucket -> must fail with GS_EDEVICE
 
 
@@ -116,7 +117,7 @@ class GsStageTimes(ctypes.Structure):
     _fields_ = [("keyinfo_ms", ctypes.c_float), ("sort_ms", ctypes.c_float), ("reduce_ms", ctypes.c_float),
                 ("total_ms", ctypes.c_float), ("sort_passes", u32), ("key_bits", u32), ("records", u64),
                 ("vertices", u64), ("pass_ms", ctypes.c_float * 8), ("key_bytes", u32), ("payload_bytes", u32),
-                ("partials", u64), ("fused_last", u32), ("path", u32), ("packed", u32), ("reserved", u32),
+                ("partials", u64), ("fused_last", u32), ("path", u32), ("packed", u32), ("speculative", u32),
                 ("escapes", u64)]
 
 

@@ -142,7 +142,11 @@ gs_status ensure_cu(gs_ctx* c) {
 
 // k_bk_plan over meta[HIST] (bucket totals): bucket starts, work items, multi-item buckets
 template <class P>
-gs_status launch_plan(gs_ctx* c, uint64_t R, uint32_t nb, int passes, int w, uint32_t item_recs) {
+// R: records (or, with cursor, the regions' total capacity) -- sizes the item and slab buffers.
+// cursor / counts_out: see BkPlanOut (speculative partition).
+gs_status launch_plan(gs_ctx* c, uint64_t R, uint32_t nb, int passes, int w, uint32_t item_recs,
+                      const uint32_t* cursor = nullptr, uint32_t* counts_out = nullptr,
+                      unsigned long long* occupied = nullptr) {
   char* sm = c->small.as<char>();
   uint32_t* meta = c->bk_meta.as<uint32_t>();
   const uint64_t max_items = R / item_recs + nb + 1;
@@ -151,7 +155,8 @@ gs_status launch_plan(gs_ctx* c, uint64_t R, uint32_t nb, int passes, int w, uin
   GS_TRY(ensure(c, c->bk_slabs, max_slabs * sizeof(typename P::Lds)));
   uint32_t* ns = (uint32_t*)(sm + SM_BK_N);
   BkPlanOut po{meta + BkMeta::DBASE, meta + BkMeta::BSTART, meta + BkMeta::BCOUNT, meta + BkMeta::BITEMS,
-               meta + BkMeta::BSLAB, meta + BkMeta::MLIST, c->bk_items.as<BkItem>(), ns + 0, ns + 1};
+               meta + BkMeta::BSLAB, meta + BkMeta::MLIST, c->bk_items.as<BkItem>(), ns + 0, ns + 1,
+               cursor, counts_out, occupied};
   hipLaunchKernelGGL(k_bk_plan, dim3(1), dim3(BK_PLAN_BLOCK), 0, c->stream, meta + BkMeta::HIST, nb, passes, w,
                      item_recs, po);
   return hip_check(c, hipGetLastError(), "k_bk_plan");
@@ -164,7 +169,8 @@ gs_status launch_plan(gs_ctx* c, uint64_t R, uint32_t nb, int passes, int w, uin
 // pass_ev[ev0 + 1 .. ev0 + 3] after the three launches.  Every launch exits at once when the
 // histogram saw a key outside the predicted range (mm[2] != 0).
 template <class P, class Src>
-gs_status bucket_accumulate(gs_ctx* c, Src rs, uint64_t R, uint32_t nb, int64_t base, typename P::Out o, int ev0) {
+gs_status bucket_accumulate(gs_ctx* c, Src rs, uint64_t R, uint32_t nb, int64_t base, typename P::Out o, int ev0,
+                           const uint32_t* seg_cur = nullptr) {
   char* sm = c->small.as<char>();
   uint32_t* meta = c->bk_meta.as<uint32_t>();
   uint32_t* ns = (uint32_t*)(sm + SM_BK_N);
@@ -175,7 +181,7 @@ gs_status bucket_accumulate(gs_ctx* c, Src rs, uint64_t R, uint32_t nb, int64_t 
   auto* slabs = c->bk_slabs.as<typename P::Lds>();
   hipLaunchKernelGGL((k_bk_accum<P, Src, GS_BK_UNROLL>), dim3(c->n_cu), dim3(BK_ACC_BLOCK), 0, c->stream, rs,
                      c->bk_items.as<BkItem>(), ns + 0, meta + BkMeta::BSTART, ns + 2, slabs, st, meta + BkMeta::BCOUNT,
-                     mm);
+                     mm, seg_cur);
   GS_HIP(hipGetLastError());
   hipEventRecord(c->pass_ev[ev0 + 1], c->stream);
   const unsigned mgrid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(nb, R / BK_ITEM + 1));
@@ -273,6 +279,21 @@ gs_status bucket_direct_t(gs_ctx* c, const int64_t* src, const int64_t* dst, con
   int64_t base = c->bk_base;
   uint32_t nb = c->bk_nbp ? c->bk_nbp : (uint32_t)BK_MAXB;
   const uint32_t item_recs = item_records(c, R);
+  // speculative partition: packed windows whose bucket counts the previous packed window of this
+  // ctx measured in the same geometry (base, S, direction)
+  bool spec = false, spec_missed = false;
+  uint64_t cap = R;
+  if constexpr (CAN_PACK && ITEMS == PK_ITEMS) {
+    GS_TRY(ensure(c, c->sp_tot, BK_MAXB * 4, true));
+    GS_TRY(ensure(c, c->sp_cur, (SP_NSEG * BK_MAXB + SP_NSEG + 1) * 4));
+    spec = pack && !(c->flags & GS_FLAG_NO_SPEC) && c->sp_ok && c->sp_skip == 0 && c->sp_base == base &&
+           c->sp_S == S && c->sp_dir == DIR && nb > 1 && sp_capacity(R, nb) < (1ull << 32);
+    if (c->sp_skip > 0) --c->sp_skip;
+    if (spec) {
+      cap = sp_capacity(R, nb);
+      GS_TRY(ensure_stage<P>(c, cap + DP_BLOCK * ITEMS));   // + the trash area of dropped runs
+    }
+  }
   uint16_t* cnt = c->dp_cnt.as<uint16_t>();
   uint32_t* csum = c->dp_csum.as<uint32_t>();
   uint16_t* k16 = c->keysB.as<uint16_t>();
@@ -282,6 +303,57 @@ gs_status bucket_direct_t(gs_ctx* c, const int64_t* src, const int64_t* dst, con
   bool part = false;
   int64_t kmin = 0, kmax = 0;
   for (int attempt = 0;; ++attempt) {
+    if constexpr (CAN_PACK && ITEMS == PK_ITEMS) {
+      if (spec && attempt == 0) {
+        // regions from the previous window's counts -> the scatter reserves runs with atomics ->
+        // items from the cursors (the counts the next window predicts from) -> accumulate
+        // each XCD slot's share of the records (k_sp_scatter_pack: slot x owns full tiles [x·per, (x+1)·per),
+        // the partial last tile runs in slot 0)
+        SpSlots slots{};
+        {
+          const uint64_t tr = (DIR == DIR_ALL ? 2 : 1) * (uint64_t)TE, nfull = n / TE, per = (nfull + 7) / 8;
+          uint64_t acc = 0;
+          for (uint32_t x = 0; x < SP_NSEG; ++x) {
+            slots.pre[x] = (uint32_t)acc;
+            const uint64_t lo = std::min<uint64_t>(nfull, SP_NSEG == 1 ? 0 : x * per);
+            const uint64_t hi = SP_NSEG == 1 ? nfull : std::min<uint64_t>(nfull, (x + 1) * per);
+            acc += (hi - lo) * tr + (x == 0 ? R - nfull * tr : 0);
+          }
+          slots.pre[SP_NSEG] = (uint32_t)acc;   // == R
+        }
+        hipLaunchKernelGGL(k_sp_regions, dim3(1), dim3(BK_PLAN_BLOCK), 0, c->stream, (const uint32_t*)c->sp_tot.as<uint32_t>(),
+                           nb, c->sp_R, R, meta + BkMeta::BSTART, c->sp_cur.as<uint32_t>(), slots, mm);
+        GS_HIP(hipMemsetAsync(sm + SM_BK_ESC, 0, 8, c->stream));
+        hipEventRecord(c->ev[1], c->stream);
+        hipEventRecord(c->pass_ev[0], c->stream);
+        hipEventRecord(c->pass_ev[1], c->stream);
+        using Load = typename P::Load;
+        const BaseSrc<Load, DIR, P::PAY> ls{src, dst, (const Load*)val, base};
+        hipLaunchKernelGGL((k_sp_scatter_pack<Load, DIR, ITEMS>), dim3(dp_scatter_grid<DIR, ITEMS>(n)), dim3(DP_BLOCK), 0,
+                           c->stream, ls, n, S, nb, (const uint32_t*)(meta + BkMeta::BSTART), c->sp_cur.as<uint32_t>(),
+                           c->keysB.as<uint32_t>(), vpart, (uint32_t)cap, mm, (unsigned long long*)(sm + SM_BK_ESC));
+        GS_HIP(hipGetLastError());
+        hipEventRecord(c->pass_ev[2], c->stream);
+        hipEventRecord(c->ev[2], c->stream);
+        GS_TRY(launch_plan<P>(c, cap, nb, 0, 0, item_recs, c->sp_cur.as<uint32_t>(), c->sp_tot.as<uint32_t>(), mm));
+        part = true;
+        GS_TRY((bucket_accumulate<P>(c, PackSrc<Raw>{c->keysB.as<uint32_t>(), vpart}, cap, nb, base, o, 2,
+                                     c->sp_cur.as<uint32_t>())));
+        GS_TRY(host_wait(c));
+        if (!c->host_small[2]) {   // hit: every key in the range; the plan reported the occupied buckets
+          kmin = (int64_t)((uint64_t)base + (c->host_small[0] << S));
+          kmax = (int64_t)((uint64_t)base + (c->host_small[1] << S) + ((1ull << S) - 1));
+          break;
+        }
+        // missed (a run past its segment, or a key outside the range): rerun through the histogram,
+        // which measures the range (and reruns once more if the prediction missed it); the next 8
+        // windows do not speculate
+        c->sp_skip = 8;
+        spec = false;
+        spec_missed = true;
+        continue;
+      }
+    }
     // 1. per-tile bucket counts against the predicted base and width (the window's one read of
     //    the keys before the scatter) + the measured range and the keys outside the prediction
     GS_TRY((launch_dp_hist<DIR, ITEMS>(c, src, dst, n, nt, base, S, nb)));
@@ -295,7 +367,7 @@ gs_status bucket_direct_t(gs_ctx* c, const int64_t* src, const int64_t* dst, con
     hipLaunchKernelGGL(k_dp_up, g2, dim3(256), 0, c->stream, cnt, nt, nb, csum);
     hipLaunchKernelGGL(k_dp_spine, dim3((nb + 63) / 64), dim3(1024), 0, c->stream, csum, nch, nb, meta + BkMeta::HIST);
     GS_HIP(hipGetLastError());
-    GS_TRY(launch_plan<P>(c, R, nb, 0, 0, item_recs));
+    GS_TRY(launch_plan<P>(c, R, nb, 0, 0, item_recs, nullptr, pack ? c->sp_tot.as<uint32_t>() : nullptr));
     if (part) {
       hipLaunchKernelGGL(k_dp_down, g2, dim3(256), 0, c->stream, cnt, csum, meta + BkMeta::BSTART, nt, nb,
                          c->dp_off.as<uint32_t>());
@@ -342,7 +414,8 @@ gs_status bucket_direct_t(gs_ctx* c, const int64_t* src, const int64_t* dst, con
     kmax = key_max(c->host_small);
     if ((((uint64_t)kmax - (uint64_t)kmin) >> S) >= (uint64_t)BK_MAXB) return GS_EUNSUPPORTED;
     if (!c->host_small[2]) break;
-    if (attempt) return set_error(c, GS_EDEVICE, "bucket path: keys outside the measured vertex range");
+    if (attempt > (spec_missed ? 1 : 0))
+      return set_error(c, GS_EDEVICE, "bucket path: keys outside the measured vertex range");
     base = predict_base(kmin, kmax, S);   // missed prediction: rerun with the measured range
     nb = (uint32_t)((((uint64_t)kmax - (uint64_t)base) >> S) + 1);
   }
@@ -371,6 +444,16 @@ gs_status bucket_direct_t(gs_ctx* c, const int64_t* src, const int64_t* dst, con
   c->times.key_bytes = 2;
   c->times.escapes = esc;
   c->times.packed = pack ? 1u : 0u;
+  c->times.speculative = spec ? 1u : spec_missed ? 2u : 0u;
+  if constexpr (CAN_PACK) {   // the counts plan wrote to sp_tot are this geometry's
+    if (pack) {
+      c->sp_ok = true;
+      c->sp_base = base;
+      c->sp_S = S;
+      c->sp_dir = DIR;
+      c->sp_R = R;
+    }
+  }
   return GS_OK;
 }
 

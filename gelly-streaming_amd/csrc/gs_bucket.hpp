@@ -55,7 +55,35 @@ struct BkPlanOut {
   BkItem* items;
   uint32_t* n_items;       // device scalars
   uint32_t* n_multi;
+  // speculative partition (k_sp_scatter_pack): bucket_start holds the regions (read, not written),
+  // the counts are the cursors' advance (clamped to the region).  counts_out (either mode, optional):
+  // every bucket's count, which the next window's regions are sized from
+  const uint32_t* cursor = nullptr;
+  uint32_t* counts_out = nullptr;
+  unsigned long long* occupied = nullptr;   // speculative: [0] lowest, [1] highest bucket with records
 };
+
+// speculative partition: a bucket's region is split into SP_NSEG segments, one per XCD slot, each with
+// its own cursor (cursor[x * BK_MAXB + b]).  A region of e - s = T + SP_NSEG·SP_PADSEG records (T the
+// predicted count with its relative slack, 4-aligned) gives segment x its share of T,
+// T·pre[x] / pre[SP_NSEG] (pre[x] = the window's records in the tiles of slots before x, i.e.
+// k_sp_scatter_pack's tile -> slot map), plus SP_PADSEG records of absolute slack.
+#ifndef GS_SP_XCD
+#define GS_SP_XCD 1
+#endif
+constexpr uint32_t SP_NSEG = GS_SP_XCD ? 8 : 1;
+constexpr uint32_t SP_PAD = 1024;                  // absolute slack per bucket
+constexpr uint32_t SP_PADSEG = SP_PAD / SP_NSEG;   // ... per segment
+static_assert(SP_PADSEG % 4 == 0, "segment starts stay 4-aligned");
+struct SpSlots {
+  uint32_t pre[SP_NSEG + 1];
+};
+__host__ __device__ inline uint32_t sp_seg_start(uint32_t s, uint32_t e, uint32_t x, const uint32_t* pre) {
+  if (x == 0) return s;
+  if (x >= SP_NSEG) return e;
+  const uint32_t T = e - s - SP_NSEG * SP_PADSEG;
+  return s + ((uint32_t)((uint64_t)T * pre[x] / (pre[SP_NSEG] ? pre[SP_NSEG] : 1)) & ~3u) + x * SP_PADSEG;
+}
 
 // ---- policies: LDS accumulator layout and the op ------------------------------------------------
 template <typename T>
@@ -431,7 +459,18 @@ static __global__ __launch_bounds__(BK_PLAN_BLOCK) void k_bk_plan(const uint32_t
   __syncthreads();
   // two buckets per thread (BK_MAXB = 2 * BK_PLAN_BLOCK)
   const uint32_t b0 = 2 * tid, b1 = 2 * tid + 1;
-  const uint32_t c0 = b0 < nb ? hist[b0] : 0u, c1 = b1 < nb ? hist[b1] : 0u;
+  const bool spec = o.cursor != nullptr;
+  auto count = [&](uint32_t b) -> uint32_t {
+    if (b >= nb) return 0u;
+    if (!spec) return hist[b];
+    const uint32_t s0 = o.bucket_start[b], e0 = o.bucket_start[b + 1];
+    const uint32_t* pre = o.cursor + SP_NSEG * BK_MAXB;
+    uint32_t n = 0;
+    for (uint32_t x = 0; x < SP_NSEG; ++x)
+      n += min(o.cursor[x * BK_MAXB + b], sp_seg_start(s0, e0, x + 1, pre)) - sp_seg_start(s0, e0, x, pre);
+    return n;
+  };
+  const uint32_t c0 = count(b0), c1 = count(b1);
   const uint32_t dmask = (1u << w) - 1;
   for (int p = 0; p < passes; ++p) {
     if (c0) atomicAdd(&s_dh[p][(b0 >> (p * w)) & dmask], c0);
@@ -439,9 +478,32 @@ static __global__ __launch_bounds__(BK_PLAN_BLOCK) void k_bk_plan(const uint32_t
   }
   uint32_t total;
   const uint32_t start0 = bk_block_scan(c0 + c1, s_w, total);
-  if (b0 < nb) o.bucket_start[b0] = start0;
-  if (b1 < nb) o.bucket_start[b1] = start0 + c0;
-  if (tid == 0) o.bucket_start[nb] = total;
+  if (spec) {   // the occupied buckets (the next window's predicted range)
+    __shared__ uint32_t s_lo, s_hi;
+    if (tid == 0) {
+      s_lo = ~0u;
+      s_hi = 0;
+    }
+    __syncthreads();
+    if (c0 | c1) {
+      atomicMin(&s_lo, c0 ? b0 : b1);
+      atomicMax(&s_hi, c1 ? b1 : b0);
+    }
+    __syncthreads();
+    if (tid == 0) {
+      o.occupied[0] = s_lo;
+      o.occupied[1] = s_hi;
+    }
+  }
+  if (o.counts_out) {   // every bucket slot (0 past nb): the next window's regions read them
+    o.counts_out[b0] = c0;
+    o.counts_out[b1] = c1;
+  }
+  if (!spec) {
+    if (b0 < nb) o.bucket_start[b0] = start0;
+    if (b1 < nb) o.bucket_start[b1] = start0 + c0;
+    if (tid == 0) o.bucket_start[nb] = total;
+  }
   // digit bases (s_dh complete after the scan's barriers)
   if (tid < passes) {   // <= 256 digits per pass, one thread each
     uint32_t run = 0;
@@ -940,6 +1002,188 @@ void k_dp_scatter_pack(BaseSrc<V, DIR, PAY_VAL> es, uint64_t n, int S, uint32_t 
   if ((tid & 63) == 0 && esc) atomicAdd(n_esc, (unsigned long long)esc);
 }
 
+// ---- speculative partition: the packed scatter without a histogram pass -------------------------
+// Consecutive windows of one stream spread their records over the buckets alike (a bucket is the sum
+// of 2^S vertices' degrees).  So bucket b gets a REGION sized from the previous window's count of b
+// (k_sp_regions: t·R/R_prev + 1/16, 4-aligned, + SP_PAD records), and a tile reserves its run of each
+// bucket with one returning atomicAdd on b's cursor instead of reading the offsets that k_dp_hist +
+// the scans computed: the window's keys are read once, not twice, and the per-tile count / offset
+// matrices (0.1 GB at C2) go away.  The reservation is issued before the tile's records go through LDS
+// and used after, so its latency hides behind the LDS scatter.  Each XCD slot reserves from its own
+// segment of the region (GS_SP_XCD): runs written at the same time by one XCD's blocks stay adjacent
+// in one L2, and each cursor sees 1/8 of the atomics.  A run that would pass its segment's end is
+// written to a trash area instead, and a key outside the predicted range is dropped; both count in
+// mm[2], every later launch exits and the host reruns the window through k_dp_hist (which cannot
+// miss).  Record order inside a bucket follows the atomics: integer SUM / MIN / MAX only (exact in
+// any order).
+
+// bucket regions from the previous window's counts (one block): starts, cursors, mm reset
+static __global__ __launch_bounds__(BK_PLAN_BLOCK) void k_sp_regions(const uint32_t* __restrict__ prev, uint32_t nb,
+                                                                     uint64_t r_prev, uint64_t r_now,
+                                                                     uint32_t* __restrict__ bucket_start,
+                                                                     uint32_t* __restrict__ cursor, SpSlots slots,
+                                                                     unsigned long long* __restrict__ mm) {
+  __shared__ uint32_t s_w[BK_PLAN_BLOCK / WAVE];
+  const int tid = threadIdx.x;
+  const uint32_t b0 = 2 * tid, b1 = 2 * tid + 1;   // BK_MAXB = 2 * BK_PLAN_BLOCK
+  auto cap = [&](uint32_t b) -> uint32_t {
+    if (b >= nb) return 0u;
+    const uint64_t t = (uint64_t)prev[b] * r_now / (r_prev ? r_prev : 1);
+    return (uint32_t)((t + (t >> 4) + 3) & ~3ull) + SP_PAD;
+  };
+  const uint32_t c0 = cap(b0), c1 = cap(b1);
+  uint32_t total;
+  const uint32_t s0 = bk_block_scan(c0 + c1, s_w, total);
+  if (b0 < nb) bucket_start[b0] = s0;
+  if (b1 < nb) bucket_start[b1] = s0 + c0;
+  for (uint32_t x = 0; x < SP_NSEG; ++x) {
+    if (b0 < nb) cursor[x * BK_MAXB + b0] = sp_seg_start(s0, s0 + c0, x, slots.pre);
+    if (b1 < nb) cursor[x * BK_MAXB + b1] = sp_seg_start(s0 + c0, s0 + c0 + c1, x, slots.pre);
+  }
+  if (tid <= (int)SP_NSEG) cursor[SP_NSEG * BK_MAXB + tid] = slots.pre[tid];   // for the later kernels
+  if (tid == 0) bucket_start[nb] = total;
+  if (tid < 4) mm[tid] = 0;
+}
+
+// the host's bound on k_sp_regions' total (sum of t <= r_now)
+__host__ __device__ inline uint64_t sp_capacity(uint64_t r_now, uint32_t nb) {
+  return r_now + (r_now >> 4) + (uint64_t)nb * (SP_PAD + 4);
+}
+
+// Branch-free: a lane past the window's last record or holding a key outside the predicted range
+// ranks into the dummy bucket BK_MAXB, whose run (the tile's last) goes to the trash area, so every
+// tile -- the partial last one too -- stores all TILE slots in one unrolled loop.  The exact key
+// range is not tracked here: on a hit every key lay in the predicted range, and k_bk_plan reports the
+// occupied buckets for the next prediction; on a miss the window's rerun measures it.
+template <typename V, int DIR, int ITEMS>
+__global__ __launch_bounds__(DP_BLOCK) __attribute__((amdgpu_waves_per_eu(GS_PK_WAVES, GS_PK_WAVES)))
+void k_sp_scatter_pack(BaseSrc<V, DIR, PAY_VAL> es, uint64_t n, int S, uint32_t nbp,
+                       const uint32_t* __restrict__ bucket_start, uint32_t* __restrict__ cursor,
+                       uint32_t* __restrict__ rec, V* __restrict__ wide, uint32_t trash,
+                       unsigned long long* __restrict__ mm, unsigned long long* __restrict__ n_esc) {
+  constexpr uint32_t TILE = DP_BLOCK * ITEMS;
+  static_assert(ITEMS <= 32 && TILE <= 65536, "ranks and an escape's tile-local index are kept in 16 bits");
+  constexpr uint32_t ESC = 1u << 31, DUMMY = (uint32_t)BK_MAXB << 16;   // kb: escaped value / dummy bucket
+  __shared__ uint32_t s_key[TILE];         // ESC | (bucket << 16) | bucket-local index, bucket order
+  __shared__ uint16_t s_v16[TILE];         // narrow value, or an escape's tile-local record index
+  __shared__ uint32_t s_cnt[BK_MAXB + 1];  // counts, then run starts inside the tile (+ the dummy bucket)
+  __shared__ uint32_t s_delta[BK_MAXB + 1];   // global position - tile position of bucket b's run
+  __shared__ uint32_t s_w[DP_BLOCK / WAVE];
+  __shared__ uint32_t s_ovf[DP_BLOCK / WAVE];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  constexpr uint32_t TE = dp_tile_edges<DIR, ITEMS>();
+  const uint32_t nfull = (uint32_t)(n / TE);
+  const uint32_t lmask = (1u << S) - 1;
+  const uint32_t b0 = 2 * tid, b1 = 2 * tid + 1;   // BK_MAXB = 2 * DP_BLOCK
+  const uint32_t bl0 = min(b0, nbp - 1), bl1 = min(b1, nbp - 1);
+  uint32_t t, nrec = TILE;
+  if (blockIdx.x == gridDim.x - 1) {   // the window's partial last tile
+    if ((uint64_t)nfull * TE >= n) return;
+    t = nfull;
+    nrec = (uint32_t)((n - (uint64_t)nfull * TE) * (DIR == DIR_ALL ? 2 : 1));
+  } else {   // XCD slot b & 7 owns a contiguous range of full tiles (k_dp_scatter)
+    const uint32_t per = (nfull + 7) / 8;
+    t = (blockIdx.x & 7u) * per + (blockIdx.x >> 3);
+    if (t >= nfull) return;
+  }
+  const uint32_t r0 = t * TILE;
+  const uint32_t xs = SP_NSEG == 1 ? 0u : blockIdx.x & 7u;   // this block's XCD slot: its segment
+  const uint32_t* pre = cursor + SP_NSEG * BK_MAXB;
+  const uint32_t end0 = sp_seg_start(bucket_start[bl0], bucket_start[bl0 + 1], xs + 1, pre);
+  const uint32_t end1 = sp_seg_start(bucket_start[bl1], bucket_start[bl1 + 1], xs + 1, pre);
+  cursor += xs * BK_MAXB;
+  uint32_t kb[ITEMS], vr[ITEMS];   // vr: narrow value (or escape index) << 16 | rank in the tile's run
+  int64_t kk[ITEMS];
+  V vv[ITEMS];
+  // every load first, unconditional and clamped into the tile (k_dp_scatter)
+#pragma unroll
+  for (int u = 0; u < ITEMS; ++u) {
+    const uint32_t r = r0 + min((uint32_t)u * DP_BLOCK + tid, nrec - 1);
+    uint32_t i = r;
+    bool rev = DIR == DIR_IN;
+    if constexpr (DIR == DIR_ALL) {
+      i = r >> 1;
+      rev = r & 1u;
+    }
+    kk[u] = (rev ? es.dst : es.src)[i];
+    vv[u] = es.val[i];
+  }
+  uint32_t ovf = 0;
+#pragma unroll
+  for (int u = 0; u < ITEMS; ++u) {
+    const uint32_t j = (uint32_t)u * DP_BLOCK + tid;
+    const uint64_t d = (uint64_t)kk[u] - (uint64_t)es.base;
+    const bool in = (d >> S) < nbp, live = j < nrec;
+    ovf += (live && !in) ? 1u : 0u;
+    const uint32_t nv = pk_narrow(vv[u]);
+    const bool e = nv == PK_ESC;
+    kb[u] = (live && in) ? ((uint32_t)(d >> S) << 16) | ((uint32_t)d & lmask) | (e ? ESC : 0u) : DUMMY;
+    vr[u] = (e ? j : nv) << 16;
+  }
+  for (uint32_t i = tid; i < nbp; i += DP_BLOCK) s_cnt[i] = 0;
+  if (tid == 0) s_cnt[BK_MAXB] = 0;
+  __syncthreads();
+#pragma unroll
+  for (int u = 0; u < ITEMS; ++u) vr[u] |= atomicAdd(&s_cnt[(kb[u] >> 16) & 0x7FFFu], 1u);
+  __syncthreads();
+  const uint32_t c0 = b0 < nbp ? s_cnt[b0] : 0u, c1 = b1 < nbp ? s_cnt[b1] : 0u;
+  // reserve the runs now; the returned offsets are needed only after the LDS scatter
+  const uint32_t o0 = c0 ? atomicAdd(&cursor[b0], c0) : 0u;
+  const uint32_t o1 = c1 ? atomicAdd(&cursor[b1], c1) : 0u;
+  uint32_t total;
+  const uint32_t st0 = bk_block_scan(c0 + c1, s_w, total);   // total: records in the predicted range
+  s_cnt[b0] = st0;   // unconditional: entries past nbp are never read
+  s_cnt[b1] = st0 + c0;
+  if (tid == 0) s_cnt[BK_MAXB] = total;   // the dummy run: the tile's last
+  __syncthreads();
+#pragma unroll
+  for (int u = 0; u < ITEMS; ++u) {
+    const uint32_t pos = s_cnt[(kb[u] >> 16) & 0x7FFFu] + (vr[u] & 0xFFFFu);
+    s_key[pos] = kb[u];
+    s_v16[pos] = (uint16_t)(vr[u] >> 16);
+  }
+  // a run that does not fit its segment goes to the trash area [trash, trash + TILE) past every
+  // region instead (nothing reads the trash)
+  const bool drop0 = c0 && o0 + c0 > end0, drop1 = c1 && o1 + c1 > end1;
+  s_delta[b0] = (drop0 ? trash : o0) - st0;
+  s_delta[b1] = (drop1 ? trash : o1) - (st0 + c0);
+  if (tid == 0) s_delta[BK_MAXB] = trash;
+  ovf += (drop0 ? 1u : 0u) + (drop1 ? 1u : 0u);
+  __syncthreads();
+  // stores without a branch; escaped values (PK_ESC in the record) after the loop, rarely taken
+  uint32_t escm = 0;
+#pragma unroll
+  for (int u = 0; u < ITEMS; ++u) {
+    const uint32_t j = (uint32_t)u * DP_BLOCK + tid;
+    const uint32_t kv = s_key[j];
+    const bool e = kv & ESC;
+    rec[s_delta[(kv >> 16) & 0x7FFFu] + j] = (kv & 0xFFFFu) | ((e ? PK_ESC : (uint32_t)s_v16[j]) << 16);
+    escm |= e ? 1u << u : 0u;
+  }
+  uint32_t esc = 0;
+  for (; escm; escm &= escm - 1, ++esc) {   // the full value from the column into the slot of `wide`
+    const uint32_t j = (uint32_t)__builtin_ctz(escm) * DP_BLOCK + tid;
+    const uint32_t kv = s_key[j];
+    const uint32_t r = r0 + s_v16[j];
+    wide[s_delta[(kv >> 16) & 0x7FFFu] + j] = es.val[DIR == DIR_ALL ? r >> 1 : r];
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    esc += __shfl_xor(esc, o, WAVE);
+    ovf += __shfl_xor(ovf, o, WAVE);
+  }
+  if (lane == 0) {
+    if (esc) atomicAdd(n_esc, (unsigned long long)esc);
+    s_ovf[w] = ovf;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    uint32_t o2 = 0;
+    for (int i = 0; i < DP_BLOCK / WAVE; ++i) o2 += s_ovf[i];
+    if (o2) atomicAdd(&mm[2], (unsigned long long)o2);
+  }
+}
+
 // ---- k_bk_accum: persistent; LDS accumulation of (bucket, record range) items ---------------------
 // Finalize (shared with k_bk_merge): the bucket's vertices in ascending order -> staging at the
 // bucket's record offset (a bucket has at least as many records as vertices).
@@ -982,7 +1226,8 @@ __global__ __launch_bounds__(BK_ACC_BLOCK) void k_bk_accum(Src src, const BkItem
                                                            uint32_t* __restrict__ ctr,
                                                            typename P::Lds* __restrict__ slabs, BkStage st,
                                                            uint32_t* __restrict__ bucket_count,
-                                                           const unsigned long long* __restrict__ mm) {
+                                                           const unsigned long long* __restrict__ mm,
+                                                           const uint32_t* __restrict__ seg_cur) {
   __shared__ typename P::Lds s;
   __shared__ uint32_t s_item;
   __shared__ uint32_t s_wc[BK_NW];
@@ -999,7 +1244,7 @@ __global__ __launch_bounds__(BK_ACC_BLOCK) void k_bk_accum(Src src, const BkItem
     const uint32_t b0 = bucket_start[m.bucket];
     P::init(s, tid);
     __syncthreads();
-    const uint32_t r0 = b0 + m.begin, r1 = b0 + m.end;
+    auto range = [&](uint32_t r0, uint32_t r1) {   // records [r0, r1) of the partition into LDS
     if constexpr (is_pack_src<Src>::value) {
       // 16-byte loads (4 records per lane per load: 4x the bytes in flight of 4-byte loads; the
       // 4-byte version was latency-bound); an unaligned head and the tail record by record
@@ -1044,6 +1289,21 @@ __global__ __launch_bounds__(BK_ACC_BLOCK) void k_bk_accum(Src src, const BkItem
           const uint32_t q = r + (uint32_t)u * BK_ACC_BLOCK;
           if (q < r1) P::add(s, k[u] & (P::W - 1), v[u]);
         }
+      }
+    }
+    };
+    if (!seg_cur) {
+      range(b0 + m.begin, b0 + m.end);
+    } else {   // speculative partition: the item's span of the bucket's SP_NSEG segments, in order
+      const uint32_t e0 = bucket_start[m.bucket + 1];
+      const uint32_t* pre = seg_cur + SP_NSEG * BK_MAXB;
+      uint32_t at = 0;   // records of the bucket in the segments before x
+      for (uint32_t x = 0; x < SP_NSEG && at < m.end; ++x) {
+        const uint32_t sg = sp_seg_start(b0, e0, x, pre);
+        const uint32_t nx = min(seg_cur[x * BK_MAXB + m.bucket], sp_seg_start(b0, e0, x + 1, pre)) - sg;
+        const uint32_t lo = max(m.begin, at), hi = min(m.end, at + nx);
+        if (lo < hi) range(sg + (lo - at), sg + (hi - at));
+        at += nx;
       }
     }
     __syncthreads();

@@ -65,14 +65,15 @@ class StageTimes:
                            # components (compact IDs, union-find, labels)
     packed: bool = False   # path 2: 4-byte packed partition records (k_dp_scatter_pack)
     escapes: int = 0       # path 2, packed: values stored in full
+    speculative: int = 0   # path 2, packed: 1 = regions from the previous window's counts, 2 = that missed
 
 
 class Engine:
     def __init__(self, device: int = 0, reserve_edges: int = 0, torch_stream: bool = True, sort_only: bool = False,
-                 bk_onesweep: bool = False, no_pack: bool = False, flags: int = 0):
+                 bk_onesweep: bool = False, no_pack: bool = False, no_spec: bool = False, flags: int = 0):
         self._L = L.load()
         flags |= (L.GS_FLAG_SORT_ONLY if sort_only else 0) | (L.GS_FLAG_BK_ONESWEEP if bk_onesweep else 0) | \
-            (L.GS_FLAG_NO_PACK if no_pack else 0)
+            (L.GS_FLAG_NO_PACK if no_pack else 0) | (L.GS_FLAG_NO_SPEC if no_spec else 0)
         cfg = L.GsConfig(device, flags, reserve_edges)
         ctx = ctypes.c_void_p()
         st = self._L.gs_create(ctypes.byref(cfg), ctypes.byref(ctx))
@@ -126,7 +127,7 @@ class Engine:
             t.sort_passes + (3 if t.path == 1 else 1 if t.fused_last else 0)
         return StageTimes(t.keyinfo_ms, t.sort_ms, t.reduce_ms, t.total_ms, t.sort_passes, t.key_bits, t.records,
                           t.vertices, list(t.pass_ms)[:launched], t.key_bytes, t.payload_bytes,
-                          t.partials, bool(t.fused_last), t.path, bool(t.packed), t.escapes)
+                          t.partials, bool(t.fused_last), t.path, bool(t.packed), t.escapes, t.speculative)
 
     # -- helpers ---------------------------------------------------------------------------------
     def _batch(self, src, dst, val):

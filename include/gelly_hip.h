@@ -88,6 +88,8 @@ typedef struct gs_ctx gs_ctx;
                                   instead of 4-byte packed records (A/B measurement; same results)  */
 #define GS_FLAG_TEST_TINY_TABLES 8u /* TEST ONLY: triangle counting sizes its LDS hash sets at one
                                   bucket, so sets overflow and the call must fail with GS_EDEVICE   */
+#define GS_FLAG_NO_SPEC 16u    /* bucket path: no speculative partition (packed windows always count
+                                  per-tile bucket histograms first; A/B measurement; same results)  */
 
 typedef struct gs_config {
   int32_t device;          /* HIP device ordinal                                           */
@@ -452,7 +454,10 @@ typedef struct gs_stage_times {
                                  adjacency entries, vertices = vertices with edges, partials = hash
                                  probes of the counting step, sort_passes = LSD passes)          */
   uint32_t packed;         /* path 2: 1 = 4-byte packed partition records (k_dp_scatter_pack)    */
-  uint32_t reserved;
+  uint32_t speculative;    /* path 2, packed: 0 = per-tile histogram + offsets (k_dp_hist);
+                              1 = speculative partition (regions from the previous window's counts,
+                                  runs reserved with atomics: keyinfo_ms = regions, pass_ms[0] = 0);
+                              2 = speculative partition missed, window rerun through k_dp_hist   */
   uint64_t escapes;        /* path 2, packed: values stored in full (outside [0, 0xFFFF))          */
 } gs_stage_times;
 GS_API gs_status gs_last_stage_times(const gs_ctx* ctx, gs_stage_times* out);

@@ -273,3 +273,51 @@ def test_packed_prediction_miss_reruns(pkg, oracle):
             gk, gv = e.reduce(*_dev(s, d, v), 1, 0)
             assert e.stage_times().path == 2
             _check(gk, gv, rk, rv, np.int64, 0)
+
+
+@pytest.mark.parametrize("direction,dtype,op", [(1, np.int64, 0), (0, np.int64, 0), (2, np.int64, 0),
+                                                (1, np.int32, 1), (2, np.int64, 2)])
+def test_speculative_partition(pkg, oracle, direction, dtype, op):
+    """k_sp_scatter_pack: a packed window whose bucket counts the ctx's previous packed window measured in
+    the same geometry (base, S, direction) sizes one region per bucket from them and reserves each tile's
+    runs with atomics on per-bucket cursors -- no histogram pass.  Hits (incl. a hub bucket of several
+    work items, escaped values, a larger window), a window crowding half its records into one bucket
+    (regions overflow) and a key outside the predicted range all end bit-exact against the oracle and
+    the histogram path (GS_FLAG_NO_SPEC); a miss reruns the window through the histogram
+    (speculative == 2) and the next 8 windows do not speculate."""
+    rng = np.random.default_rng(4242 + 10 * direction + op)
+    n = 300_001
+
+    def win(m, span=1 << 22):
+        s, d = _window(rng, m, span, hub_frac=0.1)
+        v = rng.integers(0, 0xFFFF, m)
+        v[rng.random(m) < 0.001] = -(1 << 40) if dtype == np.int64 else -(1 << 30)   # escapes
+        return s, d, v.astype(dtype)
+
+    with pkg.Engine(0) as e, pkg.Engine(0, no_spec=True) as ex:
+        def run(s, d, v, expect):
+            rk, rv = oracle.window_reduce(s, d, v, direction, op)
+            gk, gv = e.reduce(*_dev(s, d, v), direction, op)
+            t = e.stage_times()
+            assert t.path == 2 and t.packed
+            _check(gk, gv, rk, rv, dtype, op)
+            xk, xv = ex.reduce(*_dev(s, d, v), direction, op)
+            assert ex.stage_times().speculative == 0
+            assert torch.equal(gk, xk) and torch.equal(gv, xv)
+            assert t.speculative == expect, (t.speculative, expect)
+
+        run(*win(n), 0)            # first window: histogram (nothing to predict from)
+        for _ in range(4):
+            run(*win(n), 1)
+        run(*win(n * 3 // 2), 1)   # regions scale with the record count
+        s, d, v = win(n)
+        (s if direction != 0 else d)[: n // 2] = 12345   # half the records in bucket 0: regions overflow
+        if direction == 2:
+            d[: n // 2] = 12345
+        run(s, d, v, 2)
+        for _ in range(8):
+            run(*win(n), 0)
+        run(*win(n), 1)
+        s, d, v = win(n)
+        s[n // 3] = d[n // 3] = (1 << 23) + 5   # outside the predicted bucket count
+        run(s, d, v, 2)
