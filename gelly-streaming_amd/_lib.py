@@ -33,7 +33,8 @@ GS_DTYPE_OF = {np.dtype(np.int32): GS_I32, np.dtype(np.int64): GS_I64, np.dtype(
 # every symbol include/gelly_hip.h declares (checked by tests/test_abi.py)
 EXPORTS = ("gs_abi_version", "gs_create", "gs_destroy", "gs_last_error", "gs_set_stream", "gs_synchronize",
            "gs_alloc_pinned", "gs_free_pinned", "gs_window_reduce", "gs_window_fold",
-           "gs_window_fold_degree_max", "gs_window_csr", "gs_window_candidates", "gs_window_triangles",
+           "gs_window_fold_degree_max", "gs_window_csr", "gs_window_candidates", "gs_window_candidates_part",
+           "gs_window_triangles",
            "gs_window_triangles_part", "gs_window_count_candidates", "gs_tri_dist_range", "gs_tri_dist_degrees",
            "gs_tri_dist_route", "gs_tri_dist_build", "gs_tri_dist_count", "gs_window_triangles_selfpair",
            "gs_window_triangles_dist", "gs_window_components",
@@ -155,6 +156,7 @@ def load() -> ctypes.CDLL:
         "gs_window_fold_degree_max": (st, [P, ctypes.POINTER(GsEdgeBatch), i32, i64, ctypes.POINTER(GsDegreeOut)]),
         "gs_window_csr": (st, [P, ctypes.POINTER(GsEdgeBatch), i32, ctypes.POINTER(GsCsrOut)]),
         "gs_window_candidates": (st, [P, ctypes.POINTER(GsEdgeBatch), ctypes.POINTER(GsPairOut)]),
+        "gs_window_candidates_part": (st, [P, ctypes.POINTER(GsEdgeBatch), u32, u32, ctypes.POINTER(GsPairOut)]),
         "gs_window_triangles": (st, [P, ctypes.POINTER(GsEdgeBatch), ctypes.POINTER(u64), ctypes.POINTER(i32),
                                      ctypes.POINTER(i32)]),
         "gs_window_triangles_part": (st, [P, ctypes.POINTER(GsEdgeBatch), u32, u32, ctypes.POINTER(u64)]),

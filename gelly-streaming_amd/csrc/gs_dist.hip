@@ -27,15 +27,7 @@
 
 namespace gs {
 
-__host__ __device__ inline uint32_t owner_of(int64_t v, uint32_t nparts) {
-  uint64_t x = (uint64_t)v;
-  x ^= x >> 33;
-  x *= 0xff51afd7ed558ccdull;
-  x ^= x >> 33;
-  x *= 0xc4ceb9fe1a85ec53ull;
-  x ^= x >> 33;
-  return (uint32_t)(((x >> 32) * (uint64_t)nparts) >> 32);
-}
+// owner_of: gs_ops.hpp (shared with the candidate split, gs_hashset.hip)
 
 constexpr int OW_BLOCK = 256, OW_ITEMS = 16, OW_TILE = OW_BLOCK * OW_ITEMS, OW_MAXP = 64;
 

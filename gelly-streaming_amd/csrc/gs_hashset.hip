@@ -195,27 +195,41 @@ __global__ __launch_bounds__(256) void k_hs_gt(const int64_t* __restrict__ ids, 
   }
 }
 
-// row q emits (ids[q], ids[j]) for j >= q with ids[j] > v; only rows q < end-1 with ids[q] > v (:104, :108)
+// row q emits (ids[q], ids[j]) for j >= q with ids[j] > v; only rows q < end-1 with ids[q] > v (:104, :108);
+// with a split (nparts > 1) only vertices this part owns emit
 __global__ __launch_bounds__(256) void k_hs_rowlen(const uint64_t* __restrict__ gx, uint32_t M,
                                                    const uint64_t* __restrict__ doff, uint32_t U,
                                                    const int64_t* __restrict__ ids, const int64_t* __restrict__ vkeys,
-                                                   uint64_t* __restrict__ L) {
+                                                   uint32_t nparts, uint32_t part, uint64_t* __restrict__ L) {
   for (uint32_t q = blockIdx.x * 256u + threadIdx.x; q < M; q += gridDim.x * 256u) {
     const uint32_t u = seg_of(doff, U, q);
     const uint64_t end = doff[u + 1];
     const bool gt = ids[q] > vkeys[u];
-    L[q] = (gt && q + 1 < end) ? (gx[end] - gx[q]) : 0ull;
+    const bool own = nparts <= 1 || owner_of(vkeys[u], nparts) == part;
+    L[q] = (own && gt && q + 1 < end) ? (gx[end] - gx[q]) : 0ull;
   }
 }
 
+// owned vertices' record counts (their edge records, in the split's output order)
+__global__ __launch_bounds__(256) void k_hs_owned_recs(const uint64_t* __restrict__ off, uint32_t U,
+                                                       const int64_t* __restrict__ vkeys, uint32_t nparts, uint32_t part,
+                                                       uint64_t* __restrict__ F) {
+  for (uint32_t u = blockIdx.x * 256u + threadIdx.x; u < U; u += gridDim.x * 256u)
+    F[u] = owner_of(vkeys[u], nparts) == part ? off[u + 1] - off[u] : 0ull;
+}
+
+// record p of vertex u -> position fo[u] + (p - off[u]) + LS[doff[u]] (fo == off without a split)
 __global__ __launch_bounds__(256) void k_hs_emit_false(uint32_t R, const uint32_t* __restrict__ useg,
+                                                       const uint64_t* __restrict__ off, const uint64_t* __restrict__ fo,
                                                        const uint64_t* __restrict__ doff, const uint64_t* __restrict__ LS,
                                                        const int64_t* __restrict__ vkeys, const int64_t* __restrict__ nbr,
+                                                       uint32_t nparts, uint32_t part,
                                                        int64_t* __restrict__ a, int64_t* __restrict__ b,
                                                        uint8_t* __restrict__ f) {
   for (uint32_t p = blockIdx.x * 256u + threadIdx.x; p < R; p += gridDim.x * 256u) {
     const uint32_t u = useg[p];
-    const uint64_t pos = p + LS[doff[u]];
+    if (nparts > 1 && owner_of(vkeys[u], nparts) != part) continue;
+    const uint64_t pos = fo[u] + (p - off[u]) + LS[doff[u]];
     a[pos] = vkeys[u];
     b[pos] = nbr[p];
     f[pos] = 0;
@@ -641,7 +655,7 @@ namespace gs {
 
 enum { HS_VKEYS, HS_OFF, HS_NBR, HS_USEG, HS_COMP, HS_PIDX, HS_DKEY, HS_DFIRST, HS_DOFF, HS_OKEY, HS_OMID,
        HS_UKEY, HS_ORD, HS_IDS, HS_G, HS_GX, HS_L, HS_LS, HS_TILES, HS_F, HS_FX, HS_CSZ, HS_CBASE, HS_CNT, HS_CPLX,
-       HS_CLIST, HS_TSZ, HS_TBASE, HS_ARR, HS_NODES, HS_TABS, HS_COUNT };
+       HS_CLIST, HS_TSZ, HS_TBASE, HS_ARR, HS_NODES, HS_TABS, HS_FO, HS_COUNT };
 static_assert(HS_COUNT <= 32, "gs_ctx::hs");
 
 gs_status xscan(gs_ctx* c, const uint64_t* in, uint64_t n, uint64_t* out) {
@@ -824,10 +838,12 @@ gs_status triangle_selfpair_term(gs_ctx* c, const int64_t* src, const int64_t* d
 
 extern "C" {
 
-gs_status gs_window_candidates(gs_ctx* c, const gs_edge_batch* b, gs_pair_out* out) {
+gs_status gs_window_candidates_part(gs_ctx* c, const gs_edge_batch* b, uint32_t nparts, uint32_t part,
+                                    gs_pair_out* out) {
   GS_TRY(check_batch(c, b, GS_DIR_ALL));
   if (!out || !out->n_out || (out->capacity && (!out->a || !out->b || !out->is_candidate)))
     return set_error(c, GS_EINVAL, "bad gs_pair_out");
+  if (nparts == 0 || part >= nparts) return set_error(c, GS_EINVAL, "part %u of %u", part, nparts);
   GS_TRY(begin_call(c));
   out->reserved = 0;
   if (b->n == 0) {
@@ -854,14 +870,27 @@ gs_status gs_window_candidates(gs_ctx* c, const gs_edge_batch* b, gs_pair_out* o
   GS_TRY(xscan(c, c->hs[HS_G].as<uint64_t>(), M, c->hs[HS_GX].as<uint64_t>()));
   hipLaunchKernelGGL(k_hs_rowlen, dim3(g256(M)), dim3(256), 0, c->stream, c->hs[HS_GX].as<uint64_t>(), M,
                      c->hs[HS_DOFF].as<uint64_t>(), U, c->hs[HS_IDS].as<int64_t>(), c->hs[HS_VKEYS].as<int64_t>(),
-                     c->hs[HS_L].as<uint64_t>());
+                     nparts, part, c->hs[HS_L].as<uint64_t>());
   GS_HIP(hipGetLastError());
   GS_TRY(xscan(c, c->hs[HS_L].as<uint64_t>(), M, c->hs[HS_LS].as<uint64_t>()));
-  uint64_t P = 0;
+  // output position of each vertex's records: the record CSR (every vertex), or, with a split, the
+  // scan of the owned vertices' record counts
+  const uint64_t* off = c->hs[HS_OFF].as<uint64_t>();
+  const uint64_t* fo = off;
+  if (nparts > 1) {
+    GS_TRY(ensure(c, c->hs[HS_FO], (size_t)(U + 1) * 8 * 2));
+    uint64_t* F = c->hs[HS_FO].as<uint64_t>() + (U + 1);
+    hipLaunchKernelGGL(k_hs_owned_recs, dim3(g256(U)), dim3(256), 0, c->stream, off, U, c->hs[HS_VKEYS].as<int64_t>(),
+                       nparts, part, F);
+    GS_HIP(hipGetLastError());
+    GS_TRY(xscan(c, F, U, c->hs[HS_FO].as<uint64_t>()));
+    fo = c->hs[HS_FO].as<uint64_t>();
+  }
   GS_HIP(hipMemcpyAsync(&c->host_small[7], c->hs[HS_LS].as<uint64_t>() + M, 8, hipMemcpyDeviceToHost, c->stream));
+  GS_HIP(hipMemcpyAsync(&c->host_small[6], fo + U, 8, hipMemcpyDeviceToHost, c->stream));
   GS_TRY(host_wait(c));
-  P = c->host_small[7];
-  const uint64_t total = R + P;
+  const uint64_t P = c->host_small[7];
+  const uint64_t total = c->host_small[6] + P;   // edge records (R without a split) + pairs
   *out->n_out = total;
   if (total > out->capacity) return set_error(c, GS_ECAPACITY, "candidates need %llu records", (unsigned long long)total);
   int64_t *a = out->a, *bb = out->b;
@@ -876,10 +905,10 @@ gs_status gs_window_candidates(gs_ctx* c, const gs_edge_batch* b, gs_pair_out* o
     f = c->out_b.as<uint8_t>();
   }
   hipLaunchKernelGGL(k_hs_emit_false, dim3(g256(R)), dim3(256), 0, c->stream, (uint32_t)R, c->hs[HS_USEG].as<uint32_t>(),
-                     c->hs[HS_DOFF].as<uint64_t>(), c->hs[HS_LS].as<uint64_t>(), c->hs[HS_VKEYS].as<int64_t>(),
-                     c->hs[HS_NBR].as<int64_t>(), a, bb, f);
+                     off, fo, c->hs[HS_DOFF].as<uint64_t>(), c->hs[HS_LS].as<uint64_t>(), c->hs[HS_VKEYS].as<int64_t>(),
+                     c->hs[HS_NBR].as<int64_t>(), nparts, part, a, bb, f);
   hipLaunchKernelGGL(k_hs_emit_pairs, dim3(g256(M)), dim3(256), 0, c->stream, M, c->hs[HS_DOFF].as<uint64_t>(), U,
-                     c->hs[HS_OFF].as<uint64_t>(), c->hs[HS_LS].as<uint64_t>(), c->hs[HS_IDS].as<int64_t>(),
+                     fo, c->hs[HS_LS].as<uint64_t>(), c->hs[HS_IDS].as<int64_t>(),
                      c->hs[HS_VKEYS].as<int64_t>(), a, bb, f);
   GS_HIP(hipGetLastError());
   if (!direct) {
@@ -889,6 +918,10 @@ gs_status gs_window_candidates(gs_ctx* c, const gs_edge_batch* b, gs_pair_out* o
   }
   GS_TRY(host_wait(c));
   return GS_OK;
+}
+
+gs_status gs_window_candidates(gs_ctx* c, const gs_edge_batch* b, gs_pair_out* out) {
+  return gs_window_candidates_part(c, b, 1, 0, out);
 }
 
 }  // extern "C"

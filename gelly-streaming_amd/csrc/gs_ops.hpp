@@ -16,6 +16,17 @@
 
 namespace gs {
 
+// owner(v) of the multi-GPU keyBy (gs_owner_of): a murmur3 finaliser of the vertex, scaled to nparts
+__host__ __device__ inline uint32_t owner_of(int64_t v, uint32_t nparts) {
+  uint64_t x = (uint64_t)v;
+  x ^= x >> 33;
+  x *= 0xff51afd7ed558ccdull;
+  x ^= x >> 33;
+  x *= 0xc4ceb9fe1a85ec53ull;
+  x ^= x >> 33;
+  return (uint32_t)(((x >> 32) * (uint64_t)nparts) >> 32);
+}
+
 // tile shapes (overridable with -D for tuning builds: make VARIANT="-DGS_SORT_ITEMS=24")
 #ifndef GS_SORT_BLOCK
 #define GS_SORT_BLOCK 512

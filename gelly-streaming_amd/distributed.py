@@ -97,6 +97,57 @@ def fold_degree_max_window(partials, merge, src, dst, direction: int, init_max: 
     return merge(rk, rd, rm, init_max)
 
 
+def owner_of(v: torch.Tensor, nparts: int) -> torch.Tensor:
+    """gs_owner_of on a tensor (murmur3 fmix64 of the vertex, multiply-high by nparts) in int64
+    arithmetic: products wrap mod 2^64, right shifts are masked to logical shifts."""
+    m31, m32 = (1 << 31) - 1, (1 << 32) - 1
+    c1, c2 = 0xFF51AFD7ED558CCD - (1 << 64), 0xC4CEB9FE1A85EC53 - (1 << 64)
+    x = v.to(torch.int64)
+    x = x ^ ((x >> 33) & m31)
+    x = x * c1
+    x = x ^ ((x >> 33) & m31)
+    x = x * c2
+    x = x ^ ((x >> 33) & m31)
+    return (((x >> 32) & m32) * nparts) >> 32
+
+
+def route_edges_to_owners(src: torch.Tensor, dst: torch.Tensor, group=None):
+    """Every edge (a, b) of this rank's slice goes to owner(a) and to owner(b) (once when they are the
+    same rank), local order kept; each rank receives its edges concatenated in rank order (= stream
+    order when rank r holds the r-th slice of the window).  Returns (src, dst) on src's device."""
+    world = dist.get_world_size(group)
+    home = src.device
+    n = src.numel()
+    oa, ob = owner_of(src, world), owner_of(dst, world)
+    e = torch.arange(n, device=home)
+    two = ob != oa
+    dest = torch.cat([oa, ob[two]])
+    idx = torch.cat([e, e[two]])
+    order = torch.argsort(dest * max(n, 1) + idx)   # by destination, then by position in the slice
+    idx = idx[order]
+    counts = torch.bincount(dest, minlength=world)
+    cdev = _comm_device(group, src)
+    recv_counts = torch.empty_like(counts, device=cdev)
+    dist.all_to_all_single(recv_counts, counts.to(cdev), group=group)
+    sc, rc = counts.tolist(), recv_counts.tolist()
+    rows = torch.stack([src[idx], dst[idx]], dim=1).contiguous().to(cdev)
+    got = torch.empty((sum(rc), 2), dtype=src.dtype, device=cdev)
+    dist.all_to_all_single(got, rows, rc, sc, group=group)
+    got = got.to(home)
+    return got[:, 0].contiguous(), got[:, 1].contiguous()
+
+
+def candidates_window(candidates_part, src, dst, group=None):
+    """applyOnNeighbors(GenerateCandidateEdges) over a window spread over the ranks:
+    edges routed to the owners of their endpoints, then each rank emits the candidate records of the
+    vertices it owns -- candidates_part(src, dst, nparts, part) -> (a, b, is_candidate), e.g.
+    Engine.candidates (gs_window_candidates_part).  The union over ranks is the whole window's output;
+    no candidate pair crosses ranks."""
+    world, rank = dist.get_world_size(group), dist.get_rank(group)
+    rs, rd = route_edges_to_owners(src, dst, group) if world > 1 else (src, dst)
+    return candidates_part(rs, rd, world, rank)
+
+
 def engine_halves(eng):
     """The Engine's partials / merge entry points in the shape reduce_window / fold_degree_max_window take."""
     return (eng.reduce_partials, eng.merge_partials, eng.fold_degree_max_partials, eng.merge_degree_max_partials)

@@ -214,14 +214,16 @@ class Engine:
         U, RR = nv.value, nr.value
         return keys[:U], offs[:U + 1], nbrs[:RR], (None if vals is None else vals[:RR])
 
-    def candidates(self, src, dst):
+    def candidates(self, src, dst, nparts: int = 1, part: int = 0):
         """gs_window_candidates: GenerateCandidateEdges records (a, b, is_candidate), ids in exact JDK
         HashSet order.  self.last_candidates_jdk_flags: bit 0 = some neighbour set used a treeified
-        HashMap bin, bit 1 = a bin of 9 forced a resize below capacity 64 (both simulated exactly)."""
+        HashMap bin, bit 1 = a bin of 9 forced a resize below capacity 64 (both simulated exactly).
+        nparts > 1: gs_window_candidates_part, only the vertices gs_owner_of assigns to `part`."""
         b, keep, dev = self._batch(src, dst, None)
         n_out = ctypes.c_uint64(0)
+        call = lambda o: self._L.gs_window_candidates_part(self.ctx, ctypes.byref(b), nparts, part, ctypes.byref(o))
         probe = L.GsPairOut(None, None, None, 0, ctypes.pointer(n_out), L.GS_MEM_DEVICE if dev else L.GS_MEM_HOST, 0)
-        st = self._L.gs_window_candidates(self.ctx, ctypes.byref(b), ctypes.byref(probe))
+        st = call(probe)
         if st not in (L.GS_OK, L.GS_ECAPACITY):
             self._check(st)
         P = n_out.value
@@ -229,7 +231,7 @@ class Engine:
         f = self._empty(dev, P, np.uint8)
         out = L.GsPairOut(_ptr(a), _ptr(bb), _ptr(f), P, ctypes.pointer(n_out),
                           L.GS_MEM_DEVICE if dev else L.GS_MEM_HOST, 0)
-        self._check(self._L.gs_window_candidates(self.ctx, ctypes.byref(b), ctypes.byref(out)))
+        self._check(call(out))
         self.last_candidates_jdk_flags = int(out.reserved)
         return a[:P], bb[:P], f[:P]
 

@@ -201,6 +201,14 @@ GS_API gs_status gs_window_csr(gs_ctx* ctx, const gs_edge_batch* batch, int32_t 
  * collision resize. */
 GS_API gs_status gs_window_candidates(gs_ctx* ctx, const gs_edge_batch* batch, gs_pair_out* out);
 
+/* Multi-GPU candidates (partition by owner(v), no exchange of pairs): only the vertices
+ * v with gs_owner_of(v, nparts) == part emit, with exactly the records gs_window_candidates gives them
+ * over the same batch.  The batch must hold every edge incident to those vertices, in stream order
+ * (distributed.candidates_window routes each edge to the owners of its two endpoints, rank order
+ * = stream order); the union over parts is the whole window's output. */
+GS_API gs_status gs_window_candidates_part(gs_ctx* ctx, const gs_edge_batch* batch, uint32_t nparts,
+                                           uint32_t part, gs_pair_out* out);
+
 /* The whole WindowTriangles pipeline for one window (WindowTriangles.java:61-66):
  * slice(ALL) -> GenerateCandidateEdges -> keyBy(0,1) CountTriangles -> timeWindowAll sum(0).
  * *count is the exact 64-bit count; *count_ref_wrapped is the Integer the reference emits

@@ -145,6 +145,40 @@ class OracleTriEngine:
         return self.orc.window_triangles_ref(s, d)[1] - self.tri_dist_count(nbr, dp, 0, 1)
 
 
+def candidate_groups(a, b, f):
+    """GenerateCandidateEdges output split per emitting vertex: a vertex's rows start with its
+    (v, neighbour, false) records, so row i belongs to a[last false row <= i]."""
+    a, b, f = (np.asarray(x) for x in (a, b, f))
+    idx = np.maximum.accumulate(np.where(f == 0, np.arange(len(f)), -1))
+    v = a[idx]
+    starts = np.flatnonzero(np.r_[True, v[1:] != v[:-1]])
+    ends = np.r_[starts[1:], len(v)]
+    return {int(v[s0]): (a[s0:e0], b[s0:e0], f[s0:e0]) for s0, e0 in zip(starts, ends)}
+
+
+def oracle_candidates_part(orc):
+    """gs_window_candidates_part restated: the oracle's window output, rows of owned vertices only."""
+    def part_fn(src, dst, nparts, part):
+        a, b, f, _ = orc.window_candidates(src.numpy(), dst.numpy())
+        idx = np.maximum.accumulate(np.where(f == 0, np.arange(len(f)), -1))
+        keep = owner_np(a[idx], nparts) == part
+        return a[keep], b[keep], f[keep]
+    return part_fn
+
+
+def check_candidates_split(outs, full):
+    """Every vertex's rows come from exactly one rank and equal the whole window's rows for it."""
+    want = candidate_groups(*full)
+    seen = set()
+    for a, b, f in outs:
+        for v, rows in candidate_groups(a, b, f).items():
+            assert v not in seen, v
+            seen.add(v)
+            for g, w in zip(rows, want[v]):
+                assert np.array_equal(g, w), v
+    assert seen == set(want)
+
+
 def _free_port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
@@ -223,6 +257,10 @@ def _worker(rank, world, port, q):
     res["tri"] = D.triangles_window(te, torch.from_numpy(ts), torch.from_numpy(td))
     ls, ld = orc.gen_rmat(6, 1500, 0x5EED06, first_edge=rank * 1500)
     res["tri_loops"] = D.triangles_window(te, torch.from_numpy(ls), torch.from_numpy(ld))
+    # GenerateCandidateEdges over the split window: edges routed to their endpoints' owners (the real
+    # all-to-all), each rank's owned vertices from the oracle
+    cs, cd = orc.gen_rmat(8, 3000, 0x5EED07, first_edge=rank * 3000)
+    res["cand"] = D.candidates_window(oracle_candidates_part(orc), torch.from_numpy(cs), torch.from_numpy(cd))
     q.put((rank, res))
     dist.barrier()
     dist.destroy_process_group()
@@ -249,6 +287,9 @@ def test_reduce_window_two_ranks(oracle):
     assert (ls == ld).any()                       # the self-pair term is exercised
     lw, lex, _, tree = oracle.window_triangles_ref(ls, ld)
     assert not tree
+    cs, cd = oracle.gen_rmat(8, 6000, 0x5EED07)
+    assert (cs == cd).any()                       # self-loops (two records for their vertex) included
+    check_candidates_split([out[r]["cand"] for r in range(world)], oracle.window_candidates(cs, cd)[:3])
     for r in range(world):
         assert np.array_equal(out[r]["gathered"][0], s) and np.array_equal(out[r]["gathered"][1], d)
         assert out[r]["tri"] == (ex, w, True)

@@ -20,7 +20,7 @@ import torch.multiprocessing as mp
 pytestmark = pytest.mark.gpu
 ROOT = Path(__file__).resolve().parent.parent
 sys.path.insert(0, str(ROOT / "tests"))
-from test_distributed_gloo import _free_port, check_cases, owner_np, run_cases  # noqa: E402
+from test_distributed_gloo import _free_port, check_cases, check_candidates_split, owner_np, run_cases  # noqa: E402
 
 
 @pytest.mark.parametrize("nparts", [1, 2, 3, 8, 64])
@@ -79,6 +79,10 @@ def _worker(rank, world, port, q):
     v = orc.gen_values(n, 5, orc.DT_I64, first_edge=rank * n)
     eng = pkg.Engine(0)
     res = run_cases(D, D.engine_halves(eng), s, d, v, to_dev=lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda())
+    # GenerateCandidateEdges over the split window: routed edges, gs_window_candidates_part per rank
+    cs, cd = orc.gen_rmat(10, 20000, 0x5EED07, first_edge=rank * 20000)
+    a, b, f = D.candidates_window(eng.candidates, torch.from_numpy(cs).cuda(), torch.from_numpy(cd).cuda())
+    res["cand"] = (a.cpu().numpy(), b.cpu().numpy(), f.cpu().numpy())
     eng.close()
     q.put((rank, res))
     dist.barrier()
@@ -100,6 +104,28 @@ def test_engine_halves_two_ranks_gloo(oracle):
     s, d = oracle.gen_rmat(12, 2 * n, 0x5EED03, a=0.65, b=0.15, c=0.15, permute=False)
     v = oracle.gen_values(2 * n, 5, oracle.DT_I64)
     check_cases(oracle, out, world, s, d, v)
+    cs, cd = oracle.gen_rmat(10, 40000, 0x5EED07)
+    check_candidates_split([out[r]["cand"] for r in range(world)], oracle.window_candidates(cs, cd)[:3])
+
+
+@pytest.mark.parametrize("nparts", [2, 3, 8])
+def test_candidates_part(engine, oracle, nparts):
+    """gs_window_candidates_part: part p, given the edges incident to its vertices in stream order, emits
+    exactly the whole window's records of the vertices it owns (exact JDK HashSet order included: the
+    ids are multiples of 16, so large neighbour sets collide into bins of 9 and take the simulation)."""
+    s, d = oracle.gen_rmat(12, 120_000, 0x5EED08)
+    for mul in (1, 16):
+        S, D_ = s * mul, d * mul
+        full = [x.cpu().numpy() for x in engine.candidates(torch.from_numpy(S).cuda(), torch.from_numpy(D_).cuda())]
+        w = oracle.window_candidates(S, D_)
+        assert all(np.array_equal(g, x) for g, x in zip(full, w[:3]))
+        oa, ob = owner_np(S, nparts), owner_np(D_, nparts)
+        outs = []
+        for part in range(nparts):
+            keep = (oa == part) | (ob == part)
+            ps, pd = (torch.from_numpy(np.ascontiguousarray(x[keep])).cuda() for x in (S, D_))
+            outs.append([x.cpu().numpy() for x in engine.candidates(ps, pd, nparts, part)])
+        check_candidates_split(outs, full)
 
 
 def test_rccl_world_one_through_the_abi(pkg, oracle):
