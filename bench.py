@@ -141,7 +141,7 @@ def direct_kernel_table(times_list, E, U_avg):
     mean = lambda f: statistics.mean(f(t) for t in times_list)
     rows = {}
     spec = t0.speculative == 1   # regions from the previous window's counts: no histogram, no offset scans
-    name = ("sp_scatter_pack" if spec else "dp_scatter_pack") if t0.packed else "dp_scatter"
+    name = ("sp_scatter_pack" if spec else "dp_scatter_pack") if t0.packed else ("sp_scatter" if spec else "dp_scatter")
     rows[name] = {"ms": mean(lambda t: t.pass_ms[1]), "bytes": E * ((8 + lb) + (2 + vb))}
     rows["bucket_accumulate"] = {"ms": mean(lambda t: t.pass_ms[2]), "bytes": E * (2 + vb) + U_avg * (4 + ab)}
     rows["bucket_merge"] = {"ms": mean(lambda t: t.pass_ms[3]), "bytes": 0}

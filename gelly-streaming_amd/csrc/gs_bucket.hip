@@ -279,14 +279,16 @@ gs_status bucket_direct_t(gs_ctx* c, const int64_t* src, const int64_t* dst, con
   int64_t base = c->bk_base;
   uint32_t nb = c->bk_nbp ? c->bk_nbp : (uint32_t)BK_MAXB;
   const uint32_t item_recs = item_records(c, R);
-  // speculative partition: packed windows whose bucket counts the previous packed window of this
-  // ctx measured in the same geometry (base, S, direction)
+  // speculative partition: windows whose bucket counts the previous bucket-path window of this ctx
+  // measured in the same geometry (base, S, direction); packed records through k_sp_scatter_pack, the
+  // others through k_sp_scatter
+  constexpr bool SPEC_OK = (CAN_PACK && ITEMS == PK_ITEMS) || ITEMS == DP_ITEMS;
   bool spec = false, spec_missed = false;
   uint64_t cap = R;
-  if constexpr (CAN_PACK && ITEMS == PK_ITEMS) {
+  if constexpr (SPEC_OK) {
     GS_TRY(ensure(c, c->sp_tot, BK_MAXB * 4, true));
     GS_TRY(ensure(c, c->sp_cur, (SP_NSEG * BK_MAXB + SP_NSEG + 1) * 4));
-    spec = pack && !(c->flags & GS_FLAG_NO_SPEC) && c->sp_ok && c->sp_skip == 0 && c->sp_base == base &&
+    spec = !(c->flags & GS_FLAG_NO_SPEC) && c->sp_ok && c->sp_skip == 0 && c->sp_base == base &&
            c->sp_S == S && c->sp_dir == DIR && nb > 1 && sp_capacity(R, nb) < (1ull << 32);
     if (c->sp_skip > 0) --c->sp_skip;
     if (spec) {
@@ -303,7 +305,7 @@ gs_status bucket_direct_t(gs_ctx* c, const int64_t* src, const int64_t* dst, con
   bool part = false;
   int64_t kmin = 0, kmax = 0;
   for (int attempt = 0;; ++attempt) {
-    if constexpr (CAN_PACK && ITEMS == PK_ITEMS) {
+    if constexpr (SPEC_OK) {
       if (spec && attempt == 0) {
         // regions from the previous window's counts -> the scatter reserves runs with atomics ->
         // items from the cursors (the counts the next window predicts from) -> accumulate
@@ -324,21 +326,32 @@ gs_status bucket_direct_t(gs_ctx* c, const int64_t* src, const int64_t* dst, con
         hipLaunchKernelGGL(k_sp_regions, dim3(1), dim3(BK_PLAN_BLOCK), 0, c->stream, (const uint32_t*)c->sp_tot.as<uint32_t>(),
                            nb, c->sp_R, R, meta + BkMeta::BSTART, c->sp_cur.as<uint32_t>(), slots, mm);
         GS_HIP(hipMemsetAsync(sm + SM_BK_ESC, 0, 8, c->stream));
+        if constexpr (P::REL) GS_HIP(hipMemsetAsync(rel_bad, 0, 4, c->stream));
         hipEventRecord(c->ev[1], c->stream);
         hipEventRecord(c->pass_ev[0], c->stream);
         hipEventRecord(c->pass_ev[1], c->stream);
         using Load = typename P::Load;
         const BaseSrc<Load, DIR, P::PAY> ls{src, dst, (const Load*)val, base};
-        hipLaunchKernelGGL((k_sp_scatter_pack<Load, DIR, ITEMS>), dim3(dp_scatter_grid<DIR, ITEMS>(n)), dim3(DP_BLOCK), 0,
-                           c->stream, ls, n, S, nb, (const uint32_t*)(meta + BkMeta::BSTART), c->sp_cur.as<uint32_t>(),
-                           c->keysB.as<uint32_t>(), vpart, (uint32_t)cap, mm, (unsigned long long*)(sm + SM_BK_ESC));
+        const uint32_t* bst = meta + BkMeta::BSTART;
+        uint32_t* cur = c->sp_cur.as<uint32_t>();
+        if constexpr (CAN_PACK && ITEMS == PK_ITEMS) {
+          if (pack)
+            hipLaunchKernelGGL((k_sp_scatter_pack<Load, DIR, ITEMS>), dim3(dp_scatter_grid<DIR, ITEMS>(n)), dim3(DP_BLOCK), 0,
+                               c->stream, ls, n, S, nb, bst, cur, c->keysB.as<uint32_t>(), vpart, (uint32_t)cap, mm,
+                               (unsigned long long*)(sm + SM_BK_ESC));
+        }
+        if constexpr (ITEMS == DP_ITEMS) {
+          if (!pack)
+            hipLaunchKernelGGL((k_sp_scatter<Load, DIR, P::PAY, Raw, P::REL>), dim3(dp_scatter_grid<DIR, ITEMS>(n)),
+                               dim3(DP_BLOCK), 0, c->stream, ls, n, S, nb, bst, cur, k16, vpart, (uint32_t)cap, rel_bad, mm);
+        }
         GS_HIP(hipGetLastError());
         hipEventRecord(c->pass_ev[2], c->stream);
         hipEventRecord(c->ev[2], c->stream);
-        GS_TRY(launch_plan<P>(c, cap, nb, 0, 0, item_recs, c->sp_cur.as<uint32_t>(), c->sp_tot.as<uint32_t>(), mm));
+        GS_TRY(launch_plan<P>(c, cap, nb, 0, 0, item_recs, cur, c->sp_tot.as<uint32_t>(), mm));
         part = true;
-        GS_TRY((bucket_accumulate<P>(c, PackSrc<Raw>{c->keysB.as<uint32_t>(), vpart}, cap, nb, base, o, 2,
-                                     c->sp_cur.as<uint32_t>())));
+        if (pack) GS_TRY((bucket_accumulate<P>(c, PackSrc<Raw>{c->keysB.as<uint32_t>(), vpart}, cap, nb, base, o, 2, cur)));
+        else GS_TRY((bucket_accumulate<P>(c, PartSrc<Raw>{k16, vpart}, cap, nb, base, o, 2, cur)));
         GS_TRY(host_wait(c));
         if (!c->host_small[2]) {   // hit: every key in the range; the plan reported the occupied buckets
           kmin = (int64_t)((uint64_t)base + (c->host_small[0] << S));
@@ -367,7 +380,7 @@ gs_status bucket_direct_t(gs_ctx* c, const int64_t* src, const int64_t* dst, con
     hipLaunchKernelGGL(k_dp_up, g2, dim3(256), 0, c->stream, cnt, nt, nb, csum);
     hipLaunchKernelGGL(k_dp_spine, dim3((nb + 63) / 64), dim3(1024), 0, c->stream, csum, nch, nb, meta + BkMeta::HIST);
     GS_HIP(hipGetLastError());
-    GS_TRY(launch_plan<P>(c, R, nb, 0, 0, item_recs, nullptr, pack ? c->sp_tot.as<uint32_t>() : nullptr));
+    GS_TRY(launch_plan<P>(c, R, nb, 0, 0, item_recs, nullptr, SPEC_OK ? c->sp_tot.as<uint32_t>() : nullptr));
     if (part) {
       hipLaunchKernelGGL(k_dp_down, g2, dim3(256), 0, c->stream, cnt, csum, meta + BkMeta::BSTART, nt, nb,
                          c->dp_off.as<uint32_t>());
@@ -445,8 +458,8 @@ gs_status bucket_direct_t(gs_ctx* c, const int64_t* src, const int64_t* dst, con
   c->times.escapes = esc;
   c->times.packed = pack ? 1u : 0u;
   c->times.speculative = spec ? 1u : spec_missed ? 2u : 0u;
-  if constexpr (CAN_PACK) {   // the counts plan wrote to sp_tot are this geometry's
-    if (pack) {
+  if constexpr (SPEC_OK) {   // the counts plan wrote to sp_tot are this geometry's
+    if (part) {
       c->sp_ok = true;
       c->sp_base = base;
       c->sp_S = S;

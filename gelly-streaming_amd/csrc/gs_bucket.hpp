@@ -1184,6 +1184,130 @@ void k_sp_scatter_pack(BaseSrc<V, DIR, PAY_VAL> es, uint64_t n, int S, uint32_t 
   }
 }
 
+// The same speculative partition for the unpacked records (k_dp_scatter's layout: a 16-bit bucket-local
+// index in k16, the payload in vout): 8-byte values (Double sums, windows whose values escape), COUNT
+// (no payload) and the degree / max-neighbour folds (the neighbour, or REL: its 32-bit offset from the
+// window base, flagged in *rel_bad when it does not fit).  Same regions, segments, cursors, dummy bucket
+// and trash area as k_sp_scatter_pack.  Float SUM accumulates in LDS-atomic order anyway (1e-5).
+template <typename V, int DIR, int PAY, typename VO = V, bool REL = false>
+__global__ __launch_bounds__(DP_BLOCK) void k_sp_scatter(BaseSrc<V, DIR, PAY> es, uint64_t n, int S, uint32_t nbp,
+                                                         const uint32_t* __restrict__ bucket_start,
+                                                         uint32_t* __restrict__ cursor, uint16_t* __restrict__ k16,
+                                                         VO* __restrict__ vout, uint32_t trash,
+                                                         uint32_t* __restrict__ rel_bad,
+                                                         unsigned long long* __restrict__ mm) {
+  constexpr bool HAS_V = PAY != PAY_NONE;
+  constexpr uint32_t TILE = DP_TILE;
+  constexpr uint32_t DUMMY = (uint32_t)BK_MAXB << 16;
+  __shared__ uint32_t s_key[TILE];                // (bucket << 16) | bucket-local index, bucket order
+  __shared__ VO s_val[HAS_V ? TILE : 1];
+  __shared__ uint32_t s_cnt[BK_MAXB + 1];
+  __shared__ uint32_t s_delta[BK_MAXB + 1];
+  __shared__ uint32_t s_w[DP_BLOCK / WAVE];
+  __shared__ uint32_t s_ovf[DP_BLOCK / WAVE];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  constexpr uint32_t TE = dp_tile_edges<DIR>();
+  const uint32_t nfull = (uint32_t)(n / TE);
+  const uint32_t lmask = (1u << S) - 1;
+  const uint32_t b0 = 2 * tid, b1 = 2 * tid + 1;   // BK_MAXB = 2 * DP_BLOCK
+  const uint32_t bl0 = min(b0, nbp - 1), bl1 = min(b1, nbp - 1);
+  uint32_t t, nrec = TILE;
+  if (blockIdx.x == gridDim.x - 1) {   // the window's partial last tile
+    if ((uint64_t)nfull * TE >= n) return;
+    t = nfull;
+    nrec = (uint32_t)((n - (uint64_t)nfull * TE) * (DIR == DIR_ALL ? 2 : 1));
+  } else {   // XCD slot b & 7 owns a contiguous range of full tiles (k_dp_scatter)
+    const uint32_t per = (nfull + 7) / 8;
+    t = (blockIdx.x & 7u) * per + (blockIdx.x >> 3);
+    if (t >= nfull) return;
+  }
+  const uint32_t r0 = t * TILE;
+  const uint32_t xs = SP_NSEG == 1 ? 0u : blockIdx.x & 7u;
+  const uint32_t* pre = cursor + SP_NSEG * BK_MAXB;
+  const uint32_t end0 = sp_seg_start(bucket_start[bl0], bucket_start[bl0 + 1], xs + 1, pre);
+  const uint32_t end1 = sp_seg_start(bucket_start[bl1], bucket_start[bl1 + 1], xs + 1, pre);
+  cursor += xs * BK_MAXB;
+  int64_t kk[DP_ITEMS];
+  V vv[DP_ITEMS];
+#pragma unroll
+  for (int u = 0; u < DP_ITEMS; ++u) {   // every load first, unconditional and clamped into the tile
+    const uint32_t r = r0 + min((uint32_t)u * DP_BLOCK + tid, nrec - 1);
+    uint32_t i = r;
+    bool rev = DIR == DIR_IN;
+    if constexpr (DIR == DIR_ALL) {
+      i = r >> 1;
+      rev = r & 1u;
+    }
+    kk[u] = (rev ? es.dst : es.src)[i];
+    if constexpr (PAY == PAY_VAL) vv[u] = es.val[i];
+    else if constexpr (PAY == PAY_NBR) vv[u] = (V)(rev ? es.src : es.dst)[i];
+  }
+  uint32_t ovf = 0, kb[DP_ITEMS];
+  bool bad = false;
+#pragma unroll
+  for (int u = 0; u < DP_ITEMS; ++u) {
+    const uint32_t j = (uint32_t)u * DP_BLOCK + tid;
+    const uint64_t d = (uint64_t)kk[u] - (uint64_t)es.base;
+    const bool in = (d >> S) < nbp, live = j < nrec;
+    ovf += (live && !in) ? 1u : 0u;
+    kb[u] = (live && in) ? ((uint32_t)(d >> S) << 16) | ((uint32_t)d & lmask) : DUMMY;
+  }
+  for (uint32_t i = tid; i < nbp; i += DP_BLOCK) s_cnt[i] = 0;
+  if (tid == 0) s_cnt[BK_MAXB] = 0;
+  __syncthreads();
+  uint32_t rk[DP_ITEMS];
+#pragma unroll
+  for (int u = 0; u < DP_ITEMS; ++u) rk[u] = atomicAdd(&s_cnt[kb[u] >> 16], 1u);
+  __syncthreads();
+  const uint32_t c0 = b0 < nbp ? s_cnt[b0] : 0u, c1 = b1 < nbp ? s_cnt[b1] : 0u;
+  const uint32_t o0 = c0 ? atomicAdd(&cursor[b0], c0) : 0u;
+  const uint32_t o1 = c1 ? atomicAdd(&cursor[b1], c1) : 0u;
+  uint32_t total;
+  const uint32_t st0 = bk_block_scan(c0 + c1, s_w, total);
+  s_cnt[b0] = st0;
+  s_cnt[b1] = st0 + c0;
+  if (tid == 0) s_cnt[BK_MAXB] = total;
+  __syncthreads();
+#pragma unroll
+  for (int u = 0; u < DP_ITEMS; ++u) {
+    const uint32_t pos = s_cnt[kb[u] >> 16] + rk[u];
+    s_key[pos] = kb[u];
+    if constexpr (REL) {   // a dead or outside lane's payload is never checked (it goes to the trash)
+      const uint64_t rel = (uint64_t)vv[u] - (uint64_t)es.base;
+      bad |= kb[u] != DUMMY && (rel >> 32) != 0;
+      s_val[pos] = (VO)rel;
+    } else if constexpr (HAS_V) {
+      s_val[pos] = (VO)vv[u];
+    }
+  }
+  const bool drop0 = c0 && o0 + c0 > end0, drop1 = c1 && o1 + c1 > end1;
+  s_delta[b0] = (drop0 ? trash : o0) - st0;
+  s_delta[b1] = (drop1 ? trash : o1) - (st0 + c0);
+  if (tid == 0) s_delta[BK_MAXB] = trash;
+  ovf += (drop0 ? 1u : 0u) + (drop1 ? 1u : 0u);
+  __syncthreads();
+#pragma unroll
+  for (int u = 0; u < DP_ITEMS; ++u) {
+    const uint32_t j = (uint32_t)u * DP_BLOCK + tid;
+    const uint32_t kv = s_key[j];
+    const uint32_t g = s_delta[kv >> 16] + j;
+    k16[g] = (uint16_t)kv;
+    if constexpr (HAS_V) vout[g] = s_val[j];
+  }
+  if constexpr (REL) {
+    if (__any(bad) && lane == 0) atomicOr(rel_bad, 1u);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) ovf += __shfl_xor(ovf, o, WAVE);
+  if (lane == 0) s_ovf[w] = ovf;
+  __syncthreads();
+  if (tid == 0) {
+    uint32_t o2 = 0;
+    for (int i = 0; i < DP_BLOCK / WAVE; ++i) o2 += s_ovf[i];
+    if (o2) atomicAdd(&mm[2], (unsigned long long)o2);
+  }
+}
+
 // ---- k_bk_accum: persistent; LDS accumulation of (bucket, record range) items ---------------------
 // Finalize (shared with k_bk_merge): the bucket's vertices in ascending order -> staging at the
 // bucket's record offset (a bucket has at least as many records as vertices).

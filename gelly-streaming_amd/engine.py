@@ -65,7 +65,7 @@ class StageTimes:
                            # components (compact IDs, union-find, labels)
     packed: bool = False   # path 2: 4-byte packed partition records (k_dp_scatter_pack)
     escapes: int = 0       # path 2, packed: values stored in full
-    speculative: int = 0   # path 2, packed: 1 = regions from the previous window's counts, 2 = that missed
+    speculative: int = 0   # path 2: 1 = regions from the previous window's counts, 2 = that missed
 
 
 class Engine:

@@ -462,7 +462,7 @@ typedef struct gs_stage_times {
                                  adjacency entries, vertices = vertices with edges, partials = hash
                                  probes of the counting step, sort_passes = LSD passes)          */
   uint32_t packed;         /* path 2: 1 = 4-byte packed partition records (k_dp_scatter_pack)    */
-  uint32_t speculative;    /* path 2, packed: 0 = per-tile histogram + offsets (k_dp_hist);
+  uint32_t speculative;    /* path 2: 0 = per-tile histogram + offsets (k_dp_hist);
                               1 = speculative partition (regions from the previous window's counts,
                                   runs reserved with atomics: keyinfo_ms = regions, pass_ms[0] = 0);
                               2 = speculative partition missed, window rerun through k_dp_hist   */

@@ -276,7 +276,8 @@ def test_packed_prediction_miss_reruns(pkg, oracle):
 
 
 @pytest.mark.parametrize("direction,dtype,op", [(1, np.int64, 0), (0, np.int64, 0), (2, np.int64, 0),
-                                                (1, np.int32, 1), (2, np.int64, 2)])
+                                                (1, np.int32, 1), (2, np.int64, 2), (1, np.float64, 0),
+                                                (2, np.float32, 0), (0, np.int64, 3)])
 def test_speculative_partition(pkg, oracle, direction, dtype, op):
     """k_sp_scatter_pack: a packed window whose bucket counts the ctx's previous packed window measured in
     the same geometry (base, S, direction) sizes one region per bucket from them and reserves each tile's
@@ -288,22 +289,25 @@ def test_speculative_partition(pkg, oracle, direction, dtype, op):
     rng = np.random.default_rng(4242 + 10 * direction + op)
     n = 300_001
 
+    flt = np.issubdtype(np.dtype(dtype), np.floating)
+    packed = not flt and op != 3   # integer SUM / MIN / MAX: k_sp_scatter_pack; others: k_sp_scatter
+
     def win(m, span=1 << 22):
         s, d = _window(rng, m, span, hub_frac=0.1)
         v = rng.integers(0, 0xFFFF, m)
         v[rng.random(m) < 0.001] = -(1 << 40) if dtype == np.int64 else -(1 << 30)   # escapes
-        return s, d, v.astype(dtype)
+        return s, d, (rng.random(m) * 100 if flt else v).astype(dtype)
 
     with pkg.Engine(0) as e, pkg.Engine(0, no_spec=True) as ex:
         def run(s, d, v, expect):
             rk, rv = oracle.window_reduce(s, d, v, direction, op)
             gk, gv = e.reduce(*_dev(s, d, v), direction, op)
             t = e.stage_times()
-            assert t.path == 2 and t.packed
+            assert t.path == 2 and t.packed == packed
             _check(gk, gv, rk, rv, dtype, op)
             xk, xv = ex.reduce(*_dev(s, d, v), direction, op)
             assert ex.stage_times().speculative == 0
-            assert torch.equal(gk, xk) and torch.equal(gv, xv)
+            assert torch.equal(gk, xk) and (flt or torch.equal(gv, xv))   # float sums: LDS-atomic order
             assert t.speculative == expect, (t.speculative, expect)
 
         run(*win(n), 0)            # first window: histogram (nothing to predict from)
@@ -321,3 +325,23 @@ def test_speculative_partition(pkg, oracle, direction, dtype, op):
         s, d, v = win(n)
         s[n // 3] = d[n // 3] = (1 << 23) + 5   # outside the predicted bucket count
         run(s, d, v, 2)
+
+
+@pytest.mark.parametrize("direction", [0, 1, 2])
+def test_speculative_degree_max(pkg, oracle, direction):
+    """foldNeighbors(degree, max neighbour) on k_sp_scatter: neighbours as 32-bit offsets from the window
+    base (BkDeg32); a window whose neighbours leave base + 2^32 retries wide (BkDeg) and stays exact."""
+    rng = np.random.default_rng(77 + direction)
+    n = 250_001
+    with pkg.Engine(0) as e:
+        spec = []
+        for w in range(6):
+            s, d = _window(rng, n, 1 << 21, hub_frac=0.05)
+            if w == 4:
+                d[::1000] += 1 << 40   # far neighbours (keys stay in range for OUT)
+            want = oracle.window_fold_degree_max(s, d, direction)
+            got = e.fold_degree_max(*_dev(s, d), direction)
+            for g, x in zip(got, want):
+                assert np.array_equal(g.cpu().numpy(), x), w
+            spec.append(e.stage_times().speculative)
+        assert spec[1] == spec[2] == spec[3] == 1, spec

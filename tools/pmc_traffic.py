@@ -14,7 +14,7 @@ from collections import defaultdict
 from pathlib import Path
 
 NAMES = {"k_dp_scatter": "dp_scatter", "k_dp_scatter_pack": "dp_scatter_pack", "k_bk_accum": "bucket_accumulate",
-         "k_dp_hist": "dp_hist", "k_sp_scatter_pack": "sp_scatter_pack", "k_sp_regions": "sp_regions",
+         "k_dp_hist": "dp_hist", "k_sp_scatter_pack": "sp_scatter_pack", "k_sp_scatter": "sp_scatter", "k_sp_regions": "sp_regions",
          "k_bk_merge": "bucket_merge", "k_bk_emit": "bucket_emit"}
 
 
