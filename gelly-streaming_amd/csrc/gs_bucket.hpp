@@ -1457,13 +1457,20 @@ __global__ __launch_bounds__(BK_MS_BLOCK) void k_bk_merge_slices(const uint32_t*
   if (mm[2] || blockIdx.x >= *n_multi_p) return;
   const uint32_t b = mlist[blockIdx.x];
   const uint32_t n = b_items[b], f = b_slab[b];
-  typename P::Lds* d = slabs + f;
+  // d and the other slabs never overlap (restrict): d's elements stay in registers across the slabs and
+  // the slab loads of an unrolled group issue together (a dependent read-modify-write of d per slab made
+  // the merge latency-bound: Zipf hub buckets of ~100 slabs, C3 0.78 ms)
+  typename P::Lds* __restrict__ d = slabs + f;
+  const typename P::Lds* __restrict__ rest = slabs + f + 1;
   constexpr uint32_t EL = P::W / BK_MS_SLICES, PWS = (P::PWORDS + BK_MS_SLICES - 1) / BK_MS_SLICES;
   const uint32_t e0 = blockIdx.y * EL, w0 = blockIdx.y * PWS;
-  for (uint32_t k = 1; k < n; ++k) {
-    const typename P::Lds* g = slabs + f + k;
-    for (uint32_t i = threadIdx.x; i < EL; i += BK_MS_BLOCK) P::merge_el(d, g, e0 + i);
-    for (uint32_t w = threadIdx.x; w < PWS && w0 + w < P::PWORDS; w += BK_MS_BLOCK) P::merge_pw(d, g, w0 + w);
+  for (uint32_t i = threadIdx.x; i < EL; i += BK_MS_BLOCK) {
+#pragma unroll 8
+    for (uint32_t k = 0; k + 1 < n; ++k) P::merge_el(d, rest + k, e0 + i);
+  }
+  for (uint32_t w = threadIdx.x; w < PWS && w0 + w < P::PWORDS; w += BK_MS_BLOCK) {
+#pragma unroll 8
+    for (uint32_t k = 0; k + 1 < n; ++k) P::merge_pw(d, rest + k, w0 + w);
   }
 }
 
