@@ -1,8 +1,10 @@
 """Heavy-vertex span analysis for the k_tri_heavy bitmap: the degree-class renumbering
 restated in numpy on an R-MAT window, then the share of heavy work whose N+(v) span fits 2^k bits.
-    python tools/tri_span.py SCALE   (s24 needs ~20 GB of host memory)"""
+    python tests/analysis_tri_span.py SCALE   (s24 needs ~20 GB of host memory)"""
 import sys, numpy as np
-sys.path.insert(0,'/root/repo'); sys.path.insert(0,'/root/repo/tests')
+from pathlib import Path
+ROOT = Path(__file__).resolve().parent.parent
+sys.path.insert(0, str(ROOT)); sys.path.insert(0, str(ROOT / 'tests'))
 import __graft_entry__ as ge
 orc = ge.load_oracle()
 from test_distributed_gloo import OracleTriEngine
