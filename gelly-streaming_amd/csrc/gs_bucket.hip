@@ -285,12 +285,13 @@ gs_status bucket_direct_t(gs_ctx* c, const int64_t* src, const int64_t* dst, con
   constexpr bool SPEC_OK = (CAN_PACK && ITEMS == PK_ITEMS) || ITEMS == DP_ITEMS;
   bool spec = false, spec_missed = false;
   uint64_t cap = R;
+  auto& sp = c->sp[c->sp_slot];
   if constexpr (SPEC_OK) {
-    GS_TRY(ensure(c, c->sp_tot, BK_MAXB * 4, true));
+    GS_TRY(ensure(c, sp.tot, BK_MAXB * 4, true));
     GS_TRY(ensure(c, c->sp_cur, (SP_NSEG * BK_MAXB + SP_NSEG + 1) * 4));
-    spec = !(c->flags & GS_FLAG_NO_SPEC) && c->sp_ok && c->sp_skip == 0 && c->sp_base == base &&
-           c->sp_S == S && c->sp_dir == DIR && nb > 1 && sp_capacity(R, nb) < (1ull << 32);
-    if (c->sp_skip > 0) --c->sp_skip;
+    spec = !(c->flags & GS_FLAG_NO_SPEC) && sp.ok && sp.skip == 0 && sp.base == base && sp.S == S &&
+           sp.dir == DIR && nb > 1 && sp_capacity(R, nb) < (1ull << 32);
+    if (sp.skip > 0) --sp.skip;
     if (spec) {
       cap = sp_capacity(R, nb);
       GS_TRY(ensure_stage<P>(c, cap + DP_BLOCK * ITEMS));   // + the trash area of dropped runs
@@ -323,8 +324,8 @@ gs_status bucket_direct_t(gs_ctx* c, const int64_t* src, const int64_t* dst, con
           }
           slots.pre[SP_NSEG] = (uint32_t)acc;   // == R
         }
-        hipLaunchKernelGGL(k_sp_regions, dim3(1), dim3(BK_PLAN_BLOCK), 0, c->stream, (const uint32_t*)c->sp_tot.as<uint32_t>(),
-                           nb, c->sp_R, R, meta + BkMeta::BSTART, c->sp_cur.as<uint32_t>(), slots, mm);
+        hipLaunchKernelGGL(k_sp_regions, dim3(1), dim3(BK_PLAN_BLOCK), 0, c->stream, (const uint32_t*)sp.tot.as<uint32_t>(),
+                           nb, sp.R, R, meta + BkMeta::BSTART, c->sp_cur.as<uint32_t>(), slots, mm);
         GS_HIP(hipMemsetAsync(sm + SM_BK_ESC, 0, 8, c->stream));
         if constexpr (P::REL) GS_HIP(hipMemsetAsync(rel_bad, 0, 4, c->stream));
         hipEventRecord(c->ev[1], c->stream);
@@ -348,7 +349,7 @@ gs_status bucket_direct_t(gs_ctx* c, const int64_t* src, const int64_t* dst, con
         GS_HIP(hipGetLastError());
         hipEventRecord(c->pass_ev[2], c->stream);
         hipEventRecord(c->ev[2], c->stream);
-        GS_TRY(launch_plan<P>(c, cap, nb, 0, 0, item_recs, cur, c->sp_tot.as<uint32_t>(), mm));
+        GS_TRY(launch_plan<P>(c, cap, nb, 0, 0, item_recs, cur, sp.tot.as<uint32_t>(), mm));
         part = true;
         if (pack) GS_TRY((bucket_accumulate<P>(c, PackSrc<Raw>{c->keysB.as<uint32_t>(), vpart}, cap, nb, base, o, 2, cur)));
         else GS_TRY((bucket_accumulate<P>(c, PartSrc<Raw>{k16, vpart}, cap, nb, base, o, 2, cur)));
@@ -361,7 +362,7 @@ gs_status bucket_direct_t(gs_ctx* c, const int64_t* src, const int64_t* dst, con
         // missed (a run past its segment, or a key outside the range): rerun through the histogram,
         // which measures the range (and reruns once more if the prediction missed it); the next 8
         // windows do not speculate
-        c->sp_skip = 8;
+        sp.skip = 8;
         spec = false;
         spec_missed = true;
         continue;
@@ -380,7 +381,7 @@ gs_status bucket_direct_t(gs_ctx* c, const int64_t* src, const int64_t* dst, con
     hipLaunchKernelGGL(k_dp_up, g2, dim3(256), 0, c->stream, cnt, nt, nb, csum);
     hipLaunchKernelGGL(k_dp_spine, dim3((nb + 63) / 64), dim3(1024), 0, c->stream, csum, nch, nb, meta + BkMeta::HIST);
     GS_HIP(hipGetLastError());
-    GS_TRY(launch_plan<P>(c, R, nb, 0, 0, item_recs, nullptr, SPEC_OK ? c->sp_tot.as<uint32_t>() : nullptr));
+    GS_TRY(launch_plan<P>(c, R, nb, 0, 0, item_recs, nullptr, SPEC_OK ? sp.tot.as<uint32_t>() : nullptr));
     if (part) {
       hipLaunchKernelGGL(k_dp_down, g2, dim3(256), 0, c->stream, cnt, csum, meta + BkMeta::BSTART, nt, nb,
                          c->dp_off.as<uint32_t>());
@@ -460,11 +461,11 @@ gs_status bucket_direct_t(gs_ctx* c, const int64_t* src, const int64_t* dst, con
   c->times.speculative = spec ? 1u : spec_missed ? 2u : 0u;
   if constexpr (SPEC_OK) {   // the counts plan wrote to sp_tot are this geometry's
     if (part) {
-      c->sp_ok = true;
-      c->sp_base = base;
-      c->sp_S = S;
-      c->sp_dir = DIR;
-      c->sp_R = R;
+      sp.ok = true;
+      sp.base = base;
+      sp.S = S;
+      sp.dir = DIR;
+      sp.R = R;
     }
   }
   return GS_OK;

@@ -341,8 +341,16 @@ gs_status gs_window_fold_degree_max_partials(gs_ctx* c, const gs_edge_batch* b, 
   return partials_impl(c, b, dir, 0, true, INT64_MIN, nparts, out);
 }
 
+// the merges run the bucket path on received rows: their own speculative-partition slot (gs_internal.hpp)
+struct SpMergeSlot {
+  gs_ctx* c;
+  explicit SpMergeSlot(gs_ctx* cc) : c(cc) { c->sp_slot = 1; }
+  ~SpMergeSlot() { c->sp_slot = 0; }
+};
+
 gs_status gs_merge_partials(gs_ctx* c, const gs_partial_batch* p, int32_t op, const void* init, gs_vertex_out* out) {
   if (!c) return GS_EINVAL;
+  SpMergeSlot slot(c);
   if (!p || (p->n && (!p->keys || !p->vals))) return set_error(c, GS_EINVAL, "bad gs_partial_batch");
   if (op < GS_OP_SUM || op > GS_OP_COUNT) return set_error(c, GS_EINVAL, "bad op %d", op);
   const int32_t mop = op == GS_OP_COUNT ? GS_OP_SUM : op;            // counts merge by SUM
@@ -353,6 +361,7 @@ gs_status gs_merge_partials(gs_ctx* c, const gs_partial_batch* p, int32_t op, co
 
 gs_status gs_merge_degree_max_partials(gs_ctx* c, const gs_partial_batch* p, int64_t init_max, gs_degree_out* out) {
   if (!c) return GS_EINVAL;
+  SpMergeSlot slot(c);
   if (!p || (p->n && (!p->keys || !p->vals || !p->vals2))) return set_error(c, GS_EINVAL, "bad gs_partial_batch");
   if (!out || !out->n_out || (out->capacity && (!out->keys || !out->degree || !out->max_neighbor)))
     return set_error(c, GS_EINVAL, "bad gs_degree_out");

@@ -72,13 +72,19 @@ struct gs_ctx {
   gs::DevBuf bk_meta, bk_items, bk_slabs;
   // direct partition: per-tile bucket counts (u16), chunk sums, per-tile write offsets
   gs::DevBuf dp_cnt, dp_csum, dp_off;
-  // speculative partition (k_sp_scatter_pack): the last packed window's bucket counts, bucket cursors;
-  // the geometry those counts were taken in, and windows left before the next try after a miss
-  gs::DevBuf sp_tot, sp_cur;
-  bool sp_ok = false;
-  int sp_S = 0, sp_dir = -1, sp_skip = 0;
-  int64_t sp_base = 0;
-  uint64_t sp_R = 0;
+  // speculative partition (k_sp_scatter*): per stream of windows, the last window's bucket counts, the
+  // geometry they were taken in and the windows left before the next try after a miss; slot 0 = the
+  // caller's windows, slot 1 = the multi-GPU merges (their rows spread over the buckets unlike the
+  // windows', so they keep their own counts); bucket cursors shared
+  struct SpState {
+    gs::DevBuf tot;
+    bool ok = false;
+    int S = 0, dir = -1, skip = 0;
+    int64_t base = 0;
+    uint64_t R = 0;
+  } sp[2];
+  int sp_slot = 0;
+  gs::DevBuf sp_cur;
   // stage-2 candidate count (gs_pairs.hip): staged input columns, packed keys / payloads, group sums
   gs::DevBuf pr_a, pr_b, pr_f, pr_key, pr_val, pr_gk, pr_gv, pr_small;
   // edge text parser (gs_text.hip): staged text, tile newline counts, record starts

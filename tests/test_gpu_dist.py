@@ -228,3 +228,22 @@ def test_split_window_steps_and_rccl_world_one(pkg, oracle):
         e.comm_init(1, 0, pkg.Engine.comm_unique_id())
         assert e.triangles_dist(S, Dd) == whole
         e.comm_destroy()
+
+
+def test_merges_keep_their_own_speculative_counts(pkg, oracle):
+    """keyBy on one ctx alternates a window's partials and a merge of received rows: the merge's rows
+    spread over the buckets unlike the window's, so it predicts from its own counts (slot 1) and the
+    windows keep speculating from theirs (a shared slot made every window miss)."""
+    with pkg.Engine(0) as e:
+        spec = []
+        for w in range(5):
+            s, d = oracle.gen_rmat(18, 1 << 21, 0x5EED02, first_edge=w << 21)
+            v = oracle.gen_values(1 << 21, 0x5EED02, oracle.DT_I64, first_edge=w << 21)
+            S, D_, V = (torch.from_numpy(x).cuda() for x in (s, d, v))
+            k, p, counts = e.reduce_partials(S, D_, V, 1, 0, 2)
+            spec.append(e.stage_times().speculative)
+            mk, mv = e.merge_partials(k[:counts[0]], p[:counts[0]], 0)   # the rows owner 0 would get
+            rk, rv = oracle.window_reduce(s, d, v, 1, 0)
+            own = owner_np(rk, 2) == 0
+            assert np.array_equal(mk.cpu().numpy(), rk[own]) and np.array_equal(mv.cpu().numpy(), rv[own])
+        assert spec[0] == 0 and spec[1:] == [1, 1, 1, 1], spec
