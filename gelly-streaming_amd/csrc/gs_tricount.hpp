@@ -41,6 +41,10 @@ constexpr uint32_t TH_NU = GS_TH_NU, TH_HB = TH_NU / 2, TH_VCH = GS_TH_VCH;   //
 #define GS_TH_BITMAP 1   // k_tri_heavy: N+(v) as a bitmap over (v, last] when the span fits the table
 #endif
 constexpr bool TH_BITMAP = GS_TH_BITMAP;
+#ifndef GS_TH_LBITMAP
+#define GS_TH_LBITMAP 0  // k_tri_light: the same for a wave's table (spans up to TH_H·32 bits); A/B: light count s24 7.08 vs 6.92 ms hash, off
+#endif
+constexpr bool TH_LBITMAP = GS_TH_LBITMAP;
 static_assert(TH_VCH % TH_HBLOCK == 0, "TH_VCH must be a multiple of TH_HBLOCK");
 #ifndef GS_TH_DMAX
 #define GS_TH_DMAX 256   // light/heavy split; 512 -> 256: s22 66.4 -> 55.8 ms, s24 302.6 -> 289.7 (128: 56.8, 296.1)
@@ -246,11 +250,35 @@ __device__ __forceinline__ uint32_t th_wave_probe(const uint32_t* __restrict__ o
 
 // one wave: N+(v) into the wave's own LDS hash set, then the in-entries c0 .. c1 (<= TH_DMAX) of v
 __device__ __forceinline__ uint32_t th_wave_chunk(const uint32_t* __restrict__ onbr, const uint2* __restrict__ sfx,
-                                                  uint2 ro, uint32_t c0,
+                                                  uint32_t v_id, uint2 ro, uint32_t c0,
                                                   uint32_t c1, int lane, uint4* hb, uint32_t* po, uint32_t* ps,
                                                   uint64_t& probes, uint32_t nb_cap, uint32_t* err) {
   uint32_t* hs = reinterpret_cast<uint32_t*>(hb);
   const uint32_t d = ro.y - ro.x;
+  // a bitmap over (v, last] when the span fits the table's TH_H·32 bits (k_tri_heavy): the high-rank
+  // light vertices (hubs with few higher neighbours)
+  const uint32_t v = uni(v_id), span = uni(onbr[ro.y - 1] - v);
+  if (TH_LBITMAP && nb_cap > 1 && span <= TH_H * 32u) {
+    const uint32_t nw = (span + 31) / 32;
+    for (uint32_t i = lane; i < nw; i += WAVE) hs[i] = 0u;
+    wave_lds_sync();
+    for (uint32_t i = lane; i < d; i += WAVE) {
+      const uint32_t o = onbr[ro.x + i] - v - 1;
+      atomicOr(&hs[o >> 5], 1u << (o & 31));
+    }
+    wave_lds_sync();
+    return th_wave_probe<TH_DMAX>(onbr, sfx, c0, c1, lane, po, ps, probes,
+                                  [&](const uint32_t (&x)[TH_ILP], uint32_t nv) {
+                                    uint32_t c = 0;
+#pragma unroll
+                                    for (int j = 0; j < TH_ILP; ++j) {
+                                      const uint32_t o = x[j] - v - 1;
+                                      const uint32_t wv = hs[min(o, span - 1) >> 5];
+                                      c += ((uint32_t)j < nv && o < span) ? (wv >> (o & 31)) & 1u : 0u;
+                                    }
+                                    return c;
+                                  });
+  }
   uint32_t nb = 16;
   while (nb < d && nb < TH_H / 4) nb <<= 1;
   nb = min(nb, nb_cap);
@@ -314,7 +342,7 @@ __global__ __launch_bounds__(TH_BLOCK) __attribute__((amdgpu_waves_per_eu(GS_TH_
       c0 = ri.x + q.y * TH_DMAX;
       c1 = min(ri.y, c0 + TH_DMAX);
     }
-    cnt += th_wave_chunk(onbr, sfx, out_range[v], c0, c1, lane, s_hash[w], s_off[w], s_st[w], probes,
+    cnt += th_wave_chunk(onbr, sfx, v, out_range[v], c0, c1, lane, s_hash[w], s_off[w], s_st[w], probes,
                          nb_cap, err);
   }
 #pragma unroll
