@@ -8,6 +8,7 @@ way keyBy spreads it over subtasks; gso_triangles_fwd_mt — an independent forw
       foldNeighbors(degree, max neighbour) bit-exact
   C4  WindowTriangles on self-loop-free R-MAT windows at scales 20 and 22: the exact count equals the
       forward algorithm's (and the reference's Integer is its low 32 bits)
+  C2 / C3 on one fresh ctx, two windows: the second through the speculative partition
 
 The windows are generated on the device (gs_generate_*, bit-identical to the oracle's generators:
 test_gpu_parity.test_generators_match_oracle, and re-checked here on a sample of each window)."""
@@ -77,6 +78,37 @@ def test_c3_full_window_degree_max(engine, oracle, stream):
     assert np.array_equal(gd.cpu().numpy(), rd), "degrees differ"
     assert np.array_equal(gm.cpu().numpy(), rm), "max neighbours differ"
     assert int(rd.max()) > 1 << 20, "the skewed stream should have a hub"
+
+
+@pytest.mark.parametrize("kind", ["c2_long", "c3_rmat"])
+def test_speculative_partition_full_windows(pkg, oracle, kind):
+    """Two consecutive config-size windows on a fresh ctx: the first takes the histogram path, the second
+    the speculative partition (regions from the first's bucket counts, atomic run reservations) -- both
+    bit-exact against the oracle."""
+    scale, E = 24, 1 << 28
+    with pkg.Engine(0) as e:
+        for window in (0, 1):
+            fe = window * E
+            if kind == "c2_long":
+                seed = 0x5EED02
+                src, dst = e.generate_rmat(scale, E, seed, first_edge=fe)
+                val = e.generate_values(E, seed, 1, first_edge=fe)
+                got = e.reduce(src, dst, val, 1, 0)
+                spec = e.stage_times().speculative
+                hv = val.cpu().numpy()
+                del val
+            else:
+                seed = 0x5EED03
+                src, dst = e.generate_rmat(scale, E, seed, a=0.65, b=0.15, c=0.15, permute=False, first_edge=fe)
+                got = e.fold_degree_max(src, dst, 1)
+                spec = e.stage_times().speculative
+            s_h, d_h = src.cpu().numpy(), dst.cpu().numpy()
+            del src, dst
+            want = (oracle.window_reduce_mt(s_h, d_h, hv, 1, 0) if kind == "c2_long"
+                    else oracle.window_fold_degree_max_mt(s_h, d_h, 1))
+            for g, w in zip(got, want):
+                assert np.array_equal(g.cpu().numpy(), w), (kind, window)
+            assert spec == window, (kind, window, spec)   # 0: histogram path, 1: speculative
 
 
 @pytest.mark.parametrize("scale", [20, 22])
