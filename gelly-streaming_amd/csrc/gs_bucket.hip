@@ -290,7 +290,7 @@ gs_status bucket_direct_t(gs_ctx* c, const int64_t* src, const int64_t* dst, con
     GS_TRY(ensure(c, sp.tot, BK_MAXB * 4, true));
     GS_TRY(ensure(c, c->sp_cur, (SP_NSEG * BK_MAXB + SP_NSEG + 1) * 4));
     spec = !(c->flags & GS_FLAG_NO_SPEC) && sp.ok && sp.skip == 0 && sp.base == base && sp.S == S &&
-           sp.dir == DIR && nb > 1 && sp_capacity(R, nb) < (1ull << 32);
+           sp.dir == DIR && nb > 1 && sp_capacity(R, nb) + DP_BLOCK * ITEMS < (1ull << 32);   // u32 positions + trash
     if (sp.skip > 0) --sp.skip;
     if (spec) {
       cap = sp_capacity(R, nb);
