@@ -598,7 +598,7 @@ gs_status tri_count(gs_ctx* c, uint32_t B, size_t V, uint64_t M, const uint32_t*
   hipEventRecord(c->ev[4], c->stream);
   // 2. intersections: vertex-centric LDS hash sets (k_tri_light), long out-lists in k_tri_heavy
   GS_TRY(ensure(c, c->tri_heavy, (V + Ms / TH_VCH + 64) * 8));   // (v, in-chunk) items
-  GS_TRY(ensure(c, c->tri_queue, (Ms / TH_DMAX + 64) * 8));      // further in-list chunks: <= Ms / TH_DMAX
+  GS_TRY(ensure(c, c->tri_queue, (Ms / TH_LCH + 64) * 8));       // further in-list chunks: <= Ms / TH_LCH
   unsigned long long* d_total = (unsigned long long*)(sm + SM_NUNIQUE);
   uint32_t* d_nheavy = (uint32_t*)(sm + SM_COUNTERS) + 62;
   unsigned long long* d_probes = (unsigned long long*)(sm + SM_TRI_PROBES);

@@ -6,11 +6,12 @@
 // u of v the range of N+(u) past v (sfx), so a chunk's lists come from one coalesced read.
 //
 // Middle-vertex order: a wave takes v, puts N+(v) into an LDS hash set of 4-slot buckets, spreads the
-// concatenation of the suffixes over a chunk of TH_DMAX in-neighbours u across its lanes (prefix of
+// concatenation of the suffixes over a chunk of TH_LCH in-neighbours u across its lanes (prefix of
 // the lengths in LDS, one search per TH_ILP consecutive items) and probes each w with one 16-byte LDS
 // read.  Probes: sum over u of d+(u)(d+(u)-1)/2 (R-MAT scale 20: 1.23 G; whole lists 2.47 G, first-
 // vertex order 4.42 G).  In-lists longer than a chunk queue their further chunks for a second pass (a
-// hub's work spreads over many waves); vertices with more than TH_DMAX out-neighbours go to
+// hub's work spreads over many waves); vertices with more than TH_DMAX out-neighbours (or TH_HMIN when
+// the heavy bitmap covers their span) go to
 // k_tri_heavy (a block each, N+(v) in a 64 KiB LDS hash set).  Only vertices whose out-list starts in
 // [q0, q1) count (the multi-GPU split).
 #pragma once
@@ -47,12 +48,20 @@ constexpr bool TH_BITMAP = GS_TH_BITMAP;
 constexpr bool TH_LBITMAP = GS_TH_LBITMAP;
 static_assert(TH_VCH % TH_HBLOCK == 0, "TH_VCH must be a multiple of TH_HBLOCK");
 #ifndef GS_TH_DMAX
-#define GS_TH_DMAX 256   // light/heavy split; 512 -> 256: s22 66.4 -> 55.8 ms, s24 302.6 -> 289.7 (128: 56.8, 296.1)
+#define GS_TH_DMAX 512   // light capacity (out-list of a light vertex, in-entries per light chunk); with the heavy bitmaps: s26 455 -> 376 ms
+#endif
+#ifndef GS_TH_HMIN
+#define GS_TH_HMIN 256   // out-lists longer than this go to k_tri_heavy when its bitmap covers their span (the rest up to TH_DMAX stay light)
 #endif
 #ifndef GS_TH_H
 #define GS_TH_H 1024
 #endif
-constexpr uint32_t TH_DMAX = GS_TH_DMAX, TH_H = GS_TH_H, TH_EMPTY = 0xFFFFFFFFu;
+constexpr uint32_t TH_DMAX = GS_TH_DMAX, TH_HMIN = GS_TH_HMIN, TH_H = GS_TH_H, TH_EMPTY = 0xFFFFFFFFu;
+static_assert(TH_HMIN <= TH_DMAX, "TH_HMIN must be <= TH_DMAX");
+#ifndef GS_TH_LCH
+#define GS_TH_LCH 256    // k_tri_light: in-entries per chunk (the wave's list prefix arrays: 2 KiB)
+#endif
+constexpr uint32_t TH_LCH = GS_TH_LCH;
 // a light vertex's N+(v) (<= TH_DMAX entries) must leave the TH_H-slot table at most half full: insert
 // and probe chains end at a free slot, so a full table would never end them
 static_assert(TH_DMAX * 2 <= TH_H, "TH_DMAX must be <= TH_H / 2");
@@ -248,7 +257,7 @@ __device__ __forceinline__ uint32_t th_wave_probe(const uint32_t* __restrict__ o
   return cnt;
 }
 
-// one wave: N+(v) into the wave's own LDS hash set, then the in-entries c0 .. c1 (<= TH_DMAX) of v
+// one wave: N+(v) into the wave's own LDS hash set, then the in-entries c0 .. c1 (<= TH_LCH) of v
 __device__ __forceinline__ uint32_t th_wave_chunk(const uint32_t* __restrict__ onbr, const uint2* __restrict__ sfx,
                                                   uint32_t v_id, uint2 ro, uint32_t c0,
                                                   uint32_t c1, int lane, uint4* hb, uint32_t* po, uint32_t* ps,
@@ -267,7 +276,7 @@ __device__ __forceinline__ uint32_t th_wave_chunk(const uint32_t* __restrict__ o
       atomicOr(&hs[o >> 5], 1u << (o & 31));
     }
     wave_lds_sync();
-    return th_wave_probe<TH_DMAX>(onbr, sfx, c0, c1, lane, po, ps, probes,
+    return th_wave_probe<TH_LCH>(onbr, sfx, c0, c1, lane, po, ps, probes,
                                   [&](const uint32_t (&x)[TH_ILP], uint32_t nv) {
                                     uint32_t c = 0;
 #pragma unroll
@@ -287,7 +296,7 @@ __device__ __forceinline__ uint32_t th_wave_chunk(const uint32_t* __restrict__ o
   wave_lds_sync();
   for (uint32_t i = lane; i < d; i += WAVE) th_insert(hs, onbr[ro.x + i], bmask, err);
   wave_lds_sync();
-  return th_wave_probe<TH_DMAX>(onbr, sfx, c0, c1, lane, po, ps, probes,
+  return th_wave_probe<TH_LCH>(onbr, sfx, c0, c1, lane, po, ps, probes,
                                 [&](const uint32_t (&x)[TH_ILP], uint32_t nv) { return th_probe(hb, bmask, x, nv, err); });
 }
 
@@ -306,8 +315,8 @@ __global__ __launch_bounds__(TH_BLOCK) __attribute__((amdgpu_waves_per_eu(GS_TH_
                                                         uint32_t* __restrict__ err) {
   // 6 KiB per wave (4 KiB table + 2 KiB list prefix), 24 KiB per block
   __shared__ uint4 s_hash[TH_WPB][TH_H / 4];
-  __shared__ uint32_t s_off[TH_WPB][TH_DMAX];   // exclusive prefix of |N+(u)| over the non-empty u
-  __shared__ uint32_t s_st[TH_WPB][TH_DMAX];    // start of that N+(u) in onbr
+  __shared__ uint32_t s_off[TH_WPB][TH_LCH];   // exclusive prefix of |N+(u)| over the non-empty u
+  __shared__ uint32_t s_st[TH_WPB][TH_LCH];    // start of that N+(u) in onbr
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const uint32_t nw = gridDim.x * TH_WPB;
   uint64_t cnt = 0, probes = 0;
@@ -318,7 +327,13 @@ __global__ __launch_bounds__(TH_BLOCK) __attribute__((amdgpu_waves_per_eu(GS_TH_
       v = it;
       const uint2 ro = out_range[v], ri = in_range[v];
       if (ro.y == ro.x || ri.y == ri.x || ro.x < q0 || ro.x >= q1) continue;
-      if (ro.y - ro.x > TH_DMAX) {   // one heavy item per TH_VCH in-neighbours: a hub spreads over blocks
+      const uint32_t dv = ro.y - ro.x;
+      // heavy: too long for a wave's table, or long enough to gain from the heavy kernel's bitmap
+      // (k_tri_heavy: span of N+(v) within its table's bits; history: the split at 256 alone, s26 455 ms,
+      // at 512 alone s24 72 -> 78 ms)
+      const bool heavy_v = dv > TH_DMAX ||
+                           (TH_BITMAP && nb_cap > 1 && dv > TH_HMIN && onbr[ro.y - 1] - v <= TH_HB * 128u);
+      if (heavy_v) {   // one heavy item per TH_VCH in-neighbours: a hub spreads over blocks
         const uint32_t nhc = (ri.y - ri.x + TH_VCH - 1) / TH_VCH;
         uint32_t at = 0;
         if (lane == 0) at = atomicAdd(n_heavy, nhc);
@@ -326,7 +341,7 @@ __global__ __launch_bounds__(TH_BLOCK) __attribute__((amdgpu_waves_per_eu(GS_TH_
         for (uint32_t j = lane; j < nhc; j += WAVE) heavy[at + j] = make_uint2(v, j);
         continue;
       }
-      const uint32_t nch = (ri.y - ri.x + TH_DMAX - 1) / TH_DMAX;
+      const uint32_t nch = (ri.y - ri.x + TH_LCH - 1) / TH_LCH;
       if (nch > 1) {
         uint32_t at = 0;
         if (lane == 0) at = atomicAdd(n_queue, nch - 1);
@@ -334,13 +349,13 @@ __global__ __launch_bounds__(TH_BLOCK) __attribute__((amdgpu_waves_per_eu(GS_TH_
         for (uint32_t j = lane; j < nch - 1; j += WAVE) queue[at + j] = make_uint2(v, j + 1);
       }
       c0 = ri.x;
-      c1 = min(ri.y, ri.x + TH_DMAX);
+      c1 = min(ri.y, ri.x + TH_LCH);
     } else {
       const uint2 q = queue[it];
       v = q.x;
       const uint2 ri = in_range[v];
-      c0 = ri.x + q.y * TH_DMAX;
-      c1 = min(ri.y, c0 + TH_DMAX);
+      c0 = ri.x + q.y * TH_LCH;
+      c1 = min(ri.y, c0 + TH_LCH);
     }
     cnt += th_wave_chunk(onbr, sfx, v, out_range[v], c0, c1, lane, s_hash[w], s_off[w], s_st[w], probes,
                          nb_cap, err);
