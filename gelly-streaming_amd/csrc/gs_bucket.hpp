@@ -146,12 +146,35 @@ struct BkVal {
       using I = std::conditional_t<sizeof(T) == 8, long long, int>;
       atomicMax((I*)&s.acc[i], (I)v);
     }
+    mark(s, i);
+  }
+  __device__ static void mark(Lds& s, uint32_t i) {
     if constexpr (PB) reinterpret_cast<uint8_t*>(s.pm)[i] = 1;
     else atomicOr(&s.pm[i >> 5], 1u << (i & 31));
   }
+  // packed records (k_dp/sp_scatter_pack, integer ops): r is a narrow value in [0, PK_ESC) unless esc.
+  // An integer accumulator that left its identity has seen a record, and narrow values cannot bring it
+  // back (a SUM of values in [1, 2^16) over < 2^32 records never wraps to 0; a MIN / MAX of them is never
+  // the extreme identity), so presence needs its byte only for escaped values and, for SUM, zero values
+  static constexpr bool INFER_PRESENCE = std::is_integral_v<T>;
+  __device__ static void add_packed(Lds& s, uint32_t i, Raw r, bool esc) {
+    const T v = bits_as<T>(r);
+    if constexpr (OP == OP_SUM) {
+      using U = std::conditional_t<sizeof(T) == 8, unsigned long long, unsigned int>;
+      atomicAdd((U*)&s.acc[i], (U)v);
+    } else if constexpr (OP == OP_MIN) {
+      using I = std::conditional_t<sizeof(T) == 8, long long, int>;
+      atomicMin((I*)&s.acc[i], (I)v);
+    } else {
+      using I = std::conditional_t<sizeof(T) == 8, long long, int>;
+      atomicMax((I*)&s.acc[i], (I)v);
+    }
+    if (esc || (OP == OP_SUM && r == 0)) mark(s, i);
+  }
   __device__ static bool present(const Lds& s, uint32_t i) {
-    if constexpr (PB) return reinterpret_cast<const uint8_t*>(s.pm)[i] != 0;
-    else return (s.pm[i >> 5] >> (i & 31)) & 1u;
+    const bool m = PB ? reinterpret_cast<const uint8_t*>(s.pm)[i] != 0 : ((s.pm[i >> 5] >> (i & 31)) & 1u) != 0;
+    if constexpr (INFER_PRESENCE) return m || s.acc[i] != identity();
+    else return m;
   }
   __device__ static void stage(BkStage st, uint32_t pos, const Lds& s, uint32_t i) { ((A*)st.a)[pos] = s.acc[i]; }
   static constexpr uint32_t PWORDS = PW;   // presence words merged by OR
@@ -342,6 +365,10 @@ struct PackSrc {
   const uint32_t* rec;
   const V* wide;
 };
+template <class P, class = void>
+struct has_add_packed : std::false_type {};
+template <class P>
+struct has_add_packed<P, std::void_t<decltype(&P::add_packed)>> : std::bool_constant<P::INFER_PRESENCE> {};
 template <class Src>
 struct is_pack_src : std::false_type {};
 template <typename V>
@@ -1391,7 +1418,9 @@ __global__ __launch_bounds__(BK_ACC_BLOCK) void k_bk_accum(Src src, const BkItem
       // 4-byte version was latency-bound); an unaligned head and the tail record by record
       auto add1 = [&](uint32_t q, uint32_t x) {
         const uint32_t v16 = x >> 16;
-        P::add(s, x & (P::W - 1), v16 != PK_ESC ? (Raw)v16 : (Raw)src.wide[q]);
+        const bool esc = v16 == PK_ESC;
+        if constexpr (has_add_packed<P>::value) P::add_packed(s, x & (P::W - 1), !esc ? (Raw)v16 : (Raw)src.wide[q], esc);
+        else P::add(s, x & (P::W - 1), !esc ? (Raw)v16 : (Raw)src.wide[q]);
       };
       const uint32_t a0 = min(r1, (r0 + 3) & ~3u), a1 = max(a0, r1 & ~3u);
       if (r0 + tid < a0) add1(r0 + tid, src.rec[r0 + tid]);
