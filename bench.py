@@ -58,6 +58,9 @@ def parse():
                    help="ablation: reduce / fold through the full LSD sort + reduce-by-key path")
     p.add_argument("--bk-onesweep", action="store_true",
                    help="ablation: bucket path partitions with 1-2 LSD passes instead of the direct scatter")
+    p.add_argument("--exchange", default="abi", choices=["abi", "torch"],
+                   help="N > 1: the library's own RCCL communicator (gs_window_*_dist, what the Java side binds; "
+                        "default) or torch.distributed around the partials / merge halves (A/B)")
     p.add_argument("--check", action="store_true",
                    help="after timing: sum(per-vertex sums) == sum(values) and ascending keys on each window")
     p.add_argument("--windows-edges", type=float, default=1e8,
@@ -551,6 +554,13 @@ def main():
     D = import_module("gelly_streaming_amd.distributed")
 
     eng = pkg.Engine(local, sort_only=a.sort_only, bk_onesweep=a.bk_onesweep, no_pack=a.no_pack, no_spec=a.no_spec)
+    abi = dist is not None and a.exchange == "abi"
+    if abi:   # the ctx-owned RCCL communicator: rank 0's unique id broadcast over torch.distributed
+        uid = torch.zeros(128, dtype=torch.uint8, device=f"cuda:{local}")
+        if rank == 0:
+            uid.copy_(torch.frombuffer(bytearray(pkg.Engine.comm_unique_id()), dtype=torch.uint8))
+        dist.broadcast(uid, 0)
+        eng.comm_init(world, rank, bytes(uid.cpu().numpy().tobytes()))
     E = a.edge_factor << a.scale
     vdt = 1 if a.dtype == "int64" else 3
     # a.windows distinct windows of the stream (rank r holds windows r*W .. r*W+W-1), cycled by the
@@ -609,7 +619,10 @@ def main():
         src, dst, val = wins[i % len(wins)]
         local_times.clear()
         if a.workload == "triangles":
-            if dist:   # the split window: degrees, routed oriented edges, all-gathered out-lists, share of the count
+            if abi:    # the split window through gs_window_triangles_dist (RCCL inside the library)
+                tot = eng.triangles_dist(src, dst)[0]
+                local_times.append(eng.stage_times())
+            elif dist:   # the same steps with torch.distributed collectives
                 tot = D.triangles_window(eng, src, dst)[0]
                 local_times.append(eng.stage_times())
             else:
@@ -620,10 +633,18 @@ def main():
             r = eng.components(src, dst)
             return r[0], r[1], eng.stage_times()
         if a.workload == "fold":
-            r = D.fold_degree_max_window(fold_partials_timed, M_fold, src, dst, 1, -(1 << 63)) if dist \
-                else local_fold(src, dst, 1, -(1 << 63))
+            if abi:   # gs_window_fold_degree_max_dist: its stage times are the local window's pipeline
+                r = eng.fold_degree_max_dist(src, dst, 1)
+                local_times.append(eng.stage_times())
+            else:
+                r = D.fold_degree_max_window(fold_partials_timed, M_fold, src, dst, 1, -(1 << 63)) if dist \
+                    else local_fold(src, dst, 1, -(1 << 63))
             return r[0], r[1], local_times[0]
-        r = D.reduce_window(partials_timed, M_red, src, dst, val, 1, 0) if dist else local_reduce(src, dst, val, 1, 0)
+        if abi:       # gs_window_reduce_dist
+            r = eng.reduce_dist(src, dst, val, 1, 0)
+            local_times.append(eng.stage_times())
+        else:
+            r = D.reduce_window(partials_timed, M_red, src, dst, val, 1, 0) if dist else local_reduce(src, dst, val, 1, 0)
         return r[0], r[1], local_times[0]
 
     for i in range(a.warmup):
@@ -759,8 +780,12 @@ def main():
                                        f"split window over {world} GPUs: summed degrees, oriented edges to owner(u), "
                                        f"all-gathered out-lists, equal-work count shares (gs_tri_dist_*)"
                                        if a.workload == "triangles" else
-                                       f"hash keyBy over {world} GPU(s): per-rank partials (gs_window_reduce_partials) "
-                                       f"-> RCCL all-to-all -> gs_merge_partials"), **checks},
+                                       (f"hash keyBy over {world} GPU(s) through gs_window_*_dist: per-rank partials "
+                                        f"-> owner partition -> RCCL all-to-all of sizes + one packed all-to-all of "
+                                        f"rows (library communicator) -> merge" if abi else
+                                        f"hash keyBy over {world} GPU(s): per-rank partials (gs_window_reduce_partials) "
+                                        f"-> torch.distributed all-to-all -> gs_merge_partials")),
+                       "exchange": (a.exchange if dist else None), **checks},
             "roofline": roofline,
             "cpu_baseline": cpu,
             "kernels": {n: {"avg_ms": round(r["ms"], 4), "own_bytes": r["bytes"], "GB/s": round(r["GB/s"], 1),
@@ -768,6 +793,8 @@ def main():
                         for n, r in kt.items()},
         }
         print(json.dumps(line), flush=True)
+    if abi:
+        eng.comm_destroy()
     if dist:
         dist.destroy_process_group()
     eng.close()

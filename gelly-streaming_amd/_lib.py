@@ -42,7 +42,8 @@ EXPORTS = ("gs_abi_version", "gs_create", "gs_destroy", "gs_last_error", "gs_set
            "gs_merge_partials", "gs_merge_degree_max_partials", "gs_comm_unique_id", "gs_comm_init", "gs_comm_destroy",
            "gs_comm_allreduce_sum_u64", "gs_window_reduce_dist", "gs_window_fold_degree_max_dist",
            "gs_stream_create", "gs_stream_destroy", "gs_stream_append", "gs_stream_watermark", "gs_stream_flush",
-           "gs_stream_poll", "gs_stream_stats", "gs_generate_rmat", "gs_generate_uniform", "gs_generate_zipf", "gs_generate_values", "gs_last_stage_times")
+           "gs_stream_poll", "gs_stream_stats", "gs_generate_rmat", "gs_generate_uniform", "gs_generate_zipf", "gs_generate_values", "gs_last_stage_times",
+           "gs_set_max_window_records", "gs_candidates_begin", "gs_candidates_next")
 
 P = ctypes.c_void_p
 u64, i64, i32, u32 = ctypes.c_uint64, ctypes.c_int64, ctypes.c_int32, ctypes.c_uint32
@@ -53,6 +54,7 @@ GS_FLAG_BK_ONESWEEP = 2   # bucket path: 1-2 LSD partition passes instead of the
 GS_FLAG_NO_PACK = 4       # bucket path: integer SUM/MIN/MAX keep 8-byte partitioned values (A/B)
 GS_FLAG_NO_SPEC = 16      # bucket path: no speculative partition (per-tile histograms first; A/B)
 GS_FLAG_TEST_TINY_TABLES = 8   # TEST ONLY: triangle hash sets of one bucket -> must fail with GS_EDEVICE
+GS_FLAG_TEST_FORCE_EXCHANGE = 32   # TEST ONLY: *_dist on one rank still partitions, exchanges and merges
 
 
 class GsConfig(ctypes.Structure):
@@ -199,6 +201,9 @@ def load() -> ctypes.CDLL:
         "gs_generate_zipf": (st, [P, u64, ctypes.c_double, u64, u64, u64, P, P]),
         "gs_generate_values": (st, [P, u64, u64, u64, i32, P]),
         "gs_last_stage_times": (st, [P, ctypes.POINTER(GsStageTimes)]),
+        "gs_set_max_window_records": (st, [P, u64]),
+        "gs_candidates_begin": (st, [P, ctypes.POINTER(GsEdgeBatch), ctypes.POINTER(u64), ctypes.POINTER(u32)]),
+        "gs_candidates_next": (st, [P, ctypes.POINTER(GsPairOut), ctypes.POINTER(u64), ctypes.POINTER(i32)]),
     }
     for name, (res, args) in sigs.items():
         f = getattr(L, name)

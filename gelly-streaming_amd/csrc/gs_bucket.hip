@@ -285,16 +285,19 @@ gs_status bucket_direct_t(gs_ctx* c, const int64_t* src, const int64_t* dst, con
   constexpr bool SPEC_OK = (CAN_PACK && ITEMS == PK_ITEMS) || ITEMS == DP_ITEMS;
   bool spec = false, spec_missed = false;
   uint64_t cap = R;
+  // the speculative scatter's tile: k_sp_scatter_pack (SPK_BLOCK x SPK_ITEMS) or k_sp_scatter (DP_TILE)
+  const uint64_t TRASH = std::max<uint64_t>(SPK_TILE, (uint64_t)DP_BLOCK * ITEMS);
+  const uint64_t SPTE = pack ? spk_tile_edges<DIR>() : dp_tile_edges<DIR, ITEMS>();
   auto& sp = c->sp[c->sp_slot];
   if constexpr (SPEC_OK) {
     GS_TRY(ensure(c, sp.tot, BK_MAXB * 4, true));
     GS_TRY(ensure(c, c->sp_cur, (SP_NSEG * BK_MAXB + SP_NSEG + 1) * 4));
     spec = !(c->flags & GS_FLAG_NO_SPEC) && sp.ok && sp.skip == 0 && sp.base == base && sp.S == S &&
-           sp.dir == DIR && nb > 1 && sp_capacity(R, nb) + DP_BLOCK * ITEMS < (1ull << 32);   // u32 positions + trash
+           sp.dir == DIR && nb > 1 && sp_capacity(R, nb) + TRASH < (1ull << 32);   // u32 positions + trash
     if (sp.skip > 0) --sp.skip;
     if (spec) {
       cap = sp_capacity(R, nb);
-      GS_TRY(ensure_stage<P>(c, cap + DP_BLOCK * ITEMS));   // + the trash area of dropped runs
+      GS_TRY(ensure_stage<P>(c, cap + TRASH));   // + the trash area of dropped runs
     }
   }
   uint16_t* cnt = c->dp_cnt.as<uint16_t>();
@@ -314,7 +317,7 @@ gs_status bucket_direct_t(gs_ctx* c, const int64_t* src, const int64_t* dst, con
         // the partial last tile runs in slot 0)
         SpSlots slots{};
         {
-          const uint64_t tr = (DIR == DIR_ALL ? 2 : 1) * (uint64_t)TE, nfull = n / TE, per = (nfull + 7) / 8;
+          const uint64_t tr = (DIR == DIR_ALL ? 2 : 1) * SPTE, nfull = n / SPTE, per = (nfull + 7) / 8;
           uint64_t acc = 0;
           for (uint32_t x = 0; x < SP_NSEG; ++x) {
             slots.pre[x] = (uint32_t)acc;
@@ -337,7 +340,7 @@ gs_status bucket_direct_t(gs_ctx* c, const int64_t* src, const int64_t* dst, con
         uint32_t* cur = c->sp_cur.as<uint32_t>();
         if constexpr (CAN_PACK && ITEMS == PK_ITEMS) {
           if (pack)
-            hipLaunchKernelGGL((k_sp_scatter_pack<Load, DIR, ITEMS>), dim3(dp_scatter_grid<DIR, ITEMS>(n)), dim3(DP_BLOCK), 0,
+            hipLaunchKernelGGL((k_sp_scatter_pack<Load, DIR>), dim3(spk_grid<DIR>(n)), dim3(SPK_BLOCK), 0,
                                c->stream, ls, n, S, nb, bst, cur, c->keysB.as<uint32_t>(), vpart, (uint32_t)cap, mm,
                                (unsigned long long*)(sm + SM_BK_ESC));
         }

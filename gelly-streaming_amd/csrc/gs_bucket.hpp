@@ -154,9 +154,12 @@ struct BkVal {
   }
   // packed records (k_dp/sp_scatter_pack, integer ops): r is a narrow value in [0, PK_ESC) unless esc.
   // An integer accumulator that left its identity has seen a record, and narrow values cannot bring it
-  // back (a SUM of values in [1, 2^16) over < 2^32 records never wraps to 0; a MIN / MAX of them is never
-  // the extreme identity), so presence needs its byte only for escaped values and, for SUM, zero values
+  // back (a 64-bit SUM of values in [1, 2^16) over < 2^32 records never wraps to 0; a MIN / MAX of them is
+  // never the extreme identity), so presence needs its byte only for escaped values and, for SUM, zero
+  // values.  A 32-bit SUM can wrap to exactly 0 (2^16 records of 2^16 - 1 ... ), so Integer SUM marks
+  // every record.
   static constexpr bool INFER_PRESENCE = std::is_integral_v<T>;
+  static constexpr bool SUM_MARKS_ALL = OP == OP_SUM && sizeof(A) == 4;
   __device__ static void add_packed(Lds& s, uint32_t i, Raw r, bool esc) {
     const T v = bits_as<T>(r);
     if constexpr (OP == OP_SUM) {
@@ -169,7 +172,7 @@ struct BkVal {
       using I = std::conditional_t<sizeof(T) == 8, long long, int>;
       atomicMax((I*)&s.acc[i], (I)v);
     }
-    if (esc || (OP == OP_SUM && r == 0)) mark(s, i);
+    if (SUM_MARKS_ALL || esc || (OP == OP_SUM && r == 0)) mark(s, i);
   }
   __device__ static bool present(const Lds& s, uint32_t i) {
     const bool m = PB ? reinterpret_cast<const uint8_t*>(s.pm)[i] != 0 : ((s.pm[i >> 5] >> (i & 31)) & 1u) != 0;
@@ -1085,27 +1088,71 @@ __host__ __device__ inline uint64_t sp_capacity(uint64_t r_now, uint32_t nb) {
 // tile -- the partial last one too -- stores all TILE slots in one unrolled loop.  The exact key
 // range is not tracked here: on a hit every key lay in the predicted range, and k_bk_plan reports the
 // occupied buckets for the next prediction; on a miss the window's rerun measures it.
-template <typename V, int DIR, int ITEMS>
-__global__ __launch_bounds__(DP_BLOCK) __attribute__((amdgpu_waves_per_eu(GS_PK_WAVES, GS_PK_WAVES)))
+//
+// Block shape (SPK_BLOCK threads x SPK_ITEMS records): a tile's phases run in turn -- loads (HBM
+// latency), rank (LDS atomics), scan, LDS scatter, stores -- so the CU needs a second (third) block
+// whose loads are in flight while this one ranks and stores.  One bucket table serves as counts, run
+// starts and then run deltas (8 KiB), so a 512 x 16 tile takes 56 KiB of LDS: two blocks per CU at
+// <= 128 VGPRs (1024-thread blocks could not: two of them cap a lane at 64 VGPRs and spill).
+#ifndef GS_SPK_BLOCK
+#define GS_SPK_BLOCK 512
+#endif
+#ifndef GS_SPK_ITEMS
+#define GS_SPK_ITEMS 16
+#endif
+#ifndef GS_SPK_WAVES
+#define GS_SPK_WAVES (2 * GS_SPK_BLOCK / 256)   // waves per SIMD: two blocks per CU
+#endif
+constexpr int SPK_BLOCK = GS_SPK_BLOCK, SPK_ITEMS = GS_SPK_ITEMS;
+constexpr uint32_t SPK_TILE = (uint32_t)SPK_BLOCK * SPK_ITEMS;
+static_assert(BK_MAXB % SPK_BLOCK == 0 && SPK_TILE <= 65536 && SPK_ITEMS <= 32, "tile / bucket-table shape");
+template <int DIR>
+__host__ __device__ constexpr uint32_t spk_tile_edges() {
+  return DIR == DIR_ALL ? SPK_TILE / 2 : SPK_TILE;
+}
+// grid: the full tiles (in 8 XCD slots) + one block for the partial tile
+template <int DIR>
+__host__ __device__ inline uint32_t spk_grid(uint64_t n) {
+  return (uint32_t)((n / spk_tile_edges<DIR>() + 7) / 8 * 8 + 1);
+}
+
+// block-wide exclusive scan of one u32 per thread (BLOCK threads); returns the total
+template <int BLOCK>
+__device__ __forceinline__ uint32_t block_excl_scan(uint32_t x, uint32_t* s_w, uint32_t& total) {
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  constexpr int NW = BLOCK / WAVE;
+  const uint32_t inc = wave_inclusive_sum(x);
+  if (lane == 63) s_w[w] = inc;
+  __syncthreads();
+  uint32_t off = 0, tot = 0;
+#pragma unroll
+  for (int i = 0; i < NW; ++i) {
+    const uint32_t v = s_w[i];
+    off += i < w ? v : 0u;
+    tot += v;
+  }
+  total = tot;
+  return off + inc - x;
+}
+
+template <typename V, int DIR>
+__global__ __launch_bounds__(SPK_BLOCK) __attribute__((amdgpu_waves_per_eu(GS_SPK_WAVES, GS_SPK_WAVES)))
 void k_sp_scatter_pack(BaseSrc<V, DIR, PAY_VAL> es, uint64_t n, int S, uint32_t nbp,
                        const uint32_t* __restrict__ bucket_start, uint32_t* __restrict__ cursor,
                        uint32_t* __restrict__ rec, V* __restrict__ wide, uint32_t trash,
                        unsigned long long* __restrict__ mm, unsigned long long* __restrict__ n_esc) {
-  constexpr uint32_t TILE = DP_BLOCK * ITEMS;
-  static_assert(ITEMS <= 32 && TILE <= 65536, "ranks and an escape's tile-local index are kept in 16 bits");
+  constexpr int ITEMS = SPK_ITEMS, BLOCK = SPK_BLOCK, BPT = BK_MAXB / SPK_BLOCK;   // buckets per thread
+  constexpr uint32_t TILE = SPK_TILE;
   constexpr uint32_t ESC = 1u << 31, DUMMY = (uint32_t)BK_MAXB << 16;   // kb: escaped value / dummy bucket
   __shared__ uint32_t s_key[TILE];         // ESC | (bucket << 16) | bucket-local index, bucket order
   __shared__ uint16_t s_v16[TILE];         // narrow value, or an escape's tile-local record index
-  __shared__ uint32_t s_cnt[BK_MAXB + 1];  // counts, then run starts inside the tile (+ the dummy bucket)
-  __shared__ uint32_t s_delta[BK_MAXB + 1];   // global position - tile position of bucket b's run
-  __shared__ uint32_t s_w[DP_BLOCK / WAVE];
-  __shared__ uint32_t s_ovf[DP_BLOCK / WAVE];
+  __shared__ uint32_t s_tab[BK_MAXB + 1];  // counts -> run starts in the tile -> global - tile position
+  __shared__ uint32_t s_w[BLOCK / WAVE];
+  __shared__ uint32_t s_ovf[BLOCK / WAVE];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  constexpr uint32_t TE = dp_tile_edges<DIR, ITEMS>();
+  constexpr uint32_t TE = spk_tile_edges<DIR>();
   const uint32_t nfull = (uint32_t)(n / TE);
   const uint32_t lmask = (1u << S) - 1;
-  const uint32_t b0 = 2 * tid, b1 = 2 * tid + 1;   // BK_MAXB = 2 * DP_BLOCK
-  const uint32_t bl0 = min(b0, nbp - 1), bl1 = min(b1, nbp - 1);
   uint32_t t, nrec = TILE;
   if (blockIdx.x == gridDim.x - 1) {   // the window's partial last tile
     if ((uint64_t)nfull * TE >= n) return;
@@ -1119,8 +1166,6 @@ void k_sp_scatter_pack(BaseSrc<V, DIR, PAY_VAL> es, uint64_t n, int S, uint32_t 
   const uint32_t r0 = t * TILE;
   const uint32_t xs = SP_NSEG == 1 ? 0u : blockIdx.x & 7u;   // this block's XCD slot: its segment
   const uint32_t* pre = cursor + SP_NSEG * BK_MAXB;
-  const uint32_t end0 = sp_seg_start(bucket_start[bl0], bucket_start[bl0 + 1], xs + 1, pre);
-  const uint32_t end1 = sp_seg_start(bucket_start[bl1], bucket_start[bl1 + 1], xs + 1, pre);
   cursor += xs * BK_MAXB;
   uint32_t kb[ITEMS], vr[ITEMS];   // vr: narrow value (or escape index) << 16 | rank in the tile's run
   int64_t kk[ITEMS];
@@ -1128,7 +1173,7 @@ void k_sp_scatter_pack(BaseSrc<V, DIR, PAY_VAL> es, uint64_t n, int S, uint32_t 
   // every load first, unconditional and clamped into the tile (k_dp_scatter)
 #pragma unroll
   for (int u = 0; u < ITEMS; ++u) {
-    const uint32_t r = r0 + min((uint32_t)u * DP_BLOCK + tid, nrec - 1);
+    const uint32_t r = r0 + min((uint32_t)u * BLOCK + tid, nrec - 1);
     uint32_t i = r;
     bool rev = DIR == DIR_IN;
     if constexpr (DIR == DIR_ALL) {
@@ -1138,10 +1183,12 @@ void k_sp_scatter_pack(BaseSrc<V, DIR, PAY_VAL> es, uint64_t n, int S, uint32_t 
     kk[u] = (rev ? es.dst : es.src)[i];
     vv[u] = es.val[i];
   }
+  for (uint32_t i = tid; i < nbp; i += BLOCK) s_tab[i] = 0;
+  if (tid == 0) s_tab[BK_MAXB] = 0;
   uint32_t ovf = 0;
 #pragma unroll
   for (int u = 0; u < ITEMS; ++u) {
-    const uint32_t j = (uint32_t)u * DP_BLOCK + tid;
+    const uint32_t j = (uint32_t)u * BLOCK + tid;
     const uint64_t d = (uint64_t)kk[u] - (uint64_t)es.base;
     const bool in = (d >> S) < nbp, live = j < nrec;
     ovf += (live && !in) ? 1u : 0u;
@@ -1150,52 +1197,67 @@ void k_sp_scatter_pack(BaseSrc<V, DIR, PAY_VAL> es, uint64_t n, int S, uint32_t 
     kb[u] = (live && in) ? ((uint32_t)(d >> S) << 16) | ((uint32_t)d & lmask) | (e ? ESC : 0u) : DUMMY;
     vr[u] = (e ? j : nv) << 16;
   }
-  for (uint32_t i = tid; i < nbp; i += DP_BLOCK) s_cnt[i] = 0;
-  if (tid == 0) s_cnt[BK_MAXB] = 0;
   __syncthreads();
 #pragma unroll
-  for (int u = 0; u < ITEMS; ++u) vr[u] |= atomicAdd(&s_cnt[(kb[u] >> 16) & 0x7FFFu], 1u);
+  for (int u = 0; u < ITEMS; ++u) vr[u] |= atomicAdd(&s_tab[(kb[u] >> 16) & 0x7FFFu], 1u);
   __syncthreads();
-  const uint32_t c0 = b0 < nbp ? s_cnt[b0] : 0u, c1 = b1 < nbp ? s_cnt[b1] : 0u;
+  // this thread's buckets: BPT consecutive ones
+  uint32_t cb[BPT], ob[BPT], sum = 0;
+#pragma unroll
+  for (int k = 0; k < BPT; ++k) {
+    const uint32_t b = (uint32_t)tid * BPT + k;
+    cb[k] = b < nbp ? s_tab[b] : 0u;
+    sum += cb[k];
+  }
   // reserve the runs now; the returned offsets are needed only after the LDS scatter
-  const uint32_t o0 = c0 ? atomicAdd(&cursor[b0], c0) : 0u;
-  const uint32_t o1 = c1 ? atomicAdd(&cursor[b1], c1) : 0u;
+#pragma unroll
+  for (int k = 0; k < BPT; ++k) ob[k] = cb[k] ? atomicAdd(&cursor[(uint32_t)tid * BPT + k], cb[k]) : 0u;
   uint32_t total;
-  const uint32_t st0 = bk_block_scan(c0 + c1, s_w, total);   // total: records in the predicted range
-  s_cnt[b0] = st0;   // unconditional: entries past nbp are never read
-  s_cnt[b1] = st0 + c0;
-  if (tid == 0) s_cnt[BK_MAXB] = total;   // the dummy run: the tile's last
+  uint32_t st = block_excl_scan<BLOCK>(sum, s_w, total);   // total: records in the predicted range
+  uint32_t sb[BPT];
+#pragma unroll
+  for (int k = 0; k < BPT; ++k) {
+    sb[k] = st;
+    s_tab[(uint32_t)tid * BPT + k] = st;   // unconditional: entries past nbp are never read
+    st += cb[k];
+  }
+  if (tid == 0) s_tab[BK_MAXB] = total;   // the dummy run: the tile's last
   __syncthreads();
 #pragma unroll
   for (int u = 0; u < ITEMS; ++u) {
-    const uint32_t pos = s_cnt[(kb[u] >> 16) & 0x7FFFu] + (vr[u] & 0xFFFFu);
+    const uint32_t pos = s_tab[(kb[u] >> 16) & 0x7FFFu] + (vr[u] & 0xFFFFu);
     s_key[pos] = kb[u];
     s_v16[pos] = (uint16_t)(vr[u] >> 16);
   }
-  // a run that does not fit its segment goes to the trash area [trash, trash + TILE) past every
-  // region instead (nothing reads the trash)
-  const bool drop0 = c0 && o0 + c0 > end0, drop1 = c1 && o1 + c1 > end1;
-  s_delta[b0] = (drop0 ? trash : o0) - st0;
-  s_delta[b1] = (drop1 ? trash : o1) - (st0 + c0);
-  if (tid == 0) s_delta[BK_MAXB] = trash;
-  ovf += (drop0 ? 1u : 0u) + (drop1 ? 1u : 0u);
+  __syncthreads();
+  // run deltas; a run that does not fit its segment goes to the trash area [trash, trash + TILE) past
+  // every region instead (nothing reads the trash)
+#pragma unroll
+  for (int k = 0; k < BPT; ++k) {
+    const uint32_t b = min((uint32_t)tid * BPT + k, nbp - 1);
+    const uint32_t end = sp_seg_start(bucket_start[b], bucket_start[b + 1], xs + 1, pre);
+    const bool drop = cb[k] && ob[k] + cb[k] > end;
+    s_tab[(uint32_t)tid * BPT + k] = (drop ? trash : ob[k]) - sb[k];
+    ovf += drop ? 1u : 0u;
+  }
+  if (tid == 0) s_tab[BK_MAXB] = trash - total;
   __syncthreads();
   // stores without a branch; escaped values (PK_ESC in the record) after the loop, rarely taken
   uint32_t escm = 0;
 #pragma unroll
   for (int u = 0; u < ITEMS; ++u) {
-    const uint32_t j = (uint32_t)u * DP_BLOCK + tid;
+    const uint32_t j = (uint32_t)u * BLOCK + tid;
     const uint32_t kv = s_key[j];
     const bool e = kv & ESC;
-    rec[s_delta[(kv >> 16) & 0x7FFFu] + j] = (kv & 0xFFFFu) | ((e ? PK_ESC : (uint32_t)s_v16[j]) << 16);
+    rec[s_tab[(kv >> 16) & 0x7FFFu] + j] = (kv & 0xFFFFu) | ((e ? PK_ESC : (uint32_t)s_v16[j]) << 16);
     escm |= e ? 1u << u : 0u;
   }
   uint32_t esc = 0;
   for (; escm; escm &= escm - 1, ++esc) {   // the full value from the column into the slot of `wide`
-    const uint32_t j = (uint32_t)__builtin_ctz(escm) * DP_BLOCK + tid;
+    const uint32_t j = (uint32_t)__builtin_ctz(escm) * BLOCK + tid;
     const uint32_t kv = s_key[j];
     const uint32_t r = r0 + s_v16[j];
-    wide[s_delta[(kv >> 16) & 0x7FFFu] + j] = es.val[DIR == DIR_ALL ? r >> 1 : r];
+    wide[s_tab[(kv >> 16) & 0x7FFFu] + j] = es.val[DIR == DIR_ALL ? r >> 1 : r];
   }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
@@ -1209,11 +1271,10 @@ void k_sp_scatter_pack(BaseSrc<V, DIR, PAY_VAL> es, uint64_t n, int S, uint32_t 
   __syncthreads();
   if (tid == 0) {
     uint32_t o2 = 0;
-    for (int i = 0; i < DP_BLOCK / WAVE; ++i) o2 += s_ovf[i];
+    for (int i = 0; i < BLOCK / WAVE; ++i) o2 += s_ovf[i];
     if (o2) atomicAdd(&mm[2], (unsigned long long)o2);
   }
 }
-
 // The same speculative partition for the unpacked records (k_dp_scatter's layout: a 16-bit bucket-local
 // index in k16, the payload in vout): 8-byte values (Double sums, windows whose values escape), COUNT
 // (no payload) and the degree / max-neighbour folds (the neighbour, or REL: its 32-bit offset from the

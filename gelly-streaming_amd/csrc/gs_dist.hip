@@ -21,6 +21,7 @@
 #include <dlfcn.h>
 #include <string.h>
 
+#include <string>
 #include <vector>
 
 #include "gs_ops.hpp"
@@ -31,19 +32,27 @@ namespace gs {
 
 constexpr int OW_BLOCK = 256, OW_ITEMS = 16, OW_TILE = OW_BLOCK * OW_ITEMS, OW_MAXP = 64;
 
-// per tile: partials per owner -> cnt[owner * tiles + tile]
+// per tile: partials per owner -> cnt[owner * tiles + tile]; *wide |= 1 when a key lies outside
+// [0, 2^32) (the exchange then sends 8-byte keys)
 __global__ __launch_bounds__(OW_BLOCK) void k_owner_count(const int64_t* __restrict__ keys, uint64_t U, uint32_t nparts,
-                                                          uint32_t tiles, uint32_t* __restrict__ cnt) {
+                                                          uint32_t tiles, uint32_t* __restrict__ cnt,
+                                                          unsigned long long* __restrict__ wide) {
   __shared__ uint32_t s_c[OW_MAXP];
   const int tid = threadIdx.x;
   if (tid < OW_MAXP) s_c[tid] = 0;
   __syncthreads();
   const uint64_t base = (uint64_t)blockIdx.x * OW_TILE;
+  bool w = false;
 #pragma unroll
   for (int u = 0; u < OW_ITEMS; ++u) {
     const uint64_t i = base + (uint64_t)u * OW_BLOCK + tid;
-    if (i < U) atomicAdd(&s_c[owner_of(keys[i], nparts)], 1u);
+    if (i < U) {
+      const int64_t k = keys[i];
+      w |= (uint64_t)k >> 32 != 0;
+      atomicAdd(&s_c[owner_of(k, nparts)], 1u);
+    }
   }
+  if (wide && __any(w) && (tid & 63) == 0) atomicOr(wide, 1ull);
   __syncthreads();
   if (tid < (int)nparts) cnt[(uint64_t)tid * tiles + blockIdx.x] = s_c[tid];
 }
@@ -118,32 +127,81 @@ __global__ __launch_bounds__(OW_BLOCK) void k_owner_scatter(const int64_t* __res
   }
 }
 
-gs_status owner_partition(gs_ctx* c, const int64_t* keys, const void* vals, size_t vb, const int64_t* vals2, uint64_t U,
-                          uint32_t nparts, int64_t* okeys, void* ovals, int64_t* ovals2, uint64_t* counts_host) {
-  char* sm = c->small.as<char>();
+// The owner partition on the device: rows grouped by owner (ascending keys within an owner), the
+// per-owner totals in dist_cnt[0, nparts) (u64) and, with `wide`, the key-width flag.  No host wait.
+gs_status owner_partition_dev(gs_ctx* c, const int64_t* keys, const void* vals, size_t vb, const int64_t* vals2,
+                              uint64_t U, uint32_t nparts, int64_t* okeys, void* ovals, int64_t* ovals2,
+                              unsigned long long* wide) {
   const uint32_t tiles = (uint32_t)std::max<uint64_t>(1, (U + OW_TILE - 1) / OW_TILE);
   // dist_cnt: [0, 1 KiB) per-call scalars (owner totals, exchange counts), then the tile counts
   GS_TRY(ensure(c, c->dist_cnt, 1024 + (size_t)tiles * nparts * 4));
   auto* totals = c->dist_cnt.as<unsigned long long>();
   uint32_t* cnt = (uint32_t*)(c->dist_cnt.as<char>() + 1024);
-  if (U) {
-    hipLaunchKernelGGL(k_owner_count, dim3(tiles), dim3(OW_BLOCK), 0, c->stream, keys, U, nparts, tiles, cnt);
-    hipLaunchKernelGGL(k_owner_scan, dim3(1), dim3(1024), 0, c->stream, cnt, tiles * nparts, tiles, nparts, totals);
-    if (vb == 8)
-      hipLaunchKernelGGL(k_owner_scatter<uint64_t>, dim3(tiles), dim3(OW_BLOCK), 0, c->stream, keys,
-                         (const uint64_t*)vals, vals2, U, nparts, tiles, cnt, okeys, (uint64_t*)ovals, ovals2);
-    else
-      hipLaunchKernelGGL(k_owner_scatter<uint32_t>, dim3(tiles), dim3(OW_BLOCK), 0, c->stream, keys,
-                         (const uint32_t*)vals, vals2, U, nparts, tiles, cnt, okeys, (uint32_t*)ovals, ovals2);
-    GS_HIP(hipGetLastError());
-    GS_HIP(hipMemcpyAsync(c->host_small + 8, totals, nparts * 8, hipMemcpyDeviceToHost, c->stream));
-    GS_TRY(host_wait(c));
-    memcpy(counts_host, c->host_small + 8, nparts * 8);
-  } else {
-    memset(counts_host, 0, nparts * 8);
+  if (!U) {
+    GS_HIP(hipMemsetAsync(totals, 0, nparts * 8, c->stream));
+    return GS_OK;
   }
-  (void)sm;
+  hipLaunchKernelGGL(k_owner_count, dim3(tiles), dim3(OW_BLOCK), 0, c->stream, keys, U, nparts, tiles, cnt, wide);
+  hipLaunchKernelGGL(k_owner_scan, dim3(1), dim3(1024), 0, c->stream, cnt, tiles * nparts, tiles, nparts, totals);
+  if (vb == 8)
+    hipLaunchKernelGGL(k_owner_scatter<uint64_t>, dim3(tiles), dim3(OW_BLOCK), 0, c->stream, keys,
+                       (const uint64_t*)vals, vals2, U, nparts, tiles, cnt, okeys, (uint64_t*)ovals, ovals2);
+  else
+    hipLaunchKernelGGL(k_owner_scatter<uint32_t>, dim3(tiles), dim3(OW_BLOCK), 0, c->stream, keys,
+                       (const uint32_t*)vals, vals2, U, nparts, tiles, cnt, okeys, (uint32_t*)ovals, ovals2);
+  return hip_check(c, hipGetLastError(), "owner partition");
+}
+
+// ... with the per-owner totals read back (gs_window_reduce_partials: the caller runs the exchange)
+gs_status owner_partition(gs_ctx* c, const int64_t* keys, const void* vals, size_t vb, const int64_t* vals2, uint64_t U,
+                          uint32_t nparts, int64_t* okeys, void* ovals, int64_t* ovals2, uint64_t* counts_host) {
+  GS_TRY(owner_partition_dev(c, keys, vals, vb, vals2, U, nparts, okeys, ovals, ovals2, nullptr));
+  GS_HIP(hipMemcpyAsync(c->host_small + 8, c->dist_cnt.p, nparts * 8, hipMemcpyDeviceToHost, c->stream));
+  GS_TRY(host_wait(c));
+  memcpy(counts_host, c->host_small + 8, nparts * 8);
   return GS_OK;
+}
+
+// Exchange rows: key (4 bytes when every rank's keys lie in [0, 2^32), else 8), value (vb), [maximum (8)],
+// packed into one row of u32 words so the whole exchange is one grouped send / recv per peer
+__global__ __launch_bounds__(256) void k_pack_rows(const int64_t* __restrict__ keys, const uint32_t* __restrict__ vals,
+                                                   const int64_t* __restrict__ vals2, uint64_t n, int kw, int vw, int mw,
+                                                   uint32_t* __restrict__ rows) {
+  const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const int rw = kw + vw + mw;
+  uint32_t* r = rows + i * rw;
+  const uint64_t k = (uint64_t)keys[i];
+  r[0] = (uint32_t)k;
+  if (kw == 2) r[1] = (uint32_t)(k >> 32);
+  for (int j = 0; j < vw; ++j) r[kw + j] = vals[i * vw + j];
+  if (mw) {
+    const uint64_t m = (uint64_t)vals2[i];
+    r[kw + vw] = (uint32_t)m;
+    r[kw + vw + 1] = (uint32_t)(m >> 32);
+  }
+}
+
+__global__ __launch_bounds__(256) void k_unpack_rows(const uint32_t* __restrict__ rows, uint64_t n, int kw, int vw, int mw,
+                                                     int64_t* __restrict__ keys, uint32_t* __restrict__ vals,
+                                                     int64_t* __restrict__ vals2) {
+  const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const int rw = kw + vw + mw;
+  const uint32_t* r = rows + i * rw;
+  keys[i] = kw == 2 ? (int64_t)(((uint64_t)r[1] << 32) | r[0]) : (int64_t)(uint64_t)r[0];
+  for (int j = 0; j < vw; ++j) vals[i * vw + j] = r[kw + j];
+  if (mw) vals2[i] = (int64_t)(((uint64_t)r[kw + vw + 1] << 32) | r[kw + vw]);
+}
+
+// send row per peer p: [rows for p, flags] (flags: 1 = wide keys on this rank, 2 = this rank failed)
+__global__ void k_send_rows(const unsigned long long* __restrict__ totals, const unsigned long long* __restrict__ wide,
+                            uint32_t nparts, unsigned long long* __restrict__ send) {
+  const uint32_t p = threadIdx.x;
+  if (p < nparts) {
+    send[2 * p] = totals[p];
+    send[2 * p + 1] = *wide & 1ull;
+  }
 }
 
 // ---- RCCL, resolved at run time -----------------------------------------------------------------------
@@ -167,11 +225,10 @@ struct NcclId {
 };
 constexpr int NCCL_UINT8 = 1, NCCL_UINT64 = 5, NCCL_SUM = 0;   // ncclUint8, ncclUint64, ncclSum
 
-static NcclApi& nccl() {
-  static NcclApi api;
-  static bool tried = false;
-  if (tried) return api;
-  tried = true;
+// resolved once per process; a function-local static is initialised exactly once even when several
+// ctxs (Flink subtask threads) reach it concurrently
+static NcclApi load_nccl() {
+  NcclApi api;
   void* h = nullptr;
   if (dlsym(RTLD_DEFAULT, "ncclCommInitRank")) h = RTLD_DEFAULT;   // already loaded (e.g. by torch)
   if (!h) h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
@@ -190,6 +247,11 @@ static NcclApi& nccl() {
   api.GetErrorString = (const char* (*)(int))sym("ncclGetErrorString");
   api.ok = api.GetUniqueId && api.CommInitRank && api.CommDestroy && api.Send && api.Recv && api.AllToAll &&
            api.AllReduce && api.GroupStart && api.GroupEnd && api.GetErrorString;
+  return api;
+}
+
+static NcclApi& nccl() {
+  static NcclApi api = load_nccl();
   return api;
 }
 
@@ -219,6 +281,25 @@ gs_status comm_allreduce(gs_ctx* c, void* buf, size_t count, int nccl_dtype, int
   return nccl_check(c, nccl().AllReduce(buf, buf, count, nccl_dtype, nccl_op, c->comm, c->stream), "ncclAllReduce");
 }
 
+// Status agreement before the next collective: every rank reports whether its local step failed
+// (all-reduce MAX of one flag), so a failure on one rank ends the call on all of them with an error
+// instead of leaving the others blocked in a collective.  Returns the local status (its message kept),
+// GS_ECOMM when only another rank failed.
+gs_status comm_agree(gs_ctx* c, gs_status local) {
+  if (!c->comm) return local;
+  const std::string msg = c->err;
+  GS_TRY(ensure(c, c->dist_x, 64 + (size_t)c->comm_size * 32));
+  uint64_t* d = c->dist_x.as<uint64_t>() + 1;
+  c->host_small[200] = local != GS_OK ? 1 : 0;
+  GS_HIP(hipMemcpyAsync(d, c->host_small + 200, 8, hipMemcpyHostToDevice, c->stream));
+  GS_TRY(nccl_check(c, nccl().AllReduce(d, d, 1, NCCL_UINT64, NCCL_OP_MAX, c->comm, c->stream), "ncclAllReduce(status)"));
+  GS_HIP(hipMemcpyAsync(c->host_small + 201, d, 8, hipMemcpyDeviceToHost, c->stream));
+  GS_TRY(host_wait(c));
+  if (local != GS_OK) return set_error(c, local, "%s", msg.c_str());
+  if (c->host_small[201]) return set_error(c, GS_ECOMM, "another rank failed its local step of the window");
+  return GS_OK;
+}
+
 // every rank's u64 -> all[0 .. comm_size) on the host (a sum of one-hot rows)
 gs_status comm_allgather_u64(gs_ctx* c, uint64_t mine, uint64_t* all) {
   if (!c->comm) return set_error(c, GS_EINVAL, "no communicator (gs_comm_init)");
@@ -226,7 +307,7 @@ gs_status comm_allgather_u64(gs_ctx* c, uint64_t mine, uint64_t* all) {
   GS_TRY(ensure(c, c->dist_cnt, 1024 + (size_t)P * 8));
   uint64_t* d = (uint64_t*)(c->dist_cnt.as<char>() + 512);
   GS_HIP(hipMemsetAsync(d, 0, P * 8, c->stream));
-  c->host_small[100] = mine;   // pinned source (HOST_SMALL_WORDS = 128; results land in [8, 8 + P))
+  c->host_small[100] = mine;   // pinned source (HOST_SMALL_WORDS = 512; results land in [8, 8 + P))
   GS_HIP(hipMemcpyAsync(d + c->comm_rank, c->host_small + 100, 8, hipMemcpyHostToDevice, c->stream));
   GS_TRY(nccl_check(c, nccl().AllReduce(d, d, P, NCCL_UINT64, NCCL_SUM, c->comm, c->stream), "ncclAllReduce"));
   GS_HIP(hipMemcpyAsync(c->host_small + 8, d, P * 8, hipMemcpyDeviceToHost, c->stream));
@@ -441,42 +522,104 @@ gs_status gs_comm_allreduce_sum_u64(gs_ctx* c, uint64_t* value) {
 }
 
 // partials of this rank's slice -> all-to-all over the ctx's communicator -> the merge of what this
-// rank owns.  dev rows: key (8 B) + value (8 or 4 B) [+ 8 B maximum for the degree fold]
+// rank owns.  Per window: the local reduce (the bucket path's own read-back), the owner partition on the
+// device, ONE all-to-all of [rows, flags] per peer read back together (the only host wait of the
+// exchange: sizes, the key width every rank agrees on, and every rank's status -- a rank whose local
+// step failed still joins it with the failure flag, so all ranks return an error together instead of
+// the others blocking in a collective), one packed all-to-all of the rows (4-byte keys when every
+// rank's keys fit), then the merge.  One rank: the window's own output (no exchange, no merge).
 static gs_status dist_impl(gs_ctx* c, const gs_edge_batch* b, int32_t dir, int32_t op, const void* init, bool degmax,
                            int64_t init_max, gs_vertex_out* vout, gs_degree_out* dout) {
   if (!c->comm) return set_error(c, GS_EINVAL, "no communicator (gs_comm_init)");
   const uint32_t P = (uint32_t)c->comm_size;
+  if (P == 1 && !(c->flags & GS_FLAG_TEST_FORCE_EXCHANGE)) {   // the only rank owns every vertex
+    if (degmax) return gs_window_fold_degree_max(c, b, dir, init_max, dout);
+    return init ? gs_window_fold(c, b, dir, op, init, vout) : gs_window_reduce(c, b, dir, op, vout);
+  }
   const uint64_t R = dir == GS_DIR_ALL ? 2 * b->n : b->n;
-  std::vector<uint64_t> send(P), recv(P);
-  uint64_t U = 0;
-  GS_TRY(ensure(c, c->dist_k2, R * 8 + 8));
-  GS_TRY(ensure(c, c->dist_v3, R * 8 + 8));
-  if (degmax) GS_TRY(ensure(c, c->dist_v4, R * 8 + 8));
-  gs_partials_out po{c->dist_k2.as<int64_t>(), c->dist_v3.p, degmax ? c->dist_v4.as<int64_t>() : nullptr, R, &U,
-                     send.data(), GS_MEM_DEVICE, 0};
-  GS_TRY(partials_impl(c, b, dir, op, degmax, INT64_MIN, P, &po));
-  const gs_stage_times keep = c->times;
   const size_t vb = degmax ? 8 : (op == GS_OP_COUNT ? 8 : dtype_bytes(b->val_dtype));
-  // counts: all-to-all of one u64 per peer
-  GS_TRY(ensure(c, c->dist_cnt, 1024));
-  uint64_t* dc = c->dist_cnt.as<uint64_t>();
-  memcpy(c->host_small + 8, send.data(), P * 8);
-  GS_HIP(hipMemcpyAsync(dc, c->host_small + 8, P * 8, hipMemcpyHostToDevice, c->stream));
-  GS_TRY(nccl_check(c, nccl().AllToAll(dc, dc + 64, 1, NCCL_UINT64, c->comm, c->stream), "ncclAllToAll(counts)"));
-  GS_HIP(hipMemcpyAsync(c->host_small + 8, dc + 64, P * 8, hipMemcpyDeviceToHost, c->stream));
+  GS_TRY(ensure(c, c->dist_x, 64 + (size_t)P * 32));
+  auto* wide = c->dist_x.as<unsigned long long>();
+  auto* sendc = wide + 8;
+  auto* recvc = sendc + 2 * P;
+  // 1. local partials + owner partition (device); a failure is carried into the counts exchange
+  uint64_t U = 0;
+  gs_status local = GS_OK;
+  std::string local_err;
+  {
+    local = ensure(c, c->dist_k, R * 8 + 8);
+    if (local == GS_OK) local = ensure(c, c->dist_v, R * 8 + 8);
+    if (local == GS_OK && degmax) local = ensure(c, c->dist_v2, R * 8 + 8);
+    if (local == GS_OK && degmax) {
+      gs_degree_out o{c->dist_k.as<int64_t>(), c->dist_v.as<int64_t>(), c->dist_v2.as<int64_t>(), R, &U, GS_MEM_DEVICE, 0};
+      local = gs_window_fold_degree_max(c, b, dir, INT64_MIN, &o);
+    } else if (local == GS_OK) {
+      gs_vertex_out o{c->dist_k.as<int64_t>(), c->dist_v.p, R, &U, GS_MEM_DEVICE, 0};
+      local = gs_window_reduce(c, b, dir, op, &o);
+    }
+  }
+  const gs_stage_times keep = c->times;
+  if (local == GS_OK) local = ensure(c, c->dist_k2, U * 8 + 8);
+  if (local == GS_OK) local = ensure(c, c->dist_v3, U * 8 + 8);
+  if (local == GS_OK && degmax) local = ensure(c, c->dist_v4, U * 8 + 8);
+  if (local == GS_OK) {
+    GS_HIP(hipMemsetAsync(wide, 0, 8, c->stream));
+    local = owner_partition_dev(c, c->dist_k.as<int64_t>(), c->dist_v.p, vb, degmax ? c->dist_v2.as<int64_t>() : nullptr, U,
+                                P, c->dist_k2.as<int64_t>(), c->dist_v3.p, degmax ? c->dist_v4.as<int64_t>() : nullptr, wide);
+  }
+  if (local == GS_OK) {
+    hipLaunchKernelGGL(k_send_rows, dim3(1), dim3(64), 0, c->stream, c->dist_cnt.as<unsigned long long>(), wide, P, sendc);
+    local = hip_check(c, hipGetLastError(), "k_send_rows");
+  }
+  if (local != GS_OK) {   // zero rows for everyone, the failure flag set
+    local_err = c->err;
+    for (uint32_t p = 0; p < P; ++p) {
+      c->host_small[8 + 2 * p] = 0;
+      c->host_small[9 + 2 * p] = 2;
+    }
+    GS_HIP(hipMemcpyAsync(sendc, c->host_small + 8, (size_t)P * 16, hipMemcpyHostToDevice, c->stream));
+  }
+  // 2. the one exchange of sizes + flags; read back with this rank's own send counts
+  GS_TRY(nccl_check(c, nccl().AllToAll(sendc, recvc, 2, NCCL_UINT64, c->comm, c->stream), "ncclAllToAll(counts)"));
+  GS_HIP(hipMemcpyAsync(c->host_small + 8, sendc, (size_t)P * 32, hipMemcpyDeviceToHost, c->stream));
   GS_TRY(host_wait(c));
-  memcpy(recv.data(), c->host_small + 8, P * 8);
+  std::vector<uint64_t> send(P), recv(P);
+  bool wide_any = false;
+  int failed = -1;
   uint64_t nrecv = 0;
-  for (uint32_t p = 0; p < P; ++p) nrecv += recv[p];
-  // payload: keys, values (and maxima) as separate column exchanges (no packing kernel)
-  GS_TRY(ensure(c, c->dist_k, nrecv * 8 + 8));
-  GS_TRY(ensure(c, c->dist_v, nrecv * 8 + 8));
-  if (degmax) GS_TRY(ensure(c, c->dist_v2, nrecv * 8 + 8));
-  GS_TRY(exchange_rows(c, c->dist_k2.as<char>(), send.data(), c->dist_k.as<char>(), recv.data(), 8));
-  GS_TRY(exchange_rows(c, c->dist_v3.as<char>(), send.data(), c->dist_v.as<char>(), recv.data(), vb));
-  if (degmax) GS_TRY(exchange_rows(c, c->dist_v4.as<char>(), send.data(), c->dist_v2.as<char>(), recv.data(), 8));
+  for (uint32_t p = 0; p < P; ++p) {
+    send[p] = c->host_small[8 + 2 * p];
+    recv[p] = c->host_small[8 + 2 * P + 2 * p];
+    const uint64_t fl = c->host_small[8 + 2 * P + 2 * p + 1];
+    wide_any |= (fl & 1) != 0;
+    if ((fl & 2) && failed < 0) failed = (int)p;
+    nrecv += recv[p];
+  }
+  if (local != GS_OK) return set_error(c, local, "%s", local_err.c_str());
+  if (failed >= 0) return set_error(c, GS_ECOMM, "rank %d failed its local step of the window", failed);
+  // 3. one packed exchange of the rows
+  const int kw = wide_any ? 2 : 1, vw = (int)(vb / 4), mw = degmax ? 2 : 0, rw = kw + vw + mw;
+  GS_TRY(ensure(c, c->dist_k, U * (size_t)rw * 4 + 16));   // the local partials are consumed: packed rows out
+  GS_TRY(ensure(c, c->dist_x2, nrecv * (size_t)rw * 4 + 16));
+  if (U) {
+    hipLaunchKernelGGL(k_pack_rows, dim3((unsigned)((U + 255) / 256)), dim3(256), 0, c->stream, c->dist_k2.as<int64_t>(),
+                       c->dist_v3.as<uint32_t>(), degmax ? c->dist_v4.as<int64_t>() : nullptr, U, kw, vw, mw,
+                       c->dist_k.as<uint32_t>());
+    GS_HIP(hipGetLastError());
+  }
+  GS_TRY(exchange_rows(c, c->dist_k.as<char>(), send.data(), c->dist_x2.as<char>(), recv.data(), (size_t)rw * 4));
+  GS_TRY(ensure(c, c->dist_k2, nrecv * 8 + 8));
+  GS_TRY(ensure(c, c->dist_v3, nrecv * vb + 8));
+  if (degmax) GS_TRY(ensure(c, c->dist_v4, nrecv * 8 + 8));
+  if (nrecv) {
+    hipLaunchKernelGGL(k_unpack_rows, dim3((unsigned)((nrecv + 255) / 256)), dim3(256), 0, c->stream,
+                       c->dist_x2.as<uint32_t>(), nrecv, kw, vw, mw, c->dist_k2.as<int64_t>(), c->dist_v3.as<uint32_t>(),
+                       degmax ? c->dist_v4.as<int64_t>() : nullptr);
+    GS_HIP(hipGetLastError());
+  }
+  // 4. the merge of what this rank owns
   const int32_t pdt = degmax || op == GS_OP_COUNT ? GS_I64 : b->val_dtype;
-  const gs_partial_batch pb{c->dist_k.as<int64_t>(), c->dist_v.p, degmax ? c->dist_v2.as<int64_t>() : nullptr, nrecv,
+  const gs_partial_batch pb{c->dist_k2.as<int64_t>(), c->dist_v3.p, degmax ? c->dist_v4.as<int64_t>() : nullptr, nrecv,
                             pdt, GS_MEM_DEVICE};
   gs_status st = degmax ? gs_merge_degree_max_partials(c, &pb, init_max, dout) : gs_merge_partials(c, &pb, op, init, vout);
   c->times = keep;

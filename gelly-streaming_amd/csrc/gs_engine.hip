@@ -79,6 +79,7 @@ uint32_t next_epoch(gs_ctx* c, size_t) {
 }
 
 gs_status begin_call(gs_ctx* c) {
+  ++c->call_seq;   // ends a chunked-candidates session (its sets live in shared workspace)
   GS_HIP(hipSetDevice(c->device));
   GS_HIP(hipMemsetAsync(c->small.as<char>() + SM_TIMEOUT, 0, 8, c->stream));
   return GS_OK;
@@ -467,8 +468,118 @@ static gs_status finish_vertex_out(gs_ctx* c, gs_vertex_out* out, const int64_t*
   return GS_OK;
 }
 
+// ---- windows above one pass's record cap (gs_set_max_window_records) ---------------------------------
+// Edges per pass: max_records / (records per edge); for a host batch also what the free HBM holds (the
+// staged columns plus the pass's workspace, ~64 B per record).  0 = the window runs in one pass.
+static uint64_t chunk_edges(gs_ctx* c, const gs_edge_batch* b, int32_t dir) {
+  if (c->in_chunk) return 0;
+  const uint64_t per = dir == GS_DIR_ALL ? 2 : 1;
+  uint64_t cap = c->max_records / per;
+  if (b->mem == GS_MEM_HOST && b->n >= (1ull << 26)) {
+    size_t fr = 0, tot = 0;
+    if (hipMemGetInfo(&fr, &tot) == hipSuccess) {
+      const uint64_t per_edge = 16 + dtype_bytes(b->val_dtype) + 64 * per;
+      cap = std::min<uint64_t>(cap, std::max<uint64_t>(1ull << 24, (uint64_t)(fr / 2) / per_edge));
+    }
+  }
+  return b->n > cap ? std::max<uint64_t>(cap, 1) : 0;
+}
+
+// grow a device buffer keeping its first `keep` bytes
+static gs_status grow_keep(gs_ctx* c, DevBuf& d, size_t bytes, size_t keep) {
+  if (d.bytes >= bytes) return GS_OK;
+  DevBuf n;
+  GS_TRY(ensure(c, n, bytes));
+  if (keep) GS_HIP(hipMemcpyAsync(n.p, d.p, keep, hipMemcpyDeviceToDevice, c->stream));
+  GS_TRY(host_wait(c));
+  if (d.p) GS_HIP(hipFree(d.p));
+  d = n;
+  return GS_OK;
+}
+
+// The window in chunks of `ce` whole edges: each chunk's per-vertex partials (op with no init; COUNT ->
+// I64 counts; the degree fold -> degree + maximum) are appended after the running partials in one buffer,
+// and the two merged (gs_merge_partials / gs_merge_degree_max_partials) into the other buffer; the last
+// merge applies foldNeighbors' init and writes the caller's output.  Integer ops are associative and
+// commutative, so the result is the one-pass window's bit for bit; float sums change order only.
+static gs_status window_chunked(gs_ctx* c, const gs_edge_batch* b, int32_t dir, int32_t op, bool has_init,
+                                const void* init, bool deg, int64_t init_max, gs_vertex_out* vout,
+                                gs_degree_out* dout, uint64_t ce) {
+  struct InChunk {
+    gs_ctx* c;
+    explicit InChunk(gs_ctx* x) : c(x) { c->in_chunk = true; }
+    ~InChunk() { c->in_chunk = false; }
+  } guard(c);
+  const uint64_t per = dir == GS_DIR_ALL ? 2 : 1;
+  const size_t vb = dtype_bytes(b->val_dtype);
+  const size_t ob = (deg || op == GS_OP_COUNT) ? 8 : vb;
+  const int32_t pdt = (deg || op == GS_OP_COUNT) ? GS_I64 : b->val_dtype;
+  const uint64_t nch = (b->n + ce - 1) / ce;
+  int x = 0;
+  uint64_t acc = 0;   // running partials in ck_*[x][0, acc)
+  for (uint64_t k = 0; k < nch; ++k) {
+    const uint64_t e0 = k * ce, ne = std::min<uint64_t>(ce, b->n - e0), Rc = ne * per;
+    gs_edge_batch cb = *b;
+    cb.src = b->src + e0;
+    cb.dst = b->dst + e0;
+    if (b->val) cb.val = (const char*)b->val + e0 * vb;
+    cb.n = ne;
+    GS_TRY(grow_keep(c, c->ck_k[x], (acc + Rc) * 8 + 64, acc * 8));
+    GS_TRY(grow_keep(c, c->ck_a[x], (acc + Rc) * ob + 64, acc * ob));
+    if (deg) GS_TRY(grow_keep(c, c->ck_b[x], (acc + Rc) * 8 + 64, acc * 8));
+    uint64_t Uc = 0;
+    if (deg) {
+      gs_degree_out po{c->ck_k[x].as<int64_t>() + acc, c->ck_a[x].as<int64_t>() + acc, c->ck_b[x].as<int64_t>() + acc,
+                       Rc, &Uc, GS_MEM_DEVICE, 0};
+      GS_TRY(gs_window_fold_degree_max(c, &cb, dir, INT64_MIN, &po));
+    } else {
+      gs_vertex_out po{c->ck_k[x].as<int64_t>() + acc, c->ck_a[x].as<char>() + acc * ob, Rc, &Uc, GS_MEM_DEVICE, 0};
+      GS_TRY(gs_window_reduce(c, &cb, dir, op, &po));
+    }
+    const uint64_t n = acc + Uc;
+    const bool last = k + 1 == nch;
+    if (k == 0 && !last) {   // nothing to merge with yet
+      acc = n;
+      continue;
+    }
+    const gs_partial_batch pb{c->ck_k[x].as<int64_t>(), c->ck_a[x].p, deg ? c->ck_b[x].as<int64_t>() : nullptr, n, pdt,
+                              GS_MEM_DEVICE};
+    const int y = x ^ 1;
+    if (last) {   // the caller's output, with the fold's init
+      if (deg) return gs_merge_degree_max_partials(c, &pb, init_max, dout);
+      return gs_merge_partials(c, &pb, op, has_init ? init : nullptr, vout);
+    }
+    GS_TRY(ensure(c, c->ck_k[y], n * 8 + 64));
+    GS_TRY(ensure(c, c->ck_a[y], n * ob + 64));
+    uint64_t Um = 0;
+    if (deg) {
+      GS_TRY(ensure(c, c->ck_b[y], n * 8 + 64));
+      gs_degree_out mo{c->ck_k[y].as<int64_t>(), c->ck_a[y].as<int64_t>(), c->ck_b[y].as<int64_t>(), n, &Um,
+                       GS_MEM_DEVICE, 0};
+      GS_TRY(gs_merge_degree_max_partials(c, &pb, INT64_MIN, &mo));
+    } else {
+      gs_vertex_out mo{c->ck_k[y].as<int64_t>(), c->ck_a[y].p, n, &Um, GS_MEM_DEVICE, 0};
+      GS_TRY(gs_merge_partials(c, &pb, op, nullptr, &mo));
+    }
+    x = y;
+    acc = Um;
+  }
+  // one chunk only (not reached: chunk_edges returns 0 then)
+  return set_error(c, GS_EINVAL, "chunked window: no chunks");
+}
+
 static gs_status window_fold_impl(gs_ctx* c, const gs_edge_batch* b, int32_t dir, int32_t op, bool has_init,
                                   const void* init, gs_vertex_out* out) {
+  GS_TRY(check_batch_any(c, b, dir));
+  if (op < GS_OP_SUM || op > GS_OP_COUNT) return set_error(c, GS_EINVAL, "bad op %d", op);
+  if (const uint64_t ce = chunk_edges(c, b, dir)) {
+    if (!out || !out->n_out || (out->capacity && (!out->keys || !out->vals)))
+      return set_error(c, GS_EINVAL, "bad gs_vertex_out");
+    if (op != GS_OP_COUNT && (b->val_dtype == GS_NONE || (b->n && !b->val)))
+      return set_error(c, GS_EINVAL, "op %d needs edge values", op);
+    if (has_init && !init) return set_error(c, GS_EINVAL, "null init");
+    return window_chunked(c, b, dir, op, has_init, init, false, 0, out, nullptr, ce);
+  }
   GS_TRY(check_batch(c, b, dir));
   if (!out || !out->n_out || (out->capacity && (!out->keys || !out->vals)))
     return set_error(c, GS_EINVAL, "bad gs_vertex_out");
@@ -555,11 +666,21 @@ gs_status gs_window_fold(gs_ctx* c, const gs_edge_batch* b, int32_t dir, int32_t
   return window_fold_impl(c, b, dir, op, true, init, out);
 }
 
+gs_status gs_set_max_window_records(gs_ctx* c, uint64_t max_records) {
+  if (!c) return GS_EINVAL;
+  const uint64_t lim = (1ull << 32) - 1;
+  c->max_records = max_records == 0 || max_records > lim ? lim : std::max<uint64_t>(max_records, 2);
+  return GS_OK;
+}
+
 gs_status gs_window_fold_degree_max(gs_ctx* c, const gs_edge_batch* b, int32_t dir, int64_t init_max,
                                     gs_degree_out* out) {
-  GS_TRY(check_batch(c, b, dir));
+  GS_TRY(check_batch_any(c, b, dir));
   if (!out || !out->n_out || (out->capacity && (!out->keys || !out->degree || !out->max_neighbor)))
     return set_error(c, GS_EINVAL, "bad gs_degree_out");
+  if (const uint64_t ce = chunk_edges(c, b, dir)) return window_chunked(c, b, dir, 0, false, nullptr, true, init_max,
+                                                                        nullptr, out, ce);
+  GS_TRY(check_batch(c, b, dir));
   GS_TRY(begin_call(c));
   const uint64_t R = dir == GS_DIR_ALL ? 2 * b->n : b->n;
   if (R == 0) {

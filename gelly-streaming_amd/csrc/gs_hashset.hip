@@ -259,6 +259,101 @@ __global__ __launch_bounds__(256) void k_hs_emit_pairs(uint32_t M, const uint64_
   }
 }
 
+// ---- chunked emission: the records at global output positions [P0, P1) ---------------------------
+// The whole window's output order (gs_window_candidates): vertex u's edge records at p + LS[doff[u]]
+// (p = its record positions, off[u] .. off[u+1]), then its pair rows, row q at off[u+1] + LS[q] with
+// L[q] = LS[q+1] - LS[q] pairs.  Both position maps are monotone, so one thread finds by binary search
+// the records p in [b[0], b[1]) and the rows q in [b[2], b[3]) that reach into the range.
+__global__ void k_cand_bounds(const uint32_t* __restrict__ useg, uint32_t R, const uint64_t* __restrict__ off,
+                              const uint64_t* __restrict__ doff, uint32_t U, uint32_t M,
+                              const uint64_t* __restrict__ LS, uint64_t P0, uint64_t P1,
+                              unsigned long long* __restrict__ b) {
+  auto rpos = [&](uint32_t p) { return (uint64_t)p + LS[doff[useg[p]]]; };
+  auto first_rec = [&](uint64_t P) {   // first p with rpos(p) >= P
+    uint32_t lo = 0, hi = R;
+    while (lo < hi) {
+      const uint32_t mid = lo + (hi - lo) / 2;
+      if (rpos(mid) >= P) hi = mid;
+      else lo = mid + 1;
+    }
+    return lo;
+  };
+  auto rend = [&](uint32_t q) { return off[seg_of(doff, U, q) + 1] + LS[q + 1]; };    // row end position
+  auto rbeg = [&](uint32_t q) { return off[seg_of(doff, U, q) + 1] + LS[q]; };
+  auto first_row = [&](uint64_t P, bool by_end) {   // first q with end > P (by_end) / begin >= P
+    uint32_t lo = 0, hi = M;
+    while (lo < hi) {
+      const uint32_t mid = lo + (hi - lo) / 2;
+      if (by_end ? rend(mid) > P : rbeg(mid) >= P) hi = mid;
+      else lo = mid + 1;
+    }
+    return lo;
+  };
+  b[0] = first_rec(P0);
+  b[1] = first_rec(P1);
+  b[2] = first_row(P0, true);
+  b[3] = first_row(P1, false);
+}
+
+__global__ __launch_bounds__(256) void k_hs_emit_false_range(const uint32_t* __restrict__ useg,
+                                                             const uint64_t* __restrict__ doff,
+                                                             const uint64_t* __restrict__ LS,
+                                                             const int64_t* __restrict__ vkeys,
+                                                             const int64_t* __restrict__ nbr,
+                                                             const unsigned long long* __restrict__ bnd, uint64_t P0,
+                                                             int64_t* __restrict__ a, int64_t* __restrict__ b,
+                                                             uint8_t* __restrict__ f) {
+  const uint64_t p0 = bnd[0], p1 = bnd[1];
+  for (uint64_t p = p0 + blockIdx.x * 256ull + threadIdx.x; p < p1; p += (uint64_t)gridDim.x * 256u) {
+    const uint32_t u = useg[p];
+    const uint64_t pos = p + LS[doff[u]] - P0;
+    a[pos] = vkeys[u];
+    b[pos] = nbr[p];
+    f[pos] = 0;
+  }
+}
+
+// row q's pairs that fall in [P0, P1): the first one found by binary search over gx (the scan of the
+// "> v" flags: the t-th pair of row q is the j >= q with gx[j] - gx[q] == t and ids[j] > v)
+__global__ __launch_bounds__(256) void k_hs_emit_pairs_range(const uint64_t* __restrict__ doff, uint32_t U,
+                                                             const uint64_t* __restrict__ off,
+                                                             const uint64_t* __restrict__ LS,
+                                                             const uint64_t* __restrict__ gx,
+                                                             const int64_t* __restrict__ ids,
+                                                             const int64_t* __restrict__ vkeys,
+                                                             const unsigned long long* __restrict__ bnd, uint64_t P0,
+                                                             uint64_t P1, int64_t* __restrict__ a,
+                                                             int64_t* __restrict__ b, uint8_t* __restrict__ f) {
+  const uint64_t q0 = bnd[2], q1 = bnd[3];
+  for (uint64_t q = q0 + blockIdx.x * 256ull + threadIdx.x; q < q1; q += (uint64_t)gridDim.x * 256u) {
+    if (LS[q + 1] == LS[q]) continue;
+    const uint32_t u = seg_of(doff, U, q);
+    const int64_t v = vkeys[u], xi = ids[q];
+    const uint64_t rb = off[u + 1] + LS[q], end = doff[u + 1];
+    uint64_t o = rb, j = q;
+    if (rb < P0) {   // skip the row's first P0 - rb pairs
+      const uint64_t t = P0 - rb;
+      uint64_t lo = q, hi = end - 1;   // smallest j with gx[j + 1] - gx[q] > t
+      while (lo < hi) {
+        const uint64_t mid = (lo + hi) / 2;
+        if (gx[mid + 1] - gx[q] > t) hi = mid;
+        else lo = mid + 1;
+      }
+      j = lo;
+      o = P0;
+    }
+    for (; j < end && o < P1; ++j) {
+      const int64_t xj = ids[j];
+      if (xj > v) {
+        a[o - P0] = xi;
+        b[o - P0] = xj;
+        f[o - P0] = 1;
+        ++o;
+      }
+    }
+  }
+}
+
 // self-pair term of WindowTriangles: matched (x, x, true) candidates need a self-loop on x
 __global__ __launch_bounds__(256) void k_hs_selfpairs(const int64_t* __restrict__ ids, uint32_t M,
                                                       const uint64_t* __restrict__ doff, uint32_t U,
@@ -922,6 +1017,99 @@ gs_status gs_window_candidates_part(gs_ctx* c, const gs_edge_batch* b, uint32_t 
 
 gs_status gs_window_candidates(gs_ctx* c, const gs_edge_batch* b, gs_pair_out* out) {
   return gs_window_candidates_part(c, b, 1, 0, out);
+}
+
+gs_status gs_candidates_begin(gs_ctx* c, const gs_edge_batch* b, uint64_t* total_records, uint32_t* jdk_flags) {
+  GS_TRY(check_batch(c, b, GS_DIR_ALL));
+  if (!total_records) return set_error(c, GS_EINVAL, "null total_records");
+  GS_TRY(begin_call(c));
+  c->cand_seq = c->call_seq;
+  c->cand_total = c->cand_cursor = c->cand_R = 0;
+  c->cand_U = c->cand_M = 0;
+  *total_records = 0;
+  if (jdk_flags) *jdk_flags = 0;
+  if (b->n == 0) return GS_OK;
+  const int64_t *src, *dst;
+  const void* val;
+  GS_TRY(stage_batch(c, b, &src, &dst, &val, false));
+  uint32_t U = 0, M = 0, fl = 0;
+  uint64_t key_xor = 0;
+  GS_TRY(hashset_order(c, src, dst, b->n, &U, &M, &key_xor, &fl));
+  GS_TRY(ensure(c, c->hs[HS_G], (M + 1) * 8));
+  GS_TRY(ensure(c, c->hs[HS_GX], (M + 1) * 8));
+  GS_TRY(ensure(c, c->hs[HS_L], (M + 1) * 8));
+  GS_TRY(ensure(c, c->hs[HS_LS], (M + 1) * 8));
+  hipLaunchKernelGGL(k_hs_gt, dim3(g256(M)), dim3(256), 0, c->stream, c->hs[HS_IDS].as<int64_t>(), M,
+                     c->hs[HS_DOFF].as<uint64_t>(), U, c->hs[HS_VKEYS].as<int64_t>(), c->hs[HS_G].as<uint64_t>());
+  GS_HIP(hipGetLastError());
+  GS_TRY(xscan(c, c->hs[HS_G].as<uint64_t>(), M, c->hs[HS_GX].as<uint64_t>()));
+  hipLaunchKernelGGL(k_hs_rowlen, dim3(g256(M)), dim3(256), 0, c->stream, c->hs[HS_GX].as<uint64_t>(), M,
+                     c->hs[HS_DOFF].as<uint64_t>(), U, c->hs[HS_IDS].as<int64_t>(), c->hs[HS_VKEYS].as<int64_t>(),
+                     1u, 0u, c->hs[HS_L].as<uint64_t>());
+  GS_HIP(hipGetLastError());
+  GS_TRY(xscan(c, c->hs[HS_L].as<uint64_t>(), M, c->hs[HS_LS].as<uint64_t>()));
+  GS_HIP(hipMemcpyAsync(&c->host_small[7], c->hs[HS_LS].as<uint64_t>() + M, 8, hipMemcpyDeviceToHost, c->stream));
+  GS_TRY(host_wait(c));
+  c->cand_U = U;
+  c->cand_M = M;
+  c->cand_R = 2 * b->n;
+  c->cand_total = 2 * b->n + c->host_small[7];
+  *total_records = c->cand_total;
+  if (jdk_flags) *jdk_flags = fl;
+  return GS_OK;
+}
+
+gs_status gs_candidates_next(gs_ctx* c, gs_pair_out* out, uint64_t* first_record, int32_t* done) {
+  if (!c) return GS_EINVAL;
+  if (!out || !out->n_out || (out->capacity && (!out->a || !out->b || !out->is_candidate)))
+    return set_error(c, GS_EINVAL, "bad gs_pair_out");
+  if (c->cand_seq != c->call_seq)
+    return set_error(c, GS_EINVAL, "no candidates session (gs_candidates_begin; a later call on the ctx ends it)");
+  GS_HIP(hipSetDevice(c->device));
+  const uint64_t P0 = c->cand_cursor, n = std::min<uint64_t>(out->capacity, c->cand_total - P0), P1 = P0 + n;
+  if (first_record) *first_record = P0;
+  *out->n_out = n;
+  out->reserved = 0;
+  if (n == 0) {
+    if (done) *done = c->cand_cursor >= c->cand_total;
+    if (c->cand_total > P0 && out->capacity == 0) return set_error(c, GS_ECAPACITY, "capacity 0");
+    return GS_OK;
+  }
+  const uint32_t U = c->cand_U, M = c->cand_M;
+  int64_t *a = out->a, *bb = out->b;
+  uint8_t* f = out->is_candidate;
+  const bool direct = out->mem == GS_MEM_DEVICE;
+  if (!direct) {
+    GS_TRY(ensure(c, c->out_keys, n * 8));
+    GS_TRY(ensure(c, c->out_a, n * 8));
+    GS_TRY(ensure(c, c->out_b, n));
+    a = c->out_keys.as<int64_t>();
+    bb = c->out_a.as<int64_t>();
+    f = c->out_b.as<uint8_t>();
+  }
+  GS_TRY(ensure(c, c->cand_bounds, 64));
+  auto* bnd = c->cand_bounds.as<unsigned long long>();
+  const uint64_t* off = c->hs[HS_OFF].as<uint64_t>();
+  const uint64_t recs = c->cand_R;
+  hipLaunchKernelGGL(k_cand_bounds, dim3(1), dim3(1), 0, c->stream, c->hs[HS_USEG].as<uint32_t>(), (uint32_t)recs, off,
+                     c->hs[HS_DOFF].as<uint64_t>(), U, M, c->hs[HS_LS].as<uint64_t>(), P0, P1, bnd);
+  const unsigned grid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((n + 255) / 256, 8192));
+  hipLaunchKernelGGL(k_hs_emit_false_range, dim3(grid), dim3(256), 0, c->stream, c->hs[HS_USEG].as<uint32_t>(),
+                     c->hs[HS_DOFF].as<uint64_t>(), c->hs[HS_LS].as<uint64_t>(), c->hs[HS_VKEYS].as<int64_t>(),
+                     c->hs[HS_NBR].as<int64_t>(), bnd, P0, a, bb, f);
+  hipLaunchKernelGGL(k_hs_emit_pairs_range, dim3((unsigned)std::min<uint64_t>(g256(M), 8192)), dim3(256), 0, c->stream,
+                     c->hs[HS_DOFF].as<uint64_t>(), U, off, c->hs[HS_LS].as<uint64_t>(), c->hs[HS_GX].as<uint64_t>(),
+                     c->hs[HS_IDS].as<int64_t>(), c->hs[HS_VKEYS].as<int64_t>(), bnd, P0, P1, a, bb, f);
+  GS_HIP(hipGetLastError());
+  if (!direct) {
+    GS_HIP(hipMemcpyAsync(out->a, a, n * 8, hipMemcpyDeviceToHost, c->stream));
+    GS_HIP(hipMemcpyAsync(out->b, bb, n * 8, hipMemcpyDeviceToHost, c->stream));
+    GS_HIP(hipMemcpyAsync(out->is_candidate, f, n, hipMemcpyDeviceToHost, c->stream));
+  }
+  GS_TRY(host_wait(c));
+  c->cand_cursor = P1;
+  if (done) *done = P1 >= c->cand_total;
+  return GS_OK;
 }
 
 }  // extern "C"

@@ -48,6 +48,15 @@ struct gs_ctx {
   size_t last_ob = 0;
   int last_kind = 0;  // direct bucket path: > 0 = windows left that store 8-byte values (escapes were common)
   int n_cu = 0;          // compute units (persistent grids)
+  // chunked windows (gs_set_max_window_records): records per engine pass, running partials (ping-pong)
+  uint64_t max_records = (1ull << 32) - 1;
+  bool in_chunk = false;
+  gs::DevBuf ck_k[2], ck_a[2], ck_b[2];
+  // chunked candidate emission (gs_candidates_begin / _next): the window's HashSet-ordered sets stay in
+  // hs[] until the next entry point call on the ctx (call_seq) ends the session
+  uint64_t call_seq = 0, cand_seq = ~0ull, cand_total = 0, cand_cursor = 0, cand_R = 0;
+  uint32_t cand_U = 0, cand_M = 0;
+  gs::DevBuf cand_bounds;
   // input staging (host batches)
   gs::DevBuf in_src, in_dst, in_val;
   // sort ping-pong
@@ -91,7 +100,7 @@ struct gs_ctx {
   gs::DevBuf tx_text, tx_cnt, tx_starts;
   // multi-GPU keyBy (gs_dist.hip): staging of the local reduce, owner-grouped partials, received rows,
   // per-tile owner counts; the ctx-owned RCCL communicator (opaque ncclComm_t)
-  gs::DevBuf dist_k, dist_v, dist_v2, dist_k2, dist_v3, dist_v4, dist_cnt;
+  gs::DevBuf dist_k, dist_v, dist_v2, dist_k2, dist_v3, dist_v4, dist_cnt, dist_x, dist_x2;
   void* comm = nullptr;
   int comm_size = 0, comm_rank = 0;
   // relabeling of arbitrary vertex IDs (gs_relabel.hip)
@@ -128,7 +137,7 @@ constexpr size_t SM_HS = SM_DEV_ERR + 8;            // u32[4] HashSet order: com
 constexpr size_t SM_BYTES = SM_HS + 16;
 // device error flags (SM_DEV_ERR): a kernel that cannot finish its work sets one and returns
 constexpr uint32_t GS_DERR_TABLE_FULL = 1u;         // an LDS hash set filled up (triangle counting)
-constexpr size_t HOST_SMALL_WORDS = 128;            // pinned u64 mirror of small scalars
+constexpr size_t HOST_SMALL_WORDS = 512;            // pinned u64 mirror of small scalars
 
 gs_status set_error(gs_ctx* c, gs_status s, const char* fmt, ...);
 gs_status hip_check(gs_ctx* c, hipError_t e, const char* what);
@@ -163,6 +172,7 @@ gs_status triangle_selfpair_term(gs_ctx* c, const int64_t* src, const int64_t* d
 constexpr int NCCL_T_U32 = 3, NCCL_T_I64 = 4, NCCL_T_U64 = 5, NCCL_OP_SUM = 0, NCCL_OP_MAX = 2, NCCL_OP_MIN = 3;
 gs_status comm_allreduce(gs_ctx* c, void* buf, size_t count, int nccl_dtype, int nccl_op);
 gs_status comm_allgather_u64(gs_ctx* c, uint64_t mine, uint64_t* all);
+gs_status comm_agree(gs_ctx* c, gs_status local);
 gs_status exchange_rows(gs_ctx* c, const char* sendbuf, const uint64_t* send, char* recvbuf, const uint64_t* recv,
                         size_t row);
 gs_status comm_allgatherv(gs_ctx* c, const void* sendbuf, char* recvbuf, const uint64_t* counts, size_t row);

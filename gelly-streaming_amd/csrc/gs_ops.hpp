@@ -124,6 +124,17 @@ inline gs_status check_batch(gs_ctx* c, const gs_edge_batch* b, int dir) {
   return GS_OK;
 }
 
+// reduce / fold / degree fold: any window size (chunked above one pass's record cap, gs_engine.hip)
+inline gs_status check_batch_any(gs_ctx* c, const gs_edge_batch* b, int dir) {
+  if (!c) return GS_EINVAL;
+  if (!b) return set_error(c, GS_EINVAL, "null batch");
+  if (dir < 0 || dir > 2) return set_error(c, GS_EINVAL, "bad EdgeDirection %d", dir);
+  if (b->n && (!b->src || !b->dst)) return set_error(c, GS_EINVAL, "null src/dst");
+  if (b->val_dtype < GS_I32 || b->val_dtype > GS_NONE) return set_error(c, GS_EINVAL, "bad dtype %d", b->val_dtype);
+  if (b->n >= (1ull << 62)) return set_error(c, GS_EINVAL, "window has %llu edges", (unsigned long long)b->n);
+  return GS_OK;
+}
+
 // The last radix pass fused with the per-vertex combine (gs_combine.hpp), then the merge of the
 // few partials a vertex leaves when its records straddle tiles.  `s` holds passes 0..P-2.
 template <typename K, class Op, class Out>

@@ -929,7 +929,7 @@ gs_status gs_window_triangles_dist(gs_ctx* c, const gs_edge_batch* b, uint64_t* 
   const uint32_t P = (uint32_t)c->comm_size, me = (uint32_t)c->comm_rank;
   // 1. the common id range
   int64_t mm[2];
-  GS_TRY(gs_tri_dist_range(c, b, mm));
+  GS_TRY(comm_agree(c, gs_tri_dist_range(c, b, mm)));   // every local step: status agreed before the collective
   GS_TRY(ensure(c, c->tri_d[0], 64));
   long long* dmm = c->tri_d[0].as<long long>();
   c->host_small[12] = (uint64_t)mm[0];
@@ -948,16 +948,18 @@ gs_status gs_window_triangles_dist(gs_ctx* c, const gs_edge_batch* b, uint64_t* 
   if (total_n == 0) return GS_OK;
   // 2. degrees, summed over ranks
   uint64_t V = 0;
-  GS_TRY(gs_tri_dist_degrees(c, b, gmin, gmax, nullptr, &V));
-  GS_TRY(ensure(c, c->tri_d[1], V * 4));
+  gs_status st = gs_tri_dist_degrees(c, b, gmin, gmax, nullptr, &V);
+  if (st == GS_OK) st = ensure(c, c->tri_d[1], V * 4);
   uint32_t* deg = c->tri_d[1].as<uint32_t>();
-  GS_TRY(gs_tri_dist_degrees(c, b, gmin, gmax, deg, &V));
+  if (st == GS_OK) st = gs_tri_dist_degrees(c, b, gmin, gmax, deg, &V);
+  GS_TRY(comm_agree(c, st));
   GS_TRY(comm_allreduce(c, deg, V, NCCL_T_U32, NCCL_OP_SUM));
   // 3. oriented edges to owner(u): counts matrix, then the rows
-  GS_TRY(ensure(c, c->tri_d[2], b->n * 8 + 8));
   std::vector<uint64_t> send(P), recv(P);
   uint64_t loops = 0;
-  GS_TRY(gs_tri_dist_route(c, b, deg, P, c->tri_d[2].as<uint64_t>(), send.data(), &loops));
+  st = ensure(c, c->tri_d[2], b->n * 8 + 8);
+  if (st == GS_OK) st = gs_tri_dist_route(c, b, deg, P, c->tri_d[2].as<uint64_t>(), send.data(), &loops);
+  GS_TRY(comm_agree(c, st));
   GS_TRY(ensure(c, c->tri_d[0], 64 + (size_t)P * P * 8));
   uint64_t* dmat = (uint64_t*)(c->tri_d[0].as<char>() + 64);
   GS_HIP(hipMemsetAsync(dmat, 0, (size_t)P * P * 8, c->stream));
@@ -978,7 +980,7 @@ gs_status gs_window_triangles_dist(gs_ctx* c, const gs_edge_batch* b, uint64_t* 
   GS_TRY(ensure(c, c->tri_d[1], V * 4));   // the degrees are consumed: d+ reuses the buffer
   uint32_t* dplus = c->tri_d[1].as<uint32_t>();
   uint64_t m = 0;
-  GS_TRY(gs_tri_dist_build(c, c->tri_d[3].as<uint64_t>(), nrecv, c->tri_d[4].as<uint32_t>(), dplus, &m));
+  GS_TRY(comm_agree(c, gs_tri_dist_build(c, c->tri_d[3].as<uint64_t>(), nrecv, c->tri_d[4].as<uint32_t>(), dplus, &m)));
   GS_TRY(comm_allreduce(c, dplus, V, NCCL_T_U32, NCCL_OP_SUM));
   std::vector<uint64_t> ms(P);
   GS_TRY(comm_allgather_u64(c, m, ms.data()));
@@ -988,7 +990,7 @@ gs_status gs_window_triangles_dist(gs_ctx* c, const gs_edge_batch* b, uint64_t* 
   GS_TRY(comm_allgatherv(c, c->tri_d[4].p, c->tri_d[2].as<char>(), ms.data(), 4));
   // 5. this rank's share of the count, summed
   uint64_t T = 0;
-  GS_TRY(gs_tri_dist_count(c, c->tri_d[2].as<uint32_t>(), M, dplus, me, P, &T));
+  GS_TRY(comm_agree(c, gs_tri_dist_count(c, c->tri_d[2].as<uint32_t>(), M, dplus, me, P, &T)));
   // 6. the self-pair term needs whole neighbour sets: windows with self-loops gather the records
   if (loops) {
     std::vector<uint64_t> ns(P);
@@ -1001,12 +1003,14 @@ gs_status gs_window_triangles_dist(gs_ctx* c, const gs_edge_batch* b, uint64_t* 
     GS_TRY(comm_allgatherv(c, src, (char*)all, ns.data(), 8));
     GS_TRY(comm_allgatherv(c, dst, (char*)(all + total_n), ns.data(), 8));
     GS_TRY(host_wait(c));
+    gs_status sp = GS_OK;
     if (me == 0) {
       const gs_edge_batch wb{all, all + total_n, nullptr, total_n, GS_NONE, GS_MEM_DEVICE, 0};
       uint64_t S = 0;
-      GS_TRY(gs_window_triangles_selfpair(c, &wb, &S));
+      sp = gs_window_triangles_selfpair(c, &wb, &S);
       T += S;
     }
+    GS_TRY(comm_agree(c, sp));
   }
   GS_TRY(gs_comm_allreduce_sum_u64(c, &T));
   *count = T;

@@ -60,7 +60,10 @@ def exchange_partials(keys: torch.Tensor, cols: list, counts: list, group=None):
     parts = [kpart] + [c.contiguous() for c in cols]
     widths = [p.element_size() for p in parts]
     row = sum(widths)
-    packed = torch.cat([p.view(torch.uint8).view(-1, w) for p, w in zip(parts, widths)], dim=1).to(cdev)
+    # an empty slice may come as a stride-0 tensor, which cannot be viewed as bytes
+    as_bytes = lambda p, w: p.view(torch.uint8).view(-1, w) if p.numel() else \
+        torch.empty((0, w), dtype=torch.uint8, device=p.device)
+    packed = torch.cat([as_bytes(p, w) for p, w in zip(parts, widths)], dim=1).to(cdev)
     rp = torch.empty((sum(recv_counts), row), dtype=torch.uint8, device=cdev)
     dist.all_to_all_single(rp, packed, recv_counts, list(counts), group=group)
     rp = rp.to(home)
@@ -186,12 +189,16 @@ def triangles_window(eng, src, dst, group=None):
     world, rank = dist.get_world_size(group), dist.get_rank(group)
     home = src.device
     cdev = _comm_device(group, src)
+    # an empty slice reports (INT64_MAX, INT64_MIN): reduce lo by MIN and hi by MAX directly (negating
+    # INT64_MIN would overflow), so a rank with no records joins every collective like the others
     lo, hi = eng.tri_dist_range(src, dst)
-    mm = torch.tensor([lo, -hi, src.numel()], dtype=torch.int64, device=cdev)
-    dist.all_reduce(mm[:2], op=dist.ReduceOp.MIN, group=group)   # max as -min(-x)
-    nt = mm[2:].clone()
+    lo_t = torch.tensor([lo], dtype=torch.int64, device=cdev)
+    hi_t = torch.tensor([hi], dtype=torch.int64, device=cdev)
+    nt = torch.tensor([src.numel()], dtype=torch.int64, device=cdev)
+    dist.all_reduce(lo_t, op=dist.ReduceOp.MIN, group=group)
+    dist.all_reduce(hi_t, op=dist.ReduceOp.MAX, group=group)
     dist.all_reduce(nt, op=dist.ReduceOp.SUM, group=group)
-    gmin, gmax, total = int(mm[0]), -int(mm[1]), int(nt[0])
+    gmin, gmax, total = int(lo_t[0]), int(hi_t[0]), int(nt[0])
     if total == 0:
         return 0, 0, False
     deg = eng.tri_dist_degrees(src, dst, gmin, gmax)

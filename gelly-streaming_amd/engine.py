@@ -117,6 +117,11 @@ class Engine:
         with torch.cuda.device(self.device):
             self.set_stream(torch.cuda.current_stream(self.device).cuda_stream)
 
+    def set_max_window_records(self, max_records: int):
+        """gs_set_max_window_records: records per engine pass; larger reduce / fold windows run in chunks
+        merged through the partials halves (0 = the default, 2^32 - 1)."""
+        self._check(self._L.gs_set_max_window_records(self.ctx, int(max_records)))
+
     def synchronize(self):
         self._check(self._L.gs_synchronize(self.ctx))
 
@@ -234,6 +239,31 @@ class Engine:
         self._check(call(out))
         self.last_candidates_jdk_flags = int(out.reserved)
         return a[:P], bb[:P], f[:P]
+
+    def candidates_begin(self, src, dst) -> int:
+        """gs_candidates_begin: build the window's HashSet-ordered sets once; returns the record count.
+        The columns must stay alive (and unchanged) until the session's last candidates_next."""
+        b, keep, dev = self._batch(src, dst, None)
+        total, fl = ctypes.c_uint64(0), ctypes.c_uint32(0)
+        self._check(self._L.gs_candidates_begin(self.ctx, ctypes.byref(b), ctypes.byref(total), ctypes.byref(fl)))
+        self._cand_dev = dev
+        self.last_candidates_jdk_flags = int(fl.value)
+        return total.value
+
+    def candidates_next(self, capacity: int, out=None):
+        """gs_candidates_next: the next <= capacity records (a, b, is_candidate) of the session, the global
+        position of the first and whether the session is done.  out: optional (a, b, f) buffers to fill."""
+        dev = self._cand_dev
+        if out is None:
+            out = (self._empty(dev, capacity, np.int64), self._empty(dev, capacity, np.int64),
+                   self._empty(dev, capacity, np.uint8))
+        a, bb, f = out
+        n_out, first, done = ctypes.c_uint64(0), ctypes.c_uint64(0), ctypes.c_int32(0)
+        o = L.GsPairOut(_ptr(a), _ptr(bb), _ptr(f), capacity, ctypes.pointer(n_out),
+                        L.GS_MEM_DEVICE if dev else L.GS_MEM_HOST, 0)
+        self._check(self._L.gs_candidates_next(self.ctx, ctypes.byref(o), ctypes.byref(first), ctypes.byref(done)))
+        n = n_out.value
+        return a[:n], bb[:n], f[:n], first.value, bool(done.value)
 
     def candidate_count(self, src, dst) -> int:
         """Sizing call of gs_window_candidates (capacity 0): the number of records the window emits."""

@@ -90,6 +90,8 @@ typedef struct gs_ctx gs_ctx;
                                   bucket, so sets overflow and the call must fail with GS_EDEVICE   */
 #define GS_FLAG_NO_SPEC 16u    /* bucket path: no speculative partition (packed windows always count
                                   per-tile bucket histograms first; A/B measurement; same results)  */
+#define GS_FLAG_TEST_FORCE_EXCHANGE 32u /* TEST ONLY: gs_window_*_dist on a one-rank communicator still
+                                  runs the owner partition, the exchange (to itself) and the merge   */
 
 typedef struct gs_config {
   int32_t device;          /* HIP device ordinal                                           */
@@ -188,6 +190,16 @@ GS_API gs_status gs_window_fold(gs_ctx* ctx, const gs_edge_batch* batch, int32_t
 GS_API gs_status gs_window_fold_degree_max(gs_ctx* ctx, const gs_edge_batch* batch, int32_t dir,
                                     int64_t init_max, gs_degree_out* out);
 
+/* Windows of any size for reduce / fold / the degree fold (SimpleEdgeStream.java:159-167: keyBy puts
+ * no cap on a window).  One pass of the engine takes at most max_records direction-expanded records
+ * (default and upper bound 2^32 - 1: 32-bit record positions); a host batch is also cut so that each
+ * pass's columns and workspace fit the device's free HBM.  A larger window runs in chunks of whole
+ * edges, each reduced to per-vertex partials (gs_window_reduce_partials' local half) and merged into
+ * a running set of partials (gs_merge_partials; foldNeighbors' init applied once, at the end).
+ * Integer results are bit-exact; float sums stay within the API's 1e-5 relative tolerance.  Tests
+ * set a small max_records to force chunking; 0 restores the default. */
+GS_API gs_status gs_set_max_window_records(gs_ctx* ctx, uint64_t max_records);
+
 /* The grouping half of applyOnNeighbors (GraphWindowStream.java:130-175): the window's
  * neighbourhoods as a CSR in arrival order, for a host-side user EdgesApply to iterate. */
 GS_API gs_status gs_window_csr(gs_ctx* ctx, const gs_edge_batch* batch, int32_t dir, gs_csr_out* out);
@@ -200,6 +212,18 @@ GS_API gs_status gs_window_csr(gs_ctx* ctx, const gs_edge_batch* batch, int32_t 
  * capacity 64, red-black tree bins above); out->reserved reports it: bit 0 = a tree bin, bit 1 = a
  * collision resize. */
 GS_API gs_status gs_window_candidates(gs_ctx* ctx, const gs_edge_batch* batch, gs_pair_out* out);
+
+/* The same records in chunks, for consumers that stream them (a window's output is O(sum d^2): a 1e8-edge
+ * R-MAT scale-23 window emits 1.6e11 records, 2.7 TB).  gs_candidates_begin builds the window's
+ * HashSet-ordered neighbour sets once and returns the number of records gs_window_candidates would
+ * write; each gs_candidates_next then writes the next min(out->capacity, remaining) records, in
+ * gs_window_candidates' order (*first_record = the global position of the chunk's first record; a
+ * vertex's records may straddle chunks), and sets *done after the last.  The session lives in the ctx
+ * workspace: any other entry point called on the ctx ends it (gs_candidates_next then fails with
+ * GS_EINVAL). */
+GS_API gs_status gs_candidates_begin(gs_ctx* ctx, const gs_edge_batch* batch, uint64_t* total_records,
+                                     uint32_t* jdk_flags);
+GS_API gs_status gs_candidates_next(gs_ctx* ctx, gs_pair_out* out, uint64_t* first_record, int32_t* done);
 
 /* Multi-GPU candidates (partition by owner(v), no exchange of pairs): only the vertices
  * v with gs_owner_of(v, nparts) == part emit, with exactly the records gs_window_candidates gives them

@@ -754,12 +754,25 @@ GSO_API int64_t gso_window_candidates(const int64_t* src, const int64_t* dst, ui
     }
     const uint64_t k = distinct_of(c.nbr + lo, hi - lo, dist);
     *treeified |= hashset_order(dist, k, ids, tmp);
-    for (uint64_t i = 0; i + 1 < k; ++i)          /* i < len-1 :104 */
-      for (uint64_t j = i; j < k; ++j)            /* j = i (self pair) :105 */
-        if (ids[i] > v && ids[j] > v) {           /* :108 */
-          if (o < cap) { a[o] = ids[i]; b[o] = ids[j]; flag[o] = 1; }
-          ++o;
-        }
+    /* the ids above v, in HashSet order (kept in place in `ids`); the loops below emit the pairs
+     * (i, j), i < len-1, j >= i, of those: C(m, 2) + m records, less the self pair of the last element
+     * when it is above v */
+    const int last_above = k > 0 && ids[k - 1] > v;   /* then it is also the last id above v */
+    uint64_t m = 0;
+    for (uint64_t i = 0; i < k; ++i)
+      if (ids[i] > v) ids[m++] = ids[i];
+    const uint64_t cnt = m * (m - 1) / 2 + m - (uint64_t)last_above;
+    if (o + cnt > cap) {   /* a size query (or past capacity): the count only */
+      o += cnt;
+      continue;
+    }
+    for (uint64_t i = 0; i < m; ++i) {             /* i < len-1 :104 (the last element only as j) */
+      if (last_above && i + 1 == m) break;
+      for (uint64_t j = i; j < m; ++j) {          /* j = i (self pair) :105; both above v :108 */
+        a[o] = ids[i]; b[o] = ids[j]; flag[o] = 1;
+        ++o;
+      }
+    }
   }
   free(dist); free(ids); free(tmp); free_csr(&c);
   return o <= cap ? (int64_t)o : -1 - (int64_t)o;
@@ -1259,102 +1272,227 @@ static void* tri_map_worker(void* p) {   /* endpoint -> compact ID by binary sea
   return NULL;
 }
 
-static void* tri_count_worker(void* p) {
-  tri_arg* A = (tri_arg*)p;
+/* Parallel phases of the forward count (test infrastructure: makes the config-size triangle parity
+ * tests (R-MAT s24 / s26, 2^28 / 2^30 edges) run in a minute or so).  Every phase is a plain loop
+ * split over threads; shared counters use relaxed atomics. */
+typedef struct tf_ctx {
+  const int64_t *src, *dst; uint64_t n;
+  int64_t kmin; uint64_t range;            /* direct compaction: ids in [kmin, kmin + range) */
+  uint32_t* map;                           /* id - kmin -> compact id + 1 (0: absent) */
+  uint32_t *cs, *cd; uint64_t V;
+  uint64_t *off, *cur;                     /* CSR by the smaller endpoint, then by orientation */
+  uint32_t *lst, *ucnt, *deg, *nbr;
+  uint64_t* uoff; uint32_t* ulst;          /* distinct undirected edges (a < b), by a */
+  volatile uint64_t next; int P; int bad;
+  int64_t mn[64], mx[64]; uint64_t T[64];
+} tf_ctx;
+typedef struct { tf_ctx* c; int t; void (*fn)(tf_ctx*, int); } tf_job;
+static void* tf_tramp(void* p) { tf_job* j = (tf_job*)p; j->fn(j->c, j->t); return NULL; }
+static void tf_par(tf_ctx* c, void (*fn)(tf_ctx*, int)) {
+  pthread_t th[64]; tf_job jb[64];
+  for (int t = 0; t < c->P; ++t) { jb[t] = (tf_job){c, t, fn}; pthread_create(&th[t], NULL, tf_tramp, &jb[t]); }
+  for (int t = 0; t < c->P; ++t) pthread_join(th[t], NULL);
+}
+#define TF_LO(c, t, N) ((N) * (uint64_t)(t) / (uint64_t)(c)->P)
+#define TF_HI(c, t, N) ((N) * (uint64_t)((t) + 1) / (uint64_t)(c)->P)
+static void tf_minmax(tf_ctx* c, int t) {
+  int64_t lo = INT64_MAX, hi = INT64_MIN;
+  for (uint64_t i = TF_LO(c, t, c->n); i < TF_HI(c, t, c->n); ++i) {
+    const int64_t a = c->src[i], b = c->dst[i];
+    if (a == b) c->bad = 1;
+    lo = a < lo ? a : lo; lo = b < lo ? b : lo;
+    hi = a > hi ? a : hi; hi = b > hi ? b : hi;
+  }
+  c->mn[t] = lo; c->mx[t] = hi;
+}
+static void tf_mark(tf_ctx* c, int t) {
+  for (uint64_t i = TF_LO(c, t, c->n); i < TF_HI(c, t, c->n); ++i) {
+    c->map[(uint64_t)c->src[i] - (uint64_t)c->kmin] = 1;
+    c->map[(uint64_t)c->dst[i] - (uint64_t)c->kmin] = 1;
+  }
+}
+static void tf_remap(tf_ctx* c, int t) {
+  for (uint64_t i = TF_LO(c, t, c->n); i < TF_HI(c, t, c->n); ++i) {
+    c->cs[i] = c->map[(uint64_t)c->src[i] - (uint64_t)c->kmin] - 1;
+    c->cd[i] = c->map[(uint64_t)c->dst[i] - (uint64_t)c->kmin] - 1;
+  }
+}
+static void tf_count_lo(tf_ctx* c, int t) {   /* records per smaller endpoint */
+  for (uint64_t i = TF_LO(c, t, c->n); i < TF_HI(c, t, c->n); ++i) {
+    const uint32_t a = c->cs[i] < c->cd[i] ? c->cs[i] : c->cd[i];
+    __atomic_fetch_add(&c->off[a + 1], 1, __ATOMIC_RELAXED);
+  }
+}
+static void tf_fill_lo(tf_ctx* c, int t) {
+  for (uint64_t i = TF_LO(c, t, c->n); i < TF_HI(c, t, c->n); ++i) {
+    const uint32_t a = c->cs[i] < c->cd[i] ? c->cs[i] : c->cd[i], b = c->cs[i] ^ c->cd[i] ^ a;
+    c->lst[__atomic_fetch_add(&c->cur[a], 1, __ATOMIC_RELAXED)] = b;
+  }
+}
+static int tf_cmp_u32(const void* x, const void* y) {
+  const uint32_t a = *(const uint32_t*)x, b = *(const uint32_t*)y;
+  return a < b ? -1 : a > b;
+}
+static void tf_sort_unique(tf_ctx* c, int t) {   /* each vertex's partners above it: sorted, distinct */
+  for (;;) {
+    const uint64_t x0 = __sync_fetch_and_add(&c->next, 1024);
+    if (x0 >= c->V) break;
+    const uint64_t x1 = x0 + 1024 < c->V ? x0 + 1024 : c->V;
+    for (uint64_t a = x0; a < x1; ++a) {
+      uint32_t* L = c->lst + c->off[a];
+      const uint64_t k = c->off[a + 1] - c->off[a];
+      if (k > 1) qsort(L, k, 4, tf_cmp_u32);
+      uint64_t u = 0;
+      for (uint64_t i = 0; i < k; ++i)
+        if (i == 0 || L[i] != L[i - 1]) L[u++] = L[i];
+      c->ucnt[a] = (uint32_t)u;
+    }
+  }
+}
+static void tf_degrees(tf_ctx* c, int t) {
+  for (uint64_t a = TF_LO(c, t, c->V); a < TF_HI(c, t, c->V); ++a) {
+    const uint32_t* L = c->lst + c->off[a];
+    __atomic_fetch_add(&c->deg[a], c->ucnt[a], __ATOMIC_RELAXED);
+    for (uint32_t i = 0; i < c->ucnt[a]; ++i) __atomic_fetch_add(&c->deg[L[i]], 1, __ATOMIC_RELAXED);
+  }
+}
+#define TF_FWD(c, a, b) ((c)->deg[a] < (c)->deg[b] || ((c)->deg[a] == (c)->deg[b] && (a) < (b)))
+static void tf_count_out(tf_ctx* c, int t) {
+  for (uint64_t a = TF_LO(c, t, c->V); a < TF_HI(c, t, c->V); ++a) {
+    const uint32_t* L = c->lst + c->off[a];
+    for (uint32_t i = 0; i < c->ucnt[a]; ++i) {
+      const uint32_t b = L[i], x = TF_FWD(c, (uint32_t)a, b) ? (uint32_t)a : b;
+      __atomic_fetch_add(&c->uoff[x + 1], 1, __ATOMIC_RELAXED);
+    }
+  }
+}
+static void tf_fill_out(tf_ctx* c, int t) {
+  for (uint64_t a = TF_LO(c, t, c->V); a < TF_HI(c, t, c->V); ++a) {
+    const uint32_t* L = c->lst + c->off[a];
+    for (uint32_t i = 0; i < c->ucnt[a]; ++i) {
+      const uint32_t b = L[i];
+      const int f = TF_FWD(c, (uint32_t)a, b);
+      const uint32_t x = f ? (uint32_t)a : b, y = f ? b : (uint32_t)a;
+      c->nbr[__atomic_fetch_add(&c->cur[x], 1, __ATOMIC_RELAXED)] = y;
+    }
+  }
+}
+static void tf_sort_out(tf_ctx* c, int t) {
+  for (;;) {
+    const uint64_t x0 = __sync_fetch_and_add(&c->next, 1024);
+    if (x0 >= c->V) break;
+    const uint64_t x1 = x0 + 1024 < c->V ? x0 + 1024 : c->V;
+    for (uint64_t x = x0; x < x1; ++x) {
+      const uint64_t k = c->uoff[x + 1] - c->uoff[x];
+      if (k > 1) qsort(c->nbr + c->uoff[x], k, 4, tf_cmp_u32);
+    }
+  }
+}
+/* T = sum over oriented x -> y of |N+(x) ∩ N+(y)|: N+(x) stamped into a per-thread array, each w of
+ * N+(y) tested against the stamp (the same set sizes the merge intersection reads, no merge) */
+static void tf_intersect(tf_ctx* c, int t) {
+  uint32_t* stamp = (uint32_t*)malloc(c->V * sizeof(uint32_t));
+  memset(stamp, 0xFF, c->V * sizeof(uint32_t));
   uint64_t T = 0;
   for (;;) {
-    const uint64_t x0 = __sync_fetch_and_add(A->next, 256);
-    if (x0 >= A->V) break;
-    const uint64_t x1 = x0 + 256 < A->V ? x0 + 256 : A->V;
-    for (uint64_t x = x0; x < x1; ++x)
-      for (uint64_t p = A->off[x]; p < A->off[x + 1]; ++p) {
-        const uint32_t y = A->nbr[p];
-        uint64_t i = A->off[x], j = A->off[y];
-        while (i < A->off[x + 1] && j < A->off[y + 1]) {
-          if (A->nbr[i] < A->nbr[j]) ++i;
-          else if (A->nbr[i] > A->nbr[j]) ++j;
-          else { ++T; ++i; ++j; }
-        }
+    const uint64_t x0 = __sync_fetch_and_add(&c->next, 256);
+    if (x0 >= c->V) break;
+    const uint64_t x1 = x0 + 256 < c->V ? x0 + 256 : c->V;
+    for (uint64_t x = x0; x < x1; ++x) {
+      const uint64_t b = c->uoff[x], e = c->uoff[x + 1];
+      if (e - b < 2) continue;
+      for (uint64_t p = b; p < e; ++p) stamp[c->nbr[p]] = (uint32_t)x;
+      for (uint64_t p = b; p < e; ++p) {
+        const uint32_t y = c->nbr[p];
+        for (uint64_t q = c->uoff[y]; q < c->uoff[y + 1]; ++q) T += stamp[c->nbr[q]] == (uint32_t)x;
       }
+    }
   }
-  A->T = T;
-  return NULL;
+  c->T[t] = T;
+  free(stamp);
 }
 
 GSO_API int gso_triangles_fwd_mt(const int64_t* src, const int64_t* dst, uint64_t n, int threads, uint64_t* T_out) {
-  const int P = threads < 1 ? 1 : threads;
   *T_out = 0;
   if (n == 0) return 0;
-  for (uint64_t i = 0; i < n; ++i)
-    if (src[i] == dst[i]) return -1;
-  /* 1. compact IDs: sort + unique of all endpoints (sign-flipped so the order is signed) */
-  uint64_t* e = (uint64_t*)malloc(2 * n * sizeof(uint64_t));
-  uint64_t* tmp = (uint64_t*)malloc(2 * n * sizeof(uint64_t));
-  for (uint64_t i = 0; i < n; ++i) {
-    e[2 * i] = (uint64_t)src[i] ^ (1ull << 63);
-    e[2 * i + 1] = (uint64_t)dst[i] ^ (1ull << 63);
-  }
-  radix_u64(e, tmp, 2 * n, 64);
-  uint64_t V = 0;
-  for (uint64_t i = 0; i < 2 * n; ++i)
-    if (i == 0 || e[i] != e[i - 1]) e[V++] = e[i];
-  int64_t* ids = (int64_t*)malloc(V * sizeof(int64_t));
-  for (uint64_t i = 0; i < V; ++i) ids[i] = (int64_t)(e[i] ^ (1ull << 63));
-  uint32_t* cs = (uint32_t*)malloc(n * sizeof(uint32_t));
-  uint32_t* cd = (uint32_t*)malloc(n * sizeof(uint32_t));
-  pthread_t* th = (pthread_t*)malloc((size_t)P * sizeof(pthread_t));
-  tri_arg* args = (tri_arg*)calloc((size_t)P, sizeof(tri_arg));
-  for (int side = 0; side < 2; ++side) {
-    for (int t = 0; t < P; ++t) {
-      args[t] = (tri_arg){ids, V, side ? dst : src, side ? cd : cs, n * (uint64_t)t / P, n * (uint64_t)(t + 1) / P,
-                          NULL, NULL, NULL, 0};
-      pthread_create(&th[t], NULL, tri_map_worker, &args[t]);
+  tf_ctx* c = (tf_ctx*)calloc(1, sizeof(tf_ctx));
+  c->src = src; c->dst = dst; c->n = n;
+  c->P = threads < 1 ? 1 : threads > 64 ? 64 : threads;
+  tf_par(c, tf_minmax);
+  if (c->bad) { free(c); return -1; }
+  int64_t kmin = INT64_MAX, kmax = INT64_MIN;
+  for (int t = 0; t < c->P; ++t) { kmin = c->mn[t] < kmin ? c->mn[t] : kmin; kmax = c->mx[t] > kmax ? c->mx[t] : kmax; }
+  c->cs = (uint32_t*)malloc(n * sizeof(uint32_t));
+  c->cd = (uint32_t*)malloc(n * sizeof(uint32_t));
+  /* 1. compact IDs, ascending in id order: a direct map when the id span is small, else sort + unique */
+  const uint64_t span = (uint64_t)kmax - (uint64_t)kmin + 1;
+  if (span != 0 && span < (1ull << 32) && span <= 8 * n + (1u << 20)) {
+    c->kmin = kmin; c->range = span;
+    c->map = (uint32_t*)calloc(span, sizeof(uint32_t));
+    tf_par(c, tf_mark);
+    uint32_t V = 0;
+    for (uint64_t i = 0; i < span; ++i) if (c->map[i]) c->map[i] = ++V;
+    c->V = V;
+    tf_par(c, tf_remap);
+    free(c->map);
+  } else {
+    uint64_t* e = (uint64_t*)malloc(2 * n * sizeof(uint64_t));
+    uint64_t* tmp = (uint64_t*)malloc(2 * n * sizeof(uint64_t));
+    for (uint64_t i = 0; i < n; ++i) {
+      e[2 * i] = (uint64_t)src[i] ^ (1ull << 63);
+      e[2 * i + 1] = (uint64_t)dst[i] ^ (1ull << 63);
     }
-    for (int t = 0; t < P; ++t) pthread_join(th[t], NULL);
+    radix_u64(e, tmp, 2 * n, 64);
+    uint64_t V = 0;
+    for (uint64_t i = 0; i < 2 * n; ++i)
+      if (i == 0 || e[i] != e[i - 1]) e[V++] = e[i];
+    int64_t* ids = (int64_t*)malloc(V * sizeof(int64_t));
+    for (uint64_t i = 0; i < V; ++i) ids[i] = (int64_t)(e[i] ^ (1ull << 63));
+    free(e); free(tmp);
+    pthread_t* th = (pthread_t*)malloc((size_t)c->P * sizeof(pthread_t));
+    tri_arg* args = (tri_arg*)calloc((size_t)c->P, sizeof(tri_arg));
+    for (int side = 0; side < 2; ++side) {
+      for (int t = 0; t < c->P; ++t) {
+        args[t] = (tri_arg){ids, V, side ? dst : src, side ? c->cd : c->cs, n * (uint64_t)t / c->P,
+                            n * (uint64_t)(t + 1) / c->P, NULL, NULL, NULL, 0};
+        pthread_create(&th[t], NULL, tri_map_worker, &args[t]);
+      }
+      for (int t = 0; t < c->P; ++t) pthread_join(th[t], NULL);
+    }
+    free(th); free(args); free(ids);
+    c->V = V;
   }
-  /* 2. distinct undirected edges (min << 32 | max), degrees */
-  for (uint64_t i = 0; i < n; ++i) {
-    const uint64_t a = cs[i] < cd[i] ? cs[i] : cd[i], b = cs[i] < cd[i] ? cd[i] : cs[i];
-    e[i] = (a << 32) | b;
-  }
-  radix_u64(e, tmp, n, 64);
-  uint64_t m = 0;
-  for (uint64_t i = 0; i < n; ++i)
-    if (i == 0 || e[i] != e[i - 1]) e[m++] = e[i];
-  uint32_t* deg = (uint32_t*)calloc(V, sizeof(uint32_t));
-  for (uint64_t i = 0; i < m; ++i) { deg[e[i] >> 32]++; deg[(uint32_t)e[i]]++; }
-  /* 3. orientation x -> y iff (deg x, x) < (deg y, y); out-lists come out sorted (see below) */
-  uint64_t* off = (uint64_t*)calloc(V + 1, sizeof(uint64_t));
-#define TRI_FWD(a, b) (deg[a] < deg[b] || (deg[a] == deg[b] && (a) < (b)))
-  for (uint64_t i = 0; i < m; ++i) {
-    const uint32_t a = (uint32_t)(e[i] >> 32), b = (uint32_t)e[i];
-    off[(TRI_FWD(a, b) ? a : b) + 1]++;
-  }
-  for (uint64_t x = 0; x < V; ++x) off[x + 1] += off[x];
-  uint64_t* fill = (uint64_t*)malloc((V + 1) * sizeof(uint64_t));
-  memcpy(fill, off, (V + 1) * sizeof(uint64_t));
-  uint32_t* nbr = (uint32_t*)malloc((m + 1) * sizeof(uint32_t));
-  /* edges ascend by (a, b), a < b: first the partners below x (x = b, a ascending), then the
-   * partners above x (x = a, b ascending) -> every out-list ascends */
-  for (uint64_t i = 0; i < m; ++i) {
-    const uint32_t a = (uint32_t)(e[i] >> 32), b = (uint32_t)e[i];
-    if (!TRI_FWD(a, b)) nbr[fill[b]++] = a;
-  }
-  for (uint64_t i = 0; i < m; ++i) {
-    const uint32_t a = (uint32_t)(e[i] >> 32), b = (uint32_t)e[i];
-    if (TRI_FWD(a, b)) nbr[fill[a]++] = b;
-  }
-#undef TRI_FWD
-  /* 4. T = sum over oriented x -> y of |N+(x) ∩ N+(y)| */
-  volatile uint64_t next = 0;
-  for (int t = 0; t < P; ++t) {
-    args[t] = (tri_arg){NULL, V, NULL, NULL, 0, 0, off, nbr, &next, 0};
-    pthread_create(&th[t], NULL, tri_count_worker, &args[t]);
-  }
+  const uint64_t V = c->V;
+  /* 2. distinct undirected edges: records grouped by the smaller endpoint, each group sorted + unique */
+  c->off = (uint64_t*)calloc(V + 1, sizeof(uint64_t));
+  c->cur = (uint64_t*)malloc((V + 1) * sizeof(uint64_t));
+  c->lst = (uint32_t*)malloc((n + 1) * sizeof(uint32_t));
+  c->ucnt = (uint32_t*)malloc((V + 1) * sizeof(uint32_t));
+  tf_par(c, tf_count_lo);
+  for (uint64_t x = 0; x < V; ++x) c->off[x + 1] += c->off[x];
+  memcpy(c->cur, c->off, (V + 1) * sizeof(uint64_t));
+  tf_par(c, tf_fill_lo);
+  free(c->cs); free(c->cd);
+  c->next = 0;
+  tf_par(c, tf_sort_unique);
+  /* 3. degrees over distinct edges; orientation x -> y iff (deg x, x) < (deg y, y); sorted out-lists */
+  c->deg = (uint32_t*)calloc(V + 1, sizeof(uint32_t));
+  tf_par(c, tf_degrees);
+  c->uoff = (uint64_t*)calloc(V + 1, sizeof(uint64_t));
+  tf_par(c, tf_count_out);
+  for (uint64_t x = 0; x < V; ++x) c->uoff[x + 1] += c->uoff[x];
+  memcpy(c->cur, c->uoff, (V + 1) * sizeof(uint64_t));
+  c->nbr = (uint32_t*)malloc((c->uoff[V] + 1) * sizeof(uint32_t));
+  tf_par(c, tf_fill_out);
+  c->next = 0;
+  tf_par(c, tf_sort_out);
+  /* 4. the count */
+  c->next = 0;
+  tf_par(c, tf_intersect);
   uint64_t T = 0;
-  for (int t = 0; t < P; ++t) { pthread_join(th[t], NULL); T += args[t].T; }
+  for (int t = 0; t < c->P; ++t) T += c->T[t];
   *T_out = T;
-  free(e); free(tmp); free(ids); free(cs); free(cd); free(th); free(args); free(deg); free(off); free(fill); free(nbr);
+  free(c->off); free(c->cur); free(c->lst); free(c->ucnt); free(c->deg); free(c->uoff); free(c->nbr); free(c);
   return 0;
 }
 

@@ -257,6 +257,18 @@ def _worker(rank, world, port, q):
     res["tri"] = D.triangles_window(te, torch.from_numpy(ts), torch.from_numpy(td))
     ls, ld = orc.gen_rmat(6, 1500, 0x5EED06, first_edge=rank * 1500)
     res["tri_loops"] = D.triangles_window(te, torch.from_numpy(ls), torch.from_numpy(ld))
+    # a rank with an empty slice (rank 1 holds nothing) and a window with fewer records than ranks
+    es, ed = orc.gen_rmat(9, 5000, 0x5EED08, no_self_loops=True)
+    if rank:
+        es, ed = es[:0], ed[:0]
+    res["tri_empty_rank"] = D.triangles_window(te, torch.from_numpy(es), torch.from_numpy(ed))
+    one_s, one_d = (np.array([3], np.int64), np.array([7], np.int64)) if rank == 0 else \
+        (np.zeros(0, np.int64), np.zeros(0, np.int64))
+    res["tri_one_record"] = D.triangles_window(te, torch.from_numpy(one_s), torch.from_numpy(one_d))
+    ev = orc.gen_values(len(es), 9, orc.DT_I64)
+    ek, er = D.reduce_window(oracle_halves(orc)[0], oracle_halves(orc)[1], torch.from_numpy(es),
+                             torch.from_numpy(ed), torch.from_numpy(ev), 2, 0)
+    res["reduce_empty_rank"] = (ek.numpy(), er.numpy())
     # GenerateCandidateEdges over the split window: edges routed to their endpoints' owners (the real
     # all-to-all), each rank's owned vertices from the oracle
     cs, cd = orc.gen_rmat(8, 3000, 0x5EED07, first_edge=rank * 3000)
@@ -290,10 +302,20 @@ def test_reduce_window_two_ranks(oracle):
     cs, cd = oracle.gen_rmat(8, 6000, 0x5EED07)
     assert (cs == cd).any()                       # self-loops (two records for their vertex) included
     check_candidates_split([out[r]["cand"] for r in range(world)], oracle.window_candidates(cs, cd)[:3])
+    es, ed = oracle.gen_rmat(9, 5000, 0x5EED08, no_self_loops=True)
+    ew, eex, _ = oracle.window_triangles_fwd(es, ed)
+    ev = oracle.gen_values(len(es), 9, oracle.DT_I64)
+    rk = np.concatenate([out[r]["reduce_empty_rank"][0] for r in range(world)])
+    rv = np.concatenate([out[r]["reduce_empty_rank"][1] for r in range(world)])
+    o = np.argsort(rk)
+    wk, wv = oracle.window_reduce(es, ed, ev, 2, 0)
+    assert np.array_equal(rk[o], wk) and np.array_equal(rv[o], wv)
     for r in range(world):
         assert np.array_equal(out[r]["gathered"][0], s) and np.array_equal(out[r]["gathered"][1], d)
         assert out[r]["tri"] == (ex, w, True)
         assert out[r]["tri_loops"] == (lex, lw, True)
+        assert out[r]["tri_empty_rank"] == (eex, ew, True)
+        assert out[r]["tri_one_record"] == (0, 0, True)
 
 
 def test_owner_split_is_balanced():

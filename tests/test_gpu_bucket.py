@@ -345,3 +345,26 @@ def test_speculative_degree_max(pkg, oracle, direction):
                 assert np.array_equal(g.cpu().numpy(), x), w
             spec.append(e.stage_times().speculative)
         assert spec[1] == spec[2] == spec[3] == 1, spec
+
+
+@pytest.mark.parametrize("spec", [False, True])
+def test_packed_integer_sum_wraps_to_zero(pkg, oracle, spec):
+    """Integer SUM on packed records: a vertex whose narrow values total exactly 2^32 (2^17 records of
+    32768) has a 32-bit accumulator back at its identity 0; the reference still emits it, with the
+    wrapped value 0.  Presence is marked per record for 4-byte sums, so the vertex is not dropped
+    (both the histogram and the speculative partition)."""
+    rng = np.random.default_rng(99)
+    n_hub, n_rest = 1 << 17, 70_000
+    with pkg.Engine(0, no_spec=not spec) as e:
+        for w in range(3):
+            s = np.concatenate([np.full(n_hub, 4242, np.int64), rng.integers(5000, 1 << 20, n_rest)])
+            d = rng.integers(0, 1 << 20, n_hub + n_rest).astype(np.int64)
+            v = np.concatenate([np.full(n_hub, 32768), rng.integers(0, 0xFFFF, n_rest)]).astype(np.int32)
+            perm = rng.permutation(len(s))
+            s, d, v = s[perm], d[perm], v[perm]
+            rk, rv = oracle.window_reduce(s, d, v, 1, 0)   # OUT: key = src
+            assert rv[np.searchsorted(rk, 4242)] == 0
+            gk, gv = e.reduce(*_dev(s, d, v), 1, 0)
+            t = e.stage_times()
+            assert t.path == 2 and t.packed
+            _check(gk, gv, rk, rv, np.int32, 0)

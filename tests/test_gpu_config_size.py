@@ -6,12 +6,22 @@ way keyBy spreads it over subtasks; gso_triangles_fwd_mt — an independent forw
       1e-5 relative (north star), both on two distinct windows of the stream
   C3  skewed R-MAT scale 24 (.65/.15/.15/.05, no permutation) and the Zipf(1.1) source stream, E = 2^28:
       foldNeighbors(degree, max neighbour) bit-exact
-  C4  WindowTriangles on self-loop-free R-MAT windows at scales 20 and 22: the exact count equals the
-      forward algorithm's (and the reference's Integer is its low 32 bits)
+  C4  WindowTriangles on self-loop-free R-MAT windows at scales 20, 22 and 24 (2^28 edges; scale 26,
+      2^30 edges, with GS_TEST_S26=1): the exact count equals the forward algorithm's (and the
+      reference's Integer is its low 32 bits)
+  C5  one 1e8-edge R-MAT scale-23 window: applyOnNeighbors' grouping (gs_window_csr, ALL: keys, offsets,
+      neighbours in arrival order) equals oracle.window_csr, and the GenerateCandidateEdges sizing call
+      (1.6e11 records) equals oracle.candidate_count
   C2 / C3 on one fresh ctx, two windows: the second through the speculative partition
 
 The windows are generated on the device (gs_generate_*, bit-identical to the oracle's generators:
 test_gpu_parity.test_generators_match_oracle, and re-checked here on a sample of each window)."""
+import contextlib
+import os
+import threading
+import time
+from pathlib import Path
+
 import numpy as np
 import pytest
 import torch
@@ -111,15 +121,90 @@ def test_speculative_partition_full_windows(pkg, oracle, kind):
             assert spec == window, (kind, window, spec)   # 0: histogram path, 1: speculative
 
 
-@pytest.mark.parametrize("scale", [20, 22])
-def test_c4_shape_triangles_vs_forward_algorithm(engine, oracle, scale):
+@contextlib.contextmanager
+def _keepalive(tag):
+    """A long oracle call prints nothing: touch a file under gpurun_out/ every 20 s meanwhile (the GPU
+    box's hang detector watches stdout / stderr / gpurun_out)."""
+    out = Path(__file__).resolve().parent.parent / "gpurun_out"
+    stop = threading.Event()
+
+    def beat():
+        out.mkdir(exist_ok=True)
+        t0 = time.time()
+        while not stop.wait(20):
+            (out / "keepalive.txt").write_text(f"{tag}: oracle running {time.time() - t0:.0f} s\n")
+
+    th = threading.Thread(target=beat, daemon=True)
+    th.start()
+    try:
+        yield
+    finally:
+        stop.set()
+        th.join()
+
+
+def _triangles_vs_forward(engine, oracle, scale):
     E, seed = 16 << scale, 0x5EED04
     src, dst = engine.generate_rmat(scale, E, seed, no_self_loops=True)
     exact, wrapped, has = engine.triangles(src, dst)
-    want = oracle.triangles_fwd_mt(src.cpu().numpy(), dst.cpu().numpy())
+    _sample_matches_oracle(oracle, src, dst, lambda k, f: oracle.gen_rmat(scale, k, seed, no_self_loops=True,
+                                                                          first_edge=f), 0)
+    s_h, d_h = src.cpu().numpy(), dst.cpu().numpy()
+    del src, dst
+    torch.cuda.empty_cache()
+    with _keepalive(f"triangles s{scale}"):
+        want = oracle.triangles_fwd_mt(s_h, d_h)
     assert exact == want, (exact, want)
     w = want & 0xFFFFFFFF
     assert wrapped == (w - (1 << 32) if w >= 1 << 31 else w) and has
+
+
+@pytest.mark.parametrize("scale", [20, 22, 24])
+@pytest.mark.timeout(300)
+def test_c4_shape_triangles_vs_forward_algorithm(engine, oracle, scale):
+    _triangles_vs_forward(engine, oracle, scale)
+
+
+@pytest.mark.skipif(os.environ.get("GS_TEST_S26") != "1", reason="C4 window (2^30 edges): GS_TEST_S26=1")
+@pytest.mark.timeout(900)
+def test_c4_window_s26_triangles_vs_forward_algorithm(engine, oracle):
+    """The C4 window itself: R-MAT scale 26, 2^30 edges (the oracle needs ~40 GB of host memory)."""
+    _triangles_vs_forward(engine, oracle, 26)
+
+
+@pytest.fixture(scope="module")
+def c5_window(engine, oracle):
+    """One C5 window: 1e8 edges of the R-MAT scale-23 stream, on the device and host."""
+    scale, E, seed = 23, 100_000_000, 0x5EED05
+    src, dst = engine.generate_rmat(scale, E, seed)
+    _sample_matches_oracle(oracle, src, dst, lambda k, f: oracle.gen_rmat(scale, k, seed, first_edge=f), 0)
+    return src, dst, src.cpu().numpy(), dst.cpu().numpy()
+
+
+@pytest.mark.timeout(300)
+def test_c5_window_csr_vs_oracle(engine, oracle, c5_window):
+    """applyOnNeighbors over slice(ALL) (GraphWindowStream.java:130-175): every vertex's neighbours in
+    arrival order, duplicates kept -- the whole 2e8-record CSR bit-exact."""
+    src, dst, s_h, d_h = c5_window
+    gk, go, gn, _ = engine.csr(src, dst, None, 2)
+    with _keepalive("c5 csr"):
+        rk, ro, rn, _ = oracle.window_csr(s_h, d_h, None, 2)
+    assert np.array_equal(gk.cpu().numpy(), rk)
+    assert np.array_equal(go.cpu().numpy(), ro)
+    del gk, go
+    assert np.array_equal(gn.cpu().numpy(), rn)
+
+
+@pytest.mark.timeout(300)
+def test_c5_window_candidate_count_vs_oracle(engine, oracle, c5_window):
+    """GenerateCandidateEdges' record count for the whole window (WindowTriangles.java:91-114: the
+    neighbour records plus, per vertex, the HashSet-ordered pairs above it incl. self pairs)."""
+    src, dst, s_h, d_h = c5_window
+    got = engine.candidate_count(src, dst)
+    with _keepalive("c5 candidates"):
+        want = oracle.candidate_count(s_h, d_h)
+    assert got == want, (got, want)
+    assert want > 10 ** 11
 
 
 def test_zipf_generator_matches_oracle(engine, oracle):

@@ -149,6 +149,42 @@ def test_rccl_world_one_through_the_abi(pkg, oracle):
         e.comm_destroy()
 
 
+@pytest.mark.parametrize("keys", ["narrow", "wide"])
+def test_rccl_exchange_forced_at_world_one(pkg, oracle, keys):
+    """gs_window_reduce_dist's exchange itself on a one-rank communicator (GS_FLAG_TEST_FORCE_EXCHANGE):
+    local partials -> owner partition -> one all-to-all of [rows, flags] -> one packed all-to-all of rows
+    (4-byte keys; 8-byte keys when a key lies outside [0, 2^32)) -> merge.  Every op, dtype and the degree
+    fold, against the oracle."""
+    n = 200_003
+    s, d = oracle.gen_rmat(15, n, 0x5EED09)
+    if keys == "wide":
+        s, d = s * 7919 - (3 << 40), d * 7919 - (3 << 40)
+    s, d = np.ascontiguousarray(s), np.ascontiguousarray(d)
+    with pkg.Engine(0, flags=pkg._lib.GS_FLAG_TEST_FORCE_EXCHANGE) as e:
+        e.comm_init(1, 0, pkg.Engine.comm_unique_id())
+        for dt in (oracle.DT_I64, oracle.DT_I32, oracle.DT_F64):
+            v = oracle.gen_values(n, 8 + dt, dt)
+            S, D, V = (torch.from_numpy(x).cuda() for x in (s, d, v))
+            for direction, op in ((1, 0), (2, 1), (0, 2), (2, 3)):
+                if dt == oracle.DT_F64 and op in (1, 2):
+                    continue
+                gk, gv = e.reduce_dist(S, D, V, direction, op)
+                wk, wv = oracle.window_reduce(s, d, v, direction, op)
+                assert np.array_equal(gk.cpu().numpy(), wk)
+                g = gv.cpu().numpy()
+                if dt == oracle.DT_F64 and op == 0:
+                    assert np.allclose(g, wv, rtol=1e-5, atol=0)
+                else:
+                    assert np.array_equal(g, wv), (dt, direction, op)
+        gk, gv = e.reduce_dist(S, D, V, 1, 3, init=10)
+        assert np.array_equal(gv.cpu().numpy(), oracle.window_fold(s, d, v, 1, 3, 10)[1])
+        for direction in (1, 2):
+            got = e.fold_degree_max_dist(S, D, direction, -5)
+            for g, w in zip(got, oracle.window_fold_degree_max(s, d, direction, -5)):
+                assert np.array_equal(g.cpu().numpy(), w)
+        e.comm_destroy()
+
+
 # ---- WindowTriangles over a split window (gs_tri_dist_*) -------------------------------------------
 TRI_CASES = (("rmat", 14, 120_000, True), ("loops", 8, 6_000, False), ("wide", 13, 60_000, True))
 

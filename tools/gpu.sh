@@ -1,0 +1,67 @@
+#!/bin/bash
+# The one GPU-box launcher (run from the repo root, under gpurun):  bash tools/gpu.sh MODE [TAG] [ARGS...]
+#
+#   tests   TAG [pytest args]   the -m gpu suite (default: all of tests/), log in gpurun_out/TAG/tests.txt
+#   bench   TAG [bench args]    one bench.py line -> gpurun_out/TAG/bench.json
+#   c2      TAG                 the C2 headline: bench line (+ cpu_baseline), rocprofv3 kernel-trace stats of
+#                               the same command, FETCH_SIZE / WRITE_SIZE passes -> pmc_traffic.json
+#   sq      TAG [bench args]    SQ counter passes (LDS conflicts, waits, instruction mix) over a short bench
+#   tri     TAG SCALE           triangles: bench line, kernel-trace stats, FETCH / TCC hit / SQ passes
+#   evidence TAG                every secondary bench line DESIGN.md quotes
+#
+# Every GPU step has its own time limit and the chain stops at the first failure (set -e): after a
+# fault, an abort or a timeout nothing more runs on the GPU in that call.
+set -e
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+MODE=$1; TAG=${2:-run}; shift 2 || true
+O=gpurun_out/$TAG
+mkdir -p "$O"
+PYTEST="python -u -m pytest -x -v --timeout 120 --timeout-method thread"
+bench() { local name=$1; shift; timeout -k 10 300 python3 bench.py "$@" > "$O/$name.json" 2> "$O/$name.err"; echo "$name done"; }
+trace() { local name=$1; shift; timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$O/$name" -o run --output-format csv \
+            -- python3 bench.py "$@" --no-cpu-baseline > "$O/$name.log" 2>&1; echo "$name done"; }
+pmc() { local name=$1 counters=$2; shift 2; timeout -s KILL 150 rocprofv3 --pmc $counters -d "$O/$name" -o run \
+          --output-format csv -- python3 bench.py "$@" --no-cpu-baseline > "$O/$name.log" 2>&1; echo "$name done"; }
+
+case $MODE in
+  tests)
+    [ $# -gt 0 ] || set -- tests/
+    timeout -k 10 1000 $PYTEST -m gpu "$@" > "$O/tests.txt" 2>&1 ;;
+  bench)
+    bench bench "$@" ;;
+  c2)
+    bench bench_c2_i64
+    trace trace_c2
+    pmc pmc/fetch FETCH_SIZE --steps 3 --warmup 2
+    pmc pmc/write WRITE_SIZE --steps 3 --warmup 2
+    python3 tools/pmc_traffic.py "$O/pmc" -o "$O/pmc_traffic.json" ;;
+  sq)
+    pmc sq1 "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_LDS_BANK_CONFLICT SQ_WAVE_CYCLES" --steps 3 --warmup 2 "$@"
+    pmc sq2 "SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_WAIT_INST_LDS SQ_ACTIVE_INST_VMEM SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VALU SQ_BUSY_CYCLES SQ_WAVES" --steps 3 --warmup 2 "$@" ;;
+  tri)
+    S=${1:-24}; shift || true
+    A="--workload triangles --scale $S --steps 3 --warmup 1"
+    bench bench_tri_s$S $A
+    trace trace_tri_s$S $A
+    pmc pmc_tri_s$S/fetch "FETCH_SIZE TCC_HIT_sum" $A --windows 1
+    pmc pmc_tri_s$S/sq "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_LDS_BANK_CONFLICT SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_BUSY_CYCLES" $A --windows 1 ;;
+  evidence)
+    bench bench_c2_f64 --dtype float64
+    bench bench_c3_rmat --workload fold
+    bench bench_c3_zipf --workload fold --stream zipf
+    bench bench_tri_s20 --workload triangles --scale 20
+    bench bench_tri_s22 --workload triangles --scale 22
+    bench bench_tri_s24 --workload triangles --scale 24
+    bench bench_tri_s26 --workload triangles --scale 26 --steps 3 --warmup 1
+    bench bench_cc_s24 --workload cc
+    bench bench_c1 --workload c1
+    bench bench_apply --workload apply
+    bench bench_candidates --workload candidates
+    bench bench_parse --workload parse
+    bench bench_e2e_direct --workload e2e --staging direct --no-cpu-baseline
+    bench bench_e2e_pinned --workload e2e --staging pinned --no-cpu-baseline ;;
+  *)
+    echo "usage: tools/gpu.sh tests|bench|c2|sq|tri|evidence TAG [args]" >&2; exit 2 ;;
+esac
+echo "$MODE done"
