@@ -78,3 +78,47 @@ def test_struct_layouts_match_header(pkg):
     subprocess.run(["gcc", "-I", str(ROOT / "include"), str(tmp / "sz.c"), "-o", str(tmp / "sz")], check=True)
     got = [int(x) for x in subprocess.run([str(tmp / "sz")], capture_output=True, text=True).stdout.split()]
     assert got == want
+
+
+# ---- the Java side (java/): JNI binding, shim and dispatch patch (source-only: no JDK in this image) ----
+JAVA = ROOT / "java"
+GELLYHIP_JAVA = JAVA / "src/main/java/org/apache/flink/graph/streaming/gpu/GellyHip.java"
+SHIM = JAVA / "src/main/c/gellyhip_jni.c"
+
+
+def test_java_constants_match_header():
+    """Every GS_* constant GellyHip.java defines has the header's value (enum ordinals, status codes,
+    stream kinds), as the C compiler sees the header."""
+    consts = dict(re.findall(r"public static final int (GS_\w+) = (-?\d+);", GELLYHIP_JAVA.read_text()))
+    assert len(consts) >= 30 and consts["GS_DIR_OUT"] == "1"
+    names = sorted(consts)
+    src = ("#include <stdio.h>\n#include \"gelly_hip.h\"\nint main(){" +
+           "".join(f'printf("%lld\\n", (long long)({n}));' for n in names) + "}")
+    tmp = ROOT / "gpurun_out"
+    tmp.mkdir(exist_ok=True)
+    (tmp / "jconst.c").write_text(src)
+    subprocess.run(["gcc", "-I", str(ROOT / "include"), str(tmp / "jconst.c"), "-o", str(tmp / "jconst")], check=True)
+    got = subprocess.run([str(tmp / "jconst")], capture_output=True, text=True, check=True).stdout.split()
+    assert dict(zip(names, got)) == {n: consts[n] for n in names}
+
+
+def test_jni_shim_covers_every_native_and_calls_only_declared_entry_points():
+    natives = set(re.findall(r"static native [\w\[\]]+ (\w+)\(", GELLYHIP_JAVA.read_text()))
+    shim = SHIM.read_text()
+    implemented = set(re.findall(r"JNI_FN\((\w+)\)", shim)) - {"name"}   # the macro definition itself
+    assert natives and natives == implemented, (natives ^ implemented)
+    called = set(re.findall(r"\b(gs_\w+)\(", shim))
+    assert called <= set(declared()), called - set(declared())
+
+
+def test_dispatch_patch_applies_to_the_reference():
+    """java/patches/*.patch (GraphWindowStream's package-private ctor + built-in dispatch, slice() passing
+    the pre-keyBy edges) applies cleanly to the reference tree (checked without writing to it)."""
+    import pytest
+    ref = Path("/root/reference")
+    if not (ref / "src").is_dir():
+        pytest.skip("reference tree not present (GPU box)")
+    for patch in sorted((JAVA / "patches").glob("*.patch")):
+        r = subprocess.run(["git", "apply", "--check", str(patch)], cwd=ref, capture_output=True,
+                           text=True)
+        assert r.returncode == 0, r.stderr
