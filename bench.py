@@ -45,7 +45,10 @@ def parse():
     p.add_argument("--windows", type=int, default=2, help="distinct windows of the stream the timed steps cycle through")
     p.add_argument("--stream", default="rmat", choices=["rmat", "zipf"],
                    help="fold (C3): skewed R-MAT (default) or the Zipf(1.1) source stream")
-    p.add_argument("--staging", default="direct", choices=["direct", "pinned"], help="e2e: window operator staging")
+    p.add_argument("--staging", default="direct", choices=["direct", "pinned", "buffered"],
+                   help="e2e: host columns in pageable memory, appended with direct staging (direct); in caller-"
+                        "pinned memory (gs_alloc_pinned, as a Java operator's direct buffers), DMA'd straight to HBM "
+                        "(pinned); or copied into the operator's own pinned window buffers, H2D at firing (buffered)")
     p.add_argument("--e2e-kind", default="reduce", choices=["reduce", "triangles"],
                    help="e2e: reduceOnEdges(SUM) on C2 windows, or WindowTriangles on C5-size windows "
                         "(--windows-edges edges of an R-MAT --scale stream per 1000 ms window)")
@@ -202,6 +205,26 @@ def pmc_table():
         return {}
 
 
+def host_cpu():
+    """The CPU the baseline ran on: model name, nproc (every hardware thread the OS reports) and the
+    threads the baseline used.  On the GPU box the pool allots 16 CPUs per GPU (its rules cap worker
+    pools there), so the baseline runs min(16, nproc) threads; nproc is recorded beside it."""
+    model = "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    nproc = os.cpu_count() or 1
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except AttributeError:
+        affinity = nproc
+    return {"cpu_model": model, "nproc": nproc, "affinity_cpus": affinity}
+
+
 def cpu_baseline(wins, workload, threads, reps=5):
     """BASELINE.md CPU baseline: the oracle's keyBy + per-subtask arrival-order hash-map fold
     (gso_baseline_reduce; Flink's keyBy at local-env parallelism = threads) over WHOLE windows of the
@@ -265,23 +288,27 @@ def cpu_baseline_cc(src, dst, sample_log2=23):
                       f"(oracle/gs_oracle.c gso_components, one thread), median of 3: {dt:.2f} s, {len(v)} vertices"}
 
 
-def cpu_baseline_triangles(src, dst, threads, sample_log2=24):
+def cpu_baseline_triangles(wins, threads, sample_log2=28, reps=5):
     """BASELINE.md C4 CPU baseline: the forward algorithm (the reference's O(sum d^2) candidate rule is
-    infeasible at this scale) over `threads` threads (oracle gso_triangles_fwd_mt) on the first
-    2^sample_log2 edges of the window, 1 warm-up + median of 3."""
+    infeasible at this scale) over `threads` threads (oracle gso_triangles_fwd_mt) on whole windows up to
+    2^28 edges (R-MAT scale 24; larger windows: their first 2^28 edges), cycling the bench's windows:
+    1 warm-up on a 1/16 sample, then the median of `reps`."""
     orc = ge.load_oracle()
-    S = min(1 << sample_log2, src.numel())
-    s, d = src[:S].cpu().numpy(), dst[:S].cpu().numpy()
-    orc.triangles_fwd_mt(s[: S // 16], d[: S // 16], threads)
+    S = min(1 << sample_log2, wins[0][0].numel())
+    host = [(w[0][:S].cpu().numpy(), w[1][:S].cpu().numpy()) for w in wins]
+    orc.triangles_fwd_mt(host[0][0][: S // 16], host[0][1][: S // 16], threads)
     ts = []
-    for _ in range(3):
+    for r in range(reps):
+        s, d = host[r % len(host)]
         t = time.perf_counter()
         T = orc.triangles_fwd_mt(s, d, threads)
         ts.append(time.perf_counter() - t)
     dt = statistics.median(ts)
+    whole = S == wins[0][0].numel()
     return {"value": S / dt, "unit": "edges/s", "cores": threads, "kind": "port",
-            "sample": f"first 2^{sample_log2} edges of the window, forward-algorithm triangle count over {threads} "
-                      f"threads (oracle/gs_oracle.c gso_triangles_fwd_mt), median of 3: {dt:.2f} s, {T} triangles"}
+            "sample": (f"whole {S}-edge windows" if whole else f"first {S} edges of each window") +
+                      f" ({len(host)} distinct, cycled), forward-algorithm triangle count over {threads} threads "
+                      f"(oracle/gs_oracle.c gso_triangles_fwd_mt), median of {reps}: {dt:.2f} s, {T} triangles"}
 
 
 def window_stream_main(a):
@@ -471,11 +498,24 @@ def e2e_main(a):
             del v_
         del s_, d_
     torch.cuda.empty_cache()
+    pinned_bufs = []
+    if a.staging == "pinned":   # the caller's columns in pinned host memory (gs_alloc_pinned)
+        import ctypes
+        lib = L.load()
+
+        def pinned_like(x):
+            p = lib.gs_alloc_pinned(x.nbytes)
+            assert p, "gs_alloc_pinned failed"
+            pinned_bufs.append(p)
+            y = np.ctypeslib.as_array((ctypes.c_char * x.nbytes).from_address(p)).view(x.dtype)
+            y[:] = x
+            return y
+        host = [tuple(None if x is None else pinned_like(x) for x in h) for h in host]
     ts0 = (np.arange(E, dtype=np.int64) * 1000) // E
     total = a.warmup + a.steps
     tss = [ts0 + k * 1000 for k in range(total)]   # window k's event times (prepared before timing)
     lat, results = [], []
-    staging = L.GS_STAGE_DIRECT if a.staging == "direct" else L.GS_STAGE_PINNED
+    staging = L.GS_STAGE_PINNED if a.staging == "buffered" else L.GS_STAGE_DIRECT
     if tri:
         op = WindowOperator(eng, 1000, L.GS_STREAM_TRIANGLES, 2, 0, None, L.GS_WATERMARK_ASCENDING, max_window_edges=E,
                             staging=staging)
@@ -508,6 +548,8 @@ def e2e_main(a):
             v = host[(r.start // 1000) % ndist][2]
             assert int(r.columns[1].sum()) == int(v.sum()), "e2e window: sum of sums != sum of values"
     op.close()
+    for p in pinned_bufs:
+        L.load().gs_free_pinned(p)
     ms = elapsed / a.steps * 1e3
     h2d_bytes = (16 if tri else 24) * E
     print(json.dumps({
@@ -518,9 +560,12 @@ def e2e_main(a):
         "config": {"workload": (f"end-to-end C5 shape: host records of an R-MAT scale-{a.scale} stream, {E} edges per "
                                 f"1000 ms window -> gs_stream window operator ({a.staging} staging) -> WindowTriangles"
                                 if tri else
-                                f"end-to-end C2: host records -> gs_stream window operator ({a.staging} staging: "
-                                + ("pinned window buffers, H2D at firing" if a.staging == "pinned" else
-                                   "each append copied straight to HBM") + ", reduceOnEdges(SUM) OUT, D2H of results)"),
+                                f"end-to-end C2: host records -> gs_stream window operator ({a.staging}: "
+                                + {"buffered": "pageable columns copied into the operator's pinned window buffers, "
+                                               "H2D at firing",
+                                   "direct": "pageable columns, each append copied straight to HBM",
+                                   "pinned": "caller-pinned columns (gs_alloc_pinned), each append DMA'd straight to "
+                                             "HBM"}[a.staging] + ", reduceOnEdges(SUM) OUT, D2H of results)"),
                    "edges_per_window": E, "windows_timed": a.steps,
                    "latency_ms_p50": float(np.percentile(lat, 50)), "latency_ms_p99": float(np.percentile(lat, 99)),
                    "h2d_bytes_per_window": h2d_bytes, "h2d_GBps_effective": h2d_bytes / (ms * 1e-3) / 1e9,
@@ -735,12 +780,13 @@ def main():
         if a.workload in ("reduce", "fold"):
             cpu = cpu_baseline(wins, a.workload, threads)
         elif a.workload == "triangles":
-            cpu = cpu_baseline_triangles(wins[0][0], wins[0][1], threads)
+            cpu = cpu_baseline_triangles(wins, threads)
         elif a.workload == "cc":
             cpu = cpu_baseline_cc(wins[0][0], wins[0][1])
     value = E * world * a.steps / elapsed
     if cpu:
         cpu["gpu_over_cpu"] = round(value / cpu["value"], 1)
+        cpu.update(host_cpu())
 
     if rank == 0:
         t0s = times[0]

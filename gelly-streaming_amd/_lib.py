@@ -54,6 +54,7 @@ GS_FLAG_BK_ONESWEEP = 2   # bucket path: 1-2 LSD partition passes instead of the
 GS_FLAG_NO_PACK = 4       # bucket path: integer SUM/MIN/MAX keep 8-byte partitioned values (A/B)
 GS_FLAG_NO_SPEC = 16      # bucket path: no speculative partition (per-tile histograms first; A/B)
 GS_FLAG_TEST_TINY_TABLES = 8   # TEST ONLY: triangle hash sets of one bucket -> must fail with GS_EDEVICE
+GS_LATE_REFIRE, GS_LATE_DROP = 0, 1   # gs_stream_config.late_mode
 GS_FLAG_TEST_FORCE_EXCHANGE = 32   # TEST ONLY: *_dist on one rank still partitions, exchanges and merges
 
 
@@ -102,7 +103,8 @@ class GsPartialBatch(ctypes.Structure):
 
 class GsStreamConfig(ctypes.Structure):
     _fields_ = [("window_ms", i64), ("kind", i32), ("dir", i32), ("op", i32), ("val_dtype", i32),
-                ("watermark_mode", i32), ("staging", i32), ("init", P), ("init_max", i64), ("max_window_edges", u64)]
+                ("watermark_mode", i32), ("staging", i32), ("init", P), ("init_max", i64), ("max_window_edges", u64),
+                ("late_mode", i32), ("reserved", i32)]
 
 
 class GsWindowResult(ctypes.Structure):

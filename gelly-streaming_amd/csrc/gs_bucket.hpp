@@ -1100,10 +1100,23 @@ __host__ __device__ inline uint64_t sp_capacity(uint64_t r_now, uint32_t nb) {
 #ifndef GS_SPK_ITEMS
 #define GS_SPK_ITEMS 16
 #endif
+#ifndef GS_SPK_ABL_NOATOMIC
+#define GS_SPK_ABL_NOATOMIC 0
+#endif
+#ifndef GS_SPK_ABL_NOLOAD
+#define GS_SPK_ABL_NOLOAD 0
+#endif
+#ifndef GS_SPK_ABL_NOSTORE
+#define GS_SPK_ABL_NOSTORE 0
+#endif
 #ifndef GS_SPK_WAVES
 #define GS_SPK_WAVES (2 * GS_SPK_BLOCK / 256)   // waves per SIMD: two blocks per CU
 #endif
-constexpr int SPK_BLOCK = GS_SPK_BLOCK, SPK_ITEMS = GS_SPK_ITEMS;
+#ifndef GS_SPK_GROUPS
+#define GS_SPK_GROUPS 1
+#endif
+constexpr int SPK_BLOCK = GS_SPK_BLOCK, SPK_ITEMS = GS_SPK_ITEMS, SPK_GROUPS = GS_SPK_GROUPS;
+static_assert(SPK_ITEMS % SPK_GROUPS == 0, "load groups split the tile evenly");
 constexpr uint32_t SPK_TILE = (uint32_t)SPK_BLOCK * SPK_ITEMS;
 static_assert(BK_MAXB % SPK_BLOCK == 0 && SPK_TILE <= 65536 && SPK_ITEMS <= 32, "tile / bucket-table shape");
 template <int DIR>
@@ -1168,38 +1181,66 @@ void k_sp_scatter_pack(BaseSrc<V, DIR, PAY_VAL> es, uint64_t n, int S, uint32_t 
   const uint32_t* pre = cursor + SP_NSEG * BK_MAXB;
   cursor += xs * BK_MAXB;
   uint32_t kb[ITEMS], vr[ITEMS];   // vr: narrow value (or escape index) << 16 | rank in the tile's run
-  int64_t kk[ITEMS];
-  V vv[ITEMS];
-  // every load first, unconditional and clamped into the tile (k_dp_scatter)
+  uint32_t ovf = 0;
+  // SPK_GROUPS groups of IG records per lane: a group's loads are unconditional and clamped into the tile
+  // (k_dp_scatter); group g + 1's loads are issued before group g is ranked in LDS, so with two groups a
+  // tile of 24 records per lane fits the 128-VGPR budget and half its load latency hides behind ranking
+  constexpr int G = SPK_GROUPS, IG = ITEMS / G;
+  int64_t kk[IG];
+  V vv[IG];
+  auto load = [&](int g) {
 #pragma unroll
-  for (int u = 0; u < ITEMS; ++u) {
-    const uint32_t r = r0 + min((uint32_t)u * BLOCK + tid, nrec - 1);
-    uint32_t i = r;
-    bool rev = DIR == DIR_IN;
-    if constexpr (DIR == DIR_ALL) {
-      i = r >> 1;
-      rev = r & 1u;
+    for (int q = 0; q < IG; ++q) {
+      const int u = g * IG + q;
+      const uint32_t r = r0 + min((uint32_t)u * BLOCK + tid, nrec - 1);
+      uint32_t i = r;
+      bool rev = DIR == DIR_IN;
+      if constexpr (DIR == DIR_ALL) {
+        i = r >> 1;
+        rev = r & 1u;
+      }
+#if GS_SPK_ABL_NOLOAD   // timing-only ablation: synthetic keys in range, no column reads (wrong output)
+      kk[q] = (int64_t)((uint64_t)es.base + ((i * 2654435761u) % ((uint64_t)nbp << S)));
+      vv[q] = (V)(i & 0x3FFF);
+      (void)rev;
+#else
+      kk[q] = (rev ? es.dst : es.src)[i];
+      vv[q] = es.val[i];
+#endif
     }
-    kk[u] = (rev ? es.dst : es.src)[i];
-    vv[u] = es.val[i];
-  }
+  };
+  auto convert = [&](int g) {
+#pragma unroll
+    for (int q = 0; q < IG; ++q) {
+      const int u = g * IG + q;
+      const uint32_t j = (uint32_t)u * BLOCK + tid;
+      const uint64_t d = (uint64_t)kk[q] - (uint64_t)es.base;
+      const bool in = (d >> S) < nbp, live = j < nrec;
+      ovf += (live && !in) ? 1u : 0u;
+      const uint32_t nv = pk_narrow(vv[q]);
+      const bool e = nv == PK_ESC;
+      kb[u] = (live && in) ? ((uint32_t)(d >> S) << 16) | ((uint32_t)d & lmask) | (e ? ESC : 0u) : DUMMY;
+      vr[u] = (e ? j : nv) << 16;
+    }
+  };
+  auto rank = [&](int g) {
+#pragma unroll
+    for (int q = 0; q < IG; ++q) {
+      const int u = g * IG + q;
+      vr[u] |= atomicAdd(&s_tab[(kb[u] >> 16) & 0x7FFFu], 1u);
+    }
+  };
+  load(0);
   for (uint32_t i = tid; i < nbp; i += BLOCK) s_tab[i] = 0;
   if (tid == 0) s_tab[BK_MAXB] = 0;
-  uint32_t ovf = 0;
-#pragma unroll
-  for (int u = 0; u < ITEMS; ++u) {
-    const uint32_t j = (uint32_t)u * BLOCK + tid;
-    const uint64_t d = (uint64_t)kk[u] - (uint64_t)es.base;
-    const bool in = (d >> S) < nbp, live = j < nrec;
-    ovf += (live && !in) ? 1u : 0u;
-    const uint32_t nv = pk_narrow(vv[u]);
-    const bool e = nv == PK_ESC;
-    kb[u] = (live && in) ? ((uint32_t)(d >> S) << 16) | ((uint32_t)d & lmask) | (e ? ESC : 0u) : DUMMY;
-    vr[u] = (e ? j : nv) << 16;
-  }
+  convert(0);
   __syncthreads();
 #pragma unroll
-  for (int u = 0; u < ITEMS; ++u) vr[u] |= atomicAdd(&s_tab[(kb[u] >> 16) & 0x7FFFu], 1u);
+  for (int g = 0; g < G; ++g) {
+    if (g + 1 < G) load(g + 1);
+    rank(g);
+    if (g + 1 < G) convert(g + 1);
+  }
   __syncthreads();
   // this thread's buckets: BPT consecutive ones
   uint32_t cb[BPT], ob[BPT], sum = 0;
@@ -1211,7 +1252,19 @@ void k_sp_scatter_pack(BaseSrc<V, DIR, PAY_VAL> es, uint64_t n, int S, uint32_t 
   }
   // reserve the runs now; the returned offsets are needed only after the LDS scatter
 #pragma unroll
-  for (int k = 0; k < BPT; ++k) ob[k] = cb[k] ? atomicAdd(&cursor[(uint32_t)tid * BPT + k], cb[k]) : 0u;
+  for (int k = 0; k < BPT; ++k) {
+#if GS_SPK_ABL_NOATOMIC   // timing-only ablation: no reservation, runs spread over the segment (wrong output)
+    {
+      const uint32_t b = min((uint32_t)tid * BPT + k, nbp - 1);
+      const uint32_t s0 = sp_seg_start(bucket_start[b], bucket_start[b + 1], xs, pre);
+      const uint32_t e0 = sp_seg_start(bucket_start[b], bucket_start[b + 1], xs + 1, pre);
+      const uint32_t span = e0 - s0 > cb[k] ? e0 - s0 - cb[k] : 1u;
+      ob[k] = cb[k] ? s0 + (uint32_t)(((uint64_t)(blockIdx.x >> 3) * cb[k]) % span) : 0u;
+    }
+#else
+    ob[k] = cb[k] ? atomicAdd(&cursor[(uint32_t)tid * BPT + k], cb[k]) : 0u;
+#endif
+  }
   uint32_t total;
   uint32_t st = block_excl_scan<BLOCK>(sum, s_w, total);   // total: records in the predicted range
   uint32_t sb[BPT];
@@ -1238,7 +1291,7 @@ void k_sp_scatter_pack(BaseSrc<V, DIR, PAY_VAL> es, uint64_t n, int S, uint32_t 
     const uint32_t end = sp_seg_start(bucket_start[b], bucket_start[b + 1], xs + 1, pre);
     const bool drop = cb[k] && ob[k] + cb[k] > end;
     s_tab[(uint32_t)tid * BPT + k] = (drop ? trash : ob[k]) - sb[k];
-    ovf += drop ? 1u : 0u;
+    ovf += (drop && !GS_SPK_ABL_NOLOAD) ? 1u : 0u;   // (the ablation's synthetic keys overflow regions)
   }
   if (tid == 0) s_tab[BK_MAXB] = trash - total;
   __syncthreads();
@@ -1249,7 +1302,11 @@ void k_sp_scatter_pack(BaseSrc<V, DIR, PAY_VAL> es, uint64_t n, int S, uint32_t 
     const uint32_t j = (uint32_t)u * BLOCK + tid;
     const uint32_t kv = s_key[j];
     const bool e = kv & ESC;
+#if GS_SPK_ABL_NOSTORE   // timing-only ablation: no record stores (wrong output)
+    if (s_tab[(kv >> 16) & 0x7FFFu] + j == 0xFFFFFFFFu) rec[0] = (kv & 0xFFFFu) | ((uint32_t)s_v16[j] << 16);
+#else
     rec[s_tab[(kv >> 16) & 0x7FFFu] + j] = (kv & 0xFFFFu) | ((e ? PK_ESC : (uint32_t)s_v16[j]) << 16);
+#endif
     escm |= e ? 1u << u : 0u;
   }
   uint32_t esc = 0;
@@ -1258,6 +1315,166 @@ void k_sp_scatter_pack(BaseSrc<V, DIR, PAY_VAL> es, uint64_t n, int S, uint32_t 
     const uint32_t kv = s_key[j];
     const uint32_t r = r0 + s_v16[j];
     wide[s_tab[(kv >> 16) & 0x7FFFu] + j] = es.val[DIR == DIR_ALL ? r >> 1 : r];
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    esc += __shfl_xor(esc, o, WAVE);
+    ovf += __shfl_xor(ovf, o, WAVE);
+  }
+  if (lane == 0) {
+    if (esc) atomicAdd(n_esc, (unsigned long long)esc);
+    s_ovf[w] = ovf;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    uint32_t o2 = 0;
+    for (int i = 0; i < BLOCK / WAVE; ++i) o2 += s_ovf[i];
+    if (o2) atomicAdd(&mm[2], (unsigned long long)o2);
+  }
+}
+// Persistent, software-pipelined variant (GS_SPK_PP): one 1024-thread block per CU walks its XCD slot's
+// tiles; the next tile's columns are loaded while this tile ranks, scans, scatters through LDS and
+// stores, so the CU's memory pipe stays busy across the LDS phases (the one-tile-per-block kernel above
+// leaves it idle while a block is in them).  Small tiles (PP_ITEMS records per lane) keep the two tiles'
+// registers under the 128-VGPR budget of 16 waves.  The tile's cursor reservations are issued before the
+// prefetch, so waiting for them does not wait for the next tile's loads (vmcnt counts in order).
+#ifndef GS_SPK_PP
+#define GS_SPK_PP 0
+#endif
+#ifndef GS_PP_ITEMS
+#define GS_PP_ITEMS 8
+#endif
+constexpr int PP_BLOCK = 1024, PP_ITEMS = GS_PP_ITEMS;
+constexpr uint32_t PP_TILE = (uint32_t)PP_BLOCK * PP_ITEMS;
+template <int DIR>
+__host__ __device__ constexpr uint32_t pp_tile_edges() {
+  return DIR == DIR_ALL ? PP_TILE / 2 : PP_TILE;
+}
+
+template <typename V, int DIR>
+__global__ __launch_bounds__(PP_BLOCK) __attribute__((amdgpu_waves_per_eu(4, 4)))
+void k_sp_scatter_pack_pp(BaseSrc<V, DIR, PAY_VAL> es, uint64_t n, int S, uint32_t nbp,
+                          const uint32_t* __restrict__ bucket_start, uint32_t* __restrict__ cursor,
+                          uint32_t* __restrict__ rec, V* __restrict__ wide, uint32_t trash,
+                          unsigned long long* __restrict__ mm, unsigned long long* __restrict__ n_esc) {
+  constexpr int ITEMS = PP_ITEMS, BLOCK = PP_BLOCK;
+  constexpr uint32_t TILE = PP_TILE;
+  constexpr uint32_t ESC = 1u << 31, DUMMY = (uint32_t)BK_MAXB << 16;
+  __shared__ uint32_t s_key[TILE];
+  __shared__ uint16_t s_v16[TILE];
+  __shared__ uint32_t s_tab[BK_MAXB + 1];
+  __shared__ uint32_t s_w[BLOCK / WAVE];
+  __shared__ uint32_t s_ovf[BLOCK / WAVE];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  constexpr uint32_t TE = pp_tile_edges<DIR>();
+  const uint32_t nfull = (uint32_t)(n / TE);
+  const bool partial = (uint64_t)nfull * TE < n;
+  const uint32_t lmask = (1u << S) - 1;
+  // this block's tiles: slot xs = b & 7 owns full tiles [xs * per, (xs + 1) * per); its nbs blocks take
+  // them round robin (the tiles running at once on one XCD are adjacent); block 0 also takes the
+  // window's partial last tile, as its last one
+  const uint32_t xs = blockIdx.x & 7u, nbs = gridDim.x / 8, jb = blockIdx.x >> 3;
+  const uint32_t per = (nfull + 7) / 8, t_end = min(nfull, (xs + 1) * per);
+  uint32_t t = xs * per + jb;
+  const bool last_partial = blockIdx.x == 0 && partial;
+  if (t >= t_end && !last_partial) return;
+  if (t >= t_end) t = nfull;   // only the partial tile
+  const uint32_t* pre = cursor + SP_NSEG * BK_MAXB;
+  uint32_t* cur = cursor + (SP_NSEG == 1 ? 0u : xs) * BK_MAXB;
+  const uint32_t b0 = 2 * tid, b1 = 2 * tid + 1;
+  const uint32_t bl0 = min(b0, nbp - 1), bl1 = min(b1, nbp - 1);
+  const uint32_t end0 = sp_seg_start(bucket_start[bl0], bucket_start[bl0 + 1], SP_NSEG == 1 ? 1u : xs + 1, pre);
+  const uint32_t end1 = sp_seg_start(bucket_start[bl1], bucket_start[bl1 + 1], SP_NSEG == 1 ? 1u : xs + 1, pre);
+  auto nrec_of = [&](uint32_t tt) -> uint32_t {
+    return tt < nfull ? TILE : (uint32_t)((n - (uint64_t)nfull * TE) * (DIR == DIR_ALL ? 2 : 1));
+  };
+  auto next_of = [&](uint32_t tt) -> uint32_t {   // the tile after tt for this block (~0u: none)
+    if (tt >= nfull) return ~0u;
+    const uint32_t nx = tt + nbs;
+    if (nx < t_end) return nx;
+    return last_partial ? nfull : ~0u;
+  };
+  int64_t kk[ITEMS];
+  V vv[ITEMS];
+  auto load = [&](uint32_t tt, int64_t (&k)[ITEMS], V (&v)[ITEMS]) {   // unconditional, clamped
+    const uint32_t r0 = tt * TILE, nr = nrec_of(tt);
+#pragma unroll
+    for (int u = 0; u < ITEMS; ++u) {
+      const uint32_t r = r0 + min((uint32_t)u * BLOCK + tid, nr - 1);
+      uint32_t i = r;
+      bool rev = DIR == DIR_IN;
+      if constexpr (DIR == DIR_ALL) {
+        i = r >> 1;
+        rev = r & 1u;
+      }
+      k[u] = (rev ? es.dst : es.src)[i];
+      v[u] = es.val[i];
+    }
+  };
+  load(t, kk, vv);
+  uint32_t ovf = 0, esc = 0;
+  for (;;) {
+    const uint32_t nrec = nrec_of(t), r0 = t * TILE, tn = next_of(t);
+    uint32_t kb[ITEMS], vr[ITEMS];
+#pragma unroll
+    for (int u = 0; u < ITEMS; ++u) {
+      const uint32_t j = (uint32_t)u * BLOCK + tid;
+      const uint64_t d = (uint64_t)kk[u] - (uint64_t)es.base;
+      const bool in = (d >> S) < nbp, live = j < nrec;
+      ovf += (live && !in) ? 1u : 0u;
+      const uint32_t nv = pk_narrow(vv[u]);
+      const bool e = nv == PK_ESC;
+      kb[u] = (live && in) ? ((uint32_t)(d >> S) << 16) | ((uint32_t)d & lmask) | (e ? ESC : 0u) : DUMMY;
+      vr[u] = (e ? j : nv) << 16;
+    }
+    for (uint32_t i = tid; i < nbp; i += BLOCK) s_tab[i] = 0;
+    if (tid == 0) s_tab[BK_MAXB] = 0;
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < ITEMS; ++u) vr[u] |= atomicAdd(&s_tab[(kb[u] >> 16) & 0x7FFFu], 1u);
+    __syncthreads();
+    const uint32_t c0 = b0 < nbp ? s_tab[b0] : 0u, c1 = b1 < nbp ? s_tab[b1] : 0u;
+    const uint32_t o0 = c0 ? atomicAdd(&cur[b0], c0) : 0u;   // reservations first ...
+    const uint32_t o1 = c1 ? atomicAdd(&cur[b1], c1) : 0u;
+    if (tn != ~0u) load(tn, kk, vv);                           // ... then the next tile's columns
+    uint32_t total;
+    const uint32_t st0 = block_excl_scan<BLOCK>(c0 + c1, s_w, total);
+    __syncthreads();   // every count read before the starts overwrite them
+    s_tab[b0] = st0;
+    s_tab[b1] = st0 + c0;
+    if (tid == 0) s_tab[BK_MAXB] = total;
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < ITEMS; ++u) {
+      const uint32_t pos = s_tab[(kb[u] >> 16) & 0x7FFFu] + (vr[u] & 0xFFFFu);
+      s_key[pos] = kb[u];
+      s_v16[pos] = (uint16_t)(vr[u] >> 16);
+    }
+    __syncthreads();
+    const bool drop0 = c0 && o0 + c0 > end0, drop1 = c1 && o1 + c1 > end1;
+    s_tab[b0] = (drop0 ? trash : o0) - st0;
+    s_tab[b1] = (drop1 ? trash : o1) - (st0 + c0);
+    if (tid == 0) s_tab[BK_MAXB] = trash - total;
+    ovf += (drop0 ? 1u : 0u) + (drop1 ? 1u : 0u);
+    __syncthreads();
+    uint32_t escm = 0;
+#pragma unroll
+    for (int u = 0; u < ITEMS; ++u) {
+      const uint32_t j = (uint32_t)u * BLOCK + tid;
+      const uint32_t kv = s_key[j];
+      const bool e = kv & ESC;
+      rec[s_tab[(kv >> 16) & 0x7FFFu] + j] = (kv & 0xFFFFu) | ((e ? PK_ESC : (uint32_t)s_v16[j]) << 16);
+      escm |= e ? 1u << u : 0u;
+    }
+    for (; escm; escm &= escm - 1, ++esc) {
+      const uint32_t j = (uint32_t)__builtin_ctz(escm) * BLOCK + tid;
+      const uint32_t kv = s_key[j];
+      const uint32_t r = r0 + s_v16[j];
+      wide[s_tab[(kv >> 16) & 0x7FFFu] + j] = es.val[DIR == DIR_ALL ? r >> 1 : r];
+    }
+    if (tn == ~0u) break;
+    t = tn;
+    __syncthreads();   // the store phase's reads of s_tab / s_key before the next tile rewrites them
   }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {

@@ -14,8 +14,9 @@
 //   watermarks   explicit (gs_stream_watermark), or ascending: max timestamp seen - 1 after every
 //                append (AscendingTimestampExtractor, SimpleEdgeStream.java:90-94 / WindowTriangles.java
 //                :225-230); gs_stream_flush = the end of a finite source (watermark Long.MAX_VALUE)
-//   late records records of an already fired window are dropped and counted (the reference's
-//                ascending timestamps never produce any)
+//   late records records of an already fired window (the reference's ascending timestamps never
+//                produce any): GS_LATE_REFIRE, as Flink 1.0.3's WindowOperator (no lateness check: a
+//                fresh pane whose end - 1 timer fires at the next watermark), or GS_LATE_DROP; both count
 //
 // Pipelining: a fired window's columns go to one of two device slots with hipMemcpyAsync on the
 // operator's copy stream; the window's kernels run on the ctx stream when the caller polls.  So the
@@ -75,6 +76,16 @@ struct Result {   // one window's result; its rows live in the pinned buffers be
 
 // host copy into the pinned window buffers: large blocks split over threads (one thread streams
 // ~5-10 GB/s of host memory; a 2^28-edge window is 6 GB)
+// host memory the DMA engines can read directly (hipHostMalloc / registered); pageable memory is not
+bool is_pinned(const void* p) {
+  hipPointerAttribute_t a;
+  if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+    (void)hipGetLastError();   // a pageable pointer: clear the error the query left
+    return false;
+  }
+  return a.type == hipMemoryTypeHost;
+}
+
 void par_memcpy(void* dst, const void* src, size_t bytes) {
   constexpr size_t PART = 64ull << 20;
   const unsigned hw = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
@@ -156,6 +167,7 @@ struct gs_stream {
   std::vector<Result*> rpool;
   Result* current = nullptr;           // handed out by the last poll
   std::string err;
+  hipEvent_t appended = nullptr;       // direct staging from pinned columns: the append's DMAs are done
 };
 
 namespace {
@@ -429,6 +441,7 @@ gs_status gs_stream_create(gs_ctx* c, const gs_stream_config* cfg, gs_stream** o
     return set_error(c, GS_EINVAL, "bad op %d for dtype %d", cfg->op, cfg->val_dtype);
   if (cfg->kind == GS_STREAM_FOLD && !cfg->init) return set_error(c, GS_EINVAL, "foldNeighbors needs an init value");
   if (cfg->staging != GS_STAGE_PINNED && cfg->staging != GS_STAGE_DIRECT) return set_error(c, GS_EINVAL, "bad staging mode");
+  if (cfg->late_mode != GS_LATE_REFIRE && cfg->late_mode != GS_LATE_DROP) return set_error(c, GS_EINVAL, "bad late mode");
   gs_stream* s = new (std::nothrow) gs_stream();
   if (!s) return GS_ENOMEM;
   s->c = c;
@@ -466,6 +479,7 @@ void gs_stream_destroy(gs_stream* s) {
   for (Result* r : s->rpool) free_result(r);
   free_result(s->current);
   if (s->copy) hipStreamDestroy(s->copy);
+  if (s->appended) hipEventDestroy(s->appended);
   delete s;
 }
 
@@ -482,14 +496,22 @@ gs_status gs_stream_append(gs_stream* s, const int64_t* src, const int64_t* dst,
   // truncating remainder).
   uint64_t i = 0;
   int64_t mx = s->max_ts;
+  // direct staging from caller-pinned columns (gs_alloc_pinned, a Java direct buffer registered with
+  // HIP): the copies are DMAs straight from them at PCIe rate, no runtime staging copy; the append
+  // returns once they have read the columns (the caller may refill them)
+  const bool pinned_src = s->cfg.staging == GS_STAGE_DIRECT && n && is_pinned(src) && is_pinned(dst) &&
+                          (!s->vb || is_pinned(val));
+  bool queued = false;
   while (i < n) {
     const int64_t start = ts[i] - ts[i] % size;
     const int64_t lo = start > 0 ? start : start - size + 1, hi = start < 0 ? start : start + size - 1;
     const uint64_t j = run_end(ts, i, n, lo, hi, &mx);
     const uint64_t k = j - i;
-    if (start + size - 1 <= s->watermark) {   // the window already fired: late records
-      s->late += k;
-    } else if (s->cfg.staging == GS_STAGE_DIRECT) {
+    const bool late = start + size - 1 <= s->watermark;   // the window already fired
+    if (late) s->late += k;
+    if (late && s->cfg.late_mode == GS_LATE_DROP) {
+      // dropped (counted above)
+    } else if (s->cfg.staging == GS_STAGE_DIRECT) {   // (a late run opens a fresh pane: GS_LATE_REFIRE)
       auto it = s->dopen.find(start);
       if (it == s->dopen.end()) it = s->dopen.emplace(start, DirectWin{take_slot(s), 0}).first;
       DirectWin& w = it->second;
@@ -502,6 +524,7 @@ gs_status gs_stream_append(gs_stream* s, const int64_t* src, const int64_t* dst,
         GS_HIP(hipMemcpyAsync(w.slot->val + w.n * s->vb, (const char*)val + i * s->vb, k * s->vb,
                               hipMemcpyHostToDevice, s->copy));
       w.n += k;
+      queued = true;
     } else {
       auto it = s->open.find(start);
       PinnedCols* p;
@@ -519,6 +542,11 @@ gs_status gs_stream_append(gs_stream* s, const int64_t* src, const int64_t* dst,
       p->n += k;
     }
     i = j;
+  }
+  if (pinned_src && queued) {
+    if (!s->appended) GS_HIP(hipEventCreateWithFlags(&s->appended, hipEventDisableTiming));
+    GS_HIP(hipEventRecord(s->appended, s->copy));
+    GS_HIP(hipEventSynchronize(s->appended));
   }
   s->max_ts = mx;
   if (s->cfg.watermark_mode == GS_WATERMARK_ASCENDING && s->max_ts != INT64_MIN) GS_TRY(advance(s, s->max_ts - 1));

@@ -7,7 +7,9 @@ per window in pinned host memory (start = ts - ts % size, Java remainder), and a
 watermark reaches end - 1.  Its columns are copied to HBM on the operator's copy stream (overlapping the
 previous window's kernels) and its result — stamped end - 1 — comes back from poll() in firing order.
 Watermarks are explicit (watermark()) or ascending (max timestamp seen - 1 after every append, the
-AscendingTimestampExtractor of SimpleEdgeStream.java:90-94); flush() ends a finite source.
+AscendingTimestampExtractor of SimpleEdgeStream.java:90-94); flush() ends a finite source.  Records of a
+window that already fired open a fresh pane that fires at the next watermark (late_mode GS_LATE_REFIRE,
+Flink 1.0.3's WindowOperator) or are dropped (GS_LATE_DROP); both are counted in stats()["late_records"].
 """
 from __future__ import annotations
 
@@ -34,7 +36,8 @@ class WindowResult:
 class WindowOperator:
     def __init__(self, engine, window_ms: int, kind: int = L.GS_STREAM_REDUCE, direction: int = 1, op: int = 0,
                  val_dtype=np.int64, watermarks: int = L.GS_WATERMARK_ASCENDING, init=None,
-                 init_max: int = -(1 << 63), max_window_edges: int = 0, staging: int = L.GS_STAGE_PINNED):
+                 init_max: int = -(1 << 63), max_window_edges: int = 0, staging: int = L.GS_STAGE_PINNED,
+                 late_mode: int = L.GS_LATE_REFIRE):
         self._L, self.engine = engine._L, engine
         self.kind = kind
         self.op = op
@@ -45,7 +48,7 @@ class WindowOperator:
             self._init = np.array([init], dtype=np.int64 if op == L.GS_OP_COUNT else val_dtype)
         cfg = L.GsStreamConfig(int(window_ms), kind, int(direction), int(op), gdt, watermarks, int(staging),
                                None if self._init is None else self._init.ctypes.data_as(ctypes.c_void_p),
-                               int(init_max), int(max_window_edges))
+                               int(init_max), int(max_window_edges), int(late_mode), 0)
         h = ctypes.c_void_p()
         st = self._L.gs_stream_create(engine.ctx, ctypes.byref(cfg), ctypes.byref(h))
         if st != L.GS_OK:

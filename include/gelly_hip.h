@@ -396,12 +396,19 @@ GS_API gs_status gs_parse_edges_text(gs_ctx* ctx, const char* text, uint64_t byt
  * fires when the watermark reaches end - 1; its result carries the timestamp end - 1.  A fired
  * window's columns are copied to HBM on the operator's own copy stream, so window k+1's copy overlaps
  * window k's kernels.  Results come back in firing order from gs_stream_poll.  Records of a window
- * that already fired are dropped and counted (late). */
+ * that already fired: gs_stream_config.late_mode. */
 typedef struct gs_stream gs_stream;
 enum { GS_STREAM_REDUCE = 0, GS_STREAM_FOLD = 1, GS_STREAM_DEGREE_MAX = 2, GS_STREAM_TRIANGLES = 3 };
 enum { GS_WATERMARK_EXPLICIT = 0,    /* gs_stream_watermark only                                   */
        GS_WATERMARK_ASCENDING = 1 }; /* AscendingTimestampExtractor: max timestamp seen - 1        */
 enum { GS_STAGE_PINNED = 0, GS_STAGE_DIRECT = 1 };
+/* Records of a window that already fired.  GS_LATE_REFIRE (default): Flink 1.0.3's WindowOperator has no
+ * lateness check -- the record goes into fresh window state (the fired pane was purged,
+ * EventTimeTrigger FIRE_AND_PURGE) and registers a timer at end - 1, already behind the watermark, which
+ * fires at the next watermark: the window fires again with only its late records.  GS_LATE_DROP: they
+ * are dropped (Flink >= 1.1 with allowedLateness 0).  Both count them in late_records.  No reference
+ * fixture covers late records: parity unpinned. */
+enum { GS_LATE_REFIRE = 0, GS_LATE_DROP = 1 };
 
 typedef struct gs_stream_config {
   int64_t window_ms;       /* tumbling window size (Time.milliseconds)                          */
@@ -412,10 +419,14 @@ typedef struct gs_stream_config {
   int32_t watermark_mode;  /* GS_WATERMARK_*                                                    */
   int32_t staging;         /* GS_STAGE_PINNED: records copied into pinned window buffers, the
                               window's H2D at firing; GS_STAGE_DIRECT: each append is copied straight
-                              into the window's device columns (pageable H2D on the copy stream)  */
+                              into the window's device columns on the copy stream -- by DMA from the
+                              caller's columns when they are pinned (gs_alloc_pinned; the append
+                              returns once the DMA has read them), else through HIP's pageable staging */
   const void* init;        /* FOLD: one value of the result dtype (copied at create)           */
   int64_t init_max;        /* DEGREE_MAX: initial maximum                                       */
   uint64_t max_window_edges; /* expected window size: pinned / device buffers are sized for it  */
+  int32_t late_mode;       /* GS_LATE_*                                                         */
+  int32_t reserved;
 } gs_stream_config;
 
 typedef struct gs_window_result {

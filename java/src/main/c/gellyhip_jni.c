@@ -161,7 +161,7 @@ typedef struct {
 
 JNIEXPORT jlong JNI_FN(streamCreate)(JNIEnv* env, jclass cls, jlong ctx, jlong window_ms, jint kind, jint dir, jint op,
                                      jint dt, jint wm_mode, jint staging, jobject init, jlong init_max,
-                                     jlong max_edges) {
+                                     jlong max_edges, jint late_mode) {
   gs_ctx* c = (gs_ctx*)(intptr_t)ctx;
   gs_stream_config cfg;
   memset(&cfg, 0, sizeof cfg);
@@ -175,6 +175,7 @@ JNIEXPORT jlong JNI_FN(streamCreate)(JNIEnv* env, jclass cls, jlong ctx, jlong w
   cfg.init = addr(env, init);
   cfg.init_max = init_max;
   cfg.max_window_edges = (uint64_t)max_edges;
+  cfg.late_mode = late_mode;
   gs_stream* st = NULL;
   gs_status s = gs_stream_create(c, &cfg, &st);
   if (s != GS_OK) {

@@ -65,6 +65,8 @@ public final class GellyHip {
 	public static final int GS_WATERMARK_ASCENDING = 1;
 	public static final int GS_STAGE_PINNED = 0;
 	public static final int GS_STAGE_DIRECT = 1;
+	public static final int GS_LATE_REFIRE = 0;   // Flink 1.0.3 WindowOperator: a late record re-fires its window
+	public static final int GS_LATE_DROP = 1;
 
 	/* ---- lifecycle: gs_abi_version, gs_create / gs_destroy ---------------------------------------- */
 	static native int abiVersion();
@@ -110,7 +112,7 @@ public final class GellyHip {
 
 	/* ---- the window-buffer operator (gs_stream_*): event-time tumbling windows ------------------------ */
 	static native long streamCreate(long ctx, long windowMs, int kind, int direction, int op, int valDtype,
-			int watermarkMode, int staging, ByteBuffer init, long initMax, long maxWindowEdges);
+			int watermarkMode, int staging, ByteBuffer init, long initMax, long maxWindowEdges, int lateMode);
 
 	static native void streamDestroy(long stream);
 

@@ -71,7 +71,7 @@ public class GpuWindowOperator<EV, OUT extends Tuple> extends AbstractStreamOper
 			initMax = (Long) init;
 		}
 		stream = GellyHip.streamCreate(ctx, windowMs, kind, direction, op, valDtype, GellyHip.GS_WATERMARK_EXPLICIT,
-				GellyHip.GS_STAGE_PINNED, initBuf, initMax, maxWindowEdges);
+				GellyHip.GS_STAGE_PINNED, initBuf, initMax, maxWindowEdges, GellyHip.GS_LATE_REFIRE);
 		src = GellyHip.direct(8L * BATCH);
 		dst = GellyHip.direct(8L * BATCH);
 		val = valDtype == GellyHip.GS_NONE ? null : GellyHip.direct(8L * BATCH);

@@ -1,6 +1,7 @@
 """GPU: the event-time window-buffer operator (gs_stream_*, gelly_streaming_amd.window_operator) against the
 oracle applied window by window (Flink 1.0.3 TumblingEventTimeWindows semantics: start = ts - ts % size
-with Java's remainder, fire at watermark >= end - 1, results stamped end - 1, late records dropped)."""
+with Java's remainder, fire at watermark >= end - 1, results stamped end - 1; late records re-fire at the next
+watermark as a fresh pane, Flink 1.0.3's WindowOperator, or are dropped)."""
 import numpy as np
 import pytest
 
@@ -53,13 +54,13 @@ def test_ascending_stream_reduce(pkg, engine, oracle, chunk, staging):
 
 def test_out_of_order_explicit_watermarks_and_late_records(pkg, engine, oracle):
     """Out-of-order records land in their open windows; a watermark fires exactly the windows with
-    end - 1 <= watermark; records of a fired window are dropped and counted as late."""
+    end - 1 <= watermark; with GS_LATE_DROP records of a fired window are dropped and counted as late."""
     from gelly_streaming_amd import _lib as L
     n, size = 40_000, 500
     s, d, v, ts = _stream(oracle, n, size, 6, 9, ascending=False)
     ts = ts - 1200   # negative timestamps too: start = ts - ts % size rounds toward zero (Java)
     with _op(pkg, engine, window_ms=size, kind=L.GS_STREAM_REDUCE, direction=2, op=2,
-             watermarks=L.GS_WATERMARK_EXPLICIT, staging=L.GS_STAGE_DIRECT) as op:
+             watermarks=L.GS_WATERMARK_EXPLICIT, staging=L.GS_STAGE_DIRECT, late_mode=L.GS_LATE_DROP) as op:
         half = n // 2
         op.append(s[:half], d[:half], v[:half], ts[:half])
         assert op.poll(wait=False) is None                      # nothing fired yet
@@ -82,6 +83,44 @@ def test_out_of_order_explicit_watermarks_and_late_records(pkg, engine, oracle):
         ii = idx_all[idx]
         rk, rv = oracle.window_reduce(s[ii], d[ii], v[ii], 2, 2)
         assert np.array_equal(g.columns[0], rk) and np.array_equal(g.columns[1], rv)
+
+
+@pytest.mark.parametrize("staging", [0, 1])
+def test_late_records_refire_at_the_next_watermark(pkg, engine, oracle, staging):
+    """GS_LATE_REFIRE (the default; Flink 1.0.3's WindowOperator has no lateness check): records of a
+    window that already fired go into a fresh pane of that window, which fires -- with only those
+    records -- at the next watermark, before the windows that watermark newly closes.  Parity unpinned
+    (no reference fixture covers late records); the expected panes are the oracle over each batch."""
+    from gelly_streaming_amd import _lib as L
+    size = 500
+    s, d, v, ts = _stream(oracle, 30_000, size, 6, 17, ascending=False)
+    b1, b2 = slice(0, 20_000), slice(20_000, 30_000)
+    with _op(pkg, engine, window_ms=size, kind=L.GS_STREAM_REDUCE, direction=1, op=0,
+             watermarks=L.GS_WATERMARK_EXPLICIT, staging=staging) as op:
+        op.append(s[b1], d[b1], v[b1], ts[b1])
+        op.watermark(1499)                      # windows 0, 500, 1000 fire
+        first = op.drain()
+        op.append(s[b2], d[b2], v[b2], ts[b2])  # some land in fired windows: late
+        late = int(np.sum(ts[b2] < 1500))
+        assert op.stats()["late_records"] == late and late > 0
+        assert op.poll(wait=False) is None      # a late pane waits for the next watermark
+        op.watermark(1999)                      # the late panes, then window 1500
+        second = op.drain()
+        op.flush()
+        rest = op.drain()
+    def panes(idx, lo, hi):
+        sel = idx[(ts[idx] >= lo) & (ts[idx] < hi)]
+        return [(st, sel[w]) for st, w in oracle.split_windows(ts[sel], size)]
+    i1, i2 = np.arange(0, 20_000), np.arange(20_000, 30_000)
+    want_first = panes(i1, 0, 1500)
+    want_second = panes(i2, 0, 1500) + panes(np.concatenate([i1, i2]), 1500, 2000)
+    want_rest = panes(np.concatenate([i1, i2]), 2000, 6 * size)
+    for got, want in ((first, want_first), (second, want_second), (rest, want_rest)):
+        assert [g.start for g in got] == [w[0] for w in want]
+        for g, (start, idx) in zip(got, want):
+            rk, rv = oracle.window_reduce(s[idx], d[idx], v[idx], 1, 0)
+            assert g.edges == len(idx)
+            assert np.array_equal(g.columns[0], rk) and np.array_equal(g.columns[1], rv)
 
 
 def test_degree_max_and_fold_kinds(pkg, engine, oracle):

@@ -60,7 +60,8 @@ case $MODE in
     bench bench_candidates --workload candidates
     bench bench_parse --workload parse
     bench bench_e2e_direct --workload e2e --staging direct --no-cpu-baseline
-    bench bench_e2e_pinned --workload e2e --staging pinned --no-cpu-baseline ;;
+    bench bench_e2e_pinned --workload e2e --staging pinned --no-cpu-baseline
+    bench bench_e2e_buffered --workload e2e --staging buffered --no-cpu-baseline ;;
   *)
     echo "usage: tools/gpu.sh tests|bench|c2|sq|tri|evidence TAG [args]" >&2; exit 2 ;;
 esac
