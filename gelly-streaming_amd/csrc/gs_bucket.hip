@@ -286,12 +286,12 @@ gs_status bucket_direct_t(gs_ctx* c, const int64_t* src, const int64_t* dst, con
   bool spec = false, spec_missed = false;
   uint64_t cap = R;
   // the speculative scatter's tile: k_sp_scatter_pack (SPK_BLOCK x SPK_ITEMS) or k_sp_scatter (DP_TILE)
-  const uint64_t TRASH = std::max<uint64_t>(std::max(SPK_TILE, PP_TILE), (uint64_t)DP_BLOCK * ITEMS);
-  const uint64_t SPTE = !pack ? dp_tile_edges<DIR, ITEMS>() : GS_SPK_PP ? pp_tile_edges<DIR>() : spk_tile_edges<DIR>();
+  const uint64_t TRASH = std::max<uint64_t>(SPK_TILE, (uint64_t)DP_BLOCK * ITEMS);
+  const uint64_t SPTE = !pack ? dp_tile_edges<DIR, ITEMS>() : spk_tile_edges<DIR>();
   auto& sp = c->sp[c->sp_slot];
   if constexpr (SPEC_OK) {
     GS_TRY(ensure(c, sp.tot, BK_MAXB * 4, true));
-    GS_TRY(ensure(c, c->sp_cur, (SP_NSEG * BK_MAXB + SP_NSEG + 1) * 4));
+    GS_TRY(ensure(c, c->sp_cur, SP_CUR_WORDS * 4));
     spec = !(c->flags & GS_FLAG_NO_SPEC) && sp.ok && sp.skip == 0 && sp.base == base && sp.S == S &&
            sp.dir == DIR && nb > 1 && sp_capacity(R, nb) + TRASH < (1ull << 32);   // u32 positions + trash
     if (sp.skip > 0) --sp.skip;
@@ -339,13 +339,14 @@ gs_status bucket_direct_t(gs_ctx* c, const int64_t* src, const int64_t* dst, con
         const uint32_t* bst = meta + BkMeta::BSTART;
         uint32_t* cur = c->sp_cur.as<uint32_t>();
         if constexpr (CAN_PACK && ITEMS == PK_ITEMS) {
-          if (pack && GS_SPK_PP)   // persistent: one block per CU, 8 XCD slots
-            hipLaunchKernelGGL((k_sp_scatter_pack_pp<Load, DIR>), dim3(std::max(8, c->n_cu / 8 * 8)), dim3(PP_BLOCK), 0,
-                               c->stream, ls, n, S, nb, bst, cur, c->keysB.as<uint32_t>(), vpart, (uint32_t)cap, mm,
+          // the bucket tables sized for the window's buckets (1024: 8 KiB less LDS, one bucket per thread)
+          if (pack && nb <= 1024)
+            hipLaunchKernelGGL((k_sp_scatter_pack<Load, DIR, 1024>), dim3(spk_grid<DIR>(n)), dim3(SPK_BLOCK), 0,
+                               c->stream, ls, n, S, nb, cur, c->keysB.as<uint32_t>(), vpart, (uint32_t)cap, mm,
                                (unsigned long long*)(sm + SM_BK_ESC));
           else if (pack)
-            hipLaunchKernelGGL((k_sp_scatter_pack<Load, DIR>), dim3(spk_grid<DIR>(n)), dim3(SPK_BLOCK), 0,
-                               c->stream, ls, n, S, nb, bst, cur, c->keysB.as<uint32_t>(), vpart, (uint32_t)cap, mm,
+            hipLaunchKernelGGL((k_sp_scatter_pack<Load, DIR, BK_MAXB>), dim3(spk_grid<DIR>(n)), dim3(SPK_BLOCK), 0,
+                               c->stream, ls, n, S, nb, cur, c->keysB.as<uint32_t>(), vpart, (uint32_t)cap, mm,
                                (unsigned long long*)(sm + SM_BK_ESC));
         }
         if constexpr (ITEMS == DP_ITEMS) {

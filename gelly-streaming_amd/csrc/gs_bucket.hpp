@@ -31,6 +31,9 @@ namespace gs {
 
 constexpr int BK_MAXB = 2048;          // buckets (the bucket index has <= 11 bits)
 constexpr int BK_INFO_BLOCK = 512;
+#ifndef GS_BK_PIPE
+#define GS_BK_PIPE 0   // k_bk_accum (packed records), A/B: next group's loads in flight during this group's atomics (C2 accumulate 0.345 vs 0.331 ms: off)
+#endif
 constexpr int BK_ACC_BLOCK = 1024;     // 16 waves: one workgroup per CU (LDS-bound)
 constexpr int BK_NW = BK_ACC_BLOCK / WAVE;
 constexpr int BK_PLAN_BLOCK = 1024;
@@ -78,6 +81,9 @@ constexpr uint32_t SP_NSEG = GS_SP_XCD ? 8 : 1;
 constexpr uint32_t SP_PAD = 1024;                  // absolute slack per bucket
 constexpr uint32_t SP_PADSEG = SP_PAD / SP_NSEG;   // ... per segment
 static_assert(SP_PADSEG % 4 == 0, "segment starts stay 4-aligned");
+// the cursor buffer: SP_NSEG x BK_MAXB cursors | pre[SP_NSEG + 1] | SP_NSEG x BK_MAXB segment ends
+constexpr uint32_t SP_END_OFF = SP_NSEG * BK_MAXB + 16;
+constexpr uint32_t SP_CUR_WORDS = SP_END_OFF + SP_NSEG * BK_MAXB;
 struct SpSlots {
   uint32_t pre[SP_NSEG + 1];
 };
@@ -1074,6 +1080,11 @@ static __global__ __launch_bounds__(BK_PLAN_BLOCK) void k_sp_regions(const uint3
     if (b1 < nb) cursor[x * BK_MAXB + b1] = sp_seg_start(s0 + c0, s0 + c0 + c1, x, slots.pre);
   }
   if (tid <= (int)SP_NSEG) cursor[SP_NSEG * BK_MAXB + tid] = slots.pre[tid];   // for the later kernels
+  uint32_t* seg_end = cursor + SP_END_OFF;   // segment ends: the scatter's overflow test without a division
+  for (uint32_t x = 0; x < SP_NSEG; ++x) {
+    if (b0 < nb) seg_end[x * BK_MAXB + b0] = sp_seg_start(s0, s0 + c0, x + 1, slots.pre);
+    if (b1 < nb) seg_end[x * BK_MAXB + b1] = sp_seg_start(s0 + c0, s0 + c0 + c1, x + 1, slots.pre);
+  }
   if (tid == 0) bucket_start[nb] = total;
   if (tid < 4) mm[tid] = 0;
 }
@@ -1089,19 +1100,24 @@ __host__ __device__ inline uint64_t sp_capacity(uint64_t r_now, uint32_t nb) {
 // range is not tracked here: on a hit every key lay in the predicted range, and k_bk_plan reports the
 // occupied buckets for the next prediction; on a miss the window's rerun measures it.
 //
-// Block shape (SPK_BLOCK threads x SPK_ITEMS records): a tile's phases run in turn -- loads (HBM
-// latency), rank (LDS atomics), scan, LDS scatter, stores -- so the CU needs a second (third) block
-// whose loads are in flight while this one ranks and stores.  One bucket table serves as counts, run
-// starts and then run deltas (8 KiB), so a 512 x 16 tile takes 56 KiB of LDS: two blocks per CU at
-// <= 128 VGPRs (1024-thread blocks could not: two of them cap a lane at 64 VGPRs and spill).
+// LDS traffic per record (what bounds this kernel once the loads overlap: a timing-only build without
+// column loads and record stores still took 0.75 ms of the 1.3 ms C2 scatter): the rank (one returning
+// LDS atomic on the bucket's count), one 8-byte read of the bucket's run entry (tile start | global
+// start), one 8-byte write of the record's slot (packed record | global position) in bucket order and
+// one linear 8-byte read of it in the store loop -- three random LDS accesses and one linear.  The
+// reservations (one returning atomicAdd per (tile, bucket) on the XCD slot's cursor) are known before
+// the LDS scatter, so the slot already carries the record's global position and the store loop needs
+// no table lookup.  Escaped values (rare) are written to `wide` by the scattering lane, which still
+// knows the record's column index.
+//
+// Block shape: SPK_BLOCK threads x SPK_ITEMS records.  512 x 16 with the 1024-bucket tables (72 KiB of
+// LDS, <= 128 VGPRs): two blocks per CU, so one block's loads are in flight while the other ranks,
+// scatters and stores (C2: 1.08 ms against 1.14 ms for one 1024 x 16 block per CU).
 #ifndef GS_SPK_BLOCK
 #define GS_SPK_BLOCK 512
 #endif
 #ifndef GS_SPK_ITEMS
 #define GS_SPK_ITEMS 16
-#endif
-#ifndef GS_SPK_ABL_NOATOMIC
-#define GS_SPK_ABL_NOATOMIC 0
 #endif
 #ifndef GS_SPK_ABL_NOLOAD
 #define GS_SPK_ABL_NOLOAD 0
@@ -1109,14 +1125,13 @@ __host__ __device__ inline uint64_t sp_capacity(uint64_t r_now, uint32_t nb) {
 #ifndef GS_SPK_ABL_NOSTORE
 #define GS_SPK_ABL_NOSTORE 0
 #endif
+#ifndef GS_SPK_LATE
+#define GS_SPK_LATE 0   // 1: run deltas written after the LDS scatter (the reservations' latency hides behind it)
+#endif
 #ifndef GS_SPK_WAVES
-#define GS_SPK_WAVES (2 * GS_SPK_BLOCK / 256)   // waves per SIMD: two blocks per CU
+#define GS_SPK_WAVES 4   // waves per SIMD: one 1024-thread block or two 512-thread blocks per CU
 #endif
-#ifndef GS_SPK_GROUPS
-#define GS_SPK_GROUPS 1
-#endif
-constexpr int SPK_BLOCK = GS_SPK_BLOCK, SPK_ITEMS = GS_SPK_ITEMS, SPK_GROUPS = GS_SPK_GROUPS;
-static_assert(SPK_ITEMS % SPK_GROUPS == 0, "load groups split the tile evenly");
+constexpr int SPK_BLOCK = GS_SPK_BLOCK, SPK_ITEMS = GS_SPK_ITEMS;
 constexpr uint32_t SPK_TILE = (uint32_t)SPK_BLOCK * SPK_ITEMS;
 static_assert(BK_MAXB % SPK_BLOCK == 0 && SPK_TILE <= 65536 && SPK_ITEMS <= 32, "tile / bucket-table shape");
 template <int DIR>
@@ -1148,18 +1163,28 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t x, uint32_t* s_w, u
   return off + inc - x;
 }
 
-template <typename V, int DIR>
+template <typename V, int DIR, int NB>
 __global__ __launch_bounds__(SPK_BLOCK) __attribute__((amdgpu_waves_per_eu(GS_SPK_WAVES, GS_SPK_WAVES)))
 void k_sp_scatter_pack(BaseSrc<V, DIR, PAY_VAL> es, uint64_t n, int S, uint32_t nbp,
-                       const uint32_t* __restrict__ bucket_start, uint32_t* __restrict__ cursor,
-                       uint32_t* __restrict__ rec, V* __restrict__ wide, uint32_t trash,
-                       unsigned long long* __restrict__ mm, unsigned long long* __restrict__ n_esc) {
-  constexpr int ITEMS = SPK_ITEMS, BLOCK = SPK_BLOCK, BPT = BK_MAXB / SPK_BLOCK;   // buckets per thread
+                       uint32_t* __restrict__ cursor, uint32_t* __restrict__ rec, V* __restrict__ wide,
+                       uint32_t trash, unsigned long long* __restrict__ mm, unsigned long long* __restrict__ n_esc) {
+  constexpr int ITEMS = SPK_ITEMS, BLOCK = SPK_BLOCK;
+  constexpr int BPT = NB >= BLOCK ? NB / BLOCK : 1;   // buckets per thread
+  static_assert(NB <= BK_MAXB && (NB % BLOCK == 0 || NB < BLOCK), "bucket table shape");
   constexpr uint32_t TILE = SPK_TILE;
-  constexpr uint32_t ESC = 1u << 31, DUMMY = (uint32_t)BK_MAXB << 16;   // kb: escaped value / dummy bucket
-  __shared__ uint32_t s_key[TILE];         // ESC | (bucket << 16) | bucket-local index, bucket order
-  __shared__ uint16_t s_v16[TILE];         // narrow value, or an escape's tile-local record index
-  __shared__ uint32_t s_tab[BK_MAXB + 1];  // counts -> run starts in the tile -> global - tile position
+  constexpr uint32_t ESC = 1u << 31, DUMMY = (uint32_t)NB << 16;   // kb: escaped value / dummy bucket
+  __shared__ uint64_t s_slot[TILE];   // bucket order; early: packed << 32 | global position,
+                                      // late: packed << 32 | tile record << 12 | bucket
+#if GS_SPK_LATE
+  __shared__ uint32_t s_st[NB + 1];    // run starts in the tile
+  __shared__ uint32_t s_del[NB + 1];   // global start - tile start of each run
+#else
+  __shared__ uint64_t s_run[NB + 1];   // global start of the run << 32 | its start in the tile
+#endif
+  // per-bucket counts (the rank atomics): in the slots' space, read into registers before the scan's
+  // barrier
+  uint32_t* s_cnt = reinterpret_cast<uint32_t*>(s_slot);
+  static_assert((NB + 1) * 4 <= TILE * 8 && TILE <= (1u << 20), "counts fit the slot array");
   __shared__ uint32_t s_w[BLOCK / WAVE];
   __shared__ uint32_t s_ovf[BLOCK / WAVE];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -1178,304 +1203,152 @@ void k_sp_scatter_pack(BaseSrc<V, DIR, PAY_VAL> es, uint64_t n, int S, uint32_t 
   }
   const uint32_t r0 = t * TILE;
   const uint32_t xs = SP_NSEG == 1 ? 0u : blockIdx.x & 7u;   // this block's XCD slot: its segment
-  const uint32_t* pre = cursor + SP_NSEG * BK_MAXB;
+  auto col_index = [&](uint32_t j) -> uint32_t { return DIR == DIR_ALL ? (r0 + j) >> 1 : r0 + j; };
+  // this thread's buckets (BPT consecutive ones): their segment ends, issued before the columns
+  uint32_t send[BPT];
+#pragma unroll
+  for (int k = 0; k < BPT; ++k) send[k] = cursor[SP_END_OFF + xs * BK_MAXB + min((uint32_t)tid * BPT + k, nbp - 1)];
   cursor += xs * BK_MAXB;
-  uint32_t kb[ITEMS], vr[ITEMS];   // vr: narrow value (or escape index) << 16 | rank in the tile's run
-  uint32_t ovf = 0;
-  // SPK_GROUPS groups of IG records per lane: a group's loads are unconditional and clamped into the tile
-  // (k_dp_scatter); group g + 1's loads are issued before group g is ranked in LDS, so with two groups a
-  // tile of 24 records per lane fits the 128-VGPR budget and half its load latency hides behind ranking
-  constexpr int G = SPK_GROUPS, IG = ITEMS / G;
-  int64_t kk[IG];
-  V vv[IG];
-  auto load = [&](int g) {
+  // loads: unconditional, clamped into the tile (k_dp_scatter)
+  int64_t kk[ITEMS];
+  V vv[ITEMS];
 #pragma unroll
-    for (int q = 0; q < IG; ++q) {
-      const int u = g * IG + q;
-      const uint32_t r = r0 + min((uint32_t)u * BLOCK + tid, nrec - 1);
-      uint32_t i = r;
-      bool rev = DIR == DIR_IN;
-      if constexpr (DIR == DIR_ALL) {
-        i = r >> 1;
-        rev = r & 1u;
-      }
+  for (int u = 0; u < ITEMS; ++u) {
+    const uint32_t r = r0 + min((uint32_t)u * BLOCK + tid, nrec - 1);
+    uint32_t i = r;
+    bool rev = DIR == DIR_IN;
+    if constexpr (DIR == DIR_ALL) {
+      i = r >> 1;
+      rev = r & 1u;
+    }
 #if GS_SPK_ABL_NOLOAD   // timing-only ablation: synthetic keys in range, no column reads (wrong output)
-      kk[q] = (int64_t)((uint64_t)es.base + ((i * 2654435761u) % ((uint64_t)nbp << S)));
-      vv[q] = (V)(i & 0x3FFF);
-      (void)rev;
+    kk[u] = (int64_t)((uint64_t)es.base + (((uint64_t)(i * 2654435761u) * ((uint64_t)nbp << S)) >> 32));
+    vv[u] = (V)(i & 0x3FFF);
+    (void)rev;
 #else
-      kk[q] = (rev ? es.dst : es.src)[i];
-      vv[q] = es.val[i];
+    kk[u] = (rev ? es.dst : es.src)[i];
+    vv[u] = es.val[i];
 #endif
-    }
-  };
-  auto convert = [&](int g) {
+  }
+  for (uint32_t i = tid; i < nbp; i += BLOCK) s_cnt[i] = 0;
+  if (tid == 0) s_cnt[NB] = 0;
+  // kb: ESC | bucket << 16 | bucket-local vertex (DUMMY for dead lanes / keys outside the range);
+  // vr: narrow value (PK_ESC for an escape) << 16 | rank in the tile's run
+  uint32_t kb[ITEMS], vr[ITEMS];
+  uint32_t ovf = 0;
 #pragma unroll
-    for (int q = 0; q < IG; ++q) {
-      const int u = g * IG + q;
-      const uint32_t j = (uint32_t)u * BLOCK + tid;
-      const uint64_t d = (uint64_t)kk[q] - (uint64_t)es.base;
-      const bool in = (d >> S) < nbp, live = j < nrec;
-      ovf += (live && !in) ? 1u : 0u;
-      const uint32_t nv = pk_narrow(vv[q]);
-      const bool e = nv == PK_ESC;
-      kb[u] = (live && in) ? ((uint32_t)(d >> S) << 16) | ((uint32_t)d & lmask) | (e ? ESC : 0u) : DUMMY;
-      vr[u] = (e ? j : nv) << 16;
-    }
-  };
-  auto rank = [&](int g) {
-#pragma unroll
-    for (int q = 0; q < IG; ++q) {
-      const int u = g * IG + q;
-      vr[u] |= atomicAdd(&s_tab[(kb[u] >> 16) & 0x7FFFu], 1u);
-    }
-  };
-  load(0);
-  for (uint32_t i = tid; i < nbp; i += BLOCK) s_tab[i] = 0;
-  if (tid == 0) s_tab[BK_MAXB] = 0;
-  convert(0);
-  __syncthreads();
-#pragma unroll
-  for (int g = 0; g < G; ++g) {
-    if (g + 1 < G) load(g + 1);
-    rank(g);
-    if (g + 1 < G) convert(g + 1);
+  for (int u = 0; u < ITEMS; ++u) {
+    const uint32_t j = (uint32_t)u * BLOCK + tid;
+    const uint64_t d = (uint64_t)kk[u] - (uint64_t)es.base;
+    const bool in = (d >> S) < nbp, live = j < nrec;
+    ovf += (live && !in) ? 1u : 0u;
+    const uint32_t nv = pk_narrow(vv[u]);
+    kb[u] = (live && in) ? ((uint32_t)(d >> S) << 16) | ((uint32_t)d & lmask) | (nv == PK_ESC ? ESC : 0u) : DUMMY;
+    vr[u] = nv << 16;
   }
   __syncthreads();
-  // this thread's buckets: BPT consecutive ones
+#pragma unroll
+  for (int u = 0; u < ITEMS; ++u) vr[u] |= atomicAdd(&s_cnt[(kb[u] >> 16) & 0x7FFFu], 1u);
+  __syncthreads();
+  // reserve this thread's runs on the slot's cursors
   uint32_t cb[BPT], ob[BPT], sum = 0;
 #pragma unroll
   for (int k = 0; k < BPT; ++k) {
     const uint32_t b = (uint32_t)tid * BPT + k;
-    cb[k] = b < nbp ? s_tab[b] : 0u;
+    cb[k] = b < nbp ? s_cnt[b] : 0u;
     sum += cb[k];
   }
-  // reserve the runs now; the returned offsets are needed only after the LDS scatter
 #pragma unroll
-  for (int k = 0; k < BPT; ++k) {
-#if GS_SPK_ABL_NOATOMIC   // timing-only ablation: no reservation, runs spread over the segment (wrong output)
-    {
-      const uint32_t b = min((uint32_t)tid * BPT + k, nbp - 1);
-      const uint32_t s0 = sp_seg_start(bucket_start[b], bucket_start[b + 1], xs, pre);
-      const uint32_t e0 = sp_seg_start(bucket_start[b], bucket_start[b + 1], xs + 1, pre);
-      const uint32_t span = e0 - s0 > cb[k] ? e0 - s0 - cb[k] : 1u;
-      ob[k] = cb[k] ? s0 + (uint32_t)(((uint64_t)(blockIdx.x >> 3) * cb[k]) % span) : 0u;
-    }
-#else
-    ob[k] = cb[k] ? atomicAdd(&cursor[(uint32_t)tid * BPT + k], cb[k]) : 0u;
-#endif
-  }
+  for (int k = 0; k < BPT; ++k) ob[k] = cb[k] ? atomicAdd(&cursor[(uint32_t)tid * BPT + k], cb[k]) : 0u;
   uint32_t total;
   uint32_t st = block_excl_scan<BLOCK>(sum, s_w, total);   // total: records in the predicted range
+  // A run that does not fit its segment goes to the trash area [trash, trash + TILE) past every region,
+  // at its tile position (nothing reads the trash).
+#if GS_SPK_LATE
+  // late: the scatter needs only the tile starts; the reservations are waited for after it
   uint32_t sb[BPT];
 #pragma unroll
   for (int k = 0; k < BPT; ++k) {
     sb[k] = st;
-    s_tab[(uint32_t)tid * BPT + k] = st;   // unconditional: entries past nbp are never read
+    if ((uint32_t)tid * BPT + k < NB) s_st[(uint32_t)tid * BPT + k] = st;
     st += cb[k];
   }
-  if (tid == 0) s_tab[BK_MAXB] = total;   // the dummy run: the tile's last
+  if (tid == 0) s_st[NB] = total;   // the dummy run: the tile's last
   __syncthreads();
 #pragma unroll
   for (int u = 0; u < ITEMS; ++u) {
-    const uint32_t pos = s_tab[(kb[u] >> 16) & 0x7FFFu] + (vr[u] & 0xFFFFu);
-    s_key[pos] = kb[u];
-    s_v16[pos] = (uint16_t)(vr[u] >> 16);
+    const uint32_t b = (kb[u] >> 16) & 0x7FFFu;
+    const uint32_t packed = (kb[u] & 0xFFFFu) | (vr[u] & 0xFFFF0000u);
+    s_slot[s_st[b] + (vr[u] & 0xFFFFu)] = ((uint64_t)packed << 32) | (((uint32_t)u * BLOCK + tid) << 12) | b;
   }
-  __syncthreads();
-  // run deltas; a run that does not fit its segment goes to the trash area [trash, trash + TILE) past
-  // every region instead (nothing reads the trash)
 #pragma unroll
   for (int k = 0; k < BPT; ++k) {
-    const uint32_t b = min((uint32_t)tid * BPT + k, nbp - 1);
-    const uint32_t end = sp_seg_start(bucket_start[b], bucket_start[b + 1], xs + 1, pre);
-    const bool drop = cb[k] && ob[k] + cb[k] > end;
-    s_tab[(uint32_t)tid * BPT + k] = (drop ? trash : ob[k]) - sb[k];
+    const bool drop = cb[k] && ob[k] + cb[k] > send[k];
     ovf += (drop && !GS_SPK_ABL_NOLOAD) ? 1u : 0u;   // (the ablation's synthetic keys overflow regions)
+    if ((uint32_t)tid * BPT + k < NB) s_del[(uint32_t)tid * BPT + k] = drop ? trash : ob[k] - sb[k];
   }
-  if (tid == 0) s_tab[BK_MAXB] = trash - total;
+  if (tid == 0) s_del[NB] = trash;
   __syncthreads();
-  // stores without a branch; escaped values (PK_ESC in the record) after the loop, rarely taken
-  uint32_t escm = 0;
+  uint32_t esc = 0;
 #pragma unroll
   for (int u = 0; u < ITEMS; ++u) {
     const uint32_t j = (uint32_t)u * BLOCK + tid;
-    const uint32_t kv = s_key[j];
-    const bool e = kv & ESC;
+    const uint64_t e = s_slot[j];
+    const uint32_t g = j + s_del[(uint32_t)e & 0xFFFu];
+    const uint32_t packed = (uint32_t)(e >> 32);
 #if GS_SPK_ABL_NOSTORE   // timing-only ablation: no record stores (wrong output)
-    if (s_tab[(kv >> 16) & 0x7FFFu] + j == 0xFFFFFFFFu) rec[0] = (kv & 0xFFFFu) | ((uint32_t)s_v16[j] << 16);
+    if (g == 0xFFFFFFFFu) rec[0] = packed;
 #else
-    rec[s_tab[(kv >> 16) & 0x7FFFu] + j] = (kv & 0xFFFFu) | ((e ? PK_ESC : (uint32_t)s_v16[j]) << 16);
+    rec[g] = packed;
 #endif
-    escm |= e ? 1u << u : 0u;
+    if ((packed >> 16) == PK_ESC && ((uint32_t)e & 0xFFFu) != (uint32_t)NB) {   // rare: the full value into `wide`
+      wide[g] = es.val[col_index(((uint32_t)e >> 12) & 0xFFFFFu)];
+      ++esc;
+    }
+  }
+#else
+  // early: every slot carries its record's global position, so the store loop needs no table lookup
+#pragma unroll
+  for (int k = 0; k < BPT; ++k) {
+    const bool drop = cb[k] && ob[k] + cb[k] > send[k];
+    ovf += (drop && !GS_SPK_ABL_NOLOAD) ? 1u : 0u;   // (the ablation's synthetic keys overflow regions)
+    if ((uint32_t)tid * BPT + k < NB) s_run[(uint32_t)tid * BPT + k] = ((uint64_t)(drop ? trash + st : ob[k]) << 32) | st;
+    st += cb[k];
+  }
+  if (tid == 0) s_run[NB] = ((uint64_t)(trash + total) << 32) | total;   // the dummy run: the tile's last
+  __syncthreads();
+  uint32_t escm = 0;
+#pragma unroll
+  for (int u = 0; u < ITEMS; ++u) {
+    const uint64_t e = s_run[(kb[u] >> 16) & 0x7FFFu];
+    const uint32_t rk = vr[u] & 0xFFFFu;
+    const uint32_t packed = (kb[u] & 0xFFFFu) | (vr[u] & 0xFFFF0000u);
+    s_slot[(uint32_t)e + rk] = ((uint64_t)packed << 32) | ((uint32_t)(e >> 32) + rk);
+    escm |= (kb[u] & ESC) ? 1u << u : 0u;
   }
   uint32_t esc = 0;
-  for (; escm; escm &= escm - 1, ++esc) {   // the full value from the column into the slot of `wide`
-    const uint32_t j = (uint32_t)__builtin_ctz(escm) * BLOCK + tid;
-    const uint32_t kv = s_key[j];
-    const uint32_t r = r0 + s_v16[j];
-    wide[s_tab[(kv >> 16) & 0x7FFFu] + j] = es.val[DIR == DIR_ALL ? r >> 1 : r];
-  }
+  for (; escm; escm &= escm - 1, ++esc) {   // the full value from the column into the record's slot of `wide`
+    const int u = __builtin_ctz(escm);
+    uint32_t ku = 0, ru = 0;
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    esc += __shfl_xor(esc, o, WAVE);
-    ovf += __shfl_xor(ovf, o, WAVE);
-  }
-  if (lane == 0) {
-    if (esc) atomicAdd(n_esc, (unsigned long long)esc);
-    s_ovf[w] = ovf;
+    for (int q = 0; q < ITEMS; ++q) {   // (register arrays indexed by a runtime u would go to scratch)
+      ku = q == u ? kb[q] : ku;
+      ru = q == u ? vr[q] : ru;
+    }
+    const uint32_t g = (uint32_t)(s_run[(ku >> 16) & 0x7FFFu] >> 32) + (ru & 0xFFFFu);
+    wide[g] = es.val[col_index((uint32_t)u * BLOCK + tid)];
   }
   __syncthreads();
-  if (tid == 0) {
-    uint32_t o2 = 0;
-    for (int i = 0; i < BLOCK / WAVE; ++i) o2 += s_ovf[i];
-    if (o2) atomicAdd(&mm[2], (unsigned long long)o2);
-  }
-}
-// Persistent, software-pipelined variant (GS_SPK_PP): one 1024-thread block per CU walks its XCD slot's
-// tiles; the next tile's columns are loaded while this tile ranks, scans, scatters through LDS and
-// stores, so the CU's memory pipe stays busy across the LDS phases (the one-tile-per-block kernel above
-// leaves it idle while a block is in them).  Small tiles (PP_ITEMS records per lane) keep the two tiles'
-// registers under the 128-VGPR budget of 16 waves.  The tile's cursor reservations are issued before the
-// prefetch, so waiting for them does not wait for the next tile's loads (vmcnt counts in order).
-#ifndef GS_SPK_PP
-#define GS_SPK_PP 0
+#pragma unroll
+  for (int u = 0; u < ITEMS; ++u) {
+    const uint64_t e = s_slot[(uint32_t)u * BLOCK + tid];
+#if GS_SPK_ABL_NOSTORE   // timing-only ablation: no record stores (wrong output)
+    if ((uint32_t)e == 0xFFFFFFFFu) rec[0] = (uint32_t)(e >> 32);
+#else
+    rec[(uint32_t)e] = (uint32_t)(e >> 32);
 #endif
-#ifndef GS_PP_ITEMS
-#define GS_PP_ITEMS 8
-#endif
-constexpr int PP_BLOCK = 1024, PP_ITEMS = GS_PP_ITEMS;
-constexpr uint32_t PP_TILE = (uint32_t)PP_BLOCK * PP_ITEMS;
-template <int DIR>
-__host__ __device__ constexpr uint32_t pp_tile_edges() {
-  return DIR == DIR_ALL ? PP_TILE / 2 : PP_TILE;
-}
-
-template <typename V, int DIR>
-__global__ __launch_bounds__(PP_BLOCK) __attribute__((amdgpu_waves_per_eu(4, 4)))
-void k_sp_scatter_pack_pp(BaseSrc<V, DIR, PAY_VAL> es, uint64_t n, int S, uint32_t nbp,
-                          const uint32_t* __restrict__ bucket_start, uint32_t* __restrict__ cursor,
-                          uint32_t* __restrict__ rec, V* __restrict__ wide, uint32_t trash,
-                          unsigned long long* __restrict__ mm, unsigned long long* __restrict__ n_esc) {
-  constexpr int ITEMS = PP_ITEMS, BLOCK = PP_BLOCK;
-  constexpr uint32_t TILE = PP_TILE;
-  constexpr uint32_t ESC = 1u << 31, DUMMY = (uint32_t)BK_MAXB << 16;
-  __shared__ uint32_t s_key[TILE];
-  __shared__ uint16_t s_v16[TILE];
-  __shared__ uint32_t s_tab[BK_MAXB + 1];
-  __shared__ uint32_t s_w[BLOCK / WAVE];
-  __shared__ uint32_t s_ovf[BLOCK / WAVE];
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  constexpr uint32_t TE = pp_tile_edges<DIR>();
-  const uint32_t nfull = (uint32_t)(n / TE);
-  const bool partial = (uint64_t)nfull * TE < n;
-  const uint32_t lmask = (1u << S) - 1;
-  // this block's tiles: slot xs = b & 7 owns full tiles [xs * per, (xs + 1) * per); its nbs blocks take
-  // them round robin (the tiles running at once on one XCD are adjacent); block 0 also takes the
-  // window's partial last tile, as its last one
-  const uint32_t xs = blockIdx.x & 7u, nbs = gridDim.x / 8, jb = blockIdx.x >> 3;
-  const uint32_t per = (nfull + 7) / 8, t_end = min(nfull, (xs + 1) * per);
-  uint32_t t = xs * per + jb;
-  const bool last_partial = blockIdx.x == 0 && partial;
-  if (t >= t_end && !last_partial) return;
-  if (t >= t_end) t = nfull;   // only the partial tile
-  const uint32_t* pre = cursor + SP_NSEG * BK_MAXB;
-  uint32_t* cur = cursor + (SP_NSEG == 1 ? 0u : xs) * BK_MAXB;
-  const uint32_t b0 = 2 * tid, b1 = 2 * tid + 1;
-  const uint32_t bl0 = min(b0, nbp - 1), bl1 = min(b1, nbp - 1);
-  const uint32_t end0 = sp_seg_start(bucket_start[bl0], bucket_start[bl0 + 1], SP_NSEG == 1 ? 1u : xs + 1, pre);
-  const uint32_t end1 = sp_seg_start(bucket_start[bl1], bucket_start[bl1 + 1], SP_NSEG == 1 ? 1u : xs + 1, pre);
-  auto nrec_of = [&](uint32_t tt) -> uint32_t {
-    return tt < nfull ? TILE : (uint32_t)((n - (uint64_t)nfull * TE) * (DIR == DIR_ALL ? 2 : 1));
-  };
-  auto next_of = [&](uint32_t tt) -> uint32_t {   // the tile after tt for this block (~0u: none)
-    if (tt >= nfull) return ~0u;
-    const uint32_t nx = tt + nbs;
-    if (nx < t_end) return nx;
-    return last_partial ? nfull : ~0u;
-  };
-  int64_t kk[ITEMS];
-  V vv[ITEMS];
-  auto load = [&](uint32_t tt, int64_t (&k)[ITEMS], V (&v)[ITEMS]) {   // unconditional, clamped
-    const uint32_t r0 = tt * TILE, nr = nrec_of(tt);
-#pragma unroll
-    for (int u = 0; u < ITEMS; ++u) {
-      const uint32_t r = r0 + min((uint32_t)u * BLOCK + tid, nr - 1);
-      uint32_t i = r;
-      bool rev = DIR == DIR_IN;
-      if constexpr (DIR == DIR_ALL) {
-        i = r >> 1;
-        rev = r & 1u;
-      }
-      k[u] = (rev ? es.dst : es.src)[i];
-      v[u] = es.val[i];
-    }
-  };
-  load(t, kk, vv);
-  uint32_t ovf = 0, esc = 0;
-  for (;;) {
-    const uint32_t nrec = nrec_of(t), r0 = t * TILE, tn = next_of(t);
-    uint32_t kb[ITEMS], vr[ITEMS];
-#pragma unroll
-    for (int u = 0; u < ITEMS; ++u) {
-      const uint32_t j = (uint32_t)u * BLOCK + tid;
-      const uint64_t d = (uint64_t)kk[u] - (uint64_t)es.base;
-      const bool in = (d >> S) < nbp, live = j < nrec;
-      ovf += (live && !in) ? 1u : 0u;
-      const uint32_t nv = pk_narrow(vv[u]);
-      const bool e = nv == PK_ESC;
-      kb[u] = (live && in) ? ((uint32_t)(d >> S) << 16) | ((uint32_t)d & lmask) | (e ? ESC : 0u) : DUMMY;
-      vr[u] = (e ? j : nv) << 16;
-    }
-    for (uint32_t i = tid; i < nbp; i += BLOCK) s_tab[i] = 0;
-    if (tid == 0) s_tab[BK_MAXB] = 0;
-    __syncthreads();
-#pragma unroll
-    for (int u = 0; u < ITEMS; ++u) vr[u] |= atomicAdd(&s_tab[(kb[u] >> 16) & 0x7FFFu], 1u);
-    __syncthreads();
-    const uint32_t c0 = b0 < nbp ? s_tab[b0] : 0u, c1 = b1 < nbp ? s_tab[b1] : 0u;
-    const uint32_t o0 = c0 ? atomicAdd(&cur[b0], c0) : 0u;   // reservations first ...
-    const uint32_t o1 = c1 ? atomicAdd(&cur[b1], c1) : 0u;
-    if (tn != ~0u) load(tn, kk, vv);                           // ... then the next tile's columns
-    uint32_t total;
-    const uint32_t st0 = block_excl_scan<BLOCK>(c0 + c1, s_w, total);
-    __syncthreads();   // every count read before the starts overwrite them
-    s_tab[b0] = st0;
-    s_tab[b1] = st0 + c0;
-    if (tid == 0) s_tab[BK_MAXB] = total;
-    __syncthreads();
-#pragma unroll
-    for (int u = 0; u < ITEMS; ++u) {
-      const uint32_t pos = s_tab[(kb[u] >> 16) & 0x7FFFu] + (vr[u] & 0xFFFFu);
-      s_key[pos] = kb[u];
-      s_v16[pos] = (uint16_t)(vr[u] >> 16);
-    }
-    __syncthreads();
-    const bool drop0 = c0 && o0 + c0 > end0, drop1 = c1 && o1 + c1 > end1;
-    s_tab[b0] = (drop0 ? trash : o0) - st0;
-    s_tab[b1] = (drop1 ? trash : o1) - (st0 + c0);
-    if (tid == 0) s_tab[BK_MAXB] = trash - total;
-    ovf += (drop0 ? 1u : 0u) + (drop1 ? 1u : 0u);
-    __syncthreads();
-    uint32_t escm = 0;
-#pragma unroll
-    for (int u = 0; u < ITEMS; ++u) {
-      const uint32_t j = (uint32_t)u * BLOCK + tid;
-      const uint32_t kv = s_key[j];
-      const bool e = kv & ESC;
-      rec[s_tab[(kv >> 16) & 0x7FFFu] + j] = (kv & 0xFFFFu) | ((e ? PK_ESC : (uint32_t)s_v16[j]) << 16);
-      escm |= e ? 1u << u : 0u;
-    }
-    for (; escm; escm &= escm - 1, ++esc) {
-      const uint32_t j = (uint32_t)__builtin_ctz(escm) * BLOCK + tid;
-      const uint32_t kv = s_key[j];
-      const uint32_t r = r0 + s_v16[j];
-      wide[s_tab[(kv >> 16) & 0x7FFFu] + j] = es.val[DIR == DIR_ALL ? r >> 1 : r];
-    }
-    if (tn == ~0u) break;
-    t = tn;
-    __syncthreads();   // the store phase's reads of s_tab / s_key before the next tile rewrites them
   }
+#endif
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
     esc += __shfl_xor(esc, o, WAVE);
@@ -1704,24 +1577,52 @@ __global__ __launch_bounds__(BK_ACC_BLOCK) void k_bk_accum(Src src, const BkItem
       if (r0 + tid < a0) add1(r0 + tid, src.rec[r0 + tid]);
       const uint4* rec4 = reinterpret_cast<const uint4*>(src.rec);
       constexpr int U4 = UNROLL / 2 > 0 ? UNROLL / 2 : 1;
-      for (uint32_t q4 = a0 / 4 + tid; q4 < a1 / 4; q4 += BK_ACC_BLOCK * U4) {
-        uint4 x[U4];
+      constexpr uint32_t STEP = BK_ACC_BLOCK * U4;
+      const uint32_t q_end = a1 / 4;
+      auto load4 = [&](uint4 (&x)[U4], uint32_t q4) {   // unconditional, clamped: see k_dp_hist
 #pragma unroll
         for (int u = 0; u < U4; ++u) {
           const uint32_t qq = q4 + (uint32_t)u * BK_ACC_BLOCK;
-          x[u] = rec4[qq < a1 / 4 ? qq : a1 / 4 - 1];   // unconditional: see k_dp_hist
+          x[u] = rec4[qq < q_end ? qq : q_end - 1];
         }
+      };
+      auto add4 = [&](const uint4 (&x)[U4], uint32_t q4) {
 #pragma unroll
         for (int u = 0; u < U4; ++u) {
           const uint32_t qq = q4 + (uint32_t)u * BK_ACC_BLOCK;
-          if (qq < a1 / 4) {
+          if (qq < q_end) {
             add1(4 * qq, x[u].x);
             add1(4 * qq + 1, x[u].y);
             add1(4 * qq + 2, x[u].z);
             add1(4 * qq + 3, x[u].w);
           }
         }
+      };
+#if GS_BK_PIPE
+      // software-pipelined: the next group's 16-byte loads are in flight while this group's records go
+      // into LDS (one group at a time left the loads and the LDS atomics each about half busy)
+      uint32_t q4 = a0 / 4 + tid;
+      if (a0 / 4 < q_end) {
+        uint4 x[U4], y[U4];
+        load4(x, q4);
+        for (;;) {   // (the loads are unconditional: a conditional load makes hipcc wait vmcnt(0) after it)
+          load4(y, q4 + STEP);
+          add4(x, q4);
+          q4 += STEP;
+          if (q4 >= q_end) break;
+          load4(x, q4 + STEP);
+          add4(y, q4);
+          q4 += STEP;
+          if (q4 >= q_end) break;
+        }
       }
+#else
+      for (uint32_t q4 = a0 / 4 + tid; q4 < q_end; q4 += STEP) {
+        uint4 x[U4];
+        load4(x, q4);
+        add4(x, q4);
+      }
+#endif
       if (a1 + tid < r1) add1(a1 + tid, src.rec[a1 + tid]);
     } else {
       for (uint32_t r = r0 + tid; r < r1; r += BK_ACC_BLOCK * UNROLL) {
