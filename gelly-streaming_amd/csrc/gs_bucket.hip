@@ -156,7 +156,7 @@ gs_status launch_plan(gs_ctx* c, uint64_t R, uint32_t nb, int passes, int w, uin
   uint32_t* ns = (uint32_t*)(sm + SM_BK_N);
   BkPlanOut po{meta + BkMeta::DBASE, meta + BkMeta::BSTART, meta + BkMeta::BCOUNT, meta + BkMeta::BITEMS,
                meta + BkMeta::BSLAB, meta + BkMeta::MLIST, c->bk_items.as<BkItem>(), ns + 0, ns + 1,
-               cursor, counts_out, occupied};
+               cursor, counts_out, occupied, ns + 2};
   hipLaunchKernelGGL(k_bk_plan, dim3(1), dim3(BK_PLAN_BLOCK), 0, c->stream, meta + BkMeta::HIST, nb, passes, w,
                      item_recs, po);
   return hip_check(c, hipGetLastError(), "k_bk_plan");
@@ -175,7 +175,6 @@ gs_status bucket_accumulate(gs_ctx* c, Src rs, uint64_t R, uint32_t nb, int64_t 
   uint32_t* meta = c->bk_meta.as<uint32_t>();
   uint32_t* ns = (uint32_t*)(sm + SM_BK_N);
   const auto* mm = (const unsigned long long*)(sm + SM_BK_MM);
-  GS_HIP(hipMemsetAsync(ns + 2, 0, 4, c->stream));
   BkStage st{c->keysA.as<uint32_t>(), c->valsA.p,
              (std::is_same_v<P, BkDeg> || std::is_same_v<P, BkDeg32>) ? c->aux.as<int64_t>() : nullptr};
   auto* slabs = c->bk_slabs.as<typename P::Lds>();
@@ -193,13 +192,13 @@ gs_status bucket_accumulate(gs_ctx* c, Src rs, uint64_t R, uint32_t nb, int64_t 
   GS_HIP(hipGetLastError());
   hipEventRecord(c->pass_ev[ev0 + 2], c->stream);
   hipLaunchKernelGGL((k_bk_emit<P>), dim3(nb), dim3(256), 0, c->stream, meta + BkMeta::BSTART, meta + BkMeta::BCOUNT,
-                     nb, st, base, o, (unsigned long long*)(sm + SM_BK_MM + 24), mm);
+                     nb, st, base, o, (unsigned long long*)(sm + SM_BK_MM + 24), mm, (const uint32_t*)(sm + SM_TIMEOUT),
+                     (const unsigned long long*)(sm + SM_BK_ESC), (unsigned long long*)(sm + SM_BK_X));
   GS_HIP(hipGetLastError());
   hipEventRecord(c->pass_ev[ev0 + 3], c->stream);
   hipEventRecord(c->ev[3], c->stream);
-  GS_HIP(hipMemcpyAsync(c->host_small, sm + SM_BK_MM, 48, hipMemcpyDeviceToHost, c->stream));
-  GS_HIP(hipMemcpyAsync(c->host_small + 6, sm + SM_TIMEOUT, 8, hipMemcpyDeviceToHost, c->stream));
-  GS_HIP(hipMemcpyAsync(c->host_small + 7, sm + SM_BK_ESC, 8, hipMemcpyDeviceToHost, c->stream));
+  static_assert(SM_BK_N == SM_BK_MM + 32 && SM_BK_X == SM_BK_MM + 48, "one read-back block");
+  GS_HIP(hipMemcpyAsync(c->host_small, sm + SM_BK_MM, 64, hipMemcpyDeviceToHost, c->stream));
   return GS_OK;
 }
 
@@ -328,8 +327,8 @@ gs_status bucket_direct_t(gs_ctx* c, const int64_t* src, const int64_t* dst, con
           slots.pre[SP_NSEG] = (uint32_t)acc;   // == R
         }
         hipLaunchKernelGGL(k_sp_regions, dim3(1), dim3(BK_PLAN_BLOCK), 0, c->stream, (const uint32_t*)sp.tot.as<uint32_t>(),
-                           nb, sp.R, R, meta + BkMeta::BSTART, c->sp_cur.as<uint32_t>(), slots, mm);
-        GS_HIP(hipMemsetAsync(sm + SM_BK_ESC, 0, 8, c->stream));
+                           nb, sp.R, R, meta + BkMeta::BSTART, c->sp_cur.as<uint32_t>(), slots, mm,
+                           (unsigned long long*)(sm + SM_BK_ESC));
         if constexpr (P::REL) GS_HIP(hipMemsetAsync(rel_bad, 0, 4, c->stream));
         hipEventRecord(c->ev[1], c->stream);
         hipEventRecord(c->pass_ev[0], c->stream);

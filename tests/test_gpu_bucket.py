@@ -368,3 +368,29 @@ def test_packed_integer_sum_wraps_to_zero(pkg, oracle, spec):
             t = e.stage_times()
             assert t.path == 2 and t.packed
             _check(gk, gv, rk, rv, np.int32, 0)
+
+
+@pytest.mark.parametrize("op", [0, 1, 2])
+def test_packed_presence_of_zero_and_escaped_only_vertices(pkg, oracle, op):
+    """k_bk_accum's packed fast path takes 4 narrow, non-zero records with LDS atomics alone; a vertex
+    seen only through zero values (SUM: the accumulator stays at its identity) or only through escaped
+    values must still be emitted -- isolated, and mixed into groups of 4 with common records, through the
+    histogram path and the speculative partition."""
+    rng = np.random.default_rng(555 + op)
+    n = 200_000
+    with pkg.Engine(0) as e:
+        for w in range(4):
+            s, d = _window(rng, n, 1 << 16)   # ~3 records per vertex
+            v = rng.integers(1, 0xFFFF, n).astype(np.int64)
+            zero_v = rng.choice(1 << 16, 300, replace=False)
+            for j, x in enumerate(zero_v):   # vertices whose every record is 0 (first 150) or escaped
+                m = s == x
+                v[m] = 0 if j < 150 else -(1 << 40) - j
+            v[rng.random(n) < 0.0005] = 0      # and scattered zeros / escapes among common records
+            v[rng.random(n) < 0.0005] = 1 << 33
+            rk, rv = oracle.window_reduce(s, d, v, 1, op)
+            gk, gv = e.reduce(*_dev(s, d, v), 1, op)
+            t = e.stage_times()
+            assert t.path == 2 and t.packed
+            assert t.speculative == (0 if w == 0 else 1)
+            _check(gk, gv, rk, rv, np.int64, op)
