@@ -746,6 +746,8 @@ def main():
     pmc_window = None
     if a.workload == "reduce" and world == 1 and all(n in pmc for n in kt if kt[n]["bytes"]):
         pmc_window = sum(pmc[n]["bytes_per_launch"] for n in kt if n in pmc)
+        if "bucket_merge" in kt:   # the merge stage's time covers k_bk_merge_slices + k_bk_merge
+            pmc_window += pmc.get("k_bk_merge_slices", {}).get("bytes_per_launch", 0)
     window_gbs = B / (ms_step * 1e-3) / 1e9 / world
     roofline = {"bound": "hbm", "kernel": dom_name,
                 "achieved": round(B / (dom["ms"] * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",

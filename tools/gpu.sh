@@ -5,6 +5,7 @@
 #   bench   TAG [bench args]    one bench.py line -> gpurun_out/TAG/bench.json
 #   c2      TAG                 the C2 headline: bench line (+ cpu_baseline), rocprofv3 kernel-trace stats of
 #                               the same command, FETCH_SIZE / WRITE_SIZE passes -> pmc_traffic.json
+#   c2pmc   TAG                 only the FETCH_SIZE / WRITE_SIZE passes of c2
 #   sq      TAG [bench args]    SQ counter passes (LDS conflicts, waits, instruction mix) over a short bench
 #   tri     TAG SCALE           triangles: bench line, kernel-trace stats, FETCH / TCC hit / SQ passes
 #   evidence TAG                every secondary bench line DESIGN.md quotes
@@ -21,7 +22,7 @@ PYTEST="python -u -m pytest -x -v --timeout 120 --timeout-method thread"
 bench() { local name=$1; shift; timeout -k 10 300 python3 bench.py "$@" > "$O/$name.json" 2> "$O/$name.err"; echo "$name done"; }
 trace() { local name=$1; shift; timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$O/$name" -o run --output-format csv \
             -- python3 bench.py "$@" --no-cpu-baseline > "$O/$name.log" 2>&1; echo "$name done"; }
-pmc() { local name=$1 counters=$2; shift 2; timeout -s KILL 150 rocprofv3 --pmc $counters -d "$O/$name" -o run \
+pmc() { local name=$1 counters=$2; shift 2; mkdir -p "$(dirname "$O/$name")"; timeout -s KILL 150 rocprofv3 --pmc $counters -d "$O/$name" -o run \
           --output-format csv -- python3 bench.py "$@" --no-cpu-baseline > "$O/$name.log" 2>&1; echo "$name done"; }
 
 case $MODE in
@@ -33,6 +34,8 @@ case $MODE in
   c2)
     bench bench_c2_i64
     trace trace_c2
+    ;&
+  c2pmc)
     pmc pmc/fetch FETCH_SIZE --steps 3 --warmup 2
     pmc pmc/write WRITE_SIZE --steps 3 --warmup 2
     python3 tools/pmc_traffic.py "$O/pmc" -o "$O/pmc_traffic.json" ;;
