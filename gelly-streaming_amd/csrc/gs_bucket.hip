@@ -125,9 +125,12 @@ void choose_passes(uint32_t nb, int* passes, int* w) {
   else { *passes = 2; *w = 6; }
 }
 
-// records per accumulation work item: about four items per CU, at least 2^14 records
+// records per accumulation work item: about GS_BK_ITEMS_PER_CU items per CU, at least 2^14 records
+#ifndef GS_BK_ITEMS_PER_CU
+#define GS_BK_ITEMS_PER_CU 3   // C2 (ms, one box): 4 items 1.712, 3 items 1.662 (fewer multi-item buckets: merge 0.066 -> 0.029), 2 items 1.685, 6 items 1.785
+#endif
 uint32_t item_records(gs_ctx* c, uint64_t R) {
-  const uint64_t per = R / (4 * (uint64_t)std::max(1, c->n_cu));
+  const uint64_t per = R / (GS_BK_ITEMS_PER_CU * (uint64_t)std::max(1, c->n_cu));
   return (uint32_t)std::max<uint64_t>(BK_ITEM, std::min<uint64_t>(per, 1u << 20));
 }
 

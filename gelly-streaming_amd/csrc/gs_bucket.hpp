@@ -82,17 +82,26 @@ constexpr uint32_t SP_NSEG = GS_SP_XCD ? 8 : 1;
 constexpr uint32_t SP_PAD = 1024;                  // absolute slack per bucket
 constexpr uint32_t SP_PADSEG = SP_PAD / SP_NSEG;   // ... per segment
 static_assert(SP_PADSEG % 4 == 0, "segment starts stay 4-aligned");
-// the cursor buffer: SP_NSEG x BK_MAXB cursors | pre[SP_NSEG + 1] | SP_NSEG x BK_MAXB segment ends
-constexpr uint32_t SP_END_OFF = SP_NSEG * BK_MAXB + 16;
-constexpr uint32_t SP_CUR_WORDS = SP_END_OFF + SP_NSEG * BK_MAXB;
+// the cursor buffer: SP_NSEG x BK_MAXB cursors | SP_NSEG x BK_MAXB segment ends | ... starts.  k_sp_regions
+// writes all three; the later kernels read segment bounds from the tables (no division in their loops).
+constexpr uint32_t SP_END_OFF = SP_NSEG * BK_MAXB;
+constexpr uint32_t SP_LO_OFF = 2 * SP_NSEG * BK_MAXB;
+constexpr uint32_t SP_CUR_WORDS = 3 * SP_NSEG * BK_MAXB;
+__device__ __forceinline__ uint32_t sp_lo(const uint32_t* cur, uint32_t x, uint32_t b) {
+  return cur[SP_LO_OFF + x * BK_MAXB + b];
+}
+__device__ __forceinline__ uint32_t sp_hi(const uint32_t* cur, uint32_t x, uint32_t b) {
+  return cur[SP_END_OFF + x * BK_MAXB + b];
+}
 struct SpSlots {
   uint32_t pre[SP_NSEG + 1];
 };
-__host__ __device__ inline uint32_t sp_seg_start(uint32_t s, uint32_t e, uint32_t x, const uint32_t* pre) {
+// frac[x] = pre[x] / pre[SP_NSEG] in 0.32 fixed point (non-decreasing in x; k_sp_regions)
+__device__ inline uint32_t sp_seg_start(uint32_t s, uint32_t e, uint32_t x, const uint32_t* frac) {
   if (x == 0) return s;
   if (x >= SP_NSEG) return e;
   const uint32_t T = e - s - SP_NSEG * SP_PADSEG;
-  return s + ((uint32_t)((uint64_t)T * pre[x] / (pre[SP_NSEG] ? pre[SP_NSEG] : 1)) & ~3u) + x * SP_PADSEG;
+  return s + ((uint32_t)(((uint64_t)T * frac[x]) >> 32) & ~3u) + x * SP_PADSEG;
 }
 
 // ---- policies: LDS accumulator layout and the op ------------------------------------------------
@@ -523,11 +532,8 @@ static __global__ __launch_bounds__(BK_PLAN_BLOCK) void k_bk_plan(const uint32_t
   auto count = [&](uint32_t b) -> uint32_t {
     if (b >= nb) return 0u;
     if (!spec) return hist[b];
-    const uint32_t s0 = o.bucket_start[b], e0 = o.bucket_start[b + 1];
-    const uint32_t* pre = o.cursor + SP_NSEG * BK_MAXB;
     uint32_t n = 0;
-    for (uint32_t x = 0; x < SP_NSEG; ++x)
-      n += min(o.cursor[x * BK_MAXB + b], sp_seg_start(s0, e0, x + 1, pre)) - sp_seg_start(s0, e0, x, pre);
+    for (uint32_t x = 0; x < SP_NSEG; ++x) n += min(o.cursor[x * BK_MAXB + b], sp_hi(o.cursor, x, b)) - sp_lo(o.cursor, x, b);
     return n;
   };
   const uint32_t c0 = count(b0), c1 = count(b1);
@@ -1085,8 +1091,14 @@ static __global__ __launch_bounds__(BK_PLAN_BLOCK) void k_sp_regions(const uint3
                                                                      unsigned long long* __restrict__ mm,
                                                                      unsigned long long* __restrict__ n_esc) {
   __shared__ uint32_t s_w[BK_PLAN_BLOCK / WAVE];
+  __shared__ uint32_t s_frac[SP_NSEG + 1];
   const int tid = threadIdx.x;
   const uint32_t b0 = 2 * tid, b1 = 2 * tid + 1;   // BK_MAXB = 2 * BK_PLAN_BLOCK
+  if (tid <= (int)SP_NSEG) {   // each slot's share of the records (visible after the scan's barrier)
+    const uint32_t all = slots.pre[SP_NSEG];
+    const uint64_t f = all ? ((uint64_t)slots.pre[tid] << 32) / all : 0;
+    s_frac[tid] = (uint32_t)min(f, (uint64_t)0xFFFFFFFFu);
+  }
   auto cap = [&](uint32_t b) -> uint32_t {
     if (b >= nb) return 0u;
     const uint64_t t = (uint64_t)prev[b] * r_now / (r_prev ? r_prev : 1);
@@ -1097,15 +1109,22 @@ static __global__ __launch_bounds__(BK_PLAN_BLOCK) void k_sp_regions(const uint3
   const uint32_t s0 = bk_block_scan(c0 + c1, s_w, total);
   if (b0 < nb) bucket_start[b0] = s0;
   if (b1 < nb) bucket_start[b1] = s0 + c0;
+  // segment x of bucket b: [lo, hi); its cursor starts at lo
+  uint32_t l0 = s0, l1 = s0 + c0;
   for (uint32_t x = 0; x < SP_NSEG; ++x) {
-    if (b0 < nb) cursor[x * BK_MAXB + b0] = sp_seg_start(s0, s0 + c0, x, slots.pre);
-    if (b1 < nb) cursor[x * BK_MAXB + b1] = sp_seg_start(s0 + c0, s0 + c0 + c1, x, slots.pre);
-  }
-  if (tid <= (int)SP_NSEG) cursor[SP_NSEG * BK_MAXB + tid] = slots.pre[tid];   // for the later kernels
-  uint32_t* seg_end = cursor + SP_END_OFF;   // segment ends: the scatter's overflow test without a division
-  for (uint32_t x = 0; x < SP_NSEG; ++x) {
-    if (b0 < nb) seg_end[x * BK_MAXB + b0] = sp_seg_start(s0, s0 + c0, x + 1, slots.pre);
-    if (b1 < nb) seg_end[x * BK_MAXB + b1] = sp_seg_start(s0 + c0, s0 + c0 + c1, x + 1, slots.pre);
+    const uint32_t h0 = sp_seg_start(s0, s0 + c0, x + 1, s_frac), h1 = sp_seg_start(s0 + c0, s0 + c0 + c1, x + 1, s_frac);
+    if (b0 < nb) {
+      cursor[x * BK_MAXB + b0] = l0;
+      cursor[SP_LO_OFF + x * BK_MAXB + b0] = l0;
+      cursor[SP_END_OFF + x * BK_MAXB + b0] = h0;
+    }
+    if (b1 < nb) {
+      cursor[x * BK_MAXB + b1] = l1;
+      cursor[SP_LO_OFF + x * BK_MAXB + b1] = l1;
+      cursor[SP_END_OFF + x * BK_MAXB + b1] = h1;
+    }
+    l0 = h0;
+    l1 = h1;
   }
   if (tid == 0) bucket_start[nb] = total;
   if (tid < 4) mm[tid] = 0;
@@ -1427,9 +1446,7 @@ __global__ __launch_bounds__(DP_BLOCK) void k_sp_scatter(BaseSrc<V, DIR, PAY> es
   }
   const uint32_t r0 = t * TILE;
   const uint32_t xs = SP_NSEG == 1 ? 0u : blockIdx.x & 7u;
-  const uint32_t* pre = cursor + SP_NSEG * BK_MAXB;
-  const uint32_t end0 = sp_seg_start(bucket_start[bl0], bucket_start[bl0 + 1], xs + 1, pre);
-  const uint32_t end1 = sp_seg_start(bucket_start[bl1], bucket_start[bl1 + 1], xs + 1, pre);
+  const uint32_t end0 = sp_hi(cursor, xs, bl0), end1 = sp_hi(cursor, xs, bl1);
   cursor += xs * BK_MAXB;
   int64_t kk[DP_ITEMS];
   V vv[DP_ITEMS];
@@ -1688,12 +1705,10 @@ __global__ __launch_bounds__(BK_ACC_BLOCK) void k_bk_accum(Src src, const BkItem
     if (!seg_cur) {
       range(b0 + m.begin, b0 + m.end);
     } else {   // speculative partition: the item's span of the bucket's SP_NSEG segments, in order
-      const uint32_t e0 = bucket_start[m.bucket + 1];
-      const uint32_t* pre = seg_cur + SP_NSEG * BK_MAXB;
       uint32_t at = 0;   // records of the bucket in the segments before x
       for (uint32_t x = 0; x < SP_NSEG && at < m.end; ++x) {
-        const uint32_t sg = sp_seg_start(b0, e0, x, pre);
-        const uint32_t nx = min(seg_cur[x * BK_MAXB + m.bucket], sp_seg_start(b0, e0, x + 1, pre)) - sg;
+        const uint32_t sg = sp_lo(seg_cur, x, m.bucket);
+        const uint32_t nx = min(seg_cur[x * BK_MAXB + m.bucket], sp_hi(seg_cur, x, m.bucket)) - sg;
         const uint32_t lo = max(m.begin, at), hi = min(m.end, at + nx);
         if (lo < hi) range(sg + (lo - at), sg + (hi - at));
         at += nx;
