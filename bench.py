@@ -66,10 +66,13 @@ def parse():
                         "default) or torch.distributed around the partials / merge halves (A/B)")
     p.add_argument("--check", action="store_true",
                    help="after timing: sum(per-vertex sums) == sum(values) and ascending keys on each window")
+    p.add_argument("--chunk-records", type=float, default=2 ** 28,
+                   help="cand_stream: records per gs_candidates_next chunk")
     p.add_argument("--windows-edges", type=float, default=1e8,
                    help="apply (C5): edges per 1000 ms window of the continuous stream")
     p.add_argument("--workload", default="reduce",
-                   choices=["reduce", "fold", "triangles", "cc", "c1", "apply", "candidates", "parse", "e2e"],
+                   choices=["reduce", "fold", "triangles", "cc", "c1", "apply", "candidates", "cand_stream", "parse",
+                            "e2e"],
                    help="reduce = C2 (default, the headline); fold = C3 degree/max on skewed R-MAT; "
                         "triangles = WindowTriangles on an R-MAT window without self-loops (C4 shape); "
                         "cc = ConnectedComponents of an R-MAT window (SURVEY.md §8f#4)")
@@ -416,6 +419,71 @@ def window_stream_main(a):
     eng.close()
 
 
+def cand_stream_main(a):
+    """C5 emission at full size (WindowTriangles.java:91-114): every GenerateCandidateEdges
+    record of one 1e8-edge R-MAT scale-23 window, streamed in chunks of --chunk-records through
+    gs_candidates_begin / gs_candidates_next (the whole window needs ~1.6e11 records, 2.7 TB, which no
+    single buffer holds).  Each chunk is consumed on the device by the stand-in of a downstream operator:
+    the count of candidate records (is_candidate = 1) and an order-sensitive checksum of (a, b), so every
+    record is read once after it is written.  Reports records/s over the whole window, chunk latency
+    p50 / p99, and checks that the chunks add up to gs_candidates_begin's total."""
+    torch.cuda.set_device(0)
+    pkg = ge.load_package()
+    eng = pkg.Engine(0)
+    E = int(a.windows_edges)
+    src, dst = eng.generate_rmat(23, E, 0x5EED05)
+    cap = int(a.chunk_records)
+    bufs = (torch.empty(cap, dtype=torch.int64, device="cuda"), torch.empty(cap, dtype=torch.int64, device="cuda"),
+            torch.empty(cap, dtype=torch.uint8, device="cuda"))
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    total = eng.candidates_begin(src, dst)
+    torch.cuda.synchronize()
+    t_begin = time.perf_counter() - t0
+    lat, got, cands = [], 0, 0
+    chk = torch.zeros((), dtype=torch.int64, device="cuda")
+    t1 = time.perf_counter()
+    last_beat = t1
+    while True:
+        tt = time.perf_counter()
+        ca, cb, cf, first, done = eng.candidates_next(cap, bufs)
+        assert first == got, (first, got)
+        n = int(ca.numel())
+        cands += int(cf.sum())
+        chk = chk * 1000003 + (ca * 31 + cb).sum()   # consumes every record (wrapping int64)
+        torch.cuda.synchronize()
+        lat.append(time.perf_counter() - tt)
+        got += n
+        if time.perf_counter() - last_beat > 30:
+            print(f"# cand_stream: {got / total:.1%} of {total} records", file=sys.stderr, flush=True)
+            last_beat = time.perf_counter()
+        if done:
+            break
+    t_stream = time.perf_counter() - t1
+    assert got == total, (got, total)
+    elapsed = t_begin + t_stream
+    lat_ms = np.array(lat) * 1e3
+    line = {"metric": "candidate records/s (GenerateCandidateEdges, chunked emission)", "value": total / elapsed,
+            "unit": "records/s", "n_gpus": 1, "steps": 1, "warmup": 0, "ms_per_step": elapsed * 1e3,
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "int64",
+            "data": "synthetic R-MAT scale 23, seeded, generated on device",
+            "config": {"workload": f"C5 emission: every GenerateCandidateEdges record of one {E:.3g}-edge R-MAT "
+                                   f"scale-23 window (slice(ALL)), in chunks of {cap} records, each consumed on "
+                                   f"the device (candidate count + checksum)",
+                       "edges_per_window": E, "records": total, "candidate_records": cands,
+                       "chunks": len(lat), "chunk_records": cap, "begin_ms": t_begin * 1e3,
+                       "chunk_latency_ms_p50": float(np.percentile(lat_ms, 50)),
+                       "chunk_latency_ms_p99": float(np.percentile(lat_ms, 99)),
+                       "window_s": elapsed, "checksum": int(chk.item()), "parallelism": "1 GPU"},
+            "roofline": {"bound": "hbm", "kernel": "whole window (emission + consumer)",
+                         "achieved": round(17 * total / elapsed / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(17 * total / elapsed / 1e9 / HBM_PEAK_GBS, 4), "traffic": None,
+                         "algorithmic_bytes_per_launch": 17 * total, "avg_launch_ms": elapsed * 1e3},
+            "cpu_baseline": None}
+    print(json.dumps(line), flush=True)
+    eng.close()
+
+
 def parse_main(a):
     """Input path: the examples' "src trg ts" edge text (WindowTriangles.java:175-185)
     parsed on the GPU (gs_parse_edges_text) from text resident in HBM: R-MAT scale-24 edges with
@@ -581,6 +649,8 @@ def main():
         return e2e_main(a)
     if a.workload in ("c1", "apply", "candidates"):
         return window_stream_main(a)
+    if a.workload == "cand_stream":
+        return cand_stream_main(a)
     if a.workload == "parse":
         return parse_main(a)
     world = int(os.environ.get("WORLD_SIZE", "1"))

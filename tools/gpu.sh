@@ -61,6 +61,7 @@ case $MODE in
     bench bench_c1 --workload c1
     bench bench_apply --workload apply
     bench bench_candidates --workload candidates
+    bench bench_cand_stream --workload cand_stream
     bench bench_parse --workload parse
     bench bench_e2e_direct --workload e2e --staging direct --no-cpu-baseline
     bench bench_e2e_pinned --workload e2e --staging pinned --no-cpu-baseline
