@@ -31,6 +31,12 @@ namespace gs {
 
 constexpr int BK_MAXB = 2048;          // buckets (the bucket index has <= 11 bits)
 constexpr int BK_INFO_BLOCK = 512;
+#ifndef GS_ACC_ABL_NOLOAD
+#define GS_ACC_ABL_NOLOAD 0
+#endif
+#ifndef GS_ACC_ABL_NOATOM
+#define GS_ACC_ABL_NOATOM 0
+#endif
 #ifndef GS_BK_PIPE
 #define GS_BK_PIPE 0   // k_bk_accum (packed records), A/B: next group's loads in flight during this group's atomics (C2 accumulate 0.345 vs 0.331 ms: off)
 #endif
@@ -1167,6 +1173,9 @@ __host__ __device__ inline uint64_t sp_capacity(uint64_t r_now, uint32_t nb) {
 #ifndef GS_SPK_ABL_NOSTORE
 #define GS_SPK_ABL_NOSTORE 0
 #endif
+#ifndef GS_SPK_NT
+#define GS_SPK_NT 0
+#endif
 #ifndef GS_SPK_LATE
 #define GS_SPK_LATE 0   // 1: run deltas written after the LDS scatter (the reservations' latency hides behind it)
 #endif
@@ -1267,6 +1276,9 @@ void k_sp_scatter_pack(BaseSrc<V, DIR, PAY_VAL> es, uint64_t n, int S, uint32_t 
     kk[u] = (int64_t)((uint64_t)es.base + (((uint64_t)(i * 2654435761u) * ((uint64_t)nbp << S)) >> 32));
     vv[u] = (V)(i & 0x3FFF);
     (void)rev;
+#elif GS_SPK_NT   // A/B: the columns are read once: non-temporal loads
+    kk[u] = __builtin_nontemporal_load(&(rev ? es.dst : es.src)[i]);
+    vv[u] = __builtin_nontemporal_load(&es.val[i]);
 #else
     kk[u] = (rev ? es.dst : es.src)[i];
     vv[u] = es.val[i];
@@ -1623,7 +1635,13 @@ __global__ __launch_bounds__(BK_ACC_BLOCK) void k_bk_accum(Src src, const BkItem
 #pragma unroll
         for (int u = 0; u < U4; ++u) {
           const uint32_t qq = q4 + (uint32_t)u * BK_ACC_BLOCK;
+#if GS_ACC_ABL_NOLOAD   // timing-only ablation: synthetic narrow records, no partition reads (wrong output)
+          const uint32_t h = (qq * 2654435761u) >> 8;
+          x[u] = make_uint4((h & 0x3FFF) | 0x10000u, ((h >> 3) & 0x3FFF) | 0x20000u, ((h >> 6) & 0x3FFF) | 0x30000u,
+                            ((h >> 9) & 0x3FFF) | 0x40000u);
+#else
           x[u] = rec4[qq < q_end ? qq : q_end - 1];
+#endif
         }
       };
       auto add4 = [&](const uint4 (&x)[U4], uint32_t q4) {
@@ -1639,12 +1657,21 @@ __global__ __launch_bounds__(BK_ACC_BLOCK) void k_bk_accum(Src src, const BkItem
             bool rare = (h0 == PK_ESC) | (h1 == PK_ESC) | (h2 == PK_ESC) | (h3 == PK_ESC);
             if constexpr (P::OP_IS_SUM) rare |= (h0 == 0u) | (h1 == 0u) | (h2 == 0u) | (h3 == 0u);
             if (qq < q_end) {
+#if GS_ACC_ABL_NOATOM   // timing-only ablation: no LDS atomics (wrong output)
               if (!rare) {
+                if ((h0 ^ h1 ^ h2 ^ h3 ^ x[u].x ^ x[u].y ^ x[u].z ^ x[u].w) == 0x9E3779B9u) P::add_narrow(s, 0, h0);
+              } else
+#else
+              if (!rare) {
+#endif
+#if !GS_ACC_ABL_NOATOM
                 P::add_narrow(s, x[u].x & (P::W - 1), h0);
                 P::add_narrow(s, x[u].y & (P::W - 1), h1);
                 P::add_narrow(s, x[u].z & (P::W - 1), h2);
                 P::add_narrow(s, x[u].w & (P::W - 1), h3);
-              } else {
+              } else
+#endif
+              {
                 add1(4 * qq, x[u].x);
                 add1(4 * qq + 1, x[u].y);
                 add1(4 * qq + 2, x[u].z);

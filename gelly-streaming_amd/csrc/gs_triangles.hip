@@ -624,7 +624,23 @@ gs_status tri_count(gs_ctx* c, uint32_t B, size_t V, uint64_t M, const uint32_t*
   GS_HIP(hipMemcpyAsync(c->host_small + 6, d_nheavy, 4, hipMemcpyDeviceToHost, c->stream));
   GS_TRY(host_wait(c));
   const uint32_t nh = (uint32_t)c->host_small[6];
-  if (nh) {
+  if (nh && GS_TH_PHASED) {   // items in phase order, claimed one at a time
+    GS_TRY(ensure(c, c->tri_hwork, (size_t)nh * 4 + (TH_PHASES + 64) * 4));
+    uint32_t* hist = c->tri_hwork.as<uint32_t>();
+    uint32_t* claim = hist + TH_PHASES;
+    uint32_t* order = hist + TH_PHASES + 64;
+    GS_HIP(hipMemsetAsync(hist, 0, (TH_PHASES + 1) * 4, c->stream));
+    const unsigned g = (unsigned)std::min<uint64_t>((nh + 255) / 256, 4096);
+    hipLaunchKernelGGL(k_tri_hphase_count, dim3(g), dim3(256), 0, c->stream, sfx, in_range, c->tri_heavy.as<uint2>(),
+                       nh, (uint32_t)M, hist);
+    hipLaunchKernelGGL(k_tri_hphase_scan, dim3(1), dim3(256), 0, c->stream, hist);
+    hipLaunchKernelGGL(k_tri_hphase_place, dim3(g), dim3(256), 0, c->stream, sfx, in_range, c->tri_heavy.as<uint2>(),
+                       nh, (uint32_t)M, hist, order);
+    hipLaunchKernelGGL(k_tri_heavy, dim3(GS_TH_HGRID), dim3(TH_HBLOCK), 0, c->stream, nbr, sfx, out_range, in_range,
+                       c->tri_heavy.as<uint2>(), d_nheavy, nullptr, (const uint32_t*)order, claim, d_total, d_probes,
+                       nb_cap, d_err);
+    GS_HIP(hipGetLastError());
+  } else if (nh) {
     GS_TRY(ensure(c, c->tri_hwork, (size_t)nh * 16 + 8));
     unsigned long long* hw = c->tri_hwork.as<unsigned long long>();
     hipLaunchKernelGGL(k_tri_hwork, dim3((unsigned)std::min<uint64_t>((nh + 3) / 4, 16384)), dim3(256), 0, c->stream,
@@ -632,8 +648,8 @@ gs_status tri_count(gs_ctx* c, uint32_t B, size_t V, uint64_t M, const uint32_t*
     GS_HIP(hipGetLastError());
     GS_TRY(xscan(c, (const uint64_t*)hw, nh, (uint64_t*)hw + nh));
     hipLaunchKernelGGL(k_tri_heavy, dim3(GS_TH_HGRID), dim3(TH_HBLOCK), 0, c->stream, nbr, sfx, out_range, in_range,
-                       c->tri_heavy.as<uint2>(), d_nheavy, (const unsigned long long*)hw + nh, d_total, d_probes,
-                       nb_cap, d_err);
+                       c->tri_heavy.as<uint2>(), d_nheavy, (const unsigned long long*)hw + nh, nullptr, nullptr,
+                       d_total, d_probes, nb_cap, d_err);
     GS_HIP(hipGetLastError());
   }
   hipEventRecord(c->ev[3], c->stream);

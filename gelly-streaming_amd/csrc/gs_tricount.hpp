@@ -387,6 +387,43 @@ __global__ __launch_bounds__(256) void k_tri_hwork(const uint2* __restrict__ sfx
   }
 }
 
+// Phased order of the heavy items (GS_TH_PHASED): an item (v, in-chunk) gathers the suffixes of N+(u) for
+// the chunk's in-neighbours u, whose out-lists lie in one stretch of onbr (in-lists are in u order).  The
+// heavy vertices' items run at once, so in equal-work order the chip gathers from all of onbr (4 GB at
+// R-MAT s26: HBM, 7 % L2 hits).  Ordered by that stretch (TH_PHASES phases of onbr) and claimed in order,
+// the items in flight gather from a few phases' out-lists, which the Infinity Cache / L2 keep.
+#ifndef GS_TH_PHASED
+#define GS_TH_PHASED 1
+#endif
+constexpr uint32_t TH_PHASES = 256;
+__device__ __forceinline__ uint32_t th_phase(const uint2* __restrict__ sfx, const uint2* __restrict__ in_range, uint2 item,
+                                             uint32_t M) {
+  const uint32_t c0 = in_range[item.x].x + item.y * TH_VCH;
+  return (uint32_t)((uint64_t)sfx[c0].x * TH_PHASES / (M ? M : 1u));
+}
+__global__ __launch_bounds__(256) void k_tri_hphase_count(const uint2* __restrict__ sfx, const uint2* __restrict__ in_range,
+                                                          const uint2* __restrict__ heavy, uint32_t nh, uint32_t M,
+                                                          uint32_t* __restrict__ hist) {
+  for (uint32_t h = blockIdx.x * 256u + threadIdx.x; h < nh; h += gridDim.x * 256u)
+    atomicAdd(&hist[min(th_phase(sfx, in_range, heavy[h], M), TH_PHASES - 1)], 1u);
+}
+__global__ __launch_bounds__(256) void k_tri_hphase_scan(uint32_t* __restrict__ hist) {   // one block, in place
+  __shared__ uint32_t s_w[256 / WAVE];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const uint32_t x = hist[tid], inc = wave_inclusive_sum(x);
+  if (lane == 63) s_w[w] = inc;
+  __syncthreads();
+  uint32_t off = 0;
+  for (int i = 0; i < w; ++i) off += s_w[i];
+  hist[tid] = off + inc - x;
+}
+__global__ __launch_bounds__(256) void k_tri_hphase_place(const uint2* __restrict__ sfx, const uint2* __restrict__ in_range,
+                                                          const uint2* __restrict__ heavy, uint32_t nh, uint32_t M,
+                                                          uint32_t* __restrict__ off, uint32_t* __restrict__ order) {
+  for (uint32_t h = blockIdx.x * 256u + threadIdx.x; h < nh; h += gridDim.x * 256u)
+    order[atomicAdd(&off[min(th_phase(sfx, in_range, heavy[h], M), TH_PHASES - 1)], 1u)] = h;
+}
+
 // one block per heavy item (v, chunk of TH_VCH in-neighbours): N+(v) as an LDS hash set (up to TH_NU
 // entries; longer lists are binary-searched in HBM; rebuilt only when the block's item changes v),
 // the chunk's lists TH_ILP items per thread with one search.  One item per in-chunk spreads a hub over
@@ -399,6 +436,8 @@ __global__ __launch_bounds__(TH_HBLOCK) __attribute__((amdgpu_waves_per_eu(GS_TH
                                                          const uint2* __restrict__ heavy,
                                                          const uint32_t* __restrict__ n_heavy,
                                                          const unsigned long long* __restrict__ pre,
+                                                         const uint32_t* __restrict__ order,
+                                                         uint32_t* __restrict__ claim,
                                                          unsigned long long* __restrict__ total,
                                                          unsigned long long* __restrict__ n_probes, uint32_t nb_cap,
                                                          uint32_t* __restrict__ err) {
@@ -408,6 +447,7 @@ __global__ __launch_bounds__(TH_HBLOCK) __attribute__((amdgpu_waves_per_eu(GS_TH
   __shared__ uint32_t s_loff[TH_VCH + 1];       // long lists (>= TH_LONG items), compacted the same way
   __shared__ uint32_t s_lst[TH_VCH];
   __shared__ uint4 s_w4[TH_HBLOCK / WAVE];
+  __shared__ uint32_t s_claim;
   constexpr int PER = TH_VCH / TH_HBLOCK;
   constexpr int NW = TH_HBLOCK / WAVE;
   uint32_t* hs = reinterpret_cast<uint32_t*>(s_hash);
@@ -418,8 +458,8 @@ __global__ __launch_bounds__(TH_HBLOCK) __attribute__((amdgpu_waves_per_eu(GS_TH
   // a contiguous run of items per block, cut at equal shares of the items' work (k_tri_hwork +
   // exclusive scan: pre[h] = work before item h, pre[nh] = total): the chunks of one heavy vertex are
   // consecutive items, so a block rebuilds its table only when its run moves to the next vertex
-  uint32_t h0, h1;
-  {
+  uint32_t h0 = 0, h1 = 0;
+  if (!order) {   // equal-work runs (phased: items claimed one at a time in phase order)
     const unsigned long long W = pre[nh];
     auto lower = [&](unsigned long long t) {   // first h with pre[h] >= t
       uint32_t a = 0, b = nh;
@@ -434,7 +474,18 @@ __global__ __launch_bounds__(TH_HBLOCK) __attribute__((amdgpu_waves_per_eu(GS_TH
     h0 = uni(lower(lo));
     h1 = blockIdx.x + 1 == gridDim.x ? nh : uni(lower(hi));
   }
-  for (uint32_t hi = h0; hi < h1; ++hi) {
+  for (uint32_t k = 0;; ++k) {
+    uint32_t hi;
+    if (order) {
+      if (tid == 0) s_claim = atomicAdd(claim, 1u);
+      __syncthreads();
+      hi = uni(s_claim);
+      if (hi >= nh) break;
+      hi = order[hi];
+    } else {
+      hi = h0 + k;
+      if (hi >= h1) break;
+    }
     const uint2 item = heavy[hi];   // (v, in-chunk)
     const uint32_t v = item.x;
     const uint2 ro = out_range[v], ri = in_range[v];
