@@ -395,7 +395,10 @@ __global__ __launch_bounds__(256) void k_tri_hwork(const uint2* __restrict__ sfx
 #ifndef GS_TH_PHASED
 #define GS_TH_PHASED 1
 #endif
-constexpr uint32_t TH_PHASES = 256;
+#ifndef GS_TH_PHASES
+#define GS_TH_PHASES 16384   // s26 heavy count (ms): 256 phases 149, 1024 146.5, 4096 143.3, 16384 142.0, 65536 141.2
+#endif
+constexpr uint32_t TH_PHASES = GS_TH_PHASES;
 __device__ __forceinline__ uint32_t th_phase(const uint2* __restrict__ sfx, const uint2* __restrict__ in_range, uint2 item,
                                              uint32_t M) {
   const uint32_t c0 = in_range[item.x].x + item.y * TH_VCH;
@@ -408,14 +411,24 @@ __global__ __launch_bounds__(256) void k_tri_hphase_count(const uint2* __restric
     atomicAdd(&hist[min(th_phase(sfx, in_range, heavy[h], M), TH_PHASES - 1)], 1u);
 }
 __global__ __launch_bounds__(256) void k_tri_hphase_scan(uint32_t* __restrict__ hist) {   // one block, in place
+  static_assert(TH_PHASES % 256 == 0, "phases per thread");
+  constexpr uint32_t PT = TH_PHASES / 256;
   __shared__ uint32_t s_w[256 / WAVE];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const uint32_t x = hist[tid], inc = wave_inclusive_sum(x);
+  uint32_t v[PT], x = 0;
+#pragma unroll
+  for (uint32_t j = 0; j < PT; ++j) x += (v[j] = hist[tid * PT + j]);
+  const uint32_t inc = wave_inclusive_sum(x);
   if (lane == 63) s_w[w] = inc;
   __syncthreads();
   uint32_t off = 0;
   for (int i = 0; i < w; ++i) off += s_w[i];
-  hist[tid] = off + inc - x;
+  off += inc - x;
+#pragma unroll
+  for (uint32_t j = 0; j < PT; ++j) {
+    hist[tid * PT + j] = off;
+    off += v[j];
+  }
 }
 __global__ __launch_bounds__(256) void k_tri_hphase_place(const uint2* __restrict__ sfx, const uint2* __restrict__ in_range,
                                                           const uint2* __restrict__ heavy, uint32_t nh, uint32_t M,
