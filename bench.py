@@ -415,7 +415,7 @@ def window_stream_main(a):
                          "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": None,
                          "algorithmic_bytes_per_launch": algo, "avg_launch_ms": round(ms, 4)},
             "cpu_baseline": cpu}
-    print(json.dumps(line), flush=True)
+    emit(line)
     eng.close()
 
 
@@ -480,7 +480,7 @@ def cand_stream_main(a):
                          "frac": round(17 * total / elapsed / 1e9 / HBM_PEAK_GBS, 4), "traffic": None,
                          "algorithmic_bytes_per_launch": 17 * total, "avg_launch_ms": elapsed * 1e3},
             "cpu_baseline": None}
-    print(json.dumps(line), flush=True)
+    emit(line)
     eng.close()
 
 
@@ -524,7 +524,7 @@ def parse_main(a):
                "sample": f"the whole text ({len(text) / 1e6:.0f} MB) through oracle gso_parse_edges_text, one thread, "
                          f"{dt:.2f} s"}
     gbs = algo / (ms * 1e-3) / 1e9
-    print(json.dumps({
+    emit({
         "metric": METRIC, "value": n * a.steps / elapsed, "unit": "edges/s", "n_gpus": 1, "steps": a.steps,
         "warmup": a.warmup, "ms_per_step": elapsed / a.steps * 1e3, "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": "u8", "data": "synthetic R-MAT scale-24 edge text, generated on the host",
@@ -534,7 +534,7 @@ def parse_main(a):
         "roofline": {"bound": "hbm", "kernel": "parse call (stage + count + starts + parse)", "achieved": round(gbs, 1),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": None,
                      "algorithmic_bytes_per_launch": algo, "avg_launch_ms": round(ms, 4)},
-        "cpu_baseline": cpu}), flush=True)
+        "cpu_baseline": cpu})
     eng.close()
 
 
@@ -620,7 +620,7 @@ def e2e_main(a):
         L.load().gs_free_pinned(p)
     ms = elapsed / a.steps * 1e3
     h2d_bytes = (16 if tri else 24) * E
-    print(json.dumps({
+    emit({
         "metric": METRIC, "value": E * a.steps / elapsed, "unit": "edges/s", "n_gpus": 1, "steps": a.steps,
         "warmup": a.warmup, "ms_per_step": ms, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
         "dtype": "int64", "data": f"synthetic R-MAT scale-{a.scale} windows generated on device, copied to host memory "
@@ -639,12 +639,33 @@ def e2e_main(a):
                    "h2d_bytes_per_window": h2d_bytes, "h2d_GBps_effective": h2d_bytes / (ms * 1e-3) / 1e9,
                    "vertices_out_per_window": None if tri else int(timed[-1].columns[0].size),
                    "triangles_last_window": int(timed[-1].columns[0]) if tri else None, "parallelism": "1 GPU"},
-        "roofline": None, "cpu_baseline": None}), flush=True)
+        "roofline": None, "cpu_baseline": None})
     eng.close()
+
+
+_JSON_OUT = None
+
+
+def quiet_native_stdout():
+    """The driver reads ONE JSON line from stdout.  RCCL (and other native libraries) print banners to file
+    descriptor 1 at communicator init ("RCCL version : ..."), so fd 1 is pointed at stderr for the rest of
+    the run and the JSON line goes to a duplicate of the original stdout."""
+    global _JSON_OUT
+    if _JSON_OUT is None:
+        sys.stdout.flush()
+        _JSON_OUT = os.fdopen(os.dup(1), "w")
+        os.dup2(2, 1)
+
+
+def emit(line):
+    out = _JSON_OUT if _JSON_OUT is not None else sys.stdout
+    out.write(json.dumps(line) + "\n")
+    out.flush()
 
 
 def main():
     a = parse()
+    quiet_native_stdout()
     if a.workload == "e2e":
         return e2e_main(a)
     if a.workload in ("c1", "apply", "candidates"):
@@ -910,7 +931,7 @@ def main():
                             "frac": round(r["frac"], 4), "frac_on_B": round(r["frac_on_B"], 4)}
                         for n, r in kt.items()},
         }
-        print(json.dumps(line), flush=True)
+        emit(line)
     if abi:
         eng.comm_destroy()
     if dist:
