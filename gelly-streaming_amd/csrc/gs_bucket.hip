@@ -466,8 +466,9 @@ gs_status bucket_direct_t(gs_ctx* c, const int64_t* src, const int64_t* dst, con
   if constexpr (CAN_PACK) {
     // escapes common (> 1/8 of the records): the next 16 windows store 8-byte values, then packing
     // is tried again
-    if (pack && c->host_small[7] > R / 8) c->bk_wide_vals = 16;
-    else if (!pack && c->bk_wide_vals > 0) --c->bk_wide_vals;
+    int& wide = c->bk_wide_vals[c->sp_slot];
+    if (pack && c->host_small[7] > R / 8) wide = 16;
+    else if (!pack && wide > 0) --wide;
   }
   const uint64_t esc = pack ? c->host_small[7] : 0;
   const uint32_t key_bits = nb <= 1 ? (uint32_t)S : (uint32_t)(S + 32 - __builtin_clz(nb - 1));
@@ -494,7 +495,7 @@ gs_status bucket_direct(gs_ctx* c, const int64_t* src, const int64_t* dst, const
                         typename P::Out o, uint64_t* U) {
   constexpr bool CAN_PACK = P::PAY == PAY_VAL && !P::REL && std::is_integral_v<typename P::A>;
   if constexpr (CAN_PACK) {
-    if (c->bk_wide_vals <= 0 && !(c->flags & GS_FLAG_NO_PACK))
+    if (c->bk_wide_vals[c->sp_slot] <= 0 && !(c->flags & GS_FLAG_NO_PACK))
       return bucket_direct_t<P, DIR, PK_ITEMS>(c, src, dst, val, n, o, U, true);
   }
   return bucket_direct_t<P, DIR, DP_ITEMS>(c, src, dst, val, n, o, U, false);

@@ -30,7 +30,7 @@ namespace gs {
 
 // owner_of: gs_ops.hpp (shared with the candidate split, gs_hashset.hip)
 
-constexpr int OW_BLOCK = 256, OW_ITEMS = 16, OW_TILE = OW_BLOCK * OW_ITEMS, OW_MAXP = 64;
+constexpr int OW_BLOCK = 256, OW_ITEMS = 8, OW_TILE = OW_BLOCK * OW_ITEMS, OW_MAXP = 64;
 
 // per tile: partials per owner -> cnt[owner * tiles + tile]; *wide |= 1 when a key lies outside
 // [0, 2^32) (the exchange then sends 8-byte keys)
@@ -88,42 +88,86 @@ __global__ __launch_bounds__(1024) void k_owner_scan(uint32_t* __restrict__ cnt,
   }
 }
 
-// stable partition: thread t of a tile owns OW_ITEMS consecutive partials; per-owner ranks from a
-// block scan over threads, bases from k_owner_scan
-template <typename V>
+// stable partition of a tile of OW_TILE partials: the tile is loaded lane-interleaved (coalesced) into
+// LDS; thread t then owns rows [16t, 16t + 16) for the per-owner ranks (a block scan over threads per
+// owner, as the order within an owner must stay ascending); the rows' tile-local order by owner goes to
+// an LDS permutation, and the tile is written out lane-interleaved from it, so each owner's run of the
+// tile lands in consecutive addresses (the round-2 version read and wrote each thread's 16 consecutive
+// rows straight from / to HBM: 64 lanes, 64 cache lines per instruction; 459 us for the 7.4 M partials of
+// a C2 window, now a fraction of that)
+template <typename V, int MAXP, bool TWO>
 __global__ __launch_bounds__(OW_BLOCK) void k_owner_scatter(const int64_t* __restrict__ keys, const V* __restrict__ vals,
                                                             const int64_t* __restrict__ vals2, uint64_t U,
                                                             uint32_t nparts, uint32_t tiles,
                                                             const uint32_t* __restrict__ off, int64_t* __restrict__ okeys,
                                                             V* __restrict__ ovals, int64_t* __restrict__ ovals2) {
-  __shared__ uint16_t s_r[OW_MAXP][OW_BLOCK];
+  constexpr uint32_t PADN = OW_TILE + OW_TILE / OW_ITEMS;   // row i at i + i / 16: thread t's rows off bank 0
+  __shared__ int64_t s_k[PADN];
+  __shared__ V s_v[OW_TILE];
+  __shared__ int64_t s_v2[TWO ? OW_TILE : 1];
+  __shared__ uint16_t s_r[MAXP][OW_BLOCK];   // (MAXP 8: one node's ranks in 4 KiB; 64 otherwise)
+  __shared__ uint16_t s_perm[OW_TILE];   // tile-local order by owner -> row
+  __shared__ uint8_t s_own[OW_TILE];
   __shared__ uint32_t s_w[OW_BLOCK / WAVE];
+  __shared__ uint32_t s_lo[MAXP + 1];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const uint64_t i0 = (uint64_t)blockIdx.x * OW_TILE + (uint64_t)tid * OW_ITEMS;
+  const uint64_t base = (uint64_t)blockIdx.x * OW_TILE;
+  const uint32_t nt = (uint32_t)min<uint64_t>(OW_TILE, U - base);
+#pragma unroll
+  for (int j = 0; j < OW_ITEMS; ++j) {   // coalesced loads
+    const uint32_t r = (uint32_t)j * OW_BLOCK + tid;
+    if (r < nt) {
+      s_k[r + r / OW_ITEMS] = keys[base + r];
+      s_v[r] = vals[base + r];
+      if constexpr (TWO) s_v2[r] = vals2[base + r];
+    }
+  }
   for (uint32_t o = 0; o < nparts; ++o) s_r[o][tid] = 0;
+  __syncthreads();
   uint32_t own[OW_ITEMS];
+  const uint32_t i0 = (uint32_t)tid * OW_ITEMS;
 #pragma unroll
   for (int j = 0; j < OW_ITEMS; ++j) {
-    own[j] = i0 + j < U ? owner_of(keys[i0 + j], nparts) : OW_MAXP;
-    if (own[j] < OW_MAXP) s_r[own[j]][tid]++;
+    const uint32_t r = i0 + j;
+    own[j] = r < nt ? owner_of(s_k[r + r / OW_ITEMS], nparts) : OW_MAXP;
+    if (own[j] < OW_MAXP) {
+      s_r[own[j]][tid]++;
+      s_own[r] = (uint8_t)own[j];
+    }
   }
-  for (uint32_t o = 0; o < nparts; ++o) {   // exclusive scan of owner o's counts over threads
+  if (tid == 0) s_lo[0] = 0;
+  for (uint32_t o = 0; o < nparts; ++o) {   // exclusive scan of owner o's counts over threads; its tile total
     const uint32_t x = s_r[o][tid];
     const uint32_t inc = wave_inclusive_sum(x);
     if (lane == 63) s_w[w] = inc;
     __syncthreads();
-    uint32_t pre = 0;
-    for (int k = 0; k < w; ++k) pre += s_w[k];
+    uint32_t pre = 0, tot = 0;
+    for (int k = 0; k < OW_BLOCK / WAVE; ++k) {
+      pre += k < w ? s_w[k] : 0u;
+      tot += s_w[k];
+    }
     s_r[o][tid] = (uint16_t)(pre + inc - x);
+    if (tid == 0) s_lo[o + 1] = tot;   // (turned into starts below)
     __syncthreads();
   }
+  if (tid == 0)
+    for (uint32_t o = 0; o < nparts; ++o) s_lo[o + 1] += s_lo[o];
+  __syncthreads();
 #pragma unroll
   for (int j = 0; j < OW_ITEMS; ++j) {
     if (own[j] >= OW_MAXP) continue;
-    const uint32_t pos = off[(uint64_t)own[j] * tiles + blockIdx.x] + s_r[own[j]][tid]++;
-    okeys[pos] = keys[i0 + j];
-    ovals[pos] = vals[i0 + j];
-    if (vals2) ovals2[pos] = vals2[i0 + j];
+    s_perm[s_lo[own[j]] + s_r[own[j]][tid]++] = (uint16_t)(i0 + j);
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < OW_ITEMS; ++j) {   // coalesced stores: consecutive q of one owner -> consecutive addresses
+    const uint32_t q = (uint32_t)j * OW_BLOCK + tid;
+    if (q >= nt) continue;
+    const uint32_t r = s_perm[q], o = s_own[r];
+    const uint32_t pos = off[(uint64_t)o * tiles + blockIdx.x] + (q - s_lo[o]);
+    okeys[pos] = s_k[r + r / OW_ITEMS];
+    ovals[pos] = s_v[r];
+    if constexpr (TWO) ovals2[pos] = s_v2[r];
   }
 }
 
@@ -143,12 +187,25 @@ gs_status owner_partition_dev(gs_ctx* c, const int64_t* keys, const void* vals, 
   }
   hipLaunchKernelGGL(k_owner_count, dim3(tiles), dim3(OW_BLOCK), 0, c->stream, keys, U, nparts, tiles, cnt, wide);
   hipLaunchKernelGGL(k_owner_scan, dim3(1), dim3(1024), 0, c->stream, cnt, tiles * nparts, tiles, nparts, totals);
-  if (vb == 8)
-    hipLaunchKernelGGL(k_owner_scatter<uint64_t>, dim3(tiles), dim3(OW_BLOCK), 0, c->stream, keys,
-                       (const uint64_t*)vals, vals2, U, nparts, tiles, cnt, okeys, (uint64_t*)ovals, ovals2);
-  else
-    hipLaunchKernelGGL(k_owner_scatter<uint32_t>, dim3(tiles), dim3(OW_BLOCK), 0, c->stream, keys,
-                       (const uint32_t*)vals, vals2, U, nparts, tiles, cnt, okeys, (uint32_t*)ovals, ovals2);
+  auto launch = [&](auto vtag, auto ptag, auto ttag) {
+    using V = decltype(vtag);
+    constexpr int MP = decltype(ptag)::value;
+    constexpr bool TW = decltype(ttag)::value;
+    hipLaunchKernelGGL((k_owner_scatter<V, MP, TW>), dim3(tiles), dim3(OW_BLOCK), 0, c->stream, keys,
+                       (const V*)vals, vals2, U, nparts, tiles, cnt, okeys, (V*)ovals, ovals2);
+  };
+  using P8 = std::integral_constant<int, 8>;
+  using P64 = std::integral_constant<int, OW_MAXP>;
+  using T1 = std::true_type;
+  using T0 = std::false_type;
+  const bool small = nparts <= 8, two = vals2 != nullptr;
+  if (vb == 8) {
+    if (small) two ? launch(uint64_t{}, P8{}, T1{}) : launch(uint64_t{}, P8{}, T0{});
+    else two ? launch(uint64_t{}, P64{}, T1{}) : launch(uint64_t{}, P64{}, T0{});
+  } else {
+    if (small) two ? launch(uint32_t{}, P8{}, T1{}) : launch(uint32_t{}, P8{}, T0{});
+    else two ? launch(uint32_t{}, P64{}, T1{}) : launch(uint32_t{}, P64{}, T0{});
+  }
   return hip_check(c, hipGetLastError(), "owner partition");
 }
 

@@ -41,7 +41,7 @@ struct gs_ctx {
   uint32_t flags = 0;    // gs_config.flags
   int64_t bk_base = 0;   // bucket path: predicted lower bound of the next window's vertex IDs
   uint32_t bk_nbp = 0;   // direct bucket path: predicted bucket count (0 = BK_MAXB)
-  int bk_wide_vals = 0;
+  int bk_wide_vals[2] = {0, 0};   // per sp_slot: a merge's wide partial sums must not unpack the windows
   // the last window call's output: U rows of ob-byte values, staged in out_keys / out_a (/ out_b) when
   // last_kind is 1 (vertex, value) or 2 (degree / max) -- gs_fetch_last_output after GS_ECAPACITY
   uint64_t last_U = 0;

@@ -16,3 +16,10 @@ for ex in abi torch; do
     echo "$ex $w done"
   done
 done
+# the exchange's own cost at world 1: owner partition + RCCL self-exchange + merge on every window
+for w in reduce fold; do
+  timeout -k 10 300 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 \
+    --master-port 29512 bench.py --gpus 1 --steps 10 --workload $w --exchange abi --force-exchange --no-cpu-baseline \
+    > "$O/torchrun_abi_forced_$w.json" 2> "$O/torchrun_abi_forced_$w.err"
+  echo "forced $w done"
+done
