@@ -302,7 +302,10 @@ gs_status bucket_direct_t(gs_ctx* c, const int64_t* src, const int64_t* dst, con
   if constexpr (SPEC_OK) {
     GS_TRY(ensure(c, sp.tot, BK_MAXB * 4, true));
     GS_TRY(ensure(c, c->sp_cur, SP_CUR_WORDS * 4));
-    spec = !(c->flags & GS_FLAG_NO_SPEC) && sp.ok && sp.skip == 0 && sp.base == base && sp.S == S &&
+    // merges (slot 1) do not speculate: their rows are owner-grouped runs sorted by vertex, so a tile
+    // holds few buckets and a bucket's records land in one XCD slot's segment -- the proportional
+    // segments overflow (a miss, then 8 windows without speculation, every 9th merge)
+    spec = !(c->flags & GS_FLAG_NO_SPEC) && c->sp_slot == 0 && sp.ok && sp.skip == 0 && sp.base == base && sp.S == S &&
            sp.dir == DIR && nb > 1 && sp_capacity(R, nb) + TRASH < (1ull << 32);   // u32 positions + trash
     if (sp.skip > 0) --sp.skip;
     if (spec) {

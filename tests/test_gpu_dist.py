@@ -268,8 +268,9 @@ def test_split_window_steps_and_rccl_world_one(pkg, oracle):
 
 def test_merges_keep_their_own_speculative_counts(pkg, oracle):
     """keyBy on one ctx alternates a window's partials and a merge of received rows: the merge's rows
-    spread over the buckets unlike the window's, so it predicts from its own counts (slot 1) and the
-    windows keep speculating from theirs (a shared slot made every window miss)."""
+    spread over the buckets unlike the window's and arrive as sorted owner runs, so merges run in their
+    own slot (slot 1: no speculation, their own packing state) and the windows keep speculating from
+    their own counts (a shared slot made every window miss)."""
     with pkg.Engine(0) as e:
         spec = []
         for w in range(5):
@@ -282,4 +283,5 @@ def test_merges_keep_their_own_speculative_counts(pkg, oracle):
             rk, rv = oracle.window_reduce(s, d, v, 1, 0)
             own = owner_np(rk, 2) == 0
             assert np.array_equal(mk.cpu().numpy(), rk[own]) and np.array_equal(mv.cpu().numpy(), rv[own])
+            assert e.stage_times().speculative == 0   # (the merge)
         assert spec[0] == 0 and spec[1:] == [1, 1, 1, 1], spec
