@@ -296,8 +296,8 @@ gs_status bucket_direct_t(gs_ctx* c, const int64_t* src, const int64_t* dst, con
   bool spec = false, spec_missed = false;
   uint64_t cap = R;
   // the speculative scatter's tile: k_sp_scatter_pack (SPK_BLOCK x SPK_ITEMS) or k_sp_scatter (DP_TILE)
-  const uint64_t TRASH = std::max<uint64_t>(SPK_TILE, (uint64_t)DP_BLOCK * ITEMS);
-  const uint64_t SPTE = !pack ? dp_tile_edges<DIR, ITEMS>() : spk_tile_edges<DIR>();
+  const uint64_t TRASH = std::max<uint64_t>(SPK_TILE, SPU_TILE);
+  const uint64_t SPTE = !pack ? spu_tile_edges<DIR>() : spk_tile_edges<DIR>();
   auto& sp = c->sp[c->sp_slot];
   if constexpr (SPEC_OK) {
     GS_TRY(ensure(c, sp.tot, BK_MAXB * 4, true));
@@ -363,9 +363,14 @@ gs_status bucket_direct_t(gs_ctx* c, const int64_t* src, const int64_t* dst, con
                                (unsigned long long*)(sm + SM_BK_ESC));
         }
         if constexpr (ITEMS == DP_ITEMS) {
-          if (!pack)
-            hipLaunchKernelGGL((k_sp_scatter<Load, DIR, P::PAY, Raw, P::REL>), dim3(dp_scatter_grid<DIR, ITEMS>(n)),
-                               dim3(DP_BLOCK), 0, c->stream, ls, n, S, nb, bst, cur, k16, vpart, (uint32_t)cap, rel_bad, mm);
+          if (!pack) {
+            if (nb <= 1024)
+              hipLaunchKernelGGL((k_sp_scatter<Load, DIR, P::PAY, Raw, P::REL, 1024>), dim3(spu_grid<DIR>(n)),
+                                 dim3(SPU_BLOCK), 0, c->stream, ls, n, S, nb, cur, k16, vpart, (uint32_t)cap, rel_bad, mm);
+            else
+              hipLaunchKernelGGL((k_sp_scatter<Load, DIR, P::PAY, Raw, P::REL, BK_MAXB>), dim3(spu_grid<DIR>(n)),
+                                 dim3(SPU_BLOCK), 0, c->stream, ls, n, S, nb, cur, k16, vpart, (uint32_t)cap, rel_bad, mm);
+          }
         }
         GS_HIP(hipGetLastError());
         GS_PASS_EVENT(c->pass_ev[2], c->stream);

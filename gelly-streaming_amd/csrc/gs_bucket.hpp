@@ -501,6 +501,7 @@ __global__ __launch_bounds__(BK_INFO_BLOCK) void k_bk_info(const int64_t* __rest
 }
 
 // block-wide exclusive scan of one u32 per thread (BLOCK = BK_PLAN_BLOCK); returns the total
+// (1024-thread blocks only: it reads BK_PLAN_BLOCK / WAVE wave sums; block_excl_scan<BLOCK> for others)
 __device__ __forceinline__ uint32_t bk_block_scan(uint32_t x, uint32_t* s_w, uint32_t& total) {
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   constexpr int NW = BK_PLAN_BLOCK / WAVE;
@@ -1424,28 +1425,45 @@ void k_sp_scatter_pack(BaseSrc<V, DIR, PAY_VAL> es, uint64_t n, int S, uint32_t 
 // (no payload) and the degree / max-neighbour folds (the neighbour, or REL: its 32-bit offset from the
 // window base, flagged in *rel_bad when it does not fit).  Same regions, segments, cursors, dummy bucket
 // and trash area as k_sp_scatter_pack.  Float SUM accumulates in LDS-atomic order anyway (1e-5).
-template <typename V, int DIR, int PAY, typename VO = V, bool REL = false>
-__global__ __launch_bounds__(DP_BLOCK) void k_sp_scatter(BaseSrc<V, DIR, PAY> es, uint64_t n, int S, uint32_t nbp,
-                                                         const uint32_t* __restrict__ bucket_start,
-                                                         uint32_t* __restrict__ cursor, uint16_t* __restrict__ k16,
-                                                         VO* __restrict__ vout, uint32_t trash,
-                                                         uint32_t* __restrict__ rel_bad,
-                                                         unsigned long long* __restrict__ mm) {
+// Block shape (round 3, as k_sp_scatter_pack): SPU_BLOCK x SPU_ITEMS records with bucket tables sized for
+// the window's buckets (NB), so two or more blocks share a CU (8-byte payload: 68 KiB of LDS at NB 1024).
+#ifndef GS_SPU_BLOCK
+#define GS_SPU_BLOCK 512
+#endif
+#ifndef GS_SPU_ITEMS
+#define GS_SPU_ITEMS 10
+#endif
+constexpr int SPU_BLOCK = GS_SPU_BLOCK, SPU_ITEMS = GS_SPU_ITEMS;
+constexpr uint32_t SPU_TILE = (uint32_t)SPU_BLOCK * SPU_ITEMS;
+static_assert(SPU_TILE < 65536, "tile positions in 16 bits");
+template <int DIR>
+__host__ __device__ constexpr uint32_t spu_tile_edges() {
+  return DIR == DIR_ALL ? SPU_TILE / 2 : SPU_TILE;
+}
+template <int DIR>
+__host__ __device__ inline uint32_t spu_grid(uint64_t n) {
+  return (uint32_t)((n / spu_tile_edges<DIR>() + 7) / 8 * 8 + 1);
+}
+template <typename V, int DIR, int PAY, typename VO, bool REL, int NB>
+__global__ __launch_bounds__(SPU_BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void k_sp_scatter(
+    BaseSrc<V, DIR, PAY> es, uint64_t n, int S, uint32_t nbp, uint32_t* __restrict__ cursor,
+    uint16_t* __restrict__ k16, VO* __restrict__ vout, uint32_t trash, uint32_t* __restrict__ rel_bad,
+    unsigned long long* __restrict__ mm) {
   constexpr bool HAS_V = PAY != PAY_NONE;
-  constexpr uint32_t TILE = DP_TILE;
-  constexpr uint32_t DUMMY = (uint32_t)BK_MAXB << 16;
+  constexpr int BLOCK = SPU_BLOCK, ITEMS = SPU_ITEMS, BPT = NB / BLOCK;   // buckets per thread
+  static_assert(NB % BLOCK == 0 && NB <= BK_MAXB, "bucket table shape");
+  constexpr uint32_t TILE = SPU_TILE;
+  constexpr uint32_t DUMMY = (uint32_t)NB << 16;
   __shared__ uint32_t s_key[TILE];                // (bucket << 16) | bucket-local index, bucket order
   __shared__ VO s_val[HAS_V ? TILE : 1];
-  __shared__ uint32_t s_cnt[BK_MAXB + 1];
-  __shared__ uint32_t s_delta[BK_MAXB + 1];
-  __shared__ uint32_t s_w[DP_BLOCK / WAVE];
-  __shared__ uint32_t s_ovf[DP_BLOCK / WAVE];
+  __shared__ uint32_t s_cnt[NB + 1];
+  __shared__ uint32_t s_delta[NB + 1];
+  __shared__ uint32_t s_w[BLOCK / WAVE];
+  __shared__ uint32_t s_ovf[BLOCK / WAVE];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  constexpr uint32_t TE = dp_tile_edges<DIR>();
+  constexpr uint32_t TE = spu_tile_edges<DIR>();
   const uint32_t nfull = (uint32_t)(n / TE);
   const uint32_t lmask = (1u << S) - 1;
-  const uint32_t b0 = 2 * tid, b1 = 2 * tid + 1;   // BK_MAXB = 2 * DP_BLOCK
-  const uint32_t bl0 = min(b0, nbp - 1), bl1 = min(b1, nbp - 1);
   uint32_t t, nrec = TILE;
   if (blockIdx.x == gridDim.x - 1) {   // the window's partial last tile
     if ((uint64_t)nfull * TE >= n) return;
@@ -1458,13 +1476,15 @@ __global__ __launch_bounds__(DP_BLOCK) void k_sp_scatter(BaseSrc<V, DIR, PAY> es
   }
   const uint32_t r0 = t * TILE;
   const uint32_t xs = SP_NSEG == 1 ? 0u : blockIdx.x & 7u;
-  const uint32_t end0 = sp_hi(cursor, xs, bl0), end1 = sp_hi(cursor, xs, bl1);
-  cursor += xs * BK_MAXB;
-  int64_t kk[DP_ITEMS];
-  V vv[DP_ITEMS];
+  uint32_t send[BPT];
 #pragma unroll
-  for (int u = 0; u < DP_ITEMS; ++u) {   // every load first, unconditional and clamped into the tile
-    const uint32_t r = r0 + min((uint32_t)u * DP_BLOCK + tid, nrec - 1);
+  for (int k = 0; k < BPT; ++k) send[k] = sp_hi(cursor, xs, min((uint32_t)tid * BPT + k, nbp - 1));
+  cursor += xs * BK_MAXB;
+  int64_t kk[ITEMS];
+  V vv[ITEMS];
+#pragma unroll
+  for (int u = 0; u < ITEMS; ++u) {   // every load first, unconditional and clamped into the tile
+    const uint32_t r = r0 + min((uint32_t)u * BLOCK + tid, nrec - 1);
     uint32_t i = r;
     bool rev = DIR == DIR_IN;
     if constexpr (DIR == DIR_ALL) {
@@ -1475,22 +1495,22 @@ __global__ __launch_bounds__(DP_BLOCK) void k_sp_scatter(BaseSrc<V, DIR, PAY> es
     if constexpr (PAY == PAY_VAL) vv[u] = es.val[i];
     else if constexpr (PAY == PAY_NBR) vv[u] = (V)(rev ? es.src : es.dst)[i];
   }
-  uint32_t ovf = 0, kb[DP_ITEMS];
+  uint32_t ovf = 0, kb[ITEMS];
   bool bad = false;
 #pragma unroll
-  for (int u = 0; u < DP_ITEMS; ++u) {
-    const uint32_t j = (uint32_t)u * DP_BLOCK + tid;
+  for (int u = 0; u < ITEMS; ++u) {
+    const uint32_t j = (uint32_t)u * BLOCK + tid;
     const uint64_t d = (uint64_t)kk[u] - (uint64_t)es.base;
     const bool in = (d >> S) < nbp, live = j < nrec;
     ovf += (live && !in) ? 1u : 0u;
     kb[u] = (live && in) ? ((uint32_t)(d >> S) << 16) | ((uint32_t)d & lmask) : DUMMY;
   }
-  for (uint32_t i = tid; i < nbp; i += DP_BLOCK) s_cnt[i] = 0;
-  if (tid == 0) s_cnt[BK_MAXB] = 0;
+  for (uint32_t i = tid; i < nbp; i += BLOCK) s_cnt[i] = 0;
+  if (tid == 0) s_cnt[NB] = 0;
   __syncthreads();
-  uint32_t rk[DP_ITEMS];
+  uint32_t rk[ITEMS];
 #pragma unroll
-  for (int u = 0; u < DP_ITEMS; ++u) {
+  for (int u = 0; u < ITEMS; ++u) {
     if constexpr (GS_SP_MATCH && PAY == PAY_NBR) {
       // folds (C3's hub-heavy streams): the lanes sharing the wave's first lane's bucket take one atomic
       // for all of them instead of serialising same-address LDS atomics (Zipf C3 scatter 1.82 -> 1.44 ms;
@@ -1506,17 +1526,28 @@ __global__ __launch_bounds__(DP_BLOCK) void k_sp_scatter(BaseSrc<V, DIR, PAY> es
     }
   }
   __syncthreads();
-  const uint32_t c0 = b0 < nbp ? s_cnt[b0] : 0u, c1 = b1 < nbp ? s_cnt[b1] : 0u;
-  const uint32_t o0 = c0 ? atomicAdd(&cursor[b0], c0) : 0u;
-  const uint32_t o1 = c1 ? atomicAdd(&cursor[b1], c1) : 0u;
+  uint32_t cb[BPT], ob[BPT], sum = 0;
+#pragma unroll
+  for (int k = 0; k < BPT; ++k) {
+    const uint32_t b = (uint32_t)tid * BPT + k;
+    cb[k] = b < nbp ? s_cnt[b] : 0u;
+    sum += cb[k];
+  }
+#pragma unroll
+  for (int k = 0; k < BPT; ++k) ob[k] = cb[k] ? atomicAdd(&cursor[(uint32_t)tid * BPT + k], cb[k]) : 0u;
   uint32_t total;
-  const uint32_t st0 = bk_block_scan(c0 + c1, s_w, total);
-  s_cnt[b0] = st0;
-  s_cnt[b1] = st0 + c0;
-  if (tid == 0) s_cnt[BK_MAXB] = total;
+  uint32_t st = block_excl_scan<BLOCK>(sum, s_w, total);   // (bk_block_scan assumes 1024 threads)
+  uint32_t sb[BPT];
+#pragma unroll
+  for (int k = 0; k < BPT; ++k) {
+    sb[k] = st;
+    s_cnt[(uint32_t)tid * BPT + k] = st;   // (entries past nbp are never read)
+    st += cb[k];
+  }
+  if (tid == 0) s_cnt[NB] = total;
   __syncthreads();
 #pragma unroll
-  for (int u = 0; u < DP_ITEMS; ++u) {
+  for (int u = 0; u < ITEMS; ++u) {
     const uint32_t pos = s_cnt[kb[u] >> 16] + rk[u];
     s_key[pos] = kb[u];
     if constexpr (REL) {   // a dead or outside lane's payload is never checked (it goes to the trash)
@@ -1527,15 +1558,17 @@ __global__ __launch_bounds__(DP_BLOCK) void k_sp_scatter(BaseSrc<V, DIR, PAY> es
       s_val[pos] = (VO)vv[u];
     }
   }
-  const bool drop0 = c0 && o0 + c0 > end0, drop1 = c1 && o1 + c1 > end1;
-  s_delta[b0] = (drop0 ? trash : o0) - st0;
-  s_delta[b1] = (drop1 ? trash : o1) - (st0 + c0);
-  if (tid == 0) s_delta[BK_MAXB] = trash;
-  ovf += (drop0 ? 1u : 0u) + (drop1 ? 1u : 0u);
+#pragma unroll
+  for (int k = 0; k < BPT; ++k) {
+    const bool drop = cb[k] && ob[k] + cb[k] > send[k];
+    s_delta[(uint32_t)tid * BPT + k] = (drop ? trash : ob[k]) - sb[k];
+    ovf += drop ? 1u : 0u;
+  }
+  if (tid == 0) s_delta[NB] = trash;
   __syncthreads();
 #pragma unroll
-  for (int u = 0; u < DP_ITEMS; ++u) {
-    const uint32_t j = (uint32_t)u * DP_BLOCK + tid;
+  for (int u = 0; u < ITEMS; ++u) {
+    const uint32_t j = (uint32_t)u * BLOCK + tid;
     const uint32_t kv = s_key[j];
     const uint32_t g = s_delta[kv >> 16] + j;
     k16[g] = (uint16_t)kv;
@@ -1550,7 +1583,7 @@ __global__ __launch_bounds__(DP_BLOCK) void k_sp_scatter(BaseSrc<V, DIR, PAY> es
   __syncthreads();
   if (tid == 0) {
     uint32_t o2 = 0;
-    for (int i = 0; i < DP_BLOCK / WAVE; ++i) o2 += s_ovf[i];
+    for (int i = 0; i < BLOCK / WAVE; ++i) o2 += s_ovf[i];
     if (o2) atomicAdd(&mm[2], (unsigned long long)o2);
   }
 }
