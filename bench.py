@@ -884,6 +884,11 @@ def main():
     if cpu:
         cpu["gpu_over_cpu"] = round(value / cpu["value"], 1)
         cpu.update(host_cpu())
+        if cpu["cores"] > 1 and cpu["nproc"] > cpu["cores"]:
+            # P = nproc; the box allots 16 CPUs per GPU, so the nproc-thread figure is the
+            # measured rate scaled linearly (an upper bound for the CPU), labelled as such
+            cpu["value_at_nproc_linear"] = cpu["value"] * cpu["nproc"] / cpu["cores"]
+            cpu["gpu_over_cpu_at_nproc_linear"] = round(value / cpu["value_at_nproc_linear"], 1)
 
     if rank == 0:
         t0s = times[0]
@@ -928,7 +933,8 @@ def main():
                                         f"rows (library communicator) -> merge" if abi else
                                         f"hash keyBy over {world} GPU(s): per-rank partials (gs_window_reduce_partials) "
                                         f"-> torch.distributed all-to-all -> gs_merge_partials")),
-                       "exchange": (a.exchange if dist else None), **checks},
+                       "exchange": (a.exchange if dist else None),
+                       "cpu_baseline_sample": cpu["sample"] if cpu else None, **checks},
             "roofline": roofline,
             "cpu_baseline": cpu,
             "kernels": {n: {"avg_ms": round(r["ms"], 4), "own_bytes": r["bytes"], "GB/s": round(r["GB/s"], 1),

@@ -224,9 +224,9 @@ gs_status bucket_results(gs_ctx* c, uint64_t* U, uint32_t* n_items) {
 void bucket_times(gs_ctx* c, int path, int passes, int launches, uint32_t key_bits, uint64_t R, uint64_t U,
                   size_t vb, uint32_t n_items) {
   float a = 0, b = 0, d = 0;
-  hipEventElapsedTime(&a, c->ev[0], c->ev[1]);
-  hipEventElapsedTime(&b, c->ev[1], c->ev[2]);
-  hipEventElapsedTime(&d, c->ev[2], c->ev[3]);
+  a = event_ms(c->ev[0], c->ev[1]);
+  b = event_ms(c->ev[1], c->ev[2]);
+  d = event_ms(c->ev[2], c->ev[3]);
   gs_stage_times& t = c->times;
   t = gs_stage_times{};
   t.keyinfo_ms = a;
@@ -237,7 +237,7 @@ void bucket_times(gs_ctx* c, int path, int passes, int launches, uint32_t key_bi
   t.key_bits = key_bits;
   t.records = R;
   t.vertices = U;
-  for (int p = 0; p < launches && p < 8; ++p) hipEventElapsedTime(&t.pass_ms[p], c->pass_ev[p], c->pass_ev[p + 1]);
+  for (int p = 0; p < launches && p < 8; ++p) t.pass_ms[p] = event_ms(c->pass_ev[p], c->pass_ev[p + 1]);
   t.key_bytes = 2;
   t.payload_bytes = (uint32_t)vb;
   t.partials = n_items;

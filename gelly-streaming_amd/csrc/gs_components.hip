@@ -228,10 +228,10 @@ gs_status gs_window_components(gs_ctx* c, const gs_edge_batch* b, const gs_parti
       GS_TRY(host_wait(c));
       gs_stage_times& t = c->times;
       t = gs_stage_times{};
-      hipEventElapsedTime(&t.pass_ms[0], c->ev[0], c->ev[1]);   // staging + id range + init
-      hipEventElapsedTime(&t.pass_ms[1], c->ev[1], c->ev[2]);   // union-find + compression
-      hipEventElapsedTime(&t.pass_ms[2], c->ev[2], c->ev[3]);   // present vertices -> labels
-      hipEventElapsedTime(&t.total_ms, c->ev[0], c->ev[3]);
+      t.pass_ms[0] = event_ms(c->ev[0], c->ev[1]);   // staging + id range + init
+      t.pass_ms[1] = event_ms(c->ev[1], c->ev[2]);   // union-find + compression
+      t.pass_ms[2] = event_ms(c->ev[2], c->ev[3]);   // present vertices -> labels
+      t.total_ms = event_ms(c->ev[0], c->ev[3]);
       t.records = N;
       t.vertices = U;
       t.key_bits = B;
@@ -276,10 +276,10 @@ gs_status gs_window_components(gs_ctx* c, const gs_edge_batch* b, const gs_parti
   GS_TRY(host_wait(c));
   gs_stage_times& t = c->times;
   t = gs_stage_times{};
-  hipEventElapsedTime(&t.pass_ms[0], c->ev[0], c->ev[1]);   // staging + compact IDs
-  hipEventElapsedTime(&t.pass_ms[1], c->ev[1], c->ev[2]);   // union-find
-  hipEventElapsedTime(&t.pass_ms[2], c->ev[2], c->ev[3]);   // labels
-  hipEventElapsedTime(&t.total_ms, c->ev[0], c->ev[3]);
+  t.pass_ms[0] = event_ms(c->ev[0], c->ev[1]);   // staging + compact IDs
+  t.pass_ms[1] = event_ms(c->ev[1], c->ev[2]);   // union-find
+  t.pass_ms[2] = event_ms(c->ev[2], c->ev[3]);   // labels
+  t.total_ms = event_ms(c->ev[0], c->ev[3]);
   t.records = N;
   t.vertices = U;
   t.path = 4;

@@ -43,6 +43,7 @@ gs_status host_wait(gs_ctx* c) {
     if (e != hipErrorNotReady) return hip_check(c, e, "hipEventQuery");
     if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(2)) break;
   }
+  (void)hipGetLastError();   // "not ready" is a poll result, not an error for the next launch check
   return hip_check(c, hipEventSynchronize(c->sync_ev), "hipEventSynchronize");
 }
 
@@ -80,6 +81,8 @@ uint32_t next_epoch(gs_ctx* c, size_t) {
 
 gs_status begin_call(gs_ctx* c) {
   ++c->call_seq;   // ends a chunked-candidates session (its sets live in shared workspace)
+  c->last_kind = 0;   // the staged output buffers are about to be reused: nothing left to fetch
+  (void)hipGetLastError();
   GS_HIP(hipSetDevice(c->device));
   GS_HIP(hipMemsetAsync(c->small.as<char>() + SM_TIMEOUT, 0, 8, c->stream));
   return GS_OK;
@@ -427,10 +430,26 @@ const char* gs_last_error(const gs_ctx* c) { return c ? c->err.c_str() : "null c
 
 gs_status gs_set_stream(gs_ctx* c, void* s) {
   if (!c) return GS_EINVAL;
-  hipSetDevice(c->device);
-  if (c->stream) hipStreamSynchronize(c->stream);
+  (void)hipGetLastError();
+  GS_HIP(hipSetDevice(c->device));
+  // the handle must be a live stream of this process's HIP runtime on the ctx's device (NULL = the
+  // device's default stream); anything else fails here, not at the next window's first launch
+  if (s) {
+    const hipError_t q = hipStreamQuery((hipStream_t)s);
+    if (q != hipSuccess && q != hipErrorNotReady) {
+      (void)hipGetLastError();
+      return set_error(c, GS_EDEVICE, "gs_set_stream: %p is not a HIP stream of this process: %s", s,
+                       hipGetErrorString(q));
+    }
+    int dev = -1;
+    if (hipStreamGetDevice((hipStream_t)s, &dev) == hipSuccess && dev != c->device)
+      return set_error(c, GS_EINVAL, "gs_set_stream: stream %p belongs to device %d, the ctx to device %d", s, dev,
+                       c->device);
+    (void)hipGetLastError();
+  }
+  if (c->stream) GS_HIP(hipStreamSynchronize(c->stream));
   if (c->own_stream && c->stream) hipStreamDestroy(c->stream);
-  c->stream = (hipStream_t)s;  // NULL = the device's default stream
+  c->stream = (hipStream_t)s;
   c->own_stream = false;
   return GS_OK;
 }
@@ -514,11 +533,17 @@ static gs_status window_chunked(gs_ctx* c, const gs_edge_batch* b, int32_t dir, 
   const size_t vb = dtype_bytes(b->val_dtype);
   const size_t ob = (deg || op == GS_OP_COUNT) ? 8 : vb;
   const int32_t pdt = (deg || op == GS_OP_COUNT) ? GS_I64 : b->val_dtype;
-  const uint64_t nch = (b->n + ce - 1) / ce;
+  // a merge takes the running partials plus one chunk's: keep that under one pass's 2^32 - 1 rows by
+  // shrinking the chunk as the distinct vertices accumulate (a window of more distinct vertices than
+  // that cannot be merged in one pass: GS_EUNSUPPORTED)
+  const uint64_t pass_rows = (1ull << 32) - 1;
   int x = 0;
   uint64_t acc = 0;   // running partials in ck_*[x][0, acc)
-  for (uint64_t k = 0; k < nch; ++k) {
-    const uint64_t e0 = k * ce, ne = std::min<uint64_t>(ce, b->n - e0), Rc = ne * per;
+  for (uint64_t k = 0, e0 = 0; e0 < b->n; ++k) {
+    if (acc + per > pass_rows)
+      return set_error(c, GS_EUNSUPPORTED, "chunked window: %llu distinct vertices leave no room for a chunk",
+                       (unsigned long long)acc);
+    const uint64_t ne = std::min<uint64_t>({ce, b->n - e0, (pass_rows - acc) / per}), Rc = ne * per;
     gs_edge_batch cb = *b;
     cb.src = b->src + e0;
     cb.dst = b->dst + e0;
@@ -537,7 +562,8 @@ static gs_status window_chunked(gs_ctx* c, const gs_edge_batch* b, int32_t dir, 
       GS_TRY(gs_window_reduce(c, &cb, dir, op, &po));
     }
     const uint64_t n = acc + Uc;
-    const bool last = k + 1 == nch;
+    e0 += ne;
+    const bool last = e0 == b->n;
     if (k == 0 && !last) {   // nothing to merge with yet
       acc = n;
       continue;

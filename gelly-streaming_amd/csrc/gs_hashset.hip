@@ -1080,6 +1080,7 @@ gs_status gs_candidates_next(gs_ctx* c, gs_pair_out* out, uint64_t* first_record
   uint8_t* f = out->is_candidate;
   const bool direct = out->mem == GS_MEM_DEVICE;
   if (!direct) {
+    c->last_kind = 0;   // the staging buffers now hold candidate records, not a reduce's rows
     GS_TRY(ensure(c, c->out_keys, n * 8));
     GS_TRY(ensure(c, c->out_a, n * 8));
     GS_TRY(ensure(c, c->out_b, n));

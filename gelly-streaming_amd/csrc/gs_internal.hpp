@@ -194,8 +194,21 @@ gs_status bucket_degree_max(gs_ctx* c, const int64_t* src, const int64_t* dst, u
 // reads small results mid-window (vertex range, output count); a blocking wait's wake-up latency is
 // paid twice per window otherwise.
 gs_status host_wait(gs_ctx* c);
-// clear the look-back timeout word at the start of a public call
+// at the start of a public call: drain the thread's sticky HIP error (a failed call of the host process,
+// e.g. torch's, would otherwise surface at our next post-launch hipGetLastError), select the device and
+// clear the look-back timeout word
 gs_status begin_call(gs_ctx* c);
+// milliseconds between two recorded events; 0 (and no sticky error left behind) when either was not
+// recorded on this call's path -- hipEventElapsedTime's hipErrorInvalidHandle must not reach the next
+// launch check as "invalid resource handle"
+inline float event_ms(hipEvent_t a, hipEvent_t b) {
+  float ms = 0.f;
+  if (hipEventElapsedTime(&ms, a, b) != hipSuccess) {
+    (void)hipGetLastError();
+    ms = 0.f;
+  }
+  return ms;
+}
 
 // k_keyinfo over both columns (ALL): mask at SM_MASK, byte histograms at SM_HIST
 gs_status launch_keyinfo_all(gs_ctx* c, const int64_t* src, const int64_t* dst, uint64_t n, bool mask_only = false);

@@ -79,9 +79,9 @@ inline gs_status launch_rbk(gs_ctx* c, const Sorted& s, Out o, uint64_t* n_uniqu
 inline void finish_times(gs_ctx* c, const Sorted& s, uint64_t U) {
   hipEventSynchronize(c->ev[3]);
   float a = 0, b = 0, d = 0;
-  hipEventElapsedTime(&a, c->ev[0], c->ev[1]);
-  hipEventElapsedTime(&b, c->ev[1], c->ev[2]);
-  hipEventElapsedTime(&d, c->ev[2], c->ev[3]);
+  a = event_ms(c->ev[0], c->ev[1]);
+  b = event_ms(c->ev[1], c->ev[2]);
+  d = event_ms(c->ev[2], c->ev[3]);
   c->times.keyinfo_ms = a;
   c->times.sort_ms = b;
   c->times.reduce_ms = d;
@@ -93,7 +93,7 @@ inline void finish_times(gs_ctx* c, const Sorted& s, uint64_t U) {
   const int launched = s.done_passes + (s.fused ? 1 : 0);
   for (int p = 0; p < 8; ++p) {
     float t = 0;
-    if (p < launched) hipEventElapsedTime(&t, c->pass_ev[p], c->pass_ev[p + 1]);
+    if (p < launched) t = event_ms(c->pass_ev[p], c->pass_ev[p + 1]);
     c->times.pass_ms[p] = t;
   }
   c->times.sort_passes = (uint32_t)launched;

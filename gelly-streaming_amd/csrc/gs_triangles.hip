@@ -671,8 +671,8 @@ void tri_times(gs_ctx* c, const TriGeom& g, uint64_t M, uint64_t nv, uint64_t pr
   gs_stage_times& t = c->times;
   t = gs_stage_times{};
   const int order[6] = {0, 1, 2, 4, 5, 3};
-  for (int i = 0; i < 5; ++i) hipEventElapsedTime(&t.pass_ms[i], c->ev[order[i]], c->ev[order[i + 1]]);
-  hipEventElapsedTime(&t.total_ms, c->ev[0], c->ev[3]);
+  for (int i = 0; i < 5; ++i) t.pass_ms[i] = event_ms(c->ev[order[i]], c->ev[order[i + 1]]);
+  t.total_ms = event_ms(c->ev[0], c->ev[3]);
   t.sort_passes = (uint32_t)passes;
   t.key_bits = g.B;
   t.records = M;     // unique undirected edges

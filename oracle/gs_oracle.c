@@ -1281,9 +1281,11 @@ typedef struct tf_ctx {
   uint32_t* map;                           /* id - kmin -> compact id + 1 (0: absent) */
   uint32_t *cs, *cd; uint64_t V;
   uint64_t *off, *cur;                     /* CSR by the smaller endpoint, then by orientation */
-  uint32_t *lst, *ucnt, *deg, *nbr;
+  uint32_t *lst, *ucnt, *deg, *rank, *nbr;
   uint64_t* uoff; uint32_t* ulst;          /* distinct undirected edges (a < b), by a */
+  uint64_t *ioff, *ipos; uint32_t* iown;   /* in-lists: for y, the out-list positions p of x -> y, and x */
   volatile uint64_t next; int P; int bad;
+  uint64_t split[65];
   int64_t mn[64], mx[64]; uint64_t T[64];
 } tf_ctx;
 typedef struct { tf_ctx* c; int t; void (*fn)(tf_ctx*, int); } tf_job;
@@ -1323,10 +1325,22 @@ static void tf_count_lo(tf_ctx* c, int t) {   /* records per smaller endpoint */
     __atomic_fetch_add(&c->off[a + 1], 1, __ATOMIC_RELAXED);
   }
 }
+/* fills without atomics: thread t owns the keys [split[t], split[t+1]) (equal shares of the entries, by
+ * the offsets) and scans every record for its own -- an atomic cursor per key serialised the threads on
+ * the R-MAT hubs */
+static void tf_split(tf_ctx* c, const uint64_t* off, uint64_t V) {
+  uint64_t k = 0;
+  for (int t = 0; t <= c->P; ++t) {
+    const uint64_t want = off[V] * (uint64_t)t / (uint64_t)c->P;
+    while (k < V && off[k] < want) ++k;
+    c->split[t] = t == c->P ? V : k;
+  }
+}
 static void tf_fill_lo(tf_ctx* c, int t) {
-  for (uint64_t i = TF_LO(c, t, c->n); i < TF_HI(c, t, c->n); ++i) {
-    const uint32_t a = c->cs[i] < c->cd[i] ? c->cs[i] : c->cd[i], b = c->cs[i] ^ c->cd[i] ^ a;
-    c->lst[__atomic_fetch_add(&c->cur[a], 1, __ATOMIC_RELAXED)] = b;
+  const uint32_t k0 = (uint32_t)c->split[t], k1 = (uint32_t)c->split[t + 1];
+  for (uint64_t i = 0; i < c->n; ++i) {
+    const uint32_t a = c->cs[i] < c->cd[i] ? c->cs[i] : c->cd[i];
+    if (a - k0 < k1 - k0) c->lst[c->cur[a]++] = c->cs[i] ^ c->cd[i] ^ a;
   }
 }
 static int tf_cmp_u32(const void* x, const void* y) {
@@ -1356,24 +1370,33 @@ static void tf_degrees(tf_ctx* c, int t) {
     for (uint32_t i = 0; i < c->ucnt[a]; ++i) __atomic_fetch_add(&c->deg[L[i]], 1, __ATOMIC_RELAXED);
   }
 }
-#define TF_FWD(c, a, b) ((c)->deg[a] < (c)->deg[b] || ((c)->deg[a] == (c)->deg[b] && (a) < (b)))
+/* orientation x -> y iff (deg x, x) < (deg y, y), i.e. rank x < rank y; out-lists are stored over the
+ * ranks, so hot (high-degree) vertices share the top of the id space and stay in cache.  The partner
+ * lists are rewritten to ranks in place first (one random read each), then counted and filled */
+static void tf_rank_lists(tf_ctx* c, int t) {
+  for (uint64_t a = TF_LO(c, t, c->V); a < TF_HI(c, t, c->V); ++a) {
+    uint32_t* L = c->lst + c->off[a];
+    for (uint32_t i = 0; i < c->ucnt[a]; ++i) L[i] = c->rank[L[i]];
+  }
+}
 static void tf_count_out(tf_ctx* c, int t) {
   for (uint64_t a = TF_LO(c, t, c->V); a < TF_HI(c, t, c->V); ++a) {
     const uint32_t* L = c->lst + c->off[a];
+    const uint32_t ra = c->rank[a];
     for (uint32_t i = 0; i < c->ucnt[a]; ++i) {
-      const uint32_t b = L[i], x = TF_FWD(c, (uint32_t)a, b) ? (uint32_t)a : b;
+      const uint32_t x = ra < L[i] ? ra : L[i];
       __atomic_fetch_add(&c->uoff[x + 1], 1, __ATOMIC_RELAXED);
     }
   }
 }
 static void tf_fill_out(tf_ctx* c, int t) {
-  for (uint64_t a = TF_LO(c, t, c->V); a < TF_HI(c, t, c->V); ++a) {
+  const uint32_t k0 = (uint32_t)c->split[t], k1 = (uint32_t)c->split[t + 1];
+  for (uint64_t a = 0; a < c->V; ++a) {
     const uint32_t* L = c->lst + c->off[a];
+    const uint32_t ra = c->rank[a];
     for (uint32_t i = 0; i < c->ucnt[a]; ++i) {
-      const uint32_t b = L[i];
-      const int f = TF_FWD(c, (uint32_t)a, b);
-      const uint32_t x = f ? (uint32_t)a : b, y = f ? b : (uint32_t)a;
-      c->nbr[__atomic_fetch_add(&c->cur[x], 1, __ATOMIC_RELAXED)] = y;
+      const uint32_t rb = L[i], x = ra < rb ? ra : rb;
+      if (x - k0 < k1 - k0) c->nbr[c->cur[x]++] = ra ^ rb ^ x;
     }
   }
 }
@@ -1388,28 +1411,48 @@ static void tf_sort_out(tf_ctx* c, int t) {
     }
   }
 }
-/* T = sum over oriented x -> y of |N+(x) ∩ N+(y)|: N+(x) stamped into a per-thread array, each w of
- * N+(y) tested against the stamp (the same set sizes the merge intersection reads, no merge) */
+/* in-lists: every out-list entry p of x (x -> y) is listed under y with its owner x */
+static void tf_count_in(tf_ctx* c, int t) {
+  for (uint64_t p = TF_LO(c, t, c->uoff[c->V]); p < TF_HI(c, t, c->uoff[c->V]); ++p)
+    __atomic_fetch_add(&c->ioff[c->nbr[p] + 1], 1, __ATOMIC_RELAXED);
+}
+static void tf_fill_in(tf_ctx* c, int t) {
+  const uint32_t k0 = (uint32_t)c->split[t], k1 = (uint32_t)c->split[t + 1];
+  for (uint64_t x = 0; x < c->V; ++x)
+    for (uint64_t p = c->uoff[x]; p < c->uoff[x + 1]; ++p) {
+      const uint32_t y = c->nbr[p];
+      if (y - k0 >= k1 - k0) continue;
+      const uint64_t q = c->cur[y]++;
+      c->ipos[q] = p;
+      c->iown[q] = (uint32_t)x;
+    }
+}
+/* T = sum over y, over in-neighbours x of y (x -> y), of |{w in N+(x) after y} ∩ N+(y)|: a triangle
+ * x -> y -> w (ranks x < y < w) is counted once, at its middle vertex y.  N+(y) is marked in a per-thread
+ * bitmap over the ranks (V bits: 8 MB at scale 26), each w of N+(x) past y (the out-list is sorted, so
+ * that is the suffix after position p) tested against it, the marks cleared again.  The suffix makes
+ * this ~4x fewer probes than testing all of N+(y) for every x -> y (R-MAT s22: 7.2 G vs 28.7 G). */
 static void tf_intersect(tf_ctx* c, int t) {
-  uint32_t* stamp = (uint32_t*)malloc(c->V * sizeof(uint32_t));
-  memset(stamp, 0xFF, c->V * sizeof(uint32_t));
+  uint64_t* bits = (uint64_t*)calloc((c->V >> 6) + 1, sizeof(uint64_t));
   uint64_t T = 0;
   for (;;) {
-    const uint64_t x0 = __sync_fetch_and_add(&c->next, 256);
-    if (x0 >= c->V) break;
-    const uint64_t x1 = x0 + 256 < c->V ? x0 + 256 : c->V;
-    for (uint64_t x = x0; x < x1; ++x) {
-      const uint64_t b = c->uoff[x], e = c->uoff[x + 1];
-      if (e - b < 2) continue;
-      for (uint64_t p = b; p < e; ++p) stamp[c->nbr[p]] = (uint32_t)x;
-      for (uint64_t p = b; p < e; ++p) {
-        const uint32_t y = c->nbr[p];
-        for (uint64_t q = c->uoff[y]; q < c->uoff[y + 1]; ++q) T += stamp[c->nbr[q]] == (uint32_t)x;
+    const uint64_t y0 = __sync_fetch_and_add(&c->next, 256);
+    if (y0 >= c->V) break;
+    const uint64_t y1 = y0 + 256 < c->V ? y0 + 256 : c->V;
+    for (uint64_t y = y0; y < y1; ++y) {
+      const uint64_t b = c->uoff[y], e = c->uoff[y + 1];
+      if (e == b || c->ioff[y + 1] == c->ioff[y]) continue;
+      for (uint64_t p = b; p < e; ++p) bits[c->nbr[p] >> 6] |= 1ull << (c->nbr[p] & 63);
+      for (uint64_t i = c->ioff[y]; i < c->ioff[y + 1]; ++i) {
+        const uint32_t x = c->iown[i];
+        const uint32_t* L = c->nbr;
+        for (uint64_t q = c->ipos[i] + 1; q < c->uoff[x + 1]; ++q) T += (bits[L[q] >> 6] >> (L[q] & 63)) & 1;
       }
+      for (uint64_t p = b; p < e; ++p) bits[c->nbr[p] >> 6] = 0;
     }
   }
   c->T[t] = T;
-  free(stamp);
+  free(bits);
 }
 
 GSO_API int gso_triangles_fwd_mt(const int64_t* src, const int64_t* dst, uint64_t n, int threads, uint64_t* T_out) {
@@ -1471,6 +1514,7 @@ GSO_API int gso_triangles_fwd_mt(const int64_t* src, const int64_t* dst, uint64_
   tf_par(c, tf_count_lo);
   for (uint64_t x = 0; x < V; ++x) c->off[x + 1] += c->off[x];
   memcpy(c->cur, c->off, (V + 1) * sizeof(uint64_t));
+  tf_split(c, c->off, V);
   tf_par(c, tf_fill_lo);
   free(c->cs); free(c->cd);
   c->next = 0;
@@ -1478,21 +1522,41 @@ GSO_API int gso_triangles_fwd_mt(const int64_t* src, const int64_t* dst, uint64_
   /* 3. degrees over distinct edges; orientation x -> y iff (deg x, x) < (deg y, y); sorted out-lists */
   c->deg = (uint32_t*)calloc(V + 1, sizeof(uint32_t));
   tf_par(c, tf_degrees);
+  /* ranks: a counting sort by degree, ties by id */
+  uint32_t dmax = 0;
+  for (uint64_t x = 0; x < V; ++x) dmax = c->deg[x] > dmax ? c->deg[x] : dmax;
+  uint64_t* dcnt = (uint64_t*)calloc((uint64_t)dmax + 2, sizeof(uint64_t));
+  for (uint64_t x = 0; x < V; ++x) ++dcnt[c->deg[x] + 1];
+  for (uint64_t d = 0; d <= dmax; ++d) dcnt[d + 1] += dcnt[d];
+  c->rank = (uint32_t*)malloc((V + 1) * sizeof(uint32_t));
+  for (uint64_t x = 0; x < V; ++x) c->rank[x] = (uint32_t)dcnt[c->deg[x]]++;
+  free(dcnt);
+  tf_par(c, tf_rank_lists);
   c->uoff = (uint64_t*)calloc(V + 1, sizeof(uint64_t));
   tf_par(c, tf_count_out);
   for (uint64_t x = 0; x < V; ++x) c->uoff[x + 1] += c->uoff[x];
   memcpy(c->cur, c->uoff, (V + 1) * sizeof(uint64_t));
+  tf_split(c, c->uoff, V);
   c->nbr = (uint32_t*)malloc((c->uoff[V] + 1) * sizeof(uint32_t));
   tf_par(c, tf_fill_out);
   c->next = 0;
   tf_par(c, tf_sort_out);
-  /* 4. the count */
+  /* 4. in-lists, then the count */
+  const uint64_t Ep = c->uoff[V];
+  c->ioff = (uint64_t*)calloc(V + 1, sizeof(uint64_t));
+  tf_par(c, tf_count_in);
+  for (uint64_t x = 0; x < V; ++x) c->ioff[x + 1] += c->ioff[x];
+  memcpy(c->cur, c->ioff, (V + 1) * sizeof(uint64_t));
+  tf_split(c, c->ioff, V);
+  c->ipos = (uint64_t*)malloc((Ep + 1) * sizeof(uint64_t));
+  c->iown = (uint32_t*)malloc((Ep + 1) * sizeof(uint32_t));
+  tf_par(c, tf_fill_in);
   c->next = 0;
   tf_par(c, tf_intersect);
   uint64_t T = 0;
   for (int t = 0; t < c->P; ++t) T += c->T[t];
   *T_out = T;
-  free(c->off); free(c->cur); free(c->lst); free(c->ucnt); free(c->deg); free(c->uoff); free(c->nbr); free(c);
+  free(c->off); free(c->cur); free(c->lst); free(c->ucnt); free(c->deg); free(c->rank); free(c->uoff); free(c->ioff); free(c->ipos); free(c->iown); free(c->nbr); free(c);
   return 0;
 }
 
