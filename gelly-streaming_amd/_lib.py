@@ -43,7 +43,8 @@ EXPORTS = ("gs_abi_version", "gs_create", "gs_destroy", "gs_last_error", "gs_set
            "gs_comm_allreduce_sum_u64", "gs_window_reduce_dist", "gs_window_fold_degree_max_dist",
            "gs_stream_create", "gs_stream_destroy", "gs_stream_append", "gs_stream_watermark", "gs_stream_flush",
            "gs_stream_poll", "gs_stream_stats", "gs_generate_rmat", "gs_generate_uniform", "gs_generate_zipf", "gs_generate_values", "gs_last_stage_times",
-           "gs_set_max_window_records", "gs_candidates_begin", "gs_candidates_next")
+           "gs_set_max_window_records", "gs_candidates_begin", "gs_candidates_next", "gs_candidates_seek",
+           "gs_candidates_vertex_range")
 
 P = ctypes.c_void_p
 u64, i64, i32, u32 = ctypes.c_uint64, ctypes.c_int64, ctypes.c_int32, ctypes.c_uint32
@@ -206,6 +207,8 @@ def load() -> ctypes.CDLL:
         "gs_set_max_window_records": (st, [P, u64]),
         "gs_candidates_begin": (st, [P, ctypes.POINTER(GsEdgeBatch), ctypes.POINTER(u64), ctypes.POINTER(u32)]),
         "gs_candidates_next": (st, [P, ctypes.POINTER(GsPairOut), ctypes.POINTER(u64), ctypes.POINTER(i32)]),
+        "gs_candidates_seek": (st, [P, u64]),
+        "gs_candidates_vertex_range": (st, [P, i64, ctypes.POINTER(u64), ctypes.POINTER(u64)]),
     }
     for name, (res, args) in sigs.items():
         f = getattr(L, name)

@@ -195,163 +195,165 @@ __global__ __launch_bounds__(256) void k_hs_gt(const int64_t* __restrict__ ids, 
   }
 }
 
-// row q emits (ids[q], ids[j]) for j >= q with ids[j] > v; only rows q < end-1 with ids[q] > v (:104, :108);
-// with a split (nparts > 1) only vertices this part owns emit
-__global__ __launch_bounds__(256) void k_hs_rowlen(const uint64_t* __restrict__ gx, uint32_t M,
-                                                   const uint64_t* __restrict__ doff, uint32_t U,
-                                                   const int64_t* __restrict__ ids, const int64_t* __restrict__ vkeys,
-                                                   uint32_t nparts, uint32_t part, uint64_t* __restrict__ L) {
-  for (uint32_t q = blockIdx.x * 256u + threadIdx.x; q < M; q += gridDim.x * 256u) {
-    const uint32_t u = seg_of(doff, U, q);
-    const uint64_t end = doff[u + 1];
-    const bool gt = ids[q] > vkeys[u];
-    const bool own = nparts <= 1 || owner_of(vkeys[u], nparts) == part;
-    L[q] = (own && gt && q + 1 < end) ? (gx[end] - gx[q]) : 0ull;
-  }
-}
+// ---- emission by output position (whole windows and chunks alike) ------------------------------------
+// Output order (gs_window_candidates): the emitting vertices ascending ("slots": every vertex, or with a
+// split the vertices this part owns); per slot its d edge records (v, t, false) in arrival order
+// (:96-100), then its pair rows.  With G = the slot's ids > v in HashSet order (k of them), row r emits
+// (G[r], G[r]), (G[r], G[r+1]), .., (G[r], G[k-1]) (:104-114: j >= i, both > v) for r < rows, where
+// rows = k - 1 when the set's last id is > v (i < len - 1 excludes it) and k otherwise.  So a slot's
+// block is d + rows*k - rows*(rows-1)/2 records and any position inverts in closed form: no per-row
+// state, no thread-per-row loop.
+struct CandMeta {     // one per slot, 32 bytes
+  uint64_t nbr_off;   // first edge record (HS_NBR)
+  uint64_t gbase;     // first id > v (HS_GIDS)
+  uint32_t d;         // edge records
+  uint32_t k;         // distinct ids > v
+  uint32_t rows;      // pair rows
+  uint32_t u;         // vertex index (HS_VKEYS)
+};
+static_assert(sizeof(CandMeta) == 32, "CandMeta");
 
-// owned vertices' record counts (their edge records, in the split's output order)
-__global__ __launch_bounds__(256) void k_hs_owned_recs(const uint64_t* __restrict__ off, uint32_t U,
-                                                       const int64_t* __restrict__ vkeys, uint32_t nparts, uint32_t part,
-                                                       uint64_t* __restrict__ F) {
+__device__ __forceinline__ uint64_t tri_rows_before(uint64_t r, uint64_t k) { return r * k - r * (r - 1) / 2; }
+
+// G: the ids > v of every vertex, compacted in HashSet order (position gx[q])
+__global__ __launch_bounds__(256) void k_cand_gids(const int64_t* __restrict__ ids, const uint64_t* __restrict__ g,
+                                                   const uint64_t* __restrict__ gx, uint32_t M,
+                                                   int64_t* __restrict__ gids) {
+  for (uint32_t q = blockIdx.x * 256u + threadIdx.x; q < M; q += gridDim.x * 256u)
+    if (g[q]) gids[gx[q]] = ids[q];
+}
+// split: own[u] = 1 iff gs_owner_of assigns vertex u to `part`
+__global__ __launch_bounds__(256) void k_cand_own(const int64_t* __restrict__ vkeys, uint32_t U, uint32_t nparts,
+                                                  uint32_t part, uint64_t* __restrict__ own) {
   for (uint32_t u = blockIdx.x * 256u + threadIdx.x; u < U; u += gridDim.x * 256u)
-    F[u] = owner_of(vkeys[u], nparts) == part ? off[u + 1] - off[u] : 0ull;
+    own[u] = owner_of(vkeys[u], nparts) == part ? 1ull : 0ull;
 }
-
-// record p of vertex u -> position fo[u] + (p - off[u]) + LS[doff[u]] (fo == off without a split)
-__global__ __launch_bounds__(256) void k_hs_emit_false(uint32_t R, const uint32_t* __restrict__ useg,
-                                                       const uint64_t* __restrict__ off, const uint64_t* __restrict__ fo,
-                                                       const uint64_t* __restrict__ doff, const uint64_t* __restrict__ LS,
-                                                       const int64_t* __restrict__ vkeys, const int64_t* __restrict__ nbr,
-                                                       uint32_t nparts, uint32_t part,
-                                                       int64_t* __restrict__ a, int64_t* __restrict__ b,
-                                                       uint8_t* __restrict__ f) {
-  for (uint32_t p = blockIdx.x * 256u + threadIdx.x; p < R; p += gridDim.x * 256u) {
-    const uint32_t u = useg[p];
-    if (nparts > 1 && owner_of(vkeys[u], nparts) != part) continue;
-    const uint64_t pos = fo[u] + (p - off[u]) + LS[doff[u]];
-    a[pos] = vkeys[u];
-    b[pos] = nbr[p];
-    f[pos] = 0;
+// slot metadata and block sizes (slot_of: exclusive scan of own, or null = every vertex is a slot)
+__global__ __launch_bounds__(256) void k_cand_meta(const uint64_t* __restrict__ off, const uint64_t* __restrict__ doff,
+                                                   const uint64_t* __restrict__ g, const uint64_t* __restrict__ gx,
+                                                   uint32_t U, const uint64_t* __restrict__ own,
+                                                   const uint64_t* __restrict__ slot_of, CandMeta* __restrict__ meta,
+                                                   uint64_t* __restrict__ size) {
+  for (uint32_t u = blockIdx.x * 256u + threadIdx.x; u < U; u += gridDim.x * 256u) {
+    if (own && !own[u]) continue;
+    const uint32_t s = slot_of ? (uint32_t)slot_of[u] : u;
+    const uint64_t q0 = doff[u], q1 = doff[u + 1], gb = gx[q0], k = gx[q1] - gb;
+    const uint64_t rows = k ? k - g[q1 - 1] : 0;
+    CandMeta m;
+    m.nbr_off = off[u];
+    m.gbase = gb;
+    m.d = (uint32_t)(off[u + 1] - off[u]);
+    m.k = (uint32_t)k;
+    m.rows = (uint32_t)rows;
+    m.u = u;
+    meta[s] = m;
+    size[s] = m.d + tri_rows_before(rows, k);
   }
 }
 
-__global__ __launch_bounds__(256) void k_hs_emit_pairs(uint32_t M, const uint64_t* __restrict__ doff, uint32_t U,
-                                                       const uint64_t* __restrict__ off, const uint64_t* __restrict__ LS,
-                                                       const int64_t* __restrict__ ids, const int64_t* __restrict__ vkeys,
-                                                       int64_t* __restrict__ a, int64_t* __restrict__ b,
-                                                       uint8_t* __restrict__ f) {
-  for (uint32_t q = blockIdx.x * 256u + threadIdx.x; q < M; q += gridDim.x * 256u) {
-    if (LS[q + 1] == LS[q]) continue;
-    const uint32_t u = seg_of(doff, U, q);
-    const int64_t v = vkeys[u], xi = ids[q];
-    uint64_t o = off[u + 1] + LS[q];
-    const uint64_t end = doff[u + 1];
-    for (uint64_t j = q; j < end; ++j) {
-      const int64_t xj = ids[j];
-      if (xj > v) {
-        a[o] = xi;
-        b[o] = xj;
-        f[o] = 1;
-        ++o;
+// The records at output positions [P0, P1), written to a/b/f[o - P0].  Each wave owns per_wave
+// consecutive positions (a multiple of 256) and walks them 256 at a time, lane l taking positions
+// base + 64 i + l: every store of a wave is one contiguous run (512 B of a, 512 B of b, 64 B of f).
+// A wave finds the slot of its first position by a 64-ary search of the block starts vs[0..S]; each
+// 256-position step then resolves its positions against 64 consecutive block starts held one per lane
+// (binary search through lane shuffles; a step that spans more than 64 slots takes the next 64).
+__global__ __launch_bounds__(256) void k_cand_emit(const uint64_t* __restrict__ vs, uint32_t S,
+                                                   const CandMeta* __restrict__ meta, const int64_t* __restrict__ vkeys,
+                                                   const int64_t* __restrict__ nbr, const int64_t* __restrict__ gids,
+                                                   uint64_t P0, uint64_t P1, uint64_t per_wave,
+                                                   int64_t* __restrict__ a, int64_t* __restrict__ b,
+                                                   uint8_t* __restrict__ f) {
+  const uint32_t lane = threadIdx.x & 63;
+  const uint64_t wave = ((uint64_t)blockIdx.x * 256u + threadIdx.x) >> 6;
+  const uint64_t w0 = P0 + wave * per_wave;
+  if (w0 >= P1) return;   // wave-uniform
+  const uint64_t w1 = min(P1, w0 + per_wave);
+  // slot of w0: invariant vs[lo] <= w0 and (hi == S or vs[hi] > w0); vs[0] = 0 <= P0
+  uint32_t lo = 0, hi = S;
+  while (hi - lo > 1) {
+    const uint32_t step = (hi - lo + 63) / 64;
+    const uint64_t idx = (uint64_t)lo + (uint64_t)lane * step;
+    const bool t = idx < hi && vs[idx] <= w0;
+    const uint64_t m = __ballot(t);
+    const uint32_t L = 63 - __clzll(m);
+    const uint32_t nlo = lo + L * step;
+    hi = min(hi, nlo + step);
+    lo = nlo;
+  }
+  uint32_t sc = lo;
+  for (uint64_t base = w0; base < w1; base += 256) {
+    uint64_t o[4];
+    uint32_t slot[4];
+    bool need[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      o[i] = base + (uint64_t)(i * 64) + lane;
+      need[i] = o[i] < w1;
+      slot[i] = sc;
+    }
+    for (uint32_t s0 = sc;; s0 += 64) {
+      const uint64_t bj = (uint64_t)s0 + 1 + lane <= S ? vs[s0 + 1 + lane] : ~0ull;
+      bool pend = false;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        int pos = 0;   // block starts vs[s0 + 1 ..] at or below o[i]
+#pragma unroll
+        for (int st = 32; st > 0; st >>= 1) {
+          const uint64_t v = __shfl(bj, pos + st - 1, 64);
+          pos += v <= o[i] ? st : 0;
+        }
+        if (need[i] && pos < 64) {
+          slot[i] = s0 + pos;
+          need[i] = false;
+        }
+        pend |= need[i];
       }
+      if (!__any(pend)) break;
     }
-  }
-}
-
-// ---- chunked emission: the records at global output positions [P0, P1) ---------------------------
-// The whole window's output order (gs_window_candidates): vertex u's edge records at p + LS[doff[u]]
-// (p = its record positions, off[u] .. off[u+1]), then its pair rows, row q at off[u+1] + LS[q] with
-// L[q] = LS[q+1] - LS[q] pairs.  Both position maps are monotone, so one thread finds by binary search
-// the records p in [b[0], b[1]) and the rows q in [b[2], b[3]) that reach into the range.
-__global__ void k_cand_bounds(const uint32_t* __restrict__ useg, uint32_t R, const uint64_t* __restrict__ off,
-                              const uint64_t* __restrict__ doff, uint32_t U, uint32_t M,
-                              const uint64_t* __restrict__ LS, uint64_t P0, uint64_t P1,
-                              unsigned long long* __restrict__ b) {
-  auto rpos = [&](uint32_t p) { return (uint64_t)p + LS[doff[useg[p]]]; };
-  auto first_rec = [&](uint64_t P) {   // first p with rpos(p) >= P
-    uint32_t lo = 0, hi = R;
-    while (lo < hi) {
-      const uint32_t mid = lo + (hi - lo) / 2;
-      if (rpos(mid) >= P) hi = mid;
-      else lo = mid + 1;
-    }
-    return lo;
-  };
-  auto rend = [&](uint32_t q) { return off[seg_of(doff, U, q) + 1] + LS[q + 1]; };    // row end position
-  auto rbeg = [&](uint32_t q) { return off[seg_of(doff, U, q) + 1] + LS[q]; };
-  auto first_row = [&](uint64_t P, bool by_end) {   // first q with end > P (by_end) / begin >= P
-    uint32_t lo = 0, hi = M;
-    while (lo < hi) {
-      const uint32_t mid = lo + (hi - lo) / 2;
-      if (by_end ? rend(mid) > P : rbeg(mid) >= P) hi = mid;
-      else lo = mid + 1;
-    }
-    return lo;
-  };
-  b[0] = first_rec(P0);
-  b[1] = first_rec(P1);
-  b[2] = first_row(P0, true);
-  b[3] = first_row(P1, false);
-}
-
-__global__ __launch_bounds__(256) void k_hs_emit_false_range(const uint32_t* __restrict__ useg,
-                                                             const uint64_t* __restrict__ doff,
-                                                             const uint64_t* __restrict__ LS,
-                                                             const int64_t* __restrict__ vkeys,
-                                                             const int64_t* __restrict__ nbr,
-                                                             const unsigned long long* __restrict__ bnd, uint64_t P0,
-                                                             int64_t* __restrict__ a, int64_t* __restrict__ b,
-                                                             uint8_t* __restrict__ f) {
-  const uint64_t p0 = bnd[0], p1 = bnd[1];
-  for (uint64_t p = p0 + blockIdx.x * 256ull + threadIdx.x; p < p1; p += (uint64_t)gridDim.x * 256u) {
-    const uint32_t u = useg[p];
-    const uint64_t pos = p + LS[doff[u]] - P0;
-    a[pos] = vkeys[u];
-    b[pos] = nbr[p];
-    f[pos] = 0;
-  }
-}
-
-// row q's pairs that fall in [P0, P1): the first one found by binary search over gx (the scan of the
-// "> v" flags: the t-th pair of row q is the j >= q with gx[j] - gx[q] == t and ids[j] > v)
-__global__ __launch_bounds__(256) void k_hs_emit_pairs_range(const uint64_t* __restrict__ doff, uint32_t U,
-                                                             const uint64_t* __restrict__ off,
-                                                             const uint64_t* __restrict__ LS,
-                                                             const uint64_t* __restrict__ gx,
-                                                             const int64_t* __restrict__ ids,
-                                                             const int64_t* __restrict__ vkeys,
-                                                             const unsigned long long* __restrict__ bnd, uint64_t P0,
-                                                             uint64_t P1, int64_t* __restrict__ a,
-                                                             int64_t* __restrict__ b, uint8_t* __restrict__ f) {
-  const uint64_t q0 = bnd[2], q1 = bnd[3];
-  for (uint64_t q = q0 + blockIdx.x * 256ull + threadIdx.x; q < q1; q += (uint64_t)gridDim.x * 256u) {
-    if (LS[q + 1] == LS[q]) continue;
-    const uint32_t u = seg_of(doff, U, q);
-    const int64_t v = vkeys[u], xi = ids[q];
-    const uint64_t rb = off[u + 1] + LS[q], end = doff[u + 1];
-    uint64_t o = rb, j = q;
-    if (rb < P0) {   // skip the row's first P0 - rb pairs
-      const uint64_t t = P0 - rb;
-      uint64_t lo = q, hi = end - 1;   // smallest j with gx[j + 1] - gx[q] > t
-      while (lo < hi) {
-        const uint64_t mid = (lo + hi) / 2;
-        if (gx[mid + 1] - gx[q] > t) hi = mid;
-        else lo = mid + 1;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      if (o[i] >= w1) continue;
+      const uint32_t sl = slot[i];
+      const CandMeta m = meta[sl];
+      const uint64_t t = o[i] - vs[sl];
+      int64_t av, bv;
+      uint8_t fv;
+      if (t < m.d) {
+        av = vkeys[m.u];
+        bv = nbr[m.nbr_off + t];
+        fv = 0;
+      } else {
+        const uint64_t q = t - m.d, k = m.k;
+        const double k2 = 2.0 * (double)k + 1.0;
+        uint64_t r = (uint64_t)fmax(0.0, (k2 - sqrt(fmax(0.0, k2 * k2 - 8.0 * (double)q))) * 0.5);
+        if (r >= m.rows) r = m.rows - 1;
+        while (r > 0 && tri_rows_before(r, k) > q) --r;
+        while (r + 1 < m.rows && tri_rows_before(r + 1, k) <= q) ++r;
+        const uint64_t col = q - tri_rows_before(r, k);
+        av = gids[m.gbase + r];
+        bv = gids[m.gbase + r + col];
+        fv = 1;
       }
-      j = lo;
-      o = P0;
+      a[o[i] - P0] = av;
+      b[o[i] - P0] = bv;
+      f[o[i] - P0] = fv;
     }
-    for (; j < end && o < P1; ++j) {
-      const int64_t xj = ids[j];
-      if (xj > v) {
-        a[o - P0] = xi;
-        b[o - P0] = xj;
-        f[o - P0] = 1;
-        ++o;
-      }
-    }
+    sc = __shfl(slot[3], 63, 64);   // the slot of this step's last position (the next step starts there)
   }
+}
+
+// the block of vertex `x` in the session's output: first position and length (0 records if absent)
+__global__ void k_cand_find(const int64_t* __restrict__ vkeys, uint32_t U, const uint64_t* __restrict__ vs, int64_t x,
+                            unsigned long long* __restrict__ out) {
+  uint32_t lo = 0, hi = U;
+  while (lo < hi) {
+    const uint32_t mid = lo + (hi - lo) / 2;
+    if (vkeys[mid] < x) lo = mid + 1;
+    else hi = mid;
+  }
+  const bool hit = lo < U && vkeys[lo] == x;
+  out[0] = hit ? vs[lo] : (lo < U ? vs[lo] : vs[U]);
+  out[1] = hit ? vs[lo + 1] - vs[lo] : 0ull;
 }
 
 // self-pair term of WindowTriangles: matched (x, x, true) candidates need a self-loop on x
@@ -749,9 +751,10 @@ using namespace gs;
 namespace gs {
 
 enum { HS_VKEYS, HS_OFF, HS_NBR, HS_USEG, HS_COMP, HS_PIDX, HS_DKEY, HS_DFIRST, HS_DOFF, HS_OKEY, HS_OMID,
-       HS_UKEY, HS_ORD, HS_IDS, HS_G, HS_GX, HS_L, HS_LS, HS_TILES, HS_F, HS_FX, HS_CSZ, HS_CBASE, HS_CNT, HS_CPLX,
-       HS_CLIST, HS_TSZ, HS_TBASE, HS_ARR, HS_NODES, HS_TABS, HS_FO, HS_COUNT };
-static_assert(HS_COUNT <= 32, "gs_ctx::hs");
+       HS_UKEY, HS_ORD, HS_IDS, HS_G, HS_GX, HS_TILES, HS_F, HS_FX, HS_CSZ, HS_CBASE, HS_CNT, HS_CPLX,
+       HS_CLIST, HS_TSZ, HS_TBASE, HS_ARR, HS_NODES, HS_TABS, HS_GIDS, HS_OWN, HS_SLOT, HS_META, HS_SIZE, HS_VS,
+       HS_COUNT };
+static_assert(HS_COUNT <= 40, "gs_ctx::hs");
 
 gs_status xscan(gs_ctx* c, const uint64_t* in, uint64_t n, uint64_t* out) {
   const uint32_t tiles = (uint32_t)std::max<uint64_t>(1, (n + XS_TILE - 1) / XS_TILE);
@@ -929,6 +932,66 @@ gs_status triangle_selfpair_term(gs_ctx* c, const int64_t* src, const int64_t* d
   return GS_OK;
 }
 
+// Layout of a window's candidate output (see k_cand_emit): the "> v" flags and their scan, the compacted
+// ids G, per-slot metadata and block starts vs[0..S] (vs[S] = the record count).  nparts > 1: only the
+// vertices gs_owner_of assigns to `part` are slots.
+static gs_status cand_layout(gs_ctx* c, uint32_t U, uint32_t M, uint32_t nparts, uint32_t part, uint32_t* S_out,
+                             uint64_t* total) {
+  GS_TRY(ensure(c, c->hs[HS_G], (M + 1) * 8));
+  GS_TRY(ensure(c, c->hs[HS_GX], (M + 1) * 8));
+  GS_TRY(ensure(c, c->hs[HS_GIDS], (M + 1) * 8));
+  hipLaunchKernelGGL(k_hs_gt, dim3(g256(M)), dim3(256), 0, c->stream, c->hs[HS_IDS].as<int64_t>(), M,
+                     c->hs[HS_DOFF].as<uint64_t>(), U, c->hs[HS_VKEYS].as<int64_t>(), c->hs[HS_G].as<uint64_t>());
+  GS_HIP(hipGetLastError());
+  GS_TRY(xscan(c, c->hs[HS_G].as<uint64_t>(), M, c->hs[HS_GX].as<uint64_t>()));
+  hipLaunchKernelGGL(k_cand_gids, dim3(g256(M)), dim3(256), 0, c->stream, c->hs[HS_IDS].as<int64_t>(),
+                     c->hs[HS_G].as<uint64_t>(), c->hs[HS_GX].as<uint64_t>(), M, c->hs[HS_GIDS].as<int64_t>());
+  GS_HIP(hipGetLastError());
+  const uint64_t *own = nullptr, *slot_of = nullptr;
+  uint32_t S = U;
+  if (nparts > 1) {
+    GS_TRY(ensure(c, c->hs[HS_OWN], (size_t)(U + 1) * 8));
+    GS_TRY(ensure(c, c->hs[HS_SLOT], (size_t)(U + 1) * 8));
+    hipLaunchKernelGGL(k_cand_own, dim3(g256(U)), dim3(256), 0, c->stream, c->hs[HS_VKEYS].as<int64_t>(), U, nparts,
+                       part, c->hs[HS_OWN].as<uint64_t>());
+    GS_HIP(hipGetLastError());
+    GS_TRY(xscan(c, c->hs[HS_OWN].as<uint64_t>(), U, c->hs[HS_SLOT].as<uint64_t>()));
+    c->host_small[6] = 0;
+    GS_HIP(hipMemcpyAsync(&c->host_small[6], c->hs[HS_SLOT].as<uint64_t>() + U, 8, hipMemcpyDeviceToHost, c->stream));
+    GS_TRY(host_wait(c));
+    S = (uint32_t)c->host_small[6];
+    own = c->hs[HS_OWN].as<uint64_t>();
+    slot_of = c->hs[HS_SLOT].as<uint64_t>();
+  }
+  GS_TRY(ensure(c, c->hs[HS_META], (size_t)(S + 1) * sizeof(CandMeta)));
+  GS_TRY(ensure(c, c->hs[HS_SIZE], (size_t)(S + 1) * 8));
+  GS_TRY(ensure(c, c->hs[HS_VS], (size_t)(S + 1) * 8));
+  hipLaunchKernelGGL(k_cand_meta, dim3(g256(U)), dim3(256), 0, c->stream, c->hs[HS_OFF].as<uint64_t>(),
+                     c->hs[HS_DOFF].as<uint64_t>(), c->hs[HS_G].as<uint64_t>(), c->hs[HS_GX].as<uint64_t>(), U, own,
+                     slot_of, c->hs[HS_META].as<CandMeta>(), c->hs[HS_SIZE].as<uint64_t>());
+  GS_HIP(hipGetLastError());
+  GS_TRY(xscan(c, c->hs[HS_SIZE].as<uint64_t>(), S, c->hs[HS_VS].as<uint64_t>()));
+  c->host_small[7] = 0;
+  GS_HIP(hipMemcpyAsync(&c->host_small[7], c->hs[HS_VS].as<uint64_t>() + S, 8, hipMemcpyDeviceToHost, c->stream));
+  GS_TRY(host_wait(c));
+  *S_out = S;
+  *total = c->host_small[7];
+  return GS_OK;
+}
+
+// records [P0, P1) of the layout into a / b / f (device)
+static gs_status cand_emit(gs_ctx* c, uint32_t S, uint64_t P0, uint64_t P1, int64_t* a, int64_t* b, uint8_t* f) {
+  const uint64_t n = P1 - P0;
+  if (n == 0) return GS_OK;
+  const uint64_t blocks = std::max<uint64_t>(1, std::min<uint64_t>((n + 4095) / 4096, 4096));
+  const uint64_t waves = blocks * 4;
+  const uint64_t per_wave = ((n + waves - 1) / waves + 255) / 256 * 256;
+  hipLaunchKernelGGL(k_cand_emit, dim3((unsigned)blocks), dim3(256), 0, c->stream, c->hs[HS_VS].as<uint64_t>(), S,
+                     c->hs[HS_META].as<CandMeta>(), c->hs[HS_VKEYS].as<int64_t>(), c->hs[HS_NBR].as<int64_t>(),
+                     c->hs[HS_GIDS].as<int64_t>(), P0, P1, per_wave, a, b, f);
+  return hip_check(c, hipGetLastError(), "k_cand_emit");
+}
+
 }  // namespace gs
 
 extern "C" {
@@ -948,44 +1011,12 @@ gs_status gs_window_candidates_part(gs_ctx* c, const gs_edge_batch* b, uint32_t 
   const int64_t *src, *dst;
   const void* val;
   GS_TRY(stage_batch(c, b, &src, &dst, &val, false));
-  const uint64_t R = 2 * b->n;
-  uint32_t U = 0, M = 0;
-  uint64_t key_xor = 0;
+  uint32_t U = 0, M = 0, S = 0;
+  uint64_t key_xor = 0, total = 0;
   uint32_t jdk_flags = 0;
   GS_TRY(hashset_order(c, src, dst, b->n, &U, &M, &key_xor, &jdk_flags));
   out->reserved = jdk_flags;   // bit 0 = a treeified bin, bit 1 = a collision resize (both simulated exactly)
-  // rows: gt flags -> scan -> row lengths -> scan
-  GS_TRY(ensure(c, c->hs[HS_G], (M + 1) * 8));
-  GS_TRY(ensure(c, c->hs[HS_GX], (M + 1) * 8));
-  GS_TRY(ensure(c, c->hs[HS_L], (M + 1) * 8));
-  GS_TRY(ensure(c, c->hs[HS_LS], (M + 1) * 8));
-  hipLaunchKernelGGL(k_hs_gt, dim3(g256(M)), dim3(256), 0, c->stream, c->hs[HS_IDS].as<int64_t>(), M,
-                     c->hs[HS_DOFF].as<uint64_t>(), U, c->hs[HS_VKEYS].as<int64_t>(), c->hs[HS_G].as<uint64_t>());
-  GS_HIP(hipGetLastError());
-  GS_TRY(xscan(c, c->hs[HS_G].as<uint64_t>(), M, c->hs[HS_GX].as<uint64_t>()));
-  hipLaunchKernelGGL(k_hs_rowlen, dim3(g256(M)), dim3(256), 0, c->stream, c->hs[HS_GX].as<uint64_t>(), M,
-                     c->hs[HS_DOFF].as<uint64_t>(), U, c->hs[HS_IDS].as<int64_t>(), c->hs[HS_VKEYS].as<int64_t>(),
-                     nparts, part, c->hs[HS_L].as<uint64_t>());
-  GS_HIP(hipGetLastError());
-  GS_TRY(xscan(c, c->hs[HS_L].as<uint64_t>(), M, c->hs[HS_LS].as<uint64_t>()));
-  // output position of each vertex's records: the record CSR (every vertex), or, with a split, the
-  // scan of the owned vertices' record counts
-  const uint64_t* off = c->hs[HS_OFF].as<uint64_t>();
-  const uint64_t* fo = off;
-  if (nparts > 1) {
-    GS_TRY(ensure(c, c->hs[HS_FO], (size_t)(U + 1) * 8 * 2));
-    uint64_t* F = c->hs[HS_FO].as<uint64_t>() + (U + 1);
-    hipLaunchKernelGGL(k_hs_owned_recs, dim3(g256(U)), dim3(256), 0, c->stream, off, U, c->hs[HS_VKEYS].as<int64_t>(),
-                       nparts, part, F);
-    GS_HIP(hipGetLastError());
-    GS_TRY(xscan(c, F, U, c->hs[HS_FO].as<uint64_t>()));
-    fo = c->hs[HS_FO].as<uint64_t>();
-  }
-  GS_HIP(hipMemcpyAsync(&c->host_small[7], c->hs[HS_LS].as<uint64_t>() + M, 8, hipMemcpyDeviceToHost, c->stream));
-  GS_HIP(hipMemcpyAsync(&c->host_small[6], fo + U, 8, hipMemcpyDeviceToHost, c->stream));
-  GS_TRY(host_wait(c));
-  const uint64_t P = c->host_small[7];
-  const uint64_t total = c->host_small[6] + P;   // edge records (R without a split) + pairs
+  GS_TRY(cand_layout(c, U, M, nparts, part, &S, &total));
   *out->n_out = total;
   if (total > out->capacity) return set_error(c, GS_ECAPACITY, "candidates need %llu records", (unsigned long long)total);
   int64_t *a = out->a, *bb = out->b;
@@ -999,13 +1030,7 @@ gs_status gs_window_candidates_part(gs_ctx* c, const gs_edge_batch* b, uint32_t 
     bb = c->out_a.as<int64_t>();
     f = c->out_b.as<uint8_t>();
   }
-  hipLaunchKernelGGL(k_hs_emit_false, dim3(g256(R)), dim3(256), 0, c->stream, (uint32_t)R, c->hs[HS_USEG].as<uint32_t>(),
-                     off, fo, c->hs[HS_DOFF].as<uint64_t>(), c->hs[HS_LS].as<uint64_t>(), c->hs[HS_VKEYS].as<int64_t>(),
-                     c->hs[HS_NBR].as<int64_t>(), nparts, part, a, bb, f);
-  hipLaunchKernelGGL(k_hs_emit_pairs, dim3(g256(M)), dim3(256), 0, c->stream, M, c->hs[HS_DOFF].as<uint64_t>(), U,
-                     fo, c->hs[HS_LS].as<uint64_t>(), c->hs[HS_IDS].as<int64_t>(),
-                     c->hs[HS_VKEYS].as<int64_t>(), a, bb, f);
-  GS_HIP(hipGetLastError());
+  GS_TRY(cand_emit(c, S, 0, total, a, bb, f));
   if (!direct) {
     GS_HIP(hipMemcpyAsync(out->a, a, total * 8, hipMemcpyDeviceToHost, c->stream));
     GS_HIP(hipMemcpyAsync(out->b, bb, total * 8, hipMemcpyDeviceToHost, c->stream));
@@ -1024,48 +1049,37 @@ gs_status gs_candidates_begin(gs_ctx* c, const gs_edge_batch* b, uint64_t* total
   if (!total_records) return set_error(c, GS_EINVAL, "null total_records");
   GS_TRY(begin_call(c));
   c->cand_seq = c->call_seq;
-  c->cand_total = c->cand_cursor = c->cand_R = 0;
-  c->cand_U = c->cand_M = 0;
+  c->cand_total = c->cand_cursor = 0;
+  c->cand_U = c->cand_S = 0;
   *total_records = 0;
   if (jdk_flags) *jdk_flags = 0;
   if (b->n == 0) return GS_OK;
   const int64_t *src, *dst;
   const void* val;
   GS_TRY(stage_batch(c, b, &src, &dst, &val, false));
-  uint32_t U = 0, M = 0, fl = 0;
-  uint64_t key_xor = 0;
+  uint32_t U = 0, M = 0, S = 0, fl = 0;
+  uint64_t key_xor = 0, total = 0;
   GS_TRY(hashset_order(c, src, dst, b->n, &U, &M, &key_xor, &fl));
-  GS_TRY(ensure(c, c->hs[HS_G], (M + 1) * 8));
-  GS_TRY(ensure(c, c->hs[HS_GX], (M + 1) * 8));
-  GS_TRY(ensure(c, c->hs[HS_L], (M + 1) * 8));
-  GS_TRY(ensure(c, c->hs[HS_LS], (M + 1) * 8));
-  hipLaunchKernelGGL(k_hs_gt, dim3(g256(M)), dim3(256), 0, c->stream, c->hs[HS_IDS].as<int64_t>(), M,
-                     c->hs[HS_DOFF].as<uint64_t>(), U, c->hs[HS_VKEYS].as<int64_t>(), c->hs[HS_G].as<uint64_t>());
-  GS_HIP(hipGetLastError());
-  GS_TRY(xscan(c, c->hs[HS_G].as<uint64_t>(), M, c->hs[HS_GX].as<uint64_t>()));
-  hipLaunchKernelGGL(k_hs_rowlen, dim3(g256(M)), dim3(256), 0, c->stream, c->hs[HS_GX].as<uint64_t>(), M,
-                     c->hs[HS_DOFF].as<uint64_t>(), U, c->hs[HS_IDS].as<int64_t>(), c->hs[HS_VKEYS].as<int64_t>(),
-                     1u, 0u, c->hs[HS_L].as<uint64_t>());
-  GS_HIP(hipGetLastError());
-  GS_TRY(xscan(c, c->hs[HS_L].as<uint64_t>(), M, c->hs[HS_LS].as<uint64_t>()));
-  GS_HIP(hipMemcpyAsync(&c->host_small[7], c->hs[HS_LS].as<uint64_t>() + M, 8, hipMemcpyDeviceToHost, c->stream));
-  GS_TRY(host_wait(c));
+  GS_TRY(cand_layout(c, U, M, 1, 0, &S, &total));
   c->cand_U = U;
-  c->cand_M = M;
-  c->cand_R = 2 * b->n;
-  c->cand_total = 2 * b->n + c->host_small[7];
-  *total_records = c->cand_total;
+  c->cand_S = S;
+  c->cand_total = total;
+  *total_records = total;
   if (jdk_flags) *jdk_flags = fl;
   return GS_OK;
+}
+
+static gs_status cand_session(gs_ctx* c) {
+  if (c->cand_seq != c->call_seq)
+    return set_error(c, GS_EINVAL, "no candidates session (gs_candidates_begin; a later call on the ctx ends it)");
+  return hip_check(c, hipSetDevice(c->device), "hipSetDevice");
 }
 
 gs_status gs_candidates_next(gs_ctx* c, gs_pair_out* out, uint64_t* first_record, int32_t* done) {
   if (!c) return GS_EINVAL;
   if (!out || !out->n_out || (out->capacity && (!out->a || !out->b || !out->is_candidate)))
     return set_error(c, GS_EINVAL, "bad gs_pair_out");
-  if (c->cand_seq != c->call_seq)
-    return set_error(c, GS_EINVAL, "no candidates session (gs_candidates_begin; a later call on the ctx ends it)");
-  GS_HIP(hipSetDevice(c->device));
+  GS_TRY(cand_session(c));
   const uint64_t P0 = c->cand_cursor, n = std::min<uint64_t>(out->capacity, c->cand_total - P0), P1 = P0 + n;
   if (first_record) *first_record = P0;
   *out->n_out = n;
@@ -1075,7 +1089,6 @@ gs_status gs_candidates_next(gs_ctx* c, gs_pair_out* out, uint64_t* first_record
     if (c->cand_total > P0 && out->capacity == 0) return set_error(c, GS_ECAPACITY, "capacity 0");
     return GS_OK;
   }
-  const uint32_t U = c->cand_U, M = c->cand_M;
   int64_t *a = out->a, *bb = out->b;
   uint8_t* f = out->is_candidate;
   const bool direct = out->mem == GS_MEM_DEVICE;
@@ -1088,20 +1101,7 @@ gs_status gs_candidates_next(gs_ctx* c, gs_pair_out* out, uint64_t* first_record
     bb = c->out_a.as<int64_t>();
     f = c->out_b.as<uint8_t>();
   }
-  GS_TRY(ensure(c, c->cand_bounds, 64));
-  auto* bnd = c->cand_bounds.as<unsigned long long>();
-  const uint64_t* off = c->hs[HS_OFF].as<uint64_t>();
-  const uint64_t recs = c->cand_R;
-  hipLaunchKernelGGL(k_cand_bounds, dim3(1), dim3(1), 0, c->stream, c->hs[HS_USEG].as<uint32_t>(), (uint32_t)recs, off,
-                     c->hs[HS_DOFF].as<uint64_t>(), U, M, c->hs[HS_LS].as<uint64_t>(), P0, P1, bnd);
-  const unsigned grid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((n + 255) / 256, 8192));
-  hipLaunchKernelGGL(k_hs_emit_false_range, dim3(grid), dim3(256), 0, c->stream, c->hs[HS_USEG].as<uint32_t>(),
-                     c->hs[HS_DOFF].as<uint64_t>(), c->hs[HS_LS].as<uint64_t>(), c->hs[HS_VKEYS].as<int64_t>(),
-                     c->hs[HS_NBR].as<int64_t>(), bnd, P0, a, bb, f);
-  hipLaunchKernelGGL(k_hs_emit_pairs_range, dim3((unsigned)std::min<uint64_t>(g256(M), 8192)), dim3(256), 0, c->stream,
-                     c->hs[HS_DOFF].as<uint64_t>(), U, off, c->hs[HS_LS].as<uint64_t>(), c->hs[HS_GX].as<uint64_t>(),
-                     c->hs[HS_IDS].as<int64_t>(), c->hs[HS_VKEYS].as<int64_t>(), bnd, P0, P1, a, bb, f);
-  GS_HIP(hipGetLastError());
+  GS_TRY(cand_emit(c, c->cand_S, P0, P1, a, bb, f));
   if (!direct) {
     GS_HIP(hipMemcpyAsync(out->a, a, n * 8, hipMemcpyDeviceToHost, c->stream));
     GS_HIP(hipMemcpyAsync(out->b, bb, n * 8, hipMemcpyDeviceToHost, c->stream));
@@ -1110,6 +1110,34 @@ gs_status gs_candidates_next(gs_ctx* c, gs_pair_out* out, uint64_t* first_record
   GS_TRY(host_wait(c));
   c->cand_cursor = P1;
   if (done) *done = P1 >= c->cand_total;
+  return GS_OK;
+}
+
+gs_status gs_candidates_seek(gs_ctx* c, uint64_t record) {
+  if (!c) return GS_EINVAL;
+  GS_TRY(cand_session(c));
+  if (record > c->cand_total)
+    return set_error(c, GS_EINVAL, "seek to record %llu of %llu", (unsigned long long)record,
+                     (unsigned long long)c->cand_total);
+  c->cand_cursor = record;
+  return GS_OK;
+}
+
+gs_status gs_candidates_vertex_range(gs_ctx* c, int64_t vertex, uint64_t* first_record, uint64_t* records) {
+  if (!c) return GS_EINVAL;
+  if (!first_record || !records) return set_error(c, GS_EINVAL, "null output");
+  GS_TRY(cand_session(c));
+  *first_record = *records = 0;
+  if (c->cand_total == 0) return GS_OK;
+  GS_TRY(ensure(c, c->cand_bounds, 64));
+  auto* d = c->cand_bounds.as<unsigned long long>();
+  hipLaunchKernelGGL(k_cand_find, dim3(1), dim3(1), 0, c->stream, c->hs[HS_VKEYS].as<int64_t>(), c->cand_U,
+                     c->hs[HS_VS].as<uint64_t>(), vertex, d);
+  GS_HIP(hipGetLastError());
+  GS_HIP(hipMemcpyAsync(&c->host_small[6], d, 16, hipMemcpyDeviceToHost, c->stream));
+  GS_TRY(host_wait(c));
+  *first_record = c->host_small[6];
+  *records = c->host_small[7];
   return GS_OK;
 }
 

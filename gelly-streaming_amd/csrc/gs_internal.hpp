@@ -54,8 +54,8 @@ struct gs_ctx {
   gs::DevBuf ck_k[2], ck_a[2], ck_b[2];
   // chunked candidate emission (gs_candidates_begin / _next): the window's HashSet-ordered sets stay in
   // hs[] until the next entry point call on the ctx (call_seq) ends the session
-  uint64_t call_seq = 0, cand_seq = ~0ull, cand_total = 0, cand_cursor = 0, cand_R = 0;
-  uint32_t cand_U = 0, cand_M = 0;
+  uint64_t call_seq = 0, cand_seq = ~0ull, cand_total = 0, cand_cursor = 0;
+  uint32_t cand_U = 0, cand_S = 0;
   gs::DevBuf cand_bounds;
   // input staging (host batches)
   gs::DevBuf in_src, in_dst, in_val;
@@ -76,7 +76,7 @@ struct gs_ctx {
   uint32_t tri_B = 0;            // split-window triangles: id geometry of the current window
   uint64_t tri_key_xor = 0;
   // HashSet-order pipeline (gs_hashset.hip)
-  gs::DevBuf hs[32];
+  gs::DevBuf hs[40];
   // bucket path (gs_bucket.hip): plan tables, work items, LDS slabs of multi-item buckets
   gs::DevBuf bk_meta, bk_items, bk_slabs;
   // direct partition: per-tile bucket counts (u16), chunk sums, per-tile write offsets
@@ -162,7 +162,7 @@ gs_status sort_buffer(gs_ctx* c, const uint64_t* keys, const void* vals, uint64_
 
 // HashSet-ordered distinct neighbour sets of an ALL window (gs_hashset.hip)
 gs_status hashset_order(gs_ctx* c, const int64_t* src, const int64_t* dst, uint64_t n, uint32_t* U_out,
-                        uint32_t* M_out, uint64_t* key_xor_out, bool* treeified);
+                        uint32_t* M_out, uint64_t* key_xor_out, uint32_t* jdk_flags);
 // WindowTriangles self-pair term for windows with self-loops (loops: bitmap over compact IDs: x ^ loops_xor,
 // or, for a relabeled window, the rank of x among the sorted distinct IDs `relabel[0 .. nrel)`)
 gs_status triangle_selfpair_term(gs_ctx* c, const int64_t* src, const int64_t* dst, uint64_t n,

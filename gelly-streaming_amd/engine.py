@@ -265,6 +265,16 @@ class Engine:
         n = n_out.value
         return a[:n], bb[:n], f[:n], first.value, bool(done.value)
 
+    def candidates_seek(self, record: int):
+        """gs_candidates_seek: the session's next chunk starts at output position `record`."""
+        self._check(self._L.gs_candidates_seek(self.ctx, int(record)))
+
+    def candidates_vertex_range(self, vertex: int):
+        """gs_candidates_vertex_range: (first position, record count) of one vertex's block in the session."""
+        first, n = ctypes.c_uint64(0), ctypes.c_uint64(0)
+        self._check(self._L.gs_candidates_vertex_range(self.ctx, int(vertex), ctypes.byref(first), ctypes.byref(n)))
+        return first.value, n.value
+
     def candidate_count(self, src, dst) -> int:
         """Sizing call of gs_window_candidates (capacity 0): the number of records the window emits."""
         b, keep, dev = self._batch(src, dst, None)

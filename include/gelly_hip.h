@@ -224,6 +224,14 @@ GS_API gs_status gs_window_candidates(gs_ctx* ctx, const gs_edge_batch* batch, g
 GS_API gs_status gs_candidates_begin(gs_ctx* ctx, const gs_edge_batch* batch, uint64_t* total_records,
                                      uint32_t* jdk_flags);
 GS_API gs_status gs_candidates_next(gs_ctx* ctx, gs_pair_out* out, uint64_t* first_record, int32_t* done);
+/* Random access into the session (no reference counterpart: a consumer that restarts mid-window, or
+ * several consumers that split the output, e.g. one per downstream pair-keyed subtask).
+ * gs_candidates_seek moves the cursor: the next gs_candidates_next starts at `record` (<= the total).
+ * gs_candidates_vertex_range gives the block of one vertex: its records (edge records, then its pair rows)
+ * are [*first_record, *first_record + *records); a vertex absent from the window has *records = 0 and
+ * *first_record = where it would start.  Neither ends the session. */
+GS_API gs_status gs_candidates_seek(gs_ctx* ctx, uint64_t record);
+GS_API gs_status gs_candidates_vertex_range(gs_ctx* ctx, int64_t vertex, uint64_t* first_record, uint64_t* records);
 
 /* Multi-GPU candidates (partition by owner(v), no exchange of pairs): only the vertices
  * v with gs_owner_of(v, nparts) == part emit, with exactly the records gs_window_candidates gives them

@@ -128,17 +128,28 @@ JNIEXPORT jlongArray JNI_FN(windowTriangles)(JNIEnv* env, jclass cls, jlong ctx,
   return out;
 }
 
-JNIEXPORT jlong JNI_FN(candidatesBegin)(JNIEnv* env, jclass cls, jlong ctx, jobject src, jobject dst, jlong n) {
+static jlongArray long_array(JNIEnv* env, const jlong* v, jsize n) {
+  jlongArray out = (*env)->NewLongArray(env, n);
+  if (out) (*env)->SetLongArrayRegion(env, out, 0, n, v);
+  return out;
+}
+
+JNIEXPORT jlongArray JNI_FN(candidatesBegin)(JNIEnv* env, jclass cls, jlong ctx, jobject src, jobject dst, jlong n) {
   gs_ctx* c = (gs_ctx*)(intptr_t)ctx;
   gs_edge_batch b = batch(env, src, dst, NULL, n, GS_NONE);
   uint64_t total = 0;
   uint32_t flags = 0;
   gs_status s = gs_candidates_begin(c, &b, &total, &flags);
-  if (s != GS_OK) throw_status(env, c, s, "gs_candidates_begin");
-  return (jlong)total;
+  if (s != GS_OK) {
+    throw_status(env, c, s, "gs_candidates_begin");
+    return NULL;
+  }
+  const jlong r[2] = {(jlong)total, (jlong)flags};
+  return long_array(env, r, 2);
 }
 
-JNIEXPORT jlong JNI_FN(candidatesNext)(JNIEnv* env, jclass cls, jlong ctx, jobject a, jobject b, jobject f, jlong cap) {
+JNIEXPORT jlongArray JNI_FN(candidatesNext)(JNIEnv* env, jclass cls, jlong ctx, jobject a, jobject b, jobject f,
+                                            jlong cap) {
   gs_ctx* c = (gs_ctx*)(intptr_t)ctx;
   uint64_t n_out = 0, first = 0;
   int32_t done = 0;
@@ -147,9 +158,28 @@ JNIEXPORT jlong JNI_FN(candidatesNext)(JNIEnv* env, jclass cls, jlong ctx, jobje
   gs_status s = gs_candidates_next(c, &o, &first, &done);
   if (s != GS_OK) {
     throw_status(env, c, s, "gs_candidates_next");
-    return 0;
+    return NULL;
   }
-  return (jlong)n_out;
+  const jlong r[3] = {(jlong)n_out, (jlong)first, (jlong)done};
+  return long_array(env, r, 3);
+}
+
+JNIEXPORT void JNI_FN(candidatesSeek)(JNIEnv* env, jclass cls, jlong ctx, jlong record) {
+  gs_ctx* c = (gs_ctx*)(intptr_t)ctx;
+  gs_status s = gs_candidates_seek(c, (uint64_t)record);
+  if (s != GS_OK) throw_status(env, c, s, "gs_candidates_seek");
+}
+
+JNIEXPORT jlongArray JNI_FN(candidatesVertexRange)(JNIEnv* env, jclass cls, jlong ctx, jlong vertex) {
+  gs_ctx* c = (gs_ctx*)(intptr_t)ctx;
+  uint64_t first = 0, n = 0;
+  gs_status s = gs_candidates_vertex_range(c, (int64_t)vertex, &first, &n);
+  if (s != GS_OK) {
+    throw_status(env, c, s, "gs_candidates_vertex_range");
+    return NULL;
+  }
+  const jlong r[2] = {(jlong)first, (jlong)n};
+  return long_array(env, r, 2);
 }
 
 /* ---- gs_stream_*: the stream keeps its ctx (one per operator subtask) -------------------------------- */

@@ -103,12 +103,24 @@ public final class GellyHip {
 	/** gs_window_triangles: WindowTriangles.java:61-66 for one window -> {exact, Integer emitted, hasOutput}. */
 	static native long[] windowTriangles(long ctx, ByteBuffer src, ByteBuffer dst, long n);
 
-	/** gs_candidates_begin: GenerateCandidateEdges (WindowTriangles.java:83-116); returns the record count. */
-	static native long candidatesBegin(long ctx, ByteBuffer src, ByteBuffer dst, long n);
+	/**
+	 * gs_candidates_begin: GenerateCandidateEdges (WindowTriangles.java:83-116) over one window's columns;
+	 * returns {record count, JDK flags} (flags bit 0: a neighbour set used a treeified HashMap bin, bit 1: a
+	 * bin of 9 forced a resize below capacity 64 -- both simulated exactly).
+	 */
+	static native long[] candidatesBegin(long ctx, ByteBuffer src, ByteBuffer dst, long n);
 
-	/** gs_candidates_next: the next records of the session into (a, b, isCandidate); returns the count, 0 at
-	 * the end. */
-	static native long candidatesNext(long ctx, ByteBuffer a, ByteBuffer b, ByteBuffer isCandidate, long capacity);
+	/**
+	 * gs_candidates_next: the next records of the session into (a, b, isCandidate); returns {records
+	 * written, global position of the first, done (1 after the last record)}.
+	 */
+	static native long[] candidatesNext(long ctx, ByteBuffer a, ByteBuffer b, ByteBuffer isCandidate, long capacity);
+
+	/** gs_candidates_seek: the next candidatesNext starts at output position `record`. */
+	static native void candidatesSeek(long ctx, long record);
+
+	/** gs_candidates_vertex_range: {first position, records} of one vertex's block in the session. */
+	static native long[] candidatesVertexRange(long ctx, long vertex);
 
 	/* ---- the window-buffer operator (gs_stream_*): event-time tumbling windows ------------------------ */
 	static native long streamCreate(long ctx, long windowMs, int kind, int direction, int op, int valDtype,

@@ -26,6 +26,29 @@ public final class GpuBuiltins {
 		int op();
 	}
 
+	/**
+	 * An apply function the engine implements: the records of WindowTriangles.GenerateCandidateEdges
+	 * (WindowTriangles.java:83-116), which the dispatch patch marks with this interface.  Routed to
+	 * GpuCandidatesOperator (gs_candidates_begin / gs_candidates_next).
+	 */
+	public interface BuiltinApply {
+	}
+
+	/** Whether the dispatch is on: -Dgelly.gpu=false keeps every call on the Flink path. */
+	public static boolean enabled() {
+		return System.getProperty("gelly.gpu", "true").equals("true");
+	}
+
+	/**
+	 * Whether the engine takes these edges: Long vertex IDs (GpuWindowOperator reads Edge<Long, EV>) and
+	 * Integer / Long / Float / Double values, or none (NullValue) when the op needs no values.  Anything
+	 * else stays on Flink instead of failing with a ClassCastException in the operator.
+	 */
+	public static boolean supports(Class<?> keyClass, Class<?> valueClass, boolean needsValues) {
+		if (keyClass != Long.class) return false;
+		return dtypeOf(valueClass) != GellyHip.GS_NONE || !needsValues;
+	}
+
 	/** Long / Integer / Float / Double sum (Java wrapping for the integers). */
 	@SuppressWarnings({"serial", "unchecked"})
 	public static final class SumReduce<EV extends Number> implements EdgesReduce<EV>, Builtin {
@@ -71,6 +94,46 @@ public final class GpuBuiltins {
 		public Tuple2<Long, Long> foldEdges(Tuple2<Long, Long> acc, Long id, Long neighbor, Long value) {
 			acc.setField(id, 0);
 			acc.setField(acc.f1 + value, 1);
+			return acc;
+		}
+	}
+
+	/** foldNeighbors(new Tuple2<>(k, v0), new MinValuesFold()): (vertex, min(v0, values)). */
+	@SuppressWarnings("serial")
+	public static final class MinValuesFold implements EdgesFold<Long, Long, Tuple2<Long, Long>>, BuiltinFold {
+		public int op() { return GellyHip.GS_OP_MIN; }
+
+		public Tuple2<Long, Long> foldEdges(Tuple2<Long, Long> acc, Long id, Long neighbor, Long value) {
+			acc.setField(id, 0);
+			acc.setField(Math.min(acc.f1, value), 1);
+			return acc;
+		}
+	}
+
+	/** foldNeighbors(new Tuple2<>(k, v0), new MaxValuesFold()): (vertex, max(v0, values)). */
+	@SuppressWarnings("serial")
+	public static final class MaxValuesFold implements EdgesFold<Long, Long, Tuple2<Long, Long>>, BuiltinFold {
+		public int op() { return GellyHip.GS_OP_MAX; }
+
+		public Tuple2<Long, Long> foldEdges(Tuple2<Long, Long> acc, Long id, Long neighbor, Long value) {
+			acc.setField(id, 0);
+			acc.setField(Math.max(acc.f1, value), 1);
+			return acc;
+		}
+	}
+
+	/**
+	 * foldNeighbors(new Tuple2<>(k, c0), new CountFold()): (vertex, c0 + the vertex's neighbour records), the
+	 * COUNT built-in.  COUNT is a fold, not an EdgesReduce: reduceEdges(EV, EV) combines two edge values and
+	 * Flink's reduce starts from the first value, so a reducer cannot count (GraphWindowStream.java:107-121).
+	 */
+	@SuppressWarnings("serial")
+	public static final class CountFold<EV> implements EdgesFold<Long, EV, Tuple2<Long, Long>>, BuiltinFold {
+		public int op() { return GellyHip.GS_OP_COUNT; }
+
+		public Tuple2<Long, Long> foldEdges(Tuple2<Long, Long> acc, Long id, Long neighbor, EV value) {
+			acc.setField(id, 0);
+			acc.setField(acc.f1 + 1, 1);
 			return acc;
 		}
 	}

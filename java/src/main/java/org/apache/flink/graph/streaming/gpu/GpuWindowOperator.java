@@ -4,7 +4,11 @@
  * into direct column buffers and appended to the library's event-time window buffer (gs_stream_*:
  * start = ts - ts % size, Flink 1.0.3 TumblingEventTimeWindows); a watermark fires every window with
  * end - 1 <= watermark, and each fired window's rows are emitted with the timestamp end - 1
- * (window.maxTimestamp(), what Flink stamps window results with) before the watermark is forwarded.
+ * (window.maxTimestamp(), what Flink stamps window results with) before the watermark is forwarded: the
+ * operator waits for every window the watermark fired (their H2D copies and kernels are in flight when
+ * gs_stream_watermark returns), as Flink 1.0.3's WindowOperator emits results before the watermark.
+ * Emitting after it would stamp rows end - 1 <= a watermark already sent: late downstream, where e.g.
+ * WindowTriangles.java:66's timeWindowAll(..).sum(0) would split one window's count over two panes.
  *
  * One operator subtask owns one gs_ctx (one HIP stream + workspace: gelly_hip.h "Conventions"); run it
  * at parallelism 1 per GPU, or at parallelism P behind a partitionCustom by GellyHip's owner function
@@ -15,13 +19,18 @@ package org.apache.flink.graph.streaming.gpu;
 import java.nio.ByteBuffer;
 import java.nio.ByteOrder;
 
+import org.apache.flink.api.common.typeinfo.BasicTypeInfo;
+import org.apache.flink.api.common.typeinfo.TypeInformation;
 import org.apache.flink.api.java.tuple.Tuple;
 import org.apache.flink.api.java.tuple.Tuple2;
 import org.apache.flink.api.java.tuple.Tuple3;
+import org.apache.flink.api.java.typeutils.TupleTypeInfo;
 import org.apache.flink.graph.Edge;
+import org.apache.flink.streaming.api.datastream.DataStream;
 import org.apache.flink.streaming.api.operators.AbstractStreamOperator;
 import org.apache.flink.streaming.api.operators.OneInputStreamOperator;
 import org.apache.flink.streaming.api.watermark.Watermark;
+import org.apache.flink.streaming.api.windowing.time.Time;
 import org.apache.flink.streaming.runtime.streamrecord.StreamRecord;
 
 @SuppressWarnings("serial")
@@ -66,7 +75,8 @@ public class GpuWindowOperator<EV, OUT extends Tuple> extends AbstractStreamOper
 		long initMax = Long.MIN_VALUE;
 		if (kind == GellyHip.GS_STREAM_FOLD) {
 			initBuf = GellyHip.direct(8);
-			putValue(initBuf, 0, init);
+			if (op == GellyHip.GS_OP_COUNT) initBuf.putLong(0, ((Number) init).longValue());   // I64 for COUNT
+			else putValue(initBuf, 0, init);
 		} else if (kind == GellyHip.GS_STREAM_DEGREE_MAX && init != null) {
 			initMax = (Long) init;
 		}
@@ -95,7 +105,7 @@ public class GpuWindowOperator<EV, OUT extends Tuple> extends AbstractStreamOper
 	public void processWatermark(Watermark mark) throws Exception {
 		appendBatch();
 		GellyHip.streamWatermark(stream, mark.getTimestamp());
-		emitFired(false);
+		emitFired(true);   // every window this watermark fired, before the watermark goes downstream
 		output.emitWatermark(mark);
 	}
 
@@ -120,7 +130,7 @@ public class GpuWindowOperator<EV, OUT extends Tuple> extends AbstractStreamOper
 		buffered = 0;
 	}
 
-	/** every fired window's rows, stamped end - 1; after a flush, until the stream has none pending */
+	/** every fired window's rows, stamped end - 1; drain: wait until the stream has none pending */
 	@SuppressWarnings("unchecked")
 	private void emitFired(boolean drain) {
 		while (GellyHip.streamPoll(stream, drain && pending() > 0, meta, rows)) {
@@ -144,6 +154,20 @@ public class GpuWindowOperator<EV, OUT extends Tuple> extends AbstractStreamOper
 				output.collect(rec.replace(t, stamp));
 			}
 		}
+	}
+
+	/**
+	 * WindowTriangles.java:61-66 in one operator: slice(ALL) -> GenerateCandidateEdges -> keyBy(0, 1)
+	 * CountTriangles -> timeWindowAll(size).sum(0), i.e. one Tuple2<Integer, Long>(count as Integer, end - 1)
+	 * per window with output (gs_stream TRIANGLES).  Parallelism 1, as the reference's timeWindowAll.
+	 */
+	@SuppressWarnings({"unchecked", "rawtypes"})
+	public static <EV> DataStream<Tuple2<Integer, Long>> windowTriangles(DataStream<Edge<Long, EV>> edges, Time size) {
+		final TypeInformation<Tuple2<Integer, Long>> type = new TupleTypeInfo<Tuple2<Integer, Long>>(
+				BasicTypeInfo.INT_TYPE_INFO, BasicTypeInfo.LONG_TYPE_INFO);
+		return edges.transform("gpu-window-triangles", type,
+				new GpuWindowOperator<EV, Tuple2<Integer, Long>>(size.toMilliseconds(), GellyHip.GS_STREAM_TRIANGLES,
+						GellyHip.GS_DIR_ALL, 0, GellyHip.GS_NONE, null, 0, 0)).setParallelism(1);
 	}
 
 	private long pending() {

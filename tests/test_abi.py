@@ -122,3 +122,57 @@ def test_dispatch_patch_applies_to_the_reference():
         r = subprocess.run(["git", "apply", "--check", str(patch)], cwd=ref, capture_output=True,
                            text=True)
         assert r.returncode == 0, r.stderr
+
+
+GPU_JAVA = JAVA / "src/main/java/org/apache/flink/graph/streaming/gpu"
+PATCH = JAVA / "patches/gelly-streaming-gpu-dispatch.patch"
+
+
+def test_every_builtin_marker_reaches_a_native_and_an_entry_point():
+    """SURVEY.md §8(b) dispatch rule, end to end on the Java side: every built-in marker (GpuBuiltins'
+    reducers and folds, and the reference's GenerateCandidateEdges, which the patch marks BuiltinApply)
+    is dispatched by the patch to an operator; WindowTriangles.main is routed to the TRIANGLES stream;
+    every GellyHip native an operator calls is declared, implemented by the JNI shim, and the shim calls
+    only entry points include/gelly_hip.h declares."""
+    builtins = (GPU_JAVA / "GpuBuiltins.java").read_text()
+    markers = {m.group(1): m.group(2) for m in re.finditer(
+        r"public static final class (\w+)(?:<[^>]*>)?\s+implements[^{]*?\b(Builtin(?:Fold|Apply)?)\b", builtins)}
+    assert {"SumReduce", "MinReduce", "MaxReduce", "CountFold", "SumValuesFold", "DegreeMaxNeighborFold"} <= set(markers)
+    patch = PATCH.read_text()
+    added = "\n".join(line[1:] for line in patch.splitlines() if line.startswith("+") and not line.startswith("+++"))
+    after = "\n".join(line[1:] for line in patch.splitlines() if line[:1] in (" ", "+") and not line.startswith("+++"))
+    assert re.search(r"GenerateCandidateEdges implements\s*EdgesApply<[^{]*GpuBuiltins\.BuiltinApply \{", after)
+    markers["GenerateCandidateEdges"] = "BuiltinApply"
+    # marker interface -> (dispatch test in the patch, the operator it builds, the stream kind it asks for)
+    route = {"Builtin": ("GpuBuiltins.Builtin", "GpuWindowOperator", "GS_STREAM_REDUCE"),
+             "BuiltinFold": ("GpuBuiltins.BuiltinFold", "GpuWindowOperator", "GS_STREAM_FOLD"),
+             "BuiltinApply": ("GpuBuiltins.BuiltinApply", "GpuCandidatesOperator", None)}
+    for name, iface in markers.items():
+        test, op, kind = route[iface]
+        assert f"instanceof {test}" in added, (name, test)
+        assert f"new {op}" in added, (name, op)
+        if kind:
+            assert kind in added, (name, kind)
+    assert "GS_STREAM_DEGREE_MAX" in added
+    # WindowTriangles.main: slice -> candidates -> CountTriangles -> timeWindowAll.sum on one operator
+    assert "GpuWindowOperator.windowTriangles(" in added
+    assert "GS_STREAM_TRIANGLES" in (GPU_JAVA / "GpuWindowOperator.java").read_text()
+    natives = set(re.findall(r"static native [\w\[\]]+ (\w+)\(", GELLYHIP_JAVA.read_text()))
+    bodies = {re.search(r"JNI_FN\((\w+)\)", chunk).group(1): chunk
+              for chunk in SHIM.read_text().split("JNIEXPORT")[1:]}
+    for op in ("GpuWindowOperator", "GpuCandidatesOperator"):
+        used = set(re.findall(r"GellyHip\.([a-z]\w*)\(", (GPU_JAVA / f"{op}.java").read_text())) - {"direct"}
+        assert used and used <= natives, (op, used - natives)
+        for n in used:
+            calls = set(re.findall(r"\b(gs_\w+)\(", bodies[n]))
+            assert calls and calls <= set(declared()), (op, n, calls)
+
+
+def test_dispatch_falls_back_for_unsupported_types():
+    """A built-in over edges the engine does not take (non-Long keys, values that are not Integer / Long /
+    Float / Double) stays on Flink: the patch's gpu() asks GpuBuiltins.supports before dispatching."""
+    patch = PATCH.read_text()
+    assert "GpuBuiltins.supports(" in patch
+    src = (GPU_JAVA / "GpuBuiltins.java").read_text()
+    body = re.search(r"public static boolean supports\([^)]*\) \{([\s\S]*?)\n\t\}", src).group(1)
+    assert "keyClass != Long.class" in body and "dtypeOf(valueClass)" in body

@@ -258,3 +258,106 @@ def test_zipf_generator_matches_oracle(engine, oracle):
     # hubs at the lowest IDs: ID 0 is the most frequent source
     c = np.bincount(os_)
     assert c.argmax() == 0
+
+
+def _blocks_of(a, b, f, v0, v1):
+    """The records of vertices in [v0, v1) from a GenerateCandidateEdges output (vertex order): a vertex's
+    block starts at its first edge record (a = v, is_candidate = 0) and runs to the next vertex's."""
+    f = f.astype(bool)
+    start = ~f & np.concatenate([[True], f[:-1] | (a[1:] != a[:-1])])
+    owner = np.maximum.accumulate(np.where(start, np.arange(len(a)), 0))
+    keep = (a[owner] >= v0) & (a[owner] < v1)
+    return a[keep], b[keep], f[keep].astype(np.uint8)
+
+
+def _incident(s_h, d_h, vs):
+    """the window's edges incident to a set of vertices, in stream order"""
+    m = np.isin(s_h, vs) | np.isin(d_h, vs)
+    return s_h[m], d_h[m]
+
+
+def _gpu_span(engine, first, n):
+    engine.candidates_seek(first)
+    ga, gb, gf, at, _ = engine.candidates_next(n)
+    assert at == first and len(ga) == n
+    return ga.cpu().numpy(), gb.cpu().numpy(), gf.cpu().numpy()
+
+
+@pytest.mark.timeout(300)
+def test_c5_window_candidate_records_vertex_ranges(engine, oracle, c5_window):
+    """GenerateCandidateEdges records of the whole C5 window (1e8 edges, 1.6e11 records) compared record
+    for record on vertex ranges (WindowTriangles.java:91-114), streamed out of one gs_candidates session
+    with gs_candidates_vertex_range + gs_candidates_seek + gs_candidates_next:
+      * three ranges of consecutive ids (around the median-degree vertex, the lowest and the highest ids):
+        the oracle's gso_window_candidates over the edges incident to the range (a vertex's records
+        depend only on its own neighbour records), its blocks for the range's vertices;
+      * the hub (largest degree): its block length, its edge records and first pair rows, a slice from
+        its middle and its last rows, against the exact JDK HashSet order of its neighbours
+        (oracle.hashset_order) expanded by the reference's loop rule."""
+    src, dst, s_h, d_h = c5_window
+    total = engine.candidates_begin(src, dst)
+    V = int(max(s_h.max(), d_h.max())) + 1
+    deg = np.bincount(s_h, minlength=V) + np.bincount(d_h, minlength=V)   # slice(ALL) records per vertex
+    present = np.nonzero(deg)[0]
+    med = present[np.argsort(deg[present], kind="stable")[len(present) // 2]]
+    checked = 0
+    for lo_id in (int(med), int(present[0]), int(present[-1000])):
+        width = 1000
+        while True:
+            ids = present[(present >= lo_id) & (present < lo_id + width)]
+            first, _ = engine.candidates_vertex_range(int(ids[0]))
+            last_first, last_n = engine.candidates_vertex_range(int(ids[-1]))
+            span = last_first + last_n - first
+            if span <= 30_000_000 or width == 1:
+                break
+            width //= 4
+        v0, v1 = lo_id, lo_id + width
+        ss, dd = _incident(s_h, d_h, ids)
+        ra, rb, rf, _ = oracle.window_candidates(ss, dd)
+        ra, rb, rf = _blocks_of(ra, rb, rf, v0, v1)
+        assert len(ra) == span, (v0, v1, len(ra), span)
+        ga, gb, gf = _gpu_span(engine, first, span)
+        assert np.array_equal(ga, ra) and np.array_equal(gb, rb) and np.array_equal(gf, rf), (v0, v1)
+        checked += span
+    # an id absent from the window has no records
+    absent = np.setdiff1d(np.arange(present[0], present[0] + 4096), present)
+    if len(absent):
+        assert engine.candidates_vertex_range(int(absent[0]))[1] == 0
+    # the hub
+    hub = int(np.argmax(deg))
+    m = (s_h == hub) | (d_h == hub)
+    ss, dd = s_h[m], d_h[m]
+    # ALL (SimpleEdgeStream.java:354-365): per edge (src, dst) then (dst, src); the hub's neighbour records
+    recs = np.stack([dd, ss], axis=1).reshape(-1)
+    mine = np.stack([ss == hub, dd == hub], axis=1).reshape(-1)
+    nbrs = recs[mine]
+    _, fi = np.unique(nbrs, return_index=True)
+    order, _, flags = oracle.hashset_order(nbrs[np.sort(fi)])
+    G = order[order > hub]
+    k = len(G)
+    rows = k - int(order[-1] > hub) if k else 0
+    d = len(nbrs)
+    first, n = engine.candidates_vertex_range(hub)
+    assert n == d + rows * k - rows * (rows - 1) // 2, (n, d, k, rows)
+    row_off = np.arange(rows + 1, dtype=np.int64)
+    row_off = row_off * k - row_off * (row_off - 1) // 2
+
+    def expected(p0, p1):   # block positions [p0, p1) of the hub
+        p = np.arange(p0, p1, dtype=np.int64)
+        ea = np.full(len(p), hub, np.int64)
+        eb = np.empty(len(p), np.int64)
+        ef = (p >= d).astype(np.uint8)
+        eb[p < d] = nbrs[p[p < d]]
+        q = p[p >= d] - d
+        r = np.searchsorted(row_off, q, side="right") - 1
+        ea[p >= d] = G[r]
+        eb[p >= d] = G[r + (q - row_off[r])]
+        return ea, eb, ef
+
+    for p0, p1 in ((0, min(n, d + 3 * k)), (n // 2, min(n, n // 2 + 1_000_000)), (max(0, n - 3 * k), n)):
+        ga, gb, gf = _gpu_span(engine, first + p0, p1 - p0)
+        ea, eb, ef = expected(p0, p1)
+        assert np.array_equal(ga, ea) and np.array_equal(gb, eb) and np.array_equal(gf, ef), (hub, p0, p1)
+        checked += p1 - p0
+    print(f"\nC5 candidates: {total} records in the window, {checked} compared record for record; hub {hub}: "
+          f"{d} edge records, {k} ids above it, block {n}, JDK flags {flags}")
