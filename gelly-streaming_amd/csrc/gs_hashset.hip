@@ -293,15 +293,17 @@ __global__ __launch_bounds__(256) void k_cand_emit(const uint64_t* __restrict__ 
     }
     for (uint32_t s0 = sc;; s0 += 64) {
       const uint64_t bj = (uint64_t)s0 + 1 + lane <= S ? vs[s0 + 1 + lane] : ~0ull;
+      const uint64_t top = __shfl(bj, 63, 64);
       bool pend = false;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        int pos = 0;   // block starts vs[s0 + 1 ..] at or below o[i]
+        int pos = 0;   // block starts vs[s0 + 1 ..] at or below o[i]: 0..63 by halving, 64 past the window
 #pragma unroll
         for (int st = 32; st > 0; st >>= 1) {
           const uint64_t v = __shfl(bj, pos + st - 1, 64);
           pos += v <= o[i] ? st : 0;
         }
+        if (top <= o[i]) pos = 64;
         if (need[i] && pos < 64) {
           slot[i] = s0 + pos;
           need[i] = false;
@@ -322,16 +324,21 @@ __global__ __launch_bounds__(256) void k_cand_emit(const uint64_t* __restrict__ 
         av = vkeys[m.u];
         bv = nbr[m.nbr_off + t];
         fv = 0;
-      } else {
-        const uint64_t q = t - m.d, k = m.k;
+      } else if (m.rows) {
+        // row r of the block: the largest r with r k - r (r - 1) / 2 <= q (closed form, then at most a
+        // step or two of correction for the double rounding; the loops are bounded regardless)
+        const uint64_t q = t - m.d, k = m.k, rows = m.rows;
         const double k2 = 2.0 * (double)k + 1.0;
         uint64_t r = (uint64_t)fmax(0.0, (k2 - sqrt(fmax(0.0, k2 * k2 - 8.0 * (double)q))) * 0.5);
-        if (r >= m.rows) r = m.rows - 1;
-        while (r > 0 && tri_rows_before(r, k) > q) --r;
-        while (r + 1 < m.rows && tri_rows_before(r + 1, k) <= q) ++r;
-        const uint64_t col = q - tri_rows_before(r, k);
+        if (r >= rows) r = rows - 1;
+        for (int g = 0; g < 64 && r > 0 && tri_rows_before(r, k) > q; ++g) --r;
+        for (int g = 0; g < 64 && r + 1 < rows && tri_rows_before(r + 1, k) <= q; ++g) ++r;
+        const uint64_t col = min(q - tri_rows_before(r, k), k - 1 - r);
         av = gids[m.gbase + r];
         bv = gids[m.gbase + r + col];
+        fv = 1;
+      } else {   // not reached: a block without pair rows holds only its edge records
+        av = bv = 0;
         fv = 1;
       }
       a[o[i] - P0] = av;

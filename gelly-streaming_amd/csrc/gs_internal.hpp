@@ -71,10 +71,19 @@ struct gs_ctx {
   gs::DevBuf part_k, part_a, comp_k, comp_a;
   // triangles
   gs::DevBuf tri_loops, tri_tiles, tri_sfx, tri_nbr, tri_heavy, tri_range, tri_queue, tri_hwork;
-  gs::DevBuf tri_d[6];           // split-window triangles (gs_window_triangles_dist)
+  gs::DevBuf tri_d[10];          // split-window triangles (gs_window_triangles_dist)
   gs::DevBuf cc[3];              // connected components (gs_components.hip)
   uint32_t tri_B = 0;            // split-window triangles: id geometry of the current window
   uint64_t tri_key_xor = 0;
+  // split-window triangles, boundary adjacency (gs_tri_dist_plan / _need / _serve / _assemble): this
+  // rank's count range [bd_c0, bd_c1) and route range [bd_r0, bd_r1) of the degree order with their
+  // adjacency positions (bd_p*), the window's unique edges bd_M, the ids it requested (tri_bd[0]) and
+  // the prefix of their row lengths (tri_bd[1])
+  uint32_t bd_part = 0, bd_nparts = 0;
+  uint64_t bd_c0 = 0, bd_c1 = 0, bd_r0 = 0, bd_r1 = 0, bd_pc0 = 0, bd_pc1 = 0, bd_pr0 = 0, bd_pr1 = 0, bd_M = 0;
+  uint64_t bd_nreq = 0;
+  bool bd_ok = false;
+  gs::DevBuf tri_bd[4];
   // HashSet-order pipeline (gs_hashset.hip)
   gs::DevBuf hs[40];
   // bucket path (gs_bucket.hip): plan tables, work items, LDS slabs of multi-item buckets

@@ -409,6 +409,123 @@ __global__ __launch_bounds__(256) void k_tri_loops(const int64_t* __restrict__ s
   }
 }
 
+
+// ---- boundary adjacency of a split window (gs_tri_dist_plan .. _assemble) ----------------------------
+// The count share of rank `part` (u in its equal-work range C = [c0, c1)) reads the rows N+(u), u in C,
+// and the rows N+(v) of their targets v; rank q built the rows of its route range R_q = [r_q, r_q+1)
+// (owner(u) = u * P >> B).  So instead of every row, a rank fetches the rows of C (contiguous: one
+// all-to-all whose sizes every rank computes from the global d+) and then requests the rows of the
+// targets it holds neither in C nor in R (one all-to-all of ids, one of rows).  dp = d+ (u64), pre =
+// its exclusive prefix (the window positions of the rows).
+struct BdGroups {   // group starts (ids) of up to 64 requesters (+ the end), by value
+  uint64_t g[65];
+};
+// split points of every part: c_q (equal work), r_q (owner ranges), and the window position of each
+__global__ void k_bd_bounds(const unsigned long long* __restrict__ prew, const unsigned long long* __restrict__ pre,
+                            uint32_t V, uint32_t B, uint32_t P, unsigned long long* __restrict__ out) {
+  const uint32_t q = threadIdx.x;
+  if (q > P) return;
+  const unsigned long long W = prew[V];
+  auto lower = [&](unsigned long long t) {   // first u with prew[u] >= t
+    uint32_t a = 0, b = V;
+    while (a < b) {
+      const uint32_t m = (a + b) >> 1;
+      if (prew[m] < t) a = m + 1;
+      else b = m;
+    }
+    return a;
+  };
+  const uint32_t cq = q == 0 ? 0u : q == P ? V : lower(W * q / P);
+  const uint64_t sq = (uint64_t)q << B;
+  const uint32_t rq = (uint32_t)min((uint64_t)V, sq / P + (sq % P ? 1u : 0u));   // first u with u * P >> B == q
+  out[q] = cq;
+  out[P + 1 + q] = rq;
+  out[2 * (P + 1) + q] = pre[cq];
+  out[3 * (P + 1) + q] = pre[rq];
+}
+// targets of the rows of C that this rank holds neither in C nor in R -> bitmap
+__global__ __launch_bounds__(256) void k_bd_mark(const uint32_t* __restrict__ crows, uint64_t n, uint32_t c0, uint32_t c1,
+                                                 uint32_t r0, uint32_t r1, uint32_t V,
+                                                 const unsigned long long* __restrict__ dp, uint32_t* __restrict__ bits,
+                                                 uint32_t* __restrict__ bad) {
+  for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) {
+    const uint32_t v = crows[i];
+    if (v >= V) {
+      atomicOr(bad, 1u);
+      continue;
+    }
+    // (an empty row needs no request: nothing to intersect with)
+    if (v - c0 >= c1 - c0 && v - r0 >= r1 - r0 && dp[v]) atomicOr(&bits[v >> 5], 1u << (v & 31));
+  }
+}
+__global__ __launch_bounds__(256) void k_bd_popc(const uint32_t* __restrict__ bits, uint32_t words,
+                                                 uint64_t* __restrict__ cnt) {
+  for (uint32_t w = blockIdx.x * 256u + threadIdx.x; w < words; w += gridDim.x * 256u) cnt[w] = __popc(bits[w]);
+}
+// marked ids ascending (so grouped by owner) and their row lengths
+__global__ __launch_bounds__(256) void k_bd_ids(const uint32_t* __restrict__ bits, uint32_t words,
+                                                const uint64_t* __restrict__ pos, const unsigned long long* __restrict__ dp,
+                                                uint32_t* __restrict__ ids, uint64_t* __restrict__ len) {
+  for (uint32_t w = blockIdx.x * 256u + threadIdx.x; w < words; w += gridDim.x * 256u) {
+    uint32_t b = bits[w];
+    uint64_t p = pos[w];
+    for (; b; b &= b - 1, ++p) {
+      const uint32_t v = w * 32u + (uint32_t)__builtin_ctz(b);
+      ids[p] = v;
+      len[p] = dp[v];
+    }
+  }
+}
+// per owner q: the first requested id >= r_q, and the row elements before it
+__global__ void k_bd_groups(const uint32_t* __restrict__ ids, uint64_t n, const uint64_t* __restrict__ rowpre,
+                            const unsigned long long* __restrict__ bnd, uint32_t P, unsigned long long* __restrict__ out) {
+  const uint32_t q = threadIdx.x;
+  if (q > P) return;
+  const uint64_t rq = bnd[P + 1 + q];
+  uint64_t a = 0, b = n;
+  while (a < b) {
+    const uint64_t m = (a + b) >> 1;
+    if (ids[m] < rq) a = m + 1;
+    else b = m;
+  }
+  out[q] = a;
+  out[P + 1 + q] = rowpre[a];
+}
+// row lengths of requested ids (serve): an id outside this rank's route range is a caller error
+__global__ __launch_bounds__(256) void k_bd_serve_len(const uint32_t* __restrict__ ids, uint64_t n,
+                                                      const unsigned long long* __restrict__ dp, uint32_t r0, uint32_t r1,
+                                                      uint64_t* __restrict__ len, uint32_t* __restrict__ bad) {
+  for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) {
+    const uint32_t v = ids[i];
+    const bool ok = v - r0 < r1 - r0;
+    len[i] = ok ? dp[v] : 0ull;
+    if (!ok) atomicOr(bad, 1u);
+  }
+}
+// copy whole rows, one wave per id: serve (SERVE) from the local rows at pre[v] - base to the packed
+// positions pos[i]; assemble from the packed received rows at pos[i] to the window positions pre[v]
+template <bool SERVE>
+__global__ __launch_bounds__(256) void k_bd_copy(const uint32_t* __restrict__ ids, uint64_t n,
+                                                 const unsigned long long* __restrict__ pre, uint64_t base,
+                                                 const uint64_t* __restrict__ pos, const unsigned long long* __restrict__ dp,
+                                                 uint32_t r0, uint32_t r1, const uint32_t* __restrict__ from,
+                                                 uint32_t* __restrict__ to) {
+  const uint32_t lane = threadIdx.x & 63;
+  const uint64_t nw = (uint64_t)gridDim.x * 4;
+  for (uint64_t i = ((uint64_t)blockIdx.x * 256 + threadIdx.x) >> 6; i < n; i += nw) {
+    const uint32_t v = ids[i];
+    if (SERVE && v - r0 >= r1 - r0) continue;   // flagged by k_bd_serve_len
+    const uint64_t d = dp[v];
+    const uint64_t s = SERVE ? pre[v] - base : pos[i], t = SERVE ? pos[i] : pre[v];
+    for (uint64_t k = lane; k < d; k += 64) to[t + k] = from[s + k];
+  }
+}
+// one value per group start, by value (serve: the element offset of each requester's rows)
+__global__ void k_bd_pick(const uint64_t* __restrict__ pos, BdGroups g, uint32_t P, unsigned long long* __restrict__ out) {
+  const uint32_t q = threadIdx.x;
+  if (q <= P) out[q] = pos[g.g[q]];
+}
+
 }  // namespace gs
 
 using namespace gs;
@@ -910,6 +1027,200 @@ gs_status gs_tri_dist_count(gs_ctx* c, const uint32_t* nbr, uint64_t M, const ui
   return GS_OK;
 }
 
+// ---- boundary adjacency (see k_bd_bounds) -------------------------------------------------------------
+static unsigned bd_grid(uint64_t n, uint64_t per) {
+  return (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((n + per - 1) / per, 16384));
+}
+
+gs_status gs_tri_dist_plan(gs_ctx* c, const uint32_t* dplus, uint32_t part, uint32_t nparts, uint64_t* send_elems,
+                           uint64_t* recv_elems, uint64_t* M_out) {
+  if (!c) return GS_EINVAL;
+  if (!dplus || !send_elems || !recv_elems || !M_out) return set_error(c, GS_EINVAL, "null pointer");
+  if (nparts == 0 || nparts > 64 || part >= nparts) return set_error(c, GS_EINVAL, "bad part %u of %u", part, nparts);
+  if (!c->tri_B) return set_error(c, GS_EINVAL, "gs_tri_dist_degrees first (the window's id geometry)");
+  GS_TRY(begin_call(c));
+  c->bd_ok = false;
+  const uint32_t B = c->tri_B, P = nparts;
+  const size_t V = 1ull << B;
+  GS_TRY(ensure(c, c->tri_range, V * 16));
+  GS_TRY(ensure(c, c->tri_d[5], (V + 1) * 16));
+  GS_TRY(ensure(c, c->tri_hwork, (V * 2 + 2) * 8));
+  GS_TRY(ensure(c, c->tri_bd[3], 8 * 65 * 8));
+  unsigned long long* d64 = c->tri_d[5].as<unsigned long long>();   // d+ [0, V), prefix [V, 2V]
+  unsigned long long* work = c->tri_hwork.as<unsigned long long>();
+  unsigned long long* bnd = c->tri_bd[3].as<unsigned long long>();
+  uint2* out_range = reinterpret_cast<uint2*>(c->tri_range.p);
+  const unsigned gv = bd_grid(V, 256);
+  hipLaunchKernelGGL(k_u32_to_u64, dim3(gv), dim3(256), 0, c->stream, dplus, (uint32_t)V, d64);
+  GS_TRY(xscan(c, (const uint64_t*)d64, V, (uint64_t*)d64 + V));
+  hipLaunchKernelGGL(k_tri_ranges, dim3(gv), dim3(256), 0, c->stream, dplus, (const unsigned long long*)d64 + V,
+                     (uint32_t)V, out_range);
+  hipLaunchKernelGGL(k_tri_work, dim3(gv), dim3(256), 0, c->stream, out_range, (uint32_t)V, work);
+  GS_TRY(xscan(c, (const uint64_t*)work, V, (uint64_t*)work + V + 1));
+  hipLaunchKernelGGL(k_bd_bounds, dim3(1), dim3(128), 0, c->stream, (const unsigned long long*)work + V + 1,
+                     (const unsigned long long*)d64 + V, (uint32_t)V, B, P, bnd);
+  GS_HIP(hipGetLastError());
+  GS_HIP(hipMemcpyAsync(c->host_small + 64, bnd, 4 * (P + 1) * 8, hipMemcpyDeviceToHost, c->stream));
+  GS_HIP(hipMemcpyAsync(c->host_small + 63, (const unsigned long long*)d64 + 2 * V, 8, hipMemcpyDeviceToHost, c->stream));
+  GS_TRY(host_wait(c));
+  const uint64_t* h = c->host_small + 64;
+  const uint64_t *cq = h, *rq = h + (P + 1), *pc = h + 2 * (P + 1), *pr = h + 3 * (P + 1);
+  // C_a ∩ R_b as window positions: both are unions of whole rows, so the larger start / smaller end of
+  // the two ranges bound it, and their positions bound its elements
+  auto inter = [&](uint32_t a, uint32_t b) -> uint64_t {
+    const uint64_t u0 = std::max(cq[a], rq[b]), u1 = std::min(cq[a + 1], rq[b + 1]);
+    if (u0 >= u1) return 0;
+    const uint64_t p0 = cq[a] >= rq[b] ? pc[a] : pr[b], p1 = cq[a + 1] <= rq[b + 1] ? pc[a + 1] : pr[b + 1];
+    return p1 > p0 ? p1 - p0 : 0;
+  };
+  for (uint32_t q = 0; q < P; ++q) {
+    send_elems[q] = inter(q, part);   // rows this rank built that rank q counts
+    recv_elems[q] = inter(part, q);   // rows this rank counts that rank q built
+  }
+  c->bd_part = part;
+  c->bd_nparts = P;
+  c->bd_c0 = cq[part];
+  c->bd_c1 = cq[part + 1];
+  c->bd_r0 = rq[part];
+  c->bd_r1 = rq[part + 1];
+  c->bd_pc0 = pc[part];
+  c->bd_pc1 = pc[part + 1];
+  c->bd_pr0 = pr[part];
+  c->bd_pr1 = pr[part + 1];
+  c->bd_M = c->host_small[63];
+  c->bd_nreq = 0;
+  c->bd_ok = true;
+  *M_out = c->bd_M;
+  return GS_OK;
+}
+
+gs_status gs_tri_dist_need(gs_ctx* c, const uint32_t* crows, uint32_t* req_out, uint64_t capacity,
+                           uint64_t* req_counts, uint64_t* req_elems, uint64_t* nreq) {
+  if (!c) return GS_EINVAL;
+  if (!req_counts || !req_elems || !nreq) return set_error(c, GS_EINVAL, "null pointer");
+  if (!c->bd_ok) return set_error(c, GS_EINVAL, "gs_tri_dist_plan first");
+  const uint64_t nc = c->bd_pc1 - c->bd_pc0;
+  if (nc && !crows) return set_error(c, GS_EINVAL, "null crows");
+  const uint32_t P = c->bd_nparts, B = c->tri_B;
+  const size_t V = 1ull << B, words = (V + 31) / 32;
+  GS_HIP(hipSetDevice(c->device));
+  (void)hipGetLastError();
+  const size_t boff = (words * 4 + 255) & ~(size_t)255;
+  GS_TRY(ensure(c, c->tri_bd[0], V * 4 + 64));                        // the requested ids
+  GS_TRY(ensure(c, c->tri_bd[1], (V + 1) * 8 * 2));                   // row lengths, their prefix
+  GS_TRY(ensure(c, c->tri_bd[2], boff + (words + 1) * 8 * 2 + 64));  // bitmap, word counts, positions
+  uint32_t* bits = c->tri_bd[2].as<uint32_t>();
+  uint64_t* wcnt = reinterpret_cast<uint64_t*>(c->tri_bd[2].as<char>() + boff);
+  uint64_t* wpos = wcnt + words + 1;
+  uint32_t* bad = reinterpret_cast<uint32_t*>(wpos + words + 1);
+  GS_HIP(hipMemsetAsync(bits, 0, words * 4, c->stream));
+  GS_HIP(hipMemsetAsync(bad, 0, 4, c->stream));
+  if (nc)
+    hipLaunchKernelGGL(k_bd_mark, dim3(bd_grid(nc, 256)), dim3(256), 0, c->stream, crows, nc, (uint32_t)c->bd_c0,
+                       (uint32_t)c->bd_c1, (uint32_t)c->bd_r0, (uint32_t)c->bd_r1, (uint32_t)V,
+                       c->tri_d[5].as<unsigned long long>(), bits, bad);
+  hipLaunchKernelGGL(k_bd_popc, dim3(bd_grid(words, 256)), dim3(256), 0, c->stream, bits, (uint32_t)words, wcnt);
+  GS_TRY(xscan(c, wcnt, words, wpos));
+  uint32_t* ids = c->tri_bd[0].as<uint32_t>();
+  uint64_t* len = c->tri_bd[1].as<uint64_t>();
+  uint64_t* rowpre = len + V + 1;
+  const unsigned long long* d64 = c->tri_d[5].as<unsigned long long>();
+  hipLaunchKernelGGL(k_bd_ids, dim3(bd_grid(words, 256)), dim3(256), 0, c->stream, bits, (uint32_t)words,
+                     (const uint64_t*)wpos, d64, ids, len);
+  GS_HIP(hipGetLastError());
+  c->host_small[61] = 0;
+  GS_HIP(hipMemcpyAsync(c->host_small + 62, wpos + words, 8, hipMemcpyDeviceToHost, c->stream));
+  GS_HIP(hipMemcpyAsync(c->host_small + 61, bad, 4, hipMemcpyDeviceToHost, c->stream));
+  GS_TRY(host_wait(c));
+  if ((uint32_t)c->host_small[61]) return set_error(c, GS_EINVAL, "gs_tri_dist_need: a row holds an id >= V");
+  const uint64_t n = c->host_small[62];
+  GS_TRY(xscan(c, len, n, rowpre));
+  unsigned long long* g = c->tri_bd[3].as<unsigned long long>() + 4 * 65;
+  hipLaunchKernelGGL(k_bd_groups, dim3(1), dim3(128), 0, c->stream, ids, n, (const uint64_t*)rowpre,
+                     c->tri_bd[3].as<unsigned long long>(), P, g);
+  GS_HIP(hipGetLastError());
+  GS_HIP(hipMemcpyAsync(c->host_small + 64, g, 2 * (P + 1) * 8, hipMemcpyDeviceToHost, c->stream));
+  GS_TRY(host_wait(c));
+  const uint64_t* h = c->host_small + 64;
+  for (uint32_t q = 0; q < P; ++q) {
+    req_counts[q] = h[q + 1] - h[q];
+    req_elems[q] = h[P + 1 + q + 1] - h[P + 1 + q];
+  }
+  c->bd_nreq = n;
+  *nreq = n;
+  if (n > capacity) return set_error(c, GS_ECAPACITY, "gs_tri_dist_need: %llu ids", (unsigned long long)n);
+  if (n) GS_HIP(hipMemcpyAsync(req_out, ids, n * 4, hipMemcpyDeviceToDevice, c->stream));
+  return host_wait(c);
+}
+
+gs_status gs_tri_dist_serve(gs_ctx* c, const uint32_t* nbr, const uint32_t* req_in, const uint64_t* counts_in,
+                            uint32_t* rows_out, uint64_t capacity, uint64_t* send_elems) {
+  if (!c) return GS_EINVAL;
+  if (!counts_in || !send_elems) return set_error(c, GS_EINVAL, "null pointer");
+  if (!c->bd_ok) return set_error(c, GS_EINVAL, "gs_tri_dist_plan first");
+  const uint32_t P = c->bd_nparts;
+  BdGroups gr;
+  gr.g[0] = 0;
+  for (uint32_t q = 0; q < P; ++q) gr.g[q + 1] = gr.g[q] + counts_in[q];
+  const uint64_t n = gr.g[P];
+  for (uint32_t q = 0; q < P; ++q) send_elems[q] = 0;
+  if (n == 0) return GS_OK;
+  if (!req_in || !nbr) return set_error(c, GS_EINVAL, "null pointer");
+  GS_HIP(hipSetDevice(c->device));
+  (void)hipGetLastError();
+  GS_TRY(ensure(c, c->tri_bd[2], (n + 1) * 8 * 2 + 64));
+  uint64_t* len = c->tri_bd[2].as<uint64_t>();
+  uint64_t* pos = len + n + 1;
+  uint32_t* bad = reinterpret_cast<uint32_t*>(pos + n + 1);
+  GS_HIP(hipMemsetAsync(bad, 0, 4, c->stream));
+  const unsigned long long* d64 = c->tri_d[5].as<unsigned long long>();
+  hipLaunchKernelGGL(k_bd_serve_len, dim3(bd_grid(n, 256)), dim3(256), 0, c->stream, req_in, n, d64,
+                     (uint32_t)c->bd_r0, (uint32_t)c->bd_r1, len, bad);
+  GS_TRY(xscan(c, len, n, pos));
+  unsigned long long* pk = c->tri_bd[3].as<unsigned long long>() + 6 * 65;
+  hipLaunchKernelGGL(k_bd_pick, dim3(1), dim3(128), 0, c->stream, (const uint64_t*)pos, gr, P, pk);
+  GS_HIP(hipGetLastError());
+  c->host_small[61] = 0;
+  GS_HIP(hipMemcpyAsync(c->host_small + 64, pk, (P + 1) * 8, hipMemcpyDeviceToHost, c->stream));
+  GS_HIP(hipMemcpyAsync(c->host_small + 61, bad, 4, hipMemcpyDeviceToHost, c->stream));
+  GS_TRY(host_wait(c));
+  if ((uint32_t)c->host_small[61]) return set_error(c, GS_EINVAL, "gs_tri_dist_serve: a requested id is not this rank's");
+  const uint64_t* h = c->host_small + 64;
+  for (uint32_t q = 0; q < P; ++q) send_elems[q] = h[q + 1] - h[q];
+  if (h[P] > capacity) return set_error(c, GS_ECAPACITY, "gs_tri_dist_serve: %llu row elements", (unsigned long long)h[P]);
+  if (h[P] == 0) return GS_OK;
+  if (!rows_out) return set_error(c, GS_EINVAL, "null rows_out");
+  hipLaunchKernelGGL(k_bd_copy<true>, dim3(bd_grid(n, 4)), dim3(256), 0, c->stream, req_in, n,
+                     d64 + (1ull << c->tri_B), c->bd_pr0, (const uint64_t*)pos, d64, (uint32_t)c->bd_r0, (uint32_t)c->bd_r1,
+                     nbr, rows_out);
+  GS_HIP(hipGetLastError());
+  return host_wait(c);
+}
+
+gs_status gs_tri_dist_assemble(gs_ctx* c, const uint32_t* nbr, const uint32_t* crows, const uint32_t* rows_in,
+                               uint32_t* full_out) {
+  if (!c) return GS_EINVAL;
+  if (!c->bd_ok) return set_error(c, GS_EINVAL, "gs_tri_dist_plan first");
+  if (c->bd_M && !full_out) return set_error(c, GS_EINVAL, "null full_out");
+  GS_HIP(hipSetDevice(c->device));
+  (void)hipGetLastError();
+  const uint64_t nr = c->bd_pr1 - c->bd_pr0, nc = c->bd_pc1 - c->bd_pc0, n = c->bd_nreq;
+  if ((nr && !nbr) || (nc && !crows)) return set_error(c, GS_EINVAL, "null rows");
+  // rows nobody sent stay id 0 (a valid id: a missing row can only miscount, never index past V)
+  if (c->bd_M) GS_HIP(hipMemsetAsync(full_out, 0, c->bd_M * 4, c->stream));
+  if (nr) GS_HIP(hipMemcpyAsync(full_out + c->bd_pr0, nbr, nr * 4, hipMemcpyDeviceToDevice, c->stream));
+  if (nc) GS_HIP(hipMemcpyAsync(full_out + c->bd_pc0, crows, nc * 4, hipMemcpyDeviceToDevice, c->stream));
+  if (n) {
+    if (!rows_in) return set_error(c, GS_EINVAL, "null rows_in");
+    const unsigned long long* d64 = c->tri_d[5].as<unsigned long long>();
+    const uint64_t* rowpre = c->tri_bd[1].as<uint64_t>() + (1ull << c->tri_B) + 1;
+    hipLaunchKernelGGL(k_bd_copy<false>, dim3(bd_grid(n, 4)), dim3(256), 0, c->stream, c->tri_bd[0].as<uint32_t>(), n,
+                       d64 + (1ull << c->tri_B), 0ull, rowpre, d64, 0u, 0u, rows_in, full_out);
+    GS_HIP(hipGetLastError());
+  }
+  return host_wait(c);
+}
+
 gs_status gs_window_triangles_selfpair(gs_ctx* c, const gs_edge_batch* b, uint64_t* S) {
   if (!c) return GS_EINVAL;
   GS_TRY(check_batch(c, b, GS_DIR_ALL));
@@ -991,22 +1302,57 @@ gs_status gs_window_triangles_dist(gs_ctx* c, const gs_edge_batch* b, uint64_t* 
   GS_TRY(ensure(c, c->tri_d[3], nrecv * 8 + 8));
   GS_TRY(exchange_rows(c, c->tri_d[2].as<char>(), send.data(), c->tri_d[3].as<char>(), recv.data(), 8));
   GS_TRY(gs_comm_allreduce_sum_u64(c, &loops));
-  // 4. local out-lists; out-degrees summed (every u has one owner), out-lists all-gathered in rank order
+  // 4. local out-lists; out-degrees summed (every u has one owner).  Then the boundary adjacency
+  //    instead of every row: the rows of this rank's count range (one all-to-all, sizes known to every
+  //    rank from the global d+), then the rows of their targets it holds in neither range (ids
+  //    requested, rows served: two all-to-alls), assembled at their window positions
   GS_TRY(ensure(c, c->tri_d[4], nrecv * 4 + 4));
   GS_TRY(ensure(c, c->tri_d[1], V * 4));   // the degrees are consumed: d+ reuses the buffer
   uint32_t* dplus = c->tri_d[1].as<uint32_t>();
+  uint32_t* nbr = c->tri_d[4].as<uint32_t>();
   uint64_t m = 0;
-  GS_TRY(comm_agree(c, gs_tri_dist_build(c, c->tri_d[3].as<uint64_t>(), nrecv, c->tri_d[4].as<uint32_t>(), dplus, &m)));
+  GS_TRY(comm_agree(c, gs_tri_dist_build(c, c->tri_d[3].as<uint64_t>(), nrecv, nbr, dplus, &m)));
   GS_TRY(comm_allreduce(c, dplus, V, NCCL_T_U32, NCCL_OP_SUM));
-  std::vector<uint64_t> ms(P);
-  GS_TRY(comm_allgather_u64(c, m, ms.data()));
-  uint64_t M = 0;
-  for (uint32_t p = 0; p < P; ++p) M += ms[p];
-  GS_TRY(ensure(c, c->tri_d[2], M * 4 + 4));   // the routed keys are consumed
-  GS_TRY(comm_allgatherv(c, c->tri_d[4].p, c->tri_d[2].as<char>(), ms.data(), 4));
+  std::vector<uint64_t> s1(P), r1(P), rc(P), re(P), qc(P), qe(P), se(P), one(P, 1);
+  uint64_t M = 0, nreq = 0;
+  GS_TRY(comm_agree(c, gs_tri_dist_plan(c, dplus, me, P, s1.data(), r1.data(), &M)));
+  uint64_t nc = 0;
+  for (uint32_t p = 0; p < P; ++p) nc += r1[p];
+  GS_TRY(ensure(c, c->tri_d[2], nc * 4 + 4));   // the routed keys are consumed: the count range's rows
+  uint32_t* crows = c->tri_d[2].as<uint32_t>();
+  GS_TRY(exchange_rows(c, (const char*)nbr, s1.data(), (char*)crows, r1.data(), 4));
+  GS_TRY(ensure(c, c->tri_d[3], V * 4 + 4));    // the received keys are consumed: the ids requested
+  uint32_t* req = c->tri_d[3].as<uint32_t>();
+  GS_TRY(comm_agree(c, gs_tri_dist_need(c, crows, req, V, rc.data(), re.data(), &nreq)));
+  // (ids, row elements) each rank asks of each other: one 16-byte row per peer
+  GS_TRY(ensure(c, c->tri_d[0], 64 + (size_t)P * 32));
+  uint64_t* pairs = (uint64_t*)(c->tri_d[0].as<char>() + 64);
+  for (uint32_t p = 0; p < P; ++p) {
+    c->host_small[64 + 2 * p] = rc[p];
+    c->host_small[65 + 2 * p] = re[p];
+  }
+  GS_HIP(hipMemcpyAsync(pairs, c->host_small + 64, (size_t)P * 16, hipMemcpyHostToDevice, c->stream));
+  GS_TRY(exchange_rows(c, (const char*)pairs, one.data(), (char*)(pairs + 2 * P), one.data(), 16));
+  GS_HIP(hipMemcpyAsync(c->host_small + 64, pairs + 2 * P, (size_t)P * 16, hipMemcpyDeviceToHost, c->stream));
+  GS_TRY(host_wait(c));
+  uint64_t nin = 0, nel = 0, nrows = 0;
+  for (uint32_t p = 0; p < P; ++p) {
+    nin += (qc[p] = c->host_small[64 + 2 * p]);
+    nel += (qe[p] = c->host_small[65 + 2 * p]);
+    nrows += re[p];
+  }
+  GS_TRY(ensure(c, c->tri_d[6], nin * 4 + 4));
+  GS_TRY(exchange_rows(c, (const char*)req, rc.data(), c->tri_d[6].as<char>(), qc.data(), 4));
+  GS_TRY(ensure(c, c->tri_d[7], nel * 4 + 4));
+  GS_TRY(comm_agree(c, gs_tri_dist_serve(c, nbr, c->tri_d[6].as<uint32_t>(), qc.data(), c->tri_d[7].as<uint32_t>(),
+                                         nel, se.data())));
+  GS_TRY(ensure(c, c->tri_d[8], nrows * 4 + 4));
+  GS_TRY(exchange_rows(c, c->tri_d[7].as<char>(), se.data(), c->tri_d[8].as<char>(), re.data(), 4));
+  GS_TRY(ensure(c, c->tri_d[9], M * 4 + 4));
+  GS_TRY(comm_agree(c, gs_tri_dist_assemble(c, nbr, crows, c->tri_d[8].as<uint32_t>(), c->tri_d[9].as<uint32_t>())));
   // 5. this rank's share of the count, summed
   uint64_t T = 0;
-  GS_TRY(comm_agree(c, gs_tri_dist_count(c, c->tri_d[2].as<uint32_t>(), M, dplus, me, P, &T)));
+  GS_TRY(comm_agree(c, gs_tri_dist_count(c, c->tri_d[9].as<uint32_t>(), M, dplus, me, P, &T)));
   // 6. the self-pair term needs whole neighbour sets: windows with self-loops gather the records
   if (loops) {
     std::vector<uint64_t> ns(P);

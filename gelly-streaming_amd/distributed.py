@@ -174,6 +174,13 @@ def gather_window(src: torch.Tensor, dst: torch.Tensor, group=None):
     return outs[0], outs[1]
 
 
+def _exchange(t, send, recv, cdev, home, group):
+    """all-to-all of a 1-D tensor: send[p] elements to rank p (in rank order), recv[p] from it"""
+    out = torch.empty(sum(recv), dtype=t.dtype, device=cdev)
+    dist.all_to_all_single(out, t[:sum(send)].contiguous().to(cdev), recv, send, group=group)
+    return out.to(home)
+
+
 def triangles_window(eng, src, dst, group=None):
     """WindowTriangles over a window whose records are split across the ranks of `group` (SURVEY.md §8e,
     WindowTriangles.java:61-66).  The six steps of include/gelly_hip.h's gs_tri_dist_* with the
@@ -181,7 +188,9 @@ def triangles_window(eng, src, dst, group=None):
       1. id range          all-reduce MIN / MAX
       2. raw degrees       all-reduce SUM of an int32[V]          (every rank renumbers identically)
       3. oriented edges    all-to-all of 8-byte keys to owner(u)  (contiguous ranges of the degree order)
-      4. out-lists         all-reduce SUM of d+ int32[V]; all-gather of the 4-byte targets (rank order)
+      4. out-lists         all-reduce SUM of d+ int32[V]; then the boundary adjacency: the rows of this
+                           rank's equal-work count range (all-to-all, sizes from d+), the rows of their
+                           targets it holds in neither range (all-to-all of ids, then of rows)
       5. count             each rank its equal-work share of the middle-vertex intersections; all-reduce
       6. self-pair term    only when the window has self-loops: gather the records, rank 0 adds it
     eng: an Engine on this rank's GPU; src, dst: this rank's records (device tensors).
@@ -216,16 +225,21 @@ def triangles_window(eng, src, dst, group=None):
     nbr, dplus = eng.tri_dist_build(rk.to(home), deg.numel())
     dp = dplus.to(cdev)
     dist.all_reduce(dp, op=dist.ReduceOp.SUM, group=group)
-    ms = [torch.zeros(1, dtype=torch.int64, device=cdev) for _ in range(world)]
-    dist.all_gather(ms, torch.tensor([nbr.numel()], dtype=torch.int64, device=cdev), group=group)
-    ms = [int(x) for x in ms]
-    mx = max(ms)
-    pad = torch.zeros(mx, dtype=torch.int32, device=cdev)
-    pad[:nbr.numel()] = nbr.to(cdev)
-    parts = [torch.empty(mx, dtype=torch.int32, device=cdev) for _ in range(world)]
-    dist.all_gather(parts, pad, group=group)
-    allnbr = torch.cat([p[:k] for p, k in zip(parts, ms)]).to(home)
-    T = eng.tri_dist_count(allnbr, dp.to(home), rank, world)
+    dph = dp.to(home)
+    # 4. boundary adjacency: the rows of this rank's count range, then the rows of their targets it holds
+    #    in neither range (requested by id) -- not every rank's out-lists
+    s1, r1, M = eng.tri_dist_plan(dph, rank, world)
+    crows = _exchange(nbr, s1, r1, cdev, home, group)
+    req, rc, re = eng.tri_dist_need(crows, world, deg.numel())
+    mine = torch.tensor([x for pair in zip(rc, re) for x in pair], dtype=torch.int64, device=cdev)
+    theirs = torch.empty_like(mine)
+    dist.all_to_all_single(theirs, mine, group=group)
+    qc, qe = theirs.view(-1, 2)[:, 0].tolist(), theirs.view(-1, 2)[:, 1].tolist()
+    req_in = _exchange(req, rc, qc, cdev, home, group)
+    rows, se = eng.tri_dist_serve(nbr, req_in, qc, qe)
+    rows_in = _exchange(rows, se, re, cdev, home, group)
+    full = eng.tri_dist_assemble(nbr, crows, rows_in, M)
+    T = eng.tri_dist_count(full, dph, rank, world)
     if int(lt[0]):
         fs, fd = gather_window(src, dst, group)
         if rank == 0:

@@ -392,8 +392,47 @@ class Engine:
                                               ctypes.byref(m)))
         return nbr[:m.value], dplus
 
+    def tri_dist_plan(self, dplus, part: int, nparts: int):
+        """Step 4a: from the global d+, the boundary exchange's first all-to-all: (elements of this rank's
+        rows each rank counts, elements each rank built of the rows this rank counts, unique edges M)."""
+        send, recv, M = (ctypes.c_uint64 * nparts)(), (ctypes.c_uint64 * nparts)(), ctypes.c_uint64(0)
+        self._check(self._L.gs_tri_dist_plan(self.ctx, _ptr(dplus.contiguous()), part, nparts, send, recv, ctypes.byref(M)))
+        return [int(x) for x in send], [int(x) for x in recv], M.value
+
+    def tri_dist_need(self, crows, nparts: int, V: int):
+        """Step 4b: the rows this rank's count share reads but holds in neither of its ranges: (int32 ids
+        ascending, ids per owner, row elements per owner)."""
+        import torch
+
+        crows = crows.contiguous()
+        req = torch.empty(max(V, 1), dtype=torch.int32, device=f"cuda:{self.device}")
+        rc, re, n = (ctypes.c_uint64 * nparts)(), (ctypes.c_uint64 * nparts)(), ctypes.c_uint64(0)
+        self._check(self._L.gs_tri_dist_need(self.ctx, _ptr(crows), _ptr(req), V, rc, re, ctypes.byref(n)))
+        return req[:n.value], [int(x) for x in rc], [int(x) for x in re]
+
+    def tri_dist_serve(self, nbr, req_in, counts_in, elems_in):
+        """Step 4c: the rows other ranks requested (req_in grouped by requester, counts_in ids each, elems_in
+        row elements each) -> (int32 packed rows, elements per requester)."""
+        import torch
+
+        P = len(counts_in)
+        rows = torch.empty(max(sum(elems_in), 1), dtype=torch.int32, device=f"cuda:{self.device}")
+        cin, se = (ctypes.c_uint64 * P)(*[int(x) for x in counts_in]), (ctypes.c_uint64 * P)()
+        self._check(self._L.gs_tri_dist_serve(self.ctx, _ptr(nbr.contiguous()), _ptr(req_in.contiguous()), cin,
+                                              _ptr(rows), sum(elems_in), se))
+        return rows[:sum(elems_in)], [int(x) for x in se]
+
+    def tri_dist_assemble(self, nbr, crows, rows_in, M: int):
+        """Step 4d: every row this rank's count share reads, at its window position (int32 [M])."""
+        import torch
+
+        full = torch.empty(max(M, 1), dtype=torch.int32, device=f"cuda:{self.device}")
+        self._check(self._L.gs_tri_dist_assemble(self.ctx, _ptr(nbr.contiguous()), _ptr(crows.contiguous()),
+                                                 _ptr(rows_in.contiguous()), _ptr(full)))
+        return full[:M]
+
     def tri_dist_count(self, nbr, dplus, part: int, nparts: int) -> int:
-        """Step 5: this rank's share of the count over the whole out-adjacency (all-reduce SUM)."""
+        """Step 5: this rank's share of the count over the assembled rows (all-reduce SUM)."""
         cnt = ctypes.c_uint64(0)
         nbr = nbr.contiguous()
         self._check(self._L.gs_tri_dist_count(self.ctx, _ptr(nbr), nbr.numel(), _ptr(dplus.contiguous()), part, nparts,

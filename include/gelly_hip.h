@@ -267,13 +267,31 @@ GS_API gs_status gs_window_triangles_part(gs_ctx* ctx, const gs_edge_batch* batc
  *                                                           -> all-to-all of the rows; all-reduce loops
  *   4. gs_tri_dist_build     the received rows deduplicated into this rank's out-lists: nbr_out[m]
  *      (targets, sorted per u) and dplus_out[V] (d+(u) of the owned u, 0 elsewhere)
- *                                                           -> all-gather nbr (rank order), all-reduce dplus
- *   5. gs_tri_dist_count     this rank's share (part = rank, nparts = ranks) of the count over the
- *      whole out-adjacency                                  -> all-reduce (sum) of the counts
+ *                                                           -> all-reduce (sum, u32) of dplus
+ *      Boundary adjacency (north_star: "all-gathers boundary adjacency"; not every row): the count share
+ *      of a rank reads the rows of its equal-work range C of the degree order and the rows of their
+ *      targets; it built the rows of its route range R.
+ *   4a. gs_tri_dist_plan     from the global dplus: send_elems[p] = elements of this rank's rows that
+ *      rank p counts, recv_elems[p] = elements of the rows this rank counts that rank p built; *M =
+ *      the window's unique edges                            -> all-to-all of nbr (those sizes) = crows
+ *   4b. gs_tri_dist_need     the targets of crows held in neither C nor R, ascending (so grouped by
+ *      owner) into req_out[capacity]; per owner: ids and row elements
+ *                                                           -> all-to-all of (ids, elements) per peer,
+ *                                                              then of the ids (req_counts sizes)
+ *   4c. gs_tri_dist_serve    the rows of the ids other ranks requested (req_in grouped by requester,
+ *      counts_in[p] ids from rank p) packed into rows_out[capacity]; send_elems[p] per requester
+ *                                                           -> all-to-all of the rows (send_elems / the
+ *                                                              req_elems of 4b)
+ *   4d. gs_tri_dist_assemble nbr, crows and the received rows at their window positions: full_out[M]
+ *      holds every row this rank's count share reads (the rest is zero)
+ *   5. gs_tri_dist_count     this rank's share (part = rank, nparts = ranks) of the count over
+ *      full_out                                             -> all-reduce (sum) of the counts
  *   6. windows with self-loops (summed loops > 0): the self-pair term needs whole neighbour sets, so
  *      the records are gathered and rank 0 adds gs_window_triangles_selfpair of the whole window.
- * Exchanged per window: 8 B per local record (step 3), 4 B per unique edge + 4 B per id (step 4).
- * Buffers: deg, keys_out, keys, nbr_out, dplus_out, nbr, dplus are device memory. */
+ * Exchanged per window: 8 B per local record (step 3), 4 B per id (dplus) and 4 B per element of the
+ * boundary rows a rank reads but did not build (step 4; R-MAT: 0.25-0.56 of the all-gathered
+ * adjacency at 2-8 ranks).  Buffers: deg, keys_out, keys, nbr_out, dplus_out, crows,
+ * req_out, req_in, rows_out, rows_in, full_out, nbr, dplus are device memory; counts and sizes host. */
 GS_API gs_status gs_tri_dist_range(gs_ctx* ctx, const gs_edge_batch* local, int64_t* minmax /* [2] */);
 GS_API gs_status gs_tri_dist_degrees(gs_ctx* ctx, const gs_edge_batch* local, int64_t id_min, int64_t id_max,
                                      uint32_t* deg, uint64_t* V);
@@ -282,6 +300,17 @@ GS_API gs_status gs_tri_dist_route(gs_ctx* ctx, const gs_edge_batch* local, cons
                                    uint64_t* loops /* host */);
 GS_API gs_status gs_tri_dist_build(gs_ctx* ctx, const uint64_t* keys, uint64_t n, uint32_t* nbr_out /* [n] */,
                                    uint32_t* dplus_out /* [V] */, uint64_t* m_out);
+GS_API gs_status gs_tri_dist_plan(gs_ctx* ctx, const uint32_t* dplus, uint32_t part, uint32_t nparts,
+                                  uint64_t* send_elems /* host [nparts] */, uint64_t* recv_elems /* host [nparts] */,
+                                  uint64_t* M);
+GS_API gs_status gs_tri_dist_need(gs_ctx* ctx, const uint32_t* crows, uint32_t* req_out, uint64_t capacity,
+                                  uint64_t* req_counts /* host [nparts] */, uint64_t* req_elems /* host [nparts] */,
+                                  uint64_t* nreq);
+GS_API gs_status gs_tri_dist_serve(gs_ctx* ctx, const uint32_t* nbr, const uint32_t* req_in,
+                                   const uint64_t* counts_in /* host [nparts] */, uint32_t* rows_out, uint64_t capacity,
+                                   uint64_t* send_elems /* host [nparts] */);
+GS_API gs_status gs_tri_dist_assemble(gs_ctx* ctx, const uint32_t* nbr, const uint32_t* crows, const uint32_t* rows_in,
+                                      uint32_t* full_out /* [M] */);
 GS_API gs_status gs_tri_dist_count(gs_ctx* ctx, const uint32_t* nbr, uint64_t M, const uint32_t* dplus, uint32_t part,
                                    uint32_t nparts, uint64_t* partial_count);
 /* The self-pair term alone (WindowTriangles.java:105: (x, x) candidates matched by a self-loop on x)

@@ -118,6 +118,64 @@ class OracleTriEngine:
         u, v = k >> self.B, k & ((1 << self.B) - 1)
         return torch.from_numpy(v.astype(np.int32)), torch.from_numpy(np.bincount(u, minlength=V).astype(np.int32))
 
+    def tri_dist_plan(self, dplus, part, nparts):
+        """gs_tri_dist_plan: count ranges C_q (equal work), route ranges R_q (owner(u) = u * P >> B), and
+        the elements of C_q ∩ R_part / C_part ∩ R_q"""
+        dp = self._np(dplus).astype(np.int64)
+        V, B, P = len(dp), self.B, nparts
+        pre = np.concatenate([[0], np.cumsum(dp)])
+        prew = np.concatenate([[0], np.cumsum(dp * (dp + 1) // 2)])
+        W = int(prew[V])
+        lower = lambda t: int(np.searchsorted(prew[:V], t, side="left"))
+        cq = [0 if q == 0 else V if q == P else lower(W * q // P) for q in range(P + 1)]
+        rq = [min(V, -(-(q << B) // P)) for q in range(P + 1)]
+
+        def inter(a, b):
+            u0, u1 = max(cq[a], rq[b]), min(cq[a + 1], rq[b + 1])
+            return int(pre[u1] - pre[u0]) if u0 < u1 else 0
+
+        self.bd = dict(dp=dp, pre=pre, c=(cq[part], cq[part + 1]), r=(rq[part], rq[part + 1]), P=P)
+        recv = [inter(part, q) for q in range(P)]
+        # what an all-gather would have received vs the boundary exchange (rows of C, then requested rows)
+        self.allgather_elems = int(pre[V] - (pre[rq[part + 1]] - pre[rq[part]]))
+        self.boundary_elems = sum(recv) - inter(part, part)
+        return [inter(q, part) for q in range(P)], recv, int(pre[V])
+
+    def tri_dist_need(self, crows, nparts, V):
+        bd, cr = self.bd, self._np(crows).astype(np.int64)
+        (c0, c1), (r0, r1), dp = bd["c"], bd["r"], bd["dp"]
+        v = cr[((cr < c0) | (cr >= c1)) & ((cr < r0) | (cr >= r1))]
+        ids = np.unique(v[dp[v] > 0])
+        own = (ids * nparts) >> self.B
+        self.req = ids
+        counts = np.bincount(own, minlength=nparts).tolist()
+        elems = np.bincount(own, weights=dp[ids], minlength=nparts).astype(np.int64).tolist()
+        self.boundary_elems += sum(elems)
+        return torch.from_numpy(ids.astype(np.int32)), counts, elems
+
+    def tri_dist_serve(self, nbr, req_in, counts_in, elems_in):
+        bd, nb, ids = self.bd, self._np(nbr), self._np(req_in).astype(np.int64)
+        pre, dp, r0 = bd["pre"], bd["dp"], bd["r"][0]
+        assert all(bd["r"][0] <= v < bd["r"][1] for v in ids)
+        rows = [nb[pre[v] - pre[r0]: pre[v] - pre[r0] + dp[v]] for v in ids]
+        bounds = np.concatenate([[0], np.cumsum(counts_in)]).astype(np.int64)
+        send = [int(sum(dp[v] for v in ids[bounds[q]:bounds[q + 1]])) for q in range(len(counts_in))]
+        out = np.concatenate(rows).astype(np.int32) if rows else np.zeros(0, np.int32)
+        return torch.from_numpy(out), send
+
+    def tri_dist_assemble(self, nbr, crows, rows_in, M):
+        bd = self.bd
+        pre, dp = bd["pre"], bd["dp"]
+        full = np.zeros(M, np.int32)
+        (c0, c1), (r0, r1) = bd["c"], bd["r"]
+        full[pre[r0]:pre[r1]] = self._np(nbr)
+        full[pre[c0]:pre[c1]] = self._np(crows)
+        ri, at = self._np(rows_in), 0
+        for v in self.req:
+            full[pre[v]:pre[v] + dp[v]] = ri[at:at + dp[v]]
+            at += dp[v]
+        return torch.from_numpy(full)
+
     def tri_dist_count(self, nbr, dplus, part, nparts):
         nbr, dp = self._np(nbr).astype(np.int64), self._np(dplus).astype(np.int64)
         V = len(dp)
@@ -323,3 +381,47 @@ def test_owner_split_is_balanced():
     keys = np.arange(1 << 20, dtype=np.int64)
     c = np.bincount(owner_np(keys, 8), minlength=8)
     assert c.min() > 0.98 * c.max()
+
+
+def _tri_worker(rank, world, port, q):
+    sys.path.insert(0, str(ROOT))
+    import __graft_entry__ as ge
+    ge.load_package()
+    from gelly_streaming_amd import distributed as D
+    orc = ge.load_oracle()
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    te = OracleTriEngine(orc)
+    n = 12000
+    ts, td = orc.gen_rmat(12, n, 0x5EED09, no_self_loops=True, first_edge=rank * n)
+    got = D.triangles_window(te, torch.from_numpy(ts), torch.from_numpy(td))
+    q.put((rank, (got, te.boundary_elems, te.allgather_elems)))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [3, 4])
+def test_split_window_triangles_boundary_exchange(oracle, world):
+    """WindowTriangles over a window split across 3 / 4 gloo ranks: the boundary adjacency (rows of each
+    rank's count range, then the rows of their targets it holds in neither range) gives the whole
+    window's count on every rank; no rank receives more row elements than an all-gather of every other
+    rank's out-lists would deliver, and the ranks together receive well under it."""
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_tri_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = dict(q.get(timeout=300) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    ts, td = oracle.gen_rmat(12, 12000 * world, 0x5EED09, no_self_loops=True)
+    w, ex, _ = oracle.window_triangles_fwd(ts, td)
+    assert ex > 0
+    for r in range(world):
+        got, bnd, full = out[r]
+        assert got == (ex, w, True), (r, got, ex)
+        assert bnd <= full, (r, bnd, full)
+    # over the ranks, far less than every rank receiving every other rank's rows
+    assert sum(out[r][1] for r in range(world)) < 0.8 * sum(out[r][2] for r in range(world)), out
