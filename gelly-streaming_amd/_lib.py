@@ -36,7 +36,7 @@ EXPORTS = ("gs_abi_version", "gs_create", "gs_destroy", "gs_last_error", "gs_set
            "gs_window_fold_degree_max", "gs_window_csr", "gs_window_candidates", "gs_window_candidates_part",
            "gs_window_triangles",
            "gs_window_triangles_part", "gs_window_count_candidates", "gs_tri_dist_range", "gs_tri_dist_degrees",
-           "gs_tri_dist_route", "gs_tri_dist_build", "gs_tri_dist_plan", "gs_tri_dist_need", "gs_tri_dist_serve",
+           "gs_tri_dist_orient", "gs_tri_dist_route", "gs_tri_dist_build", "gs_tri_dist_plan", "gs_tri_dist_need", "gs_tri_dist_serve",
            "gs_tri_dist_assemble", "gs_tri_dist_count", "gs_window_triangles_selfpair",
            "gs_window_triangles_dist", "gs_window_components",
            "gs_parse_edges_text", "gs_fetch_last_output", "gs_fetch_last_degree_output", "gs_owner_of", "gs_window_reduce_partials", "gs_window_fold_degree_max_partials",
@@ -168,7 +168,8 @@ def load() -> ctypes.CDLL:
         "gs_window_triangles_part": (st, [P, ctypes.POINTER(GsEdgeBatch), u32, u32, ctypes.POINTER(u64)]),
         "gs_tri_dist_range": (st, [P, ctypes.POINTER(GsEdgeBatch), ctypes.POINTER(i64)]),
         "gs_tri_dist_degrees": (st, [P, ctypes.POINTER(GsEdgeBatch), i64, i64, P, ctypes.POINTER(u64)]),
-        "gs_tri_dist_route": (st, [P, ctypes.POINTER(GsEdgeBatch), P, u32, P, ctypes.POINTER(u64), ctypes.POINTER(u64)]),
+        "gs_tri_dist_orient": (st, [P, ctypes.POINTER(GsEdgeBatch), P, P, ctypes.POINTER(u64)]),
+        "gs_tri_dist_route": (st, [P, P, u32, P, P]),
         "gs_tri_dist_build": (st, [P, P, u64, P, P, ctypes.POINTER(u64)]),
         "gs_tri_dist_plan": (st, [P, P, u32, u32, P, P, ctypes.POINTER(u64)]),
         "gs_tri_dist_need": (st, [P, P, P, u64, P, P, ctypes.POINTER(u64)]),

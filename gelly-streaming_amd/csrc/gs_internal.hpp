@@ -29,6 +29,12 @@ struct Sorted {
   bool fused = false;       // the last pass ran fused with the combine (gs_combine.hpp)
 };
 
+// split points of the split-window triangle route: owner q holds the degree-order ranks
+// [s[q], s[q + 1]) (up to 64 parts); passed to kernels by value
+struct RtSplit {
+  uint32_t s[65];
+};
+
 }  // namespace gs
 
 struct gs_ctx {
@@ -83,6 +89,11 @@ struct gs_ctx {
   uint64_t bd_c0 = 0, bd_c1 = 0, bd_r0 = 0, bd_r1 = 0, bd_pc0 = 0, bd_pc1 = 0, bd_pr0 = 0, bd_pr1 = 0, bd_M = 0;
   uint64_t bd_nreq = 0;
   bool bd_ok = false;
+  // the route step's split points (owner ranges of the degree order) and the oriented keys it waits
+  // for (rt_n local keys in aux, valid while rt_seq == call_seq)
+  gs::RtSplit rt_split{};
+  uint64_t rt_n = ~0ull, rt_seq = 0;
+  uint32_t rt_nparts = 0;
   gs::DevBuf tri_bd[4];
   // HashSet-order pipeline (gs_hashset.hip)
   gs::DevBuf hs[40];

@@ -336,13 +336,55 @@ __global__ __launch_bounds__(256) void k_tri_dplus(const uint2* __restrict__ out
     dplus[u] = out_range[u].y - out_range[u].x;
 }
 
-// ---- routing oriented keys to owner(u) = u * nparts >> B (contiguous u ranges) ----------------------
+// ---- routing oriented keys to owner(u): contiguous u ranges [split[q], split[q + 1]) of the degree
+// order, cut at equal shares of the raw work (gs_tri_dist_route) ---------------------------------------
 constexpr int RT_BLOCK = 256, RT_ITEMS = 16, RT_TILE = RT_BLOCK * RT_ITEMS, RT_MAXP = 64;
-__device__ __forceinline__ uint32_t tri_owner(uint64_t key, uint32_t B, uint32_t nparts) {
-  return (uint32_t)(((key >> B) * nparts) >> B);
+static_assert(sizeof(RtSplit) == (RT_MAXP + 1) * 4, "RtSplit");   // split[0] = 0 <= .. <= split[nparts] = V
+__device__ __forceinline__ uint32_t tri_owner(uint64_t key, uint32_t B, uint32_t nparts, const RtSplit& sp) {
+  const uint32_t u = (uint32_t)(key >> B);
+  uint32_t a = 0, b = nparts;   // the last q with split[q] <= u
+  while (b - a > 1) {
+    const uint32_t m = (a + b) >> 1;
+    if (sp.s[m] <= u) a = m;
+    else b = m;
+  }
+  return a;
+}
+// raw (with duplicates) oriented out-degree of the local keys: dout[u] += 1 per key u << B | v
+__global__ __launch_bounds__(256) void k_tri_dout(const uint64_t* __restrict__ keys, uint64_t n, uint32_t B,
+                                                  uint32_t* __restrict__ dout) {
+  const uint64_t sent = (B * 2 >= 64) ? ~0ull : ((1ull << (2 * B)) - 1);
+  for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) {
+    const uint64_t k = keys[i];
+    if (k != sent) atomicAdd(&dout[k >> B], 1u);
+  }
+}
+// raw work of u: dout(dout + 1) / 2
+__global__ __launch_bounds__(256) void k_tri_rawwork(const uint32_t* __restrict__ dout, uint32_t V,
+                                                     unsigned long long* __restrict__ w) {
+  for (uint32_t u = blockIdx.x * 256u + threadIdx.x; u < V; u += gridDim.x * 256u) {
+    const uint64_t d = dout[u];
+    w[u] = d * (d + 1) / 2;
+  }
+}
+// split points at equal shares of the work prefix pre (pre[V] = total): out[q], q = 0..P
+__global__ void k_tri_split(const unsigned long long* __restrict__ pre, uint32_t V, uint32_t P,
+                            unsigned long long* __restrict__ out) {
+  const uint32_t q = threadIdx.x;
+  if (q > P) return;
+  const unsigned long long W = pre[V];
+  uint32_t a = 0, b = V;
+  const unsigned long long t = W * q / P;
+  while (a < b) {
+    const uint32_t m = (a + b) >> 1;
+    if (pre[m] < t) a = m + 1;
+    else b = m;
+  }
+  out[q] = q == 0 ? 0u : q == P ? V : a;
 }
 __global__ __launch_bounds__(RT_BLOCK) void k_route_count(const uint64_t* __restrict__ keys, uint64_t n, uint32_t B,
-                                                          uint32_t nparts, uint32_t tiles, uint32_t* __restrict__ cnt) {
+                                                          uint32_t nparts, RtSplit sp, uint32_t tiles,
+                                                          uint32_t* __restrict__ cnt) {
   __shared__ uint32_t s_c[RT_MAXP];
   const int tid = threadIdx.x;
   if (tid < RT_MAXP) s_c[tid] = 0;
@@ -351,7 +393,7 @@ __global__ __launch_bounds__(RT_BLOCK) void k_route_count(const uint64_t* __rest
   const uint64_t sent = (B * 2 >= 64) ? ~0ull : ((1ull << (2 * B)) - 1);
   for (int j = 0; j < RT_ITEMS; ++j) {
     const uint64_t i = base + (uint64_t)j * RT_BLOCK + tid;
-    if (i < n && keys[i] != sent) atomicAdd(&s_c[tri_owner(keys[i], B, nparts)], 1u);
+    if (i < n && keys[i] != sent) atomicAdd(&s_c[tri_owner(keys[i], B, nparts, sp)], 1u);
   }
   __syncthreads();
   if (tid < (int)nparts) cnt[(uint64_t)tid * tiles + blockIdx.x] = s_c[tid];
@@ -359,7 +401,7 @@ __global__ __launch_bounds__(RT_BLOCK) void k_route_count(const uint64_t* __rest
 // (k_rank_scan: the exclusive scan, owner-major) then the scatter; order inside an owner is free
 // (the owner sorts what it receives)
 __global__ __launch_bounds__(RT_BLOCK) void k_route_scatter(const uint64_t* __restrict__ keys, uint64_t n, uint32_t B,
-                                                            uint32_t nparts, uint32_t tiles,
+                                                            uint32_t nparts, RtSplit sp, uint32_t tiles,
                                                             const uint32_t* __restrict__ off, uint64_t* __restrict__ out) {
   __shared__ uint32_t s_c[RT_MAXP];
   const int tid = threadIdx.x;
@@ -371,7 +413,7 @@ __global__ __launch_bounds__(RT_BLOCK) void k_route_scatter(const uint64_t* __re
     const uint64_t i = base + (uint64_t)j * RT_BLOCK + tid;
     if (i < n) {
       const uint64_t k = keys[i];
-      if (k != sent) out[atomicAdd(&s_c[tri_owner(k, B, nparts)], 1u)] = k;
+      if (k != sent) out[atomicAdd(&s_c[tri_owner(k, B, nparts, sp)], 1u)] = k;
     }
   }
 }
@@ -412,17 +454,18 @@ __global__ __launch_bounds__(256) void k_tri_loops(const int64_t* __restrict__ s
 
 // ---- boundary adjacency of a split window (gs_tri_dist_plan .. _assemble) ----------------------------
 // The count share of rank `part` (u in its equal-work range C = [c0, c1)) reads the rows N+(u), u in C,
-// and the rows N+(v) of their targets v; rank q built the rows of its route range R_q = [r_q, r_q+1)
-// (owner(u) = u * P >> B).  So instead of every row, a rank fetches the rows of C (contiguous: one
-// all-to-all whose sizes every rank computes from the global d+) and then requests the rows of the
-// targets it holds neither in C nor in R (one all-to-all of ids, one of rows).  dp = d+ (u64), pre =
+// and the rows N+(v) of their targets v; rank q built the rows of its route range R_q = [r_q, r_q+1),
+// cut at equal shares of the raw work (duplicates included), so R_q is nearly C_q.  So instead of
+// every row, a rank fetches the rows of C it did not build (contiguous: one all-to-all whose sizes every
+// rank computes from the global d+) and then requests the rows of the targets it holds neither in C nor
+// in R (one all-to-all of ids, one of rows).  dp = d+ (u64), pre =
 // its exclusive prefix (the window positions of the rows).
 struct BdGroups {   // group starts (ids) of up to 64 requesters (+ the end), by value
   uint64_t g[65];
 };
 // split points of every part: c_q (equal work), r_q (owner ranges), and the window position of each
 __global__ void k_bd_bounds(const unsigned long long* __restrict__ prew, const unsigned long long* __restrict__ pre,
-                            uint32_t V, uint32_t B, uint32_t P, unsigned long long* __restrict__ out) {
+                            uint32_t V, RtSplit sp, uint32_t P, unsigned long long* __restrict__ out) {
   const uint32_t q = threadIdx.x;
   if (q > P) return;
   const unsigned long long W = prew[V];
@@ -436,8 +479,7 @@ __global__ void k_bd_bounds(const unsigned long long* __restrict__ prew, const u
     return a;
   };
   const uint32_t cq = q == 0 ? 0u : q == P ? V : lower(W * q / P);
-  const uint64_t sq = (uint64_t)q << B;
-  const uint32_t rq = (uint32_t)min((uint64_t)V, sq / P + (sq % P ? 1u : 0u));   // first u with u * P >> B == q
+  const uint32_t rq = sp.s[q];   // the route split: rank q built the rows of [r_q, r_q+1)
   out[q] = cq;
   out[P + 1 + q] = rq;
   out[2 * (P + 1) + q] = pre[cq];
@@ -929,14 +971,13 @@ gs_status gs_tri_dist_degrees(gs_ctx* c, const gs_edge_batch* b, int64_t gmin, i
   return host_wait(c);
 }
 
-gs_status gs_tri_dist_route(gs_ctx* c, const gs_edge_batch* b, const uint32_t* deg, uint32_t nparts, uint64_t* keys_out,
-                            uint64_t* counts, uint64_t* loops) {
+gs_status gs_tri_dist_orient(gs_ctx* c, const gs_edge_batch* b, const uint32_t* deg, uint32_t* dout, uint64_t* loops) {
   if (!c) return GS_EINVAL;
   GS_TRY(check_batch(c, b, GS_DIR_ALL));
-  if (!deg || !counts || !loops || (b->n && !keys_out)) return set_error(c, GS_EINVAL, "null pointer");
-  if (nparts < 1 || nparts > (uint32_t)RT_MAXP) return set_error(c, GS_EINVAL, "nparts %u outside [1, 64]", nparts);
+  if (!deg || !dout || !loops) return set_error(c, GS_EINVAL, "null pointer");
   if (!c->tri_B) return set_error(c, GS_EINVAL, "gs_tri_dist_degrees first (the window's id geometry)");
   GS_TRY(begin_call(c));
+  c->rt_n = ~0ull;
   TriGeom g;
   GS_TRY(dist_stage(c, b, &g));
   GS_TRY(ensure(c, c->out_b, g.V * 4));
@@ -944,25 +985,64 @@ gs_status gs_tri_dist_route(gs_ctx* c, const gs_edge_batch* b, const uint32_t* d
   GS_TRY(tri_ranks(c, g, deg, rank));
   GS_TRY(ensure(c, c->aux, g.n * 8 + 8));
   GS_TRY(tri_okeys(c, g, rank, c->aux.as<uint64_t>()));
-  const uint32_t tiles = (uint32_t)std::max<uint64_t>(1, (g.n + RT_TILE - 1) / RT_TILE);
+  GS_HIP(hipMemsetAsync(dout, 0, g.V * 4, c->stream));
+  if (g.n)
+    hipLaunchKernelGGL(k_tri_dout, dim3((unsigned)std::min<uint64_t>((g.n + 255) / 256, 16384)), dim3(256), 0, c->stream,
+                       c->aux.as<uint64_t>(), g.n, g.B, dout);
+  GS_HIP(hipGetLastError());
+  GS_TRY(host_wait(c));
+  *loops = c->host_small[4];
+  c->rt_n = g.n;   // the oriented keys wait in c->aux for gs_tri_dist_route
+  c->rt_seq = c->call_seq;
+  return GS_OK;
+}
+
+gs_status gs_tri_dist_route(gs_ctx* c, const uint32_t* dout, uint32_t nparts, uint64_t* keys_out, uint64_t* counts) {
+  if (!c) return GS_EINVAL;
+  if (!dout || !counts) return set_error(c, GS_EINVAL, "null pointer");
+  if (nparts < 1 || nparts > (uint32_t)RT_MAXP) return set_error(c, GS_EINVAL, "nparts %u outside [1, 64]", nparts);
+  if (c->rt_n == ~0ull || c->rt_seq != c->call_seq) return set_error(c, GS_EINVAL, "gs_tri_dist_orient first");
+  const uint64_t n = c->rt_n;
+  if (n && !keys_out) return set_error(c, GS_EINVAL, "null keys_out");
+  GS_HIP(hipSetDevice(c->device));
+  (void)hipGetLastError();
+  const uint32_t B = c->tri_B;
+  const size_t V = 1ull << B;
+  // split points at equal shares of the raw work (the same on every rank: dout is the all-reduced one)
+  GS_TRY(ensure(c, c->tri_hwork, (V * 2 + 2) * 8));
+  GS_TRY(ensure(c, c->tri_bd[3], 8 * 65 * 8));
+  unsigned long long* w = c->tri_hwork.as<unsigned long long>();
+  unsigned long long* sp_d = c->tri_bd[3].as<unsigned long long>() + 7 * 65;
+  const unsigned gv = (unsigned)std::min<uint64_t>((V + 255) / 256, 16384);
+  hipLaunchKernelGGL(k_tri_rawwork, dim3(gv), dim3(256), 0, c->stream, dout, (uint32_t)V, w);
+  GS_TRY(xscan(c, (const uint64_t*)w, V, (uint64_t*)w + V + 1));
+  hipLaunchKernelGGL(k_tri_split, dim3(1), dim3(128), 0, c->stream, (const unsigned long long*)w + V + 1, (uint32_t)V,
+                     nparts, sp_d);
+  GS_HIP(hipGetLastError());
+  GS_HIP(hipMemcpyAsync(c->host_small + 64, sp_d, (nparts + 1) * 8, hipMemcpyDeviceToHost, c->stream));
+  GS_TRY(host_wait(c));
+  RtSplit sp;
+  for (uint32_t q = 0; q <= nparts; ++q) sp.s[q] = (uint32_t)c->host_small[64 + q];
+  c->rt_split = sp;
+  c->rt_nparts = nparts;
+  const uint32_t tiles = (uint32_t)std::max<uint64_t>(1, (n + RT_TILE - 1) / RT_TILE);
   GS_TRY(ensure(c, c->tri_tiles, (size_t)tiles * nparts * 4 + 8));
   uint32_t* cnt = c->tri_tiles.as<uint32_t>();
-  if (g.n) {
-    hipLaunchKernelGGL(k_route_count, dim3(tiles), dim3(RT_BLOCK), 0, c->stream, c->aux.as<uint64_t>(), g.n, g.B, nparts,
+  const uint64_t kept = n - c->host_small[4];
+  if (n) {
+    hipLaunchKernelGGL(k_route_count, dim3(tiles), dim3(RT_BLOCK), 0, c->stream, c->aux.as<uint64_t>(), n, B, nparts, sp,
                        tiles, cnt);
     hipLaunchKernelGGL(k_rank_scan, dim3(1), dim3(1024), 0, c->stream, cnt, tiles * nparts);
-    hipLaunchKernelGGL(k_route_scatter, dim3(tiles), dim3(RT_BLOCK), 0, c->stream, c->aux.as<uint64_t>(), g.n, g.B,
-                       nparts, tiles, cnt, keys_out);
+    hipLaunchKernelGGL(k_route_scatter, dim3(tiles), dim3(RT_BLOCK), 0, c->stream, c->aux.as<uint64_t>(), n, B, nparts,
+                       sp, tiles, cnt, keys_out);
     GS_HIP(hipGetLastError());
     // owner o's keys start at cnt[o * tiles] (exclusive scan, owner-major)
     for (uint32_t o = 0; o < nparts; ++o)
       GS_HIP(hipMemcpyAsync((uint32_t*)(c->host_small + 16) + o, cnt + (size_t)o * tiles, 4, hipMemcpyDeviceToHost, c->stream));
   }
   GS_TRY(host_wait(c));
-  *loops = c->host_small[4];
-  const uint64_t kept = g.n - *loops;
   const uint32_t* st = (const uint32_t*)(c->host_small + 16);
-  for (uint32_t o = 0; o < nparts; ++o) counts[o] = g.n ? (o + 1 < nparts ? st[o + 1] : kept) - st[o] : 0;
+  for (uint32_t o = 0; o < nparts; ++o) counts[o] = n ? (o + 1 < nparts ? st[o + 1] : kept) - st[o] : 0;
   return GS_OK;
 }
 
@@ -1038,6 +1118,7 @@ gs_status gs_tri_dist_plan(gs_ctx* c, const uint32_t* dplus, uint32_t part, uint
   if (!dplus || !send_elems || !recv_elems || !M_out) return set_error(c, GS_EINVAL, "null pointer");
   if (nparts == 0 || nparts > 64 || part >= nparts) return set_error(c, GS_EINVAL, "bad part %u of %u", part, nparts);
   if (!c->tri_B) return set_error(c, GS_EINVAL, "gs_tri_dist_degrees first (the window's id geometry)");
+  if (c->rt_nparts != nparts) return set_error(c, GS_EINVAL, "gs_tri_dist_route over %u parts first", nparts);
   GS_TRY(begin_call(c));
   c->bd_ok = false;
   const uint32_t B = c->tri_B, P = nparts;
@@ -1058,7 +1139,7 @@ gs_status gs_tri_dist_plan(gs_ctx* c, const uint32_t* dplus, uint32_t part, uint
   hipLaunchKernelGGL(k_tri_work, dim3(gv), dim3(256), 0, c->stream, out_range, (uint32_t)V, work);
   GS_TRY(xscan(c, (const uint64_t*)work, V, (uint64_t*)work + V + 1));
   hipLaunchKernelGGL(k_bd_bounds, dim3(1), dim3(128), 0, c->stream, (const unsigned long long*)work + V + 1,
-                     (const unsigned long long*)d64 + V, (uint32_t)V, B, P, bnd);
+                     (const unsigned long long*)d64 + V, (uint32_t)V, c->rt_split, P, bnd);
   GS_HIP(hipGetLastError());
   GS_HIP(hipMemcpyAsync(c->host_small + 64, bnd, 4 * (P + 1) * 8, hipMemcpyDeviceToHost, c->stream));
   GS_HIP(hipMemcpyAsync(c->host_small + 63, (const unsigned long long*)d64 + 2 * V, 8, hipMemcpyDeviceToHost, c->stream));
@@ -1281,11 +1362,16 @@ gs_status gs_window_triangles_dist(gs_ctx* c, const gs_edge_batch* b, uint64_t* 
   if (st == GS_OK) st = gs_tri_dist_degrees(c, b, gmin, gmax, deg, &V);
   GS_TRY(comm_agree(c, st));
   GS_TRY(comm_allreduce(c, deg, V, NCCL_T_U32, NCCL_OP_SUM));
-  // 3. oriented edges to owner(u): counts matrix, then the rows
+  // 3. oriented edges; their raw out-degrees summed (the route's owner ranges cut the raw work in equal
+  //    shares, the same on every rank); keys to owner(u): counts matrix, then the rows
   std::vector<uint64_t> send(P), recv(P);
   uint64_t loops = 0;
+  GS_TRY(ensure(c, c->tri_d[6], V * 4 + 4));
+  uint32_t* dout = c->tri_d[6].as<uint32_t>();
+  GS_TRY(comm_agree(c, gs_tri_dist_orient(c, b, deg, dout, &loops)));
+  GS_TRY(comm_allreduce(c, dout, V, NCCL_T_U32, NCCL_OP_SUM));
   st = ensure(c, c->tri_d[2], b->n * 8 + 8);
-  if (st == GS_OK) st = gs_tri_dist_route(c, b, deg, P, c->tri_d[2].as<uint64_t>(), send.data(), &loops);
+  if (st == GS_OK) st = gs_tri_dist_route(c, dout, P, c->tri_d[2].as<uint64_t>(), send.data());
   GS_TRY(comm_agree(c, st));
   GS_TRY(ensure(c, c->tri_d[0], 64 + (size_t)P * P * 8));
   uint64_t* dmat = (uint64_t*)(c->tri_d[0].as<char>() + 64);

@@ -187,7 +187,8 @@ def triangles_window(eng, src, dst, group=None):
     collectives in torch.distributed: nothing of the raw window travels (unless it has self-loops):
       1. id range          all-reduce MIN / MAX
       2. raw degrees       all-reduce SUM of an int32[V]          (every rank renumbers identically)
-      3. oriented edges    all-to-all of 8-byte keys to owner(u)  (contiguous ranges of the degree order)
+      3. oriented edges    all-reduce SUM of their raw out-degrees int32[V]; all-to-all of 8-byte keys to
+                           owner(u) (ranges of the degree order at equal shares of the raw work)
       4. out-lists         all-reduce SUM of d+ int32[V]; then the boundary adjacency: the rows of this
                            rank's equal-work count range (all-to-all, sizes from d+), the rows of their
                            targets it holds in neither range (all-to-all of ids, then of rows)
@@ -213,7 +214,10 @@ def triangles_window(eng, src, dst, group=None):
     deg = eng.tri_dist_degrees(src, dst, gmin, gmax)
     d = deg.to(cdev)
     dist.all_reduce(d, op=dist.ReduceOp.SUM, group=group)
-    keys, counts, loops = eng.tri_dist_route(src, dst, d.to(home), world)
+    dout, loops = eng.tri_dist_orient(src, dst, d.to(home))
+    do = dout.to(cdev)
+    dist.all_reduce(do, op=dist.ReduceOp.SUM, group=group)
+    keys, counts = eng.tri_dist_route(do.to(home), world)
     send = torch.tensor(counts, dtype=torch.int64, device=cdev)
     recv = torch.empty_like(send)
     dist.all_to_all_single(recv, send, group=group)

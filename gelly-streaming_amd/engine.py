@@ -367,18 +367,29 @@ class Engine:
                                                 ctypes.byref(V)))
         return deg
 
-    def tri_dist_route(self, src, dst, deg, nparts: int):
-        """Step 3: oriented edges grouped by owner(u): (int64 keys tensor, rows per owner, self-loops)."""
+    def tri_dist_orient(self, src, dst, deg):
+        """Step 3a: this rank's oriented edges (kept for step 3b) -> (int32 raw out-degrees dout [V], local
+        self-loops); all-reduce SUM of both."""
         import torch
 
         b, keep, dev = self._batch(src, dst, None)
-        keys = torch.empty(max(b.n, 1), dtype=torch.int64, device=f"cuda:{self.device}")
-        counts = (ctypes.c_uint64 * nparts)()
+        dout = torch.empty(deg.numel(), dtype=torch.int32, device=f"cuda:{self.device}")
         loops = ctypes.c_uint64(0)
-        self._check(self._L.gs_tri_dist_route(self.ctx, ctypes.byref(b), _ptr(deg.contiguous()), nparts, _ptr(keys),
-                                              counts, ctypes.byref(loops)))
+        self._check(self._L.gs_tri_dist_orient(self.ctx, ctypes.byref(b), _ptr(deg.contiguous()), _ptr(dout),
+                                               ctypes.byref(loops)))
+        self._route_n = b.n
+        return dout, loops.value
+
+    def tri_dist_route(self, dout, nparts: int):
+        """Step 3b: the oriented edges grouped by owner(u) (ranges at equal shares of the raw work of the
+        summed dout): (int64 keys tensor, rows per owner)."""
+        import torch
+
+        keys = torch.empty(max(self._route_n, 1), dtype=torch.int64, device=f"cuda:{self.device}")
+        counts = (ctypes.c_uint64 * nparts)()
+        self._check(self._L.gs_tri_dist_route(self.ctx, _ptr(dout.contiguous()), nparts, _ptr(keys), counts))
         counts = [int(x) for x in counts]
-        return keys[:sum(counts)], counts, loops.value
+        return keys[:sum(counts)], counts
 
     def tri_dist_build(self, keys, V: int):
         """Step 4: the received rows -> this rank's out-lists: (int32 targets [m], int32 d+ [V])."""

@@ -262,9 +262,12 @@ GS_API gs_status gs_window_triangles_part(gs_ctx* ctx, const gs_edge_batch* batc
  *   1. gs_tri_dist_range     local [min, max] id            -> all-reduce min of [0], max of [1]
  *   2. gs_tri_dist_degrees   local raw degrees deg[V]       -> all-reduce (sum, u32) of deg
  *      (deg == NULL: *V only, to size the buffer; V = 2^bits of the common id span, <= 2^28)
- *   3. gs_tri_dist_route     oriented edges (u << B | v, u < v in the degree order) grouped by
- *      owner(u) (contiguous ranges of the order) into keys_out, counts[p] rows for rank p
- *                                                           -> all-to-all of the rows; all-reduce loops
+ *   3a. gs_tri_dist_orient   oriented edges (u << B | v, u < v in the degree order), kept in the ctx
+ *      for 3b; dout[V] = their count per u (raw, duplicates included); *loops = local self-loops
+ *                                                           -> all-reduce (sum, u32) of dout; of loops
+ *   3b. gs_tri_dist_route    owner ranges of the degree order cut at equal shares of the raw work
+ *      dout(dout+1)/2 (the same on every rank, so a rank builds nearly the rows it will count); the keys
+ *      grouped by owner(u) into keys_out, counts[p] rows for rank p   -> all-to-all of the rows
  *   4. gs_tri_dist_build     the received rows deduplicated into this rank's out-lists: nbr_out[m]
  *      (targets, sorted per u) and dplus_out[V] (d+(u) of the owned u, 0 elsewhere)
  *                                                           -> all-reduce (sum, u32) of dplus
@@ -288,16 +291,17 @@ GS_API gs_status gs_window_triangles_part(gs_ctx* ctx, const gs_edge_batch* batc
  *      full_out                                             -> all-reduce (sum) of the counts
  *   6. windows with self-loops (summed loops > 0): the self-pair term needs whole neighbour sets, so
  *      the records are gathered and rank 0 adds gs_window_triangles_selfpair of the whole window.
- * Exchanged per window: 8 B per local record (step 3), 4 B per id (dplus) and 4 B per element of the
+ * Exchanged per window: 4 B per id (deg, dout, dplus), 8 B per local record (step 3) and 4 B per element of the
  * boundary rows a rank reads but did not build (step 4; R-MAT: 0.25-0.56 of the all-gathered
  * adjacency at 2-8 ranks).  Buffers: deg, keys_out, keys, nbr_out, dplus_out, crows,
  * req_out, req_in, rows_out, rows_in, full_out, nbr, dplus are device memory; counts and sizes host. */
 GS_API gs_status gs_tri_dist_range(gs_ctx* ctx, const gs_edge_batch* local, int64_t* minmax /* [2] */);
 GS_API gs_status gs_tri_dist_degrees(gs_ctx* ctx, const gs_edge_batch* local, int64_t id_min, int64_t id_max,
                                      uint32_t* deg, uint64_t* V);
-GS_API gs_status gs_tri_dist_route(gs_ctx* ctx, const gs_edge_batch* local, const uint32_t* deg, uint32_t nparts,
-                                   uint64_t* keys_out /* [local n] */, uint64_t* counts /* host [nparts] */,
-                                   uint64_t* loops /* host */);
+GS_API gs_status gs_tri_dist_orient(gs_ctx* ctx, const gs_edge_batch* local, const uint32_t* deg,
+                                    uint32_t* dout /* [V] */, uint64_t* loops /* host */);
+GS_API gs_status gs_tri_dist_route(gs_ctx* ctx, const uint32_t* dout, uint32_t nparts,
+                                   uint64_t* keys_out /* [local n] */, uint64_t* counts /* host [nparts] */);
 GS_API gs_status gs_tri_dist_build(gs_ctx* ctx, const uint64_t* keys, uint64_t n, uint32_t* nbr_out /* [n] */,
                                    uint32_t* dplus_out /* [V] */, uint64_t* m_out);
 GS_API gs_status gs_tri_dist_plan(gs_ctx* ctx, const uint32_t* dplus, uint32_t part, uint32_t nparts,

@@ -99,7 +99,7 @@ class OracleTriEngine:
         half = np.where(lz > 0, (d >> np.maximum(lz - 1, 0)) & 1, 0)
         return np.where(d == 0, 0, np.minimum(63, 1 + 2 * lz + half))
 
-    def tri_dist_route(self, src, dst, deg, nparts):
+    def tri_dist_orient(self, src, dst, deg):
         B, V = self.B, 1 << self.B
         cls = self.deg_class(self._np(deg))
         rank = np.empty(V, np.int64)
@@ -108,10 +108,20 @@ class OracleTriEngine:
         keep = a != b
         ra, rb = rank[a[keep]], rank[b[keep]]
         u, v = np.minimum(ra, rb), np.maximum(ra, rb)
-        keys = (u << B) | v
-        own = (u * nparts) >> B
+        self.okeys = (u << B) | v
+        return torch.from_numpy(np.bincount(u, minlength=V).astype(np.int32)), int((~keep).sum())
+
+    def tri_dist_route(self, dout, nparts):
+        """owner ranges at equal shares of the raw work dout(dout+1)/2 (gs_tri_dist_route)"""
+        B, V = self.B, 1 << self.B
+        d = self._np(dout).astype(np.int64)
+        pre = np.concatenate([[0], np.cumsum(d * (d + 1) // 2)])
+        W = int(pre[V])
+        self.split = [0 if q == 0 else V if q == nparts else int(np.searchsorted(pre[:V], W * q // nparts, side="left"))
+                      for q in range(nparts + 1)]
+        own = np.searchsorted(np.array(self.split[1:nparts]), self.okeys >> B, side="right")
         order = np.argsort(own, kind="stable")
-        return torch.from_numpy(keys[order]), np.bincount(own, minlength=nparts).tolist(), int((~keep).sum())
+        return torch.from_numpy(self.okeys[order]), np.bincount(own, minlength=nparts).tolist()
 
     def tri_dist_build(self, keys, V):
         k = np.unique(self._np(keys))
@@ -128,7 +138,7 @@ class OracleTriEngine:
         W = int(prew[V])
         lower = lambda t: int(np.searchsorted(prew[:V], t, side="left"))
         cq = [0 if q == 0 else V if q == P else lower(W * q // P) for q in range(P + 1)]
-        rq = [min(V, -(-(q << B) // P)) for q in range(P + 1)]
+        rq = self.split   # the route's owner ranges
 
         def inter(a, b):
             u0, u1 = max(cq[a], rq[b]), min(cq[a + 1], rq[b + 1])
@@ -146,7 +156,7 @@ class OracleTriEngine:
         (c0, c1), (r0, r1), dp = bd["c"], bd["r"], bd["dp"]
         v = cr[((cr < c0) | (cr >= c1)) & ((cr < r0) | (cr >= r1))]
         ids = np.unique(v[dp[v] > 0])
-        own = (ids * nparts) >> self.B
+        own = np.searchsorted(np.array(self.split[1:nparts]), ids, side="right")
         self.req = ids
         counts = np.bincount(own, minlength=nparts).tolist()
         elems = np.bincount(own, weights=dp[ids], minlength=nparts).astype(np.int64).tolist()
@@ -198,7 +208,8 @@ class OracleTriEngine:
         s, d = self._np(src), self._np(dst)
         lo, hi = self.tri_dist_range(s, d)
         deg = self.tri_dist_degrees(s, d, lo, hi)
-        k, _, _ = self.tri_dist_route(s, d, deg, 1)
+        dout, _ = self.tri_dist_orient(s, d, deg)
+        k, _ = self.tri_dist_route(dout, 1)
         nbr, dp = self.tri_dist_build(k, len(deg))
         return self.orc.window_triangles_ref(s, d)[1] - self.tri_dist_count(nbr, dp, 0, 1)
 

@@ -254,8 +254,10 @@ def test_split_window_steps_and_rccl_world_one(pkg, oracle):
         lo, hi = e.tri_dist_range(S, Dd)
         assert (lo, hi) == (int(min(s.min(), d.min())), int(max(s.max(), d.max())))
         deg = e.tri_dist_degrees(S, Dd, lo, hi)
-        keys, counts, loops = e.tri_dist_route(S, Dd, deg, 1)
-        assert counts == [keys.numel()] and loops == int((s == d).sum())
+        dout, loops = e.tri_dist_orient(S, Dd, deg)
+        assert loops == int((s == d).sum()) and int(dout.sum()) == len(s) - loops
+        keys, counts = e.tri_dist_route(dout, 1)
+        assert counts == [keys.numel()] == [len(s) - loops]
         nbr, dplus = e.tri_dist_build(keys, deg.numel())
         assert int(dplus.sum()) == nbr.numel()
         T = sum(e.tri_dist_count(nbr, dplus, p, 3) for p in range(3))

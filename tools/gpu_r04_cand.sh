@@ -4,7 +4,7 @@ set -o pipefail
 cd "$(dirname "$0")/.."
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread -rP \
+timeout -k 10 600 python -u -m pytest -x -v --timeout 150 --timeout-method thread -rP \
   tests/test_gpu_candidates_chunked.py tests/test_gpu_fresh_process.py tests/test_gpu_api.py tests/test_gpu_dist.py \
   "tests/test_gpu_config_size.py::test_c5_window_candidate_records_vertex_ranges" \
   "tests/test_gpu_config_size.py::test_c5_window_candidate_count_vs_oracle" > gpurun_out/r04_cand_tests.log 2>&1 || exit 1
