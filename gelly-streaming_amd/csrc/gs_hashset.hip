@@ -282,6 +282,37 @@ __global__ __launch_bounds__(256) void k_cand_emit(const uint64_t* __restrict__ 
   }
   uint32_t sc = lo;
   for (uint64_t base = w0; base < w1; base += 256) {
+    // Fast path: the step lies inside one slot's pair rows (most records of a window: the blocks of its
+    // high-degree vertices are O(k^2)).  The slot's metadata is wave-uniform (scalar loads), the row of
+    // the step's first position is found once, and each lane walks forward from it (a 256-position span
+    // crosses at most ~23 rows: only a block's last rows are shorter than 12).
+    const uint64_t e1 = min(w1, base + 256);
+    if (vs[sc + 1] >= e1) {
+      const CandMeta m = meta[sc];
+      const uint64_t t0 = base - vs[sc];
+      if (t0 >= m.d && m.rows) {
+        const uint64_t k = m.k, rows = m.rows, q0 = t0 - m.d;
+        const double k2 = 2.0 * (double)k + 1.0;
+        uint64_t r0 = (uint64_t)fmax(0.0, (k2 - sqrt(fmax(0.0, k2 * k2 - 8.0 * (double)q0))) * 0.5);
+        if (r0 >= rows) r0 = rows - 1;
+        for (int g = 0; g < 64 && r0 > 0 && tri_rows_before(r0, k) > q0; ++g) --r0;
+        for (int g = 0; g < 64 && r0 + 1 < rows && tri_rows_before(r0 + 1, k) <= q0; ++g) ++r0;
+        const int64_t* G = gids + m.gbase;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const uint64_t oi = base + (uint64_t)(i * 64) + lane;
+          if (oi >= e1) continue;
+          const uint64_t q = q0 + (uint64_t)(i * 64) + lane;
+          uint64_t r = r0;
+          for (int g = 0; g < 64 && r + 1 < rows && tri_rows_before(r + 1, k) <= q; ++g) ++r;
+          const uint64_t col = min(q - tri_rows_before(r, k), k - 1 - r);
+          a[oi - P0] = G[r];
+          b[oi - P0] = G[r + col];
+          f[oi - P0] = 1;
+        }
+        continue;   // sc still holds the next step's first position, or an earlier slot
+      }
+    }
     uint64_t o[4];
     uint32_t slot[4];
     bool need[4];

@@ -203,6 +203,60 @@ __global__ __launch_bounds__(256) void k_tri_okeys(const int64_t* __restrict__ s
   flush_hist<4>(h, nd, hist);
 }
 
+// The same keys in two passes when the rank table outgrows the Infinity Cache (V > 2^25: 128 MB; C4's
+// scale 26 has a 256 MB table and one pass ran at the rate of its random gathers, 2 x 2^30 of them from
+// HBM): pass 1 resolves the endpoints below H through the lower half of the table and parks the rest
+// as id | ESC in a 2 x 32-bit pair; pass 2 resolves those through the upper half, orients, and counts
+// the sort's histograms.  Each pass gathers from a half table that the cache keeps.
+constexpr uint32_t OK_ESC = 1u << 31;
+__global__ __launch_bounds__(256) void k_tri_okeys_lo(const int64_t* __restrict__ src, const int64_t* __restrict__ dst,
+                                                      uint64_t n, uint64_t key_xor, uint32_t H,
+                                                      const uint32_t* __restrict__ rank, uint64_t* __restrict__ out,
+                                                      uint32_t* __restrict__ loop_bits,
+                                                      unsigned long long* __restrict__ loops) {
+  for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) {
+    const uint64_t a = (uint64_t)src[i] ^ key_xor, b = (uint64_t)dst[i] ^ key_xor;
+    uint64_t k = ~0ull;   // a self-loop: the sentinel (pass 2 keeps it)
+    if (a != b) {
+      const uint32_t xa = a < H ? rank[a] : ((uint32_t)a | OK_ESC), xb = b < H ? rank[b] : ((uint32_t)b | OK_ESC);
+      k = ((uint64_t)xa << 32) | xb;
+    } else {
+      atomicOr(&loop_bits[a >> 5], 1u << (a & 31));
+      atomicAdd(loops, 1ull);
+    }
+    out[i] = k;
+  }
+}
+__global__ __launch_bounds__(256) void k_tri_okeys_hi(uint64_t* __restrict__ keys, uint64_t n, uint32_t B,
+                                                      const uint32_t* __restrict__ rank, uint32_t* __restrict__ hist) {
+  __shared__ uint32_t h[4][8][RADIX];
+  const int tid = threadIdx.x, w = tid >> 6;
+  for (int i = tid; i < 4 * 8 * RADIX; i += 256) (&h[0][0][0])[i] = 0;
+  __syncthreads();
+  const int nd = (int)(2 * B + 7) / 8;
+  const uint64_t sent = (B * 2 >= 64) ? ~0ull : ((1ull << (2 * B)) - 1);
+  const uint64_t stride = (uint64_t)gridDim.x * 256;
+  for (uint64_t i0 = (uint64_t)blockIdx.x * 256; i0 < n; i0 += stride) {   // wave-uniform trip count
+    const uint64_t i = i0 + tid;
+    const bool ok = i < n;
+    uint64_t k = sent;
+    if (ok) {
+      const uint64_t x = keys[i];
+      if (x != ~0ull) {
+        uint32_t xa = (uint32_t)(x >> 32), xb = (uint32_t)x;
+        if (xa & OK_ESC) xa = rank[xa & ~OK_ESC];
+        if (xb & OK_ESC) xb = rank[xb & ~OK_ESC];
+        const uint64_t ra = xa, rb = xb;
+        k = ra < rb ? (ra << B) | rb : (rb << B) | ra;
+      }
+      keys[i] = k;
+    }
+    wave_hist_add(h[w], k, ok, nd);
+  }
+  __syncthreads();
+  flush_hist<4>(h, nd, hist);
+}
+
 // the unique oriented edges (sorted keys u << B | v) -> out-lists: nbr[p] = v, out_range[u] =
 // [first, last + 1) (ranges of absent vertices were zeroed)
 __global__ __launch_bounds__(256) void k_tri_out(const uint64_t* __restrict__ keys, uint32_t M, uint32_t B,
@@ -665,7 +719,16 @@ gs_status tri_okeys(gs_ctx* c, const TriGeom& g, const uint32_t* rank, uint64_t*
   unsigned long long* d_loops = (unsigned long long*)(sm + SM_NUNIQUE);
   GS_HIP(hipMemsetAsync(d_loops, 0, 8, c->stream));
   GS_HIP(hipMemsetAsync(sm + SM_HIST, 0, 8 * 256 * 4, c->stream));
-  if (g.n) {
+  static const int split_env = getenv("GS_TRI_OKEYS_SPLIT") ? atoi(getenv("GS_TRI_OKEYS_SPLIT")) : -1;   // A/B
+  const bool split = split_env >= 0 ? split_env != 0 : g.V > (1ull << 25);
+  if (g.n && split) {   // two passes over halves of the rank table (k_tri_okeys_lo / _hi)
+    const unsigned grid = (unsigned)std::min<uint64_t>((g.n + 255) / 256, 16384);
+    hipLaunchKernelGGL(k_tri_okeys_lo, dim3(grid), dim3(256), 0, c->stream, g.src, g.dst, g.n, g.key_xor,
+                       (uint32_t)(g.V / 2), rank, keys, c->tri_loops.as<uint32_t>(), d_loops);
+    hipLaunchKernelGGL(k_tri_okeys_hi, dim3((unsigned)std::min<uint64_t>((g.n + 255) / 256, 8192)), dim3(256), 0,
+                       c->stream, keys, g.n, g.B, rank, (uint32_t*)(sm + SM_HIST));
+    GS_HIP(hipGetLastError());
+  } else if (g.n) {
     const unsigned grid = (unsigned)std::min<uint64_t>((g.n + 255) / 256, 8192);
     hipLaunchKernelGGL(k_tri_okeys, dim3(grid), dim3(256), 0, c->stream, g.src, g.dst, g.n, g.key_xor, g.B, rank, keys,
                        c->tri_loops.as<uint32_t>(), d_loops, (uint32_t*)(sm + SM_HIST));
