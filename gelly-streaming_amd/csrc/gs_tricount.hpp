@@ -312,18 +312,23 @@ __global__ __launch_bounds__(TH_BLOCK) __attribute__((amdgpu_waves_per_eu(GS_TH_
                                                         uint32_t* __restrict__ n_heavy,
                                                         unsigned long long* __restrict__ total,
                                                         unsigned long long* __restrict__ n_probes, uint32_t nb_cap,
-                                                        uint32_t* __restrict__ err) {
+                                                        uint32_t* __restrict__ err,
+                                                        const uint32_t* __restrict__ order) {
   // 6 KiB per wave (4 KiB table + 2 KiB list prefix), 24 KiB per block
+  // pass 0: vertices in rank order (first in-chunk here, further chunks queued for pass 1); pass 2: every
+  // light chunk queued (nothing counted); pass 3: the queued chunks in `order` (k_tri_hphase_*: by the
+  // stretch of onbr their in-neighbours' out-lists lie in, so the chunks in flight gather from a few
+  // stretches that L2 and the Infinity Cache keep, as k_tri_heavy's items)
   __shared__ uint4 s_hash[TH_WPB][TH_H / 4];
   __shared__ uint32_t s_off[TH_WPB][TH_LCH];   // exclusive prefix of |N+(u)| over the non-empty u
   __shared__ uint32_t s_st[TH_WPB][TH_LCH];    // start of that N+(u) in onbr
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const uint32_t nw = gridDim.x * TH_WPB;
   uint64_t cnt = 0, probes = 0;
-  const uint32_t n_items = pass == 0 ? nv : *n_queue;
+  const uint32_t n_items = (pass == 0 || pass == 2) ? nv : *n_queue;
   for (uint32_t it = blockIdx.x * TH_WPB + w; it < n_items; it += nw) {   // interleaved: no claim counter
     uint32_t v, c0, c1;
-    if (pass == 0) {
+    if (pass == 0 || pass == 2) {
       v = it;
       const uint2 ro = out_range[v], ri = in_range[v];
       if (ro.y == ro.x || ri.y == ri.x || ro.x < q0 || ro.x >= q1) continue;
@@ -342,16 +347,18 @@ __global__ __launch_bounds__(TH_BLOCK) __attribute__((amdgpu_waves_per_eu(GS_TH_
         continue;
       }
       const uint32_t nch = (ri.y - ri.x + TH_LCH - 1) / TH_LCH;
-      if (nch > 1) {
+      const uint32_t first = pass == 2 ? 0u : 1u;   // pass 2 queues chunk 0 too
+      if (nch > first) {
         uint32_t at = 0;
-        if (lane == 0) at = atomicAdd(n_queue, nch - 1);
+        if (lane == 0) at = atomicAdd(n_queue, nch - first);
         at = __shfl(at, 0, WAVE);
-        for (uint32_t j = lane; j < nch - 1; j += WAVE) queue[at + j] = make_uint2(v, j + 1);
+        for (uint32_t j = lane; j < nch - first; j += WAVE) queue[at + j] = make_uint2(v, j + first);
       }
+      if (pass == 2) continue;
       c0 = ri.x;
       c1 = min(ri.y, ri.x + TH_LCH);
     } else {
-      const uint2 q = queue[it];
+      const uint2 q = queue[pass == 3 ? order[it] : it];
       v = q.x;
       const uint2 ri = in_range[v];
       c0 = ri.x + q.y * TH_LCH;
@@ -399,16 +406,19 @@ __global__ __launch_bounds__(256) void k_tri_hwork(const uint2* __restrict__ sfx
 #define GS_TH_PHASES 16384   // s26 heavy count (ms): 256 phases 149, 1024 146.5, 4096 143.3, 16384 142.0, 65536 141.2
 #endif
 constexpr uint32_t TH_PHASES = GS_TH_PHASES;
+// (CH: in-entries per item -- TH_VCH for the heavy items, TH_LCH for the light ones)
+template <uint32_t CH>
 __device__ __forceinline__ uint32_t th_phase(const uint2* __restrict__ sfx, const uint2* __restrict__ in_range, uint2 item,
                                              uint32_t M) {
-  const uint32_t c0 = in_range[item.x].x + item.y * TH_VCH;
+  const uint32_t c0 = in_range[item.x].x + item.y * CH;
   return (uint32_t)((uint64_t)sfx[c0].x * TH_PHASES / (M ? M : 1u));
 }
+template <uint32_t CH>
 __global__ __launch_bounds__(256) void k_tri_hphase_count(const uint2* __restrict__ sfx, const uint2* __restrict__ in_range,
                                                           const uint2* __restrict__ heavy, uint32_t nh, uint32_t M,
                                                           uint32_t* __restrict__ hist) {
   for (uint32_t h = blockIdx.x * 256u + threadIdx.x; h < nh; h += gridDim.x * 256u)
-    atomicAdd(&hist[min(th_phase(sfx, in_range, heavy[h], M), TH_PHASES - 1)], 1u);
+    atomicAdd(&hist[min(th_phase<CH>(sfx, in_range, heavy[h], M), TH_PHASES - 1)], 1u);
 }
 __global__ __launch_bounds__(256) void k_tri_hphase_scan(uint32_t* __restrict__ hist) {   // one block, in place
   static_assert(TH_PHASES % 256 == 0, "phases per thread");
@@ -430,11 +440,12 @@ __global__ __launch_bounds__(256) void k_tri_hphase_scan(uint32_t* __restrict__ 
     off += v[j];
   }
 }
+template <uint32_t CH>
 __global__ __launch_bounds__(256) void k_tri_hphase_place(const uint2* __restrict__ sfx, const uint2* __restrict__ in_range,
                                                           const uint2* __restrict__ heavy, uint32_t nh, uint32_t M,
                                                           uint32_t* __restrict__ off, uint32_t* __restrict__ order) {
   for (uint32_t h = blockIdx.x * 256u + threadIdx.x; h < nh; h += gridDim.x * 256u)
-    order[atomicAdd(&off[min(th_phase(sfx, in_range, heavy[h], M), TH_PHASES - 1)], 1u)] = h;
+    order[atomicAdd(&off[min(th_phase<CH>(sfx, in_range, heavy[h], M), TH_PHASES - 1)], 1u)] = h;
 }
 
 // one block per heavy item (v, chunk of TH_VCH in-neighbours): N+(v) as an LDS hash set (up to TH_NU
