@@ -71,6 +71,8 @@ def parse():
                    help="after timing: sum(per-vertex sums) == sum(values) and ascending keys on each window")
     p.add_argument("--chunk-records", type=float, default=2 ** 28,
                    help="cand_stream: records per gs_candidates_next chunk")
+    p.add_argument("--max-chunks", type=int, default=0,
+                   help="cand_stream: stop after this many chunks (profiling passes; 0 = the whole window)")
     p.add_argument("--windows-edges", type=float, default=1e8,
                    help="apply (C5): edges per 1000 ms window of the continuous stream")
     p.add_argument("--workload", default="reduce",
@@ -464,9 +466,13 @@ def cand_stream_main(a):
         if time.perf_counter() - last_beat > 30:
             print(f"# cand_stream: {got / total:.1%} of {total} records", file=sys.stderr, flush=True)
             last_beat = time.perf_counter()
-        if done:
+        if done or (a.max_chunks and len(lat) >= a.max_chunks):
             break
     t_stream = time.perf_counter() - t1
+    if a.max_chunks and got < total:   # a profiling pass over the first chunks only: no bench line
+        print(f"# cand_stream: {len(lat)} chunks, {got} of {total} records", file=sys.stderr)
+        eng.close()
+        return
     assert got == total, (got, total)
     cands = total - 2 * E   # every record past the 2E edge records (one per slice(ALL) record) is a candidate
     elapsed = t_begin + t_stream

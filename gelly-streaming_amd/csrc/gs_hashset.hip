@@ -262,7 +262,7 @@ __global__ __launch_bounds__(256) void k_cand_emit(const uint64_t* __restrict__ 
                                                    const int64_t* __restrict__ nbr, const int64_t* __restrict__ gids,
                                                    uint64_t P0, uint64_t P1, uint64_t per_wave,
                                                    int64_t* __restrict__ a, int64_t* __restrict__ b,
-                                                   uint8_t* __restrict__ f) {
+                                                   uint8_t* __restrict__ f, int f4) {
   const uint32_t lane = threadIdx.x & 63;
   const uint64_t wave = ((uint64_t)blockIdx.x * 256u + threadIdx.x) >> 6;
   const uint64_t w0 = P0 + wave * per_wave;
@@ -308,7 +308,17 @@ __global__ __launch_bounds__(256) void k_cand_emit(const uint64_t* __restrict__ 
           const uint64_t col = min(q - tri_rows_before(r, k), k - 1 - r);
           a[oi - P0] = G[r];
           b[oi - P0] = G[r + col];
-          f[oi - P0] = 1;
+          if (!f4) f[oi - P0] = 1;
+        }
+        if (f4) {   // every flag of a pair row is 1: one 4-byte store per lane (256 B per wave) instead of four 64-B byte-store runs
+          uint8_t* fr = f + (base - P0);   // base - P0 is a multiple of 256
+          const uint64_t fo = 4ull * lane;
+          if (base + fo + 4 <= e1) {
+            *reinterpret_cast<uint32_t*>(fr + fo) = 0x01010101u;
+          } else {
+            for (uint32_t j = 0; j < 4; ++j)
+              if (base + fo + j < e1) fr[fo + j] = 1;
+          }
         }
         continue;   // sc still holds the next step's first position, or an earlier slot
       }
@@ -1026,7 +1036,7 @@ static gs_status cand_emit(gs_ctx* c, uint32_t S, uint64_t P0, uint64_t P1, int6
   const uint64_t per_wave = ((n + waves - 1) / waves + 255) / 256 * 256;
   hipLaunchKernelGGL(k_cand_emit, dim3((unsigned)blocks), dim3(256), 0, c->stream, c->hs[HS_VS].as<uint64_t>(), S,
                      c->hs[HS_META].as<CandMeta>(), c->hs[HS_VKEYS].as<int64_t>(), c->hs[HS_NBR].as<int64_t>(),
-                     c->hs[HS_GIDS].as<int64_t>(), P0, P1, per_wave, a, b, f);
+                     c->hs[HS_GIDS].as<int64_t>(), P0, P1, per_wave, a, b, f, ((uintptr_t)f & 3) == 0 ? 1 : 0);
   return hip_check(c, hipGetLastError(), "k_cand_emit");
 }
 
