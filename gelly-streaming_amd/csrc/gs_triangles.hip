@@ -819,7 +819,9 @@ gs_status tri_count(gs_ctx* c, uint32_t B, size_t V, uint64_t M, const uint32_t*
   GS_HIP(hipGetLastError());
   hipEventRecord(c->ev[4], c->stream);
   // 2. intersections: vertex-centric LDS hash sets (k_tri_light), long out-lists in k_tri_heavy
-  static const int lphased_env = getenv("GS_TH_LPHASED") ? atoi(getenv("GS_TH_LPHASED")) : 1;   // A/B
+  // A/B (GS_TH_LPHASED=1): the light chunks in phase order, as the heavy items.  Slower (R-MAT s24 light
+  // count 7.1 -> 36 ms, s26 42 -> 147 ms, profiles/r04/evidence/tri_*_lph.json): off
+  static const int lphased_env = getenv("GS_TH_LPHASED") ? atoi(getenv("GS_TH_LPHASED")) : 0;
   const bool lphased = lphased_env != 0 && GS_TH_PHASED;
   GS_TRY(ensure(c, c->tri_heavy, (V + Ms / TH_VCH + 64) * 8));   // (v, in-chunk) items
   // queued light chunks: the further chunks (<= Ms / TH_LCH), or, phased, every light chunk
