@@ -176,3 +176,49 @@ def test_dispatch_falls_back_for_unsupported_types():
     src = (GPU_JAVA / "GpuBuiltins.java").read_text()
     body = re.search(r"public static boolean supports\([^)]*\) \{([\s\S]*?)\n\t\}", src).group(1)
     assert "keyClass != Long.class" in body and "dtypeOf(valueClass)" in body
+
+
+def _header_arity():
+    """entry point -> number of parameters, from include/gelly_hip.h"""
+    text = re.sub(r"/\*.*?\*/", "", HEADER.read_text(), flags=re.S)
+    out = {}
+    for m in re.finditer(r"GS_API\s+[\w\s\*]+?\b(gs_\w+)\s*\(([^)]*)\)\s*;", text):
+        params = m.group(2).strip()
+        out[m.group(1)] = 0 if params in ("", "void") else params.count(",") + 1
+    return out
+
+
+def test_panama_binding_matches_header():
+    """java/.../GellyHipPanama.java (JDK 22 FFM, north_star's "Panama FFI"): every entry point it looks up
+    is declared in gelly_hip.h with as many parameters as its FunctionDescriptor has arguments, and its
+    struct layouts have the header's field offsets (as the C compiler lays them out)."""
+    src = (GPU_JAVA / "GellyHipPanama.java").read_text()
+    arity = _header_arity()
+    found = re.findall(r'fn\("(gs_\w+)",\s*FunctionDescriptor\.(of|ofVoid)\(([^;]*?)\)\);', src)
+    assert len(found) >= 8
+    for name, kind, args in found:
+        n = len([a for a in args.split(",") if a.strip()]) - (1 if kind == "of" else 0)
+        assert name in arity and arity[name] == n, (name, n, arity.get(name))
+    # struct layouts: field order / widths against offsetof() from the C compiler
+    layouts = {"CONFIG": "gs_config", "EDGE_BATCH": "gs_edge_batch", "VERTEX_OUT": "gs_vertex_out",
+               "DEGREE_OUT": "gs_degree_out", "PAIR_OUT": "gs_pair_out"}
+    size = {"JAVA_INT": 4, "JAVA_LONG": 8, "ADDRESS": 8}
+    prog = ["#include <stdio.h>", "#include <stddef.h>", '#include "gelly_hip.h"', "int main(){"]
+    want = []
+    for jl, cs in layouts.items():
+        body = re.search(jl + r" = MemoryLayout\.structLayout\(([^;]*)\);", src).group(1)
+        off = 0
+        for ty, field in re.findall(r"(JAVA_INT|JAVA_LONG|ADDRESS)\.withName\(\"(\w+)\"\)", body):
+            off = (off + size[ty] - 1) // size[ty] * size[ty]
+            prog.append(f'printf("%zu\\n", offsetof({cs}, {field}));')
+            want.append(off)
+            off += size[ty]
+    prog.append("}")
+    tmp = ROOT / "gpurun_out"
+    tmp.mkdir(exist_ok=True)
+    (tmp / "panama_off.c").write_text("\n".join(prog))
+    subprocess.run(["gcc", "-I", str(ROOT / "include"), str(tmp / "panama_off.c"), "-o", str(tmp / "panama_off")],
+                   check=True)
+    got = [int(x) for x in subprocess.run([str(tmp / "panama_off")], capture_output=True, text=True,
+                                          check=True).stdout.split()]
+    assert got == want
