@@ -146,6 +146,11 @@ def load() -> ctypes.CDLL:
         return _lib
     if not LIB_PATH.exists():
         raise ImportError(f"{LIB_PATH} is missing: the HIP engine is not built (run __graft_entry__.build())")
+    # torch before the library: torch ships its own libamdhip64.so.7 (the soname of /opt/rocm's), and
+    # whichever loads first serves the process.  Loaded after ours, torch ran on a runtime it was not
+    # built with and found no GPU ("No HIP GPUs are available" in a process that made the library's
+    # calls before touching torch); loaded first, both share torch's (tests/test_gpu_fresh_process.py).
+    import torch  # noqa: F401
     L = ctypes.CDLL(str(LIB_PATH))
     st = ctypes.c_int32
     sigs = {

@@ -349,7 +349,6 @@ gs_status bucket_direct_t(gs_ctx* c, const int64_t* src, const int64_t* dst, con
         GS_PASS_EVENT(c->pass_ev[1], c->stream);
         using Load = typename P::Load;
         const BaseSrc<Load, DIR, P::PAY> ls{src, dst, (const Load*)val, base};
-        const uint32_t* bst = meta + BkMeta::BSTART;
         uint32_t* cur = c->sp_cur.as<uint32_t>();
         if constexpr (CAN_PACK && ITEMS == PK_ITEMS) {
           // the bucket tables sized for the window's buckets (1024: 8 KiB less LDS, one bucket per thread)

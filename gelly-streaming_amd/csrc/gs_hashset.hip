@@ -885,7 +885,6 @@ static gs_status hashset_exact(gs_ctx* c, uint64_t R, uint64_t U, uint64_t M, ui
 
 gs_status hashset_order(gs_ctx* c, const int64_t* src, const int64_t* dst, uint64_t n, uint32_t* U_out,
                         uint32_t* M_out, uint64_t* key_xor_out, uint32_t* jdk_flags) {
-  char* sm = c->small.as<char>();
   const uint64_t R = 2 * n;
   Sorted s;
   GS_TRY(sort_window(c, src, dst, nullptr, 0, n, DIR_ALL, PAY_IDX, &s));

@@ -169,7 +169,10 @@ __global__ __launch_bounds__(RK_BLOCK) void k_rank_scatter(const uint32_t* __res
 }
 
 // oriented composite keys (min rank << B | max rank); self-loops -> sentinel (sorts last) + bitmap
-// and count; the sort's digit histograms of the 2B-bit keys on the way (sort_buffer hist_ready)
+// and count; the sort's digit histograms of the 2B-bit keys on the way (sort_buffer hist_ready).
+// U edges per lane per step: every column load, then every rank gather, is issued before the first is
+// used, so a wave keeps 2U random gathers in flight (U = 1 ran at the latency of one gather chain).
+template <int U>
 __global__ __launch_bounds__(256) void k_tri_okeys(const int64_t* __restrict__ src, const int64_t* __restrict__ dst,
                                                    uint64_t n, uint64_t key_xor, uint32_t B,
                                                    const uint32_t* __restrict__ rank, uint64_t* __restrict__ out,
@@ -181,52 +184,86 @@ __global__ __launch_bounds__(256) void k_tri_okeys(const int64_t* __restrict__ s
   __syncthreads();
   const int nd = (int)(2 * B + 7) / 8;
   const uint64_t sent = (B * 2 >= 64) ? ~0ull : ((1ull << (2 * B)) - 1);
-  const uint64_t stride = (uint64_t)gridDim.x * 256;
-  for (uint64_t i0 = (uint64_t)blockIdx.x * 256; i0 < n; i0 += stride) {   // wave-uniform trip count
-    const uint64_t i = i0 + tid;
-    const bool ok = i < n;
-    uint64_t k = sent;
-    if (ok) {
-      const uint64_t a = (uint64_t)src[i] ^ key_xor, b = (uint64_t)dst[i] ^ key_xor;
-      if (a != b) {
-        const uint64_t ra = rank[a], rb = rank[b];
-        k = ra < rb ? (ra << B) | rb : (rb << B) | ra;
-      } else {
-        atomicOr(&loop_bits[a >> 5], 1u << (a & 31));
-        atomicAdd(loops, 1ull);
-      }
-      out[i] = k;
+  const uint64_t stride = (uint64_t)gridDim.x * 256 * U;
+  for (uint64_t i0 = (uint64_t)blockIdx.x * 256 * U; i0 < n; i0 += stride) {   // wave-uniform trip count
+    uint64_t a[U], b[U];
+    uint32_t ra[U], rb[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint64_t i = i0 + 256 * u + tid;
+      a[u] = b[u] = 0;
+      if (i < n) { a[u] = (uint64_t)src[i] ^ key_xor; b[u] = (uint64_t)dst[i] ^ key_xor; }
     }
-    wave_hist_add(h[w], k, ok, nd);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      ra[u] = rb[u] = 0;
+      if (i0 + 256 * u + tid < n && a[u] != b[u]) { ra[u] = rank[a[u]]; rb[u] = rank[b[u]]; }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint64_t i = i0 + 256 * u + tid;
+      const bool ok = i < n;
+      uint64_t k = sent;
+      if (ok) {
+        if (a[u] != b[u]) {
+          const uint64_t x = ra[u], y = rb[u];
+          k = x < y ? (x << B) | y : (y << B) | x;
+        } else {
+          atomicOr(&loop_bits[a[u] >> 5], 1u << (a[u] & 31));
+          atomicAdd(loops, 1ull);
+        }
+        out[i] = k;
+      }
+      wave_hist_add(h[w], k, ok, nd);
+    }
   }
   __syncthreads();
   flush_hist<4>(h, nd, hist);
 }
 
 // The same keys in two passes when the rank table outgrows the Infinity Cache (V > 2^25: 128 MB; C4's
-// scale 26 has a 256 MB table and one pass ran at the rate of its random gathers, 2 x 2^30 of them from
-// HBM): pass 1 resolves the endpoints below H through the lower half of the table and parks the rest
-// as id | ESC in a 2 x 32-bit pair; pass 2 resolves those through the upper half, orients, and counts
-// the sort's histograms.  Each pass gathers from a half table that the cache keeps.
+// scale 26 has a 256 MB table): pass 1 resolves the endpoints below H through the lower half of the
+// table and parks the rest as id | ESC in a 2 x 32-bit pair; pass 2 resolves those through the upper
+// half, orients, and counts the sort's histograms.  Each pass gathers from a half table that the cache
+// keeps.  U as in k_tri_okeys.
 constexpr uint32_t OK_ESC = 1u << 31;
+template <int U>
 __global__ __launch_bounds__(256) void k_tri_okeys_lo(const int64_t* __restrict__ src, const int64_t* __restrict__ dst,
                                                       uint64_t n, uint64_t key_xor, uint32_t H,
                                                       const uint32_t* __restrict__ rank, uint64_t* __restrict__ out,
                                                       uint32_t* __restrict__ loop_bits,
                                                       unsigned long long* __restrict__ loops) {
-  for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) {
-    const uint64_t a = (uint64_t)src[i] ^ key_xor, b = (uint64_t)dst[i] ^ key_xor;
-    uint64_t k = ~0ull;   // a self-loop: the sentinel (pass 2 keeps it)
-    if (a != b) {
-      const uint32_t xa = a < H ? rank[a] : ((uint32_t)a | OK_ESC), xb = b < H ? rank[b] : ((uint32_t)b | OK_ESC);
-      k = ((uint64_t)xa << 32) | xb;
-    } else {
-      atomicOr(&loop_bits[a >> 5], 1u << (a & 31));
-      atomicAdd(loops, 1ull);
+  const uint64_t stride = (uint64_t)gridDim.x * 256 * U;
+  for (uint64_t i0 = (uint64_t)blockIdx.x * 256 * U + threadIdx.x; i0 < n; i0 += stride) {
+    uint64_t a[U], b[U];
+    uint32_t xa[U], xb[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint64_t i = i0 + 256 * u;
+      a[u] = b[u] = 0;
+      if (i < n) { a[u] = (uint64_t)src[i] ^ key_xor; b[u] = (uint64_t)dst[i] ^ key_xor; }
     }
-    out[i] = k;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      xa[u] = a[u] < H ? rank[a[u]] : ((uint32_t)a[u] | OK_ESC);
+      xb[u] = b[u] < H ? rank[b[u]] : ((uint32_t)b[u] | OK_ESC);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint64_t i = i0 + 256 * u;
+      if (i >= n) continue;
+      uint64_t k = ~0ull;   // a self-loop: the sentinel (pass 2 keeps it)
+      if (a[u] != b[u]) {
+        k = ((uint64_t)xa[u] << 32) | xb[u];
+      } else {
+        atomicOr(&loop_bits[a[u] >> 5], 1u << (a[u] & 31));
+        atomicAdd(loops, 1ull);
+      }
+      out[i] = k;
+    }
   }
 }
+template <int U>
 __global__ __launch_bounds__(256) void k_tri_okeys_hi(uint64_t* __restrict__ keys, uint64_t n, uint32_t B,
                                                       const uint32_t* __restrict__ rank, uint32_t* __restrict__ hist) {
   __shared__ uint32_t h[4][8][RADIX];
@@ -235,23 +272,38 @@ __global__ __launch_bounds__(256) void k_tri_okeys_hi(uint64_t* __restrict__ key
   __syncthreads();
   const int nd = (int)(2 * B + 7) / 8;
   const uint64_t sent = (B * 2 >= 64) ? ~0ull : ((1ull << (2 * B)) - 1);
-  const uint64_t stride = (uint64_t)gridDim.x * 256;
-  for (uint64_t i0 = (uint64_t)blockIdx.x * 256; i0 < n; i0 += stride) {   // wave-uniform trip count
-    const uint64_t i = i0 + tid;
-    const bool ok = i < n;
-    uint64_t k = sent;
-    if (ok) {
-      const uint64_t x = keys[i];
-      if (x != ~0ull) {
-        uint32_t xa = (uint32_t)(x >> 32), xb = (uint32_t)x;
-        if (xa & OK_ESC) xa = rank[xa & ~OK_ESC];
-        if (xb & OK_ESC) xb = rank[xb & ~OK_ESC];
-        const uint64_t ra = xa, rb = xb;
-        k = ra < rb ? (ra << B) | rb : (rb << B) | ra;
-      }
-      keys[i] = k;
+  const uint64_t stride = (uint64_t)gridDim.x * 256 * U;
+  for (uint64_t i0 = (uint64_t)blockIdx.x * 256 * U; i0 < n; i0 += stride) {   // wave-uniform trip count
+    uint64_t x[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint64_t i = i0 + 256 * u + tid;
+      x[u] = i < n ? keys[i] : ~0ull;
     }
-    wave_hist_add(h[w], k, ok, nd);
+    uint32_t xa[U], xb[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      xa[u] = (uint32_t)(x[u] >> 32);
+      xb[u] = (uint32_t)x[u];
+      if (x[u] != ~0ull) {
+        if (xa[u] & OK_ESC) xa[u] = rank[xa[u] & ~OK_ESC];
+        if (xb[u] & OK_ESC) xb[u] = rank[xb[u] & ~OK_ESC];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint64_t i = i0 + 256 * u + tid;
+      const bool ok = i < n;
+      uint64_t k = sent;
+      if (ok) {
+        if (x[u] != ~0ull) {
+          const uint64_t ra = xa[u], rb = xb[u];
+          k = ra < rb ? (ra << B) | rb : (rb << B) | ra;
+        }
+        keys[i] = k;
+      }
+      wave_hist_add(h[w], k, ok, nd);
+    }
   }
   __syncthreads();
   flush_hist<4>(h, nd, hist);
@@ -720,18 +772,36 @@ gs_status tri_okeys(gs_ctx* c, const TriGeom& g, const uint32_t* rank, uint64_t*
   GS_HIP(hipMemsetAsync(d_loops, 0, 8, c->stream));
   GS_HIP(hipMemsetAsync(sm + SM_HIST, 0, 8 * 256 * 4, c->stream));
   static const int split_env = getenv("GS_TRI_OKEYS_SPLIT") ? atoi(getenv("GS_TRI_OKEYS_SPLIT")) : -1;   // A/B
+  static const int unroll = getenv("GS_TRI_OKEYS_UNROLL") ? atoi(getenv("GS_TRI_OKEYS_UNROLL")) : 4;     // A/B: 1, 2, 4
   const bool split = split_env >= 0 ? split_env != 0 : g.V > (1ull << 25);
+  const int U = unroll >= 4 ? 4 : unroll >= 2 ? 2 : 1;
+  const uint64_t steps = (g.n + 256ull * U - 1) / (256ull * U);
   if (g.n && split) {   // two passes over halves of the rank table (k_tri_okeys_lo / _hi)
-    const unsigned grid = (unsigned)std::min<uint64_t>((g.n + 255) / 256, 16384);
-    hipLaunchKernelGGL(k_tri_okeys_lo, dim3(grid), dim3(256), 0, c->stream, g.src, g.dst, g.n, g.key_xor,
-                       (uint32_t)(g.V / 2), rank, keys, c->tri_loops.as<uint32_t>(), d_loops);
-    hipLaunchKernelGGL(k_tri_okeys_hi, dim3((unsigned)std::min<uint64_t>((g.n + 255) / 256, 8192)), dim3(256), 0,
-                       c->stream, keys, g.n, g.B, rank, (uint32_t*)(sm + SM_HIST));
+    const unsigned glo = (unsigned)std::min<uint64_t>(steps, 16384 / U), ghi = (unsigned)std::min<uint64_t>(steps, 8192 / U);
+    const uint32_t H = (uint32_t)(g.V / 2);
+    uint32_t* lb = c->tri_loops.as<uint32_t>();
+    uint32_t* hs = (uint32_t*)(sm + SM_HIST);
+    if (U == 4) {
+      hipLaunchKernelGGL(k_tri_okeys_lo<4>, dim3(glo), dim3(256), 0, c->stream, g.src, g.dst, g.n, g.key_xor, H, rank, keys, lb, d_loops);
+      hipLaunchKernelGGL(k_tri_okeys_hi<4>, dim3(ghi), dim3(256), 0, c->stream, keys, g.n, g.B, rank, hs);
+    } else if (U == 2) {
+      hipLaunchKernelGGL(k_tri_okeys_lo<2>, dim3(glo), dim3(256), 0, c->stream, g.src, g.dst, g.n, g.key_xor, H, rank, keys, lb, d_loops);
+      hipLaunchKernelGGL(k_tri_okeys_hi<2>, dim3(ghi), dim3(256), 0, c->stream, keys, g.n, g.B, rank, hs);
+    } else {
+      hipLaunchKernelGGL(k_tri_okeys_lo<1>, dim3(glo), dim3(256), 0, c->stream, g.src, g.dst, g.n, g.key_xor, H, rank, keys, lb, d_loops);
+      hipLaunchKernelGGL(k_tri_okeys_hi<1>, dim3(ghi), dim3(256), 0, c->stream, keys, g.n, g.B, rank, hs);
+    }
     GS_HIP(hipGetLastError());
   } else if (g.n) {
-    const unsigned grid = (unsigned)std::min<uint64_t>((g.n + 255) / 256, 8192);
-    hipLaunchKernelGGL(k_tri_okeys, dim3(grid), dim3(256), 0, c->stream, g.src, g.dst, g.n, g.key_xor, g.B, rank, keys,
-                       c->tri_loops.as<uint32_t>(), d_loops, (uint32_t*)(sm + SM_HIST));
+    const unsigned grid = (unsigned)std::min<uint64_t>(steps, 8192 / U);
+    uint32_t* lb = c->tri_loops.as<uint32_t>();
+    uint32_t* hs = (uint32_t*)(sm + SM_HIST);
+    if (U == 4)
+      hipLaunchKernelGGL(k_tri_okeys<4>, dim3(grid), dim3(256), 0, c->stream, g.src, g.dst, g.n, g.key_xor, g.B, rank, keys, lb, d_loops, hs);
+    else if (U == 2)
+      hipLaunchKernelGGL(k_tri_okeys<2>, dim3(grid), dim3(256), 0, c->stream, g.src, g.dst, g.n, g.key_xor, g.B, rank, keys, lb, d_loops, hs);
+    else
+      hipLaunchKernelGGL(k_tri_okeys<1>, dim3(grid), dim3(256), 0, c->stream, g.src, g.dst, g.n, g.key_xor, g.B, rank, keys, lb, d_loops, hs);
     GS_HIP(hipGetLastError());
   }
   GS_HIP(hipMemcpyAsync(c->host_small + 4, d_loops, 8, hipMemcpyDeviceToHost, c->stream));
@@ -879,12 +949,26 @@ gs_status tri_count(gs_ctx* c, uint32_t B, size_t V, uint64_t M, const uint32_t*
   GS_HIP(hipMemcpyAsync(c->host_small + 6, d_nheavy, 4, hipMemcpyDeviceToHost, c->stream));
   GS_TRY(host_wait(c));
   const uint32_t nh = (uint32_t)c->host_small[6];
+  // heavy items whose v lies in the top 2^16 ranks read the 2-byte copy of the list tails (k_tri_narrow;
+  // A/B GS_TH_NARROW=0: the 4-byte lists only).  nbr must be 16-byte aligned (the copy reads uint4).
+  static const bool narrow_on = !getenv("GS_TH_NARROW") || atoi(getenv("GS_TH_NARROW")) != 0;
+  const uint32_t base16 = V > 65536 ? (uint32_t)(V - 65536) : 0u;
+  const uint16_t* nbr16 = nullptr;
+  if (nh && narrow_on && ((uintptr_t)nbr & 15) == 0) {
+    GS_TRY(ensure(c, c->tri_n16, M * 2 + 16));
+    hipLaunchKernelGGL(k_tri_narrow, dim3((unsigned)std::max<uint64_t>(1, std::min<uint64_t>((M / 4 + 255) / 256, 16384))),
+                       dim3(256), 0, c->stream, nbr, (uint32_t)M, base16, c->tri_n16.as<uint16_t>());
+    GS_HIP(hipGetLastError());
+    nbr16 = c->tri_n16.as<uint16_t>();
+  }
+  // A/B (GS_TH_XCD): claim ranges of the phase order per XCD (8) or one shared counter (1)
+  static const uint32_t hx = getenv("GS_TH_XCD") ? (uint32_t)std::max(1, std::min(8, atoi(getenv("GS_TH_XCD")))) : 8u;
   if (nh && GS_TH_PHASED) {   // items in phase order, claimed one at a time
     GS_TRY(ensure(c, c->tri_hwork, (size_t)nh * 4 + (TH_PHASES + 64) * 4));
     uint32_t* hist = c->tri_hwork.as<uint32_t>();
     uint32_t* claim = hist + TH_PHASES;
     uint32_t* order = hist + TH_PHASES + 64;
-    GS_HIP(hipMemsetAsync(hist, 0, (TH_PHASES + 1) * 4, c->stream));
+    GS_HIP(hipMemsetAsync(hist, 0, (TH_PHASES + 8) * 4, c->stream));   // phases, claim counters
     const unsigned g = (unsigned)std::min<uint64_t>((nh + 255) / 256, 4096);
     hipLaunchKernelGGL(k_tri_hphase_count<TH_VCH>, dim3(g), dim3(256), 0, c->stream, sfx, in_range, c->tri_heavy.as<uint2>(),
                        nh, (uint32_t)M, hist);
@@ -893,7 +977,7 @@ gs_status tri_count(gs_ctx* c, uint32_t B, size_t V, uint64_t M, const uint32_t*
                        nh, (uint32_t)M, hist, order);
     hipLaunchKernelGGL(k_tri_heavy, dim3(GS_TH_HGRID), dim3(TH_HBLOCK), 0, c->stream, nbr, sfx, out_range, in_range,
                        c->tri_heavy.as<uint2>(), d_nheavy, nullptr, (const uint32_t*)order, claim, d_total, d_probes,
-                       nb_cap, d_err);
+                       nb_cap, d_err, hx, nbr16, base16);
     GS_HIP(hipGetLastError());
   } else if (nh) {
     GS_TRY(ensure(c, c->tri_hwork, (size_t)nh * 16 + 8));
@@ -904,7 +988,7 @@ gs_status tri_count(gs_ctx* c, uint32_t B, size_t V, uint64_t M, const uint32_t*
     GS_TRY(xscan(c, (const uint64_t*)hw, nh, (uint64_t*)hw + nh));
     hipLaunchKernelGGL(k_tri_heavy, dim3(GS_TH_HGRID), dim3(TH_HBLOCK), 0, c->stream, nbr, sfx, out_range, in_range,
                        c->tri_heavy.as<uint2>(), d_nheavy, (const unsigned long long*)hw + nh, nullptr, nullptr,
-                       d_total, d_probes, nb_cap, d_err);
+                       d_total, d_probes, nb_cap, d_err, 1u, nbr16, base16);
     GS_HIP(hipGetLastError());
   }
   hipEventRecord(c->ev[3], c->stream);

@@ -448,6 +448,23 @@ __global__ __launch_bounds__(256) void k_tri_hphase_place(const uint2* __restric
     order[atomicAdd(&off[min(th_phase<CH>(sfx, in_range, heavy[h], M), TH_PHASES - 1)], 1u)] = h;
 }
 
+// the 2-byte copy of the out-lists' top-range items for k_tri_heavy: onbr16[p] = onbr[p] - base16 (mod 2^16;
+// only the entries >= base16, the sorted lists' tails, are ever read)
+__global__ __launch_bounds__(256) void k_tri_narrow(const uint32_t* __restrict__ onbr, uint32_t M, uint32_t base16,
+                                                    uint16_t* __restrict__ onbr16) {
+  const uint32_t n4 = M / 4;
+  const uint4* s4 = reinterpret_cast<const uint4*>(onbr);
+  uint2* d4 = reinterpret_cast<uint2*>(onbr16);
+  for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < n4; i += gridDim.x * 256u) {
+    const uint4 x = s4[i];
+    d4[i] = make_uint2(((x.x - base16) & 0xFFFFu) | ((x.y - base16) << 16), ((x.z - base16) & 0xFFFFu) | ((x.w - base16) << 16));
+  }
+  if (blockIdx.x == 0 && threadIdx.x < (M & 3u)) {
+    const uint32_t p = n4 * 4 + threadIdx.x;
+    onbr16[p] = (uint16_t)(onbr[p] - base16);
+  }
+}
+
 // one block per heavy item (v, chunk of TH_VCH in-neighbours): N+(v) as an LDS hash set (up to TH_NU
 // entries; longer lists are binary-searched in HBM; rebuilt only when the block's item changes v),
 // the chunk's lists TH_ILP items per thread with one search.  One item per in-chunk spreads a hub over
@@ -464,7 +481,8 @@ __global__ __launch_bounds__(TH_HBLOCK) __attribute__((amdgpu_waves_per_eu(GS_TH
                                                          uint32_t* __restrict__ claim,
                                                          unsigned long long* __restrict__ total,
                                                          unsigned long long* __restrict__ n_probes, uint32_t nb_cap,
-                                                         uint32_t* __restrict__ err) {
+                                                         uint32_t* __restrict__ err, uint32_t nx,
+                                                         const uint16_t* __restrict__ onbr16, uint32_t base16) {
   __shared__ uint4 s_hash[TH_HB];               // TH_NU / 2 buckets (64 KiB): N+(v) as a hash set of 4-slot buckets
   __shared__ uint32_t s_off[TH_VCH + 1];        // short lists of the chunk (compacted): prefix of |N+(u)|, [ns] = total
   __shared__ uint32_t s_st[TH_VCH];             // start of that N+(u) in onbr
@@ -498,10 +516,28 @@ __global__ __launch_bounds__(TH_HBLOCK) __attribute__((amdgpu_waves_per_eu(GS_TH
     h0 = uni(lower(lo));
     h1 = blockIdx.x + 1 == gridDim.x ? nh : uni(lower(hi));
   }
+  // phased: the ordered items cut into nx equal ranges, each with its own claim counter; a block claims
+  // from range blockIdx.x % nx first -- workgroups go to the XCDs round-robin, so with nx = 8 each XCD
+  // walks its own stretch of phases and its L2 keeps the out-lists that stretch's items share, instead
+  // of all eight L2s caching the one phase in flight -- then helps the next ranges when its own is done
+  uint32_t xs = 0;   // (tid 0's) ranges this block found exhausted
   for (uint32_t k = 0;; ++k) {
     uint32_t hi;
     if (order) {
-      if (tid == 0) s_claim = atomicAdd(claim, 1u);
+      if (tid == 0) {
+        uint32_t got = 0xFFFFFFFFu;
+        while (xs < nx) {
+          const uint32_t r = (blockIdx.x + xs) % nx;
+          const uint32_t b = (uint32_t)((uint64_t)nh * r / nx), e = (uint32_t)((uint64_t)nh * (r + 1) / nx);
+          const uint32_t c = atomicAdd(&claim[r], 1u);
+          if (c < e - b) {
+            got = b + c;
+            break;
+          }
+          ++xs;
+        }
+        s_claim = got;
+      }
       __syncthreads();
       hi = uni(s_claim);
       if (hi >= nh) break;
@@ -617,66 +653,79 @@ __global__ __launch_bounds__(TH_HBLOCK) __attribute__((amdgpu_waves_per_eu(GS_TH
     }
     probes += srun + lrun;   // block-uniform
     __syncthreads();
-    // short lists: TH_ILP consecutive items per thread, at most one list boundary per step
-    uint32_t top = 1;
-    while (2 * top < ns) top <<= 1;
-    for (uint32_t k0 = 0; k0 < srun; k0 += TH_HBLOCK * TH_ILP) {
-      const uint32_t kb = k0 + tid * TH_ILP;
-      const uint32_t kk = min(kb, srun - 1);
-      uint32_t q = 0;
-      for (uint32_t st = top; st; st >>= 1) {
-        const uint32_t t = q + st;
-        q = (t < ns && s_off[min(t, ns - 1)] <= kk) ? t : q;
-      }
-      uint32_t o = s_off[q], sst = s_st[q], nx = s_off[q + 1];
-      uint32_t x[TH_ILP];
-#pragma unroll
-      for (int j = 0; j < TH_ILP; ++j) {
-        const uint32_t kj = min(kb + j, srun - 1);
-        if (kj >= nx) {
-          ++q;
-          o = nx;
-          sst = s_st[q];
-          nx = s_off[q + 1];
-        }
-        x[j] = onbr[sst + (kj - o)];
-      }
-      cnt += probe(x, kb < srun ? min((uint32_t)TH_ILP, srun - kb) : 0u);
-    }
-    // long lists: wave w walks items [w, w + 1) * lrun / NW in 64-item segments (one load of 64
-    // consecutive items); a segment spans at most two lists (every long list >= 64 items)
-    if (lrun) {
-      const uint32_t wu = uni((uint32_t)w);
-      const uint32_t a0 = uni((uint32_t)((uint64_t)lrun * wu / NW)), a1 = uni((uint32_t)((uint64_t)lrun * (wu + 1) / NW));
-      uint32_t q = 0;
-      {
-        uint32_t t2 = 1;
-        while (2 * t2 < nl) t2 <<= 1;
-        for (uint32_t st = t2; st; st >>= 1) {
+    // The suffixes' items: 4-byte ranks from onbr, or -- when v lies in the top 2^16 ranks [base16 - 1,
+    // top), so that every suffix item w > v does too -- the 2-byte copy of the list tails (onbr16[p] =
+    // onbr[p] - base16 where onbr[p] >= base16): half the bytes for the probes that dominate the count
+    // (R-MAT s24: 83 % of them have v there, tests/analysis_tri_core.py).  Block-uniform choice.
+    auto lists = [&](auto narrow_tag) {
+      constexpr bool NARROW = decltype(narrow_tag)::value;
+      auto item = [&](uint32_t p) -> uint32_t {
+        if constexpr (NARROW) return (uint32_t)onbr16[p] + base16;
+        else return onbr[p];
+      };
+      // short lists: TH_ILP consecutive items per thread, at most one list boundary per step
+      uint32_t top = 1;
+      while (2 * top < ns) top <<= 1;
+      for (uint32_t k0 = 0; k0 < srun; k0 += TH_HBLOCK * TH_ILP) {
+        const uint32_t kb = k0 + tid * TH_ILP;
+        const uint32_t kk = min(kb, srun - 1);
+        uint32_t q = 0;
+        for (uint32_t st = top; st; st >>= 1) {
           const uint32_t t = q + st;
-          q = (t < nl && uni(s_loff[min(t, nl - 1)]) <= a0) ? t : q;
+          q = (t < ns && s_off[min(t, ns - 1)] <= kk) ? t : q;
         }
-      }
-      uint32_t qo = uni(s_loff[q]), qs = uni(s_lst[q]), qe = uni(s_loff[q + 1]), q1s = q + 1 < nl ? uni(s_lst[q + 1]) : 0u;
-      for (uint32_t k0 = a0; k0 < a1; k0 += WAVE * TH_ILP) {
+        uint32_t o = s_off[q], sst = s_st[q], nx = s_off[q + 1];
         uint32_t x[TH_ILP];
 #pragma unroll
         for (int j = 0; j < TH_ILP; ++j) {
-          const uint32_t seg = k0 + (uint32_t)j * WAVE;   // wave-uniform
-          while (qe <= seg && q + 1 < nl) {
+          const uint32_t kj = min(kb + j, srun - 1);
+          if (kj >= nx) {
             ++q;
-            qo = qe;
-            qs = q1s;
-            qe = uni(s_loff[q + 1]);
-            q1s = q + 1 < nl ? uni(s_lst[q + 1]) : 0u;
+            o = nx;
+            sst = s_st[q];
+            nx = s_off[q + 1];
           }
-          const uint32_t k = min(seg + (uint32_t)lane, a1 - 1);
-          x[j] = onbr[k < qe ? qs + (k - qo) : q1s + (k - qe)];
+          x[j] = item(sst + (kj - o));
         }
-        const uint32_t rem = a1 - k0;
-        cnt += probe(x, rem > (uint32_t)lane ? min((uint32_t)TH_ILP, (rem - lane + WAVE - 1) / WAVE) : 0u);
+        cnt += probe(x, kb < srun ? min((uint32_t)TH_ILP, srun - kb) : 0u);
       }
-    }
+      // long lists: wave w walks items [w, w + 1) * lrun / NW in 64-item segments (one load of 64
+      // consecutive items); a segment spans at most two lists (every long list >= 64 items)
+      if (lrun) {
+        const uint32_t wu = uni((uint32_t)w);
+        const uint32_t a0 = uni((uint32_t)((uint64_t)lrun * wu / NW)), a1 = uni((uint32_t)((uint64_t)lrun * (wu + 1) / NW));
+        uint32_t q = 0;
+        {
+          uint32_t t2 = 1;
+          while (2 * t2 < nl) t2 <<= 1;
+          for (uint32_t st = t2; st; st >>= 1) {
+            const uint32_t t = q + st;
+            q = (t < nl && uni(s_loff[min(t, nl - 1)]) <= a0) ? t : q;
+          }
+        }
+        uint32_t qo = uni(s_loff[q]), qs = uni(s_lst[q]), qe = uni(s_loff[q + 1]), q1s = q + 1 < nl ? uni(s_lst[q + 1]) : 0u;
+        for (uint32_t k0 = a0; k0 < a1; k0 += WAVE * TH_ILP) {
+          uint32_t x[TH_ILP];
+#pragma unroll
+          for (int j = 0; j < TH_ILP; ++j) {
+            const uint32_t seg = k0 + (uint32_t)j * WAVE;   // wave-uniform
+            while (qe <= seg && q + 1 < nl) {
+              ++q;
+              qo = qe;
+              qs = q1s;
+              qe = uni(s_loff[q + 1]);
+              q1s = q + 1 < nl ? uni(s_lst[q + 1]) : 0u;
+            }
+            const uint32_t k = min(seg + (uint32_t)lane, a1 - 1);
+            x[j] = item(k < qe ? qs + (k - qo) : q1s + (k - qe));
+          }
+          const uint32_t rem = a1 - k0;
+          cnt += probe(x, rem > (uint32_t)lane ? min((uint32_t)TH_ILP, (rem - lane + WAVE - 1) / WAVE) : 0u);
+        }
+      }
+    };
+    if (onbr16 && v + 1 >= base16) lists(std::true_type{});
+    else lists(std::false_type{});
   }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o, WAVE);

@@ -49,6 +49,38 @@ SCRIPT = textwrap.dedent("""
 """)
 
 
+LIBRARY_FIRST = textwrap.dedent("""
+    import sys
+    import numpy as np
+    sys.path.insert(0, {root!r})
+    import __graft_entry__ as ge
+    pkg, orc = ge.load_package(), ge.load_oracle()
+    eng = pkg.Engine(0)                       # the library before any torch call of this script
+    s, d = orc.gen_rmat(10, 4096, 7)
+    v = orc.gen_values(4096, 7, orc.DT_I64)
+    gk, gv = eng.reduce(s, d, v, 1, 0)
+    rk, rv = orc.window_reduce(s, d, v, 1, 0)
+    assert np.array_equal(np.asarray(gk), rk) and np.array_equal(np.asarray(gv), rv)
+    import torch
+    assert torch.cuda.is_available()
+    x = torch.arange(1000, device="cuda:0").sum().item()
+    assert x == 499500, x
+    eng.close()
+    libs = sorted({{l.split()[-1] for l in open("/proc/self/maps") if "libamdhip64" in l}})
+    assert len(libs) == 1, libs
+    print("HIP runtime:", libs[0])
+""")
+
+
+def test_library_before_torch_in_fresh_process():
+    """Loading the library first must not leave torch without a GPU (_lib.load imports torch first: the
+    two HIP runtimes share a soname, and torch on the runtime of /opt/rocm found no device)."""
+    r = subprocess.run([sys.executable, "-c", LIBRARY_FIRST.format(root=str(ROOT))], capture_output=True, text=True,
+                       timeout=170)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "HIP runtime:" in r.stdout
+
+
 @pytest.mark.parametrize("n", [1024, 65536])
 def test_first_call_in_fresh_process(n):
     r = subprocess.run([sys.executable, "-c", SCRIPT.format(root=str(ROOT), n=n)], capture_output=True, text=True,
