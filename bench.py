@@ -42,6 +42,9 @@ def parse():
     p.add_argument("--seed", type=lambda x: int(x, 0), default=0x5EED02)
     p.add_argument("--dtype", default="int64", choices=["int64", "float64"])
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--timing", default="dominant", choices=["dominant", "stages"],
+                   help="reduce / fold: stage events inside the timed region -- the dominant kernels only "
+                        "(default) or every stage (each record costs the stream a few microseconds)")
     p.add_argument("--windows", type=int, default=2, help="distinct windows of the stream the timed steps cycle through")
     p.add_argument("--stream", default="rmat", choices=["rmat", "zipf"],
                    help="fold (C3): skewed R-MAT (default) or the Zipf(1.1) source stream")
@@ -92,12 +95,15 @@ def algorithmic_bytes(workload, E, U, vb=8):
     return (8 + vb) * E + (8 + vb) * U
 
 
-def kernel_table(times_list, E, U_avg):
+def kernel_table(times_list, E, U_avg, stage_list=None):
     """Average per-launch durations (device events inside the library, same stream) and each kernel's
-    own algorithmic bytes."""
+    own algorithmic bytes.  times_list: the timed windows (GS_TIMING_DOMINANT: the direct
+    path's scatter and accumulate only); stage_list: windows after them with every stage event."""
     t0 = times_list[0]
     if t0.path == 2:
-        return direct_kernel_table(times_list, E, U_avg)
+        return direct_kernel_table(times_list, E, U_avg, stage_list or times_list)
+    times_list = stage_list or times_list   # other paths: every stage from the stage-timed windows
+    t0 = times_list[0]
     if t0.path == 1:
         return bucket_kernel_table(times_list, E, U_avg)
     kb, vb = t0.key_bytes, t0.payload_bytes
@@ -144,7 +150,7 @@ def bucket_kernel_table(times_list, E, U_avg):
     return rows, mean(lambda t: t.partials)
 
 
-def direct_kernel_table(times_list, E, U_avg):
+def direct_kernel_table(times_list, E, U_avg, stage_list):
     """Direct bucket path (gs_bucket.hpp k_dp_*): per-tile histogram, offset scans, ONE scatter, LDS
     accumulate, merge, emit.  Each kernel's own bytes (E = records): the packed scatter
     writes 4-byte records (2-byte key + 2-byte value), the plain one a 2-byte key + the payload."""
@@ -153,18 +159,19 @@ def direct_kernel_table(times_list, E, U_avg):
     lb = 8 if t0.packed else vb  # loaded value bytes
     ab = 8 if (vb or t0.packed) else 4   # staged accumulator (i64 sum / u32 count)
     mean = lambda f: statistics.mean(f(t) for t in times_list)
+    smean = lambda f: statistics.mean(f(t) for t in stage_list)   # the stages the timed windows did not time
     rows = {}
     spec = t0.speculative == 1   # regions from the previous window's counts: no histogram, no offset scans
     name = ("sp_scatter_pack" if spec else "dp_scatter_pack") if t0.packed else ("sp_scatter" if spec else "dp_scatter")
     rows[name] = {"ms": mean(lambda t: t.pass_ms[1]), "bytes": E * ((8 + lb) + (2 + vb))}
     rows["bucket_accumulate"] = {"ms": mean(lambda t: t.pass_ms[2]), "bytes": E * (2 + vb) + U_avg * (4 + ab)}
-    rows["bucket_merge"] = {"ms": mean(lambda t: t.pass_ms[3]), "bytes": 0}
-    rows["bucket_emit"] = {"ms": mean(lambda t: t.pass_ms[4]), "bytes": U_avg * (4 + ab + 16)}
+    rows["bucket_merge"] = {"ms": smean(lambda t: t.pass_ms[3]), "bytes": 0}
+    rows["bucket_emit"] = {"ms": smean(lambda t: t.pass_ms[4]), "bytes": U_avg * (4 + ab + 16)}
     if spec:
-        rows["sp_regions"] = {"ms": mean(lambda t: t.keyinfo_ms), "bytes": 0}
+        rows["sp_regions"] = {"ms": smean(lambda t: t.keyinfo_ms), "bytes": 0}
     else:
-        rows["dp_offsets(up+spine+plan+down)"] = {"ms": mean(lambda t: t.pass_ms[0]), "bytes": 0}
-        rows["dp_hist"] = {"ms": mean(lambda t: t.keyinfo_ms), "bytes": E * 8}
+        rows["dp_offsets(up+spine+plan+down)"] = {"ms": smean(lambda t: t.pass_ms[0]), "bytes": 0}
+        rows["dp_hist"] = {"ms": smean(lambda t: t.keyinfo_ms), "bytes": E * 8}
     return rows, mean(lambda t: t.partials)
 
 
@@ -802,6 +809,11 @@ def main():
 
     for i in range(a.warmup):
         step(i)
+    # the timed windows record only the dominant kernels' events (gs_set_timing: each event record costs
+    # the stream a few microseconds); the other stages are timed on windows after the timed region
+    lean = a.workload in ("reduce", "fold") and a.timing == "dominant"
+    if lean:
+        eng.set_timing(pkg._lib.GS_TIMING_DOMINANT)
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
@@ -821,6 +833,12 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+
+    stage_times_after = None
+    if lean:
+        eng.set_timing(pkg._lib.GS_TIMING_STAGES)
+        stage_times_after = [step(a.warmup + a.steps + i)[2] for i in range(3)]
+        torch.cuda.synchronize()
 
     checks = {}
     if a.check and world == 1 and a.workload == "reduce":
@@ -843,7 +861,7 @@ def main():
         partials = 0
         B = 16 * E + 16 * U_cc
     else:
-        kt, partials = kernel_table(times, E_rec, U_avg)
+        kt, partials = kernel_table(times, E_rec, U_avg, stage_times_after)
         B = algorithmic_bytes(a.workload, E, U_avg, 8)
     finish_rows(kt, B)
     dom_name = max((n for n in kt if n not in ("tri_count_light", "tri_count_heavy")), key=lambda n: kt[n]["ms"])
@@ -871,7 +889,10 @@ def main():
                                  "ms": round(ms_step, 4)},
                 "window_traffic_pmc": pmc_window,
                 "window_traffic_over_B": round(pmc_window / B, 3) if pmc_window else None,
-                "timing": "device events on the library's stream around each launch (gs_last_stage_times)"}
+                "timing": ("device events on the library's stream (gs_last_stage_times) around the scatter and the "
+                           "accumulate inside the timed region (gs_set_timing DOMINANT); the other stages on 3 "
+                           "windows after it with every stage event") if lean else
+                          "device events on the library's stream around each launch (gs_last_stage_times)"}
 
     if a.workload == "triangles":
         # the count step is bound by LDS reads, not HBM: one 16-byte bucket read per hash probe ->

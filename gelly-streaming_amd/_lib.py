@@ -21,6 +21,7 @@ GS_STREAM_REDUCE, GS_STREAM_FOLD, GS_STREAM_DEGREE_MAX, GS_STREAM_TRIANGLES = 0,
 GS_WATERMARK_EXPLICIT, GS_WATERMARK_ASCENDING = 0, 1
 GS_STAGE_PINNED, GS_STAGE_DIRECT = 0, 1
 GS_MEM_HOST, GS_MEM_DEVICE = 0, 1
+GS_TIMING_OFF, GS_TIMING_DOMINANT, GS_TIMING_STAGES = 0, 1, 2   # gs_set_timing
 GS_I32, GS_I64, GS_F32, GS_F64, GS_NONE = 0, 1, 2, 3, 4
 GS_OP_SUM, GS_OP_MIN, GS_OP_MAX, GS_OP_COUNT = 0, 1, 2, 3
 STATUS_NAMES = {0: "GS_OK", -1: "GS_EINVAL", -2: "GS_ECAPACITY", -3: "GS_EDEVICE", -4: "GS_ECOMM",
@@ -31,7 +32,7 @@ GS_DTYPE_OF = {np.dtype(np.int32): GS_I32, np.dtype(np.int64): GS_I64, np.dtype(
                np.dtype(np.float64): GS_F64}
 
 # every symbol include/gelly_hip.h declares (checked by tests/test_abi.py)
-EXPORTS = ("gs_abi_version", "gs_create", "gs_destroy", "gs_last_error", "gs_set_stream", "gs_synchronize",
+EXPORTS = ("gs_abi_version", "gs_create", "gs_destroy", "gs_last_error", "gs_set_stream", "gs_set_timing", "gs_synchronize",
            "gs_alloc_pinned", "gs_free_pinned", "gs_window_reduce", "gs_window_fold",
            "gs_window_fold_degree_max", "gs_window_csr", "gs_window_candidates", "gs_window_candidates_part",
            "gs_window_triangles",
@@ -159,6 +160,7 @@ def load() -> ctypes.CDLL:
         "gs_destroy": (None, [P]),
         "gs_last_error": (ctypes.c_char_p, [P]),
         "gs_set_stream": (st, [P, P]),
+        "gs_set_timing": (st, [P, i32]),
         "gs_synchronize": (st, [P]),
         "gs_alloc_pinned": (P, [ctypes.c_size_t]),
         "gs_free_pinned": (None, [P]),

@@ -126,14 +126,6 @@ void choose_passes(uint32_t nb, int* passes, int* w) {
 }
 
 // records per accumulation work item: about GS_BK_ITEMS_PER_CU items per CU, at least 2^14 records
-#ifndef GS_STAGE_EVENTS
-#define GS_STAGE_EVENTS 1   // A/B: 0 skips the per-launch events (stage times then read 0)
-#endif
-#if GS_STAGE_EVENTS
-#define GS_PASS_EVENT(ev, st) hipEventRecord(ev, st)
-#else
-#define GS_PASS_EVENT(ev, st) ((void)0)
-#endif
 #ifndef GS_BK_ITEMS_PER_CU
 #define GS_BK_ITEMS_PER_CU 3   // C2 (ms, one box): 4 items 1.712, 3 items 1.662 (fewer multi-item buckets: merge 0.066 -> 0.029), 2 items 1.685, 6 items 1.785
 #endif
@@ -193,7 +185,7 @@ gs_status bucket_accumulate(gs_ctx* c, Src rs, uint64_t R, uint32_t nb, int64_t 
                      c->bk_items.as<BkItem>(), ns + 0, meta + BkMeta::BSTART, ns + 2, slabs, st, meta + BkMeta::BCOUNT,
                      mm, seg_cur);
   GS_HIP(hipGetLastError());
-  GS_PASS_EVENT(c->pass_ev[ev0 + 1], c->stream);
+  stage_event(c, c->pass_ev[ev0 + 1], ev0 == 2);   // (the direct path's accumulate bracket)
   const unsigned mgrid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(nb, R / BK_ITEM + 1));
   hipLaunchKernelGGL((k_bk_merge_slices<P>), dim3(mgrid, BK_MS_SLICES), dim3(BK_MS_BLOCK), 0, c->stream,
                      meta + BkMeta::MLIST, ns + 1, meta + BkMeta::BITEMS, meta + BkMeta::BSLAB, slabs, mm);
@@ -201,13 +193,13 @@ gs_status bucket_accumulate(gs_ctx* c, Src rs, uint64_t R, uint32_t nb, int64_t 
                      meta + BkMeta::BITEMS, meta + BkMeta::BSLAB, meta + BkMeta::BSTART, slabs, st,
                      meta + BkMeta::BCOUNT, mm);
   GS_HIP(hipGetLastError());
-  GS_PASS_EVENT(c->pass_ev[ev0 + 2], c->stream);
+  stage_event(c, c->pass_ev[ev0 + 2]);
   hipLaunchKernelGGL((k_bk_emit<P>), dim3(nb), dim3(256), 0, c->stream, meta + BkMeta::BSTART, meta + BkMeta::BCOUNT,
                      nb, st, base, o, (unsigned long long*)(sm + SM_BK_MM + 24), mm, (const uint32_t*)(sm + SM_TIMEOUT),
                      (const unsigned long long*)(sm + SM_BK_ESC), (unsigned long long*)(sm + SM_BK_X));
   GS_HIP(hipGetLastError());
-  GS_PASS_EVENT(c->pass_ev[ev0 + 3], c->stream);
-  hipEventRecord(c->ev[3], c->stream);
+  stage_event(c, c->pass_ev[ev0 + 3]);
+  stage_event(c, c->ev[3]);
   static_assert(SM_BK_N == SM_BK_MM + 32 && SM_BK_X == SM_BK_MM + 48, "one read-back block");
   GS_HIP(hipMemcpyAsync(c->host_small, sm + SM_BK_MM, 64, hipMemcpyDeviceToHost, c->stream));
   return GS_OK;
@@ -243,6 +235,14 @@ void bucket_times(gs_ctx* c, int path, int passes, int launches, uint32_t key_bi
   t.partials = n_items;
   t.fused_last = 0;
   t.path = (uint32_t)path;
+  if (c->timing != GS_TIMING_STAGES) {   // only the events stage_event recorded at this level
+    t.keyinfo_ms = t.sort_ms = t.reduce_ms = t.total_ms = 0.f;
+    for (int p = 0; p < 8; ++p) t.pass_ms[p] = 0.f;
+    if (c->timing == GS_TIMING_DOMINANT && path == 2) {   // the scatter and the accumulate
+      t.pass_ms[1] = event_ms(c->pass_ev[1], c->pass_ev[2]);
+      t.pass_ms[2] = event_ms(c->pass_ev[2], c->pass_ev[3]);
+    }
+  }
 }
 
 template <class P>
@@ -344,9 +344,9 @@ gs_status bucket_direct_t(gs_ctx* c, const int64_t* src, const int64_t* dst, con
                            nb, sp.R, R, meta + BkMeta::BSTART, c->sp_cur.as<uint32_t>(), slots, mm,
                            (unsigned long long*)(sm + SM_BK_ESC));
         if constexpr (P::REL) GS_HIP(hipMemsetAsync(rel_bad, 0, 4, c->stream));
-        hipEventRecord(c->ev[1], c->stream);
-        GS_PASS_EVENT(c->pass_ev[0], c->stream);
-        GS_PASS_EVENT(c->pass_ev[1], c->stream);
+        stage_event(c, c->ev[1]);
+        stage_event(c, c->pass_ev[0]);
+        stage_event(c, c->pass_ev[1], true);
         using Load = typename P::Load;
         const BaseSrc<Load, DIR, P::PAY> ls{src, dst, (const Load*)val, base};
         uint32_t* cur = c->sp_cur.as<uint32_t>();
@@ -372,8 +372,8 @@ gs_status bucket_direct_t(gs_ctx* c, const int64_t* src, const int64_t* dst, con
           }
         }
         GS_HIP(hipGetLastError());
-        GS_PASS_EVENT(c->pass_ev[2], c->stream);
-        hipEventRecord(c->ev[2], c->stream);
+        stage_event(c, c->pass_ev[2], true);
+        stage_event(c, c->ev[2]);
         GS_TRY(launch_plan<P>(c, cap, nb, 0, 0, item_recs, cur, sp.tot.as<uint32_t>(), mm));
         part = true;
         if (pack) GS_TRY((bucket_accumulate<P>(c, PackSrc<Raw>{c->keysB.as<uint32_t>(), vpart}, cap, nb, base, o, 2, cur)));
@@ -397,8 +397,8 @@ gs_status bucket_direct_t(gs_ctx* c, const int64_t* src, const int64_t* dst, con
     //    the keys before the scatter) + the measured range and the keys outside the prediction
     GS_TRY((launch_dp_hist<DIR, ITEMS>(c, src, dst, n, nt, base, S, nb)));
     GS_HIP(hipMemsetAsync(sm + SM_BK_ESC, 0, 8, c->stream));
-    hipEventRecord(c->ev[1], c->stream);
-    GS_PASS_EVENT(c->pass_ev[0], c->stream);
+    stage_event(c, c->ev[1]);
+    stage_event(c, c->pass_ev[0]);
 
     // 2. offsets: chunk counts, per-bucket spine (-> meta[HIST] totals), plan, per-tile offsets
     part = nb > 1;
@@ -412,7 +412,7 @@ gs_status bucket_direct_t(gs_ctx* c, const int64_t* src, const int64_t* dst, con
                          c->dp_off.as<uint32_t>());
       GS_HIP(hipGetLastError());
     }
-    GS_PASS_EVENT(c->pass_ev[1], c->stream);
+    stage_event(c, c->pass_ev[1], true);
 
     // 3. the scatter: bucket-local index + payload in bucket order
     if constexpr (P::REL) {
@@ -437,8 +437,8 @@ gs_status bucket_direct_t(gs_ctx* c, const int64_t* src, const int64_t* dst, con
         GS_HIP(hipGetLastError());
       }
     }
-    GS_PASS_EVENT(c->pass_ev[2], c->stream);
-    hipEventRecord(c->ev[2], c->stream);
+    stage_event(c, c->pass_ev[2], true);
+    stage_event(c, c->ev[2]);
 
     // 4-6. accumulate, merge, emit; one read-back
     if (part) {
@@ -540,8 +540,8 @@ gs_status bucket_onesweep(gs_ctx* c, const int64_t* src, const int64_t* dst, con
   // 2. plan
   const uint32_t item_recs = item_records(c, R);
   GS_TRY(launch_plan<P>(c, R, g.nb, g.passes, g.w, item_recs));
-  hipEventRecord(c->ev[1], c->stream);
-  GS_PASS_EVENT(c->pass_ev[0], c->stream);
+  stage_event(c, c->ev[1]);
+  stage_event(c, c->pass_ev[0]);
 
   // 3. partition passes over the bucket index; the last stores the 16-bit bucket-local index
   GS_TRY(ensure_stage<P>(c, R));
@@ -553,17 +553,17 @@ gs_status bucket_onesweep(gs_ctx* c, const int64_t* src, const int64_t* dst, con
   Raw* vpart = HAS_V ? c->valsB.as<Raw>() : nullptr;
   if (g.passes == 1) {
     GS_TRY((launch_part_w<uint32_t, uint16_t, Raw, HAS_V>(c, g.w, es, k16, vpart, (uint32_t)R, 0, S)));
-    GS_PASS_EVENT(c->pass_ev[1], c->stream);
+    stage_event(c, c->pass_ev[1]);
   } else if (g.passes == 2) {
     uint32_t* k32 = c->keysA.as<uint32_t>();
     Raw* vmid = HAS_V ? c->valsA.as<Raw>() : nullptr;
     GS_TRY((launch_part_w<uint32_t, uint32_t, Raw, HAS_V>(c, g.w, es, k32, vmid, (uint32_t)R, 0, S)));
-    GS_PASS_EVENT(c->pass_ev[1], c->stream);
+    stage_event(c, c->pass_ev[1]);
     const BufSrc<uint32_t, Raw> bs{k32, vmid, 0};
     GS_TRY((launch_part_w<uint32_t, uint16_t, Raw, HAS_V>(c, g.w, bs, k16, vpart, (uint32_t)R, 1, S + g.w)));
-    GS_PASS_EVENT(c->pass_ev[2], c->stream);
+    stage_event(c, c->pass_ev[2]);
   }
-  hipEventRecord(c->ev[2], c->stream);
+  stage_event(c, c->ev[2]);
 
   // 4-6. accumulate, merge, emit
   uint32_t n_items = 0;

@@ -408,7 +408,7 @@ void gs_destroy(gs_ctx* c) {
   for (DevBuf* b : {&c->part_k, &c->part_a, &c->comp_k, &c->comp_a,
                     &c->in_src, &c->in_dst, &c->in_val, &c->keysA, &c->keysB, &c->valsA, &c->valsB, &c->sort_status,
                     &c->rbk_word, &c->rbk_agg, &c->rbk_inc, &c->small, &c->out_keys, &c->out_a, &c->out_b, &c->aux,
-                    &c->bk_meta, &c->bk_items, &c->bk_slabs, &c->dp_cnt, &c->dp_csum, &c->dp_off, &c->tri_loops, &c->tri_tiles, &c->tri_sfx, &c->tri_nbr, &c->tri_heavy, &c->tri_range, &c->tri_queue, &c->tri_hwork, &c->tri_lph, &c->tri_n16, &c->tri_d[0], &c->tri_d[1], &c->tri_d[2], &c->tri_d[3], &c->tri_d[4], &c->tri_d[5], &c->tri_d[6], &c->tri_d[7], &c->tri_d[8], &c->tri_d[9], &c->cc[0], &c->cc[1], &c->cc[2],
+                    &c->bk_meta, &c->bk_items, &c->bk_slabs, &c->dp_cnt, &c->dp_csum, &c->dp_off, &c->tri_loops, &c->tri_tiles, &c->tri_sfx, &c->tri_nbr, &c->tri_heavy, &c->tri_range, &c->tri_queue, &c->tri_hwork, &c->tri_lph, &c->tri_d[0], &c->tri_d[1], &c->tri_d[2], &c->tri_d[3], &c->tri_d[4], &c->tri_d[5], &c->tri_d[6], &c->tri_d[7], &c->tri_d[8], &c->tri_d[9], &c->cc[0], &c->cc[1], &c->cc[2],
                     &c->pr_a, &c->pr_b, &c->pr_f, &c->pr_key, &c->pr_val, &c->pr_gk, &c->pr_gv, &c->pr_small,
                     &c->tx_text, &c->tx_cnt, &c->tx_starts, &c->zipf_cdf,
                     &c->dist_k, &c->dist_v, &c->dist_v2, &c->dist_k2, &c->dist_v3, &c->dist_v4, &c->dist_cnt,
@@ -429,6 +429,13 @@ void gs_destroy(gs_ctx* c) {
 }
 
 const char* gs_last_error(const gs_ctx* c) { return c ? c->err.c_str() : "null context"; }
+
+gs_status gs_set_timing(gs_ctx* c, int32_t level) {
+  if (!c) return GS_EINVAL;
+  if (level < GS_TIMING_OFF || level > GS_TIMING_STAGES) return set_error(c, GS_EINVAL, "bad timing level %d", level);
+  c->timing = level;
+  return GS_OK;
+}
 
 gs_status gs_set_stream(gs_ctx* c, void* s) {
   if (!c) return GS_EINVAL;
@@ -621,7 +628,7 @@ static gs_status window_fold_impl(gs_ctx* c, const gs_edge_batch* b, int32_t dir
     *out->n_out = 0;
     return GS_OK;
   }
-  hipEventRecord(c->ev[0], c->stream);
+  stage_event(c, c->ev[0]);
   const int64_t *src, *dst;
   const void* val;
   GS_TRY(stage_batch(c, b, &src, &dst, &val, op != GS_OP_COUNT));
@@ -715,7 +722,7 @@ gs_status gs_window_fold_degree_max(gs_ctx* c, const gs_edge_batch* b, int32_t d
     *out->n_out = 0;
     return GS_OK;
   }
-  hipEventRecord(c->ev[0], c->stream);
+  stage_event(c, c->ev[0]);
   const int64_t *src, *dst;
   const void* val;
   GS_TRY(stage_batch(c, b, &src, &dst, &val, false));

@@ -43,6 +43,7 @@ struct gs_ctx {
   bool own_stream = false;
   std::string err;
   uint32_t epoch = 0;
+  int timing = GS_TIMING_STAGES;   // gs_set_timing: which stage events a window records (stage_event)
   int hist_digits = 4;   // key-byte histograms keyinfo computes (learned from the previous window)
   uint32_t flags = 0;    // gs_config.flags
   int64_t bk_base = 0;   // bucket path: predicted lower bound of the next window's vertex IDs
@@ -76,7 +77,7 @@ struct gs_ctx {
   // fused last pass: partials with gaps, compacted partials
   gs::DevBuf part_k, part_a, comp_k, comp_a;
   // triangles
-  gs::DevBuf tri_loops, tri_tiles, tri_sfx, tri_nbr, tri_heavy, tri_range, tri_queue, tri_hwork, tri_lph, tri_n16;
+  gs::DevBuf tri_loops, tri_tiles, tri_sfx, tri_nbr, tri_heavy, tri_range, tri_queue, tri_hwork, tri_lph;
   gs::DevBuf tri_d[10];          // split-window triangles (gs_window_triangles_dist)
   gs::DevBuf cc[3];              // connected components (gs_components.hip)
   uint32_t tri_B = 0;            // split-window triangles: id geometry of the current window
@@ -228,6 +229,12 @@ inline float event_ms(hipEvent_t a, hipEvent_t b) {
     ms = 0.f;
   }
   return ms;
+}
+
+// a stage-time event (gs_set_timing): recorded at GS_TIMING_STAGES, and at GS_TIMING_DOMINANT only when
+// `dominant` (the bucket path's scatter / accumulate brackets); never at GS_TIMING_OFF
+inline void stage_event(gs_ctx* c, hipEvent_t e, bool dominant = false) {
+  if (c->timing == GS_TIMING_STAGES || (dominant && c->timing == GS_TIMING_DOMINANT)) hipEventRecord(e, c->stream);
 }
 
 // k_keyinfo over both columns (ALL): mask at SM_MASK, byte histograms at SM_HIST

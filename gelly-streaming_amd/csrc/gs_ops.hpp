@@ -102,6 +102,10 @@ inline void finish_times(gs_ctx* c, const Sorted& s, uint64_t U) {
   c->times.payload_bytes = (uint32_t)s.payload_bytes;
   c->times.fused_last = s.fused ? 1u : 0u;
   c->times.path = 0;
+  if (c->timing != GS_TIMING_STAGES) {   // the window's start event was not recorded (stage_event)
+    c->times.keyinfo_ms = c->times.sort_ms = c->times.reduce_ms = c->times.total_ms = 0.f;
+    for (int p = 0; p < 8; ++p) c->times.pass_ms[p] = 0.f;
+  }
 }
 
 // Copy U staged outputs to the caller (host or device) — only when the direct write was impossible.

@@ -949,26 +949,12 @@ gs_status tri_count(gs_ctx* c, uint32_t B, size_t V, uint64_t M, const uint32_t*
   GS_HIP(hipMemcpyAsync(c->host_small + 6, d_nheavy, 4, hipMemcpyDeviceToHost, c->stream));
   GS_TRY(host_wait(c));
   const uint32_t nh = (uint32_t)c->host_small[6];
-  // heavy items whose v lies in the top 2^16 ranks read the 2-byte copy of the list tails (k_tri_narrow;
-  // A/B GS_TH_NARROW=0: the 4-byte lists only).  nbr must be 16-byte aligned (the copy reads uint4).
-  static const bool narrow_on = !getenv("GS_TH_NARROW") || atoi(getenv("GS_TH_NARROW")) != 0;
-  const uint32_t base16 = V > 65536 ? (uint32_t)(V - 65536) : 0u;
-  const uint16_t* nbr16 = nullptr;
-  if (nh && narrow_on && ((uintptr_t)nbr & 15) == 0) {
-    GS_TRY(ensure(c, c->tri_n16, M * 2 + 16));
-    hipLaunchKernelGGL(k_tri_narrow, dim3((unsigned)std::max<uint64_t>(1, std::min<uint64_t>((M / 4 + 255) / 256, 16384))),
-                       dim3(256), 0, c->stream, nbr, (uint32_t)M, base16, c->tri_n16.as<uint16_t>());
-    GS_HIP(hipGetLastError());
-    nbr16 = c->tri_n16.as<uint16_t>();
-  }
-  // A/B (GS_TH_XCD): claim ranges of the phase order per XCD (8) or one shared counter (1)
-  static const uint32_t hx = getenv("GS_TH_XCD") ? (uint32_t)std::max(1, std::min(8, atoi(getenv("GS_TH_XCD")))) : 8u;
   if (nh && GS_TH_PHASED) {   // items in phase order, claimed one at a time
     GS_TRY(ensure(c, c->tri_hwork, (size_t)nh * 4 + (TH_PHASES + 64) * 4));
     uint32_t* hist = c->tri_hwork.as<uint32_t>();
     uint32_t* claim = hist + TH_PHASES;
     uint32_t* order = hist + TH_PHASES + 64;
-    GS_HIP(hipMemsetAsync(hist, 0, (TH_PHASES + 8) * 4, c->stream));   // phases, claim counters
+    GS_HIP(hipMemsetAsync(hist, 0, (TH_PHASES + 1) * 4, c->stream));
     const unsigned g = (unsigned)std::min<uint64_t>((nh + 255) / 256, 4096);
     hipLaunchKernelGGL(k_tri_hphase_count<TH_VCH>, dim3(g), dim3(256), 0, c->stream, sfx, in_range, c->tri_heavy.as<uint2>(),
                        nh, (uint32_t)M, hist);
@@ -977,7 +963,7 @@ gs_status tri_count(gs_ctx* c, uint32_t B, size_t V, uint64_t M, const uint32_t*
                        nh, (uint32_t)M, hist, order);
     hipLaunchKernelGGL(k_tri_heavy, dim3(GS_TH_HGRID), dim3(TH_HBLOCK), 0, c->stream, nbr, sfx, out_range, in_range,
                        c->tri_heavy.as<uint2>(), d_nheavy, nullptr, (const uint32_t*)order, claim, d_total, d_probes,
-                       nb_cap, d_err, hx, nbr16, base16);
+                       nb_cap, d_err);
     GS_HIP(hipGetLastError());
   } else if (nh) {
     GS_TRY(ensure(c, c->tri_hwork, (size_t)nh * 16 + 8));
@@ -988,7 +974,7 @@ gs_status tri_count(gs_ctx* c, uint32_t B, size_t V, uint64_t M, const uint32_t*
     GS_TRY(xscan(c, (const uint64_t*)hw, nh, (uint64_t*)hw + nh));
     hipLaunchKernelGGL(k_tri_heavy, dim3(GS_TH_HGRID), dim3(TH_HBLOCK), 0, c->stream, nbr, sfx, out_range, in_range,
                        c->tri_heavy.as<uint2>(), d_nheavy, (const unsigned long long*)hw + nh, nullptr, nullptr,
-                       d_total, d_probes, nb_cap, d_err, 1u, nbr16, base16);
+                       d_total, d_probes, nb_cap, d_err);
     GS_HIP(hipGetLastError());
   }
   hipEventRecord(c->ev[3], c->stream);

@@ -42,6 +42,9 @@ constexpr uint32_t TH_NU = GS_TH_NU, TH_HB = TH_NU / 2, TH_VCH = GS_TH_VCH;   //
 #define GS_TH_BITMAP 1   // k_tri_heavy: N+(v) as a bitmap over (v, last] when the span fits the table
 #endif
 constexpr bool TH_BITMAP = GS_TH_BITMAP;
+// the heavy table's bits (TH_HB 16-byte buckets) less one word: the bitmap of a span of up to TH_BSPAN bits
+// keeps a zero word after its last, which items past the span index (k_tri_heavy's branch-free probe)
+constexpr uint32_t TH_BSPAN = TH_NU / 2 * 128u - 32u;
 #ifndef GS_TH_LBITMAP
 #define GS_TH_LBITMAP 0  // k_tri_light: the same for a wave's table (spans up to TH_H·32 bits); A/B: light count s24 7.08 vs 6.92 ms hash, off
 #endif
@@ -337,7 +340,7 @@ __global__ __launch_bounds__(TH_BLOCK) __attribute__((amdgpu_waves_per_eu(GS_TH_
       // (k_tri_heavy: span of N+(v) within its table's bits; history: the split at 256 alone, s26 455 ms,
       // at 512 alone s24 72 -> 78 ms)
       const bool heavy_v = dv > TH_DMAX ||
-                           (TH_BITMAP && nb_cap > 1 && dv > TH_HMIN && onbr[ro.y - 1] - v <= TH_HB * 128u);
+                           (TH_BITMAP && nb_cap > 1 && dv > TH_HMIN && onbr[ro.y - 1] - v <= TH_BSPAN);
       if (heavy_v) {   // one heavy item per TH_VCH in-neighbours: a hub spreads over blocks
         const uint32_t nhc = (ri.y - ri.x + TH_VCH - 1) / TH_VCH;
         uint32_t at = 0;
@@ -448,23 +451,6 @@ __global__ __launch_bounds__(256) void k_tri_hphase_place(const uint2* __restric
     order[atomicAdd(&off[min(th_phase<CH>(sfx, in_range, heavy[h], M), TH_PHASES - 1)], 1u)] = h;
 }
 
-// the 2-byte copy of the out-lists' top-range items for k_tri_heavy: onbr16[p] = onbr[p] - base16 (mod 2^16;
-// only the entries >= base16, the sorted lists' tails, are ever read)
-__global__ __launch_bounds__(256) void k_tri_narrow(const uint32_t* __restrict__ onbr, uint32_t M, uint32_t base16,
-                                                    uint16_t* __restrict__ onbr16) {
-  const uint32_t n4 = M / 4;
-  const uint4* s4 = reinterpret_cast<const uint4*>(onbr);
-  uint2* d4 = reinterpret_cast<uint2*>(onbr16);
-  for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < n4; i += gridDim.x * 256u) {
-    const uint4 x = s4[i];
-    d4[i] = make_uint2(((x.x - base16) & 0xFFFFu) | ((x.y - base16) << 16), ((x.z - base16) & 0xFFFFu) | ((x.w - base16) << 16));
-  }
-  if (blockIdx.x == 0 && threadIdx.x < (M & 3u)) {
-    const uint32_t p = n4 * 4 + threadIdx.x;
-    onbr16[p] = (uint16_t)(onbr[p] - base16);
-  }
-}
-
 // one block per heavy item (v, chunk of TH_VCH in-neighbours): N+(v) as an LDS hash set (up to TH_NU
 // entries; longer lists are binary-searched in HBM; rebuilt only when the block's item changes v),
 // the chunk's lists TH_ILP items per thread with one search.  One item per in-chunk spreads a hub over
@@ -481,8 +467,7 @@ __global__ __launch_bounds__(TH_HBLOCK) __attribute__((amdgpu_waves_per_eu(GS_TH
                                                          uint32_t* __restrict__ claim,
                                                          unsigned long long* __restrict__ total,
                                                          unsigned long long* __restrict__ n_probes, uint32_t nb_cap,
-                                                         uint32_t* __restrict__ err, uint32_t nx,
-                                                         const uint16_t* __restrict__ onbr16, uint32_t base16) {
+                                                         uint32_t* __restrict__ err) {
   __shared__ uint4 s_hash[TH_HB];               // TH_NU / 2 buckets (64 KiB): N+(v) as a hash set of 4-slot buckets
   __shared__ uint32_t s_off[TH_VCH + 1];        // short lists of the chunk (compacted): prefix of |N+(u)|, [ns] = total
   __shared__ uint32_t s_st[TH_VCH];             // start of that N+(u) in onbr
@@ -516,28 +501,10 @@ __global__ __launch_bounds__(TH_HBLOCK) __attribute__((amdgpu_waves_per_eu(GS_TH
     h0 = uni(lower(lo));
     h1 = blockIdx.x + 1 == gridDim.x ? nh : uni(lower(hi));
   }
-  // phased: the ordered items cut into nx equal ranges, each with its own claim counter; a block claims
-  // from range blockIdx.x % nx first -- workgroups go to the XCDs round-robin, so with nx = 8 each XCD
-  // walks its own stretch of phases and its L2 keeps the out-lists that stretch's items share, instead
-  // of all eight L2s caching the one phase in flight -- then helps the next ranges when its own is done
-  uint32_t xs = 0;   // (tid 0's) ranges this block found exhausted
   for (uint32_t k = 0;; ++k) {
     uint32_t hi;
     if (order) {
-      if (tid == 0) {
-        uint32_t got = 0xFFFFFFFFu;
-        while (xs < nx) {
-          const uint32_t r = (blockIdx.x + xs) % nx;
-          const uint32_t b = (uint32_t)((uint64_t)nh * r / nx), e = (uint32_t)((uint64_t)nh * (r + 1) / nx);
-          const uint32_t c = atomicAdd(&claim[r], 1u);
-          if (c < e - b) {
-            got = b + c;
-            break;
-          }
-          ++xs;
-        }
-        s_claim = got;
-      }
+      if (tid == 0) s_claim = atomicAdd(claim, 1u);
       __syncthreads();
       hi = uni(s_claim);
       if (hi >= nh) break;
@@ -555,7 +522,7 @@ __global__ __launch_bounds__(TH_HBLOCK) __attribute__((amdgpu_waves_per_eu(GS_TH
     // the table a binary search in HBM.  Degree-class ranks put every heavy vertex near the top of the
     // order, so the span is short (R-MAT s22: < 2^16 for all of the heavy work).
     const uint32_t span = uni(d ? onbr[ro.y - 1] - v : 0u);
-    const bool bitmap = TH_BITMAP && span <= TH_HB * 128u && nb_cap > 1;   // (tiny test tables: hash only)
+    const bool bitmap = TH_BITMAP && span <= TH_BSPAN && nb_cap > 1;   // (tiny test tables: hash only)
     const bool in_lds = bitmap || d <= TH_NU;
     uint32_t nb = 16;
     while (nb * 2 < d && nb < TH_HB) nb <<= 1;
@@ -563,9 +530,9 @@ __global__ __launch_bounds__(TH_HBLOCK) __attribute__((amdgpu_waves_per_eu(GS_TH
     const uint32_t bmask = nb - 1;
     __syncthreads();   // the previous item is done with the table and the list arrays
     if (in_lds && table_v != v) {
-      if (bitmap) {   // bit (w - v - 1) for w in N+(v)
+      if (bitmap) {   // bit (w - v - 1) for w in N+(v); word nw stays zero
         const uint32_t nw = (span + 31) / 32;
-        for (uint32_t i = tid; i < nw; i += TH_HBLOCK) hs[i] = 0u;
+        for (uint32_t i = tid; i <= nw; i += TH_HBLOCK) hs[i] = 0u;
         __syncthreads();
         for (uint32_t i = tid; i < d; i += TH_HBLOCK) {
           const uint32_t o = onbr[ro.x + i] - v - 1;
@@ -580,14 +547,22 @@ __global__ __launch_bounds__(TH_HBLOCK) __attribute__((amdgpu_waves_per_eu(GS_TH
     }
     const uint32_t* nvl = onbr + ro.x;
     auto probe = [&](const uint32_t (&x)[TH_ILP], uint32_t nv) -> uint32_t {
-      if (bitmap) {   // items lie past v (suffixes of N+(u) after v); past the span: not members
-        uint32_t c = 0;
+      if (bitmap) {
+        // items lie past v (suffixes of N+(u) after v): bit o = w - v - 1.  Branch-free, so the TH_ILP LDS
+        // reads issue together: an item past the span reads a zero bit (its word's bits past the span,
+        // or the zero word nw), and the lane's invalid items are masked arithmetically.  (Written with
+        // a conditional per item, the compiler put each item's LDS read in its own branch and waited
+        // for it there: eight LDS round trips in series per step.)
+        const uint32_t nw = (span + 31) / 32;
+        uint32_t o[TH_ILP], wv[TH_ILP];
 #pragma unroll
         for (int j = 0; j < TH_ILP; ++j) {
-          const uint32_t o = x[j] - v - 1;
-          const uint32_t wv = hs[min(o, span - 1) >> 5];
-          c += ((uint32_t)j < nv && o < span) ? (wv >> (o & 31)) & 1u : 0u;
+          o[j] = x[j] - v - 1;
+          wv[j] = hs[min(o[j] >> 5, nw)];
         }
+        uint32_t c = 0;
+#pragma unroll
+        for (int j = 0; j < TH_ILP; ++j) c += (wv[j] >> (o[j] & 31)) & ((uint32_t)j < nv ? 1u : 0u);
         return c;
       }
       if (in_lds) return th_probe(s_hash, bmask, x, nv, err);
@@ -653,79 +628,67 @@ __global__ __launch_bounds__(TH_HBLOCK) __attribute__((amdgpu_waves_per_eu(GS_TH
     }
     probes += srun + lrun;   // block-uniform
     __syncthreads();
-    // The suffixes' items: 4-byte ranks from onbr, or -- when v lies in the top 2^16 ranks [base16 - 1,
-    // top), so that every suffix item w > v does too -- the 2-byte copy of the list tails (onbr16[p] =
-    // onbr[p] - base16 where onbr[p] >= base16): half the bytes for the probes that dominate the count
-    // (R-MAT s24: 83 % of them have v there, tests/analysis_tri_core.py).  Block-uniform choice.
-    auto lists = [&](auto narrow_tag) {
-      constexpr bool NARROW = decltype(narrow_tag)::value;
-      auto item = [&](uint32_t p) -> uint32_t {
-        if constexpr (NARROW) return (uint32_t)onbr16[p] + base16;
-        else return onbr[p];
-      };
-      // short lists: TH_ILP consecutive items per thread, at most one list boundary per step
-      uint32_t top = 1;
-      while (2 * top < ns) top <<= 1;
-      for (uint32_t k0 = 0; k0 < srun; k0 += TH_HBLOCK * TH_ILP) {
-        const uint32_t kb = k0 + tid * TH_ILP;
-        const uint32_t kk = min(kb, srun - 1);
-        uint32_t q = 0;
-        for (uint32_t st = top; st; st >>= 1) {
-          const uint32_t t = q + st;
-          q = (t < ns && s_off[min(t, ns - 1)] <= kk) ? t : q;
+    // short lists: TH_ILP consecutive items per thread, at most one list boundary per step
+    uint32_t top = 1;
+    while (2 * top < ns) top <<= 1;
+    for (uint32_t k0 = 0; k0 < srun; k0 += TH_HBLOCK * TH_ILP) {
+      const uint32_t kb = k0 + tid * TH_ILP;
+      const uint32_t kk = min(kb, srun - 1);
+      uint32_t q = 0;
+      for (uint32_t st = top; st; st >>= 1) {
+        const uint32_t t = q + st;
+        q = (t < ns && s_off[min(t, ns - 1)] <= kk) ? t : q;
+      }
+      uint32_t nx = s_off[q + 1], base = s_st[q] - s_off[q];   // item kj of list q: onbr[kj + base]
+      uint32_t x[TH_ILP];
+#pragma unroll
+      for (int j = 0; j < TH_ILP; ++j) {
+        const uint32_t kj = min(kb + j, srun - 1);
+        if (kj >= nx) {
+          ++q;
+          base = s_st[q] - nx;
+          nx = s_off[q + 1];
         }
-        uint32_t o = s_off[q], sst = s_st[q], nx = s_off[q + 1];
+        x[j] = onbr[kj + base];
+      }
+      cnt += probe(x, kb < srun ? min((uint32_t)TH_ILP, srun - kb) : 0u);
+    }
+    // long lists: wave w walks items [w, w + 1) * lrun / NW in 64-item segments (one load of 64
+    // consecutive items); a segment spans at most two lists (every long list >= 64 items)
+    if (lrun) {
+      const uint32_t wu = uni((uint32_t)w);
+      const uint32_t a0 = uni((uint32_t)((uint64_t)lrun * wu / NW)), a1 = uni((uint32_t)((uint64_t)lrun * (wu + 1) / NW));
+      uint32_t q = 0;
+      {
+        uint32_t t2 = 1;
+        while (2 * t2 < nl) t2 <<= 1;
+        for (uint32_t st = t2; st; st >>= 1) {
+          const uint32_t t = q + st;
+          q = (t < nl && uni(s_loff[min(t, nl - 1)]) <= a0) ? t : q;
+        }
+      }
+      // item k of list q: onbr[k + dq]; of list q + 1: onbr[k + dq1] (wave-uniform offsets)
+      uint32_t qe = uni(s_loff[q + 1]), q1s = q + 1 < nl ? uni(s_lst[q + 1]) : 0u;
+      uint32_t dq = uni(s_lst[q]) - uni(s_loff[q]), dq1 = q1s - qe;
+      for (uint32_t k0 = a0; k0 < a1; k0 += WAVE * TH_ILP) {
         uint32_t x[TH_ILP];
 #pragma unroll
         for (int j = 0; j < TH_ILP; ++j) {
-          const uint32_t kj = min(kb + j, srun - 1);
-          if (kj >= nx) {
+          const uint32_t seg = k0 + (uint32_t)j * WAVE;   // wave-uniform
+          while (qe <= seg && q + 1 < nl) {
             ++q;
-            o = nx;
-            sst = s_st[q];
-            nx = s_off[q + 1];
+            dq = dq1;
+            qe = uni(s_loff[q + 1]);
+            q1s = q + 1 < nl ? uni(s_lst[q + 1]) : 0u;
+            dq1 = q1s - qe;
           }
-          x[j] = item(sst + (kj - o));
+          const uint32_t k = min(seg + (uint32_t)lane, a1 - 1);
+          x[j] = onbr[k + (k < qe ? dq : dq1)];
         }
-        cnt += probe(x, kb < srun ? min((uint32_t)TH_ILP, srun - kb) : 0u);
+        const uint32_t rem = a1 - k0;
+        cnt += probe(x, rem > (uint32_t)lane ? min((uint32_t)TH_ILP, (rem - lane + WAVE - 1) / WAVE) : 0u);
       }
-      // long lists: wave w walks items [w, w + 1) * lrun / NW in 64-item segments (one load of 64
-      // consecutive items); a segment spans at most two lists (every long list >= 64 items)
-      if (lrun) {
-        const uint32_t wu = uni((uint32_t)w);
-        const uint32_t a0 = uni((uint32_t)((uint64_t)lrun * wu / NW)), a1 = uni((uint32_t)((uint64_t)lrun * (wu + 1) / NW));
-        uint32_t q = 0;
-        {
-          uint32_t t2 = 1;
-          while (2 * t2 < nl) t2 <<= 1;
-          for (uint32_t st = t2; st; st >>= 1) {
-            const uint32_t t = q + st;
-            q = (t < nl && uni(s_loff[min(t, nl - 1)]) <= a0) ? t : q;
-          }
-        }
-        uint32_t qo = uni(s_loff[q]), qs = uni(s_lst[q]), qe = uni(s_loff[q + 1]), q1s = q + 1 < nl ? uni(s_lst[q + 1]) : 0u;
-        for (uint32_t k0 = a0; k0 < a1; k0 += WAVE * TH_ILP) {
-          uint32_t x[TH_ILP];
-#pragma unroll
-          for (int j = 0; j < TH_ILP; ++j) {
-            const uint32_t seg = k0 + (uint32_t)j * WAVE;   // wave-uniform
-            while (qe <= seg && q + 1 < nl) {
-              ++q;
-              qo = qe;
-              qs = q1s;
-              qe = uni(s_loff[q + 1]);
-              q1s = q + 1 < nl ? uni(s_lst[q + 1]) : 0u;
-            }
-            const uint32_t k = min(seg + (uint32_t)lane, a1 - 1);
-            x[j] = item(k < qe ? qs + (k - qo) : q1s + (k - qe));
-          }
-          const uint32_t rem = a1 - k0;
-          cnt += probe(x, rem > (uint32_t)lane ? min((uint32_t)TH_ILP, (rem - lane + WAVE - 1) / WAVE) : 0u);
-        }
-      }
-    };
-    if (onbr16 && v + 1 >= base16) lists(std::true_type{});
-    else lists(std::false_type{});
+    }
   }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o, WAVE);

@@ -111,6 +111,10 @@ class Engine:
         """Run on an existing hipStream_t (e.g. torch.cuda.current_stream().cuda_stream; 0 = default stream)."""
         self._check(self._L.gs_set_stream(self.ctx, ctypes.c_void_p(hip_stream_ptr) if hip_stream_ptr else None))
 
+    def set_timing(self, level: int):
+        """gs_set_timing: which stage-time events a window records (L.GS_TIMING_OFF / _DOMINANT / _STAGES)."""
+        self._check(self._L.gs_set_timing(self.ctx, int(level)))
+
     def use_torch_stream(self):
         import torch
 

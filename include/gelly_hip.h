@@ -545,6 +545,16 @@ typedef struct gs_stage_times {
   uint64_t escapes;        /* path 2, packed: values stored in full (outside [0, 0xFFFF))          */
 } gs_stage_times;
 GS_API gs_status gs_last_stage_times(const gs_ctx* ctx, gs_stage_times* out);
+/* Which device events a window records for gs_last_stage_times (diagnostics; replaces nothing in the
+ * reference).  GS_TIMING_STAGES (the default): every stage of every path.  GS_TIMING_DOMINANT: on the
+ * bucket path (path 2) only the brackets of the partition scatter and the accumulate (pass_ms[1],
+ * pass_ms[2]; every other time reads 0) -- each event record costs the stream a few microseconds,
+ * ~30 us per C2 window at the default.  GS_TIMING_OFF: none on the bucket path.  path / packed /
+ * speculative / escapes and the counts stay valid at every level. */
+#define GS_TIMING_OFF 0
+#define GS_TIMING_DOMINANT 1
+#define GS_TIMING_STAGES 2
+GS_API gs_status gs_set_timing(gs_ctx* ctx, int32_t level);
 
 #ifdef __cplusplus
 }

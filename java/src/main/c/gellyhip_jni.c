@@ -62,6 +62,12 @@ JNIEXPORT jlong JNI_FN(create)(JNIEnv* env, jclass cls, jint device, jint flags,
 
 JNIEXPORT void JNI_FN(destroy)(JNIEnv* env, jclass cls, jlong ctx) { gs_destroy((gs_ctx*)(intptr_t)ctx); }
 
+JNIEXPORT void JNI_FN(setTiming)(JNIEnv* env, jclass cls, jlong ctx, jint level) {
+  gs_ctx* c = (gs_ctx*)(intptr_t)ctx;
+  gs_status s = gs_set_timing(c, (int32_t)level);
+  if (s != GS_OK) throw_status(env, c, s, "gs_set_timing");
+}
+
 JNIEXPORT void JNI_FN(setMaxWindowRecords)(JNIEnv* env, jclass cls, jlong ctx, jlong max_records) {
   gs_ctx* c = (gs_ctx*)(intptr_t)ctx;
   gs_status s = gs_set_max_window_records(c, (uint64_t)max_records);

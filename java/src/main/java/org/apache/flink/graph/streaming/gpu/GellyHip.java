@@ -68,6 +68,11 @@ public final class GellyHip {
 	public static final int GS_LATE_REFIRE = 0;   // Flink 1.0.3 WindowOperator: a late record re-fires its window
 	public static final int GS_LATE_DROP = 1;
 
+	/* gs_set_timing levels */
+	public static final int GS_TIMING_OFF = 0;
+	public static final int GS_TIMING_DOMINANT = 1;
+	public static final int GS_TIMING_STAGES = 2;
+
 	/* ---- lifecycle: gs_abi_version, gs_create / gs_destroy ---------------------------------------- */
 	static native int abiVersion();
 
@@ -75,6 +80,9 @@ public final class GellyHip {
 	static native long create(int device, int flags, long reserveEdges);
 
 	static native void destroy(long ctx);
+
+	/** gs_set_timing: which stage-time events a window records (GS_TIMING_*; the operators run OFF). */
+	static native void setTiming(long ctx, int level);
 
 	/** gs_set_max_window_records: records per engine pass (larger reduce / fold windows run in chunks). */
 	static native void setMaxWindowRecords(long ctx, long maxRecords);

@@ -73,6 +73,7 @@ public class GpuCandidatesOperator<EV> extends AbstractStreamOperator<Tuple3<Lon
 	public void open() throws Exception {
 		super.open();
 		ctx = GellyHip.create(device, 0, 0);
+		GellyHip.setTiming(ctx, GellyHip.GS_TIMING_OFF);   // no stage-time events in production
 		open = new TreeMap<Long, Columns>();
 		a = GellyHip.direct(8L * CHUNK);
 		b = GellyHip.direct(8L * CHUNK);

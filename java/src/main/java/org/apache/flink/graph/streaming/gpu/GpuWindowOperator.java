@@ -71,6 +71,7 @@ public class GpuWindowOperator<EV, OUT extends Tuple> extends AbstractStreamOper
 	public void open() throws Exception {
 		super.open();
 		ctx = GellyHip.create(device, 0, maxWindowEdges);
+		GellyHip.setTiming(ctx, GellyHip.GS_TIMING_OFF);   // no stage-time events in production
 		ByteBuffer initBuf = null;
 		long initMax = Long.MIN_VALUE;
 		if (kind == GellyHip.GS_STREAM_FOLD) {

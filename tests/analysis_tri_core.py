@@ -7,6 +7,8 @@ analysis_tri_boundary.geometry (degree-class ranks, oriented unique edges u -> v
     N+(u) past v against N+(v));
   * smaller side: probing min(|suffix of N+(u) past v|, d+(v)) per edge instead;
   * range cut: probing only the suffix items inside [min N+(v), max N+(v)] (a binary search each end);
+  * narrow items: the share of the probes whose v lies in the top 2^k ranks, so that every item of the
+    suffixes it reads does too and fits 2 bytes relative to the top range (k_tri_heavy's onbr16, k = 16);
   * dense core: the share of the probes whose three vertices all lie among the top K ranks (where a
     dense K x K 0/1 product on the matrix cores, 2K^3 int8 operations, could count them instead).
 python tests/analysis_tri_core.py 22 [24]
@@ -41,6 +43,9 @@ def report(scale):
     b = np.minimum(np.searchsorted(key, u * V + hi[v], "right"), suf_hi)
     cut = np.where(dplus[v] > 0, np.maximum(b - a, 0), 0)
     print(f"range cut: {cut.sum() / 1e9:.2f} G ({cut.sum() / total:.3f})")
+    for k in (14, 15, 16, 17, 18):
+        m = v >= V - (1 << k) - 1
+        print(f"v in the top 2^{k} ranks: {suf[m].sum() / 1e9:.2f} G probes ({suf[m].sum() / total:.3f})")
     for K in (4096, 8192, 16384, 32768, 65536):
         c = V - K
         core = int((dplus[c:] * (dplus[c:] - 1) // 2).sum())

@@ -394,3 +394,37 @@ def test_packed_presence_of_zero_and_escaped_only_vertices(pkg, oracle, op):
             assert t.path == 2 and t.packed
             assert t.speculative == (0 if w == 0 else 1)
             _check(gk, gv, rk, rv, np.int64, op)
+
+
+def test_timing_levels_same_results(pkg, oracle):
+    """gs_set_timing: the stage events a window records change nothing but the stage times.  STAGES times
+    every stage; DOMINANT only the direct path's scatter and accumulate (pass_ms[1], [2]); OFF none.  The
+    speculative partition (windows after the first) runs at every level."""
+    L = pkg._lib
+    rng = np.random.default_rng(77)
+    n = 1 << 20
+    s, d = _window(rng, n, 1 << 22)
+    v = oracle.gen_values(n, 5, oracle.DT_I64)
+    rk, rv = oracle.window_reduce(s, d, v, 1, 0)
+    e = pkg.Engine(0)
+    try:
+        with pytest.raises(pkg.GsError):
+            e.set_timing(7)
+        cols = _dev(s, d, v)
+        for level in (L.GS_TIMING_STAGES, L.GS_TIMING_DOMINANT, L.GS_TIMING_OFF, L.GS_TIMING_STAGES):
+            e.set_timing(level)
+            for _ in range(2):
+                gk, gv = e.reduce(*cols, 1, 0)
+                _check(gk, gv, rk, rv, np.int64, 0)
+                t = e.stage_times()
+                assert t.path == 2
+            pm = list(t.pass_ms)
+            if level == L.GS_TIMING_STAGES:
+                assert pm[1] > 0 and pm[2] > 0 and pm[4] > 0 and t.total_ms > 0
+            elif level == L.GS_TIMING_DOMINANT:
+                assert pm[1] > 0 and pm[2] > 0 and pm[3] == 0 and pm[4] == 0 and t.total_ms == 0
+            else:
+                assert not any(pm) and t.total_ms == 0
+            assert t.speculative == 1   # the second window of each level
+    finally:
+        e.close()
