@@ -208,6 +208,7 @@ gs_status bucket_accumulate(gs_ctx* c, Src rs, uint64_t R, uint32_t nb, int64_t 
 // after host_wait: the accumulate's results (GS_EDEVICE on a look-back timeout)
 gs_status bucket_results(gs_ctx* c, uint64_t* U, uint32_t* n_items) {
   if ((uint32_t)c->host_small[6] != 0) return set_error(c, GS_EDEVICE, "look-back spin timed out");
+  c->timeout_clean = true;   // read back as zero at the end of this window (begin_call skips its clear)
   *U = c->host_small[3];
   *n_items = (uint32_t)c->host_small[4];
   return GS_OK;

@@ -84,7 +84,10 @@ gs_status begin_call(gs_ctx* c) {
   c->last_kind = 0;   // the staged output buffers are about to be reused: nothing left to fetch
   (void)hipGetLastError();
   GS_HIP(hipSetDevice(c->device));
-  GS_HIP(hipMemsetAsync(c->small.as<char>() + SM_TIMEOUT, 0, 8, c->stream));
+  // the look-back timeout word: cleared unless the previous call's read-back saw it zero (the bucket
+  // path reads it back with every window, so back-to-back windows skip this launch)
+  if (!c->timeout_clean) GS_HIP(hipMemsetAsync(c->small.as<char>() + SM_TIMEOUT, 0, 8, c->stream));
+  c->timeout_clean = false;
   return GS_OK;
 }
 

@@ -43,6 +43,7 @@ struct gs_ctx {
   bool own_stream = false;
   std::string err;
   uint32_t epoch = 0;
+  bool timeout_clean = false;      // SM_TIMEOUT known zero (begin_call)
   int timing = GS_TIMING_STAGES;   // gs_set_timing: which stage events a window records (stage_event)
   int hist_digits = 4;   // key-byte histograms keyinfo computes (learned from the previous window)
   uint32_t flags = 0;    // gs_config.flags

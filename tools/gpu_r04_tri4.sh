@@ -14,7 +14,7 @@ for i in 1 2; do
   timeout -k 10 200 python3 bench.py --steps 30 --warmup 5 --no-cpu-baseline --timing stages > $O/c2_stages_$i.json 2> $O/c2_stages_$i.err
 done
 echo c2 done
-for v in default ilp4 ilp16; do
+for v in default ilp4 ilp16 hmin128 hmin64; do
   lib=""; [ $v = default ] || lib=$PWD/gelly-streaming_amd/variants/$v/libgellyhip.so
   for s in 24 26; do
     env ${lib:+GELLY_HIP_LIB=$lib} timeout -k 10 300 python3 bench.py --workload triangles --scale $s --steps 2 --warmup 1 \
