@@ -893,9 +893,11 @@ gs_status tri_count(gs_ctx* c, uint32_t B, size_t V, uint64_t M, const uint32_t*
   // count 7.1 -> 36 ms, s26 42 -> 147 ms, profiles/r04/evidence/tri_*_lph.json): off
   static const int lphased_env = getenv("GS_TH_LPHASED") ? atoi(getenv("GS_TH_LPHASED")) : 0;
   const bool lphased = lphased_env != 0 && GS_TH_PHASED;
+  // A/B (GS_TH_LCLASS=0): the light kernel's own vertex pass (a wave per id) instead of k_tri_lclass
+  static const bool lclass = !getenv("GS_TH_LCLASS") || atoi(getenv("GS_TH_LCLASS")) != 0;
   GS_TRY(ensure(c, c->tri_heavy, (V + Ms / TH_VCH + 64) * 8));   // (v, in-chunk) items
   // queued light chunks: the further chunks (<= Ms / TH_LCH), or, phased, every light chunk
-  GS_TRY(ensure(c, c->tri_queue, ((lphased ? V : 0) + Ms / TH_LCH + 64) * 8));
+  GS_TRY(ensure(c, c->tri_queue, (std::min<uint64_t>(V, Ms) + Ms / TH_LCH + 64) * 8));
   unsigned long long* d_total = (unsigned long long*)(sm + SM_NUNIQUE);
   uint32_t* d_nheavy = (uint32_t*)(sm + SM_COUNTERS) + 62;
   unsigned long long* d_probes = (unsigned long long*)(sm + SM_TRI_PROBES);
@@ -935,6 +937,14 @@ gs_status tri_count(gs_ctx* c, uint32_t B, size_t V, uint64_t M, const uint32_t*
                          d_probes, nb_cap, d_err, (const uint32_t*)order);
       GS_HIP(hipGetLastError());
     }
+  } else if (lclass) {   // the vertices with work queued by one lane per id, then the light chunks
+    hipLaunchKernelGGL(k_tri_lclass, dim3((unsigned)std::max<uint64_t>(1, std::min<uint64_t>((V + 255) / 256, 16384))),
+                       dim3(256), 0, c->stream, nbr, out_range, in_range, (uint32_t)V, 0u, 0xFFFFFFFFu, nb_cap, queue,
+                       d_nqueue, c->tri_heavy.as<uint2>(), d_nheavy);
+    hipLaunchKernelGGL(k_tri_light, dim3(8192u), dim3(TH_BLOCK), 0, c->stream, nbr, sfx, out_range, in_range,
+                       (uint32_t)V, 0u, 0xFFFFFFFFu, 1, queue, d_nqueue, c->tri_heavy.as<uint2>(), d_nheavy, d_total,
+                       d_probes, nb_cap, d_err, (const uint32_t*)nullptr);
+    GS_HIP(hipGetLastError());
   } else {
     for (int pass = 0; pass < 2; ++pass) {
       hipLaunchKernelGGL(k_tri_light, dim3(pass == 0 ? nvb : 4096u), dim3(TH_BLOCK), 0, c->stream, nbr, sfx, out_range,

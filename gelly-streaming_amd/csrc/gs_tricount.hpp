@@ -79,6 +79,12 @@ constexpr int TH_ILP = GS_TH_ILP;   // items per lane: TH_ILP probes in flight
 #define GS_TH_LONG 64    // light kernel: out-lists of >= TH_LONG items are gathered lane-interleaved (64 per load)
 #endif
 constexpr uint32_t TH_LONG = GS_TH_LONG;
+#ifndef GS_TH_LPREF_Q
+#define GS_TH_LPREF_Q 1  // k_tri_light passes 1 / 3: prefetch the next queued chunk's entry (2: and its ranges)
+#endif
+#ifndef GS_TH_LPREF_S
+#define GS_TH_LPREF_S 1  // k_tri_light: a chunk's first 64 suffix ranges loaded before its table is built
+#endif
 #ifndef GS_TH_LWAVES
 #define GS_TH_LWAVES 6   // k_tri_light waves per SIMD the registers are capped for (4 -> 6: s22 3.03 -> 2.38 ms)
 #endif
@@ -167,15 +173,19 @@ __device__ __forceinline__ uint32_t th_probe(const uint4* hb, uint32_t bmask, co
 // lists of >= TH_LONG items ("long") are gathered lane-interleaved (64 consecutive items per load:
 // 2 cache lines); the short ones TH_ILP consecutive items per lane.  Short lists fill po / ps from the
 // front (po = prefix of their lengths), long ones from the back (po = prefix over long lists)
+// first = sfx[c0 + lane] (zero past c1), loaded by the caller before it built the table
 template <uint32_t CAP, class Probe>
 __device__ __forceinline__ uint32_t th_wave_probe(const uint32_t* __restrict__ onbr, const uint2* __restrict__ sfx,
                                                   uint32_t c0, uint32_t c1, int lane, uint32_t* po, uint32_t* ps,
-                                                  uint64_t& probes, Probe probe) {
+                                                  uint64_t& probes, Probe probe, uint2 first) {
   uint32_t run = 0, dn = 0, lrun = 0, nl = 0;
   for (uint32_t i0 = c0; i0 < c1; i0 += WAVE) {
     const uint32_t i = i0 + lane;
     uint32_t du = 0, su = 0;
-    if (i < c1) {
+    if (GS_TH_LPREF_S && i0 == c0) {
+      du = first.y - first.x;
+      su = first.x;
+    } else if (i < c1) {
       const uint2 ru = sfx[i];
       du = ru.y - ru.x;
       su = ru.x;
@@ -267,6 +277,9 @@ __device__ __forceinline__ uint32_t th_wave_chunk(const uint32_t* __restrict__ o
                                                   uint64_t& probes, uint32_t nb_cap, uint32_t* err) {
   uint32_t* hs = reinterpret_cast<uint32_t*>(hb);
   const uint32_t d = ro.y - ro.x;
+  // the first 64 suffix ranges, issued before the table's loads (one dependent round trip less)
+  uint2 first = make_uint2(0u, 0u);
+  if (GS_TH_LPREF_S && c0 + lane < c1) first = sfx[c0 + lane];
   // a bitmap over (v, last] when the span fits the table's TH_H·32 bits (k_tri_heavy): the high-rank
   // light vertices (hubs with few higher neighbours)
   const uint32_t v = uni(v_id), span = uni(onbr[ro.y - 1] - v);
@@ -289,7 +302,7 @@ __device__ __forceinline__ uint32_t th_wave_chunk(const uint32_t* __restrict__ o
                                       c += ((uint32_t)j < nv && o < span) ? (wv >> (o & 31)) & 1u : 0u;
                                     }
                                     return c;
-                                  });
+                                  }, first);
   }
   uint32_t nb = 16;
   while (nb < d && nb < TH_H / 4) nb <<= 1;
@@ -300,7 +313,8 @@ __device__ __forceinline__ uint32_t th_wave_chunk(const uint32_t* __restrict__ o
   for (uint32_t i = lane; i < d; i += WAVE) th_insert(hs, onbr[ro.x + i], bmask, err);
   wave_lds_sync();
   return th_wave_probe<TH_LCH>(onbr, sfx, c0, c1, lane, po, ps, probes,
-                                [&](const uint32_t (&x)[TH_ILP], uint32_t nv) { return th_probe(hb, bmask, x, nv, err); });
+                                [&](const uint32_t (&x)[TH_ILP], uint32_t nv) { return th_probe(hb, bmask, x, nv, err); },
+                                first);
 }
 
 // pass 0: vertices, interleaved; first in-chunk here, further chunks queued, long out-lists to the
@@ -329,8 +343,20 @@ __global__ __launch_bounds__(TH_BLOCK) __attribute__((amdgpu_waves_per_eu(GS_TH_
   const uint32_t nw = gridDim.x * TH_WPB;
   uint64_t cnt = 0, probes = 0;
   const uint32_t n_items = (pass == 0 || pass == 2) ? nv : *n_queue;
+  // passes 1 / 3: the next queued chunk's entry and ranges are loaded while this one is counted
+  auto qload = [&](uint32_t it, uint2& q, uint2& ri, uint2& ro) {
+    q = queue[pass == 3 ? order[it] : it];
+    if (GS_TH_LPREF_Q > 1) {   // (1: the entry only; its ranges are loaded when it is counted)
+      ri = in_range[q.x];
+      ro = out_range[q.x];
+    }
+  };
+  uint2 nq = make_uint2(0u, 0u), nri = nq, nro = nq;
+  if (GS_TH_LPREF_Q && (pass == 1 || pass == 3) && blockIdx.x * TH_WPB + w < n_items)
+    qload(blockIdx.x * TH_WPB + w, nq, nri, nro);
   for (uint32_t it = blockIdx.x * TH_WPB + w; it < n_items; it += nw) {   // interleaved: no claim counter
     uint32_t v, c0, c1;
+    uint2 ro_v;
     if (pass == 0 || pass == 2) {
       v = it;
       const uint2 ro = out_range[v], ri = in_range[v];
@@ -360,20 +386,72 @@ __global__ __launch_bounds__(TH_BLOCK) __attribute__((amdgpu_waves_per_eu(GS_TH_
       if (pass == 2) continue;
       c0 = ri.x;
       c1 = min(ri.y, ri.x + TH_LCH);
+      ro_v = ro;
     } else {
-      const uint2 q = queue[pass == 3 ? order[it] : it];
+      uint2 q, ri;
+      if (GS_TH_LPREF_Q) {
+        q = make_uint2(uni(nq.x), uni(nq.y));
+        if (GS_TH_LPREF_Q > 1) {
+          ri = make_uint2(uni(nri.x), uni(nri.y));
+          ro_v = make_uint2(uni(nro.x), uni(nro.y));
+        } else {
+          ri = in_range[q.x];
+          ro_v = out_range[q.x];
+        }
+        if (it + nw < n_items) qload(it + nw, nq, nri, nro);
+      } else {
+        q = queue[pass == 3 ? order[it] : it];
+        ri = in_range[q.x];
+        ro_v = out_range[q.x];
+      }
       v = q.x;
-      const uint2 ri = in_range[v];
       c0 = ri.x + q.y * TH_LCH;
       c1 = min(ri.y, c0 + TH_LCH);
     }
-    cnt += th_wave_chunk(onbr, sfx, v, out_range[v], c0, c1, lane, s_hash[w], s_off[w], s_st[w], probes,
+    cnt += th_wave_chunk(onbr, sfx, v, ro_v, c0, c1, lane, s_hash[w], s_off[w], s_st[w], probes,
                          nb_cap, err);
   }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o, WAVE);
   if (lane == 0 && cnt) atomicAdd(total, (unsigned long long)cnt);
   if (lane == 0 && probes) atomicAdd(n_probes, (unsigned long long)probes);   // wave-uniform
+}
+
+// The light kernel's vertex pass as its own launch, one lane per vertex: every vertex with in- and
+// out-entries whose out-list starts in [q0, q1) becomes heavy items (its in-chunks of TH_VCH) or light
+// queue entries (its in-chunks of TH_LCH, the first included), and k_tri_light runs over the queue only.
+// (A wave per id in rank order paid a dependent load per id -- 2^26 of them at s26, most without work.)
+// The heavy rule is k_tri_light pass 0's.  Appends are wave-aggregated (one atomic per wave and list).
+__global__ __launch_bounds__(256) void k_tri_lclass(const uint32_t* __restrict__ onbr, const uint2* __restrict__ out_range,
+                                                    const uint2* __restrict__ in_range, uint32_t nv, uint32_t q0,
+                                                    uint32_t q1, uint32_t nb_cap, uint2* __restrict__ queue,
+                                                    uint32_t* __restrict__ n_queue, uint2* __restrict__ heavy,
+                                                    uint32_t* __restrict__ n_heavy) {
+  const int lane = threadIdx.x & 63;
+  for (uint32_t v0 = blockIdx.x * 256u; v0 < nv; v0 += gridDim.x * 256u) {   // wave-uniform trip count
+    const uint32_t v = v0 + threadIdx.x;
+    uint32_t nh = 0, nl = 0;
+    if (v < nv) {
+      const uint2 ro = out_range[v], ri = in_range[v];
+      if (ro.y != ro.x && ri.y != ri.x && ro.x >= q0 && ro.x < q1) {
+        const uint32_t dv = ro.y - ro.x;
+        const bool heavy_v = dv > TH_DMAX ||
+                             (TH_BITMAP && nb_cap > 1 && dv > TH_HMIN && onbr[ro.y - 1] - v <= TH_BSPAN);
+        if (heavy_v) nh = (ri.y - ri.x + TH_VCH - 1) / TH_VCH;
+        else nl = (ri.y - ri.x + TH_LCH - 1) / TH_LCH;
+      }
+    }
+    const uint32_t ih = wave_inclusive_sum(nh), il = wave_inclusive_sum(nl);
+    uint32_t bh = 0, bl = 0;
+    if (lane == 63) {
+      if (ih) bh = atomicAdd(n_heavy, ih);
+      if (il) bl = atomicAdd(n_queue, il);
+    }
+    bh = __shfl(bh, 63, WAVE) + ih - nh;
+    bl = __shfl(bl, 63, WAVE) + il - nl;
+    for (uint32_t j = 0; j < nh; ++j) heavy[bh + j] = make_uint2(v, j);
+    for (uint32_t j = 0; j < nl; ++j) queue[bl + j] = make_uint2(v, j);
+  }
 }
 
 // work of each heavy item (v, chunk of TH_VCH in-entries): its probes (the suffix lengths) plus a
