@@ -79,12 +79,6 @@ constexpr int TH_ILP = GS_TH_ILP;   // items per lane: TH_ILP probes in flight
 #define GS_TH_LONG 64    // light kernel: out-lists of >= TH_LONG items are gathered lane-interleaved (64 per load)
 #endif
 constexpr uint32_t TH_LONG = GS_TH_LONG;
-#ifndef GS_TH_LPREF_Q
-#define GS_TH_LPREF_Q 1  // k_tri_light passes 1 / 3: prefetch the next queued chunk's entry (2: and its ranges)
-#endif
-#ifndef GS_TH_LPREF_S
-#define GS_TH_LPREF_S 1  // k_tri_light: a chunk's first 64 suffix ranges loaded before its table is built
-#endif
 #ifndef GS_TH_LWAVES
 #define GS_TH_LWAVES 6   // k_tri_light waves per SIMD the registers are capped for (4 -> 6: s22 3.03 -> 2.38 ms)
 #endif
@@ -173,19 +167,15 @@ __device__ __forceinline__ uint32_t th_probe(const uint4* hb, uint32_t bmask, co
 // lists of >= TH_LONG items ("long") are gathered lane-interleaved (64 consecutive items per load:
 // 2 cache lines); the short ones TH_ILP consecutive items per lane.  Short lists fill po / ps from the
 // front (po = prefix of their lengths), long ones from the back (po = prefix over long lists)
-// first = sfx[c0 + lane] (zero past c1), loaded by the caller before it built the table
 template <uint32_t CAP, class Probe>
 __device__ __forceinline__ uint32_t th_wave_probe(const uint32_t* __restrict__ onbr, const uint2* __restrict__ sfx,
                                                   uint32_t c0, uint32_t c1, int lane, uint32_t* po, uint32_t* ps,
-                                                  uint64_t& probes, Probe probe, uint2 first) {
+                                                  uint64_t& probes, Probe probe) {
   uint32_t run = 0, dn = 0, lrun = 0, nl = 0;
   for (uint32_t i0 = c0; i0 < c1; i0 += WAVE) {
     const uint32_t i = i0 + lane;
     uint32_t du = 0, su = 0;
-    if (GS_TH_LPREF_S && i0 == c0) {
-      du = first.y - first.x;
-      su = first.x;
-    } else if (i < c1) {
+    if (i < c1) {
       const uint2 ru = sfx[i];
       du = ru.y - ru.x;
       su = ru.x;
@@ -277,9 +267,6 @@ __device__ __forceinline__ uint32_t th_wave_chunk(const uint32_t* __restrict__ o
                                                   uint64_t& probes, uint32_t nb_cap, uint32_t* err) {
   uint32_t* hs = reinterpret_cast<uint32_t*>(hb);
   const uint32_t d = ro.y - ro.x;
-  // the first 64 suffix ranges, issued before the table's loads (one dependent round trip less)
-  uint2 first = make_uint2(0u, 0u);
-  if (GS_TH_LPREF_S && c0 + lane < c1) first = sfx[c0 + lane];
   // a bitmap over (v, last] when the span fits the table's TH_H·32 bits (k_tri_heavy): the high-rank
   // light vertices (hubs with few higher neighbours)
   const uint32_t v = uni(v_id), span = uni(onbr[ro.y - 1] - v);
@@ -302,7 +289,7 @@ __device__ __forceinline__ uint32_t th_wave_chunk(const uint32_t* __restrict__ o
                                       c += ((uint32_t)j < nv && o < span) ? (wv >> (o & 31)) & 1u : 0u;
                                     }
                                     return c;
-                                  }, first);
+                                  });
   }
   uint32_t nb = 16;
   while (nb < d && nb < TH_H / 4) nb <<= 1;
@@ -313,8 +300,7 @@ __device__ __forceinline__ uint32_t th_wave_chunk(const uint32_t* __restrict__ o
   for (uint32_t i = lane; i < d; i += WAVE) th_insert(hs, onbr[ro.x + i], bmask, err);
   wave_lds_sync();
   return th_wave_probe<TH_LCH>(onbr, sfx, c0, c1, lane, po, ps, probes,
-                                [&](const uint32_t (&x)[TH_ILP], uint32_t nv) { return th_probe(hb, bmask, x, nv, err); },
-                                first);
+                                [&](const uint32_t (&x)[TH_ILP], uint32_t nv) { return th_probe(hb, bmask, x, nv, err); });
 }
 
 // pass 0: vertices, interleaved; first in-chunk here, further chunks queued, long out-lists to the
@@ -343,20 +329,8 @@ __global__ __launch_bounds__(TH_BLOCK) __attribute__((amdgpu_waves_per_eu(GS_TH_
   const uint32_t nw = gridDim.x * TH_WPB;
   uint64_t cnt = 0, probes = 0;
   const uint32_t n_items = (pass == 0 || pass == 2) ? nv : *n_queue;
-  // passes 1 / 3: the next queued chunk's entry and ranges are loaded while this one is counted
-  auto qload = [&](uint32_t it, uint2& q, uint2& ri, uint2& ro) {
-    q = queue[pass == 3 ? order[it] : it];
-    if (GS_TH_LPREF_Q > 1) {   // (1: the entry only; its ranges are loaded when it is counted)
-      ri = in_range[q.x];
-      ro = out_range[q.x];
-    }
-  };
-  uint2 nq = make_uint2(0u, 0u), nri = nq, nro = nq;
-  if (GS_TH_LPREF_Q && (pass == 1 || pass == 3) && blockIdx.x * TH_WPB + w < n_items)
-    qload(blockIdx.x * TH_WPB + w, nq, nri, nro);
   for (uint32_t it = blockIdx.x * TH_WPB + w; it < n_items; it += nw) {   // interleaved: no claim counter
     uint32_t v, c0, c1;
-    uint2 ro_v;
     if (pass == 0 || pass == 2) {
       v = it;
       const uint2 ro = out_range[v], ri = in_range[v];
@@ -386,29 +360,14 @@ __global__ __launch_bounds__(TH_BLOCK) __attribute__((amdgpu_waves_per_eu(GS_TH_
       if (pass == 2) continue;
       c0 = ri.x;
       c1 = min(ri.y, ri.x + TH_LCH);
-      ro_v = ro;
     } else {
-      uint2 q, ri;
-      if (GS_TH_LPREF_Q) {
-        q = make_uint2(uni(nq.x), uni(nq.y));
-        if (GS_TH_LPREF_Q > 1) {
-          ri = make_uint2(uni(nri.x), uni(nri.y));
-          ro_v = make_uint2(uni(nro.x), uni(nro.y));
-        } else {
-          ri = in_range[q.x];
-          ro_v = out_range[q.x];
-        }
-        if (it + nw < n_items) qload(it + nw, nq, nri, nro);
-      } else {
-        q = queue[pass == 3 ? order[it] : it];
-        ri = in_range[q.x];
-        ro_v = out_range[q.x];
-      }
+      const uint2 q = queue[pass == 3 ? order[it] : it];
       v = q.x;
+      const uint2 ri = in_range[v];
       c0 = ri.x + q.y * TH_LCH;
       c1 = min(ri.y, c0 + TH_LCH);
     }
-    cnt += th_wave_chunk(onbr, sfx, v, ro_v, c0, c1, lane, s_hash[w], s_off[w], s_st[w], probes,
+    cnt += th_wave_chunk(onbr, sfx, v, out_range[v], c0, c1, lane, s_hash[w], s_off[w], s_st[w], probes,
                          nb_cap, err);
   }
 #pragma unroll
