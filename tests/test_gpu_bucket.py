@@ -428,3 +428,42 @@ def test_timing_levels_same_results(pkg, oracle):
             assert t.speculative == 1   # the second window of each level
     finally:
         e.close()
+
+
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+def test_float_sum_presence_with_signed_zeros(engine, oracle, dtype):
+    """Float SUM infers a vertex's presence from its accumulator (it starts at -0.0; a sum that cancels
+    ends at +0.0) and marks presence only for -0.0 values (gs_bucket.hpp BkVal::FLOAT_SUM).  Vertices whose
+    records are all +0.0, all -0.0, cancel exactly, or mix -0.0 with others must all be present, with the
+    reference's signed zeros, including across the slabs of a multi-item hub bucket."""
+    rng = np.random.default_rng(2024)
+    n = 1 << 20
+    hub = 5000
+    s = rng.integers(0, 1 << 20, n).astype(np.int64)
+    s[: n // 2] = hub                                   # a hub bucket of many items (slabs)
+    v = rng.standard_normal(n).astype(dtype)
+    special = {hub + 1: [0.0] * 40, hub + 2: [-0.0] * 40, hub + 3: [1.5, -1.5] * 20, hub + 4: [-0.0, 2.0] * 20,
+               hub + 5: [-0.0] * 3, 700001: [0.0], 700002: [-0.0]}
+    pos = rng.permutation(n)[: sum(len(x) for x in special.values())]
+    at = 0
+    for vid, vals in special.items():
+        for x in vals:
+            s[pos[at]], v[pos[at]] = vid, x
+            at += 1
+    d = rng.integers(0, 1 << 20, n).astype(np.int64)
+    rk, rv = oracle.window_reduce(s, d, v, 1, 0)
+    gk, gv = engine.reduce(*_dev(s, d, v), 1, 0)
+    gk, gv = gk.cpu().numpy(), gv.cpu().numpy()
+    assert np.array_equal(gk, rk)
+    for vid in special:
+        i = int(np.searchsorted(rk, vid))
+        assert rk[i] == vid
+        if rv[i] == 0:   # exact zeros: the same sign as the reference's sequential sum
+            assert gv[i] == 0 and np.signbit(gv[i]) == np.signbit(rv[i]), (vid, gv[i], rv[i])
+    # against the exact per-vertex sums (f64 over the values; the hub's 2^19 normal values cancel, so the
+    # reference's own sequential f32 fold drifts past 1e-5 of its small sum there -- the f32 config-size test
+    # bounds that drift)
+    idx = np.searchsorted(rk, s)
+    exact = np.bincount(idx, weights=v.astype(np.float64), minlength=len(rk))
+    mag = np.bincount(idx, weights=np.abs(v.astype(np.float64)), minlength=len(rk))
+    assert not (np.abs(gv.astype(np.float64) - exact) > 1e-6 * mag + 1e-300).any()
