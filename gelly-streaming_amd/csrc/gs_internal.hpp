@@ -78,7 +78,7 @@ struct gs_ctx {
   // fused last pass: partials with gaps, compacted partials
   gs::DevBuf part_k, part_a, comp_k, comp_a;
   // triangles
-  gs::DevBuf tri_loops, tri_tiles, tri_sfx, tri_nbr, tri_heavy, tri_range, tri_queue, tri_hwork, tri_lph;
+  gs::DevBuf tri_loops, tri_tiles, tri_sfx, tri_nbr, tri_heavy, tri_range, tri_queue, tri_hwork;
   gs::DevBuf tri_d[10];          // split-window triangles (gs_window_triangles_dist)
   gs::DevBuf cc[3];              // connected components (gs_components.hip)
   uint32_t tri_B = 0;            // split-window triangles: id geometry of the current window

@@ -889,15 +889,10 @@ gs_status tri_count(gs_ctx* c, uint32_t B, size_t V, uint64_t M, const uint32_t*
   GS_HIP(hipGetLastError());
   hipEventRecord(c->ev[4], c->stream);
   // 2. intersections: vertex-centric LDS hash sets (k_tri_light), long out-lists in k_tri_heavy
-  // A/B (GS_TH_LPHASED=1): the light chunks in phase order, as the heavy items.  Slower (R-MAT s24 light
-  // count 7.1 -> 36 ms, s26 42 -> 147 ms, profiles/r04/evidence/tri_*_lph.json): off
-  static const int lphased_env = getenv("GS_TH_LPHASED") ? atoi(getenv("GS_TH_LPHASED")) : 0;
-  const bool lphased = lphased_env != 0 && GS_TH_PHASED;
-  // A/B (GS_TH_LCLASS=0): the light kernel's own vertex pass (a wave per id) instead of k_tri_lclass
-  static const bool lclass = !getenv("GS_TH_LCLASS") || atoi(getenv("GS_TH_LCLASS")) != 0;
+  // (A/B of round 4, not kept: the light chunks in the heavy items' phase order, s24 light 7.1 -> 36 ms,
+  // s26 42 -> 147 ms, profiles/r04/evidence/tri_*_lph.json)
   GS_TRY(ensure(c, c->tri_heavy, (V + Ms / TH_VCH + 64) * 8));   // (v, in-chunk) items
-  // queued light chunks: the further chunks (<= Ms / TH_LCH), or, phased, every light chunk
-  GS_TRY(ensure(c, c->tri_queue, (std::min<uint64_t>(V, Ms) + Ms / TH_LCH + 64) * 8));
+  GS_TRY(ensure(c, c->tri_queue, (std::min<uint64_t>(V, Ms) + Ms / TH_LCH + 64) * 8));   // light chunks
   unsigned long long* d_total = (unsigned long long*)(sm + SM_NUNIQUE);
   uint32_t* d_nheavy = (uint32_t*)(sm + SM_COUNTERS) + 62;
   unsigned long long* d_probes = (unsigned long long*)(sm + SM_TRI_PROBES);
@@ -909,50 +904,13 @@ gs_status tri_count(gs_ctx* c, uint32_t B, size_t V, uint64_t M, const uint32_t*
   // LDS hash-set bucket cap: unlimited, or one bucket under GS_FLAG_TEST_TINY_TABLES (tests only)
   const uint32_t nb_cap = (c->flags & GS_FLAG_TEST_TINY_TABLES) ? 1u : 0xFFFFFFFFu;
   uint32_t* d_nqueue = d_nheavy + 1;
-  const unsigned nvb = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((V + TH_WPB - 1) / TH_WPB, 8192));
   uint2* queue = c->tri_queue.as<uint2>();
-  if (lphased) {
-    // every light chunk queued, ordered by the stretch of onbr its in-neighbours' lists lie in, counted
-    hipLaunchKernelGGL(k_tri_light, dim3(nvb), dim3(TH_BLOCK), 0, c->stream, nbr, sfx, out_range, in_range, (uint32_t)V,
-                       0u, 0xFFFFFFFFu, 2, queue, d_nqueue, c->tri_heavy.as<uint2>(), d_nheavy, d_total, d_probes, nb_cap,
-                       d_err, (const uint32_t*)nullptr);
-    GS_HIP(hipGetLastError());
-    c->host_small[6] = 0;
-    GS_HIP(hipMemcpyAsync(c->host_small + 6, d_nqueue, 4, hipMemcpyDeviceToHost, c->stream));
-    GS_TRY(host_wait(c));
-    const uint32_t nq = (uint32_t)c->host_small[6];
-    if (nq) {
-      GS_TRY(ensure(c, c->tri_lph, (size_t)nq * 4 + (TH_PHASES + 64) * 4));
-      uint32_t* hist = c->tri_lph.as<uint32_t>();
-      uint32_t* order = hist + TH_PHASES + 64;
-      GS_HIP(hipMemsetAsync(hist, 0, (TH_PHASES + 1) * 4, c->stream));
-      const unsigned g = (unsigned)std::min<uint64_t>((nq + 255) / 256, 4096);
-      hipLaunchKernelGGL(k_tri_hphase_count<TH_LCH>, dim3(g), dim3(256), 0, c->stream, sfx, in_range, queue, nq,
-                         (uint32_t)M, hist);
-      hipLaunchKernelGGL(k_tri_hphase_scan, dim3(1), dim3(256), 0, c->stream, hist);
-      hipLaunchKernelGGL(k_tri_hphase_place<TH_LCH>, dim3(g), dim3(256), 0, c->stream, sfx, in_range, queue, nq,
-                         (uint32_t)M, hist, order);
-      hipLaunchKernelGGL(k_tri_light, dim3(8192), dim3(TH_BLOCK), 0, c->stream, nbr, sfx, out_range, in_range,
-                         (uint32_t)V, 0u, 0xFFFFFFFFu, 3, queue, d_nqueue, c->tri_heavy.as<uint2>(), d_nheavy, d_total,
-                         d_probes, nb_cap, d_err, (const uint32_t*)order);
-      GS_HIP(hipGetLastError());
-    }
-  } else if (lclass) {   // the vertices with work queued by one lane per id, then the light chunks
-    hipLaunchKernelGGL(k_tri_lclass, dim3((unsigned)std::max<uint64_t>(1, std::min<uint64_t>((V + 255) / 256, 16384))),
-                       dim3(256), 0, c->stream, nbr, out_range, in_range, (uint32_t)V, 0u, 0xFFFFFFFFu, nb_cap, queue,
-                       d_nqueue, c->tri_heavy.as<uint2>(), d_nheavy);
-    hipLaunchKernelGGL(k_tri_light, dim3(8192u), dim3(TH_BLOCK), 0, c->stream, nbr, sfx, out_range, in_range,
-                       (uint32_t)V, 0u, 0xFFFFFFFFu, 1, queue, d_nqueue, c->tri_heavy.as<uint2>(), d_nheavy, d_total,
-                       d_probes, nb_cap, d_err, (const uint32_t*)nullptr);
-    GS_HIP(hipGetLastError());
-  } else {
-    for (int pass = 0; pass < 2; ++pass) {
-      hipLaunchKernelGGL(k_tri_light, dim3(pass == 0 ? nvb : 4096u), dim3(TH_BLOCK), 0, c->stream, nbr, sfx, out_range,
-                         in_range, (uint32_t)V, 0u, 0xFFFFFFFFu, pass, queue, d_nqueue, c->tri_heavy.as<uint2>(), d_nheavy,
-                         d_total, d_probes, nb_cap, d_err, (const uint32_t*)nullptr);
-      GS_HIP(hipGetLastError());
-    }
-  }
+  hipLaunchKernelGGL(k_tri_lclass, dim3((unsigned)std::max<uint64_t>(1, std::min<uint64_t>((V + 255) / 256, 16384))),
+                     dim3(256), 0, c->stream, nbr, out_range, in_range, (uint32_t)V, 0u, 0xFFFFFFFFu, nb_cap, queue,
+                     d_nqueue, c->tri_heavy.as<uint2>(), d_nheavy);
+  hipLaunchKernelGGL(k_tri_light, dim3(8192u), dim3(TH_BLOCK), 0, c->stream, nbr, sfx, out_range, in_range, queue,
+                     d_nqueue, d_total, d_probes, nb_cap, d_err);
+  GS_HIP(hipGetLastError());
   hipEventRecord(c->ev[5], c->stream);
   // heavy items: work per item, exclusive scan, then equal-work runs per block
   c->host_small[6] = 0;

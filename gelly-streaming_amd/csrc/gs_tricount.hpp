@@ -303,70 +303,32 @@ __device__ __forceinline__ uint32_t th_wave_chunk(const uint32_t* __restrict__ o
                                 [&](const uint32_t (&x)[TH_ILP], uint32_t nv) { return th_probe(hb, bmask, x, nv, err); });
 }
 
-// pass 0: vertices, interleaved; first in-chunk here, further chunks queued, long out-lists to the
-//   heavy list.  pass 1: the queued (v, chunk) items.  n_probes counts the hash probes (bench bytes).
+// The light chunks k_tri_lclass queued, (v, in-chunk of TH_LCH), a wave each: N+(v) into the wave's LDS
+// hash set, then the chunk's in-entries (th_wave_chunk).  Interleaved over the queue (no claim counter);
+// n_probes counts the hash probes (bench bytes).
 // 24 KiB of LDS per block -> six blocks (24 waves) per CU: registers capped to match (80 VGPRs)
 __global__ __launch_bounds__(TH_BLOCK) __attribute__((amdgpu_waves_per_eu(GS_TH_LWAVES, GS_TH_LWAVES))) void k_tri_light(const uint32_t* __restrict__ onbr,
                                                         const uint2* __restrict__ sfx,
                                                         const uint2* __restrict__ out_range,
-                                                        const uint2* __restrict__ in_range, uint32_t nv, uint32_t q0,
-                                                        uint32_t q1, int pass, uint2* __restrict__ queue,
-                                                        uint32_t* __restrict__ n_queue, uint2* __restrict__ heavy,
-                                                        uint32_t* __restrict__ n_heavy,
+                                                        const uint2* __restrict__ in_range,
+                                                        const uint2* __restrict__ queue,
+                                                        const uint32_t* __restrict__ n_queue,
                                                         unsigned long long* __restrict__ total,
                                                         unsigned long long* __restrict__ n_probes, uint32_t nb_cap,
-                                                        uint32_t* __restrict__ err,
-                                                        const uint32_t* __restrict__ order) {
+                                                        uint32_t* __restrict__ err) {
   // 6 KiB per wave (4 KiB table + 2 KiB list prefix), 24 KiB per block
-  // pass 0: vertices in rank order (first in-chunk here, further chunks queued for pass 1); pass 2: every
-  // light chunk queued (nothing counted); pass 3: the queued chunks in `order` (k_tri_hphase_*: by the
-  // stretch of onbr their in-neighbours' out-lists lie in, so the chunks in flight gather from a few
-  // stretches that L2 and the Infinity Cache keep, as k_tri_heavy's items)
   __shared__ uint4 s_hash[TH_WPB][TH_H / 4];
   __shared__ uint32_t s_off[TH_WPB][TH_LCH];   // exclusive prefix of |N+(u)| over the non-empty u
   __shared__ uint32_t s_st[TH_WPB][TH_LCH];    // start of that N+(u) in onbr
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const uint32_t nw = gridDim.x * TH_WPB;
   uint64_t cnt = 0, probes = 0;
-  const uint32_t n_items = (pass == 0 || pass == 2) ? nv : *n_queue;
-  for (uint32_t it = blockIdx.x * TH_WPB + w; it < n_items; it += nw) {   // interleaved: no claim counter
-    uint32_t v, c0, c1;
-    if (pass == 0 || pass == 2) {
-      v = it;
-      const uint2 ro = out_range[v], ri = in_range[v];
-      if (ro.y == ro.x || ri.y == ri.x || ro.x < q0 || ro.x >= q1) continue;
-      const uint32_t dv = ro.y - ro.x;
-      // heavy: too long for a wave's table, or long enough to gain from the heavy kernel's bitmap
-      // (k_tri_heavy: span of N+(v) within its table's bits; history: the split at 256 alone, s26 455 ms,
-      // at 512 alone s24 72 -> 78 ms)
-      const bool heavy_v = dv > TH_DMAX ||
-                           (TH_BITMAP && nb_cap > 1 && dv > TH_HMIN && onbr[ro.y - 1] - v <= TH_BSPAN);
-      if (heavy_v) {   // one heavy item per TH_VCH in-neighbours: a hub spreads over blocks
-        const uint32_t nhc = (ri.y - ri.x + TH_VCH - 1) / TH_VCH;
-        uint32_t at = 0;
-        if (lane == 0) at = atomicAdd(n_heavy, nhc);
-        at = __shfl(at, 0, WAVE);
-        for (uint32_t j = lane; j < nhc; j += WAVE) heavy[at + j] = make_uint2(v, j);
-        continue;
-      }
-      const uint32_t nch = (ri.y - ri.x + TH_LCH - 1) / TH_LCH;
-      const uint32_t first = pass == 2 ? 0u : 1u;   // pass 2 queues chunk 0 too
-      if (nch > first) {
-        uint32_t at = 0;
-        if (lane == 0) at = atomicAdd(n_queue, nch - first);
-        at = __shfl(at, 0, WAVE);
-        for (uint32_t j = lane; j < nch - first; j += WAVE) queue[at + j] = make_uint2(v, j + first);
-      }
-      if (pass == 2) continue;
-      c0 = ri.x;
-      c1 = min(ri.y, ri.x + TH_LCH);
-    } else {
-      const uint2 q = queue[pass == 3 ? order[it] : it];
-      v = q.x;
-      const uint2 ri = in_range[v];
-      c0 = ri.x + q.y * TH_LCH;
-      c1 = min(ri.y, c0 + TH_LCH);
-    }
+  const uint32_t n_items = *n_queue;
+  for (uint32_t it = blockIdx.x * TH_WPB + w; it < n_items; it += nw) {
+    const uint2 q = queue[it];
+    const uint32_t v = q.x;
+    const uint2 ri = in_range[v];
+    const uint32_t c0 = ri.x + q.y * TH_LCH, c1 = min(ri.y, c0 + TH_LCH);
     cnt += th_wave_chunk(onbr, sfx, v, out_range[v], c0, c1, lane, s_hash[w], s_off[w], s_st[w], probes,
                          nb_cap, err);
   }
@@ -376,11 +338,13 @@ __global__ __launch_bounds__(TH_BLOCK) __attribute__((amdgpu_waves_per_eu(GS_TH_
   if (lane == 0 && probes) atomicAdd(n_probes, (unsigned long long)probes);   // wave-uniform
 }
 
-// The light kernel's vertex pass as its own launch, one lane per vertex: every vertex with in- and
-// out-entries whose out-list starts in [q0, q1) becomes heavy items (its in-chunks of TH_VCH) or light
-// queue entries (its in-chunks of TH_LCH, the first included), and k_tri_light runs over the queue only.
-// (A wave per id in rank order paid a dependent load per id -- 2^26 of them at s26, most without work.)
-// The heavy rule is k_tri_light pass 0's.  Appends are wave-aggregated (one atomic per wave and list).
+// The count's vertex pass, one lane per vertex: every vertex with in- and out-entries whose out-list
+// starts in [q0, q1) becomes heavy items (its in-chunks of TH_VCH) or light queue entries (its in-chunks
+// of TH_LCH).  Heavy: too long for a wave's table, or long enough to gain from the heavy kernel's bitmap
+// (the span of N+(v) within its table's bits; history: the split at 256 alone, s26 455 ms, at 512 alone
+// s24 72 -> 78 ms).  (Round 4: this pass ran inside k_tri_light, a wave per id in rank order, a dependent
+// load per id, 2^26 ids at s26, most without work: light count 41.9 -> 39.0 ms.)  Appends are
+// wave-aggregated (one atomic per wave and list).
 __global__ __launch_bounds__(256) void k_tri_lclass(const uint32_t* __restrict__ onbr, const uint2* __restrict__ out_range,
                                                     const uint2* __restrict__ in_range, uint32_t nv, uint32_t q0,
                                                     uint32_t q1, uint32_t nb_cap, uint2* __restrict__ queue,
@@ -446,7 +410,7 @@ __global__ __launch_bounds__(256) void k_tri_hwork(const uint2* __restrict__ sfx
 #define GS_TH_PHASES 16384   // s26 heavy count (ms): 256 phases 149, 1024 146.5, 4096 143.3, 16384 142.0, 65536 141.2
 #endif
 constexpr uint32_t TH_PHASES = GS_TH_PHASES;
-// (CH: in-entries per item -- TH_VCH for the heavy items, TH_LCH for the light ones)
+// (CH: in-entries per item, TH_VCH)
 template <uint32_t CH>
 __device__ __forceinline__ uint32_t th_phase(const uint2* __restrict__ sfx, const uint2* __restrict__ in_range, uint2 item,
                                              uint32_t M) {

@@ -4,8 +4,7 @@ The key step has a one-pass form (k_tri_okeys: the whole rank table) and a two-p
 tables past the Infinity Cache (k_tri_okeys_lo / _hi, chosen when V > 2^25), each with U = 1, 2 or 4
 edges per lane per step.  The default picks one combination per window size; GS_TRI_OKEYS_SPLIT and
 GS_TRI_OKEYS_UNROLL force the others (read once per process, so every case runs in its own
-interpreter).  GS_TH_LCLASS=0 takes the light kernel's own vertex pass instead of k_tri_lclass.  Every
-combination must give the forward algorithm's count (WindowTriangles.java:83-140
+interpreter).  Every combination must give the forward algorithm's count (WindowTriangles.java:83-140
 restated in oracle/gs_oracle.c) on a self-loop-free R-MAT scale-18 window.
 """
 import subprocess
@@ -22,7 +21,7 @@ ROOT = Path(__file__).resolve().parent.parent
 SCRIPT = textwrap.dedent("""
     import os
     import sys
-    os.environ.update(GS_TRI_OKEYS_SPLIT="{split}", GS_TRI_OKEYS_UNROLL="{unroll}", GS_TH_LCLASS="{lclass}")
+    os.environ.update(GS_TRI_OKEYS_SPLIT="{split}", GS_TRI_OKEYS_UNROLL="{unroll}")
     import numpy as np
     sys.path.insert(0, {root!r})
     import __graft_entry__ as ge
@@ -37,11 +36,11 @@ SCRIPT = textwrap.dedent("""
 """)
 
 
-@pytest.mark.parametrize("split,unroll,lclass", [(0, 1, 1), (0, 2, 1), (1, 1, 1), (1, 2, 1), (1, 4, 1), (0, 4, 0)])
-def test_okeys_variants_same_count(split, unroll, lclass):
+@pytest.mark.parametrize("split,unroll", [(0, 1), (0, 2), (1, 1), (1, 2), (1, 4)])
+def test_okeys_variants_same_count(split, unroll):
     # (the knobs are set inside the child, before the library reads them: the child inherits this
     # process's environment unchanged)
-    r = subprocess.run([sys.executable, "-c", SCRIPT.format(root=str(ROOT), split=split, unroll=unroll, lclass=lclass)],
+    r = subprocess.run([sys.executable, "-c", SCRIPT.format(root=str(ROOT), split=split, unroll=unroll)],
                        capture_output=True, text=True, timeout=170)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "triangles" in r.stdout
