@@ -136,7 +136,14 @@ struct BkVal {
     A acc[W];
     uint32_t pm[PW];
   };
+  // Float SUM (f32 / f64 values, f64 accumulators) starts from -0.0, the additive identity of IEEE
+  // arithmetic: x + -0.0 is x for every x, so a vertex whose values are all -0.0 sums to -0.0 as the
+  // reference's reduce (which starts from the first value) does -- from +0.0 it summed to +0.0.  A sum that
+  // cancels ends at +0.0, so an accumulator that still holds -0.0's bits has seen no record or only -0.0
+  // values, which mark presence themselves: the presence byte is written for those records only.
+  static constexpr bool FLOAT_SUM = OP == OP_SUM && std::is_floating_point_v<T>;
   __device__ static A identity() {
+    if constexpr (FLOAT_SUM) return -0.0;
     if constexpr (OP == OP_SUM) return A(0);
     else if constexpr (OP == OP_MIN) return std::numeric_limits<A>::max();
     else return std::numeric_limits<A>::lowest();
@@ -160,6 +167,8 @@ struct BkVal {
         atomicAdd((U*)&s.acc[i], (U)v);
       } else {
         atomicAdd(&s.acc[i], (double)v);
+        if (__double_as_longlong((double)v) == (long long)0x8000000000000000ull) mark(s, i);   // -0.0
+        return;
       }
     } else if constexpr (OP == OP_MIN) {
       using I = std::conditional_t<sizeof(T) == 8, long long, int>;
@@ -213,6 +222,7 @@ struct BkVal {
   __device__ static bool present(const Lds& s, uint32_t i) {
     const bool m = PB ? reinterpret_cast<const uint8_t*>(s.pm)[i] != 0 : ((s.pm[i >> 5] >> (i & 31)) & 1u) != 0;
     if constexpr (INFER_PRESENCE) return m || s.acc[i] != identity();
+    else if constexpr (FLOAT_SUM) return m || __double_as_longlong(s.acc[i]) != (long long)0x8000000000000000ull;
     else return m;
   }
   __device__ static void stage(BkStage st, uint32_t pos, const Lds& s, uint32_t i) { ((A*)st.a)[pos] = s.acc[i]; }

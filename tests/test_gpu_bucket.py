@@ -432,10 +432,12 @@ def test_timing_levels_same_results(pkg, oracle):
 
 @pytest.mark.parametrize("dtype", [np.float64, np.float32])
 def test_float_sum_presence_with_signed_zeros(engine, oracle, dtype):
-    """Float SUM infers a vertex's presence from its accumulator (it starts at -0.0; a sum that cancels
-    ends at +0.0) and marks presence only for -0.0 values (gs_bucket.hpp BkVal::FLOAT_SUM).  Vertices whose
-    records are all +0.0, all -0.0, cancel exactly, or mix -0.0 with others must all be present, with the
-    reference's signed zeros, including across the slabs of a multi-item hub bucket."""
+    """Float SUM starts its accumulators at -0.0 (gs_bucket.hpp BkVal::FLOAT_SUM): a vertex whose values
+    are all -0.0 sums to -0.0 as the reference's reduce does (it starts from the first value; from a +0.0
+    start the bucket path returned +0.0 -- this test found it), a sum that cancels ends at +0.0, and
+    presence is inferred from the accumulator except for -0.0 values.  Vertices whose records are all +0.0,
+    all -0.0, cancel exactly, or mix -0.0 with others must all be present with the reference's signed
+    zeros, including across the slabs of a multi-item hub bucket."""
     rng = np.random.default_rng(2024)
     n = 1 << 20
     hub = 5000
