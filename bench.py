@@ -35,8 +35,8 @@ METRIC = "edges/sec per tumbling slice (reduceOnEdges, window triangles) at 1/2/
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=10)
-    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--steps", type=int, default=30)
+    p.add_argument("--warmup", type=int, default=10)
     p.add_argument("--scale", type=int, default=24)
     p.add_argument("--edge-factor", type=int, default=16)
     p.add_argument("--seed", type=lambda x: int(x, 0), default=0x5EED02)
