@@ -281,15 +281,27 @@ __global__ __launch_bounds__(256) void k_cand_emit(const uint64_t* __restrict__ 
     lo = nlo;
   }
   uint32_t sc = lo;
+  // the current slot's block start / end and metadata, reloaded only when the step moves to another slot
+  // (a fast step then issues no load before its id gathers; re-reading them every step put two dependent
+  // loads in front of each step's stores)
+  uint32_t cs = 0xFFFFFFFFu;
+  uint64_t c_beg = 0, c_end = 0;
+  CandMeta cm{};
   for (uint64_t base = w0; base < w1; base += 256) {
     // Fast path: the step lies inside one slot's pair rows (most records of a window: the blocks of its
     // high-degree vertices are O(k^2)).  The slot's metadata is wave-uniform (scalar loads), the row of
     // the step's first position is found once, and each lane walks forward from it (a 256-position span
     // crosses at most ~23 rows: only a block's last rows are shorter than 12).
     const uint64_t e1 = min(w1, base + 256);
-    if (vs[sc + 1] >= e1) {
-      const CandMeta m = meta[sc];
-      const uint64_t t0 = base - vs[sc];
+    if (cs != sc) {
+      cs = sc;
+      c_beg = vs[sc];
+      c_end = vs[sc + 1];
+      cm = meta[sc];
+    }
+    if (c_end >= e1) {
+      const CandMeta m = cm;
+      const uint64_t t0 = base - c_beg;
       if (t0 >= m.d && m.rows) {
         const uint64_t k = m.k, rows = m.rows, q0 = t0 - m.d;
         const double k2 = 2.0 * (double)k + 1.0;
