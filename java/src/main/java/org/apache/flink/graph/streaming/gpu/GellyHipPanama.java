@@ -65,6 +65,7 @@ public final class GellyHipPanama implements AutoCloseable {
 			FunctionDescriptor.of(JAVA_INT, ADDRESS, ADDRESS, ADDRESS, ADDRESS));
 	private static final MethodHandle FETCH_LAST_OUTPUT = fn("gs_fetch_last_output",
 			FunctionDescriptor.of(JAVA_INT, ADDRESS, ADDRESS));
+	private static final MethodHandle SET_TIMING = fn("gs_set_timing", FunctionDescriptor.of(JAVA_INT, ADDRESS, JAVA_INT));
 
 	private final Arena arena = Arena.ofConfined();
 	private final MemorySegment ctx;
@@ -77,6 +78,8 @@ public final class GellyHipPanama implements AutoCloseable {
 		final int st = (int) CREATE.invokeExact(cfg, out);
 		if (st != GellyHip.GS_OK) throw new RuntimeException("gs_create: status " + st + " (a HIP device is required)");
 		ctx = out.get(ADDRESS, 0);
+		// no stage events inside operator windows (each hipEventRecord costs the stream a few microseconds)
+		check((int) SET_TIMING.invokeExact(ctx, GellyHip.GS_TIMING_OFF), "gs_set_timing");
 	}
 
 	@Override
