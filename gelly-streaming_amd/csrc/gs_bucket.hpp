@@ -37,9 +37,8 @@ constexpr int BK_INFO_BLOCK = 512;
 #ifndef GS_ACC_ABL_NOATOM
 #define GS_ACC_ABL_NOATOM 0
 #endif
-#ifndef GS_BK_PIPE
-#define GS_BK_PIPE 0   // k_bk_accum (packed records), A/B: next group's loads in flight during this group's atomics (C2 accumulate 0.345 vs 0.331 ms: off)
-#endif
+// (k_bk_accum, packed records, A/B of round 3: the next group's loads in flight during this group's
+// atomics, C2 accumulate 0.345 vs 0.331 ms: removed)
 constexpr int BK_ACC_BLOCK = 1024;     // 16 waves: one workgroup per CU (LDS-bound)
 constexpr int BK_NW = BK_ACC_BLOCK / WAVE;
 constexpr int BK_PLAN_BLOCK = 1024;
@@ -1649,6 +1648,7 @@ __global__ __launch_bounds__(BK_ACC_BLOCK) void k_bk_accum(Src src, const BkItem
   __shared__ typename P::Lds s;
   __shared__ uint32_t s_item;
   __shared__ uint32_t s_wc[BK_NW];
+  __shared__ uint32_t s_pre4[SP_NSEG + 1], s_qb[SP_NSEG];   // packed records: the item's pieces as one stream
   using Raw = typename P::Raw;
   const int tid = threadIdx.x;
   if (mm[2]) return;   // keys outside the predicted range: the window is rerun
@@ -1662,104 +1662,119 @@ __global__ __launch_bounds__(BK_ACC_BLOCK) void k_bk_accum(Src src, const BkItem
     const uint32_t b0 = bucket_start[m.bucket];
     P::init(s, tid);
     __syncthreads();
-    auto range = [&](uint32_t r0, uint32_t r1) {   // records [r0, r1) of the partition into LDS
     if constexpr (is_pack_src<Src>::value) {
-      // 16-byte loads (4 records per lane per load: 4x the bytes in flight of 4-byte loads; the
-      // 4-byte version was latency-bound); an unaligned head and the tail record by record
+      // packed records: 16-byte loads (4 records per lane per load: 4x the bytes in flight of 4-byte
+      // loads; the 4-byte version was latency-bound); unaligned heads and tails record by record
       auto add1 = [&](uint32_t q, uint32_t x) {
         const uint32_t v16 = x >> 16;
         const bool esc = v16 == PK_ESC;
         if constexpr (has_add_packed<P>::value) P::add_packed(s, x & (P::W - 1), !esc ? (Raw)v16 : (Raw)src.wide[q], esc);
         else P::add(s, x & (P::W - 1), !esc ? (Raw)v16 : (Raw)src.wide[q]);
       };
-      const uint32_t a0 = min(r1, (r0 + 3) & ~3u), a1 = max(a0, r1 & ~3u);
-      if (r0 + tid < a0) add1(r0 + tid, src.rec[r0 + tid]);
       const uint4* rec4 = reinterpret_cast<const uint4*>(src.rec);
       constexpr int U4 = UNROLL / 2 > 0 ? UNROLL / 2 : 1;
       constexpr uint32_t STEP = BK_ACC_BLOCK * U4;
-      const uint32_t q_end = a1 / 4;
-      auto load4 = [&](uint4 (&x)[U4], uint32_t q4) {   // unconditional, clamped: see k_dp_hist
+      // n4 groups of 4 records, group g at uint4 index q4_of(g) of the partition
+      auto stream = [&](uint32_t n4, auto q4_of) {
+        for (uint32_t g4 = tid; g4 < n4; g4 += STEP) {
+          uint4 x[U4];
+          uint32_t qi[U4];
 #pragma unroll
-        for (int u = 0; u < U4; ++u) {
-          const uint32_t qq = q4 + (uint32_t)u * BK_ACC_BLOCK;
+          for (int u = 0; u < U4; ++u) {   // unconditional, clamped: see k_dp_hist
+            const uint32_t g = g4 + (uint32_t)u * BK_ACC_BLOCK;
+            qi[u] = q4_of(g < n4 ? g : n4 - 1);
 #if GS_ACC_ABL_NOLOAD   // timing-only ablation: synthetic narrow records, no partition reads (wrong output)
-          const uint32_t h = (qq * 2654435761u) >> 8;
-          x[u] = make_uint4((h & 0x3FFF) | 0x10000u, ((h >> 3) & 0x3FFF) | 0x20000u, ((h >> 6) & 0x3FFF) | 0x30000u,
-                            ((h >> 9) & 0x3FFF) | 0x40000u);
+            const uint32_t h = (qi[u] * 2654435761u) >> 8;
+            x[u] = make_uint4((h & 0x3FFF) | 0x10000u, ((h >> 3) & 0x3FFF) | 0x20000u, ((h >> 6) & 0x3FFF) | 0x30000u,
+                              ((h >> 9) & 0x3FFF) | 0x40000u);
 #else
-          x[u] = rec4[qq < q_end ? qq : q_end - 1];
+            x[u] = rec4[qi[u]];
 #endif
-        }
-      };
-      auto add4 = [&](const uint4 (&x)[U4], uint32_t q4) {
+          }
 #pragma unroll
-        for (int u = 0; u < U4; ++u) {
-          const uint32_t qq = q4 + (uint32_t)u * BK_ACC_BLOCK;
-          if constexpr (fast_packed<P>::value) {
-            // one branch per 4 records: the common case (narrow values, for SUM non-zero) is 4 LDS atomics
-            // and nothing else; escapes and zero SUM values (presence bytes, the wide value) take add1.
-            // (A branch per record cost ~4 scalar instructions each: the accumulate ran 7x more SALU than
-            // LDS instructions.)
-            const uint32_t h0 = x[u].x >> 16, h1 = x[u].y >> 16, h2 = x[u].z >> 16, h3 = x[u].w >> 16;
-            bool rare = (h0 == PK_ESC) | (h1 == PK_ESC) | (h2 == PK_ESC) | (h3 == PK_ESC);
-            if constexpr (P::OP_IS_SUM) rare |= (h0 == 0u) | (h1 == 0u) | (h2 == 0u) | (h3 == 0u);
-            if (qq < q_end) {
+          for (int u = 0; u < U4; ++u) {
+            if (g4 + (uint32_t)u * BK_ACC_BLOCK >= n4) continue;
+            const uint32_t q = 4 * qi[u];
+            if constexpr (fast_packed<P>::value) {
+              // one branch per 4 records: the common case (narrow values, for SUM non-zero) is 4 LDS atomics
+              // and nothing else; escapes and zero SUM values (presence bytes, the wide value) take add1.
+              // (A branch per record cost ~4 scalar instructions each: the accumulate ran 7x more SALU than
+              // LDS instructions.)
+              const uint32_t h0 = x[u].x >> 16, h1 = x[u].y >> 16, h2 = x[u].z >> 16, h3 = x[u].w >> 16;
+              bool rare = (h0 == PK_ESC) | (h1 == PK_ESC) | (h2 == PK_ESC) | (h3 == PK_ESC);
+              if constexpr (P::OP_IS_SUM) rare |= (h0 == 0u) | (h1 == 0u) | (h2 == 0u) | (h3 == 0u);
 #if GS_ACC_ABL_NOATOM   // timing-only ablation: no LDS atomics (wrong output)
               if (!rare) {
                 if ((h0 ^ h1 ^ h2 ^ h3 ^ x[u].x ^ x[u].y ^ x[u].z ^ x[u].w) == 0x9E3779B9u) P::add_narrow(s, 0, h0);
-              } else
+                continue;
+              }
 #else
               if (!rare) {
-#endif
-#if !GS_ACC_ABL_NOATOM
                 P::add_narrow(s, x[u].x & (P::W - 1), h0);
                 P::add_narrow(s, x[u].y & (P::W - 1), h1);
                 P::add_narrow(s, x[u].z & (P::W - 1), h2);
                 P::add_narrow(s, x[u].w & (P::W - 1), h3);
-              } else
-#endif
-              {
-                add1(4 * qq, x[u].x);
-                add1(4 * qq + 1, x[u].y);
-                add1(4 * qq + 2, x[u].z);
-                add1(4 * qq + 3, x[u].w);
+                continue;
               }
+#endif
             }
-          } else if (qq < q_end) {
-            add1(4 * qq, x[u].x);
-            add1(4 * qq + 1, x[u].y);
-            add1(4 * qq + 2, x[u].z);
-            add1(4 * qq + 3, x[u].w);
+            add1(q, x[u].x);
+            add1(q + 1, x[u].y);
+            add1(q + 2, x[u].z);
+            add1(q + 3, x[u].w);
           }
         }
       };
-#if GS_BK_PIPE
-      // software-pipelined: the next group's 16-byte loads are in flight while this group's records go
-      // into LDS (one group at a time left the loads and the LDS atomics each about half busy)
-      uint32_t q4 = a0 / 4 + tid;
-      if (a0 / 4 < q_end) {
-        uint4 x[U4], y[U4];
-        load4(x, q4);
-        for (;;) {   // (the loads are unconditional: a conditional load makes hipcc wait vmcnt(0) after it)
-          load4(y, q4 + STEP);
-          add4(x, q4);
-          q4 += STEP;
-          if (q4 >= q_end) break;
-          load4(x, q4 + STEP);
-          add4(y, q4);
-          q4 += STEP;
-          if (q4 >= q_end) break;
+      if (!seg_cur) {   // records [r0, r1) of the partition
+        const uint32_t r0 = b0 + m.begin, r1 = b0 + m.end;
+        const uint32_t a0 = min(r1, (r0 + 3) & ~3u), a1 = max(a0, r1 & ~3u);
+        if (r0 + tid < a0) add1(r0 + tid, src.rec[r0 + tid]);
+        if (a1 + tid < r1) add1(a1 + tid, src.rec[a1 + tid]);
+        stream((a1 - a0) / 4, [&](uint32_t g) { return a0 / 4 + g; });
+      } else {
+        // speculative partition: the item's pieces of the bucket's SP_NSEG segments, in segment order,
+        // as ONE stream of 16-byte groups (a loop per segment drained and refilled the loads in flight
+        // at each of the item's segment boundaries).  Wave 0: lane x < SP_NSEG takes segment x's piece
+        // [p0, p1), its head and tail record by record, and publishes its groups' place in the stream.
+        if (tid < WAVE) {
+          const bool on = tid < (int)SP_NSEG;
+          const uint32_t x = on ? (uint32_t)tid : 0u;
+          const uint32_t sg = sp_lo(seg_cur, x, m.bucket);
+          const uint32_t nx = on ? min(seg_cur[x * BK_MAXB + m.bucket], sp_hi(seg_cur, x, m.bucket)) - sg : 0u;
+          const uint32_t at = wave_inclusive_sum(nx) - nx;   // records of the bucket in the segments before x
+          const uint32_t lo = max(m.begin, at), hi = min(m.end, at + nx);
+          uint32_t p0 = 0, p1 = 0;
+          if (on && lo < hi) {
+            p0 = sg + (lo - at);
+            p1 = sg + (hi - at);
+          }
+          const uint32_t a0 = min(p1, (p0 + 3) & ~3u), a1 = max(a0, p1 & ~3u);
+          const uint32_t n4 = (a1 - a0) / 4;
+          const uint32_t e4 = wave_inclusive_sum(n4);
+          if (on) {
+            s_pre4[x + 1] = e4;
+            s_qb[x] = a0 / 4 - (e4 - n4);   // group g of piece x: uint4 index g + s_qb[x]
+          }
+          if (tid == 0) s_pre4[0] = 0;
+          for (uint32_t q = p0; q < a0; ++q) add1(q, src.rec[q]);
+          for (uint32_t q = a1; q < p1; ++q) add1(q, src.rec[q]);
         }
+        __syncthreads();
+        // each lane's groups come in increasing g: a cursor over the pieces (a piece is ~2^13 groups,
+        // one step of the stream 2^12, so the cursor rarely moves)
+        uint32_t cx = 0, cnext = s_pre4[1], cbase = s_qb[0];
+        stream(s_pre4[SP_NSEG], [&](uint32_t g) {
+          while (g >= cnext) {   // g < s_pre4[SP_NSEG]: cx stays < SP_NSEG
+            ++cx;
+            cnext = s_pre4[cx + 1];
+            cbase = s_qb[cx];
+          }
+          return g + cbase;
+        });
       }
-#else
-      for (uint32_t q4 = a0 / 4 + tid; q4 < q_end; q4 += STEP) {
-        uint4 x[U4];
-        load4(x, q4);
-        add4(x, q4);
-      }
-#endif
-      if (a1 + tid < r1) add1(a1 + tid, src.rec[a1 + tid]);
-    } else if constexpr (is_part_src<Src>::value) {
+    } else {
+    auto range = [&](uint32_t r0, uint32_t r1) {   // records [r0, r1) of the partition into LDS
+    if constexpr (is_part_src<Src>::value) {
       // unpacked partition (2-byte keys + the payload, k_dp_scatter / k_sp_scatter): 4 consecutive records
       // per lane and step -- one 8-byte load of their keys, one (4-byte values) or two (8-byte values)
       // 16-byte loads of their values; an unaligned head and the tail record by record.  (A 2-byte key
@@ -1842,6 +1857,7 @@ __global__ __launch_bounds__(BK_ACC_BLOCK) void k_bk_accum(Src src, const BkItem
         if (lo < hi) range(sg + (lo - at), sg + (hi - at));
         at += nx;
       }
+    }
     }
     __syncthreads();
     if (m.slab == ~0u) {
