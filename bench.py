@@ -95,17 +95,19 @@ def algorithmic_bytes(workload, E, U, vb=8):
     return (8 + vb) * E + (8 + vb) * U
 
 
-def kernel_table(times_list, E, U_avg, stage_list=None):
+def kernel_table(times_list, E, U_avg, stage_list=None, nbr_payload=False):
     """Average per-launch durations (device events inside the library, same stream) and each kernel's
     own algorithmic bytes.  times_list: the timed windows (GS_TIMING_DOMINANT: the direct
-    path's scatter and accumulate only); stage_list: windows after them with every stage event."""
+    path's scatter and accumulate only); stage_list: windows after them with every stage event.
+    nbr_payload: the records' payload is the neighbour id (the degree / max-neighbour fold), read from
+    the int64 neighbour column and stored in payload_bytes."""
     t0 = times_list[0]
     if t0.path == 2:
-        return direct_kernel_table(times_list, E, U_avg, stage_list or times_list)
+        return direct_kernel_table(times_list, E, U_avg, stage_list or times_list, nbr_payload)
     times_list = stage_list or times_list   # other paths: every stage from the stage-timed windows
     t0 = times_list[0]
     if t0.path == 1:
-        return bucket_kernel_table(times_list, E, U_avg)
+        return bucket_kernel_table(times_list, E, U_avg, nbr_payload)
     kb, vb = t0.key_bytes, t0.payload_bytes
     ab = 8                      # partial accumulator of a Long sum
     passes = t0.sort_passes
@@ -129,7 +131,7 @@ def kernel_table(times_list, E, U_avg, stage_list=None):
     return rows, P
 
 
-def bucket_kernel_table(times_list, E, U_avg):
+def bucket_kernel_table(times_list, E, U_avg, nbr_payload=False):
     """Bucket path (gs_bucket.hpp): bk_info, 1-2 partition passes over the bucket index, LDS accumulate,
     merge of multi-item buckets, emit.  Algorithmic bytes per launch as in DESIGN.md."""
     t0 = times_list[0]
@@ -139,10 +141,10 @@ def bucket_kernel_table(times_list, E, U_avg):
     mean = lambda f: statistics.mean(f(t) for t in times_list)
     rows = {}
     for p in range(passes):
-        rd = (8 + vb) if p == 0 else (4 + vb)
+        rd = (8 + (8 if nbr_payload else vb)) if p == 0 else (4 + vb)
         wr = (2 if p == passes - 1 else 4) + vb
         rows[f"bucket_partition{p}"] = {"ms": mean(lambda t: t.pass_ms[p]), "bytes": E * (rd + wr)}
-    rd = (2 + vb) if passes else (8 + vb)
+    rd = (2 + vb) if passes else (8 + (8 if nbr_payload else vb))
     rows["bucket_accumulate"] = {"ms": mean(lambda t: t.pass_ms[passes]), "bytes": E * rd + U_avg * (4 + ab)}
     rows["bucket_merge"] = {"ms": mean(lambda t: t.pass_ms[passes + 1]), "bytes": 0}
     rows["bucket_emit"] = {"ms": mean(lambda t: t.pass_ms[passes + 2]), "bytes": U_avg * (4 + ab + 16)}
@@ -150,13 +152,13 @@ def bucket_kernel_table(times_list, E, U_avg):
     return rows, mean(lambda t: t.partials)
 
 
-def direct_kernel_table(times_list, E, U_avg, stage_list):
+def direct_kernel_table(times_list, E, U_avg, stage_list, nbr_payload=False):
     """Direct bucket path (gs_bucket.hpp k_dp_*): per-tile histogram, offset scans, ONE scatter, LDS
     accumulate, merge, emit.  Each kernel's own bytes (E = records): the packed scatter
     writes 4-byte records (2-byte key + 2-byte value), the plain one a 2-byte key + the payload."""
     t0 = times_list[0]
     vb = t0.payload_bytes        # packed: 2
-    lb = 8 if t0.packed else vb  # loaded value bytes
+    lb = 8 if (t0.packed or nbr_payload) else vb  # loaded value bytes (the int64 neighbour column for a fold)
     ab = 8 if (vb or t0.packed) else 4   # staged accumulator (i64 sum / u32 count)
     mean = lambda f: statistics.mean(f(t) for t in times_list)
     smean = lambda f: statistics.mean(f(t) for t in stage_list)   # the stages the timed windows did not time
@@ -861,7 +863,7 @@ def main():
         partials = 0
         B = 16 * E + 16 * U_cc
     else:
-        kt, partials = kernel_table(times, E_rec, U_avg, stage_times_after)
+        kt, partials = kernel_table(times, E_rec, U_avg, stage_times_after, nbr_payload=a.workload == "fold")
         B = algorithmic_bytes(a.workload, E, U_avg, 8)
     finish_rows(kt, B)
     dom_name = max((n for n in kt if n not in ("tri_count_light", "tri_count_heavy")), key=lambda n: kt[n]["ms"])
