@@ -31,12 +31,6 @@ namespace gs {
 
 constexpr int BK_MAXB = 2048;          // buckets (the bucket index has <= 11 bits)
 constexpr int BK_INFO_BLOCK = 512;
-#ifndef GS_ACC_ABL_NOLOAD
-#define GS_ACC_ABL_NOLOAD 0
-#endif
-#ifndef GS_ACC_ABL_NOATOM
-#define GS_ACC_ABL_NOATOM 0
-#endif
 // (k_bk_accum, packed records, A/B of round 3: the next group's loads in flight during this group's
 // atomics, C2 accumulate 0.345 vs 0.331 ms: removed)
 constexpr int BK_ACC_BLOCK = 1024;     // 16 waves: one workgroup per CU (LDS-bound)
@@ -1181,12 +1175,6 @@ __host__ __device__ inline uint64_t sp_capacity(uint64_t r_now, uint32_t nb) {
 #ifndef GS_SPK_ITEMS
 #define GS_SPK_ITEMS 16
 #endif
-#ifndef GS_SPK_ABL_NOLOAD
-#define GS_SPK_ABL_NOLOAD 0
-#endif
-#ifndef GS_SPK_ABL_NOSTORE
-#define GS_SPK_ABL_NOSTORE 0
-#endif
 #ifndef GS_SPK_NT
 #define GS_SPK_NT 0
 #endif
@@ -1286,11 +1274,7 @@ void k_sp_scatter_pack(BaseSrc<V, DIR, PAY_VAL> es, uint64_t n, int S, uint32_t 
       i = r >> 1;
       rev = r & 1u;
     }
-#if GS_SPK_ABL_NOLOAD   // timing-only ablation: synthetic keys in range, no column reads (wrong output)
-    kk[u] = (int64_t)((uint64_t)es.base + (((uint64_t)(i * 2654435761u) * ((uint64_t)nbp << S)) >> 32));
-    vv[u] = (V)(i & 0x3FFF);
-    (void)rev;
-#elif GS_SPK_NT   // A/B: the columns are read once: non-temporal loads
+#if GS_SPK_NT   // A/B: the columns are read once: non-temporal loads
     kk[u] = __builtin_nontemporal_load(&(rev ? es.dst : es.src)[i]);
     vv[u] = __builtin_nontemporal_load(&es.val[i]);
 #else
@@ -1352,7 +1336,7 @@ void k_sp_scatter_pack(BaseSrc<V, DIR, PAY_VAL> es, uint64_t n, int S, uint32_t 
 #pragma unroll
   for (int k = 0; k < BPT; ++k) {
     const bool drop = cb[k] && ob[k] + cb[k] > send[k];
-    ovf += (drop && !GS_SPK_ABL_NOLOAD) ? 1u : 0u;   // (the ablation's synthetic keys overflow regions)
+    ovf += drop ? 1u : 0u;
     if ((uint32_t)tid * BPT + k < NB) s_del[(uint32_t)tid * BPT + k] = drop ? trash : ob[k] - sb[k];
   }
   if (tid == 0) s_del[NB] = trash;
@@ -1364,11 +1348,7 @@ void k_sp_scatter_pack(BaseSrc<V, DIR, PAY_VAL> es, uint64_t n, int S, uint32_t 
     const uint64_t e = s_slot[j];
     const uint32_t g = j + s_del[(uint32_t)e & 0xFFFu];
     const uint32_t packed = (uint32_t)(e >> 32);
-#if GS_SPK_ABL_NOSTORE   // timing-only ablation: no record stores (wrong output)
-    if (g == 0xFFFFFFFFu) rec[0] = packed;
-#else
     rec[g] = packed;
-#endif
     if ((packed >> 16) == PK_ESC && ((uint32_t)e & 0xFFFu) != (uint32_t)NB) {   // rare: the full value into `wide`
       wide[g] = es.val[col_index(((uint32_t)e >> 12) & 0xFFFFFu)];
       ++esc;
@@ -1379,7 +1359,7 @@ void k_sp_scatter_pack(BaseSrc<V, DIR, PAY_VAL> es, uint64_t n, int S, uint32_t 
 #pragma unroll
   for (int k = 0; k < BPT; ++k) {
     const bool drop = cb[k] && ob[k] + cb[k] > send[k];
-    ovf += (drop && !GS_SPK_ABL_NOLOAD) ? 1u : 0u;   // (the ablation's synthetic keys overflow regions)
+    ovf += drop ? 1u : 0u;
     if ((uint32_t)tid * BPT + k < NB) s_run[(uint32_t)tid * BPT + k] = ((uint64_t)(drop ? trash + st : ob[k]) << 32) | st;
     st += cb[k];
   }
@@ -1410,11 +1390,7 @@ void k_sp_scatter_pack(BaseSrc<V, DIR, PAY_VAL> es, uint64_t n, int S, uint32_t 
 #pragma unroll
   for (int u = 0; u < ITEMS; ++u) {
     const uint64_t e = s_slot[(uint32_t)u * BLOCK + tid];
-#if GS_SPK_ABL_NOSTORE   // timing-only ablation: no record stores (wrong output)
-    if ((uint32_t)e == 0xFFFFFFFFu) rec[0] = (uint32_t)(e >> 32);
-#else
     rec[(uint32_t)e] = (uint32_t)(e >> 32);
-#endif
   }
 #endif
 #pragma unroll
@@ -1683,13 +1659,7 @@ __global__ __launch_bounds__(BK_ACC_BLOCK) void k_bk_accum(Src src, const BkItem
           for (int u = 0; u < U4; ++u) {   // unconditional, clamped: see k_dp_hist
             const uint32_t g = g4 + (uint32_t)u * BK_ACC_BLOCK;
             qi[u] = q4_of(g < n4 ? g : n4 - 1);
-#if GS_ACC_ABL_NOLOAD   // timing-only ablation: synthetic narrow records, no partition reads (wrong output)
-            const uint32_t h = (qi[u] * 2654435761u) >> 8;
-            x[u] = make_uint4((h & 0x3FFF) | 0x10000u, ((h >> 3) & 0x3FFF) | 0x20000u, ((h >> 6) & 0x3FFF) | 0x30000u,
-                              ((h >> 9) & 0x3FFF) | 0x40000u);
-#else
             x[u] = rec4[qi[u]];
-#endif
           }
 #pragma unroll
           for (int u = 0; u < U4; ++u) {
@@ -1703,12 +1673,6 @@ __global__ __launch_bounds__(BK_ACC_BLOCK) void k_bk_accum(Src src, const BkItem
               const uint32_t h0 = x[u].x >> 16, h1 = x[u].y >> 16, h2 = x[u].z >> 16, h3 = x[u].w >> 16;
               bool rare = (h0 == PK_ESC) | (h1 == PK_ESC) | (h2 == PK_ESC) | (h3 == PK_ESC);
               if constexpr (P::OP_IS_SUM) rare |= (h0 == 0u) | (h1 == 0u) | (h2 == 0u) | (h3 == 0u);
-#if GS_ACC_ABL_NOATOM   // timing-only ablation: no LDS atomics (wrong output)
-              if (!rare) {
-                if ((h0 ^ h1 ^ h2 ^ h3 ^ x[u].x ^ x[u].y ^ x[u].z ^ x[u].w) == 0x9E3779B9u) P::add_narrow(s, 0, h0);
-                continue;
-              }
-#else
               if (!rare) {
                 P::add_narrow(s, x[u].x & (P::W - 1), h0);
                 P::add_narrow(s, x[u].y & (P::W - 1), h1);
@@ -1716,7 +1680,6 @@ __global__ __launch_bounds__(BK_ACC_BLOCK) void k_bk_accum(Src src, const BkItem
                 P::add_narrow(s, x[u].w & (P::W - 1), h3);
                 continue;
               }
-#endif
             }
             add1(q, x[u].x);
             add1(q + 1, x[u].y);

@@ -266,7 +266,7 @@ __global__ __launch_bounds__(BLOCK) void k_onesweep_combine(Src src, K* __restri
 
 // region d of the partial array = [digit_base[d], end[d]); end from the last tile's INCLUSIVE granule.
 // table[0..255] = physical starts, table[256..512] = logical starts (table[512] = total partials)
-static __global__ __launch_bounds__(256) void k_region_table(const uint64_t* __restrict__ status, uint32_t last_tile,
+[[maybe_unused]] static __global__ __launch_bounds__(256) void k_region_table(const uint64_t* __restrict__ status, uint32_t last_tile,
                                                              const uint32_t* __restrict__ digit_base,
                                                              uint32_t* __restrict__ table,
                                                              unsigned long long* __restrict__ total) {

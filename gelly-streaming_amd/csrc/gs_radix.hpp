@@ -101,7 +101,7 @@ __device__ __forceinline__ void flush_hist(uint32_t (*h)[8][RADIX], int nd, uint
 
 // XOR-mask of a key buffer + the 256-bin histograms of its nd low bytes (the caller's bound on the
 // key width), one table per wave (wave_hist_add)
-static __global__ __launch_bounds__(256) void k_keyinfo_buf(const uint64_t* __restrict__ keys, uint64_t n, int nd,
+[[maybe_unused]] static __global__ __launch_bounds__(256) void k_keyinfo_buf(const uint64_t* __restrict__ keys, uint64_t n, int nd,
                                                      unsigned long long* __restrict__ mask_out,
                                                      uint32_t* __restrict__ hist_out /*[8][256]*/) {
   __shared__ uint32_t h[4][8][RADIX];   // [wave][byte][bin]
@@ -224,7 +224,7 @@ __global__ __launch_bounds__(256) void k_hist_bytes(const int64_t* __restrict__ 
 }
 
 // hist[p][256] -> base[p][256] exclusive scans, one wave-parallel scan per pass (block = 256)
-static __global__ __launch_bounds__(256) void k_digit_base(const uint32_t* __restrict__ hist, uint32_t* __restrict__ base,
+[[maybe_unused]] static __global__ __launch_bounds__(256) void k_digit_base(const uint32_t* __restrict__ hist, uint32_t* __restrict__ base,
                                                     int passes) {
   __shared__ uint32_t wsum[4];
   const int tid = threadIdx.x, l = tid & 63, w = tid >> 6;
@@ -327,10 +327,6 @@ __global__ __launch_bounds__(BLOCK) void k_onesweep(Src src, KO* __restrict__ ko
     for (int w = 0; w < wid; ++w) off += s_wtot[w];
     s_start[tid] += off;
     uint64_t excl;
-#ifdef GS_ABLATE_NO_LOOKBACK   // timing-only build: plausible but WRONG offsets, no inter-tile wait
-    excl = digit_base[tid] + (uint64_t)tile * cnt;
-    if (excl + cnt > n) excl = n > cnt ? n - cnt : 0;
-#else
     if (tile == 0) {
       excl = digit_base[tid];
     } else {
@@ -342,7 +338,6 @@ __global__ __launch_bounds__(BLOCK) void k_onesweep(Src src, KO* __restrict__ ko
       }
       st_agent(status + (uint64_t)tile * RADIX + tid, granule(FLAG_INC, epoch, excl + cnt));
     }
-#endif
     s_goff[tid] = (uint32_t)excl;
   }
   __syncthreads();
