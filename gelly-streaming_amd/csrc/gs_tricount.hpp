@@ -72,9 +72,6 @@ static_assert(TH_DMAX * 2 <= TH_H, "TH_DMAX must be <= TH_H / 2");
 #define GS_TH_ILP 8    // R-MAT s22 (DMAX 512): 2 -> 93.9 ms, 4 -> 70.2, 6 -> 62.6, 8 -> 62.0, 12 -> 64.5, 16 -> 137.8; DMAX 256: 6 -> 55.3, 8 -> 55.8, 10 -> 54.5 (s24 291.9, 289.6, 279.7); 6 waves/SIMD: 6 -> 23.8, 8 -> 23.7, 10 -> 23.8 (spills)
 #endif
 constexpr int TH_ILP = GS_TH_ILP;   // items per lane: TH_ILP probes in flight
-#ifndef GS_TH_LANEIL
-#define GS_TH_LANEIL 0   // light kernel: lane-interleaved items (1) or TH_ILP consecutive items per lane (0)
-#endif
 #ifndef GS_TH_LONG
 #define GS_TH_LONG 64    // light kernel: out-lists of >= TH_LONG items are gathered lane-interleaved (64 per load)
 #endif
