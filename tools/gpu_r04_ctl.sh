@@ -1,6 +1,7 @@
 #!/bin/bash
 # round 4: bench.py under torch.distributed.run (as the driver launches N > 1) at world 1, control plane
 # nccl vs gloo (--control-pg), alternating, same box
+# (the --control-pg switch lived in an A/B build of bench.py only; the kept bench uses the nccl process group)
 set -e
 cd "$(dirname "$0")/.."
 export TMPDIR=/tmp
