@@ -155,6 +155,7 @@ constexpr size_t SM_BK_N = SM_BK_MM + 32;            // u32[4] bucket path: item
 constexpr size_t SM_BK_X = SM_BK_N + 16;            // u64[2] bucket path: copies of the timeout flag and the escape
                                                     // count (k_bk_emit), so the window reads back one 64-byte block
 constexpr size_t SM_TRI_PROBES = SM_BK_X + 16;      // u64 triangles: hash probes of the counting step
+constexpr size_t SM_TRI_NV = SM_TRI_PROBES + 8;     // u64 triangles: vertices with an edge (k_tri_lclass)
 constexpr size_t SM_BK_ESC = SM_TRI_PROBES + 16;    // u64 packed scatter: escaped values
 constexpr size_t SM_DEV_ERR = SM_BK_ESC + 8;        // u32 device error flags (GS_DERR_*)
 constexpr size_t SM_HS = SM_DEV_ERR + 8;            // u32[4] HashSet order: complex vertices, JDK flags

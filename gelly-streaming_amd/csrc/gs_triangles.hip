@@ -832,7 +832,8 @@ gs_status tri_unique(gs_ctx* c, const uint64_t* keys, uint64_t n, uint32_t B, bo
 // balanced u-range's edges sorted by target (in-lists with suffix ranges), then the LDS hash-set
 // kernels.  okeys: the sorted unique keys (row of every position), else rows come from out_range.
 gs_status tri_count(gs_ctx* c, uint32_t B, size_t V, uint64_t M, const uint32_t* nbr, const uint2* out_range,
-                    const uint64_t* okeys, uint32_t part, uint32_t nparts, uint64_t* T, uint64_t* probes) {
+                    const uint64_t* okeys, uint32_t part, uint32_t nparts, uint64_t* T, uint64_t* probes,
+                    const uint32_t* loops = nullptr, const uint32_t* rank = nullptr, uint64_t* active = nullptr) {
   char* sm = c->small.as<char>();
   *T = 0;
   *probes = 0;
@@ -899,6 +900,8 @@ gs_status tri_count(gs_ctx* c, uint32_t B, size_t V, uint64_t M, const uint32_t*
   GS_HIP(hipMemsetAsync(d_total, 0, 8, c->stream));
   GS_HIP(hipMemsetAsync(d_probes, 0, 8, c->stream));
   GS_HIP(hipMemsetAsync(d_nheavy, 0, 8, c->stream));   // heavy items, queued chunks
+  unsigned long long* d_active = active ? (unsigned long long*)(sm + SM_TRI_NV) : nullptr;
+  if (d_active) GS_HIP(hipMemsetAsync(d_active, 0, 8, c->stream));
   uint32_t* d_err = (uint32_t*)(sm + SM_DEV_ERR);
   GS_HIP(hipMemsetAsync(d_err, 0, 4, c->stream));
   // LDS hash-set bucket cap: unlimited, or one bucket under GS_FLAG_TEST_TINY_TABLES (tests only)
@@ -907,7 +910,12 @@ gs_status tri_count(gs_ctx* c, uint32_t B, size_t V, uint64_t M, const uint32_t*
   uint2* queue = c->tri_queue.as<uint2>();
   hipLaunchKernelGGL(k_tri_lclass, dim3((unsigned)std::max<uint64_t>(1, std::min<uint64_t>((V + 255) / 256, 16384))),
                      dim3(256), 0, c->stream, nbr, out_range, in_range, (uint32_t)V, 0u, 0xFFFFFFFFu, nb_cap, queue,
-                     d_nqueue, c->tri_heavy.as<uint2>(), d_nheavy);
+                     d_nqueue, c->tri_heavy.as<uint2>(), d_nheavy, d_active);
+  if (d_active && loops && rank) {
+    const uint32_t words = (uint32_t)((V + 31) / 32);
+    hipLaunchKernelGGL(k_tri_loop_only, dim3((unsigned)std::max<uint64_t>(1, std::min<uint64_t>((words + 255) / 256, 4096))),
+                       dim3(256), 0, c->stream, loops, words, rank, out_range, in_range, d_active);
+  }
   hipLaunchKernelGGL(k_tri_light, dim3(8192u), dim3(TH_BLOCK), 0, c->stream, nbr, sfx, out_range, in_range, queue,
                      d_nqueue, d_total, d_probes, nb_cap, d_err);
   GS_HIP(hipGetLastError());
@@ -950,7 +958,9 @@ gs_status tri_count(gs_ctx* c, uint32_t B, size_t V, uint64_t M, const uint32_t*
   GS_HIP(hipMemcpyAsync(c->host_small + 6, d_probes, 8, hipMemcpyDeviceToHost, c->stream));
   c->host_small[7] = 0;   // (the copy below fills the low 4 bytes)
   GS_HIP(hipMemcpyAsync(c->host_small + 7, d_err, 4, hipMemcpyDeviceToHost, c->stream));
+  if (d_active) GS_HIP(hipMemcpyAsync(c->host_small + 9, d_active, 8, hipMemcpyDeviceToHost, c->stream));
   GS_TRY(host_wait(c));
+  if (active) *active = c->host_small[9];
   if ((uint32_t)c->host_small[3] != 0) return set_error(c, GS_EDEVICE, "look-back spin timed out");
   if ((uint32_t)c->host_small[7] & GS_DERR_TABLE_FULL)
     return set_error(c, GS_EDEVICE, "window triangles: an LDS hash set filled up (counting aborted)");
@@ -993,7 +1003,21 @@ gs_status triangles_impl(gs_ctx* c, const gs_edge_batch* b, uint32_t part, uint3
   GS_TRY(ensure(c, c->out_b, g.V * 4));
   uint32_t* deg = c->out_a.as<uint32_t>();
   uint32_t* rank = c->out_b.as<uint32_t>();
-  GS_TRY(tri_degrees(c, g, deg));
+  // The orientation needs only SOME total order of the ids (any order gives the exact count: each
+  // triangle is counted once, at its lowest-ranked vertex); the degree classes keep the out-lists short.
+  // A large window's classes come from the degrees of its first n / 4 edges (R-MAT s26: ranks + keys +
+  // sort 98.2 -> 86.5 ms, count +0.9 ms, window 329.0 -> 318.4 ms; s24 62.6 -> 61.3 ms, same box;
+  // profiles/r04/evidence/deg_sample/); the vertices-with-edges figure then comes from the count's
+  // vertex pass (k_tri_lclass, k_tri_loop_only).  GS_TRI_DEG_SAMPLE = k overrides the 4 (1 = exact
+  // degrees).  The split-window steps (gs_tri_dist_*) keep exact, all-reduced degrees.
+  static const int deg_sample_env = getenv("GS_TRI_DEG_SAMPLE") ? atoi(getenv("GS_TRI_DEG_SAMPLE")) : 4;
+  const uint64_t ds = deg_sample_env > 1 ? (uint64_t)deg_sample_env : 1;
+  const bool sampled = ds > 1 && nparts == 1 && g.n >= (1ull << 26);
+  {
+    TriGeom gd = g;
+    if (sampled) gd.n = g.n / ds;
+    GS_TRY(tri_degrees(c, gd, deg));
+  }
   GS_TRY(tri_ranks(c, g, deg, rank));
   GS_TRY(ensure(c, c->aux, g.n * 8));
   GS_TRY(tri_okeys(c, g, rank, c->aux.as<uint64_t>()));
@@ -1016,9 +1040,10 @@ gs_status triangles_impl(gs_ctx* c, const gs_edge_batch* b, uint32_t part, uint3
                        c->out_keys.as<uint64_t>(), (uint32_t)M, g.B, c->tri_nbr.as<uint32_t>(),
                        reinterpret_cast<uint32_t*>(out_range));
     GS_HIP(hipGetLastError());
+    uint64_t active = 0;
     GS_TRY(tri_count(c, g.B, g.V, M, c->tri_nbr.as<uint32_t>(), out_range, c->out_keys.as<uint64_t>(), part, nparts,
-                     &T, &probes));
-    tri_times(c, g, M, nv, probes, s.passes);
+                     &T, &probes, c->tri_loops.as<uint32_t>(), rank, sampled ? &active : nullptr));
+    tri_times(c, g, M, sampled ? active : nv, probes, s.passes);
   }
   if (loops && part == 0) {   // self-pair candidates (x, x, true) matched by a self-loop on x (:105)
     uint64_t S = 0;

@@ -346,13 +346,16 @@ __global__ __launch_bounds__(256) void k_tri_lclass(const uint32_t* __restrict__
                                                     const uint2* __restrict__ in_range, uint32_t nv, uint32_t q0,
                                                     uint32_t q1, uint32_t nb_cap, uint2* __restrict__ queue,
                                                     uint32_t* __restrict__ n_queue, uint2* __restrict__ heavy,
-                                                    uint32_t* __restrict__ n_heavy) {
+                                                    uint32_t* __restrict__ n_heavy,
+                                                    unsigned long long* __restrict__ n_active) {
   const int lane = threadIdx.x & 63;
+  uint32_t act = 0;   // this lane's ranks with an out- or in-entry (n_active, when asked for)
   for (uint32_t v0 = blockIdx.x * 256u; v0 < nv; v0 += gridDim.x * 256u) {   // wave-uniform trip count
     const uint32_t v = v0 + threadIdx.x;
     uint32_t nh = 0, nl = 0;
     if (v < nv) {
       const uint2 ro = out_range[v], ri = in_range[v];
+      if (n_active) act += (ro.y != ro.x || ri.y != ri.x) ? 1u : 0u;
       if (ro.y != ro.x && ri.y != ri.x && ro.x >= q0 && ro.x < q1) {
         const uint32_t dv = ro.y - ro.x;
         const bool heavy_v = dv > TH_DMAX ||
@@ -372,6 +375,30 @@ __global__ __launch_bounds__(256) void k_tri_lclass(const uint32_t* __restrict__
     for (uint32_t j = 0; j < nh; ++j) heavy[bh + j] = make_uint2(v, j);
     for (uint32_t j = 0; j < nl; ++j) queue[bl + j] = make_uint2(v, j);
   }
+  if (n_active) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) act += __shfl_xor(act, o, WAVE);
+    if (lane == 0 && act) atomicAdd(n_active, (unsigned long long)act);
+  }
+}
+
+// ... plus the ids whose only edges are self-loops (loops: the id-indexed self-loop bitmap; their ranks
+// have no out- or in-entries), so n_active = the window's vertices with an edge
+__global__ __launch_bounds__(256) void k_tri_loop_only(const uint32_t* __restrict__ loops, uint32_t words,
+                                                       const uint32_t* __restrict__ rank, const uint2* __restrict__ out_range,
+                                                       const uint2* __restrict__ in_range,
+                                                       unsigned long long* __restrict__ n_active) {
+  uint32_t cnt = 0;
+  for (uint32_t w = blockIdx.x * 256u + threadIdx.x; w < words; w += gridDim.x * 256u) {
+    for (uint32_t bits = loops[w]; bits; bits &= bits - 1) {
+      const uint32_t r = rank[w * 32u + (uint32_t)__builtin_ctz(bits)];
+      const uint2 ro = out_range[r], ri = in_range[r];
+      cnt += (ro.y == ro.x && ri.y == ri.x) ? 1u : 0u;
+    }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o, WAVE);
+  if ((threadIdx.x & 63) == 0 && cnt) atomicAdd(n_active, (unsigned long long)cnt);
 }
 
 // work of each heavy item (v, chunk of TH_VCH in-entries): its probes (the suffix lengths) plus a
