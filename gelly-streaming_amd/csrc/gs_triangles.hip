@@ -323,6 +323,90 @@ __global__ __launch_bounds__(256) void k_tri_out(const uint64_t* __restrict__ ke
   }
 }
 
+// ---- the unique oriented edges straight into out-lists (wide keys, the whole window) -----------------
+// One read of the sorted keys counts each tile's heads (a key other than its predecessor and other than the
+// self-loop sentinel, which sorts last), an exclusive scan of the tile counts places them, and a second read
+// writes nbr[p] = v and rowid[p] = u at each head's unique index p and the row bounds out_range[u] --
+// instead of writing the unique keys (reduce-by-key) and reading them back to cut them into rows.
+constexpr uint32_t UO_BLOCK = 256, UO_ITEMS = 16, UO_TILE = UO_BLOCK * UO_ITEMS;
+__global__ __launch_bounds__(UO_BLOCK) void k_tri_uo_count(const uint64_t* __restrict__ keys, uint64_t n, uint64_t sent,
+                                                           unsigned long long* __restrict__ tile_cnt) {
+  __shared__ uint32_t s_w[UO_BLOCK / WAVE];
+  const uint64_t t0 = (uint64_t)blockIdx.x * UO_TILE;
+  uint64_t k[UO_ITEMS], kp[UO_ITEMS];
+#pragma unroll
+  for (int j = 0; j < UO_ITEMS; ++j) {   // unconditional, clamped loads
+    const uint64_t i = min(t0 + (uint64_t)j * UO_BLOCK + threadIdx.x, n - 1);
+    k[j] = keys[i];
+    kp[j] = keys[i ? i - 1 : 0];
+  }
+  uint32_t c = 0;
+#pragma unroll
+  for (int j = 0; j < UO_ITEMS; ++j) {
+    const uint64_t i = t0 + (uint64_t)j * UO_BLOCK + threadIdx.x;
+    c += (i < n && k[j] != sent && (i == 0 || kp[j] != k[j])) ? 1u : 0u;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, WAVE);
+  if ((threadIdx.x & 63) == 0) s_w[threadIdx.x >> 6] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t t = 0;
+#pragma unroll
+    for (int w = 0; w < (int)(UO_BLOCK / WAVE); ++w) t += s_w[w];
+    tile_cnt[blockIdx.x] = t;
+  }
+}
+
+__global__ __launch_bounds__(UO_BLOCK) void k_tri_uo_write(const uint64_t* __restrict__ keys, uint64_t n, uint64_t sent,
+                                                           uint32_t B, const unsigned long long* __restrict__ tile_pre,
+                                                           uint32_t* __restrict__ nbr, uint32_t* __restrict__ rowid,
+                                                           uint32_t* __restrict__ out_range) {
+  constexpr int NW = UO_BLOCK / WAVE;
+  __shared__ uint32_t s_cnt[UO_ITEMS][NW];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const uint64_t t0 = (uint64_t)blockIdx.x * UO_TILE;
+  const uint64_t mask = (1ull << B) - 1;
+  uint64_t k[UO_ITEMS], kp[UO_ITEMS], hb[UO_ITEMS];
+#pragma unroll
+  for (int j = 0; j < UO_ITEMS; ++j) {
+    const uint64_t i = min(t0 + (uint64_t)j * UO_BLOCK + threadIdx.x, n - 1);
+    k[j] = keys[i];
+    kp[j] = keys[i ? i - 1 : 0];
+  }
+#pragma unroll
+  for (int j = 0; j < UO_ITEMS; ++j) {
+    const uint64_t i = t0 + (uint64_t)j * UO_BLOCK + threadIdx.x;
+    hb[j] = __ballot(i < n && k[j] != sent && (i == 0 || kp[j] != k[j]));
+    if (lane == 0) s_cnt[j][w] = (uint32_t)__popcll(hb[j]);
+  }
+  __syncthreads();
+  uint64_t run = tile_pre[blockIdx.x];   // heads before this tile, then before round j
+#pragma unroll
+  for (int j = 0; j < UO_ITEMS; ++j) {
+    uint32_t before = 0, tot = 0;
+#pragma unroll
+    for (int x = 0; x < NW; ++x) {
+      const uint32_t c = s_cnt[j][x];
+      tot += c;
+      before += x < w ? c : 0u;
+    }
+    const uint64_t i = t0 + (uint64_t)j * UO_BLOCK + threadIdx.x;
+    const uint64_t excl = run + before + mbcnt(hb[j]);   // heads before key i
+    run += tot;
+    if (i >= n || k[j] == sent) continue;
+    const bool head = (hb[j] >> lane) & 1ull;
+    const uint32_t u = (uint32_t)(k[j] >> B);
+    if (head) {
+      nbr[excl] = (uint32_t)(k[j] & mask);
+      rowid[excl] = u;
+      if (i == 0 || (uint32_t)(kp[j] >> B) != u) out_range[2 * u] = (uint32_t)excl;
+    }
+    const uint64_t kn = i + 1 < n ? keys[i + 1] : sent;   // the row ends at key i: the next key is another row's
+    if (kn == sent || (uint32_t)(kn >> B) != u) out_range[2 * u + 1] = (uint32_t)(excl + (head ? 1u : 0u));
+  }
+}
+
 // row (u) of each adjacency position of a slice, from the out-lists (one thread per u; d+(u) is
 // small under the degree orientation)
 __global__ __launch_bounds__(256) void k_tri_rowid(const uint2* __restrict__ out_range, uint32_t u0, uint32_t u1,
@@ -833,7 +917,8 @@ gs_status tri_unique(gs_ctx* c, const uint64_t* keys, uint64_t n, uint32_t B, bo
 // kernels.  okeys: the sorted unique keys (row of every position), else rows come from out_range.
 gs_status tri_count(gs_ctx* c, uint32_t B, size_t V, uint64_t M, const uint32_t* nbr, const uint2* out_range,
                     const uint64_t* okeys, uint32_t part, uint32_t nparts, uint64_t* T, uint64_t* probes,
-                    const uint32_t* loops = nullptr, const uint32_t* rank = nullptr, uint64_t* active = nullptr) {
+                    const uint32_t* loops = nullptr, const uint32_t* rank = nullptr, uint64_t* active = nullptr,
+                    const uint32_t* rowid_all = nullptr) {
   char* sm = c->small.as<char>();
   *T = 0;
   *probes = 0;
@@ -871,6 +956,9 @@ gs_status tri_count(gs_ctx* c, uint32_t B, size_t V, uint64_t M, const uint32_t*
   if (okeys) {
     hipLaunchKernelGGL(k_tri_tpay<false>, dim3(ge), dim3(256), 0, c->stream, okeys, nullptr, nbr, p0, p1, B, out_range,
                        c->aux.as<uint64_t>(), c->tri_sfx.as<uint2>(), (uint32_t*)(sm + SM_HIST));
+  } else if (rowid_all) {   // the row of every position, written with the out-lists (k_tri_uo_write)
+    hipLaunchKernelGGL(k_tri_tpay<true>, dim3(ge), dim3(256), 0, c->stream, nullptr, rowid_all + p0, nbr, p0, p1, B,
+                       out_range, c->aux.as<uint64_t>(), c->tri_sfx.as<uint2>(), (uint32_t*)(sm + SM_HIST));
   } else {
     GS_TRY(ensure(c, c->tri_queue, Ms * 4));
     hipLaunchKernelGGL(k_tri_rowid, dim3((unsigned)std::min<uint64_t>((u1 - u0 + 255) / 256, 16384)), dim3(256), 0,
@@ -1021,28 +1109,69 @@ gs_status triangles_impl(gs_ctx* c, const gs_edge_batch* b, uint32_t part, uint3
   GS_TRY(tri_ranks(c, g, deg, rank));
   GS_TRY(ensure(c, c->aux, g.n * 8));
   GS_TRY(tri_okeys(c, g, rank, c->aux.as<uint64_t>()));
-  // 2. sort + unique -> the simple oriented graph, sorted by (u, v)
+  // 2. sort + unique -> the simple oriented graph, sorted by (u, v); 3. out-lists
   Sorted s;
   uint64_t M = 0;
-  GS_TRY(tri_unique(c, c->aux.as<uint64_t>(), g.n, g.B, true, false, &M, &s));
-  const uint64_t loops = c->host_small[4];
-  const uint64_t nv = g.V - (uint32_t)c->host_small[5];
-  hipEventRecord(c->ev[2], c->stream);
-  if (loops) M -= 1;   // the self-loop sentinel sorts last
-  uint64_t T = 0, probes = 0;
-  if (M) {
-    // 3. out-lists; 4. the count
+  static const int uo_env = getenv("GS_TRI_FUSED_UNIQUE") ? atoi(getenv("GS_TRI_FUSED_UNIQUE")) : 1;   // A/B
+  const bool fused = uo_env != 0 && 2 * g.B > 32;   // wide (u64) sorted keys
+  const uint32_t* rowid_all = nullptr;
+  uint2* out_range = nullptr;
+  uint64_t loops = 0, nv = 0;
+  if (fused) {
+    GS_TRY(sort_buffer(c, c->aux.as<uint64_t>(), nullptr, g.n, &s, 2 * (int)g.B, 4, true));
+    if (!s.wide) return set_error(c, GS_EDEVICE, "window triangles: oriented keys narrower than expected");
+    hipEventRecord(c->ev[1], c->stream);
+    const uint64_t* sk = static_cast<const uint64_t*>(s.keys);
+    const uint64_t sent = (g.B * 2 >= 64) ? ~0ull : ((1ull << (2 * g.B)) - 1);
+    const uint64_t tiles = (g.n + UO_TILE - 1) / UO_TILE;
+    GS_TRY(ensure(c, c->tri_tiles, (size_t)(2 * tiles + 2) * 8));
+    unsigned long long* tcnt = c->tri_tiles.as<unsigned long long>();
+    unsigned long long* tpre = tcnt + tiles + 1;
+    hipLaunchKernelGGL(k_tri_uo_count, dim3((unsigned)tiles), dim3(UO_BLOCK), 0, c->stream, sk, g.n, sent, tcnt);
+    GS_HIP(hipGetLastError());
+    GS_TRY(xscan(c, (const uint64_t*)tcnt, tiles, (uint64_t*)tpre));
+    GS_HIP(hipMemcpyAsync(c->host_small + 10, tpre + tiles, 8, hipMemcpyDeviceToHost, c->stream));
+    GS_TRY(host_wait(c));
+    M = c->host_small[10];
+    loops = c->host_small[4];
+    nv = g.V - (uint32_t)c->host_small[5];
+    if (M >= (1ull << 32)) return set_error(c, GS_EINVAL, "window triangles: %llu unique edges (limit 2^32 - 1)",
+                                            (unsigned long long)M);
     GS_TRY(ensure(c, c->tri_range, g.V * 16));
-    GS_TRY(ensure(c, c->tri_nbr, M * 4));
-    uint2* out_range = reinterpret_cast<uint2*>(c->tri_range.p);
+    GS_TRY(ensure(c, c->tri_nbr, M * 4 + 4));
+    GS_TRY(ensure(c, c->out_keys, M * 4 + 4));
+    out_range = reinterpret_cast<uint2*>(c->tri_range.p);
     GS_HIP(hipMemsetAsync(out_range, 0, g.V * 8, c->stream));
-    hipLaunchKernelGGL(k_tri_out, dim3((unsigned)std::min<uint64_t>((M + 255) / 256, 16384)), dim3(256), 0, c->stream,
-                       c->out_keys.as<uint64_t>(), (uint32_t)M, g.B, c->tri_nbr.as<uint32_t>(),
+    hipLaunchKernelGGL(k_tri_uo_write, dim3((unsigned)tiles), dim3(UO_BLOCK), 0, c->stream, sk, g.n, sent, g.B,
+                       (const unsigned long long*)tpre, c->tri_nbr.as<uint32_t>(), c->out_keys.as<uint32_t>(),
                        reinterpret_cast<uint32_t*>(out_range));
     GS_HIP(hipGetLastError());
+    rowid_all = c->out_keys.as<uint32_t>();
+    hipEventRecord(c->ev[2], c->stream);
+  } else {
+    GS_TRY(tri_unique(c, c->aux.as<uint64_t>(), g.n, g.B, true, false, &M, &s));
+    loops = c->host_small[4];
+    nv = g.V - (uint32_t)c->host_small[5];
+    hipEventRecord(c->ev[2], c->stream);
+    if (loops) M -= 1;   // the self-loop sentinel sorts last
+    if (M) {
+      GS_TRY(ensure(c, c->tri_range, g.V * 16));
+      GS_TRY(ensure(c, c->tri_nbr, M * 4));
+      out_range = reinterpret_cast<uint2*>(c->tri_range.p);
+      GS_HIP(hipMemsetAsync(out_range, 0, g.V * 8, c->stream));
+      hipLaunchKernelGGL(k_tri_out, dim3((unsigned)std::min<uint64_t>((M + 255) / 256, 16384)), dim3(256), 0,
+                         c->stream, c->out_keys.as<uint64_t>(), (uint32_t)M, g.B, c->tri_nbr.as<uint32_t>(),
+                         reinterpret_cast<uint32_t*>(out_range));
+      GS_HIP(hipGetLastError());
+    }
+  }
+  uint64_t T = 0, probes = 0;
+  if (M) {
+    // 4. the count
     uint64_t active = 0;
-    GS_TRY(tri_count(c, g.B, g.V, M, c->tri_nbr.as<uint32_t>(), out_range, c->out_keys.as<uint64_t>(), part, nparts,
-                     &T, &probes, c->tri_loops.as<uint32_t>(), rank, sampled ? &active : nullptr));
+    GS_TRY(tri_count(c, g.B, g.V, M, c->tri_nbr.as<uint32_t>(), out_range, fused ? nullptr : c->out_keys.as<uint64_t>(),
+                     part, nparts, &T, &probes, c->tri_loops.as<uint32_t>(), rank, sampled ? &active : nullptr,
+                     rowid_all));
     tri_times(c, g, M, sampled ? active : nv, probes, s.passes);
   }
   if (loops && part == 0) {   // self-pair candidates (x, x, true) matched by a self-loop on x (:105)
