@@ -11,7 +11,7 @@ The directory name contains a hyphen, so it is loaded by path:
 or with ``load_package()`` from __graft_entry__.py.
 """
 from ._lib import GsError, load as load_library  # noqa: F401
-from .engine import Engine, StageTimes  # noqa: F401
+from .engine import CommGroup, Engine, StageTimes  # noqa: F401
 from .functions import (Collector, CountFold, CountReduce, DegreeMaxNeighborFold, EdgesApply, EdgesFold,  # noqa: F401
                         EdgesReduce, MaxReduce, MaxValuesFold, MinReduce, MinValuesFold, SumReduce, SumValuesFold)
 from .stream import (AscendingTimestampExtractor, DataStream, EdgeColumns, EdgeDirection,  # noqa: F401

@@ -42,6 +42,7 @@ EXPORTS = ("gs_abi_version", "gs_create", "gs_destroy", "gs_last_error", "gs_set
            "gs_window_triangles_dist", "gs_window_components",
            "gs_parse_edges_text", "gs_fetch_last_output", "gs_fetch_last_degree_output", "gs_owner_of", "gs_window_reduce_partials", "gs_window_fold_degree_max_partials",
            "gs_merge_partials", "gs_merge_degree_max_partials", "gs_comm_unique_id", "gs_comm_init", "gs_comm_destroy",
+           "gs_comm_group_create", "gs_comm_group_destroy", "gs_comm_init_group",
            "gs_comm_allreduce_sum_u64", "gs_window_reduce_dist", "gs_window_fold_degree_max_dist",
            "gs_stream_create", "gs_stream_destroy", "gs_stream_append", "gs_stream_watermark", "gs_stream_flush",
            "gs_stream_poll", "gs_stream_stats", "gs_generate_rmat", "gs_generate_uniform", "gs_generate_zipf", "gs_generate_values", "gs_last_stage_times",
@@ -209,6 +210,9 @@ def load() -> ctypes.CDLL:
         "gs_comm_unique_id": (st, [P]),
         "gs_comm_init": (st, [P, i32, i32, P]),
         "gs_comm_destroy": (st, [P]),
+        "gs_comm_group_create": (st, [i32, ctypes.POINTER(P)]),
+        "gs_comm_group_destroy": (None, [P]),
+        "gs_comm_init_group": (st, [P, P, i32]),
         "gs_comm_allreduce_sum_u64": (st, [P, ctypes.POINTER(u64)]),
         "gs_window_reduce_dist": (st, [P, ctypes.POINTER(GsEdgeBatch), i32, i32, P, ctypes.POINTER(GsVertexOut)]),
         "gs_window_fold_degree_max_dist": (st, [P, ctypes.POINTER(GsEdgeBatch), i32, i64, ctypes.POINTER(GsDegreeOut)]),

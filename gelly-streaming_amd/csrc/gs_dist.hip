@@ -18,7 +18,6 @@
 // bit-exact (the ops are associative and commutative); float sums move within the 1e-5 tolerance.
 // RCCL is resolved at gs_comm_init time (dlopen / the process's already-loaded RCCL, e.g. torch's), so
 // libgellyhip.so itself has no RCCL dependency.
-#include <dlfcn.h>
 #include <string.h>
 
 #include <string>
@@ -261,139 +260,6 @@ __global__ void k_send_rows(const unsigned long long* __restrict__ totals, const
   }
 }
 
-// ---- RCCL, resolved at run time -----------------------------------------------------------------------
-// ncclUniqueId is 128 bytes; ncclComm_t an opaque pointer; the enums below are RCCL's values.
-typedef void* nccl_comm_t;
-struct NcclApi {
-  int (*GetUniqueId)(void*) = nullptr;
-  int (*CommInitRank)(nccl_comm_t*, int, /* ncclUniqueId by value */ struct NcclId, int) = nullptr;
-  int (*CommDestroy)(nccl_comm_t) = nullptr;
-  int (*Send)(const void*, size_t, int, int, nccl_comm_t, hipStream_t) = nullptr;
-  int (*Recv)(void*, size_t, int, int, nccl_comm_t, hipStream_t) = nullptr;
-  int (*AllToAll)(const void*, void*, size_t, int, nccl_comm_t, hipStream_t) = nullptr;
-  int (*AllReduce)(const void*, void*, size_t, int, int, nccl_comm_t, hipStream_t) = nullptr;
-  int (*GroupStart)() = nullptr;
-  int (*GroupEnd)() = nullptr;
-  const char* (*GetErrorString)(int) = nullptr;
-  bool ok = false;
-};
-struct NcclId {
-  char internal[128];
-};
-constexpr int NCCL_UINT8 = 1, NCCL_UINT64 = 5, NCCL_SUM = 0;   // ncclUint8, ncclUint64, ncclSum
-
-// resolved once per process; a function-local static is initialised exactly once even when several
-// ctxs (Flink subtask threads) reach it concurrently
-static NcclApi load_nccl() {
-  NcclApi api;
-  void* h = nullptr;
-  if (dlsym(RTLD_DEFAULT, "ncclCommInitRank")) h = RTLD_DEFAULT;   // already loaded (e.g. by torch)
-  if (!h) h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
-  if (!h) h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
-  if (!h) return api;
-  auto sym = [&](const char* n) { return dlsym(h, n); };
-  api.GetUniqueId = (int (*)(void*))sym("ncclGetUniqueId");
-  api.CommInitRank = (int (*)(nccl_comm_t*, int, NcclId, int))sym("ncclCommInitRank");
-  api.CommDestroy = (int (*)(nccl_comm_t))sym("ncclCommDestroy");
-  api.Send = (int (*)(const void*, size_t, int, int, nccl_comm_t, hipStream_t))sym("ncclSend");
-  api.Recv = (int (*)(void*, size_t, int, int, nccl_comm_t, hipStream_t))sym("ncclRecv");
-  api.AllToAll = (int (*)(const void*, void*, size_t, int, nccl_comm_t, hipStream_t))sym("ncclAllToAll");
-  api.AllReduce = (int (*)(const void*, void*, size_t, int, int, nccl_comm_t, hipStream_t))sym("ncclAllReduce");
-  api.GroupStart = (int (*)())sym("ncclGroupStart");
-  api.GroupEnd = (int (*)())sym("ncclGroupEnd");
-  api.GetErrorString = (const char* (*)(int))sym("ncclGetErrorString");
-  api.ok = api.GetUniqueId && api.CommInitRank && api.CommDestroy && api.Send && api.Recv && api.AllToAll &&
-           api.AllReduce && api.GroupStart && api.GroupEnd && api.GetErrorString;
-  return api;
-}
-
-static NcclApi& nccl() {
-  static NcclApi api = load_nccl();
-  return api;
-}
-
-static gs_status nccl_check(gs_ctx* c, int r, const char* what) {
-  if (r == 0) return GS_OK;
-  return set_error(c, GS_ECOMM, "%s: %s", what, nccl().GetErrorString ? nccl().GetErrorString(r) : "RCCL error");
-}
-
-// exchange owner-grouped rows: send[p] rows of `row` bytes to peer p, receive recv[p] from each
-gs_status exchange_rows(gs_ctx* c, const char* sendbuf, const uint64_t* send, char* recvbuf, const uint64_t* recv,
-                               size_t row) {
-  NcclApi& A = nccl();
-  const int P = c->comm_size;
-  GS_TRY(nccl_check(c, A.GroupStart(), "ncclGroupStart"));
-  uint64_t so = 0, ro = 0;
-  for (int p = 0; p < P; ++p) {
-    if (send[p]) GS_TRY(nccl_check(c, A.Send(sendbuf + so * row, send[p] * row, NCCL_UINT8, p, c->comm, c->stream), "ncclSend"));
-    if (recv[p]) GS_TRY(nccl_check(c, A.Recv(recvbuf + ro * row, recv[p] * row, NCCL_UINT8, p, c->comm, c->stream), "ncclRecv"));
-    so += send[p];
-    ro += recv[p];
-  }
-  return nccl_check(c, A.GroupEnd(), "ncclGroupEnd");
-}
-
-gs_status comm_allreduce(gs_ctx* c, void* buf, size_t count, int nccl_dtype, int nccl_op) {
-  if (!c->comm) return set_error(c, GS_EINVAL, "no communicator (gs_comm_init)");
-  return nccl_check(c, nccl().AllReduce(buf, buf, count, nccl_dtype, nccl_op, c->comm, c->stream), "ncclAllReduce");
-}
-
-// Status agreement before the next collective: every rank reports whether its local step failed
-// (all-reduce MAX of one flag), so a failure on one rank ends the call on all of them with an error
-// instead of leaving the others blocked in a collective.  Returns the local status (its message kept),
-// GS_ECOMM when only another rank failed.
-gs_status comm_agree(gs_ctx* c, gs_status local) {
-  if (!c->comm) return local;
-  const std::string msg = c->err;
-  GS_TRY(ensure(c, c->dist_x, 64 + (size_t)c->comm_size * 32));
-  uint64_t* d = c->dist_x.as<uint64_t>() + 1;
-  c->host_small[200] = local != GS_OK ? 1 : 0;
-  GS_HIP(hipMemcpyAsync(d, c->host_small + 200, 8, hipMemcpyHostToDevice, c->stream));
-  GS_TRY(nccl_check(c, nccl().AllReduce(d, d, 1, NCCL_UINT64, NCCL_OP_MAX, c->comm, c->stream), "ncclAllReduce(status)"));
-  GS_HIP(hipMemcpyAsync(c->host_small + 201, d, 8, hipMemcpyDeviceToHost, c->stream));
-  GS_TRY(host_wait(c));
-  if (local != GS_OK) return set_error(c, local, "%s", msg.c_str());
-  if (c->host_small[201]) return set_error(c, GS_ECOMM, "another rank failed its local step of the window");
-  return GS_OK;
-}
-
-// every rank's u64 -> all[0 .. comm_size) on the host (a sum of one-hot rows)
-gs_status comm_allgather_u64(gs_ctx* c, uint64_t mine, uint64_t* all) {
-  if (!c->comm) return set_error(c, GS_EINVAL, "no communicator (gs_comm_init)");
-  const int P = c->comm_size;
-  GS_TRY(ensure(c, c->dist_cnt, 1024 + (size_t)P * 8));
-  uint64_t* d = (uint64_t*)(c->dist_cnt.as<char>() + 512);
-  GS_HIP(hipMemsetAsync(d, 0, P * 8, c->stream));
-  c->host_small[100] = mine;   // pinned source (HOST_SMALL_WORDS = 512; results land in [8, 8 + P))
-  GS_HIP(hipMemcpyAsync(d + c->comm_rank, c->host_small + 100, 8, hipMemcpyHostToDevice, c->stream));
-  GS_TRY(nccl_check(c, nccl().AllReduce(d, d, P, NCCL_UINT64, NCCL_SUM, c->comm, c->stream), "ncclAllReduce"));
-  GS_HIP(hipMemcpyAsync(c->host_small + 8, d, P * 8, hipMemcpyDeviceToHost, c->stream));
-  GS_TRY(host_wait(c));
-  memcpy(all, c->host_small + 8, P * 8);
-  return GS_OK;
-}
-
-// every rank's `mine` rows (row bytes each) concatenated in rank order into recvbuf; counts[p] = rows of
-// rank p (comm_allgather_u64)
-gs_status comm_allgatherv(gs_ctx* c, const void* sendbuf, char* recvbuf, const uint64_t* counts, size_t row) {
-  NcclApi& A = nccl();
-  const int P = c->comm_size, me = c->comm_rank;
-  uint64_t off = 0;
-  std::vector<uint64_t> at(P);
-  for (int p = 0; p < P; ++p) {
-    at[p] = off;
-    off += counts[p];
-  }
-  if (counts[me]) GS_HIP(hipMemcpyAsync(recvbuf + at[me] * row, sendbuf, counts[me] * row, hipMemcpyDeviceToDevice, c->stream));
-  GS_TRY(nccl_check(c, A.GroupStart(), "ncclGroupStart"));
-  for (int p = 0; p < P; ++p) {
-    if (p == me) continue;
-    if (counts[me]) GS_TRY(nccl_check(c, A.Send(sendbuf, counts[me] * row, NCCL_UINT8, p, c->comm, c->stream), "ncclSend"));
-    if (counts[p]) GS_TRY(nccl_check(c, A.Recv(recvbuf + at[p] * row, counts[p] * row, NCCL_UINT8, p, c->comm, c->stream), "ncclRecv"));
-  }
-  return nccl_check(c, A.GroupEnd(), "ncclGroupEnd");
-}
-
 }  // namespace gs
 
 using namespace gs;
@@ -526,58 +392,6 @@ gs_status gs_merge_degree_max_partials(gs_ctx* c, const gs_partial_batch* p, int
   return host_wait(c);
 }
 
-// ---- ctx-owned RCCL communicator ----------------------------------------------------------------------
-gs_status gs_comm_unique_id(void* id128) {
-  if (!id128) return GS_EINVAL;
-  NcclApi& A = nccl();
-  if (!A.ok) return GS_ECOMM;
-  return A.GetUniqueId(id128) == 0 ? GS_OK : GS_ECOMM;
-}
-
-gs_status gs_comm_init(gs_ctx* c, int32_t nranks, int32_t rank, const void* id128) {
-  if (!c) return GS_EINVAL;
-  if (!id128 || nranks < 1 || nranks > OW_MAXP || rank < 0 || rank >= nranks)
-    return set_error(c, GS_EINVAL, "bad communicator arguments (%d ranks, rank %d)", nranks, rank);
-  NcclApi& A = nccl();
-  if (!A.ok) return set_error(c, GS_ECOMM, "RCCL not found (librccl.so.1)");
-  if (c->comm) {
-    A.CommDestroy(c->comm);
-    c->comm = nullptr;
-  }
-  GS_HIP(hipSetDevice(c->device));
-  NcclId id;
-  memcpy(id.internal, id128, 128);
-  nccl_comm_t comm = nullptr;
-  GS_TRY(nccl_check(c, A.CommInitRank(&comm, nranks, id, rank), "ncclCommInitRank"));
-  c->comm = comm;
-  c->comm_size = nranks;
-  c->comm_rank = rank;
-  return GS_OK;
-}
-
-gs_status gs_comm_destroy(gs_ctx* c) {
-  if (!c) return GS_EINVAL;
-  if (c->comm && nccl().ok) nccl().CommDestroy(c->comm);
-  c->comm = nullptr;
-  c->comm_size = 0;
-  return GS_OK;
-}
-
-// exact triangle count etc. add up over ranks: all-reduce (sum) of one u64
-gs_status gs_comm_allreduce_sum_u64(gs_ctx* c, uint64_t* value) {
-  if (!c || !value) return GS_EINVAL;
-  if (!c->comm) return set_error(c, GS_EINVAL, "no communicator (gs_comm_init)");
-  GS_TRY(ensure(c, c->dist_cnt, 1024));
-  uint64_t* d = c->dist_cnt.as<uint64_t>();
-  c->host_small[8] = *value;
-  GS_HIP(hipMemcpyAsync(d, c->host_small + 8, 8, hipMemcpyHostToDevice, c->stream));
-  GS_TRY(nccl_check(c, nccl().AllReduce(d, d, 1, NCCL_UINT64, NCCL_SUM, c->comm, c->stream), "ncclAllReduce"));
-  GS_HIP(hipMemcpyAsync(c->host_small + 8, d, 8, hipMemcpyDeviceToHost, c->stream));
-  GS_TRY(host_wait(c));
-  *value = c->host_small[8];
-  return GS_OK;
-}
-
 // partials of this rank's slice -> all-to-all over the ctx's communicator -> the merge of what this
 // rank owns.  Per window: the local reduce (the bucket path's own read-back), the owner partition on the
 // device, ONE all-to-all of [rows, flags] per peer read back together (the only host wait of the
@@ -637,7 +451,7 @@ static gs_status dist_impl(gs_ctx* c, const gs_edge_batch* b, int32_t dir, int32
     GS_HIP(hipMemcpyAsync(sendc, c->host_small + 8, (size_t)P * 16, hipMemcpyHostToDevice, c->stream));
   }
   // 2. the one exchange of sizes + flags; read back with this rank's own send counts
-  GS_TRY(nccl_check(c, nccl().AllToAll(sendc, recvc, 2, NCCL_UINT64, c->comm, c->stream), "ncclAllToAll(counts)"));
+  GS_TRY(comm_alltoall(c, sendc, recvc, 2, NCCL_T_U64));
   GS_HIP(hipMemcpyAsync(c->host_small + 8, sendc, (size_t)P * 32, hipMemcpyDeviceToHost, c->stream));
   GS_TRY(host_wait(c));
   std::vector<uint64_t> send(P), recv(P);

@@ -97,6 +97,7 @@ struct gs_ctx {
   uint64_t rt_n = ~0ull, rt_seq = 0;
   uint32_t rt_nparts = 0;
   gs::DevBuf tri_bd[4];
+  gs::DevBuf tri_rl[4];          // split-window triangles over wide ids: compact columns, local / all ids
   // HashSet-order pipeline (gs_hashset.hip)
   gs::DevBuf hs[40];
   // bucket path (gs_bucket.hip): plan tables, work items, LDS slabs of multi-item buckets
@@ -121,10 +122,13 @@ struct gs_ctx {
   // edge text parser (gs_text.hip): staged text, tile newline counts, record starts
   gs::DevBuf tx_text, tx_cnt, tx_starts;
   // multi-GPU keyBy (gs_dist.hip): staging of the local reduce, owner-grouped partials, received rows,
-  // per-tile owner counts; the ctx-owned RCCL communicator (opaque ncclComm_t)
+  // per-tile owner counts; the ctx communicator (gs_comm.hip): an RCCL ncclComm_t (comm_kind
+  // GS_COMM_KIND_RCCL) or an in-process gs_comm_group (GS_COMM_KIND_GROUP; comm_scratch: its all-reduce)
   gs::DevBuf dist_k, dist_v, dist_v2, dist_k2, dist_v3, dist_v4, dist_cnt, dist_x, dist_x2;
   void* comm = nullptr;
+  int comm_kind = 0;
   int comm_size = 0, comm_rank = 0;
+  gs::DevBuf comm_scratch;
   // relabeling of arbitrary vertex IDs (gs_relabel.hip)
   gs::DevBuf rl[8];
   // Zipf generator: CDF table of (zipf_v, zipf_s)
@@ -191,11 +195,13 @@ gs_status hashset_order(gs_ctx* c, const int64_t* src, const int64_t* dst, uint6
 gs_status triangle_selfpair_term(gs_ctx* c, const int64_t* src, const int64_t* dst, uint64_t n,
                                  const uint32_t* loops, uint64_t loops_xor, const int64_t* relabel, uint64_t nrel,
                                  uint64_t* S);
-// ctx communicator helpers (gs_dist.hip; RCCL enums: ncclInt64 4, ncclUint32 3, ncclUint64 5; ncclSum 0,
+// ctx communicator helpers (gs_comm.hip; RCCL enums: ncclInt64 4, ncclUint32 3, ncclUint64 5; ncclSum 0,
 // ncclMax 2, ncclMin 3): in-place all-reduce of a device buffer; every rank's u64 to the host;
 // grouped send / recv of owner-grouped rows
 constexpr int NCCL_T_U32 = 3, NCCL_T_I64 = 4, NCCL_T_U64 = 5, NCCL_OP_SUM = 0, NCCL_OP_MAX = 2, NCCL_OP_MIN = 3;
+constexpr int GS_COMM_KIND_RCCL = 1, GS_COMM_KIND_GROUP = 2;
 gs_status comm_allreduce(gs_ctx* c, void* buf, size_t count, int nccl_dtype, int nccl_op);
+gs_status comm_alltoall(gs_ctx* c, const void* send, void* recv, size_t count, int nccl_dtype);
 gs_status comm_allgather_u64(gs_ctx* c, uint64_t mine, uint64_t* all);
 gs_status comm_agree(gs_ctx* c, gs_status local);
 gs_status exchange_rows(gs_ctx* c, const char* sendbuf, const uint64_t* send, char* recvbuf, const uint64_t* recv,
@@ -207,6 +213,10 @@ gs_status xscan(gs_ctx* c, const uint64_t* in, uint64_t n, uint64_t* out);
 // *V sorted distinct IDs *uniq (device buffers of the ctx, valid until the next relabel)
 gs_status relabel_endpoints(gs_ctx* c, const int64_t* a, const int64_t* b, uint64_t n, const int64_t** ca,
                             const int64_t** cb, const int64_t** uniq, uint64_t* V);
+// local compact columns ca / cb (ranks among the nloc sorted distinct ids loc) -> ranks among the ng
+// sorted distinct ids G (loc ⊂ G), in place; map: nloc u32 of scratch
+gs_status relabel_to_global(gs_ctx* c, const int64_t* loc, uint64_t nloc, const int64_t* G, uint64_t ng, uint32_t* map,
+                            int64_t* ca, int64_t* cb, uint64_t n);
 // Bucket path (gs_bucket.hip) for the associative built-ins; GS_EUNSUPPORTED (no message) when the
 // window or op does not fit it and the caller should take the sort path.  keys/vals: device.
 gs_status bucket_reduce(gs_ctx* c, const int64_t* src, const int64_t* dst, const void* val, uint64_t n, int dir,

@@ -93,4 +93,41 @@ gs_status relabel_endpoints(gs_ctx* c, const int64_t* a, const int64_t* b, uint6
   return GS_OK;
 }
 
+// Compact ids of a window split over ranks (gs_window_triangles_dist): a rank's local compact ids
+// (relabel_endpoints over its own records: ranks among ITS distinct ids) become ranks among the WHOLE
+// window's sorted distinct ids G (every rank's distinct ids all-gathered and relabeled the same way, so
+// every rank holds the same G).  Each local distinct id is searched in G once; the columns are gathered
+// through that map in place.
+__global__ __launch_bounds__(256) void k_rl_rank(const int64_t* __restrict__ loc, uint64_t nloc,
+                                                 const int64_t* __restrict__ G, uint64_t ng, uint32_t* __restrict__ map) {
+  for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < nloc; i += (uint64_t)gridDim.x * 256) {
+    const int64_t x = loc[i];
+    uint64_t lo = 0, hi = ng;   // first position with G[p] >= x (x is in G)
+    while (lo < hi) {
+      const uint64_t mid = (lo + hi) >> 1;
+      if (G[mid] < x) lo = mid + 1;
+      else hi = mid;
+    }
+    map[i] = (uint32_t)lo;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_rl_map(int64_t* __restrict__ ca, int64_t* __restrict__ cb, uint64_t n,
+                                                const uint32_t* __restrict__ map) {
+  for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) {
+    ca[i] = map[ca[i]];
+    cb[i] = map[cb[i]];
+  }
+}
+
+gs_status relabel_to_global(gs_ctx* c, const int64_t* loc, uint64_t nloc, const int64_t* G, uint64_t ng, uint32_t* map,
+                            int64_t* ca, int64_t* cb, uint64_t n) {
+  if (!n) return GS_OK;
+  const unsigned gl = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((nloc + 255) / 256, 8192));
+  const unsigned g = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((n + 255) / 256, 8192));
+  hipLaunchKernelGGL(k_rl_rank, dim3(gl), dim3(256), 0, c->stream, loc, nloc, G, ng, map);
+  hipLaunchKernelGGL(k_rl_map, dim3(g), dim3(256), 0, c->stream, ca, cb, n, (const uint32_t*)map);
+  return hip_check(c, hipGetLastError(), "relabel_to_global");
+}
+
 }  // namespace gs

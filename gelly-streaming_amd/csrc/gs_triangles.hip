@@ -1214,6 +1214,52 @@ gs_status dist_stage(gs_ctx* c, const gs_edge_batch* b, TriGeom* g) {
   return GS_OK;
 }
 
+// Split window over ids that span more than 2^TRI_MAX_BITS values (any Long key,
+// SimpleEdgeStream.java:173-183): every rank relabels its records to ranks among the WHOLE window's
+// sorted distinct ids -- its own distinct ids (relabel_endpoints), all-gathered, relabeled again on every
+// rank (the same G everywhere), then each local id searched in G once.  Order-preserving, as the
+// single-GPU relabel (tri_geometry), so the orientation ties and the count are unchanged.  *lb: this
+// rank's compact columns (device, the ctx's tri_rl), *vmax = |G| - 1.
+gs_status tri_dist_relabel(gs_ctx* c, const gs_edge_batch* b, gs_edge_batch* lb, int64_t* vmax) {
+  const uint32_t P = (uint32_t)c->comm_size;
+  const uint64_t n = b->n;
+  uint64_t nloc = 0;
+  gs_status st = GS_OK;
+  if (n) {
+    const int64_t *src = nullptr, *dst = nullptr, *ca = nullptr, *cb = nullptr, *uq = nullptr;
+    const void* val;
+    st = stage_batch(c, b, &src, &dst, &val, false);
+    if (st == GS_OK) st = relabel_endpoints(c, src, dst, n, &ca, &cb, &uq, &nloc);
+    if (st == GS_OK) st = ensure(c, c->tri_rl[0], n * 8 + 8);
+    if (st == GS_OK) st = ensure(c, c->tri_rl[1], n * 8 + 8);
+    if (st == GS_OK) st = ensure(c, c->tri_rl[2], nloc * 8 + 8);
+    if (st == GS_OK) st = hip_check(c, hipMemcpyAsync(c->tri_rl[0].p, ca, n * 8, hipMemcpyDeviceToDevice, c->stream), "relabel");
+    if (st == GS_OK) st = hip_check(c, hipMemcpyAsync(c->tri_rl[1].p, cb, n * 8, hipMemcpyDeviceToDevice, c->stream), "relabel");
+    if (st == GS_OK) st = hip_check(c, hipMemcpyAsync(c->tri_rl[2].p, uq, nloc * 8, hipMemcpyDeviceToDevice, c->stream), "relabel");
+  }
+  GS_TRY(comm_agree(c, st));
+  std::vector<uint64_t> cnt(P);
+  GS_TRY(comm_allgather_u64(c, nloc, cnt.data()));
+  uint64_t T = 0;
+  for (uint32_t p = 0; p < P; ++p) T += cnt[p];
+  GS_TRY(ensure(c, c->tri_rl[3], T * 8 + 8));
+  GS_TRY(comm_allgatherv(c, c->tri_rl[2].p, c->tri_rl[3].as<char>(), cnt.data(), 8));
+  const int64_t *ga = nullptr, *gb = nullptr, *G = nullptr;
+  uint64_t ng = 0;
+  st = T ? relabel_endpoints(c, c->tri_rl[3].as<int64_t>(), c->tri_rl[3].as<int64_t>(), T, &ga, &gb, &G, &ng) : GS_OK;
+  if (st == GS_OK && ng > (1ull << TRI_MAX_BITS))
+    st = set_error(c, GS_EUNSUPPORTED, "split window triangles: %llu distinct vertices (> 2^%llu)", (unsigned long long)ng,
+                   (unsigned long long)TRI_MAX_BITS);
+  // (the gathered ids are consumed: tri_rl[3] holds the map)
+  if (st == GS_OK && n)
+    st = relabel_to_global(c, c->tri_rl[2].as<int64_t>(), nloc, G, ng, c->tri_rl[3].as<uint32_t>(), c->tri_rl[0].as<int64_t>(),
+                           c->tri_rl[1].as<int64_t>(), n);
+  GS_TRY(comm_agree(c, st));
+  *lb = gs_edge_batch{c->tri_rl[0].as<int64_t>(), c->tri_rl[1].as<int64_t>(), nullptr, n, GS_NONE, GS_MEM_DEVICE, 0};
+  *vmax = ng ? (int64_t)ng - 1 : 0;
+  return GS_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -1635,19 +1681,30 @@ gs_status gs_window_triangles_dist(gs_ctx* c, const gs_edge_batch* b, uint64_t* 
   GS_TRY(comm_allreduce(c, dmm + 1, 1, NCCL_T_I64, NCCL_OP_MAX));
   GS_HIP(hipMemcpyAsync(c->host_small + 12, dmm, 16, hipMemcpyDeviceToHost, c->stream));
   GS_TRY(host_wait(c));
-  const int64_t gmin = (int64_t)c->host_small[12], gmax = (int64_t)c->host_small[13];
+  int64_t gmin = (int64_t)c->host_small[12], gmax = (int64_t)c->host_small[13];
   uint64_t total_n = b->n;
   GS_TRY(gs_comm_allreduce_sum_u64(c, &total_n));
   *count = 0;
   *count_ref_wrapped = 0;
   *has_output = total_n > 0;
   if (total_n == 0) return GS_OK;
+  // ids spanning more than 2^TRI_MAX_BITS values: steps 2-5 run on compact ids of the whole window
+  // (step 6, the self-pair term, keeps the original records: its HashSet order needs the values)
+  const gs_edge_batch* lb = b;
+  gs_edge_batch rb{};
+  if (const uint64_t dx = (uint64_t)gmin ^ (uint64_t)gmax; dx && 64 - __builtin_clzll(dx) > (int)TRI_MAX_BITS) {
+    int64_t vmax = 0;
+    GS_TRY(tri_dist_relabel(c, b, &rb, &vmax));
+    lb = &rb;
+    gmin = 0;
+    gmax = vmax;
+  }
   // 2. degrees, summed over ranks
   uint64_t V = 0;
-  gs_status st = gs_tri_dist_degrees(c, b, gmin, gmax, nullptr, &V);
+  gs_status st = gs_tri_dist_degrees(c, lb, gmin, gmax, nullptr, &V);
   if (st == GS_OK) st = ensure(c, c->tri_d[1], V * 4);
   uint32_t* deg = c->tri_d[1].as<uint32_t>();
-  if (st == GS_OK) st = gs_tri_dist_degrees(c, b, gmin, gmax, deg, &V);
+  if (st == GS_OK) st = gs_tri_dist_degrees(c, lb, gmin, gmax, deg, &V);
   GS_TRY(comm_agree(c, st));
   GS_TRY(comm_allreduce(c, deg, V, NCCL_T_U32, NCCL_OP_SUM));
   // 3. oriented edges; their raw out-degrees summed (the route's owner ranges cut the raw work in equal
@@ -1656,9 +1713,9 @@ gs_status gs_window_triangles_dist(gs_ctx* c, const gs_edge_batch* b, uint64_t* 
   uint64_t loops = 0;
   GS_TRY(ensure(c, c->tri_d[6], V * 4 + 4));
   uint32_t* dout = c->tri_d[6].as<uint32_t>();
-  GS_TRY(comm_agree(c, gs_tri_dist_orient(c, b, deg, dout, &loops)));
+  GS_TRY(comm_agree(c, gs_tri_dist_orient(c, lb, deg, dout, &loops)));
   GS_TRY(comm_allreduce(c, dout, V, NCCL_T_U32, NCCL_OP_SUM));
-  st = ensure(c, c->tri_d[2], b->n * 8 + 8);
+  st = ensure(c, c->tri_d[2], lb->n * 8 + 8);
   if (st == GS_OK) st = gs_tri_dist_route(c, dout, P, c->tri_d[2].as<uint64_t>(), send.data());
   GS_TRY(comm_agree(c, st));
   GS_TRY(ensure(c, c->tri_d[0], 64 + (size_t)P * P * 8));

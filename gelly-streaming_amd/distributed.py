@@ -181,6 +181,20 @@ def _exchange(t, send, recv, cdev, home, group):
     return out.to(home)
 
 
+TRI_MAX_BITS = 28   # gs_triangles.hip: the composite-key budget of one id
+
+
+def relabel_window(src, dst, group=None):
+    """Ids spanning more than 2^TRI_MAX_BITS values (any Long key, SimpleEdgeStream.java:173-183): the
+    order-preserving compact ids of the WHOLE window -- every rank's distinct ids all-gathered, the
+    sorted union G the same on every rank, each endpoint replaced by its rank in G (what
+    gs_window_triangles_dist does inside the library).  Returns (src, dst, |G| - 1)."""
+    mine = torch.unique(torch.cat([src, dst]))
+    a, _ = gather_window(mine, mine, group)
+    G = torch.unique(a)
+    return torch.searchsorted(G, src), torch.searchsorted(G, dst), int(G.numel()) - 1
+
+
 def triangles_window(eng, src, dst, group=None):
     """WindowTriangles over a window whose records are split across the ranks of `group` (SURVEY.md §8e,
     WindowTriangles.java:61-66).  The six steps of include/gelly_hip.h's gs_tri_dist_* with the
@@ -211,6 +225,10 @@ def triangles_window(eng, src, dst, group=None):
     gmin, gmax, total = int(lo_t[0]), int(hi_t[0]), int(nt[0])
     if total == 0:
         return 0, 0, False
+    osrc, odst = src, dst   # the self-pair term (step 6) needs the original ids: their HashSet order
+    if ((gmin ^ gmax) & ((1 << 64) - 1)).bit_length() > TRI_MAX_BITS:
+        src, dst, gmax = relabel_window(src, dst, group)
+        gmin = 0
     deg = eng.tri_dist_degrees(src, dst, gmin, gmax)
     d = deg.to(cdev)
     dist.all_reduce(d, op=dist.ReduceOp.SUM, group=group)
@@ -245,7 +263,7 @@ def triangles_window(eng, src, dst, group=None):
     full = eng.tri_dist_assemble(nbr, crows, rows_in, M)
     T = eng.tri_dist_count(full, dph, rank, world)
     if int(lt[0]):
-        fs, fd = gather_window(src, dst, group)
+        fs, fd = gather_window(osrc, odst, group)
         if rank == 0:
             T += eng.triangles_selfpair(fs, fd)
     t = torch.tensor([T], dtype=torch.int64, device=cdev)

@@ -68,6 +68,31 @@ class StageTimes:
     speculative: int = 0   # path 2: 1 = regions from the previous window's counts, 2 = that missed
 
 
+class CommGroup:
+    """gs_comm_group: P ranks in this process (one Engine per rank, e.g. P ranks on one GPU); the
+    gs_window_*_dist orchestration runs over it exactly as over RCCL (include/gelly_hip.h)."""
+
+    def __init__(self, nranks: int):
+        self._L = L.load()
+        h = ctypes.c_void_p()
+        st = self._L.gs_comm_group_create(int(nranks), ctypes.byref(h))
+        if st != L.GS_OK:
+            raise GsError(st, f"gs_comm_group_create({nranks}) failed")
+        self.handle = h
+        self.nranks = nranks
+
+    def close(self):
+        if getattr(self, "handle", None):
+            self._L.gs_comm_group_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 class Engine:
     def __init__(self, device: int = 0, reserve_edges: int = 0, torch_stream: bool = True, sort_only: bool = False,
                  bk_onesweep: bool = False, no_pack: bool = False, no_spec: bool = False, flags: int = 0):
@@ -565,7 +590,7 @@ class Engine:
     def owner_of(self, vertex: int, nparts: int) -> int:
         return int(self._L.gs_owner_of(int(vertex), nparts))
 
-    # -- ctx-owned RCCL communicator -----------------------------------------------------------------
+    # -- the ctx communicator: RCCL (one rank per process) or an in-process CommGroup ---------------------
     @staticmethod
     def comm_unique_id() -> bytes:
         buf = ctypes.create_string_buffer(128)
@@ -577,6 +602,11 @@ class Engine:
     def comm_init(self, nranks: int, rank: int, unique_id: bytes):
         buf = ctypes.create_string_buffer(bytes(unique_id), 128)
         self._check(self._L.gs_comm_init(self.ctx, nranks, rank, buf))
+
+    def comm_init_group(self, group: "CommGroup", rank: int):
+        """gs_comm_init_group: this ctx becomes rank `rank` of an in-process thread group; every rank's
+        calls then come from its own thread (ctypes releases the GIL for the call)."""
+        self._check(self._L.gs_comm_init_group(self.ctx, group.handle, int(rank)))
 
     def comm_destroy(self):
         self._check(self._L.gs_comm_destroy(self.ctx))

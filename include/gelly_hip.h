@@ -40,7 +40,9 @@
 extern "C" {
 #endif
 
-#define GS_ABI_VERSION 1
+/* 2: gs_tri_dist_route lost two parameters (gs_tri_dist_orient runs first), the JNI candidates
+ *    natives changed return types, and the in-process comm group (gs_comm_group_*) was added. */
+#define GS_ABI_VERSION 2
 
 #if defined(__GNUC__) || defined(__clang__)
 #define GS_API __attribute__((visibility("default")))
@@ -258,7 +260,7 @@ GS_API gs_status gs_window_triangles_part(gs_ctx* ctx, const gs_edge_batch* batc
 /* ---- WindowTriangles over a window split across ranks ------------------------
  * Every rank holds only its own records of the window (the reference's subtasks after slice()).
  * The steps, with the collective the caller runs after each (torch.distributed, the JVM's, or the
- * ctx communicator: gs_window_triangles_dist does all of them with RCCL):
+ * ctx communicator: gs_window_triangles_dist does all of them over RCCL or the comm group):
  *   1. gs_tri_dist_range     local [min, max] id            -> all-reduce min of [0], max of [1]
  *   2. gs_tri_dist_degrees   local raw degrees deg[V]       -> all-reduce (sum, u32) of deg
  *      (deg == NULL: *V only, to size the buffer; V = 2^bits of the common id span, <= 2^28)
@@ -320,7 +322,8 @@ GS_API gs_status gs_tri_dist_count(gs_ctx* ctx, const uint32_t* nbr, uint64_t M,
 /* The self-pair term alone (WindowTriangles.java:105: (x, x) candidates matched by a self-loop on x)
  * of a whole window. */
 GS_API gs_status gs_window_triangles_selfpair(gs_ctx* ctx, const gs_edge_batch* window, uint64_t* S);
-/* Steps 1-6 with the ctx communicator (gs_comm_init); every rank gets the window's count. */
+/* Steps 1-6 with the ctx communicator (gs_comm_init / gs_comm_init_group); every rank gets the
+ * window's count. */
 GS_API gs_status gs_window_triangles_dist(gs_ctx* ctx, const gs_edge_batch* local, uint64_t* count,
                                           int32_t* count_ref_wrapped, int32_t* has_output);
 
@@ -375,14 +378,30 @@ GS_API gs_status gs_merge_partials(gs_ctx* ctx, const gs_partial_batch* partials
 GS_API gs_status gs_merge_degree_max_partials(gs_ctx* ctx, const gs_partial_batch* partials, int64_t init_max,
                                               gs_degree_out* out);
 
-/* ctx-owned RCCL communicator (one rank per ctx; RCCL is loaded at gs_comm_init time).  Rank 0 calls
- * gs_comm_unique_id and ships the 128 bytes to every rank out of band; every rank calls gs_comm_init. */
+/* The ctx communicator: every gs_window_*_dist call and gs_comm_allreduce_sum_u64 run over it.  Two
+ * kinds, the same collectives and results:
+ *  - RCCL (one rank per process and GPU; RCCL is loaded at gs_comm_init time).  Rank 0 calls
+ *    gs_comm_unique_id and ships the 128 bytes to every rank out of band; every rank calls gs_comm_init.
+ *  - an in-process thread group (one rank per ctx, all ctxs in one process, on one or several GPUs):
+ *    gs_comm_group_create once, then gs_comm_init_group(ctx_r, group, r) for every rank r, and each
+ *    rank's calls from its own thread (a JVM driving several GPUs without RCCL; the tests run P ranks
+ *    on one GPU this way).  The group checks that the ranks enter the same collectives with matching
+ *    sizes; a mismatch, a failed copy or a rank missing for GS_COMM_TIMEOUT_MS (env, default 120000)
+ *    breaks the group: every rank's call returns GS_ECOMM.  gs_comm_group_destroy drops the creator's
+ *    reference; the group lives until every ctx has left it (gs_comm_destroy / gs_destroy).
+ * nranks <= GS_COMM_MAX_RANKS. */
+#define GS_COMM_MAX_RANKS 64
+typedef struct gs_comm_group gs_comm_group;
 GS_API gs_status gs_comm_unique_id(void* id128);
 GS_API gs_status gs_comm_init(gs_ctx* ctx, int32_t nranks, int32_t rank, const void* id128);
+GS_API gs_status gs_comm_group_create(int32_t nranks, gs_comm_group** group);
+GS_API void gs_comm_group_destroy(gs_comm_group* group);
+GS_API gs_status gs_comm_init_group(gs_ctx* ctx, gs_comm_group* group, int32_t rank);
 GS_API gs_status gs_comm_destroy(gs_ctx* ctx);
 /* *value = the sum of *value over the communicator's ranks (e.g. per-rank triangle counts). */
 GS_API gs_status gs_comm_allreduce_sum_u64(gs_ctx* ctx, uint64_t* value);
-/* Partials -> RCCL all-to-all (counts, then rows) -> merge: `out` receives the vertices this rank owns. */
+/* Partials -> all-to-all (counts, then rows) over the ctx communicator -> merge: `out` receives the
+ * vertices this rank owns. */
 GS_API gs_status gs_window_reduce_dist(gs_ctx* ctx, const gs_edge_batch* batch, int32_t dir, int32_t op,
                                        const void* init, gs_vertex_out* out);
 GS_API gs_status gs_window_fold_degree_max_dist(gs_ctx* ctx, const gs_edge_batch* batch, int32_t dir,

@@ -22,7 +22,7 @@ public final class GellyHip {
 	private GellyHip() {
 	}
 
-	public static final int GS_ABI_VERSION = 1;
+	public static final int GS_ABI_VERSION = 2;
 
 	/* gs_status */
 	public static final int GS_OK = 0;

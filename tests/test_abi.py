@@ -33,7 +33,10 @@ def test_library_exports_every_declared_symbol(pkg):
 
 def test_abi_version_and_no_device_error(pkg):
     lib = pkg.load_library()
-    assert lib.gs_abi_version() == 1
+    want = int(re.search(r"#define GS_ABI_VERSION (\d+)", HEADER.read_text()).group(1))
+    assert want == 2 and lib.gs_abi_version() == want
+    java = re.search(r"GS_ABI_VERSION = (\d+);", GELLYHIP_JAVA.read_text()).group(1)
+    assert int(java) == want   # the JNI binding refuses a library of another ABI
     import torch
     if not torch.cuda.is_available():
         # lifecycle only: gs_create must fail cleanly (status, no abort) when no HIP device exists

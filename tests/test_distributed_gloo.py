@@ -206,12 +206,8 @@ class OracleTriEngine:
     def triangles_selfpair(self, src, dst):
         """reference rule minus the simple graph's triangles (this pipeline on the whole window)"""
         s, d = self._np(src), self._np(dst)
-        lo, hi = self.tri_dist_range(s, d)
-        deg = self.tri_dist_degrees(s, d, lo, hi)
-        dout, _ = self.tri_dist_orient(s, d, deg)
-        k, _ = self.tri_dist_route(dout, 1)
-        nbr, dp = self.tri_dist_build(k, len(deg))
-        return self.orc.window_triangles_ref(s, d)[1] - self.tri_dist_count(nbr, dp, 0, 1)
+        keep = s != d
+        return self.orc.window_triangles_ref(s, d)[1] - self.orc.window_triangles_fwd(s[keep], d[keep])[1]
 
 
 def candidate_groups(a, b, f):
@@ -436,3 +432,56 @@ def test_split_window_triangles_boundary_exchange(oracle, world):
         assert bnd <= full, (r, bnd, full)
     # over the ranks, far less than every rank receiving every other rank's rows
     assert sum(out[r][1] for r in range(world)) < 0.8 * sum(out[r][2] for r in range(world)), out
+
+
+def _sparse(x):
+    """an order-preserving injective map of small ids onto Long ids spanning more than 2^52 values"""
+    return x * ((1 << 40) + 12345) - (1 << 60)
+
+
+def _tri_sparse_worker(rank, world, port, q):
+    sys.path.insert(0, str(ROOT))
+    import __graft_entry__ as ge
+    ge.load_package()
+    from gelly_streaming_amd import distributed as D
+    orc = ge.load_oracle()
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    te = OracleTriEngine(orc)
+    out = {}
+    n = 9000
+    ts, td = orc.gen_rmat(12, n, 0x5EED0E, no_self_loops=True, first_edge=rank * n)
+    out["sparse"] = D.triangles_window(te, torch.from_numpy(_sparse(ts)), torch.from_numpy(_sparse(td)))
+    ls, ld = orc.gen_rmat(9, 3000, 0x5EED0F, first_edge=rank * 3000)
+    out["sparse_loops"] = D.triangles_window(te, torch.from_numpy(_sparse(ls)), torch.from_numpy(_sparse(ld)))
+    q.put((rank, out))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_split_window_triangles_sparse_long_ids():
+    """Split-window WindowTriangles over Long ids spanning more than 2^52 values (SimpleEdgeStream.java
+    :173-183 keys any Long): the ranks relabel to the whole window's compact ids (relabel_window: distinct
+    ids all-gathered) and count the whole window's triangles; with self-loops the self-pair term keeps
+    the original ids (its HashSet order)."""
+    import __graft_entry__ as ge
+    orc = ge.load_oracle()
+    world, port = 3, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_tri_sparse_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = dict(q.get(timeout=300) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    ts, td = orc.gen_rmat(12, 9000 * world, 0x5EED0E, no_self_loops=True)
+    w, ex, _ = orc.window_triangles_fwd(_sparse(ts), _sparse(td))
+    assert ex > 0 and (w, ex) == orc.window_triangles_fwd(ts, td)[:2]
+    ls, ld = orc.gen_rmat(9, 3000 * world, 0x5EED0F)
+    assert (ls == ld).any()
+    lw, lex, _, tree = orc.window_triangles_ref(_sparse(ls), _sparse(ld))
+    for r in range(world):
+        assert out[r]["sparse"] == (ex, w, True), (r, out[r]["sparse"], ex)
+        assert out[r]["sparse_loops"] == (lex, lw, True), (r, out[r]["sparse_loops"], lex)
