@@ -209,3 +209,26 @@ def test_group_rejects_a_rank_twice(pkg):
             b.comm_init_group(grp, 2)
         b.comm_init_group(grp, 1)
     grp.close()
+
+
+def test_split_window_s20_four_ranks(pkg, oracle):
+    """A larger split window (R-MAT s20, 2^24 edges, Graph500 skew) over 4 ranks: reduceOnEdges Long SUM
+    (ALL) and the degree / max-neighbour fold against the whole-window oracle, WindowTriangles against the
+    oracle's forward count."""
+    P, n = 4, 1 << 24
+    s, d = oracle.gen_rmat(20, n, 0x5EED10, no_self_loops=True)
+    v = oracle.gen_values(n, 0x5EED10, oracle.DT_I64)
+    sl = slices(n, P)
+
+    def fn(r, e):
+        a, b = sl[r]
+        return (e.reduce_dist(s[a:b], d[a:b], v[a:b], 2, 0), e.fold_degree_max_dist(s[a:b], d[a:b], 1),
+                e.triangles_dist(s[a:b], d[a:b]))
+
+    res, errs = run_group(pkg, P, fn)
+    assert not errs, errs
+    check_union([res[r][0] for r in range(P)], oracle.window_reduce_mt(s, d, v, 2, 0), P)
+    check_union([res[r][1] for r in range(P)], oracle.window_fold_degree_max(s, d, 1), P)
+    w, ex, has = oracle.window_triangles_fwd(s, d)
+    for r in range(P):
+        assert res[r][2] == (ex, w, has), (r, res[r][2], ex)
