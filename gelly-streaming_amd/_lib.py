@@ -32,7 +32,7 @@ GS_DTYPE_OF = {np.dtype(np.int32): GS_I32, np.dtype(np.int64): GS_I64, np.dtype(
                np.dtype(np.float64): GS_F64}
 
 # every symbol include/gelly_hip.h declares (checked by tests/test_abi.py)
-EXPORTS = ("gs_abi_version", "gs_create", "gs_destroy", "gs_last_error", "gs_set_stream", "gs_set_timing", "gs_synchronize",
+EXPORTS = ("gs_abi_version", "gs_device_count", "gs_create", "gs_destroy", "gs_last_error", "gs_set_stream", "gs_set_timing", "gs_synchronize",
            "gs_alloc_pinned", "gs_free_pinned", "gs_window_reduce", "gs_window_fold",
            "gs_window_fold_degree_max", "gs_window_csr", "gs_window_candidates", "gs_window_candidates_part",
            "gs_window_triangles",
@@ -46,7 +46,7 @@ EXPORTS = ("gs_abi_version", "gs_create", "gs_destroy", "gs_last_error", "gs_set
            "gs_comm_allreduce_sum_u64", "gs_window_reduce_dist", "gs_window_fold_degree_max_dist",
            "gs_stream_create", "gs_stream_destroy", "gs_stream_append", "gs_stream_watermark", "gs_stream_flush",
            "gs_stream_poll", "gs_stream_stats", "gs_generate_rmat", "gs_generate_uniform", "gs_generate_zipf", "gs_generate_values", "gs_last_stage_times",
-           "gs_set_max_window_records", "gs_candidates_begin", "gs_candidates_next", "gs_candidates_seek",
+           "gs_set_max_window_records", "gs_candidates_begin", "gs_candidates_begin_part", "gs_candidates_next", "gs_candidates_seek",
            "gs_candidates_vertex_range")
 
 P = ctypes.c_void_p
@@ -157,6 +157,7 @@ def load() -> ctypes.CDLL:
     st = ctypes.c_int32
     sigs = {
         "gs_abi_version": (i32, []),
+        "gs_device_count": (st, [ctypes.POINTER(i32)]),
         "gs_create": (st, [ctypes.POINTER(GsConfig), ctypes.POINTER(P)]),
         "gs_destroy": (None, [P]),
         "gs_last_error": (ctypes.c_char_p, [P]),
@@ -223,6 +224,8 @@ def load() -> ctypes.CDLL:
         "gs_last_stage_times": (st, [P, ctypes.POINTER(GsStageTimes)]),
         "gs_set_max_window_records": (st, [P, u64]),
         "gs_candidates_begin": (st, [P, ctypes.POINTER(GsEdgeBatch), ctypes.POINTER(u64), ctypes.POINTER(u32)]),
+        "gs_candidates_begin_part": (st, [P, ctypes.POINTER(GsEdgeBatch), u32, u32, ctypes.POINTER(u64),
+                                          ctypes.POINTER(u32)]),
         "gs_candidates_next": (st, [P, ctypes.POINTER(GsPairOut), ctypes.POINTER(u64), ctypes.POINTER(i32)]),
         "gs_candidates_seek": (st, [P, u64]),
         "gs_candidates_vertex_range": (st, [P, i64, ctypes.POINTER(u64), ctypes.POINTER(u64)]),

@@ -364,6 +364,18 @@ extern "C" {
 
 int32_t gs_abi_version(void) { return GS_ABI_VERSION; }
 
+gs_status gs_device_count(int32_t* n) {
+  if (!n) return GS_EINVAL;
+  *n = 0;
+  int d = 0;
+  if (hipGetDeviceCount(&d) != hipSuccess) {
+    (void)hipGetLastError();
+    return GS_EDEVICE;
+  }
+  *n = d;
+  return GS_OK;
+}
+
 gs_status gs_create(const gs_config* cfg, gs_ctx** out) {
   if (!out) return GS_EINVAL;
   *out = nullptr;

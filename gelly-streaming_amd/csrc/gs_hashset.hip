@@ -1103,9 +1103,11 @@ gs_status gs_window_candidates(gs_ctx* c, const gs_edge_batch* b, gs_pair_out* o
   return gs_window_candidates_part(c, b, 1, 0, out);
 }
 
-gs_status gs_candidates_begin(gs_ctx* c, const gs_edge_batch* b, uint64_t* total_records, uint32_t* jdk_flags) {
+gs_status gs_candidates_begin_part(gs_ctx* c, const gs_edge_batch* b, uint32_t nparts, uint32_t part,
+                                   uint64_t* total_records, uint32_t* jdk_flags) {
   GS_TRY(check_batch(c, b, GS_DIR_ALL));
   if (!total_records) return set_error(c, GS_EINVAL, "null total_records");
+  if (nparts == 0 || part >= nparts) return set_error(c, GS_EINVAL, "part %u of %u", part, nparts);
   GS_TRY(begin_call(c));
   c->cand_seq = c->call_seq;
   c->cand_total = c->cand_cursor = 0;
@@ -1119,13 +1121,18 @@ gs_status gs_candidates_begin(gs_ctx* c, const gs_edge_batch* b, uint64_t* total
   uint32_t U = 0, M = 0, S = 0, fl = 0;
   uint64_t key_xor = 0, total = 0;
   GS_TRY(hashset_order(c, src, dst, b->n, &U, &M, &key_xor, &fl));
-  GS_TRY(cand_layout(c, U, M, 1, 0, &S, &total));
+  GS_TRY(cand_layout(c, U, M, nparts, part, &S, &total));
+  c->cand_nparts = nparts;
   c->cand_U = U;
   c->cand_S = S;
   c->cand_total = total;
   *total_records = total;
   if (jdk_flags) *jdk_flags = fl;
   return GS_OK;
+}
+
+gs_status gs_candidates_begin(gs_ctx* c, const gs_edge_batch* b, uint64_t* total_records, uint32_t* jdk_flags) {
+  return gs_candidates_begin_part(c, b, 1, 0, total_records, jdk_flags);
 }
 
 static gs_status cand_session(gs_ctx* c) {
@@ -1187,6 +1194,8 @@ gs_status gs_candidates_vertex_range(gs_ctx* c, int64_t vertex, uint64_t* first_
   if (!first_record || !records) return set_error(c, GS_EINVAL, "null output");
   GS_TRY(cand_session(c));
   *first_record = *records = 0;
+  if (c->cand_nparts > 1)   // (a part's slots are its own vertices only: the block table is not per vertex)
+    return set_error(c, GS_EUNSUPPORTED, "gs_candidates_vertex_range on a part session (gs_candidates_begin_part)");
   if (c->cand_total == 0) return GS_OK;
   GS_TRY(ensure(c, c->cand_bounds, 64));
   auto* d = c->cand_bounds.as<unsigned long long>();

@@ -63,7 +63,7 @@ struct gs_ctx {
   // chunked candidate emission (gs_candidates_begin / _next): the window's HashSet-ordered sets stay in
   // hs[] until the next entry point call on the ctx (call_seq) ends the session
   uint64_t call_seq = 0, cand_seq = ~0ull, cand_total = 0, cand_cursor = 0;
-  uint32_t cand_U = 0, cand_S = 0;
+  uint32_t cand_U = 0, cand_S = 0, cand_nparts = 1;
   gs::DevBuf cand_bounds;
   // input staging (host batches)
   gs::DevBuf in_src, in_dst, in_val;

@@ -269,12 +269,18 @@ class Engine:
         self.last_candidates_jdk_flags = int(out.reserved)
         return a[:P], bb[:P], f[:P]
 
-    def candidates_begin(self, src, dst) -> int:
-        """gs_candidates_begin: build the window's HashSet-ordered sets once; returns the record count.
-        The columns must stay alive (and unchanged) until the session's last candidates_next."""
+    def candidates_begin(self, src, dst, nparts: int = 1, part: int = 0) -> int:
+        """gs_candidates_begin (gs_candidates_begin_part with nparts > 1: only part's vertices emit): build
+        the window's HashSet-ordered sets once; returns the record count.  The columns must stay alive (and
+        unchanged) until the session's last candidates_next."""
         b, keep, dev = self._batch(src, dst, None)
         total, fl = ctypes.c_uint64(0), ctypes.c_uint32(0)
-        self._check(self._L.gs_candidates_begin(self.ctx, ctypes.byref(b), ctypes.byref(total), ctypes.byref(fl)))
+        if nparts == 1:
+            st = self._L.gs_candidates_begin(self.ctx, ctypes.byref(b), ctypes.byref(total), ctypes.byref(fl))
+        else:
+            st = self._L.gs_candidates_begin_part(self.ctx, ctypes.byref(b), int(nparts), int(part), ctypes.byref(total),
+                                                  ctypes.byref(fl))
+        self._check(st)
         self._cand_dev = dev
         self.last_candidates_jdk_flags = int(fl.value)
         return total.value
@@ -591,6 +597,14 @@ class Engine:
         return int(self._L.gs_owner_of(int(vertex), nparts))
 
     # -- the ctx communicator: RCCL (one rank per process) or an in-process CommGroup ---------------------
+    @staticmethod
+    def device_count() -> int:
+        n = ctypes.c_int32(0)
+        st = L.load().gs_device_count(ctypes.byref(n))
+        if st != L.GS_OK:
+            raise GsError(st, "gs_device_count failed")
+        return n.value
+
     @staticmethod
     def comm_unique_id() -> bytes:
         buf = ctypes.create_string_buffer(128)

@@ -41,7 +41,8 @@ extern "C" {
 #endif
 
 /* 2: gs_tri_dist_route lost two parameters (gs_tri_dist_orient runs first), the JNI candidates
- *    natives changed return types, and the in-process comm group (gs_comm_group_*) was added. */
+ *    natives changed return types, and the in-process comm group (gs_comm_group_*),
+ *    gs_candidates_begin_part and gs_device_count were added. */
 #define GS_ABI_VERSION 2
 
 #if defined(__GNUC__) || defined(__clang__)
@@ -164,6 +165,9 @@ typedef struct gs_pair_out {
 
 /* ---- lifecycle ---------------------------------------------------------------------- */
 GS_API int32_t gs_abi_version(void);
+/* HIP devices visible to this process (*n); a Flink job sizes its GPU operators' parallelism by it and
+ * puts subtask i on device i % n. */
+GS_API gs_status gs_device_count(int32_t* n);
 GS_API gs_status gs_create(const gs_config* cfg, gs_ctx** out);
 GS_API void gs_destroy(gs_ctx* ctx);
 GS_API const char* gs_last_error(const gs_ctx* ctx);
@@ -226,6 +230,12 @@ GS_API gs_status gs_window_candidates(gs_ctx* ctx, const gs_edge_batch* batch, g
 GS_API gs_status gs_candidates_begin(gs_ctx* ctx, const gs_edge_batch* batch, uint64_t* total_records,
                                      uint32_t* jdk_flags);
 GS_API gs_status gs_candidates_next(gs_ctx* ctx, gs_pair_out* out, uint64_t* first_record, int32_t* done);
+/* A session over one part of a window split by owner (the chunked gs_window_candidates_part, below):
+ * only the vertices v with gs_owner_of(v, nparts) == part emit; the batch holds every edge incident to
+ * them in stream order (a Flink subtask behind an owner partitioner: GpuCandidatesOperator).
+ * gs_candidates_vertex_range is not offered on such a session (GS_EUNSUPPORTED). */
+GS_API gs_status gs_candidates_begin_part(gs_ctx* ctx, const gs_edge_batch* batch, uint32_t nparts, uint32_t part,
+                                          uint64_t* total_records, uint32_t* jdk_flags);
 /* Random access into the session (no reference counterpart: a consumer that restarts mid-window, or
  * several consumers that split the output, e.g. one per downstream pair-keyed subtask).
  * gs_candidates_seek moves the cursor: the next gs_candidates_next starts at `record` (<= the total).
@@ -263,7 +273,9 @@ GS_API gs_status gs_window_triangles_part(gs_ctx* ctx, const gs_edge_batch* batc
  * ctx communicator: gs_window_triangles_dist does all of them over RCCL or the comm group):
  *   1. gs_tri_dist_range     local [min, max] id            -> all-reduce min of [0], max of [1]
  *   2. gs_tri_dist_degrees   local raw degrees deg[V]       -> all-reduce (sum, u32) of deg
- *      (deg == NULL: *V only, to size the buffer; V = 2^bits of the common id span, <= 2^28)
+ *      (deg == NULL: *V only, to size the buffer; V = 2^bits of the common id span, <= 2^28: a window
+ *      whose ids span more is relabeled to the whole window's compact ids first, as gs_window_triangles_dist
+ *      does inside and distributed.relabel_window shows for a caller)
  *   3a. gs_tri_dist_orient   oriented edges (u << B | v, u < v in the degree order), kept in the ctx
  *      for 3b; dout[V] = their count per u (raw, duplicates included); *loops = local self-loops
  *                                                           -> all-reduce (sum, u32) of dout; of loops
@@ -294,7 +306,7 @@ GS_API gs_status gs_window_triangles_part(gs_ctx* ctx, const gs_edge_batch* batc
  *   6. windows with self-loops (summed loops > 0): the self-pair term needs whole neighbour sets, so
  *      the records are gathered and rank 0 adds gs_window_triangles_selfpair of the whole window.
  * Exchanged per window: 4 B per id (deg, dout, dplus), 8 B per local record (step 3) and 4 B per element of the
- * boundary rows a rank reads but did not build (step 4; R-MAT: 0.25-0.56 of the all-gathered
+ * boundary rows a rank reads but did not build (step 4; R-MAT s22-s24: 0.16-0.47 of the all-gathered
  * adjacency at 2-8 ranks).  Buffers: deg, keys_out, keys, nbr_out, dplus_out, crows,
  * req_out, req_in, rows_out, rows_in, full_out, nbr, dplus are device memory; counts and sizes host. */
 GS_API gs_status gs_tri_dist_range(gs_ctx* ctx, const gs_edge_batch* local, int64_t* minmax /* [2] */);

@@ -62,6 +62,13 @@ JNIEXPORT jlong JNI_FN(create)(JNIEnv* env, jclass cls, jint device, jint flags,
 
 JNIEXPORT void JNI_FN(destroy)(JNIEnv* env, jclass cls, jlong ctx) { gs_destroy((gs_ctx*)(intptr_t)ctx); }
 
+JNIEXPORT jint JNI_FN(deviceCount)(JNIEnv* env, jclass cls) {
+  int32_t n = 0;
+  gs_status s = gs_device_count(&n);
+  if (s != GS_OK) throw_status(env, NULL, s, "gs_device_count");
+  return (jint)n;
+}
+
 JNIEXPORT void JNI_FN(setTiming)(JNIEnv* env, jclass cls, jlong ctx, jint level) {
   gs_ctx* c = (gs_ctx*)(intptr_t)ctx;
   gs_status s = gs_set_timing(c, (int32_t)level);
@@ -140,14 +147,15 @@ static jlongArray long_array(JNIEnv* env, const jlong* v, jsize n) {
   return out;
 }
 
-JNIEXPORT jlongArray JNI_FN(candidatesBegin)(JNIEnv* env, jclass cls, jlong ctx, jobject src, jobject dst, jlong n) {
+JNIEXPORT jlongArray JNI_FN(candidatesBegin)(JNIEnv* env, jclass cls, jlong ctx, jobject src, jobject dst, jlong n,
+                                             jint nparts, jint part) {
   gs_ctx* c = (gs_ctx*)(intptr_t)ctx;
   gs_edge_batch b = batch(env, src, dst, NULL, n, GS_NONE);
   uint64_t total = 0;
   uint32_t flags = 0;
-  gs_status s = gs_candidates_begin(c, &b, &total, &flags);
+  gs_status s = gs_candidates_begin_part(c, &b, (uint32_t)nparts, (uint32_t)part, &total, &flags);
   if (s != GS_OK) {
-    throw_status(env, c, s, "gs_candidates_begin");
+    throw_status(env, c, s, "gs_candidates_begin_part");
     return NULL;
   }
   const jlong r[2] = {(jlong)total, (jlong)flags};
@@ -186,6 +194,22 @@ JNIEXPORT jlongArray JNI_FN(candidatesVertexRange)(JNIEnv* env, jclass cls, jlon
   }
   const jlong r[2] = {(jlong)first, (jlong)n};
   return long_array(env, r, 2);
+}
+
+JNIEXPORT jlong JNI_FN(windowComponents)(JNIEnv* env, jclass cls, jlong ctx, jobject src, jobject dst, jlong n,
+                                         jobject pk, jobject pl, jlong m, jobject ok, jobject ol, jlong cap) {
+  gs_ctx* c = (gs_ctx*)(intptr_t)ctx;
+  gs_edge_batch b = batch(env, src, dst, NULL, n, GS_NONE);
+  gs_partial_batch prev;
+  memset(&prev, 0, sizeof prev);
+  prev.keys = (const int64_t*)addr(env, pk);
+  prev.vals = addr(env, pl);
+  prev.n = (uint64_t)m;
+  prev.val_dtype = GS_I64;
+  prev.mem = GS_MEM_HOST;
+  uint64_t n_out = 0;
+  gs_vertex_out o = {(int64_t*)addr(env, ok), addr(env, ol), (uint64_t)cap, &n_out, GS_MEM_HOST, 0};
+  return rows_or_throw(env, c, gs_window_components(c, &b, m ? &prev : NULL, &o), n_out, "gs_window_components");
 }
 
 /* ---- gs_stream_*: the stream keeps its ctx (one per operator subtask) -------------------------------- */

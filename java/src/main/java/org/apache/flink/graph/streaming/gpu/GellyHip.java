@@ -17,6 +17,11 @@ public final class GellyHip {
 
 	static {
 		System.loadLibrary("gellyhip_jni");   // java/Makefile: links libgellyhip.so
+		// the shim was compiled against one gelly_hip.h: refuse a library of another ABI (struct layouts and
+		// entry point signatures change with GS_ABI_VERSION) instead of passing it wrong arguments
+		final int abi = abiVersion();
+		if (abi != GS_ABI_VERSION)
+			throw new UnsatisfiedLinkError("libgellyhip.so has ABI " + abi + ", this binding needs " + GS_ABI_VERSION);
 	}
 
 	private GellyHip() {
@@ -81,6 +86,9 @@ public final class GellyHip {
 
 	static native void destroy(long ctx);
 
+	/** gs_device_count: HIP devices visible to this JVM (the GPU operators' parallelism, GpuBuiltins). */
+	static native int deviceCount();
+
 	/** gs_set_timing: which stage-time events a window records (GS_TIMING_*; the operators run OFF). */
 	static native void setTiming(long ctx, int level);
 
@@ -112,11 +120,13 @@ public final class GellyHip {
 	static native long[] windowTriangles(long ctx, ByteBuffer src, ByteBuffer dst, long n);
 
 	/**
-	 * gs_candidates_begin: GenerateCandidateEdges (WindowTriangles.java:83-116) over one window's columns;
-	 * returns {record count, JDK flags} (flags bit 0: a neighbour set used a treeified HashMap bin, bit 1: a
-	 * bin of 9 forced a resize below capacity 64 -- both simulated exactly).
+	 * gs_candidates_begin_part: GenerateCandidateEdges (WindowTriangles.java:83-116) over one window's
+	 * columns, emitting the vertices v with owner(v, nparts) == part (nparts 1: every vertex; the columns
+	 * hold every edge incident to them, GpuBuiltins.RouteToOwners); returns {record count, JDK flags}
+	 * (flags bit 0: a neighbour set used a treeified HashMap bin, bit 1: a bin of 9 forced a resize below
+	 * capacity 64 -- both simulated exactly).
 	 */
-	static native long[] candidatesBegin(long ctx, ByteBuffer src, ByteBuffer dst, long n);
+	static native long[] candidatesBegin(long ctx, ByteBuffer src, ByteBuffer dst, long n, int nparts, int part);
 
 	/**
 	 * gs_candidates_next: the next records of the session into (a, b, isCandidate); returns {records
@@ -129,6 +139,15 @@ public final class GellyHip {
 
 	/** gs_candidates_vertex_range: {first position, records} of one vertex's block in the session. */
 	static native long[] candidatesVertexRange(long ctx, long vertex);
+
+	/**
+	 * gs_window_components: ConnectedComponents (library/ConnectedComponents.java:56-131) over one window:
+	 * the previous state's m (vertex, label) rows merged with the window's n edges into out (every vertex
+	 * seen so far, ascending, labelled by its component's smallest vertex).  Returns the rows written, or
+	 * -(rows needed) when capacity is short (m + 2n always suffices).
+	 */
+	static native long windowComponents(long ctx, ByteBuffer src, ByteBuffer dst, long n, ByteBuffer prevKeys,
+			ByteBuffer prevLabels, long m, ByteBuffer outKeys, ByteBuffer outLabels, long capacity);
 
 	/* ---- the window-buffer operator (gs_stream_*): event-time tumbling windows ------------------------ */
 	static native long streamCreate(long ctx, long windowMs, int kind, int direction, int op, int valDtype,

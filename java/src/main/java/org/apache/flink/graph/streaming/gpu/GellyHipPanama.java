@@ -59,8 +59,10 @@ public final class GellyHipPanama implements AutoCloseable {
 			FunctionDescriptor.of(JAVA_INT, ADDRESS, ADDRESS, JAVA_INT, JAVA_LONG, ADDRESS));
 	private static final MethodHandle WINDOW_TRIANGLES = fn("gs_window_triangles",
 			FunctionDescriptor.of(JAVA_INT, ADDRESS, ADDRESS, ADDRESS, ADDRESS, ADDRESS));
-	private static final MethodHandle CANDIDATES_BEGIN = fn("gs_candidates_begin",
-			FunctionDescriptor.of(JAVA_INT, ADDRESS, ADDRESS, ADDRESS, ADDRESS));
+	private static final MethodHandle CANDIDATES_BEGIN = fn("gs_candidates_begin_part",
+			FunctionDescriptor.of(JAVA_INT, ADDRESS, ADDRESS, JAVA_INT, JAVA_INT, ADDRESS, ADDRESS));
+	private static final MethodHandle DEVICE_COUNT = fn("gs_device_count", FunctionDescriptor.of(JAVA_INT, ADDRESS));
+	private static final MethodHandle ABI_VERSION = fn("gs_abi_version", FunctionDescriptor.of(JAVA_INT));
 	private static final MethodHandle CANDIDATES_NEXT = fn("gs_candidates_next",
 			FunctionDescriptor.of(JAVA_INT, ADDRESS, ADDRESS, ADDRESS, ADDRESS));
 	private static final MethodHandle FETCH_LAST_OUTPUT = fn("gs_fetch_last_output",
@@ -70,8 +72,21 @@ public final class GellyHipPanama implements AutoCloseable {
 	private final Arena arena = Arena.ofConfined();
 	private final MemorySegment ctx;
 
+	/** gs_device_count: HIP devices visible to this process. */
+	public static int deviceCount() throws Throwable {
+		try (Arena a = Arena.ofConfined()) {
+			final MemorySegment n = a.allocate(JAVA_INT);
+			final int st = (int) DEVICE_COUNT.invokeExact(n);
+			if (st != GellyHip.GS_OK) throw new RuntimeException("gs_device_count: status " + st);
+			return n.get(JAVA_INT, 0);
+		}
+	}
+
 	/** gs_create on `device`: one ctx (HIP stream + workspace) per operator subtask thread. */
 	public GellyHipPanama(int device) throws Throwable {
+		final int abi = (int) ABI_VERSION.invokeExact();
+		if (abi != GellyHip.GS_ABI_VERSION)
+			throw new UnsatisfiedLinkError("libgellyhip.so has ABI " + abi + ", this binding needs " + GellyHip.GS_ABI_VERSION);
 		final MemorySegment cfg = arena.allocate(CONFIG);
 		cfg.set(JAVA_INT, 0, device);
 		final MemorySegment out = arena.allocate(ADDRESS);
@@ -164,11 +179,14 @@ public final class GellyHipPanama implements AutoCloseable {
 		return new long[] {count.get(JAVA_LONG, 0), wrapped.get(JAVA_INT, 0), has.get(JAVA_INT, 0)};
 	}
 
-	/** gs_candidates_begin (GenerateCandidateEdges, WindowTriangles.java:83-116): {records, JDK flags}. */
-	public long[] candidatesBegin(MemorySegment src, MemorySegment dst, long n) throws Throwable {
+	/**
+	 * gs_candidates_begin_part (GenerateCandidateEdges, WindowTriangles.java:83-116; nparts 1 = the whole
+	 * window): {records, JDK flags}.
+	 */
+	public long[] candidatesBegin(MemorySegment src, MemorySegment dst, long n, int nparts, int part) throws Throwable {
 		final MemorySegment total = arena.allocate(JAVA_LONG), flags = arena.allocate(JAVA_INT);
-		check((int) CANDIDATES_BEGIN.invokeExact(ctx, batch(src, dst, null, n, GellyHip.GS_NONE), total, flags),
-				"gs_candidates_begin");
+		check((int) CANDIDATES_BEGIN.invokeExact(ctx, batch(src, dst, null, n, GellyHip.GS_NONE), nparts, part, total,
+				flags), "gs_candidates_begin_part");
 		return new long[] {total.get(JAVA_LONG, 0), flags.get(JAVA_INT, 0)};
 	}
 

@@ -6,10 +6,14 @@
  */
 package org.apache.flink.graph.streaming.gpu;
 
+import org.apache.flink.api.common.functions.FlatMapFunction;
+import org.apache.flink.api.common.functions.Partitioner;
 import org.apache.flink.api.java.tuple.Tuple2;
 import org.apache.flink.api.java.tuple.Tuple3;
+import org.apache.flink.graph.Edge;
 import org.apache.flink.graph.streaming.EdgesFold;
 import org.apache.flink.graph.streaming.EdgesReduce;
+import org.apache.flink.util.Collector;
 
 public final class GpuBuiltins {
 
@@ -149,6 +153,84 @@ public final class GpuBuiltins {
 			acc.setField(acc.f1 + 1, 1);
 			acc.setField(Math.max(acc.f2, neighbor), 2);
 			return acc;
+		}
+	}
+
+	/* ---- parallelism: one operator subtask per GPU ------------------------------------------------------
+	 * Flink runs a window operator at the environment's parallelism (local env: the host's cores), and
+	 * keyBy(NeighborKeySelector) (SimpleEdgeStream.java:159-167) gives every record of a vertex to one
+	 * subtask.  The GPU operators keep that contract: at parallelism 1 one subtask takes the whole stream;
+	 * at P > 1 the records go through partitionCustom(OwnerPartitioner) on their key (reduce / folds), or
+	 * every edge to the owners of both endpoints (RouteToOwners -> TargetPartitioner, candidates), and
+	 * subtask i runs on device i % deviceCount() with its own gs_ctx. */
+
+	/**
+	 * The GPU operators' parallelism: min(the environment's parallelism, visible HIP devices), at least 1;
+	 * -Dgelly.gpu.parallelism=N overrides it (e.g. several subtasks per device).
+	 */
+	public static int parallelism(int envParallelism) {
+		final String forced = System.getProperty("gelly.gpu.parallelism");
+		if (forced != null) return Math.max(1, Integer.parseInt(forced));
+		final int devices = Math.max(1, GellyHip.deviceCount());
+		return Math.max(1, Math.min(envParallelism > 0 ? envParallelism : devices, devices));
+	}
+
+	/** The device a subtask's gs_ctx lives on. */
+	public static int deviceFor(int subtaskIndex) {
+		return subtaskIndex % Math.max(1, GellyHip.deviceCount());
+	}
+
+	/**
+	 * gs_owner_of (gs_ops.hpp owner_of): murmur3's 64-bit finaliser of the vertex, scaled to nparts by a
+	 * multiply-high -- the same function the library's part entry points (gs_candidates_begin_part) filter
+	 * by, so the routing and the emission agree (tests/test_abi.py compares the constants).
+	 */
+	public static int ownerOf(long v, int nparts) {
+		long x = v;
+		x ^= x >>> 33;
+		x *= 0xff51afd7ed558ccdL;
+		x ^= x >>> 33;
+		x *= 0xc4ceb9fe1a85ec53L;
+		x ^= x >>> 33;
+		return (int) (((x >>> 32) * (long) nparts) >>> 32);
+	}
+
+	/** keyBy on a Long vertex key: the record goes to subtask ownerOf(key, P). */
+	@SuppressWarnings("serial")
+	public static final class OwnerPartitioner implements Partitioner<Long> {
+		@Override
+		public int partition(Long key, int numPartitions) {
+			return ownerOf(key, numPartitions);
+		}
+	}
+
+	/** Records already tagged with their target subtask (RouteToOwners' f0). */
+	@SuppressWarnings("serial")
+	public static final class TargetPartitioner implements Partitioner<Integer> {
+		@Override
+		public int partition(Integer target, int numPartitions) {
+			return target;
+		}
+	}
+
+	/**
+	 * Every edge to the owners of both its endpoints (once when they are the same subtask), stream order
+	 * kept per channel: the subtask that owns v then holds every edge incident to v, which
+	 * GenerateCandidateEdges needs (its HashSet is built from all of v's neighbour records).
+	 */
+	@SuppressWarnings("serial")
+	public static final class RouteToOwners<EV> implements FlatMapFunction<Edge<Long, EV>, Tuple2<Integer, Edge<Long, EV>>> {
+		private final int parts;
+
+		public RouteToOwners(int parts) {
+			this.parts = parts;
+		}
+
+		@Override
+		public void flatMap(Edge<Long, EV> e, Collector<Tuple2<Integer, Edge<Long, EV>>> out) {
+			final int a = ownerOf(e.f0, parts), b = ownerOf(e.f1, parts);
+			out.collect(new Tuple2<Integer, Edge<Long, EV>>(a, e));
+			if (b != a) out.collect(new Tuple2<Integer, Edge<Long, EV>>(b, e));
 		}
 	}
 

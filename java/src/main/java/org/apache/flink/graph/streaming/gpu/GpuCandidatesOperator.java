@@ -11,8 +11,11 @@
  *
  * A record for a window that already fired (late) opens that window again and fires it at the next
  * watermark with only the late records, as Flink 1.0.3's WindowOperator does without allowed lateness.
- * One operator subtask owns one gs_ctx; the window's edges must all reach it (parallelism 1, or one
- * subtask per owner partition fed through GellyHip's owner routing and gs_window_candidates_part).
+ * One operator subtask owns one gs_ctx on device subtask % devices.  applyOnNeighbors() builds it the way
+ * slice(ALL)'s keyBy would (SimpleEdgeStream.java:163-167): one subtask over the whole stream, or P
+ * subtasks each fed every edge incident to the vertices it owns (GpuBuiltins.RouteToOwners ->
+ * partitionCustom), each emitting only those vertices' records (gs_candidates_begin_part).  The input is
+ * the edge itself (P = 1) or the routed Tuple2(target subtask, edge).
  */
 package org.apache.flink.graph.streaming.gpu;
 
@@ -20,8 +23,14 @@ import java.nio.ByteBuffer;
 import java.util.Map;
 import java.util.TreeMap;
 
+import org.apache.flink.api.common.typeinfo.BasicTypeInfo;
+import org.apache.flink.api.common.typeinfo.TypeInformation;
+import org.apache.flink.api.java.tuple.Tuple;
+import org.apache.flink.api.java.tuple.Tuple2;
 import org.apache.flink.api.java.tuple.Tuple3;
+import org.apache.flink.api.java.typeutils.TupleTypeInfo;
 import org.apache.flink.graph.Edge;
+import org.apache.flink.streaming.api.datastream.DataStream;
 import org.apache.flink.streaming.api.operators.AbstractStreamOperator;
 import org.apache.flink.streaming.api.operators.OneInputStreamOperator;
 import org.apache.flink.streaming.api.watermark.Watermark;
@@ -29,64 +38,61 @@ import org.apache.flink.streaming.runtime.streamrecord.StreamRecord;
 
 @SuppressWarnings("serial")
 public class GpuCandidatesOperator<EV> extends AbstractStreamOperator<Tuple3<Long, Long, Boolean>>
-		implements OneInputStreamOperator<Edge<Long, EV>, Tuple3<Long, Long, Boolean>> {
+		implements OneInputStreamOperator<Tuple, Tuple3<Long, Long, Boolean>> {
 
 	private static final int CHUNK = 1 << 20;   // records per gs_candidates_next
 
 	private final long windowMs;
-	private final int device;
+	private final int parts;
 
 	private transient long ctx;
-	private transient TreeMap<Long, Columns> open;   // window start -> its edges, in arrival order
+	private transient int part;
+	private transient TreeMap<Long, WindowColumns> open;   // window start -> its edges, in arrival order
 	private transient ByteBuffer a, b, f;
 
-	/** one window's edges as growable direct columns (what gs_candidates_begin reads, no copy) */
-	private static final class Columns {
-		ByteBuffer src = GellyHip.direct(8L * 1024), dst = GellyHip.direct(8L * 1024);
-		int n;
-
-		void add(long s, long d) {
-			if ((long) (n + 1) * 8 > src.capacity()) {   // a direct buffer holds < 2^31 bytes: 2^28 edges per window
-				src = grow(src);
-				dst = grow(dst);
-			}
-			src.putLong(n * 8, s);
-			dst.putLong(n * 8, d);
-			++n;
-		}
-
-		private static ByteBuffer grow(ByteBuffer old) {
-			final ByteBuffer nb = GellyHip.direct(2L * old.capacity());
-			old.clear();
-			nb.put(old);
-			nb.clear();
-			return nb;
-		}
+	/** parts: the operator's parallelism (1: every vertex on one subtask) */
+	public GpuCandidatesOperator(long windowMs, int parts) {
+		this.windowMs = windowMs;
+		this.parts = parts;
 	}
 
-	public GpuCandidatesOperator(long windowMs, int device) {
-		this.windowMs = windowMs;
-		this.device = device;
+	/** applyOnNeighbors(GenerateCandidateEdges) over slice(ALL) on the engine (GraphWindowStream.java:130-182). */
+	@SuppressWarnings({"unchecked", "rawtypes"})
+	public static <EV, T> DataStream<T> applyOnNeighbors(DataStream<Edge<Long, EV>> edges, long windowMs,
+			TypeInformation<T> type) {
+		final int p = GpuBuiltins.parallelism(edges.getExecutionEnvironment().getParallelism());
+		if (p == 1)
+			return ((DataStream) edges).transform("gpu-applyOnNeighbors", type, new GpuCandidatesOperator<EV>(windowMs, 1))
+					.setParallelism(1);
+		final TypeInformation<Tuple2<Integer, Edge<Long, EV>>> routed = new TupleTypeInfo<Tuple2<Integer, Edge<Long, EV>>>(
+				BasicTypeInfo.INT_TYPE_INFO, edges.getType());
+		return ((DataStream) edges.flatMap(new GpuBuiltins.RouteToOwners<EV>(p)).returns(routed)
+				.partitionCustom(new GpuBuiltins.TargetPartitioner(), 0))
+				.transform("gpu-applyOnNeighbors", type, new GpuCandidatesOperator<EV>(windowMs, p)).setParallelism(p);
 	}
 
 	@Override
 	public void open() throws Exception {
 		super.open();
-		ctx = GellyHip.create(device, 0, 0);
+		part = getRuntimeContext().getIndexOfThisSubtask();
+		if (part >= parts) throw new IllegalStateException("subtask " + part + " of an operator built for " + parts);
+		ctx = GellyHip.create(GpuBuiltins.deviceFor(part), 0, 0);
 		GellyHip.setTiming(ctx, GellyHip.GS_TIMING_OFF);   // no stage-time events in production
-		open = new TreeMap<Long, Columns>();
+		open = new TreeMap<Long, WindowColumns>();
 		a = GellyHip.direct(8L * CHUNK);
 		b = GellyHip.direct(8L * CHUNK);
 		f = GellyHip.direct(CHUNK);
 	}
 
 	@Override
-	public void processElement(StreamRecord<Edge<Long, EV>> element) throws Exception {
+	@SuppressWarnings("unchecked")
+	public void processElement(StreamRecord<Tuple> element) throws Exception {
 		final long ts = element.getTimestamp();
 		final long start = ts - ts % windowMs;   // Java remainder, as TumblingEventTimeWindows
-		Columns w = open.get(start);
-		if (w == null) open.put(start, w = new Columns());
-		final Edge<Long, EV> e = element.getValue();
+		WindowColumns w = open.get(start);
+		if (w == null) open.put(start, w = new WindowColumns());
+		final Tuple v = element.getValue();
+		final Edge<Long, EV> e = v instanceof Edge ? (Edge<Long, EV>) v : ((Tuple2<Integer, Edge<Long, EV>>) v).f1;
 		w.add(e.f0, e.f1);
 	}
 
@@ -111,7 +117,7 @@ public class GpuCandidatesOperator<EV> extends AbstractStreamOperator<Tuple3<Lon
 	/** fires, in window order, every buffered window with end - 1 <= watermark */
 	private void fireUpTo(long watermark) {
 		while (!open.isEmpty()) {
-			final Map.Entry<Long, Columns> first = open.firstEntry();
+			final Map.Entry<Long, WindowColumns> first = open.firstEntry();
 			final long stamp = first.getKey() + windowMs - 1;
 			if (stamp > watermark) return;
 			open.remove(first.getKey());
@@ -119,8 +125,8 @@ public class GpuCandidatesOperator<EV> extends AbstractStreamOperator<Tuple3<Lon
 		}
 	}
 
-	private void emitWindow(Columns w, long stamp) {
-		final long total = GellyHip.candidatesBegin(ctx, w.src, w.dst, w.n)[0];
+	private void emitWindow(WindowColumns w, long stamp) {
+		final long total = GellyHip.candidatesBegin(ctx, w.src, w.dst, w.n, parts, part)[0];
 		final StreamRecord<Tuple3<Long, Long, Boolean>> rec = new StreamRecord<Tuple3<Long, Long, Boolean>>(null, stamp);
 		long got = 0;
 		while (got < total) {

@@ -10,9 +10,11 @@
  * Emitting after it would stamp rows end - 1 <= a watermark already sent: late downstream, where e.g.
  * WindowTriangles.java:66's timeWindowAll(..).sum(0) would split one window's count over two panes.
  *
- * One operator subtask owns one gs_ctx (one HIP stream + workspace: gelly_hip.h "Conventions"); run it
- * at parallelism 1 per GPU, or at parallelism P behind a partitionCustom by GellyHip's owner function
- * (the keyBy of SimpleEdgeStream.java:159-167) with one GPU per subtask.  Flink 1.0.3 operator API.
+ * One operator subtask owns one gs_ctx (one HIP stream + workspace: gelly_hip.h "Conventions") on device
+ * subtask % devices.  neighborhood() builds it the way keyBy would (SimpleEdgeStream.java:159-167): one
+ * subtask over the whole stream, or P subtasks behind partitionCustom(OwnerPartitioner) on the
+ * direction-expanded records, so every record of a vertex reaches the subtask that owns it.  Flink 1.0.3
+ * operator API.
  */
 package org.apache.flink.graph.streaming.gpu;
 
@@ -42,7 +44,6 @@ public class GpuWindowOperator<EV, OUT extends Tuple> extends AbstractStreamOper
 	private final long windowMs;
 	private final int kind, direction, op, valDtype;
 	private final Object init;                  // FOLD: the fold's initial value (its f1); DEGREE_MAX: Long
-	private final int device;
 	private final long maxWindowEdges;
 
 	private transient long ctx, stream;
@@ -55,7 +56,7 @@ public class GpuWindowOperator<EV, OUT extends Tuple> extends AbstractStreamOper
 	 * @param kind GellyHip.GS_STREAM_REDUCE / _FOLD / _DEGREE_MAX / _TRIANGLES
 	 * @param init FOLD: the initial value (Long / Integer / Float / Double); DEGREE_MAX: the initial maximum
 	 */
-	public GpuWindowOperator(long windowMs, int kind, int direction, int op, int valDtype, Object init, int device,
+	public GpuWindowOperator(long windowMs, int kind, int direction, int op, int valDtype, Object init,
 			long maxWindowEdges) {
 		this.windowMs = windowMs;
 		this.kind = kind;
@@ -63,13 +64,33 @@ public class GpuWindowOperator<EV, OUT extends Tuple> extends AbstractStreamOper
 		this.op = op;
 		this.valDtype = valDtype;
 		this.init = init;
-		this.device = device;
 		this.maxWindowEdges = maxWindowEdges;
+	}
+
+	/**
+	 * reduceOnEdges / foldNeighbors with a built-in on the engine (GraphWindowStream.java:62-121).
+	 * edges: the stream before keyBy; keyed: the direction-expanded records keyBy sees (getEdges(),
+	 * reverse() or undirected(): SimpleEdgeStream.java:153-171).  At parallelism 1 the operator expands the
+	 * direction itself on the original edges; at P > 1 the keyed records are partitioned by their key's
+	 * owner and every subtask reduces its share as OUT (each vertex's records all on one subtask).
+	 */
+	@SuppressWarnings({"unchecked", "rawtypes"})
+	public static <EV, OUT extends Tuple> DataStream<OUT> neighborhood(String name, DataStream<Edge<Long, EV>> edges,
+			DataStream<Edge<Long, EV>> keyed, long windowMs, int kind, int direction, int op, int valDtype, Object init,
+			TypeInformation<OUT> type) {
+		final int p = GpuBuiltins.parallelism(edges.getExecutionEnvironment().getParallelism());
+		if (p == 1)
+			return edges.transform(name, type, new GpuWindowOperator<EV, OUT>(windowMs, kind, direction, op, valDtype,
+					init, 0)).setParallelism(1);
+		return keyed.partitionCustom(new GpuBuiltins.OwnerPartitioner(), 0).transform(name, type,
+				new GpuWindowOperator<EV, OUT>(windowMs, kind, GellyHip.GS_DIR_OUT, op, valDtype, init, 0))
+				.setParallelism(p);
 	}
 
 	@Override
 	public void open() throws Exception {
 		super.open();
+		final int device = GpuBuiltins.deviceFor(getRuntimeContext().getIndexOfThisSubtask());
 		ctx = GellyHip.create(device, 0, maxWindowEdges);
 		GellyHip.setTiming(ctx, GellyHip.GS_TIMING_OFF);   // no stage-time events in production
 		ByteBuffer initBuf = null;
@@ -168,7 +189,7 @@ public class GpuWindowOperator<EV, OUT extends Tuple> extends AbstractStreamOper
 				BasicTypeInfo.INT_TYPE_INFO, BasicTypeInfo.LONG_TYPE_INFO);
 		return edges.transform("gpu-window-triangles", type,
 				new GpuWindowOperator<EV, Tuple2<Integer, Long>>(size.toMilliseconds(), GellyHip.GS_STREAM_TRIANGLES,
-						GellyHip.GS_DIR_ALL, 0, GellyHip.GS_NONE, null, 0, 0)).setParallelism(1);
+						GellyHip.GS_DIR_ALL, 0, GellyHip.GS_NONE, null, 0)).setParallelism(1);
 	}
 
 	private long pending() {

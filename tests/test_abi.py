@@ -147,15 +147,22 @@ def test_every_builtin_marker_reaches_a_native_and_an_entry_point():
     assert re.search(r"GenerateCandidateEdges implements\s*EdgesApply<[^{]*GpuBuiltins\.BuiltinApply \{", after)
     markers["GenerateCandidateEdges"] = "BuiltinApply"
     # marker interface -> (dispatch test in the patch, the operator it builds, the stream kind it asks for)
-    route = {"Builtin": ("GpuBuiltins.Builtin", "GpuWindowOperator", "GS_STREAM_REDUCE"),
-             "BuiltinFold": ("GpuBuiltins.BuiltinFold", "GpuWindowOperator", "GS_STREAM_FOLD"),
-             "BuiltinApply": ("GpuBuiltins.BuiltinApply", "GpuCandidatesOperator", None)}
+    # (marker -> dispatch test, the operator factory the patch calls, the stream kind it asks for); each
+    # factory builds its operator
+    route = {"Builtin": ("GpuBuiltins.Builtin", "GpuWindowOperator.neighborhood(", "GS_STREAM_REDUCE"),
+             "BuiltinFold": ("GpuBuiltins.BuiltinFold", "GpuWindowOperator.neighborhood(", "GS_STREAM_FOLD"),
+             "BuiltinApply": ("GpuBuiltins.BuiltinApply", "GpuCandidatesOperator.applyOnNeighbors(", None)}
     for name, iface in markers.items():
-        test, op, kind = route[iface]
+        test, factory, kind = route[iface]
         assert f"instanceof {test}" in added, (name, test)
-        assert f"new {op}" in added, (name, op)
+        assert factory in added, (name, factory)
+        cls = factory.split(".")[0]
+        assert f"new {cls}" in (GPU_JAVA / f"{cls}.java").read_text(), (name, cls)
         if kind:
             assert kind in added, (name, kind)
+    # ConnectedComponents: SimpleEdgeStream.aggregate routes it to GpuComponentsOperator
+    assert "instanceof ConnectedComponents" in added and "GpuComponentsOperator.connectedComponents(" in added
+    assert "getWindowMillis()" in added
     assert "GS_STREAM_DEGREE_MAX" in added
     # WindowTriangles.main: slice -> candidates -> CountTriangles -> timeWindowAll.sum on one operator
     assert "GpuWindowOperator.windowTriangles(" in added
@@ -163,7 +170,7 @@ def test_every_builtin_marker_reaches_a_native_and_an_entry_point():
     natives = set(re.findall(r"static native [\w\[\]]+ (\w+)\(", GELLYHIP_JAVA.read_text()))
     bodies = {re.search(r"JNI_FN\((\w+)\)", chunk).group(1): chunk
               for chunk in SHIM.read_text().split("JNIEXPORT")[1:]}
-    for op in ("GpuWindowOperator", "GpuCandidatesOperator"):
+    for op in ("GpuWindowOperator", "GpuCandidatesOperator", "GpuComponentsOperator"):
         used = set(re.findall(r"GellyHip\.([a-z]\w*)\(", (GPU_JAVA / f"{op}.java").read_text())) - {"direct"}
         assert used and used <= natives, (op, used - natives)
         for n in used:
@@ -225,3 +232,96 @@ def test_panama_binding_matches_header():
     got = [int(x) for x in subprocess.run([str(tmp / "panama_off")], capture_output=True, text=True,
                                           check=True).stdout.split()]
     assert got == want
+
+
+def _statements(text, token):
+    """the Java statements (up to the next ';') that contain token"""
+    out, at = [], 0
+    while (i := text.find(token, at)) >= 0:
+        start = text.rfind(";", 0, i) + 1
+        start = max(start, text.rfind("{", 0, i) + 1, text.rfind("}", 0, i) + 1)
+        end = text.find(";", i)
+        out.append(text[start:end + 1])
+        at = i + len(token)
+    return out
+
+
+def test_gpu_operators_keep_the_keyby_contract():
+    """SURVEY.md §8(b) "Threading" / keyBy (SimpleEdgeStream.java:159-167): Flink runs an operator at the
+    environment's parallelism (TestSlice's mini-cluster and the local env: several subtasks), and keyBy
+    gives every record of a vertex to ONE subtask.  So every GPU operator the patch or the factories build
+    is pinned: `transform(...)` is followed by `.setParallelism(1)`, or by `.setParallelism(p)` with a
+    partitionCustom by the owner in the same statement; and no operator hard-codes a device (each
+    subtask's gs_ctx goes to GpuBuiltins.deviceFor(subtask index))."""
+    patch = PATCH.read_text()
+    added = "\n".join(line[1:] for line in patch.splitlines() if line.startswith("+") and not line.startswith("+++"))
+    sources = {"patch": added}
+    for f in GPU_JAVA.glob("Gpu*Operator.java"):
+        sources[f.name] = f.read_text()
+    n = 0
+    for where, text in sources.items():
+        for st in _statements(text, ".transform("):
+            n += 1
+            m = re.search(r"\.setParallelism\((\w+)\)", st)
+            assert m, (where, st)
+            if m.group(1) != "1":
+                assert "partitionCustom(" in st, (where, st)
+        for st in _statements(text, "GellyHip.create("):
+            assert "GpuBuiltins.deviceFor(" in st or re.search(r"create\(device,", st), (where, st)
+            if "create(device," in st:   # the device variable comes from deviceFor in the same method
+                assert re.search(r"final int device = GpuBuiltins\.deviceFor\(", text), where
+    assert n >= 5
+    # the owner routing is keyed the way the library filters (gs_candidates_begin_part)
+    cand = (GPU_JAVA / "GpuCandidatesOperator.java").read_text()
+    assert "RouteToOwners" in cand and "TargetPartitioner" in cand and "candidatesBegin(ctx, w.src, w.dst, w.n, parts, part)" in cand
+
+
+def test_java_owner_function_is_the_librarys():
+    """GpuBuiltins.ownerOf (the Flink partitioner) restates gs_owner_of (gs_ops.hpp owner_of): the same
+    multipliers, shifts and multiply-high, so a vertex's records reach the subtask whose
+    gs_candidates_begin_part emits it."""
+    java = (GPU_JAVA / "GpuBuiltins.java").read_text()
+    body = re.search(r"public static int ownerOf\(long v, int nparts\) \{([\s\S]*?)\n\t\}", java).group(1)
+    cpp = (ROOT / "gelly-streaming_amd/csrc/gs_ops.hpp").read_text()
+    cbody = re.search(r"owner_of\(int64_t v, uint32_t nparts\) \{([\s\S]*?)\n\}", cpp).group(1)
+    jm = [int(x, 16) for x in re.findall(r"0x([0-9a-f]+)L", body)]
+    cm = [int(x, 16) for x in re.findall(r"0x([0-9a-f]+)ull", cbody)]
+    assert jm == cm and len(cm) == 2
+    assert re.findall(r">>> (\d+)", body)[:3] == re.findall(r">> (\d+)", cbody)[:3] == ["33", "33", "33"]
+    assert "((x >>> 32) * (long) nparts) >>> 32" in body and "((x >> 32) * (uint64_t)nparts) >> 32" in cbody
+
+
+JNI_STUB = r"""
+/* test infrastructure: the jni.h subset gellyhip_jni.c uses, so gcc can type-check the shim here
+ * (no JDK in this image); the real header comes from the JDK at java/Makefile build time */
+#include <stdint.h>
+#define JNIEXPORT __attribute__((visibility("default")))
+#define JNICALL
+#define JNI_TRUE 1
+#define JNI_FALSE 0
+typedef int32_t jint; typedef int64_t jlong; typedef uint8_t jboolean; typedef jint jsize;
+typedef void* jobject; typedef jobject jclass; typedef jobject jstring; typedef jobject jarray;
+typedef jarray jlongArray; typedef jarray jobjectArray; typedef jint jthrowable;
+struct JNINativeInterface_;
+typedef const struct JNINativeInterface_* JNIEnv;
+struct JNINativeInterface_ {
+  void* (*GetDirectBufferAddress)(JNIEnv*, jobject);
+  jobject (*NewDirectByteBuffer)(JNIEnv*, void*, jlong);
+  jclass (*FindClass)(JNIEnv*, const char*);
+  jint (*ThrowNew)(JNIEnv*, jclass, const char*);
+  jlongArray (*NewLongArray)(JNIEnv*, jsize);
+  void (*SetLongArrayRegion)(JNIEnv*, jlongArray, jsize, jsize, const jlong*);
+  void (*SetObjectArrayElement)(JNIEnv*, jobjectArray, jsize, jobject);
+};
+"""
+
+
+def test_jni_shim_type_checks_against_the_header():
+    """gcc -fsyntax-only of java/src/main/c/gellyhip_jni.c against include/gelly_hip.h (with a stub of
+    the jni.h subset it uses): every ABI call in the shim has the header's argument types and count."""
+    tmp = ROOT / "gpurun_out" / "jni_stub"
+    tmp.mkdir(parents=True, exist_ok=True)
+    (tmp / "jni.h").write_text(JNI_STUB)
+    r = subprocess.run(["gcc", "-fsyntax-only", "-Wall", "-Werror", "-Wno-unused-parameter", "-I", str(tmp), "-I",
+                        str(ROOT / "include"), str(SHIM)], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr

@@ -109,7 +109,7 @@ def test_engine_halves_two_ranks_gloo(oracle):
 
 
 @pytest.mark.parametrize("nparts", [2, 3, 8])
-def test_candidates_part(engine, oracle, nparts):
+def test_candidates_part(pkg, engine, oracle, nparts):
     """gs_window_candidates_part: part p, given the edges incident to its vertices in stream order, emits
     exactly the whole window's records of the vertices it owns (exact JDK HashSet order included: the
     ids are multiples of 16, so large neighbour sets collide into bins of 9 and take the simulation)."""
@@ -125,7 +125,25 @@ def test_candidates_part(engine, oracle, nparts):
             keep = (oa == part) | (ob == part)
             ps, pd = (torch.from_numpy(np.ascontiguousarray(x[keep])).cuda() for x in (S, D_))
             outs.append([x.cpu().numpy() for x in engine.candidates(ps, pd, nparts, part)])
+            # the chunked part session (gs_candidates_begin_part, GpuCandidatesOperator at parallelism P):
+            # the same records in the same order, in chunks
+            total = engine.candidates_begin(ps, pd, nparts, part)
+            assert total == len(outs[-1][0])
+            got, done = [], total == 0
+            while not done:
+                a, b, f, first, done = engine.candidates_next(50_000)
+                assert first == sum(len(g[0]) for g in got)
+                got.append((a.cpu().numpy(), b.cpu().numpy(), f.cpu().numpy()))
+            if total:
+                for j in range(3):
+                    assert np.array_equal(np.concatenate([g[j] for g in got]), outs[-1][j]), (mul, part, j)
+                with pytest.raises(pkg.GsError):
+                    engine.candidates_vertex_range(int(ps[0]))   # not offered on a part session
         check_candidates_split(outs, full)
+
+
+def test_device_count(pkg):
+    assert pkg.Engine.device_count() >= 1
 
 
 def test_rccl_world_one_through_the_abi(pkg, oracle):
@@ -218,7 +236,8 @@ def _tri_worker(rank, world, port, q):
 
 def test_split_window_triangles_two_ranks_gloo(oracle):
     """Two processes sharing this GPU, gloo between them: every rank holds half of the window's records;
-    degrees all-reduced, oriented edges routed to owner(u), out-lists all-gathered, each rank counts its
+    degrees all-reduced, oriented edges routed to owner(u), the boundary adjacency exchanged (rows of the
+    rank's count range, then the rows of their targets it holds in neither range), each rank counts its
     equal-work share -> the whole window's count (forward algorithm; the reference rule with loops)."""
     world, port = 2, _free_port()
     ctx = mp.get_context("spawn")
