@@ -27,6 +27,9 @@ gs_status set_error(gs_ctx* c, gs_status s, const char* fmt, ...) {
     vsnprintf(buf, sizeof buf, fmt, ap);
     va_end(ap);
     c->err = buf;
+    // a failed call may have left the look-back timeout word set (e.g. a later kernel of the call timed out
+    // after an earlier read-back saw it zero): the next call clears it (begin_call)
+    c->timeout_clean = false;
   }
   return s;
 }

@@ -256,6 +256,11 @@ gs_status launch_keyinfo_all(gs_ctx* c, const int64_t* src, const int64_t* dst, 
 gs_status stage_batch(gs_ctx* c, const gs_edge_batch* b, const int64_t** src, const int64_t** dst,
                       const void** val, bool need_val);
 
+// floor(W * q / P) for q <= P without the 64-bit overflow of W * q (equal-work split points)
+__host__ __device__ inline unsigned long long frac_share(unsigned long long W, unsigned long long q, unsigned long long P) {
+  return (W / P) * q + (W % P) * q / P;
+}
+
 inline size_t dtype_bytes(int dt) { return (dt == GS_I32 || dt == GS_F32) ? 4 : (dt == GS_NONE ? 0 : 8); }
 
 }  // namespace gs

@@ -498,8 +498,8 @@ __global__ void k_tri_bounds(const unsigned long long* __restrict__ pre, uint32_
     }
     return a;
   };
-  const uint32_t u0 = part == 0 ? 0u : lower(W * part / nparts);
-  const uint32_t u1 = part + 1 == nparts ? V : lower(W * (part + 1) / nparts);
+  const uint32_t u0 = part == 0 ? 0u : lower(frac_share(W, part, nparts));
+  const uint32_t u1 = part + 1 == nparts ? V : lower(frac_share(W, part + 1, nparts));
   out[0] = u0;
   out[1] = u1;
   out[2] = pos(u0);
@@ -564,7 +564,7 @@ __global__ void k_tri_split(const unsigned long long* __restrict__ pre, uint32_t
   if (q > P) return;
   const unsigned long long W = pre[V];
   uint32_t a = 0, b = V;
-  const unsigned long long t = W * q / P;
+  const unsigned long long t = frac_share(W, q, P);
   while (a < b) {
     const uint32_t m = (a + b) >> 1;
     if (pre[m] < t) a = m + 1;
@@ -668,7 +668,7 @@ __global__ void k_bd_bounds(const unsigned long long* __restrict__ prew, const u
     }
     return a;
   };
-  const uint32_t cq = q == 0 ? 0u : q == P ? V : lower(W * q / P);
+  const uint32_t cq = q == 0 ? 0u : q == P ? V : lower(frac_share(W, q, P));
   const uint32_t rq = sp.s[q];   // the route split: rank q built the rows of [r_q, r_q+1)
   out[q] = cq;
   out[P + 1 + q] = rq;
@@ -828,6 +828,22 @@ gs_status tri_degrees(gs_ctx* c, const TriGeom& g, uint32_t* deg) {
     return bs;
   }
   return hip_check(c, hipGetLastError(), "degrees");
+}
+
+// the degree sample of a large window: TRI_SAMPLE_SLICES contiguous slices spread evenly over the window,
+// `per` records each, gathered into out_src / out_dst (a prefix alone misses most hubs of a window whose
+// records arrive sorted by source, e.g. a replayed edge list: they would get class 0, the lowest rank,
+// and their whole adjacency would become their out-list)
+constexpr uint64_t TRI_SAMPLE_SLICES = 16;
+__global__ __launch_bounds__(256) void k_tri_sample(const int64_t* __restrict__ src, const int64_t* __restrict__ dst,
+                                                    uint64_t n, uint64_t per, int64_t* __restrict__ out_src,
+                                                    int64_t* __restrict__ out_dst) {
+  const uint64_t stride = n / TRI_SAMPLE_SLICES, total = per * TRI_SAMPLE_SLICES;
+  for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (uint64_t)gridDim.x * 256) {
+    const uint64_t k = i / per, j = i - k * per, at = k * stride + j;
+    out_src[i] = src[at];
+    out_dst[i] = dst[at];
+  }
 }
 
 // degree-class ranks; the ids without an edge (class 0) -> host_small[5] after the next wait
@@ -1093,9 +1109,10 @@ gs_status triangles_impl(gs_ctx* c, const gs_edge_batch* b, uint32_t part, uint3
   uint32_t* rank = c->out_b.as<uint32_t>();
   // The orientation needs only SOME total order of the ids (any order gives the exact count: each
   // triangle is counted once, at its lowest-ranked vertex); the degree classes keep the out-lists short.
-  // A large window's classes come from the degrees of its first n / 4 edges (R-MAT s26: ranks + keys +
-  // sort 98.2 -> 86.5 ms, count +0.9 ms, window 329.0 -> 318.4 ms; s24 62.6 -> 61.3 ms, same box;
-  // profiles/r04/evidence/deg_sample/); the vertices-with-edges figure then comes from the count's
+  // A large window's classes come from the degrees of n / 4 of its edges, in 16 slices spread over the
+  // window (round 4 took the first n / 4: R-MAT s26 ranks + keys + sort 98.2 -> 86.5 ms, count +0.9 ms,
+  // window 329.0 -> 318.4 ms; s24 62.6 -> 61.3 ms, same box; profiles/r04/evidence/deg_sample/; a prefix
+  // misses the hubs of a source-sorted window); the vertices-with-edges figure then comes from the count's
   // vertex pass (k_tri_lclass, k_tri_loop_only).  GS_TRI_DEG_SAMPLE = k overrides the 4 (1 = exact
   // degrees).  The split-window steps (gs_tri_dist_*) keep exact, all-reduced degrees.
   static const int deg_sample_env = getenv("GS_TRI_DEG_SAMPLE") ? atoi(getenv("GS_TRI_DEG_SAMPLE")) : 4;
@@ -1103,7 +1120,17 @@ gs_status triangles_impl(gs_ctx* c, const gs_edge_batch* b, uint32_t part, uint3
   const bool sampled = ds > 1 && nparts == 1 && g.n >= (1ull << 26);
   {
     TriGeom gd = g;
-    if (sampled) gd.n = g.n / ds;
+    if (sampled) {   // n / ds records in TRI_SAMPLE_SLICES slices spread over the window (c->aux: the keys later)
+      const uint64_t per = g.n / ds / TRI_SAMPLE_SLICES;
+      GS_TRY(ensure(c, c->aux, g.n * 8));
+      int64_t* ss = c->aux.as<int64_t>();
+      hipLaunchKernelGGL(k_tri_sample, dim3(8192), dim3(256), 0, c->stream, g.src, g.dst, g.n, per, ss,
+                         ss + per * TRI_SAMPLE_SLICES);
+      GS_HIP(hipGetLastError());
+      gd.src = ss;
+      gd.dst = ss + per * TRI_SAMPLE_SLICES;
+      gd.n = per * TRI_SAMPLE_SLICES;
+    }
     GS_TRY(tri_degrees(c, gd, deg));
   }
   GS_TRY(tri_ranks(c, g, deg, rank));
@@ -1356,7 +1383,11 @@ gs_status gs_tri_dist_route(gs_ctx* c, const uint32_t* dout, uint32_t nparts, ui
   GS_HIP(hipMemcpyAsync(c->host_small + 64, sp_d, (nparts + 1) * 8, hipMemcpyDeviceToHost, c->stream));
   GS_TRY(host_wait(c));
   RtSplit sp;
-  for (uint32_t q = 0; q <= nparts; ++q) sp.s[q] = (uint32_t)c->host_small[64 + q];
+  for (uint32_t q = 0; q <= nparts; ++q) {   // monotone owner ranges (route / plan / need / serve assume them)
+    sp.s[q] = (uint32_t)std::min<uint64_t>(c->host_small[64 + q], V);
+    if (q && sp.s[q] < sp.s[q - 1]) sp.s[q] = sp.s[q - 1];
+  }
+  sp.s[nparts] = (uint32_t)V;
   c->rt_split = sp;
   c->rt_nparts = nparts;
   const uint32_t tiles = (uint32_t)std::max<uint64_t>(1, (n + RT_TILE - 1) / RT_TILE);

@@ -522,7 +522,7 @@ __global__ __launch_bounds__(TH_HBLOCK) __attribute__((amdgpu_waves_per_eu(GS_TH
       }
       return a;
     };
-    const unsigned long long lo = W * blockIdx.x / gridDim.x, hi = W * (blockIdx.x + 1) / gridDim.x;
+    const unsigned long long lo = frac_share(W, blockIdx.x, gridDim.x), hi = frac_share(W, blockIdx.x + 1, gridDim.x);
     h0 = uni(lower(lo));
     h1 = blockIdx.x + 1 == gridDim.x ? nh : uni(lower(hi));
   }

@@ -3,11 +3,12 @@
 The orientation needs only some total order of the ids -- every triangle is counted once, at its
 lowest-ranked vertex, whatever the order (WindowTriangles.java:83-140 emits each candidate pair once per
 vertex; the count does not depend on which vertex) -- and the degree classes only keep the out-lists
-short.  Windows of >= 2^26 edges take their classes from the degrees of their first n / 4 edges by
-default; GS_TRI_DEG_SAMPLE = 1 restores the exact degrees (read once per process, so each setting runs
+short.  Windows of >= 2^26 edges take their classes from the degrees of n / 4 of their edges by
+default (16 slices spread over the window); GS_TRI_DEG_SAMPLE = 1 restores the exact degrees (read once per process, so each setting runs
 in its own interpreter).  On an R-MAT scale-22 window (2^26 edges, self-loops kept) both settings must
 give the same count, and the stage times' "vertices with edges" must equal the window's distinct ids
-in both (with sampled classes it comes from the count's vertex pass, k_tri_lclass).
+in both (with sampled classes it comes from the count's vertex pass, k_tri_lclass).  The same window
+sorted by source (a replayed edge list) must give the same count at about the exact-degree time.
 """
 import subprocess
 import sys
@@ -23,6 +24,7 @@ ROOT = Path(__file__).resolve().parent.parent
 SCRIPT = textwrap.dedent("""
     import os
     import sys
+    import time
     os.environ["GS_TRI_DEG_SAMPLE"] = "{k}"
     import torch
     sys.path.insert(0, {root!r})
@@ -33,7 +35,22 @@ SCRIPT = textwrap.dedent("""
     exact, wrapped, has = eng.triangles(s, d)
     t = eng.stage_times()
     distinct = int(torch.unique(torch.cat([s, d])).numel())
-    print("RESULT", exact, t.vertices, distinct)
+    # the same window with its records sorted by source (a replayed edge list): same count, and the
+    # sample (slices spread over the window) still finds the hubs, so the window costs about the same
+    o = torch.sort(s, stable=True).indices
+    ss, sd = s[o].contiguous(), d[o].contiguous()
+    def best(a, b):
+        ms = []
+        for _ in range(3):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            r = eng.triangles(a, b)
+            torch.cuda.synchronize()
+            ms.append((time.perf_counter() - t0) * 1e3)
+        return r[0], min(ms)
+    c_shuf, ms_shuf = best(s, d)
+    c_sort, ms_sort = best(ss, sd)
+    print("RESULT", exact, t.vertices, distinct, c_sort, int(ms_shuf * 1000), int(ms_sort * 1000))
     eng.close()
 """)
 
@@ -47,9 +64,13 @@ def _run(k):
 
 
 def test_sampled_degree_classes_same_count_and_vertices():
-    count_s, verts_s, distinct = _run(4)
-    count_e, verts_e, distinct_e = _run(1)
+    count_s, verts_s, distinct, sorted_s, us_shuf, us_sort = _run(4)
+    count_e, verts_e, distinct_e, sorted_e, us_shuf_e, us_sort_e = _run(1)
     assert distinct == distinct_e
-    assert count_s == count_e, (count_s, count_e)
+    assert count_s == count_e == sorted_s == sorted_e, (count_s, count_e, sorted_s, sorted_e)
     assert verts_e == distinct, (verts_e, distinct)
     assert verts_s == distinct, (verts_s, distinct)
+    print(f"shuffled / source-sorted window: sampled {us_shuf / 1e3:.2f} / {us_sort / 1e3:.2f} ms, "
+          f"exact {us_shuf_e / 1e3:.2f} / {us_sort_e / 1e3:.2f} ms")
+    # a source-sorted window keeps the sampled classes' work bound (a prefix sample lost it)
+    assert us_sort < 1.5 * us_sort_e, (us_sort, us_sort_e)
