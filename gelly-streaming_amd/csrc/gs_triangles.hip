@@ -1719,11 +1719,15 @@ gs_status gs_window_triangles_dist(gs_ctx* c, const gs_edge_batch* b, uint64_t* 
   *count_ref_wrapped = 0;
   *has_output = total_n > 0;
   if (total_n == 0) return GS_OK;
-  // ids spanning more than 2^TRI_MAX_BITS values: steps 2-5 run on compact ids of the whole window
-  // (step 6, the self-pair term, keeps the original records: its HashSet order needs the values)
+  // ids spanning more than 2^TRI_MAX_BITS values, or an id space more than 4x sparser than the window's
+  // endpoints (the dense per-id tables -- degrees, out-degrees, d+ -- are all-reduced, 4 B per id each):
+  // steps 2-5 run on compact ids of the whole window (step 6, the self-pair term, keeps the original
+  // records: its HashSet order needs the values)
   const gs_edge_batch* lb = b;
   gs_edge_batch rb{};
-  if (const uint64_t dx = (uint64_t)gmin ^ (uint64_t)gmax; dx && 64 - __builtin_clzll(dx) > (int)TRI_MAX_BITS) {
+  const uint64_t dx = (uint64_t)gmin ^ (uint64_t)gmax;
+  const int span_bits = dx ? 64 - __builtin_clzll(dx) : 1;
+  if (span_bits > (int)TRI_MAX_BITS || (span_bits > 20 && (1ull << span_bits) > 8 * total_n)) {
     int64_t vmax = 0;
     GS_TRY(tri_dist_relabel(c, b, &rb, &vmax));
     lb = &rb;

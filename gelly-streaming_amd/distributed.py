@@ -226,7 +226,9 @@ def triangles_window(eng, src, dst, group=None):
     if total == 0:
         return 0, 0, False
     osrc, odst = src, dst   # the self-pair term (step 6) needs the original ids: their HashSet order
-    if ((gmin ^ gmax) & ((1 << 64) - 1)).bit_length() > TRI_MAX_BITS:
+    span_bits = max(1, ((gmin ^ gmax) & ((1 << 64) - 1)).bit_length())
+    if span_bits > TRI_MAX_BITS or (span_bits > 20 and (1 << span_bits) > 8 * total):
+        # (also when the id space is far sparser than the window: the per-id tables are all-reduced)
         src, dst, gmax = relabel_window(src, dst, group)
         gmin = 0
     deg = eng.tri_dist_degrees(src, dst, gmin, gmax)

@@ -14,7 +14,9 @@ the union of the ranks' outputs must equal the whole-window oracle (reference ke
 SimpleEdgeStream.java:159-167), each rank holding exactly the vertices gs_owner_of gives it; the
 triangle count equals the oracle's count of the whole window on every rank (WindowTriangles.java:64-66),
 with self-loops (the reference's self-pair rule), with ids far from 0, and with sparse Long ids spanning
-more than 2^56 values (the split window relabels to the whole window's compact ids: tri_dist_relabel)."""
+more than 2^56 values (the split window relabels to the whole window's compact ids: tri_dist_relabel;
+so does a window whose id space is far sparser than its records, whose per-id tables would be
+all-reduced)."""
 import threading
 
 import numpy as np
@@ -137,7 +139,7 @@ def _tri_windows(oracle):
     s, d = oracle.gen_rmat(SCALE, N, 0x5EED0B, no_self_loops=True)
     ls, ld = oracle.gen_rmat(11, 30_000, 0x5EED0C)           # self-loops kept: the reference's rule
     assert (ls == ld).any()
-    ws, wd = s * 3001 + (5 << 40), d * 3001 + (5 << 40)      # ids far from 0 (a 28-bit span)
+    ws, wd = s * 3 + (5 << 40), d * 3 + (5 << 40)            # ids far from 0, a dense 18-bit span (no relabel)
     sparse = lambda x: x * ((1 << 40) + 12345) - (1 << 60)   # Long ids spanning > 2^56: relabeled
     return {"rmat": (s, d), "loops": (ls, ld), "far": (ws, wd), "sparse": (sparse(s), sparse(d)),
             "sparse_loops": (sparse(ls), sparse(ld))}
