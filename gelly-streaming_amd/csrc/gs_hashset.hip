@@ -257,6 +257,10 @@ __global__ __launch_bounds__(256) void k_cand_meta(const uint64_t* __restrict__ 
 // A wave finds the slot of its first position by a 64-ary search of the block starts vs[0..S]; each
 // 256-position step then resolves its positions against 64 consecutive block starts held one per lane
 // (binary search through lane shuffles; a step that spans more than 64 slots takes the next 64).
+// MODE 0: every step; MODE 1: the fast steps only (the pair rows of one slot: ~99% of a window's steps),
+// compiled without the general path so the kernel holds fewer registers and more of its stores are in
+// flight; MODE 2: the other steps only (run after MODE 1 over the same range).
+template <int MODE>
 __global__ __launch_bounds__(256) void k_cand_emit(const uint64_t* __restrict__ vs, uint32_t S,
                                                    const CandMeta* __restrict__ meta, const int64_t* __restrict__ vkeys,
                                                    const int64_t* __restrict__ nbr, const int64_t* __restrict__ gids,
@@ -303,6 +307,7 @@ __global__ __launch_bounds__(256) void k_cand_emit(const uint64_t* __restrict__ 
       const CandMeta m = cm;
       const uint64_t t0 = base - c_beg;
       if (t0 >= m.d && m.rows) {
+        if constexpr (MODE == 2) continue;   // (MODE 1 wrote it)
         const uint64_t k = m.k, rows = m.rows, q0 = t0 - m.d;
         const double k2 = 2.0 * (double)k + 1.0;
         uint64_t r0 = (uint64_t)fmax(0.0, (k2 - sqrt(fmax(0.0, k2 * k2 - 8.0 * (double)q0))) * 0.5);
@@ -310,12 +315,12 @@ __global__ __launch_bounds__(256) void k_cand_emit(const uint64_t* __restrict__ 
         for (int g = 0; g < 64 && r0 > 0 && tri_rows_before(r0, k) > q0; ++g) --r0;
         for (int g = 0; g < 64 && r0 + 1 < rows && tri_rows_before(r0 + 1, k) <= q0; ++g) ++r0;
         const int64_t* G = gids + m.gbase;
+        uint64_t r = r0;   // a lane's positions increase with i: its row walk carries over
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const uint64_t oi = base + (uint64_t)(i * 64) + lane;
           if (oi >= e1) continue;
           const uint64_t q = q0 + (uint64_t)(i * 64) + lane;
-          uint64_t r = r0;
           for (int g = 0; g < 64 && r + 1 < rows && tri_rows_before(r + 1, k) <= q; ++g) ++r;
           const uint64_t col = min(q - tri_rows_before(r, k), k - 1 - r);
           a[oi - P0] = G[r];
@@ -334,6 +339,18 @@ __global__ __launch_bounds__(256) void k_cand_emit(const uint64_t* __restrict__ 
         }
         continue;   // sc still holds the next step's first position, or an earlier slot
       }
+    }
+    if constexpr (MODE == 1) {
+      // a step for MODE 2: only the slot of the next step's first position (e1), searched forward from sc
+      // over 64 block starts at a time
+      for (;;) {
+        const uint64_t bj = (uint64_t)sc + 1 + lane <= S ? vs[sc + 1 + lane] : ~0ull;
+        const uint64_t at = __ballot(bj <= e1);   // block starts at or below e1 (a prefix of the lanes)
+        const uint32_t c = (uint32_t)__popcll(at);
+        sc += c;
+        if (c < 64) break;
+      }
+      continue;
     }
     uint64_t o[4];
     uint32_t slot[4];
@@ -780,7 +797,253 @@ __device__ void j_put(JMap& m, int32_t x) {
   }
   if (++m.size > m.thr) j_resize(m);
 }
+// ---- the simulation in parallel over bin groups ---------------------------------------------------
+// Until the table reaches capacity 64, a bin of 9 resizes the whole table (treeifyBin below
+// MIN_TREEIFY_CAPACITY): the prefix of the insertions up to that point is simulated by one thread per set
+// (at most a few dozen keys: the size threshold alone takes the table to 64 by the 25th).  From capacity
+// 64 on every bin evolves alone: a resize happens right after the insertion whose index equals the
+// threshold 3C/4 (it depends on the count only), treeifyBin converts its own bin, and a resize splits
+// old bin j into new bins j and j + C only.  So the keys of one group g = hash & 63 -- bins g, g + 64,
+// g + 128, ... at every capacity >= 64 -- are simulated by their own thread: its keys in arrival order
+// (k_hs_jdk_order), the resizes applied at the global insertion indices where they occur, its bins'
+// chains walked in bin order at the end.  At capacity 64 every bin is still a plain list in arrival
+// order (no tree can form below 64), so a group starts from its prefix keys as bin g's list.  The critical
+// path of a hub's set of ~10^5 ids drops from k inserts to ~k / 64.
+__global__ __launch_bounds__(64) void k_hs_jdk_prefix(const uint32_t* __restrict__ list, const uint32_t* __restrict__ nc,
+                                                      const uint64_t* __restrict__ doff, const int64_t* __restrict__ arr,
+                                                      const uint64_t* __restrict__ tbase, JNode* __restrict__ nodes,
+                                                      int32_t* __restrict__ tabs, int64_t* __restrict__ ids,
+                                                      uint32_t* __restrict__ p0, uint32_t* __restrict__ flags) {
+  const uint32_t count = *nc;
+  for (uint32_t s = blockIdx.x * 64u + threadIdx.x; s < count; s += gridDim.x * 64u) {
+    const uint32_t u = list[s];
+    const uint64_t d0 = doff[u], k = doff[u + 1] - d0;
+    JMap m{nodes + d0, arr + d0, tabs + tbase[s], 0, 0, 0, 0};
+    uint32_t j = 0;
+    for (; j < k && m.cap < 64; ++j) {
+      const int64_t x = m.key[j];
+      const uint32_t h0 = (uint32_t)((uint64_t)x ^ ((uint64_t)x >> 32));
+      m.n[j].hash = h0 ^ (h0 >> 16);
+      j_put(m, (int32_t)j);
+    }
+    if (m.flags) atomicOr(flags, m.flags);
+    if (m.cap >= 64) {   // the groups take it from here (the keys before j are plain lists at capacity 64)
+      p0[s] = j;
+      continue;
+    }
+    p0[s] = ~0u;   // the whole set stayed below capacity 64: done here
+    uint64_t o = d0;
+    for (uint32_t b = 0; b < m.cap; ++b)
+      for (int32_t e = m.tab[b]; e >= 0; e = m.n[e].next) ids[o++] = m.key[e];
+  }
+}
+
+// one wave per set: the set's keys stably partitioned by group (hash & 63), as arrival indices, into
+// ord[d0 ..] with the group starts in gofs[65 s ..] (two passes: counts, then positions)
+__global__ __launch_bounds__(64) void k_hs_jdk_order(const uint32_t* __restrict__ list, const uint32_t* __restrict__ nc,
+                                                     const uint64_t* __restrict__ doff, const int64_t* __restrict__ arr,
+                                                     const uint32_t* __restrict__ p0, uint32_t* __restrict__ ord,
+                                                     uint32_t* __restrict__ gofs) {
+  __shared__ uint32_t s_run[64];
+  const uint32_t count = *nc, lane = threadIdx.x;
+  for (uint32_t s = blockIdx.x; s < count; s += gridDim.x) {
+    if (p0[s] == ~0u) continue;   // (uniform over the block)
+    const uint32_t u = list[s];
+    const uint64_t d0 = doff[u], k = doff[u + 1] - d0;
+    s_run[lane] = 0;
+    __syncthreads();
+    for (int pass = 0; pass < 2; ++pass) {
+      for (uint64_t j0 = 0; j0 < k; j0 += 64) {
+        const uint64_t j = j0 + lane;
+        const bool on = j < k;
+        const uint64_t act = ballot(on);
+        uint32_t g = 0;
+        if (on) {
+          const int64_t x = arr[d0 + j];
+          const uint32_t h0 = (uint32_t)((uint64_t)x ^ ((uint64_t)x >> 32));
+          g = (h0 ^ (h0 >> 16)) & 63u;
+        }
+        const uint64_t peers = match_digit<6>(g, act);
+        const uint32_t rank = mbcnt(peers);
+        const bool leader = on && rank == 0;
+        if (pass == 1 && on) ord[d0 + s_run[g] + rank] = (uint32_t)j;
+        __syncthreads();
+        if (leader) s_run[g] += (uint32_t)__popcll(peers);
+        __syncthreads();
+      }
+      if (pass == 0) {   // counts -> group starts
+        const uint32_t c = s_run[lane], inc = wave_inclusive_sum(c);
+        __syncthreads();
+        s_run[lane] = inc - c;
+        gofs[65ull * s + lane] = inc - c;
+        if (lane == 63) gofs[65ull * s + 64] = inc;
+        __syncthreads();
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// insertion at capacity >= 64 (no size bookkeeping: the resizes come from the caller's schedule)
+__device__ void j_put_group(JMap& m, int32_t x) {
+  JNode* n = m.n;
+  const uint32_t h = n[x].hash, i = h & (m.cap - 1);
+  n[x].next = n[x].prev = n[x].parent = n[x].left = n[x].right = -1;
+  n[x].red = 0;
+  n[x].tree = 0;
+  int32_t p = m.tab[i];
+  if (p < 0) {
+    m.tab[i] = x;
+  } else if (n[p].tree) {   // putTreeVal from the bin's root
+    int32_t root = p;
+    while (n[root].parent >= 0) root = n[root].parent;
+    n[x].tree = 1;
+    for (int32_t q = root;;) {
+      const int dir = j_dir(m, q, h, m.key[x]);
+      const int32_t xp = q;
+      if ((q = dir <= 0 ? n[q].left : n[q].right) < 0) {
+        const int32_t xpn = n[xp].next;
+        n[x].next = xpn;
+        if (dir <= 0) n[xp].left = x;
+        else n[xp].right = x;
+        n[xp].next = x;
+        n[x].parent = n[x].prev = xp;
+        if (xpn >= 0) n[xpn].prev = x;
+        j_root_front(m, j_balance(n, root, x));
+        break;
+      }
+    }
+  } else {
+    for (int bin = 0;; ++bin) {
+      const int32_t e = n[p].next;
+      if (e < 0) {
+        n[p].next = x;
+        if (bin >= 7) j_treeify_bin(m, h);   // TREEIFY_THRESHOLD - 1 (capacity >= 64: the bin itself)
+        break;
+      }
+      p = e;
+    }
+  }
+}
+
+// the group's bins of a resize from m.cap to 2 m.cap (the split of j_resize, bins j = g mod 64 only)
+__device__ void j_resize_group(JMap& m, uint32_t g) {
+  const uint32_t ocap = m.cap, ncap = ocap * 2;
+  JNode* n = m.n;
+  for (uint32_t i = ocap + g; i < ncap; i += 64) m.tab[i] = -1;
+  m.cap = ncap;
+  for (uint32_t j = g; j < ocap; j += 64) {
+    const int32_t e = m.tab[j];
+    if (e < 0) continue;
+    m.tab[j] = -1;
+    if (n[e].next < 0) {
+      m.tab[n[e].hash & (ncap - 1)] = e;
+    } else if (n[e].tree) {
+      j_split(m, e, j, ocap);
+    } else {
+      int32_t loH = -1, loT = -1, hiH = -1, hiT = -1;
+      for (int32_t x = e, nx; x >= 0; x = nx) {
+        nx = n[x].next;
+        if ((n[x].hash & ocap) == 0) {
+          if (loT < 0) loH = x;
+          else n[loT].next = x;
+          loT = x;
+        } else {
+          if (hiT < 0) hiH = x;
+          else n[hiT].next = x;
+          hiT = x;
+        }
+      }
+      if (loT >= 0) {
+        n[loT].next = -1;
+        m.tab[j] = loH;
+      }
+      if (hiT >= 0) {
+        n[hiT].next = -1;
+        m.tab[j + ocap] = hiH;
+      }
+    }
+  }
+}
+
+// thread per (set, group): the group's keys from capacity 64 on; then the sizes of its final bins
+__global__ __launch_bounds__(64) void k_hs_jdk_group(const uint32_t* __restrict__ list, const uint32_t* __restrict__ nc,
+                                                     const uint64_t* __restrict__ doff, const int64_t* __restrict__ arr,
+                                                     const uint64_t* __restrict__ tbase, const uint32_t* __restrict__ p0,
+                                                     const uint32_t* __restrict__ ord, const uint32_t* __restrict__ gofs,
+                                                     JNode* __restrict__ nodes, int32_t* __restrict__ tabs,
+                                                     uint64_t* __restrict__ bcnt, uint32_t* __restrict__ flags) {
+  const uint64_t total = (uint64_t)*nc * 64;
+  for (uint64_t t = (uint64_t)blockIdx.x * 64 + threadIdx.x; t < total; t += (uint64_t)gridDim.x * 64) {
+    const uint32_t s = (uint32_t)(t >> 6), g = (uint32_t)(t & 63);
+    const uint32_t P0 = p0[s];
+    if (P0 == ~0u) continue;
+    const uint32_t u = list[s];
+    const uint64_t d0 = doff[u], k = doff[u + 1] - d0;
+    JMap m{nodes + d0, arr + d0, tabs + tbase[s], 64, 0, 0, 0};
+    JNode* n = m.n;
+    const uint32_t* o = ord + d0;
+    const uint32_t a = gofs[65ull * s + g], b = gofs[65ull * s + g + 1];
+    // bin g at capacity 64: the group's prefix keys, a plain list in arrival order
+    int32_t tail = -1;
+    m.tab[g] = -1;
+    uint32_t q = a;
+    for (; q < b && o[q] < P0; ++q) {
+      const int32_t j = (int32_t)o[q];
+      const int64_t x = m.key[j];
+      const uint32_t h0 = (uint32_t)((uint64_t)x ^ ((uint64_t)x >> 32));
+      n[j].hash = h0 ^ (h0 >> 16);
+      n[j].next = n[j].prev = n[j].parent = n[j].left = n[j].right = -1;
+      n[j].red = n[j].tree = 0;
+      if (tail < 0) m.tab[g] = j;
+      else n[tail].next = j;
+      tail = j;
+    }
+    for (; q < b; ++q) {
+      const uint32_t j = o[q];
+      while ((uint64_t)m.cap * 3 / 4 < j) j_resize_group(m, g);   // the resizes after inserts 3C/4 < j
+      const int64_t x = m.key[j];
+      const uint32_t h0 = (uint32_t)((uint64_t)x ^ ((uint64_t)x >> 32));
+      n[j].hash = h0 ^ (h0 >> 16);
+      j_put_group(m, (int32_t)j);
+    }
+    while ((uint64_t)m.cap * 3 / 4 < k) j_resize_group(m, g);   // the resizes after the set's last inserts
+    if (m.flags) atomicOr(flags, m.flags);
+    uint64_t* bc = bcnt + tbase[s];
+    for (uint32_t bin = g; bin < m.cap; bin += 64) {
+      uint64_t c = 0;
+      for (int32_t e = m.tab[bin]; e >= 0; e = n[e].next) ++c;
+      bc[bin] = c;
+    }
+  }
+}
+
+// thread per (set, group): the chains of the group's bins at their iteration positions
+__global__ __launch_bounds__(64) void k_hs_jdk_write(const uint32_t* __restrict__ list, const uint32_t* __restrict__ nc,
+                                                     const uint64_t* __restrict__ doff, const int64_t* __restrict__ arr,
+                                                     const uint64_t* __restrict__ tbase, const uint32_t* __restrict__ p0,
+                                                     const JNode* __restrict__ nodes, const int32_t* __restrict__ tabs,
+                                                     const uint64_t* __restrict__ bpos, int64_t* __restrict__ ids) {
+  const uint64_t total = (uint64_t)*nc * 64;
+  for (uint64_t t = (uint64_t)blockIdx.x * 64 + threadIdx.x; t < total; t += (uint64_t)gridDim.x * 64) {
+    const uint32_t s = (uint32_t)(t >> 6), g = (uint32_t)(t & 63);
+    if (p0[s] == ~0u) continue;
+    const uint32_t u = list[s];
+    const uint64_t d0 = doff[u], k = doff[u + 1] - d0;
+    uint64_t cap = 64;
+    while (cap * 3 / 4 < k) cap <<= 1;
+    const JNode* n = nodes + d0;
+    const int32_t* tab = tabs + tbase[s];
+    const uint64_t* bp = bpos + tbase[s];
+    for (uint64_t bin = g; bin < cap; bin += 64) {
+      uint64_t at = d0 + (bp[bin] - bp[0]);
+      for (int32_t e = tab[bin]; e >= 0; e = n[e].next) ids[at++] = arr[d0 + e];
+    }
+  }
+}
+
 // thread per complex vertex: insert its ids in arrival order, then write them in iteration order
+// (GS_HS_JDK_SERIAL = 1: the round-4 kernel, for A/B; the default is the group-parallel one above)
 __global__ __launch_bounds__(64) void k_hs_jdk(const uint32_t* __restrict__ list, const uint32_t* __restrict__ nc,
                                                const uint64_t* __restrict__ doff, const int64_t* __restrict__ arr,
                                                const uint64_t* __restrict__ tbase, JNode* __restrict__ nodes,
@@ -813,7 +1076,7 @@ namespace gs {
 enum { HS_VKEYS, HS_OFF, HS_NBR, HS_USEG, HS_COMP, HS_PIDX, HS_DKEY, HS_DFIRST, HS_DOFF, HS_OKEY, HS_OMID,
        HS_UKEY, HS_ORD, HS_IDS, HS_G, HS_GX, HS_TILES, HS_F, HS_FX, HS_CSZ, HS_CBASE, HS_CNT, HS_CPLX,
        HS_CLIST, HS_TSZ, HS_TBASE, HS_ARR, HS_NODES, HS_TABS, HS_GIDS, HS_OWN, HS_SLOT, HS_META, HS_SIZE, HS_VS,
-       HS_COUNT };
+       HS_P0, HS_GORD, HS_GOFS, HS_BCNT, HS_BPOS, HS_COUNT };
 static_assert(HS_COUNT <= 40, "gs_ctx::hs");
 
 gs_status xscan(gs_ctx* c, const uint64_t* in, uint64_t n, uint64_t* out) {
@@ -884,9 +1147,38 @@ static gs_status hashset_exact(gs_ctx* c, uint64_t R, uint64_t U, uint64_t M, ui
   GS_TRY(ensure(c, c->hs[HS_NODES], M * sizeof(JNode)));
   GS_TRY(ensure(c, c->hs[HS_TABS], T * 4));
   const unsigned grid = (unsigned)std::min<uint64_t>((nc + 63) / 64, 4096);
-  hipLaunchKernelGGL(k_hs_jdk, dim3(grid), dim3(64), 0, c->stream, c->hs[HS_CLIST].as<uint32_t>(), d_hs,
-                     c->hs[HS_DOFF].as<uint64_t>(), c->hs[HS_ARR].as<int64_t>(), c->hs[HS_TBASE].as<uint64_t>(),
-                     c->hs[HS_NODES].as<JNode>(), c->hs[HS_TABS].as<int32_t>(), c->hs[HS_IDS].as<int64_t>(), d_hs + 1);
+  static const bool serial = getenv("GS_HS_JDK_SERIAL") && atoi(getenv("GS_HS_JDK_SERIAL")) != 0;   // A/B
+  if (serial) {
+    hipLaunchKernelGGL(k_hs_jdk, dim3(grid), dim3(64), 0, c->stream, c->hs[HS_CLIST].as<uint32_t>(), d_hs,
+                       c->hs[HS_DOFF].as<uint64_t>(), c->hs[HS_ARR].as<int64_t>(), c->hs[HS_TBASE].as<uint64_t>(),
+                       c->hs[HS_NODES].as<JNode>(), c->hs[HS_TABS].as<int32_t>(), c->hs[HS_IDS].as<int64_t>(), d_hs + 1);
+  } else {
+    GS_TRY(ensure(c, c->hs[HS_P0], nc * 4 + 4));
+    GS_TRY(ensure(c, c->hs[HS_GORD], M * 4 + 4));
+    GS_TRY(ensure(c, c->hs[HS_GOFS], nc * 65 * 4 + 4));
+    GS_TRY(ensure(c, c->hs[HS_BCNT], (T + 1) * 8));
+    GS_TRY(ensure(c, c->hs[HS_BPOS], (T + 1) * 8));
+    const uint32_t* cl = c->hs[HS_CLIST].as<uint32_t>();
+    uint32_t* p0 = c->hs[HS_P0].as<uint32_t>();
+    hipLaunchKernelGGL(k_hs_jdk_prefix, dim3(grid), dim3(64), 0, c->stream, cl, d_hs, c->hs[HS_DOFF].as<uint64_t>(),
+                       c->hs[HS_ARR].as<int64_t>(), c->hs[HS_TBASE].as<uint64_t>(), c->hs[HS_NODES].as<JNode>(),
+                       c->hs[HS_TABS].as<int32_t>(), c->hs[HS_IDS].as<int64_t>(), p0, d_hs + 1);
+    hipLaunchKernelGGL(k_hs_jdk_order, dim3((unsigned)std::min<uint64_t>(nc, 16384)), dim3(64), 0, c->stream, cl, d_hs,
+                       c->hs[HS_DOFF].as<uint64_t>(), c->hs[HS_ARR].as<int64_t>(), (const uint32_t*)p0,
+                       c->hs[HS_GORD].as<uint32_t>(), c->hs[HS_GOFS].as<uint32_t>());
+    GS_HIP(hipMemsetAsync(c->hs[HS_BCNT].p, 0, (T + 1) * 8, c->stream));
+    const unsigned ggrid = (unsigned)std::min<uint64_t>(nc, 16384);   // 64 threads (groups) per set
+    hipLaunchKernelGGL(k_hs_jdk_group, dim3(ggrid), dim3(64), 0, c->stream, cl, d_hs, c->hs[HS_DOFF].as<uint64_t>(),
+                       c->hs[HS_ARR].as<int64_t>(), c->hs[HS_TBASE].as<uint64_t>(), (const uint32_t*)p0,
+                       (const uint32_t*)c->hs[HS_GORD].as<uint32_t>(), (const uint32_t*)c->hs[HS_GOFS].as<uint32_t>(),
+                       c->hs[HS_NODES].as<JNode>(), c->hs[HS_TABS].as<int32_t>(), c->hs[HS_BCNT].as<uint64_t>(), d_hs + 1);
+    GS_HIP(hipGetLastError());
+    GS_TRY(xscan(c, c->hs[HS_BCNT].as<uint64_t>(), T, c->hs[HS_BPOS].as<uint64_t>()));
+    hipLaunchKernelGGL(k_hs_jdk_write, dim3(ggrid), dim3(64), 0, c->stream, cl, d_hs, c->hs[HS_DOFF].as<uint64_t>(),
+                       c->hs[HS_ARR].as<int64_t>(), c->hs[HS_TBASE].as<uint64_t>(), (const uint32_t*)p0,
+                       (const JNode*)c->hs[HS_NODES].as<JNode>(), (const int32_t*)c->hs[HS_TABS].as<int32_t>(),
+                       (const uint64_t*)c->hs[HS_BPOS].as<uint64_t>(), c->hs[HS_IDS].as<int64_t>());
+  }
   GS_HIP(hipGetLastError());
   c->host_small[6] = 0;
   GS_HIP(hipMemcpyAsync(c->host_small + 6, d_hs, 8, hipMemcpyDeviceToHost, c->stream));
@@ -1045,9 +1337,19 @@ static gs_status cand_emit(gs_ctx* c, uint32_t S, uint64_t P0, uint64_t P1, int6
   const uint64_t blocks = std::max<uint64_t>(1, std::min<uint64_t>((n + 4095) / 4096, 4096));
   const uint64_t waves = blocks * 4;
   const uint64_t per_wave = ((n + waves - 1) / waves + 255) / 256 * 256;
-  hipLaunchKernelGGL(k_cand_emit, dim3((unsigned)blocks), dim3(256), 0, c->stream, c->hs[HS_VS].as<uint64_t>(), S,
-                     c->hs[HS_META].as<CandMeta>(), c->hs[HS_VKEYS].as<int64_t>(), c->hs[HS_NBR].as<int64_t>(),
-                     c->hs[HS_GIDS].as<int64_t>(), P0, P1, per_wave, a, b, f, ((uintptr_t)f & 3) == 0 ? 1 : 0);
+  const int f4 = ((uintptr_t)f & 3) == 0 ? 1 : 0;
+  static const int split_env = getenv("GS_CAND_SPLIT") ? atoi(getenv("GS_CAND_SPLIT")) : 1;   // A/B
+  auto launch = [&](auto kern) {
+    hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(256), 0, c->stream, c->hs[HS_VS].as<uint64_t>(), S,
+                       c->hs[HS_META].as<CandMeta>(), c->hs[HS_VKEYS].as<int64_t>(), c->hs[HS_NBR].as<int64_t>(),
+                       c->hs[HS_GIDS].as<int64_t>(), P0, P1, per_wave, a, b, f, f4);
+  };
+  if (split_env) {   // the pair-row steps in a lean kernel, then the rest
+    launch(k_cand_emit<1>);
+    launch(k_cand_emit<2>);
+  } else {
+    launch(k_cand_emit<0>);
+  }
   return hip_check(c, hipGetLastError(), "k_cand_emit");
 }
 
@@ -1172,8 +1474,11 @@ gs_status gs_candidates_next(gs_ctx* c, gs_pair_out* out, uint64_t* first_record
     GS_HIP(hipMemcpyAsync(out->a, a, n * 8, hipMemcpyDeviceToHost, c->stream));
     GS_HIP(hipMemcpyAsync(out->b, bb, n * 8, hipMemcpyDeviceToHost, c->stream));
     GS_HIP(hipMemcpyAsync(out->is_candidate, f, n, hipMemcpyDeviceToHost, c->stream));
+    GS_TRY(host_wait(c));
   }
-  GS_TRY(host_wait(c));
+  // device output: the chunk is enqueued on the ctx stream and the call returns without waiting (the
+  // record count is known on the host), so a consumer ordered after it on that stream -- or waiting on an
+  // event recorded there -- streams chunk after chunk with no host round trip between them
   c->cand_cursor = P1;
   if (done) *done = P1 >= c->cand_total;
   return GS_OK;

@@ -224,7 +224,10 @@ GS_API gs_status gs_window_candidates(gs_ctx* ctx, const gs_edge_batch* batch, g
  * HashSet-ordered neighbour sets once and returns the number of records gs_window_candidates would
  * write; each gs_candidates_next then writes the next min(out->capacity, remaining) records, in
  * gs_window_candidates' order (*first_record = the global position of the chunk's first record; a
- * vertex's records may straddle chunks), and sets *done after the last.  The session lives in the ctx
+ * vertex's records may straddle chunks), and sets *done after the last.  With device output
+ * (out->mem == GS_MEM_DEVICE) the chunk is only enqueued on the ctx stream: the call returns without
+ * waiting for it, and the records are there for work ordered after it on that stream (gs_set_stream) or
+ * after gs_synchronize; host output returns with the records copied.  The session lives in the ctx
  * workspace: any other entry point called on the ctx ends it (gs_candidates_next then fails with
  * GS_EINVAL). */
 GS_API gs_status gs_candidates_begin(gs_ctx* ctx, const gs_edge_batch* batch, uint64_t* total_records,

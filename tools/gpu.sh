@@ -9,6 +9,8 @@
 #   sq      TAG [bench args]    SQ counter passes (LDS conflicts, waits, instruction mix) over a short bench
 #   tri     TAG SCALE           triangles: bench line, kernel-trace stats, FETCH / TCC hit / SQ passes
 #   evidence TAG                every secondary bench line DESIGN.md quotes
+#   ab      TAG "V1 V2.." [args] A/B of tuning builds (csrc/Makefile bvariant / variant -> variants/NAME; "base" =
+#                               the in-tree library): bench lines alternated twice on one box -> ab_NAME_REP.json
 #
 # Every GPU step has its own time limit and the chain stops at the first failure (set -e): after a
 # fault, an abort or a timeout nothing more runs on the GPU in that call.
@@ -49,6 +51,14 @@ case $MODE in
     trace trace_tri_s$S $A
     pmc pmc_tri_s$S/fetch "FETCH_SIZE TCC_HIT_sum" $A --windows 1
     pmc pmc_tri_s$S/sq "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_LDS_BANK_CONFLICT SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_BUSY_CYCLES" $A --windows 1 ;;
+  ab)
+    VARIANTS=$1; shift
+    for rep in 1 2; do
+      for v in $VARIANTS; do
+        if [ "$v" = base ]; then lib=gelly-streaming_amd/libgellyhip.so; else lib=gelly-streaming_amd/variants/$v/libgellyhip.so; fi
+        GELLY_HIP_LIB=$lib bench ab_${v}_$rep "$@" --no-cpu-baseline
+      done
+    done ;;
   evidence)
     bench bench_c2_f64 --dtype float64
     bench bench_c3_rmat --workload fold
