@@ -74,6 +74,8 @@ def parse():
                    help="after timing: sum(per-vertex sums) == sum(values) and ascending keys on each window")
     p.add_argument("--chunk-records", type=float, default=2 ** 28,
                    help="cand_stream: records per gs_candidates_next chunk")
+    p.add_argument("--cand-consumer", default="sum", choices=["sum", "none"],
+                   help="cand_stream: a device consumer reads every record (column sums), or none (emission alone)")
     p.add_argument("--cand-windows", type=int, default=2,
                    help="cand_stream: consecutive windows streamed (the next window's sets built while the current "
                         "one's chunks drain)")
@@ -497,13 +499,18 @@ def cand_stream_main(a):
                 emitted.record(est)
             assert first == got, (first, got)
             n = int(ca.numel())
-            with torch.cuda.stream(cons):
-                cons.wait_event(emitted)
-                n8 = (n // 8) * 8
-                sums.append(torch.stack([ca.sum(), cb.sum(), cf[:n8].view(torch.int64).sum() + cf[n8:].sum()]))
-                ev1 = torch.cuda.Event(enable_timing=True)
-                ev1.record(cons)
-                freed[k] = ev1
+            if a.cand_consumer == "none":   # emission alone: the result is available in HBM
+                ev1 = emitted = torch.cuda.Event(enable_timing=True)
+                with torch.cuda.stream(est):
+                    ev1.record(est)
+            else:
+                with torch.cuda.stream(cons):
+                    cons.wait_event(emitted)
+                    n8 = (n // 8) * 8
+                    sums.append(torch.stack([ca.sum(), cb.sum(), cf[:n8].view(torch.int64).sum() + cf[n8:].sum()]))
+                    ev1 = torch.cuda.Event(enable_timing=True)
+                    ev1.record(cons)
+                    freed[k] = ev1
             ev_pairs.append((ev0, ev1))
             got += n
             nchunk += 1
@@ -537,7 +544,8 @@ def cand_stream_main(a):
                        "chunk_latency_ms_p50": float(np.percentile(lat_ms, 50)),
                        "chunk_latency_ms_p99": float(np.percentile(lat_ms, 99)),
                        "window_period_s": period, "sustained_edges_per_s": E / period,
-                       "target_edges_per_s": 1e8, "checksum": int(chk), "parallelism": "1 GPU"},
+                       "target_edges_per_s": 1e8, "checksum": int(chk), "consumer": a.cand_consumer,
+                       "parallelism": "1 GPU"},
             "roofline": {"bound": "hbm", "kernel": "whole window (emission + consumer)",
                          "achieved": round(17 * total / elapsed / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(17 * total / elapsed / 1e9 / HBM_PEAK_GBS, 4), "traffic": None,

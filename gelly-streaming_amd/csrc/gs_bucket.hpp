@@ -34,9 +34,6 @@ constexpr int BK_INFO_BLOCK = 512;
 // (k_bk_accum, packed records, A/B of round 3: the next group's loads in flight during this group's
 // atomics, C2 accumulate 0.345 vs 0.331 ms: removed)
 constexpr int BK_ACC_BLOCK = 1024;     // 16 waves: one workgroup per CU (LDS-bound)
-#ifndef GS_ACC_HUB
-#define GS_ACC_HUB 0   // A/B: wave-combined hub records in k_bk_accum (records of the group on one key)
-#endif
 constexpr int BK_NW = BK_ACC_BLOCK / WAVE;
 constexpr int BK_PLAN_BLOCK = 1024;
 
@@ -1676,36 +1673,11 @@ __global__ __launch_bounds__(BK_ACC_BLOCK) void k_bk_accum(Src src, const BkItem
               const uint32_t h0 = x[u].x >> 16, h1 = x[u].y >> 16, h2 = x[u].z >> 16, h3 = x[u].w >> 16;
               bool rare = (h0 == PK_ESC) | (h1 == PK_ESC) | (h2 == PK_ESC) | (h3 == PK_ESC);
               if constexpr (P::OP_IS_SUM) rare |= (h0 == 0u) | (h1 == 0u) | (h2 == 0u) | (h3 == 0u);
-              uint32_t done4 = 0;   // records already added by the wave's hub sum
-#if GS_ACC_HUB
-              if constexpr (P::OP_IS_SUM) {
-                // a hub's records meet in one LDS address (same-address atomics of one instruction
-                // serialize): when >= GS_ACC_HUB records of the group's 256 carry the first lane's first key,
-                // the wave sums them (a full wave only) and lane 0 adds the sum once
-                if (ballot(true) == ~0ull) {
-                  const uint32_t k0 = x[u].x & (P::W - 1), k1 = x[u].y & (P::W - 1), k2 = x[u].z & (P::W - 1),
-                                 k3 = x[u].w & (P::W - 1);
-                  const uint32_t kf = __builtin_amdgcn_readfirstlane(k0);
-                  done4 = rare ? 0u : ((k0 == kf) | (k1 == kf) << 1 | (k2 == kf) << 2 | (k3 == kf) << 3);
-                  const uint32_t many = (uint32_t)__popcll(ballot(done4 & 1)) + (uint32_t)__popcll(ballot(done4 & 2)) +
-                                        (uint32_t)__popcll(ballot(done4 & 4)) + (uint32_t)__popcll(ballot(done4 & 8));
-                  if (many >= GS_ACC_HUB) {
-                    uint32_t part = (done4 & 1 ? h0 : 0u) + (done4 & 2 ? h1 : 0u) + (done4 & 4 ? h2 : 0u) +
-                                    (done4 & 8 ? h3 : 0u);   // < 2^18 per lane, < 2^24 per wave
-#pragma unroll
-                    for (int o = 32; o > 0; o >>= 1) part += __shfl_xor(part, o, WAVE);
-                    if ((threadIdx.x & 63) == 0) P::add_narrow(s, kf, part);
-                  } else {
-                    done4 = 0;
-                  }
-                }
-              }
-#endif
               if (!rare) {
-                if (!(done4 & 1)) P::add_narrow(s, x[u].x & (P::W - 1), h0);
-                if (!(done4 & 2)) P::add_narrow(s, x[u].y & (P::W - 1), h1);
-                if (!(done4 & 4)) P::add_narrow(s, x[u].z & (P::W - 1), h2);
-                if (!(done4 & 8)) P::add_narrow(s, x[u].w & (P::W - 1), h3);
+                P::add_narrow(s, x[u].x & (P::W - 1), h0);
+                P::add_narrow(s, x[u].y & (P::W - 1), h1);
+                P::add_narrow(s, x[u].z & (P::W - 1), h2);
+                P::add_narrow(s, x[u].w & (P::W - 1), h3);
                 continue;
               }
             }

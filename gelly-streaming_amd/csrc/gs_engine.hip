@@ -430,7 +430,7 @@ void gs_destroy(gs_ctx* c) {
                     &c->pr_a, &c->pr_b, &c->pr_f, &c->pr_key, &c->pr_val, &c->pr_gk, &c->pr_gv, &c->pr_small,
                     &c->tx_text, &c->tx_cnt, &c->tx_starts, &c->zipf_cdf,
                     &c->dist_k, &c->dist_v, &c->dist_v2, &c->dist_k2, &c->dist_v3, &c->dist_v4, &c->dist_cnt,
-                    &c->dist_x, &c->dist_x2, &c->comm_scratch, &c->cand_bounds, &c->ck_k[0], &c->ck_k[1], &c->ck_a[0],
+                    &c->dist_x, &c->dist_x2, &c->comm_scratch, &c->cand_bounds, &c->cand_steps, &c->hs_rank, &c->ck_k[0], &c->ck_k[1], &c->ck_a[0],
                     &c->ck_a[1], &c->ck_b[0], &c->ck_b[1], &c->sp[0].tot, &c->sp[1].tot, &c->sp_cur})
     if (b->p) hipFree(b->p);
   for (DevBuf& b : c->rl)

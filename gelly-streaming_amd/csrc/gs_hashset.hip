@@ -111,10 +111,20 @@ __global__ __launch_bounds__(XS_BLOCK) void k_xs_apply(const uint64_t* __restric
 // ---- pipeline kernels -------------------------------------------------------------------------
 // per sorted record position p: neighbour (original ID), owning vertex, composite (u << B | x)
 // (composite = (u << B) | rank(x): vertices are densely ranked, so any Long ID range fits 64 bits)
+// dense rank table of the window's vertices when every id differs from the first sorted id only in its low
+// bits (<= HS_RANK_BITS of them: the sort's key mask): rank[x ^ vkeys[0]] = u, so k_hs_prep ranks a
+// neighbour with one read instead of a binary search
+constexpr int HS_RANK_BITS = 28;
+__global__ __launch_bounds__(256) void k_hs_rank(const int64_t* __restrict__ vkeys, uint32_t U, uint32_t* __restrict__ rank) {
+  const uint64_t k0 = (uint64_t)vkeys[0];
+  for (uint32_t u = blockIdx.x * 256u + threadIdx.x; u < U; u += gridDim.x * 256u) rank[(uint64_t)vkeys[u] ^ k0] = u;
+}
+
 __global__ __launch_bounds__(256) void k_hs_prep(const uint32_t* __restrict__ rec, uint32_t R,
                                                  const int64_t* __restrict__ src, const int64_t* __restrict__ dst,
                                                  const uint64_t* __restrict__ off, const int64_t* __restrict__ vkeys,
-                                                 uint32_t U, uint32_t B, int64_t* __restrict__ nbr,
+                                                 uint32_t U, uint32_t B, const uint32_t* __restrict__ rank,
+                                                 int64_t* __restrict__ nbr,
                                                  uint32_t* __restrict__ useg, uint64_t* __restrict__ comp,
                                                  uint32_t* __restrict__ pidx) {
   for (uint32_t p = blockIdx.x * 256u + threadIdx.x; p < R; p += gridDim.x * 256u) {
@@ -123,10 +133,14 @@ __global__ __launch_bounds__(256) void k_hs_prep(const uint32_t* __restrict__ re
     const int64_t x = (r & 1u) ? src[i] : dst[i];   // ALL: r = 2i -> (src, dst), 2i+1 -> (dst, src)
     const uint32_t u = seg_of(off, U, p);
     uint32_t lo = 0, hi = U - 1;                      // rank of x among the window's vertices
-    while (lo < hi) {
-      const uint32_t mid = (lo + hi) >> 1;
-      if (vkeys[mid] < x) lo = mid + 1;
-      else hi = mid;
+    if (rank) {
+      lo = rank[(uint64_t)x ^ (uint64_t)vkeys[0]];
+    } else {
+      while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (vkeys[mid] < x) lo = mid + 1;
+        else hi = mid;
+      }
     }
     nbr[p] = x;
     useg[p] = u;
@@ -251,40 +265,120 @@ __global__ __launch_bounds__(256) void k_cand_meta(const uint64_t* __restrict__ 
   }
 }
 
-// The records at output positions [P0, P1), written to a/b/f[o - P0].  Each wave owns per_wave
-// consecutive positions (a multiple of 256) and walks them 256 at a time, lane l taking positions
-// base + 64 i + l: every store of a wave is one contiguous run (512 B of a, 512 B of b, 64 B of f).
-// A wave finds the slot of its first position by a 64-ary search of the block starts vs[0..S]; each
-// 256-position step then resolves its positions against 64 consecutive block starts held one per lane
-// (binary search through lane shuffles; a step that spans more than 64 slots takes the next 64).
-// MODE 0: every step; MODE 1: the fast steps only (the pair rows of one slot: ~99% of a window's steps),
-// compiled without the general path so the kernel holds fewer registers and more of its stores are in
-// flight; MODE 2: the other steps only (run after MODE 1 over the same range).
-template <int MODE>
-__global__ __launch_bounds__(256) void k_cand_emit(const uint64_t* __restrict__ vs, uint32_t S,
+// One 256-position step [base, min(w1, base + 256)) by the general path: lane l takes positions
+// base + 64 i + l; each position's slot is resolved against 64 consecutive block starts held one per lane
+// (binary search through lane shuffles; a step that spans more than 64 slots takes the next 64), starting
+// at slot sc (the slot of base or an earlier one).  Returns the slot of the step's last position.
+__device__ __forceinline__ uint32_t cand_slow_step(const uint64_t* __restrict__ vs, uint32_t S,
                                                    const CandMeta* __restrict__ meta, const int64_t* __restrict__ vkeys,
                                                    const int64_t* __restrict__ nbr, const int64_t* __restrict__ gids,
-                                                   uint64_t P0, uint64_t P1, uint64_t per_wave,
-                                                   int64_t* __restrict__ a, int64_t* __restrict__ b,
-                                                   uint8_t* __restrict__ f, int f4) {
-  const uint32_t lane = threadIdx.x & 63;
-  const uint64_t wave = ((uint64_t)blockIdx.x * 256u + threadIdx.x) >> 6;
-  const uint64_t w0 = P0 + wave * per_wave;
-  if (w0 >= P1) return;   // wave-uniform
-  const uint64_t w1 = min(P1, w0 + per_wave);
-  // slot of w0: invariant vs[lo] <= w0 and (hi == S or vs[hi] > w0); vs[0] = 0 <= P0
+                                                   uint64_t P0, uint64_t base, uint64_t w1, uint32_t sc, uint32_t lane,
+                                                   int64_t* __restrict__ a, int64_t* __restrict__ b, uint8_t* __restrict__ f) {
+  uint64_t o[4];
+  uint32_t slot[4];
+  bool need[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    o[i] = base + (uint64_t)(i * 64) + lane;
+    need[i] = o[i] < w1;
+    slot[i] = sc;
+  }
+  for (uint32_t s0 = sc;; s0 += 64) {
+    const uint64_t bj = (uint64_t)s0 + 1 + lane <= S ? vs[s0 + 1 + lane] : ~0ull;
+    const uint64_t top = __shfl(bj, 63, 64);
+    bool pend = false;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      int pos = 0;   // block starts vs[s0 + 1 ..] at or below o[i]: 0..63 by halving, 64 past the window
+#pragma unroll
+      for (int st = 32; st > 0; st >>= 1) {
+        const uint64_t v = __shfl(bj, pos + st - 1, 64);
+        pos += v <= o[i] ? st : 0;
+      }
+      if (top <= o[i]) pos = 64;
+      if (need[i] && pos < 64) {
+        slot[i] = s0 + pos;
+        need[i] = false;
+      }
+      pend |= need[i];
+    }
+    if (!__any(pend)) break;
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    if (o[i] >= w1) continue;
+    const uint32_t sl = slot[i];
+    const CandMeta m = meta[sl];
+    const uint64_t t = o[i] - vs[sl];
+    int64_t av, bv;
+    uint8_t fv;
+    if (t < m.d) {
+      av = vkeys[m.u];
+      bv = nbr[m.nbr_off + t];
+      fv = 0;
+    } else if (m.rows) {
+      // row r of the block: the largest r with r k - r (r - 1) / 2 <= q (closed form, then at most a
+      // step or two of correction for the double rounding; the loops are bounded regardless)
+      const uint64_t q = t - m.d, k = m.k, rows = m.rows;
+      const double k2 = 2.0 * (double)k + 1.0;
+      uint64_t r = (uint64_t)fmax(0.0, (k2 - sqrt(fmax(0.0, k2 * k2 - 8.0 * (double)q))) * 0.5);
+      if (r >= rows) r = rows - 1;
+      for (int g = 0; g < 64 && r > 0 && tri_rows_before(r, k) > q; ++g) --r;
+      for (int g = 0; g < 64 && r + 1 < rows && tri_rows_before(r + 1, k) <= q; ++g) ++r;
+      const uint64_t col = min(q - tri_rows_before(r, k), k - 1 - r);
+      av = gids[m.gbase + r];
+      bv = gids[m.gbase + r + col];
+      fv = 1;
+    } else {   // not reached: a block without pair rows holds only its edge records
+      av = bv = 0;
+      fv = 1;
+    }
+    a[o[i] - P0] = av;
+    b[o[i] - P0] = bv;
+    f[o[i] - P0] = fv;
+  }
+  return __shfl(slot[3], 63, 64);   // the slot of this step's last position (the next step starts there)
+}
+
+// slot of position w: invariant vs[lo] <= w and (hi == S or vs[hi] > w) (a 64-ary search; vs[0] = 0)
+__device__ __forceinline__ uint32_t cand_find_slot(const uint64_t* __restrict__ vs, uint32_t S, uint64_t w,
+                                                   uint32_t lane) {
   uint32_t lo = 0, hi = S;
   while (hi - lo > 1) {
     const uint32_t step = (hi - lo + 63) / 64;
     const uint64_t idx = (uint64_t)lo + (uint64_t)lane * step;
-    const bool t = idx < hi && vs[idx] <= w0;
+    const bool t = idx < hi && vs[idx] <= w;
     const uint64_t m = __ballot(t);
     const uint32_t L = 63 - __clzll(m);
     const uint32_t nlo = lo + L * step;
     hi = min(hi, nlo + step);
     lo = nlo;
   }
-  uint32_t sc = lo;
+  return lo;
+}
+
+// The records at output positions [P0, P1), written to a/b/f[o - P0].  Each wave owns per_wave
+// consecutive positions (a multiple of 256) and walks them 256 at a time, lane l taking positions
+// base + 64 i + l: every store of a wave is one contiguous run (512 B of a, 512 B of b, 64 B of f).
+// A wave finds the slot of its first position by a 64-ary search of the block starts vs[0..S].
+// MODE 0: every step, by the fast path where it applies and cand_slow_step otherwise.  MODE 1: the fast
+// steps only (the pair rows of one slot: ~99% of a window's steps), compiled without the general path
+// so the kernel holds fewer registers and more of its stores are in flight; every other step's base is
+// appended to `steps` (count in steps_n) for k_cand_emit_rest.
+template <int MODE>
+__global__ __launch_bounds__(256) void k_cand_emit(const uint64_t* __restrict__ vs, uint32_t S,
+                                                   const CandMeta* __restrict__ meta, const int64_t* __restrict__ vkeys,
+                                                   const int64_t* __restrict__ nbr, const int64_t* __restrict__ gids,
+                                                   uint64_t P0, uint64_t P1, uint64_t per_wave,
+                                                   int64_t* __restrict__ a, int64_t* __restrict__ b,
+                                                   uint8_t* __restrict__ f, int f4, uint64_t* __restrict__ steps,
+                                                   uint32_t* __restrict__ steps_n) {
+  const uint32_t lane = threadIdx.x & 63;
+  const uint64_t wave = ((uint64_t)blockIdx.x * 256u + threadIdx.x) >> 6;
+  const uint64_t w0 = P0 + wave * per_wave;
+  if (w0 >= P1) return;   // wave-uniform
+  const uint64_t w1 = min(P1, w0 + per_wave);
+  uint32_t sc = cand_find_slot(vs, S, w0, lane);
   // the current slot's block start / end and metadata, reloaded only when the step moves to another slot
   // (a fast step then issues no load before its id gathers; re-reading them every step put two dependent
   // loads in front of each step's stores)
@@ -307,7 +401,6 @@ __global__ __launch_bounds__(256) void k_cand_emit(const uint64_t* __restrict__ 
       const CandMeta m = cm;
       const uint64_t t0 = base - c_beg;
       if (t0 >= m.d && m.rows) {
-        if constexpr (MODE == 2) continue;   // (MODE 1 wrote it)
         const uint64_t k = m.k, rows = m.rows, q0 = t0 - m.d;
         const double k2 = 2.0 * (double)k + 1.0;
         uint64_t r0 = (uint64_t)fmax(0.0, (k2 - sqrt(fmax(0.0, k2 * k2 - 8.0 * (double)q0))) * 0.5);
@@ -341,81 +434,36 @@ __global__ __launch_bounds__(256) void k_cand_emit(const uint64_t* __restrict__ 
       }
     }
     if constexpr (MODE == 1) {
-      // a step for MODE 2: only the slot of the next step's first position (e1), searched forward from sc
-      // over 64 block starts at a time
+      // the step goes to k_cand_emit_rest; here only the slot of the next step's first position (e1),
+      // searched forward from sc over 64 block starts at a time
+      if (lane == 0) steps[atomicAdd(steps_n, 1u)] = base;
       for (;;) {
         const uint64_t bj = (uint64_t)sc + 1 + lane <= S ? vs[sc + 1 + lane] : ~0ull;
-        const uint64_t at = __ballot(bj <= e1);   // block starts at or below e1 (a prefix of the lanes)
-        const uint32_t c = (uint32_t)__popcll(at);
+        const uint32_t c = (uint32_t)__popcll(__ballot(bj <= e1));   // block starts at or below e1
         sc += c;
         if (c < 64) break;
       }
-      continue;
+    } else {
+      sc = cand_slow_step(vs, S, meta, vkeys, nbr, gids, P0, base, w1, sc, lane, a, b, f);
     }
-    uint64_t o[4];
-    uint32_t slot[4];
-    bool need[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      o[i] = base + (uint64_t)(i * 64) + lane;
-      need[i] = o[i] < w1;
-      slot[i] = sc;
-    }
-    for (uint32_t s0 = sc;; s0 += 64) {
-      const uint64_t bj = (uint64_t)s0 + 1 + lane <= S ? vs[s0 + 1 + lane] : ~0ull;
-      const uint64_t top = __shfl(bj, 63, 64);
-      bool pend = false;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        int pos = 0;   // block starts vs[s0 + 1 ..] at or below o[i]: 0..63 by halving, 64 past the window
-#pragma unroll
-        for (int st = 32; st > 0; st >>= 1) {
-          const uint64_t v = __shfl(bj, pos + st - 1, 64);
-          pos += v <= o[i] ? st : 0;
-        }
-        if (top <= o[i]) pos = 64;
-        if (need[i] && pos < 64) {
-          slot[i] = s0 + pos;
-          need[i] = false;
-        }
-        pend |= need[i];
-      }
-      if (!__any(pend)) break;
-    }
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      if (o[i] >= w1) continue;
-      const uint32_t sl = slot[i];
-      const CandMeta m = meta[sl];
-      const uint64_t t = o[i] - vs[sl];
-      int64_t av, bv;
-      uint8_t fv;
-      if (t < m.d) {
-        av = vkeys[m.u];
-        bv = nbr[m.nbr_off + t];
-        fv = 0;
-      } else if (m.rows) {
-        // row r of the block: the largest r with r k - r (r - 1) / 2 <= q (closed form, then at most a
-        // step or two of correction for the double rounding; the loops are bounded regardless)
-        const uint64_t q = t - m.d, k = m.k, rows = m.rows;
-        const double k2 = 2.0 * (double)k + 1.0;
-        uint64_t r = (uint64_t)fmax(0.0, (k2 - sqrt(fmax(0.0, k2 * k2 - 8.0 * (double)q))) * 0.5);
-        if (r >= rows) r = rows - 1;
-        for (int g = 0; g < 64 && r > 0 && tri_rows_before(r, k) > q; ++g) --r;
-        for (int g = 0; g < 64 && r + 1 < rows && tri_rows_before(r + 1, k) <= q; ++g) ++r;
-        const uint64_t col = min(q - tri_rows_before(r, k), k - 1 - r);
-        av = gids[m.gbase + r];
-        bv = gids[m.gbase + r + col];
-        fv = 1;
-      } else {   // not reached: a block without pair rows holds only its edge records
-        av = bv = 0;
-        fv = 1;
-      }
-      a[o[i] - P0] = av;
-      b[o[i] - P0] = bv;
-      f[o[i] - P0] = fv;
-    }
-    sc = __shfl(slot[3], 63, 64);   // the slot of this step's last position (the next step starts there)
+  }
+}
+
+// the steps k_cand_emit<1> left (their bases in steps[0 .. *steps_n)), one wave per step at a time
+__global__ __launch_bounds__(256) void k_cand_emit_rest(const uint64_t* __restrict__ vs, uint32_t S,
+                                                        const CandMeta* __restrict__ meta,
+                                                        const int64_t* __restrict__ vkeys, const int64_t* __restrict__ nbr,
+                                                        const int64_t* __restrict__ gids, uint64_t P0, uint64_t P1,
+                                                        int64_t* __restrict__ a, int64_t* __restrict__ b,
+                                                        uint8_t* __restrict__ f, const uint64_t* __restrict__ steps,
+                                                        const uint32_t* __restrict__ steps_n) {
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t n = *steps_n;
+  const uint32_t nw = gridDim.x * 4u;
+  for (uint32_t i = (blockIdx.x * 256u + threadIdx.x) >> 6; i < n; i += nw) {   // wave-uniform
+    const uint64_t base = steps[i];
+    const uint32_t sc = cand_find_slot(vs, S, base, lane);
+    cand_slow_step(vs, S, meta, vkeys, nbr, gids, P0, base, min(P1, base + 256), sc, lane, a, b, f);
   }
 }
 
@@ -799,16 +847,17 @@ __device__ void j_put(JMap& m, int32_t x) {
 }
 // ---- the simulation in parallel over bin groups ---------------------------------------------------
 // Until the table reaches capacity 64, a bin of 9 resizes the whole table (treeifyBin below
-// MIN_TREEIFY_CAPACITY): the prefix of the insertions up to that point is simulated by one thread per set
-// (at most a few dozen keys: the size threshold alone takes the table to 64 by the 25th).  From capacity
-// 64 on every bin evolves alone: a resize happens right after the insertion whose index equals the
-// threshold 3C/4 (it depends on the count only), treeifyBin converts its own bin, and a resize splits
-// old bin j into new bins j and j + C only.  So the keys of one group g = hash & 63 -- bins g, g + 64,
-// g + 128, ... at every capacity >= 64 -- are simulated by their own thread: its keys in arrival order
-// (k_hs_jdk_order), the resizes applied at the global insertion indices where they occur, its bins'
-// chains walked in bin order at the end.  At capacity 64 every bin is still a plain list in arrival
-// order (no tree can form below 64), so a group starts from its prefix keys as bin g's list.  The critical
-// path of a hub's set of ~10^5 ids drops from k inserts to ~k / 64.
+// MIN_TREEIFY_CAPACITY); from 64 on every bin evolves alone: a resize happens right after the insertion
+// whose index equals the threshold 3C/4 (it depends on the count only), treeifyBin converts its own bin,
+// and a resize splits old bin j into new bins j and j + C only.  So one thread per set simulates the
+// insertions until the table reaches HS_JG bins (at most 3 HS_JG / 4 + 1 keys: the size threshold alone
+// takes it there), exactly as the JDK (trees may already form from capacity 64), and from there the keys
+// of one group g = hash & (HS_JG - 1) -- bins g, g + HS_JG, g + 2 HS_JG, ... at every capacity >= HS_JG --
+// are simulated by their own thread, continuing from the table the prefix left: its keys in arrival
+// order (k_hs_jdk_order), the resizes applied at the global insertion indices where they occur, its
+// bins' chains walked in bin order at the end.  The critical path of a hub's set of ~10^5 ids drops
+// from k inserts to ~k / HS_JG.
+constexpr uint32_t HS_JG = 256;
 __global__ __launch_bounds__(64) void k_hs_jdk_prefix(const uint32_t* __restrict__ list, const uint32_t* __restrict__ nc,
                                                       const uint64_t* __restrict__ doff, const int64_t* __restrict__ arr,
                                                       const uint64_t* __restrict__ tbase, JNode* __restrict__ nodes,
@@ -820,37 +869,38 @@ __global__ __launch_bounds__(64) void k_hs_jdk_prefix(const uint32_t* __restrict
     const uint64_t d0 = doff[u], k = doff[u + 1] - d0;
     JMap m{nodes + d0, arr + d0, tabs + tbase[s], 0, 0, 0, 0};
     uint32_t j = 0;
-    for (; j < k && m.cap < 64; ++j) {
+    for (; j < k && m.cap < HS_JG; ++j) {
       const int64_t x = m.key[j];
       const uint32_t h0 = (uint32_t)((uint64_t)x ^ ((uint64_t)x >> 32));
       m.n[j].hash = h0 ^ (h0 >> 16);
       j_put(m, (int32_t)j);
     }
     if (m.flags) atomicOr(flags, m.flags);
-    if (m.cap >= 64) {   // the groups take it from here (the keys before j are plain lists at capacity 64)
+    if (m.cap >= HS_JG) {   // the groups take it from here (the table of the keys before j stays for them)
       p0[s] = j;
       continue;
     }
-    p0[s] = ~0u;   // the whole set stayed below capacity 64: done here
+    p0[s] = ~0u;   // the whole set stayed below capacity HS_JG: done here
     uint64_t o = d0;
     for (uint32_t b = 0; b < m.cap; ++b)
       for (int32_t e = m.tab[b]; e >= 0; e = m.n[e].next) ids[o++] = m.key[e];
   }
 }
 
-// one wave per set: the set's keys stably partitioned by group (hash & 63), as arrival indices, into
-// ord[d0 ..] with the group starts in gofs[65 s ..] (two passes: counts, then positions)
+// one wave per set: the set's keys stably partitioned by group (hash & (HS_JG - 1)), as arrival indices,
+// into ord[d0 ..] with the group starts in gofs[(HS_JG + 1) s ..] (two passes: counts, then positions)
 __global__ __launch_bounds__(64) void k_hs_jdk_order(const uint32_t* __restrict__ list, const uint32_t* __restrict__ nc,
                                                      const uint64_t* __restrict__ doff, const int64_t* __restrict__ arr,
                                                      const uint32_t* __restrict__ p0, uint32_t* __restrict__ ord,
                                                      uint32_t* __restrict__ gofs) {
-  __shared__ uint32_t s_run[64];
+  __shared__ uint32_t s_run[HS_JG];
+  constexpr uint32_t PER = HS_JG / 64;   // groups per lane in the scans
   const uint32_t count = *nc, lane = threadIdx.x;
   for (uint32_t s = blockIdx.x; s < count; s += gridDim.x) {
     if (p0[s] == ~0u) continue;   // (uniform over the block)
     const uint32_t u = list[s];
     const uint64_t d0 = doff[u], k = doff[u + 1] - d0;
-    s_run[lane] = 0;
+    for (uint32_t i = 0; i < PER; ++i) s_run[lane * PER + i] = 0;
     __syncthreads();
     for (int pass = 0; pass < 2; ++pass) {
       for (uint64_t j0 = 0; j0 < k; j0 += 64) {
@@ -861,9 +911,10 @@ __global__ __launch_bounds__(64) void k_hs_jdk_order(const uint32_t* __restrict_
         if (on) {
           const int64_t x = arr[d0 + j];
           const uint32_t h0 = (uint32_t)((uint64_t)x ^ ((uint64_t)x >> 32));
-          g = (h0 ^ (h0 >> 16)) & 63u;
+          g = (h0 ^ (h0 >> 16)) & (HS_JG - 1);
         }
-        const uint64_t peers = match_digit<6>(g, act);
+        const uint64_t peers = match_digit<8>(g, act);
+        static_assert(HS_JG == 256, "match_digit width");
         const uint32_t rank = mbcnt(peers);
         const bool leader = on && rank == 0;
         if (pass == 1 && on) ord[d0 + s_run[g] + rank] = (uint32_t)j;
@@ -871,12 +922,17 @@ __global__ __launch_bounds__(64) void k_hs_jdk_order(const uint32_t* __restrict_
         if (leader) s_run[g] += (uint32_t)__popcll(peers);
         __syncthreads();
       }
-      if (pass == 0) {   // counts -> group starts
-        const uint32_t c = s_run[lane], inc = wave_inclusive_sum(c);
+      if (pass == 0) {   // counts -> group starts (lane l holds groups [PER l, PER l + PER))
+        uint32_t c[PER], t = 0;
+        for (uint32_t i = 0; i < PER; ++i) t += (c[i] = s_run[lane * PER + i]);
+        uint32_t at = wave_inclusive_sum(t) - t;
         __syncthreads();
-        s_run[lane] = inc - c;
-        gofs[65ull * s + lane] = inc - c;
-        if (lane == 63) gofs[65ull * s + 64] = inc;
+        for (uint32_t i = 0; i < PER; ++i) {
+          s_run[lane * PER + i] = at;
+          gofs[(uint64_t)(HS_JG + 1) * s + lane * PER + i] = at;
+          at += c[i];
+        }
+        if (lane == 63) gofs[(uint64_t)(HS_JG + 1) * s + HS_JG] = at;
         __syncthreads();
       }
     }
@@ -884,7 +940,7 @@ __global__ __launch_bounds__(64) void k_hs_jdk_order(const uint32_t* __restrict_
   }
 }
 
-// insertion at capacity >= 64 (no size bookkeeping: the resizes come from the caller's schedule)
+// insertion at capacity >= HS_JG (no size bookkeeping: the resizes come from the caller's schedule)
 __device__ void j_put_group(JMap& m, int32_t x) {
   JNode* n = m.n;
   const uint32_t h = n[x].hash, i = h & (m.cap - 1);
@@ -926,13 +982,13 @@ __device__ void j_put_group(JMap& m, int32_t x) {
   }
 }
 
-// the group's bins of a resize from m.cap to 2 m.cap (the split of j_resize, bins j = g mod 64 only)
+// the group's bins of a resize from m.cap to 2 m.cap (the split of j_resize, bins j = g mod HS_JG only)
 __device__ void j_resize_group(JMap& m, uint32_t g) {
   const uint32_t ocap = m.cap, ncap = ocap * 2;
   JNode* n = m.n;
-  for (uint32_t i = ocap + g; i < ncap; i += 64) m.tab[i] = -1;
+  for (uint32_t i = ocap + g; i < ncap; i += HS_JG) m.tab[i] = -1;
   m.cap = ncap;
-  for (uint32_t j = g; j < ocap; j += 64) {
+  for (uint32_t j = g; j < ocap; j += HS_JG) {
     const int32_t e = m.tab[j];
     if (e < 0) continue;
     m.tab[j] = -1;
@@ -973,32 +1029,20 @@ __global__ __launch_bounds__(64) void k_hs_jdk_group(const uint32_t* __restrict_
                                                      const uint32_t* __restrict__ ord, const uint32_t* __restrict__ gofs,
                                                      JNode* __restrict__ nodes, int32_t* __restrict__ tabs,
                                                      uint64_t* __restrict__ bcnt, uint32_t* __restrict__ flags) {
-  const uint64_t total = (uint64_t)*nc * 64;
+  const uint64_t total = (uint64_t)*nc * HS_JG;
   for (uint64_t t = (uint64_t)blockIdx.x * 64 + threadIdx.x; t < total; t += (uint64_t)gridDim.x * 64) {
-    const uint32_t s = (uint32_t)(t >> 6), g = (uint32_t)(t & 63);
+    const uint32_t s = (uint32_t)(t / HS_JG), g = (uint32_t)(t % HS_JG);
     const uint32_t P0 = p0[s];
     if (P0 == ~0u) continue;
     const uint32_t u = list[s];
     const uint64_t d0 = doff[u], k = doff[u + 1] - d0;
-    JMap m{nodes + d0, arr + d0, tabs + tbase[s], 64, 0, 0, 0};
+    // bin g of the prefix's table at capacity HS_JG (plain or tree, as the JDK left it)
+    JMap m{nodes + d0, arr + d0, tabs + tbase[s], HS_JG, 0, 0, 0};
     JNode* n = m.n;
     const uint32_t* o = ord + d0;
-    const uint32_t a = gofs[65ull * s + g], b = gofs[65ull * s + g + 1];
-    // bin g at capacity 64: the group's prefix keys, a plain list in arrival order
-    int32_t tail = -1;
-    m.tab[g] = -1;
+    const uint32_t a = gofs[(uint64_t)(HS_JG + 1) * s + g], b = gofs[(uint64_t)(HS_JG + 1) * s + g + 1];
     uint32_t q = a;
-    for (; q < b && o[q] < P0; ++q) {
-      const int32_t j = (int32_t)o[q];
-      const int64_t x = m.key[j];
-      const uint32_t h0 = (uint32_t)((uint64_t)x ^ ((uint64_t)x >> 32));
-      n[j].hash = h0 ^ (h0 >> 16);
-      n[j].next = n[j].prev = n[j].parent = n[j].left = n[j].right = -1;
-      n[j].red = n[j].tree = 0;
-      if (tail < 0) m.tab[g] = j;
-      else n[tail].next = j;
-      tail = j;
-    }
+    while (q < b && o[q] < P0) ++q;   // (the prefix inserted them)
     for (; q < b; ++q) {
       const uint32_t j = o[q];
       while ((uint64_t)m.cap * 3 / 4 < j) j_resize_group(m, g);   // the resizes after inserts 3C/4 < j
@@ -1010,7 +1054,7 @@ __global__ __launch_bounds__(64) void k_hs_jdk_group(const uint32_t* __restrict_
     while ((uint64_t)m.cap * 3 / 4 < k) j_resize_group(m, g);   // the resizes after the set's last inserts
     if (m.flags) atomicOr(flags, m.flags);
     uint64_t* bc = bcnt + tbase[s];
-    for (uint32_t bin = g; bin < m.cap; bin += 64) {
+    for (uint32_t bin = g; bin < m.cap; bin += HS_JG) {
       uint64_t c = 0;
       for (int32_t e = m.tab[bin]; e >= 0; e = n[e].next) ++c;
       bc[bin] = c;
@@ -1024,9 +1068,9 @@ __global__ __launch_bounds__(64) void k_hs_jdk_write(const uint32_t* __restrict_
                                                      const uint64_t* __restrict__ tbase, const uint32_t* __restrict__ p0,
                                                      const JNode* __restrict__ nodes, const int32_t* __restrict__ tabs,
                                                      const uint64_t* __restrict__ bpos, int64_t* __restrict__ ids) {
-  const uint64_t total = (uint64_t)*nc * 64;
+  const uint64_t total = (uint64_t)*nc * HS_JG;
   for (uint64_t t = (uint64_t)blockIdx.x * 64 + threadIdx.x; t < total; t += (uint64_t)gridDim.x * 64) {
-    const uint32_t s = (uint32_t)(t >> 6), g = (uint32_t)(t & 63);
+    const uint32_t s = (uint32_t)(t / HS_JG), g = (uint32_t)(t % HS_JG);
     if (p0[s] == ~0u) continue;
     const uint32_t u = list[s];
     const uint64_t d0 = doff[u], k = doff[u + 1] - d0;
@@ -1035,7 +1079,7 @@ __global__ __launch_bounds__(64) void k_hs_jdk_write(const uint32_t* __restrict_
     const JNode* n = nodes + d0;
     const int32_t* tab = tabs + tbase[s];
     const uint64_t* bp = bpos + tbase[s];
-    for (uint64_t bin = g; bin < cap; bin += 64) {
+    for (uint64_t bin = g; bin < cap; bin += HS_JG) {
       uint64_t at = d0 + (bp[bin] - bp[0]);
       for (int32_t e = tab[bin]; e >= 0; e = n[e].next) ids[at++] = arr[d0 + e];
     }
@@ -1155,7 +1199,7 @@ static gs_status hashset_exact(gs_ctx* c, uint64_t R, uint64_t U, uint64_t M, ui
   } else {
     GS_TRY(ensure(c, c->hs[HS_P0], nc * 4 + 4));
     GS_TRY(ensure(c, c->hs[HS_GORD], M * 4 + 4));
-    GS_TRY(ensure(c, c->hs[HS_GOFS], nc * 65 * 4 + 4));
+    GS_TRY(ensure(c, c->hs[HS_GOFS], nc * (HS_JG + 1) * 4 + 4));
     GS_TRY(ensure(c, c->hs[HS_BCNT], (T + 1) * 8));
     GS_TRY(ensure(c, c->hs[HS_BPOS], (T + 1) * 8));
     const uint32_t* cl = c->hs[HS_CLIST].as<uint32_t>();
@@ -1167,7 +1211,7 @@ static gs_status hashset_exact(gs_ctx* c, uint64_t R, uint64_t U, uint64_t M, ui
                        c->hs[HS_DOFF].as<uint64_t>(), c->hs[HS_ARR].as<int64_t>(), (const uint32_t*)p0,
                        c->hs[HS_GORD].as<uint32_t>(), c->hs[HS_GOFS].as<uint32_t>());
     GS_HIP(hipMemsetAsync(c->hs[HS_BCNT].p, 0, (T + 1) * 8, c->stream));
-    const unsigned ggrid = (unsigned)std::min<uint64_t>(nc, 16384);   // 64 threads (groups) per set
+    const unsigned ggrid = (unsigned)std::min<uint64_t>(nc * (HS_JG / 64), 65536);   // HS_JG threads (groups) per set
     hipLaunchKernelGGL(k_hs_jdk_group, dim3(ggrid), dim3(64), 0, c->stream, cl, d_hs, c->hs[HS_DOFF].as<uint64_t>(),
                        c->hs[HS_ARR].as<int64_t>(), c->hs[HS_TBASE].as<uint64_t>(), (const uint32_t*)p0,
                        (const uint32_t*)c->hs[HS_GORD].as<uint32_t>(), (const uint32_t*)c->hs[HS_GOFS].as<uint32_t>(),
@@ -1206,8 +1250,17 @@ gs_status hashset_order(gs_ctx* c, const int64_t* src, const int64_t* dst, uint6
   GS_TRY(ensure(c, c->hs[HS_ORD], R * 4));
   GS_HIP(hipMemcpyAsync(c->hs[HS_ORD].p, s.vals, R * 4, hipMemcpyDeviceToDevice, c->stream));
   const uint32_t B = U > 1 ? 64 - __builtin_clzll(U - 1) : 1;   // bits of a dense vertex rank
+  // every id differs from the first in its low s.bits bits (the sort's key mask): a dense rank table when
+  // that span is small (R-MAT s23 C5 window: 32 MB; k_hs_prep spent 23 ms in binary searches without it)
+  const uint32_t* rank = nullptr;
+  if (s.bits <= HS_RANK_BITS) {
+    GS_TRY(ensure(c, c->hs_rank, (1ull << std::max(s.bits, 1)) * 4));
+    hipLaunchKernelGGL(k_hs_rank, dim3(g256(U)), dim3(256), 0, c->stream, c->hs[HS_VKEYS].as<int64_t>(), (uint32_t)U,
+                       c->hs_rank.as<uint32_t>());
+    rank = c->hs_rank.as<uint32_t>();
+  }
   hipLaunchKernelGGL(k_hs_prep, dim3(g256(R)), dim3(256), 0, c->stream, c->hs[HS_ORD].as<uint32_t>(), (uint32_t)R, src,
-                     dst, c->hs[HS_OFF].as<uint64_t>(), c->hs[HS_VKEYS].as<int64_t>(), (uint32_t)U, B,
+                     dst, c->hs[HS_OFF].as<uint64_t>(), c->hs[HS_VKEYS].as<int64_t>(), (uint32_t)U, B, rank,
                      c->hs[HS_NBR].as<int64_t>(),
                      c->hs[HS_USEG].as<uint32_t>(), c->hs[HS_COMP].as<uint64_t>(), c->hs[HS_PIDX].as<uint32_t>());
   GS_HIP(hipGetLastError());
@@ -1339,16 +1392,22 @@ static gs_status cand_emit(gs_ctx* c, uint32_t S, uint64_t P0, uint64_t P1, int6
   const uint64_t per_wave = ((n + waves - 1) / waves + 255) / 256 * 256;
   const int f4 = ((uintptr_t)f & 3) == 0 ? 1 : 0;
   static const int split_env = getenv("GS_CAND_SPLIT") ? atoi(getenv("GS_CAND_SPLIT")) : 1;   // A/B
-  auto launch = [&](auto kern) {
-    hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(256), 0, c->stream, c->hs[HS_VS].as<uint64_t>(), S,
-                       c->hs[HS_META].as<CandMeta>(), c->hs[HS_VKEYS].as<int64_t>(), c->hs[HS_NBR].as<int64_t>(),
-                       c->hs[HS_GIDS].as<int64_t>(), P0, P1, per_wave, a, b, f, f4);
-  };
-  if (split_env) {   // the pair-row steps in a lean kernel, then the rest
-    launch(k_cand_emit<1>);
-    launch(k_cand_emit<2>);
+  const uint64_t* vs = c->hs[HS_VS].as<uint64_t>();
+  const CandMeta* meta = c->hs[HS_META].as<CandMeta>();
+  const int64_t *vkeys = c->hs[HS_VKEYS].as<int64_t>(), *nbr = c->hs[HS_NBR].as<int64_t>(),
+                *gids = c->hs[HS_GIDS].as<int64_t>();
+  if (split_env) {   // the pair-row steps in a lean kernel, then the steps it listed
+    GS_TRY(ensure(c, c->cand_steps, (n / 256 + waves + 16) * 8 + 64));
+    uint32_t* steps_n = reinterpret_cast<uint32_t*>(c->cand_steps.p);
+    uint64_t* steps = c->cand_steps.as<uint64_t>() + 8;
+    GS_HIP(hipMemsetAsync(steps_n, 0, 4, c->stream));
+    hipLaunchKernelGGL(k_cand_emit<1>, dim3((unsigned)blocks), dim3(256), 0, c->stream, vs, S, meta, vkeys, nbr, gids,
+                       P0, P1, per_wave, a, b, f, f4, steps, steps_n);
+    hipLaunchKernelGGL(k_cand_emit_rest, dim3(1024), dim3(256), 0, c->stream, vs, S, meta, vkeys, nbr, gids, P0, P1, a, b,
+                       f, (const uint64_t*)steps, (const uint32_t*)steps_n);
   } else {
-    launch(k_cand_emit<0>);
+    hipLaunchKernelGGL(k_cand_emit<0>, dim3((unsigned)blocks), dim3(256), 0, c->stream, vs, S, meta, vkeys, nbr, gids,
+                       P0, P1, per_wave, a, b, f, f4, nullptr, nullptr);
   }
   return hip_check(c, hipGetLastError(), "k_cand_emit");
 }

@@ -64,7 +64,7 @@ struct gs_ctx {
   // hs[] until the next entry point call on the ctx (call_seq) ends the session
   uint64_t call_seq = 0, cand_seq = ~0ull, cand_total = 0, cand_cursor = 0;
   uint32_t cand_U = 0, cand_S = 0, cand_nparts = 1;
-  gs::DevBuf cand_bounds;
+  gs::DevBuf cand_bounds, cand_steps;   // (cand_steps: the steps k_cand_emit<1> leaves to k_cand_emit_rest)
   // input staging (host batches)
   gs::DevBuf in_src, in_dst, in_val;
   // sort ping-pong
@@ -100,6 +100,7 @@ struct gs_ctx {
   gs::DevBuf tri_rl[4];          // split-window triangles over wide ids: compact columns, local / all ids
   // HashSet-order pipeline (gs_hashset.hip)
   gs::DevBuf hs[40];
+  gs::DevBuf hs_rank;            // dense vertex-rank table of the window (k_hs_rank)
   // bucket path (gs_bucket.hip): plan tables, work items, LDS slabs of multi-item buckets
   gs::DevBuf bk_meta, bk_items, bk_slabs;
   // direct partition: per-tile bucket counts (u16), chunk sums, per-tile write offsets

@@ -419,6 +419,13 @@ def _jdk_case(oracle, case):
         s, d = np.zeros(200, np.int64), np.arange(1, 201, dtype=np.int64) << 24
     elif case == "tree20_split":      # tree bins split and re-treeified by later resizes
         s, d = np.zeros(3000, np.int64), np.arange(1, 3001, dtype=np.int64) << 20
+    elif case == "hub_groups":        # large sets mixing tree bins and plain ones, well past capacity 256:
+        ids = np.concatenate([np.arange(1, 4_001, dtype=np.int64) << 24,                   # bins of many
+                              rng.integers(1, 1 << 40, 6_000).astype(np.int64)])          # spread
+        ids = np.unique(ids)
+        rng.shuffle(ids)
+        s = np.concatenate([np.zeros(len(ids), np.int64), np.full(len(ids) // 2, 7, np.int64)])
+        d = np.concatenate([ids, ids[: len(ids) // 2]])
     elif case == "many_vertices":     # hundreds of complex sets in one window, plus plain ones
         V = 400
         s = np.repeat(-np.arange(1, V + 1, dtype=np.int64), 20)
@@ -431,12 +438,13 @@ def _jdk_case(oracle, case):
     return np.ascontiguousarray(s[p]), np.ascontiguousarray(d[p])
 
 
-@pytest.mark.parametrize("case", ["resize16", "tree24", "tree20_split", "many_vertices", "rmat_shifted"])
+@pytest.mark.parametrize("case", ["resize16", "tree24", "tree20_split", "hub_groups", "many_vertices", "rmat_shifted"])
 def test_candidates_exact_jdk_order(engine, oracle, case):
     """Neighbour sets whose java.util.HashMap leaves the plain-bin model -- a bin of 9 that makes
-    treeifyBin resize below capacity 64, red-black tree bins, tree bins split by later resizes, many such
-    sets in one window -- are simulated exactly on the GPU (k_hs_detect finds them, k_hs_jdk replays
-    putVal): the records equal the oracle's exact JDK restatement, and the reported flags agree."""
+    treeifyBin resize below capacity 64, red-black tree bins, tree bins split by later resizes, hub sets of
+    10^4 ids simulated by 256 bin groups past capacity 256, many such sets in one window -- are simulated
+    exactly on the GPU (k_hs_detect finds them, k_hs_jdk_prefix / _group replay putVal): the records equal
+    the oracle's exact JDK restatement, and the reported flags agree."""
     s, d = _jdk_case(oracle, case)
     ra, rb, rf, flags = oracle.window_candidates(s, d)
     assert flags
