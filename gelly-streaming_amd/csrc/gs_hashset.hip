@@ -364,15 +364,16 @@ __device__ __forceinline__ uint32_t cand_find_slot(const uint64_t* __restrict__ 
 // MODE 0: every step, by the fast path where it applies and cand_slow_step otherwise.  MODE 1: the fast
 // steps only (the pair rows of one slot: ~99% of a window's steps), compiled without the general path
 // so the kernel holds fewer registers and more of its stores are in flight; every other step's base is
-// appended to `steps` (count in steps_n) for k_cand_emit_rest.
+// appended to `steps` (count in steps_n) for k_cand_emit_rest.  Kernels: k_cand_emit_all (MODE 0),
+// k_cand_emit_fast (MODE 1).
 template <int MODE>
-__global__ __launch_bounds__(256) void k_cand_emit(const uint64_t* __restrict__ vs, uint32_t S,
-                                                   const CandMeta* __restrict__ meta, const int64_t* __restrict__ vkeys,
-                                                   const int64_t* __restrict__ nbr, const int64_t* __restrict__ gids,
-                                                   uint64_t P0, uint64_t P1, uint64_t per_wave,
-                                                   int64_t* __restrict__ a, int64_t* __restrict__ b,
-                                                   uint8_t* __restrict__ f, int f4, uint64_t* __restrict__ steps,
-                                                   uint32_t* __restrict__ steps_n) {
+__device__ __forceinline__ void cand_emit_body(const uint64_t* __restrict__ vs, uint32_t S,
+                                               const CandMeta* __restrict__ meta, const int64_t* __restrict__ vkeys,
+                                               const int64_t* __restrict__ nbr, const int64_t* __restrict__ gids,
+                                               uint64_t P0, uint64_t P1, uint64_t per_wave,
+                                               int64_t* __restrict__ a, int64_t* __restrict__ b,
+                                               uint8_t* __restrict__ f, int f4, uint64_t* __restrict__ steps,
+                                               uint32_t* __restrict__ steps_n) {
   const uint32_t lane = threadIdx.x & 63;
   const uint64_t wave = ((uint64_t)blockIdx.x * 256u + threadIdx.x) >> 6;
   const uint64_t w0 = P0 + wave * per_wave;
@@ -449,7 +450,16 @@ __global__ __launch_bounds__(256) void k_cand_emit(const uint64_t* __restrict__ 
   }
 }
 
-// the steps k_cand_emit<1> left (their bases in steps[0 .. *steps_n)), one wave per step at a time
+#define GS_CAND_EMIT_ARGS                                                                                        \
+  const uint64_t *__restrict__ vs, uint32_t S, const CandMeta *__restrict__ meta, const int64_t *__restrict__ vkeys, \
+      const int64_t *__restrict__ nbr, const int64_t *__restrict__ gids, uint64_t P0, uint64_t P1, uint64_t per_wave,  \
+      int64_t *__restrict__ a, int64_t *__restrict__ b, uint8_t *__restrict__ f, int f4, uint64_t *__restrict__ steps, \
+      uint32_t *__restrict__ steps_n
+#define GS_CAND_EMIT_PASS vs, S, meta, vkeys, nbr, gids, P0, P1, per_wave, a, b, f, f4, steps, steps_n
+__global__ __launch_bounds__(256) void k_cand_emit_all(GS_CAND_EMIT_ARGS) { cand_emit_body<0>(GS_CAND_EMIT_PASS); }
+__global__ __launch_bounds__(256) void k_cand_emit_fast(GS_CAND_EMIT_ARGS) { cand_emit_body<1>(GS_CAND_EMIT_PASS); }
+
+// the steps k_cand_emit_fast left (their bases in steps[0 .. *steps_n)), one wave per step at a time
 __global__ __launch_bounds__(256) void k_cand_emit_rest(const uint64_t* __restrict__ vs, uint32_t S,
                                                         const CandMeta* __restrict__ meta,
                                                         const int64_t* __restrict__ vkeys, const int64_t* __restrict__ nbr,
@@ -1401,12 +1411,14 @@ static gs_status cand_emit(gs_ctx* c, uint32_t S, uint64_t P0, uint64_t P1, int6
     uint32_t* steps_n = reinterpret_cast<uint32_t*>(c->cand_steps.p);
     uint64_t* steps = c->cand_steps.as<uint64_t>() + 8;
     GS_HIP(hipMemsetAsync(steps_n, 0, 4, c->stream));
-    hipLaunchKernelGGL(k_cand_emit<1>, dim3((unsigned)blocks), dim3(256), 0, c->stream, vs, S, meta, vkeys, nbr, gids,
+    // (k_cand_emit_fast holds 90 VGPRs: 5 waves per SIMD; held to 80 for 6 it spills and ran 0.99 -> 1.00 ms
+    // per 2^28 records, profiles/r05/c5/)
+    hipLaunchKernelGGL(k_cand_emit_fast, dim3((unsigned)blocks), dim3(256), 0, c->stream, vs, S, meta, vkeys, nbr, gids,
                        P0, P1, per_wave, a, b, f, f4, steps, steps_n);
     hipLaunchKernelGGL(k_cand_emit_rest, dim3(1024), dim3(256), 0, c->stream, vs, S, meta, vkeys, nbr, gids, P0, P1, a, b,
                        f, (const uint64_t*)steps, (const uint32_t*)steps_n);
   } else {
-    hipLaunchKernelGGL(k_cand_emit<0>, dim3((unsigned)blocks), dim3(256), 0, c->stream, vs, S, meta, vkeys, nbr, gids,
+    hipLaunchKernelGGL(k_cand_emit_all, dim3((unsigned)blocks), dim3(256), 0, c->stream, vs, S, meta, vkeys, nbr, gids,
                        P0, P1, per_wave, a, b, f, f4, nullptr, nullptr);
   }
   return hip_check(c, hipGetLastError(), "k_cand_emit");
