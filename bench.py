@@ -42,6 +42,10 @@ def parse():
     p.add_argument("--seed", type=lambda x: int(x, 0), default=0x5EED02)
     p.add_argument("--dtype", default="int64", choices=["int64", "float64"])
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-sample-log2", type=int, default=28,
+                   help="triangles: the CPU baseline counts windows up to 2^this many edges (larger windows: their "
+                        "first 2^this); 30 = the whole C4 (s26) window")
+    p.add_argument("--cpu-reps", type=int, default=5, help="triangles: CPU baseline windows timed (median)")
     p.add_argument("--timing", default="dominant", choices=["dominant", "stages"],
                    help="reduce / fold: stage events inside the timed region -- the dominant kernels only "
                         "(default) or every stage (each record costs the stream a few microseconds)")
@@ -317,7 +321,7 @@ def cpu_baseline_triangles(wins, threads, sample_log2=28, reps=5):
     1 warm-up on a 1/16 sample, then the median of `reps`."""
     orc = ge.load_oracle()
     S = min(1 << sample_log2, wins[0][0].numel())
-    host = [(w[0][:S].cpu().numpy(), w[1][:S].cpu().numpy()) for w in wins]
+    host = [(w[0][:S].cpu().numpy(), w[1][:S].cpu().numpy()) for w in wins[:max(1, min(reps, len(wins)))]]
     orc.triangles_fwd_mt(host[0][0][: S // 16], host[0][1][: S // 16], threads)
     ts = []
     for r in range(reps):
@@ -978,7 +982,7 @@ def main():
         if a.workload in ("reduce", "fold"):
             cpu = cpu_baseline(wins, a.workload, threads)
         elif a.workload == "triangles":
-            cpu = cpu_baseline_triangles(wins, threads)
+            cpu = cpu_baseline_triangles(wins, threads, a.cpu_sample_log2, a.cpu_reps)
         elif a.workload == "cc":
             cpu = cpu_baseline_cc(wins[0][0], wins[0][1])
     value = E * world * a.steps / elapsed
