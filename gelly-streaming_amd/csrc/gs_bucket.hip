@@ -303,10 +303,11 @@ gs_status bucket_direct_t(gs_ctx* c, const int64_t* src, const int64_t* dst, con
   if constexpr (SPEC_OK) {
     GS_TRY(ensure(c, sp.tot, BK_MAXB * 4, true));
     GS_TRY(ensure(c, c->sp_cur, SP_CUR_WORDS * 4));
-    // merges (slot 1) do not speculate: their rows are owner-grouped runs sorted by vertex, so a tile
-    // holds few buckets and a bucket's records land in one XCD slot's segment -- the proportional
-    // segments overflow (a miss, then 8 windows without speculation, every 9th merge)
-    spec = !(c->flags & GS_FLAG_NO_SPEC) && c->sp_slot == 0 && sp.ok && sp.skip == 0 && sp.base == base && sp.S == S &&
+    // merges (slot 1) speculate with ONE segment per bucket: their rows are sender runs sorted by
+    // vertex, so a tile holds few buckets and a bucket's records come from the tiles of one XCD slot
+    // -- proportional per-slot segments would overflow.  A tile reserves one run per bucket it
+    // touches (a handful), so the single cursor sees few atomics.
+    spec = !(c->flags & GS_FLAG_NO_SPEC) && sp.ok && sp.skip == 0 && sp.base == base && sp.S == S &&
            sp.dir == DIR && nb > 1 && sp_capacity(R, nb) + TRASH < (1ull << 32);   // u32 positions + trash
     if (sp.skip > 0) --sp.skip;
     if (spec) {
@@ -330,7 +331,10 @@ gs_status bucket_direct_t(gs_ctx* c, const int64_t* src, const int64_t* dst, con
         // each XCD slot's share of the records (k_sp_scatter_pack: slot x owns full tiles [x·per, (x+1)·per),
         // the partial last tile runs in slot 0)
         SpSlots slots{};
-        {
+        const uint32_t xmask = c->sp_slot == 0 ? 7u : 0u;
+        if (!xmask) {   // segment 0 = the whole region
+          for (uint32_t x = 1; x <= SP_NSEG; ++x) slots.pre[x] = (uint32_t)R;
+        } else {
           const uint64_t tr = (DIR == DIR_ALL ? 2 : 1) * SPTE, nfull = n / SPTE, per = (nfull + 7) / 8;
           uint64_t acc = 0;
           for (uint32_t x = 0; x < SP_NSEG; ++x) {
@@ -356,20 +360,20 @@ gs_status bucket_direct_t(gs_ctx* c, const int64_t* src, const int64_t* dst, con
           if (pack && nb <= 1024)
             hipLaunchKernelGGL((k_sp_scatter_pack<Load, DIR, 1024>), dim3(spk_grid<DIR>(n)), dim3(SPK_BLOCK), 0,
                                c->stream, ls, n, S, nb, cur, c->keysB.as<uint32_t>(), vpart, (uint32_t)cap, mm,
-                               (unsigned long long*)(sm + SM_BK_ESC));
+                               (unsigned long long*)(sm + SM_BK_ESC), xmask);
           else if (pack)
             hipLaunchKernelGGL((k_sp_scatter_pack<Load, DIR, BK_MAXB>), dim3(spk_grid<DIR>(n)), dim3(SPK_BLOCK), 0,
                                c->stream, ls, n, S, nb, cur, c->keysB.as<uint32_t>(), vpart, (uint32_t)cap, mm,
-                               (unsigned long long*)(sm + SM_BK_ESC));
+                               (unsigned long long*)(sm + SM_BK_ESC), xmask);
         }
         if constexpr (ITEMS == DP_ITEMS) {
           if (!pack) {
             if (nb <= 1024)
               hipLaunchKernelGGL((k_sp_scatter<Load, DIR, P::PAY, Raw, P::REL, 1024>), dim3(spu_grid<DIR>(n)),
-                                 dim3(SPU_BLOCK), 0, c->stream, ls, n, S, nb, cur, k16, vpart, (uint32_t)cap, rel_bad, mm);
+                                 dim3(SPU_BLOCK), 0, c->stream, ls, n, S, nb, cur, k16, vpart, (uint32_t)cap, rel_bad, mm, xmask);
             else
               hipLaunchKernelGGL((k_sp_scatter<Load, DIR, P::PAY, Raw, P::REL, BK_MAXB>), dim3(spu_grid<DIR>(n)),
-                                 dim3(SPU_BLOCK), 0, c->stream, ls, n, S, nb, cur, k16, vpart, (uint32_t)cap, rel_bad, mm);
+                                 dim3(SPU_BLOCK), 0, c->stream, ls, n, S, nb, cur, k16, vpart, (uint32_t)cap, rel_bad, mm, xmask);
           }
         }
         GS_HIP(hipGetLastError());

@@ -1220,7 +1220,8 @@ template <typename V, int DIR, int NB>
 __global__ __launch_bounds__(SPK_BLOCK) __attribute__((amdgpu_waves_per_eu(GS_SPK_WAVES, GS_SPK_WAVES)))
 void k_sp_scatter_pack(BaseSrc<V, DIR, PAY_VAL> es, uint64_t n, int S, uint32_t nbp,
                        uint32_t* __restrict__ cursor, uint32_t* __restrict__ rec, V* __restrict__ wide,
-                       uint32_t trash, unsigned long long* __restrict__ mm, unsigned long long* __restrict__ n_esc) {
+                       uint32_t trash, unsigned long long* __restrict__ mm, unsigned long long* __restrict__ n_esc,
+                       uint32_t xmask) {
   constexpr int ITEMS = SPK_ITEMS, BLOCK = SPK_BLOCK;
   constexpr int BPT = NB >= BLOCK ? NB / BLOCK : 1;   // buckets per thread
   static_assert(NB <= BK_MAXB && (NB % BLOCK == 0 || NB < BLOCK), "bucket table shape");
@@ -1255,7 +1256,12 @@ void k_sp_scatter_pack(BaseSrc<V, DIR, PAY_VAL> es, uint64_t n, int S, uint32_t 
     if (t >= nfull) return;
   }
   const uint32_t r0 = t * TILE;
-  const uint32_t xs = SP_NSEG == 1 ? 0u : blockIdx.x & 7u;   // this block's XCD slot: its segment
+  // this block's XCD slot: its segment (xmask 0: one segment per bucket, the merges' sorted runs)
+#ifdef GS_SP_X7
+  const uint32_t xs = SP_NSEG == 1 ? 0u : blockIdx.x & 7u;
+#else
+  const uint32_t xs = SP_NSEG == 1 ? 0u : blockIdx.x & xmask;
+#endif
   auto col_index = [&](uint32_t j) -> uint32_t { return DIR == DIR_ALL ? (r0 + j) >> 1 : r0 + j; };
   // this thread's buckets (BPT consecutive ones): their segment ends, issued before the columns
   uint32_t send[BPT];
@@ -1437,7 +1443,7 @@ template <typename V, int DIR, int PAY, typename VO, bool REL, int NB>
 __global__ __launch_bounds__(SPU_BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void k_sp_scatter(
     BaseSrc<V, DIR, PAY> es, uint64_t n, int S, uint32_t nbp, uint32_t* __restrict__ cursor,
     uint16_t* __restrict__ k16, VO* __restrict__ vout, uint32_t trash, uint32_t* __restrict__ rel_bad,
-    unsigned long long* __restrict__ mm) {
+    unsigned long long* __restrict__ mm, uint32_t xmask) {
   constexpr bool HAS_V = PAY != PAY_NONE;
   constexpr int BLOCK = SPU_BLOCK, ITEMS = SPU_ITEMS, BPT = NB / BLOCK;   // buckets per thread
   static_assert(NB % BLOCK == 0 && NB <= BK_MAXB, "bucket table shape");
@@ -1464,7 +1470,11 @@ __global__ __launch_bounds__(SPU_BLOCK) __attribute__((amdgpu_waves_per_eu(4))) 
     if (t >= nfull) return;
   }
   const uint32_t r0 = t * TILE;
+#ifdef GS_SP_X7
   const uint32_t xs = SP_NSEG == 1 ? 0u : blockIdx.x & 7u;
+#else
+  const uint32_t xs = SP_NSEG == 1 ? 0u : blockIdx.x & xmask;
+#endif
   uint32_t send[BPT];
 #pragma unroll
   for (int k = 0; k < BPT; ++k) send[k] = sp_hi(cursor, xs, min((uint32_t)tid * BPT + k, nbp - 1));

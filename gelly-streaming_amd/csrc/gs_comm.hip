@@ -257,7 +257,7 @@ static gs_status group_alltoall(gs_ctx* c, const void* send, void* recv, size_t 
 // owner-grouped rows: peer q's rows for this rank start after the rows it sends ranks 0 .. me-1; their
 // number must equal recv[q]
 static gs_status group_exchange(gs_ctx* c, const char* sendbuf, const uint64_t* send, char* recvbuf, const uint64_t* recv,
-                                size_t row) {
+                                size_t row, bool skip_self) {
   gs_comm_group* g = (gs_comm_group*)c->comm;
   gs_comm_group::Post p;
   p.kind = gs_comm_group::EXCHANGE;
@@ -269,6 +269,7 @@ static gs_status group_exchange(gs_ctx* c, const char* sendbuf, const uint64_t* 
   const int me = c->comm_rank;
   uint64_t ro = 0;
   for (int q = 0; q < g->P && st == GS_OK; ++q) {
+    if (skip_self && q == me) continue;
     const gs_comm_group::Post& pq = g->post[q];
     uint64_t off = 0;
     for (int k = 0; k < me; ++k) off += pq.scount[k];
@@ -315,14 +316,18 @@ static bool is_group(const gs_ctx* c) { return c->comm_kind == GS_COMM_KIND_GROU
 
 // ---- the primitives (gs_internal.hpp) -------------------------------------------------------------------
 gs_status exchange_rows(gs_ctx* c, const char* sendbuf, const uint64_t* send, char* recvbuf, const uint64_t* recv,
-                        size_t row) {
+                        size_t row, bool skip_self) {
   if (!c->comm) return set_error(c, GS_EINVAL, "no communicator (gs_comm_init)");
-  if (is_group(c)) return group_exchange(c, sendbuf, send, recvbuf, recv, row);
+  if (is_group(c)) return group_exchange(c, sendbuf, send, recvbuf, recv, row, skip_self);
   NcclApi& A = nccl();
   const int P = c->comm_size;
   GS_TRY(nccl_check(c, A.GroupStart(), "ncclGroupStart"));
   uint64_t so = 0, ro = 0;
   for (int p = 0; p < P; ++p) {
+    if (skip_self && p == c->comm_rank) {
+      so += send[p];
+      continue;
+    }
     if (send[p]) GS_TRY(nccl_check(c, A.Send(sendbuf + so * row, send[p] * row, NCCL_UINT8, p, c->comm, c->stream), "ncclSend"));
     if (recv[p]) GS_TRY(nccl_check(c, A.Recv(recvbuf + ro * row, recv[p] * row, NCCL_UINT8, p, c->comm, c->stream), "ncclRecv"));
     so += send[p];
@@ -350,7 +355,7 @@ gs_status comm_alltoall(gs_ctx* c, const void* send, void* recv, size_t count, i
 gs_status comm_agree(gs_ctx* c, gs_status local) {
   if (!c->comm) return local;
   const std::string msg = c->err;
-  GS_TRY(ensure(c, c->dist_x, 64 + (size_t)c->comm_size * 32));
+  GS_TRY(ensure(c, c->dist_x, 64 + (size_t)c->comm_size * 32, true));   // (word 0: gs_dist.hip's key-width flag)
   uint64_t* d = c->dist_x.as<uint64_t>() + 1;
   c->host_small[200] = local != GS_OK ? 1 : 0;
   GS_HIP(hipMemcpyAsync(d, c->host_small + 200, 8, hipMemcpyHostToDevice, c->stream));

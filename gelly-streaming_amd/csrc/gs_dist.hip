@@ -32,7 +32,10 @@ namespace gs {
 constexpr int OW_BLOCK = 256, OW_ITEMS = 8, OW_TILE = OW_BLOCK * OW_ITEMS, OW_MAXP = 64;
 
 // per tile: partials per owner -> cnt[owner * tiles + tile]; *wide |= 1 when a key lies outside
-// [0, 2^32) (the exchange then sends 8-byte keys)
+// [0, 2^32) (the exchange then sends 8-byte keys).  MAXP 8: each thread counts its rows per owner in
+// registers, one wave sum per owner, one LDS atomic per wave and owner (per-row LDS atomics on a few
+// addresses serialise: 29 us for a C2 window's partials at one owner); MAXP 64: per-row LDS atomics.
+template <int MAXP>
 __global__ __launch_bounds__(OW_BLOCK) void k_owner_count(const int64_t* __restrict__ keys, uint64_t U, uint32_t nparts,
                                                           uint32_t tiles, uint32_t* __restrict__ cnt,
                                                           unsigned long long* __restrict__ wide) {
@@ -42,13 +45,28 @@ __global__ __launch_bounds__(OW_BLOCK) void k_owner_count(const int64_t* __restr
   __syncthreads();
   const uint64_t base = (uint64_t)blockIdx.x * OW_TILE;
   bool w = false;
+  uint32_t mine[MAXP <= 8 ? MAXP : 1] = {};
 #pragma unroll
   for (int u = 0; u < OW_ITEMS; ++u) {
     const uint64_t i = base + (uint64_t)u * OW_BLOCK + tid;
     if (i < U) {
       const int64_t k = keys[i];
       w |= (uint64_t)k >> 32 != 0;
-      atomicAdd(&s_c[owner_of(k, nparts)], 1u);
+      const uint32_t o = owner_of(k, nparts);
+      if constexpr (MAXP <= 8) {
+#pragma unroll
+        for (int j = 0; j < MAXP; ++j) mine[j] += o == (uint32_t)j ? 1u : 0u;
+      } else {
+        atomicAdd(&s_c[o], 1u);
+      }
+    }
+  }
+  if constexpr (MAXP <= 8) {
+#pragma unroll
+    for (int j = 0; j < MAXP; ++j) {
+      if (j >= (int)nparts) break;
+      const uint32_t t = wave_inclusive_sum(mine[j]);
+      if ((tid & 63) == 63 && t) atomicAdd(&s_c[j], t);
     }
   }
   if (wide && __any(w) && (tid & 63) == 0) atomicOr(wide, 1ull);
@@ -94,12 +112,18 @@ __global__ __launch_bounds__(1024) void k_owner_scan(uint32_t* __restrict__ cnt,
 // tile lands in consecutive addresses (the round-2 version read and wrote each thread's 16 consecutive
 // rows straight from / to HBM: 64 lanes, 64 cache lines per instruction; 459 us for the 7.4 M partials of
 // a C2 window, now a fraction of that)
-template <typename V, int MAXP, bool TWO>
+//
+// PACK (the exchange of gs_window_*_dist): the rows go out as the exchange's packed rows instead --
+// key (1 word, 2 when k_owner_count found a key outside [0, 2^32) on this rank), value, [maximum] --
+// into `rows`; no separate pack pass over the partitioned partials
+template <typename V, int MAXP, bool TWO, bool PACK>
 __global__ __launch_bounds__(OW_BLOCK) void k_owner_scatter(const int64_t* __restrict__ keys, const V* __restrict__ vals,
                                                             const int64_t* __restrict__ vals2, uint64_t U,
                                                             uint32_t nparts, uint32_t tiles,
                                                             const uint32_t* __restrict__ off, int64_t* __restrict__ okeys,
-                                                            V* __restrict__ ovals, int64_t* __restrict__ ovals2) {
+                                                            V* __restrict__ ovals, int64_t* __restrict__ ovals2,
+                                                            uint32_t* __restrict__ rows,
+                                                            const unsigned long long* __restrict__ wide) {
   constexpr uint32_t PADN = OW_TILE + OW_TILE / OW_ITEMS;   // row i at i + i / 16: thread t's rows off bank 0
   __shared__ int64_t s_k[PADN];
   __shared__ V s_v[OW_TILE];
@@ -158,23 +182,44 @@ __global__ __launch_bounds__(OW_BLOCK) void k_owner_scatter(const int64_t* __res
     s_perm[s_lo[own[j]] + s_r[own[j]][tid]++] = (uint16_t)(i0 + j);
   }
   __syncthreads();
+  constexpr uint32_t VW = sizeof(V) / 4, MW = TWO ? 2 : 0;
+  uint32_t kw = 1;
+  if constexpr (PACK) kw = (*wide & 1ull) ? 2u : 1u;
 #pragma unroll
   for (int j = 0; j < OW_ITEMS; ++j) {   // coalesced stores: consecutive q of one owner -> consecutive addresses
     const uint32_t q = (uint32_t)j * OW_BLOCK + tid;
     if (q >= nt) continue;
     const uint32_t r = s_perm[q], o = s_own[r];
     const uint32_t pos = off[(uint64_t)o * tiles + blockIdx.x] + (q - s_lo[o]);
-    okeys[pos] = s_k[r + r / OW_ITEMS];
-    ovals[pos] = s_v[r];
-    if constexpr (TWO) ovals2[pos] = s_v2[r];
+    if constexpr (PACK) {
+      uint32_t* w = rows + (uint64_t)pos * (kw + VW + MW);
+      const uint64_t k = (uint64_t)s_k[r + r / OW_ITEMS];
+      w[0] = (uint32_t)k;
+      if (kw == 2) w[1] = (uint32_t)(k >> 32);
+      const uint64_t v = (uint64_t)s_v[r];
+      w[kw] = (uint32_t)v;
+      if constexpr (VW == 2) w[kw + 1] = (uint32_t)(v >> 32);
+      if constexpr (TWO) {
+        const uint64_t m = (uint64_t)s_v2[r];
+        w[kw + VW] = (uint32_t)m;
+        w[kw + VW + 1] = (uint32_t)(m >> 32);
+      }
+    } else {
+      okeys[pos] = s_k[r + r / OW_ITEMS];
+      ovals[pos] = s_v[r];
+      if constexpr (TWO) ovals2[pos] = s_v2[r];
+    }
   }
 }
 
 // The owner partition on the device: rows grouped by owner (ascending keys within an owner), the
-// per-owner totals in dist_cnt[0, nparts) (u64) and, with `wide`, the key-width flag.  No host wait.
+// per-owner totals in dist_cnt[0, nparts) (u64) and, with `wide`, the key-width flag.  With `rows` the
+// partition writes the exchange's packed rows (k_owner_scatter PACK; needs `wide`) instead of okeys /
+// ovals / ovals2.  No host wait.
 gs_status owner_partition_dev(gs_ctx* c, const int64_t* keys, const void* vals, size_t vb, const int64_t* vals2,
                               uint64_t U, uint32_t nparts, int64_t* okeys, void* ovals, int64_t* ovals2,
-                              unsigned long long* wide) {
+                              unsigned long long* wide, uint32_t* rows = nullptr) {
+  if (rows && !wide) return set_error(c, GS_EINVAL, "packed owner partition without the key-width flag");
   const uint32_t tiles = (uint32_t)std::max<uint64_t>(1, (U + OW_TILE - 1) / OW_TILE);
   // dist_cnt: [0, 1 KiB) per-call scalars (owner totals, exchange counts), then the tile counts
   GS_TRY(ensure(c, c->dist_cnt, 1024 + (size_t)tiles * nparts * 4));
@@ -184,14 +229,22 @@ gs_status owner_partition_dev(gs_ctx* c, const int64_t* keys, const void* vals, 
     GS_HIP(hipMemsetAsync(totals, 0, nparts * 8, c->stream));
     return GS_OK;
   }
-  hipLaunchKernelGGL(k_owner_count, dim3(tiles), dim3(OW_BLOCK), 0, c->stream, keys, U, nparts, tiles, cnt, wide);
+  if (nparts <= 8)
+    hipLaunchKernelGGL(k_owner_count<8>, dim3(tiles), dim3(OW_BLOCK), 0, c->stream, keys, U, nparts, tiles, cnt, wide);
+  else
+    hipLaunchKernelGGL(k_owner_count<OW_MAXP>, dim3(tiles), dim3(OW_BLOCK), 0, c->stream, keys, U, nparts, tiles, cnt, wide);
   hipLaunchKernelGGL(k_owner_scan, dim3(1), dim3(1024), 0, c->stream, cnt, tiles * nparts, tiles, nparts, totals);
   auto launch = [&](auto vtag, auto ptag, auto ttag) {
     using V = decltype(vtag);
     constexpr int MP = decltype(ptag)::value;
     constexpr bool TW = decltype(ttag)::value;
-    hipLaunchKernelGGL((k_owner_scatter<V, MP, TW>), dim3(tiles), dim3(OW_BLOCK), 0, c->stream, keys,
-                       (const V*)vals, vals2, U, nparts, tiles, cnt, okeys, (V*)ovals, ovals2);
+    if (rows)
+      hipLaunchKernelGGL((k_owner_scatter<V, MP, TW, true>), dim3(tiles), dim3(OW_BLOCK), 0, c->stream, keys,
+                         (const V*)vals, vals2, U, nparts, tiles, cnt, nullptr, nullptr, nullptr, rows,
+                         (const unsigned long long*)wide);
+    else
+      hipLaunchKernelGGL((k_owner_scatter<V, MP, TW, false>), dim3(tiles), dim3(OW_BLOCK), 0, c->stream, keys,
+                         (const V*)vals, vals2, U, nparts, tiles, cnt, okeys, (V*)ovals, ovals2, nullptr, nullptr);
   };
   using P8 = std::integral_constant<int, 8>;
   using P64 = std::integral_constant<int, OW_MAXP>;
@@ -218,46 +271,48 @@ gs_status owner_partition(gs_ctx* c, const int64_t* keys, const void* vals, size
   return GS_OK;
 }
 
-// Exchange rows: key (4 bytes when every rank's keys lie in [0, 2^32), else 8), value (vb), [maximum (8)],
-// packed into one row of u32 words so the whole exchange is one grouped send / recv per peer
-__global__ __launch_bounds__(256) void k_pack_rows(const int64_t* __restrict__ keys, const uint32_t* __restrict__ vals,
-                                                   const int64_t* __restrict__ vals2, uint64_t n, int kw, int vw, int mw,
-                                                   uint32_t* __restrict__ rows) {
-  const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-  if (i >= n) return;
-  const int rw = kw + vw + mw;
-  uint32_t* r = rows + i * rw;
-  const uint64_t k = (uint64_t)keys[i];
-  r[0] = (uint32_t)k;
-  if (kw == 2) r[1] = (uint32_t)(k >> 32);
-  for (int j = 0; j < vw; ++j) r[kw + j] = vals[i * vw + j];
-  if (mw) {
-    const uint64_t m = (uint64_t)vals2[i];
-    r[kw + vw] = (uint32_t)m;
-    r[kw + vw + 1] = (uint32_t)(m >> 32);
-  }
-}
+// Exchange rows: key (1 u32 word when the sender's keys lie in [0, 2^32), else 2), value (vb / 4 words),
+// [maximum (2 words)]: one row of u32 words, so the whole exchange is one grouped send / recv per peer.
+// The receiver unpacks them by sender: segment q = rows [row0[q], row0[q + 1]) of the merge's input, from
+// src[q] with sender q's key width (this rank's own segment straight from its send buffer: it does not
+// travel)
+struct RowSegs {
+  const uint32_t* src[OW_MAXP];
+  uint64_t row0[OW_MAXP + 1];
+  uint32_t kw[OW_MAXP];
+  uint32_t nseg;
+};
 
-__global__ __launch_bounds__(256) void k_unpack_rows(const uint32_t* __restrict__ rows, uint64_t n, int kw, int vw, int mw,
-                                                     int64_t* __restrict__ keys, uint32_t* __restrict__ vals,
-                                                     int64_t* __restrict__ vals2) {
+__global__ __launch_bounds__(256) void k_unpack_rows(RowSegs segs, uint64_t n, int vw, int mw, int64_t* __restrict__ keys,
+                                                     uint32_t* __restrict__ vals, int64_t* __restrict__ vals2) {
   const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
   if (i >= n) return;
-  const int rw = kw + vw + mw;
-  const uint32_t* r = rows + i * rw;
+  uint32_t lo = 0, hi = segs.nseg - 1;   // the last segment q with row0[q] <= i
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi + 1) >> 1;
+    if (segs.row0[mid] <= i) lo = mid;
+    else hi = mid - 1;
+  }
+  const uint32_t kw = segs.kw[lo];
+  const uint32_t* r = segs.src[lo] + (i - segs.row0[lo]) * (kw + vw + mw);
   keys[i] = kw == 2 ? (int64_t)(((uint64_t)r[1] << 32) | r[0]) : (int64_t)(uint64_t)r[0];
   for (int j = 0; j < vw; ++j) vals[i * vw + j] = r[kw + j];
   if (mw) vals2[i] = (int64_t)(((uint64_t)r[kw + vw + 1] << 32) | r[kw + vw]);
 }
 
-// send row per peer p: [rows for p, flags] (flags: 1 = wide keys on this rank, 2 = this rank failed)
-__global__ void k_send_rows(const unsigned long long* __restrict__ totals, const unsigned long long* __restrict__ wide,
+// send row per peer p: [rows for p, flags] (flags: 1 = wide keys on this rank, 2 = this rank failed);
+// then the key-width flag is cleared for the next window's k_owner_count (no memset per window; a flag
+// left set by a failed window only widens that next window's keys)
+__global__ void k_send_rows(const unsigned long long* __restrict__ totals, unsigned long long* __restrict__ wide,
                             uint32_t nparts, unsigned long long* __restrict__ send) {
   const uint32_t p = threadIdx.x;
+  const unsigned long long fl = *wide & 1ull;
   if (p < nparts) {
     send[2 * p] = totals[p];
-    send[2 * p + 1] = *wide & 1ull;
+    send[2 * p + 1] = fl;
   }
+  __syncthreads();
+  if (p == 0) *wide = 0;
 }
 
 }  // namespace gs
@@ -409,7 +464,7 @@ static gs_status dist_impl(gs_ctx* c, const gs_edge_batch* b, int32_t dir, int32
   }
   const uint64_t R = dir == GS_DIR_ALL ? 2 * b->n : b->n;
   const size_t vb = degmax ? 8 : (op == GS_OP_COUNT ? 8 : dtype_bytes(b->val_dtype));
-  GS_TRY(ensure(c, c->dist_x, 64 + (size_t)P * 32));
+  GS_TRY(ensure(c, c->dist_x, 64 + (size_t)P * 32, true));   // (zeroed when allocated: the key-width flag)
   auto* wide = c->dist_x.as<unsigned long long>();
   auto* sendc = wide + 8;
   auto* recvc = sendc + 2 * P;
@@ -430,13 +485,12 @@ static gs_status dist_impl(gs_ctx* c, const gs_edge_batch* b, int32_t dir, int32
     }
   }
   const gs_stage_times keep = c->times;
-  if (local == GS_OK) local = ensure(c, c->dist_k2, U * 8 + 8);
-  if (local == GS_OK) local = ensure(c, c->dist_v3, U * 8 + 8);
-  if (local == GS_OK && degmax) local = ensure(c, c->dist_v4, U * 8 + 8);
+  const int vw = (int)(vb / 4), mw = degmax ? 2 : 0;
+  // the packed rows this rank sends (room for 2-word keys; the partition picks the width on the device)
+  if (local == GS_OK) local = ensure(c, c->dist_k2, U * (size_t)(2 + vw + mw) * 4 + 16);
   if (local == GS_OK) {
-    GS_HIP(hipMemsetAsync(wide, 0, 8, c->stream));
     local = owner_partition_dev(c, c->dist_k.as<int64_t>(), c->dist_v.p, vb, degmax ? c->dist_v2.as<int64_t>() : nullptr, U,
-                                P, c->dist_k2.as<int64_t>(), c->dist_v3.p, degmax ? c->dist_v4.as<int64_t>() : nullptr, wide);
+                                P, nullptr, nullptr, nullptr, wide, c->dist_k2.as<uint32_t>());
   }
   if (local == GS_OK) {
     hipLaunchKernelGGL(k_send_rows, dim3(1), dim3(64), 0, c->stream, c->dist_cnt.as<unsigned long long>(), wide, P, sendc);
@@ -454,45 +508,59 @@ static gs_status dist_impl(gs_ctx* c, const gs_edge_batch* b, int32_t dir, int32
   GS_TRY(comm_alltoall(c, sendc, recvc, 2, NCCL_T_U64));
   GS_HIP(hipMemcpyAsync(c->host_small + 8, sendc, (size_t)P * 32, hipMemcpyDeviceToHost, c->stream));
   GS_TRY(host_wait(c));
-  std::vector<uint64_t> send(P), recv(P);
-  bool wide_any = false;
+  const uint32_t me = (uint32_t)c->comm_rank;
+  std::vector<uint64_t> send_b(P), recv_b(P);
+  RowSegs segs{};
+  segs.nseg = P;
   int failed = -1;
-  uint64_t nrecv = 0;
+  uint64_t nrecv = 0, so = 0, ro = 0;
+  const uint32_t kw_me = (c->host_small[9] & 1) ? 2u : 1u;   // (every send flag carries this rank's width)
   for (uint32_t p = 0; p < P; ++p) {
-    send[p] = c->host_small[8 + 2 * p];
-    recv[p] = c->host_small[8 + 2 * P + 2 * p];
     const uint64_t fl = c->host_small[8 + 2 * P + 2 * p + 1];
-    wide_any |= (fl & 1) != 0;
     if ((fl & 2) && failed < 0) failed = (int)p;
-    nrecv += recv[p];
   }
   if (local != GS_OK) return set_error(c, local, "%s", local_err.c_str());
   if (failed >= 0) return set_error(c, GS_ECOMM, "rank %d failed its local step of the window", failed);
-  // 3. one packed exchange of the rows
-  const int kw = wide_any ? 2 : 1, vw = (int)(vb / 4), mw = degmax ? 2 : 0, rw = kw + vw + mw;
-  GS_TRY(ensure(c, c->dist_k, U * (size_t)rw * 4 + 16));   // the local partials are consumed: packed rows out
-  GS_TRY(ensure(c, c->dist_x2, nrecv * (size_t)rw * 4 + 16));
-  if (U) {
-    hipLaunchKernelGGL(k_pack_rows, dim3((unsigned)((U + 255) / 256)), dim3(256), 0, c->stream, c->dist_k2.as<int64_t>(),
-                       c->dist_v3.as<uint32_t>(), degmax ? c->dist_v4.as<int64_t>() : nullptr, U, kw, vw, mw,
-                       c->dist_k.as<uint32_t>());
-    GS_HIP(hipGetLastError());
+  const uint32_t* sendrows = c->dist_k2.as<uint32_t>();
+  for (uint32_t p = 0; p < P; ++p) {
+    const uint64_t sn = c->host_small[8 + 2 * p], rn = c->host_small[8 + 2 * P + 2 * p];
+    const uint32_t kw = (c->host_small[8 + 2 * P + 2 * p + 1] & 1) ? 2u : 1u;
+    segs.row0[p] = nrecv;
+    segs.kw[p] = kw;
+    if (p == me) segs.src[p] = sendrows + so * (kw_me + vw + mw);   // own rows: read where the partition wrote them
+    send_b[p] = sn * (kw_me + vw + mw) * 4;
+    recv_b[p] = rn * (kw + vw + mw) * 4;
+    so += sn;
+    nrecv += rn;
   }
-  GS_TRY(exchange_rows(c, c->dist_k.as<char>(), send.data(), c->dist_x2.as<char>(), recv.data(), (size_t)rw * 4));
-  GS_TRY(ensure(c, c->dist_k2, nrecv * 8 + 8));
-  GS_TRY(ensure(c, c->dist_v3, nrecv * vb + 8));
-  if (degmax) GS_TRY(ensure(c, c->dist_v4, nrecv * 8 + 8));
+  segs.row0[P] = nrecv;
+  uint64_t recv_bytes = 0;
+  for (uint32_t p = 0; p < P; ++p) recv_bytes += p == me ? 0 : recv_b[p];
+  // 3. one exchange of the packed rows (bytes; nothing to or from this rank itself)
+  GS_TRY(ensure(c, c->dist_x2, recv_bytes + 16));
+  GS_TRY(exchange_rows(c, c->dist_k2.as<char>(), send_b.data(), c->dist_x2.as<char>(), recv_b.data(), 1, true));
+  for (uint32_t p = 0; p < P; ++p) {
+    if (p == me) continue;
+    segs.src[p] = c->dist_x2.as<uint32_t>() + ro / 4;
+    ro += recv_b[p];
+  }
+  // unpacked merge input: the local partials are consumed, their buffers take it
+  GS_TRY(ensure(c, c->dist_k, nrecv * 8 + 8));
+  GS_TRY(ensure(c, c->dist_v, nrecv * vb + 8));
+  if (degmax) GS_TRY(ensure(c, c->dist_v2, nrecv * 8 + 8));
   if (nrecv) {
-    hipLaunchKernelGGL(k_unpack_rows, dim3((unsigned)((nrecv + 255) / 256)), dim3(256), 0, c->stream,
-                       c->dist_x2.as<uint32_t>(), nrecv, kw, vw, mw, c->dist_k2.as<int64_t>(), c->dist_v3.as<uint32_t>(),
-                       degmax ? c->dist_v4.as<int64_t>() : nullptr);
+    hipLaunchKernelGGL(k_unpack_rows, dim3((unsigned)((nrecv + 255) / 256)), dim3(256), 0, c->stream, segs, nrecv, vw, mw,
+                       c->dist_k.as<int64_t>(), c->dist_v.as<uint32_t>(), degmax ? c->dist_v2.as<int64_t>() : nullptr);
     GS_HIP(hipGetLastError());
   }
   // 4. the merge of what this rank owns
   const int32_t pdt = degmax || op == GS_OP_COUNT ? GS_I64 : b->val_dtype;
-  const gs_partial_batch pb{c->dist_k2.as<int64_t>(), c->dist_v3.p, degmax ? c->dist_v4.as<int64_t>() : nullptr, nrecv,
+  const gs_partial_batch pb{c->dist_k.as<int64_t>(), c->dist_v.p, degmax ? c->dist_v2.as<int64_t>() : nullptr, nrecv,
                             pdt, GS_MEM_DEVICE};
+  const int timing = c->timing;   // the merge's stage times are not reported (the window's are): no events
+  c->timing = GS_TIMING_OFF;
   gs_status st = degmax ? gs_merge_degree_max_partials(c, &pb, init_max, dout) : gs_merge_partials(c, &pb, op, init, vout);
+  c->timing = timing;
   c->times = keep;
   return st;
 }

@@ -205,8 +205,10 @@ gs_status comm_allreduce(gs_ctx* c, void* buf, size_t count, int nccl_dtype, int
 gs_status comm_alltoall(gs_ctx* c, const void* send, void* recv, size_t count, int nccl_dtype);
 gs_status comm_allgather_u64(gs_ctx* c, uint64_t mine, uint64_t* all);
 gs_status comm_agree(gs_ctx* c, gs_status local);
+// skip_self: this rank's own rows (send[me] == recv[me]) stay in sendbuf -- not copied, and the receive
+// buffer holds only the peers' rows
 gs_status exchange_rows(gs_ctx* c, const char* sendbuf, const uint64_t* send, char* recvbuf, const uint64_t* recv,
-                        size_t row);
+                        size_t row, bool skip_self = false);
 gs_status comm_allgatherv(gs_ctx* c, const void* sendbuf, char* recvbuf, const uint64_t* counts, size_t row);
 // exclusive scan of n u64 (gs_hashset.hip)
 gs_status xscan(gs_ctx* c, const uint64_t* in, uint64_t n, uint64_t* out);

@@ -135,6 +135,29 @@ def test_reduce_and_fold_dist(pkg, oracle, window, P):
         check_union([res[r][len(cases) + j] for r in range(P)], want, P)
 
 
+@pytest.mark.parametrize("P", (2, 3))
+def test_reduce_dist_mixed_key_widths(pkg, oracle, window, P):
+    """Each sender picks its own key width for the packed rows (1 word when its partials' keys lie in
+    [0, 2^32), else 2): here the last rank's slice holds ids past 2^32, the others' do not, so every
+    owner unpacks segments of both widths (its own segment straight from its send buffer)."""
+    s, d = window
+    s, d = s.copy(), d.copy()
+    sl = slices(N, P)
+    a, b = sl[-1]
+    s[a:b] += 3 << 33
+    d[a:b] += 3 << 33
+    v = oracle.gen_values(N, 0x5EED0C, oracle.DT_I64)
+
+    def fn(r, e):
+        a, b = sl[r]
+        return [e.reduce_dist(s[a:b], d[a:b], v[a:b], 2, 0), e.fold_degree_max_dist(s[a:b], d[a:b], 1, -5)]
+
+    res, errs = run_group(pkg, P, fn)
+    assert not errs, errs
+    check_union([res[r][0] for r in range(P)], oracle.window_reduce(s, d, v, 2, 0), P)
+    check_union([res[r][1] for r in range(P)], oracle.window_fold_degree_max(s, d, 1, -5), P)
+
+
 def _tri_windows(oracle):
     s, d = oracle.gen_rmat(SCALE, N, 0x5EED0B, no_self_loops=True)
     ls, ld = oracle.gen_rmat(11, 30_000, 0x5EED0C)           # self-loops kept: the reference's rule

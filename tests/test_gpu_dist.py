@@ -289,20 +289,33 @@ def test_split_window_steps_and_rccl_world_one(pkg, oracle):
 
 def test_merges_keep_their_own_speculative_counts(pkg, oracle):
     """keyBy on one ctx alternates a window's partials and a merge of received rows: the merge's rows
-    spread over the buckets unlike the window's and arrive as sorted owner runs, so merges run in their
-    own slot (slot 1: no speculation, their own packing state) and the windows keep speculating from
-    their own counts (a shared slot made every window miss)."""
+    spread over the buckets unlike the window's and arrive as sorted sender runs, so merges run in their
+    own slot (slot 1: their own bucket counts, one segment per bucket, their own packing state) and the
+    windows keep speculating from their own counts (a shared slot made every window miss).  Each merge
+    here gets two sender runs with common vertices: owner 0's partials of windows w and w + 1."""
+    def win(w):
+        s, d = oracle.gen_rmat(18, 1 << 21, 0x5EED02, first_edge=w << 21)
+        v = oracle.gen_values(1 << 21, 0x5EED02, oracle.DT_I64, first_edge=w << 21)
+        return s, d, v
+
     with pkg.Engine(0) as e:
-        spec = []
-        for w in range(5):
-            s, d = oracle.gen_rmat(18, 1 << 21, 0x5EED02, first_edge=w << 21)
-            v = oracle.gen_values(1 << 21, 0x5EED02, oracle.DT_I64, first_edge=w << 21)
-            S, D_, V = (torch.from_numpy(x).cuda() for x in (s, d, v))
-            k, p, counts = e.reduce_partials(S, D_, V, 1, 0, 2)
-            spec.append(e.stage_times().speculative)
-            mk, mv = e.merge_partials(k[:counts[0]], p[:counts[0]], 0)   # the rows owner 0 would get
-            rk, rv = oracle.window_reduce(s, d, v, 1, 0)
+        spec, mspec = [], []
+        nxt = win(0)
+        for w in range(6):
+            (s, d, v), nxt = nxt, win(w + 1)
+            runs_k, runs_v = [], []
+            for j, (a, b, c) in enumerate(((s, d, v), nxt)):
+                S, D_, V = (torch.from_numpy(x).cuda() for x in (a, b, c))
+                k, p, counts = e.reduce_partials(S, D_, V, 1, 0, 2)
+                if j == 0:
+                    spec.append(e.stage_times().speculative)
+                runs_k.append(k[:counts[0]].clone())
+                runs_v.append(p[:counts[0]].clone())
+            mk, mv = e.merge_partials(torch.cat(runs_k), torch.cat(runs_v), 0)
+            mspec.append(e.stage_times().speculative)
+            rk, rv = oracle.window_reduce(np.concatenate([s, nxt[0]]), np.concatenate([d, nxt[1]]),
+                                          np.concatenate([v, nxt[2]]), 1, 0)
             own = owner_np(rk, 2) == 0
             assert np.array_equal(mk.cpu().numpy(), rk[own]) and np.array_equal(mv.cpu().numpy(), rv[own])
-            assert e.stage_times().speculative == 0   # (the merge)
-        assert spec[0] == 0 and spec[1:] == [1, 1, 1, 1], spec
+        assert spec[0] == 0 and spec[1:] == [1] * 5, spec
+        assert mspec[0] == 0 and mspec[1:] == [1] * 5, mspec

@@ -4,6 +4,8 @@ cd "${GRAFT_REPO_ROOT}"
 O=gpurun_out/$1
 mkdir -p $O
 export TMPDIR=/tmp
+timeout -k 10 400 python3 -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_gpu_comm_group.py tests/test_gpu_dist.py > $O/tests.txt 2>&1
+echo tests done
 export WORLD_SIZE=1 RANK=0 LOCAL_RANK=0 MASTER_ADDR=127.0.0.1 MASTER_PORT=29555
 timeout -k 10 300 python3 bench.py --force-exchange --no-cpu-baseline > $O/forced.json 2> $O/forced.err
 echo forced done
