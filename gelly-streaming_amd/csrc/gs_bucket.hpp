@@ -528,6 +528,10 @@ __device__ __forceinline__ uint32_t bk_block_scan(uint32_t x, uint32_t* s_w, uin
 }
 
 // ---- k_bk_plan: digit bases of the partition passes, bucket starts, work items (one block) -------
+#ifndef GS_BK_LPT
+#define GS_BK_LPT 1
+#endif
+constexpr int BK_LPT_CLASSES = 64;
 // pass p ranks digit (bucket >> (p * w)) & (2^w - 1); bucket b's records end up at
 // [bucket_start[b], bucket_start[b + 1]).  Items: a bucket of cnt records is split into
 // ceil(cnt / item_recs) items; multi-item buckets get consecutive slabs.
@@ -600,6 +604,33 @@ static __global__ __launch_bounds__(BK_PLAN_BLOCK) void k_bk_plan(const uint32_t
   const uint32_t first0 = bk_block_scan(i0 + i1, s_w, n_items);
   const uint32_t slab0 = bk_block_scan(m0 + m1, s_w, n_slabs);
   const uint32_t mb0 = bk_block_scan((m0 ? 1u : 0u) + (m1 ? 1u : 0u), s_w, n_multi);
+#if GS_BK_LPT
+  // claim order: largest items first (k_bk_accum's workgroups take items from a counter, so the small
+  // ones fill the gaps at the end instead of a large one starting last): a counting sort over
+  // BK_LPT_CLASSES size classes, descending; the order within a class is free
+  __shared__ uint32_t s_cls[BK_LPT_CLASSES];
+  for (int i = tid; i < BK_LPT_CLASSES; i += BK_PLAN_BLOCK) s_cls[i] = 0;
+  __syncthreads();
+  auto size_class = [&](uint32_t n) -> uint32_t {   // larger items -> smaller class
+    return BK_LPT_CLASSES - 1 - min<uint32_t>(BK_LPT_CLASSES - 1, (uint32_t)((uint64_t)n * BK_LPT_CLASSES / (item_recs + 1)));
+  };
+  auto count_items = [&](uint32_t b, uint32_t c, uint32_t ni) {
+    if (b >= nb) return;
+    for (uint32_t k = 0; k < ni; ++k) atomicAdd(&s_cls[size_class(min(c, (k + 1) * item_recs) - k * item_recs)], 1u);
+  };
+  count_items(b0, c0, i0);
+  count_items(b1, c1, i1);
+  __syncthreads();
+  if (tid == 0) {
+    uint32_t run = 0;
+    for (int i = 0; i < BK_LPT_CLASSES; ++i) {
+      const uint32_t x = s_cls[i];
+      s_cls[i] = run;
+      run += x;
+    }
+  }
+  __syncthreads();
+#endif
   auto emit_bucket = [&](uint32_t b, uint32_t c, uint32_t ni, uint32_t first, uint32_t slab, uint32_t mb) {
     if (b >= nb) return;
     o.bucket_count[b] = 0;
@@ -612,7 +643,11 @@ static __global__ __launch_bounds__(BK_PLAN_BLOCK) void k_bk_plan(const uint32_t
       it.begin = k * item_recs;   // relative; made absolute below
       it.end = min(c, (k + 1) * item_recs);
       it.slab = ni > 1 ? slab + k : ~0u;
+#if GS_BK_LPT
+      o.items[atomicAdd(&s_cls[size_class(it.end - it.begin)], 1u)] = it;
+#else
       o.items[first + k] = it;
+#endif
     }
   };
   emit_bucket(b0, c0, i0, first0, slab0, mb0);
@@ -1257,11 +1292,7 @@ void k_sp_scatter_pack(BaseSrc<V, DIR, PAY_VAL> es, uint64_t n, int S, uint32_t 
   }
   const uint32_t r0 = t * TILE;
   // this block's XCD slot: its segment (xmask 0: one segment per bucket, the merges' sorted runs)
-#ifdef GS_SP_X7
-  const uint32_t xs = SP_NSEG == 1 ? 0u : blockIdx.x & 7u;
-#else
   const uint32_t xs = SP_NSEG == 1 ? 0u : blockIdx.x & xmask;
-#endif
   auto col_index = [&](uint32_t j) -> uint32_t { return DIR == DIR_ALL ? (r0 + j) >> 1 : r0 + j; };
   // this thread's buckets (BPT consecutive ones): their segment ends, issued before the columns
   uint32_t send[BPT];
@@ -1470,11 +1501,7 @@ __global__ __launch_bounds__(SPU_BLOCK) __attribute__((amdgpu_waves_per_eu(4))) 
     if (t >= nfull) return;
   }
   const uint32_t r0 = t * TILE;
-#ifdef GS_SP_X7
-  const uint32_t xs = SP_NSEG == 1 ? 0u : blockIdx.x & 7u;
-#else
   const uint32_t xs = SP_NSEG == 1 ? 0u : blockIdx.x & xmask;
-#endif
   uint32_t send[BPT];
 #pragma unroll
   for (int k = 0; k < BPT; ++k) send[k] = sp_hi(cursor, xs, min((uint32_t)tid * BPT + k, nbp - 1));
