@@ -975,6 +975,18 @@ def main():
                                       "peak": round(peak, 1), "unit": "G probes/s", "frac": round(ach / peak, 4),
                                       "probes_per_window": int(partials),
                                       "peak_formula": "LDS 128 B/clk/CU x 256 CUs x 2.4 GHz / 16 B per bucket read"}
+        # SURVEY.md §8(d)'s intersection term beside 16E: a per-edge merge intersection reads both out-lists,
+        # 4 B per entry, sum over the oriented edges u -> v of d+(u) + d+(v) (gs_stage_times.escapes, path 3)
+        ment = statistics.mean(t.escapes for t in times)
+        mb = 4 * ment
+        whole_s = ms_step * 1e-3
+        roofline["merge_intersection_term"] = {
+            "bytes_per_window": int(mb), "formula": "4 * sum over oriented edges u->v of (d+(u) + d+(v))",
+            "over_16E": round(mb / B, 2),
+            "window_16E_plus_term": {"achieved": round((B + mb) / whole_s / 1e9 / world, 1), "unit": "GB/s",
+                                     "frac": round((B + mb) / whole_s / 1e9 / world / HBM_PEAK_GBS, 4)},
+            "count_kernels_on_term": {"achieved": round(mb / t_cnt / 1e9, 1) if t_cnt > 0 else 0.0, "unit": "GB/s",
+                                      "frac": round(mb / t_cnt / 1e9 / HBM_PEAK_GBS, 4) if t_cnt > 0 else 0.0}}
 
     cpu = None
     threads = max(1, min(16, os.cpu_count() or 1))

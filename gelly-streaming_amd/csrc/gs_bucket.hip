@@ -181,11 +181,14 @@ gs_status bucket_accumulate(gs_ctx* c, Src rs, uint64_t R, uint32_t nb, int64_t 
   BkStage st{c->keysA.as<uint32_t>(), c->valsA.p,
              (std::is_same_v<P, BkDeg> || std::is_same_v<P, BkDeg32>) ? c->aux.as<int64_t>() : nullptr};
   auto* slabs = c->bk_slabs.as<typename P::Lds>();
-  hipLaunchKernelGGL((k_bk_accum<P, Src, GS_BK_UNROLL>), dim3(c->n_cu), dim3(BK_ACC_BLOCK), 0, c->stream, rs,
-                     c->bk_items.as<BkItem>(), ns + 0, meta + BkMeta::BSTART, ns + 2, slabs, st, meta + BkMeta::BCOUNT,
-                     mm, seg_cur);
+  // the direct path's accumulate (ev0 2) is a dominant kernel: its own start (pass_ev[7]) and stop events
+  const bool dom = ev0 == 2 && c->timing == GS_TIMING_DOMINANT;
+  launch_dominant(c, dom ? c->pass_ev[7] : nullptr, dom ? c->pass_ev[ev0 + 1] : nullptr, k_bk_accum<P, Src, GS_BK_UNROLL>,
+                  dim3(c->n_cu * GS_BK_ACC_PER_CU), dim3(BK_ACC_BLOCK), rs, (const BkItem*)c->bk_items.as<BkItem>(),
+                  (const uint32_t*)(ns + 0), (const uint32_t*)(meta + BkMeta::BSTART), ns + 2, slabs, st,
+                  meta + BkMeta::BCOUNT, mm, seg_cur);
   GS_HIP(hipGetLastError());
-  stage_event(c, c->pass_ev[ev0 + 1], ev0 == 2);   // (the direct path's accumulate bracket)
+  stage_event(c, c->pass_ev[ev0 + 1]);
   const unsigned mgrid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(nb, R / BK_ITEM + 1));
   hipLaunchKernelGGL((k_bk_merge_slices<P>), dim3(mgrid, BK_MS_SLICES), dim3(BK_MS_BLOCK), 0, c->stream,
                      meta + BkMeta::MLIST, ns + 1, meta + BkMeta::BITEMS, meta + BkMeta::BSLAB, slabs, mm);
@@ -239,9 +242,9 @@ void bucket_times(gs_ctx* c, int path, int passes, int launches, uint32_t key_bi
   if (c->timing != GS_TIMING_STAGES) {   // only the events stage_event recorded at this level
     t.keyinfo_ms = t.sort_ms = t.reduce_ms = t.total_ms = 0.f;
     for (int p = 0; p < 8; ++p) t.pass_ms[p] = 0.f;
-    if (c->timing == GS_TIMING_DOMINANT && path == 2) {   // the scatter and the accumulate
-      t.pass_ms[1] = event_ms(c->pass_ev[1], c->pass_ev[2]);
-      t.pass_ms[2] = event_ms(c->pass_ev[2], c->pass_ev[3]);
+    if (c->timing == GS_TIMING_DOMINANT && path == 2) {   // the scatter and the accumulate (launch_dominant)
+      if (passes) t.pass_ms[1] = event_ms(c->pass_ev[1], c->pass_ev[2]);
+      t.pass_ms[2] = event_ms(c->pass_ev[7], c->pass_ev[3]);
     }
   }
 }
@@ -351,33 +354,35 @@ gs_status bucket_direct_t(gs_ctx* c, const int64_t* src, const int64_t* dst, con
         if constexpr (P::REL) GS_HIP(hipMemsetAsync(rel_bad, 0, 4, c->stream));
         stage_event(c, c->ev[1]);
         stage_event(c, c->pass_ev[0]);
-        stage_event(c, c->pass_ev[1], true);
+        stage_event(c, c->pass_ev[1]);
         using Load = typename P::Load;
         const BaseSrc<Load, DIR, P::PAY> ls{src, dst, (const Load*)val, base};
         uint32_t* cur = c->sp_cur.as<uint32_t>();
+        hipEvent_t e0 = c->pass_ev[1], e1 = c->pass_ev[2];
+        uint32_t* kp = c->keysB.as<uint32_t>();
+        auto* esc = (unsigned long long*)(sm + SM_BK_ESC);
+        const uint32_t trash = (uint32_t)cap;
         if constexpr (CAN_PACK && ITEMS == PK_ITEMS) {
           // the bucket tables sized for the window's buckets (1024: 8 KiB less LDS, one bucket per thread)
           if (pack && nb <= 1024)
-            hipLaunchKernelGGL((k_sp_scatter_pack<Load, DIR, 1024>), dim3(spk_grid<DIR>(n)), dim3(SPK_BLOCK), 0,
-                               c->stream, ls, n, S, nb, cur, c->keysB.as<uint32_t>(), vpart, (uint32_t)cap, mm,
-                               (unsigned long long*)(sm + SM_BK_ESC), xmask);
+            launch_dominant(c, e0, e1, k_sp_scatter_pack<Load, DIR, 1024>, dim3(spk_grid<DIR>(n)), dim3(SPK_BLOCK), ls, n,
+                            S, nb, cur, kp, vpart, trash, mm, esc, xmask);
           else if (pack)
-            hipLaunchKernelGGL((k_sp_scatter_pack<Load, DIR, BK_MAXB>), dim3(spk_grid<DIR>(n)), dim3(SPK_BLOCK), 0,
-                               c->stream, ls, n, S, nb, cur, c->keysB.as<uint32_t>(), vpart, (uint32_t)cap, mm,
-                               (unsigned long long*)(sm + SM_BK_ESC), xmask);
+            launch_dominant(c, e0, e1, k_sp_scatter_pack<Load, DIR, BK_MAXB>, dim3(spk_grid<DIR>(n)), dim3(SPK_BLOCK), ls,
+                            n, S, nb, cur, kp, vpart, trash, mm, esc, xmask);
         }
         if constexpr (ITEMS == DP_ITEMS) {
           if (!pack) {
             if (nb <= 1024)
-              hipLaunchKernelGGL((k_sp_scatter<Load, DIR, P::PAY, Raw, P::REL, 1024>), dim3(spu_grid<DIR>(n)),
-                                 dim3(SPU_BLOCK), 0, c->stream, ls, n, S, nb, cur, k16, vpart, (uint32_t)cap, rel_bad, mm, xmask);
+              launch_dominant(c, e0, e1, k_sp_scatter<Load, DIR, P::PAY, Raw, P::REL, 1024>, dim3(spu_grid<DIR>(n)),
+                              dim3(SPU_BLOCK), ls, n, S, nb, cur, k16, vpart, trash, rel_bad, mm, xmask);
             else
-              hipLaunchKernelGGL((k_sp_scatter<Load, DIR, P::PAY, Raw, P::REL, BK_MAXB>), dim3(spu_grid<DIR>(n)),
-                                 dim3(SPU_BLOCK), 0, c->stream, ls, n, S, nb, cur, k16, vpart, (uint32_t)cap, rel_bad, mm, xmask);
+              launch_dominant(c, e0, e1, k_sp_scatter<Load, DIR, P::PAY, Raw, P::REL, BK_MAXB>, dim3(spu_grid<DIR>(n)),
+                              dim3(SPU_BLOCK), ls, n, S, nb, cur, k16, vpart, trash, rel_bad, mm, xmask);
           }
         }
         GS_HIP(hipGetLastError());
-        stage_event(c, c->pass_ev[2], true);
+        stage_event(c, c->pass_ev[2]);
         stage_event(c, c->ev[2]);
         GS_TRY(launch_plan<P>(c, cap, nb, 0, 0, item_recs, cur, sp.tot.as<uint32_t>(), mm));
         part = true;
@@ -417,7 +422,7 @@ gs_status bucket_direct_t(gs_ctx* c, const int64_t* src, const int64_t* dst, con
                          c->dp_off.as<uint32_t>());
       GS_HIP(hipGetLastError());
     }
-    stage_event(c, c->pass_ev[1], true);
+    stage_event(c, c->pass_ev[1], !part);   // (a partitioned window's scatter carries its own events)
 
     // 3. the scatter: bucket-local index + payload in bucket order
     if constexpr (P::REL) {
@@ -427,22 +432,23 @@ gs_status bucket_direct_t(gs_ctx* c, const int64_t* src, const int64_t* dst, con
     const BaseSrc<Load, DIR, P::PAY> ls{src, dst, (const Load*)val, base};
     if (part) {
       const unsigned grid = dp_scatter_grid<DIR, ITEMS>(n);
+      const uint32_t* off = c->dp_off.as<uint32_t>();
+      const auto* mmc = (const unsigned long long*)mm;
       if constexpr (CAN_PACK) {
         if (pack) {
-          hipLaunchKernelGGL((k_dp_scatter_pack<Load, DIR, ITEMS>), dim3(grid), dim3(DP_BLOCK), 0, c->stream, ls, n, S, nb,
-                             (const uint32_t*)c->dp_off.as<uint32_t>(), c->keysB.as<uint32_t>(), vpart,
-                             (const unsigned long long*)mm, (unsigned long long*)(sm + SM_BK_ESC));
+          launch_dominant(c, c->pass_ev[1], c->pass_ev[2], k_dp_scatter_pack<Load, DIR, ITEMS>, dim3(grid), dim3(DP_BLOCK),
+                          ls, n, S, nb, off, c->keysB.as<uint32_t>(), vpart, mmc, (unsigned long long*)(sm + SM_BK_ESC));
           GS_HIP(hipGetLastError());
         }
       }
       if constexpr (ITEMS == DP_ITEMS) if (!pack) {
         if constexpr (P::REL) GS_HIP(hipMemsetAsync(rel_bad, 0, 4, c->stream));
-        hipLaunchKernelGGL((k_dp_scatter<Load, DIR, P::PAY, Raw, P::REL>), dim3(grid), dim3(DP_BLOCK), 0, c->stream, ls,
-                           n, S, nb, c->dp_off.as<uint32_t>(), k16, vpart, rel_bad, (const unsigned long long*)mm);
+        launch_dominant(c, c->pass_ev[1], c->pass_ev[2], k_dp_scatter<Load, DIR, P::PAY, Raw, P::REL>, dim3(grid),
+                        dim3(DP_BLOCK), ls, n, S, nb, c->dp_off.as<uint32_t>(), k16, vpart, rel_bad, mmc);
         GS_HIP(hipGetLastError());
       }
     }
-    stage_event(c, c->pass_ev[2], true);
+    stage_event(c, c->pass_ev[2], !part);
     stage_event(c, c->ev[2]);
 
     // 4-6. accumulate, merge, emit; one read-back
@@ -653,3 +659,11 @@ gs_status bucket_degree_max(gs_ctx* c, const int64_t* src, const int64_t* dst, u
 }
 
 }  // namespace gs
+
+#ifdef GS_BK_TRACE
+// tuning builds only (tools/accum_trace.py): the last accumulate's per-item records
+extern "C" __attribute__((visibility("default"))) int gs_debug_bk_trace(void* dst, uint32_t n) {
+  return (int)hipMemcpyFromSymbol(dst, HIP_SYMBOL(gs::g_bk_trace), (size_t)std::min<uint32_t>(n, gs::BK_TRACE_MAX) * 32, 0,
+                                  hipMemcpyDeviceToHost);
+}
+#endif

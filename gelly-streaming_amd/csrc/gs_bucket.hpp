@@ -33,7 +33,16 @@ constexpr int BK_MAXB = 2048;          // buckets (the bucket index has <= 11 bi
 constexpr int BK_INFO_BLOCK = 512;
 // (k_bk_accum, packed records, A/B of round 3: the next group's loads in flight during this group's
 // atomics, C2 accumulate 0.345 vs 0.331 ms: removed)
-constexpr int BK_ACC_BLOCK = 1024;     // 16 waves: one workgroup per CU (LDS-bound)
+#ifndef GS_BK_ACC_BLOCK
+#define GS_BK_ACC_BLOCK 1024
+#endif
+#ifndef GS_BK_ACC_PER_CU
+#define GS_BK_ACC_PER_CU 1
+#endif
+#ifndef GS_BK_S8
+#define GS_BK_S8 14   // 2^S vertices per bucket with 8-byte accumulators (BkVal)
+#endif
+constexpr int BK_ACC_BLOCK = GS_BK_ACC_BLOCK;     // 16 waves: one workgroup per CU (LDS-bound)
 constexpr int BK_NW = BK_ACC_BLOCK / WAVE;
 constexpr int BK_PLAN_BLOCK = 1024;
 
@@ -117,7 +126,7 @@ struct BkVal {
   using Load = Raw;                   // what the scatter loads (Raw: what it stores)
   static constexpr bool REL = false;  // payload stored as an offset from the window base
   using A = std::conditional_t<std::is_floating_point_v<T>, double, T>;
-  static constexpr int S = sizeof(A) == 8 ? 14 : 15;
+  static constexpr int S = sizeof(A) == 8 ? GS_BK_S8 : 15;
   static constexpr uint32_t W = 1u << S;
   static constexpr bool HAS_V = true;
   static constexpr int PAY = PAY_VAL;
@@ -1649,6 +1658,10 @@ __device__ __forceinline__ void bk_finalize(const typename P::Lds& s, uint32_t b
   if (tid == 0) bucket_count[bucket] = tot;
 }
 
+#ifdef GS_BK_TRACE
+constexpr uint32_t BK_TRACE_MAX = 16384;
+__device__ uint64_t g_bk_trace[BK_TRACE_MAX][4];
+#endif
 template <class P, class Src, int UNROLL>
 __global__ __launch_bounds__(BK_ACC_BLOCK) void k_bk_accum(Src src, const BkItem* __restrict__ items,
                                                            const uint32_t* __restrict__ n_items_p,
@@ -1672,6 +1685,9 @@ __global__ __launch_bounds__(BK_ACC_BLOCK) void k_bk_accum(Src src, const BkItem
     const uint32_t it = s_item;
     if (it >= n_items) break;
     const BkItem m = items[it];
+#ifdef GS_BK_TRACE
+    const uint64_t t_item0 = wall_clock64();
+#endif
     const uint32_t b0 = bucket_start[m.bucket];
     P::init(s, tid);
     __syncthreads();
@@ -1698,6 +1714,9 @@ __global__ __launch_bounds__(BK_ACC_BLOCK) void k_bk_accum(Src src, const BkItem
             qi[u] = q4_of(g < n4 ? g : n4 - 1);
             x[u] = rec4[qi[u]];
           }
+          // every load of the group issued before the first use (the scheduler moved the first
+          // group's decode, and its wait, between the loads)
+          __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
           for (int u = 0; u < U4; ++u) {
             if (g4 + (uint32_t)u * BK_ACC_BLOCK >= n4) continue;
@@ -1760,16 +1779,21 @@ __global__ __launch_bounds__(BK_ACC_BLOCK) void k_bk_accum(Src src, const BkItem
           for (uint32_t q = a1; q < p1; ++q) add1(q, src.rec[q]);
         }
         __syncthreads();
-        // each lane's groups come in increasing g: a cursor over the pieces (a piece is ~2^13 groups,
-        // one step of the stream 2^12, so the cursor rarely moves)
-        uint32_t cx = 0, cnext = s_pre4[1], cbase = s_qb[0];
+        // group g of the stream lies in the last piece x with s_pre4[x] <= g (empty pieces share their
+        // start with the next one): the pieces' bounds in registers, a branch-free select per load (a
+        // cursor walking s_pre4 in LDS put an LDS read and its wait between consecutive loads)
+        // (as a sum of the bases' steps: a select chain compiled to a table in scratch memory)
+        uint32_t pre[SP_NSEG], dq[SP_NSEG];
+#pragma unroll
+        for (uint32_t x = 0; x < SP_NSEG; ++x) {
+          pre[x] = s_pre4[x];
+          dq[x] = x ? s_qb[x] - s_qb[x - 1] : s_qb[0];
+        }
         stream(s_pre4[SP_NSEG], [&](uint32_t g) {
-          while (g >= cnext) {   // g < s_pre4[SP_NSEG]: cx stays < SP_NSEG
-            ++cx;
-            cnext = s_pre4[cx + 1];
-            cbase = s_qb[cx];
-          }
-          return g + cbase;
+          uint32_t b = dq[0];
+#pragma unroll
+          for (uint32_t x = 1; x < SP_NSEG; ++x) b += g >= pre[x] ? dq[x] : 0u;
+          return g + b;
         });
       }
     } else {
@@ -1869,6 +1893,14 @@ __global__ __launch_bounds__(BK_ACC_BLOCK) void k_bk_accum(Src src, const BkItem
       for (uint32_t i = tid; i < sizeof(typename P::Lds) / 16; i += BK_ACC_BLOCK) gs[i] = ls[i];
     }
     __syncthreads();
+#ifdef GS_BK_TRACE   // tuning builds only: per item (workgroup, item, wall clock at 100 MHz, records)
+    if (tid == 0 && it < BK_TRACE_MAX) {
+      g_bk_trace[it][0] = blockIdx.x;
+      g_bk_trace[it][1] = t_item0;
+      g_bk_trace[it][2] = wall_clock64();
+      g_bk_trace[it][3] = m.end - m.begin;
+    }
+#endif
   }
 }
 

@@ -1,6 +1,7 @@
 // gs_internal.hpp — host-side context, workspace and the window sort shared by all operators.
 #pragma once
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 #include <stdint.h>
 
 #include <string>
@@ -117,6 +118,7 @@ struct gs_ctx {
     uint64_t R = 0;
   } sp[2];
   int sp_slot = 0;
+  uint64_t tri_merge = 0;   // the last count's sum of d+(u) + d+(v) over its oriented edges (tri_times)
   gs::DevBuf sp_cur;
   // stage-2 candidate count (gs_pairs.hip): staged input columns, packed keys / payloads, group sums
   gs::DevBuf pr_a, pr_b, pr_f, pr_key, pr_val, pr_gk, pr_gv, pr_small;
@@ -164,7 +166,8 @@ constexpr size_t SM_TRI_NV = SM_TRI_PROBES + 8;     // u64 triangles: vertices w
 constexpr size_t SM_BK_ESC = SM_TRI_PROBES + 16;    // u64 packed scatter: escaped values
 constexpr size_t SM_DEV_ERR = SM_BK_ESC + 8;        // u32 device error flags (GS_DERR_*)
 constexpr size_t SM_HS = SM_DEV_ERR + 8;            // u32[4] HashSet order: complex vertices, JDK flags
-constexpr size_t SM_BYTES = SM_HS + 16;
+constexpr size_t SM_TRI_MERGE = SM_HS + 16;      // u64 triangles: sum of d+(u) + d+(v) over the oriented edges
+constexpr size_t SM_BYTES = SM_TRI_MERGE + 8;
 // device error flags (SM_DEV_ERR): a kernel that cannot finish its work sets one and returns
 constexpr uint32_t GS_DERR_TABLE_FULL = 1u;         // an LDS hash set filled up (triangle counting)
 constexpr size_t HOST_SMALL_WORDS = 512;            // pinned u64 mirror of small scalars
@@ -250,6 +253,15 @@ inline float event_ms(hipEvent_t a, hipEvent_t b) {
 // `dominant` (the bucket path's scatter / accumulate brackets); never at GS_TIMING_OFF
 inline void stage_event(gs_ctx* c, hipEvent_t e, bool dominant = false) {
   if (c->timing == GS_TIMING_STAGES || (dominant && c->timing == GS_TIMING_DOMINANT)) hipEventRecord(e, c->stream);
+}
+// a dominant kernel (the bucket path's scatter and accumulate): at GS_TIMING_DOMINANT its start / stop
+// events ride on its own dispatch (hipExtLaunchKernelGGL) -- an event record of its own is a packet
+// between two kernels, ~5-10 us of idle GPU each; otherwise a plain launch, bracketed by the caller's
+// stage_event records at GS_TIMING_STAGES
+template <typename F, typename... A>
+inline void launch_dominant(gs_ctx* c, hipEvent_t e0, hipEvent_t e1, F k, dim3 grid, dim3 block, A... args) {
+  if (c->timing == GS_TIMING_DOMINANT) hipExtLaunchKernelGGL(k, grid, block, 0, c->stream, e0, e1, 0, args...);
+  else hipLaunchKernelGGL(k, grid, block, 0, c->stream, args...);
 }
 
 // k_keyinfo over both columns (ALL): mask at SM_MASK, byte histograms at SM_HIST

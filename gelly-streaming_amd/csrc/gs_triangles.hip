@@ -1008,13 +1008,15 @@ gs_status tri_count(gs_ctx* c, uint32_t B, size_t V, uint64_t M, const uint32_t*
   if (d_active) GS_HIP(hipMemsetAsync(d_active, 0, 8, c->stream));
   uint32_t* d_err = (uint32_t*)(sm + SM_DEV_ERR);
   GS_HIP(hipMemsetAsync(d_err, 0, 4, c->stream));
+  auto* d_merge = (unsigned long long*)(sm + SM_TRI_MERGE);
+  GS_HIP(hipMemsetAsync(d_merge, 0, 8, c->stream));
   // LDS hash-set bucket cap: unlimited, or one bucket under GS_FLAG_TEST_TINY_TABLES (tests only)
   const uint32_t nb_cap = (c->flags & GS_FLAG_TEST_TINY_TABLES) ? 1u : 0xFFFFFFFFu;
   uint32_t* d_nqueue = d_nheavy + 1;
   uint2* queue = c->tri_queue.as<uint2>();
   hipLaunchKernelGGL(k_tri_lclass, dim3((unsigned)std::max<uint64_t>(1, std::min<uint64_t>((V + 255) / 256, 16384))),
                      dim3(256), 0, c->stream, nbr, out_range, in_range, (uint32_t)V, 0u, 0xFFFFFFFFu, nb_cap, queue,
-                     d_nqueue, c->tri_heavy.as<uint2>(), d_nheavy, d_active);
+                     d_nqueue, c->tri_heavy.as<uint2>(), d_nheavy, d_active, d_merge);
   if (d_active && loops && rank) {
     const uint32_t words = (uint32_t)((V + 31) / 32);
     hipLaunchKernelGGL(k_tri_loop_only, dim3((unsigned)std::max<uint64_t>(1, std::min<uint64_t>((words + 255) / 256, 4096))),
@@ -1063,8 +1065,10 @@ gs_status tri_count(gs_ctx* c, uint32_t B, size_t V, uint64_t M, const uint32_t*
   c->host_small[7] = 0;   // (the copy below fills the low 4 bytes)
   GS_HIP(hipMemcpyAsync(c->host_small + 7, d_err, 4, hipMemcpyDeviceToHost, c->stream));
   if (d_active) GS_HIP(hipMemcpyAsync(c->host_small + 9, d_active, 8, hipMemcpyDeviceToHost, c->stream));
+  GS_HIP(hipMemcpyAsync(c->host_small + 10, d_merge, 8, hipMemcpyDeviceToHost, c->stream));
   GS_TRY(host_wait(c));
   if (active) *active = c->host_small[9];
+  c->tri_merge = c->host_small[10];
   if ((uint32_t)c->host_small[3] != 0) return set_error(c, GS_EDEVICE, "look-back spin timed out");
   if ((uint32_t)c->host_small[7] & GS_DERR_TABLE_FULL)
     return set_error(c, GS_EDEVICE, "window triangles: an LDS hash set filled up (counting aborted)");
@@ -1085,6 +1089,7 @@ void tri_times(gs_ctx* c, const TriGeom& g, uint64_t M, uint64_t nv, uint64_t pr
   t.records = M;     // unique undirected edges
   t.vertices = nv;   // vertices with edges
   t.partials = probes;
+  t.escapes = c->tri_merge;
   t.path = 3;
 }
 

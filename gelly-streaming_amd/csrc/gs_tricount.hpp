@@ -347,15 +347,21 @@ __global__ __launch_bounds__(256) void k_tri_lclass(const uint32_t* __restrict__
                                                     uint32_t q1, uint32_t nb_cap, uint2* __restrict__ queue,
                                                     uint32_t* __restrict__ n_queue, uint2* __restrict__ heavy,
                                                     uint32_t* __restrict__ n_heavy,
-                                                    unsigned long long* __restrict__ n_active) {
+                                                    unsigned long long* __restrict__ n_active,
+                                                    unsigned long long* __restrict__ merge) {
   const int lane = threadIdx.x & 63;
   uint32_t act = 0;   // this lane's ranks with an out- or in-entry (n_active, when asked for)
+  // sum over the oriented edges u -> v counted here of d+(u) + d+(v) (the list entries a merge
+  // intersection per edge would read; bench's roofline): per vertex x, d+(x) (d+(x) + d-(x))
+  unsigned long long mg = 0;
   for (uint32_t v0 = blockIdx.x * 256u; v0 < nv; v0 += gridDim.x * 256u) {   // wave-uniform trip count
     const uint32_t v = v0 + threadIdx.x;
     uint32_t nh = 0, nl = 0;
     if (v < nv) {
       const uint2 ro = out_range[v], ri = in_range[v];
       if (n_active) act += (ro.y != ro.x || ri.y != ri.x) ? 1u : 0u;
+      if (ro.x >= q0 && ro.x < q1)
+        mg += (unsigned long long)(ro.y - ro.x) * ((ro.y - ro.x) + (ri.y - ri.x));
       if (ro.y != ro.x && ri.y != ri.x && ro.x >= q0 && ro.x < q1) {
         const uint32_t dv = ro.y - ro.x;
         const bool heavy_v = dv > TH_DMAX ||
@@ -379,6 +385,11 @@ __global__ __launch_bounds__(256) void k_tri_lclass(const uint32_t* __restrict__
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) act += __shfl_xor(act, o, WAVE);
     if (lane == 0 && act) atomicAdd(n_active, (unsigned long long)act);
+  }
+  if (merge) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) mg += __shfl_xor(mg, o, WAVE);
+    if (lane == 0 && mg) atomicAdd(merge, mg);
   }
 }
 

@@ -576,14 +576,16 @@ typedef struct gs_stage_times {
                               1 = speculative partition (regions from the previous window's counts,
                                   runs reserved with atomics: keyinfo_ms = regions, pass_ms[0] = 0);
                               2 = speculative partition missed, window rerun through k_dp_hist   */
-  uint64_t escapes;        /* path 2, packed: values stored in full (outside [0, 0xFFFF))          */
+  uint64_t escapes;        /* path 2, packed: values stored in full (outside [0, 0xFFFF));
+                              path 3: sum over the oriented edges u -> v of d+(u) + d+(v), the list
+                                 entries a per-edge merge intersection would read (a roofline term)   */
 } gs_stage_times;
 GS_API gs_status gs_last_stage_times(const gs_ctx* ctx, gs_stage_times* out);
 /* Which device events a window records for gs_last_stage_times (diagnostics; replaces nothing in the
  * reference).  GS_TIMING_STAGES (the default): every stage of every path.  GS_TIMING_DOMINANT: on the
- * bucket path (path 2) only the brackets of the partition scatter and the accumulate (pass_ms[1],
- * pass_ms[2]; every other time reads 0) -- each event record costs the stream a few microseconds,
- * ~30 us per C2 window at the default.  GS_TIMING_OFF: none on the bucket path.  path / packed /
+ * bucket path (path 2) only the partition scatter and the accumulate (pass_ms[1], pass_ms[2], from
+ * events carried by those two kernels' own dispatches; every other time reads 0) -- each separate event
+ * record costs the stream a few microseconds, ~30 us per C2 window at the default.  GS_TIMING_OFF: none on the bucket path.  path / packed /
  * speculative / escapes and the counts stay valid at every level. */
 #define GS_TIMING_OFF 0
 #define GS_TIMING_DOMINANT 1

@@ -4,10 +4,10 @@ cd "${GRAFT_REPO_ROOT}"
 O=gpurun_out/$1
 mkdir -p $O
 export TMPDIR=/tmp
-true > $O/tests.txt
+timeout -k 10 400 python3 -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_gpu_bucket.py > $O/tests.txt 2>&1
 echo tests done
 for rep in 1 2; do
-  for v in base i2 i4 i6; do
+  for v in base pre; do
     if [ "$v" = base ]; then lib=gelly-streaming_amd/libgellyhip.so; else lib=gelly-streaming_amd/variants/$v/libgellyhip.so; fi
     GELLY_HIP_LIB=$lib timeout -k 10 300 python3 bench.py --no-cpu-baseline > $O/ab_${v}_$rep.json 2> $O/ab_${v}_$rep.err
     echo $v $rep done
