@@ -42,10 +42,11 @@ def parse():
     p.add_argument("--seed", type=lambda x: int(x, 0), default=0x5EED02)
     p.add_argument("--dtype", default="int64", choices=["int64", "float64"])
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--cpu-sample-log2", type=int, default=28,
+    p.add_argument("--cpu-sample-log2", type=int, default=30,
                    help="triangles: the CPU baseline counts windows up to 2^this many edges (larger windows: their "
-                        "first 2^this); 30 = the whole C4 (s26) window")
-    p.add_argument("--cpu-reps", type=int, default=5, help="triangles: CPU baseline windows timed (median)")
+                        "first 2^this); 30 = the whole C4 (s26) window (~65 s of 16-thread CPU)")
+    p.add_argument("--cpu-reps", type=int, default=None,
+                   help="triangles: CPU baseline windows timed (median); default 5, 1 for windows over 2^28 edges")
     p.add_argument("--timing", default="dominant", choices=["dominant", "stages"],
                    help="reduce / fold: stage events inside the timed region -- the dominant kernels only "
                         "(default) or every stage (each record costs the stream a few microseconds)")
@@ -314,13 +315,16 @@ def cpu_baseline_cc(src, dst, sample_log2=23):
                       f"(oracle/gs_oracle.c gso_components, one thread), median of 3: {dt:.2f} s, {len(v)} vertices"}
 
 
-def cpu_baseline_triangles(wins, threads, sample_log2=28, reps=5):
+def cpu_baseline_triangles(wins, threads, sample_log2=30, reps=None):
     """BASELINE.md C4 CPU baseline: the forward algorithm (the reference's O(sum d^2) candidate rule is
     infeasible at this scale) over `threads` threads (oracle gso_triangles_fwd_mt) on whole windows up to
-    2^28 edges (R-MAT scale 24; larger windows: their first 2^28 edges), cycling the bench's windows:
-    1 warm-up on a 1/16 sample, then the median of `reps`."""
+    2^sample_log2 edges (default 2^30: the whole C4 s26 window; larger windows: their first 2^sample_log2
+    edges), cycling the bench's windows: 1 warm-up on a 1/16 sample, then the median of `reps` (default 5,
+    1 above 2^28 edges: one s26 window is ~65 s of 16-thread CPU)."""
     orc = ge.load_oracle()
     S = min(1 << sample_log2, wins[0][0].numel())
+    if reps is None:
+        reps = 5 if S <= (1 << 28) else 1
     host = [(w[0][:S].cpu().numpy(), w[1][:S].cpu().numpy()) for w in wins[:max(1, min(reps, len(wins)))]]
     orc.triangles_fwd_mt(host[0][0][: S // 16], host[0][1][: S // 16], threads)
     ts = []
