@@ -623,20 +623,20 @@ static __global__ __launch_bounds__(BK_PLAN_BLOCK) void k_bk_plan(const uint32_t
   auto size_class = [&](uint32_t n) -> uint32_t {   // larger items -> smaller class
     return BK_LPT_CLASSES - 1 - min<uint32_t>(BK_LPT_CLASSES - 1, (uint32_t)((uint64_t)n * BK_LPT_CLASSES / (item_recs + 1)));
   };
+  // a bucket's items are ni - 1 full ones and its last piece: one atomic for each group (a hub bucket of
+  // a Zipf stream has hundreds of items; one atomic per item serialised the plan's thread)
   auto count_items = [&](uint32_t b, uint32_t c, uint32_t ni) {
-    if (b >= nb) return;
-    for (uint32_t k = 0; k < ni; ++k) atomicAdd(&s_cls[size_class(min(c, (k + 1) * item_recs) - k * item_recs)], 1u);
+    if (b >= nb || !ni) return;
+    if (ni > 1) atomicAdd(&s_cls[size_class(item_recs)], ni - 1);
+    atomicAdd(&s_cls[size_class(c - (ni - 1) * item_recs)], 1u);
   };
   count_items(b0, c0, i0);
   count_items(b1, c1, i1);
   __syncthreads();
-  if (tid == 0) {
-    uint32_t run = 0;
-    for (int i = 0; i < BK_LPT_CLASSES; ++i) {
-      const uint32_t x = s_cls[i];
-      s_cls[i] = run;
-      run += x;
-    }
+  static_assert(BK_LPT_CLASSES == WAVE, "one wave scans the classes");
+  if (tid < WAVE) {
+    const uint32_t x = s_cls[tid];
+    s_cls[tid] = wave_inclusive_sum(x) - x;
   }
   __syncthreads();
 #endif
@@ -646,6 +646,11 @@ static __global__ __launch_bounds__(BK_PLAN_BLOCK) void k_bk_plan(const uint32_t
     o.b_items[b] = ni;
     o.b_slab[b] = slab;
     if (ni > 1) o.mlist[mb] = b;
+    if (!ni) return;
+#if GS_BK_LPT
+    const uint32_t fpos = ni > 1 ? atomicAdd(&s_cls[size_class(item_recs)], ni - 1) : 0u;   // the full items
+    const uint32_t lpos = atomicAdd(&s_cls[size_class(c - (ni - 1) * item_recs)], 1u);     // the last piece
+#endif
     for (uint32_t k = 0; k < ni; ++k) {
       BkItem it;
       it.bucket = b;
@@ -653,7 +658,7 @@ static __global__ __launch_bounds__(BK_PLAN_BLOCK) void k_bk_plan(const uint32_t
       it.end = min(c, (k + 1) * item_recs);
       it.slab = ni > 1 ? slab + k : ~0u;
 #if GS_BK_LPT
-      o.items[atomicAdd(&s_cls[size_class(it.end - it.begin)], 1u)] = it;
+      o.items[k + 1 < ni ? fpos + k : lpos] = it;
 #else
       o.items[first + k] = it;
 #endif

@@ -1,15 +1,16 @@
-# one-off GPU probe of round 5: accumulate item order (LPT) A/B + bucket tests
+# one-off GPU probe of round 5: the secondary bench lines DESIGN.md quotes
 set -e
 cd "${GRAFT_REPO_ROOT}"
 O=gpurun_out/$1
 mkdir -p $O
 export TMPDIR=/tmp
-timeout -k 10 400 python3 -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_gpu_bucket.py > $O/tests.txt 2>&1
-echo tests done
-for rep in 1 2; do
-  for v in base pre; do
-    if [ "$v" = base ]; then lib=gelly-streaming_amd/libgellyhip.so; else lib=gelly-streaming_amd/variants/$v/libgellyhip.so; fi
-    GELLY_HIP_LIB=$lib timeout -k 10 300 python3 bench.py --no-cpu-baseline > $O/ab_${v}_$rep.json 2> $O/ab_${v}_$rep.err
-    echo $v $rep done
-  done
-done
+b() { local name=$1; shift; timeout -k 10 300 python3 bench.py "$@" > $O/$name.json 2> $O/$name.err; echo "$name done"; }
+b bench_c2_f64 --dtype float64
+b bench_c3_rmat --workload fold
+b bench_c3_zipf --workload fold --stream zipf
+b bench_tri_s20 --workload triangles --scale 20
+b bench_tri_s22 --workload triangles --scale 22
+b bench_tri_s24 --workload triangles --scale 24
+b bench_cc_s24 --workload cc
+b bench_cand_stream --workload cand_stream
+b bench_cand_stream_emit_only --workload cand_stream --cand-consumer none --cand-windows 1
