@@ -449,11 +449,12 @@ gs_status gs_merge_degree_max_partials(gs_ctx* c, const gs_partial_batch* p, int
 
 // partials of this rank's slice -> all-to-all over the ctx's communicator -> the merge of what this
 // rank owns.  Per window: the local reduce (the bucket path's own read-back), the owner partition on the
-// device, ONE all-to-all of [rows, flags] per peer read back together (the only host wait of the
-// exchange: sizes, the key width every rank agrees on, and every rank's status -- a rank whose local
+// device straight into packed rows, ONE all-to-all of [rows, flags] per peer read back together (the only
+// host wait of the exchange: sizes, each sender's key width, and every rank's status -- a rank whose local
 // step failed still joins it with the failure flag, so all ranks return an error together instead of
-// the others blocking in a collective), one packed all-to-all of the rows (4-byte keys when every
-// rank's keys fit), then the merge.  One rank: the window's own output (no exchange, no merge).
+// the others blocking in a collective), one packed all-to-all of the rows (4-byte keys from a sender whose
+// keys all fit; a rank's own rows stay in place), the unpack by sender, then the merge.  One rank: the
+// window's own output (no exchange, no merge).
 static gs_status dist_impl(gs_ctx* c, const gs_edge_batch* b, int32_t dir, int32_t op, const void* init, bool degmax,
                            int64_t init_max, gs_vertex_out* vout, gs_degree_out* dout) {
   if (!c->comm) return set_error(c, GS_EINVAL, "no communicator (gs_comm_init)");
