@@ -151,16 +151,17 @@ static gs_status launch_hist_bytes(gs_ctx* c, const int64_t* src, const int64_t*
   return hip_check(c, hipGetLastError(), "k_hist_bytes");
 }
 
-template <typename K, typename V, bool HAS_V, class Src>
+template <typename K, typename V, bool HAS_V, class Src, int DBITS = RADIX_BITS>
 static gs_status launch_pass(gs_ctx* c, Src src, K* kout, V* vout, uint32_t R, int pass, uint32_t shift) {
   char* sm = c->small.as<char>();
   const uint32_t tiles = (R + SORT_TILE - 1) / SORT_TILE;
   const uint32_t ep = next_epoch(c, 0);
+  const uint32_t* base = DBITS == RADIX_BITS ? (const uint32_t*)(sm + SM_BASE) + pass * RADIX
+                                             : (const uint32_t*)(sm + SM_BASE9) + pass * (1 << DBITS);
   GS_HIP(hipMemsetAsync((uint32_t*)(sm + SM_COUNTERS) + pass, 0, 4, c->stream));
-  hipLaunchKernelGGL((k_onesweep<K, V, HAS_V, SORT_BLOCK, SORT_ITEMS, Src>), dim3(tiles), dim3(SORT_BLOCK), 0,
-                     c->stream, src, kout, vout, R, shift, (const uint32_t*)(sm + SM_BASE) + pass * RADIX,
-                     c->sort_status.as<uint64_t>(), (uint32_t*)(sm + SM_COUNTERS) + pass, ep,
-                     (uint32_t*)(sm + SM_TIMEOUT));
+  hipLaunchKernelGGL((k_onesweep<K, V, HAS_V, SORT_BLOCK, SORT_ITEMS, Src, DBITS>), dim3(tiles), dim3(SORT_BLOCK), 0,
+                     c->stream, src, kout, vout, R, shift, base, c->sort_status.as<uint64_t>(),
+                     (uint32_t*)(sm + SM_COUNTERS) + pass, ep, (uint32_t*)(sm + SM_TIMEOUT));
   return hip_check(c, hipGetLastError(), "k_onesweep");
 }
 
@@ -244,7 +245,7 @@ static gs_status sort_dir(gs_ctx* c, const int64_t* src, const int64_t* dst, con
   return dispatch_payload<uint32_t, DIR>(c, src, dst, val, vbytes, (uint32_t)R, payload, out);
 }
 
-template <typename K, typename V, bool HAS_V>
+template <typename K, typename V, bool HAS_V, int DBITS = RADIX_BITS>
 static gs_status buffer_passes(gs_ctx* c, const uint64_t* keys, const V* vals, uint32_t R, Sorted* out) {
   K* ka = c->keysA.as<K>();
   K* kb = c->keysB.as<K>();
@@ -252,11 +253,11 @@ static gs_status buffer_passes(gs_ctx* c, const uint64_t* keys, const V* vals, u
   V* vb = c->valsB.as<V>();
   ConvSrc<K, V> cs{keys, HAS_V ? vals : nullptr, out->key_xor};
   hipEventRecord(c->pass_ev[0], c->stream);
-  GS_TRY((launch_pass<K, V, HAS_V>(c, cs, ka, va, R, 0, 0)));
+  GS_TRY((launch_pass<K, V, HAS_V, ConvSrc<K, V>, DBITS>(c, cs, ka, va, R, 0, 0)));
   hipEventRecord(c->pass_ev[1], c->stream);
   for (int p = 1; p < out->passes; ++p) {
     BufSrc<K, V> bs{ka, HAS_V ? va : nullptr, 0};
-    GS_TRY((launch_pass<K, V, HAS_V>(c, bs, kb, vb, R, p, 8u * p)));
+    GS_TRY((launch_pass<K, V, HAS_V, BufSrc<K, V>, DBITS>(c, bs, kb, vb, R, p, (uint32_t)DBITS * p)));
     hipEventRecord(c->pass_ev[p + 1], c->stream);
     std::swap(ka, kb);
     std::swap(va, vb);
@@ -267,9 +268,19 @@ static gs_status buffer_passes(gs_ctx* c, const uint64_t* keys, const V* vals, u
   return GS_OK;
 }
 
+// 9-bit digits are off by default: on the s26 triangle window one pass less of each sort still cost more
+// than it saved (6 x 9-bit passes of the oriented keys 96.8-98.7 vs 89.8 ms for 7 x 8-bit, the transposed
+// sort 40 vs 36.6 ms; same box, profiles/r05/tri/d9_ab/): each 512-bin pass looks back over twice the
+// digits, ranks with 9 ballots and writes runs of half the length.  GS_SORT_DIGIT9=1 turns them on (A/B).
+int sort_digit_bits(int bits) {
+  static const bool on = getenv("GS_SORT_DIGIT9") && getenv("GS_SORT_DIGIT9")[0] == '1';
+  return on && bits > 0 && (bits + 8) / 9 < (bits + 7) / 8 ? 9 : 8;
+}
+
 gs_status sort_buffer(gs_ctx* c, const uint64_t* keys, const void* vals, uint64_t n, Sorted* out, int bits_hint,
-                      int val_bytes, bool hist_ready) {
+                      int val_bytes, bool hist_ready, int digit_bits) {
   char* sm = c->small.as<char>();
+  if (digit_bits == 9 && !hist_ready) return set_error(c, GS_EINVAL, "sort_buffer: 9-bit digits need a known key width");
   const int nd = std::min(8, std::max(1, (bits_hint + 7) / 8));
   int bits = bits_hint;
   uint64_t k0 = 0;
@@ -290,12 +301,22 @@ gs_status sort_buffer(gs_ctx* c, const uint64_t* keys, const void* vals, uint64_
   // (hist_ready: the producer of the keys filled SM_HIST for bits_hint-bit keys; no host round trip)
   out->bits = bits;
   out->wide = bits > 32;
-  out->passes = std::max(1, (bits + RADIX_BITS - 1) / RADIX_BITS);
+  const bool d9 = digit_bits == 9;
+  out->passes = std::max(1, (bits + (d9 ? 8 : RADIX_BITS - 1)) / (d9 ? 9 : RADIX_BITS));
   out->done_passes = out->passes;
   out->records = n;
   out->key_xor = (out->wide || hist_ready) ? 0 : (k0 & 0xFFFFFFFF00000000ull);
-  hipLaunchKernelGGL(k_digit_base, dim3(1), dim3(256), 0, c->stream, (const uint32_t*)(sm + SM_HIST),
-                     (uint32_t*)(sm + SM_BASE), out->passes);
+  if (d9) {   // the 9-bit digits' histograms: one more read of the keys
+    GS_HIP(hipMemsetAsync(sm + SM_HIST9, 0, (size_t)out->passes * 512 * 4, c->stream));
+    if (n)
+      hipLaunchKernelGGL(k_hist_digits<9>, dim3(grid_for(n, 256 * 8, 2048)), dim3(256), 0, c->stream, keys, n, out->passes,
+                         (uint32_t*)(sm + SM_HIST9));
+    hipLaunchKernelGGL(k_digit_base_bits<9>, dim3(1), dim3(512), 0, c->stream, (const uint32_t*)(sm + SM_HIST9),
+                       (uint32_t*)(sm + SM_BASE9), out->passes);
+  } else {
+    hipLaunchKernelGGL(k_digit_base, dim3(1), dim3(256), 0, c->stream, (const uint32_t*)(sm + SM_HIST),
+                       (uint32_t*)(sm + SM_BASE), out->passes);
+  }
   GS_HIP(hipGetLastError());
   const size_t kb = out->wide ? 8 : 4;
   const uint64_t tiles = (n + SORT_TILE - 1) / SORT_TILE;
@@ -306,9 +327,19 @@ gs_status sort_buffer(gs_ctx* c, const uint64_t* keys, const void* vals, uint64_
     GS_TRY(ensure(c, c->valsA, n * val_bytes));
     GS_TRY(ensure(c, c->valsB, n * val_bytes));
   }
-  GS_TRY(ensure(c, c->sort_status, tiles * RADIX * 8, true));
+  GS_TRY(ensure(c, c->sort_status, tiles * (d9 ? 512 : RADIX) * 8, true));
   const auto* v4 = (const uint32_t*)vals;
   const auto* v8 = (const uint64_t*)vals;
+  if (d9) {
+    if (out->wide) {
+      if (!vals) return buffer_passes<uint64_t, uint8_t, false, 9>(c, keys, nullptr, (uint32_t)n, out);
+      return val_bytes == 8 ? buffer_passes<uint64_t, uint64_t, true, 9>(c, keys, v8, (uint32_t)n, out)
+                            : buffer_passes<uint64_t, uint32_t, true, 9>(c, keys, v4, (uint32_t)n, out);
+    }
+    if (!vals) return buffer_passes<uint32_t, uint8_t, false, 9>(c, keys, nullptr, (uint32_t)n, out);
+    return val_bytes == 8 ? buffer_passes<uint32_t, uint64_t, true, 9>(c, keys, v8, (uint32_t)n, out)
+                          : buffer_passes<uint32_t, uint32_t, true, 9>(c, keys, v4, (uint32_t)n, out);
+  }
   if (out->wide) {
     if (!vals) return buffer_passes<uint64_t, uint8_t, false>(c, keys, nullptr, (uint32_t)n, out);
     return val_bytes == 8 ? buffer_passes<uint64_t, uint64_t, true>(c, keys, v8, (uint32_t)n, out)

@@ -167,7 +167,9 @@ constexpr size_t SM_BK_ESC = SM_TRI_PROBES + 16;    // u64 packed scatter: escap
 constexpr size_t SM_DEV_ERR = SM_BK_ESC + 8;        // u32 device error flags (GS_DERR_*)
 constexpr size_t SM_HS = SM_DEV_ERR + 8;            // u32[4] HashSet order: complex vertices, JDK flags
 constexpr size_t SM_TRI_MERGE = SM_HS + 16;      // u64 triangles: sum of d+(u) + d+(v) over the oriented edges
-constexpr size_t SM_BYTES = SM_TRI_MERGE + 8;
+constexpr size_t SM_HIST9 = SM_TRI_MERGE + 8;      // u32[8][512] digit histograms of a 9-bit-digit sort
+constexpr size_t SM_BASE9 = SM_HIST9 + 8 * 512 * 4;  // u32[8][512] their exclusive scans
+constexpr size_t SM_BYTES = SM_BASE9 + 8 * 512 * 4;
 // device error flags (SM_DEV_ERR): a kernel that cannot finish its work sets one and returns
 constexpr uint32_t GS_DERR_TABLE_FULL = 1u;         // an LDS hash set filled up (triangle counting)
 constexpr size_t HOST_SMALL_WORDS = 512;            // pinned u64 mirror of small scalars
@@ -188,8 +190,12 @@ gs_status sort_window(gs_ctx* c, const int64_t* src, const int64_t* dst, const v
 // bits_hint: an upper bound on the key width (the histograms cover only those bytes); payload of
 // val_bytes (4 or 8) per key, or none.  hist_ready: the kernel that wrote the keys (all < 2^bits_hint)
 // already filled the digit histograms (SM_HIST, wave_hist_add): no scan, no host round trip
+// digit_bits 9 (hist_ready callers only: bits_hint is then the key width): 9-bit digits, their histograms
+// from one extra read of the keys -- one LSD pass less where 8-bit digits would leave a last pass of 1-2 bits
 gs_status sort_buffer(gs_ctx* c, const uint64_t* keys, const void* vals, uint64_t n, Sorted* out,
-                      int bits_hint = 64, int val_bytes = 4, bool hist_ready = false);
+                      int bits_hint = 64, int val_bytes = 4, bool hist_ready = false, int digit_bits = 8);
+// the digit width for a sort of `bits`-bit keys: 8, or with GS_SORT_DIGIT9=1 9 when that saves a pass
+int sort_digit_bits(int bits);
 
 // HashSet-ordered distinct neighbour sets of an ALL window (gs_hashset.hip)
 gs_status hashset_order(gs_ctx* c, const int64_t* src, const int64_t* dst, uint64_t n, uint32_t* U_out,

@@ -16,6 +16,8 @@
 // Keys are compacted to 32 bits whenever only the low 32 bits vary (vertex IDs < 2^32 or
 // any window whose IDs share their high half) — halving key traffic in every pass.
 #pragma once
+#include <type_traits>
+
 #include "gs_device.hpp"
 
 namespace gs {
@@ -240,8 +242,62 @@ __global__ __launch_bounds__(256) void k_hist_bytes(const int64_t* __restrict__ 
   }
 }
 
+// ---- wider digits (9 bits: one LSD pass less where 8-bit digits would leave a pass 1-2 bits wide) --
+// The histograms of every DBITS-bit digit of a u64 key buffer, one table per wave as wave_hist_add (the
+// wave's leading bin counted once), into hist_out[nd][1 << DBITS]
+template <int DBITS>
+__global__ __launch_bounds__(256) void k_hist_digits(const uint64_t* __restrict__ keys, uint64_t n, int nd,
+                                                     uint32_t* __restrict__ hist_out) {
+  constexpr int R = 1 << DBITS, MAXD = (64 + DBITS - 1) / DBITS;
+  __shared__ uint32_t h[4][MAXD * R];
+  const int tid = threadIdx.x, w = tid >> 6;
+  for (int i = tid; i < 4 * MAXD * R; i += 256) (&h[0][0])[i] = 0;
+  __syncthreads();
+  const uint64_t lt = (1ull << (tid & 63)) - 1;
+  const uint64_t stride = (uint64_t)gridDim.x * 256u;
+  for (uint64_t q0 = (uint64_t)blockIdx.x * 256u; q0 < n; q0 += stride) {   // same trip count on every lane
+    const uint64_t q = q0 + tid;
+    const bool valid = q < n;
+    const uint64_t k = valid ? keys[q] : 0ull;
+    for (int b = 0; b < nd; ++b) {
+      const uint32_t d = (uint32_t)(k >> (DBITS * b)) & (R - 1);
+      const uint32_t L = __builtin_amdgcn_readfirstlane(d);
+      const uint64_t same = __ballot(valid && d == L);
+      if (valid && d == L) {
+        if ((same & lt) == 0) atomicAdd(&h[w][b * R + L], (uint32_t)__popcll(same));
+      } else if (valid) {
+        atomicAdd(&h[w][b * R + d], 1u);
+      }
+    }
+  }
+  __syncthreads();
+  for (int i = tid; i < nd * R; i += 256) {
+    const uint32_t c = h[0][i] + h[1][i] + h[2][i] + h[3][i];
+    if (c) atomicAdd(&hist_out[i], c);
+  }
+}
+
+// hist[p][R] -> base[p][R] exclusive scans (block = R threads)
+template <int DBITS>
+__global__ __launch_bounds__(1 << DBITS) void k_digit_base_bits(const uint32_t* __restrict__ hist, uint32_t* __restrict__ base,
+                                                               int passes) {
+  constexpr int R = 1 << DBITS, NW = R / WAVE;
+  __shared__ uint32_t wsum[NW];
+  const int tid = threadIdx.x, l = tid & 63, w = tid >> 6;
+  for (int p = 0; p < passes; ++p) {
+    const uint32_t c = hist[p * R + tid];
+    const uint32_t inc = wave_inclusive_sum(c);
+    if (l == 63) wsum[w] = inc;
+    __syncthreads();
+    uint32_t off = 0;
+    for (int i = 0; i < w; ++i) off += wsum[i];
+    base[p * R + tid] = off + inc - c;
+    __syncthreads();
+  }
+}
+
 // ---- k_onesweep ------------------------------------------------------------------------------
-// One stable counting-sort pass on digit (key >> shift) & 255 over records [0, n).
+// One stable counting-sort pass on digit (key >> shift) & (2^DBITS - 1) over records [0, n).
 // Tile = BLOCK*ITEMS records, wave-striped (wave w owns records [w*ITEMS*64, (w+1)*ITEMS*64)
 // of the tile, item j at lane l is record j*64 + l), so (wave, item, lane) order == record order
 // and ranking in that order keeps the pass stable.
@@ -259,7 +315,11 @@ __global__ __launch_bounds__(BLOCK) void k_onesweep(Src src, KO* __restrict__ ko
   constexpr int NW = BLOCK / WAVE;
   constexpr int TILE = BLOCK * ITEMS;
   constexpr int XBYTES = (sizeof(K) > sizeof(V) || !HAS_V) ? sizeof(K) : sizeof(V);
-  __shared__ uint32_t s_whist[NW][RADIX];
+  // per-wave digit counters: 16-bit for wider digits (a tile's counts fit; 512 bins x 8 waves in 8 KiB keeps
+  // two blocks per CU with an 8-byte exchange tile)
+  using WH = std::conditional_t<(DBITS > 8), uint16_t, uint32_t>;
+  static_assert(DBITS <= 8 || TILE < 65536, "16-bit wave counters");
+  __shared__ WH s_whist[NW][RADIX];
   __shared__ uint32_t s_start[RADIX];
   __shared__ uint32_t s_goff[RADIX];
   __shared__ uint32_t s_wtot[NW];
@@ -298,7 +358,7 @@ __global__ __launch_bounds__(BLOCK) void k_onesweep(Src src, KO* __restrict__ ko
     uint32_t base = 0;
     if (valid) base = s_whist[wid][d];
     pos[j] = base + lt;
-    if (valid && lt == 0) s_whist[wid][d] = base + (uint32_t)__popcll(peers);
+    if (valid && lt == 0) s_whist[wid][d] = (WH)(base + (uint32_t)__popcll(peers));
   }
   __syncthreads();
 
@@ -308,7 +368,7 @@ __global__ __launch_bounds__(BLOCK) void k_onesweep(Src src, KO* __restrict__ ko
 #pragma unroll
     for (int w = 0; w < NW; ++w) {
       const uint32_t c = s_whist[w][tid];
-      s_whist[w][tid] = cnt;
+      s_whist[w][tid] = (WH)cnt;
       cnt += c;
     }
     uint64_t* st = status + (uint64_t)tile * RADIX + tid;

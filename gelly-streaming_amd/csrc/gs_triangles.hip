@@ -914,7 +914,7 @@ gs_status tri_unique(gs_ctx* c, const uint64_t* keys, uint64_t n, uint32_t B, bo
                      uint64_t* M, Sorted* s) {
   *M = 0;
   if (n == 0) return GS_OK;
-  GS_TRY(sort_buffer(c, keys, nullptr, n, s, 2 * (int)B, 4, hist_ready));
+  GS_TRY(sort_buffer(c, keys, nullptr, n, s, 2 * (int)B, 4, hist_ready, hist_ready ? sort_digit_bits(2 * (int)B) : 8));
   hipEventRecord(c->ev[1], c->stream);
   GS_TRY(ensure(c, c->out_keys, n * 8));
   UniqueOut uo{c->out_keys.as<uint64_t>(), nullptr};
@@ -984,7 +984,7 @@ gs_status tri_count(gs_ctx* c, uint32_t B, size_t V, uint64_t M, const uint32_t*
   }
   GS_HIP(hipGetLastError());
   Sorted t;
-  GS_TRY(sort_buffer(c, c->aux.as<uint64_t>(), c->tri_sfx.p, Ms, &t, (int)B, 8, true));
+  GS_TRY(sort_buffer(c, c->aux.as<uint64_t>(), c->tri_sfx.p, Ms, &t, (int)B, 8, true, sort_digit_bits((int)B)));
   if (t.wide || t.key_xor) return set_error(c, GS_EDEVICE, "window triangles: transposed keys wider than 32 bits");
   const uint2* sfx = (const uint2*)t.vals;   // the sort's payload buffer (valsA / valsB): read-only from here
   uint2* in_range = const_cast<uint2*>(out_range) + V;
@@ -1150,7 +1150,7 @@ gs_status triangles_impl(gs_ctx* c, const gs_edge_batch* b, uint32_t part, uint3
   uint2* out_range = nullptr;
   uint64_t loops = 0, nv = 0;
   if (fused) {
-    GS_TRY(sort_buffer(c, c->aux.as<uint64_t>(), nullptr, g.n, &s, 2 * (int)g.B, 4, true));
+    GS_TRY(sort_buffer(c, c->aux.as<uint64_t>(), nullptr, g.n, &s, 2 * (int)g.B, 4, true, sort_digit_bits(2 * (int)g.B)));
     if (!s.wide) return set_error(c, GS_EDEVICE, "window triangles: oriented keys narrower than expected");
     hipEventRecord(c->ev[1], c->stream);
     const uint64_t* sk = static_cast<const uint64_t*>(s.keys);
