@@ -13,8 +13,8 @@
 //           bucket index (k_onesweep with a global digit histogram), kept as the A/B baseline.
 #include <algorithm>
 
-#include "gs_bucket.hpp"
 #include "gs_ops.hpp"
+#include "gs_bucket.hpp"
 
 namespace gs {
 
@@ -197,9 +197,28 @@ gs_status bucket_accumulate(gs_ctx* c, Src rs, uint64_t R, uint32_t nb, int64_t 
                      meta + BkMeta::BCOUNT, mm);
   GS_HIP(hipGetLastError());
   stage_event(c, c->pass_ev[ev0 + 2]);
-  hipLaunchKernelGGL((k_bk_emit<P>), dim3(nb), dim3(256), 0, c->stream, meta + BkMeta::BSTART, meta + BkMeta::BCOUNT,
-                     nb, st, base, o, (unsigned long long*)(sm + SM_BK_MM + 24), mm, (const uint32_t*)(sm + SM_TIMEOUT),
-                     (const unsigned long long*)(sm + SM_BK_ESC), (unsigned long long*)(sm + SM_BK_X));
+  if (c->oe.nparts) {   // gs_window_reduce_dist: the exchange's rows instead of the ascending output
+    const OwnerEmit& e = c->oe;
+    hipLaunchKernelGGL(k_bk_owner_count, dim3(nb, BK_OE_SLICES), dim3(256), 0, c->stream, (const uint32_t*)(meta + BkMeta::BSTART),
+                       (const uint32_t*)(meta + BkMeta::BCOUNT), nb, (const uint32_t*)st.k, base, e.nparts, e.cnt, e.wide,
+                       mm, (const uint32_t*)(sm + SM_TIMEOUT), (const unsigned long long*)(sm + SM_BK_ESC),
+                       (unsigned long long*)(sm + SM_BK_X));
+    hipLaunchKernelGGL(k_owner_scan, dim3(1), dim3(1024), 0, c->stream, e.cnt, nb * BK_OE_SLICES * e.nparts,
+                       nb * BK_OE_SLICES, e.nparts, e.totals,
+                       (unsigned long long*)(sm + SM_BK_MM + 24));
+    hipLaunchKernelGGL((k_bk_owner_emit<P>), dim3(nb, BK_OE_SLICES), dim3(256), 0, c->stream, (const uint32_t*)(meta + BkMeta::BSTART),
+                       (const uint32_t*)(meta + BkMeta::BCOUNT), nb, st, base, o, e.nparts, (const uint32_t*)e.cnt, e.rows,
+                       (const unsigned long long*)e.wide, e.vw, e.mw, mm);
+    // the counts exchange's send rows too, before the read-back: after its wait the caller goes straight
+    // to the collective
+    hipLaunchKernelGGL(k_send_rows, dim3(1), dim3(64), 0, c->stream, (const unsigned long long*)e.totals, e.wide,
+                       e.nparts, e.send);
+    c->oe.done = true;
+  } else {
+    hipLaunchKernelGGL((k_bk_emit<P>), dim3(nb), dim3(256), 0, c->stream, meta + BkMeta::BSTART, meta + BkMeta::BCOUNT,
+                       nb, st, base, o, (unsigned long long*)(sm + SM_BK_MM + 24), mm, (const uint32_t*)(sm + SM_TIMEOUT),
+                       (const unsigned long long*)(sm + SM_BK_ESC), (unsigned long long*)(sm + SM_BK_X));
+  }
   GS_HIP(hipGetLastError());
   stage_event(c, c->pass_ev[ev0 + 3]);
   stage_event(c, c->ev[3]);

@@ -236,6 +236,8 @@ struct BkVal {
     T* vals;
     T init;
     bool has_init;
+    // the same output into other arrays (k_bk_owner_emit: a chunk's rows staged in LDS)
+    __device__ Out retarget(int64_t* k, void* v, int64_t*) const { return Out{k, (T*)v, init, has_init}; }
   };
   __device__ static void emit(const Out& o, uint64_t u, int64_t key, BkStage st, uint32_t j, int64_t) {
     const A a = ((const A*)st.a)[j];
@@ -274,6 +276,7 @@ struct BkCount {
     int64_t* keys;
     int64_t* vals;
     int64_t init;
+    __device__ Out retarget(int64_t* k, void* v, int64_t*) const { return Out{k, (int64_t*)v, init}; }
   };
   __device__ static void emit(const Out& o, uint64_t u, int64_t key, BkStage st, uint32_t j, int64_t) {
     o.keys[u] = key;
@@ -321,6 +324,7 @@ struct BkDeg {
     int64_t* deg;
     int64_t* mx;
     int64_t init_max;
+    __device__ Out retarget(int64_t* k, void* v, int64_t* v2) const { return Out{k, (int64_t*)v, v2, init_max}; }
   };
   __device__ static void emit(const Out& o, uint64_t u, int64_t key, BkStage st, uint32_t j, int64_t) {
     o.keys[u] = key;
@@ -1997,6 +2001,129 @@ __global__ __launch_bounds__(256) void k_bk_emit(const uint32_t* __restrict__ bu
     P::emit(o, off + i, (int64_t)((uint64_t)base + st.k[j]), st, j, base);
   }
   if (b == nb - 1 && tid == 0) *n_out = off + n;
+}
+
+// ---- the keyBy exchange's emit (gs_dist.hip): staging -> packed rows grouped by owner ----------------
+// Instead of k_bk_emit's ascending (vertex, value) output, which gs_window_reduce_dist then partitioned by
+// owner and packed: per bucket, its rows per owner (k_bk_owner_count), an owner-major scan (k_owner_scan),
+// then each bucket's rows written straight into the exchange's rows of their owner, in vertex order
+// (k_bk_owner_emit).  Row: key (1 word; 2 when a key of this window lies outside [0, 2^32)), the value
+// (vw words, as P::emit converts it), [the maximum (mw words)].
+// Each bucket's rows in BK_OE_SLICES slices (grid (buckets, slices)): a C2 window has ~7 K rows per bucket,
+// which one block per bucket walked in 256-row steps (owner count 27 us, emit 65 us at one block per bucket)
+constexpr uint32_t BK_OE_SLICES = 8;
+__global__ __launch_bounds__(256) void k_bk_owner_count(const uint32_t* __restrict__ bucket_start,
+                                                        const uint32_t* __restrict__ bucket_count, uint32_t nb,
+                                                        const uint32_t* __restrict__ stk, int64_t base, uint32_t nparts,
+                                                        uint32_t* __restrict__ cnt, unsigned long long* __restrict__ wide,
+                                                        const unsigned long long* __restrict__ mm,
+                                                        const uint32_t* __restrict__ timeout,
+                                                        const unsigned long long* __restrict__ n_esc,
+                                                        unsigned long long* __restrict__ res) {
+  __shared__ uint32_t s_c[64];
+  const int tid = threadIdx.x;
+  const uint32_t b = blockIdx.x;
+  if (b == 0 && blockIdx.y == 0 && tid == 0) {   // the read-back block: [timeout flag, escapes] (as k_bk_emit)
+    res[0] = *timeout;
+    res[1] = *n_esc;
+  }
+  if (tid < 64) s_c[tid] = 0;
+  __syncthreads();
+  if (mm[2]) return;
+  const uint64_t lt = (1ull << (tid & 63)) - 1;
+  const uint32_t nbk = bucket_count[b], sl = blockIdx.y;
+  const uint32_t r0 = (uint32_t)((uint64_t)nbk * sl / BK_OE_SLICES), r1 = (uint32_t)((uint64_t)nbk * (sl + 1) / BK_OE_SLICES);
+  const uint32_t n = r1 - r0, j0 = bucket_start[b] + r0;
+  bool w = false;
+  constexpr int U = 4;   // rows per lane per step: their loads issued together
+  for (uint32_t i0 = 0; i0 < n; i0 += 256 * U) {   // same trip count on every lane (ballots)
+    uint32_t kc[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t i = i0 + (uint32_t)u * 256 + tid;
+      kc[u] = i < n ? stk[j0 + i] : 0u;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const bool valid = i0 + (uint32_t)u * 256 + tid < n;
+      const int64_t key = (int64_t)((uint64_t)base + kc[u]);
+      w |= valid && ((uint64_t)key >> 32) != 0;
+      const uint32_t o = valid ? owner_of(key, nparts) : 0u;
+      const uint64_t peers = match_digit<6>(o, ballot(valid));
+      if (valid && (peers & lt) == 0) atomicAdd(&s_c[o], (uint32_t)__popcll(peers));
+    }
+  }
+  if (wide && __any(w) && (tid & 63) == 0) atomicOr(wide, 1ull);
+  __syncthreads();
+  if (tid < (int)nparts) cnt[(uint64_t)tid * nb * BK_OE_SLICES + b * BK_OE_SLICES + sl] = s_c[tid];
+}
+
+template <class P>
+__global__ __launch_bounds__(256) void k_bk_owner_emit(const uint32_t* __restrict__ bucket_start,
+                                                       const uint32_t* __restrict__ bucket_count, uint32_t nb,
+                                                       BkStage st, int64_t base, typename P::Out o, uint32_t nparts,
+                                                       const uint32_t* __restrict__ off, uint32_t* __restrict__ rows,
+                                                       const unsigned long long* __restrict__ wide, int vw, int mw,
+                                                       const unsigned long long* __restrict__ mm) {
+  __shared__ int64_t s_key[256];
+  __shared__ uint64_t s_v[256];
+  __shared__ int64_t s_v2[256];
+  __shared__ uint32_t s_wc[4][64];   // per wave: rows of each owner in this chunk
+  __shared__ uint32_t s_run[64];     // per owner: rows of this bucket written before this chunk
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  if (mm[2]) return;
+  const uint32_t b = blockIdx.x, sl = blockIdx.y;
+  const uint32_t nbk = bucket_count[b];
+  const uint32_t r0 = (uint32_t)((uint64_t)nbk * sl / BK_OE_SLICES), r1 = (uint32_t)((uint64_t)nbk * (sl + 1) / BK_OE_SLICES);
+  const uint32_t n = r1 - r0, j0 = bucket_start[b] + r0;
+  const uint64_t cslot = (uint64_t)b * BK_OE_SLICES + sl, cstride = (uint64_t)nb * BK_OE_SLICES;
+  const uint32_t kw = (*wide & 1ull) ? 2u : 1u, rw = kw + (uint32_t)vw + (uint32_t)mw;
+  const typename P::Out lo = o.retarget(s_key, s_v, s_v2);
+  const uint64_t lt = (1ull << lane) - 1;
+  if (tid < 64) s_run[tid] = 0;
+  for (uint32_t i0 = 0; i0 < n; i0 += 256) {
+    (&s_wc[0][0])[tid] = 0;
+    __syncthreads();
+    const uint32_t i = i0 + tid;
+    const bool valid = i < n;
+    uint32_t ow = 0, r = 0;
+    if (valid) {
+      const uint32_t j = j0 + i;
+      const int64_t key = (int64_t)((uint64_t)base + st.k[j]);
+      P::emit(lo, (uint64_t)tid, key, st, j, base);   // this row's key and converted value(s), in LDS
+      ow = owner_of(key, nparts);
+    }
+    const uint64_t peers = match_digit<6>(ow, ballot(valid));
+    if (valid) {
+      r = (uint32_t)__popcll(peers & lt);
+      if (r == 0) s_wc[w][ow] = (uint32_t)__popcll(peers);
+    }
+    __syncthreads();
+    if (valid) {
+      uint32_t before = s_run[ow];
+      for (int x = 0; x < w; ++x) before += s_wc[x][ow];
+      const uint64_t pos = (uint64_t)off[(uint64_t)ow * cstride + cslot] + before + r;
+      uint32_t* wr = rows + pos * rw;
+      const uint64_t k = (uint64_t)s_key[tid];
+      wr[0] = (uint32_t)k;
+      if (kw == 2) wr[1] = (uint32_t)(k >> 32);
+      if (vw == 1) {
+        wr[kw] = reinterpret_cast<const uint32_t*>(s_v)[tid];
+      } else {
+        const uint64_t v = s_v[tid];
+        wr[kw] = (uint32_t)v;
+        wr[kw + 1] = (uint32_t)(v >> 32);
+      }
+      if (mw) {
+        const uint64_t m = (uint64_t)s_v2[tid];
+        wr[kw + vw] = (uint32_t)m;
+        wr[kw + vw + 1] = (uint32_t)(m >> 32);
+      }
+    }
+    __syncthreads();
+    if (tid < (int)nparts) s_run[tid] += s_wc[0][tid] + s_wc[1][tid] + s_wc[2][tid] + s_wc[3][tid];
+    __syncthreads();   // (the next chunk clears s_wc)
+  }
 }
 
 }  // namespace gs

@@ -30,6 +30,8 @@ namespace gs {
 // owner_of: gs_ops.hpp (shared with the candidate split, gs_hashset.hip)
 
 constexpr int OW_BLOCK = 256, OW_ITEMS = 8, OW_TILE = OW_BLOCK * OW_ITEMS, OW_MAXP = 64;
+constexpr size_t BK_MAXB_DIST = 2048;   // the bucket path's most buckets (gs_bucket.hpp BK_MAXB) ...
+constexpr size_t BK_OE_SLICES_DIST = 8;  // ... and slices per bucket (BK_OE_SLICES): OwnerEmit's counts
 
 // per tile: partials per owner -> cnt[owner * tiles + tile]; *wide |= 1 when a key lies outside
 // [0, 2^32) (the exchange then sends 8-byte keys).  MAXP 8: each thread counts its rows per owner in
@@ -72,37 +74,6 @@ __global__ __launch_bounds__(OW_BLOCK) void k_owner_count(const int64_t* __restr
   if (wide && __any(w) && (tid & 63) == 0) atomicOr(wide, 1ull);
   __syncthreads();
   if (tid < (int)nparts) cnt[(uint64_t)tid * tiles + blockIdx.x] = s_c[tid];
-}
-
-// one block: exclusive scan of cnt[0 .. n) (owner-major) in place; totals[o] = partials of owner o
-__global__ __launch_bounds__(1024) void k_owner_scan(uint32_t* __restrict__ cnt, uint32_t n, uint32_t tiles,
-                                                     uint32_t nparts, unsigned long long* __restrict__ totals) {
-  __shared__ uint32_t s_w[16];
-  __shared__ uint32_t s_tot;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const uint32_t per = (n + 1023) / 1024, a = min(n, tid * per), b = min(n, a + per);
-  uint32_t sum = 0;
-  for (uint32_t i = a; i < b; ++i) sum += cnt[i];
-  const uint32_t inc = wave_inclusive_sum(sum);
-  if (lane == 63) s_w[w] = inc;
-  __syncthreads();
-  uint32_t off = 0, tot = 0;
-  for (int i = 0; i < 16; ++i) {
-    off += i < w ? s_w[i] : 0u;
-    tot += s_w[i];
-  }
-  uint32_t run = off + inc - sum;
-  for (uint32_t i = a; i < b; ++i) {
-    const uint32_t x = cnt[i];
-    cnt[i] = run;
-    run += x;
-  }
-  if (tid == 0) s_tot = tot;
-  __syncthreads();
-  if (tid < (int)nparts) {
-    const uint32_t lo = cnt[(uint64_t)tid * tiles], hi = tid + 1 < (int)nparts ? cnt[(uint64_t)(tid + 1) * tiles] : s_tot;
-    totals[tid] = hi - lo;
-  }
 }
 
 // stable partition of a tile of OW_TILE partials: the tile is loaded lane-interleaved (coalesced) into
@@ -233,7 +204,8 @@ gs_status owner_partition_dev(gs_ctx* c, const int64_t* keys, const void* vals, 
     hipLaunchKernelGGL(k_owner_count<8>, dim3(tiles), dim3(OW_BLOCK), 0, c->stream, keys, U, nparts, tiles, cnt, wide);
   else
     hipLaunchKernelGGL(k_owner_count<OW_MAXP>, dim3(tiles), dim3(OW_BLOCK), 0, c->stream, keys, U, nparts, tiles, cnt, wide);
-  hipLaunchKernelGGL(k_owner_scan, dim3(1), dim3(1024), 0, c->stream, cnt, tiles * nparts, tiles, nparts, totals);
+  hipLaunchKernelGGL(k_owner_scan, dim3(1), dim3(1024), 0, c->stream, cnt, tiles * nparts, tiles, nparts, totals,
+                     nullptr);
   auto launch = [&](auto vtag, auto ptag, auto ttag) {
     using V = decltype(vtag);
     constexpr int MP = decltype(ptag)::value;
@@ -298,21 +270,6 @@ __global__ __launch_bounds__(256) void k_unpack_rows(RowSegs segs, uint64_t n, i
   keys[i] = kw == 2 ? (int64_t)(((uint64_t)r[1] << 32) | r[0]) : (int64_t)(uint64_t)r[0];
   for (int j = 0; j < vw; ++j) vals[i * vw + j] = r[kw + j];
   if (mw) vals2[i] = (int64_t)(((uint64_t)r[kw + vw + 1] << 32) | r[kw + vw]);
-}
-
-// send row per peer p: [rows for p, flags] (flags: 1 = wide keys on this rank, 2 = this rank failed);
-// then the key-width flag is cleared for the next window's k_owner_count (no memset per window; a flag
-// left set by a failed window only widens that next window's keys)
-__global__ void k_send_rows(const unsigned long long* __restrict__ totals, unsigned long long* __restrict__ wide,
-                            uint32_t nparts, unsigned long long* __restrict__ send) {
-  const uint32_t p = threadIdx.x;
-  const unsigned long long fl = *wide & 1ull;
-  if (p < nparts) {
-    send[2 * p] = totals[p];
-    send[2 * p + 1] = fl;
-  }
-  __syncthreads();
-  if (p == 0) *wide = 0;
 }
 
 }  // namespace gs
@@ -469,14 +426,32 @@ static gs_status dist_impl(gs_ctx* c, const gs_edge_batch* b, int32_t dir, int32
   auto* wide = c->dist_x.as<unsigned long long>();
   auto* sendc = wide + 8;
   auto* recvc = sendc + 2 * P;
-  // 1. local partials + owner partition (device); a failure is carried into the counts exchange
+  // 1. local partials, written by the bucket path's last stage straight as the exchange's rows grouped by
+  //    owner (OwnerEmit); a window that takes another path (sort path, chunks) leaves the ascending output,
+  //    which the owner partition turns into the rows.  A failure is carried into the counts exchange.
   uint64_t U = 0;
   gs_status local = GS_OK;
   std::string local_err;
+  const int vw = (int)(vb / 4), mw = degmax ? 2 : 0;
+  bool emitted = false;
   {
     local = ensure(c, c->dist_k, R * 8 + 8);
     if (local == GS_OK) local = ensure(c, c->dist_v, R * 8 + 8);
     if (local == GS_OK && degmax) local = ensure(c, c->dist_v2, R * 8 + 8);
+    // the packed rows this rank sends (room for 2-word keys: the width is picked on the device)
+    if (local == GS_OK) local = ensure(c, c->dist_k2, R * (size_t)(2 + vw + mw) * 4 + 16);
+    if (local == GS_OK) local = ensure(c, c->dist_cnt, 1024 + (size_t)OW_MAXP * BK_MAXB_DIST * BK_OE_SLICES_DIST * 4);
+    if (local == GS_OK) {
+      c->oe = OwnerEmit{};
+      c->oe.nparts = P;
+      c->oe.rows = c->dist_k2.as<uint32_t>();
+      c->oe.cnt = (uint32_t*)(c->dist_cnt.as<char>() + 1024);
+      c->oe.totals = c->dist_cnt.as<unsigned long long>();
+      c->oe.wide = wide;
+      c->oe.vw = vw;
+      c->oe.mw = mw;
+      c->oe.send = sendc;
+    }
     if (local == GS_OK && degmax) {
       gs_degree_out o{c->dist_k.as<int64_t>(), c->dist_v.as<int64_t>(), c->dist_v2.as<int64_t>(), R, &U, GS_MEM_DEVICE, 0};
       local = gs_window_fold_degree_max(c, b, dir, INT64_MIN, &o);
@@ -484,16 +459,15 @@ static gs_status dist_impl(gs_ctx* c, const gs_edge_batch* b, int32_t dir, int32
       gs_vertex_out o{c->dist_k.as<int64_t>(), c->dist_v.p, R, &U, GS_MEM_DEVICE, 0};
       local = gs_window_reduce(c, b, dir, op, &o);
     }
+    emitted = c->oe.done;
+    c->oe = OwnerEmit{};
   }
   const gs_stage_times keep = c->times;
-  const int vw = (int)(vb / 4), mw = degmax ? 2 : 0;
-  // the packed rows this rank sends (room for 2-word keys; the partition picks the width on the device)
-  if (local == GS_OK) local = ensure(c, c->dist_k2, U * (size_t)(2 + vw + mw) * 4 + 16);
-  if (local == GS_OK) {
+  if (local == GS_OK && !emitted) {
     local = owner_partition_dev(c, c->dist_k.as<int64_t>(), c->dist_v.p, vb, degmax ? c->dist_v2.as<int64_t>() : nullptr, U,
                                 P, nullptr, nullptr, nullptr, wide, c->dist_k2.as<uint32_t>());
   }
-  if (local == GS_OK) {
+  if (local == GS_OK && !emitted) {   // (the owner-grouped emit launched it already)
     hipLaunchKernelGGL(k_send_rows, dim3(1), dim3(64), 0, c->stream, c->dist_cnt.as<unsigned long long>(), wide, P, sendc);
     local = hip_check(c, hipGetLastError(), "k_send_rows");
   }

@@ -587,7 +587,10 @@ static gs_status window_chunked(gs_ctx* c, const gs_edge_batch* b, int32_t dir, 
                                 gs_degree_out* dout, uint64_t ce) {
   struct InChunk {
     gs_ctx* c;
-    explicit InChunk(gs_ctx* x) : c(x) { c->in_chunk = true; }
+    explicit InChunk(gs_ctx* x) : c(x) {
+      c->in_chunk = true;
+      c->oe.nparts = 0;   // the chunks' partials and merges emit ascending rows (gs_window_reduce_dist partitions them)
+    }
     ~InChunk() { c->in_chunk = false; }
   } guard(c);
   const uint64_t per = dir == GS_DIR_ALL ? 2 : 1;
@@ -701,6 +704,7 @@ static gs_status window_fold_impl(gs_ctx* c, const gs_edge_batch* b, int32_t dir
     GS_TRY(bs);
     return finish_vertex_out(c, out, kd, vd, ob, U, direct);
   }
+  c->oe.done = false;   // (an attempt that launched the owner-grouped emit, then gave up) the output is the sort path's
   Sorted s;
   GS_TRY(sort_window(c, src, dst, val, vbytes, b->n, dir, op == GS_OP_COUNT ? PAY_NONE : PAY_VAL, &s, true));
   s.fused = true;
@@ -793,6 +797,7 @@ gs_status gs_window_fold_degree_max(gs_ctx* c, const gs_edge_batch* b, int32_t d
   if (bs != GS_EUNSUPPORTED) {
     GS_TRY(bs);
   } else {
+    c->oe.done = false;   // the output is the sort path's
     Sorted s;
     GS_TRY(sort_window(c, src, dst, nullptr, 0, b->n, dir, PAY_NBR, &s, true));
     s.fused = true;

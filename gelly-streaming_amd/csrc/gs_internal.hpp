@@ -18,6 +18,21 @@ struct DevBuf {
 };
 
 // Result of the window sort: compact keys + payload in key order (stable).
+// gs_window_reduce_dist's local window: with nparts set, the bucket path's last stage writes the
+// exchange's packed rows grouped by owner (k_bk_owner_count / k_owner_scan / k_bk_owner_emit) instead of
+// the ascending (vertex, value) output, and sets `done` (a window that took another path leaves it unset:
+// the caller partitions that output itself)
+struct OwnerEmit {
+  uint32_t nparts = 0;                   // 0: off
+  uint32_t* rows = nullptr;              // packed rows, owner-major
+  uint32_t* cnt = nullptr;               // [nparts][buckets] rows per (owner, bucket) -> write offsets
+  unsigned long long* totals = nullptr;  // [nparts] rows per owner
+  unsigned long long* wide = nullptr;    // key-width flag
+  int vw = 0, mw = 0;                    // value / maximum words per row
+  unsigned long long* send = nullptr;    // [nparts][2] the counts exchange's send rows (k_send_rows)
+  bool done = false;
+};
+
 struct Sorted {
   void* keys = nullptr;     // uint32_t or uint64_t
   void* vals = nullptr;     // payload (nullptr when none)
@@ -119,6 +134,7 @@ struct gs_ctx {
   } sp[2];
   int sp_slot = 0;
   uint64_t tri_merge = 0;   // the last count's sum of d+(u) + d+(v) over its oriented edges (tri_times)
+  gs::OwnerEmit oe;         // gs_window_reduce_dist: the bucket path emits the exchange's rows (gs_dist.hip)
   gs::DevBuf sp_cur;
   // stage-2 candidate count (gs_pairs.hip): staged input columns, packed keys / payloads, group sums
   gs::DevBuf pr_a, pr_b, pr_f, pr_key, pr_val, pr_gk, pr_gv, pr_small;

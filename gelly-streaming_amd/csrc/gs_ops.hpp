@@ -27,6 +27,57 @@ __host__ __device__ inline uint32_t owner_of(int64_t v, uint32_t nparts) {
   return (uint32_t)(((x >> 32) * (uint64_t)nparts) >> 32);
 }
 
+// one block: exclusive scan of cnt[0 .. n) (owner-major) in place; totals[o] = partials of owner o, *n_out
+// (optional) = all of them (gs_dist.hip's owner partition; the bucket path's owner-grouped emit)
+static __global__ __launch_bounds__(1024) void k_owner_scan(uint32_t* __restrict__ cnt, uint32_t n, uint32_t tiles,
+                                                            uint32_t nparts, unsigned long long* __restrict__ totals,
+                                                            unsigned long long* __restrict__ n_out) {
+  __shared__ uint32_t s_w[16];
+  __shared__ uint32_t s_tot;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const uint32_t per = (n + 1023) / 1024, a = min(n, tid * per), b = min(n, a + per);
+  uint32_t sum = 0;
+  for (uint32_t i = a; i < b; ++i) sum += cnt[i];
+  const uint32_t inc = wave_inclusive_sum(sum);
+  if (lane == 63) s_w[w] = inc;
+  __syncthreads();
+  uint32_t off = 0, tot = 0;
+  for (int i = 0; i < 16; ++i) {
+    off += i < w ? s_w[i] : 0u;
+    tot += s_w[i];
+  }
+  uint32_t run = off + inc - sum;
+  for (uint32_t i = a; i < b; ++i) {
+    const uint32_t x = cnt[i];
+    cnt[i] = run;
+    run += x;
+  }
+  if (tid == 0) {
+    s_tot = tot;
+    if (n_out) *n_out = tot;
+  }
+  __syncthreads();
+  if (tid < (int)nparts) {
+    const uint32_t lo = cnt[(uint64_t)tid * tiles], hi = tid + 1 < (int)nparts ? cnt[(uint64_t)(tid + 1) * tiles] : s_tot;
+    totals[tid] = hi - lo;
+  }
+}
+
+// send row per peer p: [rows for p, flags] (flags: 1 = wide keys on this rank, 2 = this rank failed);
+// then the key-width flag is cleared for the next window's k_owner_count (no memset per window; a flag
+// left set by a failed window only widens that next window's keys)
+static __global__ void k_send_rows(const unsigned long long* __restrict__ totals, unsigned long long* __restrict__ wide,
+                            uint32_t nparts, unsigned long long* __restrict__ send) {
+  const uint32_t p = threadIdx.x;
+  const unsigned long long fl = *wide & 1ull;
+  if (p < nparts) {
+    send[2 * p] = totals[p];
+    send[2 * p + 1] = fl;
+  }
+  __syncthreads();
+  if (p == 0) *wide = 0;
+}
+
 // tile shapes (overridable with -D for tuning builds: make VARIANT="-DGS_SORT_ITEMS=24")
 #ifndef GS_SORT_BLOCK
 #define GS_SORT_BLOCK 512
