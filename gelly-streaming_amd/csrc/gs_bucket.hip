@@ -212,7 +212,7 @@ gs_status bucket_accumulate(gs_ctx* c, Src rs, uint64_t R, uint32_t nb, int64_t 
     // the counts exchange's send rows too, before the read-back: after its wait the caller goes straight
     // to the collective
     hipLaunchKernelGGL(k_send_rows, dim3(1), dim3(64), 0, c->stream, (const unsigned long long*)e.totals, e.wide,
-                       e.nparts, e.send);
+                       e.nparts, e.send, mm, (const uint32_t*)(sm + SM_TIMEOUT));
     c->oe.done = true;
   } else {
     hipLaunchKernelGGL((k_bk_emit<P>), dim3(nb), dim3(256), 0, c->stream, meta + BkMeta::BSTART, meta + BkMeta::BCOUNT,
@@ -347,6 +347,22 @@ gs_status bucket_direct_t(gs_ctx* c, const int64_t* src, const int64_t* dst, con
   int64_t kmin = 0, kmax = 0;
   for (int attempt = 0;; ++attempt) {
     if constexpr (SPEC_OK) {
+      // gs_window_reduce_dist's deferred window (OwnerEmit::defer; not the 32-bit-neighbour policies, whose
+      // read-back can still ask for the wide one): the launches return at once, the resumed call skips them
+      const bool defer = !P::REL && c->oe.nparts && c->oe.defer;
+      if (spec && attempt == 0 && defer && c->oe.resume) {
+        c->oe.resume = false;
+        if (!c->host_small[2]) {   // hit
+          kmin = (int64_t)((uint64_t)base + (c->host_small[0] << S));
+          kmax = (int64_t)((uint64_t)base + (c->host_small[1] << S) + ((1ull << S) - 1));
+          part = true;
+          break;
+        }
+        sp.skip = 8;
+        spec = false;
+        spec_missed = true;
+        continue;
+      }
       if (spec && attempt == 0) {
         // regions from the previous window's counts -> the scatter reserves runs with atomics ->
         // items from the cursors (the counts the next window predicts from) -> accumulate
@@ -407,6 +423,7 @@ gs_status bucket_direct_t(gs_ctx* c, const int64_t* src, const int64_t* dst, con
         part = true;
         if (pack) GS_TRY((bucket_accumulate<P>(c, PackSrc<Raw>{c->keysB.as<uint32_t>(), vpart}, cap, nb, base, o, 2, cur)));
         else GS_TRY((bucket_accumulate<P>(c, PartSrc<Raw>{k16, vpart}, cap, nb, base, o, 2, cur)));
+        if (defer) return GS_PENDING_LOCAL;
         GS_TRY(host_wait(c));
         if (!c->host_small[2]) {   // hit: every key in the range; the plan reported the occupied buckets
           kmin = (int64_t)((uint64_t)base + (c->host_small[0] << S));

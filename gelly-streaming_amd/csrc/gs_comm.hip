@@ -321,6 +321,10 @@ gs_status exchange_rows(gs_ctx* c, const char* sendbuf, const uint64_t* send, ch
   if (is_group(c)) return group_exchange(c, sendbuf, send, recvbuf, recv, row, skip_self);
   NcclApi& A = nccl();
   const int P = c->comm_size;
+  bool any = false;   // nothing to or from any peer (e.g. one rank): no group at all
+  for (int p = 0; p < P; ++p)
+    if (!(skip_self && p == c->comm_rank)) any |= send[p] != 0 || recv[p] != 0;
+  if (!any) return GS_OK;
   GS_TRY(nccl_check(c, A.GroupStart(), "ncclGroupStart"));
   uint64_t so = 0, ro = 0;
   for (int p = 0; p < P; ++p) {

@@ -404,6 +404,12 @@ gs_status gs_merge_degree_max_partials(gs_ctx* c, const gs_partial_batch* p, int
   return host_wait(c);
 }
 
+// A/B switch: GS_DIST_NO_DEFER=1 waits for the local window's read-back before the counts exchange
+static bool dist_no_defer() {
+  static const bool v = getenv("GS_DIST_NO_DEFER") && getenv("GS_DIST_NO_DEFER")[0] == '1';
+  return v;
+}
+
 // partials of this rank's slice -> all-to-all over the ctx's communicator -> the merge of what this
 // rank owns.  Per window: the local reduce (the bucket path's own read-back), the owner partition on the
 // device straight into packed rows, ONE all-to-all of [rows, flags] per peer read back together (the only
@@ -433,7 +439,15 @@ static gs_status dist_impl(gs_ctx* c, const gs_edge_batch* b, int32_t dir, int32
   gs_status local = GS_OK;
   std::string local_err;
   const int vw = (int)(vb / 4), mw = degmax ? 2 : 0;
-  bool emitted = false;
+  bool emitted = false, pending = false;
+  auto run_local = [&]() -> gs_status {
+    if (degmax) {
+      gs_degree_out o{c->dist_k.as<int64_t>(), c->dist_v.as<int64_t>(), c->dist_v2.as<int64_t>(), R, &U, GS_MEM_DEVICE, 0};
+      return gs_window_fold_degree_max(c, b, dir, INT64_MIN, &o);
+    }
+    gs_vertex_out o{c->dist_k.as<int64_t>(), c->dist_v.p, R, &U, GS_MEM_DEVICE, 0};
+    return gs_window_reduce(c, b, dir, op, &o);
+  };
   {
     local = ensure(c, c->dist_k, R * 8 + 8);
     if (local == GS_OK) local = ensure(c, c->dist_v, R * 8 + 8);
@@ -451,38 +465,64 @@ static gs_status dist_impl(gs_ctx* c, const gs_edge_batch* b, int32_t dir, int32
       c->oe.vw = vw;
       c->oe.mw = mw;
       c->oe.send = sendc;
-    }
-    if (local == GS_OK && degmax) {
-      gs_degree_out o{c->dist_k.as<int64_t>(), c->dist_v.as<int64_t>(), c->dist_v2.as<int64_t>(), R, &U, GS_MEM_DEVICE, 0};
-      local = gs_window_fold_degree_max(c, b, dir, INT64_MIN, &o);
-    } else if (local == GS_OK) {
-      gs_vertex_out o{c->dist_k.as<int64_t>(), c->dist_v.p, R, &U, GS_MEM_DEVICE, 0};
-      local = gs_window_reduce(c, b, dir, op, &o);
+      // a speculative window's read-back is left to the counts exchange's wait (device columns only: a
+      // resumed call must not stage host columns again); its miss and timeout words ride in the flags
+      c->oe.defer = b->mem == GS_MEM_DEVICE && !dist_no_defer();
+      local = run_local();
+      if (local == GS_PENDING_LOCAL) {
+        pending = true;
+        local = GS_OK;
+      }
     }
     emitted = c->oe.done;
-    c->oe = OwnerEmit{};
+    if (!pending) c->oe = OwnerEmit{};
   }
-  const gs_stage_times keep = c->times;
-  if (local == GS_OK && !emitted) {
-    local = owner_partition_dev(c, c->dist_k.as<int64_t>(), c->dist_v.p, vb, degmax ? c->dist_v2.as<int64_t>() : nullptr, U,
-                                P, nullptr, nullptr, nullptr, wide, c->dist_k2.as<uint32_t>());
-  }
-  if (local == GS_OK && !emitted) {   // (the owner-grouped emit launched it already)
-    hipLaunchKernelGGL(k_send_rows, dim3(1), dim3(64), 0, c->stream, c->dist_cnt.as<unsigned long long>(), wide, P, sendc);
-    local = hip_check(c, hipGetLastError(), "k_send_rows");
-  }
-  if (local != GS_OK) {   // zero rows for everyone, the failure flag set
-    local_err = c->err;
-    for (uint32_t p = 0; p < P; ++p) {
-      c->host_small[8 + 2 * p] = 0;
-      c->host_small[9 + 2 * p] = 2;
+  gs_stage_times keep = c->times;   // the local window's (a deferred one's after its resume, below)
+  // the send rows (owner partition of the ascending output when the window did not emit rows itself), or
+  // zero rows for everyone with the failure flag
+  auto prepare_send = [&]() -> gs_status {
+    if (local == GS_OK && !emitted)
+      local = owner_partition_dev(c, c->dist_k.as<int64_t>(), c->dist_v.p, vb, degmax ? c->dist_v2.as<int64_t>() : nullptr,
+                                  U, P, nullptr, nullptr, nullptr, wide, c->dist_k2.as<uint32_t>());
+    if (local == GS_OK && !emitted) {   // (the owner-grouped emit launched it already)
+      hipLaunchKernelGGL(k_send_rows, dim3(1), dim3(64), 0, c->stream, (const unsigned long long*)c->dist_cnt.as<unsigned long long>(),
+                         wide, P, sendc, (const unsigned long long*)nullptr, (const uint32_t*)nullptr);
+      local = hip_check(c, hipGetLastError(), "k_send_rows");
     }
-    GS_HIP(hipMemcpyAsync(sendc, c->host_small + 8, (size_t)P * 16, hipMemcpyHostToDevice, c->stream));
+    if (local != GS_OK) {
+      local_err = c->err;
+      for (uint32_t p = 0; p < P; ++p) {
+        c->host_small[8 + 2 * p] = 0;
+        c->host_small[9 + 2 * p] = 2;
+      }
+      GS_HIP(hipMemcpyAsync(sendc, c->host_small + 8, (size_t)P * 16, hipMemcpyHostToDevice, c->stream));
+    }
+    return GS_OK;
+  };
+  // the exchange of sizes + flags; read back with this rank's own send counts (with a deferred window, this
+  // wait also brings back its read-back block)
+  auto exchange_counts = [&]() -> gs_status {
+    GS_TRY(comm_alltoall(c, sendc, recvc, 2, NCCL_T_U64));
+    GS_HIP(hipMemcpyAsync(c->host_small + 8, sendc, (size_t)P * 32, hipMemcpyDeviceToHost, c->stream));
+    return host_wait(c);
+  };
+  // 2. the counts exchange
+  GS_TRY(prepare_send());
+  GS_TRY(exchange_counts());
+  if (pending) {   // the deferred window: its checks now (a missed speculation reruns it, which waits inside)
+    c->oe.resume = true;
+    local = run_local();
+    emitted = c->oe.done;
+    c->oe = OwnerEmit{};
+    keep = c->times;
   }
-  // 2. the one exchange of sizes + flags; read back with this rank's own send counts
-  GS_TRY(comm_alltoall(c, sendc, recvc, 2, NCCL_T_U64));
-  GS_HIP(hipMemcpyAsync(c->host_small + 8, sendc, (size_t)P * 32, hipMemcpyDeviceToHost, c->stream));
-  GS_TRY(host_wait(c));
+  bool redo = false;
+  for (uint32_t p = 0; p < P; ++p) redo |= (c->host_small[8 + 2 * P + 2 * p + 1] & 4) != 0;
+  if (redo) {   // some rank's window missed its speculation: every rank sends its counts again
+    const bool mine_missed = (c->host_small[9] & 4) != 0;
+    if (mine_missed || local != GS_OK) GS_TRY(prepare_send());   // (the others' send rows stand)
+    GS_TRY(exchange_counts());
+  }
   const uint32_t me = (uint32_t)c->comm_rank;
   std::vector<uint64_t> send_b(P), recv_b(P);
   RowSegs segs{};
@@ -490,6 +530,7 @@ static gs_status dist_impl(gs_ctx* c, const gs_edge_batch* b, int32_t dir, int32
   int failed = -1;
   uint64_t nrecv = 0, so = 0, ro = 0;
   const uint32_t kw_me = (c->host_small[9] & 1) ? 2u : 1u;   // (every send flag carries this rank's width)
+  if (local != GS_OK && local_err.empty()) local_err = c->err;
   for (uint32_t p = 0; p < P; ++p) {
     const uint64_t fl = c->host_small[8 + 2 * P + 2 * p + 1];
     if ((fl & 2) && failed < 0) failed = (int)p;

@@ -89,7 +89,9 @@ gs_status begin_call(gs_ctx* c) {
   GS_HIP(hipSetDevice(c->device));
   // the look-back timeout word: cleared unless the previous call's read-back saw it zero (the bucket
   // path reads it back with every window, so back-to-back windows skip this launch)
-  if (!c->timeout_clean) GS_HIP(hipMemsetAsync(c->small.as<char>() + SM_TIMEOUT, 0, 8, c->stream));
+  // (a resumed deferred window, gs_dist.hip: its read-back of the word is already on the host and checked
+  // by the resumed call)
+  if (!c->timeout_clean && !c->oe.resume) GS_HIP(hipMemsetAsync(c->small.as<char>() + SM_TIMEOUT, 0, 8, c->stream));
   c->timeout_clean = false;
   return GS_OK;
 }

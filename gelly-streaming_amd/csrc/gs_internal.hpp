@@ -31,7 +31,12 @@ struct OwnerEmit {
   int vw = 0, mw = 0;                    // value / maximum words per row
   unsigned long long* send = nullptr;    // [nparts][2] the counts exchange's send rows (k_send_rows)
   bool done = false;
+  // defer: a speculative window returns GS_PENDING_LOCAL right after its launches (no host wait); the
+  // caller's next wait brings its read-back block, and the same call again with `resume` checks it
+  // (a missed speculation reruns there) and completes the window
+  bool defer = false, resume = false;
 };
+constexpr gs_status GS_PENDING_LOCAL = -101;   // internal (never returned across the ABI)
 
 struct Sorted {
   void* keys = nullptr;     // uint32_t or uint64_t

@@ -66,10 +66,14 @@ static __global__ __launch_bounds__(1024) void k_owner_scan(uint32_t* __restrict
 // send row per peer p: [rows for p, flags] (flags: 1 = wide keys on this rank, 2 = this rank failed);
 // then the key-width flag is cleared for the next window's k_owner_count (no memset per window; a flag
 // left set by a failed window only widens that next window's keys)
+// With `miss` / `timeout` (the owner-grouped emit of a window whose read-back the caller defers): 4 = this
+// rank's speculative partition missed (every rank then sends its counts again after this rank reruns), 2 =
+// its look-back timed out
 static __global__ void k_send_rows(const unsigned long long* __restrict__ totals, unsigned long long* __restrict__ wide,
-                            uint32_t nparts, unsigned long long* __restrict__ send) {
+                            uint32_t nparts, unsigned long long* __restrict__ send,
+                            const unsigned long long* __restrict__ miss, const uint32_t* __restrict__ timeout) {
   const uint32_t p = threadIdx.x;
-  const unsigned long long fl = *wide & 1ull;
+  const unsigned long long fl = (*wide & 1ull) | (miss && miss[2] ? 4ull : 0ull) | (timeout && *timeout ? 2ull : 0ull);
   if (p < nparts) {
     send[2 * p] = totals[p];
     send[2 * p + 1] = fl;

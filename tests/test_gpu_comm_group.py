@@ -158,6 +158,40 @@ def test_reduce_dist_mixed_key_widths(pkg, oracle, window, P):
     check_union([res[r][1] for r in range(P)], oracle.window_fold_degree_max(s, d, 1, -5), P)
 
 
+@pytest.mark.parametrize("P", (2, 3))
+def test_reduce_dist_speculation_miss_on_one_rank(pkg, oracle, window, P):
+    """A rank's speculative window is not waited for before the counts exchange: its miss word rides in
+    the flags, and when one rank missed (its window's records fell into other buckets than its previous
+    window's), every rank sends its counts again after that rank reran.  Three windows per rank: two of the
+    same shape (the second speculates and hits), then the last rank alone gets a window whose records all
+    land in one bucket (its speculation misses, the others' hits)."""
+    s, d = window
+    sl = slices(N, P)
+    v = oracle.gen_values(N, 0x5EED0D, oracle.DT_I64)
+    skew = (s % 97).astype(np.int64)   # every source in the first bucket
+
+    def src_of(r, w):
+        a, b = sl[r]
+        return (skew if (w == 2 and r == P - 1) else s)[a:b]
+
+    def fn(r, e):
+        a, b = sl[r]
+        out, spec = [], []
+        for w in range(3):
+            out.append(e.reduce_dist(src_of(r, w), d[a:b], v[a:b], 1, 0))
+            spec.append(e.stage_times().speculative)
+        return out, spec
+
+    res, errs = run_group(pkg, P, fn)
+    assert not errs, errs
+    for w in range(3):
+        ss = np.concatenate([src_of(r, w) for r in range(P)])
+        check_union([res[r][0][w] for r in range(P)], oracle.window_reduce(ss, d, v, 1, 0), P)
+    for r in range(P):   # window 1 speculates everywhere; window 2 misses (2) on the last rank only
+        assert res[r][1][1] == 1, (r, res[r][1])
+        assert res[r][1][2] == (2 if r == P - 1 else 1), (r, res[r][1])
+
+
 def _tri_windows(oracle):
     s, d = oracle.gen_rmat(SCALE, N, 0x5EED0B, no_self_loops=True)
     ls, ld = oracle.gen_rmat(11, 30_000, 0x5EED0C)           # self-loops kept: the reference's rule

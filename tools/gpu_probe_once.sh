@@ -4,7 +4,7 @@ cd "${GRAFT_REPO_ROOT}"
 O=gpurun_out/$1
 mkdir -p $O
 export TMPDIR=/tmp
-timeout -k 10 600 python3 -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_comm_group.py tests/test_gpu_dist.py -k "reduce or fold or rccl or merges" > $O/tests.txt 2>&1
+timeout -k 10 600 python3 -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_comm_group.py tests/test_gpu_dist.py -k "reduce or fold or rccl or merges or miss" > $O/tests.txt 2>&1
 echo tests done
 export WORLD_SIZE=1 RANK=0 LOCAL_RANK=0 MASTER_ADDR=127.0.0.1 MASTER_PORT=29555
 for rep in 1 2; do
