@@ -79,6 +79,10 @@ def parse():
                    help="after timing: sum(per-vertex sums) == sum(values) and ascending keys on each window")
     p.add_argument("--chunk-records", type=float, default=2 ** 28,
                    help="cand_stream: records per gs_candidates_next chunk")
+    p.add_argument("--cand-overlap", action="store_true",
+                   help="cand_stream: run the consumer on a second stream, overlapping the next chunk's emission "
+                        "(default: on the emission stream right after its chunk -- the mixed read/write traffic of "
+                        "the overlap ran slower than the two in turn)")
     p.add_argument("--cand-consumer", default="sum", choices=["sum", "none"],
                    help="cand_stream: a device consumer reads every record (column sums), or none (emission alone)")
     p.add_argument("--cand-windows", type=int, default=2,
@@ -453,9 +457,9 @@ def cand_stream_main(a):
     gs_candidates_begin / gs_candidates_next (a window has ~1.6e11 records, 2.7 TB, which no single buffer
     holds).  Each chunk is consumed on the device by the stand-in of a downstream operator: per-chunk sums
     of the a, b and is_candidate columns (three reductions, no temporaries), so every record is read once
-    after it is written.  The emission runs on the engine's stream into one of two chunk buffers while the
-    consumer reads the other on a second stream (events order them; no host round trip per chunk:
-    gs_candidates_next only enqueues device output).  --cand-windows W > 1 streams W consecutive windows of
+    after it is written.  By default the consumer runs on the emission stream right after its chunk
+    (--cand-overlap: on a second stream while the next chunk is emitted into the other of two buffers;
+    no host round trip per chunk either way: gs_candidates_next only enqueues device output).  --cand-windows W > 1 streams W consecutive windows of
     the stream through two engines (sessions), the next window's gs_candidates_begin overlapping the
     current window's emission: the sustained window period.  Reports records/s, the window period, chunk
     latency p50 / p99 (device events, emission start to consumer end) and checks that the chunks add up to
@@ -512,13 +516,15 @@ def cand_stream_main(a):
                 with torch.cuda.stream(est):
                     ev1.record(est)
             else:
-                with torch.cuda.stream(cons):
-                    cons.wait_event(emitted)
+                cst = cons if a.cand_overlap else est   # the consumer's stream
+                with torch.cuda.stream(cst):
+                    if a.cand_overlap:
+                        cons.wait_event(emitted)
                     n8 = (n // 8) * 8
                     sums.append(torch.stack([ca.sum(), cb.sum(), cf[:n8].view(torch.int64).sum() + cf[n8:].sum()]))
                     ev1 = torch.cuda.Event(enable_timing=True)
-                    ev1.record(cons)
-                    freed[k] = ev1
+                    ev1.record(cst)
+                    freed[k] = ev1 if a.cand_overlap else None
             ev_pairs.append((ev0, ev1))
             got += n
             nchunk += 1
@@ -546,7 +552,10 @@ def cand_stream_main(a):
             "data": "synthetic R-MAT scale 23, seeded, generated on device",
             "config": {"workload": f"C5 emission: every GenerateCandidateEdges record of {W} consecutive "
                                    f"{E:.3g}-edge R-MAT scale-23 windows (slice(ALL)), in chunks of {cap} records, "
-                                   f"each consumed on the device (column sums) while the next is emitted",
+                                   + ("each consumed on the device (column sums) while the next is emitted"
+                                      if a.cand_overlap else
+                                      "each consumed on the device (column sums) right after it is emitted, on the "
+                                      "same stream (the next window's sets built on a second stream meanwhile)"),
                        "edges_per_window": E, "windows": W, "records": total, "candidate_records": cands,
                        "chunks": nchunk, "chunk_records": cap, "begin_ms": begin_ms,
                        "chunk_latency_ms_p50": float(np.percentile(lat_ms, 50)),
