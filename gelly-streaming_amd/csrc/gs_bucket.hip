@@ -189,10 +189,12 @@ gs_status bucket_accumulate(gs_ctx* c, Src rs, uint64_t R, uint32_t nb, int64_t 
                   meta + BkMeta::BCOUNT, mm, seg_cur);
   GS_HIP(hipGetLastError());
   stage_event(c, c->pass_ev[ev0 + 1]);
-  const unsigned mgrid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(nb, R / BK_ITEM + 1));
+  // blocks loop over the multi-item buckets (their number stays on the device)
+  const unsigned mgrid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>({(uint64_t)nb, R / BK_ITEM + 1, 64}));
+  const unsigned fgrid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>({(uint64_t)nb, R / BK_ITEM + 1, (uint64_t)c->n_cu}));
   hipLaunchKernelGGL((k_bk_merge_slices<P>), dim3(mgrid, BK_MS_SLICES), dim3(BK_MS_BLOCK), 0, c->stream,
                      meta + BkMeta::MLIST, ns + 1, meta + BkMeta::BITEMS, meta + BkMeta::BSLAB, slabs, mm);
-  hipLaunchKernelGGL((k_bk_merge<P>), dim3(mgrid), dim3(BK_ACC_BLOCK), 0, c->stream, meta + BkMeta::MLIST, ns + 1,
+  hipLaunchKernelGGL((k_bk_merge<P>), dim3(fgrid), dim3(BK_ACC_BLOCK), 0, c->stream, meta + BkMeta::MLIST, ns + 1,
                      meta + BkMeta::BITEMS, meta + BkMeta::BSLAB, meta + BkMeta::BSTART, slabs, st,
                      meta + BkMeta::BCOUNT, mm);
   GS_HIP(hipGetLastError());

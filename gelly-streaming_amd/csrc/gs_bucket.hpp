@@ -1924,23 +1924,28 @@ __global__ __launch_bounds__(BK_MS_BLOCK) void k_bk_merge_slices(const uint32_t*
                                                                  const uint32_t* __restrict__ b_slab,
                                                                  typename P::Lds* __restrict__ slabs,
                                                                  const unsigned long long* __restrict__ mm) {
-  if (mm[2] || blockIdx.x >= *n_multi_p) return;
-  const uint32_t b = mlist[blockIdx.x];
-  const uint32_t n = b_items[b], f = b_slab[b];
-  // d and the other slabs never overlap (restrict): d's elements stay in registers across the slabs and
-  // the slab loads of an unrolled group issue together (a dependent read-modify-write of d per slab made
-  // the merge latency-bound: Zipf hub buckets of ~100 slabs, C3 0.78 ms)
-  typename P::Lds* __restrict__ d = slabs + f;
-  const typename P::Lds* __restrict__ rest = slabs + f + 1;
-  constexpr uint32_t EL = P::W / BK_MS_SLICES, PWS = (P::PWORDS + BK_MS_SLICES - 1) / BK_MS_SLICES;
-  const uint32_t e0 = blockIdx.y * EL, w0 = blockIdx.y * PWS;
-  for (uint32_t i = threadIdx.x; i < EL; i += BK_MS_BLOCK) {
+  if (mm[2]) return;
+  const uint32_t n_multi = *n_multi_p;
+  // blocks loop over the multi-item buckets (the grid is sized without a read-back of their number: one
+  // block per possible bucket and slice left ~65 K blocks exiting at once for C2's ~30, 16 us of dispatch)
+  for (uint32_t mb = blockIdx.x; mb < n_multi; mb += gridDim.x) {
+    const uint32_t b = mlist[mb];
+    const uint32_t n = b_items[b], f = b_slab[b];
+    // d and the other slabs never overlap (restrict): d's elements stay in registers across the slabs and
+    // the slab loads of an unrolled group issue together (a dependent read-modify-write of d per slab made
+    // the merge latency-bound: Zipf hub buckets of ~100 slabs, C3 0.78 ms)
+    typename P::Lds* __restrict__ d = slabs + f;
+    const typename P::Lds* __restrict__ rest = slabs + f + 1;
+    constexpr uint32_t EL = P::W / BK_MS_SLICES, PWS = (P::PWORDS + BK_MS_SLICES - 1) / BK_MS_SLICES;
+    const uint32_t e0 = blockIdx.y * EL, w0 = blockIdx.y * PWS;
+    for (uint32_t i = threadIdx.x; i < EL; i += BK_MS_BLOCK) {
 #pragma unroll 8
-    for (uint32_t k = 0; k + 1 < n; ++k) P::merge_el(d, rest + k, e0 + i);
-  }
-  for (uint32_t w = threadIdx.x; w < PWS && w0 + w < P::PWORDS; w += BK_MS_BLOCK) {
+      for (uint32_t k = 0; k + 1 < n; ++k) P::merge_el(d, rest + k, e0 + i);
+    }
+    for (uint32_t w = threadIdx.x; w < PWS && w0 + w < P::PWORDS; w += BK_MS_BLOCK) {
 #pragma unroll 8
-    for (uint32_t k = 0; k + 1 < n; ++k) P::merge_pw(d, rest + k, w0 + w);
+      for (uint32_t k = 0; k + 1 < n; ++k) P::merge_pw(d, rest + k, w0 + w);
+    }
   }
 }
 
@@ -1957,17 +1962,20 @@ __global__ __launch_bounds__(BK_ACC_BLOCK) void k_bk_merge(const uint32_t* __res
   __shared__ typename P::Lds s;
   __shared__ uint32_t s_wc[BK_NW];
   const int tid = threadIdx.x;
-  if (mm[2] || blockIdx.x >= *n_multi_p) return;
-  const uint32_t b = mlist[blockIdx.x];
-  const uint32_t n = b_items[b], f = b_slab[b];
-  (void)n;
-  {
-    const uint4* gs = reinterpret_cast<const uint4*>(slabs + f);
-    uint4* ls = reinterpret_cast<uint4*>(&s);
-    for (uint32_t i = tid; i < sizeof(typename P::Lds) / 16; i += BK_ACC_BLOCK) ls[i] = gs[i];
+  if (mm[2]) return;
+  const uint32_t n_multi = *n_multi_p;
+  for (uint32_t mb = blockIdx.x; mb < n_multi; mb += gridDim.x) {   // (grid: see k_bk_merge_slices)
+    const uint32_t b = mlist[mb];
+    const uint32_t f = b_slab[b];
+    {
+      const uint4* gs = reinterpret_cast<const uint4*>(slabs + f);
+      uint4* ls = reinterpret_cast<uint4*>(&s);
+      for (uint32_t i = tid; i < sizeof(typename P::Lds) / 16; i += BK_ACC_BLOCK) ls[i] = gs[i];
+    }
+    __syncthreads();
+    bk_finalize<P>(s, b, bucket_start[b], st, bucket_count, s_wc);
+    __syncthreads();   // (the next bucket's slab overwrites s)
   }
-  __syncthreads();
-  bk_finalize<P>(s, b, bucket_start[b], st, bucket_count, s_wc);
 }
 
 // ---- k_bk_emit: staging -> outputs, vertices ascending --------------------------------------------
