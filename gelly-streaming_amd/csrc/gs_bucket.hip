@@ -34,7 +34,8 @@ constexpr gs_status GS_RETRY_WIDE = -100;
 struct BkMeta {   // offsets (u32 units) inside ctx->bk_meta
   static constexpr size_t HIST = 0, DBASE = HIST + BK_MAXB, BSTART = DBASE + 512, BCOUNT = BSTART + BK_MAXB + 4,
                           BITEMS = BCOUNT + BK_MAXB, BSLAB = BITEMS + BK_MAXB, MLIST = BSLAB + BK_MAXB,
-                          TOTAL = MLIST + BK_MAXB;
+                          MAXIT = MLIST + BK_MAXB,   // the most items of one bucket (k_bk_merge_groups)
+                          TOTAL = MAXIT + 4;
 };
 
 struct BkGeom {
@@ -159,7 +160,7 @@ gs_status launch_plan(gs_ctx* c, uint64_t R, uint32_t nb, int passes, int w, uin
   uint32_t* ns = (uint32_t*)(sm + SM_BK_N);
   BkPlanOut po{meta + BkMeta::DBASE, meta + BkMeta::BSTART, meta + BkMeta::BCOUNT, meta + BkMeta::BITEMS,
                meta + BkMeta::BSLAB, meta + BkMeta::MLIST, c->bk_items.as<BkItem>(), ns + 0, ns + 1,
-               cursor, counts_out, occupied, ns + 2};
+               cursor, counts_out, occupied, ns + 2, meta + BkMeta::MAXIT};
   hipLaunchKernelGGL(k_bk_plan, dim3(1), dim3(BK_PLAN_BLOCK), 0, c->stream, meta + BkMeta::HIST, nb, passes, w,
                      item_recs, po);
   return hip_check(c, hipGetLastError(), "k_bk_plan");
@@ -192,6 +193,8 @@ gs_status bucket_accumulate(gs_ctx* c, Src rs, uint64_t R, uint32_t nb, int64_t 
   // blocks loop over the multi-item buckets (their number stays on the device)
   const unsigned mgrid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>({(uint64_t)nb, R / BK_ITEM + 1, 64}));
   const unsigned fgrid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>({(uint64_t)nb, R / BK_ITEM + 1, (uint64_t)c->n_cu}));
+  hipLaunchKernelGGL((k_bk_merge_groups<P>), dim3(2048), dim3(BK_MS_BLOCK), 0, c->stream, meta + BkMeta::MLIST, ns + 1,
+                     meta + BkMeta::BITEMS, meta + BkMeta::BSLAB, slabs, mm, (const uint32_t*)(meta + BkMeta::MAXIT));
   hipLaunchKernelGGL((k_bk_merge_slices<P>), dim3(mgrid, BK_MS_SLICES), dim3(BK_MS_BLOCK), 0, c->stream,
                      meta + BkMeta::MLIST, ns + 1, meta + BkMeta::BITEMS, meta + BkMeta::BSLAB, slabs, mm);
   hipLaunchKernelGGL((k_bk_merge<P>), dim3(fgrid), dim3(BK_ACC_BLOCK), 0, c->stream, meta + BkMeta::MLIST, ns + 1,

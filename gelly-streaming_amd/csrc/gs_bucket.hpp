@@ -73,6 +73,7 @@ struct BkPlanOut {
   uint32_t* counts_out = nullptr;
   unsigned long long* occupied = nullptr;   // speculative: [0] lowest, [1] highest bucket with records
   uint32_t* claim = nullptr;                // k_bk_accum's item counter, zeroed here
+  uint32_t* max_items = nullptr;            // the most items of one bucket (k_bk_merge_groups skips when <= 16)
 };
 
 // speculative partition: a bucket's region is split into SP_NSEG segments, one per XCD slot, each with
@@ -553,8 +554,10 @@ static __global__ __launch_bounds__(BK_PLAN_BLOCK) void k_bk_plan(const uint32_t
                                                                   BkPlanOut o) {
   __shared__ uint32_t s_dh[2][256];
   __shared__ uint32_t s_w[BK_PLAN_BLOCK / WAVE];
+  __shared__ uint32_t s_maxit;
   const int tid = threadIdx.x;
   for (int i = tid; i < 2 * 256; i += BK_PLAN_BLOCK) (&s_dh[0][0])[i] = 0;
+  if (tid == 0) s_maxit = 0;
   if (tid == 0 && o.claim) *o.claim = 0;
   __syncthreads();
   // two buckets per thread (BK_MAXB = 2 * BK_PLAN_BLOCK)
@@ -670,7 +673,12 @@ static __global__ __launch_bounds__(BK_PLAN_BLOCK) void k_bk_plan(const uint32_t
   };
   emit_bucket(b0, c0, i0, first0, slab0, mb0);
   emit_bucket(b1, c1, i1, first0 + i0, slab0 + m0, mb0 + (m0 ? 1u : 0u));
+  if (o.max_items) {   // (s_maxit complete after the item scans' barriers)
+    if (i0 > 1 || i1 > 1) atomicMax(&s_maxit, max(i0, i1));
+    __syncthreads();
+  }
   if (tid == 0) {
+    if (o.max_items) *o.max_items = s_maxit;
     *o.n_items = n_items;
     *o.n_multi = n_multi;
   }
@@ -1915,8 +1923,44 @@ __global__ __launch_bounds__(BK_ACC_BLOCK) void k_bk_accum(Src src, const BkItem
 
 // Slabs of a multi-item bucket merged into its first slab, BK_MS_SLICES blocks per bucket, each over
 // one slice of the vertex range (a hub bucket can leave hundreds of slabs: one block per bucket
-// merged them serially).  Fixed element -> thread map: deterministic merge order.
-constexpr uint32_t BK_MS_SLICES = 64, BK_MS_BLOCK = 256;
+// merged them serially).  Fixed element -> thread map: deterministic merge order.  Two levels: slab k
+// of a bucket with more than BK_MS_GROUPS slabs is first merged into slab k mod BK_MS_GROUPS
+// (k_bk_merge_groups: a Zipf hub bucket's ~700 slabs as 16 chains of ~44 instead of one of 700, which
+// ran the C3 Zipf merge at 0.19 ms), then slabs 1 .. 15 into slab 0 (k_bk_merge_slices).
+constexpr uint32_t BK_MS_SLICES = 64, BK_MS_BLOCK = 256, BK_MS_GROUPS = 16;
+
+// level 1: work unit (multi bucket, slice, group z): slabs z + 16, z + 32, ... into slab z
+template <class P>
+__global__ __launch_bounds__(BK_MS_BLOCK) void k_bk_merge_groups(const uint32_t* __restrict__ mlist,
+                                                                 const uint32_t* __restrict__ n_multi_p,
+                                                                 const uint32_t* __restrict__ b_items,
+                                                                 const uint32_t* __restrict__ b_slab,
+                                                                 typename P::Lds* __restrict__ slabs,
+                                                                 const unsigned long long* __restrict__ mm,
+                                                                 const uint32_t* __restrict__ max_items) {
+  if (mm[2] || *max_items <= BK_MS_GROUPS) return;   // (every bucket's slabs fit level 2: C2's 2-3)
+  const uint32_t units = *n_multi_p * BK_MS_SLICES * BK_MS_GROUPS;
+  constexpr uint32_t EL = P::W / BK_MS_SLICES, PWS = (P::PWORDS + BK_MS_SLICES - 1) / BK_MS_SLICES;
+  for (uint32_t u = blockIdx.x; u < units; u += gridDim.x) {
+    const uint32_t mb = u / (BK_MS_SLICES * BK_MS_GROUPS), rem = u % (BK_MS_SLICES * BK_MS_GROUPS);
+    const uint32_t sl = rem / BK_MS_GROUPS, z = rem % BK_MS_GROUPS;
+    const uint32_t b = mlist[mb];
+    const uint32_t n = b_items[b], f = b_slab[b];
+    if (z + BK_MS_GROUPS >= n) continue;   // (block-uniform)
+    typename P::Lds* __restrict__ d = slabs + f + z;
+    const typename P::Lds* __restrict__ rest = slabs + f + z + BK_MS_GROUPS;   // slab z + 16 (k + 1)
+    const uint32_t nk = (n - z - 1) / BK_MS_GROUPS;                            // slabs in this chain
+    const uint32_t e0 = sl * EL, w0 = sl * PWS;
+    for (uint32_t i = threadIdx.x; i < EL; i += BK_MS_BLOCK) {
+#pragma unroll 8
+      for (uint32_t k = 0; k < nk; ++k) P::merge_el(d, rest + (size_t)k * BK_MS_GROUPS, e0 + i);
+    }
+    for (uint32_t w = threadIdx.x; w < PWS && w0 + w < P::PWORDS; w += BK_MS_BLOCK) {
+#pragma unroll 8
+      for (uint32_t k = 0; k < nk; ++k) P::merge_pw(d, rest + (size_t)k * BK_MS_GROUPS, w0 + w);
+    }
+  }
+}
 template <class P>
 __global__ __launch_bounds__(BK_MS_BLOCK) void k_bk_merge_slices(const uint32_t* __restrict__ mlist,
                                                                  const uint32_t* __restrict__ n_multi_p,
@@ -1936,15 +1980,16 @@ __global__ __launch_bounds__(BK_MS_BLOCK) void k_bk_merge_slices(const uint32_t*
     // the merge latency-bound: Zipf hub buckets of ~100 slabs, C3 0.78 ms)
     typename P::Lds* __restrict__ d = slabs + f;
     const typename P::Lds* __restrict__ rest = slabs + f + 1;
+    const uint32_t nk = min(n, BK_MS_GROUPS) - 1;   // the group heads 1 .. 15 (k_bk_merge_groups)
     constexpr uint32_t EL = P::W / BK_MS_SLICES, PWS = (P::PWORDS + BK_MS_SLICES - 1) / BK_MS_SLICES;
     const uint32_t e0 = blockIdx.y * EL, w0 = blockIdx.y * PWS;
     for (uint32_t i = threadIdx.x; i < EL; i += BK_MS_BLOCK) {
 #pragma unroll 8
-      for (uint32_t k = 0; k + 1 < n; ++k) P::merge_el(d, rest + k, e0 + i);
+      for (uint32_t k = 0; k < nk; ++k) P::merge_el(d, rest + k, e0 + i);
     }
     for (uint32_t w = threadIdx.x; w < PWS && w0 + w < P::PWORDS; w += BK_MS_BLOCK) {
 #pragma unroll 8
-      for (uint32_t k = 0; k + 1 < n; ++k) P::merge_pw(d, rest + k, w0 + w);
+      for (uint32_t k = 0; k < nk; ++k) P::merge_pw(d, rest + k, w0 + w);
     }
   }
 }
