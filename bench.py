@@ -42,6 +42,8 @@ def parse():
     p.add_argument("--seed", type=lambda x: int(x, 0), default=0x5EED02)
     p.add_argument("--dtype", default="int64", choices=["int64", "float64"])
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--alloc-outputs", action="store_true",
+                   help="reduce / fold: allocate the output tensors per window (A/B; default: reused across windows, as a streaming operator keeps its buffers)")
     p.add_argument("--cpu-sample-log2", type=int, default=30,
                    help="triangles: the CPU baseline counts windows up to 2^this many edges (larger windows: their "
                         "first 2^this); 30 = the whole C4 (s26) window (~65 s of 16-thread CPU)")
@@ -828,14 +830,27 @@ def main():
 
     local_times = []
 
+    red_out = None   # the output buffers a streaming operator keeps across windows
+
     def local_reduce(s_, d_, v_, direction, op):
-        r = eng.reduce(s_, d_, v_, direction, op)
+        nonlocal red_out
+        R = s_.numel() * (2 if direction == 2 else 1)
+        if red_out is None or red_out[0].numel() < R:
+            red_out = (torch.empty(R, dtype=torch.int64, device=s_.device),
+                       torch.empty(R, dtype=v_.dtype if v_ is not None else torch.int64, device=s_.device))
+        r = eng.reduce(s_, d_, v_, direction, op, out=None if a.alloc_outputs else red_out)
         if not local_times:
             local_times.append(eng.stage_times())   # the window's own pipeline, not the merge
         return r
 
+    fold_out = None
+
     def local_fold(s_, d_, direction, init_max):
-        r = eng.fold_degree_max(s_, d_, direction, init_max)
+        nonlocal fold_out
+        R = s_.numel() * (2 if direction == 2 else 1)
+        if fold_out is None or fold_out[0].numel() < R:
+            fold_out = tuple(torch.empty(R, dtype=torch.int64, device=s_.device) for _ in range(3))
+        r = eng.fold_degree_max(s_, d_, direction, init_max, out=None if a.alloc_outputs else fold_out)
         if not local_times:
             local_times.append(eng.stage_times())
         return r

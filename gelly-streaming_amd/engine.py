@@ -194,20 +194,27 @@ class Engine:
         return 2 * n if int(direction) == 2 else n
 
     # -- operators ------------------------------------------------------------------------------
-    def reduce(self, src, dst, val, direction, op):
-        """gs_window_reduce: reduceOnEdges with a built-in op. Returns (keys, values) trimmed to U."""
-        return self._fold(src, dst, val, direction, op, None)
+    def reduce(self, src, dst, val, direction, op, out=None):
+        """gs_window_reduce: reduceOnEdges with a built-in op. Returns (keys, values) trimmed to U.
+        out: optional (keys, values) device tensors of at least the window's record count, reused across
+        windows (a streaming operator's output buffers) instead of allocating per call."""
+        return self._fold(src, dst, val, direction, op, None, out)
 
     def fold(self, src, dst, val, direction, op, init):
         """gs_window_fold: foldNeighbors(init, op). Returns (keys, values)."""
         return self._fold(src, dst, val, direction, op, init)
 
-    def _fold(self, src, dst, val, direction, op, init):
+    def _fold(self, src, dst, val, direction, op, init, out=None):
         b, keep, dev = self._batch(src, dst, None if op == L.GS_OP_COUNT else val)
         R = self._records(b.n, direction)
         odt = np.int64 if op == L.GS_OP_COUNT else L.NP_DTYPE[b.val_dtype]
-        keys = self._empty(dev, R, np.int64)
-        vals = self._empty(dev, R, odt)
+        if out is not None:
+            keys, vals = out
+            if not (dev and _is_torch(keys) and keys.is_cuda and keys.numel() >= R and vals.numel() >= R):
+                raise ValueError("out: device tensors of at least the window's records")
+        else:
+            keys = self._empty(dev, R, np.int64)
+            vals = self._empty(dev, R, odt)
         n_out = ctypes.c_uint64(0)
         out = L.GsVertexOut(_ptr(keys), _ptr(vals), R, ctypes.pointer(n_out),
                             L.GS_MEM_DEVICE if dev else L.GS_MEM_HOST, 0)
@@ -221,10 +228,17 @@ class Engine:
         U = n_out.value
         return keys[:U], vals[:U]
 
-    def fold_degree_max(self, src, dst, direction, init_max: int = -(1 << 63)):
+    def fold_degree_max(self, src, dst, direction, init_max: int = -(1 << 63), out=None):
+        """gs_window_fold_degree_max: (keys, degrees, max neighbours).  out: optional (keys, degrees, maxima)
+        device tensors of at least the window's records, reused across windows."""
         b, keep, dev = self._batch(src, dst, None)
         R = self._records(b.n, direction)
-        keys, deg, mx = (self._empty(dev, R, np.int64) for _ in range(3))
+        if out is not None:
+            keys, deg, mx = out
+            if not (dev and _is_torch(keys) and keys.is_cuda and min(x.numel() for x in out) >= R):
+                raise ValueError("out: device tensors of at least the window's records")
+        else:
+            keys, deg, mx = (self._empty(dev, R, np.int64) for _ in range(3))
         n_out = ctypes.c_uint64(0)
         out = L.GsDegreeOut(_ptr(keys), _ptr(deg), _ptr(mx), R, ctypes.pointer(n_out),
                             L.GS_MEM_DEVICE if dev else L.GS_MEM_HOST, 0)
