@@ -874,6 +874,8 @@ def main():
         local_times.append(eng.stage_times())
         return r
 
+    dist_out = None
+
     def step(i):
         src, dst, val = wins[i % len(wins)]
         local_times.clear()
@@ -900,7 +902,11 @@ def main():
                     else local_fold(src, dst, 1, -(1 << 63))
             return r[0], r[1], local_times[0]
         if abi:       # gs_window_reduce_dist
-            r = eng.reduce_dist(src, dst, val, 1, 0)
+            nonlocal dist_out
+            if dist_out is None and not a.alloc_outputs:   # (kept across windows; 2x the slice's records)
+                dist_out = (torch.empty(2 * src.numel() + 1024, dtype=torch.int64, device=src.device),
+                            torch.empty(2 * src.numel() + 1024, dtype=val.dtype, device=src.device))
+            r = eng.reduce_dist(src, dst, val, 1, 0, out=dist_out)
             local_times.append(eng.stage_times())
         else:
             r = D.reduce_window(partials_timed, M_red, src, dst, val, 1, 0) if dist else local_reduce(src, dst, val, 1, 0)

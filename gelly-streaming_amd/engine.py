@@ -644,13 +644,20 @@ class Engine:
         self._check(self._L.gs_comm_allreduce_sum_u64(self.ctx, ctypes.byref(v)))
         return v.value
 
-    def reduce_dist(self, src, dst, val, direction, op, init=None):
+    def reduce_dist(self, src, dst, val, direction, op, init=None, out=None):
         """gs_window_reduce_dist: this rank's slice through partials -> RCCL all-to-all -> merge; returns
-        the (keys, values) this rank owns."""
+        the (keys, values) this rank owns.  out: optional (keys, values) device tensors reused across
+        windows (their length is the capacity)."""
         b, keep, dev = self._batch(src, dst, None if op == L.GS_OP_COUNT else val)
         odt = np.int64 if op == L.GS_OP_COUNT else L.NP_DTYPE[b.val_dtype]
-        cap = self._records(b.n, direction) + 1024   # a guess; more owned vertices: gs_fetch_last_output
-        keys, vals = self._empty(dev, cap, np.int64), self._empty(dev, cap, odt)
+        if out is not None:
+            keys, vals = out
+            if not (dev and _is_torch(keys) and keys.is_cuda):
+                raise ValueError("out: device tensors")
+            cap = min(keys.numel(), vals.numel())
+        else:
+            cap = self._records(b.n, direction) + 1024   # a guess; more owned vertices: gs_fetch_last_output
+            keys, vals = self._empty(dev, cap, np.int64), self._empty(dev, cap, odt)
         n_out = ctypes.c_uint64(0)
         out = L.GsVertexOut(_ptr(keys), _ptr(vals), cap, ctypes.pointer(n_out), L.GS_MEM_DEVICE if dev else L.GS_MEM_HOST, 0)
         ia = None if init is None else np.array([init], dtype=odt)
