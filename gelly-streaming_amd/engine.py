@@ -652,8 +652,8 @@ class Engine:
         odt = np.int64 if op == L.GS_OP_COUNT else L.NP_DTYPE[b.val_dtype]
         if out is not None:
             keys, vals = out
-            if not (dev and _is_torch(keys) and keys.is_cuda):
-                raise ValueError("out: device tensors")
+            if not (dev and _is_torch(keys) and keys.is_cuda and _is_torch(vals) and vals.is_cuda):
+                raise ValueError("out: device tensors, with device inputs")
             cap = min(keys.numel(), vals.numel())
         else:
             cap = self._records(b.n, direction) + 1024   # a guess; more owned vertices: gs_fetch_last_output

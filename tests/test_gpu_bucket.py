@@ -469,3 +469,27 @@ def test_float_sum_presence_with_signed_zeros(engine, oracle, dtype):
     exact = np.bincount(idx, weights=v.astype(np.float64), minlength=len(rk))
     mag = np.bincount(idx, weights=np.abs(v.astype(np.float64)), minlength=len(rk))
     assert not (np.abs(gv.astype(np.float64) - exact) > 1e-6 * mag + 1e-300).any()
+
+
+def test_reused_output_buffers(engine, oracle):
+    """reduce / fold_degree_max with out=: one set of output tensors reused over windows of different sizes
+    and shapes (a streaming operator's buffers, as bench.py's C2 line holds them) gives the same rows as
+    fresh outputs; a buffer shorter than the window's records is refused before any launch."""
+    rng = np.random.default_rng(0x0B0F)
+    cap = 2 * 90000
+    kv = (torch.empty(cap, dtype=torch.int64, device="cuda"), torch.empty(cap, dtype=torch.int64, device="cuda"))
+    kdm = tuple(torch.empty(cap, dtype=torch.int64, device="cuda") for _ in range(3))
+    for n, span in ((90000, 1 << 19), (20000, 1 << 13), (60000, 1 << 24)):
+        s, d = _window(rng, n, span)
+        v = oracle.gen_values(n, 0x0B1, oracle.DT_I64)
+        gk, gv = engine.reduce(*_dev(s, d, v), 2, 0, out=kv)
+        assert gk.data_ptr() == kv[0].data_ptr()
+        _check(gk, gv, *oracle.window_reduce(s, d, v, 2, 0), np.int64, 0)
+        gk, gdeg, gmx = engine.fold_degree_max(*_dev(s, d), 1, -5, out=kdm)
+        wk, wdeg, wmx = oracle.window_fold_degree_max(s, d, 1, -5)
+        assert np.array_equal(gk.cpu().numpy(), wk)
+        assert np.array_equal(gdeg.cpu().numpy(), wdeg) and np.array_equal(gmx.cpu().numpy(), wmx)
+    s, d = _window(rng, 1000, 1 << 13)
+    short = (kv[0][:1999], kv[1][:1999])
+    with pytest.raises(ValueError):
+        engine.reduce(*_dev(s, d, s), 2, 0, out=short)

@@ -21,6 +21,7 @@ import threading
 
 import numpy as np
 import pytest
+import torch
 
 pytestmark = pytest.mark.gpu
 
@@ -291,3 +292,32 @@ def test_split_window_s20_four_ranks(pkg, oracle):
     w, ex, has = oracle.window_triangles_fwd(s, d)
     for r in range(P):
         assert res[r][2] == (ex, w, has), (r, res[r][2], ex)
+
+
+@pytest.mark.parametrize("P", (2,))
+def test_reduce_dist_reused_outputs(pkg, oracle, window, P):
+    """reduce_dist with out=: each rank keeps one (keys, values) pair over three windows (the second
+    speculates); the owned rows land in the same tensors and match the oracle's union every window."""
+    s, d = window
+    sl = slices(N, P)
+    v = oracle.gen_values(N, 0x5EED0E, oracle.DT_I64)
+
+    def fn(r, e):
+        a, b = sl[r]
+        cap = 2 * (b - a) + 1024
+        buf = (torch.empty(cap, dtype=torch.int64, device="cuda"), torch.empty(cap, dtype=torch.int64, device="cuda"))
+        ds, dd, dv = (torch.from_numpy(np.ascontiguousarray(x[a:b])).cuda() for x in (s, d, v))
+        out = []
+        for w in range(3):
+            k, val = e.reduce_dist(ds, dd, dv, 2, 0, out=buf)
+            assert k.data_ptr() == buf[0].data_ptr()
+            out.append((k.cpu().numpy(), val.cpu().numpy()))
+        with pytest.raises(ValueError):   # device outputs for host inputs: refused
+            e.reduce_dist(s[a:b], d[a:b], v[a:b], 2, 0, out=buf)
+        return out
+
+    res, errs = run_group(pkg, P, fn)
+    assert not errs, errs
+    want = oracle.window_reduce(s, d, v, 2, 0)
+    for w in range(3):
+        check_union([res[r][w] for r in range(P)], want, P)
