@@ -87,6 +87,9 @@ def parse():
                         "the overlap ran slower than the two in turn)")
     p.add_argument("--cand-consumer", default="sum", choices=["sum", "none"],
                    help="cand_stream: a device consumer reads every record (column sums), or none (emission alone)")
+    p.add_argument("--cand-ids", default="i64", choices=["i64", "u32"],
+                   help="cand_stream: id columns as int64 (gs_candidates_next: 17-byte records) or as uint32 relative "
+                        "to the window's smallest id (gs_candidates_next_u32: 9-byte records, the same records)")
     p.add_argument("--cand-windows", type=int, default=2,
                    help="cand_stream: consecutive windows streamed (the next window's sets built while the current "
                         "one's chunks drain)")
@@ -481,7 +484,10 @@ def cand_stream_main(a):
         with torch.cuda.stream(emit_streams[w % len(engines)]):
             wins.append(engines[w % len(engines)].generate_rmat(23, E, 0x5EED05, first_edge=w * E))
     torch.cuda.synchronize()
-    bufs = [(torch.empty(cap, dtype=torch.int64, device="cuda"), torch.empty(cap, dtype=torch.int64, device="cuda"),
+    u32 = a.cand_ids == "u32"
+    idt = torch.uint32 if u32 else torch.int64
+    rec_bytes = 9 if u32 else 17
+    bufs = [(torch.empty(cap, dtype=idt, device="cuda"), torch.empty(cap, dtype=idt, device="cuda"),
              torch.empty(cap, dtype=torch.uint8, device="cuda")) for _ in range(2)]
     freed = [None, None]   # consumer events after which a buffer may be written again
     sums = []              # per chunk: a, b, flag-word sums (device scalars, read at the end)
@@ -508,7 +514,10 @@ def cand_stream_main(a):
                 if freed[k] is not None:
                     est.wait_event(freed[k])
                 ev0.record(est)
-                ca, cb, cf, first, done = eng.candidates_next(cap, bufs[k])   # enqueued, no wait
+                if u32:
+                    ca, cb, cf, first, done, idb = eng.candidates_next_u32(cap, bufs[k])   # enqueued, no wait
+                else:
+                    ca, cb, cf, first, done = eng.candidates_next(cap, bufs[k])   # enqueued, no wait
                 emitted = torch.cuda.Event()
                 emitted.record(est)
             assert first == got, (first, got)
@@ -523,7 +532,13 @@ def cand_stream_main(a):
                     if a.cand_overlap:
                         cons.wait_event(emitted)
                     n8 = (n // 8) * 8
-                    sums.append(torch.stack([ca.sum(), cb.sum(), cf[:n8].view(torch.int64).sum() + cf[n8:].sum()]))
+                    if u32:   # the id columns read as 8-byte words (two ids each; a widening int32 sum ran 3x slower)
+                        n2 = (n // 2) * 2
+                        sums.append(torch.stack([ca[:n2].view(torch.int64).sum() + ca[n2:].view(torch.int32).sum(),
+                                                 cb[:n2].view(torch.int64).sum() + cb[n2:].view(torch.int32).sum(),
+                                                 cf[:n8].view(torch.int64).sum() + cf[n8:].sum()]))
+                    else:
+                        sums.append(torch.stack([ca.sum(), cb.sum(), cf[:n8].view(torch.int64).sum() + cf[n8:].sum()]))
                     ev1 = torch.cuda.Event(enable_timing=True)
                     ev1.record(cst)
                     freed[k] = ev1 if a.cand_overlap else None
@@ -564,11 +579,15 @@ def cand_stream_main(a):
                        "chunk_latency_ms_p99": float(np.percentile(lat_ms, 99)),
                        "window_period_s": period, "sustained_edges_per_s": E / period,
                        "target_edges_per_s": 1e8, "checksum": int(chk), "consumer": a.cand_consumer,
+                       "id_columns": ("uint32, id - the window's smallest id (gs_candidates_next_u32)" if u32
+                                      else "int64 (gs_candidates_next)"), "record_bytes": rec_bytes,
+                       "checksum_of": ("the columns' 8-byte words (u32: two ids a word; not comparable across "
+                                       "--cand-ids)"),
                        "parallelism": "1 GPU"},
             "roofline": {"bound": "hbm", "kernel": "whole window (emission + consumer)",
-                         "achieved": round(17 * total / elapsed / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(17 * total / elapsed / 1e9 / HBM_PEAK_GBS, 4), "traffic": None,
-                         "algorithmic_bytes_per_launch": 17 * total, "avg_launch_ms": elapsed * 1e3},
+                         "achieved": round(rec_bytes * total / elapsed / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(rec_bytes * total / elapsed / 1e9 / HBM_PEAK_GBS, 4), "traffic": None,
+                         "algorithmic_bytes_per_launch": rec_bytes * total, "avg_launch_ms": elapsed * 1e3},
             "cpu_baseline": None}
     if not a.no_cpu_baseline:
         line["cpu_baseline"] = cand_cpu_baseline(E)

@@ -46,7 +46,7 @@ EXPORTS = ("gs_abi_version", "gs_device_count", "gs_create", "gs_destroy", "gs_l
            "gs_comm_allreduce_sum_u64", "gs_window_reduce_dist", "gs_window_fold_degree_max_dist",
            "gs_stream_create", "gs_stream_destroy", "gs_stream_append", "gs_stream_watermark", "gs_stream_flush",
            "gs_stream_poll", "gs_stream_stats", "gs_generate_rmat", "gs_generate_uniform", "gs_generate_zipf", "gs_generate_values", "gs_last_stage_times",
-           "gs_set_max_window_records", "gs_candidates_begin", "gs_candidates_begin_part", "gs_candidates_next", "gs_candidates_seek",
+           "gs_set_max_window_records", "gs_candidates_begin", "gs_candidates_begin_part", "gs_candidates_next", "gs_candidates_next_u32", "gs_candidates_seek",
            "gs_candidates_vertex_range")
 
 P = ctypes.c_void_p
@@ -88,6 +88,11 @@ class GsCsrOut(ctypes.Structure):
 
 
 class GsPairOut(ctypes.Structure):
+    _fields_ = [("a", P), ("b", P), ("is_candidate", P), ("capacity", u64), ("n_out", ctypes.POINTER(u64)),
+                ("mem", i32), ("reserved", i32)]
+
+
+class GsPairOutU32(ctypes.Structure):   # gs_pair_out_u32: the same fields, uint32_t id columns
     _fields_ = [("a", P), ("b", P), ("is_candidate", P), ("capacity", u64), ("n_out", ctypes.POINTER(u64)),
                 ("mem", i32), ("reserved", i32)]
 
@@ -227,6 +232,8 @@ def load() -> ctypes.CDLL:
         "gs_candidates_begin_part": (st, [P, ctypes.POINTER(GsEdgeBatch), u32, u32, ctypes.POINTER(u64),
                                           ctypes.POINTER(u32)]),
         "gs_candidates_next": (st, [P, ctypes.POINTER(GsPairOut), ctypes.POINTER(u64), ctypes.POINTER(i32)]),
+        "gs_candidates_next_u32": (st, [P, ctypes.POINTER(GsPairOutU32), ctypes.POINTER(i64), ctypes.POINTER(u64),
+                                        ctypes.POINTER(i32)]),
         "gs_candidates_seek": (st, [P, u64]),
         "gs_candidates_vertex_range": (st, [P, i64, ctypes.POINTER(u64), ctypes.POINTER(u64)]),
     }

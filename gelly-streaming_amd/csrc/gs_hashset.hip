@@ -269,11 +269,14 @@ __global__ __launch_bounds__(256) void k_cand_meta(const uint64_t* __restrict__ 
 // base + 64 i + l; each position's slot is resolved against 64 consecutive block starts held one per lane
 // (binary search through lane shuffles; a step that spans more than 64 slots takes the next 64), starting
 // at slot sc (the slot of base or an earlier one).  Returns the slot of the step's last position.
+// OT: the id columns' type -- int64_t (the reference's Long), or uint32_t holding id - idb (gs_candidates_next_u32).
+template <typename OT>
 __device__ __forceinline__ uint32_t cand_slow_step(const uint64_t* __restrict__ vs, uint32_t S,
                                                    const CandMeta* __restrict__ meta, const int64_t* __restrict__ vkeys,
                                                    const int64_t* __restrict__ nbr, const int64_t* __restrict__ gids,
                                                    uint64_t P0, uint64_t base, uint64_t w1, uint32_t sc, uint32_t lane,
-                                                   int64_t* __restrict__ a, int64_t* __restrict__ b, uint8_t* __restrict__ f) {
+                                                   OT* __restrict__ a, OT* __restrict__ b, uint8_t* __restrict__ f,
+                                                   int64_t idb) {
   uint64_t o[4];
   uint32_t slot[4];
   bool need[4];
@@ -333,8 +336,8 @@ __device__ __forceinline__ uint32_t cand_slow_step(const uint64_t* __restrict__ 
       av = bv = 0;
       fv = 1;
     }
-    a[o[i] - P0] = av;
-    b[o[i] - P0] = bv;
+    a[o[i] - P0] = (OT)(av - idb);
+    b[o[i] - P0] = (OT)(bv - idb);
     f[o[i] - P0] = fv;
   }
   return __shfl(slot[3], 63, 64);   // the slot of this step's last position (the next step starts there)
@@ -366,14 +369,14 @@ __device__ __forceinline__ uint32_t cand_find_slot(const uint64_t* __restrict__ 
 // so the kernel holds fewer registers and more of its stores are in flight; every other step's base is
 // appended to `steps` (count in steps_n) for k_cand_emit_rest.  Kernels: k_cand_emit_all (MODE 0),
 // k_cand_emit_fast (MODE 1).
-template <int MODE>
+template <int MODE, typename OT>
 __device__ __forceinline__ void cand_emit_body(const uint64_t* __restrict__ vs, uint32_t S,
                                                const CandMeta* __restrict__ meta, const int64_t* __restrict__ vkeys,
                                                const int64_t* __restrict__ nbr, const int64_t* __restrict__ gids,
                                                uint64_t P0, uint64_t P1, uint64_t per_wave,
-                                               int64_t* __restrict__ a, int64_t* __restrict__ b,
+                                               OT* __restrict__ a, OT* __restrict__ b,
                                                uint8_t* __restrict__ f, int f4, uint64_t* __restrict__ steps,
-                                               uint32_t* __restrict__ steps_n) {
+                                               uint32_t* __restrict__ steps_n, int64_t idb) {
   const uint32_t lane = threadIdx.x & 63;
   const uint64_t wave = ((uint64_t)blockIdx.x * 256u + threadIdx.x) >> 6;
   const uint64_t w0 = P0 + wave * per_wave;
@@ -417,8 +420,8 @@ __device__ __forceinline__ void cand_emit_body(const uint64_t* __restrict__ vs, 
           const uint64_t q = q0 + (uint64_t)(i * 64) + lane;
           for (int g = 0; g < 64 && r + 1 < rows && tri_rows_before(r + 1, k) <= q; ++g) ++r;
           const uint64_t col = min(q - tri_rows_before(r, k), k - 1 - r);
-          a[oi - P0] = G[r];
-          b[oi - P0] = G[r + col];
+          a[oi - P0] = (OT)(G[r] - idb);
+          b[oi - P0] = (OT)(G[r + col] - idb);
           if (!f4) f[oi - P0] = 1;
         }
         if (f4) {   // every flag of a pair row is 1: one 4-byte store per lane (256 B per wave) instead of four 64-B byte-store runs
@@ -445,7 +448,7 @@ __device__ __forceinline__ void cand_emit_body(const uint64_t* __restrict__ vs, 
         if (c < 64) break;
       }
     } else {
-      sc = cand_slow_step(vs, S, meta, vkeys, nbr, gids, P0, base, w1, sc, lane, a, b, f);
+      sc = cand_slow_step<OT>(vs, S, meta, vkeys, nbr, gids, P0, base, w1, sc, lane, a, b, f, idb);
     }
   }
 }
@@ -453,27 +456,30 @@ __device__ __forceinline__ void cand_emit_body(const uint64_t* __restrict__ vs, 
 #define GS_CAND_EMIT_ARGS                                                                                        \
   const uint64_t *__restrict__ vs, uint32_t S, const CandMeta *__restrict__ meta, const int64_t *__restrict__ vkeys, \
       const int64_t *__restrict__ nbr, const int64_t *__restrict__ gids, uint64_t P0, uint64_t P1, uint64_t per_wave,  \
-      int64_t *__restrict__ a, int64_t *__restrict__ b, uint8_t *__restrict__ f, int f4, uint64_t *__restrict__ steps, \
-      uint32_t *__restrict__ steps_n
-#define GS_CAND_EMIT_PASS vs, S, meta, vkeys, nbr, gids, P0, P1, per_wave, a, b, f, f4, steps, steps_n
-__global__ __launch_bounds__(256) void k_cand_emit_all(GS_CAND_EMIT_ARGS) { cand_emit_body<0>(GS_CAND_EMIT_PASS); }
-__global__ __launch_bounds__(256) void k_cand_emit_fast(GS_CAND_EMIT_ARGS) { cand_emit_body<1>(GS_CAND_EMIT_PASS); }
+      OT *__restrict__ a, OT *__restrict__ b, uint8_t *__restrict__ f, int f4, uint64_t *__restrict__ steps,           \
+      uint32_t *__restrict__ steps_n, int64_t idb
+#define GS_CAND_EMIT_PASS vs, S, meta, vkeys, nbr, gids, P0, P1, per_wave, a, b, f, f4, steps, steps_n, idb
+template <typename OT>
+__global__ __launch_bounds__(256) void k_cand_emit_all(GS_CAND_EMIT_ARGS) { cand_emit_body<0, OT>(GS_CAND_EMIT_PASS); }
+template <typename OT>
+__global__ __launch_bounds__(256) void k_cand_emit_fast(GS_CAND_EMIT_ARGS) { cand_emit_body<1, OT>(GS_CAND_EMIT_PASS); }
 
 // the steps k_cand_emit_fast left (their bases in steps[0 .. *steps_n)), one wave per step at a time
+template <typename OT>
 __global__ __launch_bounds__(256) void k_cand_emit_rest(const uint64_t* __restrict__ vs, uint32_t S,
                                                         const CandMeta* __restrict__ meta,
                                                         const int64_t* __restrict__ vkeys, const int64_t* __restrict__ nbr,
                                                         const int64_t* __restrict__ gids, uint64_t P0, uint64_t P1,
-                                                        int64_t* __restrict__ a, int64_t* __restrict__ b,
+                                                        OT* __restrict__ a, OT* __restrict__ b,
                                                         uint8_t* __restrict__ f, const uint64_t* __restrict__ steps,
-                                                        const uint32_t* __restrict__ steps_n) {
+                                                        const uint32_t* __restrict__ steps_n, int64_t idb) {
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t n = *steps_n;
   const uint32_t nw = gridDim.x * 4u;
   for (uint32_t i = (blockIdx.x * 256u + threadIdx.x) >> 6; i < n; i += nw) {   // wave-uniform
     const uint64_t base = steps[i];
     const uint32_t sc = cand_find_slot(vs, S, base, lane);
-    cand_slow_step(vs, S, meta, vkeys, nbr, gids, P0, base, min(P1, base + 256), sc, lane, a, b, f);
+    cand_slow_step<OT>(vs, S, meta, vkeys, nbr, gids, P0, base, min(P1, base + 256), sc, lane, a, b, f, idb);
   }
 }
 
@@ -1393,8 +1399,9 @@ static gs_status cand_layout(gs_ctx* c, uint32_t U, uint32_t M, uint32_t nparts,
   return GS_OK;
 }
 
-// records [P0, P1) of the layout into a / b / f (device)
-static gs_status cand_emit(gs_ctx* c, uint32_t S, uint64_t P0, uint64_t P1, int64_t* a, int64_t* b, uint8_t* f) {
+// records [P0, P1) of the layout into a / b / f (device); OT = uint32_t: the ids as id - idb
+template <typename OT>
+static gs_status cand_emit(gs_ctx* c, uint32_t S, uint64_t P0, uint64_t P1, OT* a, OT* b, uint8_t* f, int64_t idb = 0) {
   const uint64_t n = P1 - P0;
   if (n == 0) return GS_OK;
   const uint64_t blocks = std::max<uint64_t>(1, std::min<uint64_t>((n + 4095) / 4096, 4096));
@@ -1413,13 +1420,13 @@ static gs_status cand_emit(gs_ctx* c, uint32_t S, uint64_t P0, uint64_t P1, int6
     GS_HIP(hipMemsetAsync(steps_n, 0, 4, c->stream));
     // (k_cand_emit_fast holds 90 VGPRs: 5 waves per SIMD; held to 80 for 6 it spills and ran 0.99 -> 1.00 ms
     // per 2^28 records, profiles/r05/c5/)
-    hipLaunchKernelGGL(k_cand_emit_fast, dim3((unsigned)blocks), dim3(256), 0, c->stream, vs, S, meta, vkeys, nbr, gids,
-                       P0, P1, per_wave, a, b, f, f4, steps, steps_n);
-    hipLaunchKernelGGL(k_cand_emit_rest, dim3(1024), dim3(256), 0, c->stream, vs, S, meta, vkeys, nbr, gids, P0, P1, a, b,
-                       f, (const uint64_t*)steps, (const uint32_t*)steps_n);
+    hipLaunchKernelGGL(k_cand_emit_fast<OT>, dim3((unsigned)blocks), dim3(256), 0, c->stream, vs, S, meta, vkeys, nbr,
+                       gids, P0, P1, per_wave, a, b, f, f4, steps, steps_n, idb);
+    hipLaunchKernelGGL(k_cand_emit_rest<OT>, dim3(1024), dim3(256), 0, c->stream, vs, S, meta, vkeys, nbr, gids, P0, P1,
+                       a, b, f, (const uint64_t*)steps, (const uint32_t*)steps_n, idb);
   } else {
-    hipLaunchKernelGGL(k_cand_emit_all, dim3((unsigned)blocks), dim3(256), 0, c->stream, vs, S, meta, vkeys, nbr, gids,
-                       P0, P1, per_wave, a, b, f, f4, nullptr, nullptr);
+    hipLaunchKernelGGL(k_cand_emit_all<OT>, dim3((unsigned)blocks), dim3(256), 0, c->stream, vs, S, meta, vkeys, nbr,
+                       gids, P0, P1, per_wave, a, b, f, f4, nullptr, nullptr, idb);
   }
   return hip_check(c, hipGetLastError(), "k_cand_emit");
 }
@@ -1494,7 +1501,14 @@ gs_status gs_candidates_begin_part(gs_ctx* c, const gs_edge_batch* b, uint32_t n
   uint32_t U = 0, M = 0, S = 0, fl = 0;
   uint64_t key_xor = 0, total = 0;
   GS_TRY(hashset_order(c, src, dst, b->n, &U, &M, &key_xor, &fl));
-  GS_TRY(cand_layout(c, U, M, nparts, part, &S, &total));
+  // the window's smallest and largest ids (vkeys ascending), read back with the layout's sizes: whether the
+  // session can emit 32-bit id columns (gs_candidates_next_u32)
+  const int64_t* vk = c->hs[HS_VKEYS].as<int64_t>();
+  GS_HIP(hipMemcpyAsync(&c->host_small[300], vk, 8, hipMemcpyDeviceToHost, c->stream));
+  GS_HIP(hipMemcpyAsync(&c->host_small[301], vk + (U - 1), 8, hipMemcpyDeviceToHost, c->stream));
+  GS_TRY(cand_layout(c, U, M, nparts, part, &S, &total));   // (waits)
+  c->cand_idmin = (int64_t)c->host_small[300];
+  c->cand_idmax = (int64_t)c->host_small[301];
   c->cand_nparts = nparts;
   c->cand_U = U;
   c->cand_S = S;
@@ -1514,11 +1528,13 @@ static gs_status cand_session(gs_ctx* c) {
   return hip_check(c, hipSetDevice(c->device), "hipSetDevice");
 }
 
-gs_status gs_candidates_next(gs_ctx* c, gs_pair_out* out, uint64_t* first_record, int32_t* done) {
-  if (!c) return GS_EINVAL;
-  if (!out || !out->n_out || (out->capacity && (!out->a || !out->b || !out->is_candidate)))
-    return set_error(c, GS_EINVAL, "bad gs_pair_out");
-  GS_TRY(cand_session(c));
+}  // extern "C"
+
+namespace gs {
+// gs_candidates_next / gs_candidates_next_u32: OT = the id columns' type, idb = what the u32 columns are
+// relative to
+template <typename OT, class Out>
+static gs_status cand_next(gs_ctx* c, Out* out, int64_t idb, uint64_t* first_record, int32_t* done) {
   const uint64_t P0 = c->cand_cursor, n = std::min<uint64_t>(out->capacity, c->cand_total - P0), P1 = P0 + n;
   if (first_record) *first_record = P0;
   *out->n_out = n;
@@ -1528,7 +1544,7 @@ gs_status gs_candidates_next(gs_ctx* c, gs_pair_out* out, uint64_t* first_record
     if (c->cand_total > P0 && out->capacity == 0) return set_error(c, GS_ECAPACITY, "capacity 0");
     return GS_OK;
   }
-  int64_t *a = out->a, *bb = out->b;
+  OT *a = out->a, *bb = out->b;
   uint8_t* f = out->is_candidate;
   const bool direct = out->mem == GS_MEM_DEVICE;
   if (!direct) {
@@ -1536,14 +1552,14 @@ gs_status gs_candidates_next(gs_ctx* c, gs_pair_out* out, uint64_t* first_record
     GS_TRY(ensure(c, c->out_keys, n * 8));
     GS_TRY(ensure(c, c->out_a, n * 8));
     GS_TRY(ensure(c, c->out_b, n));
-    a = c->out_keys.as<int64_t>();
-    bb = c->out_a.as<int64_t>();
+    a = c->out_keys.as<OT>();
+    bb = c->out_a.as<OT>();
     f = c->out_b.as<uint8_t>();
   }
-  GS_TRY(cand_emit(c, c->cand_S, P0, P1, a, bb, f));
+  GS_TRY(cand_emit<OT>(c, c->cand_S, P0, P1, a, bb, f, idb));
   if (!direct) {
-    GS_HIP(hipMemcpyAsync(out->a, a, n * 8, hipMemcpyDeviceToHost, c->stream));
-    GS_HIP(hipMemcpyAsync(out->b, bb, n * 8, hipMemcpyDeviceToHost, c->stream));
+    GS_HIP(hipMemcpyAsync(out->a, a, n * sizeof(OT), hipMemcpyDeviceToHost, c->stream));
+    GS_HIP(hipMemcpyAsync(out->b, bb, n * sizeof(OT), hipMemcpyDeviceToHost, c->stream));
     GS_HIP(hipMemcpyAsync(out->is_candidate, f, n, hipMemcpyDeviceToHost, c->stream));
     GS_TRY(host_wait(c));
   }
@@ -1553,6 +1569,29 @@ gs_status gs_candidates_next(gs_ctx* c, gs_pair_out* out, uint64_t* first_record
   c->cand_cursor = P1;
   if (done) *done = P1 >= c->cand_total;
   return GS_OK;
+}
+}  // namespace gs
+
+extern "C" {
+
+gs_status gs_candidates_next(gs_ctx* c, gs_pair_out* out, uint64_t* first_record, int32_t* done) {
+  if (!c) return GS_EINVAL;
+  if (!out || !out->n_out || (out->capacity && (!out->a || !out->b || !out->is_candidate)))
+    return set_error(c, GS_EINVAL, "bad gs_pair_out");
+  GS_TRY(cand_session(c));
+  return cand_next<int64_t>(c, out, 0, first_record, done);
+}
+
+gs_status gs_candidates_next_u32(gs_ctx* c, gs_pair_out_u32* out, int64_t* id_base, uint64_t* first_record,
+                                 int32_t* done) {
+  if (!c) return GS_EINVAL;
+  if (!out || !out->n_out || !id_base || (out->capacity && (!out->a || !out->b || !out->is_candidate)))
+    return set_error(c, GS_EINVAL, "bad gs_pair_out_u32");
+  GS_TRY(cand_session(c));
+  *id_base = c->cand_idmin;
+  if (c->cand_total && (uint64_t)c->cand_idmax - (uint64_t)c->cand_idmin > 0xFFFFFFFFull)
+    return set_error(c, GS_EUNSUPPORTED, "the window's ids span more than 2^32 values: gs_candidates_next");
+  return cand_next<uint32_t>(c, out, c->cand_idmin, first_record, done);
 }
 
 gs_status gs_candidates_seek(gs_ctx* c, uint64_t record) {

@@ -85,6 +85,7 @@ struct gs_ctx {
   // hs[] until the next entry point call on the ctx (call_seq) ends the session
   uint64_t call_seq = 0, cand_seq = ~0ull, cand_total = 0, cand_cursor = 0;
   uint32_t cand_U = 0, cand_S = 0, cand_nparts = 1;
+  int64_t cand_idmin = 0, cand_idmax = 0;   // the session's id range (gs_candidates_next_u32)
   gs::DevBuf cand_bounds, cand_steps;   // (cand_steps: the steps k_cand_emit<1> leaves to k_cand_emit_rest)
   // input staging (host batches)
   gs::DevBuf in_src, in_dst, in_val;

@@ -185,7 +185,8 @@ class Engine:
             import torch
 
             tdt = {np.int64: torch.int64, np.int32: torch.int32, np.float32: torch.float32,
-                   np.float64: torch.float64, np.uint64: torch.int64, np.uint8: torch.uint8}[np_dtype]
+                   np.float64: torch.float64, np.uint64: torch.int64, np.uint8: torch.uint8,
+                   np.uint32: torch.uint32}[np_dtype]
             return torch.empty(max(n, 1), dtype=tdt, device=f"cuda:{self.device}")
         return np.empty(max(n, 1), dtype=np_dtype)
 
@@ -313,6 +314,23 @@ class Engine:
         self._check(self._L.gs_candidates_next(self.ctx, ctypes.byref(o), ctypes.byref(first), ctypes.byref(done)))
         n = n_out.value
         return a[:n], bb[:n], f[:n], first.value, bool(done.value)
+
+    def candidates_next_u32(self, capacity: int, out=None):
+        """gs_candidates_next_u32: the next <= capacity records with the ids as uint32 columns relative to the
+        window's smallest id.  Returns (a32, b32, is_candidate, first position, done, id_base): a = id_base +
+        a32.  Raises GsError (GS_EUNSUPPORTED) when the window's ids span more than 2^32 values."""
+        dev = self._cand_dev
+        if out is None:
+            out = (self._empty(dev, capacity, np.uint32), self._empty(dev, capacity, np.uint32),
+                   self._empty(dev, capacity, np.uint8))
+        a, bb, f = out
+        n_out, first, done, base = ctypes.c_uint64(0), ctypes.c_uint64(0), ctypes.c_int32(0), ctypes.c_int64(0)
+        o = L.GsPairOutU32(_ptr(a), _ptr(bb), _ptr(f), capacity, ctypes.pointer(n_out),
+                           L.GS_MEM_DEVICE if dev else L.GS_MEM_HOST, 0)
+        self._check(self._L.gs_candidates_next_u32(self.ctx, ctypes.byref(o), ctypes.byref(base), ctypes.byref(first),
+                                                   ctypes.byref(done)))
+        n = n_out.value
+        return a[:n], bb[:n], f[:n], first.value, bool(done.value), base.value
 
     def candidates_seek(self, record: int):
         """gs_candidates_seek: the session's next chunk starts at output position `record`."""

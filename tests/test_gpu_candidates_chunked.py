@@ -67,3 +67,55 @@ def test_session_ends_at_the_next_call(pkg, engine, oracle):
     engine.reduce(s, d, np.ones(len(s), np.int64), 1, 0)   # another entry point on the ctx
     with pytest.raises(pkg.GsError):
         engine.candidates_next(10)
+
+
+def _stream_u32(engine, s, d, cap, dev=True):
+    args = (torch.from_numpy(s).cuda(), torch.from_numpy(d).cuda()) if dev else (s, d)
+    total = engine.candidates_begin(*args)
+    parts, at, done, base = [], 0, False, None
+    while not done:
+        a, b, f, first, done, base = engine.candidates_next_u32(cap)
+        assert first == at and (len(a) == cap or done)
+        at += len(a)
+        parts.append([x.cpu().numpy() if isinstance(x, torch.Tensor) else np.asarray(x) for x in (a, b, f)])
+    assert at == total
+    a, b, f = (np.concatenate([p[i] for p in parts]) for i in range(3))
+    assert a.dtype == np.uint32 and b.dtype == np.uint32
+    return (a.astype(np.int64) + base, b.astype(np.int64) + base, f), base
+
+
+@pytest.mark.parametrize("kind", ["small_ids", "sparse_ids", "negative_ids", "rmat"])
+@pytest.mark.parametrize("cap", [7, 1 << 20])
+def test_u32_chunks_equal_the_oracle(engine, oracle, kind, cap):
+    """gs_candidates_next_u32: the same records as gs_candidates_next with every id as id - id_base in a
+    uint32 column (id_base = the window's smallest id; negative and sparse ids included)."""
+    rng = np.random.default_rng(hash(("u32", kind, cap)) & 0xFFFF)
+    for trial in range(3):
+        s, d = _cand_case(oracle, rng, kind)
+        ra, rb, rf, flags = oracle.window_candidates(s, d)
+        (ga, gb, gf), base = _stream_u32(engine, s, d, cap, dev=trial != 1)
+        assert base == min(s.min(), d.min())
+        assert np.array_equal(ga, ra) and np.array_equal(gb, rb) and np.array_equal(gf, rf), (kind, cap, trial)
+
+
+def test_u32_chunks_of_a_hub_window(engine, oracle):
+    s, d = oracle.gen_rmat(14, 600_000, 0x5EED06)
+    s, d = s + (5 << 40), d + (5 << 40)   # ids far from 0, span < 2^32
+    S, D = torch.from_numpy(s).cuda(), torch.from_numpy(d).cuda()
+    wa, wb, wf = engine.candidates(S, D)
+    (ga, gb, gf), base = _stream_u32(engine, s, d, 1 << 20)
+    assert len(ga) == len(wa) > 10 ** 7 and base == min(s.min(), d.min())
+    assert np.array_equal(ga, wa.cpu().numpy()) and np.array_equal(gb, wb.cpu().numpy())
+    assert np.array_equal(gf, wf.cpu().numpy())
+
+
+def test_u32_refuses_a_span_past_2_32(pkg, engine, oracle):
+    s, d = oracle.gen_rmat(8, 3000, 9)
+    s = s.copy()
+    s[0] = 1 << 33   # one id 2^33 away from the rest
+    engine.candidates_begin(s, d)
+    with pytest.raises(pkg.GsError):
+        engine.candidates_next_u32(100)
+    a, b, f, first, done = engine.candidates_next(1 << 20)   # the session stays usable with 64-bit ids
+    ra, rb, rf, flags = oracle.window_candidates(s, d)
+    assert first == 0 and done and np.array_equal(np.asarray(a), ra) and np.array_equal(np.asarray(b), rb)
