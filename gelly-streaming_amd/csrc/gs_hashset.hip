@@ -412,14 +412,23 @@ __device__ __forceinline__ void cand_emit_body(const uint64_t* __restrict__ vs, 
         for (int g = 0; g < 64 && r0 > 0 && tri_rows_before(r0, k) > q0; ++g) --r0;
         for (int g = 0; g < 64 && r0 + 1 < rows && tri_rows_before(r0 + 1, k) <= q0; ++g) ++r0;
         const int64_t* G = gids + m.gbase;
-        uint64_t r = r0;   // a lane's positions increase with i: its row walk carries over
+        // a lane's positions increase with i, so its row walk carries over; it runs in 32 bits relative to
+        // the step's first row (row r holds k - r entries; off = q - rows_before(r) < k + 256), one add and
+        // compare per row crossed instead of two 64-bit row products per record
+        uint32_t r = (uint32_t)r0, len = (uint32_t)(k - r0);
+        uint32_t off = (uint32_t)(q0 - tri_rows_before(r0, k)) + lane;
+        const uint32_t rows32 = (uint32_t)rows;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
+          if (i) off += 64;
           const uint64_t oi = base + (uint64_t)(i * 64) + lane;
           if (oi >= e1) continue;
-          const uint64_t q = q0 + (uint64_t)(i * 64) + lane;
-          for (int g = 0; g < 64 && r + 1 < rows && tri_rows_before(r + 1, k) <= q; ++g) ++r;
-          const uint64_t col = min(q - tri_rows_before(r, k), k - 1 - r);
+          for (int g = 0; g < 64 && r + 1 < rows32 && off >= len; ++g) {
+            off -= len;
+            --len;
+            ++r;
+          }
+          const uint32_t col = min(off, len - 1);
           a[oi - P0] = (OT)(G[r] - idb);
           b[oi - P0] = (OT)(G[r + col] - idb);
           if (!f4) f[oi - P0] = 1;
