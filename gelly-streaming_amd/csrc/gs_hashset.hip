@@ -369,6 +369,9 @@ __device__ __forceinline__ uint32_t cand_find_slot(const uint64_t* __restrict__ 
 // so the kernel holds fewer registers and more of its stores are in flight; every other step's base is
 // appended to `steps` (count in steps_n) for k_cand_emit_rest.  Kernels: k_cand_emit_all (MODE 0),
 // k_cand_emit_fast (MODE 1).
+#ifndef GS_CAND_LANE4
+#define GS_CAND_LANE4 1   // fast path: four consecutive positions per lane (A/B: 0 = positions strided by 64)
+#endif
 template <int MODE, typename OT>
 __device__ __forceinline__ void cand_emit_body(const uint64_t* __restrict__ vs, uint32_t S,
                                                const CandMeta* __restrict__ meta, const int64_t* __restrict__ vkeys,
@@ -412,12 +415,59 @@ __device__ __forceinline__ void cand_emit_body(const uint64_t* __restrict__ vs, 
         for (int g = 0; g < 64 && r0 > 0 && tri_rows_before(r0, k) > q0; ++g) --r0;
         for (int g = 0; g < 64 && r0 + 1 < rows && tri_rows_before(r0 + 1, k) <= q0; ++g) ++r0;
         const int64_t* G = gids + m.gbase;
+        const uint32_t rows32 = (uint32_t)rows;
+#if GS_CAND_LANE4
+        // lane l takes the step's positions base + 4l .. 4l + 3: its four records are consecutive (mostly in one
+        // row), and a wave's a / b stores are one contiguous 1 KiB (u32) or 2 KiB (int64) run of 16-byte stores.
+        // The row walk runs in 32 bits relative to the step's first row (row r holds k - r entries; off = q -
+        // rows_before(r) < k + 256): one add and compare per row crossed, no 64-bit row products per record.
+        uint32_t r = (uint32_t)r0, len = (uint32_t)(k - r0);
+        uint32_t off = (uint32_t)(q0 - tri_rows_before(r0, k)) + 4u * lane;
+        const uint64_t o0 = base + 4ull * lane;
+        OT av[4], bv[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          if (j) ++off;
+          for (int g = 0; g < 64 && r + 1 < rows32 && off >= len; ++g) {
+            off -= len;
+            --len;
+            ++r;
+          }
+          const uint32_t col = min(off, len - 1);
+          av[j] = (OT)(G[r] - idb);
+          bv[j] = (OT)(G[r + col] - idb);
+        }
+        if ((f4 & 2) && o0 + 4 <= e1) {   // a and b 16-byte aligned; o0 - P0 is a multiple of 4
+          if constexpr (sizeof(OT) == 4) {
+            *reinterpret_cast<uint4*>(a + (o0 - P0)) = make_uint4(av[0], av[1], av[2], av[3]);
+            *reinterpret_cast<uint4*>(b + (o0 - P0)) = make_uint4(bv[0], bv[1], bv[2], bv[3]);
+          } else {
+            longlong2* pa = reinterpret_cast<longlong2*>(a + (o0 - P0));
+            longlong2* pb = reinterpret_cast<longlong2*>(b + (o0 - P0));
+            pa[0] = make_longlong2(av[0], av[1]);
+            pa[1] = make_longlong2(av[2], av[3]);
+            pb[0] = make_longlong2(bv[0], bv[1]);
+            pb[1] = make_longlong2(bv[2], bv[3]);
+          }
+        } else {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            if (o0 + j < e1) {
+              a[o0 + j - P0] = av[j];
+              b[o0 + j - P0] = bv[j];
+            }
+          }
+        }
+        if (!(f4 & 1)) {
+          for (int j = 0; j < 4; ++j)
+            if (o0 + j < e1) f[o0 + j - P0] = 1;
+        }
+#else
         // a lane's positions increase with i, so its row walk carries over; it runs in 32 bits relative to
         // the step's first row (row r holds k - r entries; off = q - rows_before(r) < k + 256), one add and
         // compare per row crossed instead of two 64-bit row products per record
         uint32_t r = (uint32_t)r0, len = (uint32_t)(k - r0);
         uint32_t off = (uint32_t)(q0 - tri_rows_before(r0, k)) + lane;
-        const uint32_t rows32 = (uint32_t)rows;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           if (i) off += 64;
@@ -431,9 +481,10 @@ __device__ __forceinline__ void cand_emit_body(const uint64_t* __restrict__ vs, 
           const uint32_t col = min(off, len - 1);
           a[oi - P0] = (OT)(G[r] - idb);
           b[oi - P0] = (OT)(G[r + col] - idb);
-          if (!f4) f[oi - P0] = 1;
+          if (!(f4 & 1)) f[oi - P0] = 1;
         }
-        if (f4) {   // every flag of a pair row is 1: one 4-byte store per lane (256 B per wave) instead of four 64-B byte-store runs
+#endif
+        if (f4 & 1) {   // every flag of a pair row is 1: one 4-byte store per lane (256 B per wave) instead of four 64-B byte-store runs
           uint8_t* fr = f + (base - P0);   // base - P0 is a multiple of 256
           const uint64_t fo = 4ull * lane;
           if (base + fo + 4 <= e1) {
@@ -1416,7 +1467,8 @@ static gs_status cand_emit(gs_ctx* c, uint32_t S, uint64_t P0, uint64_t P1, OT* 
   const uint64_t blocks = std::max<uint64_t>(1, std::min<uint64_t>((n + 4095) / 4096, 4096));
   const uint64_t waves = blocks * 4;
   const uint64_t per_wave = ((n + waves - 1) / waves + 255) / 256 * 256;
-  const int f4 = ((uintptr_t)f & 3) == 0 ? 1 : 0;
+  // bit 0: the flag column 4-byte aligned; bit 1: a and b 16-byte aligned (the fast path's vector stores)
+  const int f4 = (((uintptr_t)f & 3) == 0 ? 1 : 0) | ((((uintptr_t)a | (uintptr_t)b) & 15) == 0 ? 2 : 0);
   static const int split_env = getenv("GS_CAND_SPLIT") ? atoi(getenv("GS_CAND_SPLIT")) : 1;   // A/B
   const uint64_t* vs = c->hs[HS_VS].as<uint64_t>();
   const CandMeta* meta = c->hs[HS_META].as<CandMeta>();

@@ -119,3 +119,29 @@ def test_u32_refuses_a_span_past_2_32(pkg, engine, oracle):
     a, b, f, first, done = engine.candidates_next(1 << 20)   # the session stays usable with 64-bit ids
     ra, rb, rf, flags = oracle.window_candidates(s, d)
     assert first == 0 and done and np.array_equal(np.asarray(a), ra) and np.array_equal(np.asarray(b), rb)
+
+
+@pytest.mark.parametrize("u32", [False, True])
+def test_chunks_into_unaligned_columns(engine, oracle, u32):
+    """Output columns that start off their natural 16-byte (ids) and 4-byte (flags) alignment: the emission's
+    vector stores give way to per-record stores, with the same records."""
+    s, d = oracle.gen_rmat(12, 40_000, 0x5EED07)
+    ra, rb, rf, flags = oracle.window_candidates(s, d)
+    cap = 1 << 18
+    idt = torch.uint32 if u32 else torch.int64
+    raw = [torch.zeros(cap + 3, dtype=idt, device="cuda") for _ in range(2)] + \
+          [torch.zeros(cap + 5, dtype=torch.uint8, device="cuda")]
+    bufs = (raw[0][1:cap + 1], raw[1][3:cap + 3], raw[2][1:cap + 1])   # a, b off 16-byte alignment, f off 4
+    total = engine.candidates_begin(torch.from_numpy(s).cuda(), torch.from_numpy(d).cuda())
+    got, done = [], False
+    while not done:
+        if u32:
+            a, b, f, first, done, base = engine.candidates_next_u32(cap, bufs)
+            a, b = a.cpu().numpy().astype(np.int64) + base, b.cpu().numpy().astype(np.int64) + base
+        else:
+            a, b, f, first, done = engine.candidates_next(cap, bufs)
+            a, b = a.cpu().numpy(), b.cpu().numpy()
+        got.append((a, b, f.cpu().numpy()))
+    ga, gb, gf = (np.concatenate([g[i] for g in got]) for i in range(3))
+    assert len(ga) == total == len(ra)
+    assert np.array_equal(ga, ra) and np.array_equal(gb, rb) and np.array_equal(gf, rf)
