@@ -521,8 +521,18 @@ __device__ __forceinline__ void cand_emit_body(const uint64_t* __restrict__ vs, 
 #define GS_CAND_EMIT_PASS vs, S, meta, vkeys, nbr, gids, P0, P1, per_wave, a, b, f, f4, steps, steps_n, idb
 template <typename OT>
 __global__ __launch_bounds__(256) void k_cand_emit_all(GS_CAND_EMIT_ARGS) { cand_emit_body<0, OT>(GS_CAND_EMIT_PASS); }
+#ifndef GS_CAND_FAST_WAVES
+#define GS_CAND_FAST_WAVES 0   // A/B: a waves-per-SIMD target for k_cand_emit_fast (0 = the compiler's choice)
+#endif
+#if GS_CAND_FAST_WAVES
+#define GS_CAND_FAST_ATTR __attribute__((amdgpu_waves_per_eu(GS_CAND_FAST_WAVES)))
+#else
+#define GS_CAND_FAST_ATTR
+#endif
 template <typename OT>
-__global__ __launch_bounds__(256) void k_cand_emit_fast(GS_CAND_EMIT_ARGS) { cand_emit_body<1, OT>(GS_CAND_EMIT_PASS); }
+__global__ __launch_bounds__(256) GS_CAND_FAST_ATTR void k_cand_emit_fast(GS_CAND_EMIT_ARGS) {
+  cand_emit_body<1, OT>(GS_CAND_EMIT_PASS);
+}
 
 // the steps k_cand_emit_fast left (their bases in steps[0 .. *steps_n)), one wave per step at a time
 template <typename OT>
