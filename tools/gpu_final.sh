@@ -31,6 +31,6 @@ case $MODE in
   E)
     timeout -k 10 400 python3 bench.py --workload cand_stream --cand-ids u32 > "$O/bench_cand_stream_u32.json" 2> "$O/bench_cand_stream_u32.err"
     timeout -k 10 400 python3 bench.py --workload cand_stream > "$O/bench_cand_stream.json" 2> "$O/bench_cand_stream.err"
-    timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$O/cand_u32_trace" -o run -- python3 bench.py --workload cand_stream \
+    timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$O/cand_u32_trace" -o run --output-format csv -- python3 bench.py --workload cand_stream \
       --cand-ids u32 --cand-consumer none --cand-windows 1 --max-chunks 40 --no-cpu-baseline > "$O/cand_u32_trace.log" 2>&1 ;;
 esac
