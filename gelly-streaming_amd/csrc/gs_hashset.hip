@@ -372,6 +372,9 @@ __device__ __forceinline__ uint32_t cand_find_slot(const uint64_t* __restrict__ 
 #ifndef GS_CAND_LANE4
 #define GS_CAND_LANE4 1   // fast path: four consecutive positions per lane (A/B: 0 = positions strided by 64)
 #endif
+#ifndef GS_CAND_CARRY
+#define GS_CAND_CARRY 1   // fast path: a step after a fast step in the same slot starts from its row state (A/B: 0)
+#endif
 template <int MODE, typename OT>
 __device__ __forceinline__ void cand_emit_body(const uint64_t* __restrict__ vs, uint32_t S,
                                                const CandMeta* __restrict__ meta, const int64_t* __restrict__ vkeys,
@@ -392,6 +395,12 @@ __device__ __forceinline__ void cand_emit_body(const uint64_t* __restrict__ vs, 
   uint32_t cs = 0xFFFFFFFFu;
   uint64_t c_beg = 0, c_end = 0;
   CandMeta cm{};
+#if GS_CAND_LANE4 && GS_CAND_CARRY
+  // the row state (row, its length, offset into it) of position k_next in slot k_slot: what the previous fast
+  // step's last lane walked to, so a fast step that follows one in the same slot skips the closed-form row search
+  uint32_t k_r = 0, k_len = 0, k_off = 0, k_slot = 0xFFFFFFFFu;
+  uint64_t k_next = ~0ull;
+#endif
   for (uint64_t base = w0; base < w1; base += 256) {
     // Fast path: the step lies inside one slot's pair rows (most records of a window: the blocks of its
     // high-degree vertices are O(k^2)).  The slot's metadata is wave-uniform (scalar loads), the row of
@@ -409,20 +418,32 @@ __device__ __forceinline__ void cand_emit_body(const uint64_t* __restrict__ vs, 
       const uint64_t t0 = base - c_beg;
       if (t0 >= m.d && m.rows) {
         const uint64_t k = m.k, rows = m.rows, q0 = t0 - m.d;
-        const double k2 = 2.0 * (double)k + 1.0;
-        uint64_t r0 = (uint64_t)fmax(0.0, (k2 - sqrt(fmax(0.0, k2 * k2 - 8.0 * (double)q0))) * 0.5);
-        if (r0 >= rows) r0 = rows - 1;
-        for (int g = 0; g < 64 && r0 > 0 && tri_rows_before(r0, k) > q0; ++g) --r0;
-        for (int g = 0; g < 64 && r0 + 1 < rows && tri_rows_before(r0 + 1, k) <= q0; ++g) ++r0;
         const int64_t* G = gids + m.gbase;
         const uint32_t rows32 = (uint32_t)rows;
 #if GS_CAND_LANE4
+        uint32_t r, len, off;
+#if GS_CAND_CARRY
+        if (k_next == base && k_slot == sc) {
+          r = k_r;
+          len = k_len;
+          off = k_off;
+        } else
+#endif
+        {
+          const double k2 = 2.0 * (double)k + 1.0;
+          uint64_t r0 = (uint64_t)fmax(0.0, (k2 - sqrt(fmax(0.0, k2 * k2 - 8.0 * (double)q0))) * 0.5);
+          if (r0 >= rows) r0 = rows - 1;
+          for (int g = 0; g < 64 && r0 > 0 && tri_rows_before(r0, k) > q0; ++g) --r0;
+          for (int g = 0; g < 64 && r0 + 1 < rows && tri_rows_before(r0 + 1, k) <= q0; ++g) ++r0;
+          r = (uint32_t)r0;
+          len = (uint32_t)(k - r0);
+          off = (uint32_t)(q0 - tri_rows_before(r0, k));
+        }
         // lane l takes the step's positions base + 4l .. 4l + 3: its four records are consecutive (mostly in one
         // row), and a wave's a / b stores are one contiguous 1 KiB (u32) or 2 KiB (int64) run of 16-byte stores.
         // The row walk runs in 32 bits relative to the step's first row (row r holds k - r entries; off = q -
         // rows_before(r) < k + 256): one add and compare per row crossed, no 64-bit row products per record.
-        uint32_t r = (uint32_t)r0, len = (uint32_t)(k - r0);
-        uint32_t off = (uint32_t)(q0 - tri_rows_before(r0, k)) + 4u * lane;
+        off += 4u * lane;
         const uint64_t o0 = base + 4ull * lane;
         OT av[4], bv[4];
 #pragma unroll
@@ -437,6 +458,13 @@ __device__ __forceinline__ void cand_emit_body(const uint64_t* __restrict__ vs, 
           av[j] = (OT)(G[r] - idb);
           bv[j] = (OT)(G[r + col] - idb);
         }
+#if GS_CAND_CARRY
+        k_r = __shfl(r, 63, 64);   // the last lane's position is base + 255: one on is the next step's first
+        k_len = __shfl(len, 63, 64);
+        k_off = __shfl(off, 63, 64) + 1u;
+        k_next = base + 256;
+        k_slot = sc;
+#endif
         if ((f4 & 2) && o0 + 4 <= e1) {   // a and b 16-byte aligned; o0 - P0 is a multiple of 4
           if constexpr (sizeof(OT) == 4) {
             *reinterpret_cast<uint4*>(a + (o0 - P0)) = make_uint4(av[0], av[1], av[2], av[3]);
@@ -463,6 +491,11 @@ __device__ __forceinline__ void cand_emit_body(const uint64_t* __restrict__ vs, 
             if (o0 + j < e1) f[o0 + j - P0] = 1;
         }
 #else
+        const double k2 = 2.0 * (double)k + 1.0;
+        uint64_t r0 = (uint64_t)fmax(0.0, (k2 - sqrt(fmax(0.0, k2 * k2 - 8.0 * (double)q0))) * 0.5);
+        if (r0 >= rows) r0 = rows - 1;
+        for (int g = 0; g < 64 && r0 > 0 && tri_rows_before(r0, k) > q0; ++g) --r0;
+        for (int g = 0; g < 64 && r0 + 1 < rows && tri_rows_before(r0 + 1, k) <= q0; ++g) ++r0;
         // a lane's positions increase with i, so its row walk carries over; it runs in 32 bits relative to
         // the step's first row (row r holds k - r entries; off = q - rows_before(r) < k + 256), one add and
         // compare per row crossed instead of two 64-bit row products per record
