@@ -160,15 +160,24 @@ static gs_status group_begin(gs_ctx* c, gs_comm_group* g, const gs_comm_group::P
     group_break(g, "rank " + std::to_string(c->comm_rank) + ": " + c->err);
     return st;
   }
-  g->post[c->comm_rank] = p;
+  {   // a broken group takes no new post: a rank that saw a mismatch below and returned must not
+      // overwrite its post while a slower peer still runs the same check
+    std::lock_guard<std::mutex> lk(g->m);
+    if (g->broken) return set_error(c, GS_ECOMM, "comm group broken: %s", g->why.c_str());
+    g->post[c->comm_rank] = p;
+  }
   GS_TRY(group_barrier(c, g));
   const gs_comm_group::Post& a = g->post[0];
   for (int q = 0; q < g->P; ++q) {   // the same check on every rank: all agree on a mismatch
     const gs_comm_group::Post& b = g->post[q];
     if (b.kind != a.kind || b.row != a.row || b.dtype != a.dtype || b.op != a.op ||
-        (a.kind != gs_comm_group::EXCHANGE && a.kind != gs_comm_group::ALLGATHERV && b.count != a.count))
-      return set_error(c, GS_ECOMM, "comm group: rank %d entered collective %d (count %zu) where rank 0 entered %d (count %zu)",
-                       q, b.kind, b.count, a.kind, a.count);
+        (a.kind != gs_comm_group::EXCHANGE && a.kind != gs_comm_group::ALLGATHERV && b.count != a.count)) {
+      set_error(c, GS_ECOMM, "comm group: rank %d entered collective %d (count %zu) where rank 0 entered %d (count %zu)",
+                q, b.kind, b.count, a.kind, a.count);
+      const std::string why = c->err;
+      group_break(g, why);   // every rank breaks it (the same check): later collectives fail, none races on post[]
+      return GS_ECOMM;
+    }
   }
   return GS_OK;
 }

@@ -418,7 +418,20 @@ static bool dist_no_defer() {
 // the others blocking in a collective), one packed all-to-all of the rows (4-byte keys from a sender whose
 // keys all fit; a rank's own rows stay in place), the unpack by sender, then the merge.  One rank: the
 // window's own output (no exchange, no merge).
+static gs_status dist_body(gs_ctx* c, const gs_edge_batch* b, int32_t dir, int32_t op, const void* init, bool degmax,
+                           int64_t init_max, gs_vertex_out* vout, gs_degree_out* dout);
 static gs_status dist_impl(gs_ctx* c, const gs_edge_batch* b, int32_t dir, int32_t op, const void* init, bool degmax,
+                           int64_t init_max, gs_vertex_out* vout, gs_degree_out* dout) {
+  // The owner-grouped emit (c->oe) is set for this call's local window only: whatever way the call leaves
+  // (a failed counts exchange with a deferred window still pending included), the next plain window of
+  // this ctx must not find it set and write exchange rows instead of its output.
+  struct OeReset {
+    gs_ctx* c;
+    ~OeReset() { c->oe = OwnerEmit{}; }
+  } guard{c};
+  return dist_body(c, b, dir, op, init, degmax, init_max, vout, dout);
+}
+static gs_status dist_body(gs_ctx* c, const gs_edge_batch* b, int32_t dir, int32_t op, const void* init, bool degmax,
                            int64_t init_max, gs_vertex_out* vout, gs_degree_out* dout) {
   if (!c->comm) return set_error(c, GS_EINVAL, "no communicator (gs_comm_init)");
   const uint32_t P = (uint32_t)c->comm_size;

@@ -1371,12 +1371,19 @@ gs_status hashset_order(gs_ctx* c, const int64_t* src, const int64_t* dst, uint6
   const uint32_t B = U > 1 ? 64 - __builtin_clzll(U - 1) : 1;   // bits of a dense vertex rank
   // every id differs from the first in its low s.bits bits (the sort's key mask): a dense rank table when
   // that span is small (R-MAT s23 C5 window: 32 MB; k_hs_prep spent 23 ms in binary searches without it)
+  // Only when the span is within a small multiple of the vertices (a small window with sparse ids would
+  // otherwise take up to 1 GiB), and a table that cannot be allocated leaves the binary search.
   const uint32_t* rank = nullptr;
-  if (s.bits <= HS_RANK_BITS) {
-    GS_TRY(ensure(c, c->hs_rank, (1ull << std::max(s.bits, 1)) * 4));
-    hipLaunchKernelGGL(k_hs_rank, dim3(g256(U)), dim3(256), 0, c->stream, c->hs[HS_VKEYS].as<int64_t>(), (uint32_t)U,
-                       c->hs_rank.as<uint32_t>());
-    rank = c->hs_rank.as<uint32_t>();
+  const uint64_t span = 1ull << std::max(s.bits, 1);
+  if (s.bits <= HS_RANK_BITS && span <= std::max<uint64_t>(16 * U, 1ull << 20)) {
+    if (ensure(c, c->hs_rank, span * 4) == GS_OK) {
+      hipLaunchKernelGGL(k_hs_rank, dim3(g256(U)), dim3(256), 0, c->stream, c->hs[HS_VKEYS].as<int64_t>(), (uint32_t)U,
+                         c->hs_rank.as<uint32_t>());
+      rank = c->hs_rank.as<uint32_t>();
+    } else {
+      (void)hipGetLastError();   // the failed allocation's sticky error: the search needs no table
+      c->err.clear();
+    }
   }
   hipLaunchKernelGGL(k_hs_prep, dim3(g256(R)), dim3(256), 0, c->stream, c->hs[HS_ORD].as<uint32_t>(), (uint32_t)R, src,
                      dst, c->hs[HS_OFF].as<uint64_t>(), c->hs[HS_VKEYS].as<int64_t>(), (uint32_t)U, B, rank,
@@ -1596,6 +1603,10 @@ gs_status gs_candidates_begin_part(gs_ctx* c, const gs_edge_batch* b, uint32_t n
   c->cand_seq = c->call_seq;
   c->cand_total = c->cand_cursor = 0;
   c->cand_U = c->cand_S = 0;
+  // the session's part and id range before the empty-batch return: an empty session after a part
+  // session must not keep the earlier nparts (gs_candidates_vertex_range would refuse it)
+  c->cand_nparts = nparts;
+  c->cand_idmin = c->cand_idmax = 0;
   *total_records = 0;
   if (jdk_flags) *jdk_flags = 0;
   if (b->n == 0) return GS_OK;

@@ -194,6 +194,25 @@ class Engine:
     def _records(n, direction):
         return 2 * n if int(direction) == 2 else n
 
+    def _check_out(self, out, dev: bool, np_dtypes, min_records=None):
+        """out= buffers: device tensors (with device inputs), contiguous, of the dtypes the library writes
+        (it writes 8-byte keys and the op's value width at raw addresses: a narrower or strided tensor
+        would take out-of-bounds or misplaced writes), and at least min_records long when given."""
+        import torch
+
+        tdt = {np.int64: torch.int64, np.int32: torch.int32, np.float32: torch.float32, np.float64: torch.float64}
+        if len(out) != len(np_dtypes):
+            raise ValueError(f"out: {len(np_dtypes)} tensors expected")
+        for t, want in zip(out, np_dtypes):
+            if not (dev and _is_torch(t) and t.is_cuda):
+                raise ValueError("out: device tensors, with device inputs")
+            if t.dtype != tdt[want]:
+                raise ValueError(f"out: dtype {t.dtype}, the library writes {tdt[want]}")
+            if not t.is_contiguous():
+                raise ValueError("out: contiguous tensors")
+            if min_records is not None and t.numel() < min_records:
+                raise ValueError("out: device tensors of at least the window's records")
+
     # -- operators ------------------------------------------------------------------------------
     def reduce(self, src, dst, val, direction, op, out=None):
         """gs_window_reduce: reduceOnEdges with a built-in op. Returns (keys, values) trimmed to U.
@@ -210,9 +229,8 @@ class Engine:
         R = self._records(b.n, direction)
         odt = np.int64 if op == L.GS_OP_COUNT else L.NP_DTYPE[b.val_dtype]
         if out is not None:
+            self._check_out(out, dev, (np.int64, odt), R)
             keys, vals = out
-            if not (dev and _is_torch(keys) and keys.is_cuda and keys.numel() >= R and vals.numel() >= R):
-                raise ValueError("out: device tensors of at least the window's records")
         else:
             keys = self._empty(dev, R, np.int64)
             vals = self._empty(dev, R, odt)
@@ -235,9 +253,8 @@ class Engine:
         b, keep, dev = self._batch(src, dst, None)
         R = self._records(b.n, direction)
         if out is not None:
+            self._check_out(out, dev, (np.int64, np.int64, np.int64), R)
             keys, deg, mx = out
-            if not (dev and _is_torch(keys) and keys.is_cuda and min(x.numel() for x in out) >= R):
-                raise ValueError("out: device tensors of at least the window's records")
         else:
             keys, deg, mx = (self._empty(dev, R, np.int64) for _ in range(3))
         n_out = ctypes.c_uint64(0)
@@ -669,9 +686,8 @@ class Engine:
         b, keep, dev = self._batch(src, dst, None if op == L.GS_OP_COUNT else val)
         odt = np.int64 if op == L.GS_OP_COUNT else L.NP_DTYPE[b.val_dtype]
         if out is not None:
+            self._check_out(out, dev, (np.int64, odt))
             keys, vals = out
-            if not (dev and _is_torch(keys) and keys.is_cuda and _is_torch(vals) and vals.is_cuda):
-                raise ValueError("out: device tensors, with device inputs")
             cap = min(keys.numel(), vals.numel())
         else:
             cap = self._records(b.n, direction) + 1024   # a guess; more owned vertices: gs_fetch_last_output

@@ -79,6 +79,18 @@ class StreamExecutionEnvironment:
     def __init__(self, device: int = 0):
         self.device = device
         self._engine = None
+        self._parallelism = 1
+
+    def setParallelism(self, parallelism: int) -> "StreamExecutionEnvironment":
+        """env.setParallelism: the operators' parallelism; on this path it changes what the windowed
+        graph aggregation emits (one running state per partition's partial, aggregation.py)."""
+        if int(parallelism) < 1:
+            raise ValueError("parallelism must be at least 1")
+        self._parallelism = int(parallelism)
+        return self
+
+    def getParallelism(self) -> int:
+        return self._parallelism
 
     @classmethod
     def getExecutionEnvironment(cls) -> "StreamExecutionEnvironment":
@@ -226,10 +238,11 @@ class SimpleEdgeStream:
         return GraphWindowStream(self, size.toMilliseconds(), EdgeDirection(direction))
 
     # tumbling windows of this stream: [(start, end, columns of that window in arrival order)]
-    def _windows(self, size_ms: int):
+    def _windows(self, size_ms: int, with_index: bool = False):
+        """with_index: each window also carries its records' positions in the stream (arrival order)."""
         e = self.edges
         if e.ts is None:
-            return [(0, size_ms, e)]
+            return [(0, size_ms, e, np.arange(len(e)))] if with_index else [(0, size_ms, e)]
         ts = np.asarray(e.ts, dtype=np.int64)
         start = ts - np.fmod(ts, size_ms)
         order = np.argsort(start, kind="stable")
@@ -244,7 +257,7 @@ class SimpleEdgeStream:
                 cols = EdgeColumns(e.src[sl], e.dst[sl], None if e.val is None else e.val[sl], ts[sl])
             else:
                 cols = EdgeColumns(_take(e.src, idx), _take(e.dst, idx), _take(e.val, idx), ts[idx])
-            out.append((int(s), int(s) + size_ms, cols))
+            out.append((int(s), int(s) + size_ms, cols, idx) if with_index else (int(s), int(s) + size_ms, cols))
         return out
 
 

@@ -13,6 +13,15 @@
  * window's partials (which vertex DisjointSet keeps as root depends on HashMap iteration order and is not
  * observable: ConnectedComponentsTest compares the components), before the watermark is forwarded.  The
  * reference's merger runs at parallelism 1; so does this operator (the whole window on one GPU).
+ *
+ * Parallelism (GraphAggregation.java:103-116, WindowGraphAggregation.java:54-58): at environment
+ * parallelism P the reference folds each of P partitions separately (InitialMapper keys every edge by the
+ * index of the map subtask that saw it) and the Merger emits the running state after EVERY partial, so a
+ * window emits one state per non-empty partition, the last one the state after the whole window.  This
+ * operator keeps that record stream: it deals the edges to P partitions as Flink's rebalance from a
+ * parallelism-1 source does (round robin over arrival order), runs gs_window_components once per non-empty
+ * partition in partition order (one of the orders the partials can reach the merger in) and emits the
+ * state after each.  P = 1: one call and one state per window.
  */
 package org.apache.flink.graph.streaming.gpu;
 
@@ -35,14 +44,18 @@ public class GpuComponentsOperator<EV> extends AbstractStreamOperator<DisjointSe
 		implements OneInputStreamOperator<Edge<Long, EV>, DisjointSet<Long>> {
 
 	private final long windowMs;
+	private final int partitions;   // the reference's fold parallelism: states emitted per window, at most
 
 	private transient long ctx;
-	private transient TreeMap<Long, WindowColumns> open;   // window start -> its edges, in arrival order
+	private transient long seq;                              // records seen: record i -> partition i % partitions
+	private transient TreeMap<Long, WindowColumns[]> open;   // window start -> its edges per partition, in arrival order
 	private transient ByteBuffer keys, labels;             // the running state: m (vertex, label) rows
 	private transient long m;
 
-	public GpuComponentsOperator(long windowMs) {
+	public GpuComponentsOperator(long windowMs, int partitions) {
+		if (partitions < 1) throw new IllegalArgumentException("partitions must be at least 1");
 		this.windowMs = windowMs;
+		this.partitions = partitions;
 	}
 
 	/** SimpleEdgeStream.aggregate(new ConnectedComponents(windowMs)) on the engine. */
@@ -50,7 +63,8 @@ public class GpuComponentsOperator<EV> extends AbstractStreamOperator<DisjointSe
 	public static <EV> DataStream<DisjointSet<Long>> connectedComponents(DataStream<Edge<Long, EV>> edges,
 			long windowMs) {
 		final TypeInformation<DisjointSet<Long>> type = (TypeInformation) TypeExtractor.getForClass(DisjointSet.class);
-		return edges.transform("gpu-connected-components", type, new GpuComponentsOperator<EV>(windowMs))
+		final int p = Math.max(1, edges.getExecutionEnvironment().getParallelism());
+		return edges.transform("gpu-connected-components", type, new GpuComponentsOperator<EV>(windowMs, p))
 				.setParallelism(1);
 	}
 
@@ -59,7 +73,8 @@ public class GpuComponentsOperator<EV> extends AbstractStreamOperator<DisjointSe
 		super.open();
 		ctx = GellyHip.create(GpuBuiltins.deviceFor(getRuntimeContext().getIndexOfThisSubtask()), 0, 0);
 		GellyHip.setTiming(ctx, GellyHip.GS_TIMING_OFF);   // no stage-time events in production
-		open = new TreeMap<Long, WindowColumns>();
+		open = new TreeMap<Long, WindowColumns[]>();
+		seq = 0;
 		keys = GellyHip.direct(8);
 		labels = GellyHip.direct(8);
 		m = 0;
@@ -69,10 +84,12 @@ public class GpuComponentsOperator<EV> extends AbstractStreamOperator<DisjointSe
 	public void processElement(StreamRecord<Edge<Long, EV>> element) throws Exception {
 		final long ts = element.getTimestamp();
 		final long start = ts - ts % windowMs;   // Java remainder, as TumblingEventTimeWindows
-		WindowColumns w = open.get(start);
-		if (w == null) open.put(start, w = new WindowColumns());
+		WindowColumns[] w = open.get(start);
+		if (w == null) open.put(start, w = new WindowColumns[partitions]);
+		final int k = (int) (seq++ % partitions);
+		if (w[k] == null) w[k] = new WindowColumns();
 		final Edge<Long, EV> e = element.getValue();
-		w.add(e.f0, e.f1);
+		w[k].add(e.f0, e.f1);
 	}
 
 	@Override
@@ -95,15 +112,17 @@ public class GpuComponentsOperator<EV> extends AbstractStreamOperator<DisjointSe
 
 	private void fireUpTo(long watermark) {
 		while (!open.isEmpty()) {
-			final Map.Entry<Long, WindowColumns> first = open.firstEntry();
+			final Map.Entry<Long, WindowColumns[]> first = open.firstEntry();
 			final long stamp = first.getKey() + windowMs - 1;
 			if (stamp > watermark) return;
 			open.remove(first.getKey());
-			fire(first.getValue(), stamp);
+			for (WindowColumns part : first.getValue()) {   // a partition without records has no partial
+				if (part != null && part.n > 0) fire(part, stamp);
+			}
 		}
 	}
 
-	/** the state after one window (CombineCC of the running state and the window's UpdateCC fold) */
+	/** the state after one partial (CombineCC of the running state and one partition's UpdateCC fold) */
 	private void fire(WindowColumns w, long stamp) {
 		final long cap = m + 2L * w.n;   // every vertex seen so far at most
 		final ByteBuffer ok = GellyHip.direct(8 * cap), ol = GellyHip.direct(8 * cap);

@@ -321,3 +321,36 @@ def test_reduce_dist_reused_outputs(pkg, oracle, window, P):
     want = oracle.window_reduce(s, d, v, 2, 0)
     for w in range(3):
         check_union([res[r][w] for r in range(P)], want, P)
+
+
+def test_failed_reduce_dist_leaves_plain_reduce_intact(pkg, oracle, window):
+    """A reduce_dist whose counts exchange fails while its local window is deferred (device columns, a
+    speculative second window) must not leave the owner-grouped emit set on the ctx: the next plain
+    reduceOnEdges of that ctx returns its own output (gs_dist.hip dist_impl's reset on every exit).  Rank 1
+    enters WindowTriangles in the second window, so the comm group sees a collective mismatch and both
+    ranks' calls fail with GS_ECOMM; rank 0 then runs a plain window on the same ctx."""
+    s, d = window
+    v = oracle.gen_values(N, 0x5EED0F, oracle.DT_I64)
+    sl = slices(N, 2)
+
+    def fn(r, e):
+        a, b = sl[r]
+        ds, dd, dv = (torch.from_numpy(np.ascontiguousarray(x[a:b])).cuda() for x in (s, d, v))
+        e.reduce_dist(ds, dd, dv, 1, 0)   # window 0: histogram path, measures the buckets
+        with pytest.raises(pkg.GsError) as ei:
+            if r == 0:
+                e.reduce_dist(ds, dd, dv, 1, 0)   # window 1: speculative, deferred read-back
+            else:
+                e.triangles_dist(ds.cpu().numpy(), dd.cpu().numpy())
+        assert ei.value.status == -4
+        if r == 0:
+            k, val = e.reduce(ds, dd, dv, 1, 0)
+            return k.cpu().numpy(), val.cpu().numpy()
+        return None
+
+    res, errs = run_group(pkg, 2, fn, timeout=120)
+    assert not errs, errs
+    a, b = sl[0]
+    want = oracle.window_reduce(s[a:b], d[a:b], v[a:b], 1, 0)
+    assert np.array_equal(res[0][0], want[0])
+    assert np.array_equal(res[0][1], want[1])

@@ -69,3 +69,24 @@ def test_components_config_size(engine, oracle):
     s, d = oracle.gen_rmat(20, 1 << 24, 0x5EED0C)
     want = oracle.components(s, d)
     _same(engine.components(torch.from_numpy(s).cuda(), torch.from_numpy(d).cuda()), want)
+
+
+def test_components_partials_at_parallelism(pkg, oracle):
+    """Environment parallelism 4 (GraphAggregation.java:103-116): one running state per non-empty
+    partition's partial, through gs_window_components, each against the oracle's DisjointSet over the
+    previous state and that partition's records (arrival index mod 4)."""
+    s, d = oracle.gen_rmat(12, 20_000, 0x5EED0D)
+    ts = (np.arange(len(s)) * 2).astype(np.int64)             # windows of 500 records (1000 ms)
+    env = pkg.StreamExecutionEnvironment()
+    env.setParallelism(4)
+    out = pkg.SimpleEdgeStream(pkg.EdgeColumns(s, d, None, ts), env).aggregate(pkg.ConnectedComponents(1000))
+    assert len(out.windows) == 4 * (len(s) // 500)
+    state, i = None, 0
+    for w0 in range(0, len(s), 500):
+        for k in range(4):
+            sel = np.arange(w0, w0 + 500)
+            sel = sel[sel % 4 == k]
+            state = oracle.components(s[sel], d[sel], state)
+            _same(out.windows[i].columns, state)
+            i += 1
+    _same(out.windows[-1].columns, oracle.components(s, d))   # the last state = every edge's components

@@ -64,3 +64,52 @@ def test_candidates_dispatch_marker(pkg):
     from gelly_streaming_amd import triangles
     with pytest.raises(RuntimeError):
         triangles.GenerateCandidateEdges().applyOnEdges(1, [], None)
+
+
+def test_components_emit_one_state_per_partial(pkg, oracle):
+    """ConnectedComponents at environment parallelism P (GraphAggregation.java:103-116, WindowGraphAggregation
+    .java:54-58): the reference's Merger emits the running state after every partition's partial, so a window
+    emits one state per NON-EMPTY partition and the last equals the whole window's state.  The mirror's host
+    logic (partition = arrival index mod P, one gs_window_components call per non-empty partition) with a
+    stub engine whose components() is the oracle's DisjointSet restatement."""
+    class Stub:
+        calls = []
+
+        def components(self, src, dst, prev=None):
+            self.calls.append(len(src))
+            return oracle.components(np.asarray(src), np.asarray(dst), prev)
+
+    src = np.array([1, 1, 2, 1, 6, 8, 3, 10, 12], dtype=np.int64)
+    dst = np.array([2, 3, 3, 5, 7, 9, 4, 11, 13], dtype=np.int64)
+    ts = np.array([0, 10, 20, 30, 40, 50, 60, 400, 410], dtype=np.int64)   # windows of 7 and 2 records
+    env = pkg.StreamExecutionEnvironment()
+    env._engine = Stub()
+    assert env.getParallelism() == 1
+    env.setParallelism(3)
+    out = pkg.SimpleEdgeStream(pkg.EdgeColumns(src, dst, None, ts), env).aggregate(pkg.ConnectedComponents(400))
+    starts = [w.start for w in out.windows]
+    assert starts == [0, 0, 0, 400, 400]                 # 3 partials, then 2 (records 7, 8: partitions 1, 2)
+    assert env._engine.calls == [3, 2, 2, 1, 1]
+    w0 = oracle.components(src[:7], dst[:7])
+    for got, want in ((out.windows[0].columns, oracle.components(src[[0, 3, 6]], dst[[0, 3, 6]])),
+                      (out.windows[2].columns, w0),
+                      (out.windows[4].columns, oracle.components(src[7:], dst[7:], w0))):
+        assert all(np.array_equal(np.asarray(g), np.asarray(x)) for g, x in zip(got, want))
+    env.setParallelism(1)                                 # one state per window
+    Stub.calls = []
+    out1 = pkg.SimpleEdgeStream(pkg.EdgeColumns(src, dst, None, ts), env).aggregate(pkg.ConnectedComponents(400))
+    assert [w.start for w in out1.windows] == [0, 400] and Stub.calls == [7, 2]
+    with pytest.raises(ValueError):
+        env.setParallelism(0)
+
+
+def test_components_operator_partials_contract():
+    """The Java operator keeps the same record stream: P from the environment, round-robin partitions, one
+    gs_window_components call and one emitted state per non-empty partition (source-only: no JDK here)."""
+    from pathlib import Path
+
+    src = (Path(__file__).resolve().parent.parent / "java/src/main/java/org/apache/flink/graph/streaming/gpu/"
+           "GpuComponentsOperator.java").read_text()
+    assert "getExecutionEnvironment().getParallelism()" in src
+    assert "seq++ % partitions" in src
+    assert "if (part != null && part.n > 0) fire(part, stamp);" in src

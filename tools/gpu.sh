@@ -76,7 +76,13 @@ case $MODE in
     bench bench_e2e_direct --workload e2e --staging direct --no-cpu-baseline
     bench bench_e2e_pinned --workload e2e --staging pinned --no-cpu-baseline
     bench bench_e2e_buffered --workload e2e --staging buffered --no-cpu-baseline ;;
+  counters)
+    timeout -k 10 120 rocprofv3 -L > "$O/counters.txt" 2>&1 ;;
+  wr)
+    # where a kernel's WRITE_SIZE comes from: 64-byte vs other write requests and atomics at the fabric
+    pmc pmc_wr/a "TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_64B_sum TCC_EA0_ATOMIC_sum" --steps 3 --warmup 2 "$@"
+    pmc pmc_wr/b "WRITE_SIZE" --steps 3 --warmup 2 "$@" ;;
   *)
-    echo "usage: tools/gpu.sh tests|bench|c2|sq|tri|evidence TAG [args]" >&2; exit 2 ;;
+    echo "usage: tools/gpu.sh tests|bench|c2|sq|tri|evidence|counters|wr TAG [args]" >&2; exit 2 ;;
 esac
 echo "$MODE done"
