@@ -93,6 +93,9 @@ def parse():
     p.add_argument("--cand-windows", type=int, default=2,
                    help="cand_stream: consecutive windows streamed (the next window's sets built while the current "
                         "one's chunks drain)")
+    p.add_argument("--cand-cadence-ms", type=float, default=0,
+                   help="cand_stream: fire window w at w x this many ms (the stream's window cadence, e.g. 1000) "
+                        "instead of back to back; the window latency is measured from each fire")
     p.add_argument("--max-chunks", type=int, default=0,
                    help="cand_stream: stop after this many chunks (profiling passes; 0 = the whole window)")
     p.add_argument("--windows-edges", type=float, default=1e8,
@@ -221,12 +224,21 @@ def triangle_kernel_table(times_list, n):
 
 
 def finish_rows(rows, B):
-    """GB/s and HBM fraction of each kernel on its own bytes, and on the window's §8(d) bytes B."""
+    """GB/s and HBM fraction of each kernel on its own bytes; on the window's §8(d) bytes B only for the
+    kernel that reads the window's columns (B over a small kernel's time is no fraction of anything)."""
     for r in rows.values():
         r["GB/s"] = r["bytes"] / (r["ms"] * 1e-3) / 1e9 if r["ms"] > 0 else 0.0
         r["frac"] = r["GB/s"] / HBM_PEAK_GBS
         r["frac_on_B"] = (B / (r["ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS) if r["ms"] > 0 else 0.0
     return rows
+
+
+def lib_sha16():
+    """sha256 prefix of the library this process runs (GELLY_HIP_LIB or the in-tree build)."""
+    import hashlib
+
+    p = Path(os.environ.get("GELLY_HIP_LIB", ROOT / "gelly-streaming_amd" / "libgellyhip.so"))
+    return hashlib.sha256(p.read_bytes()).hexdigest()[:16] if p.exists() else None
 
 
 def pmc_table():
@@ -492,11 +504,19 @@ def cand_stream_main(a):
     freed = [None, None]   # consumer events after which a buffer may be written again
     sums = []              # per chunk: a, b, flag-word sums (device scalars, read at the end)
     ev_pairs = []          # (emission start, consumer end) per chunk
-    totals, begin_ms, win_end = [], [], []
+    totals, begin_ms, win_end, fire = [], [], [], []
+    cadence = float(a.cand_cadence_ms) / 1e3
+    # host <-> device clock: an event recorded on an idle stream at a known host time maps every later
+    # device event to the host clock (window latency = host fire time -> its last record consumed)
+    ev_ref = torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
+    ev_ref.record(emit_streams[0])
 
     def begin(w):
         eng = engines[w % len(engines)]
+        if cadence > 0:   # the stream's own cadence: window w fires at t0 + w * cadence
+            time.sleep(max(0.0, t0 + w * cadence - time.perf_counter()))
+        fire.append(time.perf_counter())
         tb = time.perf_counter()
         total = eng.candidates_begin(*wins[w])   # (returns after the sets are built: it reads back sizes)
         begin_ms.append((time.perf_counter() - tb) * 1e3)
@@ -559,6 +579,9 @@ def cand_stream_main(a):
         return
     total = sum(totals)
     lat_ms = np.array([e0.elapsed_time(e1) for e0, e1 in ev_pairs])
+    # window latency: from the window's fire (its gs_candidates_begin call) to its last
+    # record consumed on the device
+    wlat_ms = np.array([(ev_ref.elapsed_time(win_end[w]) / 1e3 + t0 - fire[w]) * 1e3 for w in range(len(win_end))])
     s = torch.stack(sums).sum(0).tolist() if sums else [0, 0, 0]
     chk = (s[0] * 31 + s[1] + s[2]) & ((1 << 63) - 1)
     cands = total - 2 * E * W   # every record past the 2E edge records (one per slice(ALL) record) is a candidate
@@ -577,6 +600,15 @@ def cand_stream_main(a):
                        "chunks": nchunk, "chunk_records": cap, "begin_ms": begin_ms,
                        "chunk_latency_ms_p50": float(np.percentile(lat_ms, 50)),
                        "chunk_latency_ms_p99": float(np.percentile(lat_ms, 99)),
+                       "window_latency_ms": [round(x, 1) for x in wlat_ms.tolist()],
+                       "window_latency_ms_p50": float(np.percentile(wlat_ms, 50)),
+                       "window_latency_ms_p99": float(np.percentile(wlat_ms, 99)),
+                       "window_fire": (f"every {a.cand_cadence_ms:g} ms (the stream's window cadence)" if cadence > 0
+                                       else "back to back (each window fires as soon as the previous one's chunks "
+                                            "are enqueued)"),
+                       "window_latency_definition": "window fire (gs_candidates_begin call, host clock) -> the "
+                                                    "consumer's end event of its last chunk (device clock mapped "
+                                                    "to the host's)",
                        "window_period_s": period, "sustained_edges_per_s": E / period,
                        "target_edges_per_s": 1e8, "checksum": int(chk), "consumer": a.cand_consumer,
                        "id_columns": ("uint32, id - the window's smallest id (gs_candidates_next_u32)" if u32
@@ -590,26 +622,35 @@ def cand_stream_main(a):
                          "algorithmic_bytes_per_launch": rec_bytes * total, "avg_launch_ms": elapsed * 1e3},
             "cpu_baseline": None}
     if not a.no_cpu_baseline:
-        line["cpu_baseline"] = cand_cpu_baseline(E)
+        cpu = cand_cpu_baseline(E)
+        cpu["gpu_over_cpu"] = round(line["value"] / cpu["value"], 1)
+        cpu["window_s_equivalent"] = round(total / W / cpu["value"], 1)   # this window's records at the CPU rate
+        line["cpu_baseline"] = cpu
     emit(line)
     for e in engines:
         e.close()
 
 
-def cand_cpu_baseline(E):
-    """The oracle's GenerateCandidateEdges (gso_window_candidates: the reference's JDK HashSet order) on a
-    bounded sample: the first 2^20 edges of the same R-MAT scale-23 stream as one window, one thread,
-    records/s (the whole 1e8-edge window emits 1.6e11 records, days of one CPU thread)."""
+def cand_cpu_baseline(E, sample_log2=24, threads=None):
+    """The oracle's GenerateCandidateEdges (the reference's JDK HashSet order) over min(16, nproc) threads WITH
+    a consumer that reads every record back (gso_candidates_mt: per-thread chunks of 2^20 records, each summed
+    column by column before it is reused -- the GPU line's device consumer), on the largest sample that keeps
+    the CPU leg within ~10-30 s: the first 2^sample_log2 edges of the same R-MAT scale-23 stream as one
+    window (the whole 1e8-edge window emits 1.6e11 records, minutes of 16 CPU threads).  The CSR build inside
+    it runs on one thread, as in gso_window_candidates."""
     orc = ge.load_oracle()
-    n = 1 << 20
+    threads = threads or max(1, min(16, os.cpu_count() or 1))
+    n = min(E, 1 << sample_log2)
     s, d = orc.gen_rmat(23, n, 0x5EED05)
+    orc.candidates_mt(s[: n // 16], d[: n // 16], threads)   # warm-up
     t = time.perf_counter()
-    ra = orc.window_candidates(s, d)[0]
+    recs, _ = orc.candidates_mt(s, d, threads)
     dt = time.perf_counter() - t
-    return {"value": len(ra) / dt, "unit": "records/s", "cores": 1, "kind": "port",
-            "sample": f"first 2^20 edges of the R-MAT s23 stream as one window ({len(ra)} records), "
-                      f"oracle gso_window_candidates, 1 thread, {dt:.1f} s",
-            **host_cpu()}
+    return {"value": recs / dt, "unit": "records/s", "cores": threads, "kind": "port",
+            "sample": f"first 2^{sample_log2} edges of the R-MAT s23 stream as one window ({recs} records), "
+                      f"oracle gso_candidates_mt (emission + a consumer summing every chunk's columns), "
+                      f"{threads} threads, {dt:.1f} s",
+            "window_s_equivalent": None, **host_cpu()}
 
 
 def parse_main(a):
@@ -1013,11 +1054,30 @@ def main():
                                  "ms": round(ms_step, 4)},
                 "window_traffic_pmc": pmc_window,
                 "window_traffic_over_B": round(pmc_window / B, 3) if pmc_window else None,
+                "traffic_source": ({"file": "profiles/pmc_traffic.json", **pmc.get("_meta", {}),
+                                    "running_lib_sha16": lib_sha16(),
+                                    "same_build": pmc.get("_meta", {}).get("lib_sha16") == lib_sha16()}
+                                   if pmc_dom is not None or pmc_window else None),
                 "timing": ("device events on the library's stream (gs_last_stage_times) around the scatter and the "
                            "accumulate inside the timed region (gs_set_timing DOMINANT); the other stages on 3 "
                            "windows after it with every stage event") if lean else
                           "device events on the library's stream around each launch (gs_last_stage_times)"}
 
+    if a.workload == "reduce" and "bucket_accumulate" in kt and dom_name in ("sp_scatter_pack", "sp_scatter",
+                                                                            "dp_scatter_pack", "dp_scatter"):
+        # north_star's segmented reduce = the partition scatter + the LDS accumulate: B over both kernels'
+        # time; and the accumulate alone on its own bytes (the PMC bytes when the table has them)
+        acc = kt["bucket_accumulate"]
+        t_seg = (dom["ms"] + acc["ms"]) * 1e-3
+        acc_b = pmc.get("bucket_accumulate", {}).get("bytes_per_launch") or acc["bytes"]
+        roofline["segmented_reduce"] = {
+            "kernels": f"{dom_name} + bucket_accumulate", "ms": round(t_seg * 1e3, 4),
+            "achieved": round(B / t_seg / 1e9, 1), "frac": round(B / t_seg / 1e9 / HBM_PEAK_GBS, 4),
+            "formula": "B / (scatter + accumulate device time)",
+            "accumulate": {"ms": round(acc["ms"], 4), "bytes": acc_b,
+                           "bytes_source": "PMC" if pmc.get("bucket_accumulate") else "algorithmic",
+                           "achieved": round(acc_b / (acc["ms"] * 1e-3) / 1e9, 1) if acc["ms"] > 0 else 0.0,
+                           "frac": round(acc_b / (acc["ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4) if acc["ms"] > 0 else 0.0}}
     if a.workload == "triangles":
         # the count step is bound by LDS reads, not HBM: one 16-byte bucket read per hash probe ->
         # 128 B/clk/CU x 256 CUs x 2.4 GHz / 16 B = 4.9 T probes/s (MI355X_MICROARCH.md LDS bandwidth)
@@ -1032,14 +1092,21 @@ def main():
         # 4 B per entry, sum over the oriented edges u -> v of d+(u) + d+(v) (gs_stage_times.escapes, path 3)
         ment = statistics.mean(t.escapes for t in times)
         mb = 4 * ment
-        whole_s = ms_step * 1e-3
-        roofline["merge_intersection_term"] = {
-            "bytes_per_window": int(mb), "formula": "4 * sum over oriented edges u->v of (d+(u) + d+(v))",
-            "over_16E": round(mb / B, 2),
-            "window_16E_plus_term": {"achieved": round((B + mb) / whole_s / 1e9 / world, 1), "unit": "GB/s",
-                                     "frac": round((B + mb) / whole_s / 1e9 / world / HBM_PEAK_GBS, 4)},
-            "count_kernels_on_term": {"achieved": round(mb / t_cnt / 1e9, 1) if t_cnt > 0 else 0.0, "unit": "GB/s",
-                                      "frac": round(mb / t_cnt / 1e9 / HBM_PEAK_GBS, 4) if t_cnt > 0 else 0.0}}
+        # The count is bound by its LDS probes, not by HBM: the probe roofline governs the line.  The HBM
+        # figures of the edge-list term stay beside it; the merge-intersection term is reported as bytes only
+        # (the count does not read those bytes -- it probes hash sets / bitmaps -- so bytes over its time would
+        # be no fraction of anything: above 1 on every window)
+        hbm = {k: roofline.pop(k) for k in list(roofline) if k not in ("probe_roofline",)}
+        pr = roofline.pop("probe_roofline")
+        roofline.update({"bound": "lds", "kernel": pr["kernel"], "achieved": pr["achieved"], "peak": pr["peak"],
+                         "unit": pr["unit"], "frac": pr["frac"], "traffic": None,
+                         "probes_per_window": pr["probes_per_window"], "peak_formula": pr["peak_formula"],
+                         "hbm_edge_list_term": hbm,
+                         "merge_intersection_term": {
+                             "bytes_per_window": int(mb), "formula": "4 * sum over oriented edges u->v of (d+(u) + d+(v))",
+                             "over_16E": round(mb / B, 2),
+                             "note": "what a per-edge merge intersection would read; the count reads one 4-byte list "
+                                     "item per probe instead (probes_per_window)"}})
 
     cpu = None
     threads = max(1, min(16, os.cpu_count() or 1))
@@ -1108,7 +1175,8 @@ def main():
             "roofline": roofline,
             "cpu_baseline": cpu,
             "kernels": {n: {"avg_ms": round(r["ms"], 4), "own_bytes": r["bytes"], "GB/s": round(r["GB/s"], 1),
-                            "frac": round(r["frac"], 4), "frac_on_B": round(r["frac_on_B"], 4)}
+                            "frac": round(r["frac"], 4),
+                            **({"frac_on_B": round(r["frac_on_B"], 4)} if n == dom_name else {})}
                         for n, r in kt.items()},
         }
         emit(line)

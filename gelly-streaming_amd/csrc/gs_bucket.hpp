@@ -39,6 +39,14 @@ constexpr int BK_INFO_BLOCK = 512;
 #ifndef GS_BK_ACC_PER_CU
 #define GS_BK_ACC_PER_CU 1
 #endif
+#ifndef GS_BK_PREFETCH
+#define GS_BK_PREFETCH 0   // k_bk_accum: the next item's first loads issued before the current item's finalize
+                           // (A/B, round 6: accumulate 0.2560 -> 0.2728 ms on C2 -- the barrier after the finalize
+                           // waits for them, so they hide nothing and hold VGPRs: off)
+#endif
+#ifndef GS_BK_FUSED_RESET
+#define GS_BK_FUSED_RESET 1   // k_bk_accum: each wave resets its own finalized entries (no block-wide init pass)
+#endif
 #ifndef GS_BK_S8
 #define GS_BK_S8 14   // 2^S vertices per bucket with 8-byte accumulators (BkVal)
 #endif
@@ -162,6 +170,12 @@ struct BkVal {
     for (uint32_t i = tid; i < W; i += BK_ACC_BLOCK) s.acc[i] = identity();
     for (uint32_t i = tid; i < PW; i += BK_ACC_BLOCK) s.pm[i] = 0;
   }
+  // entries [lo, hi) back to the identity by one wave (lo, hi multiples of 32: whole presence words)
+  __device__ static void init_range(Lds& s, uint32_t lo, uint32_t hi, int lane) {
+    for (uint32_t i = lo + lane; i < hi; i += WAVE) s.acc[i] = identity();
+    constexpr uint32_t PER_WORD = PB ? 4 : 32;
+    for (uint32_t i = lo / PER_WORD + lane; i < hi / PER_WORD; i += WAVE) s.pm[i] = 0;
+  }
   __device__ static void add(Lds& s, uint32_t i, Raw r) {
     const T v = bits_as<T>(r);
     if constexpr (OP == OP_SUM) {
@@ -267,6 +281,9 @@ struct BkCount {
   __device__ static void init(Lds& s, int tid) {
     for (uint32_t i = tid; i < W; i += BK_ACC_BLOCK) s.cnt[i] = 0;
   }
+  __device__ static void init_range(Lds& s, uint32_t lo, uint32_t hi, int lane) {
+    for (uint32_t i = lo + lane; i < hi; i += WAVE) s.cnt[i] = 0;
+  }
   __device__ static void add(Lds& s, uint32_t i, Raw) { atomicAdd(&s.cnt[i], 1u); }
   __device__ static bool present(const Lds& s, uint32_t i) { return s.cnt[i] != 0; }
   __device__ static void stage(BkStage st, uint32_t pos, const Lds& s, uint32_t i) { ((uint32_t*)st.a)[pos] = s.cnt[i]; }
@@ -301,6 +318,12 @@ struct BkDeg {
   };
   __device__ static void init(Lds& s, int tid) {
     for (uint32_t i = tid; i < W; i += BK_ACC_BLOCK) {
+      s.cnt[i] = 0;
+      s.mx[i] = std::numeric_limits<long long>::lowest();
+    }
+  }
+  __device__ static void init_range(Lds& s, uint32_t lo, uint32_t hi, int lane) {
+    for (uint32_t i = lo + lane; i < hi; i += WAVE) {
       s.cnt[i] = 0;
       s.mx[i] = std::numeric_limits<long long>::lowest();
     }
@@ -354,6 +377,12 @@ struct BkDeg32 {
   };
   __device__ static void init(Lds& s, int tid) {
     for (uint32_t i = tid; i < W; i += BK_ACC_BLOCK) {
+      s.cnt[i] = 0;
+      s.mx[i] = 0;
+    }
+  }
+  __device__ static void init_range(Lds& s, uint32_t lo, uint32_t hi, int lane) {
+    for (uint32_t i = lo + lane; i < hi; i += WAVE) {
       s.cnt[i] = 0;
       s.mx[i] = 0;
     }
@@ -1277,6 +1306,17 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t x, uint32_t* s_w, u
   return off + inc - x;
 }
 
+// The bucket a thread reserves (k of its BPT): k-major (tid + k * BLOCK), so one wave-instruction of
+// the reservation atomics covers 64 consecutive cursors -- 256 B, four 64-byte atomic transactions at the
+// memory side -- instead of 64 cursors two apart (eight transactions).  The run order inside a tile follows
+// the threads and is free (a run is contiguous either way).  A/B: GS_SPK_KMAJOR=0 (tid * BPT + k).
+#ifndef GS_SPK_VEC
+#define GS_SPK_VEC 1   // k_sp_scatter_pack: two records per lane and 16-byte column loads on full aligned tiles
+#endif
+#ifndef GS_SPK_KMAJOR
+#define GS_SPK_KMAJOR 1
+#endif
+#define SP_BK(k) (GS_SPK_KMAJOR ? (uint32_t)tid + (uint32_t)(k) * (uint32_t)BLOCK : (uint32_t)tid * BPT + (uint32_t)(k))
 template <typename V, int DIR, int NB>
 __global__ __launch_bounds__(SPK_BLOCK) __attribute__((amdgpu_waves_per_eu(GS_SPK_WAVES, GS_SPK_WAVES)))
 void k_sp_scatter_pack(BaseSrc<V, DIR, PAY_VAL> es, uint64_t n, int S, uint32_t nbp,
@@ -1323,27 +1363,56 @@ void k_sp_scatter_pack(BaseSrc<V, DIR, PAY_VAL> es, uint64_t n, int S, uint32_t 
   // this thread's buckets (BPT consecutive ones): their segment ends, issued before the columns
   uint32_t send[BPT];
 #pragma unroll
-  for (int k = 0; k < BPT; ++k) send[k] = cursor[SP_END_OFF + xs * BK_MAXB + min((uint32_t)tid * BPT + k, nbp - 1)];
+  for (int k = 0; k < BPT; ++k) send[k] = cursor[SP_END_OFF + xs * BK_MAXB + min(SP_BK(k), nbp - 1)];
   cursor += xs * BK_MAXB;
-  // loads: unconditional, clamped into the tile (k_dp_scatter)
+  // loads: unconditional, clamped into the tile (k_dp_scatter).  Full OUT / IN tiles of 16-byte aligned
+  // columns (GS_SPK_VEC): two consecutive records per lane and load -- 16-byte key loads (and 16- or 8-byte
+  // value loads) instead of 8-byte ones, half the load instructions for the same bytes; record u of a
+  // thread is then 2 ((u >> 1) BLOCK + tid) + (u & 1) of the tile (jof), which the ranking, the escapes and
+  // the dead-lane check use -- the LDS slots and the stores do not depend on it.
+  const int64_t* kcol = DIR == DIR_IN ? es.dst : es.src;
+  const bool vec = GS_SPK_VEC && DIR != DIR_ALL && nrec == TILE &&
+                   ((((uintptr_t)kcol) | ((uintptr_t)es.val)) & 15u) == 0;
+  auto jof = [&](int u) -> uint32_t {
+    return vec ? 2u * ((uint32_t)(u >> 1) * BLOCK + tid) + (uint32_t)(u & 1) : (uint32_t)u * BLOCK + tid;
+  };
   int64_t kk[ITEMS];
   V vv[ITEMS];
+  if (vec) {
 #pragma unroll
-  for (int u = 0; u < ITEMS; ++u) {
-    const uint32_t r = r0 + min((uint32_t)u * BLOCK + tid, nrec - 1);
-    uint32_t i = r;
-    bool rev = DIR == DIR_IN;
-    if constexpr (DIR == DIR_ALL) {
-      i = r >> 1;
-      rev = r & 1u;
+    for (int u = 0; u < ITEMS; u += 2) {
+      const uint32_t r = r0 + 2u * ((uint32_t)(u >> 1) * BLOCK + tid);
+      const ulonglong2 k2 = *reinterpret_cast<const ulonglong2*>(kcol + r);
+      kk[u] = (int64_t)k2.x;
+      kk[u + 1] = (int64_t)k2.y;
+      if constexpr (sizeof(V) == 8) {
+        const ulonglong2 v2 = *reinterpret_cast<const ulonglong2*>(es.val + r);
+        vv[u] = (V)v2.x;
+        vv[u + 1] = (V)v2.y;
+      } else {
+        const uint2 v2 = *reinterpret_cast<const uint2*>(es.val + r);
+        vv[u] = (V)v2.x;
+        vv[u + 1] = (V)v2.y;
+      }
     }
+  } else {
+#pragma unroll
+    for (int u = 0; u < ITEMS; ++u) {
+      const uint32_t r = r0 + min((uint32_t)u * BLOCK + tid, nrec - 1);
+      uint32_t i = r;
+      bool rev = DIR == DIR_IN;
+      if constexpr (DIR == DIR_ALL) {
+        i = r >> 1;
+        rev = r & 1u;
+      }
 #if GS_SPK_NT   // A/B: the columns are read once: non-temporal loads
-    kk[u] = __builtin_nontemporal_load(&(rev ? es.dst : es.src)[i]);
-    vv[u] = __builtin_nontemporal_load(&es.val[i]);
+      kk[u] = __builtin_nontemporal_load(&(rev ? es.dst : es.src)[i]);
+      vv[u] = __builtin_nontemporal_load(&es.val[i]);
 #else
-    kk[u] = (rev ? es.dst : es.src)[i];
-    vv[u] = es.val[i];
+      kk[u] = (rev ? es.dst : es.src)[i];
+      vv[u] = es.val[i];
 #endif
+    }
   }
   for (uint32_t i = tid; i < nbp; i += BLOCK) s_cnt[i] = 0;
   if (tid == 0) s_cnt[NB] = 0;
@@ -1353,7 +1422,7 @@ void k_sp_scatter_pack(BaseSrc<V, DIR, PAY_VAL> es, uint64_t n, int S, uint32_t 
   uint32_t ovf = 0;
 #pragma unroll
   for (int u = 0; u < ITEMS; ++u) {
-    const uint32_t j = (uint32_t)u * BLOCK + tid;
+    const uint32_t j = jof(u);
     const uint64_t d = (uint64_t)kk[u] - (uint64_t)es.base;
     const bool in = (d >> S) < nbp, live = j < nrec;
     ovf += (live && !in) ? 1u : 0u;
@@ -1369,12 +1438,12 @@ void k_sp_scatter_pack(BaseSrc<V, DIR, PAY_VAL> es, uint64_t n, int S, uint32_t 
   uint32_t cb[BPT], ob[BPT], sum = 0;
 #pragma unroll
   for (int k = 0; k < BPT; ++k) {
-    const uint32_t b = (uint32_t)tid * BPT + k;
+    const uint32_t b = SP_BK(k);
     cb[k] = b < nbp ? s_cnt[b] : 0u;
     sum += cb[k];
   }
 #pragma unroll
-  for (int k = 0; k < BPT; ++k) ob[k] = cb[k] ? atomicAdd(&cursor[(uint32_t)tid * BPT + k], cb[k]) : 0u;
+  for (int k = 0; k < BPT; ++k) ob[k] = cb[k] ? atomicAdd(&cursor[SP_BK(k)], cb[k]) : 0u;
   uint32_t total;
   uint32_t st = block_excl_scan<BLOCK>(sum, s_w, total);   // total: records in the predicted range
   // A run that does not fit its segment goes to the trash area [trash, trash + TILE) past every region,
@@ -1385,7 +1454,7 @@ void k_sp_scatter_pack(BaseSrc<V, DIR, PAY_VAL> es, uint64_t n, int S, uint32_t 
 #pragma unroll
   for (int k = 0; k < BPT; ++k) {
     sb[k] = st;
-    if ((uint32_t)tid * BPT + k < NB) s_st[(uint32_t)tid * BPT + k] = st;
+    if (SP_BK(k) < NB) s_st[SP_BK(k)] = st;
     st += cb[k];
   }
   if (tid == 0) s_st[NB] = total;   // the dummy run: the tile's last
@@ -1394,13 +1463,13 @@ void k_sp_scatter_pack(BaseSrc<V, DIR, PAY_VAL> es, uint64_t n, int S, uint32_t 
   for (int u = 0; u < ITEMS; ++u) {
     const uint32_t b = (kb[u] >> 16) & 0x7FFFu;
     const uint32_t packed = (kb[u] & 0xFFFFu) | (vr[u] & 0xFFFF0000u);
-    s_slot[s_st[b] + (vr[u] & 0xFFFFu)] = ((uint64_t)packed << 32) | (((uint32_t)u * BLOCK + tid) << 12) | b;
+    s_slot[s_st[b] + (vr[u] & 0xFFFFu)] = ((uint64_t)packed << 32) | (jof(u) << 12) | b;
   }
 #pragma unroll
   for (int k = 0; k < BPT; ++k) {
     const bool drop = cb[k] && ob[k] + cb[k] > send[k];
     ovf += drop ? 1u : 0u;
-    if ((uint32_t)tid * BPT + k < NB) s_del[(uint32_t)tid * BPT + k] = drop ? trash : ob[k] - sb[k];
+    if (SP_BK(k) < NB) s_del[SP_BK(k)] = drop ? trash : ob[k] - sb[k];
   }
   if (tid == 0) s_del[NB] = trash;
   __syncthreads();
@@ -1423,7 +1492,7 @@ void k_sp_scatter_pack(BaseSrc<V, DIR, PAY_VAL> es, uint64_t n, int S, uint32_t 
   for (int k = 0; k < BPT; ++k) {
     const bool drop = cb[k] && ob[k] + cb[k] > send[k];
     ovf += drop ? 1u : 0u;
-    if ((uint32_t)tid * BPT + k < NB) s_run[(uint32_t)tid * BPT + k] = ((uint64_t)(drop ? trash + st : ob[k]) << 32) | st;
+    if (SP_BK(k) < NB) s_run[SP_BK(k)] = ((uint64_t)(drop ? trash + st : ob[k]) << 32) | st;
     st += cb[k];
   }
   if (tid == 0) s_run[NB] = ((uint64_t)(trash + total) << 32) | total;   // the dummy run: the tile's last
@@ -1447,7 +1516,7 @@ void k_sp_scatter_pack(BaseSrc<V, DIR, PAY_VAL> es, uint64_t n, int S, uint32_t 
       ru = q == u ? vr[q] : ru;
     }
     const uint32_t g = (uint32_t)(s_run[(ku >> 16) & 0x7FFFu] >> 32) + (ru & 0xFFFFu);
-    wide[g] = es.val[col_index((uint32_t)u * BLOCK + tid)];
+    wide[g] = es.val[col_index(jof(u))];
   }
   __syncthreads();
 #pragma unroll
@@ -1530,28 +1599,61 @@ __global__ __launch_bounds__(SPU_BLOCK) __attribute__((amdgpu_waves_per_eu(4))) 
   const uint32_t xs = SP_NSEG == 1 ? 0u : blockIdx.x & xmask;
   uint32_t send[BPT];
 #pragma unroll
-  for (int k = 0; k < BPT; ++k) send[k] = sp_hi(cursor, xs, min((uint32_t)tid * BPT + k, nbp - 1));
+  for (int k = 0; k < BPT; ++k) send[k] = sp_hi(cursor, xs, min(SP_BK(k), nbp - 1));
   cursor += xs * BK_MAXB;
   int64_t kk[ITEMS];
   V vv[ITEMS];
+  // full OUT / IN tiles of 16-byte aligned columns: two records per lane and load, as k_sp_scatter_pack
+  // (GS_SPK_VEC; record u of a thread is jof(u) of the tile, which only the dead-lane check uses)
+  static_assert(ITEMS % 2 == 0, "two records per lane and load");
+  const int64_t* kcol = DIR == DIR_IN ? es.dst : es.src;
+  const void* pcol = PAY == PAY_VAL ? (const void*)es.val : PAY == PAY_NBR ? (const void*)(DIR == DIR_IN ? es.src : es.dst)
+                                                                          : (const void*)kcol;
+  const bool vec = GS_SPK_VEC && DIR != DIR_ALL && nrec == TILE && ((((uintptr_t)kcol) | ((uintptr_t)pcol)) & 15u) == 0;
+  auto jof = [&](int u) -> uint32_t {
+    return vec ? 2u * ((uint32_t)(u >> 1) * BLOCK + tid) + (uint32_t)(u & 1) : (uint32_t)u * BLOCK + tid;
+  };
+  if (vec) {
 #pragma unroll
-  for (int u = 0; u < ITEMS; ++u) {   // every load first, unconditional and clamped into the tile
-    const uint32_t r = r0 + min((uint32_t)u * BLOCK + tid, nrec - 1);
-    uint32_t i = r;
-    bool rev = DIR == DIR_IN;
-    if constexpr (DIR == DIR_ALL) {
-      i = r >> 1;
-      rev = r & 1u;
+    for (int u = 0; u < ITEMS; u += 2) {
+      const uint32_t r = r0 + 2u * ((uint32_t)(u >> 1) * BLOCK + tid);
+      const ulonglong2 k2 = *reinterpret_cast<const ulonglong2*>(kcol + r);
+      kk[u] = (int64_t)k2.x;
+      kk[u + 1] = (int64_t)k2.y;
+      if constexpr (PAY == PAY_NBR) {
+        const ulonglong2 v2 = *reinterpret_cast<const ulonglong2*>((const int64_t*)pcol + r);
+        vv[u] = (V)v2.x;
+        vv[u + 1] = (V)v2.y;
+      } else if constexpr (PAY == PAY_VAL && sizeof(V) == 8) {
+        const ulonglong2 v2 = *reinterpret_cast<const ulonglong2*>(es.val + r);
+        vv[u] = __builtin_bit_cast(V, v2.x);
+        vv[u + 1] = __builtin_bit_cast(V, v2.y);
+      } else if constexpr (PAY == PAY_VAL && sizeof(V) == 4) {
+        const uint2 v2 = *reinterpret_cast<const uint2*>(es.val + r);
+        vv[u] = __builtin_bit_cast(V, v2.x);
+        vv[u + 1] = __builtin_bit_cast(V, v2.y);
+      }
     }
-    kk[u] = (rev ? es.dst : es.src)[i];
-    if constexpr (PAY == PAY_VAL) vv[u] = es.val[i];
-    else if constexpr (PAY == PAY_NBR) vv[u] = (V)(rev ? es.src : es.dst)[i];
+  } else {
+#pragma unroll
+    for (int u = 0; u < ITEMS; ++u) {   // every load first, unconditional and clamped into the tile
+      const uint32_t r = r0 + min((uint32_t)u * BLOCK + tid, nrec - 1);
+      uint32_t i = r;
+      bool rev = DIR == DIR_IN;
+      if constexpr (DIR == DIR_ALL) {
+        i = r >> 1;
+        rev = r & 1u;
+      }
+      kk[u] = (rev ? es.dst : es.src)[i];
+      if constexpr (PAY == PAY_VAL) vv[u] = es.val[i];
+      else if constexpr (PAY == PAY_NBR) vv[u] = (V)(rev ? es.src : es.dst)[i];
+    }
   }
   uint32_t ovf = 0, kb[ITEMS];
   bool bad = false;
 #pragma unroll
   for (int u = 0; u < ITEMS; ++u) {
-    const uint32_t j = (uint32_t)u * BLOCK + tid;
+    const uint32_t j = jof(u);
     const uint64_t d = (uint64_t)kk[u] - (uint64_t)es.base;
     const bool in = (d >> S) < nbp, live = j < nrec;
     ovf += (live && !in) ? 1u : 0u;
@@ -1581,19 +1683,19 @@ __global__ __launch_bounds__(SPU_BLOCK) __attribute__((amdgpu_waves_per_eu(4))) 
   uint32_t cb[BPT], ob[BPT], sum = 0;
 #pragma unroll
   for (int k = 0; k < BPT; ++k) {
-    const uint32_t b = (uint32_t)tid * BPT + k;
+    const uint32_t b = SP_BK(k);
     cb[k] = b < nbp ? s_cnt[b] : 0u;
     sum += cb[k];
   }
 #pragma unroll
-  for (int k = 0; k < BPT; ++k) ob[k] = cb[k] ? atomicAdd(&cursor[(uint32_t)tid * BPT + k], cb[k]) : 0u;
+  for (int k = 0; k < BPT; ++k) ob[k] = cb[k] ? atomicAdd(&cursor[SP_BK(k)], cb[k]) : 0u;
   uint32_t total;
   uint32_t st = block_excl_scan<BLOCK>(sum, s_w, total);   // (bk_block_scan assumes 1024 threads)
   uint32_t sb[BPT];
 #pragma unroll
   for (int k = 0; k < BPT; ++k) {
     sb[k] = st;
-    s_cnt[(uint32_t)tid * BPT + k] = st;   // (entries past nbp are never read)
+    s_cnt[SP_BK(k)] = st;   // (entries past nbp are never read)
     st += cb[k];
   }
   if (tid == 0) s_cnt[NB] = total;
@@ -1613,7 +1715,7 @@ __global__ __launch_bounds__(SPU_BLOCK) __attribute__((amdgpu_waves_per_eu(4))) 
 #pragma unroll
   for (int k = 0; k < BPT; ++k) {
     const bool drop = cb[k] && ob[k] + cb[k] > send[k];
-    s_delta[(uint32_t)tid * BPT + k] = (drop ? trash : ob[k]) - sb[k];
+    s_delta[SP_BK(k)] = (drop ? trash : ob[k]) - sb[k];
     ovf += drop ? 1u : 0u;
   }
   if (tid == 0) s_delta[NB] = trash;
@@ -1643,8 +1745,10 @@ __global__ __launch_bounds__(SPU_BLOCK) __attribute__((amdgpu_waves_per_eu(4))) 
 // ---- k_bk_accum: persistent; LDS accumulation of (bucket, record range) items ---------------------
 // Finalize (shared with k_bk_merge): the bucket's vertices in ascending order -> staging at the
 // bucket's record offset (a bucket has at least as many records as vertices).
-template <class P>
-__device__ __forceinline__ void bk_finalize(const typename P::Lds& s, uint32_t bucket, uint32_t stage_at,
+// RESET (k_bk_accum): each wave then returns its own entries to the identity -- the next item needs no
+// block-wide init pass and no barrier for it.
+template <class P, bool RESET = false>
+__device__ __forceinline__ void bk_finalize(typename P::Lds& s, uint32_t bucket, uint32_t stage_at,
                                             BkStage st, uint32_t* bucket_count, uint32_t* s_wc) {
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   constexpr uint32_t PER = P::W / BK_NW;   // entries per wave
@@ -1672,6 +1776,10 @@ __device__ __forceinline__ void bk_finalize(const typename P::Lds& s, uint32_t b
     }
     off += (uint32_t)__popcll(m);
   }
+  if constexpr (RESET) {
+    static_assert(PER % 32 == 0, "a wave's entries are whole presence words");
+    P::init_range(s, e0, e0 + PER, lane);
+  }
   if (tid == 0) bucket_count[bucket] = tot;
 }
 
@@ -1679,6 +1787,12 @@ __device__ __forceinline__ void bk_finalize(const typename P::Lds& s, uint32_t b
 constexpr uint32_t BK_TRACE_MAX = 16384;
 __device__ uint64_t g_bk_trace[BK_TRACE_MAX][4];
 #endif
+// The item loop is pipelined (round 6): wave 0 claims the NEXT item, reads its descriptor and bucket start,
+// computes its pieces (speculative packed partition) and loads their unaligned head / tail records while the
+// other waves finish the current item's stream; the block then finalizes the current item, re-initializes
+// the table and starts the next one with all of that already in LDS and registers.  Before, each item began
+// with a chain of dependent global-memory latencies (claim -> descriptor -> bucket start -> segment bounds ->
+// head / tail records, one record after another) behind two barriers, with no stream load in flight on the CU.
 template <class P, class Src, int UNROLL>
 __global__ __launch_bounds__(BK_ACC_BLOCK) void k_bk_accum(Src src, const BkItem* __restrict__ items,
                                                            const uint32_t* __restrict__ n_items_p,
@@ -1689,47 +1803,116 @@ __global__ __launch_bounds__(BK_ACC_BLOCK) void k_bk_accum(Src src, const BkItem
                                                            const unsigned long long* __restrict__ mm,
                                                            const uint32_t* __restrict__ seg_cur) {
   __shared__ typename P::Lds s;
-  __shared__ uint32_t s_item;
+  __shared__ uint32_t s_item[2], s_b0[2];   // two slots: the current item and the one wave 0 stages
+  __shared__ BkItem s_m[2];
   __shared__ uint32_t s_wc[BK_NW];
-  __shared__ uint32_t s_pre4[SP_NSEG + 1], s_qb[SP_NSEG];   // packed records: the item's pieces as one stream
+  __shared__ uint32_t s_pre4[2][SP_NSEG + 1], s_qb[2][SP_NSEG];   // packed records: the item's pieces as one stream
   using Raw = typename P::Raw;
-  const int tid = threadIdx.x;
+  constexpr bool PACKED = is_pack_src<Src>::value;
+  const int tid = threadIdx.x, lane = tid & (WAVE - 1);
   if (mm[2]) return;   // keys outside the predicted range: the window is rerun
   const uint32_t n_items = *n_items_p;
-  for (;;) {
-    if (tid == 0) s_item = atomicAdd(ctr, 1u);
-    __syncthreads();
-    const uint32_t it = s_item;
-    if (it >= n_items) break;
+  // packed records: one record into LDS (the value from `wide` when escaped)
+  auto add1 = [&](const auto& sr, uint32_t q, uint32_t x) {
+    const uint32_t v16 = x >> 16;
+    const bool esc = v16 == PK_ESC;
+    if constexpr (has_add_packed<P>::value) P::add_packed(s, x & (P::W - 1), !esc ? (Raw)v16 : (Raw)sr.wide[q], esc);
+    else P::add(s, x & (P::W - 1), !esc ? (Raw)v16 : (Raw)sr.wide[q]);
+  };
+  // wave 0: claim an item into slot b and stage its descriptor, bucket start and (speculative packed
+  // partition) its pieces; lane 6x + j (< 6 SP_NSEG) loads record j of piece x's unaligned head (j < 3) or
+  // tail, which it adds once the table is ready (hh: it holds one)
+  uint32_t hq = 0, hx = 0;
+  bool hh = false;
+  auto prepare = [&](int b) {
+    uint32_t it = 0;
+    if (lane == 0) it = atomicAdd(ctr, 1u);
+    it = __shfl(it, 0, WAVE);
+    if (lane == 0) s_item[b] = it;
+    hh = false;
+    if (it >= n_items) return;
     const BkItem m = items[it];
+    const uint32_t b0 = bucket_start[m.bucket];
+    if (lane == 0) {
+      s_m[b] = m;
+      s_b0[b] = b0;
+    }
+    if constexpr (PACKED) {
+      if (seg_cur) {
+        // the item's pieces of the bucket's SP_NSEG segments, in segment order, as ONE stream of 16-byte
+        // groups (a loop per segment drained and refilled the loads in flight at each segment boundary):
+        // lane x < SP_NSEG takes segment x's piece [p0, p1) and publishes its groups' place in the stream
+        const bool on = lane < (int)SP_NSEG;
+        const uint32_t x = on ? (uint32_t)lane : 0u;
+        const uint32_t sg = sp_lo(seg_cur, x, m.bucket);
+        const uint32_t nx = on ? min(seg_cur[x * BK_MAXB + m.bucket], sp_hi(seg_cur, x, m.bucket)) - sg : 0u;
+        const uint32_t at = wave_inclusive_sum(nx) - nx;   // records of the bucket in the segments before x
+        const uint32_t lo = max(m.begin, at), hi = min(m.end, at + nx);
+        uint32_t p0 = 0, p1 = 0;
+        if (on && lo < hi) {
+          p0 = sg + (lo - at);
+          p1 = sg + (hi - at);
+        }
+        const uint32_t a0 = min(p1, (p0 + 3) & ~3u), a1 = max(a0, p1 & ~3u);
+        const uint32_t n4 = (a1 - a0) / 4;
+        const uint32_t e4 = wave_inclusive_sum(n4);
+        if (on) {
+          s_pre4[b][x + 1] = e4;
+          s_qb[b][x] = a0 / 4 - (e4 - n4);   // group g of piece x: uint4 index g + s_qb[x]
+        }
+        if (lane == 0) s_pre4[b][0] = 0;
+        const uint32_t px = (uint32_t)lane / 6, j = (uint32_t)lane % 6;
+        const uint32_t xp0 = __shfl(p0, (int)px, WAVE), xa0 = __shfl(a0, (int)px, WAVE);
+        const uint32_t xa1 = __shfl(a1, (int)px, WAVE), xp1 = __shfl(p1, (int)px, WAVE);
+        const uint32_t q = j < 3 ? xp0 + j : xa1 + (j - 3);
+        hh = px < SP_NSEG && (j < 3 ? q < xa0 : q < xp1);
+        if (hh) {
+          hq = q;
+          hx = src.rec[q];
+        }
+      }
+    }
+  };
+  if (tid < WAVE) prepare(0);
+  P::init(s, tid);
+  __syncthreads();
+  constexpr int U4 = UNROLL / 2 > 0 ? UNROLL / 2 : 1;
+  // (GS_BK_PREFETCH) the next item's first group of 16-byte loads, issued before this item's finalize
+  uint4 xp[U4];
+  uint32_t qp[U4];
+  bool pf = false;
+  for (int sl = 0;; sl ^= 1) {
+    const uint32_t it = s_item[sl];
+    if (it >= n_items) break;
+    const BkItem m = s_m[sl];
+    const uint32_t b0 = s_b0[sl];
 #ifdef GS_BK_TRACE
     const uint64_t t_item0 = wall_clock64();
 #endif
-    const uint32_t b0 = bucket_start[m.bucket];
-    P::init(s, tid);
-    __syncthreads();
-    if constexpr (is_pack_src<Src>::value) {
+    if constexpr (PACKED) {
       // packed records: 16-byte loads (4 records per lane per load: 4x the bytes in flight of 4-byte
       // loads; the 4-byte version was latency-bound); unaligned heads and tails record by record
-      auto add1 = [&](uint32_t q, uint32_t x) {
-        const uint32_t v16 = x >> 16;
-        const bool esc = v16 == PK_ESC;
-        if constexpr (has_add_packed<P>::value) P::add_packed(s, x & (P::W - 1), !esc ? (Raw)v16 : (Raw)src.wide[q], esc);
-        else P::add(s, x & (P::W - 1), !esc ? (Raw)v16 : (Raw)src.wide[q]);
-      };
       const uint4* rec4 = reinterpret_cast<const uint4*>(src.rec);
-      constexpr int U4 = UNROLL / 2 > 0 ? UNROLL / 2 : 1;
       constexpr uint32_t STEP = BK_ACC_BLOCK * U4;
       // n4 groups of 4 records, group g at uint4 index q4_of(g) of the partition
       auto stream = [&](uint32_t n4, auto q4_of) {
         for (uint32_t g4 = tid; g4 < n4; g4 += STEP) {
           uint4 x[U4];
           uint32_t qi[U4];
+          if (pf) {   // the first group, loaded before the previous item's finalize
 #pragma unroll
-          for (int u = 0; u < U4; ++u) {   // unconditional, clamped: see k_dp_hist
-            const uint32_t g = g4 + (uint32_t)u * BK_ACC_BLOCK;
-            qi[u] = q4_of(g < n4 ? g : n4 - 1);
-            x[u] = rec4[qi[u]];
+            for (int u = 0; u < U4; ++u) {
+              x[u] = xp[u];
+              qi[u] = qp[u];
+            }
+            pf = false;
+          } else {
+#pragma unroll
+            for (int u = 0; u < U4; ++u) {   // unconditional, clamped: see k_dp_hist
+              const uint32_t g = g4 + (uint32_t)u * BK_ACC_BLOCK;
+              qi[u] = q4_of(g < n4 ? g : n4 - 1);
+              x[u] = rec4[qi[u]];
+            }
           }
           // every load of the group issued before the first use (the scheduler moved the first
           // group's decode, and its wait, between the loads)
@@ -1754,48 +1937,22 @@ __global__ __launch_bounds__(BK_ACC_BLOCK) void k_bk_accum(Src src, const BkItem
                 continue;
               }
             }
-            add1(q, x[u].x);
-            add1(q + 1, x[u].y);
-            add1(q + 2, x[u].z);
-            add1(q + 3, x[u].w);
+            add1(src, q, x[u].x);
+            add1(src, q + 1, x[u].y);
+            add1(src, q + 2, x[u].z);
+            add1(src, q + 3, x[u].w);
           }
         }
+        pf = false;   // (a thread with no group in this item drops its prefetch)
       };
       if (!seg_cur) {   // records [r0, r1) of the partition
         const uint32_t r0 = b0 + m.begin, r1 = b0 + m.end;
         const uint32_t a0 = min(r1, (r0 + 3) & ~3u), a1 = max(a0, r1 & ~3u);
-        if (r0 + tid < a0) add1(r0 + tid, src.rec[r0 + tid]);
-        if (a1 + tid < r1) add1(a1 + tid, src.rec[a1 + tid]);
+        if (r0 + tid < a0) add1(src, r0 + tid, src.rec[r0 + tid]);
+        if (a1 + tid < r1) add1(src, a1 + tid, src.rec[a1 + tid]);
         stream((a1 - a0) / 4, [&](uint32_t g) { return a0 / 4 + g; });
       } else {
-        // speculative partition: the item's pieces of the bucket's SP_NSEG segments, in segment order,
-        // as ONE stream of 16-byte groups (a loop per segment drained and refilled the loads in flight
-        // at each of the item's segment boundaries).  Wave 0: lane x < SP_NSEG takes segment x's piece
-        // [p0, p1), its head and tail record by record, and publishes its groups' place in the stream.
-        if (tid < WAVE) {
-          const bool on = tid < (int)SP_NSEG;
-          const uint32_t x = on ? (uint32_t)tid : 0u;
-          const uint32_t sg = sp_lo(seg_cur, x, m.bucket);
-          const uint32_t nx = on ? min(seg_cur[x * BK_MAXB + m.bucket], sp_hi(seg_cur, x, m.bucket)) - sg : 0u;
-          const uint32_t at = wave_inclusive_sum(nx) - nx;   // records of the bucket in the segments before x
-          const uint32_t lo = max(m.begin, at), hi = min(m.end, at + nx);
-          uint32_t p0 = 0, p1 = 0;
-          if (on && lo < hi) {
-            p0 = sg + (lo - at);
-            p1 = sg + (hi - at);
-          }
-          const uint32_t a0 = min(p1, (p0 + 3) & ~3u), a1 = max(a0, p1 & ~3u);
-          const uint32_t n4 = (a1 - a0) / 4;
-          const uint32_t e4 = wave_inclusive_sum(n4);
-          if (on) {
-            s_pre4[x + 1] = e4;
-            s_qb[x] = a0 / 4 - (e4 - n4);   // group g of piece x: uint4 index g + s_qb[x]
-          }
-          if (tid == 0) s_pre4[0] = 0;
-          for (uint32_t q = p0; q < a0; ++q) add1(q, src.rec[q]);
-          for (uint32_t q = a1; q < p1; ++q) add1(q, src.rec[q]);
-        }
-        __syncthreads();
+        if (hh) add1(src, hq, hx);   // wave 0's staged head / tail records
         // group g of the stream lies in the last piece x with s_pre4[x] <= g (empty pieces share their
         // start with the next one): the pieces' bounds in registers, a branch-free select per load (a
         // cursor walking s_pre4 in LDS put an LDS read and its wait between consecutive loads)
@@ -1803,10 +1960,10 @@ __global__ __launch_bounds__(BK_ACC_BLOCK) void k_bk_accum(Src src, const BkItem
         uint32_t pre[SP_NSEG], dq[SP_NSEG];
 #pragma unroll
         for (uint32_t x = 0; x < SP_NSEG; ++x) {
-          pre[x] = s_pre4[x];
-          dq[x] = x ? s_qb[x] - s_qb[x - 1] : s_qb[0];
+          pre[x] = s_pre4[sl][x];
+          dq[x] = x ? s_qb[sl][x] - s_qb[sl][x - 1] : s_qb[sl][0];
         }
-        stream(s_pre4[SP_NSEG], [&](uint32_t g) {
+        stream(s_pre4[sl][SP_NSEG], [&](uint32_t g) {
           uint32_t b = dq[0];
 #pragma unroll
           for (uint32_t x = 1; x < SP_NSEG; ++x) b += g >= pre[x] ? dq[x] : 0u;
@@ -1900,9 +2057,38 @@ __global__ __launch_bounds__(BK_ACC_BLOCK) void k_bk_accum(Src src, const BkItem
       }
     }
     }
+    // the next item: wave 0 claims and stages it in the other slot while the other waves finish this one
+    if (tid < WAVE) prepare(sl ^ 1);
     __syncthreads();
+#if GS_BK_PREFETCH
+    if constexpr (PACKED) {   // the next item's first group in flight during this item's finalize
+      const int nx = sl ^ 1;
+      if (seg_cur && s_item[nx] < n_items && s_pre4[nx][SP_NSEG]) {
+        const uint32_t n4n = s_pre4[nx][SP_NSEG];
+        uint32_t pre[SP_NSEG], dq[SP_NSEG];
+#pragma unroll
+        for (uint32_t x = 0; x < SP_NSEG; ++x) {
+          pre[x] = s_pre4[nx][x];
+          dq[x] = x ? s_qb[nx][x] - s_qb[nx][x - 1] : s_qb[nx][0];
+        }
+        const uint4* rec4 = reinterpret_cast<const uint4*>(src.rec);
+#pragma unroll
+        for (int u = 0; u < U4; ++u) {
+          const uint32_t g0 = (uint32_t)tid + (uint32_t)u * BK_ACC_BLOCK, g = g0 < n4n ? g0 : n4n - 1;
+          uint32_t b = dq[0];
+#pragma unroll
+          for (uint32_t x = 1; x < SP_NSEG; ++x) b += g >= pre[x] ? dq[x] : 0u;
+          qp[u] = g + b;
+          xp[u] = rec4[qp[u]];
+        }
+        pf = true;
+      }
+    }
+#endif
+    bool reset = false;
     if (m.slab == ~0u) {
-      bk_finalize<P>(s, m.bucket, b0, st, bucket_count, s_wc);
+      bk_finalize<P, GS_BK_FUSED_RESET != 0>(s, m.bucket, b0, st, bucket_count, s_wc);
+      reset = GS_BK_FUSED_RESET != 0;
     } else {
       // dump the LDS accumulators (k_bk_merge, a later launch, combines the bucket's slabs)
       const uint4* ls = reinterpret_cast<const uint4*>(&s);
@@ -1918,6 +2104,10 @@ __global__ __launch_bounds__(BK_ACC_BLOCK) void k_bk_accum(Src src, const BkItem
       g_bk_trace[it][3] = m.end - m.begin;
     }
 #endif
+    if (!reset) {   // (block-uniform: the item's slab)
+      P::init(s, tid);
+      __syncthreads();
+    }
   }
 }
 

@@ -396,6 +396,23 @@ gs_status comm_allgather_u64(gs_ctx* c, uint64_t mine, uint64_t* all) {
   return GS_OK;
 }
 
+// every rank's W words -> all[p * W + j] on the host (a sum of one-hot rows; W * comm_size <= 256)
+gs_status comm_allgather_words(gs_ctx* c, const uint64_t* mine, int W, uint64_t* all) {
+  if (!c->comm) return set_error(c, GS_EINVAL, "no communicator (gs_comm_init)");
+  const int P = c->comm_size;
+  if (W < 1 || (size_t)W * P > 256) return set_error(c, GS_EINVAL, "comm_allgather_words: %d x %d words", W, P);
+  GS_TRY(ensure(c, c->dist_cnt, 1024 + (size_t)P * W * 8));
+  uint64_t* d = (uint64_t*)(c->dist_cnt.as<char>() + 512);
+  GS_HIP(hipMemsetAsync(d, 0, (size_t)P * W * 8, c->stream));
+  memcpy(c->host_small + 100, mine, (size_t)W * 8);   // pinned source; results land in [200, 200 + P W)
+  GS_HIP(hipMemcpyAsync(d + (size_t)c->comm_rank * W, c->host_small + 100, (size_t)W * 8, hipMemcpyHostToDevice, c->stream));
+  GS_TRY(comm_allreduce(c, d, (size_t)P * W, NCCL_T_U64, NCCL_OP_SUM));
+  GS_HIP(hipMemcpyAsync(c->host_small + 200, d, (size_t)P * W * 8, hipMemcpyDeviceToHost, c->stream));
+  GS_TRY(host_wait(c));
+  memcpy(all, c->host_small + 200, (size_t)P * W * 8);
+  return GS_OK;
+}
+
 // every rank's `mine` rows (row bytes each) concatenated in rank order into recvbuf; counts[p] = rows of
 // rank p (comm_allgather_u64)
 gs_status comm_allgatherv(gs_ctx* c, const void* sendbuf, char* recvbuf, const uint64_t* counts, size_t row) {

@@ -235,6 +235,7 @@ constexpr int GS_COMM_KIND_RCCL = 1, GS_COMM_KIND_GROUP = 2;
 gs_status comm_allreduce(gs_ctx* c, void* buf, size_t count, int nccl_dtype, int nccl_op);
 gs_status comm_alltoall(gs_ctx* c, const void* send, void* recv, size_t count, int nccl_dtype);
 gs_status comm_allgather_u64(gs_ctx* c, uint64_t mine, uint64_t* all);
+gs_status comm_allgather_words(gs_ctx* c, const uint64_t* mine, int W, uint64_t* all);
 gs_status comm_agree(gs_ctx* c, gs_status local);
 // skip_self: this rank's own rows (send[me] == recv[me]) stay in sendbuf -- not copied, and the receive
 // buffer holds only the peers' rows

@@ -1705,21 +1705,24 @@ gs_status gs_window_triangles_dist(gs_ctx* c, const gs_edge_batch* b, uint64_t* 
   if (!count || !count_ref_wrapped || !has_output) return set_error(c, GS_EINVAL, "null output pointer");
   if (!c->comm) return set_error(c, GS_EINVAL, "no communicator (gs_comm_init)");
   const uint32_t P = (uint32_t)c->comm_size, me = (uint32_t)c->comm_rank;
-  // 1. the common id range
+  // 1. the common id range, the window's record count and every rank's status in ONE collective (each
+  //    rank's [failed, min, max, records] row; round 5 ran an agreement, a MIN, a MAX and a SUM, each with
+  //    its own host wait).  Later steps agree on their status before the collective that follows them.
   int64_t mm[2];
-  GS_TRY(comm_agree(c, gs_tri_dist_range(c, b, mm)));   // every local step: status agreed before the collective
-  GS_TRY(ensure(c, c->tri_d[0], 64));
-  long long* dmm = c->tri_d[0].as<long long>();
-  c->host_small[12] = (uint64_t)mm[0];
-  c->host_small[13] = (uint64_t)mm[1];
-  GS_HIP(hipMemcpyAsync(dmm, c->host_small + 12, 16, hipMemcpyHostToDevice, c->stream));
-  GS_TRY(comm_allreduce(c, dmm, 1, NCCL_T_I64, NCCL_OP_MIN));
-  GS_TRY(comm_allreduce(c, dmm + 1, 1, NCCL_T_I64, NCCL_OP_MAX));
-  GS_HIP(hipMemcpyAsync(c->host_small + 12, dmm, 16, hipMemcpyDeviceToHost, c->stream));
-  GS_TRY(host_wait(c));
-  int64_t gmin = (int64_t)c->host_small[12], gmax = (int64_t)c->host_small[13];
-  uint64_t total_n = b->n;
-  GS_TRY(gs_comm_allreduce_sum_u64(c, &total_n));
+  const gs_status rs = gs_tri_dist_range(c, b, mm);
+  const std::string rerr = c->err;
+  const uint64_t mine[4] = {rs != GS_OK ? 1ull : 0ull, (uint64_t)mm[0], (uint64_t)mm[1], rs == GS_OK ? b->n : 0};
+  std::vector<uint64_t> rows((size_t)P * 4);
+  GS_TRY(comm_allgather_words(c, mine, 4, rows.data()));
+  if (rs != GS_OK) return set_error(c, rs, "%s", rerr.c_str());
+  int64_t gmin = INT64_MAX, gmax = INT64_MIN;
+  uint64_t total_n = 0;
+  for (uint32_t p = 0; p < P; ++p) {
+    if (rows[4 * p]) return set_error(c, GS_ECOMM, "rank %u failed its local step of the window", p);
+    gmin = std::min(gmin, (int64_t)rows[4 * p + 1]);
+    gmax = std::max(gmax, (int64_t)rows[4 * p + 2]);
+    total_n += rows[4 * p + 3];
+  }
   *count = 0;
   *count_ref_wrapped = 0;
   *has_output = total_n > 0;

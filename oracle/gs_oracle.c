@@ -778,6 +778,96 @@ GSO_API int64_t gso_window_candidates(const int64_t* src, const int64_t* dst, ui
   return o <= cap ? (int64_t)o : -1 - (int64_t)o;
 }
 
+/* GenerateCandidateEdges over `threads` threads with a consumer (bench.py's C5 cpu_baseline): the same
+ * records as gso_window_candidates (WindowTriangles.java:91-114: the edge records, then the HashSet-ordered
+ * pairs), each thread taking blocks of 64 vertices from a shared counter and writing its records into its
+ * own chunk of `chunk` records (a, b, flag columns), which a consumer then reads back whole (column sums,
+ * as the GPU line's device consumer does) before the chunk is reused.  The CSR is built first, on one
+ * thread.  Returns the record count; sums[0..2] = the a, b and flag column sums (order-free, so they equal
+ * the sums over gso_window_candidates' output). */
+typedef struct {
+  const csr_t* c;
+  uint64_t chunk, maxd;
+  volatile uint64_t* next;
+  uint64_t recs, s[3];
+} cand_mt_arg;
+static void cand_consume(const int64_t* a, const int64_t* b, const uint8_t* f, uint64_t n, uint64_t* s) {
+  uint64_t sa = 0, sb = 0, sf = 0;
+  for (uint64_t i = 0; i < n; ++i) {
+    sa += (uint64_t)a[i];
+    sb += (uint64_t)b[i];
+    sf += f[i];
+  }
+  s[0] += sa; s[1] += sb; s[2] += sf;
+}
+static void* cand_mt_worker(void* p) {
+  cand_mt_arg* g = (cand_mt_arg*)p;
+  const csr_t* c = g->c;
+  const uint64_t C = g->chunk;
+  int64_t* a = (int64_t*)malloc(C * sizeof(int64_t));
+  int64_t* b = (int64_t*)malloc(C * sizeof(int64_t));
+  uint8_t* f = (uint8_t*)malloc(C);
+  int64_t* dist = (int64_t*)malloc((g->maxd + 1) * sizeof(int64_t));
+  int64_t* ids = (int64_t*)malloc((g->maxd + 1) * sizeof(int64_t));
+  hsent* tmp = (hsent*)malloc((g->maxd + 1) * sizeof(hsent));
+  uint64_t o = 0;
+#define CAND_PUT(x, y, fl) do { a[o] = (x); b[o] = (y); f[o] = (fl); if (++o == C) { cand_consume(a, b, f, o, g->s); g->recs += o; o = 0; } } while (0)
+  for (;;) {
+    const uint64_t u0 = __sync_fetch_and_add(g->next, 64);
+    if (u0 >= c->U) break;
+    const uint64_t u1 = u0 + 64 < c->U ? u0 + 64 : c->U;
+    for (uint64_t u = u0; u < u1; ++u) {
+      const int64_t v = c->keys[u];
+      const uint64_t lo = c->off[u], hi = c->off[u + 1];
+      for (uint64_t j = lo; j < hi; ++j) CAND_PUT(v, c->nbr[j], 0);
+      const uint64_t k = distinct_of(c->nbr + lo, hi - lo, dist);
+      hashset_order(dist, k, ids, tmp);
+      const int last_above = k > 0 && ids[k - 1] > v;
+      uint64_t m = 0;
+      for (uint64_t i = 0; i < k; ++i)
+        if (ids[i] > v) ids[m++] = ids[i];
+      for (uint64_t i = 0; i < m; ++i) {
+        if (last_above && i + 1 == m) break;
+        for (uint64_t j = i; j < m; ++j) CAND_PUT(ids[i], ids[j], 1);
+      }
+    }
+  }
+#undef CAND_PUT
+  cand_consume(a, b, f, o, g->s);
+  g->recs += o;
+  free(a); free(b); free(f); free(dist); free(ids); free(tmp);
+  return NULL;
+}
+GSO_API int64_t gso_candidates_mt(const int64_t* src, const int64_t* dst, uint64_t n, int threads, uint64_t chunk,
+                                  uint64_t* sums) {
+  csr_t c;
+  if (build_csr_all(src, dst, n, &c) != 0) return -2;
+  uint64_t maxd = 1;
+  for (uint64_t u = 0; u < c.U; ++u)
+    if (c.off[u + 1] - c.off[u] > maxd) maxd = c.off[u + 1] - c.off[u];
+  if (threads < 1) threads = 1;
+  if (chunk < 1) chunk = 1;
+  volatile uint64_t next = 0;
+  pthread_t* th = (pthread_t*)malloc(sizeof(pthread_t) * (size_t)threads);
+  cand_mt_arg* args = (cand_mt_arg*)calloc((size_t)threads, sizeof(cand_mt_arg));
+  for (int t = 0; t < threads; ++t) {
+    args[t].c = &c;
+    args[t].chunk = chunk;
+    args[t].maxd = maxd;
+    args[t].next = &next;
+    pthread_create(&th[t], NULL, cand_mt_worker, &args[t]);
+  }
+  uint64_t recs = 0;
+  sums[0] = sums[1] = sums[2] = 0;
+  for (int t = 0; t < threads; ++t) {
+    pthread_join(th[t], NULL);
+    recs += args[t].recs;
+    for (int q = 0; q < 3; ++q) sums[q] += args[t].s[q];
+  }
+  free(th); free(args); free_csr(&c);
+  return (int64_t)recs;
+}
+
 /* ------------------------------------------------------------------------------------ */
 /* WindowTriangles, reference rule: candidates -> keyBy(0,1) CountTriangles -> sum(0)    */
 /* ------------------------------------------------------------------------------------ */

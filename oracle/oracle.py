@@ -48,6 +48,7 @@ def lib():
             "gso_window_fold_degree_max": (i64, [P, P, u64, i32, i64, P, P, P, u64]),
             "gso_window_csr": (i64, [P, P, P, u64, i32, i32, P, P, P, P, u64]),
             "gso_window_candidates": (i64, [P, P, u64, P, P, P, u64, P]),
+            "gso_candidates_mt": (i64, [P, P, u64, i32, u64, P]),
             "gso_window_triangles_ref": (ctypes.c_int32, [P, P, u64, P, P, P]),
             "gso_window_triangles_fwd": (ctypes.c_int32, [P, P, u64, P, P]),
             "gso_baseline_reduce": (u64, [P, P, P, u64, i32, i32, i32, i32]),
@@ -184,6 +185,17 @@ def window_candidates(src, dst):
     got = lib().gso_window_candidates(_p(src), _p(dst), len(src), _p(a), _p(b), _p(f), P, ctypes.byref(tree))
     assert got == P
     return a, b, f, int(tree.value)   # JDK flags of hashset_order (nonzero: some set left the plain model)
+
+
+def candidates_mt(src, dst, threads=None, chunk=1 << 20):
+    """GenerateCandidateEdges over `threads` threads with a consumer that reads every chunk of `chunk`
+    records back (column sums): (records, [sum a, sum b, sum flags]) -- bench.py's C5 cpu_baseline."""
+    src, dst = _i64(src), _i64(dst)
+    sums = np.zeros(3, np.uint64)
+    n = lib().gso_candidates_mt(_p(src), _p(dst), len(src), threads or default_threads(), chunk, _p(sums))
+    if n < 0:
+        raise ValueError("gso_candidates_mt failed")
+    return int(n), [int(x) for x in sums]
 
 
 def candidate_count(src, dst):

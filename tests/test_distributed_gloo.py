@@ -314,8 +314,8 @@ def _worker(rank, world, port, q):
     res = run_cases(D, oracle_halves(orc), s, d, v)
     fs, fd = D.gather_window(torch.from_numpy(s), torch.from_numpy(d))
     res["gathered"] = (fs.numpy(), fd.numpy())
-    # WindowTriangles over the split window: the real exchanges (ranges, degrees, routed oriented edges,
-    # all-gathered out-lists, equal-work parts) with the steps restated in numpy; plus a small window
+    # WindowTriangles over the split window: the real exchanges (ranges, degrees, routed oriented edges, the
+    # boundary adjacency rows, equal-work parts) with the steps restated in numpy; plus a small window
     # with self-loops (the gathered self-pair term)
     te = OracleTriEngine(orc)
     ts, td = orc.gen_rmat(11, 20000, 0x5EED05, no_self_loops=True, first_edge=rank * 20000)

@@ -354,3 +354,34 @@ def test_failed_reduce_dist_leaves_plain_reduce_intact(pkg, oracle, window):
     want = oracle.window_reduce(s[a:b], d[a:b], v[a:b], 1, 0)
     assert np.array_equal(res[0][0], want[0])
     assert np.array_equal(res[0][1], want[1])
+
+
+def test_split_window_s22_eight_ranks(pkg, oracle):
+    """The memory-scaling case: eight ranks on one GPU, each with 1/8 of an R-MAT s22 window (2^26 edges).
+    WindowTriangles over the split window against the oracle's forward count of the whole window, and the
+    C3-shaped degree / max-neighbour fold (skewed R-MAT, hubs at low ids, no permutation) against the
+    whole-window fold (WindowTriangles.java:64-66; GraphWindowStream.java:62-87)."""
+    P, n = 8, 1 << 26
+    s, d = oracle.gen_rmat(22, n, 0x5EED11, no_self_loops=True)
+    sl = slices(n, P)
+
+    def fn_tri(r, e):
+        a, b = sl[r]
+        return e.triangles_dist(s[a:b], d[a:b])
+
+    res, errs = run_group(pkg, P, fn_tri, timeout=600)
+    assert not errs, errs
+    T = oracle.triangles_fwd_mt(s, d)
+    want = (T, ((T + (1 << 31)) % (1 << 32)) - (1 << 31), True)   # Integer sum(0) wraps (WindowTriangles.java:66)
+    for r in range(P):
+        assert res[r] == want, (r, res[r], want)
+    del s, d
+    fs, fd = oracle.gen_rmat(22, n, 0x5EED12, a=0.65, b=0.15, c=0.15, permute=False)
+
+    def fn_fold(r, e):
+        a, b = sl[r]
+        return e.fold_degree_max_dist(fs[a:b], fd[a:b], 1, -5)
+
+    res, errs = run_group(pkg, P, fn_fold, timeout=600)
+    assert not errs, errs
+    check_union(res, oracle.window_fold_degree_max_mt(fs, fd, 1, -5), P)

@@ -160,3 +160,20 @@ def test_reduce_unaligned_device_slices(engine, oracle):
         rk, rv = oracle.window_reduce(s[1:], d[1:], v[1:], direction, 0)
         gk, gv = engine.reduce(S[1:], D[1:], Vv[1:], direction, 0)
         assert np.array_equal(_np(gk), rk) and np.array_equal(_np(gv), rv)
+
+
+def test_speculative_window_unaligned_device_slices(engine, oracle):
+    """The speculative scatter reads two records per lane with 16-byte loads only from 16-byte aligned
+    columns (k_sp_scatter_pack, GS_SPK_VEC): a second window of the same geometry (it speculates) over views
+    at an odd offset -- keys only, values only, both -- takes the 8-byte path and gives the same output."""
+    n = 1 << 18
+    s, d = oracle.gen_rmat(16, n + 2, 79)
+    v = oracle.gen_values(n + 2, 80, oracle.DT_I64)
+    S, D, Vv = _dev(s, d, v)
+    for direction in (0, 1):
+        for ko, vo in ((0, 0), (1, 1), (1, 0), (0, 1)):
+            ks, kd, vv = S[ko:ko + n], D[ko:ko + n], Vv[vo:vo + n]
+            want = oracle.window_reduce(s[ko:ko + n], d[ko:ko + n], v[vo:vo + n], direction, 0)
+            for w in range(2):   # the second window speculates
+                gk, gv = engine.reduce(ks, kd, vv, direction, 0)
+                assert np.array_equal(_np(gk), want[0]) and np.array_equal(_np(gv), want[1]), (direction, ko, vo, w)

@@ -36,6 +36,8 @@ if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("prof")
     ap.add_argument("-o", default="profiles/pmc_traffic.json")
+    ap.add_argument("--lib", default=str(Path(__file__).resolve().parent.parent / "gelly-streaming_amd" / "libgellyhip.so"),
+                    help="the library the passes ran (its sha256 goes into _meta: bench.py checks it)")
     a = ap.parse_args()
     d = Path(a.prof)
     fetch, write = per_launch(d / "fetch", "FETCH_SIZE"), per_launch(d / "write", "WRITE_SIZE")
@@ -44,5 +46,13 @@ if __name__ == "__main__":
         rd, wr = 2 * fetch.get(k, 0.0) * 1024, write.get(k, 0.0) * 1024
         out[k] = {"read_bytes": rd, "write_bytes": wr, "bytes_per_launch": rd + wr,
                   "note": "2 x FETCH_SIZE (gfx950 wide-read tally) + WRITE_SIZE, KiB -> bytes, mean per launch"}
-    Path(a.o).write_text(json.dumps(out, indent=1) + "\n")
+    import hashlib
+    import subprocess
+
+    lib = Path(a.lib)
+    head = subprocess.run(["git", "rev-parse", "--short=12", "HEAD"], capture_output=True, text=True,
+                          cwd=Path(__file__).resolve().parent.parent).stdout.strip() or None
+    meta = {"lib_sha16": hashlib.sha256(lib.read_bytes()).hexdigest()[:16] if lib.exists() else None,
+            "git_head": head, "passes": str(d)}
+    Path(a.o).write_text(json.dumps({"_meta": meta, **out}, indent=1) + "\n")
     print(json.dumps({k: round(v["bytes_per_launch"] / 1e9, 3) for k, v in out.items()}))
