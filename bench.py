@@ -270,7 +270,9 @@ def host_cpu():
         affinity = len(os.sched_getaffinity(0))
     except AttributeError:
         affinity = nproc
-    return {"cpu_model": model, "nproc": nproc, "affinity_cpus": affinity}
+    # the worker-pool caps the GPU box exports (16 per GPU there), as they were when the baseline ran
+    env = {k: os.environ[k] for k in ("OMP_NUM_THREADS", "MAX_JOBS", "CMAKE_BUILD_PARALLEL_LEVEL") if k in os.environ}
+    return {"cpu_model": model, "nproc": nproc, "affinity_cpus": affinity, "pool_env": env or None}
 
 
 def cpu_baseline(wins, workload, threads, reps=5):
@@ -631,7 +633,7 @@ def cand_stream_main(a):
         e.close()
 
 
-def cand_cpu_baseline(E, sample_log2=24, threads=None):
+def cand_cpu_baseline(E, sample_log2=25, threads=None):
     """The oracle's GenerateCandidateEdges (the reference's JDK HashSet order) over min(16, nproc) threads WITH
     a consumer that reads every record back (gso_candidates_mt: per-thread chunks of 2^20 records, each summed
     column by column before it is reused -- the GPU line's device consumer), on the largest sample that keeps
@@ -900,7 +902,7 @@ def main():
                        torch.empty(R, dtype=v_.dtype if v_ is not None else torch.int64, device=s_.device))
         r = eng.reduce(s_, d_, v_, direction, op, out=None if a.alloc_outputs else red_out)
         if not local_times:
-            local_times.append(eng.stage_times())   # the window's own pipeline, not the merge
+            local_times.append(eng.stage_times_raw())   # the window's own pipeline, not the merge
         return r
 
     fold_out = None
@@ -912,7 +914,7 @@ def main():
             fold_out = tuple(torch.empty(R, dtype=torch.int64, device=s_.device) for _ in range(3))
         r = eng.fold_degree_max(s_, d_, direction, init_max, out=None if a.alloc_outputs else fold_out)
         if not local_times:
-            local_times.append(eng.stage_times())
+            local_times.append(eng.stage_times_raw())
         return r
 
     P_red, M_red, P_fold, M_fold = D.engine_halves(eng)
@@ -920,18 +922,18 @@ def main():
     def partials_timed(*args):   # the window's own pipeline runs inside the partials half
         r = P_red(*args)
         if not local_times:
-            local_times.append(eng.stage_times())
+            local_times.append(eng.stage_times_raw())
         return r
 
     def fold_partials_timed(*args):
         r = P_fold(*args)
         if not local_times:
-            local_times.append(eng.stage_times())
+            local_times.append(eng.stage_times_raw())
         return r
 
     def part_count(s_, d_, part, nparts):
         r = eng.triangles_part(s_, d_, part, nparts)
-        local_times.append(eng.stage_times())
+        local_times.append(eng.stage_times_raw())
         return r
 
     dist_out = None
@@ -942,10 +944,10 @@ def main():
         if a.workload == "triangles":
             if abi:    # the split window through gs_window_triangles_dist (RCCL inside the library)
                 tot = eng.triangles_dist(src, dst)[0]
-                local_times.append(eng.stage_times())
+                local_times.append(eng.stage_times_raw())
             elif dist:   # the same steps with torch.distributed collectives
                 tot = D.triangles_window(eng, src, dst)[0]
-                local_times.append(eng.stage_times())
+                local_times.append(eng.stage_times_raw())
             else:
                 tot = part_count(src, dst, 0, 1)
             z = torch.zeros(1, dtype=torch.int64, device=src.device)
@@ -956,7 +958,7 @@ def main():
         if a.workload == "fold":
             if abi:   # gs_window_fold_degree_max_dist: its stage times are the local window's pipeline
                 r = eng.fold_degree_max_dist(src, dst, 1)
-                local_times.append(eng.stage_times())
+                local_times.append(eng.stage_times_raw())
             else:
                 r = D.fold_degree_max_window(fold_partials_timed, M_fold, src, dst, 1, -(1 << 63)) if dist \
                     else local_fold(src, dst, 1, -(1 << 63))
@@ -967,7 +969,7 @@ def main():
                 dist_out = (torch.empty(2 * src.numel() + 1024, dtype=torch.int64, device=src.device),
                             torch.empty(2 * src.numel() + 1024, dtype=val.dtype, device=src.device))
             r = eng.reduce_dist(src, dst, val, 1, 0, out=dist_out)
-            local_times.append(eng.stage_times())
+            local_times.append(eng.stage_times_raw())
         else:
             r = D.reduce_window(partials_timed, M_red, src, dst, val, 1, 0) if dist else local_reduce(src, dst, val, 1, 0)
         return r[0], r[1], local_times[0]
@@ -994,6 +996,8 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    # (the timed loop kept each window's raw stage-time struct: StageTimes objects are built after it)
+    times = [eng.stage_times_of(t) for t in times]
     if dist:
         t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -1002,7 +1006,7 @@ def main():
     stage_times_after = None
     if lean:
         eng.set_timing(pkg._lib.GS_TIMING_STAGES)
-        stage_times_after = [step(a.warmup + a.steps + i)[2] for i in range(3)]
+        stage_times_after = [eng.stage_times_of(step(a.warmup + a.steps + i)[2]) for i in range(3)]
         torch.cuda.synchronize()
 
     checks = {}

@@ -243,10 +243,15 @@ gs_status bucket_results(gs_ctx* c, uint64_t* U, uint32_t* n_items) {
 
 void bucket_times(gs_ctx* c, int path, int passes, int launches, uint32_t key_bits, uint64_t R, uint64_t U,
                   size_t vb, uint32_t n_items) {
+  // only the events this timing level recorded are read (each hipEventElapsedTime is a driver call on the
+  // window's critical path: the host turnaround between two windows)
+  const bool all = c->timing == GS_TIMING_STAGES;
   float a = 0, b = 0, d = 0;
-  a = event_ms(c->ev[0], c->ev[1]);
-  b = event_ms(c->ev[1], c->ev[2]);
-  d = event_ms(c->ev[2], c->ev[3]);
+  if (all) {
+    a = event_ms(c->ev[0], c->ev[1]);
+    b = event_ms(c->ev[1], c->ev[2]);
+    d = event_ms(c->ev[2], c->ev[3]);
+  }
   gs_stage_times& t = c->times;
   t = gs_stage_times{};
   t.keyinfo_ms = a;
@@ -257,15 +262,14 @@ void bucket_times(gs_ctx* c, int path, int passes, int launches, uint32_t key_bi
   t.key_bits = key_bits;
   t.records = R;
   t.vertices = U;
-  for (int p = 0; p < launches && p < 8; ++p) t.pass_ms[p] = event_ms(c->pass_ev[p], c->pass_ev[p + 1]);
+  if (all)
+    for (int p = 0; p < launches && p < 8; ++p) t.pass_ms[p] = event_ms(c->pass_ev[p], c->pass_ev[p + 1]);
   t.key_bytes = 2;
   t.payload_bytes = (uint32_t)vb;
   t.partials = n_items;
   t.fused_last = 0;
   t.path = (uint32_t)path;
-  if (c->timing != GS_TIMING_STAGES) {   // only the events stage_event recorded at this level
-    t.keyinfo_ms = t.sort_ms = t.reduce_ms = t.total_ms = 0.f;
-    for (int p = 0; p < 8; ++p) t.pass_ms[p] = 0.f;
+  if (!all) {   // only the events stage_event recorded at this level
     if (c->timing == GS_TIMING_DOMINANT && path == 2) {   // the scatter and the accumulate (launch_dominant)
       if (passes) t.pass_ms[1] = event_ms(c->pass_ev[1], c->pass_ev[2]);
       t.pass_ms[2] = event_ms(c->pass_ev[7], c->pass_ev[3]);

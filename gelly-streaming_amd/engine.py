@@ -93,6 +93,20 @@ class CommGroup:
             pass
 
 
+_OUT_DTYPES = None
+
+
+def _out_dtypes():
+    """numpy -> torch dtype of the out= buffers (built once: Engine._check_out runs between windows)"""
+    global _OUT_DTYPES
+    if _OUT_DTYPES is None:
+        import torch
+
+        _OUT_DTYPES = {np.int64: torch.int64, np.int32: torch.int32, np.float32: torch.float32,
+                       np.float64: torch.float64}
+    return _OUT_DTYPES
+
+
 class Engine:
     def __init__(self, device: int = 0, reserve_edges: int = 0, torch_stream: bool = True, sort_only: bool = False,
                  bk_onesweep: bool = False, no_pack: bool = False, no_spec: bool = False, flags: int = 0):
@@ -155,8 +169,19 @@ class Engine:
         self._check(self._L.gs_synchronize(self.ctx))
 
     def stage_times(self) -> StageTimes:
+        return self.stage_times_of(self.stage_times_raw())
+
+    def stage_times_raw(self):
+        """The last window's gs_stage_times as the raw ctypes struct (a copy): cheap enough for a timed loop
+        between windows; stage_times_of() turns it into StageTimes afterwards."""
         t = L.GsStageTimes()
         self._check(self._L.gs_last_stage_times(self.ctx, ctypes.byref(t)))
+        return t
+
+    @staticmethod
+    def stage_times_of(t) -> StageTimes:
+        if isinstance(t, StageTimes):
+            return t
         launched = 5 if t.path in (2, 3) else 3 if t.path == 4 else \
             t.sort_passes + (3 if t.path == 1 else 1 if t.fused_last else 0)
         return StageTimes(t.keyinfo_ms, t.sort_ms, t.reduce_ms, t.total_ms, t.sort_passes, t.key_bits, t.records,
@@ -198,9 +223,7 @@ class Engine:
         """out= buffers: device tensors (with device inputs), contiguous, of the dtypes the library writes
         (it writes 8-byte keys and the op's value width at raw addresses: a narrower or strided tensor
         would take out-of-bounds or misplaced writes), and at least min_records long when given."""
-        import torch
-
-        tdt = {np.int64: torch.int64, np.int32: torch.int32, np.float32: torch.float32, np.float64: torch.float64}
+        tdt = _out_dtypes()
         if len(out) != len(np_dtypes):
             raise ValueError(f"out: {len(np_dtypes)} tensors expected")
         for t, want in zip(out, np_dtypes):

@@ -9,6 +9,8 @@ in its own interpreter).  On an R-MAT scale-22 window (2^26 edges, self-loops ke
 give the same count, and the stage times' "vertices with edges" must equal the window's distinct ids
 in both (with sampled classes it comes from the count's vertex pass, k_tri_lclass).  The same window
 sorted by source (a replayed edge list) must count as with exact classes, at about the exact-degree time.
+Both orders are also checked against the oracle: the count less the order's self-pair term is the
+window's triangle count from the oracle's forward algorithm on the self-loop-free edges.
 """
 import subprocess
 import sys
@@ -50,22 +52,34 @@ SCRIPT = textwrap.dedent("""
         return r[0], min(ms)
     c_shuf, ms_shuf = best(s, d)
     c_sort, ms_sort = best(ss, sd)
-    print("RESULT", exact, t.vertices, distinct, c_sort, int(ms_shuf * 1000), int(ms_sort * 1000))
+    # the independent check (first run only): each order's count less its self-pair term (the reference's
+    # HashSet-order quirk for self-loops) is the window's triangle count, which the oracle's forward
+    # algorithm gives on the self-loop-free edges (oracle/gs_oracle.c gso_triangles_fwd_mt)
+    sp, sp_sort, T = eng.triangles_selfpair(s, d), eng.triangles_selfpair(ss, sd), -1
+    if {k} == 4:
+        orc = ge.load_oracle()
+        sn, dn = s.cpu().numpy(), d.cpu().numpy()
+        keep = sn != dn
+        T = orc.triangles_fwd_mt(sn[keep], dn[keep])
+    print("RESULT", exact, t.vertices, distinct, c_sort, int(ms_shuf * 1000), int(ms_sort * 1000), sp, sp_sort, T)
     eng.close()
 """)
 
 
 def _run(k):
     r = subprocess.run([sys.executable, "-c", SCRIPT.format(root=str(ROOT), k=k)], capture_output=True, text=True,
-                       timeout=170)
+                       timeout=190)
     assert r.returncode == 0, r.stdout + r.stderr
     line = [x for x in r.stdout.splitlines() if x.startswith("RESULT")][-1]
     return tuple(int(x) for x in line.split()[1:])
 
 
+@pytest.mark.timeout(400)   # two interpreters, each a 2^26-edge window seven times; the first also runs the oracle
 def test_sampled_degree_classes_same_count_and_vertices():
-    count_s, verts_s, distinct, sorted_s, us_shuf, us_sort = _run(4)
-    count_e, verts_e, distinct_e, sorted_e, us_shuf_e, us_sort_e = _run(1)
+    count_s, verts_s, distinct, sorted_s, us_shuf, us_sort, sp, sp_sort, T = _run(4)
+    count_e, verts_e, distinct_e, sorted_e, us_shuf_e, us_sort_e = _run(1)[:6]
+    # both orders against the oracle: count = triangles + the order's self-pair term
+    assert count_s - sp == T and sorted_s - sp_sort == T, (count_s, sp, sorted_s, sp_sort, T)
     assert distinct == distinct_e
     # (the window keeps its self-loops, so the reference's count depends on the record order -- the
     # self-pair term follows HashSet order, which follows insertion order -- and the sorted window may

@@ -76,6 +76,11 @@ case $MODE in
     bench bench_e2e_direct --workload e2e --staging direct --no-cpu-baseline
     bench bench_e2e_pinned --workload e2e --staging pinned --no-cpu-baseline
     bench bench_e2e_buffered --workload e2e --staging buffered --no-cpu-baseline ;;
+  c2trace)
+    # the C2 window's kernel timeline (gaps between kernels and between windows), from a kernel trace
+    trace trace_c2 "$@"
+    python3 tools/timeline.py "$(find "$O/trace_c2" -name '*kernel_trace.csv' | head -1)" k_sp_scatter_pack 3 > "$O/c2_timeline.txt"
+    python3 tools/window_gaps.py "$(find "$O/trace_c2" -name '*kernel_trace.csv' | head -1)" > "$O/c2_window_gaps.txt" ;;
   counters)
     timeout -k 10 120 rocprofv3 -L > "$O/counters.txt" 2>&1 ;;
   wr)
