@@ -77,6 +77,9 @@ def parse():
     p.add_argument("--force-exchange", action="store_true",
                    help="rehearsal: at world size 1 the ABI path still partitions by owner, exchanges through RCCL "
                         "and merges (what each rank pays at N > 1, minus the link transfer)")
+    p.add_argument("--sync-outputs", action="store_true",
+                   help="reduce / fold: every call waits for its outputs (A/B; default GS_FLAG_ASYNC_OUTPUT: a call "
+                        "returns once the window's sizes are known, its outputs complete in the stream's order)")
     p.add_argument("--check", action="store_true",
                    help="after timing: sum(per-vertex sums) == sum(values) and ascending keys on each window")
     p.add_argument("--chunk-records", type=float, default=2 ** 28,
@@ -861,7 +864,8 @@ def main():
     D = import_module("gelly_streaming_amd.distributed")
 
     eng = pkg.Engine(local, sort_only=a.sort_only, bk_onesweep=a.bk_onesweep, no_pack=a.no_pack, no_spec=a.no_spec,
-                     flags=pkg._lib.GS_FLAG_TEST_FORCE_EXCHANGE if a.force_exchange else 0)
+                     flags=pkg._lib.GS_FLAG_TEST_FORCE_EXCHANGE if a.force_exchange else 0,
+                     async_outputs=not a.sync_outputs)
     abi = dist is not None and a.exchange == "abi"
     if abi:   # the ctx-owned RCCL communicator: rank 0's unique id broadcast over torch.distributed
         uid = torch.zeros(128, dtype=torch.uint8, device=f"cuda:{local}")

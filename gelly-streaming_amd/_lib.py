@@ -60,6 +60,7 @@ GS_FLAG_NO_SPEC = 16      # bucket path: no speculative partition (per-tile hist
 GS_FLAG_TEST_TINY_TABLES = 8   # TEST ONLY: triangle hash sets of one bucket -> must fail with GS_EDEVICE
 GS_LATE_REFIRE, GS_LATE_DROP = 0, 1   # gs_stream_config.late_mode
 GS_FLAG_TEST_FORCE_EXCHANGE = 32   # TEST ONLY: *_dist on one rank still partitions, exchanges and merges
+GS_FLAG_ASYNC_OUTPUT = 64   # device outputs of reduce / fold complete in the ctx stream's order (no wait for them)
 
 
 class GsConfig(ctypes.Structure):

@@ -14,6 +14,9 @@
 #include <algorithm>
 
 #include "gs_ops.hpp"
+#include <atomic>
+#include <chrono>
+
 #include "gs_bucket.hpp"
 
 namespace gs {
@@ -220,15 +223,52 @@ gs_status bucket_accumulate(gs_ctx* c, Src rs, uint64_t R, uint32_t nb, int64_t 
                        e.nparts, e.send, mm, (const uint32_t*)(sm + SM_TIMEOUT));
     c->oe.done = true;
   } else {
+    // GS_FLAG_ASYNC_OUTPUT (the entry point allowed it for this window): the emit's first block writes the
+    // read-back block into pinned host memory and bucket_wait spins on it -- the host does not wait for the
+    // emit (its outputs are complete in stream order), and there is no copy launch
+    const bool early = c->rb_allow && !c->in_chunk;
+    if (early && !c->rb_host) {
+      if (hipHostMalloc((void**)&c->rb_host, 128, hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess ||
+          hipHostGetDevicePointer((void**)&c->rb_dev, c->rb_host, 0) != hipSuccess)
+        return set_error(c, GS_ENOMEM, "pinned read-back block");
+      c->rb_host[8] = 0;
+    }
+    const uint64_t seq = early ? ++c->rb_seq : 0;
     hipLaunchKernelGGL((k_bk_emit<P>), dim3(nb), dim3(256), 0, c->stream, meta + BkMeta::BSTART, meta + BkMeta::BCOUNT,
                        nb, st, base, o, (unsigned long long*)(sm + SM_BK_MM + 24), mm, (const uint32_t*)(sm + SM_TIMEOUT),
-                       (const unsigned long long*)(sm + SM_BK_ESC), (unsigned long long*)(sm + SM_BK_X));
+                       (const unsigned long long*)(sm + SM_BK_ESC), (unsigned long long*)(sm + SM_BK_X),
+                       early ? (unsigned long long*)c->rb_dev : nullptr, seq);
+    if (early) {
+      GS_HIP(hipGetLastError());
+      c->rb_pending = true;
+      return GS_OK;
+    }
   }
   GS_HIP(hipGetLastError());
   stage_event(c, c->pass_ev[ev0 + 3]);
   stage_event(c, c->ev[3]);
   static_assert(SM_BK_N == SM_BK_MM + 32 && SM_BK_X == SM_BK_MM + 48, "one read-back block");
   GS_HIP(hipMemcpyAsync(c->host_small, sm + SM_BK_MM, 64, hipMemcpyDeviceToHost, c->stream));
+  return GS_OK;
+}
+
+gs_status bucket_wait(gs_ctx* c) {
+  if (!c->rb_pending) return host_wait(c);
+  c->rb_pending = false;
+  volatile uint64_t* h = c->rb_host;
+  const uint64_t seq = c->rb_seq;
+  const auto t0 = std::chrono::steady_clock::now();
+  for (uint32_t spin = 0; h[8] != seq; ++spin) {
+    // every 4096 polls: past 2 ms of spinning, wait for the stream instead (a long window, or a fault: its
+    // error surfaces there); the block must then be there
+    if ((spin & 4095) == 4095 && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(2)) {
+      GS_TRY(hip_check(c, hipStreamSynchronize(c->stream), "hipStreamSynchronize"));
+      if (h[8] != seq) return set_error(c, GS_EDEVICE, "bucket path: the read-back block never arrived");
+      break;
+    }
+  }
+  std::atomic_thread_fence(std::memory_order_acquire);
+  for (int i = 0; i < 8; ++i) c->host_small[i] = h[i];
   return GS_OK;
 }
 
@@ -433,7 +473,7 @@ gs_status bucket_direct_t(gs_ctx* c, const int64_t* src, const int64_t* dst, con
         if (pack) GS_TRY((bucket_accumulate<P>(c, PackSrc<Raw>{c->keysB.as<uint32_t>(), vpart}, cap, nb, base, o, 2, cur)));
         else GS_TRY((bucket_accumulate<P>(c, PartSrc<Raw>{k16, vpart}, cap, nb, base, o, 2, cur)));
         if (defer) return GS_PENDING_LOCAL;
-        GS_TRY(host_wait(c));
+        GS_TRY(bucket_wait(c));
         if (!c->host_small[2]) {   // hit: every key in the range; the plan reported the occupied buckets
           kmin = (int64_t)((uint64_t)base + (c->host_small[0] << S));
           kmax = (int64_t)((uint64_t)base + (c->host_small[1] << S) + ((1ull << S) - 1));
@@ -504,7 +544,7 @@ gs_status bucket_direct_t(gs_ctx* c, const int64_t* src, const int64_t* dst, con
       const BaseSrc<Raw, DIR, P::PAY> es{src, dst, (const Raw*)val, base};
       GS_TRY((bucket_accumulate<P>(c, es, R, nb, base, o, 2)));
     }
-    GS_TRY(host_wait(c));
+    GS_TRY(bucket_wait(c));
     kmin = key_min(c->host_small);
     kmax = key_max(c->host_small);
     if ((((uint64_t)kmax - (uint64_t)kmin) >> S) >= (uint64_t)BK_MAXB) return GS_EUNSUPPORTED;
@@ -627,7 +667,7 @@ gs_status bucket_onesweep(gs_ctx* c, const int64_t* src, const int64_t* dst, con
     GS_TRY((bucket_accumulate<P>(c, es, R, g.nb, base, o, g.passes)));
   else
     GS_TRY((bucket_accumulate<P>(c, PartSrc<Raw>{k16, vpart}, R, g.nb, base, o, g.passes)));
-  GS_TRY(host_wait(c));
+  GS_TRY(bucket_wait(c));
   GS_TRY(bucket_results(c, U, &n_items));
   const uint32_t key_bits = g.nb <= 1 ? (uint32_t)S : (uint32_t)(S + 32 - __builtin_clz(g.nb - 1));
   bucket_times(c, 1, g.passes, g.passes + 3, key_bits, R, *U, HAS_V ? sizeof(Raw) : 0, n_items);

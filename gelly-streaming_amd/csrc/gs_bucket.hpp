@@ -2215,6 +2215,10 @@ __global__ __launch_bounds__(BK_ACC_BLOCK) void k_bk_merge(const uint32_t* __res
 
 // ---- k_bk_emit: staging -> outputs, vertices ascending --------------------------------------------
 template <class P>
+// host (GS_FLAG_ASYNC_OUTPUT): block 0 first writes the window's whole read-back block -- the plan's and the
+// scatter's words, U (every bucket's count, final after the merges), the timeout flag and the escapes --
+// into pinned host memory, then `seq` behind a system-scope fence; the host returns on it while the other
+// blocks still emit (the outputs are complete in stream order).
 __global__ __launch_bounds__(256) void k_bk_emit(const uint32_t* __restrict__ bucket_start,
                                                  const uint32_t* __restrict__ bucket_count, uint32_t nb,
                                                  BkStage st, int64_t base, typename P::Out o,
@@ -2222,12 +2226,36 @@ __global__ __launch_bounds__(256) void k_bk_emit(const uint32_t* __restrict__ bu
                                                  const unsigned long long* __restrict__ mm,
                                                  const uint32_t* __restrict__ timeout,
                                                  const unsigned long long* __restrict__ n_esc,
-                                                 unsigned long long* __restrict__ res) {
+                                                 unsigned long long* __restrict__ res,
+                                                 unsigned long long* __restrict__ host = nullptr, uint64_t seq = 0) {
   __shared__ uint32_t s_w[4];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   if (blockIdx.x == 0 && tid == 0) {   // the read-back block: [timeout flag, escapes] after mm / ns
     res[0] = *timeout;
     res[1] = *n_esc;
+  }
+  if (host && blockIdx.x == 0) {
+    uint64_t tot = 0;
+    if (!mm[2])
+      for (uint32_t i = tid; i < nb; i += 256) tot += bucket_count[i];
+#pragma unroll
+    for (int o2 = 32; o2 > 0; o2 >>= 1) tot += __shfl_xor(tot, o2, WAVE);
+    __shared__ uint64_t s_tot[4];
+    if (lane == 0) s_tot[w] = tot;
+    __syncthreads();
+    if (tid == 0) {
+      const unsigned long long* ns = mm + 4;   // SM_BK_N = SM_BK_MM + 32: the plan's counts, two words
+      host[0] = mm[0];
+      host[1] = mm[1];
+      host[2] = mm[2];
+      host[3] = s_tot[0] + s_tot[1] + s_tot[2] + s_tot[3];
+      host[4] = ns[0];
+      host[5] = ns[1];
+      host[6] = *timeout;
+      host[7] = *n_esc;
+      __threadfence_system();
+      __hip_atomic_store(host + 8, (unsigned long long)seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
   }
   if (mm[2]) return;
   const uint32_t b = blockIdx.x;

@@ -478,6 +478,7 @@ void gs_destroy(gs_ctx* c) {
     if (e) hipEventDestroy(e);
   if (c->sync_ev) hipEventDestroy(c->sync_ev);
   if (c->host_small) hipHostFree(c->host_small);
+  if (c->rb_host) hipHostFree(c->rb_host);
   if (c->own_stream && c->stream) hipStreamDestroy(c->stream);
   delete c;
 }
@@ -660,6 +661,19 @@ static gs_status window_chunked(gs_ctx* c, const gs_edge_batch* b, int32_t dir, 
   return set_error(c, GS_EINVAL, "chunked window: no chunks");
 }
 
+// GS_FLAG_ASYNC_OUTPUT for one window: the bucket path may leave its read-back to the emit kernel's first block
+// (bucket_wait) when the outputs go straight to the caller's device buffers; cleared on every exit
+struct RbAllow {
+  gs_ctx* c;
+  RbAllow(gs_ctx* c_, bool direct) : c(c_) {
+    c->rb_allow = (c->flags & GS_FLAG_ASYNC_OUTPUT) && direct && c->timing != GS_TIMING_STAGES && !c->oe.nparts;
+  }
+  ~RbAllow() {
+    c->rb_allow = false;
+    c->rb_pending = false;
+  }
+};
+
 static gs_status window_fold_impl(gs_ctx* c, const gs_edge_batch* b, int32_t dir, int32_t op, bool has_init,
                                   const void* init, gs_vertex_out* out) {
   GS_TRY(check_batch_any(c, b, dir));
@@ -692,6 +706,7 @@ static gs_status window_fold_impl(gs_ctx* c, const gs_edge_batch* b, int32_t dir
   const int vbytes = (int)dtype_bytes(b->val_dtype);
   const size_t ob = op == GS_OP_COUNT ? 8 : (size_t)vbytes;
   const bool direct = out->mem == GS_MEM_DEVICE && out->capacity >= R;
+  const RbAllow rb(c, direct);
   int64_t* kd = out->keys;
   void* vd = out->vals;
   if (!direct) {
@@ -785,6 +800,7 @@ gs_status gs_window_fold_degree_max(gs_ctx* c, const gs_edge_batch* b, int32_t d
   const void* val;
   GS_TRY(stage_batch(c, b, &src, &dst, &val, false));
   const bool direct = out->mem == GS_MEM_DEVICE && out->capacity >= R;
+  const RbAllow rb(c, direct);
   int64_t *kd = out->keys, *dd = out->degree, *md = out->max_neighbor;
   if (!direct) {
     GS_TRY(ensure(c, c->out_keys, R * 8));

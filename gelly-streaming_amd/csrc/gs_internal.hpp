@@ -165,6 +165,13 @@ struct gs_ctx {
   hipEvent_t pass_ev[9] = {};
   gs_stage_times times{};
   uint64_t* host_small = nullptr;  // pinned mirror of small scalars
+  // GS_FLAG_ASYNC_OUTPUT: the bucket path's read-back block, written into pinned host memory by the emit
+  // kernel's first block (rb_dev is its device address) and followed by a sequence word the host spins on
+  uint64_t* rb_host = nullptr;
+  uint64_t* rb_dev = nullptr;
+  uint64_t rb_seq = 0;
+  bool rb_allow = false;     // set by the entry point for this window (direct device outputs, not STAGES)
+  bool rb_pending = false;   // the last bucket_accumulate left its read-back to bucket_wait
 };
 
 namespace gs {
@@ -266,6 +273,9 @@ gs_status host_wait(gs_ctx* c);
 // e.g. torch's, would otherwise surface at our next post-launch hipGetLastError), select the device and
 // clear the look-back timeout word
 gs_status begin_call(gs_ctx* c);
+// after bucket_accumulate: the read-back block in host_small[0..7] (a host-memory spin when the window's
+// read-back went through rb_host, else host_wait)
+gs_status bucket_wait(gs_ctx* c);
 // milliseconds between two recorded events; 0 (and no sticky error left behind) when either was not
 // recorded on this call's path -- hipEventElapsedTime's hipErrorInvalidHandle must not reach the next
 // launch check as "invalid resource handle"

@@ -109,10 +109,16 @@ def _out_dtypes():
 
 class Engine:
     def __init__(self, device: int = 0, reserve_edges: int = 0, torch_stream: bool = True, sort_only: bool = False,
-                 bk_onesweep: bool = False, no_pack: bool = False, no_spec: bool = False, flags: int = 0):
+                 bk_onesweep: bool = False, no_pack: bool = False, no_spec: bool = False, flags: int = 0,
+                 async_outputs: bool = True):
+        """torch_stream: the library runs on torch's current stream (its tensors are ordered with our kernels).
+        async_outputs (with torch_stream): reduce / fold / fold_degree_max into device tensors return as soon
+        as the window's sizes are known; the last kernel may still be writing the outputs, which torch work on
+        the same stream sees complete (GS_FLAG_ASYNC_OUTPUT) -- switch torch streams only after synchronizing."""
         self._L = L.load()
         flags |= (L.GS_FLAG_SORT_ONLY if sort_only else 0) | (L.GS_FLAG_BK_ONESWEEP if bk_onesweep else 0) | \
-            (L.GS_FLAG_NO_PACK if no_pack else 0) | (L.GS_FLAG_NO_SPEC if no_spec else 0)
+            (L.GS_FLAG_NO_PACK if no_pack else 0) | (L.GS_FLAG_NO_SPEC if no_spec else 0) | \
+            (L.GS_FLAG_ASYNC_OUTPUT if (torch_stream and async_outputs) else 0)
         cfg = L.GsConfig(device, flags, reserve_edges)
         ctx = ctypes.c_void_p()
         st = self._L.gs_create(ctypes.byref(cfg), ctypes.byref(ctx))
@@ -247,7 +253,36 @@ class Engine:
         """gs_window_fold: foldNeighbors(init, op). Returns (keys, values)."""
         return self._fold(src, dst, val, direction, op, init)
 
+    # A streaming operator calls reduce with the same device columns and out= buffers window after window
+    # (the bench cycles its windows): the ctypes arguments built for such a call are kept, keyed by the
+    # tensors' identities and checked against their data pointers, so the next call goes straight to the
+    # library -- the Python between two windows is GPU idle time.
+    _ARGS_KEEP = 8
+
     def _fold(self, src, dst, val, direction, op, init, out=None):
+        if init is None and out is not None and _is_torch(src):
+            v = None if op == L.GS_OP_COUNT else val
+            key = (id(src), id(dst), id(v), int(direction), int(op), id(out[0]), id(out[1]))
+            ptrs = (src.data_ptr(), dst.data_ptr(), v.data_ptr() if v is not None else 0, out[0].data_ptr(),
+                    out[1].data_ptr(), src.numel())
+            args = getattr(self, "_args", None)
+            if args is None:
+                args = self._args = {}
+            hit = args.get(key)
+            if hit is None or hit[0] != ptrs:
+                b, _, dev = self._batch(src, dst, v)
+                R = self._records(b.n, direction)
+                odt = np.int64 if op == L.GS_OP_COUNT else L.NP_DTYPE[b.val_dtype]
+                self._check_out(out, dev, (np.int64, odt), R)
+                n_out = ctypes.c_uint64(0)
+                vo = L.GsVertexOut(_ptr(out[0]), _ptr(out[1]), R, ctypes.pointer(n_out), L.GS_MEM_DEVICE, 0)
+                if len(args) >= self._ARGS_KEEP:
+                    args.pop(next(iter(args)))
+                # (the tensors are held: their ids stay theirs while the entry lives)
+                hit = args[key] = (ptrs, ctypes.byref(b), ctypes.byref(vo), n_out, (b, vo, src, dst, v, out))
+            self._check(self._L.gs_window_reduce(self.ctx, hit[1], int(direction), int(op), hit[2]))
+            U = hit[3].value
+            return out[0][:U], out[1][:U]
         b, keep, dev = self._batch(src, dst, None if op == L.GS_OP_COUNT else val)
         R = self._records(b.n, direction)
         odt = np.int64 if op == L.GS_OP_COUNT else L.NP_DTYPE[b.val_dtype]

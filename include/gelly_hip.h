@@ -95,6 +95,14 @@ typedef struct gs_ctx gs_ctx;
                                   per-tile bucket histograms first; A/B measurement; same results)  */
 #define GS_FLAG_TEST_FORCE_EXCHANGE 32u /* TEST ONLY: gs_window_*_dist on a one-rank communicator still
                                   runs the owner partition, the exchange (to itself) and the merge   */
+#define GS_FLAG_ASYNC_OUTPUT 64u /* gs_window_reduce / gs_window_fold / gs_window_fold_degree_max with
+                                  DEVICE outputs (GS_MEM_DEVICE, capacity >= the window's records):
+                                  the call returns once the window's sizes are known (*n_out), while
+                                  the last kernel may still be writing the outputs; they are complete
+                                  in the order of the ctx's stream (gs_set_stream), so a caller that
+                                  reads them on that stream -- or after gs_synchronize -- needs no
+                                  wait.  Host outputs and every other entry point are unchanged.
+                                  Default (0): every call returns with its outputs complete.        */
 
 typedef struct gs_config {
   int32_t device;          /* HIP device ordinal                                           */

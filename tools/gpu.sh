@@ -76,6 +76,12 @@ case $MODE in
     bench bench_e2e_direct --workload e2e --staging direct --no-cpu-baseline
     bench bench_e2e_pinned --workload e2e --staging pinned --no-cpu-baseline
     bench bench_e2e_buffered --workload e2e --staging buffered --no-cpu-baseline ;;
+  syncab)
+    # A/B of GS_FLAG_ASYNC_OUTPUT (default) against calls that wait for their outputs, alternated twice
+    for rep in 1 2; do
+      bench ab_async_$rep --no-cpu-baseline "$@"
+      bench ab_sync_$rep --no-cpu-baseline --sync-outputs "$@"
+    done ;;
   c2trace)
     # the C2 window's kernel timeline (gaps between kernels and between windows), from a kernel trace
     trace trace_c2 "$@"
