@@ -191,7 +191,9 @@ def direct_kernel_table(times_list, E, U_avg, stage_list, nbr_payload=False):
     spec = t0.speculative == 1   # regions from the previous window's counts: no histogram, no offset scans
     name = ("sp_scatter_pack" if spec else "dp_scatter_pack") if t0.packed else ("sp_scatter" if spec else "dp_scatter")
     rows[name] = {"ms": mean(lambda t: t.pass_ms[1]), "bytes": E * ((8 + lb) + (2 + vb))}
-    rows["bucket_accumulate"] = {"ms": mean(lambda t: t.pass_ms[2]), "bytes": E * (2 + vb) + U_avg * (4 + ab)}
+    acc_ms = mean(lambda t: t.pass_ms[2])   # (0: the timed windows bracketed the scatter only)
+    rows["bucket_accumulate"] = {"ms": acc_ms if acc_ms > 0 else smean(lambda t: t.pass_ms[2]),
+                                 "bytes": E * (2 + vb) + U_avg * (4 + ab)}
     rows["bucket_merge"] = {"ms": smean(lambda t: t.pass_ms[3]), "bytes": 0}
     rows["bucket_emit"] = {"ms": smean(lambda t: t.pass_ms[4]), "bytes": U_avg * (4 + ab + 16)}
     if spec:

@@ -16,6 +16,11 @@
 #include "gs_ops.hpp"
 #include <atomic>
 #include <chrono>
+// GS_TIMING_DOMINANT brackets the scatter and (1) the accumulate with dispatch-carried events; 0: the scatter
+// only (the accumulate's time then comes from windows timed at GS_TIMING_STAGES)
+#ifndef GS_DOM_ACCUM
+#define GS_DOM_ACCUM 1
+#endif
 
 #include "gs_bucket.hpp"
 
@@ -186,7 +191,7 @@ gs_status bucket_accumulate(gs_ctx* c, Src rs, uint64_t R, uint32_t nb, int64_t 
              (std::is_same_v<P, BkDeg> || std::is_same_v<P, BkDeg32>) ? c->aux.as<int64_t>() : nullptr};
   auto* slabs = c->bk_slabs.as<typename P::Lds>();
   // the direct path's accumulate (ev0 2) is a dominant kernel: its own start (pass_ev[7]) and stop events
-  const bool dom = ev0 == 2 && c->timing == GS_TIMING_DOMINANT;
+  const bool dom = GS_DOM_ACCUM && ev0 == 2 && c->timing == GS_TIMING_DOMINANT;
   launch_dominant(c, dom ? c->pass_ev[7] : nullptr, dom ? c->pass_ev[ev0 + 1] : nullptr, k_bk_accum<P, Src, GS_BK_UNROLL>,
                   dim3(c->n_cu * GS_BK_ACC_PER_CU), dim3(BK_ACC_BLOCK), rs, (const BkItem*)c->bk_items.as<BkItem>(),
                   (const uint32_t*)(ns + 0), (const uint32_t*)(meta + BkMeta::BSTART), ns + 2, slabs, st,
@@ -312,7 +317,7 @@ void bucket_times(gs_ctx* c, int path, int passes, int launches, uint32_t key_bi
   if (!all) {   // only the events stage_event recorded at this level
     if (c->timing == GS_TIMING_DOMINANT && path == 2) {   // the scatter and the accumulate (launch_dominant)
       if (passes) t.pass_ms[1] = event_ms(c->pass_ev[1], c->pass_ev[2]);
-      t.pass_ms[2] = event_ms(c->pass_ev[7], c->pass_ev[3]);
+      if (GS_DOM_ACCUM) t.pass_ms[2] = event_ms(c->pass_ev[7], c->pass_ev[3]);
     }
   }
 }
