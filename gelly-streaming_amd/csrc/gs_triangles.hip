@@ -309,6 +309,107 @@ __global__ __launch_bounds__(256) void k_tri_okeys_hi(uint64_t* __restrict__ key
   flush_hist<4>(h, nd, hist);
 }
 
+// ---- the same keys with cache-local rank gathers (round 6) -------------------------------------------
+// The split above still gathers each endpoint's rank at random from a 128 MB half table (2^31 gathers at
+// s26, each a 32-64 byte sector beyond L2: ~120 GB of fabric traffic, 38.6 ms).  Here the records are
+// first partitioned by the top PB bits of their source id (one onesweep pass over a << 32 | b), so the
+// records in flight all gather rank[a] from one 2^(B-PB)-entry slice of the table (1 MB at s26), which
+// every XCD's L2 keeps; the second pass gathers rank[a] on its load and partitions b << 32 | rank(a) by the
+// top bits of b; the last pass resolves rank(b) the same way, orients and counts the sort's histograms.
+// Partition histograms of both endpoints (k_tri_phist) give the two passes their digit bases.
+constexpr uint32_t OK_LOOP = 0xFFFFFFFFu;   // pass 2's rank(a) of a self-loop
+struct TriPartA {   // pass 1 records: the window's columns -> a << 32 | b
+  const int64_t* src;
+  const int64_t* dst;
+  uint64_t key_xor;
+  __device__ __forceinline__ void load(uint32_t r, uint64_t& k, uint8_t&) const {
+    const uint64_t a = ((uint64_t)src[r] ^ key_xor) & 0xFFFFFFFFull, b = ((uint64_t)dst[r] ^ key_xor) & 0xFFFFFFFFull;
+    k = (a << 32) | b;
+  }
+};
+struct TriPartB {   // pass 2 records: a << 32 | b -> b << 32 | rank(a), gathered from the partition's slice
+  const uint64_t* keys;
+  const uint32_t* rank;
+  __device__ __forceinline__ void load(uint32_t r, uint64_t& k, uint8_t&) const {
+    const uint64_t x = keys[r];
+    const uint32_t a = (uint32_t)(x >> 32), b = (uint32_t)x;
+    const uint32_t ra = rank[a];   // unconditional: the ITEMS gathers of a lane issue together
+    k = ((uint64_t)b << 32) | (a != b ? ra : OK_LOOP);
+  }
+};
+
+// 256-bin histograms of both endpoints' top bits (id >> sh): hist[0][..] sources, hist[1][..] targets
+__global__ __launch_bounds__(256) void k_tri_phist(const int64_t* __restrict__ src, const int64_t* __restrict__ dst,
+                                                   uint64_t n, uint64_t key_xor, uint32_t sh,
+                                                   uint32_t* __restrict__ hist) {
+  __shared__ uint32_t h[4][8][RADIX];
+  const int tid = threadIdx.x, w = tid >> 6;
+  for (int i = tid; i < 4 * 8 * RADIX; i += 256) (&h[0][0][0])[i] = 0;
+  __syncthreads();
+  constexpr int U = 4;
+  const uint64_t stride = (uint64_t)gridDim.x * 256 * U;
+  for (uint64_t i0 = (uint64_t)blockIdx.x * 256 * U; i0 < n; i0 += stride) {   // wave-uniform trip count
+    uint64_t a[U], b[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint64_t i = min(i0 + 256 * u + tid, n - 1);
+      a[u] = (uint64_t)src[i] ^ key_xor;
+      b[u] = (uint64_t)dst[i] ^ key_xor;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint64_t k = ((a[u] >> sh) & 255u) | (((b[u] >> sh) & 255u) << 8);
+      wave_hist_add(h[w], k, i0 + 256 * u + tid < n, 2);
+    }
+  }
+  __syncthreads();
+  flush_hist<4>(h, 2, hist);
+}
+
+// pass 3: b << 32 | rank(a) (partitioned by b) -> oriented keys, self-loops, the sort's histograms
+template <int U>
+__global__ __launch_bounds__(256) void k_tri_okeys_part(const uint64_t* __restrict__ in, uint64_t n, uint32_t B,
+                                                        const uint32_t* __restrict__ rank, uint64_t* __restrict__ out,
+                                                        uint32_t* __restrict__ loop_bits,
+                                                        unsigned long long* __restrict__ loops,
+                                                        uint32_t* __restrict__ hist) {
+  __shared__ uint32_t h[4][8][RADIX];
+  const int tid = threadIdx.x, w = tid >> 6;
+  for (int i = tid; i < 4 * 8 * RADIX; i += 256) (&h[0][0][0])[i] = 0;
+  __syncthreads();
+  const int nd = (int)(2 * B + 7) / 8;
+  const uint64_t sent = (B * 2 >= 64) ? ~0ull : ((1ull << (2 * B)) - 1);
+  const uint64_t stride = (uint64_t)gridDim.x * 256 * U;
+  for (uint64_t i0 = (uint64_t)blockIdx.x * 256 * U; i0 < n; i0 += stride) {   // wave-uniform trip count
+    uint64_t x[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) x[u] = in[min(i0 + 256 * u + tid, n - 1)];
+    uint32_t rb[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) rb[u] = rank[(uint32_t)(x[u] >> 32)];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint64_t i = i0 + 256 * u + tid;
+      const bool ok = i < n;
+      const uint32_t b = (uint32_t)(x[u] >> 32), ra = (uint32_t)x[u];
+      uint64_t k = sent;
+      if (ok) {
+        if (ra != OK_LOOP) {
+          const uint64_t p = ra, q = rb[u];
+          k = p < q ? (p << B) | q : (q << B) | p;
+        } else {
+          atomicOr(&loop_bits[b >> 5], 1u << (b & 31));
+          atomicAdd(loops, 1ull);
+        }
+        out[i] = k;
+      }
+      wave_hist_add(h[w], k, ok, nd);
+    }
+  }
+  __syncthreads();
+  flush_hist<4>(h, nd, hist);
+}
+
 // the unique oriented edges (sorted keys u << B | v) -> out-lists: nbr[p] = v, out_range[u] =
 // [first, last + 1) (ranges of absent vertices were zeroed)
 __global__ __launch_bounds__(256) void k_tri_out(const uint64_t* __restrict__ keys, uint32_t M, uint32_t B,
@@ -873,10 +974,38 @@ gs_status tri_okeys(gs_ctx* c, const TriGeom& g, const uint32_t* rank, uint64_t*
   GS_HIP(hipMemsetAsync(sm + SM_HIST, 0, 8 * 256 * 4, c->stream));
   static const int split_env = getenv("GS_TRI_OKEYS_SPLIT") ? atoi(getenv("GS_TRI_OKEYS_SPLIT")) : -1;   // A/B
   static const int unroll = getenv("GS_TRI_OKEYS_UNROLL") ? atoi(getenv("GS_TRI_OKEYS_UNROLL")) : 4;     // A/B: 1, 2, 4
+  static const int part_env = getenv("GS_TRI_OKEYS_PART") ? atoi(getenv("GS_TRI_OKEYS_PART")) : -1;     // A/B
   const bool split = split_env >= 0 ? split_env != 0 : g.V > (1ull << 25);
+  const bool part = g.n && g.n < (1ull << 32) && g.B >= 8 && (part_env >= 0 ? part_env != 0 : g.V > (1ull << 25));
   const int U = unroll >= 4 ? 4 : unroll >= 2 ? 2 : 1;
   const uint64_t steps = (g.n + 256ull * U - 1) / (256ull * U);
-  if (g.n && split) {   // two passes over halves of the rank table (k_tri_okeys_lo / _hi)
+  if (part) {   // records partitioned by each endpoint in turn: L2-local rank gathers (TriPartA / TriPartB)
+    const uint32_t sh = g.B - 8, R = (uint32_t)g.n, tiles = (R + SORT_TILE - 1) / SORT_TILE;
+    uint32_t* ph = (uint32_t*)(sm + SM_HIST9);   // [2][256] partition histograms, then (SM_BASE9) their bases
+    uint32_t* pb = (uint32_t*)(sm + SM_BASE9);
+    uint32_t* ctr = (uint32_t*)(sm + SM_COUNTERS) + 56;
+    GS_HIP(hipMemsetAsync(ph, 0, 2 * RADIX * 4, c->stream));
+    GS_HIP(hipMemsetAsync(ctr, 0, 8, c->stream));
+    hipLaunchKernelGGL(k_tri_phist, dim3((unsigned)std::min<uint64_t>((g.n + 1023) / 1024, 4096)), dim3(256), 0, c->stream,
+                       g.src, g.dst, g.n, g.key_xor, sh, ph);
+    hipLaunchKernelGGL(k_digit_base, dim3(1), dim3(256), 0, c->stream, (const uint32_t*)ph, pb, 2);
+    GS_TRY(ensure(c, c->keysA, g.n * 8));
+    GS_TRY(ensure(c, c->keysB, g.n * 8));
+    GS_TRY(ensure(c, c->sort_status, (size_t)tiles * RADIX * 8, true));
+    uint64_t* ka = c->keysA.as<uint64_t>();
+    uint64_t* kb = c->keysB.as<uint64_t>();
+    const uint32_t ep1 = next_epoch(c, 0);
+    hipLaunchKernelGGL((k_onesweep<uint64_t, uint8_t, false, SORT_BLOCK, SORT_ITEMS, TriPartA>), dim3(tiles), dim3(SORT_BLOCK),
+                       0, c->stream, TriPartA{g.src, g.dst, g.key_xor}, ka, nullptr, R, 32 + sh, (const uint32_t*)pb,
+                       c->sort_status.as<uint64_t>(), ctr, ep1, (uint32_t*)(sm + SM_TIMEOUT));
+    const uint32_t ep2 = next_epoch(c, 0);
+    hipLaunchKernelGGL((k_onesweep<uint64_t, uint8_t, false, SORT_BLOCK, SORT_ITEMS, TriPartB>), dim3(tiles), dim3(SORT_BLOCK),
+                       0, c->stream, TriPartB{ka, rank}, kb, nullptr, R, 32 + sh, (const uint32_t*)pb + RADIX,
+                       c->sort_status.as<uint64_t>(), ctr + 1, ep2, (uint32_t*)(sm + SM_TIMEOUT));
+    hipLaunchKernelGGL(k_tri_okeys_part<4>, dim3((unsigned)std::min<uint64_t>((g.n + 1023) / 1024, 8192)), dim3(256), 0,
+                       c->stream, kb, g.n, g.B, rank, keys, c->tri_loops.as<uint32_t>(), d_loops, (uint32_t*)(sm + SM_HIST));
+    GS_HIP(hipGetLastError());
+  } else if (g.n && split) {   // two passes over halves of the rank table (k_tri_okeys_lo / _hi)
     const unsigned glo = (unsigned)std::min<uint64_t>(steps, 16384 / U), ghi = (unsigned)std::min<uint64_t>(steps, 8192 / U);
     const uint32_t H = (uint32_t)(g.V / 2);
     uint32_t* lb = c->tri_loops.as<uint32_t>();

@@ -79,6 +79,9 @@ constexpr uint32_t TH_LONG = GS_TH_LONG;
 #ifndef GS_TH_LWAVES
 #define GS_TH_LWAVES 6   // k_tri_light waves per SIMD the registers are capped for (4 -> 6: s22 3.03 -> 2.38 ms)
 #endif
+#ifndef GS_TH_PIPE
+#define GS_TH_PIPE 0     // k_tri_heavy: gathers of the next step issued before this step's probes (A/B)
+#endif
 #ifndef GS_TH_HWAVES
 #define GS_TH_HWAVES 6   // k_tri_heavy: three 512-thread blocks per CU (4 -> 6: s22 11.4 -> 9.8 ms, s24 72.3 -> 62.5)
 #endif
@@ -667,7 +670,7 @@ __global__ __launch_bounds__(TH_HBLOCK) __attribute__((amdgpu_waves_per_eu(GS_TH
     // short lists: TH_ILP consecutive items per thread, at most one list boundary per step
     uint32_t top = 1;
     while (2 * top < ns) top <<= 1;
-    for (uint32_t k0 = 0; k0 < srun; k0 += TH_HBLOCK * TH_ILP) {
+    auto gather_short = [&](uint32_t k0, uint32_t (&x)[TH_ILP]) -> uint32_t {
       const uint32_t kb = k0 + tid * TH_ILP;
       const uint32_t kk = min(kb, srun - 1);
       uint32_t q = 0;
@@ -676,7 +679,6 @@ __global__ __launch_bounds__(TH_HBLOCK) __attribute__((amdgpu_waves_per_eu(GS_TH
         q = (t < ns && s_off[min(t, ns - 1)] <= kk) ? t : q;
       }
       uint32_t nx = s_off[q + 1], base = s_st[q] - s_off[q];   // item kj of list q: onbr[kj + base]
-      uint32_t x[TH_ILP];
 #pragma unroll
       for (int j = 0; j < TH_ILP; ++j) {
         const uint32_t kj = min(kb + j, srun - 1);
@@ -687,8 +689,36 @@ __global__ __launch_bounds__(TH_HBLOCK) __attribute__((amdgpu_waves_per_eu(GS_TH
         }
         x[j] = onbr[kj + base];
       }
-      cnt += probe(x, kb < srun ? min((uint32_t)TH_ILP, srun - kb) : 0u);
+      return kb < srun ? min((uint32_t)TH_ILP, srun - kb) : 0u;
+    };
+    constexpr uint32_t SSTEP = TH_HBLOCK * TH_ILP, LSTEP = WAVE * TH_ILP;
+#if GS_TH_PIPE
+    // (round 6) software-pipelined: step s + 1's list search and gathers issue before step s's probes,
+    // so the LDS search chain and the gathers' HBM latency of consecutive steps overlap
+    if (srun) {
+      uint32_t xa[TH_ILP];
+      uint32_t nva = gather_short(0, xa);
+      for (uint32_t k0 = 0; k0 < srun; k0 += SSTEP) {
+        uint32_t xb[TH_ILP], nvb = 0;
+        if (k0 + SSTEP < srun) {   // block-uniform
+          nvb = gather_short(k0 + SSTEP, xb);
+        } else {
+#pragma unroll
+          for (int j = 0; j < TH_ILP; ++j) xb[j] = 0u;
+        }
+        cnt += probe(xa, nva);
+#pragma unroll
+        for (int j = 0; j < TH_ILP; ++j) xa[j] = xb[j];
+        nva = nvb;
+      }
     }
+#else
+    for (uint32_t k0 = 0; k0 < srun; k0 += SSTEP) {
+      uint32_t x[TH_ILP];
+      const uint32_t nv = gather_short(k0, x);
+      cnt += probe(x, nv);
+    }
+#endif
     // long lists: wave w walks items [w, w + 1) * lrun / NW in 64-item segments (one load of 64
     // consecutive items); a segment spans at most two lists (every long list >= 64 items)
     if (lrun) {
@@ -706,8 +736,7 @@ __global__ __launch_bounds__(TH_HBLOCK) __attribute__((amdgpu_waves_per_eu(GS_TH
       // item k of list q: onbr[k + dq]; of list q + 1: onbr[k + dq1] (wave-uniform offsets)
       uint32_t qe = uni(s_loff[q + 1]), q1s = q + 1 < nl ? uni(s_lst[q + 1]) : 0u;
       uint32_t dq = uni(s_lst[q]) - uni(s_loff[q]), dq1 = q1s - qe;
-      for (uint32_t k0 = a0; k0 < a1; k0 += WAVE * TH_ILP) {
-        uint32_t x[TH_ILP];
+      auto gather_long = [&](uint32_t k0, uint32_t (&x)[TH_ILP]) -> uint32_t {
 #pragma unroll
         for (int j = 0; j < TH_ILP; ++j) {
           const uint32_t seg = k0 + (uint32_t)j * WAVE;   // wave-uniform
@@ -722,8 +751,33 @@ __global__ __launch_bounds__(TH_HBLOCK) __attribute__((amdgpu_waves_per_eu(GS_TH
           x[j] = onbr[k + (k < qe ? dq : dq1)];
         }
         const uint32_t rem = a1 - k0;
-        cnt += probe(x, rem > (uint32_t)lane ? min((uint32_t)TH_ILP, (rem - lane + WAVE - 1) / WAVE) : 0u);
+        return rem > (uint32_t)lane ? min((uint32_t)TH_ILP, (rem - lane + WAVE - 1) / WAVE) : 0u;
+      };
+#if GS_TH_PIPE
+      if (a0 < a1) {
+        uint32_t xa[TH_ILP];
+        uint32_t nva = gather_long(a0, xa);
+        for (uint32_t k0 = a0; k0 < a1; k0 += LSTEP) {
+          uint32_t xb[TH_ILP], nvb = 0;
+          if (k0 + LSTEP < a1) {   // wave-uniform
+            nvb = gather_long(k0 + LSTEP, xb);
+          } else {
+#pragma unroll
+            for (int j = 0; j < TH_ILP; ++j) xb[j] = 0u;
+          }
+          cnt += probe(xa, nva);
+#pragma unroll
+          for (int j = 0; j < TH_ILP; ++j) xa[j] = xb[j];
+          nva = nvb;
+        }
       }
+#else
+      for (uint32_t k0 = a0; k0 < a1; k0 += LSTEP) {
+        uint32_t x[TH_ILP];
+        const uint32_t nv = gather_long(k0, x);
+        cnt += probe(x, nv);
+      }
+#endif
     }
   }
 #pragma unroll

@@ -1,11 +1,14 @@
 """GPU: the oriented-key variants of the triangle count (gs_triangles.hip tri_okeys) on the same window.
 
 The key step has a one-pass form (k_tri_okeys: the whole rank table) and a two-pass form for rank
-tables past the Infinity Cache (k_tri_okeys_lo / _hi, chosen when V > 2^25), each with U = 1, 2 or 4
-edges per lane per step.  The default picks one combination per window size; GS_TRI_OKEYS_SPLIT and
-GS_TRI_OKEYS_UNROLL force the others (read once per process, so every case runs in its own
+tables past the Infinity Cache (k_tri_okeys_lo / _hi), each with U = 1, 2 or 4 edges per lane per step,
+and (round 6, chosen when V > 2^25) the partitioned form: the records partitioned by each endpoint's top
+id bits in turn, so each rank gather hits an L2-resident slice of the table (TriPartA / TriPartB,
+k_tri_okeys_part).  The default picks one form per window size; GS_TRI_OKEYS_PART, GS_TRI_OKEYS_SPLIT
+and GS_TRI_OKEYS_UNROLL force the others (read once per process, so every case runs in its own
 interpreter).  Every combination must give the forward algorithm's count (WindowTriangles.java:83-140
-restated in oracle/gs_oracle.c) on a self-loop-free R-MAT scale-18 window.
+restated in oracle/gs_oracle.c) on a self-loop-free R-MAT scale-18 window; the partitioned form also on
+a window that keeps its self-loops (the count less the self-pair term), where its pass 2 marks them.
 """
 import subprocess
 import sys
@@ -21,7 +24,7 @@ ROOT = Path(__file__).resolve().parent.parent
 SCRIPT = textwrap.dedent("""
     import os
     import sys
-    os.environ.update(GS_TRI_OKEYS_SPLIT="{split}", GS_TRI_OKEYS_UNROLL="{unroll}")
+    os.environ.update(GS_TRI_OKEYS_SPLIT="{split}", GS_TRI_OKEYS_UNROLL="{unroll}", GS_TRI_OKEYS_PART="{part}")
     import numpy as np
     sys.path.insert(0, {root!r})
     import __graft_entry__ as ge
@@ -31,16 +34,25 @@ SCRIPT = textwrap.dedent("""
     exact, wrapped, has = eng.triangles(s, d)
     want = orc.triangles_fwd_mt(s, d)
     assert exact == want, (exact, want)
+    if {loops}:   # R-MAT with its self-loops: count = triangles of the loop-free edges + the self-pair term
+        s, d = orc.gen_rmat(18, 16 << 18, 0x5EED05)
+        keep = s != d
+        assert (~keep).any()
+        exact, wrapped, has = eng.triangles(s, d)
+        sp = eng.triangles_selfpair(s, d)
+        want = orc.triangles_fwd_mt(s[keep], d[keep])
+        assert exact - sp == want, (exact, sp, want)
     eng.close()
     print("triangles", exact)
 """)
 
 
-@pytest.mark.parametrize("split,unroll", [(0, 1), (0, 2), (1, 1), (1, 2), (1, 4)])
-def test_okeys_variants_same_count(split, unroll):
+@pytest.mark.parametrize("split,unroll,part", [(0, 1, 0), (0, 2, 0), (1, 1, 0), (1, 2, 0), (1, 4, 0), (0, 4, 1)])
+def test_okeys_variants_same_count(split, unroll, part):
     # (the knobs are set inside the child, before the library reads them: the child inherits this
     # process's environment unchanged)
-    r = subprocess.run([sys.executable, "-c", SCRIPT.format(root=str(ROOT), split=split, unroll=unroll)],
+    r = subprocess.run([sys.executable, "-c", SCRIPT.format(root=str(ROOT), split=split, unroll=unroll,
+                                                                part=part, loops=part)],
                        capture_output=True, text=True, timeout=170)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "triangles" in r.stdout

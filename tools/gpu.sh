@@ -9,6 +9,7 @@
 #   sq      TAG [bench args]    SQ counter passes (LDS conflicts, waits, instruction mix) over a short bench
 #   tri     TAG SCALE           triangles: bench line, kernel-trace stats, FETCH / TCC hit / SQ passes
 #   evidence TAG                every secondary bench line DESIGN.md quotes
+#   envab   TAG "base K=V .." [args] A/B of environment knobs, alternated twice on one box
 #   ab      TAG "V1 V2.." [args] A/B of tuning builds (csrc/Makefile bvariant / variant -> variants/NAME; "base" =
 #                               the in-tree library): bench lines alternated twice on one box -> ab_NAME_REP.json
 #
@@ -76,6 +77,16 @@ case $MODE in
     bench bench_e2e_direct --workload e2e --staging direct --no-cpu-baseline
     bench bench_e2e_pinned --workload e2e --staging pinned --no-cpu-baseline
     bench bench_e2e_buffered --workload e2e --staging buffered --no-cpu-baseline ;;
+  envab)
+    # A/B of library knobs read from the environment ("base" = none; e.g. "base GS_TRI_OKEYS_PART=0"),
+    # alternated twice on one box -> ab_NAME_REP.json
+    VARIANTS=$1; shift
+    for rep in 1 2; do
+      for v in $VARIANTS; do
+        if [ "$v" = base ]; then bench ab_base_$rep "$@" --no-cpu-baseline
+        else ( export "$v"; bench "ab_${v//=/_}_$rep" "$@" --no-cpu-baseline ); fi
+      done
+    done ;;
   syncab)
     # A/B of GS_FLAG_ASYNC_OUTPUT (default) against calls that wait for their outputs, alternated twice
     for rep in 1 2; do
