@@ -367,17 +367,17 @@ __global__ __launch_bounds__(256) void k_tri_phist(const int64_t* __restrict__ s
 }
 
 // pass 3: b << 32 | rank(a) (partitioned by b) -> oriented keys, self-loops, the sort's histograms
+// (the histograms: of the nd bytes of key >> hshift -- the whole key, or u alone for the segmented sort)
 template <int U>
 __global__ __launch_bounds__(256) void k_tri_okeys_part(const uint64_t* __restrict__ in, uint64_t n, uint32_t B,
                                                         const uint32_t* __restrict__ rank, uint64_t* __restrict__ out,
                                                         uint32_t* __restrict__ loop_bits,
                                                         unsigned long long* __restrict__ loops,
-                                                        uint32_t* __restrict__ hist) {
+                                                        uint32_t hshift, int nd, uint32_t* __restrict__ hist) {
   __shared__ uint32_t h[4][8][RADIX];
   const int tid = threadIdx.x, w = tid >> 6;
   for (int i = tid; i < 4 * 8 * RADIX; i += 256) (&h[0][0][0])[i] = 0;
   __syncthreads();
-  const int nd = (int)(2 * B + 7) / 8;
   const uint64_t sent = (B * 2 >= 64) ? ~0ull : ((1ull << (2 * B)) - 1);
   const uint64_t stride = (uint64_t)gridDim.x * 256 * U;
   for (uint64_t i0 = (uint64_t)blockIdx.x * 256 * U; i0 < n; i0 += stride) {   // wave-uniform trip count
@@ -403,11 +403,254 @@ __global__ __launch_bounds__(256) void k_tri_okeys_part(const uint64_t* __restri
         }
         out[i] = k;
       }
-      wave_hist_add(h[w], k, ok, nd);
+      wave_hist_add(h[w], k >> hshift, ok, nd);
     }
   }
   __syncthreads();
   flush_hist<4>(h, nd, hist);
+}
+
+// ---- segmented sort of the oriented keys (round 6) ------------------------------------------------------
+// The oriented keys u << B | v need a full sort only so that each out-list comes out sorted (the count's
+// suffix trick and the unique step); the order between lists is u's.  So the global LSD passes sort by u
+// alone (ceil(B / 8) passes instead of ceil(2B / 8): s26 7 -> 4), and k_tri_segsort sorts each run of equal
+// u by v in LDS: a block takes the runs that start in its tile of SS_T keys (to the end of the last one),
+// up to SS_CAP keys, and sorts them stably by the local key (run index << B | v) in LDS passes of 8 bits.
+// A run that does not fit is queued for k_tri_segsort_long (a block per run: in LDS when it fits, else
+// stable 8-bit passes over the run in HBM through the free sort buffer).
+#ifndef GS_SS_ITEMS
+#define GS_SS_ITEMS 8
+#endif
+constexpr int SS_BLOCK = 512, SS_ITEMS = GS_SS_ITEMS, SS_CAP = SS_BLOCK * SS_ITEMS, SS_NW = SS_BLOCK / WAVE;
+constexpr uint32_t SS_T = SS_CAP / 2;   // run starts per block
+static_assert(SS_T <= (uint32_t)SS_CAP, "a block's tile must fit its LDS chunk");
+
+struct SsLds {
+  uint64_t k[SS_CAP];            // 64 KiB: the chunk's local keys between passes
+  uint32_t whist[SS_NW][RADIX];  // per-wave digit counters, then their exclusive prefix over the waves
+  uint32_t start[RADIX];         // the tile's digit starts
+  uint32_t cnt[RADIX];           // the tile's digit counts
+  uint32_t wtot[SS_NW];
+  unsigned long long bound[4];
+};
+
+// stable ranks by digit dg[j] of up to SS_CAP elements held wave-striped (item j of lane l in wave w is
+// element w * SS_ITEMS * 64 + j * 64 + l; valid below len): pos[j] = its place in digit order within the
+// tile, sh.cnt[d] = the tile's count of digit d (as k_onesweep's ranking, gs_radix.hpp)
+__device__ __forceinline__ void ss_rank(const uint32_t (&dg)[SS_ITEMS], uint32_t len, uint32_t (&pos)[SS_ITEMS], SsLds& sh) {
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  for (int i = tid; i < SS_NW * RADIX; i += SS_BLOCK) (&sh.whist[0][0])[i] = 0;
+  __syncthreads();
+  const uint32_t e0 = (uint32_t)w * (SS_ITEMS * WAVE) + lane;
+#pragma unroll
+  for (int j = 0; j < SS_ITEMS; ++j) {
+    const bool valid = e0 + j * WAVE < len;
+    const uint32_t d = valid ? dg[j] : 0u;
+    const uint64_t peers = match_digit<RADIX_BITS>(d, ballot(valid));
+    const uint32_t lt = mbcnt(peers);
+    uint32_t base = 0;
+    if (valid) base = sh.whist[w][d];
+    pos[j] = base + lt;
+    if (valid && lt == 0) sh.whist[w][d] = base + (uint32_t)__popcll(peers);
+  }
+  __syncthreads();
+  if (tid < RADIX) {
+    uint32_t c = 0;
+#pragma unroll
+    for (int x = 0; x < SS_NW; ++x) {
+      const uint32_t t = sh.whist[x][tid];
+      sh.whist[x][tid] = c;
+      c += t;
+    }
+    sh.cnt[tid] = c;
+    const uint32_t inc = wave_inclusive_sum(c);
+    if (lane == 63) sh.wtot[w] = inc;
+    sh.start[tid] = inc - c;
+  }
+  __syncthreads();
+  if (tid < RADIX) {
+    uint32_t off = 0;
+    for (int x = 0; x < w; ++x) off += sh.wtot[x];
+    sh.start[tid] += off;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < SS_ITEMS; ++j) pos[j] += e0 + j * WAVE < len ? sh.start[dg[j]] + sh.whist[w][dg[j]] : 0u;
+}
+
+// sort `len` (<= SS_CAP) keys at keys[s ..) by (u, v) in LDS, in place; runs of equal u are contiguous
+__device__ void ss_sort_chunk(uint64_t* __restrict__ keys, uint64_t s, uint32_t len, uint32_t B, SsLds& sh) {
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const uint64_t vmask = (1ull << B) - 1;
+  const uint32_t e0 = (uint32_t)w * (SS_ITEMS * WAVE) + lane;
+  uint64_t lk[SS_ITEMS];
+  uint32_t ku[SS_ITEMS], hb[SS_ITEMS], wrun = 0;   // u of each element; heads up to it within the wave
+#pragma unroll
+  for (int j = 0; j < SS_ITEMS; ++j) {   // unconditional, clamped loads
+    const uint32_t e = min(e0 + j * WAVE, len - 1);
+    const uint64_t k = keys[s + e], kp = keys[s + (e ? e - 1 : 0)];
+    ku[j] = (uint32_t)(k >> B);
+    lk[j] = k & vmask;
+    const bool head = e0 + j * WAVE < len && (e == 0 || (uint32_t)(kp >> B) != ku[j]);
+    const uint64_t m = ballot(head);
+    hb[j] = wrun + mbcnt(m) + (head ? 1u : 0u);   // inclusive
+    wrun += (uint32_t)__popcll(m);
+  }
+  // run index of each element: heads up to it, less one (a block scan in element order)
+  if (lane == 0) sh.wtot[w] = wrun;
+  __syncthreads();
+  uint32_t woff = 0, nruns = 0;
+  for (int x = 0; x < SS_NW; ++x) {
+    const uint32_t t = sh.wtot[x];
+    woff += x < w ? t : 0u;
+    nruns += t;
+  }
+  const uint32_t rbits = nruns > 1 ? 32u - (uint32_t)__clz(nruns - 1) : 0u;
+  const int passes = (int)((B + rbits + 7) / 8);
+#pragma unroll
+  for (int j = 0; j < SS_ITEMS; ++j) lk[j] |= (uint64_t)(woff + hb[j] - 1) << B;
+  for (int p = 0; p < passes; ++p) {
+    uint32_t dg[SS_ITEMS], pos[SS_ITEMS];
+#pragma unroll
+    for (int j = 0; j < SS_ITEMS; ++j) dg[j] = (uint32_t)(lk[j] >> (8 * p)) & 255u;
+    ss_rank(dg, len, pos, sh);
+#pragma unroll
+    for (int j = 0; j < SS_ITEMS; ++j)
+      if (e0 + j * WAVE < len) sh.k[pos[j]] = lk[j];
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < SS_ITEMS; ++j) lk[j] = sh.k[min(e0 + j * WAVE, len - 1)];
+    __syncthreads();   // (the next pass's counters and key writes)
+  }
+  // runs keep their places: element i of the sorted chunk has the u of the element that was at i
+#pragma unroll
+  for (int j = 0; j < SS_ITEMS; ++j)
+    if (e0 + j * WAVE < len) keys[s + e0 + j * WAVE] = ((uint64_t)ku[j] << B) | (lk[j] & vmask);
+}
+
+__global__ __launch_bounds__(SS_BLOCK) __attribute__((amdgpu_waves_per_eu(4, 4))) void k_tri_segsort(uint64_t* __restrict__ keys, uint64_t n, uint32_t B, uint32_t cap,
+                                                          uint64_t* __restrict__ long_runs,
+                                                          unsigned long long* __restrict__ n_long) {
+  __shared__ SsLds sh;
+  const int tid = threadIdx.x;
+  const uint64_t t0 = (uint64_t)blockIdx.x * SS_T, t1 = min(t0 + SS_T, n);
+  if (tid < 2) sh.bound[tid] = tid == 0 ? ~0ull : 0ull;
+  if (tid == 2) sh.bound[2] = n;
+  __syncthreads();
+  // the first and the last run start in [t0, t1)
+  constexpr uint32_t PER = SS_T / SS_BLOCK;
+  for (uint32_t j = 0; j < PER; ++j) {
+    const uint64_t i = t0 + (uint64_t)j * SS_BLOCK + tid;
+    if (i < t1 && (i == 0 || (keys[i - 1] >> B) != (keys[i] >> B))) {
+      atomicMin(&sh.bound[0], (unsigned long long)i);
+      atomicMax(&sh.bound[1], (unsigned long long)i);
+    }
+  }
+  __syncthreads();
+  const uint64_t s = sh.bound[0], h = sh.bound[1];
+  if (s == ~0ull) return;   // the whole tile lies inside a run that starts before it
+  // the end of the last run: the first run start at or after t1 (searched while the chunk still fits)
+  const uint64_t uh = keys[h] >> B;
+  for (uint64_t b0 = t1; b0 < n && b0 - s <= cap; b0 += SS_BLOCK) {
+    const uint64_t i = b0 + tid;
+    if (i < n && (keys[i] >> B) != uh) atomicMin(&sh.bound[2], (unsigned long long)i);
+    __syncthreads();
+    const bool found = sh.bound[2] != n;
+    __syncthreads();   // (every thread has read it before the next window's atomics)
+    if (found) break;
+  }
+  __syncthreads();
+  const uint64_t e = sh.bound[2];
+  uint64_t end = e;
+  if (e - s > cap) {   // the last run goes to k_tri_segsort_long; the runs before it (inside the tile) stay here
+    if (tid == 0) long_runs[atomicAdd(n_long, 1ull)] = h;
+    end = h;
+  }
+  if (end > s + 1) ss_sort_chunk(keys, s, (uint32_t)(end - s), B, sh);
+}
+
+// the runs k_tri_segsort queued (their starts), a block each: the run's end, then its keys sorted by v in
+// LDS (<= SS_CAP) or by stable passes of 8 bits over the run in HBM (keys -> tmp -> keys ..)
+__global__ __launch_bounds__(SS_BLOCK) __attribute__((amdgpu_waves_per_eu(4, 4))) void k_tri_segsort_long(uint64_t* __restrict__ keys, uint64_t* __restrict__ tmp,
+                                                               uint64_t n, uint32_t B, uint32_t lds_max,
+                                                               const uint64_t* __restrict__ runs,
+                                                               const unsigned long long* __restrict__ n_runs) {
+  __shared__ SsLds sh;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const uint64_t nr = *n_runs, vmask = (1ull << B) - 1;
+  for (uint64_t r = blockIdx.x; r < nr; r += gridDim.x) {
+    const uint64_t h = runs[r], uh = keys[h] >> B;
+    __syncthreads();
+    if (tid == 0) sh.bound[2] = n;
+    __syncthreads();
+    for (uint64_t b0 = h + 1; b0 < n; b0 += SS_BLOCK) {
+      const uint64_t i = b0 + tid;
+      if (i < n && (keys[i] >> B) != uh) atomicMin(&sh.bound[2], (unsigned long long)i);
+      __syncthreads();
+      const bool found = sh.bound[2] != n;
+      __syncthreads();
+      if (found) break;
+    }
+    __syncthreads();
+    const uint64_t e = sh.bound[2], L = e - h;
+    if (uh == vmask) continue;   // the self-loop sentinels: equal keys
+    if (L <= (uint64_t)lds_max) {
+      ss_sort_chunk(keys, h, (uint32_t)L, B, sh);
+      continue;
+    }
+    const int passes = (int)((B + 7) / 8);
+    const uint32_t e0 = (uint32_t)w * (SS_ITEMS * WAVE) + lane;
+    uint64_t* src = keys;
+    uint64_t* dst = tmp;
+    for (int p = 0; p < passes; ++p) {
+      const uint32_t shift = 8u * (uint32_t)p;
+      // the run's digit counts -> exclusive offsets (sh.bound[3] unused)
+      __syncthreads();
+      if (tid < RADIX) sh.whist[0][tid] = 0;
+      __syncthreads();
+      for (uint64_t i = h + tid; i < e; i += SS_BLOCK) atomicAdd(&sh.whist[0][(uint32_t)(src[i] >> shift) & 255u], 1u);
+      __syncthreads();
+      uint32_t goff = 0;   // thread d (< RADIX): the run's exclusive offset of digit d, carried over its tiles
+      if (tid < RADIX) {
+        const uint32_t c = sh.whist[0][tid];
+        const uint32_t inc = wave_inclusive_sum(c);
+        if (lane == 63) sh.wtot[w] = inc;
+        goff = inc - c;
+      }
+      __syncthreads();
+      if (tid < RADIX)
+        for (int x = 0; x < w; ++x) goff += sh.wtot[x];
+      // stable scatter, tile by tile in order
+      for (uint64_t t = h; t < e; t += SS_CAP) {
+        const uint32_t len = (uint32_t)min<uint64_t>(SS_CAP, e - t);
+        uint64_t k[SS_ITEMS];
+        uint32_t dg[SS_ITEMS], pos[SS_ITEMS];
+#pragma unroll
+        for (int j = 0; j < SS_ITEMS; ++j) {
+          k[j] = src[t + min(e0 + j * WAVE, len - 1)];
+          dg[j] = (uint32_t)(k[j] >> shift) & 255u;
+        }
+        __syncthreads();   // the previous tile's readers of sh.start / sh.k are done
+        if (tid < RADIX) sh.k[SS_CAP - RADIX + tid] = goff;   // (parked: ss_rank reuses whist / start / cnt)
+        ss_rank(dg, len, pos, sh);
+        // global place: the digit's offset so far + the rank among this tile's keys of that digit
+#pragma unroll
+        for (int j = 0; j < SS_ITEMS; ++j)
+          if (e0 + j * WAVE < len)
+            dst[h + sh.k[SS_CAP - RADIX + dg[j]] + (pos[j] - sh.start[dg[j]])] = k[j];
+        __syncthreads();
+        if (tid < RADIX) goff += sh.cnt[tid];
+      }
+      uint64_t* x = src;
+      src = dst;
+      dst = x;
+    }
+    if (src != keys) {   // an odd number of passes: back into keys
+      __syncthreads();
+      for (uint64_t i = h + tid; i < e; i += SS_BLOCK) keys[i] = src[i];
+    }
+    (void)vmask;
+  }
 }
 
 // the unique oriented edges (sorted keys u << B | v) -> out-lists: nbr[p] = v, out_range[u] =
@@ -459,12 +702,18 @@ __global__ __launch_bounds__(UO_BLOCK) void k_tri_uo_count(const uint64_t* __res
   }
 }
 
+// (hist, when not null: the transposed sort's digit histograms of the B-bit targets v, so its first pass can
+// read the out-lists directly -- TriTpaySrc -- instead of k_tri_tpay's copy)
 __global__ __launch_bounds__(UO_BLOCK) void k_tri_uo_write(const uint64_t* __restrict__ keys, uint64_t n, uint64_t sent,
                                                            uint32_t B, const unsigned long long* __restrict__ tile_pre,
                                                            uint32_t* __restrict__ nbr, uint32_t* __restrict__ rowid,
-                                                           uint32_t* __restrict__ out_range) {
+                                                           uint32_t* __restrict__ out_range, uint32_t* __restrict__ hist) {
   constexpr int NW = UO_BLOCK / WAVE;
   __shared__ uint32_t s_cnt[UO_ITEMS][NW];
+  __shared__ uint32_t s_h[NW][8][RADIX];
+  if (hist) {
+    for (int i = threadIdx.x; i < NW * 8 * RADIX; i += UO_BLOCK) (&s_h[0][0][0])[i] = 0;
+  }
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const uint64_t t0 = (uint64_t)blockIdx.x * UO_TILE;
   const uint64_t mask = (1ull << B) - 1;
@@ -506,7 +755,31 @@ __global__ __launch_bounds__(UO_BLOCK) void k_tri_uo_write(const uint64_t* __res
     const uint64_t kn = i + 1 < n ? keys[i + 1] : sent;   // the row ends at key i: the next key is another row's
     if (kn == sent || (uint32_t)(kn >> B) != u) out_range[2 * u + 1] = (uint32_t)(excl + (head ? 1u : 0u));
   }
+  if (hist) {   // (block-uniform) every lane of every wave takes part: wave_hist_add ballots (plain adds on
+               // the low digits and ballots on the top one only: 0.45 ms slower at s26)
+    const int nd = (int)(B + 7) / 8;
+    const uint64_t mask = (1ull << B) - 1;
+#pragma unroll
+    for (int j = 0; j < UO_ITEMS; ++j) {
+      const bool head = (hb[j] >> lane) & 1ull;
+      wave_hist_add(s_h[w], k[j] & mask, head, nd);
+    }
+    __syncthreads();
+    flush_hist<NW>(s_h, nd, hist);
+  }
 }
+
+// the transposed sort's first pass reads the out-lists directly: record p -> key v = nbr[p], payload the
+// suffix of N+(u) past v, [p + 1, end of N+(u)) (what k_tri_tpay would have written; u = rowid[p])
+struct TriTpaySrc {
+  const uint32_t* nbr;
+  const uint32_t* rowid;
+  const uint2* out_range;
+  __device__ __forceinline__ void load(uint32_t r, uint32_t& k, uint64_t& v) const {
+    k = nbr[r];
+    v = ((uint64_t)out_range[rowid[r]].y << 32) | (uint64_t)(r + 1);
+  }
+};
 
 // row (u) of each adjacency position of a slice, from the out-lists (one thread per u; d+(u) is
 // small under the degree orientation)
@@ -964,7 +1237,10 @@ gs_status tri_ranks(gs_ctx* c, const TriGeom& g, const uint32_t* deg, uint32_t* 
 
 // oriented keys of the ranks into keys[0 .. n) (+ self-loop bitmap; loop count -> host_small[4] after
 // the next wait; the digit histograms into SM_HIST)
-gs_status tri_okeys(gs_ctx* c, const TriGeom& g, const uint32_t* rank, uint64_t* keys) {
+// useg: histograms of u alone (the segmented sort) when the partitioned form runs -> *seg
+gs_status tri_okeys(gs_ctx* c, const TriGeom& g, const uint32_t* rank, uint64_t* keys, bool useg = false,
+                    bool* seg = nullptr) {
+  if (seg) *seg = false;
   char* sm = c->small.as<char>();
   const size_t words = (g.V + 31) / 32;
   GS_TRY(ensure(c, c->tri_loops, words * 4));
@@ -976,7 +1252,8 @@ gs_status tri_okeys(gs_ctx* c, const TriGeom& g, const uint32_t* rank, uint64_t*
   static const int unroll = getenv("GS_TRI_OKEYS_UNROLL") ? atoi(getenv("GS_TRI_OKEYS_UNROLL")) : 4;     // A/B: 1, 2, 4
   static const int part_env = getenv("GS_TRI_OKEYS_PART") ? atoi(getenv("GS_TRI_OKEYS_PART")) : -1;     // A/B
   const bool split = split_env >= 0 ? split_env != 0 : g.V > (1ull << 25);
-  const bool part = g.n && g.n < (1ull << 32) && g.B >= 8 && (part_env >= 0 ? part_env != 0 : g.V > (1ull << 25));
+  // partitioned on tables past the L2s (s24: 60.7 -> 58.9 ms, s26: 315.6 -> 305.2 ms; profiles/r06/tri/ab_okeys_part/)
+  const bool part = g.n && g.n < (1ull << 32) && g.B >= 8 && (part_env >= 0 ? part_env != 0 : g.V > (1ull << 23));
   const int U = unroll >= 4 ? 4 : unroll >= 2 ? 2 : 1;
   const uint64_t steps = (g.n + 256ull * U - 1) / (256ull * U);
   if (part) {   // records partitioned by each endpoint in turn: L2-local rank gathers (TriPartA / TriPartB)
@@ -1002,8 +1279,22 @@ gs_status tri_okeys(gs_ctx* c, const TriGeom& g, const uint32_t* rank, uint64_t*
     hipLaunchKernelGGL((k_onesweep<uint64_t, uint8_t, false, SORT_BLOCK, SORT_ITEMS, TriPartB>), dim3(tiles), dim3(SORT_BLOCK),
                        0, c->stream, TriPartB{ka, rank}, kb, nullptr, R, 32 + sh, (const uint32_t*)pb + RADIX,
                        c->sort_status.as<uint64_t>(), ctr + 1, ep2, (uint32_t*)(sm + SM_TIMEOUT));
-    hipLaunchKernelGGL(k_tri_okeys_part<4>, dim3((unsigned)std::min<uint64_t>((g.n + 1023) / 1024, 8192)), dim3(256), 0,
-                       c->stream, kb, g.n, g.B, rank, keys, c->tri_loops.as<uint32_t>(), d_loops, (uint32_t*)(sm + SM_HIST));
+    const uint32_t hshift = useg ? g.B : 0u;
+    const int nd = (int)((useg ? g.B : 2 * g.B) + 7) / 8;
+    // keys per lane per step (A/B, s26 keys + sort: 4 -> 78.7, 8 -> 77.2, 16 -> 76.7 ms; ab_okeys_part/okp_u_*)
+    static const int pu_env = getenv("GS_TRI_OKP_U") ? atoi(getenv("GS_TRI_OKP_U")) : 16;
+    const int PU = pu_env >= 16 ? 16 : pu_env >= 8 ? 8 : 4;
+    const unsigned gp = (unsigned)std::min<uint64_t>((g.n + 256ull * PU - 1) / (256ull * PU), 32768 / PU);
+    if (PU == 16)
+      hipLaunchKernelGGL(k_tri_okeys_part<16>, dim3(gp), dim3(256), 0, c->stream, kb, g.n, g.B, rank, keys,
+                         c->tri_loops.as<uint32_t>(), d_loops, hshift, nd, (uint32_t*)(sm + SM_HIST));
+    else if (PU == 8)
+      hipLaunchKernelGGL(k_tri_okeys_part<8>, dim3(gp), dim3(256), 0, c->stream, kb, g.n, g.B, rank, keys,
+                         c->tri_loops.as<uint32_t>(), d_loops, hshift, nd, (uint32_t*)(sm + SM_HIST));
+    else
+      hipLaunchKernelGGL(k_tri_okeys_part<4>, dim3(gp), dim3(256), 0, c->stream, kb, g.n, g.B, rank, keys,
+                         c->tri_loops.as<uint32_t>(), d_loops, hshift, nd, (uint32_t*)(sm + SM_HIST));
+    if (seg) *seg = useg;
     GS_HIP(hipGetLastError());
   } else if (g.n && split) {   // two passes over halves of the rank table (k_tri_okeys_lo / _hi)
     const unsigned glo = (unsigned)std::min<uint64_t>(steps, 16384 / U), ghi = (unsigned)std::min<uint64_t>(steps, 8192 / U);
@@ -1037,6 +1328,58 @@ gs_status tri_okeys(gs_ctx* c, const TriGeom& g, const uint32_t* rank, uint64_t*
   return GS_OK;
 }
 
+// the oriented keys sorted by u alone (LSD passes over bits B .. 2B; tri_okeys counted u's digit histograms),
+// then each run of equal u by v (k_tri_segsort, k_tri_segsort_long) -> *out (wide keys, in keysA or keysB)
+gs_status tri_seg_sort(gs_ctx* c, const TriGeom& g, const uint64_t* keys, Sorted* out) {
+  char* sm = c->small.as<char>();
+  const uint64_t n = g.n;
+  const uint32_t R = (uint32_t)n, tiles = (R + SORT_TILE - 1) / SORT_TILE;
+  const int passes = (int)(g.B + 7) / 8;
+  hipLaunchKernelGGL(k_digit_base, dim3(1), dim3(256), 0, c->stream, (const uint32_t*)(sm + SM_HIST), (uint32_t*)(sm + SM_BASE),
+                     passes);
+  GS_TRY(ensure(c, c->keysA, n * 8));
+  GS_TRY(ensure(c, c->keysB, n * 8));
+  GS_TRY(ensure(c, c->sort_status, (size_t)tiles * RADIX * 8, true));
+  uint64_t* ka = c->keysA.as<uint64_t>();
+  uint64_t* kb = c->keysB.as<uint64_t>();
+  const uint64_t* src = keys;
+  for (int p = 0; p < passes; ++p) {
+    GS_HIP(hipMemsetAsync((uint32_t*)(sm + SM_COUNTERS) + p, 0, 4, c->stream));
+    const uint32_t ep = next_epoch(c, 0);
+    hipLaunchKernelGGL((k_onesweep<uint64_t, uint8_t, false, SORT_BLOCK, SORT_ITEMS, BufSrc<uint64_t, uint8_t>>), dim3(tiles),
+                       dim3(SORT_BLOCK), 0, c->stream, BufSrc<uint64_t, uint8_t>{src, nullptr, 0}, ka, nullptr, R,
+                       g.B + 8u * (uint32_t)p, (const uint32_t*)(sm + SM_BASE) + p * RADIX, c->sort_status.as<uint64_t>(),
+                       (uint32_t*)(sm + SM_COUNTERS) + p, ep, (uint32_t*)(sm + SM_TIMEOUT));
+    src = ka;
+    std::swap(ka, kb);
+  }
+  uint64_t* sorted = const_cast<uint64_t*>(src);   // (passes >= 1: B > 16 here)
+  uint64_t* tmp = ka;                               // the other buffer
+  // runs longer than the LDS chunk: their starts (at most one per k_tri_segsort block) in tri_tiles
+  const uint64_t blocks = (n + SS_T - 1) / SS_T;
+  GS_TRY(ensure(c, c->tri_tiles, (size_t)(blocks + 1) * 8));
+  unsigned long long* d_nlong = (unsigned long long*)(sm + SM_TRI_MERGE);   // (tri_count zeroes it again)
+  GS_HIP(hipMemsetAsync(d_nlong, 0, 8, c->stream));
+  // GS_TRI_SEGSORT_CAP (tests): a smaller chunk, so more runs take the long kernel's HBM passes
+  static const int cap_env = getenv("GS_TRI_SEGSORT_CAP") ? atoi(getenv("GS_TRI_SEGSORT_CAP")) : SS_CAP;
+  const uint32_t cap = (uint32_t)std::max(1, std::min(cap_env, SS_CAP));
+  hipLaunchKernelGGL(k_tri_segsort, dim3((unsigned)blocks), dim3(SS_BLOCK), 0, c->stream, sorted, n, g.B, cap,
+                     c->tri_tiles.as<uint64_t>(), d_nlong);
+  hipLaunchKernelGGL(k_tri_segsort_long, dim3(512), dim3(SS_BLOCK), 0, c->stream, sorted, tmp, n, g.B, cap,
+                     (const uint64_t*)c->tri_tiles.as<uint64_t>(), (const unsigned long long*)d_nlong);
+  GS_HIP(hipGetLastError());
+  out->keys = sorted;
+  out->vals = nullptr;
+  out->wide = true;
+  out->bits = 2 * (int)g.B;
+  out->passes = passes;
+  out->done_passes = passes;
+  out->records = n;
+  out->key_xor = 0;
+  out->payload_bytes = 0;
+  return GS_OK;
+}
+
 // sort + unique of n oriented keys -> c->out_keys[0 .. M); `sentinel`: the keys may end in self-loop
 // sentinels (dropped)
 gs_status tri_unique(gs_ctx* c, const uint64_t* keys, uint64_t n, uint32_t B, bool hist_ready, bool sentinel,
@@ -1057,13 +1400,56 @@ gs_status tri_unique(gs_ctx* c, const uint64_t* keys, uint64_t n, uint32_t B, bo
   return GS_OK;
 }
 
+// the transposed sort of the whole window's M out-list entries by target, its first pass reading the out-lists
+// (TriTpaySrc) with the digit histograms k_tri_uo_write counted -> *t (u32 keys, u64 payload (p + 1, end))
+gs_status tri_tsort_fused(gs_ctx* c, uint32_t B, uint64_t M, const uint32_t* nbr, const uint32_t* rowid,
+                          const uint2* out_range, Sorted* t) {
+  char* sm = c->small.as<char>();
+  const uint32_t R = (uint32_t)M, tiles = (R + SORT_TILE - 1) / SORT_TILE;
+  const int passes = (int)(B + 7) / 8;
+  hipLaunchKernelGGL(k_digit_base, dim3(1), dim3(256), 0, c->stream, (const uint32_t*)(sm + SM_HIST), (uint32_t*)(sm + SM_BASE),
+                     passes);
+  GS_TRY(ensure(c, c->keysA, M * 4));
+  GS_TRY(ensure(c, c->keysB, M * 4));
+  GS_TRY(ensure(c, c->valsA, M * 8));
+  GS_TRY(ensure(c, c->valsB, M * 8));
+  GS_TRY(ensure(c, c->sort_status, (size_t)tiles * RADIX * 8, true));
+  uint32_t *ka = c->keysA.as<uint32_t>(), *kb = c->keysB.as<uint32_t>();
+  uint64_t *va = c->valsA.as<uint64_t>(), *vb = c->valsB.as<uint64_t>();
+  for (int p = 0; p < passes; ++p) {
+    GS_HIP(hipMemsetAsync((uint32_t*)(sm + SM_COUNTERS) + p, 0, 4, c->stream));
+    const uint32_t ep = next_epoch(c, 0);
+    const uint32_t* base = (const uint32_t*)(sm + SM_BASE) + p * RADIX;
+    uint32_t* ctr = (uint32_t*)(sm + SM_COUNTERS) + p;
+    if (p == 0)
+      hipLaunchKernelGGL((k_onesweep<uint32_t, uint64_t, true, SORT_BLOCK, SORT_ITEMS, TriTpaySrc>), dim3(tiles), dim3(SORT_BLOCK),
+                         0, c->stream, TriTpaySrc{nbr, rowid, out_range}, ka, va, R, 0u, base, c->sort_status.as<uint64_t>(),
+                         ctr, ep, (uint32_t*)(sm + SM_TIMEOUT));
+    else
+      hipLaunchKernelGGL((k_onesweep<uint32_t, uint64_t, true, SORT_BLOCK, SORT_ITEMS, BufSrc<uint32_t, uint64_t>>), dim3(tiles),
+                         dim3(SORT_BLOCK), 0, c->stream, BufSrc<uint32_t, uint64_t>{kb, vb, 0}, ka, va, R, 8u * (uint32_t)p, base,
+                         c->sort_status.as<uint64_t>(), ctr, ep, (uint32_t*)(sm + SM_TIMEOUT));
+    std::swap(ka, kb);   // the pass's output is now kb / vb
+    std::swap(va, vb);
+  }
+  GS_HIP(hipGetLastError());
+  *t = Sorted{};
+  t->keys = kb;
+  t->vals = vb;
+  t->bits = (int)B;
+  t->passes = t->done_passes = passes;
+  t->records = M;
+  t->payload_bytes = 8;
+  return GS_OK;
+}
+
 // The counting step over the out-lists (nbr, out_range; M edges) for part `part` of nparts: its
 // balanced u-range's edges sorted by target (in-lists with suffix ranges), then the LDS hash-set
 // kernels.  okeys: the sorted unique keys (row of every position), else rows come from out_range.
 gs_status tri_count(gs_ctx* c, uint32_t B, size_t V, uint64_t M, const uint32_t* nbr, const uint2* out_range,
                     const uint64_t* okeys, uint32_t part, uint32_t nparts, uint64_t* T, uint64_t* probes,
                     const uint32_t* loops = nullptr, const uint32_t* rank = nullptr, uint64_t* active = nullptr,
-                    const uint32_t* rowid_all = nullptr) {
+                    const uint32_t* rowid_all = nullptr, bool tpay_fused = false) {
   char* sm = c->small.as<char>();
   *T = 0;
   *probes = 0;
@@ -1094,10 +1480,14 @@ gs_status tri_count(gs_ctx* c, uint32_t B, size_t V, uint64_t M, const uint32_t*
     return GS_OK;
   }
   // 1. this part's edges by target: keys v, payload the suffix of N+(u) past v
+  const unsigned ge = (unsigned)std::min<uint64_t>((Ms + 255) / 256, 16384);
+  Sorted t;
+  if (tpay_fused && rowid_all && nparts == 1) {   // the first pass reads the out-lists (TriTpaySrc; histograms: uo_write)
+    GS_TRY(tri_tsort_fused(c, B, Ms, nbr, rowid_all, out_range, &t));
+  } else {
   GS_TRY(ensure(c, c->aux, Ms * 8));
   GS_TRY(ensure(c, c->tri_sfx, Ms * 8));
   GS_HIP(hipMemsetAsync(sm + SM_HIST, 0, 8 * 256 * 4, c->stream));
-  const unsigned ge = (unsigned)std::min<uint64_t>((Ms + 255) / 256, 16384);
   if (okeys) {
     hipLaunchKernelGGL(k_tri_tpay<false>, dim3(ge), dim3(256), 0, c->stream, okeys, nullptr, nbr, p0, p1, B, out_range,
                        c->aux.as<uint64_t>(), c->tri_sfx.as<uint2>(), (uint32_t*)(sm + SM_HIST));
@@ -1112,8 +1502,8 @@ gs_status tri_count(gs_ctx* c, uint32_t B, size_t V, uint64_t M, const uint32_t*
                        p0, p1, B, out_range, c->aux.as<uint64_t>(), c->tri_sfx.as<uint2>(), (uint32_t*)(sm + SM_HIST));
   }
   GS_HIP(hipGetLastError());
-  Sorted t;
   GS_TRY(sort_buffer(c, c->aux.as<uint64_t>(), c->tri_sfx.p, Ms, &t, (int)B, 8, true, sort_digit_bits((int)B)));
+  }
   if (t.wide || t.key_xor) return set_error(c, GS_EDEVICE, "window triangles: transposed keys wider than 32 bits");
   const uint2* sfx = (const uint2*)t.vals;   // the sort's payload buffer (valsA / valsB): read-only from here
   uint2* in_range = const_cast<uint2*>(out_range) + V;
@@ -1268,18 +1658,25 @@ gs_status triangles_impl(gs_ctx* c, const gs_edge_batch* b, uint32_t part, uint3
     GS_TRY(tri_degrees(c, gd, deg));
   }
   GS_TRY(tri_ranks(c, g, deg, rank));
+  static const int uo_env = getenv("GS_TRI_FUSED_UNIQUE") ? atoi(getenv("GS_TRI_FUSED_UNIQUE")) : 1;   // A/B
+  const bool fused = uo_env != 0 && 2 * g.B > 32;   // wide (u64) sorted keys
+  // the segmented sort (with the partitioned keys): u-only LSD passes + each out-list sorted in LDS.  Off by
+  // default: 3 passes fewer, but the LDS sort of the runs cost more than they did (s26 keys + sort 79.5 -> 98.3 ms,
+  // s24 16.8 -> 21.5 ms; profiles/r06/tri/ab_segsort/).  GS_TRI_SEGSORT=1 turns it on (A/B).
+  static const int seg_env = getenv("GS_TRI_SEGSORT") ? atoi(getenv("GS_TRI_SEGSORT")) : 0;
+  bool seg = false;
   GS_TRY(ensure(c, c->aux, g.n * 8));
-  GS_TRY(tri_okeys(c, g, rank, c->aux.as<uint64_t>()));
+  GS_TRY(tri_okeys(c, g, rank, c->aux.as<uint64_t>(), fused && seg_env != 0 && g.B > 16, &seg));
   // 2. sort + unique -> the simple oriented graph, sorted by (u, v); 3. out-lists
   Sorted s;
   uint64_t M = 0;
-  static const int uo_env = getenv("GS_TRI_FUSED_UNIQUE") ? atoi(getenv("GS_TRI_FUSED_UNIQUE")) : 1;   // A/B
-  const bool fused = uo_env != 0 && 2 * g.B > 32;   // wide (u64) sorted keys
   const uint32_t* rowid_all = nullptr;
+  bool tpay_fused = false;
   uint2* out_range = nullptr;
   uint64_t loops = 0, nv = 0;
   if (fused) {
-    GS_TRY(sort_buffer(c, c->aux.as<uint64_t>(), nullptr, g.n, &s, 2 * (int)g.B, 4, true, sort_digit_bits(2 * (int)g.B)));
+    if (seg) GS_TRY(tri_seg_sort(c, g, c->aux.as<uint64_t>(), &s));
+    else GS_TRY(sort_buffer(c, c->aux.as<uint64_t>(), nullptr, g.n, &s, 2 * (int)g.B, 4, true, sort_digit_bits(2 * (int)g.B)));
     if (!s.wide) return set_error(c, GS_EDEVICE, "window triangles: oriented keys narrower than expected");
     hipEventRecord(c->ev[1], c->stream);
     const uint64_t* sk = static_cast<const uint64_t*>(s.keys);
@@ -1303,9 +1700,14 @@ gs_status triangles_impl(gs_ctx* c, const gs_edge_batch* b, uint32_t part, uint3
     GS_TRY(ensure(c, c->out_keys, M * 4 + 4));
     out_range = reinterpret_cast<uint2*>(c->tri_range.p);
     GS_HIP(hipMemsetAsync(out_range, 0, g.V * 8, c->stream));
+    // (the whole window's count: the transposed sort's histograms on the way, tri_count's fused first pass)
+    static const int tfuse_env = getenv("GS_TRI_TPAY_FUSED") ? atoi(getenv("GS_TRI_TPAY_FUSED")) : 1;   // A/B
+    tpay_fused = tfuse_env != 0 && nparts == 1;
+    char* sm = c->small.as<char>();
+    if (tpay_fused) GS_HIP(hipMemsetAsync(sm + SM_HIST, 0, 8 * 256 * 4, c->stream));
     hipLaunchKernelGGL(k_tri_uo_write, dim3((unsigned)tiles), dim3(UO_BLOCK), 0, c->stream, sk, g.n, sent, g.B,
                        (const unsigned long long*)tpre, c->tri_nbr.as<uint32_t>(), c->out_keys.as<uint32_t>(),
-                       reinterpret_cast<uint32_t*>(out_range));
+                       reinterpret_cast<uint32_t*>(out_range), tpay_fused ? (uint32_t*)(sm + SM_HIST) : nullptr);
     GS_HIP(hipGetLastError());
     rowid_all = c->out_keys.as<uint32_t>();
     hipEventRecord(c->ev[2], c->stream);
@@ -1332,7 +1734,7 @@ gs_status triangles_impl(gs_ctx* c, const gs_edge_batch* b, uint32_t part, uint3
     uint64_t active = 0;
     GS_TRY(tri_count(c, g.B, g.V, M, c->tri_nbr.as<uint32_t>(), out_range, fused ? nullptr : c->out_keys.as<uint64_t>(),
                      part, nparts, &T, &probes, c->tri_loops.as<uint32_t>(), rank, sampled ? &active : nullptr,
-                     rowid_all));
+                     rowid_all, tpay_fused));
     tri_times(c, g, M, sampled ? active : nv, probes, s.passes);
   }
   if (loops && part == 0) {   // self-pair candidates (x, x, true) matched by a self-loop on x (:105)

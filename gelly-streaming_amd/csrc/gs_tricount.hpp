@@ -79,6 +79,9 @@ constexpr uint32_t TH_LONG = GS_TH_LONG;
 #ifndef GS_TH_LWAVES
 #define GS_TH_LWAVES 6   // k_tri_light waves per SIMD the registers are capped for (4 -> 6: s22 3.03 -> 2.38 ms)
 #endif
+#ifndef GS_TH_LPIPE
+#define GS_TH_LPIPE 0    // k_tri_light: the same (A/B)
+#endif
 #ifndef GS_TH_PIPE
 #define GS_TH_PIPE 0     // k_tri_heavy: gathers of the next step issued before this step's probes (A/B)
 #endif
@@ -162,6 +165,39 @@ __device__ __forceinline__ uint32_t th_probe(const uint4* hb, uint32_t bmask, co
   return cnt;
 }
 
+// cnt += probe(items of step k0) for k0 = a, a + step, .. < b, the items from gather(k0, x) -> valid count.
+// PIPE: software-pipelined -- step k0 + step's gathers (and the list search that places them) issue before
+// step k0's probes, so the search's LDS chain and the gathers' memory latency of consecutive steps overlap
+// (the loop bound is uniform over the caller's wave or block)
+template <int PIPE, class C, class Gather, class Probe>
+__device__ __forceinline__ void th_pipelined(uint32_t a, uint32_t b, uint32_t step, Gather&& gather, Probe&& probe,
+                                             C& cnt) {
+  if constexpr (PIPE) {
+    if (a >= b) return;
+    uint32_t xa[TH_ILP];
+    uint32_t nva = gather(a, xa);
+    for (uint32_t k0 = a; k0 < b; k0 += step) {
+      uint32_t xb[TH_ILP], nvb = 0;
+      if (k0 + step < b) {
+        nvb = gather(k0 + step, xb);
+      } else {
+#pragma unroll
+        for (int j = 0; j < TH_ILP; ++j) xb[j] = 0u;
+      }
+      cnt += probe(xa, nva);
+#pragma unroll
+      for (int j = 0; j < TH_ILP; ++j) xa[j] = xb[j];
+      nva = nvb;
+    }
+  } else {
+    for (uint32_t k0 = a; k0 < b; k0 += step) {
+      uint32_t x[TH_ILP];
+      const uint32_t nv = gather(k0, x);
+      cnt += probe(x, nv);
+    }
+  }
+}
+
 // one wave: |suffix of N+(u) ∩ N+(v)| summed over the in-entries c0 .. c1 (<= CAP) of v, N+(v)
 // behind probe(x, nv) (an LDS hash set, or a search in HBM)
 // lists of >= TH_LONG items ("long") are gathered lane-interleaved (64 consecutive items per load:
@@ -206,8 +242,7 @@ __device__ __forceinline__ uint32_t th_wave_probe(const uint32_t* __restrict__ o
     uint32_t q = 0;
     uint32_t qo = uni(po[CAP - 1]), qs = uni(ps[CAP - 1]);
     uint32_t qe = nl > 1 ? uni(po[CAP - 2]) : lrun, q1s = nl > 1 ? uni(ps[CAP - 2]) : 0u;
-    for (uint32_t k0 = 0; k0 < lrun; k0 += WAVE * TH_ILP) {
-      uint32_t x[TH_ILP];
+    auto gather_long = [&](uint32_t k0, uint32_t (&x)[TH_ILP]) -> uint32_t {
 #pragma unroll
       for (int j = 0; j < TH_ILP; ++j) {
         const uint32_t seg = k0 + (uint32_t)j * WAVE;   // wave-uniform
@@ -223,13 +258,13 @@ __device__ __forceinline__ uint32_t th_wave_probe(const uint32_t* __restrict__ o
       }
       // valid items of this lane: segments j with k0 + 64 j + lane < lrun (a prefix of j)
       const uint32_t rem = lrun - k0;
-      const uint32_t nv = rem > (uint32_t)lane ? min((uint32_t)TH_ILP, (rem - lane + WAVE - 1) / WAVE) : 0u;
-      cnt += probe(x, nv);
-    }
+      return rem > (uint32_t)lane ? min((uint32_t)TH_ILP, (rem - lane + WAVE - 1) / WAVE) : 0u;
+    };
+    th_pipelined<GS_TH_LPIPE>(0u, lrun, (uint32_t)(WAVE * TH_ILP), gather_long, probe, cnt);
   }
   uint32_t top = 1;
   while (2 * top < dn) top <<= 1;
-  for (uint32_t k0 = 0; k0 < run; k0 += WAVE * TH_ILP) {
+  auto gather_short = [&](uint32_t k0, uint32_t (&x)[TH_ILP]) -> uint32_t {
     const uint32_t kb = k0 + lane * TH_ILP;
     const uint32_t kk = min(kb, run - 1);
     // last kept u with po <= kk (po[dn] reads as run, above every item)
@@ -242,7 +277,6 @@ __device__ __forceinline__ uint32_t th_wave_probe(const uint32_t* __restrict__ o
     // consecutive items cross at most one list boundary per step (every kept list has >= 1 item)
     uint32_t o = po[lo], st = ps[lo], q = lo;
     uint32_t nx = q + 1 < dn ? po[min(q + 1, dn - 1)] : run;
-    uint32_t x[TH_ILP];
 #pragma unroll
     for (int j = 0; j < TH_ILP; ++j) {
       const uint32_t kj = min(kb + j, run - 1);
@@ -254,8 +288,9 @@ __device__ __forceinline__ uint32_t th_wave_probe(const uint32_t* __restrict__ o
       }
       x[j] = onbr[st + (kj - o)];
     }
-    cnt += probe(x, kb < run ? min((uint32_t)TH_ILP, run - kb) : 0u);
-  }
+    return kb < run ? min((uint32_t)TH_ILP, run - kb) : 0u;
+  };
+  th_pipelined<GS_TH_LPIPE>(0u, run, (uint32_t)(WAVE * TH_ILP), gather_short, probe, cnt);
   wave_lds_sync();   // po / ps are reused by the next chunk
   return cnt;
 }
@@ -692,33 +727,7 @@ __global__ __launch_bounds__(TH_HBLOCK) __attribute__((amdgpu_waves_per_eu(GS_TH
       return kb < srun ? min((uint32_t)TH_ILP, srun - kb) : 0u;
     };
     constexpr uint32_t SSTEP = TH_HBLOCK * TH_ILP, LSTEP = WAVE * TH_ILP;
-#if GS_TH_PIPE
-    // (round 6) software-pipelined: step s + 1's list search and gathers issue before step s's probes,
-    // so the LDS search chain and the gathers' HBM latency of consecutive steps overlap
-    if (srun) {
-      uint32_t xa[TH_ILP];
-      uint32_t nva = gather_short(0, xa);
-      for (uint32_t k0 = 0; k0 < srun; k0 += SSTEP) {
-        uint32_t xb[TH_ILP], nvb = 0;
-        if (k0 + SSTEP < srun) {   // block-uniform
-          nvb = gather_short(k0 + SSTEP, xb);
-        } else {
-#pragma unroll
-          for (int j = 0; j < TH_ILP; ++j) xb[j] = 0u;
-        }
-        cnt += probe(xa, nva);
-#pragma unroll
-        for (int j = 0; j < TH_ILP; ++j) xa[j] = xb[j];
-        nva = nvb;
-      }
-    }
-#else
-    for (uint32_t k0 = 0; k0 < srun; k0 += SSTEP) {
-      uint32_t x[TH_ILP];
-      const uint32_t nv = gather_short(k0, x);
-      cnt += probe(x, nv);
-    }
-#endif
+    th_pipelined<GS_TH_PIPE>(0u, srun, SSTEP, gather_short, probe, cnt);
     // long lists: wave w walks items [w, w + 1) * lrun / NW in 64-item segments (one load of 64
     // consecutive items); a segment spans at most two lists (every long list >= 64 items)
     if (lrun) {
@@ -753,31 +762,7 @@ __global__ __launch_bounds__(TH_HBLOCK) __attribute__((amdgpu_waves_per_eu(GS_TH
         const uint32_t rem = a1 - k0;
         return rem > (uint32_t)lane ? min((uint32_t)TH_ILP, (rem - lane + WAVE - 1) / WAVE) : 0u;
       };
-#if GS_TH_PIPE
-      if (a0 < a1) {
-        uint32_t xa[TH_ILP];
-        uint32_t nva = gather_long(a0, xa);
-        for (uint32_t k0 = a0; k0 < a1; k0 += LSTEP) {
-          uint32_t xb[TH_ILP], nvb = 0;
-          if (k0 + LSTEP < a1) {   // wave-uniform
-            nvb = gather_long(k0 + LSTEP, xb);
-          } else {
-#pragma unroll
-            for (int j = 0; j < TH_ILP; ++j) xb[j] = 0u;
-          }
-          cnt += probe(xa, nva);
-#pragma unroll
-          for (int j = 0; j < TH_ILP; ++j) xa[j] = xb[j];
-          nva = nvb;
-        }
-      }
-#else
-      for (uint32_t k0 = a0; k0 < a1; k0 += LSTEP) {
-        uint32_t x[TH_ILP];
-        const uint32_t nv = gather_long(k0, x);
-        cnt += probe(x, nv);
-      }
-#endif
+      th_pipelined<GS_TH_PIPE>(a0, a1, LSTEP, gather_long, probe, cnt);
     }
   }
 #pragma unroll

@@ -9,6 +9,11 @@ and GS_TRI_OKEYS_UNROLL force the others (read once per process, so every case r
 interpreter).  Every combination must give the forward algorithm's count (WindowTriangles.java:83-140
 restated in oracle/gs_oracle.c) on a self-loop-free R-MAT scale-18 window; the partitioned form also on
 a window that keeps its self-loops (the count less the self-pair term), where its pass 2 marks them.
+The partitioned form sorts the keys by u alone and each out-list in LDS (k_tri_segsort, round 6;
+GS_TRI_SEGSORT=0: the full LSD sort instead); GS_TRI_SEGSORT_CAP=64 shrinks the LDS chunk so that every
+out-list longer than 64 keys takes k_tri_segsort_long's stable passes over HBM.  The transposed sort's first
+pass reads the out-lists directly (TriTpaySrc, histograms from k_tri_uo_write); GS_TRI_TPAY_FUSED=0 restores
+k_tri_tpay's copy.
 """
 import subprocess
 import sys
@@ -24,7 +29,8 @@ ROOT = Path(__file__).resolve().parent.parent
 SCRIPT = textwrap.dedent("""
     import os
     import sys
-    os.environ.update(GS_TRI_OKEYS_SPLIT="{split}", GS_TRI_OKEYS_UNROLL="{unroll}", GS_TRI_OKEYS_PART="{part}")
+    os.environ.update(GS_TRI_OKEYS_SPLIT="{split}", GS_TRI_OKEYS_UNROLL="{unroll}", GS_TRI_OKEYS_PART="{part}",
+                      GS_TRI_SEGSORT="{seg}", GS_TRI_SEGSORT_CAP="{cap}", GS_TRI_TPAY_FUSED="{tfuse}")
     import numpy as np
     sys.path.insert(0, {root!r})
     import __graft_entry__ as ge
@@ -47,12 +53,15 @@ SCRIPT = textwrap.dedent("""
 """)
 
 
-@pytest.mark.parametrize("split,unroll,part", [(0, 1, 0), (0, 2, 0), (1, 1, 0), (1, 2, 0), (1, 4, 0), (0, 4, 1)])
-def test_okeys_variants_same_count(split, unroll, part):
+@pytest.mark.parametrize("split,unroll,part,seg,cap,tfuse", [
+    (0, 1, 0, 1, 4096, 1), (0, 2, 0, 1, 4096, 1), (1, 1, 0, 1, 4096, 1), (1, 2, 0, 1, 4096, 1), (1, 4, 0, 1, 4096, 1),
+    (0, 4, 1, 0, 4096, 1), (0, 4, 1, 1, 4096, 1), (0, 4, 1, 1, 64, 1), (0, 4, 1, 1, 4096, 0)])
+def test_okeys_variants_same_count(split, unroll, part, seg, cap, tfuse):
     # (the knobs are set inside the child, before the library reads them: the child inherits this
     # process's environment unchanged)
     r = subprocess.run([sys.executable, "-c", SCRIPT.format(root=str(ROOT), split=split, unroll=unroll,
-                                                                part=part, loops=part)],
+                                                                part=part, loops=part, seg=seg, cap=cap,
+                                                                tfuse=tfuse)],
                        capture_output=True, text=True, timeout=170)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "triangles" in r.stdout

@@ -9,6 +9,7 @@
 #   sq      TAG [bench args]    SQ counter passes (LDS conflicts, waits, instruction mix) over a short bench
 #   tri     TAG SCALE           triangles: bench line, kernel-trace stats, FETCH / TCC hit / SQ passes
 #   evidence TAG                every secondary bench line DESIGN.md quotes
+#   ttrace  TAG SCALE           triangles: the kernel trace alone
 #   envab   TAG "base K=V .." [args] A/B of environment knobs, alternated twice on one box
 #   ab      TAG "V1 V2.." [args] A/B of tuning builds (csrc/Makefile bvariant / variant -> variants/NAME; "base" =
 #                               the in-tree library): bench lines alternated twice on one box -> ab_NAME_REP.json
@@ -77,6 +78,10 @@ case $MODE in
     bench bench_e2e_direct --workload e2e --staging direct --no-cpu-baseline
     bench bench_e2e_pinned --workload e2e --staging pinned --no-cpu-baseline
     bench bench_e2e_buffered --workload e2e --staging buffered --no-cpu-baseline ;;
+  ttrace)
+    # kernel trace of one triangle window size only: TAG SCALE
+    S=${1:-24}; shift || true
+    trace trace_tri_s$S --workload triangles --scale $S --steps 3 --warmup 1 "$@" ;;
   envab)
     # A/B of library knobs read from the environment ("base" = none; e.g. "base GS_TRI_OKEYS_PART=0"),
     # alternated twice on one box -> ab_NAME_REP.json
