@@ -103,6 +103,7 @@ struct gs_ctx {
   gs::DevBuf tri_loops, tri_tiles, tri_sfx, tri_nbr, tri_heavy, tri_range, tri_queue, tri_hwork;
   gs::DevBuf tri_d[10];          // split-window triangles (gs_window_triangles_dist)
   gs::DevBuf cc[3];              // connected components (gs_components.hip)
+  uint32_t tri_guess_B = 0;      // triangles: the previous window's id width (its partition histograms ride the id scan)
   uint32_t tri_B = 0;            // split-window triangles: id geometry of the current window
   uint64_t tri_key_xor = 0;
   // split-window triangles, boundary adjacency (gs_tri_dist_plan / _need / _serve / _assemble): this

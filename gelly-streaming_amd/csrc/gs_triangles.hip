@@ -338,12 +338,16 @@ struct TriPartB {   // pass 2 records: a << 32 | b -> b << 32 | rank(a), gathere
   }
 };
 
-// 256-bin histograms of both endpoints' top bits (id >> sh): hist[0][..] sources, hist[1][..] targets
+// 256-bin histograms of both endpoints' top bits (id >> sh): hist[0][..] sources, hist[1][..] targets.
+// mask_out (tri_geometry's id scan, when it guesses the width from the previous window): also the OR of
+// (id ^ src[0]) over both columns, as k_keyinfo's mask
 __global__ __launch_bounds__(256) void k_tri_phist(const int64_t* __restrict__ src, const int64_t* __restrict__ dst,
                                                    uint64_t n, uint64_t key_xor, uint32_t sh,
-                                                   uint32_t* __restrict__ hist) {
+                                                   uint32_t* __restrict__ hist, unsigned long long* __restrict__ mask_out) {
   __shared__ uint32_t h[4][8][RADIX];
   const int tid = threadIdx.x, w = tid >> 6;
+  const uint64_t k0 = (uint64_t)src[0];
+  uint64_t m = 0;
   for (int i = tid; i < 4 * 8 * RADIX; i += 256) (&h[0][0][0])[i] = 0;
   __syncthreads();
   constexpr int U = 4;
@@ -360,7 +364,12 @@ __global__ __launch_bounds__(256) void k_tri_phist(const int64_t* __restrict__ s
     for (int u = 0; u < U; ++u) {
       const uint64_t k = ((a[u] >> sh) & 255u) | (((b[u] >> sh) & 255u) << 8);
       wave_hist_add(h[w], k, i0 + 256 * u + tid < n, 2);
+      if (mask_out) m |= (a[u] ^ key_xor ^ k0) | (b[u] ^ key_xor ^ k0);   // (clamped tail loads repeat an id)
     }
+  }
+  if (mask_out) {
+    m = wave_or(m);
+    if ((tid & 63) == 0 && m) atomicOr(mask_out, (unsigned long long)m);
   }
   __syncthreads();
   flush_hist<4>(h, 2, hist);
@@ -1147,6 +1156,7 @@ struct TriGeom {
   uint32_t B = 1;
   uint64_t key_xor = 0;
   size_t V = 2;
+  bool phist_ready = false;   // SM_HIST9 holds the top-8-bit histograms of src / dst at this B (tri_okeys)
 };
 
 void set_bits(TriGeom* g, uint32_t B) {
@@ -1160,7 +1170,18 @@ gs_status tri_geometry(gs_ctx* c, const int64_t* src, const int64_t* dst, uint64
   char* sm = c->small.as<char>();
   GS_HIP(hipMemsetAsync(sm, 0, SM_TIMEOUT, c->stream));
   GS_HIP(hipMemsetAsync(sm + SM_COUNTERS, 0, SM_BASE - SM_COUNTERS, c->stream));
-  GS_TRY(launch_keyinfo_all(c, src, dst, n, true));   // the id range (no histograms)
+  // the id range; windows after the first also count the partitioned keys' histograms (tri_okeys) on the way,
+  // at the width the previous window had (a miss -- another width -- only costs k_tri_phist's own scan later)
+  static const int guess_env = getenv("GS_TRI_PHIST_GUESS") ? atoi(getenv("GS_TRI_PHIST_GUESS")) : 1;   // A/B
+  const uint32_t guess = guess_env ? c->tri_guess_B : 0u;
+  if (n && guess >= 8 && guess <= TRI_MAX_BITS) {
+    GS_HIP(hipMemsetAsync(sm + SM_HIST9, 0, 2 * RADIX * 4, c->stream));
+    hipLaunchKernelGGL(k_tri_phist, dim3((unsigned)std::min<uint64_t>((n + 1023) / 1024, 4096)), dim3(256), 0, c->stream,
+                       src, dst, n, 0ull, guess - 8, (uint32_t*)(sm + SM_HIST9), (unsigned long long*)(sm + SM_MASK));
+    GS_HIP(hipGetLastError());
+  } else {
+    GS_TRY(launch_keyinfo_all(c, src, dst, n, true));   // the id range (no histograms)
+  }
   GS_HIP(hipMemcpyAsync(sm + SM_K0, src, 8, hipMemcpyDeviceToDevice, c->stream));
   GS_HIP(hipMemcpyAsync(c->host_small, sm, 16, hipMemcpyDeviceToHost, c->stream));
   GS_TRY(host_wait(c));
@@ -1170,7 +1191,10 @@ gs_status tri_geometry(gs_ctx* c, const int64_t* src, const int64_t* dst, uint64
   g->n = n;
   set_bits(g, mask ? 64 - __builtin_clzll(mask) : 1);
   g->key_xor = k0 & ~((1ull << g->B) - 1);
+  g->phist_ready = n && guess >= 8 && guess == g->B;   // (ids within B bits: (id ^ key_xor) >> (B - 8) = (id >> (B - 8)) & 255)
+  if (g->B <= TRI_MAX_BITS) c->tri_guess_B = g->B;
   if (g->B > TRI_MAX_BITS) {
+    g->phist_ready = false;
     GS_TRY(relabel_endpoints(c, src, dst, n, &g->src, &g->dst, &g->uniq, &g->nuniq));
     set_bits(g, g->nuniq > 1 ? 64 - __builtin_clzll(g->nuniq - 1) : 1);
     g->key_xor = 0;
@@ -1261,10 +1285,12 @@ gs_status tri_okeys(gs_ctx* c, const TriGeom& g, const uint32_t* rank, uint64_t*
     uint32_t* ph = (uint32_t*)(sm + SM_HIST9);   // [2][256] partition histograms, then (SM_BASE9) their bases
     uint32_t* pb = (uint32_t*)(sm + SM_BASE9);
     uint32_t* ctr = (uint32_t*)(sm + SM_COUNTERS) + 56;
-    GS_HIP(hipMemsetAsync(ph, 0, 2 * RADIX * 4, c->stream));
     GS_HIP(hipMemsetAsync(ctr, 0, 8, c->stream));
-    hipLaunchKernelGGL(k_tri_phist, dim3((unsigned)std::min<uint64_t>((g.n + 1023) / 1024, 4096)), dim3(256), 0, c->stream,
-                       g.src, g.dst, g.n, g.key_xor, sh, ph);
+    if (!g.phist_ready) {   // (else tri_geometry's id scan counted them, with the width the previous window had)
+      GS_HIP(hipMemsetAsync(ph, 0, 2 * RADIX * 4, c->stream));
+      hipLaunchKernelGGL(k_tri_phist, dim3((unsigned)std::min<uint64_t>((g.n + 1023) / 1024, 4096)), dim3(256), 0, c->stream,
+                         g.src, g.dst, g.n, g.key_xor, sh, ph, nullptr);
+    }
     hipLaunchKernelGGL(k_digit_base, dim3(1), dim3(256), 0, c->stream, (const uint32_t*)ph, pb, 2);
     GS_TRY(ensure(c, c->keysA, g.n * 8));
     GS_TRY(ensure(c, c->keysB, g.n * 8));

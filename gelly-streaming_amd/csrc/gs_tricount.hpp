@@ -79,6 +79,13 @@ constexpr uint32_t TH_LONG = GS_TH_LONG;
 #ifndef GS_TH_LWAVES
 #define GS_TH_LWAVES 6   // k_tri_light waves per SIMD the registers are capped for (4 -> 6: s22 3.03 -> 2.38 ms)
 #endif
+#ifndef GS_TH_WALK
+#define GS_TH_WALK 1     // k_tri_heavy: branch-free list walk (A/B, s26 heavy 144.5 -> 140.7 ms; 0 = a branch and an
+                         // LDS round trip per item, in series)
+#endif
+#ifndef GS_TH_LWALK
+#define GS_TH_LWALK 0    // k_tri_light: the same (A/B: light 39.6 -> 40.2 ms at s26, not kept)
+#endif
 #ifndef GS_TH_LPIPE
 #define GS_TH_LPIPE 0    // k_tri_light: the same (A/B)
 #endif
@@ -223,7 +230,7 @@ __device__ __forceinline__ uint32_t th_wave_probe(const uint32_t* __restrict__ o
     if (sh) {
       const uint32_t at = dn + mbcnt(ms);
       po[at] = run + inc - ds;
-      ps[at] = su;
+      ps[at] = GS_TH_LWALK ? su - (run + inc - ds) : su;   // (walk: item k of list at is onbr[k + ps[at]])
     }
     if (lg) {
       const uint32_t at = CAP - 1 - (nl + mbcnt(ml));
@@ -274,6 +281,22 @@ __device__ __forceinline__ uint32_t th_wave_probe(const uint32_t* __restrict__ o
       const uint32_t pv = t < dn ? po[min(t, dn - 1)] : run;
       lo = pv <= kk ? t : lo;
     }
+#if GS_TH_LWALK
+    // branch-free, as k_tri_heavy's walk: the next TH_ILP - 1 list starts as a mask of the items that start one
+    uint32_t m = 0;
+#pragma unroll
+    for (int i = 1; i < TH_ILP; ++i) {
+      const uint32_t t = lo + (uint32_t)i;
+      const uint32_t d = (t < dn ? po[min(t, dn - 1)] : run) - kb;
+      m |= d < (uint32_t)TH_ILP ? 1u << d : 0u;
+    }
+#pragma unroll
+    for (int j = 0; j < TH_ILP; ++j) {
+      const uint32_t ql = min(lo + (uint32_t)__builtin_popcount(m & ((2u << j) - 1u)), dn - 1);
+      x[j] = onbr[min(kb + j, run - 1) + ps[ql]];
+    }
+    return kb < run ? min((uint32_t)TH_ILP, run - kb) : 0u;
+#endif
     // consecutive items cross at most one list boundary per step (every kept list has >= 1 item)
     uint32_t o = po[lo], st = ps[lo], q = lo;
     uint32_t nx = q + 1 < dn ? po[min(q + 1, dn - 1)] : run;
@@ -690,7 +713,7 @@ __global__ __launch_bounds__(TH_HBLOCK) __attribute__((amdgpu_waves_per_eu(GS_TH
         lo_ += du[j];
       } else if (du[j]) {
         s_off[si] = so;
-        s_st[si] = su[j];
+        s_st[si] = GS_TH_WALK ? su[j] - so : su[j];   // (walk: item k of list si is onbr[k + s_st[si]])
         ++si;
         so += du[j];
       }
@@ -713,6 +736,24 @@ __global__ __launch_bounds__(TH_HBLOCK) __attribute__((amdgpu_waves_per_eu(GS_TH
         const uint32_t t = q + st;
         q = (t < ns && s_off[min(t, ns - 1)] <= kk) ? t : q;
       }
+#if GS_TH_WALK
+      // (round 6) branch-free: the next TH_ILP - 1 list starts in one batch of LDS reads, as a mask of the
+      // items that start a list (s_off[ns] = srun lies past every item); item j lies in list q + (starts at
+      // or before j), whose base is one more batch of reads -- instead of a branch and an LDS round trip
+      // per item, in series
+      uint32_t m = 0;
+#pragma unroll
+      for (int i = 1; i < TH_ILP; ++i) {
+        const uint32_t d = s_off[min(q + (uint32_t)i, ns)] - kb;
+        m |= d < (uint32_t)TH_ILP ? 1u << d : 0u;
+      }
+#pragma unroll
+      for (int j = 0; j < TH_ILP; ++j) {
+        const uint32_t ql = min(q + (uint32_t)__builtin_popcount(m & ((2u << j) - 1u)), ns - 1);
+        x[j] = onbr[min(kb + j, srun - 1) + s_st[ql]];
+      }
+      return kb < srun ? min((uint32_t)TH_ILP, srun - kb) : 0u;
+#endif
       uint32_t nx = s_off[q + 1], base = s_st[q] - s_off[q];   // item kj of list q: onbr[kj + base]
 #pragma unroll
       for (int j = 0; j < TH_ILP; ++j) {

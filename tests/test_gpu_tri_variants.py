@@ -65,3 +65,17 @@ def test_okeys_variants_same_count(split, unroll, part, seg, cap, tfuse):
                        capture_output=True, text=True, timeout=170)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "triangles" in r.stdout
+
+
+def test_partition_histograms_guessed_from_the_previous_window(pkg, oracle):
+    """Windows after the first count the partitioned keys' histograms in their id scan at the previous window's id
+    width (tri_geometry); a window of another width misses and counts them itself.  Widths 24, 24, 20, 24 (R-MAT
+    scale 24 ids and 20), each window against the forward algorithm."""
+    eng = pkg.Engine(0)
+    try:
+        for scale, seed in [(24, 0x5EED21), (24, 0x5EED22), (20, 0x5EED23), (24, 0x5EED24)]:
+            s, d = oracle.gen_rmat(scale, 1 << 21, seed, no_self_loops=True)
+            exact, wrapped, has = eng.triangles(s, d)
+            assert exact == oracle.triangles_fwd_mt(s, d), (scale, seed)
+    finally:
+        eng.close()
