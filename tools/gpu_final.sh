@@ -8,6 +8,8 @@
 #   bash tools/gpu_final.sh F TAG   round 6: C2 evidence (line, trace, PMC, write attribution, timeline, atomics microbench)
 #   bash tools/gpu_final.sh G TAG   round 6: secondary lines (Double, C3, CC, C1, apply, candidates, parse, e2e)
 #   bash tools/gpu_final.sh H TAG   round 6: triangles s20-s26 (s26 with the whole-window CPU baseline), C5 lines
+#   bash tools/gpu_final.sh I TAG   round 6, last build: C2 line + trace + PMC traffic; triangles s26 line (whole-window
+#                                   CPU baseline) + trace + FETCH / SQ passes; s20 / s22 / s24 lines
 set -e
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
@@ -57,6 +59,14 @@ case $MODE in
     timeout -k 10 300 python3 bench.py --workload cand_stream --cand-windows 4 > "$O/bench_cand_stream.json" 2> "$O/bench_cand_stream.err"
     timeout -k 10 300 python3 bench.py --workload cand_stream --cand-windows 4 --cand-ids u32 > "$O/bench_cand_stream_u32.json" 2> "$O/bench_cand_stream_u32.err"
     timeout -k 10 300 python3 bench.py --workload cand_stream --cand-windows 4 --cand-cadence-ms 1000 --no-cpu-baseline > "$O/bench_cand_stream_cadence.json" 2> "$O/bench_cand_stream_cadence.err" ;;
+  I)
+    bash tools/gpu.sh c2 "$TAG"
+    bash tools/gpu.sh tri "$TAG" 26
+    for x in "bench_tri_s20 --workload triangles --scale 20" "bench_tri_s22 --workload triangles --scale 22" \
+             "bench_tri_s24 --workload triangles --scale 24"; do
+      set -- $x; n=$1; shift
+      timeout -k 10 300 python3 bench.py "$@" > "$O/$n.json" 2> "$O/$n.err"; echo "$n done"
+    done ;;
   E)
     timeout -k 10 400 python3 bench.py --workload cand_stream --cand-ids u32 > "$O/bench_cand_stream_u32.json" 2> "$O/bench_cand_stream_u32.err"
     timeout -k 10 400 python3 bench.py --workload cand_stream > "$O/bench_cand_stream.json" 2> "$O/bench_cand_stream.err"
