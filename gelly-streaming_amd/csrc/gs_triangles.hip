@@ -1559,8 +1559,9 @@ gs_status tri_count(gs_ctx* c, uint32_t B, size_t V, uint64_t M, const uint32_t*
   const uint32_t nb_cap = (c->flags & GS_FLAG_TEST_TINY_TABLES) ? 1u : 0xFFFFFFFFu;
   uint32_t* d_nqueue = d_nheavy + 1;
   uint2* queue = c->tri_queue.as<uint2>();
-  hipLaunchKernelGGL(k_tri_lclass, dim3((unsigned)std::max<uint64_t>(1, std::min<uint64_t>((V + 255) / 256, 16384))),
-                     dim3(256), 0, c->stream, nbr, out_range, in_range, (uint32_t)V, 0u, 0xFFFFFFFFu, nb_cap, queue,
+  hipLaunchKernelGGL(k_tri_lclass, dim3((unsigned)std::max<uint64_t>(1, std::min<uint64_t>((V + TH_LCBLOCK - 1) / TH_LCBLOCK,
+                                                                                        4194304 / TH_LCBLOCK))),
+                     dim3(TH_LCBLOCK), 0, c->stream, nbr, out_range, in_range, (uint32_t)V, 0u, 0xFFFFFFFFu, nb_cap, queue,
                      d_nqueue, c->tri_heavy.as<uint2>(), d_nheavy, d_active, d_merge);
   if (d_active && loops && rank) {
     const uint32_t words = (uint32_t)((V + 31) / 32);

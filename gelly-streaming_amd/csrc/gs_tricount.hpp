@@ -402,20 +402,25 @@ __global__ __launch_bounds__(TH_BLOCK) __attribute__((amdgpu_waves_per_eu(GS_TH_
 // (the span of N+(v) within its table's bits; history: the split at 256 alone, s26 455 ms, at 512 alone
 // s24 72 -> 78 ms).  (Round 4: this pass ran inside k_tri_light, a wave per id in rank order, a dependent
 // load per id, 2^26 ids at s26, most without work: light count 41.9 -> 39.0 ms.)  Appends are
-// wave-aggregated (one atomic per wave and list).
-__global__ __launch_bounds__(256) void k_tri_lclass(const uint32_t* __restrict__ onbr, const uint2* __restrict__ out_range,
+// block-aggregated (one atomic per block and list: round 5 took one per wave).
+#ifndef GS_TH_LCBLOCK
+#define GS_TH_LCBLOCK 1024   // k_tri_lclass block: its appends are aggregated per block (one atomic per list per block)
+#endif
+constexpr int TH_LCBLOCK = GS_TH_LCBLOCK, TH_LCNW = TH_LCBLOCK / WAVE;
+__global__ __launch_bounds__(TH_LCBLOCK) void k_tri_lclass(const uint32_t* __restrict__ onbr, const uint2* __restrict__ out_range,
                                                     const uint2* __restrict__ in_range, uint32_t nv, uint32_t q0,
                                                     uint32_t q1, uint32_t nb_cap, uint2* __restrict__ queue,
                                                     uint32_t* __restrict__ n_queue, uint2* __restrict__ heavy,
                                                     uint32_t* __restrict__ n_heavy,
                                                     unsigned long long* __restrict__ n_active,
                                                     unsigned long long* __restrict__ merge) {
-  const int lane = threadIdx.x & 63;
+  __shared__ uint32_t s_h[TH_LCNW], s_l[TH_LCNW];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   uint32_t act = 0;   // this lane's ranks with an out- or in-entry (n_active, when asked for)
   // sum over the oriented edges u -> v counted here of d+(u) + d+(v) (the list entries a merge
   // intersection per edge would read; bench's roofline): per vertex x, d+(x) (d+(x) + d-(x))
   unsigned long long mg = 0;
-  for (uint32_t v0 = blockIdx.x * 256u; v0 < nv; v0 += gridDim.x * 256u) {   // wave-uniform trip count
+  for (uint32_t v0 = blockIdx.x * (uint32_t)TH_LCBLOCK; v0 < nv; v0 += gridDim.x * (uint32_t)TH_LCBLOCK) {   // block-uniform
     const uint32_t v = v0 + threadIdx.x;
     uint32_t nh = 0, nl = 0;
     if (v < nv) {
@@ -431,16 +436,30 @@ __global__ __launch_bounds__(256) void k_tri_lclass(const uint32_t* __restrict__
         else nl = (ri.y - ri.x + TH_LCH - 1) / TH_LCH;
       }
     }
+    // appends aggregated per block: the waves' totals, one atomic per list (R-MAT s26: 2^26 ids, most waves
+    // with an append -- one atomic per wave on the same two counters serialized)
     const uint32_t ih = wave_inclusive_sum(nh), il = wave_inclusive_sum(nl);
-    uint32_t bh = 0, bl = 0;
     if (lane == 63) {
-      if (ih) bh = atomicAdd(n_heavy, ih);
-      if (il) bl = atomicAdd(n_queue, il);
+      s_h[w] = ih;
+      s_l[w] = il;
     }
-    bh = __shfl(bh, 63, WAVE) + ih - nh;
-    bl = __shfl(bl, 63, WAVE) + il - nl;
+    __syncthreads();
+    if (threadIdx.x < 2) {   // thread 0: heavy, thread 1: light -- exclusive prefix over the waves + the block's base
+      uint32_t* t = threadIdx.x == 0 ? s_h : s_l;
+      uint32_t run = 0;
+      for (int x = 0; x < TH_LCNW; ++x) {
+        const uint32_t c = t[x];
+        t[x] = run;
+        run += c;
+      }
+      const uint32_t base = run ? atomicAdd(threadIdx.x == 0 ? n_heavy : n_queue, run) : 0u;
+      for (int x = 0; x < TH_LCNW; ++x) t[x] += base;
+    }
+    __syncthreads();
+    const uint32_t bh = s_h[w] + ih - nh, bl = s_l[w] + il - nl;
     for (uint32_t j = 0; j < nh; ++j) heavy[bh + j] = make_uint2(v, j);
     for (uint32_t j = 0; j < nl; ++j) queue[bl + j] = make_uint2(v, j);
+    __syncthreads();   // (the next round's totals)
   }
   if (n_active) {
 #pragma unroll
