@@ -682,47 +682,61 @@ __global__ __launch_bounds__(256) void k_tri_out(const uint64_t* __restrict__ ke
 // writes nbr[p] = v and rowid[p] = u at each head's unique index p and the row bounds out_range[u] --
 // instead of writing the unique keys (reduce-by-key) and reading them back to cut them into rows.
 constexpr uint32_t UO_BLOCK = 256, UO_ITEMS = 16, UO_TILE = UO_BLOCK * UO_ITEMS;
+// (hist, when not null: the transposed sort's digit histograms of the unique targets v (B bits), counted here
+// -- tiles grid-strided over the blocks, so each block flushes its tables once -- for TriTpaySrc's first pass)
 __global__ __launch_bounds__(UO_BLOCK) void k_tri_uo_count(const uint64_t* __restrict__ keys, uint64_t n, uint64_t sent,
-                                                           unsigned long long* __restrict__ tile_cnt) {
-  __shared__ uint32_t s_w[UO_BLOCK / WAVE];
-  const uint64_t t0 = (uint64_t)blockIdx.x * UO_TILE;
-  uint64_t k[UO_ITEMS], kp[UO_ITEMS];
-#pragma unroll
-  for (int j = 0; j < UO_ITEMS; ++j) {   // unconditional, clamped loads
-    const uint64_t i = min(t0 + (uint64_t)j * UO_BLOCK + threadIdx.x, n - 1);
-    k[j] = keys[i];
-    kp[j] = keys[i ? i - 1 : 0];
-  }
-  uint32_t c = 0;
-#pragma unroll
-  for (int j = 0; j < UO_ITEMS; ++j) {
-    const uint64_t i = t0 + (uint64_t)j * UO_BLOCK + threadIdx.x;
-    c += (i < n && k[j] != sent && (i == 0 || kp[j] != k[j])) ? 1u : 0u;
-  }
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, WAVE);
-  if ((threadIdx.x & 63) == 0) s_w[threadIdx.x >> 6] = c;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    uint32_t t = 0;
-#pragma unroll
-    for (int w = 0; w < (int)(UO_BLOCK / WAVE); ++w) t += s_w[w];
-    tile_cnt[blockIdx.x] = t;
-  }
-}
-
-// (hist, when not null: the transposed sort's digit histograms of the B-bit targets v, so its first pass can
-// read the out-lists directly -- TriTpaySrc -- instead of k_tri_tpay's copy)
-__global__ __launch_bounds__(UO_BLOCK) void k_tri_uo_write(const uint64_t* __restrict__ keys, uint64_t n, uint64_t sent,
-                                                           uint32_t B, const unsigned long long* __restrict__ tile_pre,
-                                                           uint32_t* __restrict__ nbr, uint32_t* __restrict__ rowid,
-                                                           uint32_t* __restrict__ out_range, uint32_t* __restrict__ hist) {
+                                                           uint64_t tiles, unsigned long long* __restrict__ tile_cnt,
+                                                           uint32_t B, uint32_t* __restrict__ hist) {
   constexpr int NW = UO_BLOCK / WAVE;
-  __shared__ uint32_t s_cnt[UO_ITEMS][NW];
+  __shared__ uint32_t s_w[NW];
   __shared__ uint32_t s_h[NW][8][RADIX];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int nd = (int)(B + 7) / 8;
+  const uint64_t vmask = (1ull << B) - 1;
   if (hist) {
     for (int i = threadIdx.x; i < NW * 8 * RADIX; i += UO_BLOCK) (&s_h[0][0][0])[i] = 0;
   }
+  for (uint64_t tile = blockIdx.x; tile < tiles; tile += gridDim.x) {   // block-uniform
+    const uint64_t t0 = tile * UO_TILE;
+    uint64_t k[UO_ITEMS], kp[UO_ITEMS];
+#pragma unroll
+    for (int j = 0; j < UO_ITEMS; ++j) {   // unconditional, clamped loads
+      const uint64_t i = min(t0 + (uint64_t)j * UO_BLOCK + threadIdx.x, n - 1);
+      k[j] = keys[i];
+      kp[j] = keys[i ? i - 1 : 0];
+    }
+    uint32_t c = 0;
+#pragma unroll
+    for (int j = 0; j < UO_ITEMS; ++j) {
+      const uint64_t i = t0 + (uint64_t)j * UO_BLOCK + threadIdx.x;
+      const bool head = i < n && k[j] != sent && (i == 0 || kp[j] != k[j]);
+      c += head ? 1u : 0u;
+      if (hist) wave_hist_add(s_h[w], k[j] & vmask, head, nd);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, WAVE);
+    if (lane == 0) s_w[w] = c;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      uint32_t t = 0;
+#pragma unroll
+      for (int x = 0; x < NW; ++x) t += s_w[x];
+      tile_cnt[tile] = t;
+    }
+    __syncthreads();   // (s_w of the next tile)
+  }
+  if (hist) {
+    __syncthreads();
+    flush_hist<NW>(s_h, nd, hist);
+  }
+}
+
+__global__ __launch_bounds__(UO_BLOCK) void k_tri_uo_write(const uint64_t* __restrict__ keys, uint64_t n, uint64_t sent,
+                                                           uint32_t B, const unsigned long long* __restrict__ tile_pre,
+                                                           uint32_t* __restrict__ nbr, uint32_t* __restrict__ rowid,
+                                                           uint32_t* __restrict__ out_range) {
+  constexpr int NW = UO_BLOCK / WAVE;
+  __shared__ uint32_t s_cnt[UO_ITEMS][NW];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const uint64_t t0 = (uint64_t)blockIdx.x * UO_TILE;
   const uint64_t mask = (1ull << B) - 1;
@@ -764,21 +778,10 @@ __global__ __launch_bounds__(UO_BLOCK) void k_tri_uo_write(const uint64_t* __res
     const uint64_t kn = i + 1 < n ? keys[i + 1] : sent;   // the row ends at key i: the next key is another row's
     if (kn == sent || (uint32_t)(kn >> B) != u) out_range[2 * u + 1] = (uint32_t)(excl + (head ? 1u : 0u));
   }
-  if (hist) {   // (block-uniform) every lane of every wave takes part: wave_hist_add ballots (plain adds on
-               // the low digits and ballots on the top one only: 0.45 ms slower at s26)
-    const int nd = (int)(B + 7) / 8;
-    const uint64_t mask = (1ull << B) - 1;
-#pragma unroll
-    for (int j = 0; j < UO_ITEMS; ++j) {
-      const bool head = (hb[j] >> lane) & 1ull;
-      wave_hist_add(s_h[w], k[j] & mask, head, nd);
-    }
-    __syncthreads();
-    flush_hist<NW>(s_h, nd, hist);
-  }
 }
 
-// the transposed sort's first pass reads the out-lists directly: record p -> key v = nbr[p], payload the
+// the transposed sort's first pass reads the out-lists directly (its histograms: k_tri_uo_count): record p ->
+// key v = nbr[p], payload the
 // suffix of N+(u) past v, [p + 1, end of N+(u)) (what k_tri_tpay would have written; u = rowid[p])
 struct TriTpaySrc {
   const uint32_t* nbr;
@@ -1427,7 +1430,7 @@ gs_status tri_unique(gs_ctx* c, const uint64_t* keys, uint64_t n, uint32_t B, bo
 }
 
 // the transposed sort of the whole window's M out-list entries by target, its first pass reading the out-lists
-// (TriTpaySrc) with the digit histograms k_tri_uo_write counted -> *t (u32 keys, u64 payload (p + 1, end))
+// (TriTpaySrc) with the digit histograms k_tri_uo_count counted -> *t (u32 keys, u64 payload (p + 1, end))
 gs_status tri_tsort_fused(gs_ctx* c, uint32_t B, uint64_t M, const uint32_t* nbr, const uint32_t* rowid,
                           const uint2* out_range, Sorted* t) {
   char* sm = c->small.as<char>();
@@ -1508,7 +1511,7 @@ gs_status tri_count(gs_ctx* c, uint32_t B, size_t V, uint64_t M, const uint32_t*
   // 1. this part's edges by target: keys v, payload the suffix of N+(u) past v
   const unsigned ge = (unsigned)std::min<uint64_t>((Ms + 255) / 256, 16384);
   Sorted t;
-  if (tpay_fused && rowid_all && nparts == 1) {   // the first pass reads the out-lists (TriTpaySrc; histograms: uo_write)
+  if (tpay_fused && rowid_all && nparts == 1) {   // the first pass reads the out-lists (TriTpaySrc; histograms: uo_count)
     GS_TRY(tri_tsort_fused(c, B, Ms, nbr, rowid_all, out_range, &t));
   } else {
   GS_TRY(ensure(c, c->aux, Ms * 8));
@@ -1712,7 +1715,13 @@ gs_status triangles_impl(gs_ctx* c, const gs_edge_batch* b, uint32_t part, uint3
     GS_TRY(ensure(c, c->tri_tiles, (size_t)(2 * tiles + 2) * 8));
     unsigned long long* tcnt = c->tri_tiles.as<unsigned long long>();
     unsigned long long* tpre = tcnt + tiles + 1;
-    hipLaunchKernelGGL(k_tri_uo_count, dim3((unsigned)tiles), dim3(UO_BLOCK), 0, c->stream, sk, g.n, sent, tcnt);
+    // (the whole window's count: the transposed sort's histograms on the way, for tri_count's fused first pass)
+    static const int tfuse_env = getenv("GS_TRI_TPAY_FUSED") ? atoi(getenv("GS_TRI_TPAY_FUSED")) : 1;   // A/B
+    tpay_fused = tfuse_env != 0 && nparts == 1;
+    char* sm = c->small.as<char>();
+    if (tpay_fused) GS_HIP(hipMemsetAsync(sm + SM_HIST, 0, 8 * 256 * 4, c->stream));
+    hipLaunchKernelGGL(k_tri_uo_count, dim3((unsigned)std::min<uint64_t>(tiles, 2048)), dim3(UO_BLOCK), 0, c->stream, sk, g.n,
+                       sent, tiles, tcnt, g.B, tpay_fused ? (uint32_t*)(sm + SM_HIST) : nullptr);
     GS_HIP(hipGetLastError());
     GS_TRY(xscan(c, (const uint64_t*)tcnt, tiles, (uint64_t*)tpre));
     GS_HIP(hipMemcpyAsync(c->host_small + 10, tpre + tiles, 8, hipMemcpyDeviceToHost, c->stream));
@@ -1727,14 +1736,9 @@ gs_status triangles_impl(gs_ctx* c, const gs_edge_batch* b, uint32_t part, uint3
     GS_TRY(ensure(c, c->out_keys, M * 4 + 4));
     out_range = reinterpret_cast<uint2*>(c->tri_range.p);
     GS_HIP(hipMemsetAsync(out_range, 0, g.V * 8, c->stream));
-    // (the whole window's count: the transposed sort's histograms on the way, tri_count's fused first pass)
-    static const int tfuse_env = getenv("GS_TRI_TPAY_FUSED") ? atoi(getenv("GS_TRI_TPAY_FUSED")) : 1;   // A/B
-    tpay_fused = tfuse_env != 0 && nparts == 1;
-    char* sm = c->small.as<char>();
-    if (tpay_fused) GS_HIP(hipMemsetAsync(sm + SM_HIST, 0, 8 * 256 * 4, c->stream));
     hipLaunchKernelGGL(k_tri_uo_write, dim3((unsigned)tiles), dim3(UO_BLOCK), 0, c->stream, sk, g.n, sent, g.B,
                        (const unsigned long long*)tpre, c->tri_nbr.as<uint32_t>(), c->out_keys.as<uint32_t>(),
-                       reinterpret_cast<uint32_t*>(out_range), tpay_fused ? (uint32_t*)(sm + SM_HIST) : nullptr);
+                       reinterpret_cast<uint32_t*>(out_range));
     GS_HIP(hipGetLastError());
     rowid_all = c->out_keys.as<uint32_t>();
     hipEventRecord(c->ev[2], c->stream);
