@@ -106,6 +106,32 @@ __global__ __launch_bounds__(256) void k_cc_hook_ids(const int64_t* __restrict__
   }
 }
 
+// (round 6) the same unions in two phases: the window's every (mask + 1)-th edge first (phase 0), then -- after a
+// full compression, so every vertex those edges linked points at its tree's root -- the rest (phase 1), which
+// skips an edge whose endpoints already share that root (on a skewed graph the sampled edges leave one giant
+// tree, so most of the rest end after two parent reads: no find chains, no CAS, no pointer-halving writes)
+__global__ __launch_bounds__(256) void k_cc_hook_ids_phase(const int64_t* __restrict__ a, const int64_t* __restrict__ b,
+                                                           uint64_t n, uint64_t key_xor, uint32_t* parent,
+                                                           uint8_t* __restrict__ mark, uint32_t mask, int phase) {
+  for (uint64_t e = (uint64_t)blockIdx.x * 256 + threadIdx.x; e < n; e += (uint64_t)gridDim.x * 256) {
+    if (((e & mask) == 0) != (phase == 0)) continue;
+    const uint32_t x = (uint32_t)((uint64_t)a[e] ^ key_xor), y = (uint32_t)((uint64_t)b[e] ^ key_xor);
+    if (x == y) {
+      mark[x] = 1;
+      continue;
+    }
+    if (phase == 1 && parent[x] == parent[y]) continue;   // one tree already (parents only move to smaller ids)
+    uint32_t p = cc_find(parent, x), q = cc_find(parent, y);
+    while (p != q) {
+      const uint32_t hi = p > q ? p : q, lo = p > q ? q : p;
+      const uint32_t old = atomicCAS(&parent[hi], hi, lo);
+      if (old == hi) break;
+      p = cc_find(parent, old);
+      q = lo;
+    }
+  }
+}
+
 // full compression; a linked vertex is present and so is its root (every root of a linked tree is an
 // endpoint: links only ever join the roots of trees that hold endpoints)
 __global__ __launch_bounds__(256) void k_cc_compress(uint32_t* parent, uint32_t V, uint8_t* __restrict__ mark) {
@@ -195,7 +221,18 @@ gs_status gs_window_components(gs_ctx* c, const gs_edge_batch* b, const gs_parti
       hipLaunchKernelGGL(k_cc_init, dim3(gv), dim3(256), 0, c->stream, parent, V);
       GS_HIP(hipMemsetAsync(mark, 0, V, c->stream));
       hipEventRecord(c->ev[1], c->stream);
-      hipLaunchKernelGGL(k_cc_hook_ids, dim3(gN), dim3(256), 0, c->stream, A, Bc, N, key_xor, parent, mark);
+      // GS_CC_SAMPLE = k (a power of two): the two-phase unions over every k-th edge first (0 or 1: one pass
+      // over every edge)
+      static const int sample_env = getenv("GS_CC_SAMPLE") ? atoi(getenv("GS_CC_SAMPLE")) : 8;
+      if (sample_env > 1 && (sample_env & (sample_env - 1)) == 0 && N >= 65536) {
+        hipLaunchKernelGGL(k_cc_hook_ids_phase, dim3(gN), dim3(256), 0, c->stream, A, Bc, N, key_xor, parent, mark,
+                           (uint32_t)sample_env - 1, 0);
+        hipLaunchKernelGGL(k_cc_compress, dim3(gv), dim3(256), 0, c->stream, parent, V, mark);
+        hipLaunchKernelGGL(k_cc_hook_ids_phase, dim3(gN), dim3(256), 0, c->stream, A, Bc, N, key_xor, parent, mark,
+                           (uint32_t)sample_env - 1, 1);
+      } else {
+        hipLaunchKernelGGL(k_cc_hook_ids, dim3(gN), dim3(256), 0, c->stream, A, Bc, N, key_xor, parent, mark);
+      }
       hipLaunchKernelGGL(k_cc_compress, dim3(gv), dim3(256), 0, c->stream, parent, V, mark);
       GS_HIP(hipGetLastError());
       hipEventRecord(c->ev[2], c->stream);
