@@ -112,7 +112,8 @@ __global__ __launch_bounds__(256) void k_cc_hook_ids(const int64_t* __restrict__
 // tree, so most of the rest end after two parent reads: no find chains, no CAS, no pointer-halving writes)
 __global__ __launch_bounds__(256) void k_cc_hook_ids_phase(const int64_t* __restrict__ a, const int64_t* __restrict__ b,
                                                            uint64_t n, uint64_t key_xor, uint32_t* parent,
-                                                           uint8_t* __restrict__ mark, uint32_t mask, int phase) {
+                                                           uint8_t* __restrict__ mark, uint32_t mask, int phase,
+                                                           const uint32_t* __restrict__ gbits) {
   for (uint64_t e = (uint64_t)blockIdx.x * 256 + threadIdx.x; e < n; e += (uint64_t)gridDim.x * 256) {
     if (((e & mask) == 0) != (phase == 0)) continue;
     const uint32_t x = (uint32_t)((uint64_t)a[e] ^ key_xor), y = (uint32_t)((uint64_t)b[e] ^ key_xor);
@@ -120,7 +121,12 @@ __global__ __launch_bounds__(256) void k_cc_hook_ids_phase(const int64_t* __rest
       mark[x] = 1;
       continue;
     }
-    if (phase == 1 && parent[x] == parent[y]) continue;   // one tree already (parents only move to smaller ids)
+    if (phase == 1) {
+      // both in the giant tree (an L2-resident bit per vertex), or one tree already (parents only move to
+      // smaller ids): nothing to join
+      if (gbits && ((gbits[x >> 5] >> (x & 31)) & (gbits[y >> 5] >> (y & 31)) & 1u)) continue;
+      if (parent[x] == parent[y]) continue;
+    }
     uint32_t p = cc_find(parent, x), q = cc_find(parent, y);
     while (p != q) {
       const uint32_t hi = p > q ? p : q, lo = p > q ? q : p;
@@ -129,6 +135,35 @@ __global__ __launch_bounds__(256) void k_cc_hook_ids_phase(const int64_t* __rest
       p = cc_find(parent, old);
       q = lo;
     }
+  }
+}
+
+// the giant tree after phase 0: the most frequent root among the parents of 1024 sampled edges' sources
+// (one block; any root would be correct -- the bits only let edges skip that are joined already)
+__global__ __launch_bounds__(1024) void k_cc_giant(const int64_t* __restrict__ a, uint64_t n, uint64_t key_xor,
+                                                   const uint32_t* __restrict__ parent, uint32_t* __restrict__ giant) {
+  __shared__ uint32_t s_r[1024];
+  __shared__ unsigned long long s_best;
+  const uint32_t t = threadIdx.x;
+  const uint64_t e = (uint64_t)t * (n / 1024);
+  s_r[t] = parent[(uint32_t)((uint64_t)a[e] ^ key_xor)];
+  if (t == 0) s_best = 0;
+  __syncthreads();
+  const uint32_t mine = s_r[t];
+  uint32_t c = 0;
+  for (int i = 0; i < 1024; ++i) c += s_r[i] == mine ? 1u : 0u;
+  atomicMax(&s_best, ((unsigned long long)c << 32) | mine);
+  __syncthreads();
+  if (t == 0) *giant = (uint32_t)s_best;
+}
+// bit v of gbits: parent[v] is the giant root (after the compression, parent[v] is v's root)
+__global__ __launch_bounds__(256) void k_cc_gbits(const uint32_t* __restrict__ parent, uint32_t V,
+                                                  const uint32_t* __restrict__ giant, uint32_t* __restrict__ gbits) {
+  const uint32_t g = *giant;
+  for (uint32_t w = blockIdx.x * 256u + threadIdx.x; w < (V + 31) / 32; w += gridDim.x * 256u) {
+    uint32_t bits = 0;
+    for (uint32_t k = 0; k < 32 && w * 32 + k < V; ++k) bits |= (parent[w * 32 + k] == g ? 1u : 0u) << k;
+    gbits[w] = bits;
   }
 }
 
@@ -177,34 +212,42 @@ gs_status gs_window_components(gs_ctx* c, const gs_edge_batch* b, const gs_parti
   const uint64_t n = b->n, m = prev ? prev->n : 0, N = n + m;
   *out->n_out = 0;
   if (N == 0) return GS_OK;
-  // 1. the window's edges + the state's (vertex, label) rows, on the device
+  // 1. the state's (vertex, label) rows on the device (cc[0] / cc[1] rows [0, m)); the window's columns are read
+  //    where they are (round 6: no copy of them into one edge list -- 16 B read + 16 B written per edge --
+  //    unless the ids take the relabel path, which appends them at rows [m, N))
   GS_TRY(ensure(c, c->cc[0], N * 8));
   GS_TRY(ensure(c, c->cc[1], N * 8));
   int64_t* A = c->cc[0].as<int64_t>();
   int64_t* Bc = c->cc[1].as<int64_t>();
+  const int64_t *src = nullptr, *dst = nullptr;
   if (n) {
-    const int64_t *src, *dst;
     const void* val;
     GS_TRY(stage_batch(c, b, &src, &dst, &val, false));
-    hipLaunchKernelGGL(k_cc_concat, dim3((unsigned)std::min<uint64_t>((n + 255) / 256, 8192)), dim3(256), 0, c->stream,
-                       src, dst, n, A, Bc);
   }
   if (m) {
     const hipMemcpyKind k = prev->mem == GS_MEM_DEVICE ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
-    GS_HIP(hipMemcpyAsync(A + n, prev->keys, m * 8, k, c->stream));
-    GS_HIP(hipMemcpyAsync(Bc + n, prev->vals, m * 8, k, c->stream));
+    GS_HIP(hipMemcpyAsync(A, prev->keys, m * 8, k, c->stream));
+    GS_HIP(hipMemcpyAsync(Bc, prev->vals, m * 8, k, c->stream));
   }
   GS_HIP(hipGetLastError());
+  // the two segments of pairs: the window's edges, the state's rows
+  struct Seg {
+    const int64_t *a, *b;
+    uint64_t n;
+  };
+  const Seg seg[2] = {{src, dst, n}, {A, Bc, m}};
+  const int64_t* k0p = n ? src : A;
   // 2a. ids spanning <= CC_DIRECT_BITS bits: union-find over the ids themselves (no relabel sort)
   {
     char* sm = c->small.as<char>();
     unsigned long long* dmask = (unsigned long long*)(sm + SM_TABLE);
     GS_HIP(hipMemsetAsync(dmask, 0, 8, c->stream));
-    const unsigned gN = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((N + 255) / 256, 8192));
-    hipLaunchKernelGGL(k_cc_mask, dim3(gN), dim3(256), 0, c->stream, A, Bc, N, A, dmask);
+    auto grid = [](uint64_t x) { return (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((x + 255) / 256, 8192)); };
+    for (const Seg& g : seg)
+      if (g.n) hipLaunchKernelGGL(k_cc_mask, dim3(grid(g.n)), dim3(256), 0, c->stream, g.a, g.b, g.n, k0p, dmask);
     GS_HIP(hipGetLastError());
     GS_HIP(hipMemcpyAsync(c->host_small + 12, dmask, 8, hipMemcpyDeviceToHost, c->stream));
-    GS_HIP(hipMemcpyAsync(c->host_small + 13, A, 8, hipMemcpyDeviceToHost, c->stream));
+    GS_HIP(hipMemcpyAsync(c->host_small + 13, k0p, 8, hipMemcpyDeviceToHost, c->stream));
     GS_TRY(host_wait(c));
     const uint64_t mask = c->host_small[12], k0 = c->host_small[13];
     const uint32_t B = mask ? 64 - __builtin_clzll(mask) : 1;
@@ -225,13 +268,32 @@ gs_status gs_window_components(gs_ctx* c, const gs_edge_batch* b, const gs_parti
       // over every edge)
       static const int sample_env = getenv("GS_CC_SAMPLE") ? atoi(getenv("GS_CC_SAMPLE")) : 8;
       if (sample_env > 1 && (sample_env & (sample_env - 1)) == 0 && N >= 65536) {
-        hipLaunchKernelGGL(k_cc_hook_ids_phase, dim3(gN), dim3(256), 0, c->stream, A, Bc, N, key_xor, parent, mark,
-                           (uint32_t)sample_env - 1, 0);
+        for (const Seg& g : seg)
+          if (g.n)
+            hipLaunchKernelGGL(k_cc_hook_ids_phase, dim3(grid(g.n)), dim3(256), 0, c->stream, g.a, g.b, g.n, key_xor, parent,
+                               mark, (uint32_t)sample_env - 1, 0, (const uint32_t*)nullptr);
         hipLaunchKernelGGL(k_cc_compress, dim3(gv), dim3(256), 0, c->stream, parent, V, mark);
-        hipLaunchKernelGGL(k_cc_hook_ids_phase, dim3(gN), dim3(256), 0, c->stream, A, Bc, N, key_xor, parent, mark,
-                           (uint32_t)sample_env - 1, 1);
+        // the giant tree's vertices as a bit table (V / 8 bytes: L2-resident) for phase 1's skip test (the
+        // larger segment's sources are sampled)
+        static const int giant_env = getenv("GS_CC_GIANT") ? atoi(getenv("GS_CC_GIANT")) : 1;   // A/B
+        uint32_t* gbits = nullptr;
+        const Seg& big = n >= m ? seg[0] : seg[1];
+        if (giant_env && big.n >= 1024) {
+          GS_TRY(ensure(c, c->cc[3], (size_t)(V + 31) / 32 * 4 + 64));
+          gbits = c->cc[3].as<uint32_t>();
+          uint32_t* giant = gbits + (V + 31) / 32;
+          hipLaunchKernelGGL(k_cc_giant, dim3(1), dim3(1024), 0, c->stream, big.a, big.n, key_xor, parent, giant);
+          hipLaunchKernelGGL(k_cc_gbits, dim3((unsigned)std::min<uint64_t>(((V + 31) / 32 + 255) / 256, 16384)), dim3(256),
+                             0, c->stream, parent, V, giant, gbits);
+        }
+        for (const Seg& g : seg)
+          if (g.n)
+            hipLaunchKernelGGL(k_cc_hook_ids_phase, dim3(grid(g.n)), dim3(256), 0, c->stream, g.a, g.b, g.n, key_xor, parent,
+                               mark, (uint32_t)sample_env - 1, 1, (const uint32_t*)gbits);
       } else {
-        hipLaunchKernelGGL(k_cc_hook_ids, dim3(gN), dim3(256), 0, c->stream, A, Bc, N, key_xor, parent, mark);
+        for (const Seg& g : seg)
+          if (g.n)
+            hipLaunchKernelGGL(k_cc_hook_ids, dim3(grid(g.n)), dim3(256), 0, c->stream, g.a, g.b, g.n, key_xor, parent, mark);
       }
       hipLaunchKernelGGL(k_cc_compress, dim3(gv), dim3(256), 0, c->stream, parent, V, mark);
       GS_HIP(hipGetLastError());
@@ -276,7 +338,10 @@ gs_status gs_window_components(gs_ctx* c, const gs_edge_batch* b, const gs_parti
       return GS_OK;
     }
   }
-  // 2b. compact IDs
+  // 2b. compact IDs: the window's edges appended to the state's rows (one edge list for the relabel sort)
+  if (n)
+    hipLaunchKernelGGL(k_cc_concat, dim3((unsigned)std::min<uint64_t>((n + 255) / 256, 8192)), dim3(256), 0, c->stream,
+                       src, dst, n, A + m, Bc + m);
   const int64_t *ca, *cb, *uniq;
   uint64_t U = 0;
   GS_TRY(relabel_endpoints(c, A, Bc, N, &ca, &cb, &uniq, &U));

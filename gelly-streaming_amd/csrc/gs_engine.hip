@@ -459,7 +459,7 @@ void gs_destroy(gs_ctx* c) {
   for (DevBuf* b : {&c->part_k, &c->part_a, &c->comp_k, &c->comp_a,
                     &c->in_src, &c->in_dst, &c->in_val, &c->keysA, &c->keysB, &c->valsA, &c->valsB, &c->sort_status,
                     &c->rbk_word, &c->rbk_agg, &c->rbk_inc, &c->small, &c->out_keys, &c->out_a, &c->out_b, &c->aux,
-                    &c->bk_meta, &c->bk_items, &c->bk_slabs, &c->dp_cnt, &c->dp_csum, &c->dp_off, &c->tri_loops, &c->tri_tiles, &c->tri_sfx, &c->tri_nbr, &c->tri_heavy, &c->tri_range, &c->tri_queue, &c->tri_hwork, &c->tri_d[0], &c->tri_d[1], &c->tri_d[2], &c->tri_d[3], &c->tri_d[4], &c->tri_d[5], &c->tri_d[6], &c->tri_d[7], &c->tri_d[8], &c->tri_d[9], &c->cc[0], &c->cc[1], &c->cc[2],
+                    &c->bk_meta, &c->bk_items, &c->bk_slabs, &c->dp_cnt, &c->dp_csum, &c->dp_off, &c->tri_loops, &c->tri_tiles, &c->tri_sfx, &c->tri_nbr, &c->tri_heavy, &c->tri_range, &c->tri_queue, &c->tri_hwork, &c->tri_d[0], &c->tri_d[1], &c->tri_d[2], &c->tri_d[3], &c->tri_d[4], &c->tri_d[5], &c->tri_d[6], &c->tri_d[7], &c->tri_d[8], &c->tri_d[9], &c->cc[0], &c->cc[1], &c->cc[2], &c->cc[3],
                     &c->pr_a, &c->pr_b, &c->pr_f, &c->pr_key, &c->pr_val, &c->pr_gk, &c->pr_gv, &c->pr_small,
                     &c->tx_text, &c->tx_cnt, &c->tx_starts, &c->zipf_cdf,
                     &c->dist_k, &c->dist_v, &c->dist_v2, &c->dist_k2, &c->dist_v3, &c->dist_v4, &c->dist_cnt,

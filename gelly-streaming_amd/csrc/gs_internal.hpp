@@ -102,7 +102,7 @@ struct gs_ctx {
   // triangles
   gs::DevBuf tri_loops, tri_tiles, tri_sfx, tri_nbr, tri_heavy, tri_range, tri_queue, tri_hwork;
   gs::DevBuf tri_d[10];          // split-window triangles (gs_window_triangles_dist)
-  gs::DevBuf cc[3];              // connected components (gs_components.hip)
+  gs::DevBuf cc[4];              // connected components (gs_components.hip; [3]: the giant tree's bits)
   uint32_t tri_guess_B = 0;      // triangles: the previous window's id width (its partition histograms ride the id scan)
   uint32_t tri_B = 0;            // split-window triangles: id geometry of the current window
   uint64_t tri_key_xor = 0;
