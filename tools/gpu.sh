@@ -10,6 +10,7 @@
 #   tri     TAG SCALE           triangles: bench line, kernel-trace stats, FETCH / TCC hit / SQ passes
 #   evidence TAG                every secondary bench line DESIGN.md quotes
 #   ttrace  TAG SCALE           triangles: the kernel trace alone
+#   ktrace  TAG NAME [args]     the kernel trace of any bench line
 #   envab   TAG "base K=V .." [args] A/B of environment knobs, alternated twice on one box
 #   ab      TAG "V1 V2.." [args] A/B of tuning builds (csrc/Makefile bvariant / variant -> variants/NAME; "base" =
 #                               the in-tree library): bench lines alternated twice on one box -> ab_NAME_REP.json
@@ -78,6 +79,10 @@ case $MODE in
     bench bench_e2e_direct --workload e2e --staging direct --no-cpu-baseline
     bench bench_e2e_pinned --workload e2e --staging pinned --no-cpu-baseline
     bench bench_e2e_buffered --workload e2e --staging buffered --no-cpu-baseline ;;
+  ktrace)
+    # kernel trace of any bench line: TAG NAME [bench args]
+    N=${1:-run}; shift || true
+    trace "trace_$N" "$@" ;;
   ttrace)
     # kernel trace of one triangle window size only: TAG SCALE
     S=${1:-24}; shift || true
