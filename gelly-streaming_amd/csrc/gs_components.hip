@@ -52,6 +52,36 @@ __global__ __launch_bounds__(256) void k_cc_hook(const uint32_t* __restrict__ at
   }
 }
 
+// the two-phase unions of k_cc_hook_ids_phase over compact endpoint pairs (the relabel path)
+__global__ __launch_bounds__(256) void k_cc_hook_phase(const uint32_t* __restrict__ at, uint64_t ne, uint32_t* parent,
+                                                       uint32_t mask, int phase, const uint32_t* __restrict__ gbits) {
+  for (uint64_t e = (uint64_t)blockIdx.x * 256 + threadIdx.x; e < ne; e += (uint64_t)gridDim.x * 256) {
+    if (((e & mask) == 0) != (phase == 0)) continue;
+    const uint32_t x = at[2 * e], y = at[2 * e + 1];
+    if (phase == 1) {
+      if (gbits && ((gbits[x >> 5] >> (x & 31)) & (gbits[y >> 5] >> (y & 31)) & 1u)) continue;
+      if (parent[x] == parent[y]) continue;
+    }
+    uint32_t a = cc_find(parent, x), b = cc_find(parent, y);
+    while (a != b) {
+      const uint32_t hi = a > b ? a : b, lo = a > b ? b : a;
+      const uint32_t old = atomicCAS(&parent[hi], hi, lo);
+      if (old == hi) break;
+      a = cc_find(parent, old);
+      b = lo;
+    }
+  }
+}
+// full compression (every compact id is present: no marks)
+__global__ __launch_bounds__(256) void k_cc_compress_all(uint32_t* parent, uint32_t U) {
+  for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < U; i += gridDim.x * 256u) {
+    uint32_t r = parent[i];
+    if (r == i) continue;
+    while (parent[r] != r) r = parent[r];
+    parent[i] = r;
+  }
+}
+
 // roots (= smallest compact ID of the component) -> labels in original IDs
 __global__ __launch_bounds__(256) void k_cc_emit(uint32_t* parent, const int64_t* __restrict__ uniq, uint32_t n,
                                                  int64_t* __restrict__ keys, int64_t* __restrict__ labels) {
@@ -140,13 +170,15 @@ __global__ __launch_bounds__(256) void k_cc_hook_ids_phase(const int64_t* __rest
 
 // the giant tree after phase 0: the most frequent root among the parents of 1024 sampled edges' sources
 // (one block; any root would be correct -- the bits only let edges skip that are joined already)
-__global__ __launch_bounds__(1024) void k_cc_giant(const int64_t* __restrict__ a, uint64_t n, uint64_t key_xor,
-                                                   const uint32_t* __restrict__ parent, uint32_t* __restrict__ giant) {
+// (compact ids: at != nullptr, the sources at[2e] instead of a[e] ^ key_xor)
+__global__ __launch_bounds__(1024) void k_cc_giant(const int64_t* __restrict__ a, const uint32_t* __restrict__ at,
+                                                   uint64_t n, uint64_t key_xor, const uint32_t* __restrict__ parent,
+                                                   uint32_t* __restrict__ giant) {
   __shared__ uint32_t s_r[1024];
   __shared__ unsigned long long s_best;
   const uint32_t t = threadIdx.x;
   const uint64_t e = (uint64_t)t * (n / 1024);
-  s_r[t] = parent[(uint32_t)((uint64_t)a[e] ^ key_xor)];
+  s_r[t] = parent[at ? at[2 * e] : (uint32_t)((uint64_t)a[e] ^ key_xor)];
   if (t == 0) s_best = 0;
   __syncthreads();
   const uint32_t mine = s_r[t];
@@ -282,7 +314,8 @@ gs_status gs_window_components(gs_ctx* c, const gs_edge_batch* b, const gs_parti
           GS_TRY(ensure(c, c->cc[3], (size_t)(V + 31) / 32 * 4 + 64));
           gbits = c->cc[3].as<uint32_t>();
           uint32_t* giant = gbits + (V + 31) / 32;
-          hipLaunchKernelGGL(k_cc_giant, dim3(1), dim3(1024), 0, c->stream, big.a, big.n, key_xor, parent, giant);
+          hipLaunchKernelGGL(k_cc_giant, dim3(1), dim3(1024), 0, c->stream, big.a, (const uint32_t*)nullptr, big.n, key_xor,
+                             parent, giant);
           hipLaunchKernelGGL(k_cc_gbits, dim3((unsigned)std::min<uint64_t>(((V + 31) / 32 + 255) / 256, 16384)), dim3(256),
                              0, c->stream, parent, V, giant, gbits);
         }
@@ -352,7 +385,30 @@ gs_status gs_window_components(gs_ctx* c, const gs_edge_batch* b, const gs_parti
   const unsigned gu = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((U + 255) / 256, 16384));
   const unsigned ge = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((N + 255) / 256, 16384));
   hipLaunchKernelGGL(k_cc_init, dim3(gu), dim3(256), 0, c->stream, parent, (uint32_t)U);
-  hipLaunchKernelGGL(k_cc_hook, dim3(ge), dim3(256), 0, c->stream, c->rl[4].as<uint32_t>(), N, parent);
+  {
+    // the two-phase unions and the giant tree's bits, as the direct path (GS_CC_SAMPLE, GS_CC_GIANT)
+    static const int sample_env = getenv("GS_CC_SAMPLE") ? atoi(getenv("GS_CC_SAMPLE")) : 16;
+    static const int giant_env = getenv("GS_CC_GIANT") ? atoi(getenv("GS_CC_GIANT")) : 1;
+    const uint32_t* at = c->rl[4].as<uint32_t>();
+    if (sample_env > 1 && (sample_env & (sample_env - 1)) == 0 && N >= 65536) {
+      hipLaunchKernelGGL(k_cc_hook_phase, dim3(ge), dim3(256), 0, c->stream, at, N, parent, (uint32_t)sample_env - 1, 0,
+                         (const uint32_t*)nullptr);
+      hipLaunchKernelGGL(k_cc_compress_all, dim3(gu), dim3(256), 0, c->stream, parent, (uint32_t)U);
+      uint32_t* gbits = nullptr;
+      if (giant_env) {
+        GS_TRY(ensure(c, c->cc[3], (size_t)(U + 31) / 32 * 4 + 64));
+        gbits = c->cc[3].as<uint32_t>();
+        uint32_t* giant = gbits + (U + 31) / 32;
+        hipLaunchKernelGGL(k_cc_giant, dim3(1), dim3(1024), 0, c->stream, (const int64_t*)nullptr, at, N, 0ull, parent, giant);
+        hipLaunchKernelGGL(k_cc_gbits, dim3((unsigned)std::min<uint64_t>(((U + 31) / 32 + 255) / 256, 16384)), dim3(256), 0,
+                           c->stream, parent, (uint32_t)U, giant, gbits);
+      }
+      hipLaunchKernelGGL(k_cc_hook_phase, dim3(ge), dim3(256), 0, c->stream, at, N, parent, (uint32_t)sample_env - 1, 1,
+                         (const uint32_t*)gbits);
+    } else {
+      hipLaunchKernelGGL(k_cc_hook, dim3(ge), dim3(256), 0, c->stream, at, N, parent);
+    }
+  }
   GS_HIP(hipGetLastError());
   hipEventRecord(c->ev[2], c->stream);
   // 4. labels

@@ -31,13 +31,16 @@ def test_connected_components_itcase_through_the_api(pkg):
     assert sorted(sorted(c) for c in comps.values()) == sorted(cc["expected"])
 
 
-@pytest.mark.parametrize("kind", ["rmat", "sparse_ids", "chains", "loops"])
+@pytest.mark.parametrize("kind", ["rmat", "sparse_ids", "sparse_ids_large", "chains", "loops"])
 def test_components_vs_oracle(engine, oracle, kind):
     rng = np.random.default_rng(3)
     if kind == "rmat":
         s, d = oracle.gen_rmat(16, 60_000, 0x5EED09)           # many small components + a giant one
     elif kind == "sparse_ids":                                  # negative and 64-bit spread ids
         s, d = oracle.gen_rmat(12, 5_000, 0x5EED0A)
+        s, d = s * 7_919_000_003 - (1 << 61), d * 7_919_000_003 - (1 << 61)
+    elif kind == "sparse_ids_large":                            # the relabel path's two-phase unions (>= 65536 records)
+        s, d = oracle.gen_rmat(16, 300_000, 0x5EED0E)
         s, d = s * 7_919_000_003 - (1 << 61), d * 7_919_000_003 - (1 << 61)
     elif kind == "chains":                                      # long paths: deep union chains
         p = rng.permutation(200_000).astype(np.int64)
