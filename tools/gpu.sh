@@ -79,6 +79,12 @@ case $MODE in
     bench bench_e2e_direct --workload e2e --staging direct --no-cpu-baseline
     bench bench_e2e_pinned --workload e2e --staging pinned --no-cpu-baseline
     bench bench_e2e_buffered --workload e2e --staging buffered --no-cpu-baseline ;;
+  tapmc)
+    # texture-address / L1 counters of the triangle count (why its scattered loads are or are not the bound)
+    S=${1:-24}; shift || true
+    A="--workload triangles --scale $S --steps 1 --warmup 0 --windows 1"
+    pmc tapmc_s$S/ta "TA_TA_BUSY_sum TA_ADDR_STALLED_BY_TC_CYCLES_sum GRBM_GUI_ACTIVE" $A
+    pmc tapmc_s$S/tcp "TCP_TCC_READ_REQ_sum TCP_TOTAL_ACCESSES_sum TCP_PENDING_STALL_CYCLES_sum TCP_TCP_TA_ADDR_STALL_CYCLES_sum" $A ;;
   ktrace)
     # kernel trace of any bench line: TAG NAME [bench args]
     N=${1:-run}; shift || true
